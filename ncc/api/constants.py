@@ -1,0 +1,96 @@
+"""Wire-level constants of the Nexus configuration-sync contract.
+
+Every value here is part of the observable contract with the reference controller
+(SneaksAndData/nexus-configuration-controller) and with the `nexus-core` CRD module it
+consumes, so a cluster managed by the reference can be taken over by this framework
+without any object being rewritten.
+
+Citations (reference snapshot, /root/reference):
+  * metric names            controller.go:50-56
+  * agent / field manager   controller.go:58,83
+  * event reasons/messages  controller.go:60-81
+  * queue kinds             controller.go:93-96
+  * owner labels            controller_test.go:183-188 (nexus-core shards.OwnerLabels)
+  * group/version/plurals   .helm/templates/cluster-role-template-editor.yaml:25-36
+"""
+
+GROUP = "science.sneaksanddata.com"
+VERSION = "v1"
+API_VERSION = f"{GROUP}/{VERSION}"
+
+TEMPLATE_KIND = "NexusAlgorithmTemplate"
+WORKGROUP_KIND = "NexusAlgorithmWorkgroup"
+TEMPLATE_PLURAL = "nexusalgorithmtemplates"
+WORKGROUP_PLURAL = "nexusalgorithmworkgroups"
+
+# controller.go:58 — also used as the Event source component and the field manager.
+CONTROLLER_AGENT_NAME = "nexus-configuration-controller"
+FIELD_MANAGER = CONTROLLER_AGENT_NAME
+
+# statsd metric names, controller.go:50-56; namespace from main.go:44
+METRIC_NAMESPACE = "nexus_configuration_controller"
+RECONCILE_LATENCY_METRIC = "reconcile_latency"
+WORKQUEUE_LENGTH_METRIC = "workqueue_length"
+
+# Event reasons, controller.go:60-70
+SUCCESS_SYNCED = "Synced"
+ERR_RESOURCE_EXISTS = "ErrResourceExists"
+ERR_RESOURCE_MISSING = "ErrResourceMissing"
+ERR_RESOURCE_SYNC_ERROR = "ErrResourceSyncError"
+
+# Event message formats, controller.go:72-81.  Go's %q is rendered by `go_quote`.
+MESSAGE_RESOURCE_EXISTS = "Resource {0} already exists and is not managed by any Machine Learning Algorithm"
+MESSAGE_RESOURCE_SYNCED = "Resource of type {0} synced successfully"
+MESSAGE_RESOURCE_MISSING = "Resource {0} referenced by NexusAlgorithmTemplate {1} is missing in the controller cluster"
+MESSAGE_RESOURCE_OPERATION_FAILED = (
+    "Synchronization/update of a resource {0} referenced by NexusAlgorithmTemplate {1} failed with a fatal error {2}"
+)
+
+EVENT_TYPE_NORMAL = "Normal"
+EVENT_TYPE_WARNING = "Warning"
+
+# Queue element kinds, controller.go:93-96
+KIND_TEMPLATE = "template"
+KIND_WORKGROUP = "workgroup"
+
+# Labels stamped on every object created in a shard (nexus-core shards.OwnerLabels).
+LABEL_CONTROLLER_APP = f"{GROUP}/controller-app"
+LABEL_CONFIGURATION_OWNER = f"{GROUP}/configuration-owner"
+
+# Status condition (nexus-core v1.NewResourceReadyCondition).  The Reason string of the
+# upstream helper is not visible from the reference; "ResourceReady" is a documented
+# assumption and only matters for display.
+CONDITION_READY = "Ready"
+CONDITION_READY_REASON = "ResourceReady"
+CONDITION_TRUE = "True"
+CONDITION_FALSE = "False"
+
+
+def go_quote(s: str) -> str:
+    """Render a string the way Go's fmt `%q` verb does for printable ASCII input."""
+    out = ['"']
+    for ch in s:
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ord(ch) < 0x20 or ord(ch) == 0x7F:
+            out.append("\\x%02x" % ord(ch))
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def owner_labels(alias: str) -> dict:
+    """Labels nexus-core stamps on shard objects it creates (controller_test.go:183-188)."""
+    return {
+        LABEL_CONTROLLER_APP: CONTROLLER_AGENT_NAME,
+        LABEL_CONFIGURATION_OWNER: alias,
+    }

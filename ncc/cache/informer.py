@@ -1,0 +1,279 @@
+"""SharedInformer: list → watch → resync, feeding a `Store` and fanning out to handlers.
+
+Re-creates the client-go machinery the reference gets from
+`SharedInformerFactory(..., 30s, WithNamespace(ns))` (main.go:70-71):
+
+* initial (paginated) LIST → `Store.replace` → `has_synced()` becomes true;
+* WATCH from the list resourceVersion with bookmarks; a clean stream end re-watches from the
+  last seen RV; `410 Gone` (HTTP or in-stream ERROR) triggers a relist;
+* transport errors back off exponentially (client-go's 800ms→30s reflector backoff);
+* a relist delivers Add for new keys, Update for kept keys, and Delete with a
+  `DeletedFinalStateUnknown` tombstone for keys that vanished while we were not watching;
+* every `resync_period` seconds each cached object is re-delivered as Update(obj, obj),
+  which is what makes the reference re-reconcile every template every 30 s
+  (controller.go:288-290).
+
+Handlers run inline on the event loop; a handler may be a coroutine function, in which case
+the informer awaits it before processing the next event (the reference's template-delete
+handler blocks its informer the same way, controller.go:195-205).
+"""
+from __future__ import annotations
+
+import asyncio
+import inspect
+import logging
+import random
+from dataclasses import dataclass
+from typing import Callable
+
+from ..api.objects import ObjectKey, key_of
+from ..api.resources import ResourceType
+from ..kube import errors as E
+from ..kube.client import KubeClient
+from .store import Store
+
+log = logging.getLogger("ncc.informer")
+
+
+@dataclass(frozen=True)
+class DeletedFinalStateUnknown:
+    """Tombstone for an object whose delete event was missed (client-go cache.DeletedFinalStateUnknown)."""
+    key: ObjectKey
+    obj: dict
+
+
+class Lister:
+    """Namespace-aware read view over a store; `get` raises `NotFound` like a client-go lister."""
+
+    def __init__(self, store: Store, rt: ResourceType):
+        self.store = store
+        self.rt = rt
+
+    def get(self, namespace: str, name: str) -> dict:
+        o = self.store.get(namespace, name)
+        if o is None:
+            gr = f"{self.rt.plural}.{self.rt.group}" if self.rt.group else self.rt.plural
+            raise E.NotFound(f'{gr} "{name}" not found', details={"name": name, "kind": self.rt.plural})
+        return o
+
+    def try_get(self, namespace: str, name: str) -> dict | None:
+        return self.store.get(namespace, name)
+
+    def list(self, namespace: str | None = None) -> list[dict]:
+        return self.store.list(namespace)
+
+
+@dataclass
+class _Handler:
+    on_add: Callable | None
+    on_update: Callable | None
+    on_delete: Callable | None
+
+
+async def _call(fn, *args):
+    if fn is None:
+        return
+    r = fn(*args)
+    if inspect.isawaitable(r):
+        await r
+
+
+class Informer:
+    def __init__(self, client: KubeClient, rt: ResourceType, namespace: str | None, *,
+                 resync_period: float = 0.0, transform: Callable[[dict], dict] | None = None,
+                 label_selector: str | None = None, page_size: int = 500, watch_timeout: tuple = (300, 600),
+                 name: str = ""):
+        self.client = client
+        self.rt = rt
+        self.namespace = namespace
+        self.resync_period = resync_period
+        self.label_selector = label_selector
+        self.page_size = page_size
+        self.watch_timeout = watch_timeout
+        self.name = name or f"{client.cluster_name}/{rt.plural}"
+        self.store = Store(transform=transform)
+        self.lister = Lister(self.store, rt)
+        self._handlers: list[_Handler] = []
+        self._synced = asyncio.Event()
+        self._task: asyncio.Task | None = None
+        self._resync_task: asyncio.Task | None = None
+        self.last_rv: str = ""
+        self.relists = 0
+        self.events = 0
+        self.last_error: BaseException | None = None
+
+    # ------------------------------------------------------------- public API
+    def add_event_handler(self, on_add=None, on_update=None, on_delete=None) -> None:
+        self._handlers.append(_Handler(on_add, on_update, on_delete))
+
+    def has_synced(self) -> bool:
+        return self._synced.is_set()
+
+    async def wait_for_sync(self, timeout: float | None = None) -> bool:
+        try:
+            await asyncio.wait_for(self._synced.wait(), timeout)
+            return True
+        except asyncio.TimeoutError:
+            return False
+
+    def start(self) -> asyncio.Task:
+        if self._task is None:
+            self._task = asyncio.ensure_future(self._run())
+            if self.resync_period > 0:
+                self._resync_task = asyncio.ensure_future(self._resync_loop())
+        return self._task
+
+    async def stop(self) -> None:
+        for t in (self._task, self._resync_task):
+            if t is not None:
+                t.cancel()
+        for t in (self._task, self._resync_task):
+            if t is not None:
+                try:
+                    await t
+                except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                    pass
+        self._task = self._resync_task = None
+
+    # ------------------------------------------------------------- dispatch
+    async def _dispatch_add(self, obj):
+        for h in self._handlers:
+            await _call(h.on_add, obj)
+
+    async def _dispatch_update(self, old, new):
+        for h in self._handlers:
+            await _call(h.on_update, old, new)
+
+    async def _dispatch_delete(self, obj):
+        for h in self._handlers:
+            await _call(h.on_delete, obj)
+
+    # ------------------------------------------------------------- reflector
+    async def _list(self) -> str:
+        items: list[dict] = []
+        token = None
+        rv = ""
+        while True:
+            resp = await self.client.list(self.rt, self.namespace, label_selector=self.label_selector,
+                                          limit=self.page_size, continue_token=token)
+            items.extend(resp.get("items") or ())
+            lm = resp.get("metadata") or {}
+            rv = lm.get("resourceVersion", rv)
+            token = lm.get("continue")
+            if not token:
+                break
+        added, updated, deleted = self.store.replace(items)
+        self.relists += 1
+        synced_before = self.has_synced()
+        self._synced.set()
+        for o in added:
+            await self._dispatch_add(o)
+        for old, new in updated:
+            await self._dispatch_update(old, new)
+        if synced_before:
+            for o in deleted:
+                await self._dispatch_delete(DeletedFinalStateUnknown(key_of(o), o))
+        return rv
+
+    async def _watch(self, rv: str) -> str:
+        """Consume one watch stream; returns the last RV seen.  Raises Gone to force a relist."""
+        lo, hi = self.watch_timeout
+        async for ev in self.client.watch(self.rt, self.namespace, resource_version=rv,
+                                          timeout_seconds=random.randint(lo, hi), allow_bookmarks=True,
+                                          label_selector=self.label_selector):
+            t = ev.type
+            obj = ev.object
+            if t == "ERROR":
+                code = int(obj.get("code") or 0)
+                if code == 410:
+                    raise E.Gone(obj.get("message", "watch expired"))
+                raise E.from_status(code, obj)
+            new_rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
+            if t == "BOOKMARK":
+                rv = new_rv
+                continue
+            self.events += 1
+            if t in ("ADDED", "MODIFIED"):
+                stored, old = self.store.upsert(obj)
+                rv = new_rv
+                if old is None:
+                    await self._dispatch_add(stored)
+                else:
+                    await self._dispatch_update(old, stored)
+            elif t == "DELETED":
+                old = self.store.delete(obj)
+                rv = new_rv
+                await self._dispatch_delete(old if old is not None else obj)
+            self.last_rv = rv
+        return rv
+
+    async def _run(self) -> None:
+        backoff = 0.8
+        rv = ""
+        need_list = True
+        while True:
+            try:
+                if need_list:
+                    rv = await self._list()
+                    self.last_rv = rv
+                    need_list = False
+                rv = await self._watch(rv)
+                backoff = 0.8
+            except asyncio.CancelledError:
+                raise
+            except E.Gone:
+                need_list = True
+                log.debug("%s: watch expired, relisting", self.name)
+            except Exception as e:  # noqa: BLE001 — transport errors, 5xx, etc.
+                self.last_error = e
+                log.debug("%s: list/watch failed: %r; retry in %.2fs", self.name, e, backoff)
+                await asyncio.sleep(backoff * (1 + random.random() * 0.2))
+                backoff = min(backoff * 2, 30.0)
+                if not isinstance(e, E.TransportError):
+                    need_list = True
+
+    async def _resync_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.resync_period)
+            if not self.has_synced():
+                continue
+            for o in self.store.list():
+                await self._dispatch_update(o, o)
+
+
+class InformerFactory:
+    """One informer per resource type for one (client, namespace) — SharedInformerFactory analogue."""
+
+    def __init__(self, client: KubeClient, namespace: str | None, resync_period: float = 0.0, **informer_kw):
+        self.client = client
+        self.namespace = namespace
+        self.resync_period = resync_period
+        self.informer_kw = informer_kw
+        self._informers: dict[ResourceType, Informer] = {}
+
+    def informer(self, rt: ResourceType, **kw) -> Informer:
+        inf = self._informers.get(rt)
+        if inf is None:
+            opts = dict(self.informer_kw)
+            opts.update(kw)
+            inf = self._informers[rt] = Informer(self.client, rt, self.namespace,
+                                                 resync_period=self.resync_period, **opts)
+        return inf
+
+    def start(self) -> None:
+        for inf in self._informers.values():
+            inf.start()
+
+    async def stop(self) -> None:
+        for inf in self._informers.values():
+            await inf.stop()
+
+    def has_synced(self) -> bool:
+        return all(i.has_synced() for i in self._informers.values())
+
+    async def wait_for_sync(self, timeout: float | None = None) -> bool:
+        res = await asyncio.gather(*(i.wait_for_sync(timeout) for i in self._informers.values()))
+        return all(res)
+
+    def informers(self) -> list[Informer]:
+        return list(self._informers.values())

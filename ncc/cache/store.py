@@ -1,0 +1,151 @@
+"""Thread-confined object store with secondary indices and a write-through mutation overlay.
+
+The client-go analogues are `cache.Indexer` (thread-safe store + indices) and
+`cache.MutationCache` (`NewIntegerResourceVersionMutationCache`).  The reference reads all
+state through listers backed by this kind of store (controller.go:107-121), so reconciles
+issue zero GETs.
+
+The mutation overlay (`assume`) lets a reconcile see its own successful writes before the
+watch event for them arrives: a subsequent reconcile of the same key then neither re-creates
+an object it just created (→ 409 AlreadyExists) nor updates from a stale resourceVersion
+(→ 409 Conflict).  An assumed object is shadowed as soon as the informer stores a version at
+least as new, or after `assume_ttl` seconds.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Iterable
+
+from ..api.objects import ObjectKey, key_of, rv_int
+
+IndexFunc = Callable[[dict], Iterable[str]]
+
+
+class Store:
+    def __init__(self, transform: Callable[[dict], dict] | None = None, assume_ttl: float = 60.0):
+        self._items: dict[ObjectKey, dict] = {}
+        self._indexers: dict[str, IndexFunc] = {}
+        self._indices: dict[str, dict[str, set]] = {}
+        self._assumed: dict[ObjectKey, tuple[dict, int, float]] = {}
+        self.transform = transform
+        self.assume_ttl = assume_ttl
+
+    # ------------------------------------------------------------ indices
+    def add_indexer(self, name: str, fn: IndexFunc) -> None:
+        self._indexers[name] = fn
+        idx: dict[str, set] = {}
+        for k, o in self._items.items():
+            for v in fn(o):
+                idx.setdefault(v, set()).add(k)
+        self._indices[name] = idx
+
+    def _index(self, key: ObjectKey, old: dict | None, new: dict | None) -> None:
+        for name, fn in self._indexers.items():
+            idx = self._indices[name]
+            if old is not None:
+                for v in fn(old):
+                    s = idx.get(v)
+                    if s is not None:
+                        s.discard(key)
+                        if not s:
+                            del idx[v]
+            if new is not None:
+                for v in fn(new):
+                    idx.setdefault(v, set()).add(key)
+
+    def by_index(self, name: str, value: str) -> list[dict]:
+        return [self._items[k] for k in self._indices.get(name, {}).get(value, ()) if k in self._items]
+
+    # ------------------------------------------------------------ mutation
+    def upsert(self, obj: dict) -> tuple[dict, dict | None]:
+        """Store `obj` (after transform); return (stored, previous)."""
+        if self.transform is not None:
+            obj = self.transform(obj)
+        key = key_of(obj)
+        old = self._items.get(key)
+        self._items[key] = obj
+        if self._indexers:
+            self._index(key, old, obj)
+        return obj, old
+
+    def delete(self, obj_or_key) -> dict | None:
+        key = obj_or_key if isinstance(obj_or_key, tuple) else key_of(obj_or_key)
+        old = self._items.pop(key, None)
+        self._assumed.pop(key, None)
+        if old is not None and self._indexers:
+            self._index(key, old, None)
+        return old
+
+    def replace(self, objs: Iterable[dict]) -> tuple[list, list, list]:
+        """Swap the whole content (relist).  Returns (added, updated[(old,new)], deleted)."""
+        new_items: dict[ObjectKey, dict] = {}
+        for o in objs:
+            if self.transform is not None:
+                o = self.transform(o)
+            new_items[key_of(o)] = o
+        old_items = self._items
+        added, updated, deleted = [], [], []
+        for k, o in new_items.items():
+            prev = old_items.get(k)
+            if prev is None:
+                added.append(o)
+            else:
+                updated.append((prev, o))
+        for k, o in old_items.items():
+            if k not in new_items:
+                deleted.append(o)
+        self._items = new_items
+        for name, fn in self._indexers.items():
+            idx: dict[str, set] = {}
+            for k, o in new_items.items():
+                for v in fn(o):
+                    idx.setdefault(v, set()).add(k)
+            self._indices[name] = idx
+        return added, updated, deleted
+
+    def assume(self, obj: dict) -> None:
+        """Record a write result we made; visible to `get` until the informer catches up."""
+        if self.transform is not None:
+            obj = self.transform(obj)
+        key = key_of(obj)
+        rv = rv_int((obj.get("metadata") or {}).get("resourceVersion"))
+        if rv < 0:
+            return
+        cur = self._items.get(key)
+        if cur is not None and rv_int((cur.get("metadata") or {}).get("resourceVersion")) >= rv:
+            return
+        prev = self._assumed.get(key)
+        if prev is not None and prev[1] >= rv:
+            return
+        self._assumed[key] = (obj, rv, time.monotonic() + self.assume_ttl)
+
+    # ------------------------------------------------------------ reads
+    def get(self, namespace: str, name: str) -> dict | None:
+        key = ObjectKey(namespace, name)
+        cur = self._items.get(key)
+        if self._assumed:
+            a = self._assumed.get(key)
+            if a is not None:
+                if (cur is not None and rv_int((cur.get("metadata") or {}).get("resourceVersion")) >= a[1]) \
+                        or time.monotonic() > a[2]:
+                    del self._assumed[key]
+                else:
+                    return a[0]
+        return cur
+
+    def get_key(self, key: ObjectKey) -> dict | None:
+        return self.get(key.namespace, key.name)
+
+    def list(self, namespace: str | None = None) -> list[dict]:
+        if namespace is None:
+            return list(self._items.values())
+        return [o for k, o in self._items.items() if k.namespace == namespace]
+
+    def keys(self) -> list[ObjectKey]:
+        return list(self._items.keys())
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+    def __contains__(self, key: ObjectKey) -> bool:
+        return key in self._items

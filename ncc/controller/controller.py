@@ -1,0 +1,379 @@
+"""The controller: informer event handlers, the work queue, and the worker pool.
+
+Reference: `Controller` / `NewController` / `Run` / `processNextWorkItem` / `enqueueResource` /
+`handleObject` in controller.go:98-426,851-884.  Queue elements are the strings
+`"<kind>/<namespace>/<name>"` with kind ∈ {template, workgroup} — the reference's
+`Element{objRef, objTypeName}` (controller.go:88-96) in a form the native C++ queue can hash.
+
+Handler wiring (controller.go:286-355):
+  template/workgroup  add/update → enqueue; delete → `handle_object`
+  secret/configmap    add → handle_object; update → handle_object if the RV changed; delete → handle_object
+`handle_object` unwraps tombstones; a deleted template is removed from every shard (compat:
+inline, sequential, first error aborts; native: queued and retried); any other object
+enqueues the NexusAlgorithmTemplates named in its ownerRefs that exist in the lister.
+"""
+from __future__ import annotations
+
+import asyncio
+import contextvars
+import logging
+import time
+
+from ..api import constants as C
+from ..api.objects import ObjectKey, meta
+from ..api.refs import template_owner_names
+from ..cache.informer import DeletedFinalStateUnknown, Informer
+from ..telemetry.statsd import Metrics, NullMetrics
+from ..workqueue.queue import WorkQueue
+from .events import EventRecorder, FakeRecorder
+from .options import ControllerOptions
+from .reconcile import ReconcileMixin, spec_matches, data_matches
+
+log = logging.getLogger("ncc.controller")
+
+_pass_state: contextvars.ContextVar = contextvars.ContextVar("ncc_pass_state", default=None)
+
+
+def make_key(kind: str, namespace: str, name: str) -> str:
+    return f"{kind}/{namespace}/{name}"
+
+
+def split_key(key: str) -> tuple[str, str, str]:
+    kind, ns, name = key.split("/", 2)
+    return kind, ns, name
+
+
+class Controller(ReconcileMixin):
+    def __init__(self, *, alias: str, namespace: str, client, shards: list,
+                 template_informer: Informer, workgroup_informer: Informer,
+                 secret_informer: Informer, configmap_informer: Informer,
+                 options: ControllerOptions | None = None, recorder: EventRecorder | None = None,
+                 metrics: Metrics | None = None, queue: WorkQueue | None = None):
+        self.alias = alias
+        self.namespace = namespace
+        self.client = client
+        self.shards = list(shards)
+        self.options = options or ControllerOptions.compat()
+        self.recorder = recorder or FakeRecorder(keep=False)
+        self.metrics = metrics or NullMetrics()
+        self.template_informer = template_informer
+        self.workgroup_informer = workgroup_informer
+        self.secret_informer = secret_informer
+        self.configmap_informer = configmap_informer
+        self.template_lister = template_informer.lister
+        self.workgroup_lister = workgroup_informer.lister
+        self.secret_lister = secret_informer.lister
+        self.configmap_lister = configmap_informer.lister
+        o = self.options
+        self.queue = queue or WorkQueue(base_delay=o.failure_base_delay, max_delay=o.failure_max_delay,
+                                        qps=o.rate_limit_qps, burst=o.rate_limit_burst, native=o.native_queue)
+        self._pending_deletes: set = set()
+        self._pending_workgroup_deletes: set = set()
+        self._workers: list[asyncio.Task] = []
+        self._aux: list[asyncio.Task] = []
+        self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0}
+        self.ready = asyncio.Event()
+        self._register_handlers()
+
+    # ================================================================== handlers
+    def _register_handlers(self) -> None:
+        o = self.options
+        self.template_informer.add_event_handler(
+            on_add=lambda obj: self.enqueue_resource(obj, C.KIND_TEMPLATE),
+            on_update=lambda old, new: self._on_crd_update(old, new, C.KIND_TEMPLATE),
+            on_delete=self._on_template_delete)
+        self.workgroup_informer.add_event_handler(
+            on_add=lambda obj: self.enqueue_resource(obj, C.KIND_WORKGROUP),
+            on_update=lambda old, new: self._on_crd_update(old, new, C.KIND_WORKGROUP),
+            on_delete=self._on_workgroup_delete)
+        for inf in (self.secret_informer, self.configmap_informer):
+            inf.add_event_handler(on_add=self.handle_object, on_update=self._on_dependent_update,
+                                  on_delete=self.handle_object)
+        if o.watch_shards:
+            for shard in self.shards:
+                self._register_shard_handlers(shard)
+
+    def _on_crd_update(self, old: dict, new: dict, kind: str) -> None:
+        if self.options.generation_filter:
+            om, nm = meta(old), meta(new)
+            if om.get("resourceVersion") == nm.get("resourceVersion"):
+                return  # informer resync: nothing changed
+            if om.get("generation") == nm.get("generation") and om.get("generation") is not None \
+                    and om.get("labels") == nm.get("labels") and om.get("annotations") == nm.get("annotations") \
+                    and old.get("spec") == new.get("spec"):
+                return  # status-only change (typically our own status write)
+        self.enqueue_resource(new, kind)
+
+    def _on_dependent_update(self, old: dict, new: dict) -> None:
+        om, nm = meta(old), meta(new)
+        if om.get("resourceVersion") == nm.get("resourceVersion"):
+            # Periodic resync will send update events for all known Secrets/ConfigMaps (controller.go:324-328).
+            return
+        if self.options.dependent_data_filter and old.get("data") == new.get("data") \
+                and old.get("binaryData") == new.get("binaryData") and old.get("type") == new.get("type") \
+                and template_owner_names(old) == template_owner_names(new):
+            return  # e.g. our own adoption PUT: ownerRef UIDs changed, payload did not
+        self.handle_object(new)
+
+    def enqueue_resource(self, obj, kind: str) -> None:
+        """enqueueResource (controller.go:136-162)."""
+        if isinstance(obj, DeletedFinalStateUnknown):
+            obj = obj.obj
+        m = meta(obj)
+        self.queue.add(make_key(kind, m.get("namespace", "") or "", m.get("name", "")))
+
+    def _unwrap(self, obj):
+        if isinstance(obj, DeletedFinalStateUnknown):
+            log.debug("Recovered deleted object %s", obj.key)
+            return obj.obj
+        return obj
+
+    def _on_template_delete(self, obj):
+        obj = self._unwrap(obj)
+        return self._handle_template_delete(obj)
+
+    def _on_workgroup_delete(self, obj):
+        obj = self._unwrap(obj)
+        if self.options.propagate_workgroup_deletes:
+            key = ObjectKey(meta(obj).get("namespace", ""), meta(obj).get("name", ""))
+            self._pending_workgroup_deletes.add(tuple(key))
+            self.enqueue_resource(obj, C.KIND_WORKGROUP)
+            return None
+        # reference: a deleted workgroup goes through handleObject's default branch (controller.go:206-223)
+        return self._handle_dependent(obj)
+
+    def handle_object(self, obj):
+        """handleObject (controller.go:169-224).  Returns an awaitable for the inline template-delete path."""
+        obj = self._unwrap(obj)
+        if not isinstance(obj, dict):
+            log.error("Error decoding object, invalid type %s", type(obj).__name__)
+            return None
+        if obj.get("kind") == C.TEMPLATE_KIND:
+            return self._handle_template_delete(obj)
+        return self._handle_dependent(obj)
+
+    def _handle_dependent(self, obj: dict):
+        ns = meta(obj).get("namespace", "") or ""
+        for ref in meta(obj).get("ownerReferences") or ():
+            if ref.get("kind") != C.TEMPLATE_KIND:
+                continue
+            template = self.template_lister.try_get(ns, ref.get("name", ""))
+            if template is None:
+                log.debug("Ignore orphaned object %s/%s (template %s)", ns, meta(obj).get("name"), ref.get("name"))
+                return None  # the reference returns on the first orphaned owner (controller.go:215-218)
+            self.enqueue_resource(template, C.KIND_TEMPLATE)
+        return None
+
+    def _handle_template_delete(self, obj: dict):
+        ns, name = meta(obj).get("namespace", "") or "", meta(obj).get("name", "")
+        if self.options.queued_deletes:
+            self._pending_deletes.add((ns, name))
+            self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+            return None
+        return self._delete_template_inline(obj)
+
+    async def _delete_template_inline(self, obj: dict) -> None:
+        """controller.go:195-205: sequential, no retry, abort on the first failing shard."""
+        for shard in self.shards:
+            try:
+                await shard.delete_template(obj)
+            except Exception as e:  # noqa: BLE001
+                log.error("Error deleting Template from a connected shard %s: %s", shard.name, e)
+                return
+
+    # ------------------------------------------------------------ shard-side drift watch (native)
+    def _register_shard_handlers(self, shard) -> None:
+        def template_changed(old, new=None):
+            obj = self._unwrap(new if new is not None else old)
+            deleted = new is None
+            ns, name = meta(obj).get("namespace", ""), meta(obj).get("name", "")
+            ctl = self.template_lister.try_get(ns, name)
+            if ctl is None:
+                return
+            if deleted or not spec_matches(ctl.get("spec"), obj):
+                self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+
+        def workgroup_changed(old, new=None):
+            obj = self._unwrap(new if new is not None else old)
+            deleted = new is None
+            ns, name = meta(obj).get("namespace", ""), meta(obj).get("name", "")
+            ctl = self.workgroup_lister.try_get(ns, name)
+            if ctl is None:
+                return
+            if deleted or not spec_matches(ctl.get("spec"), obj):
+                self.queue.add(make_key(C.KIND_WORKGROUP, ns, name))
+
+        def dependent_changed(lister, with_binary):
+            def h(old, new=None):
+                obj = self._unwrap(new if new is not None else old)
+                deleted = new is None
+                ns, name = meta(obj).get("namespace", ""), meta(obj).get("name", "")
+                src = lister.try_get(ns, name)
+                if src is None:
+                    return
+                if not deleted and data_matches(src, obj, with_binary):
+                    return
+                for owner in template_owner_names(obj) or template_owner_names(src):
+                    if self.template_lister.try_get(ns, owner) is not None:
+                        self.queue.add(make_key(C.KIND_TEMPLATE, ns, owner))
+            return h
+
+        shard.template_informer.add_event_handler(on_update=template_changed, on_delete=template_changed)
+        shard.workgroup_informer.add_event_handler(on_update=workgroup_changed, on_delete=workgroup_changed)
+        shard.secret_informer.add_event_handler(on_update=dependent_changed(self.secret_lister, False),
+                                                on_delete=dependent_changed(self.secret_lister, False))
+        shard.configmap_informer.add_event_handler(
+            on_update=dependent_changed(self.configmap_lister, self.options.sync_binary_data),
+            on_delete=dependent_changed(self.configmap_lister, self.options.sync_binary_data))
+
+    # ================================================================== helpers
+    def _assume(self, informer: Informer, res):
+        if self.options.assume_writes and isinstance(res, dict):
+            informer.store.assume(res)
+        return res
+
+    def _pass_wrote(self) -> None:
+        st = _pass_state.get()
+        if st is not None:
+            st[0] = True
+
+    def _last_pass_wrote(self) -> bool:
+        st = _pass_state.get()
+        return bool(st and st[0])
+
+    # ================================================================== worker loop
+    async def process_next_work_item(self) -> bool:
+        """processNextWorkItem (controller.go:373-426)."""
+        key = await self.queue.get()
+        if key is None:
+            return False
+        start = time.monotonic()
+        depth = len(self.queue)
+        _pass_state.set([False])
+        try:
+            kind, ns, name = split_key(key)
+            self.stats["reconciles"] += 1
+            if kind == C.KIND_TEMPLATE:
+                handler = self.sync_template
+            elif kind == C.KIND_WORKGROUP:
+                handler = self.sync_workgroup
+            else:
+                self.queue.forget(key)
+                return True
+            self.stats[kind] += 1
+            try:
+                await handler(ns, name)
+                self.queue.forget(key)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                self.stats["errors"] += 1
+                log.info("Error syncing %s; re-queuing for later retry: %s", key, e)
+                self.queue.add_rate_limited(key)
+        finally:
+            self.metrics.gauge(C.WORKQUEUE_LENGTH_METRIC, depth)
+            self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, start)
+            self.queue.done(key)
+        return True
+
+    async def _run_worker(self) -> None:
+        """wait.UntilWithContext(ctx, runWorker, 1s): restart the loop a second after a crash."""
+        while True:
+            try:
+                while await self.process_next_work_item():
+                    pass
+                return
+            except asyncio.CancelledError:
+                raise
+            except Exception:  # noqa: BLE001 — HandleCrash
+                log.exception("worker crashed; restarting in 1s")
+                await asyncio.sleep(1.0)
+
+    async def wait_for_caches(self) -> bool:
+        """Run's cache barrier (controller.go:862-871)."""
+        ok = await asyncio.gather(*(i.wait_for_sync() for i in (self.secret_informer, self.configmap_informer,
+                                                                 self.template_informer, self.workgroup_informer)))
+        if not all(ok):
+            return False
+        log.info("Controller informers synced")
+        t = self.options.wait_for_shards_timeout
+        if t is None:
+            for shard in self.shards:  # sequential and unbounded, like the reference
+                await shard.wait_for_sync()
+        else:
+            res = await asyncio.gather(*(s.wait_for_sync(t) for s in self.shards))
+            for s, r in zip(self.shards, res):
+                if not r:
+                    log.warning("shard %s did not sync within %.1fs; continuing without it for now", s.name, t)
+        log.info("Shard informers synced")
+        return True
+
+    def start_workers(self, workers: int | None = None) -> None:
+        n = workers or self.options.workers
+        self._workers = [asyncio.ensure_future(self._run_worker()) for _ in range(n)]
+        if self.options.orphan_sweep:
+            self.sweep_orphans()
+        if self.options.full_resync_period > 0:
+            self._aux.append(asyncio.ensure_future(self._full_resync_loop()))
+        self.ready.set()
+        log.info("Started %d workers", n)
+
+    def sweep_orphans(self) -> int:
+        """Enqueue shard objects we own whose controller object no longer exists."""
+        n = 0
+        for shard in self.shards:
+            for st in shard.template_lister.list():
+                ns, name = meta(st).get("namespace", ""), meta(st).get("name", "")
+                if self._is_ours(st) and self.template_lister.try_get(ns, name) is None:
+                    self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+                    n += 1
+            if self.options.propagate_workgroup_deletes:
+                for sw in shard.workgroup_lister.list():
+                    ns, name = meta(sw).get("namespace", ""), meta(sw).get("name", "")
+                    if self._is_ours(sw) and self.workgroup_lister.try_get(ns, name) is None:
+                        self.queue.add(make_key(C.KIND_WORKGROUP, ns, name))
+                        n += 1
+        return n
+
+    def enqueue_all(self) -> None:
+        for t in self.template_lister.list():
+            self.enqueue_resource(t, C.KIND_TEMPLATE)
+        for w in self.workgroup_lister.list():
+            self.enqueue_resource(w, C.KIND_WORKGROUP)
+
+    async def _full_resync_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.options.full_resync_period)
+            self.enqueue_all()
+            if self.options.orphan_sweep:
+                self.sweep_orphans()
+
+    async def run(self, stop: asyncio.Event, workers: int | None = None) -> None:
+        """Run (controller.go:851-884): cache barrier, workers, block until `stop`."""
+        log.info("Starting NexusAlgorithmTemplate controller")
+        log.info("Waiting for informer caches to sync")
+        sync = asyncio.ensure_future(self.wait_for_caches())
+        stopper = asyncio.ensure_future(stop.wait())
+        done, _ = await asyncio.wait({sync, stopper}, return_when=asyncio.FIRST_COMPLETED)
+        if stopper in done:
+            sync.cancel()
+            await self.shutdown()
+            return
+        stopper.cancel()
+        if not sync.result():
+            raise RuntimeError("failed to wait for caches to sync")
+        self.start_workers(workers)
+        await stop.wait()
+        log.info("Shutting down workers")
+        await self.shutdown()
+
+    async def shutdown(self) -> None:
+        self.queue.shutdown()
+        for t in self._aux:
+            t.cancel()
+        if self._workers:
+            _, pending = await asyncio.wait(self._workers, timeout=5.0)
+            for t in pending:
+                t.cancel()
+        self._workers = []
+        self._aux = []

@@ -1,0 +1,200 @@
+"""Kubernetes Event recording: recorder → broadcaster → correlator → sink.
+
+The reference builds `record.NewBroadcaster` with structured logging and a sink writing to
+the controller cluster (controller.go:252-256); recorded reasons are in controller.go:60-81.
+This module re-creates the parts of client-go `tools/record` that shape the API traffic:
+
+* non-blocking `event()` into a bounded buffer (client-go drops on overflow, 1000 entries);
+* the **spam filter**: a token bucket per (source, involved object), burst 25, refill 1/300 s;
+* **aggregation**: >10 distinct messages for the same (object, type, reason) within 10 minutes
+  collapse into one "(combined from similar events): …" event;
+* **dedup**: a repeat of an identical event PATCHes `count`/`lastTimestamp` of the existing
+  Event instead of creating a new one;
+* bounded retries of failed sink writes.
+
+`FakeRecorder` mirrors client-go's: it keeps "Type Reason Message" strings (or drops them).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+
+from ..api import constants as C
+from ..api import resources as R
+from ..api.objects import meta, now_rfc3339
+from ..kube.client import PATCH_STRATEGIC, KubeClient
+from ..kube.ratelimit import TokenBucket
+
+log = logging.getLogger("ncc.events")
+
+SPAM_BURST = 25
+SPAM_QPS = 1.0 / 300.0
+AGGREGATE_MAX_EVENTS = 10
+AGGREGATE_INTERVAL_S = 600.0
+BUFFER = 1000
+
+
+class EventRecorder:
+    def event(self, obj: dict, event_type: str, reason: str, message: str, kind: str | None = None) -> None:
+        raise NotImplementedError
+
+
+class FakeRecorder(EventRecorder):
+    """client-go record.FakeRecorder: with `keep=False` events are discarded (as in the reference tests)."""
+
+    def __init__(self, keep: bool = True):
+        self.keep = keep
+        self.events: list[str] = []
+
+    def event(self, obj, event_type, reason, message, kind=None):
+        if self.keep:
+            self.events.append(f"{event_type} {reason} {message}")
+
+
+def involved_object(obj: dict, kind: str | None) -> dict:
+    m = meta(obj)
+    ref = {
+        "kind": kind or obj.get("kind", ""),
+        "namespace": m.get("namespace", ""),
+        "name": m.get("name", ""),
+        "uid": m.get("uid", ""),
+        "apiVersion": obj.get("apiVersion", ""),
+        "resourceVersion": m.get("resourceVersion", ""),
+    }
+    if not ref["apiVersion"] and ref["kind"]:
+        try:
+            ref["apiVersion"] = R.by_kind(ref["kind"]).api_version
+        except KeyError:
+            pass
+    return ref
+
+
+class BroadcastRecorder(EventRecorder):
+    """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
+
+    def __init__(self, client: KubeClient, component: str = C.CONTROLLER_AGENT_NAME, *, spam_filter: bool = True,
+                 log_events: bool = True):
+        self.client = client
+        self.component = component
+        self.spam_filter = spam_filter
+        self.log_events = log_events
+        self._queue: asyncio.Queue = asyncio.Queue(maxsize=BUFFER)
+        self._buckets: dict[tuple, TokenBucket] = {}
+        self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
+        self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
+        self._task: asyncio.Task | None = None
+        self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0}
+
+    def start(self) -> None:
+        if self._task is None:
+            self._task = asyncio.ensure_future(self._run())
+
+    async def stop(self, drain_timeout: float = 1.0) -> None:
+        if self._task is None:
+            return
+        try:
+            await asyncio.wait_for(self._queue.join(), drain_timeout)
+        except asyncio.TimeoutError:
+            pass
+        self._task.cancel()
+        try:
+            await self._task
+        except (asyncio.CancelledError, Exception):  # noqa: BLE001
+            pass
+        self._task = None
+
+    def event(self, obj, event_type, reason, message, kind=None):
+        self.stats["recorded"] += 1
+        ref = involved_object(obj, kind)
+        if self.log_events:
+            log.info("Event occurred", extra={"object": f"{ref['namespace']}/{ref['name']}", "kind": ref["kind"],
+                                              "type": event_type, "reason": reason, "message": message})
+        try:
+            self._queue.put_nowait((ref, event_type, reason, message, time.monotonic()))
+        except asyncio.QueueFull:
+            self.stats["dropped_full"] += 1
+
+    # ------------------------------------------------------------------ correlator
+    def _allow(self, ref: dict, now: float) -> bool:
+        if not self.spam_filter:
+            return True
+        k = (self.component, ref["kind"], ref["namespace"], ref["name"], ref["uid"], ref["apiVersion"])
+        b = self._buckets.get(k)
+        if b is None:
+            b = self._buckets[k] = TokenBucket(SPAM_QPS, SPAM_BURST, now=now)
+        return b.reserve(now) <= 0.0 or self._refund(b)
+
+    @staticmethod
+    def _refund(b: TokenBucket) -> bool:
+        b._tokens += 1.0  # a rejected event must not consume future capacity (TokenBucket.TryAccept)
+        return False
+
+    def _aggregate(self, ref: dict, event_type: str, reason: str, message: str, now: float) -> tuple[str, tuple]:
+        akey = (self.component, ref["kind"], ref["namespace"], ref["name"], ref["uid"], event_type, reason)
+        msgs, first = self._similar.get(akey, (set(), now))
+        if now - first > AGGREGATE_INTERVAL_S:
+            msgs, first = set(), now
+        msgs.add(message)
+        self._similar[akey] = (msgs, first)
+        if len(msgs) >= AGGREGATE_MAX_EVENTS:
+            return "(combined from similar events): " + message, akey
+        return message, akey + (message,)
+
+    async def _write(self, ref, event_type, reason, message) -> None:
+        now = time.monotonic()
+        if not self._allow(ref, now):
+            self.stats["dropped_spam"] += 1
+            return
+        message, key = self._aggregate(ref, event_type, reason, message, now)
+        ts = now_rfc3339()
+        prev = self._seen.get(key)
+        ns = ref["namespace"] or "default"
+        if prev is not None:
+            count = int(prev.get("count", 1)) + 1
+            patch = {"count": count, "lastTimestamp": ts, "message": message}
+            res = await self.client.patch(R.EVENTS, ns, prev["metadata"]["name"], patch,
+                                          patch_type=PATCH_STRATEGIC)
+            self._seen[key] = res if isinstance(res, dict) else dict(prev, count=count)
+            self.stats["patched"] += 1
+            return
+        ev = {
+            "apiVersion": "v1",
+            "kind": "Event",
+            "metadata": {"name": f"{ref['name']}.{time.time_ns():x}", "namespace": ns},
+            "involvedObject": ref,
+            "reason": reason,
+            "message": message,
+            "source": {"component": self.component},
+            "firstTimestamp": ts,
+            "lastTimestamp": ts,
+            "count": 1,
+            "type": event_type,
+            "reportingComponent": self.component,
+            "reportingInstance": "",
+        }
+        res = await self.client.create(R.EVENTS, ns, ev)
+        self._seen[key] = res if isinstance(res, dict) else ev
+        if len(self._seen) > 4096:  # LRU-ish bound like client-go's 4096-entry cache
+            for k in list(self._seen)[:1024]:
+                del self._seen[k]
+        self.stats["created"] += 1
+
+    async def _run(self) -> None:
+        while True:
+            ref, event_type, reason, message, _t = await self._queue.get()
+            try:
+                for attempt in range(3):
+                    try:
+                        await self._write(ref, event_type, reason, message)
+                        break
+                    except asyncio.CancelledError:
+                        raise
+                    except Exception as e:  # noqa: BLE001
+                        if attempt == 2:
+                            self.stats["failed"] += 1
+                            log.debug("unable to write event: %r", e)
+                        else:
+                            await asyncio.sleep(0.1 * (attempt + 1))
+            finally:
+                self._queue.task_done()

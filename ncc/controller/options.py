@@ -1,0 +1,81 @@
+"""Controller behaviour switches: reference-compat semantics vs native (improved) semantics.
+
+`ControllerOptions.compat()` reproduces the reference's scheduling and quirks exactly
+ so its cost can be measured on the same substrate; every field
+defaults to that behaviour.  `ControllerOptions.native()` turns on the improvements listed in
+SURVEY.md §7.3 step 10, each independently switchable for ablation benchmarks.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, fields, replace
+
+
+@dataclass
+class ControllerOptions:
+    mode: str = "compat"
+    workers: int = 2                       # values.yaml:157
+    failure_base_delay: float = 0.030      # values.yaml:159-163
+    failure_max_delay: float = 5.0
+    rate_limit_qps: float = 50.0           # values.yaml:165-169
+    rate_limit_burst: int = 300
+    resync_period: float = 30.0            # main.go:70-71
+
+    # ---- native-mode improvements (all False/None == reference behaviour) ----
+    concurrent_fanout: bool = False        # controller.go:790 loops shards sequentially
+    shard_failure_isolation: bool = False  # controller.go:790-831 fails fast on the first shard error
+    concurrent_dependents: bool = False    # controller.go:505,567 loop dependents sequentially
+    generation_filter: bool = False        # controller.go:286-305 enqueues on every update incl. resync
+    dependent_data_filter: bool = False    # controller.go:319-355 re-reconciles on any RV change
+    event_on_noop: bool = True             # controller.go:754,843 emit Synced on every pass
+    single_put_dependents: bool = False    # controller.go:539-560 may PUT twice from a stale object
+    queued_deletes: bool = False           # controller.go:195-205 deletes inline, no retry
+    propagate_workgroup_deletes: bool = False  # controller.go:206-223 never deletes shard workgroups
+    orphan_sweep: bool = False             # no orphan sweep
+    watch_shards: bool = False             # shard drift only repaired on resync
+    tolerate_write_races: bool = False     # AlreadyExists / Conflict → refetch instead of error
+    assume_writes: bool = False            # no mutation cache in the reference
+    sync_binary_data: bool = False         # ConfigMap.binaryData not synced (controller.go:600)
+    slim_shard_cache: bool = False         # shard caches hold full objects
+    wait_for_shards_timeout: float | None = None  # controller.go:866-870 waits forever
+    full_resync_period: float = 0.0        # periodic enqueue-all sweep (native replaces informer resync)
+    native_queue: bool | None = None       # None: use the C++ queue when built
+
+    @classmethod
+    def compat(cls, **kw) -> "ControllerOptions":
+        return replace(cls(), **kw)
+
+    @classmethod
+    def native(cls, **kw) -> "ControllerOptions":
+        base = cls(
+            mode="native",
+            workers=32,
+            concurrent_fanout=True,
+            shard_failure_isolation=True,
+            concurrent_dependents=True,
+            generation_filter=True,
+            dependent_data_filter=True,
+            event_on_noop=False,
+            single_put_dependents=True,
+            queued_deletes=True,
+            propagate_workgroup_deletes=True,
+            orphan_sweep=True,
+            watch_shards=True,
+            tolerate_write_races=True,
+            assume_writes=True,
+            sync_binary_data=True,
+            slim_shard_cache=True,
+            wait_for_shards_timeout=10.0,
+            full_resync_period=600.0,
+        )
+        return replace(base, **kw)
+
+    @classmethod
+    def for_mode(cls, mode: str, **kw) -> "ControllerOptions":
+        if mode == "compat":
+            return cls.compat(**kw)
+        if mode == "native":
+            return cls.native(**kw)
+        raise ValueError(f"unknown controller mode {mode!r} (expected 'compat' or 'native')")
+
+    def as_dict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in fields(self)}

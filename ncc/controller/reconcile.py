@@ -1,0 +1,460 @@
+"""Reconcilers: template fan-out, workgroup fan-out, adoption, status conditions, ownership.
+
+Reference-compat semantics follow controller.go line by line in *behaviour* (ordering of API
+writes, error/event emission, fail-fast), which the parity tests pin against the reference's
+expected action lists (controller_test.go:800-1285).  Native semantics (selected by
+`ControllerOptions`) change scheduling, not outcomes: shards are reconciled concurrently with
+per-shard failure isolation, dependents within a shard are written concurrently after the
+template exists (the template UID is needed for their ownerRefs), write races
+are resolved by refetching, and data+owner changes go out as a single PUT.
+
+Citations: template sync controller.go:761-845; workgroup sync :697-756; adoption :647-695;
+dependents :504-626; ownership :482-502; status :428-480; shard names :628-635.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+
+from ..api import constants as C
+from ..api import resources as R
+from ..api.constants import go_quote as q
+from ..api.fingerprint import SLIM_FP, fingerprint
+from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
+from ..api.refs import configmap_names, is_owned_by_uid, ready_condition, secret_names, template_owner_ref
+from ..kube import errors as E
+
+log = logging.getLogger("ncc.reconcile")
+
+
+class RogueResourceError(Exception):
+    """A shard dependent exists without any owner reference (controller.go:494-499)."""
+
+
+class ShardNotReadyError(Exception):
+    """A shard's caches have not synced yet (native mode defers instead of blocking startup)."""
+
+
+class ShardSyncError(Exception):
+    """Aggregate of per-shard failures under failure isolation."""
+
+    def __init__(self, failures: dict):
+        self.failures = failures
+        super().__init__("; ".join(f"{k}: {v}" for k, v in failures.items()))
+
+
+# ---------------------------------------------------------------- equality helpers
+def spec_matches(desired_spec, shard_obj: dict) -> bool:
+    """reflect.DeepEqual(shard.Spec, template.Spec) — O(1) against a slim-cache digest."""
+    fp = shard_obj.get(SLIM_FP)
+    if fp is not None:
+        return fingerprint(desired_spec) == fp[0]
+    return desired_spec == shard_obj.get("spec")
+
+
+def data_matches(src: dict, shard_obj: dict, with_binary: bool) -> bool:
+    """reflect.DeepEqual(src.Data, shard.Data) (+ binaryData in native mode)."""
+    fp = shard_obj.get(SLIM_FP)
+    if fp is not None:
+        if fingerprint(src.get("data") or None) != fp[0]:
+            return False
+        return (not with_binary) or fingerprint(src.get("binaryData") or None) == fp[1]
+    if normalize_data(src.get("data")) != normalize_data(shard_obj.get("data")):
+        return False
+    return (not with_binary) or normalize_data(src.get("binaryData")) == normalize_data(shard_obj.get("binaryData"))
+
+
+def slim_spec(obj: dict) -> dict:
+    """Informer transform for shard templates/workgroups: keep metadata, replace spec by its digest."""
+    out = {k: v for k, v in obj.items() if k not in ("spec", "status")}
+    out[SLIM_FP] = (fingerprint(obj.get("spec")),)
+    return out
+
+
+def slim_data(obj: dict) -> dict:
+    """Informer transform for shard secrets/configmaps: keep metadata/type, replace payloads by digests."""
+    out = {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
+    out[SLIM_FP] = (fingerprint(obj.get("data") or None), fingerprint(obj.get("binaryData") or None))
+    return out
+
+
+class ReconcileMixin:
+    """Reconcile logic; mixed into `Controller` (which provides clients, listers, options)."""
+
+    # ============================================================ status (controller.go:428-480)
+    async def report_template_init_condition(self, template: dict) -> dict:
+        status = template.get("status") or {}
+        if not status.get("conditions"):
+            name = meta(template).get("name", "")
+            new = with_fields(template, status=dict(status, conditions=[
+                ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Algorithm {q(name)} initializing")]))
+            self._pass_wrote()
+            res = await self.client.update_status(R.TEMPLATES, meta(template).get("namespace", ""), new,
+                                                  field_manager=C.FIELD_MANAGER)
+            return self._assume(self.template_informer, res)
+        return template
+
+    async def report_workgroup_init_condition(self, workgroup: dict) -> dict:
+        status = workgroup.get("status") or {}
+        if not status.get("conditions"):
+            name = meta(workgroup).get("name", "")
+            new = with_fields(workgroup, status=dict(status, conditions=[
+                ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Workgroup {q(name)} initializing")]))
+            self._pass_wrote()
+            res = await self.client.update_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""), new,
+                                                  field_manager=C.FIELD_MANAGER)
+            return self._assume(self.workgroup_informer, res)
+        return workgroup
+
+    async def report_workgroup_synced_condition(self, workgroup: dict, ready: bool = True,
+                                                message: str | None = None) -> dict:
+        status = workgroup.get("status") or {}
+        conds = list(status.get("conditions") or [])
+        name = meta(workgroup).get("name", "")
+        msg = message or f"Workgroup {q(name)} ready"
+        conds[0] = ready_condition(conds[0].get("lastTransitionTime", ""),
+                                   C.CONDITION_TRUE if ready else C.CONDITION_FALSE, msg)
+        new_status = dict(status, conditions=conds)
+        if new_status != status:
+            conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
+            self._pass_wrote()
+            res = await self.client.update_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""),
+                                                  with_fields(workgroup, status=new_status),
+                                                  field_manager=C.FIELD_MANAGER)
+            return self._assume(self.workgroup_informer, res)
+        return workgroup
+
+    async def report_template_synced_condition(self, template: dict, secrets: list, configmaps: list, shards: list,
+                                               ready: bool = True, message: str | None = None) -> dict:
+        status = template.get("status") or {}
+        conds = list(status.get("conditions") or [])
+        name = meta(template).get("name", "")
+        msg = message or f"Algorithm {q(name)} ready"
+        conds[0] = ready_condition(conds[0].get("lastTransitionTime", ""),
+                                   C.CONDITION_TRUE if ready else C.CONDITION_FALSE, msg)
+        new_status = dict(status, conditions=conds, syncedSecrets=list(secrets),
+                          syncedConfigurations=list(configmaps), syncedToClusters=list(shards))
+        if new_status != status:
+            conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
+            self._pass_wrote()
+            res = await self.client.update_status(R.TEMPLATES, meta(template).get("namespace", ""),
+                                                  with_fields(template, status=new_status),
+                                                  field_manager=C.FIELD_MANAGER)
+            return self._assume(self.template_informer, res)
+        return template
+
+    # ============================================================ ownership (controller.go:482-502)
+    def is_missing_ownership(self, obj: dict, owner: dict, kind: str) -> bool:
+        refs = meta(obj).get("ownerReferences") or []
+        if refs:
+            owner_uid = meta(owner).get("uid", "") or ""
+            for r in refs:
+                if r.get("kind") == C.TEMPLATE_KIND and (r.get("uid", "") or "") == owner_uid:
+                    return False
+            return True
+        msg = C.MESSAGE_RESOURCE_EXISTS.format(q(meta(obj).get("name", "")))
+        # The reference records this against the *shard* object into the controller cluster (controller.go:497).
+        self.recorder.event(obj, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_EXISTS, msg, kind=kind)
+        raise RogueResourceError(msg)
+
+    # ============================================================ adoption (controller.go:647-695)
+    async def adopt_references(self, template: dict) -> None:
+        ns = meta(template).get("namespace", "")
+        tname = meta(template).get("name", "")
+        tuid = meta(template).get("uid", "") or ""
+        pending = []
+        for rt, names, lister, informer in ((R.SECRETS, secret_names(template), self.secret_lister,
+                                             self.secret_informer),
+                                            (R.CONFIGMAPS, configmap_names(template), self.configmap_lister,
+                                             self.configmap_informer)):
+            for nm in names:
+                ref = lister.try_get(ns, nm)
+                if ref is None:
+                    self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
+                                        C.MESSAGE_RESOURCE_MISSING.format(q(nm), q(tname)), kind=C.TEMPLATE_KIND)
+                    lister.get(ns, nm)  # raises the typed NotFound
+                if not is_owned_by_uid(ref, tuid):
+                    m = dict(meta(ref))
+                    m["ownerReferences"] = list(m.get("ownerReferences") or []) + [template_owner_ref(template)]
+                    args = (rt, ns, with_fields(ref, metadata=m), template, nm, informer)
+                    if self.options.concurrent_dependents:
+                        pending.append(args)  # validate every reference first, then write concurrently
+                    else:
+                        await self._adopt_one(*args)
+        if pending:
+            await self._gather_raise([self._adopt_one(*a) for a in pending])
+
+    async def _adopt_one(self, rt, ns, obj, template, nm, informer):
+        self._pass_wrote()
+        try:
+            res = await self.client.update(rt, ns, obj)
+            self._assume(informer, res)
+        except Exception as e:  # noqa: BLE001
+            self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
+                                C.MESSAGE_RESOURCE_OPERATION_FAILED.format(q(nm), q(meta(template).get("name", "")),
+                                                                          e), kind=C.TEMPLATE_KIND)
+            raise
+
+    @staticmethod
+    async def _gather_raise(jobs: list) -> None:
+        res = await asyncio.gather(*jobs, return_exceptions=True)
+        jobs.clear()
+        for r in res:
+            if isinstance(r, BaseException):
+                raise r
+
+    # ============================================================ templates (controller.go:761-845)
+    async def sync_template(self, namespace: str, name: str) -> None:
+        template = self.template_lister.try_get(namespace, name)
+        if template is None:
+            log.debug("NexusAlgorithmTemplate %s/%s referenced by item in work queue no longer exists",
+                      namespace, name)
+            if self.options.queued_deletes:
+                await self.propagate_template_delete(namespace, name)
+            return
+        template = await self.report_template_init_condition(template)
+        await self.adopt_references(template)
+
+        shard_names = self.shard_names()
+        spec = template.get("spec")
+        spec_fp = fingerprint(spec) if self.options.slim_shard_cache else None
+        if self.options.concurrent_fanout:
+            results = await asyncio.gather(*(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards),
+                                           return_exceptions=True)
+            failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
+            for r in failures.values():
+                if isinstance(r, asyncio.CancelledError):
+                    raise r
+            if failures:
+                if not self.options.shard_failure_isolation:
+                    raise next(iter(failures.values()))
+                ok = [n for n in shard_names if n not in failures]
+                await self.report_template_synced_condition(
+                    template, secret_names(template), configmap_names(template), ok, ready=False,
+                    message=f"Algorithm {q(name)} failed to sync to shards: {', '.join(sorted(failures))}")
+                raise ShardSyncError(failures)
+        else:
+            for shard in self.shards:
+                await self._sync_template_to_shard(template, shard, spec_fp)
+
+        template = await self.report_template_synced_condition(template, secret_names(template),
+                                                               configmap_names(template), shard_names)
+        if self.options.event_on_noop or self._last_pass_wrote():
+            self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                C.MESSAGE_RESOURCE_SYNCED.format("NexusAlgorithmTemplate"), kind=C.TEMPLATE_KIND)
+
+    async def _sync_template_to_shard(self, template: dict, shard, spec_fp) -> None:
+        if self.options.wait_for_shards_timeout is not None and not shard.has_synced():
+            raise ShardNotReadyError(f"shard {shard.name} caches not synced")
+        ns = meta(template).get("namespace", "")
+        name = meta(template).get("name", "")
+        spec = template.get("spec")
+        shard_template = shard.template_lister.try_get(ns, name)
+        if shard_template is not None and not spec_matches(spec, shard_template):
+            log.debug("Content changed for NexusAlgorithmTemplate %s, updating", name)
+            shard_template = await self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
+                                               shard_template, spec, C.FIELD_MANAGER)
+        elif shard_template is None:
+            log.debug("Algorithm %s not found in shard %s, creating", name, shard.name)
+            shard_template = await self._write(shard, "create_template", shard.template_informer, R.TEMPLATES,
+                                               name, ns, spec, C.FIELD_MANAGER)
+        if self.options.concurrent_dependents:
+            await asyncio.gather(self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard),
+                                 self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard))
+        else:
+            await self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard)
+            await self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard)
+
+    async def _write(self, shard, op: str, informer, rt, *args):
+        """Issue a shard write; in native mode resolve create/update races by refetching."""
+        self._pass_wrote()
+        try:
+            return await getattr(shard, op)(*args)
+        except (E.AlreadyExists, E.Conflict) as e:
+            if not self.options.tolerate_write_races:
+                raise
+            # Our cache was stale: fetch the live object, publish it, let the caller continue from it.
+            target = args[0]
+            if isinstance(target, dict):
+                ns, nm = meta(target).get("namespace", ""), meta(target).get("name", "")
+            else:
+                nm, ns = args[0], args[1]
+            live = await shard.client.get(rt, ns, nm)
+            informer.store.assume(live)
+            if isinstance(e, E.Conflict) and op.startswith("update"):
+                retry_args = (informer.store.get(ns, nm) or live,) + tuple(args[1:])
+                return await getattr(shard, op)(*retry_args)
+            return informer.store.get(ns, nm) or live
+
+    async def _sync_dependents_to_shard(self, rt, template: dict, shard_template: dict, shard) -> None:
+        """syncSecretsToShard / syncConfigMapsToShard (controller.go:504-626)."""
+        is_secret = rt is R.SECRETS
+        # GetSecretNames() is read from the shard template (controller.go:505); its spec equals the
+        # controller's after create/update.  A slim-cache shard template carries no spec: use the source.
+        holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) else shard_template
+        names = secret_names(holder) if is_secret else configmap_names(holder)
+        if self.options.concurrent_dependents and len(names) > 1:
+            res = await asyncio.gather(*(self._sync_dependent(rt, template, shard_template, shard, n) for n in names),
+                                       return_exceptions=True)
+            for r in res:
+                if isinstance(r, BaseException):
+                    raise r
+        else:
+            for n in names:
+                await self._sync_dependent(rt, template, shard_template, shard, n)
+
+    async def _sync_dependent(self, rt, template: dict, shard_template: dict, shard, dep_name: str) -> None:
+        is_secret = rt is R.SECRETS
+        kind = rt.kind
+        tname = meta(template).get("name", "")
+        ns = meta(template).get("namespace", "")
+        lister = self.secret_lister if is_secret else self.configmap_lister
+        shard_lister = shard.secret_lister if is_secret else shard.configmap_lister
+        shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
+        src = lister.try_get(ns, dep_name)
+        if src is None:
+            self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
+                                C.MESSAGE_RESOURCE_MISSING.format(q(dep_name), q(tname)), kind=C.TEMPLATE_KIND)
+            lister.get(ns, dep_name)  # raises NotFound
+        shard_ns = meta(shard_template).get("namespace", "")
+
+        def fail(e: BaseException):
+            self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
+                                C.MESSAGE_RESOURCE_OPERATION_FAILED.format(q(dep_name), q(tname), e),
+                                kind=C.TEMPLATE_KIND)
+            return e
+
+        shard_obj = shard_lister.try_get(shard_ns, meta(src).get("name", ""))
+        if shard_obj is None:
+            try:
+                shard_obj = await self._write(shard, "create_secret" if is_secret else "create_configmap",
+                                              shard_informer, rt, shard_template, src, C.FIELD_MANAGER)
+            except Exception as e:  # noqa: BLE001
+                raise fail(e)
+        try:
+            missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind)
+        except RogueResourceError as e:
+            raise fail(e)
+        with_binary = self.options.sync_binary_data and not is_secret
+        differs = not data_matches(src, shard_obj, with_binary)
+        update = shard.update_secret if is_secret else shard.update_configmap
+        op = "update_secret" if is_secret else "update_configmap"
+
+        async def put(obj, data, owner):
+            args = (obj, data, owner, C.FIELD_MANAGER)
+            if with_binary:
+                args = args + (normalize_data(src.get("binaryData")),)
+            if self.options.tolerate_write_races:
+                return await self._write(shard, op, shard_informer, rt, *args)
+            self._pass_wrote()
+            return await update(*args)
+
+        try:
+            if self.options.single_put_dependents or SLIM_FP in shard_obj:
+                if differs or missing_owner:
+                    await put(shard_obj, normalize_data(src.get("data")) if (differs or SLIM_FP in shard_obj)
+                              else None, shard_template if missing_owner else None)
+            else:
+                if differs:
+                    log.debug("Content changed for %s %s, updating", kind, dep_name)
+                    await put(shard_obj, src.get("data"), None)
+                if missing_owner:
+                    log.debug("Ownership missing for %s %s, updating", kind, dep_name)
+                    # The reference re-uses the pre-update object here (controller.go:552,614).
+                    await put(shard_obj, None, shard_template)
+        except Exception as e:  # noqa: BLE001
+            raise fail(e)
+
+    async def propagate_template_delete(self, namespace: str, name: str) -> None:
+        """Level-triggered shard delete (native `queued_deletes`): retried through the queue."""
+        key = (namespace, name)
+        explicit = key in self._pending_deletes
+        jobs = []
+        for shard in self.shards:
+            st = shard.template_lister.try_get(namespace, name)
+            if st is None:
+                continue
+            if not explicit and not self._is_ours(st):
+                continue
+            jobs.append(self._delete_one(shard, shard.delete_template, st))
+        if jobs:
+            res = await asyncio.gather(*jobs, return_exceptions=True)
+            errs = [r for r in res if isinstance(r, BaseException)]
+            if errs:
+                raise errs[0]
+        self._pending_deletes.discard(key)
+
+    async def propagate_workgroup_delete(self, namespace: str, name: str) -> None:
+        key = (namespace, name)
+        explicit = key in self._pending_workgroup_deletes
+        jobs = []
+        for shard in self.shards:
+            sw = shard.workgroup_lister.try_get(namespace, name)
+            if sw is None or (not explicit and not self._is_ours(sw)):
+                continue
+            jobs.append(self._delete_one(shard, shard.delete_workgroup, sw))
+        if jobs:
+            res = await asyncio.gather(*jobs, return_exceptions=True)
+            errs = [r for r in res if isinstance(r, BaseException)]
+            if errs:
+                raise errs[0]
+        self._pending_workgroup_deletes.discard(key)
+
+    async def _delete_one(self, shard, fn, obj) -> None:
+        if self.options.wait_for_shards_timeout is not None and not shard.has_synced():
+            raise ShardNotReadyError(f"shard {shard.name} caches not synced")
+        try:
+            await fn(obj)
+        except E.NotFound:
+            pass
+
+    def _is_ours(self, obj: dict) -> bool:
+        lbl = meta(obj).get("labels") or {}
+        return lbl.get(C.LABEL_CONFIGURATION_OWNER) == self.alias and \
+            lbl.get(C.LABEL_CONTROLLER_APP) == C.CONTROLLER_AGENT_NAME
+
+    # ============================================================ workgroups (controller.go:697-756)
+    async def sync_workgroup(self, namespace: str, name: str) -> None:
+        workgroup = self.workgroup_lister.try_get(namespace, name)
+        if workgroup is None:
+            log.debug("NexusAlgorithmWorkgroup %s/%s referenced by item in work queue no longer exists",
+                      namespace, name)
+            if self.options.propagate_workgroup_deletes:
+                await self.propagate_workgroup_delete(namespace, name)
+            return
+        workgroup = await self.report_workgroup_init_condition(workgroup)
+        if self.options.concurrent_fanout:
+            results = await asyncio.gather(*(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards),
+                                           return_exceptions=True)
+            failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
+            if failures:
+                if self.options.shard_failure_isolation:
+                    await self.report_workgroup_synced_condition(
+                        workgroup, ready=False,
+                        message=f"Workgroup {q(name)} failed to sync to shards: {', '.join(sorted(failures))}")
+                    raise ShardSyncError(failures)
+                raise next(iter(failures.values()))
+        else:
+            for shard in self.shards:
+                await self._sync_workgroup_to_shard(workgroup, shard)
+        workgroup = await self.report_workgroup_synced_condition(workgroup)
+        if self.options.event_on_noop or self._last_pass_wrote():
+            self.recorder.event(workgroup, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                C.MESSAGE_RESOURCE_SYNCED.format("NexusAlgorithmWorkgroup"), kind=C.WORKGROUP_KIND)
+
+    async def _sync_workgroup_to_shard(self, workgroup: dict, shard) -> None:
+        if self.options.wait_for_shards_timeout is not None and not shard.has_synced():
+            raise ShardNotReadyError(f"shard {shard.name} caches not synced")
+        ns = meta(workgroup).get("namespace", "")
+        name = meta(workgroup).get("name", "")
+        spec = workgroup.get("spec")
+        sw = shard.workgroup_lister.try_get(ns, name)
+        if sw is not None and not spec_matches(spec, sw):
+            await self._write(shard, "update_workgroup", shard.workgroup_informer, R.WORKGROUPS, sw, spec,
+                              C.FIELD_MANAGER)
+        elif sw is None:
+            await self._write(shard, "create_workgroup", shard.workgroup_informer, R.WORKGROUPS, name, ns, spec,
+                              C.FIELD_MANAGER)
+
+    def shard_names(self) -> list[str]:
+        return [s.name for s in self.shards]

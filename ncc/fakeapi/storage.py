@@ -1,0 +1,426 @@
+"""In-memory versioned object store with watch fan-out and ownerRef garbage collection.
+
+This is the state machine behind both the HTTP fake kube-apiserver (`ncc.fakeapi.server`)
+and the in-process recording client (`ncc.testing.fake_client`).  It stands in for the
+envtest/kind clusters the reference's CI provisions (.github/workflows/build.yaml:44-66)
+and implements the apiserver behaviours the controller depends on:
+
+* monotonically increasing integer resourceVersions (one counter per cluster, like etcd);
+* list + watch from a resourceVersion with replay from a bounded history and
+  `410 Gone` once the requested version has been compacted away;
+* status subresource isolation (main-resource writes ignore `.status`, `/status` writes
+  touch only `.status`) and no-op updates that neither bump the RV nor emit events;
+* optimistic concurrency (`409 Conflict` on a stale `metadata.resourceVersion`);
+* `AlreadyExists` on create, UID/creationTimestamp/generation management;
+* background-style garbage collection: deleting an owner deletes dependents whose owners
+  are all gone and strips dangling references from dependents that keep a live owner.
+
+`simple=True` switches to client-go `fake.NewSimpleClientset` semantics used by the parity
+tests (no UIDs, no RVs, no conflict checks, no GC, status stored verbatim) so recorded
+request objects match the reference's expected actions (controller_test.go:383-466).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import uuid
+from collections import deque
+from typing import Callable
+
+from ..api import resources as R
+from ..api import selectors
+from ..api.objects import deep_copy, now_rfc3339
+from ..api.patch import apply_patch, json_patch, merge_patch, strategic_merge_patch
+from ..api.resources import ResourceType
+from ..kube import errors as E
+from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+
+RtKey = tuple  # (group, plural)
+
+
+class EventRecord:
+    __slots__ = ("rv", "rt_key", "namespace", "type", "obj", "_line")
+
+    def __init__(self, rv: int, rt_key: RtKey, namespace: str, type_: str, obj: dict):
+        self.rv, self.rt_key, self.namespace, self.type, self.obj = rv, rt_key, namespace, type_, obj
+        self._line = None
+
+    def line(self) -> bytes:
+        """Serialised watch-stream line, computed once and shared by every watcher."""
+        if self._line is None:
+            self._line = json.dumps({"type": self.type, "object": self.obj}, separators=(",", ":")).encode() + b"\n"
+        return self._line
+
+
+class Watcher:
+    def __init__(self, state: "ClusterState", rt_key: RtKey, namespace: str | None, selector: str | None):
+        self.state = state
+        self.rt_key = rt_key
+        self.namespace = namespace or None
+        self.match_labels = selectors.parse(selector)
+        self.queue: asyncio.Queue = asyncio.Queue()
+        self.closed = False
+
+    def wants(self, rec: EventRecord) -> bool:
+        if rec.rt_key != self.rt_key:
+            return False
+        if self.namespace and rec.namespace != self.namespace:
+            return False
+        return self.match_labels((rec.obj.get("metadata") or {}).get("labels") or {})
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            self.state._watchers.discard(self)
+            self.queue.put_nowait(None)
+
+
+def _conflict(rt: ResourceType, name: str) -> E.Conflict:
+    gr = f"{rt.plural}.{rt.group}" if rt.group else rt.plural
+    return E.Conflict(f'Operation cannot be fulfilled on {gr} "{name}": the object has been modified; '
+                      f"please apply your changes to the latest version and try again",
+                      details={"name": name, "kind": rt.plural, "group": rt.group})
+
+
+def _not_found(rt: ResourceType, name: str) -> E.NotFound:
+    gr = f"{rt.plural}.{rt.group}" if rt.group else rt.plural
+    return E.NotFound(f'{gr} "{name}" not found', details={"name": name, "kind": rt.plural, "group": rt.group})
+
+
+def _content(obj: dict) -> dict:
+    """Everything except metadata and status — the part whose change bumps `generation`."""
+    return {k: v for k, v in obj.items() if k not in ("metadata", "status", "apiVersion", "kind")}
+
+
+class ClusterState:
+    def __init__(self, name: str = "cluster", *, simple: bool = False, history: int = 500_000,
+                 status_subresource: bool = True):
+        self.name = name
+        self.simple = simple
+        self.status_subresource = status_subresource and not simple
+        self.rv = 0
+        self._objects: dict[RtKey, dict[str, dict[str, dict]]] = {}
+        self._types: dict[RtKey, ResourceType] = {(rt.group, rt.plural): rt for rt in R.BUILTIN}
+        self._history: deque[EventRecord] = deque(maxlen=max(history, 1))
+        self._watchers: set[Watcher] = set()
+        self._uids: dict[str, tuple] = {}  # uid -> (rt_key, ns, name)
+        self._dependents: dict[str, set] = {}  # owner uid -> {(rt_key, ns, name)}
+        self.write_hooks: list[Callable[[str, ResourceType, dict], None]] = []
+        self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
+                      "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
+
+    # ------------------------------------------------------------------ registry
+    def register(self, rt: ResourceType) -> None:
+        self._types[(rt.group, rt.plural)] = rt
+
+    def resource(self, group: str, plural: str) -> ResourceType:
+        rt = self._types.get((group, plural))
+        if rt is None:
+            raise E.NotFound(f"the server could not find the requested resource ({plural}.{group})")
+        return rt
+
+    def _bucket(self, rt: ResourceType, ns: str) -> dict[str, dict]:
+        by_ns = self._objects.setdefault((rt.group, rt.plural), {})
+        b = by_ns.get(ns)
+        if b is None:
+            b = by_ns[ns] = {}
+        return b
+
+    # ------------------------------------------------------------------ events
+    def _next_rv(self) -> int:
+        self.rv += 1
+        return self.rv
+
+    def _emit(self, rv: int, rt: ResourceType, ns: str, type_: str, obj: dict) -> None:
+        rec = EventRecord(rv, (rt.group, rt.plural), ns, type_, obj)
+        if not self.simple:
+            self._history.append(rec)
+        for w in tuple(self._watchers):
+            if w.wants(rec):
+                w.queue.put_nowait(rec)
+        for hook in self.write_hooks:
+            hook(type_, rt, obj)
+
+    # ------------------------------------------------------------------ owner index
+    def _index_owners(self, rt: ResourceType, obj: dict, add: bool) -> None:
+        if self.simple:
+            return
+        m = obj.get("metadata") or {}
+        ref = ((rt.group, rt.plural), m.get("namespace", "") or "", m.get("name", ""))
+        for o in m.get("ownerReferences") or ():
+            u = o.get("uid")
+            if not u:
+                continue
+            if add:
+                self._dependents.setdefault(u, set()).add(ref)
+            else:
+                s = self._dependents.get(u)
+                if s is not None:
+                    s.discard(ref)
+                    if not s:
+                        del self._dependents[u]
+
+    # ------------------------------------------------------------------ reads
+    def get(self, rt: ResourceType, ns: str, name: str) -> dict:
+        self.stats["get"] += 1
+        obj = self._bucket(rt, ns if rt.namespaced else "").get(name)
+        if obj is None:
+            raise _not_found(rt, name)
+        return obj
+
+    def list(self, rt: ResourceType, ns: str | None, *, label_selector: str | None = None,
+             limit: int | None = None, continue_token: str | None = None) -> dict:
+        self.stats["list"] += 1
+        match = selectors.parse(label_selector)
+        by_ns = self._objects.get((rt.group, rt.plural), {})
+        if ns and rt.namespaced:
+            buckets = [(ns, by_ns.get(ns, {}))]
+        else:
+            buckets = sorted(by_ns.items())
+        start_after = None
+        list_rv = self.rv
+        if continue_token:
+            try:
+                tok = json.loads(base64.urlsafe_b64decode(continue_token.encode()).decode())
+                start_after, list_rv = tuple(tok["k"]), int(tok["rv"])
+            except Exception as e:  # noqa: BLE001
+                raise E.BadRequest(f"invalid continue token: {e}")
+        items = []
+        next_tok = None
+        for bns, b in buckets:
+            for nm in sorted(b):
+                if start_after is not None and (bns, nm) <= start_after:
+                    continue
+                o = b[nm]
+                if label_selector and not match((o.get("metadata") or {}).get("labels") or {}):
+                    continue
+                if limit and len(items) >= limit:
+                    last = items[-1]["metadata"]
+                    next_tok = base64.urlsafe_b64encode(json.dumps(
+                        {"k": [last.get("namespace", ""), last["name"]], "rv": list_rv}).encode()).decode()
+                    break
+                items.append(o)
+            if next_tok:
+                break
+        lmeta = {"resourceVersion": str(list_rv)}
+        if next_tok:
+            lmeta["continue"] = next_tok
+        return {"apiVersion": rt.api_version, "kind": rt.list_kind, "metadata": lmeta, "items": items}
+
+    # ------------------------------------------------------------------ writes
+    def create(self, rt: ResourceType, ns: str, obj: dict) -> dict:
+        obj = deep_copy(obj)
+        m = obj.setdefault("metadata", {})
+        ns = ns if rt.namespaced else ""
+        if rt.namespaced:
+            if m.get("namespace") and ns and m["namespace"] != ns:
+                raise E.BadRequest("the namespace of the provided object does not match the namespace sent on the request")
+            m["namespace"] = ns or m.get("namespace", "")
+            ns = m["namespace"]
+        name = m.get("name")
+        if not name:
+            gen = m.get("generateName")
+            if not gen:
+                raise E.Invalid("metadata.name: Required value: name or generateName is required")
+            name = m["name"] = gen + uuid.uuid4().hex[:5]
+        b = self._bucket(rt, ns)
+        if name in b:
+            gr = f"{rt.plural}.{rt.group}" if rt.group else rt.plural
+            raise E.AlreadyExists(f'{gr} "{name}" already exists', details={"name": name, "kind": rt.plural})
+        if not self.simple:
+            if m.get("resourceVersion"):
+                raise E.BadRequest("resourceVersion should not be set on objects to be created")
+            m["uid"] = str(uuid.uuid4())
+            m["creationTimestamp"] = now_rfc3339()
+            m["generation"] = 1
+            m["resourceVersion"] = str(self._next_rv())
+            obj["apiVersion"] = rt.api_version
+            obj["kind"] = rt.kind
+            if self.status_subresource and rt.has_status:
+                obj.pop("status", None)
+            self._uids[m["uid"]] = ((rt.group, rt.plural), ns, name)
+        b[name] = obj
+        self._index_owners(rt, obj, True)
+        self.stats["create"] += 1
+        self._emit(self.rv, rt, ns, "ADDED", obj)
+        return obj
+
+    def update(self, rt: ResourceType, ns: str, obj: dict, *, subresource: str | None = None) -> dict:
+        ns = ns if rt.namespaced else ""
+        m_in = obj.get("metadata") or {}
+        name = m_in.get("name", "")
+        b = self._bucket(rt, ns)
+        cur = b.get(name)
+        if cur is None:
+            raise _not_found(rt, name)
+        if self.simple:
+            new = deep_copy(obj)
+            b[name] = new
+            self.stats["status" if subresource == "status" else "update"] += 1
+            self._emit(self.rv, rt, ns, "MODIFIED", new)
+            return new
+        cm = cur["metadata"]
+        rv_in = m_in.get("resourceVersion")
+        if rv_in and rv_in != cm.get("resourceVersion"):
+            self.stats["conflict"] += 1
+            raise _conflict(rt, name)
+        if subresource == "status":
+            new = dict(cur)
+            if "status" in obj:
+                new["status"] = deep_copy(obj["status"])
+            else:
+                new.pop("status", None)
+            new["metadata"] = dict(cm)
+        else:
+            new = deep_copy(obj)
+            nm = new.setdefault("metadata", {})
+            for k in ("uid", "creationTimestamp", "namespace", "name", "generation", "deletionTimestamp"):
+                if k in cm:
+                    nm[k] = cm[k]
+                else:
+                    nm.pop(k, None)
+            new["apiVersion"] = rt.api_version
+            new["kind"] = rt.kind
+            if self.status_subresource and rt.has_status:
+                if "status" in cur:
+                    new["status"] = cur["status"]
+                else:
+                    new.pop("status", None)
+            if _content(new) != _content(cur):
+                nm["generation"] = int(cm.get("generation", 1)) + 1
+        new["metadata"]["resourceVersion"] = cm.get("resourceVersion")
+        if new == cur:
+            self.stats["noop_update"] += 1
+            return cur
+        new["metadata"]["resourceVersion"] = str(self._next_rv())
+        self._index_owners(rt, cur, False)
+        b[name] = new
+        self._index_owners(rt, new, True)
+        self.stats["status" if subresource == "status" else "update"] += 1
+        self._emit(self.rv, rt, ns, "MODIFIED", new)
+        return new
+
+    def patch(self, rt: ResourceType, ns: str, name: str, body, patch_type: str, *,
+              subresource: str | None = None) -> dict:
+        self.stats["patch"] += 1
+        ns = ns if rt.namespaced else ""
+        cur = self._bucket(rt, ns).get(name)
+        if patch_type == PATCH_APPLY:
+            if cur is None:
+                body = dict(body)
+                body.setdefault("metadata", {}).setdefault("name", name)
+                return self.create(rt, ns, body)
+            new = apply_patch(cur, body)
+        else:
+            if cur is None:
+                raise _not_found(rt, name)
+            if patch_type == PATCH_JSON:
+                try:
+                    new = json_patch(cur, body)
+                except Exception as e:  # noqa: BLE001
+                    raise E.Invalid(f"json patch failed: {e}")
+            elif patch_type == PATCH_STRATEGIC:
+                new = strategic_merge_patch(cur, body)
+            elif patch_type == PATCH_MERGE:
+                new = merge_patch(cur, body)
+            else:
+                raise E.ApiError(f"unsupported patch type {patch_type}", code=415, reason="UnsupportedMediaType")
+        new = dict(new)
+        new["metadata"] = dict(new.get("metadata") or {})
+        # a patch carries no precondition unless it sets one explicitly
+        want_rv = ((body.get("metadata") or {}) if isinstance(body, dict) else {}).get("resourceVersion")
+        new["metadata"]["resourceVersion"] = want_rv or cur["metadata"].get("resourceVersion")
+        return self.update(rt, ns, new, subresource=subresource)
+
+    def delete(self, rt: ResourceType, ns: str, name: str, *, preconditions: dict | None = None,
+               propagation_policy: str | None = None) -> dict:
+        ns = ns if rt.namespaced else ""
+        b = self._bucket(rt, ns)
+        cur = b.get(name)
+        if cur is None:
+            raise _not_found(rt, name)
+        cm = cur.get("metadata") or {}
+        if preconditions:
+            if preconditions.get("uid") and preconditions["uid"] != cm.get("uid"):
+                raise _conflict(rt, name)
+            if preconditions.get("resourceVersion") and preconditions["resourceVersion"] != cm.get("resourceVersion"):
+                raise _conflict(rt, name)
+        del b[name]
+        self.stats["delete"] += 1
+        if self.simple:
+            self._emit(self.rv, rt, ns, "DELETED", cur)
+            return cur
+        self._index_owners(rt, cur, False)
+        u = cm.get("uid")
+        if u:
+            self._uids.pop(u, None)
+        gone = dict(cur)
+        gone["metadata"] = dict(cm, resourceVersion=str(self._next_rv()))
+        self._emit(self.rv, rt, ns, "DELETED", gone)
+        if u:
+            self._collect(u, orphan=(propagation_policy == "Orphan"))
+        return gone
+
+    def _collect(self, owner_uid: str, orphan: bool = False) -> None:
+        """Garbage-collect dependents of a deleted owner (K8s GC `attemptToDeleteItem`)."""
+        deps = self._dependents.pop(owner_uid, set())
+        for rt_key, ns, nm in sorted(deps):
+            rt = self._types[rt_key]
+            obj = self._bucket(rt, ns).get(nm)
+            if obj is None:
+                continue
+            refs = (obj.get("metadata") or {}).get("ownerReferences") or []
+            solid = [r for r in refs if r.get("uid") in self._uids]
+            if solid and not orphan:
+                self.update(rt, ns, _with_refs(obj, solid))
+            elif orphan:
+                self.update(rt, ns, _with_refs(obj, [r for r in refs if r.get("uid") != owner_uid]))
+            else:
+                self.stats["gc_delete"] += 1
+                self.delete(rt, ns, nm)
+
+    # ------------------------------------------------------------------ watch
+    def watch(self, rt: ResourceType, ns: str | None, resource_version: str | None,
+              label_selector: str | None = None) -> Watcher:
+        self.stats["watch"] += 1
+        w = Watcher(self, (rt.group, rt.plural), ns if rt.namespaced else None, label_selector)
+        if resource_version in (None, "", "0"):
+            for obj in self.list(rt, ns, label_selector=label_selector)["items"]:
+                w.queue.put_nowait(EventRecord(self.rv, w.rt_key, (obj.get("metadata") or {}).get("namespace", ""),
+                                               "ADDED", obj))
+        else:
+            try:
+                since = int(resource_version)
+            except ValueError:
+                raise E.BadRequest(f"invalid resourceVersion {resource_version!r}")
+            if since < self.rv:
+                if not self._history or self._history[0].rv > since + 1:
+                    raise E.Gone(f"too old resource version: {since} ({self._history[0].rv - 1 if self._history else self.rv})")
+                for rec in self._history:
+                    if rec.rv > since and w.wants(rec):
+                        w.queue.put_nowait(rec)
+        self._watchers.add(w)
+        return w
+
+    def compact(self) -> None:
+        """Drop all watch history (forces 410 Gone on every resume), like an etcd compaction."""
+        self._history.clear()
+
+    def close_watchers(self) -> None:
+        for w in tuple(self._watchers):
+            w.close()
+
+    def count(self, rt: ResourceType, ns: str | None = None) -> int:
+        by_ns = self._objects.get((rt.group, rt.plural), {})
+        if ns:
+            return len(by_ns.get(ns, {}))
+        return sum(len(b) for b in by_ns.values())
+
+
+def _with_refs(obj: dict, refs: list) -> dict:
+    o = dict(obj)
+    o["metadata"] = dict(obj.get("metadata") or {}, ownerReferences=refs)
+    if not refs:
+        o["metadata"].pop("ownerReferences")
+    return o

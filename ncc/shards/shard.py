@@ -1,0 +1,190 @@
+"""A connected shard cluster: its client, its four namespace-scoped informers, and the write ops.
+
+Re-creates nexus-core `shards.Shard` whose source is not in the
+reference; the object shapes are pinned by the reference's test expectations:
+
+* `create_template` / `create_workgroup`  — X8a/X8d: `{apiVersion, kind, metadata{name, namespace,
+  labels: OwnerLabels}, spec}`; status is not copied (controller_test.go:190-196).
+* `update_template` / `update_workgroup`  — X8b/X8d: the shard object with `spec` replaced; shard
+  metadata (UID, labels) preserved (controller_test.go:1099-1136, 1234-1285).
+* `delete_template`                       — X8c: delete by namespace/name.
+* `create_secret` / `create_configmap`     — X8e: copy of the controller object's content into the
+  shard template's namespace, `labels = OwnerLabels`, `ownerReferences = [shard template]`
+  (controller_test.go:198-228).
+* `update_secret` / `update_configmap`     — X8f: replace `data` when given, append the owner ref
+  when given, preserve everything else (controller_test.go:970-1006, 1085-1087).
+
+Native-mode additions: `assume_writes` publishes every write result into the informer's
+mutation overlay; `sync_binary_data` also carries `ConfigMap.binaryData`; deletes for
+workgroups and dependents support the orphan sweep.
+"""
+from __future__ import annotations
+
+from ..api import constants as C
+from ..api import resources as R
+from ..api.objects import meta
+from ..api.refs import template_owner_ref
+from ..cache.informer import Informer, InformerFactory
+from ..kube.client import KubeClient
+
+
+class Shard:
+    def __init__(self, owner_alias: str, name: str, client: KubeClient, namespace: str, *,
+                 resync_period: float = 0.0, assume_writes: bool = False, sync_binary_data: bool = False,
+                 transforms: dict | None = None, informer_kw: dict | None = None):
+        self.owner_alias = owner_alias
+        self.name = name
+        self.client = client
+        self.namespace = namespace
+        self.assume_writes = assume_writes
+        self.sync_binary_data = sync_binary_data
+        self.labels = C.owner_labels(owner_alias)
+        transforms = transforms or {}
+        self.factory = InformerFactory(client, namespace, resync_period, **(informer_kw or {}))
+        self.template_informer: Informer = self.factory.informer(R.TEMPLATES, transform=transforms.get(R.TEMPLATES))
+        self.workgroup_informer: Informer = self.factory.informer(R.WORKGROUPS, transform=transforms.get(R.WORKGROUPS))
+        self.secret_informer: Informer = self.factory.informer(R.SECRETS, transform=transforms.get(R.SECRETS))
+        self.configmap_informer: Informer = self.factory.informer(R.CONFIGMAPS, transform=transforms.get(R.CONFIGMAPS))
+        self.template_lister = self.template_informer.lister
+        self.workgroup_lister = self.workgroup_informer.lister
+        self.secret_lister = self.secret_informer.lister
+        self.configmap_lister = self.configmap_informer.lister
+        self.healthy = True  # flipped by the controller's per-shard circuit breaker
+
+    # ---------------------------------------------------------------- lifecycle
+    def start(self) -> None:
+        self.factory.start()
+
+    async def stop(self) -> None:
+        await self.factory.stop()
+        await self.client.close()
+
+    def has_synced(self) -> bool:
+        return self.factory.has_synced()
+
+    async def wait_for_sync(self, timeout: float | None = None) -> bool:
+        return await self.factory.wait_for_sync(timeout)
+
+    def _assume(self, informer: Informer, obj):
+        if self.assume_writes and isinstance(obj, dict):
+            informer.store.assume(obj)
+        return obj
+
+    # ---------------------------------------------------------------- templates
+    async def create_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
+        obj = {
+            "apiVersion": C.API_VERSION,
+            "kind": C.TEMPLATE_KIND,
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
+            "spec": spec,
+        }
+        res = await self.client.create(R.TEMPLATES, namespace, obj, field_manager=field_manager)
+        return self._assume(self.template_informer, res)
+
+    async def update_template(self, shard_obj: dict, spec, field_manager: str) -> dict:
+        obj = _strip_slim(dict(shard_obj))
+        obj["spec"] = spec
+        res = await self.client.update(R.TEMPLATES, meta(shard_obj).get("namespace", ""), obj,
+                                       field_manager=field_manager)
+        return self._assume(self.template_informer, res)
+
+    async def delete_template(self, obj: dict) -> None:
+        m = meta(obj)
+        await self.client.delete(R.TEMPLATES, m.get("namespace", ""), m.get("name", ""))
+
+    # ---------------------------------------------------------------- workgroups
+    async def create_workgroup(self, name: str, namespace: str, spec, field_manager: str) -> dict:
+        obj = {
+            "apiVersion": C.API_VERSION,
+            "kind": C.WORKGROUP_KIND,
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
+            "spec": spec,
+        }
+        res = await self.client.create(R.WORKGROUPS, namespace, obj, field_manager=field_manager)
+        return self._assume(self.workgroup_informer, res)
+
+    async def update_workgroup(self, shard_obj: dict, spec, field_manager: str) -> dict:
+        obj = _strip_slim(dict(shard_obj))
+        obj["spec"] = spec
+        res = await self.client.update(R.WORKGROUPS, meta(shard_obj).get("namespace", ""), obj,
+                                       field_manager=field_manager)
+        return self._assume(self.workgroup_informer, res)
+
+    async def delete_workgroup(self, obj: dict) -> None:
+        m = meta(obj)
+        await self.client.delete(R.WORKGROUPS, m.get("namespace", ""), m.get("name", ""))
+
+    # ---------------------------------------------------------------- dependents
+    def _dependent_body(self, rt: R.ResourceType, shard_template: dict, src: dict) -> dict:
+        obj = {
+            "apiVersion": "v1",
+            "kind": rt.kind,
+            "metadata": {
+                "name": meta(src).get("name", ""),
+                "namespace": meta(shard_template).get("namespace", ""),
+                "labels": dict(self.labels),
+                "ownerReferences": [template_owner_ref(shard_template)],
+            },
+        }
+        if src.get("data") is not None:
+            obj["data"] = src["data"]
+        if rt is R.SECRETS:
+            if src.get("type"):
+                obj["type"] = src["type"]
+        elif self.sync_binary_data and src.get("binaryData") is not None:
+            obj["binaryData"] = src["binaryData"]
+        return obj
+
+    def _updated_dependent(self, shard_obj: dict, data, new_owner: dict | None, binary_data=None) -> dict:
+        obj = _strip_slim(dict(shard_obj))
+        if data is not None:
+            obj["data"] = data
+        if binary_data is not None:
+            if binary_data:
+                obj["binaryData"] = binary_data
+            else:
+                obj.pop("binaryData", None)
+        if new_owner is not None:
+            m = dict(meta(shard_obj))
+            refs = list(m.get("ownerReferences") or [])
+            new_ref = template_owner_ref(new_owner)
+            if not any(r.get("uid") == new_ref["uid"] and r.get("kind") == new_ref["kind"] for r in refs):
+                refs.append(new_ref)
+            m["ownerReferences"] = refs
+            obj["metadata"] = m
+        return obj
+
+    async def create_secret(self, shard_template: dict, secret: dict, field_manager: str) -> dict:
+        body = self._dependent_body(R.SECRETS, shard_template, secret)
+        res = await self.client.create(R.SECRETS, body["metadata"]["namespace"], body, field_manager=field_manager)
+        return self._assume(self.secret_informer, res)
+
+    async def update_secret(self, shard_secret: dict, data, new_owner: dict | None, field_manager: str) -> dict:
+        body = self._updated_dependent(shard_secret, data, new_owner)
+        res = await self.client.update(R.SECRETS, meta(shard_secret).get("namespace", ""), body,
+                                       field_manager=field_manager)
+        return self._assume(self.secret_informer, res)
+
+    async def create_configmap(self, shard_template: dict, configmap: dict, field_manager: str) -> dict:
+        body = self._dependent_body(R.CONFIGMAPS, shard_template, configmap)
+        res = await self.client.create(R.CONFIGMAPS, body["metadata"]["namespace"], body,
+                                       field_manager=field_manager)
+        return self._assume(self.configmap_informer, res)
+
+    async def update_configmap(self, shard_configmap: dict, data, new_owner: dict | None, field_manager: str,
+                               binary_data=None) -> dict:
+        body = self._updated_dependent(shard_configmap, data, new_owner, binary_data)
+        res = await self.client.update(R.CONFIGMAPS, meta(shard_configmap).get("namespace", ""), body,
+                                       field_manager=field_manager)
+        return self._assume(self.configmap_informer, res)
+
+    async def delete_dependent(self, rt: R.ResourceType, obj: dict) -> None:
+        m = meta(obj)
+        await self.client.delete(rt, m.get("namespace", ""), m.get("name", ""))
+
+
+def _strip_slim(obj: dict) -> dict:
+    """Drop the slim-cache digest key before an object is sent back to an apiserver."""
+    from ..api.fingerprint import SLIM_FP
+    obj.pop(SLIM_FP, None)
+    return obj
