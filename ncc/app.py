@@ -1,0 +1,191 @@
+"""Process entry point: `python -m ncc` (reference `main()`, main.go:35-109).
+
+Boot sequence, as in the reference:
+  signals → config → logger + statsd → controller-cluster client → namespace-scoped informers
+  (resync 30 s) → shards from the kubeconfig directory (informers started) → controller →
+  start controller informers → `controller.run()` until SIGTERM/SIGINT.
+A setup error exits with status 1 (`klog.FlushAndExit`).  Unlike the reference
+(main.go:97-103) the controller is built *before* anything is started, so a construction
+error cannot leave informers running.
+
+`mode=compat` reproduces the reference's runtime semantics including client-go's default
+client-side QPS (5/burst 10 per API group) — used for baseline measurements;
+`mode=native` (default) enables the improvements in `ControllerOptions.native()`.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+
+from . import __version__
+from .api import constants as C
+from .api import resources as R
+from .cache.informer import InformerFactory
+from .config import AppConfig, load_config
+from .controller.controller import Controller
+from .controller.events import BroadcastRecorder
+from .controller.options import ControllerOptions
+from .kube.client import RateLimitedClient
+from .kube.kubeconfig import build_config
+from .kube.rest import RestClient
+from .shards.loader import default_client_factory, load_shards
+from .telemetry.logging import configure_logging
+from .telemetry.statsd import MultiMetrics, StatsdClient
+
+log = logging.getLogger("ncc")
+
+COMPAT_QPS, COMPAT_BURST = 5.0, 10  # client-go rest.DefaultQPS / DefaultBurst
+
+
+def options_from_config(cfg: AppConfig) -> ControllerOptions:
+    kw = dict(workers=cfg.workers, failure_base_delay=cfg.failure_rate_base_delay,
+              failure_max_delay=cfg.failure_rate_max_delay, rate_limit_qps=float(cfg.rate_limit_elements_per_second),
+              rate_limit_burst=cfg.rate_limit_elements_burst, resync_period=cfg.resync_period)
+    if cfg.mode == "native":
+        kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout)
+    return ControllerOptions.for_mode(cfg.mode, **kw)
+
+
+def client_limits(cfg: AppConfig) -> tuple[float, int]:
+    if cfg.client_qps > 0:
+        return cfg.client_qps, cfg.client_burst
+    if cfg.mode == "compat":
+        return COMPAT_QPS, COMPAT_BURST
+    return 0.0, cfg.client_burst
+
+
+class App:
+    """Wires and owns every component of one controller process."""
+
+    def __init__(self, cfg: AppConfig, *, client_factory=None, controller_client=None, metrics=None,
+                 options: ControllerOptions | None = None):
+        self.cfg = cfg
+        self.options = options or options_from_config(cfg)
+        qps, burst = client_limits(cfg)
+        self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size)
+        self._controller_client = controller_client
+        self.metrics = metrics
+        self.ops = None
+        self.controller: Controller | None = None
+
+    async def build(self) -> Controller:
+        cfg, o = self.cfg, self.options
+        prom = None
+        if self.metrics is None:
+            sinks = [StatsdClient(C.METRIC_NAMESPACE)]
+            if cfg.metrics_bind_address:
+                from .telemetry.http import PrometheusMetrics
+                prom = PrometheusMetrics(C.METRIC_NAMESPACE)
+                sinks.append(prom)
+            self.metrics = MultiMetrics(*sinks)
+        client = self._controller_client
+        if client is None:
+            qps, burst = client_limits(cfg)
+            client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.client_pool_size,
+                                cluster_name=cfg.alias)
+            if qps > 0:
+                client = RateLimitedClient(client, qps, burst)
+        self.client = client
+        self.factory = InformerFactory(client, cfg.controller_namespace, o.resync_period)
+        infs = {rt: self.factory.informer(rt) for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
+        self.shards = load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
+                                  client_factory=self.client_factory,
+                                  resync_period=0.0 if o.watch_shards else o.resync_period,
+                                  assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
+                                  slim=o.slim_shard_cache, start=False)
+        self.recorder = BroadcastRecorder(client, log_events=log.isEnabledFor(logging.DEBUG))
+        self.controller = Controller(alias=cfg.alias, namespace=cfg.controller_namespace, client=client,
+                                     shards=self.shards, template_informer=infs[R.TEMPLATES],
+                                     workgroup_informer=infs[R.WORKGROUPS], secret_informer=infs[R.SECRETS],
+                                     configmap_informer=infs[R.CONFIGMAPS], options=o, recorder=self.recorder,
+                                     metrics=self.metrics)
+        if cfg.metrics_bind_address or cfg.health_bind_address:
+            from .telemetry.http import OpsServer
+            self.ops = OpsServer(ready=lambda: self.controller is not None and self.controller.ready.is_set(),
+                                 prometheus=prom, extra=self.debug_state)
+        return self.controller
+
+    def debug_state(self) -> dict:
+        c = self.controller
+        return {"queue_depth": len(c.queue), "stats": c.stats, "queue": c.queue.metrics,
+                "shards": {s.name: {"synced": s.has_synced()} for s in c.shards},
+                "events": self.recorder.stats}
+
+    async def run(self, stop: asyncio.Event) -> None:
+        controller = self.controller or await self.build()
+        if self.ops is not None:
+            await self.ops.start(self.cfg.health_bind_address or self.cfg.metrics_bind_address)
+        for s in self.shards:
+            s.start()
+        self.recorder.start()
+        self.factory.start()
+        log.info("nexus-configuration-controller %s starting: mode=%s alias=%s namespace=%s shards=%s workers=%d",
+                 __version__, self.cfg.mode, self.cfg.alias, self.cfg.controller_namespace,
+                 [s.name for s in self.shards], self.options.workers)
+        try:
+            await controller.run(stop)
+        finally:
+            await self.close()
+
+    async def close(self) -> None:
+        await self.recorder.stop()
+        await self.factory.stop()
+        for s in self.shards:
+            await s.stop()
+        await self.client.close()
+        if self.ops is not None:
+            await self.ops.stop()
+        if self.metrics is not None:
+            self.metrics.close()
+
+
+def setup_signal_handler(stop: asyncio.Event) -> None:
+    """signals.SetupSignalHandler: first SIGINT/SIGTERM cancels, a second one exits immediately."""
+    loop = asyncio.get_running_loop()
+    hits = {"n": 0}
+
+    def on_signal():
+        hits["n"] += 1
+        if hits["n"] > 1:
+            os._exit(1)
+        stop.set()
+
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, on_signal)
+        except (NotImplementedError, RuntimeError):  # pragma: no cover - non-main thread
+            pass
+
+
+async def _amain(cfg: AppConfig) -> int:
+    stop = asyncio.Event()
+    setup_signal_handler(stop)
+    app = App(cfg)
+    try:
+        await app.build()
+    except Exception as e:  # noqa: BLE001
+        log.error("Error building controller: %s", e)
+        return 1
+    await app.run(stop)
+    return 0
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(prog="python -m ncc", description="Nexus multi-cluster configuration controller")
+    p.add_argument("--config-dir", default=None, help="directory holding appconfig.yaml (default: cwd)")
+    p.add_argument("--version", action="store_true")
+    args = p.parse_args(argv)
+    if args.version:
+        print(__version__)
+        return 0
+    try:
+        cfg = load_config(args.config_dir)
+    except ValueError as e:
+        print(f"configuration error: {e}", file=sys.stderr)
+        return 1
+    configure_logging(cfg.log_level, cfg.log_format)
+    return asyncio.run(_amain(cfg))

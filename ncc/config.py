@@ -1,0 +1,137 @@
+"""Application configuration: `appconfig.yaml` + `appconfig.<env>.yaml` + `NEXUS__*` environment.
+
+Reference contract:
+* typed target `AppConfig` with ten keys (pkg/models/app_config.go:21-32);
+* nexus-core `LoadConfig[T]` reads `appconfig.yaml`, overlays `appconfig.<APPLICATION_ENVIRONMENT>.yaml`
+  (CI sets `local`, build.yaml:79), then environment overrides with the `NEXUS__` prefix where the
+  key's `-` becomes `_` and the name is upper-cased (deployment.yaml:50-69, build.yaml:68-79);
+* durations are Go duration strings (`30ms`, `5s`, `1m30s`).
+The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an empty value means
+"not set here".  Unset keys take the Helm chart's defaults (values.yaml:135-169) rather than
+Go zero values, so a bare `python -m ncc` is usable.
+
+Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
+`client-burst`, `client-pool-size`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`metrics-bind-address`, `health-bind-address`, `log-format`.
+"""
+from __future__ import annotations
+
+import os
+import re
+from dataclasses import dataclass, field, fields
+
+import yaml
+
+ENV_PREFIX = "NEXUS__"
+
+_DUR_RE = re.compile(r"([0-9]*\.?[0-9]+)(ns|us|µs|μs|ms|s|m|h)")
+_UNITS = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "μs": 1e-6, "ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0}
+
+
+def parse_duration(v) -> float:
+    """Go `time.ParseDuration` → seconds.  Bare numbers are taken as seconds."""
+    if isinstance(v, (int, float)):
+        return float(v)
+    s = str(v).strip()
+    if not s:
+        raise ValueError("empty duration")
+    sign = 1.0
+    if s[0] in "+-":
+        sign = -1.0 if s[0] == "-" else 1.0
+        s = s[1:]
+    if s == "0":
+        return 0.0
+    try:
+        return sign * float(s)
+    except ValueError:
+        pass
+    pos, total = 0, 0.0
+    for m in _DUR_RE.finditer(s):
+        if m.start() != pos:
+            raise ValueError(f"invalid duration {v!r}")
+        total += float(m.group(1)) * _UNITS[m.group(2)]
+        pos = m.end()
+    if pos != len(s):
+        raise ValueError(f"invalid duration {v!r}")
+    return sign * total
+
+
+def _dur(default: float):
+    return field(default=default, metadata={"type": "duration"})
+
+
+@dataclass
+class AppConfig:
+    # ---- the reference's ten keys (pkg/models/app_config.go:22-31) ----
+    alias: str = "controller-cluster"
+    controller_config_path: str = ""
+    shard_config_path: str = "/app/config/shards"
+    controller_namespace: str = "nexus"
+    log_level: str = "INFO"
+    workers: int = 2
+    failure_rate_base_delay: float = _dur(0.030)
+    failure_rate_max_delay: float = _dur(5.0)
+    rate_limit_elements_per_second: int = 50
+    rate_limit_elements_burst: int = 300
+    # ---- framework extensions ----
+    mode: str = "native"
+    client_qps: float = 0.0          # 0 = unlimited (compat mode forces client-go's 5/10)
+    client_burst: int = 10
+    client_pool_size: int = 64
+    resync_period: float = _dur(30.0)
+    full_resync_period: float = _dur(600.0)
+    shard_sync_timeout: float = _dur(10.0)
+    metrics_bind_address: str = ""   # e.g. ":9090" → Prometheus /metrics
+    health_bind_address: str = ""    # e.g. ":8081" → /healthz, /readyz
+    log_format: str = "json"
+
+    @staticmethod
+    def key_of(attr: str) -> str:
+        return attr.replace("_", "-")
+
+    @staticmethod
+    def env_of(attr: str) -> str:
+        return ENV_PREFIX + attr.upper()
+
+
+def _coerce(f, raw):
+    if f.metadata.get("type") == "duration":
+        return parse_duration(raw)
+    t = f.type if isinstance(f.type, str) else getattr(f.type, "__name__", str(f.type))
+    if t == "int":
+        return int(float(raw))
+    if t == "float":
+        return float(raw)
+    if t == "bool":
+        return str(raw).lower() in ("1", "true", "yes", "on")
+    return str(raw)
+
+
+def _read_yaml(path: str) -> dict:
+    if not os.path.exists(path):
+        return {}
+    with open(path) as fh:
+        return yaml.safe_load(fh) or {}
+
+
+def load_config(config_dir: str | None = None, env: dict | None = None) -> AppConfig:
+    env = os.environ if env is None else env
+    config_dir = config_dir or env.get("NCC_CONFIG_DIR") or os.getcwd()
+    merged: dict = {}
+    merged.update(_read_yaml(os.path.join(config_dir, "appconfig.yaml")))
+    app_env = env.get("APPLICATION_ENVIRONMENT")
+    if app_env:
+        merged.update(_read_yaml(os.path.join(config_dir, f"appconfig.{app_env}.yaml")))
+    cfg = AppConfig()
+    for f in fields(AppConfig):
+        raw = merged.get(AppConfig.key_of(f.name))
+        ev = env.get(AppConfig.env_of(f.name))
+        if ev not in (None, ""):
+            raw = ev
+        if raw is None or raw == "":
+            continue
+        try:
+            setattr(cfg, f.name, _coerce(f, raw))
+        except ValueError as e:
+            raise ValueError(f"invalid value for {AppConfig.key_of(f.name)}: {raw!r} ({e})") from e
+    return cfg

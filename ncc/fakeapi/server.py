@@ -1,0 +1,400 @@
+"""HTTP front-end of the fake kube-apiserver (aiohttp), over `ClusterState`.
+
+Serves the REST surface the controller uses — core `/api/v1` and CRD `/apis/{group}/{version}`
+paths, namespaced and cluster-wide, `GET` (get / list / `?watch=1`), `POST`, `PUT`
+(incl. `/status`), `PATCH` (merge, strategic, json, apply) and `DELETE` — with Kubernetes
+`Status` error bodies, chunked JSON-lines watch streams with periodic `BOOKMARK`s, and
+`timeoutSeconds`.  It replaces envtest/kind for tests and benchmarks.
+
+Test/bench control endpoints (not part of the Kubernetes API):
+  GET  /_fake/stats    request counters and object counts
+  POST /_fake/faults   {"latency_ms", "jitter_ms", "error_rate", "error_code", "throttle_rate",
+                        "down", "drop_watches", "compact"} — fault injection for the
+                       retry/backoff benchmark (BASELINE.json config 5)
+  POST /_fake/objects  bulk create `{"items": [...]}` without per-request overhead (bench seeding)
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import random
+import signal
+import ssl
+import time
+
+from aiohttp import web
+
+from ..api import resources as R
+from ..kube import errors as E
+from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+from .storage import ClusterState
+
+log = logging.getLogger("ncc.fakeapi")
+
+_JSON = "application/json"
+
+
+def _dumps(o) -> bytes:
+    return json.dumps(o, separators=(",", ":")).encode()
+
+
+def _status_response(err: E.ApiError) -> web.Response:
+    headers = {}
+    if err.retry_after is not None:
+        headers["Retry-After"] = str(int(err.retry_after))
+    return web.Response(status=err.code or 500, body=_dumps(err.status_object()), content_type=_JSON,
+                        headers=headers)
+
+
+class Faults:
+    def __init__(self):
+        self.latency_ms = 0.0
+        self.jitter_ms = 0.0
+        self.error_rate = 0.0
+        self.error_code = 500
+        self.throttle_rate = 0.0
+        self.down = False
+        self.write_only = True  # error_rate applies to mutating requests only
+
+    def update(self, d: dict) -> None:
+        for k in ("latency_ms", "jitter_ms", "error_rate", "throttle_rate"):
+            if k in d:
+                setattr(self, k, float(d[k]))
+        if "error_code" in d:
+            self.error_code = int(d["error_code"])
+        if "down" in d:
+            self.down = bool(d["down"])
+        if "write_only" in d:
+            self.write_only = bool(d["write_only"])
+
+    def as_dict(self) -> dict:
+        return dict(self.__dict__)
+
+
+class FakeApiServer:
+    def __init__(self, state: ClusterState | None = None, *, name: str = "fake", token: str | None = None,
+                 bookmark_interval: float = 5.0):
+        self.state = state or ClusterState(name)
+        self.name = name
+        self.token = token
+        self.bookmark_interval = bookmark_interval
+        self.faults = Faults()
+        self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
+        self._streams: set = set()
+        self.app = web.Application(client_max_size=64 * 1024 * 1024)
+        self.app.router.add_route("*", "/{tail:.*}", self._dispatch)
+        self._runner: web.AppRunner | None = None
+        self.port: int | None = None
+        self.url: str | None = None
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context: ssl.SSLContext | None = None) -> str:
+        self._runner = web.AppRunner(self.app, access_log=None, handle_signals=False)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, host, port, ssl_context=ssl_context, backlog=1024)
+        await site.start()
+        sock = site._server.sockets[0]  # type: ignore[union-attr]
+        self.port = sock.getsockname()[1]
+        self.url = f"{'https' if ssl_context else 'http'}://{host}:{self.port}"
+        return self.url
+
+    async def stop(self) -> None:
+        self.state.close_watchers()
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+    def drop_watches(self) -> None:
+        self.state.close_watchers()
+
+    # ------------------------------------------------------------------ routing
+    def _parse(self, path: str):
+        """→ (rt, namespace, name, subresource) or a special-route string."""
+        parts = [p for p in path.split("/") if p]
+        if not parts:
+            return "root"
+        if parts[0] == "api":
+            if len(parts) == 1:
+                return "api"
+            group, version, rest = "", parts[1], parts[2:]
+        elif parts[0] == "apis":
+            if len(parts) == 1:
+                return "apis"
+            if len(parts) < 3:
+                return "apigroup"
+            group, version, rest = parts[1], parts[2], parts[3:]
+        else:
+            return "/".join(parts)
+        if not rest:
+            return ("resources", group, version)
+        ns = None
+        if rest[0] == "namespaces" and len(rest) >= 3:
+            ns, rest = rest[1], rest[2:]
+        elif rest[0] == "namespaces" and len(rest) <= 2:
+            rt = self.state.resource("", "namespaces")
+            return rt, None, (rest[1] if len(rest) == 2 else None), None
+        plural = rest[0]
+        name = rest[1] if len(rest) > 1 else None
+        sub = rest[2] if len(rest) > 2 else None
+        rt = self.state.resource(group, plural)
+        if rt.version != version:
+            raise E.NotFound(f"version {version} of {plural}.{group} not served")
+        return rt, ns, name, sub
+
+    async def _dispatch(self, request: web.Request) -> web.StreamResponse:
+        self.requests["total"] += 1
+        path = request.path
+        if path.startswith("/_fake/"):
+            return await self._control(request, path[len("/_fake/"):])
+        if path in ("/healthz", "/readyz", "/livez"):
+            return web.Response(text="ok")
+        if path == "/version":
+            return web.Response(body=_dumps({"major": "1", "minor": "33", "gitVersion": "v1.33.0-ncc-fake",
+                                             "platform": "linux/amd64"}), content_type=_JSON)
+        try:
+            if self.token is not None:
+                auth = request.headers.get("Authorization", "")
+                if auth != f"Bearer {self.token}":
+                    raise E.Unauthorized("Unauthorized")
+            f = self.faults
+            if f.down:
+                raise E.ServiceUnavailable("the server is currently unable to handle the request")
+            if f.latency_ms or f.jitter_ms:
+                await asyncio.sleep((f.latency_ms + random.random() * f.jitter_ms) / 1000.0)
+            mutating = request.method in ("POST", "PUT", "PATCH", "DELETE")
+            if f.throttle_rate and random.random() < f.throttle_rate:
+                self.requests["throttled"] += 1
+                raise E.TooManyRequests("too many requests, please try again later", retry_after=1)
+            if f.error_rate and (mutating or not f.write_only) and random.random() < f.error_rate:
+                self.requests["errors_injected"] += 1
+                raise E.from_status(f.error_code, {"message": "injected fault"})
+            target = self._parse(path)
+            if isinstance(target, str):
+                return self._discovery(target)
+            if target[0] == "resources":
+                return self._resource_list(target[1], target[2])
+            rt, ns, name, sub = target
+            q = request.query
+            m = request.method
+            if m == "GET":
+                if name is None:
+                    if q.get("watch") in ("1", "true"):
+                        return await self._watch(request, rt, ns)
+                    limit = int(q["limit"]) if q.get("limit") else None
+                    return self._json(self.state.list(rt, ns, label_selector=q.get("labelSelector"), limit=limit,
+                                                      continue_token=q.get("continue")))
+                return self._json(self.state.get(rt, ns or "", name))
+            body = await self._body(request) if m != "DELETE" or request.can_read_body else None
+            if m == "POST" and name is None:
+                return self._json(self.state.create(rt, ns or "", body), 201)
+            if m == "PUT" and name is not None:
+                if (body.get("metadata") or {}).get("name") not in (None, name):
+                    raise E.BadRequest("the name of the object does not match the name on the URL")
+                body.setdefault("metadata", {})["name"] = name
+                if sub not in (None, "status"):
+                    raise E.NotFound(f"subresource {sub} not found")
+                if sub == "status" and not rt.has_status:
+                    raise E.NotFound(f"{rt.plural} has no status subresource")
+                return self._json(self.state.update(rt, ns or "", body, subresource=sub))
+            if m == "PATCH" and name is not None:
+                ctype = request.content_type
+                if ctype not in (PATCH_MERGE, PATCH_STRATEGIC, PATCH_JSON, PATCH_APPLY):
+                    raise E.ApiError(f"unsupported patch type {ctype}", code=415, reason="UnsupportedMediaType")
+                return self._json(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
+            if m == "DELETE" and name is not None:
+                opts = body or {}
+                return self._json(self.state.delete(rt, ns or "", name, preconditions=opts.get("preconditions"),
+                                                    propagation_policy=opts.get("propagationPolicy")
+                                                    or q.get("propagationPolicy")))
+            raise E.MethodNotAllowed(f"method {m} not allowed on {path}")
+        except E.ApiError as e:
+            return _status_response(e)
+        except (ValueError, KeyError, TypeError) as e:
+            return _status_response(E.BadRequest(f"bad request: {e}"))
+
+    async def _body(self, request: web.Request):
+        raw = await request.read()
+        if not raw:
+            return {}
+        if request.content_type == PATCH_APPLY:
+            try:
+                return json.loads(raw)
+            except ValueError:
+                import yaml
+                return yaml.safe_load(raw)
+        return json.loads(raw)
+
+    @staticmethod
+    def _json(obj, status: int = 200) -> web.Response:
+        return web.Response(status=status, body=_dumps(obj), content_type=_JSON)
+
+    # ------------------------------------------------------------------ discovery
+    def _discovery(self, target: str) -> web.Response:
+        if target == "api":
+            return self._json({"kind": "APIVersions", "versions": ["v1"]})
+        if target == "apis":
+            groups = sorted({(g, v) for (g, _p), rt in self.state._types.items() if g for v in [rt.version]})
+            return self._json({"kind": "APIGroupList", "apiVersion": "v1", "groups": [
+                {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v}],
+                 "preferredVersion": {"groupVersion": f"{g}/{v}", "version": v}} for g, v in groups]})
+        if target == "root":
+            return self._json({"paths": ["/api", "/apis", "/healthz", "/version"]})
+        raise E.NotFound(f"the server could not find the requested resource {target}")
+
+    def _resource_list(self, group: str, version: str) -> web.Response:
+        res = []
+        for (g, plural), rt in sorted(self.state._types.items()):
+            if g == group and rt.version == version:
+                res.append({"name": plural, "namespaced": rt.namespaced, "kind": rt.kind,
+                            "verbs": ["create", "delete", "get", "list", "patch", "update", "watch"]})
+                if rt.has_status:
+                    res.append({"name": f"{plural}/status", "namespaced": rt.namespaced, "kind": rt.kind,
+                                "verbs": ["get", "patch", "update"]})
+        gv = f"{group}/{version}" if group else version
+        return self._json({"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": gv, "resources": res})
+
+    # ------------------------------------------------------------------ watch
+    async def _watch(self, request: web.Request, rt: R.ResourceType, ns: str | None) -> web.StreamResponse:
+        q = request.query
+        timeout = float(q["timeoutSeconds"]) if q.get("timeoutSeconds") else None
+        bookmarks = q.get("allowWatchBookmarks") in ("1", "true")
+        try:
+            w = self.state.watch(rt, ns, q.get("resourceVersion"), q.get("labelSelector"))
+        except E.Gone as e:
+            # like the apiserver: an in-stream ERROR event carrying a 410 Status
+            resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON})
+            await resp.prepare(request)
+            await resp.write(_dumps({"type": "ERROR", "object": e.status_object()}) + b"\n")
+            await resp.write_eof()
+            return resp
+        resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON, "Transfer-Encoding": "chunked"})
+        await resp.prepare(request)
+        self.requests["watch_streams"] += 1
+        self._streams.add(w)
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout if timeout else None
+        last_bookmark = loop.time()
+        try:
+            while True:
+                now = loop.time()
+                wait = self.bookmark_interval if bookmarks else 3600.0
+                if deadline is not None:
+                    wait = min(wait, deadline - now)
+                    if wait <= 0:
+                        break
+                try:
+                    rec = await asyncio.wait_for(w.queue.get(), max(wait, 0.0))
+                except asyncio.TimeoutError:
+                    rec = False
+                if rec is None:
+                    break
+                chunks = []
+                if rec is not False:
+                    chunks.append(rec.line())
+                    while not w.queue.empty():  # batch everything already queued into one write
+                        nxt = w.queue.get_nowait()
+                        if nxt is None:
+                            rec = None
+                            break
+                        chunks.append(nxt.line())
+                if bookmarks and loop.time() - last_bookmark >= self.bookmark_interval:
+                    chunks.append(_dumps({"type": "BOOKMARK", "object": {
+                        "kind": rt.kind, "apiVersion": rt.api_version,
+                        "metadata": {"resourceVersion": str(self.state.rv)}}}) + b"\n")
+                    last_bookmark = loop.time()
+                if chunks:
+                    await resp.write(b"".join(chunks))
+                if rec is None:
+                    break
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            w.close()
+            self._streams.discard(w)
+        try:
+            await resp.write_eof()
+        except (ConnectionResetError, RuntimeError):
+            pass
+        return resp
+
+    # ------------------------------------------------------------------ control
+    async def _control(self, request: web.Request, what: str) -> web.Response:
+        if what == "stats":
+            counts = {f"{g or 'core'}/{p}": self.state.count(rt) for (g, p), rt in self.state._types.items()}
+            return self._json({"name": self.name, "rv": self.state.rv, "requests": self.requests,
+                               "state": self.state.stats, "objects": counts, "faults": self.faults.as_dict(),
+                               "watchers": len(self.state._watchers)})
+        if what == "faults" and request.method == "POST":
+            body = await self._body(request)
+            self.faults.update(body)
+            if body.get("drop_watches") or body.get("down"):
+                self.drop_watches()
+            if body.get("compact"):
+                self.state.compact()
+            return self._json(self.faults.as_dict())
+        if what == "objects" and request.method == "POST":
+            body = await self._body(request)
+            n = 0
+            for o in body.get("items") or []:
+                rt = R.by_kind(o["kind"])
+                try:
+                    self.state.create(rt, (o.get("metadata") or {}).get("namespace", ""), o)
+                    n += 1
+                except E.AlreadyExists:
+                    pass
+            return self._json({"created": n, "rv": self.state.rv})
+        return web.Response(status=404, text="unknown control endpoint")
+
+
+async def serve(args) -> None:
+    logging.basicConfig(level=logging.WARNING)
+    server = FakeApiServer(name=args.name, token=args.token, bookmark_interval=args.bookmark_interval)
+    ctx = None
+    if args.tls_cert:
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(args.tls_cert, args.tls_key)
+    url = await server.start(args.host, args.port, ctx)
+    if args.port_file:
+        tmp = args.port_file + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(url)
+        os.replace(tmp, args.port_file)
+    print(url, flush=True)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    if args.parent_pid:
+        async def watch_parent():
+            while True:
+                await asyncio.sleep(1.0)
+                try:
+                    os.kill(args.parent_pid, 0)
+                except OSError:
+                    stop.set()
+                    return
+        asyncio.ensure_future(watch_parent())
+    await stop.wait()
+    await server.stop()
+
+
+def main(argv=None) -> None:
+    p = argparse.ArgumentParser(prog="python -m ncc.fakeapi", description="in-process fake kube-apiserver")
+    p.add_argument("--name", default="fake")
+    p.add_argument("--host", default="127.0.0.1")
+    p.add_argument("--port", type=int, default=0)
+    p.add_argument("--port-file")
+    p.add_argument("--token")
+    p.add_argument("--tls-cert")
+    p.add_argument("--tls-key")
+    p.add_argument("--bookmark-interval", type=float, default=5.0)
+    p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
+    args = p.parse_args(argv)
+    asyncio.run(serve(args))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+"""aiohttp REST transport: one keep-alive connection pool per cluster.
+
+This is the "distributed communication backend" of the system: JSON over
+HTTP(S) to kube-apiservers, with TLS and credentials from kubeconfig (CA, client cert/key,
+bearer token, token file, exec plugin), a bounded keep-alive pool sized for fan-out
+concurrency, chunked JSON-lines watch streams, typed errors, `Retry-After`-driven retries of
+throttled/unavailable responses (client-go `rest.Request` semantics) and one credential
+refresh on 401 for exec-plugin users.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import ssl
+import tempfile
+from typing import AsyncIterator
+from urllib.parse import urlencode
+
+import aiohttp
+
+from ..api.resources import ResourceType
+from . import errors as E
+from .client import PATCH_MERGE, KubeClient, WatchEvent
+from .kubeconfig import ClusterConfig, CredentialSource
+
+USER_AGENT = "nexus-configuration-controller/ncc (linux/amd64)"
+_JSON = "application/json"
+
+
+def _ssl_context(cfg: ClusterConfig, exec_cert: tuple | None = None) -> ssl.SSLContext | bool:
+    if not cfg.is_tls:
+        return False
+    ctx = ssl.create_default_context()
+    if cfg.insecure:
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+    elif cfg.ca_data:
+        ctx.load_verify_locations(cadata=cfg.ca_data.decode())
+    cert = exec_cert or ((cfg.client_cert_data, cfg.client_key_data)
+                         if cfg.client_cert_data and cfg.client_key_data else None)
+    if cert:
+        # ssl needs files for the key pair; keep them private and short-lived.
+        with tempfile.TemporaryDirectory(prefix="ncc-tls-") as d:
+            cp, kp = os.path.join(d, "tls.crt"), os.path.join(d, "tls.key")
+            for p, data in ((cp, cert[0]), (kp, cert[1])):
+                fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+                with os.fdopen(fd, "wb") as f:
+                    f.write(data)
+            ctx.load_cert_chain(cp, kp)
+    return ctx
+
+
+class RestClient(KubeClient):
+    def __init__(self, cfg: ClusterConfig, *, pool_size: int = 64, request_timeout: float = 30.0,
+                 max_retries: int = 5, cluster_name: str | None = None):
+        self.cfg = cfg
+        self.cluster_name = cluster_name or cfg.name or cfg.server
+        self.pool_size = pool_size
+        self.request_timeout = request_timeout
+        self.max_retries = max_retries
+        self.creds = CredentialSource(cfg)
+        self._session: aiohttp.ClientSession | None = None
+        self._session_lock = asyncio.Lock()
+        self.stats = {"requests": 0, "retries": 0, "errors": 0, "watch_streams": 0}
+
+    async def _get_session(self) -> aiohttp.ClientSession:
+        if self._session is None or self._session.closed:
+            async with self._session_lock:
+                if self._session is None or self._session.closed:
+                    exec_cert = await self.creds.exec_client_cert()
+                    ctx = _ssl_context(self.cfg, exec_cert)
+                    conn = aiohttp.TCPConnector(limit=self.pool_size, limit_per_host=self.pool_size, ssl=ctx,
+                                                ttl_dns_cache=300, keepalive_timeout=60,
+                                                enable_cleanup_closed=False)
+                    self._session = aiohttp.ClientSession(connector=conn, json_serialize=json.dumps,
+                                                          headers={"User-Agent": USER_AGENT, "Accept": _JSON},
+                                                          skip_auto_headers=("Accept-Encoding",))
+        return self._session
+
+    async def _headers(self, content_type: str | None, refresh: bool = False) -> dict:
+        h = {}
+        if content_type:
+            h["Content-Type"] = content_type
+        tok = await self.creds.token(force_refresh=refresh)
+        if tok:
+            h["Authorization"] = f"Bearer {tok}"
+        elif self.cfg.username is not None:
+            import base64
+            h["Authorization"] = "Basic " + base64.b64encode(
+                f"{self.cfg.username}:{self.cfg.password or ''}".encode()).decode()
+        if self.cfg.tls_server_name:
+            h["Host"] = self.cfg.tls_server_name
+        return h
+
+    async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
+                      content_type: str = _JSON):
+        session = await self._get_session()
+        url = self.cfg.server + path
+        if params:
+            url += "?" + urlencode({k: v for k, v in params.items() if v is not None})
+        data = None
+        if body is not None:
+            data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
+        refreshed = False
+        attempt = 0
+        while True:
+            self.stats["requests"] += 1
+            try:
+                headers = await self._headers(content_type if data is not None else None, refresh=False)
+                async with session.request(method, url, data=data, headers=headers,
+                                           timeout=aiohttp.ClientTimeout(total=self.request_timeout)) as resp:
+                    raw = await resp.read()
+                    status = resp.status
+                    retry_after = resp.headers.get("Retry-After")
+            except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
+                self.stats["errors"] += 1
+                raise E.TransportError(f"{method} {url}: {type(e).__name__}: {e}") from e
+            if status < 300:
+                return json.loads(raw) if raw else None
+            if status == 401 and self.cfg.exec is not None and not refreshed:
+                refreshed = True
+                await self.creds.token(force_refresh=True)
+                continue
+            if status in (429, 500, 502, 503, 504) and retry_after is not None and attempt < self.max_retries:
+                attempt += 1
+                self.stats["retries"] += 1
+                try:
+                    delay = min(float(retry_after), 10.0)
+                except ValueError:
+                    delay = 1.0
+                await asyncio.sleep(delay)
+                continue
+            self.stats["errors"] += 1
+            try:
+                st = json.loads(raw) if raw else None
+            except ValueError:
+                st = None
+            err = E.from_status(status, st if isinstance(st, dict) else None,
+                                fallback_message=raw[:200].decode(errors="replace"))
+            if retry_after is not None:
+                try:
+                    err.retry_after = float(retry_after)
+                except ValueError:
+                    pass
+            raise err
+
+    # ------------------------------------------------------------------ verbs
+    async def get(self, rt, namespace, name):
+        return await self.request("GET", rt.item_path(namespace, name))
+
+    async def list(self, rt, namespace, *, label_selector=None, limit=None, continue_token=None,
+                   resource_version=None):
+        return await self.request("GET", rt.base_path(namespace), params={
+            "labelSelector": label_selector, "limit": limit, "continue": continue_token,
+            "resourceVersion": resource_version})
+
+    async def create(self, rt, namespace, obj, *, field_manager=None):
+        return await self.request("POST", rt.base_path(namespace), params={"fieldManager": field_manager}, body=obj)
+
+    async def update(self, rt, namespace, obj, *, field_manager=None):
+        name = (obj.get("metadata") or {}).get("name", "")
+        return await self.request("PUT", rt.item_path(namespace, name), params={"fieldManager": field_manager},
+                                  body=obj)
+
+    async def update_status(self, rt, namespace, obj, *, field_manager=None):
+        name = (obj.get("metadata") or {}).get("name", "")
+        return await self.request("PUT", rt.item_path(namespace, name, "status"),
+                                  params={"fieldManager": field_manager}, body=obj)
+
+    async def patch(self, rt, namespace, name, body, *, patch_type=PATCH_MERGE, field_manager=None, force=None,
+                    subresource=None):
+        params = {"fieldManager": field_manager}
+        if force is not None:
+            params["force"] = "true" if force else "false"
+        return await self.request("PATCH", rt.item_path(namespace, name, subresource), params=params, body=body,
+                                  content_type=patch_type)
+
+    async def delete(self, rt, namespace, name, *, propagation_policy=None, preconditions=None):
+        body = None
+        if propagation_policy or preconditions:
+            body = {"kind": "DeleteOptions", "apiVersion": "v1"}
+            if propagation_policy:
+                body["propagationPolicy"] = propagation_policy
+            if preconditions:
+                body["preconditions"] = preconditions
+        return await self.request("DELETE", rt.item_path(namespace, name), body=body)
+
+    async def watch(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
+                    allow_bookmarks=True, label_selector=None) -> AsyncIterator[WatchEvent]:
+        session = await self._get_session()
+        params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": timeout_seconds,
+                  "allowWatchBookmarks": "true" if allow_bookmarks else None, "labelSelector": label_selector}
+        url = self.cfg.server + rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items()
+                                                                            if v is not None})
+        client_timeout = aiohttp.ClientTimeout(total=(timeout_seconds + 30) if timeout_seconds else None,
+                                               sock_connect=self.request_timeout)
+        self.stats["watch_streams"] += 1
+        try:
+            headers = await self._headers(None)
+            async with session.get(url, headers=headers, timeout=client_timeout) as resp:
+                if resp.status >= 300:
+                    raw = await resp.read()
+                    try:
+                        st = json.loads(raw)
+                    except ValueError:
+                        st = None
+                    raise E.from_status(resp.status, st if isinstance(st, dict) else None)
+                buf = b""
+                async for chunk in resp.content.iter_any():
+                    buf += chunk
+                    if b"\n" not in chunk:
+                        continue
+                    lines = buf.split(b"\n")
+                    buf = lines.pop()
+                    for line in lines:
+                        if line:
+                            ev = json.loads(line)
+                            yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+                if buf.strip():
+                    ev = json.loads(buf)
+                    yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+        except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
+            raise E.TransportError(f"watch {url}: {type(e).__name__}: {e}") from e
+
+    async def close(self) -> None:
+        if self._session is not None and not self._session.closed:
+            await self._session.close()
+        self._session = None

@@ -1,0 +1,165 @@
+"""End-to-end: `App` against fake apiservers over real HTTP (Test_ControllerMain analogue, controller_test.go:1287-1336)."""
+import asyncio
+
+import pytest
+
+from ncc.api import constants as C
+from ncc.api import resources as R
+from ncc.app import App
+from ncc.kube import errors as E
+from ncc.testing.env import FakeEnvironment
+from ncc.testing.workload import make_configmap, make_secret, make_template, make_workgroup
+
+NS = "nexus"
+
+
+async def wait_for(pred, timeout=5.0, interval=0.02):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    last = None
+    while loop.time() < end:
+        try:
+            last = await pred()
+            if last:
+                return last
+        except E.NotFound:
+            pass
+        await asyncio.sleep(interval)
+    raise AssertionError(f"condition not met within {timeout}s (last={last!r})")
+
+
+async def _get(client, rt, name):
+    return await client.get(rt, NS, name)
+
+
+class Running:
+    def __init__(self, env, mode, **cfg_kw):
+        self.app = App(env.app_config(mode=mode, **cfg_kw))
+        self.stop = asyncio.Event()
+
+    async def __aenter__(self):
+        await self.app.build()
+        self.task = asyncio.ensure_future(self.app.run(self.stop))
+        await asyncio.wait_for(self.app.controller.ready.wait(), 10)
+        return self.app
+
+    async def __aexit__(self, *exc):
+        self.stop.set()
+        await asyncio.wait_for(self.task, 15)
+
+
+@pytest.mark.parametrize("mode", ["compat", "native"])
+async def test_controller_main_propagates_create_and_update(tmp_path, mode):
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    try:
+        t = make_template(0, NS)
+        await cc.create(R.TEMPLATES, NS, t)
+        async with Running(env, mode):
+            # the reference's integration test allows 1 s for each propagation step
+            await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00000"), timeout=1.0)
+            cur = await cc.get(R.TEMPLATES, NS, "algo-00000")
+            cur["spec"]["container"]["versionTag"] = "v2.3.4"
+            await cc.update(R.TEMPLATES, NS, cur)
+
+            async def propagated():
+                o = await sc.get(R.TEMPLATES, NS, "algo-00000")
+                return o["spec"]["container"]["versionTag"] == "v2.3.4"
+            await wait_for(propagated, timeout=1.0)
+            shard_t = await sc.get(R.TEMPLATES, NS, "algo-00000")
+            assert shard_t["metadata"]["labels"] == C.owner_labels("controller-cluster")
+
+            async def ready():
+                o = await cc.get(R.TEMPLATES, NS, "algo-00000")
+                conds = (o.get("status") or {}).get("conditions") or []
+                return conds and conds[0]["status"] == "True" and o["status"]["syncedToClusters"] == ["shard-0"]
+            await wait_for(ready, timeout=2.0)
+    finally:
+        await cc.close()
+        await sc.close()
+        await env.stop()
+
+
+@pytest.mark.parametrize("mode", ["compat", "native"])
+async def test_dependents_fan_out_and_delete(tmp_path, mode):
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc = env.controller_client()
+    scs = [env.shard_client(i) for i in range(2)]
+    try:
+        await cc.create(R.SECRETS, NS, make_secret("s0", NS))
+        await cc.create(R.CONFIGMAPS, NS, make_configmap("c0", NS))
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=["c0"]))
+        await cc.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        async with Running(env, mode):
+            for sc in scs:
+                st = await wait_for(lambda sc=sc: _get(sc, R.TEMPLATES, "algo-00000"), timeout=3)
+                sec = await wait_for(lambda sc=sc: _get(sc, R.SECRETS, "s0"), timeout=3)
+                cm = await wait_for(lambda sc=sc: _get(sc, R.CONFIGMAPS, "c0"), timeout=3)
+                await wait_for(lambda sc=sc: _get(sc, R.WORKGROUPS, "mi355x"), timeout=3)
+                for dep in (sec, cm):
+                    refs = dep["metadata"]["ownerReferences"]
+                    assert [r["uid"] for r in refs] == [st["metadata"]["uid"]]
+                    assert dep["metadata"]["labels"][C.LABEL_CONFIGURATION_OWNER] == "controller-cluster"
+            ctrl_secret = await cc.get(R.SECRETS, NS, "s0")
+            assert ctrl_secret["metadata"]["ownerReferences"][0]["kind"] == C.TEMPLATE_KIND
+
+            # data change in the controller cluster propagates to every shard
+            ctrl_secret["data"] = {"token": "bmV3"}
+            await cc.update(R.SECRETS, NS, ctrl_secret)
+            for sc in scs:
+                async def updated(sc=sc):
+                    return (await sc.get(R.SECRETS, NS, "s0")).get("data") == {"token": "bmV3"}
+                await wait_for(updated, timeout=3)
+
+            # template deletion removes it from shards; shard GC collects the dependents
+            await cc.delete(R.TEMPLATES, NS, "algo-00000")
+            for sc in scs:
+                async def gone(sc=sc):
+                    try:
+                        await sc.get(R.TEMPLATES, NS, "algo-00000")
+                        return False
+                    except E.NotFound:
+                        pass
+                    try:
+                        await sc.get(R.SECRETS, NS, "s0")
+                        return False
+                    except E.NotFound:
+                        return True
+                await wait_for(gone, timeout=3)
+    finally:
+        await cc.close()
+        for sc in scs:
+            await sc.close()
+        await env.stop()
+
+
+async def test_native_repairs_shard_drift_and_workgroup_delete(tmp_path):
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    try:
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS))
+        await cc.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        async with Running(env, "native"):
+            st = await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00000"), timeout=2)
+            # someone edits the shard copy: native mode watches shards and repairs it without waiting for resync
+            st["spec"]["container"]["versionTag"] = "tampered"
+            await sc.update(R.TEMPLATES, NS, st)
+
+            async def repaired():
+                o = await sc.get(R.TEMPLATES, NS, "algo-00000")
+                return o["spec"]["container"]["versionTag"] == "v1.0.0"
+            await wait_for(repaired, timeout=2)
+            await wait_for(lambda: _get(sc, R.WORKGROUPS, "mi355x"), timeout=2)
+            await cc.delete(R.WORKGROUPS, NS, "mi355x")
+
+            async def wg_gone():
+                try:
+                    await sc.get(R.WORKGROUPS, NS, "mi355x")
+                    return False
+                except E.NotFound:
+                    return True
+            await wait_for(wg_gone, timeout=2)
+    finally:
+        await cc.close()
+        await sc.close()
+        await env.stop()
