@@ -1,0 +1,295 @@
+#!/usr/bin/env python
+"""Headline benchmark: objects synced/s and p50/p99 controller→shard propagation latency at N shards.
+
+Metric and topology come from BASELINE.json ("objects synced/sec + p50 controller->shard latency
+at 1/2/4/8 shards").  `--gpus N` is the number of shard clusters: under
+`torch.distributed.run --nproc-per-node N` every rank hosts one shard kube-apiserver process (the
+shard clusters are 8×MI355X nodes; one rank per GPU == one shard per GPU), rank 0 additionally
+hosts the controller-cluster apiserver and runs the controller (`python -m ncc`) as a separate
+process exactly as deployed.  Ranks rendezvous over gloo (no tensors are exchanged; RCCL is not
+involved in a control plane).
+
+Workload (synthetic, BASELINE.json config 3 shape by default): T NexusAlgorithmTemplates, each
+referencing 1 Secret + 1 ConfigMap, in namespace `nexus`.  Warm-up = cold start (controller
+boots against pre-seeded objects and fans everything out) + W update waves; then K timed waves.
+A wave bumps every template's `versionTag` and every Secret/ConfigMap payload in one burst on
+the controller cluster; the step ends when every shard has committed all 3·T new versions.
+Per-object latency = shard commit time − controller commit time (server-side clocks, same host).
+
+value = K · 3 · T · N / (wall time of the K timed waves, max over ranks)   [objects/s, weak scaling]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import base64
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "objects synced/sec + p50 controller->shard latency at 1/2/4/8 shards"
+NS = "nexus"
+MARKERS = ["nexusalgorithmtemplates=spec.container.versionTag", "secrets=data.version", "configmaps=data.version"]
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                   help="number of shard clusters (one per rank/GPU)")
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--templates", type=int, default=1000)
+    p.add_argument("--payload", type=int, default=512, help="bytes per Secret/ConfigMap payload")
+    p.add_argument("--mode", default="native", choices=["native", "compat"])
+    p.add_argument("--workers", type=int, default=0, help="controller workers (0 = mode default)")
+    p.add_argument("--timeout", type=float, default=600.0, help="per-wave convergence timeout (s)")
+    p.add_argument("--keep", action="store_true", help="keep the work directory")
+    p.add_argument("--extra-env", action="append", default=[], help="KEY=VAL passed to the controller process")
+    return p.parse_args(argv)
+
+
+# ------------------------------------------------------------------ distributed plumbing
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+        self._cuda = None
+
+    def all_gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast(self, obj):
+        if self.dist is None:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def sync(self):
+        """barrier + torch.cuda.synchronize() (the bench contract); GPUs do no work in a control plane."""
+        if self.dist is not None:
+            self.dist.barrier()
+        if self._cuda is None:
+            try:
+                import torch
+                self._cuda = torch.cuda.is_available()
+                if self._cuda:
+                    torch.cuda.set_device(self.local_rank % max(torch.cuda.device_count(), 1))
+            except Exception:  # noqa: BLE001
+                self._cuda = False
+        if self._cuda:
+            import torch
+            torch.cuda.synchronize()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        return max(self.all_gather(x))
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ workload
+def wave_objects(T: int, version: int, payload: int) -> list:
+    from ncc.testing.workload import configmap_name, make_configmap, make_secret, make_template, secret_name
+    items = []
+    for i in range(T):
+        items.append(make_template(i, NS, secrets=[secret_name(i)], configmaps=[configmap_name(i)],
+                                   version=f"v{version}"))
+        s = make_secret(secret_name(i), NS, payload=payload, version=version)
+        items.append(s)
+        items.append(make_configmap(configmap_name(i), NS, payload=payload, version=version))
+    return items
+
+
+def want(T: int, version: int) -> list:
+    return [{"plural": "nexusalgorithmtemplates", "value": f"v{version}", "count": T},
+            {"plural": "secrets", "value": base64.b64encode(str(version).encode()).decode(), "count": T},
+            {"plural": "configmaps", "value": str(version), "count": T}]
+
+
+async def post(session, url, body, timeout=None):
+    import aiohttp
+    async with session.post(url, data=json.dumps(body), headers={"Content-Type": "application/json"},
+                            timeout=aiohttp.ClientTimeout(total=timeout)) as r:
+        r.raise_for_status()
+        return await r.json()
+
+
+def pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    k = min(len(xs) - 1, max(0, int(round(q / 100.0 * (len(xs) - 1)))))
+    return xs[k]
+
+
+# ------------------------------------------------------------------ main
+async def run(args, d: Dist) -> dict | None:
+    import aiohttp
+    from ncc.kube.kubeconfig import render_kubeconfig
+    from ncc.testing.env import spawn_fakeapi, wait_port_file
+
+    work = tempfile.mkdtemp(prefix=f"ncc-bench-r{d.rank}-")
+    procs = []
+    try:
+        extra = sum((["--marker", m] for m in MARKERS), [])
+        pf = os.path.join(work, "shard.url")
+        procs.append(spawn_fakeapi(f"shard-{d.rank}", pf, extra=extra))
+        my_url = wait_port_file(pf, procs[-1])
+        urls = d.all_gather(my_url)
+        ctrl_url = None
+        controller = None
+        T = args.templates
+        if d.rank == 0:
+            cpf = os.path.join(work, "controller.url")
+            procs.append(spawn_fakeapi("controller", cpf))
+            ctrl_url = wait_port_file(cpf, procs[-1])
+            shard_dir = os.path.join(work, "shards")
+            os.makedirs(shard_dir)
+            for i, u in enumerate(urls):
+                with open(os.path.join(shard_dir, f"shard-{i}.kubeconfig"), "w") as f:
+                    f.write(render_kubeconfig(u, f"shard-{i}"))
+            ckc = os.path.join(work, "controller.kubeconfig")
+            with open(ckc, "w") as f:
+                f.write(render_kubeconfig(ctrl_url, "controller"))
+        async with aiohttp.ClientSession() as session:
+            if d.rank == 0:
+                await post(session, f"{ctrl_url}/_fake/apply", {"items": wave_objects(T, 0, args.payload)})
+                env = dict(os.environ)
+                env.update({"NEXUS__CONTROLLER_CONFIG_PATH": ckc, "NEXUS__SHARD_CONFIG_PATH": shard_dir,
+                            "NEXUS__CONTROLLER_NAMESPACE": NS, "NEXUS__ALIAS": "controller-cluster",
+                            "NEXUS__MODE": args.mode, "NEXUS__LOG_LEVEL": "WARNING",
+                            "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+                if args.workers:
+                    env["NEXUS__WORKERS"] = str(args.workers)
+                elif args.mode == "native":
+                    env["NEXUS__WORKERS"] = "64"
+                for kv in args.extra_env:
+                    k, _, v = kv.partition("=")
+                    env[k] = v
+                log = open(os.path.join(work, "controller.log"), "wb")
+                t_boot = time.time_ns()
+                controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=log,
+                                              stderr=subprocess.STDOUT, cwd=work)
+                procs.append(controller)
+            t_boot = d.broadcast(t_boot if d.rank == 0 else None)
+
+            async def converge(version: int, times: bool):
+                r = await post(session, f"{my_url}/_fake/markers/wait",
+                               {"want": want(T, version), "timeout": args.timeout, "times": times},
+                               timeout=args.timeout + 30)
+                if not r["ok"]:
+                    tail = ""
+                    if controller is not None:
+                        with open(os.path.join(work, "controller.log"), "rb") as f:
+                            tail = f.read()[-3000:].decode(errors="replace")
+                    raise RuntimeError(f"rank {d.rank}: wave v{version} did not converge: {r['counts']}\n{tail}")
+                return r
+
+            # ---- cold start (warm-up 0): boot + full fan-out of pre-seeded objects
+            r = await converge(0, True)
+            cold_local = max(max(v) for v in r["times"].values()) - t_boot
+            cold = d.max(cold_local / 1e9)
+
+            lat_ms: list[float] = []
+            t_start = None
+            total = args.warmup + args.steps
+            for step in range(1, total + 1):
+                timed = step > args.warmup
+                if step == args.warmup + 1:
+                    d.sync()
+                    t_start = time.perf_counter()
+                t0 = None
+                if d.rank == 0:
+                    a = await post(session, f"{ctrl_url}/_fake/apply",
+                                   {"items": wave_objects(T, step, args.payload)})
+                    t0 = a["t1_ns"]
+                t0 = d.broadcast(t0)
+                r = await converge(step, timed)
+                if timed:
+                    for ts in r["times"].values():
+                        lat_ms.extend((t - t0) / 1e6 for t in ts)
+            d.sync()
+            elapsed = time.perf_counter() - t_start
+            elapsed = d.max(elapsed)
+            all_lat = d.all_gather(lat_ms)
+            if d.rank != 0:
+                return None
+            lat = [x for part in all_lat for x in part]
+            objs = args.steps * 3 * T * d.world
+            value = objs / elapsed
+            ctrl_alive = controller.poll() is None
+            return {
+                "metric": METRIC,
+                "value": round(value, 1),
+                "unit": "objects/s",
+                "n_gpus": d.world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(elapsed * 1000 / args.steps, 2),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "bf16",
+                "data": "synthetic (fake kube-apiservers, random NexusAlgorithmTemplate/Secret/ConfigMap objects)",
+                "config": {"model": "NexusAlgorithmTemplate fan-out (1 Secret + 1 ConfigMap each)",
+                           "global_batch": T, "seq_len": 3, "parallelism": f"shards{d.world}",
+                           "templates": T, "shards": d.world, "mode": args.mode, "payload_bytes": args.payload},
+                "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
+                "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
+                "cold_start_s": round(cold, 3),
+                "cold_start_objects_per_s": round(3 * T * d.world / cold, 1) if cold > 0 else None,
+                "controller_alive": ctrl_alive,
+            }
+    finally:
+        for p in reversed(procs):
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        if not args.keep:
+            shutil.rmtree(work, ignore_errors=True)
+
+
+def main():
+    args = parse_args()
+    d = Dist()
+    if d.world != args.gpus and d.world > 1:
+        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {d.world}; using WORLD_SIZE", file=sys.stderr)
+    if d.world == 1 and args.gpus > 1:
+        raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
+    try:
+        res = asyncio.run(run(args, d))
+    finally:
+        d.close()
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,7 @@ from aiohttp import web
 from ..api import resources as R
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+from .markers import MarkerTracker
 from .storage import ClusterState
 
 log = logging.getLogger("ncc.fakeapi")
@@ -82,6 +83,8 @@ class FakeApiServer:
         self.token = token
         self.bookmark_interval = bookmark_interval
         self.faults = Faults()
+        self.markers = MarkerTracker()
+        self.state.write_hooks.append(self.markers.on_write)
         self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
         self._streams: set = set()
         self.app = web.Application(client_max_size=64 * 1024 * 1024)
@@ -335,6 +338,47 @@ class FakeApiServer:
             if body.get("compact"):
                 self.state.compact()
             return self._json(self.faults.as_dict())
+        if what == "markers" and request.method == "POST":
+            body = await self._body(request)
+            for plural, path in (body.get("specs") or {}).items():
+                self.markers.add_spec(plural, path)
+            return self._json({"specs": {k: ".".join(v) for k, v in self.markers.paths.items()}})
+        if what == "markers/wait" and request.method == "POST":
+            body = await self._body(request)
+            want = body.get("want") or []
+            ok = await self.markers.wait(want, float(body.get("timeout", 60)))
+            out = {"ok": ok, "counts": {f"{w['plural']}={w['value']}": len(self.markers.times(w["plural"], w["value"]))
+                                        for w in want}}
+            if body.get("times"):
+                out["times"] = {f"{w['plural']}={w['value']}": self.markers.times(w["plural"], w["value"])
+                                for w in want}
+            return self._json(out)
+        if what == "apply" and request.method == "POST":
+            body = await self._body(request)
+            t0 = time.time_ns()
+            n = 0
+            for o in body.get("items") or []:
+                rt = R.by_kind(o["kind"])
+                m = o.get("metadata") or {}
+                ns = m.get("namespace", "")
+                try:
+                    cur = self.state.get(rt, ns, m["name"])
+                except E.NotFound:
+                    cur = None
+                if cur is None:
+                    self.state.create(rt, ns, o)
+                else:
+                    new = dict(cur)
+                    for k, v in o.items():
+                        if k not in ("metadata", "status", "apiVersion", "kind"):
+                            new[k] = v
+                    new["metadata"] = dict(cur["metadata"])
+                    for mk in ("labels", "annotations"):
+                        if mk in m:
+                            new["metadata"][mk] = m[mk]
+                    self.state.update(rt, ns, new)
+                n += 1
+            return self._json({"applied": n, "t0_ns": t0, "t1_ns": time.time_ns(), "rv": self.state.rv})
         if what == "objects" and request.method == "POST":
             body = await self._body(request)
             n = 0
@@ -352,6 +396,9 @@ class FakeApiServer:
 async def serve(args) -> None:
     logging.basicConfig(level=logging.WARNING)
     server = FakeApiServer(name=args.name, token=args.token, bookmark_interval=args.bookmark_interval)
+    for m in args.marker:
+        plural, _, path = m.partition("=")
+        server.markers.add_spec(plural, path)
     ctx = None
     if args.tls_cert:
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
@@ -392,6 +439,7 @@ def main(argv=None) -> None:
     p.add_argument("--tls-key")
     p.add_argument("--bookmark-interval", type=float, default=5.0)
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
+    p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")
     args = p.parse_args(argv)
     asyncio.run(serve(args))
 
