@@ -1,0 +1,58 @@
+#!/usr/bin/env python
+"""Build the in-tree native extension `ncc/_native*.so` (C++17 + pybind11).
+
+Usage: python native/build.py [--debug] [--sanitize]
+`--sanitize` builds with AddressSanitizer/UBSan for host-side testing (run the tests with
+`LD_PRELOAD=$(g++ -print-file-name=libasan.so)`).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shlex
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SOURCES = [os.path.join(HERE, "ncc_native.cpp")]
+
+
+def target_path() -> str:
+    return os.path.join(ROOT, "ncc", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
+    import pybind11
+
+    out = target_path()
+    if not debug and not sanitize and os.path.exists(out):
+        so_m = os.path.getmtime(out)
+        if all(os.path.getmtime(s) <= so_m for s in SOURCES + [__file__]):
+            return out
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+    if debug or sanitize:
+        flags += ["-O1", "-g", "-fno-omit-frame-pointer"]
+    else:
+        flags += ["-O3", "-DNDEBUG"]
+    if sanitize:
+        flags += ["-fsanitize=address,undefined"]
+    incs = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+    tmp = out + ".tmp"
+    cmd = [cxx, *flags, *incs, *SOURCES, "-o", tmp]
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--sanitize", action="store_true")
+    a = ap.parse_args()
+    print(build(a.debug, a.sanitize, verbose=True))
+    sys.exit(0)

@@ -1,0 +1,45 @@
+"""Deployment-target tier, run by the driver on the MI355X box (`pytest -m gpu`).
+
+The controller has no GPU kernels (the workload is control-plane I/O; see README.md), so these
+tests exercise what must hold on the box the framework ships to: the in-tree C++ extension
+loads (no silent Python fallback), the flagship end-to-end sync works, and the benchmark
+harness produces a valid result line.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_extension_loaded():
+    from ncc import native
+    m = native.load(required=True)
+    q = m.RateLimitingQueue(0.03, 5.0, 50.0, 300)
+    assert q.add("template/nexus/a") and not q.add("template/nexus/a")
+    assert q.try_get() == "template/nexus/a"
+    from ncc.api import fingerprint as fp
+    assert fp.IMPL == "native"
+
+
+def test_smoke_on_box():
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    g.smoke()
+
+
+def test_bench_contract_single_shard():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--templates", "100", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in res
+    assert res["n_gpus"] == 1 and res["value"] > 0 and res["controller_alive"]
