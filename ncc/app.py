@@ -66,7 +66,8 @@ class App:
         self.cfg = cfg
         self.options = options or options_from_config(cfg)
         qps, burst = client_limits(cfg)
-        self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size)
+        self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size,
+                                                                       cfg.transport)
         self._controller_client = controller_client
         self.metrics = metrics
         self.ops = None
@@ -86,7 +87,7 @@ class App:
         if client is None:
             qps, burst = client_limits(cfg)
             client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.client_pool_size,
-                                cluster_name=cfg.alias)
+                                cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)
         self.client = client
@@ -188,4 +189,14 @@ def main(argv=None) -> int:
         print(f"configuration error: {e}", file=sys.stderr)
         return 1
     configure_logging(cfg.log_level, cfg.log_format)
+    prof_path = os.environ.get("NCC_PROFILE")
+    if prof_path:  # host-side profiling of the control loop: NCC_PROFILE=/path/out.prof
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            return asyncio.run(_amain(cfg))
+        finally:
+            prof.disable()
+            prof.dump_stats(prof_path)
     return asyncio.run(_amain(cfg))

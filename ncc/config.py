@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`client-burst`, `client-pool-size`, `transport`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
 `metrics-bind-address`, `health-bind-address`, `log-format`.
 """
 from __future__ import annotations
@@ -78,6 +78,7 @@ class AppConfig:
     client_qps: float = 0.0          # 0 = unlimited (compat mode forces client-go's 5/10)
     client_burst: int = 10
     client_pool_size: int = 64
+    transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     resync_period: float = _dur(30.0)
     full_resync_period: float = _dur(600.0)
     shard_sync_timeout: float = _dur(10.0)

@@ -1,4 +1,7 @@
-"""aiohttp REST transport: one keep-alive connection pool per cluster.
+"""REST client for kube-apiservers: one keep-alive connection pool per cluster.
+
+Two interchangeable transports: `fast` (default; raw asyncio protocols, `ncc.kube.transport`)
+and `aiohttp`.
 
 This is the "distributed communication backend" of the system: JSON over
 HTTP(S) to kube-apiservers, with TLS and credentials from kubeconfig (CA, client cert/key,
@@ -23,6 +26,7 @@ from ..api.resources import ResourceType
 from . import errors as E
 from .client import PATCH_MERGE, KubeClient, WatchEvent
 from .kubeconfig import ClusterConfig, CredentialSource
+from .transport import ConnectionPool
 
 USER_AGENT = "nexus-configuration-controller/ncc (linux/amd64)"
 _JSON = "application/json"
@@ -53,7 +57,11 @@ def _ssl_context(cfg: ClusterConfig, exec_cert: tuple | None = None) -> ssl.SSLC
 
 class RestClient(KubeClient):
     def __init__(self, cfg: ClusterConfig, *, pool_size: int = 64, request_timeout: float = 30.0,
-                 max_retries: int = 5, cluster_name: str | None = None):
+                 max_retries: int = 5, cluster_name: str | None = None, transport: str = "fast"):
+        if transport not in ("fast", "aiohttp"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = transport
+        self._pool: ConnectionPool | None = None
         self.cfg = cfg
         self.cluster_name = cluster_name or cfg.name or cfg.server
         self.pool_size = pool_size
@@ -78,8 +86,35 @@ class RestClient(KubeClient):
                                                           skip_auto_headers=("Accept-Encoding",))
         return self._session
 
+    async def _get_pool(self) -> ConnectionPool:
+        if self._pool is None:
+            async with self._session_lock:
+                if self._pool is None:
+                    exec_cert = await self.creds.exec_client_cert()
+                    ctx = _ssl_context(self.cfg, exec_cert)
+                    self._pool = ConnectionPool(self.cfg.server, ssl_context=ctx or None,
+                                                server_hostname=self.cfg.tls_server_name, max_size=self.pool_size,
+                                                connect_timeout=self.request_timeout)
+        return self._pool
+
+    async def _send(self, method: str, target: str, headers: dict, data):
+        """One HTTP exchange → (status, raw body, Retry-After header or None)."""
+        if self.transport == "fast":
+            pool = await self._get_pool()
+            body = data.encode() if isinstance(data, str) else data
+            resp = await pool.request(method, target, headers, body, timeout=self.request_timeout)
+            return resp.status, resp.body, resp.headers.get("retry-after")
+        session = await self._get_session()
+        try:
+            async with session.request(method, self.cfg.server + target, data=data, headers=headers,
+                                       timeout=aiohttp.ClientTimeout(total=self.request_timeout)) as resp:
+                raw = await resp.read()
+                return resp.status, raw, resp.headers.get("Retry-After")
+        except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
+            raise E.TransportError(f"{method} {target}: {type(e).__name__}: {e}") from e
+
     async def _headers(self, content_type: str | None, refresh: bool = False) -> dict:
-        h = {}
+        h = {"User-Agent": USER_AGENT, "Accept": _JSON}
         if content_type:
             h["Content-Type"] = content_type
         tok = await self.creds.token(force_refresh=refresh)
@@ -95,10 +130,11 @@ class RestClient(KubeClient):
 
     async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
                       content_type: str = _JSON):
-        session = await self._get_session()
-        url = self.cfg.server + path
+        target = path
         if params:
-            url += "?" + urlencode({k: v for k, v in params.items() if v is not None})
+            q = {k: v for k, v in params.items() if v is not None}
+            if q:
+                target += "?" + urlencode(q)
         data = None
         if body is not None:
             data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
@@ -106,16 +142,12 @@ class RestClient(KubeClient):
         attempt = 0
         while True:
             self.stats["requests"] += 1
+            headers = await self._headers(content_type if data is not None else None)
             try:
-                headers = await self._headers(content_type if data is not None else None, refresh=False)
-                async with session.request(method, url, data=data, headers=headers,
-                                           timeout=aiohttp.ClientTimeout(total=self.request_timeout)) as resp:
-                    raw = await resp.read()
-                    status = resp.status
-                    retry_after = resp.headers.get("Retry-After")
-            except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
+                status, raw, retry_after = await self._send(method, target, headers, data)
+            except E.TransportError:
                 self.stats["errors"] += 1
-                raise E.TransportError(f"{method} {url}: {type(e).__name__}: {e}") from e
+                raise
             if status < 300:
                 return json.loads(raw) if raw else None
             if status == 401 and self.cfg.exec is not None and not refreshed:
@@ -137,7 +169,7 @@ class RestClient(KubeClient):
             except ValueError:
                 st = None
             err = E.from_status(status, st if isinstance(st, dict) else None,
-                                fallback_message=raw[:200].decode(errors="replace"))
+                                fallback_message=bytes(raw[:200]).decode(errors="replace"))
             if retry_after is not None:
                 try:
                     err.retry_after = float(retry_after)
@@ -188,21 +220,40 @@ class RestClient(KubeClient):
 
     async def watch(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
                     allow_bookmarks=True, label_selector=None) -> AsyncIterator[WatchEvent]:
-        session = await self._get_session()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": timeout_seconds,
                   "allowWatchBookmarks": "true" if allow_bookmarks else None, "labelSelector": label_selector}
-        url = self.cfg.server + rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items()
-                                                                            if v is not None})
+        target = rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items() if v is not None})
+        self.stats["watch_streams"] += 1
+        headers = await self._headers(None)
+        loads = json.loads
+        if self.transport == "fast":
+            pool = await self._get_pool()
+            stream = pool.stream(target, headers, timeout=(timeout_seconds + 30) if timeout_seconds else None)
+            try:
+                async for resp, line in stream:
+                    if resp is not None:
+                        if resp.status >= 300:
+                            try:
+                                st = loads(line) if line else None
+                            except ValueError:
+                                st = None
+                            raise E.from_status(resp.status, st if isinstance(st, dict) else None)
+                        continue
+                    ev = loads(line)
+                    yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+            finally:
+                await stream.aclose()
+            return
+        session = await self._get_session()
+        url = self.cfg.server + target
         client_timeout = aiohttp.ClientTimeout(total=(timeout_seconds + 30) if timeout_seconds else None,
                                                sock_connect=self.request_timeout)
-        self.stats["watch_streams"] += 1
         try:
-            headers = await self._headers(None)
             async with session.get(url, headers=headers, timeout=client_timeout) as resp:
                 if resp.status >= 300:
                     raw = await resp.read()
                     try:
-                        st = json.loads(raw)
+                        st = loads(raw)
                     except ValueError:
                         st = None
                     raise E.from_status(resp.status, st if isinstance(st, dict) else None)
@@ -215,15 +266,18 @@ class RestClient(KubeClient):
                     buf = lines.pop()
                     for line in lines:
                         if line:
-                            ev = json.loads(line)
+                            ev = loads(line)
                             yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
                 if buf.strip():
-                    ev = json.loads(buf)
+                    ev = loads(buf)
                     yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
             raise E.TransportError(f"watch {url}: {type(e).__name__}: {e}") from e
 
     async def close(self) -> None:
+        if self._pool is not None:
+            self._pool.close()
+            self._pool = None
         if self._session is not None and not self._session.closed:
             await self._session.close()
         self._session = None

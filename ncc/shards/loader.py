@@ -38,9 +38,11 @@ def discover(shard_config_path: str) -> list[tuple[str, str]]:
     return out
 
 
-def default_client_factory(qps: float = 0.0, burst: int = 10, pool_size: int = 64) -> Callable[[str, str], KubeClient]:
+def default_client_factory(qps: float = 0.0, burst: int = 10, pool_size: int = 64,
+                           transport: str = "fast") -> Callable[[str, str], KubeClient]:
     def make(name: str, path: str) -> KubeClient:
-        client: KubeClient = RestClient(load_kubeconfig(path, name=name), pool_size=pool_size, cluster_name=name)
+        client: KubeClient = RestClient(load_kubeconfig(path, name=name), pool_size=pool_size, cluster_name=name,
+                                        transport=transport)
         if qps > 0:
             client = RateLimitedClient(client, qps, burst)
         return client

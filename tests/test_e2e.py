@@ -28,6 +28,18 @@ async def wait_for(pred, timeout=5.0, interval=0.02):
     raise AssertionError(f"condition not met within {timeout}s (last={last!r})")
 
 
+async def mutate(client, rt, name, fn, attempts=20):
+    """GET-modify-PUT with optimistic-concurrency retries (the controller writes status concurrently)."""
+    for _ in range(attempts):
+        cur = await client.get(rt, NS, name)
+        fn(cur)
+        try:
+            return await client.update(rt, NS, cur)
+        except E.Conflict:
+            await asyncio.sleep(0.01)
+    raise AssertionError(f"could not update {name}")
+
+
 async def _get(client, rt, name):
     return await client.get(rt, NS, name)
 
@@ -58,9 +70,8 @@ async def test_controller_main_propagates_create_and_update(tmp_path, mode):
         async with Running(env, mode):
             # the reference's integration test allows 1 s for each propagation step
             await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00000"), timeout=1.0)
-            cur = await cc.get(R.TEMPLATES, NS, "algo-00000")
-            cur["spec"]["container"]["versionTag"] = "v2.3.4"
-            await cc.update(R.TEMPLATES, NS, cur)
+            await mutate(cc, R.TEMPLATES, "algo-00000", lambda o: o["spec"]["container"].__setitem__("versionTag",
+                                                                                                  "v2.3.4"))
 
             async def propagated():
                 o = await sc.get(R.TEMPLATES, NS, "algo-00000")
@@ -80,8 +91,8 @@ async def test_controller_main_propagates_create_and_update(tmp_path, mode):
         await env.stop()
 
 
-@pytest.mark.parametrize("mode", ["compat", "native"])
-async def test_dependents_fan_out_and_delete(tmp_path, mode):
+@pytest.mark.parametrize("mode,transport", [("compat", "fast"), ("native", "fast"), ("native", "aiohttp")])
+async def test_dependents_fan_out_and_delete(tmp_path, mode, transport):
     env = await FakeEnvironment(2, str(tmp_path)).start()
     cc = env.controller_client()
     scs = [env.shard_client(i) for i in range(2)]
@@ -90,7 +101,7 @@ async def test_dependents_fan_out_and_delete(tmp_path, mode):
         await cc.create(R.CONFIGMAPS, NS, make_configmap("c0", NS))
         await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=["c0"]))
         await cc.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
-        async with Running(env, mode):
+        async with Running(env, mode, transport=transport):
             for sc in scs:
                 st = await wait_for(lambda sc=sc: _get(sc, R.TEMPLATES, "algo-00000"), timeout=3)
                 sec = await wait_for(lambda sc=sc: _get(sc, R.SECRETS, "s0"), timeout=3)
@@ -104,8 +115,7 @@ async def test_dependents_fan_out_and_delete(tmp_path, mode):
             assert ctrl_secret["metadata"]["ownerReferences"][0]["kind"] == C.TEMPLATE_KIND
 
             # data change in the controller cluster propagates to every shard
-            ctrl_secret["data"] = {"token": "bmV3"}
-            await cc.update(R.SECRETS, NS, ctrl_secret)
+            await mutate(cc, R.SECRETS, "s0", lambda o: o.__setitem__("data", {"token": "bmV3"}))
             for sc in scs:
                 async def updated(sc=sc):
                     return (await sc.get(R.SECRETS, NS, "s0")).get("data") == {"token": "bmV3"}
@@ -142,8 +152,8 @@ async def test_native_repairs_shard_drift_and_workgroup_delete(tmp_path):
         async with Running(env, "native"):
             st = await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00000"), timeout=2)
             # someone edits the shard copy: native mode watches shards and repairs it without waiting for resync
-            st["spec"]["container"]["versionTag"] = "tampered"
-            await sc.update(R.TEMPLATES, NS, st)
+            await mutate(sc, R.TEMPLATES, "algo-00000", lambda o: o["spec"]["container"].__setitem__(
+                "versionTag", "tampered"))
 
             async def repaired():
                 o = await sc.get(R.TEMPLATES, NS, "algo-00000")
