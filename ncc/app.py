@@ -25,14 +25,15 @@ from . import __version__
 from .api import constants as C
 from .api import resources as R
 from .cache.informer import InformerFactory
-from .config import AppConfig, load_config
+from .config import AppConfig, config_to_env, load_config
 from .controller.controller import Controller
-from .controller.events import BroadcastRecorder
+from .controller.events import BroadcastRecorder, FakeRecorder
+from .controller.executor import ExecutorPool
 from .controller.options import ControllerOptions
 from .kube.client import RateLimitedClient
 from .kube.kubeconfig import build_config
 from .kube.rest import RestClient
-from .shards.loader import default_client_factory, load_shards
+from .shards.loader import default_client_factory, discover, load_shards
 from .telemetry.logging import configure_logging
 from .telemetry.statsd import MultiMetrics, StatsdClient
 
@@ -47,7 +48,22 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
               rate_limit_burst=cfg.rate_limit_elements_burst, resync_period=cfg.resync_period)
     if cfg.mode == "native":
         kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout)
-    return ControllerOptions.for_mode(cfg.mode, **kw)
+    opts = ControllerOptions.for_mode(cfg.mode, **kw)
+    # expert/ablation overrides: NCC_OPT_<FIELD>=value (e.g. NCC_OPT_COALESCE_WINDOW=0)
+    for f, cur in opts.as_dict().items():
+        raw = os.environ.get("NCC_OPT_" + f.upper())
+        if raw is None:
+            continue
+        if isinstance(cur, bool) or cur is None and raw.lower() in ("true", "false"):
+            val = raw.lower() in ("1", "true", "yes")
+        elif isinstance(cur, int):
+            val = int(raw)
+        elif isinstance(cur, float) or cur is None:
+            val = float(raw)
+        else:
+            val = raw
+        setattr(opts, f, val)
+    return opts
 
 
 def client_limits(cfg: AppConfig) -> tuple[float, int]:
@@ -62,9 +78,14 @@ class App:
     """Wires and owns every component of one controller process."""
 
     def __init__(self, cfg: AppConfig, *, client_factory=None, controller_client=None, metrics=None,
-                 options: ControllerOptions | None = None):
+                 options: ControllerOptions | None = None, role: str | None = None, shard_filter: set | None = None):
         self.cfg = cfg
         self.options = options or options_from_config(cfg)
+        if role is not None:
+            self.options.role = role
+        self.shard_filter = shard_filter
+        self.pool: ExecutorPool | None = None
+        self.n_executors = 0
         qps, burst = client_limits(cfg)
         self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size,
                                                                        cfg.transport)
@@ -93,17 +114,30 @@ class App:
         self.client = client
         self.factory = InformerFactory(client, cfg.controller_namespace, o.resync_period)
         infs = {rt: self.factory.informer(rt) for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
-        self.shards = load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
-                                  client_factory=self.client_factory,
-                                  resync_period=0.0 if o.watch_shards else o.resync_period,
-                                  assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
-                                  slim=o.slim_shard_cache, start=False)
-        self.recorder = BroadcastRecorder(client, log_events=log.isEnabledFor(logging.DEBUG))
+        all_names = [n for n, _ in discover(cfg.shard_config_path)]
+        if o.role == "all" and o.mode == "native" and all_names:
+            n = cfg.executors if cfg.executors >= 0 else len(all_names)
+            self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
+            if self.n_executors > 0:
+                o.role = "coordinator"
+        if o.role == "coordinator":
+            self.shards = []
+        else:
+            self.shards = load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
+                                      client_factory=self.client_factory,
+                                      resync_period=0.0 if o.watch_shards else o.resync_period,
+                                      assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
+                                      slim=o.slim_shard_cache, start=False, names=self.shard_filter)
+        if o.role == "executor":
+            self.recorder = FakeRecorder(keep=False)  # executors never write to the controller cluster
+        else:
+            self.recorder = BroadcastRecorder(client, log_events=log.isEnabledFor(logging.DEBUG))
         self.controller = Controller(alias=cfg.alias, namespace=cfg.controller_namespace, client=client,
                                      shards=self.shards, template_informer=infs[R.TEMPLATES],
                                      workgroup_informer=infs[R.WORKGROUPS], secret_informer=infs[R.SECRETS],
                                      configmap_informer=infs[R.CONFIGMAPS], options=o, recorder=self.recorder,
-                                     metrics=self.metrics)
+                                     metrics=self.metrics,
+                                     shard_names=all_names if o.role == "coordinator" else None)
         if cfg.metrics_bind_address or cfg.health_bind_address:
             from .telemetry.http import OpsServer
             self.ops = OpsServer(ready=lambda: self.controller is not None and self.controller.ready.is_set(),
@@ -112,9 +146,12 @@ class App:
 
     def debug_state(self) -> dict:
         c = self.controller
-        return {"queue_depth": len(c.queue), "stats": c.stats, "queue": c.queue.metrics,
-                "shards": {s.name: {"synced": s.has_synced()} for s in c.shards},
-                "events": self.recorder.stats}
+        out = {"role": c.role, "queue_depth": len(c.queue), "stats": c.stats, "queue": c.queue.metrics,
+               "shards": {s.name: {"synced": s.has_synced()} for s in c.shards},
+               "events": getattr(self.recorder, "stats", {})}
+        if self.pool is not None:
+            out["executors"] = self.pool.stats()
+        return out
 
     async def run(self, stop: asyncio.Event) -> None:
         controller = self.controller or await self.build()
@@ -122,18 +159,28 @@ class App:
             await self.ops.start(self.cfg.health_bind_address or self.cfg.metrics_bind_address)
         for s in self.shards:
             s.start()
-        self.recorder.start()
+        if isinstance(self.recorder, BroadcastRecorder):
+            self.recorder.start()
         self.factory.start()
-        log.info("nexus-configuration-controller %s starting: mode=%s alias=%s namespace=%s shards=%s workers=%d",
-                 __version__, self.cfg.mode, self.cfg.alias, self.cfg.controller_namespace,
-                 [s.name for s in self.shards], self.options.workers)
+        if self.options.role == "coordinator":
+            env = dict(os.environ)
+            env.update(config_to_env(self.cfg))
+            self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
+                                     env=env)
+            self.pool.start()
+        log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
+                 "executors=%d workers=%d", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
+                 self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.options.workers)
         try:
             await controller.run(stop)
         finally:
             await self.close()
 
     async def close(self) -> None:
-        await self.recorder.stop()
+        if self.pool is not None:
+            await self.pool.stop()
+        if isinstance(self.recorder, BroadcastRecorder):
+            await self.recorder.stop()
         await self.factory.stop()
         for s in self.shards:
             await s.stop()

@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `transport`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`client-burst`, `client-pool-size`, `transport`, `executors`, `max-executors`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
 `metrics-bind-address`, `health-bind-address`, `log-format`.
 """
 from __future__ import annotations
@@ -79,6 +79,8 @@ class AppConfig:
     client_burst: int = 10
     client_pool_size: int = 64
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
+    executors: int = -1              # shard-executor processes; -1 = auto (native: one per shard, ≤ max)
+    max_executors: int = 16
     resync_period: float = _dur(30.0)
     full_resync_period: float = _dur(600.0)
     shard_sync_timeout: float = _dur(10.0)
@@ -136,3 +138,12 @@ def load_config(config_dir: str | None = None, env: dict | None = None) -> AppCo
         except ValueError as e:
             raise ValueError(f"invalid value for {AppConfig.key_of(f.name)}: {raw!r} ({e})") from e
     return cfg
+
+
+def config_to_env(cfg: AppConfig) -> dict:
+    """Render a config as NEXUS__* variables (how the coordinator hands its config to executors)."""
+    out = {}
+    for f in fields(AppConfig):
+        v = getattr(cfg, f.name)
+        out[AppConfig.env_of(f.name)] = repr(v) if isinstance(v, float) else str(v)
+    return out

@@ -21,7 +21,7 @@ import time
 
 from ..api import constants as C
 from ..api.objects import ObjectKey, meta
-from ..api.refs import template_owner_names
+from ..api.refs import configmap_names, secret_names, template_owner_names
 from ..cache.informer import DeletedFinalStateUnknown, Informer
 from ..telemetry.statsd import Metrics, NullMetrics
 from ..workqueue.queue import WorkQueue
@@ -48,7 +48,8 @@ class Controller(ReconcileMixin):
                  template_informer: Informer, workgroup_informer: Informer,
                  secret_informer: Informer, configmap_informer: Informer,
                  options: ControllerOptions | None = None, recorder: EventRecorder | None = None,
-                 metrics: Metrics | None = None, queue: WorkQueue | None = None):
+                 metrics: Metrics | None = None, queue: WorkQueue | None = None,
+                 shard_names: list[str] | None = None):
         self.alias = alias
         self.namespace = namespace
         self.client = client
@@ -71,8 +72,21 @@ class Controller(ReconcileMixin):
         self._pending_workgroup_deletes: set = set()
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
-        self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0}
+        self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0}
         self.ready = asyncio.Event()
+        self.role = o.role
+        self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
+        self.reporter = None  # executor role: callable(msg) sending results to the coordinator
+        self.on_ready = None  # executor role: called once caches are synced and workers run
+        self.shard_state: dict[str, dict] = {}  # coordinator role: key -> {shard: (uid, generation, error)}
+        self._pending_event: set = set()
+        if o.mode == "native":
+            # reverse index template ← referenced Secret/ConfigMap, so dependents map to templates even
+            # before adoption has stamped ownerRefs on them
+            self.template_informer.store.add_indexer(
+                "secret", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in secret_names(t)])
+            self.template_informer.store.add_indexer(
+                "configmap", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in configmap_names(t)])
         self._register_handlers()
 
     # ================================================================== handlers
@@ -86,9 +100,10 @@ class Controller(ReconcileMixin):
             on_add=lambda obj: self.enqueue_resource(obj, C.KIND_WORKGROUP),
             on_update=lambda old, new: self._on_crd_update(old, new, C.KIND_WORKGROUP),
             on_delete=self._on_workgroup_delete)
-        for inf in (self.secret_informer, self.configmap_informer):
-            inf.add_event_handler(on_add=self.handle_object, on_update=self._on_dependent_update,
-                                  on_delete=self.handle_object)
+        for inf, idx in ((self.secret_informer, "secret"), (self.configmap_informer, "configmap")):
+            inf.add_event_handler(on_add=lambda o, i=idx: self._on_dependent(o, i),
+                                  on_update=lambda old, new, i=idx: self._on_dependent_update(old, new, i),
+                                  on_delete=lambda o, i=idx: self._on_dependent(o, i))
         if o.watch_shards:
             for shard in self.shards:
                 self._register_shard_handlers(shard)
@@ -104,7 +119,15 @@ class Controller(ReconcileMixin):
                 return  # status-only change (typically our own status write)
         self.enqueue_resource(new, kind)
 
-    def _on_dependent_update(self, old: dict, new: dict) -> None:
+    def _on_dependent(self, obj, index: str):
+        obj = self._unwrap(obj)
+        if self.options.mode == "native":
+            ns, name = meta(obj).get("namespace", "") or "", meta(obj).get("name", "")
+            for t in self.template_informer.store.by_index(index, f"{ns}/{name}"):
+                self.enqueue_resource(t, C.KIND_TEMPLATE)
+        return self.handle_object(obj)
+
+    def _on_dependent_update(self, old: dict, new: dict, index: str = "secret") -> None:
         om, nm = meta(old), meta(new)
         if om.get("resourceVersion") == nm.get("resourceVersion"):
             # Periodic resync will send update events for all known Secrets/ConfigMaps (controller.go:324-328).
@@ -113,14 +136,23 @@ class Controller(ReconcileMixin):
                 and old.get("binaryData") == new.get("binaryData") and old.get("type") == new.get("type") \
                 and template_owner_names(old) == template_owner_names(new):
             return  # e.g. our own adoption PUT: ownerRef UIDs changed, payload did not
-        self.handle_object(new)
+        self._on_dependent(new, index)
 
     def enqueue_resource(self, obj, kind: str) -> None:
         """enqueueResource (controller.go:136-162)."""
         if isinstance(obj, DeletedFinalStateUnknown):
             obj = obj.obj
         m = meta(obj)
-        self.queue.add(make_key(kind, m.get("namespace", "") or "", m.get("name", "")))
+        self._enqueue_key(make_key(kind, m.get("namespace", "") or "", m.get("name", "")))
+
+    def _enqueue_key(self, key: str) -> None:
+        """Event-driven enqueue; native mode coalesces bursts (a template and its Secret/ConfigMap
+        changing together) into one reconcile by parking the key for `coalesce_window` seconds."""
+        w = self.options.coalesce_window
+        if w > 0:
+            self.queue.add_after(key, w)
+        else:
+            self.queue.add(key)
 
     def _unwrap(self, obj):
         if isinstance(obj, DeletedFinalStateUnknown):
@@ -168,7 +200,7 @@ class Controller(ReconcileMixin):
         ns, name = meta(obj).get("namespace", "") or "", meta(obj).get("name", "")
         if self.options.queued_deletes:
             self._pending_deletes.add((ns, name))
-            self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+            self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, name))
             return None
         return self._delete_template_inline(obj)
 
@@ -191,7 +223,7 @@ class Controller(ReconcileMixin):
             if ctl is None:
                 return
             if deleted or not spec_matches(ctl.get("spec"), obj):
-                self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+                self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, name))
 
         def workgroup_changed(old, new=None):
             obj = self._unwrap(new if new is not None else old)
@@ -201,7 +233,7 @@ class Controller(ReconcileMixin):
             if ctl is None:
                 return
             if deleted or not spec_matches(ctl.get("spec"), obj):
-                self.queue.add(make_key(C.KIND_WORKGROUP, ns, name))
+                self._enqueue_key(make_key(C.KIND_WORKGROUP, ns, name))
 
         def dependent_changed(lister, with_binary):
             def h(old, new=None):
@@ -215,7 +247,7 @@ class Controller(ReconcileMixin):
                     return
                 for owner in template_owner_names(obj) or template_owner_names(src):
                     if self.template_lister.try_get(ns, owner) is not None:
-                        self.queue.add(make_key(C.KIND_TEMPLATE, ns, owner))
+                        self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, owner))
             return h
 
         shard.template_informer.add_event_handler(on_update=template_changed, on_delete=template_changed)
@@ -225,6 +257,41 @@ class Controller(ReconcileMixin):
         shard.configmap_informer.add_event_handler(
             on_update=dependent_changed(self.configmap_lister, self.options.sync_binary_data),
             on_delete=dependent_changed(self.configmap_lister, self.options.sync_binary_data))
+
+    # ================================================================== coordinator / executor plumbing
+    def _report(self, kind: str, namespace: str, name: str, obj: dict, results: dict) -> None:
+        """Executor → coordinator: outcome of one pass over this executor's shards."""
+        if self.reporter is None:
+            return
+        m = meta(obj)
+        self.reporter({"t": "report", "k": make_key(kind, namespace, name), "u": m.get("uid", ""),
+                       "g": int(m.get("generation") or 0), "r": results, "w": self._last_pass_wrote()})
+
+    def on_executor_message(self, index: int, msg: dict) -> None:
+        """Coordinator: fold an executor report into `shard_state` and re-evaluate that object."""
+        if msg.get("t") != "report":
+            return
+        self.stats["reports"] += 1
+        key = msg["k"]
+        st = self.shard_state.setdefault(key, {})
+        for shard, err in msg["r"].items():
+            st[shard] = (msg["u"], msg["g"], err)
+        if msg.get("w"):
+            self._pending_event.add(key)
+        self._enqueue_key(key)
+
+    def shard_readiness(self, key: str, obj: dict):
+        """None while some shard has not reported on this object version, else {shard: error|None}."""
+        m = meta(obj)
+        uid, gen = m.get("uid", ""), int(m.get("generation") or 0)
+        st = self.shard_state.get(key) or {}
+        out = {}
+        for s in self.all_shard_names:
+            e = st.get(s)
+            if e is None or e[0] != uid or e[1] < gen:
+                return None
+            out[s] = e[2]
+        return out
 
     # ================================================================== helpers
     def _assume(self, informer: Informer, res):
@@ -316,6 +383,8 @@ class Controller(ReconcileMixin):
         if self.options.full_resync_period > 0:
             self._aux.append(asyncio.ensure_future(self._full_resync_loop()))
         self.ready.set()
+        if self.on_ready is not None:
+            self.on_ready()
         log.info("Started %d workers", n)
 
     def sweep_orphans(self) -> int:
@@ -325,13 +394,13 @@ class Controller(ReconcileMixin):
             for st in shard.template_lister.list():
                 ns, name = meta(st).get("namespace", ""), meta(st).get("name", "")
                 if self._is_ours(st) and self.template_lister.try_get(ns, name) is None:
-                    self.queue.add(make_key(C.KIND_TEMPLATE, ns, name))
+                    self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, name))
                     n += 1
             if self.options.propagate_workgroup_deletes:
                 for sw in shard.workgroup_lister.list():
                     ns, name = meta(sw).get("namespace", ""), meta(sw).get("name", "")
                     if self._is_ours(sw) and self.workgroup_lister.try_get(ns, name) is None:
-                        self.queue.add(make_key(C.KIND_WORKGROUP, ns, name))
+                        self._enqueue_key(make_key(C.KIND_WORKGROUP, ns, name))
                         n += 1
         return n
 

@@ -1,0 +1,195 @@
+"""Shard executors: one OS process per group of shards, supervised by the coordinator.
+
+The reference reconciles every shard from one process, sequentially (controller.go:790).  A
+Python control plane is CPU-bound per request, so native mode splits the work the way a
+multi-GPU trainer splits ranks — one process per shard (MI355X node) — while keeping a single
+writer for the controller cluster:
+
+* **coordinator** (the `python -m ncc` process): controller-cluster informers, status
+  conditions, adoption of referenced Secrets/ConfigMaps, Events; aggregates per-shard results.
+* **executors** (`python -m ncc.executor`, spawned here): each watches the controller cluster
+  read-only (desired state) plus its own shards, and reconciles desired → shard with its own
+  queue and workers.  After every pass it reports `(key, generation, {shard: error|None}, wrote)`
+  to the coordinator over a socketpair (msgpack frames, `ncc.controller.ipc`).
+
+Executors never write to the controller cluster, so the coordinator stays the only writer of
+status and ownerRefs and no cross-process write races are introduced.  A crashed executor is
+restarted with exponential backoff; its shards are level-triggered, so the restart resyncs them.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import socket
+import sys
+
+from .ipc import Channel
+
+log = logging.getLogger("ncc.executor")
+
+
+def partition(names: list[str], n: int) -> list[list[str]]:
+    """Round-robin shard → executor assignment (stable for a given shard list)."""
+    n = max(1, min(n, len(names)))
+    parts: list[list[str]] = [[] for _ in range(n)]
+    for i, s in enumerate(names):
+        parts[i % n].append(s)
+    return parts
+
+
+class ExecutorHandle:
+    def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None):
+        self.index = index
+        self.shards = shards
+        self.on_message = on_message
+        self.env = env
+        self.proc: asyncio.subprocess.Process | None = None
+        self.channel: Channel | None = None
+        self.ready = asyncio.Event()
+        self.restarts = 0
+        self._task: asyncio.Task | None = None
+        self._stopping = False
+
+    async def _spawn(self) -> None:
+        parent, child = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(self.env or os.environ)
+        env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+        self.proc = await asyncio.create_subprocess_exec(
+            sys.executable, "-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
+            "--shards", ",".join(self.shards), pass_fds=(child.fileno(),), env=env)
+        child.close()
+        reader, writer = await asyncio.open_connection(sock=parent)
+        self.channel = Channel(reader, writer)
+
+    async def _run(self) -> None:
+        backoff = 1.0
+        while not self._stopping:
+            self.ready.clear()
+            await self._spawn()
+            while True:
+                batch = await self.channel.recv()
+                if batch is None:
+                    break
+                for msg in batch:
+                    if msg.get("t") == "ready":
+                        self.ready.set()
+                    self.on_message(self.index, msg)
+            rc = await self.proc.wait()
+            self.channel.close()
+            if self._stopping:
+                return
+            self.restarts += 1
+            log.error("executor %d (shards %s) exited with %s; restarting in %.1fs", self.index, self.shards, rc,
+                      backoff)
+            await asyncio.sleep(backoff)
+            backoff = min(backoff * 2, 30.0)
+
+    def start(self) -> None:
+        self._task = asyncio.ensure_future(self._run())
+
+    async def stop(self, timeout: float = 10.0) -> None:
+        self._stopping = True
+        if self.proc is not None and self.proc.returncode is None:
+            try:
+                self.proc.terminate()
+                await asyncio.wait_for(self.proc.wait(), timeout)
+            except (ProcessLookupError, asyncio.TimeoutError):
+                try:
+                    self.proc.kill()
+                except ProcessLookupError:
+                    pass
+        if self._task is not None:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+
+
+class ExecutorPool:
+    def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None):
+        self.handles = [ExecutorHandle(i, part, on_message, env) for i, part in enumerate(partition(shard_names, n))]
+
+    def start(self) -> None:
+        for h in self.handles:
+            h.start()
+
+    async def wait_ready(self, timeout: float | None = None) -> bool:
+        try:
+            await asyncio.wait_for(asyncio.gather(*(h.ready.wait() for h in self.handles)), timeout)
+            return True
+        except asyncio.TimeoutError:
+            return False
+
+    async def stop(self) -> None:
+        await asyncio.gather(*(h.stop() for h in self.handles))
+
+    def stats(self) -> dict:
+        return {h.index: {"shards": h.shards, "restarts": h.restarts,
+                          "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
+
+
+# ---------------------------------------------------------------------------------------- executor side
+async def executor_main(fd: int, index: int, shards: list[str]) -> int:
+    from ..app import App, setup_signal_handler
+    from ..config import load_config
+
+    cfg = load_config()
+    sock = socket.socket(fileno=fd)
+    reader, writer = await asyncio.open_connection(sock=sock)
+    channel = Channel(reader, writer)
+    stop = asyncio.Event()
+    setup_signal_handler(stop)
+    app = App(cfg, role="executor", shard_filter=set(shards))
+    await app.build()
+    ctl = app.controller
+    ctl.reporter = channel.send
+    ctl.on_ready = lambda: channel.send({"t": "ready", "i": index})
+
+    async def watch_parent():
+        # the coordinator closing its end (or dying) ends this executor
+        while True:
+            if await channel.recv() is None:
+                stop.set()
+                return
+
+    wp = asyncio.ensure_future(watch_parent())
+    try:
+        await app.run(stop)
+    finally:
+        wp.cancel()
+        try:
+            await channel.drain()
+        except Exception:  # noqa: BLE001
+            pass
+        channel.close()
+    return 0
+
+
+def main(argv=None) -> int:
+    import argparse
+
+    from ..config import load_config
+    from ..telemetry.logging import configure_logging
+
+    p = argparse.ArgumentParser(prog="python -m ncc.executor")
+    p.add_argument("--fd", type=int, required=True)
+    p.add_argument("--index", type=int, default=0)
+    p.add_argument("--shards", default="")
+    a = p.parse_args(argv)
+    cfg = load_config()
+    configure_logging(cfg.log_level, cfg.log_format)
+    logging.getLogger().handlers[0].addFilter(lambda r: setattr(r, "executor", a.index) or True)
+    prof_path = os.environ.get("NCC_PROFILE")
+    if prof_path:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s]))
+        finally:
+            prof.disable()
+            prof.dump_stats(f"{prof_path}.executor{a.index}")
+    return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s]))

@@ -39,6 +39,8 @@ class ControllerOptions:
     wait_for_shards_timeout: float | None = None  # controller.go:866-870 waits forever
     full_resync_period: float = 0.0        # periodic enqueue-all sweep (native replaces informer resync)
     native_queue: bool | None = None       # None: use the C++ queue when built
+    coalesce_window: float = 0.0           # seconds to park event-triggered keys so bursts collapse
+    role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
 
     @classmethod
     def compat(cls, **kw) -> "ControllerOptions":
@@ -66,6 +68,7 @@ class ControllerOptions:
             slim_shard_cache=True,
             wait_for_shards_timeout=10.0,
             full_resync_period=600.0,
+            coalesce_window=0.005,
         )
         return replace(base, **kw)
 

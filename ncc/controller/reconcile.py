@@ -209,11 +209,20 @@ class ReconcileMixin:
         if template is None:
             log.debug("NexusAlgorithmTemplate %s/%s referenced by item in work queue no longer exists",
                       namespace, name)
-            if self.options.queued_deletes:
+            if self.role == "coordinator":
+                self.shard_state.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
+                self._pending_event.discard(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
+            elif self.options.queued_deletes:
                 await self.propagate_template_delete(namespace, name)
+            return
+        if self.role == "executor":
+            await self._executor_sync_template(template)
             return
         template = await self.report_template_init_condition(template)
         await self.adopt_references(template)
+        if self.role == "coordinator":
+            await self._coordinator_finish(C.KIND_TEMPLATE, template)
+            return
 
         shard_names = self.shard_names()
         spec = template.get("spec")
@@ -242,6 +251,57 @@ class ReconcileMixin:
         if self.options.event_on_noop or self._last_pass_wrote():
             self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
                                 C.MESSAGE_RESOURCE_SYNCED.format("NexusAlgorithmTemplate"), kind=C.TEMPLATE_KIND)
+
+    async def _executor_sync_template(self, template: dict) -> None:
+        """Executor role: fan out to this process's shards only and report to the coordinator."""
+        ns, name = meta(template).get("namespace", ""), meta(template).get("name", "")
+        # the coordinator adopts; an executor only refuses to write when a reference is missing (as adoption would)
+        for nm in secret_names(template):
+            self.secret_lister.get(ns, nm)
+        for nm in configmap_names(template):
+            self.configmap_lister.get(ns, nm)
+        results = await asyncio.gather(*(self._sync_template_to_shard(template, s, None) for s in self.shards),
+                                       return_exceptions=True)
+        failures = {}
+        for s, r in zip(self.shards, results):
+            if isinstance(r, asyncio.CancelledError):
+                raise r
+            if isinstance(r, BaseException):
+                failures[s.name] = r
+        self._report(C.KIND_TEMPLATE, ns, name, template,
+                     {s.name: (f"{type(failures[s.name]).__name__}: {failures[s.name]}"[:500]
+                               if s.name in failures else None) for s in self.shards})
+        if failures:
+            raise ShardSyncError(failures)
+
+    async def _coordinator_finish(self, kind: str, obj: dict) -> None:
+        """Coordinator role: turn the executors' per-shard reports into the status condition."""
+        ns, name = meta(obj).get("namespace", ""), meta(obj).get("name", "")
+        key = f"{kind}/{ns}/{name}"
+        results = self.shard_readiness(key, obj)
+        if results is None:
+            return  # some shard has not reported on this version yet; its report re-enqueues the key
+        failures = sorted(s for s, e in results.items() if e)
+        ok = [s for s in self.all_shard_names if not results[s]]
+        is_template = kind == C.KIND_TEMPLATE
+        if failures:
+            what = f"Algorithm {q(name)}" if is_template else f"Workgroup {q(name)}"
+            msg = f"{what} failed to sync to shards: {', '.join(failures)}"
+            if is_template:
+                await self.report_template_synced_condition(obj, secret_names(obj), configmap_names(obj), ok,
+                                                            ready=False, message=msg)
+            else:
+                await self.report_workgroup_synced_condition(obj, ready=False, message=msg)
+            return
+        if is_template:
+            obj = await self.report_template_synced_condition(obj, secret_names(obj), configmap_names(obj), ok)
+        else:
+            obj = await self.report_workgroup_synced_condition(obj)
+        if key in self._pending_event or self._last_pass_wrote() or self.options.event_on_noop:
+            self._pending_event.discard(key)
+            kind_name = C.TEMPLATE_KIND if is_template else C.WORKGROUP_KIND
+            self.recorder.event(obj, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                C.MESSAGE_RESOURCE_SYNCED.format(kind_name), kind=kind_name)
 
     async def _sync_template_to_shard(self, template: dict, shard, spec_fp) -> None:
         if self.options.wait_for_shards_timeout is not None and not shard.has_synced():
@@ -419,10 +479,26 @@ class ReconcileMixin:
         if workgroup is None:
             log.debug("NexusAlgorithmWorkgroup %s/%s referenced by item in work queue no longer exists",
                       namespace, name)
-            if self.options.propagate_workgroup_deletes:
+            if self.role == "coordinator":
+                self.shard_state.pop(f"{C.KIND_WORKGROUP}/{namespace}/{name}", None)
+                self._pending_event.discard(f"{C.KIND_WORKGROUP}/{namespace}/{name}")
+            elif self.options.propagate_workgroup_deletes:
                 await self.propagate_workgroup_delete(namespace, name)
             return
+        if self.role == "executor":
+            results = await asyncio.gather(*(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards),
+                                           return_exceptions=True)
+            failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
+            self._report(C.KIND_WORKGROUP, namespace, name, workgroup,
+                         {s.name: (f"{type(failures[s.name]).__name__}: {failures[s.name]}"[:500]
+                                   if s.name in failures else None) for s in self.shards})
+            if failures:
+                raise ShardSyncError(failures)
+            return
         workgroup = await self.report_workgroup_init_condition(workgroup)
+        if self.role == "coordinator":
+            await self._coordinator_finish(C.KIND_WORKGROUP, workgroup)
+            return
         if self.options.concurrent_fanout:
             results = await asyncio.gather(*(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards),
                                            return_exceptions=True)
