@@ -1,0 +1,216 @@
+"""Minimal HTTP/1.1 server on asyncio Protocols for the fake kube-apiserver.
+
+A real kube-apiserver is a multi-core Go process that sustains tens of thousands of writes per
+second; a benchmark substrate that spends ~150 µs of Python per request in a generic web
+framework would make the *substrate* the bottleneck of every fan-out measurement.  This server
+implements exactly what the fake apiserver needs — keep-alive connections, Content-Length
+request bodies, Content-Length responses and chunked streaming responses (watches) with write
+back-pressure — with one Python-level pass over each request head.
+
+The handler API mirrors the subset of aiohttp.web the fake apiserver was written against
+(`request.path/.method/.query/.headers/.content_type/.read()`, `Response`, `StreamResponse`).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+from urllib.parse import parse_qsl, unquote
+
+_CRLF2 = b"\r\n\r\n"
+_REASONS = {200: "OK", 201: "Created", 204: "No Content", 400: "Bad Request", 401: "Unauthorized",
+            403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed", 409: "Conflict", 410: "Gone",
+            415: "Unsupported Media Type", 422: "Unprocessable Entity", 429: "Too Many Requests",
+            500: "Internal Server Error", 503: "Service Unavailable", 504: "Gateway Timeout"}
+
+
+class Request:
+    __slots__ = ("method", "path", "raw_query", "headers", "body", "_query", "_conn")
+
+    def __init__(self, method: str, target: str, headers: dict, body: bytes):
+        self.method = method
+        path, _, q = target.partition("?")
+        self.path = unquote(path)
+        self.raw_query = q
+        self.headers = headers
+        self.body = body
+        self._query = None
+
+    @property
+    def query(self) -> dict:
+        if self._query is None:
+            self._query = dict(parse_qsl(self.raw_query, keep_blank_values=True))
+        return self._query
+
+    @property
+    def content_type(self) -> str:
+        return self.headers.get("content-type", "application/octet-stream").split(";", 1)[0].strip()
+
+    @property
+    def can_read_body(self) -> bool:
+        return bool(self.body)
+
+    async def read(self) -> bytes:
+        return self.body
+
+
+class Response:
+    __slots__ = ("status", "body", "content_type", "headers")
+
+    def __init__(self, status: int = 200, body: bytes | None = None, text: str | None = None,
+                 content_type: str | None = None, headers: dict | None = None):
+        self.status = status
+        if text is not None:
+            body = text.encode()
+            content_type = content_type or "text/plain"
+        self.body = body or b""
+        self.content_type = content_type or "application/json"
+        self.headers = headers or {}
+
+    def encode(self) -> bytes:
+        h = [f"HTTP/1.1 {self.status} {_REASONS.get(self.status, 'Status')}", f"Content-Type: {self.content_type}",
+             f"Content-Length: {len(self.body)}"]
+        for k, v in self.headers.items():
+            h.append(f"{k}: {v}")
+        return ("\r\n".join(h) + "\r\n\r\n").encode() + self.body
+
+
+def json_response(obj, status: int = 200) -> Response:
+    return Response(status=status, body=json.dumps(obj, separators=(",", ":")).encode())
+
+
+class StreamResponse:
+    """Chunked streaming response (watch).  `prepare` sends the head; `write` sends one chunk."""
+
+    def __init__(self, status: int = 200, headers: dict | None = None):
+        self.status = status
+        self.headers = {k: v for k, v in (headers or {}).items() if k.lower() != "transfer-encoding"}
+        self._conn: "_ServerConn | None" = None
+        self.prepared = False
+
+    async def prepare(self, request: Request) -> None:
+        conn = request._conn  # type: ignore[attr-defined]
+        self._conn = conn
+        h = [f"HTTP/1.1 {self.status} {_REASONS.get(self.status, 'Status')}", "Transfer-Encoding: chunked"]
+        for k, v in self.headers.items():
+            h.append(f"{k}: {v}")
+        conn.transport.write(("\r\n".join(h) + "\r\n\r\n").encode())
+        self.prepared = True
+
+    async def write(self, data: bytes) -> None:
+        c = self._conn
+        if c is None or c.closed:
+            raise ConnectionResetError("client went away")
+        if data:
+            c.transport.write(b"%x\r\n%s\r\n" % (len(data), data))
+        await c.drain()
+
+    async def write_eof(self) -> None:
+        c = self._conn
+        if c is not None and not c.closed:
+            c.transport.write(b"0\r\n\r\n")
+
+
+class _ServerConn(asyncio.Protocol):
+    def __init__(self, server: "HttpServer"):
+        self.server = server
+        self.transport = None
+        self.buf = bytearray()
+        self.closed = False
+        self.busy = False
+        self._drain: asyncio.Future | None = None
+
+    def connection_made(self, transport):
+        self.transport = transport
+        self.server._conns.add(self)
+
+    def connection_lost(self, exc):
+        self.closed = True
+        self.server._conns.discard(self)
+        if self._drain is not None and not self._drain.done():
+            self._drain.set_result(None)
+
+    def pause_writing(self):
+        if self._drain is None or self._drain.done():
+            self._drain = asyncio.get_running_loop().create_future()
+
+    def resume_writing(self):
+        if self._drain is not None and not self._drain.done():
+            self._drain.set_result(None)
+
+    async def drain(self):
+        if self._drain is not None and not self._drain.done():
+            await self._drain
+
+    def data_received(self, data: bytes):
+        self.buf += data
+        if not self.busy:
+            self._next()
+
+    def _next(self):
+        buf = self.buf
+        i = buf.find(_CRLF2)
+        if i < 0:
+            if len(buf) > 1 << 20:
+                self.transport.close()
+            return
+        lines = bytes(buf[:i]).split(b"\r\n")
+        try:
+            method, target, _ = lines[0].decode("latin-1").split(" ", 2)
+        except ValueError:
+            self.transport.close()
+            return
+        headers = {}
+        for ln in lines[1:]:
+            k, _, v = ln.partition(b":")
+            headers[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
+        clen = int(headers.get("content-length", "0") or 0)
+        if len(buf) < i + 4 + clen:
+            return  # wait for the full body
+        body = bytes(buf[i + 4:i + 4 + clen])
+        del buf[:i + 4 + clen]
+        req = Request(method, target, headers, body)
+        req._conn = self  # type: ignore[attr-defined]
+        self.busy = True
+        keep = headers.get("connection", "").lower() != "close"
+        coro = self.server.handler(req)
+        task = asyncio.ensure_future(coro)
+        task.add_done_callback(lambda t, k=keep: self._done(t, k))
+
+    def _done(self, task: asyncio.Task, keep: bool):
+        self.busy = False
+        if self.closed:
+            return
+        try:
+            resp = task.result()
+        except Exception as e:  # noqa: BLE001
+            resp = Response(500, text=f"internal error: {e}")
+        if isinstance(resp, Response):
+            self.transport.write(resp.encode())
+        if not keep:
+            self.transport.close()
+            return
+        if self.buf:
+            self._next()
+
+
+class HttpServer:
+    def __init__(self, handler):
+        self.handler = handler
+        self._server: asyncio.AbstractServer | None = None
+        self._conns: set = set()
+        self.port: int | None = None
+
+    async def start(self, host: str, port: int, ssl_context=None) -> int:
+        loop = asyncio.get_running_loop()
+        self._server = await loop.create_server(lambda: _ServerConn(self), host, port, ssl=ssl_context, backlog=1024)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self.port
+
+    async def stop(self) -> None:
+        if self._server is not None:
+            self._server.close()
+            for c in list(self._conns):
+                if c.transport is not None:
+                    c.transport.close()
+            await self._server.wait_closed()
+            self._server = None

@@ -1,4 +1,4 @@
-"""HTTP front-end of the fake kube-apiserver (aiohttp), over `ClusterState`.
+"""HTTP front-end of the fake kube-apiserver (lean asyncio HTTP/1.1 server), over `ClusterState`.
 
 Serves the REST surface the controller uses — core `/api/v1` and CRD `/apis/{group}/{version}`
 paths, namespaced and cluster-wide, `GET` (get / list / `?watch=1`), `POST`, `PUT`
@@ -25,7 +25,7 @@ import signal
 import ssl
 import time
 
-from aiohttp import web
+from . import httpserver as web
 
 from ..api import resources as R
 from ..kube import errors as E
@@ -87,28 +87,19 @@ class FakeApiServer:
         self.state.write_hooks.append(self.markers.on_write)
         self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
         self._streams: set = set()
-        self.app = web.Application(client_max_size=64 * 1024 * 1024)
-        self.app.router.add_route("*", "/{tail:.*}", self._dispatch)
-        self._runner: web.AppRunner | None = None
+        self._http = web.HttpServer(self._dispatch)
         self.port: int | None = None
         self.url: str | None = None
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context: ssl.SSLContext | None = None) -> str:
-        self._runner = web.AppRunner(self.app, access_log=None, handle_signals=False)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, host, port, ssl_context=ssl_context, backlog=1024)
-        await site.start()
-        sock = site._server.sockets[0]  # type: ignore[union-attr]
-        self.port = sock.getsockname()[1]
+        self.port = await self._http.start(host, port, ssl_context)
         self.url = f"{'https' if ssl_context else 'http'}://{host}:{self.port}"
         return self.url
 
     async def stop(self) -> None:
         self.state.close_watchers()
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        await self._http.stop()
 
     def drop_watches(self) -> None:
         self.state.close_watchers()
@@ -273,7 +264,7 @@ class FakeApiServer:
             await resp.write(_dumps({"type": "ERROR", "object": e.status_object()}) + b"\n")
             await resp.write_eof()
             return resp
-        resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON, "Transfer-Encoding": "chunked"})
+        resp = web.StreamResponse(status=200, headers={"Content-Type": _JSON})
         await resp.prepare(request)
         self.requests["watch_streams"] += 1
         self._streams.add(w)
