@@ -27,6 +27,7 @@ class Store:
         self._indexers: dict[str, IndexFunc] = {}
         self._indices: dict[str, dict[str, set]] = {}
         self._assumed: dict[ObjectKey, tuple[dict, int, float]] = {}
+        self._tombstones: dict[ObjectKey, int] = {}  # key -> RV of the observed delete
         self.transform = transform
         self.assume_ttl = assume_ttl
 
@@ -72,6 +73,12 @@ class Store:
         key = obj_or_key if isinstance(obj_or_key, tuple) else key_of(obj_or_key)
         old = self._items.pop(key, None)
         self._assumed.pop(key, None)
+        if not isinstance(obj_or_key, tuple):
+            rv = rv_int((obj_or_key.get("metadata") or {}).get("resourceVersion"))
+            if rv >= 0:
+                if len(self._tombstones) > 16384:
+                    self._tombstones.clear()
+                self._tombstones[key] = rv
         if old is not None and self._indexers:
             self._index(key, old, None)
         return old
@@ -95,6 +102,11 @@ class Store:
             if k not in new_items:
                 deleted.append(o)
         self._items = new_items
+        if self._assumed:  # a relist is authoritative: drop overlays for vanished or caught-up keys
+            for k in list(self._assumed):
+                cur = new_items.get(k)
+                if cur is None or rv_int((cur.get("metadata") or {}).get("resourceVersion")) >= self._assumed[k][1]:
+                    del self._assumed[k]
         for name, fn in self._indexers.items():
             idx: dict[str, set] = {}
             for k, o in new_items.items():
@@ -114,6 +126,8 @@ class Store:
         cur = self._items.get(key)
         if cur is not None and rv_int((cur.get("metadata") or {}).get("resourceVersion")) >= rv:
             return
+        if cur is None and self._tombstones.get(key, -1) >= rv:
+            return  # a late write result for an object we have already seen deleted
         prev = self._assumed.get(key)
         if prev is not None and prev[1] >= rv:
             return

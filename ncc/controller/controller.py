@@ -299,6 +299,10 @@ class Controller(ReconcileMixin):
             informer.store.assume(res)
         return res
 
+    def _begin_pass(self) -> None:
+        """Start write-tracking for one reconcile (children spawned by gather share the state)."""
+        _pass_state.set([False])
+
     def _pass_wrote(self) -> None:
         st = _pass_state.get()
         if st is not None:

@@ -205,6 +205,7 @@ class ReconcileMixin:
 
     # ============================================================ templates (controller.go:761-845)
     async def sync_template(self, namespace: str, name: str) -> None:
+        self._begin_pass()
         template = self.template_lister.try_get(namespace, name)
         if template is None:
             log.debug("NexusAlgorithmTemplate %s/%s referenced by item in work queue no longer exists",
@@ -475,6 +476,7 @@ class ReconcileMixin:
 
     # ============================================================ workgroups (controller.go:697-756)
     async def sync_workgroup(self, namespace: str, name: str) -> None:
+        self._begin_pass()
         workgroup = self.workgroup_lister.try_get(namespace, name)
         if workgroup is None:
             log.debug("NexusAlgorithmWorkgroup %s/%s referenced by item in work queue no longer exists",

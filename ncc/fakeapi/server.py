@@ -150,7 +150,7 @@ class FakeApiServer:
                                              "platform": "linux/amd64"}), content_type=_JSON)
         try:
             if self.token is not None:
-                auth = request.headers.get("Authorization", "")
+                auth = request.headers.get("authorization", "")
                 if auth != f"Bearer {self.token}":
                     raise E.Unauthorized("Unauthorized")
             f = self.faults

@@ -10,7 +10,20 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def _ensure_native():
+    """Build the in-tree C++ extension once if it is missing or stale (seconds with g++)."""
+    sys.path.insert(0, os.path.join(ROOT, "native"))
+    try:
+        import build as native_build
+        native_build.build()
+    except Exception as e:  # noqa: BLE001 — tests that need it skip or fail loudly on their own
+        print(f"[conftest] native extension build skipped: {e}", file=sys.stderr)
+    finally:
+        sys.path.pop(0)
+
+
 def pytest_configure(config):
+    _ensure_native()
     config.addinivalue_line("markers", "gpu: needs the MI355X box (run by the driver's `pytest -m gpu` tier)")
     config.addinivalue_line("markers", "slow: multi-second scale / soak tests")
 

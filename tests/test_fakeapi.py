@@ -1,0 +1,192 @@
+"""Fake kube-apiserver fidelity: the substrate every integration test and benchmark stands on."""
+import asyncio
+
+import pytest
+
+from ncc.api import resources as R
+from ncc.fakeapi.server import FakeApiServer
+from ncc.fakeapi.storage import ClusterState
+from ncc.kube import errors as E
+from ncc.kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+from ncc.kube.kubeconfig import ClusterConfig
+from ncc.kube.rest import RestClient
+from ncc.testing.workload import make_configmap, make_secret, make_template
+
+NS = "nexus"
+
+
+def test_create_assigns_metadata_and_rejects_duplicates():
+    s = ClusterState()
+    o = s.create(R.TEMPLATES, NS, make_template(1, NS))
+    m = o["metadata"]
+    assert m["uid"] and m["resourceVersion"] == "1" and m["generation"] == 1 and m["creationTimestamp"]
+    with pytest.raises(E.AlreadyExists):
+        s.create(R.TEMPLATES, NS, make_template(1, NS))
+    bad = make_template(2, NS)
+    bad["metadata"]["resourceVersion"] = "5"
+    with pytest.raises(E.BadRequest):
+        s.create(R.TEMPLATES, NS, bad)
+
+
+def test_update_conflicts_noops_generation_and_status_isolation():
+    s = ClusterState()
+    o = s.create(R.TEMPLATES, NS, make_template(1, NS))
+    stale = dict(o, metadata=dict(o["metadata"]))
+    o2 = s.update(R.TEMPLATES, NS, dict(o, spec=dict(o["spec"], command="bash")))
+    assert o2["metadata"]["generation"] == 2 and o2["metadata"]["resourceVersion"] == "2"
+    with pytest.raises(E.Conflict):
+        s.update(R.TEMPLATES, NS, stale)
+    same = s.update(R.TEMPLATES, NS, o2)   # no-op: no RV bump, no event
+    assert same["metadata"]["resourceVersion"] == "2" and s.stats["noop_update"] == 1
+    st = s.update(R.TEMPLATES, NS, dict(o2, status={"conditions": [{"type": "Ready"}]}), subresource="status")
+    assert st["metadata"]["generation"] == 2 and st["status"]["conditions"][0]["type"] == "Ready"
+    # a main-resource write cannot change status
+    back = s.update(R.TEMPLATES, NS, dict(st, status={}, spec=dict(st["spec"], command="sh")))
+    assert back["status"] == st["status"] and back["metadata"]["generation"] == 3
+
+
+def test_gc_deletes_orphans_and_strips_dangling_refs():
+    s = ClusterState()
+    t1 = s.create(R.TEMPLATES, NS, make_template(1, NS))
+    t2 = s.create(R.TEMPLATES, NS, make_template(2, NS))
+    ref = lambda t: {"apiVersion": "science.sneaksanddata.com/v1", "kind": "NexusAlgorithmTemplate",  # noqa: E731
+                     "name": t["metadata"]["name"], "uid": t["metadata"]["uid"]}
+    only = make_secret("only", NS)
+    only["metadata"]["ownerReferences"] = [ref(t1)]
+    shared = make_configmap("shared", NS)
+    shared["metadata"]["ownerReferences"] = [ref(t1), ref(t2)]
+    s.create(R.SECRETS, NS, only)
+    s.create(R.CONFIGMAPS, NS, shared)
+    s.delete(R.TEMPLATES, NS, t1["metadata"]["name"])
+    with pytest.raises(E.NotFound):
+        s.get(R.SECRETS, NS, "only")
+    left = s.get(R.CONFIGMAPS, NS, "shared")
+    assert [r["uid"] for r in left["metadata"]["ownerReferences"]] == [t2["metadata"]["uid"]]
+
+
+async def test_watch_replay_and_gone():
+    s = ClusterState(history=3)
+    s.create(R.SECRETS, NS, make_secret("a", NS))      # rv1
+    w = s.watch(R.SECRETS, NS, "1")
+    s.create(R.SECRETS, NS, make_secret("b", NS))      # rv2
+    s.delete(R.SECRETS, NS, "a")                       # rv3
+    evs = [await w.queue.get(), await w.queue.get()]
+    assert [e.type for e in evs] == ["ADDED", "DELETED"] and evs[1].obj["metadata"]["resourceVersion"] == "3"
+    for i in range(5):
+        s.create(R.SECRETS, NS, make_secret(f"x{i}", NS))
+    with pytest.raises(E.Gone):
+        s.watch(R.SECRETS, NS, "1")
+    w0 = s.watch(R.SECRETS, NS, "0")                    # synthetic ADDED for current objects
+    assert w0.queue.qsize() == 6
+
+
+def test_patches():
+    s = ClusterState()
+    s.create(R.CONFIGMAPS, NS, make_configmap("c", NS))
+    o = s.patch(R.CONFIGMAPS, NS, "c", {"data": {"k": "v", "version": None}}, PATCH_MERGE)
+    assert o["data"]["k"] == "v" and "version" not in o["data"]
+    o = s.patch(R.CONFIGMAPS, NS, "c", [{"op": "replace", "path": "/data/k", "value": "w"}], PATCH_JSON)
+    assert o["data"]["k"] == "w"
+    o = s.patch(R.CONFIGMAPS, NS, "c", {"metadata": {"ownerReferences": [{"uid": "u1", "name": "t"}]}},
+                PATCH_STRATEGIC)
+    o = s.patch(R.CONFIGMAPS, NS, "c", {"metadata": {"ownerReferences": [{"uid": "u2", "name": "t2"}]}},
+                PATCH_STRATEGIC)
+    assert [r["uid"] for r in o["metadata"]["ownerReferences"]] == ["u1", "u2"]
+    a = s.patch(R.SECRETS, NS, "applied", {"apiVersion": "v1", "kind": "Secret", "data": {"x": "eQ=="}}, PATCH_APPLY)
+    assert a["metadata"]["uid"] and a["data"] == {"x": "eQ=="}
+
+
+def test_list_pagination_and_selectors():
+    s = ClusterState()
+    for i in range(7):
+        sec = make_secret(f"s{i}", NS)
+        sec["metadata"]["labels"] = {"tier": "gpu" if i % 2 else "cpu"}
+        s.create(R.SECRETS, NS, sec)
+    page = s.list(R.SECRETS, NS, limit=3)
+    names = [o["metadata"]["name"] for o in page["items"]]
+    while page["metadata"].get("continue"):
+        page = s.list(R.SECRETS, NS, limit=3, continue_token=page["metadata"]["continue"])
+        names += [o["metadata"]["name"] for o in page["items"]]
+    assert names == [f"s{i}" for i in range(7)]
+    assert len(s.list(R.SECRETS, NS, label_selector="tier=gpu")["items"]) == 3
+    assert len(s.list(R.SECRETS, NS, label_selector="tier in (gpu,cpu),tier!=cpu")["items"]) == 3
+
+
+@pytest.mark.parametrize("transport", ["fast", "aiohttp"])
+async def test_http_roundtrip_watch_bookmarks_auth_and_faults(transport):
+    srv = FakeApiServer(name="t", token="sekret", bookmark_interval=0.05)
+    url = await srv.start()
+    good = RestClient(ClusterConfig(server=url, token="sekret"), transport=transport)
+    bad = RestClient(ClusterConfig(server=url, token="nope"), transport=transport)
+    try:
+        with pytest.raises(E.Unauthorized):
+            await bad.list(R.SECRETS, NS)
+        created = await good.create(R.TEMPLATES, NS, make_template(0, NS))
+        got = await good.get(R.TEMPLATES, NS, created["metadata"]["name"])
+        assert got == created
+        with pytest.raises(E.NotFound):
+            await good.get(R.TEMPLATES, NS, "missing")
+        with pytest.raises(E.AlreadyExists):
+            await good.create(R.TEMPLATES, NS, make_template(0, NS))
+        lst = await good.list(R.TEMPLATES, NS)
+        rv = lst["metadata"]["resourceVersion"]
+        events = []
+
+        async def consume():
+            async for ev in good.watch(R.TEMPLATES, NS, resource_version=rv, timeout_seconds=1):
+                events.append(ev.type)
+                if ev.type == "MODIFIED":
+                    return
+        task = asyncio.ensure_future(consume())
+        await asyncio.sleep(0.15)
+        upd = dict(got, spec=dict(got["spec"], command="bash"))
+        await good.update(R.TEMPLATES, NS, upd)
+        await asyncio.wait_for(task, 3)
+        assert "BOOKMARK" in events and events[-1] == "MODIFIED"
+        st = await good.update_status(R.TEMPLATES, NS, dict(await good.get(R.TEMPLATES, NS, "algo-00000"),
+                                                             status={"syncedToClusters": ["a"]}))
+        assert st["status"]["syncedToClusters"] == ["a"]
+        srv.faults.update({"error_rate": 1.0, "error_code": 500})
+        with pytest.raises(E.InternalError):
+            await good.create(R.SECRETS, NS, make_secret("s", NS))
+        srv.faults.update({"error_rate": 0.0, "down": True})
+        with pytest.raises(E.ServiceUnavailable):
+            await good.list(R.SECRETS, NS)
+        srv.faults.update({"down": False})
+        await good.delete(R.TEMPLATES, NS, "algo-00000")
+        with pytest.raises(E.NotFound):
+            await good.delete(R.TEMPLATES, NS, "algo-00000")
+    finally:
+        await good.close()
+        await bad.close()
+        await srv.stop()
+
+
+async def test_http_gone_is_reported_in_stream():
+    srv = FakeApiServer(state=ClusterState(history=2))
+    url = await srv.start()
+    c = RestClient(ClusterConfig(server=url))
+    try:
+        for i in range(5):
+            await c.create(R.SECRETS, NS, make_secret(f"s{i}", NS))
+        evs = [ev async for ev in c.watch(R.SECRETS, NS, resource_version="1", timeout_seconds=1)]
+        assert evs[0].type == "ERROR" and evs[0].object["code"] == 410
+    finally:
+        await c.close()
+        await srv.stop()
+
+
+async def test_transport_survives_server_side_close():
+    """A keep-alive connection the server closed is retried once on a fresh connection."""
+    srv = FakeApiServer()
+    url = await srv.start()
+    c = RestClient(ClusterConfig(server=url), transport="fast")
+    try:
+        await c.create(R.SECRETS, NS, make_secret("a", NS))
+        for conn in list(srv._http._conns):
+            conn.transport.close()
+        await asyncio.sleep(0.05)
+        assert (await c.get(R.SECRETS, NS, "a"))["metadata"]["name"] == "a"
+    finally:
+        await c.close()
+        await srv.stop()

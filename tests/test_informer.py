@@ -1,0 +1,149 @@
+"""SharedInformer behaviour: list/watch, relist on 410 with tombstones, resync, transforms, mutation overlay."""
+import asyncio
+
+from ncc.api import resources as R
+from ncc.cache.informer import DeletedFinalStateUnknown, Informer
+from ncc.cache.store import Store
+from ncc.fakeapi.server import FakeApiServer
+from ncc.fakeapi.storage import ClusterState
+from ncc.kube.kubeconfig import ClusterConfig
+from ncc.kube.rest import RestClient
+from ncc.testing.fake_client import FakeClient
+from ncc.testing.workload import make_secret
+
+NS = "nexus"
+
+
+class Rec:
+    def __init__(self):
+        self.log = []
+
+    def add(self, o):
+        self.log.append(("add", o["metadata"]["name"]))
+
+    def update(self, old, new):
+        self.log.append(("update", new["metadata"]["name"], old is new))
+
+    def delete(self, o):
+        if isinstance(o, DeletedFinalStateUnknown):
+            self.log.append(("tombstone", o.key.name))
+        else:
+            self.log.append(("delete", o["metadata"]["name"]))
+
+
+async def wait_until(pred, timeout=3.0):
+    end = asyncio.get_running_loop().time() + timeout
+    while asyncio.get_running_loop().time() < end:
+        if pred():
+            return True
+        await asyncio.sleep(0.01)
+    raise AssertionError("timeout")
+
+
+async def test_list_then_watch_events_in_order():
+    state = ClusterState()
+    state.create(R.SECRETS, NS, make_secret("pre", NS))
+    client = FakeClient(state, simple=False)
+    inf = Informer(client, R.SECRETS, NS)
+    rec = Rec()
+    inf.add_event_handler(rec.add, rec.update, rec.delete)
+    inf.start()
+    assert await inf.wait_for_sync(2)
+    state.create(R.SECRETS, NS, make_secret("a", NS))
+    cur = state.get(R.SECRETS, NS, "a")
+    state.update(R.SECRETS, NS, dict(cur, data={"k": "dg=="}))
+    state.delete(R.SECRETS, NS, "pre")
+    await wait_until(lambda: len(rec.log) == 4)
+    assert rec.log == [("add", "pre"), ("add", "a"), ("update", "a", False), ("delete", "pre")]
+    assert inf.lister.get(NS, "a")["data"] == {"k": "dg=="}
+    await inf.stop()
+
+
+async def test_relist_after_gone_emits_tombstones():
+    state = ClusterState(history=2)
+    for n in ("a", "b"):
+        state.create(R.SECRETS, NS, make_secret(n, NS))
+    srv = FakeApiServer(state=state)
+    url = await srv.start()
+    client = RestClient(ClusterConfig(server=url))
+    inf = Informer(client, R.SECRETS, NS)
+    rec = Rec()
+    inf.add_event_handler(rec.add, rec.update, rec.delete)
+    inf.start()
+    assert await inf.wait_for_sync(2)
+    # while the watch is down, history is compacted and "a" disappears: the resume gets 410 → relist
+    srv.drop_watches()
+    state.compact()
+    state.delete(R.SECRETS, NS, "a")
+    state.compact()
+    state.create(R.SECRETS, NS, make_secret("c", NS))
+    state.compact()
+    await wait_until(lambda: ("tombstone", "a") in rec.log and ("add", "c") in rec.log)
+    assert inf.relists >= 2
+    assert sorted(o["metadata"]["name"] for o in inf.lister.list()) == ["b", "c"]
+    await inf.stop()
+    await client.close()
+    await srv.stop()
+
+
+async def test_resync_redelivers_same_object():
+    state = ClusterState()
+    state.create(R.SECRETS, NS, make_secret("a", NS))
+    inf = Informer(FakeClient(state, simple=False), R.SECRETS, NS, resync_period=0.05)
+    rec = Rec()
+    inf.add_event_handler(rec.add, rec.update, rec.delete)
+    inf.start()
+    await wait_until(lambda: ("update", "a", True) in rec.log)
+    await inf.stop()
+
+
+async def test_transform_and_async_handler():
+    state = ClusterState()
+    state.create(R.SECRETS, NS, make_secret("a", NS))
+    inf = Informer(FakeClient(state, simple=False), R.SECRETS, NS,
+                   transform=lambda o: {"metadata": o["metadata"], "slim": True})
+    seen = []
+
+    async def on_add(o):
+        await asyncio.sleep(0)
+        seen.append(o)
+    inf.add_event_handler(on_add=on_add)
+    inf.start()
+    await wait_until(lambda: seen)
+    assert seen[0]["slim"] is True and "data" not in inf.lister.get(NS, "a")
+    await inf.stop()
+
+
+async def test_informer_recovers_from_transport_errors():
+    srv = FakeApiServer()
+    url = await srv.start()
+    client = RestClient(ClusterConfig(server=url))
+    inf = Informer(client, R.SECRETS, NS)
+    srv.faults.update({"down": True, "write_only": False})
+    inf.start()
+    await asyncio.sleep(0.3)
+    assert not inf.has_synced() and inf.last_error is not None
+    srv.faults.update({"down": False})
+    assert await inf.wait_for_sync(5)
+    await inf.stop()
+    await client.close()
+    await srv.stop()
+
+
+def test_store_indices_and_mutation_overlay():
+    s = Store()
+    s.add_indexer("owner", lambda o: [r["uid"] for r in o["metadata"].get("ownerReferences", [])])
+    o = make_secret("a", NS)
+    o["metadata"].update(resourceVersion="5", ownerReferences=[{"uid": "u1"}])
+    s.upsert(o)
+    assert [x["metadata"]["name"] for x in s.by_index("owner", "u1")] == ["a"]
+    newer = dict(o, metadata=dict(o["metadata"], resourceVersion="7", ownerReferences=[]))
+    s.assume(newer)
+    assert s.get(NS, "a")["metadata"]["resourceVersion"] == "7"     # overlay visible before the watch catches up
+    s.assume(dict(o, metadata=dict(o["metadata"], resourceVersion="6")))  # older than overlay: ignored
+    assert s.get(NS, "a")["metadata"]["resourceVersion"] == "7"
+    s.upsert(dict(newer))                                            # informer catches up → overlay dropped
+    assert s.get(NS, "a")["metadata"]["resourceVersion"] == "7" and not s._assumed
+    assert s.by_index("owner", "u1") == []
+    added, updated, deleted = s.replace([make_secret("b", NS)])
+    assert [x["metadata"]["name"] for x in added] == ["b"] and [x["metadata"]["name"] for x in deleted] == ["a"]

@@ -1,0 +1,237 @@
+"""Native-mode behaviours that deliberately differ from the reference."""
+import pytest
+
+from ncc.api import constants as C
+from ncc.api import resources as R
+from ncc.cache.informer import Informer
+from ncc.controller.controller import Controller, make_key
+from ncc.controller.events import FakeRecorder
+from ncc.controller.options import ControllerOptions
+from ncc.controller.reconcile import ShardSyncError, slim_data, slim_spec
+from ncc.fakeapi.storage import ClusterState
+from ncc.kube import errors as E
+from ncc.shards.shard import Shard
+from ncc.testing.fake_client import FakeClient
+from ncc.testing.workload import make_configmap, make_secret, make_template, make_workgroup
+
+NS = "nexus"
+ALIAS = "ctl"
+
+
+class Env:
+    """Controller + N shards on in-memory clusters with real apiserver semantics (UIDs, RVs, GC)."""
+
+    def __init__(self, n_shards=2, **opt):
+        self.cstate = ClusterState("controller")
+        self.cclient = FakeClient(self.cstate, cluster_name="controller", simple=False)
+        self.sstates = [ClusterState(f"s{i}") for i in range(n_shards)]
+        self.sclients = [FakeClient(s, cluster_name=f"s{i}", simple=False) for i, s in enumerate(self.sstates)]
+        self.opts = ControllerOptions.native(native_queue=False, coalesce_window=0.0, **opt)
+
+    def build(self, role="all"):
+        self.opts.role = role
+        infs = {rt: Informer(self.cclient, rt, NS) for rt in (R.TEMPLATES, R.WORKGROUPS, R.SECRETS, R.CONFIGMAPS)}
+        slim = {R.TEMPLATES: slim_spec, R.WORKGROUPS: slim_spec, R.SECRETS: slim_data, R.CONFIGMAPS: slim_data}
+        self.shards = [Shard(ALIAS, f"s{i}", c, NS, assume_writes=True, sync_binary_data=True, transforms=slim)
+                       for i, c in enumerate(self.sclients)]
+        self.recorder = FakeRecorder()
+        self.ctl = Controller(alias=ALIAS, namespace=NS, client=self.cclient,
+                              shards=self.shards if role != "coordinator" else [],
+                              template_informer=infs[R.TEMPLATES], workgroup_informer=infs[R.WORKGROUPS],
+                              secret_informer=infs[R.SECRETS], configmap_informer=infs[R.CONFIGMAPS],
+                              options=self.opts, recorder=self.recorder,
+                              shard_names=[f"s{i}" for i in range(len(self.sstates))])
+        self.refresh()
+        return self.ctl
+
+    def refresh(self):
+        """Simulate informers catching up: replace every store with the cluster's current content."""
+        for rt, inf in ((R.TEMPLATES, self.ctl.template_informer), (R.WORKGROUPS, self.ctl.workgroup_informer),
+                        (R.SECRETS, self.ctl.secret_informer), (R.CONFIGMAPS, self.ctl.configmap_informer)):
+            inf.store.replace(self.cstate.list(rt, NS)["items"])
+            inf._synced.set()
+        for sh, st in zip(self.shards, self.sstates):
+            for rt, inf in ((R.TEMPLATES, sh.template_informer), (R.WORKGROUPS, sh.workgroup_informer),
+                            (R.SECRETS, sh.secret_informer), (R.CONFIGMAPS, sh.configmap_informer)):
+                inf.store.replace(st.list(rt, NS)["items"])
+                inf._synced.set()
+
+    def seed(self, i=0, secrets=("s",), configmaps=("c",)):
+        for s in secrets:
+            self.cstate.create(R.SECRETS, NS, make_secret(s, NS))
+        for c in configmaps:
+            self.cstate.create(R.CONFIGMAPS, NS, make_configmap(c, NS))
+        return self.cstate.create(R.TEMPLATES, NS, make_template(i, NS, secrets=list(secrets),
+                                                                 configmaps=list(configmaps)))
+
+
+async def test_fanout_to_all_shards_and_status():
+    env = Env(3)
+    t = env.seed()
+    ctl = env.build()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    for st in env.sstates:
+        assert st.count(R.TEMPLATES) == 1 and st.count(R.SECRETS) == 1 and st.count(R.CONFIGMAPS) == 1
+        sec = st.get(R.SECRETS, NS, "s")
+        assert sec["metadata"]["ownerReferences"][0]["uid"] == st.get(R.TEMPLATES, NS, t["metadata"]["name"])[
+            "metadata"]["uid"]
+    got = env.cstate.get(R.TEMPLATES, NS, t["metadata"]["name"])
+    assert got["status"]["conditions"][0]["status"] == "True"
+    assert got["status"]["syncedToClusters"] == ["s0", "s1", "s2"]
+    assert env.recorder.events[-1].startswith("Normal Synced")
+    # second pass is a no-op: no writes, no event (event_on_noop=False)
+    n_actions = [len(c.writes()) for c in env.sclients]
+    env.refresh()
+    env.recorder.events.clear()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    assert [len(c.writes()) for c in env.sclients] == n_actions and env.recorder.events == []
+
+
+async def test_single_put_for_data_and_owner():
+    env = Env(1)
+    t = env.seed()
+    ctl = env.build()
+    # shard already has the secret, owned by some other template, with stale data
+    other = env.sstates[0].create(R.TEMPLATES, NS, make_template(99, NS))
+    sec = make_secret("s", NS, version=42)
+    sec["metadata"]["ownerReferences"] = [{"apiVersion": C.API_VERSION, "kind": C.TEMPLATE_KIND,
+                                           "name": other["metadata"]["name"], "uid": other["metadata"]["uid"]}]
+    env.sstates[0].create(R.SECRETS, NS, sec)
+    env.refresh()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    secret_writes = [a for a in env.sclients[0].writes() if a.resource.plural == "secrets"]
+    assert len(secret_writes) == 1 and secret_writes[0].verb == "update"
+    live = env.sstates[0].get(R.SECRETS, NS, "s")
+    assert live["data"] == env.cstate.get(R.SECRETS, NS, "s")["data"]
+    assert len(live["metadata"]["ownerReferences"]) == 2
+
+
+async def test_failure_isolation_reports_failed_shard():
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build()
+    env.sclients[1].prepend_reactor("create", "*", lambda a: (True, None, E.ServiceUnavailable("shard down")))
+    with pytest.raises(ShardSyncError) as ei:
+        await ctl.sync_template(NS, t["metadata"]["name"])
+    assert set(ei.value.failures) == {"s1"}
+    assert env.sstates[0].count(R.TEMPLATES) == 1 and env.sstates[1].count(R.TEMPLATES) == 0
+    st = env.cstate.get(R.TEMPLATES, NS, t["metadata"]["name"])["status"]
+    assert st["conditions"][0]["status"] == "False" and "s1" in st["conditions"][0]["message"]
+    assert st["syncedToClusters"] == ["s0"]
+    env.sclients[1].reactors.clear()
+    env.refresh()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    st = env.cstate.get(R.TEMPLATES, NS, t["metadata"]["name"])["status"]
+    assert st["conditions"][0]["status"] == "True" and st["syncedToClusters"] == ["s0", "s1"]
+
+
+async def test_write_race_already_exists_is_tolerated():
+    env = Env(1)
+    t = env.seed()
+    ctl = env.build()
+    # the shard template exists but our cache has not seen it yet
+    env.sstates[0].create(R.TEMPLATES, NS, dict(make_template(0, NS), metadata={
+        "name": t["metadata"]["name"], "namespace": NS, "labels": C.owner_labels(ALIAS)}))
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    assert env.sstates[0].count(R.SECRETS) == 1
+
+
+async def test_queued_delete_retries_and_orphan_sweep():
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build()
+    name = t["metadata"]["name"]
+    await ctl.sync_template(NS, name)
+    env.cstate.delete(R.TEMPLATES, NS, name)
+    env.refresh()
+    ctl._handle_template_delete(t)
+    assert len(ctl.queue) == 1
+    env.sclients[1].prepend_reactor("delete", "*", lambda a: (True, None, E.InternalError("boom")))
+    with pytest.raises(E.InternalError):
+        await ctl.sync_template(NS, name)
+    assert env.sstates[0].count(R.TEMPLATES) == 0 and env.sstates[1].count(R.TEMPLATES) == 1
+    env.sclients[1].reactors.clear()
+    env.refresh()
+    await ctl.sync_template(NS, name)          # retry succeeds; dependents are garbage-collected
+    assert env.sstates[1].count(R.TEMPLATES) == 0 and env.sstates[1].count(R.SECRETS) == 0
+    # orphan sweep: labelled shard objects without a controller object are removed; foreign ones are kept
+    mine = make_template(5, NS)
+    mine["metadata"]["labels"] = C.owner_labels(ALIAS)
+    env.sstates[0].create(R.TEMPLATES, NS, mine)
+    env.sstates[0].create(R.TEMPLATES, NS, make_template(6, NS))
+    env.refresh()
+    while len(ctl.queue):
+        ctl.queue.try_get()
+    assert ctl.sweep_orphans() == 1
+    await ctl.sync_template(NS, mine["metadata"]["name"])
+    names = [o["metadata"]["name"] for o in env.sstates[0].list(R.TEMPLATES, NS)["items"]]
+    assert names == ["algo-00006"]
+
+
+async def test_binary_data_and_workgroup_delete_propagation():
+    env = Env(1)
+    cm = make_configmap("c", NS)
+    cm["binaryData"] = {"blob": "AAEC"}
+    env.cstate.create(R.CONFIGMAPS, NS, cm)
+    t = env.cstate.create(R.TEMPLATES, NS, make_template(0, NS, configmaps=["c"]))
+    w = env.cstate.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+    ctl = env.build()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    await ctl.sync_workgroup(NS, "mi355x")
+    assert env.sstates[0].get(R.CONFIGMAPS, NS, "c")["binaryData"] == {"blob": "AAEC"}
+    assert env.sstates[0].count(R.WORKGROUPS) == 1
+    env.cstate.delete(R.WORKGROUPS, NS, "mi355x")
+    env.refresh()
+    ctl._on_workgroup_delete(w)
+    await ctl.sync_workgroup(NS, "mi355x")
+    assert env.sstates[0].count(R.WORKGROUPS) == 0
+
+
+async def test_executor_refuses_missing_references_and_reports():
+    env = Env(2)
+    t = env.cstate.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["missing"]))
+    ctl = env.build(role="executor")
+    reports = []
+    ctl.reporter = reports.append
+    with pytest.raises(E.NotFound):
+        await ctl.sync_template(NS, t["metadata"]["name"])
+    assert all(st.count(R.TEMPLATES) == 0 for st in env.sstates) and reports == []
+    env.cstate.create(R.SECRETS, NS, make_secret("missing", NS))
+    env.refresh()
+    await ctl.sync_template(NS, t["metadata"]["name"])
+    assert reports and reports[-1]["r"] == {"s0": None, "s1": None}
+    assert reports[-1]["k"] == make_key(C.KIND_TEMPLATE, NS, t["metadata"]["name"])
+    # executors never write to the controller cluster
+    assert env.cclient.writes() == []
+
+
+async def test_coordinator_waits_for_all_shard_reports():
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build(role="coordinator")
+    name = t["metadata"]["name"]
+    key = make_key(C.KIND_TEMPLATE, NS, name)
+    await ctl.sync_template(NS, name)
+    st = env.cstate.get(R.TEMPLATES, NS, name)["status"]
+    assert st["conditions"][0]["status"] == "False"          # initialized, waiting for executors
+    env.refresh()
+    cur = env.cstate.get(R.TEMPLATES, NS, name)["metadata"]
+    ctl.on_executor_message(0, {"t": "report", "k": key, "u": cur["uid"], "g": cur["generation"],
+                                "r": {"s0": None}, "w": True})
+    await ctl.sync_template(NS, name)
+    assert env.cstate.get(R.TEMPLATES, NS, name)["status"]["conditions"][0]["status"] == "False"
+    ctl.on_executor_message(1, {"t": "report", "k": key, "u": cur["uid"], "g": cur["generation"],
+                                "r": {"s1": "ServiceUnavailable: down"}, "w": False})
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    st = env.cstate.get(R.TEMPLATES, NS, name)["status"]
+    assert st["conditions"][0]["status"] == "False" and "s1" in st["conditions"][0]["message"]
+    ctl.on_executor_message(1, {"t": "report", "k": key, "u": cur["uid"], "g": cur["generation"],
+                                "r": {"s1": None}, "w": True})
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    st = env.cstate.get(R.TEMPLATES, NS, name)["status"]
+    assert st["conditions"][0]["status"] == "True" and st["syncedToClusters"] == ["s0", "s1"]
+    assert any(e.startswith("Normal Synced") for e in env.recorder.events)
+    # a report about an older incarnation (different UID) does not count
+    assert ctl.shard_readiness(key, {"metadata": {"uid": "other", "generation": 1}}) is None
