@@ -1,0 +1,185 @@
+"""Config loading (appconfig.yaml + env overlay + NEXUS__ env) and kubeconfig/exec-credential handling."""
+import base64
+import json
+import os
+import stat
+import sys
+
+import pytest
+
+from ncc.api import resources as R
+from ncc.config import AppConfig, config_to_env, load_config, parse_duration
+from ncc.fakeapi.server import FakeApiServer
+from ncc.kube import errors as E
+from ncc.kube.kubeconfig import (ClusterConfig, ConfigError, CredentialSource, build_config, in_cluster_config,
+                                 load_kubeconfig, parse_kubeconfig, render_kubeconfig)
+from ncc.kube.rest import RestClient
+from ncc.shards.loader import discover
+
+REF_KEYS = ["alias", "controller-config-path", "shard-config-path", "controller-namespace", "log-level", "workers",
+            "failure-rate-base-delay", "failure-rate-max-delay", "rate-limit-elements-per-second",
+            "rate-limit-elements-burst"]
+
+
+@pytest.mark.parametrize("text,sec", [("30ms", 0.03), ("5s", 5.0), ("1m30s", 90.0), ("1h", 3600.0), ("2", 2.0),
+                                      ("1.5s", 1.5), ("-1s", -1.0), ("100us", 1e-4), ("0", 0.0)])
+def test_go_durations(text, sec):
+    assert parse_duration(text) == pytest.approx(sec)
+
+
+@pytest.mark.parametrize("bad", ["", "5x", "s", "1s2"])
+def test_bad_durations(bad):
+    with pytest.raises(ValueError):
+        parse_duration(bad)
+
+
+def test_reference_config_surface_and_precedence(tmp_path):
+    # the reference's key-declaration file: every key present with "" (.container/appconfig.yaml:1-10)
+    (tmp_path / "appconfig.yaml").write_text("".join(f'{k}: ""\n' for k in REF_KEYS) + "workers: 3\n")
+    (tmp_path / "appconfig.local.yaml").write_text("workers: 5\nalias: local-alias\n")
+    env = {"APPLICATION_ENVIRONMENT": "local", "NEXUS__WORKERS": "10", "NEXUS__FAILURE_RATE_BASE_DELAY": "30ms",
+           "NEXUS__FAILURE_RATE_MAX_DELAY": "5s", "NEXUS__RATE_LIMIT_ELEMENTS_PER_SECOND": "50",
+           "NEXUS__RATE_LIMIT_ELEMENTS_BURST": "300", "NEXUS__CONTROLLER_NAMESPACE": "nexus",
+           "NEXUS__LOG_LEVEL": "DEBUG", "NEXUS__SHARD_CONFIG_PATH": "./shards"}
+    cfg = load_config(str(tmp_path), env)
+    assert cfg.workers == 10 and cfg.alias == "local-alias"       # env > env-specific yaml > base yaml
+    assert cfg.failure_rate_base_delay == pytest.approx(0.03) and cfg.failure_rate_max_delay == 5.0
+    assert (cfg.rate_limit_elements_per_second, cfg.rate_limit_elements_burst) == (50, 300)
+    assert cfg.controller_namespace == "nexus" and cfg.log_level == "DEBUG" and cfg.shard_config_path == "./shards"
+    assert {AppConfig.key_of(a) for a in AppConfig.__dataclass_fields__} >= set(REF_KEYS)
+    with pytest.raises(ValueError):
+        load_config(str(tmp_path), {"NEXUS__WORKERS": "many"})
+
+
+def test_config_roundtrips_through_env():
+    cfg = AppConfig(workers=7, failure_rate_base_delay=0.25, mode="compat", transport="aiohttp")
+    back = load_config("/nonexistent", config_to_env(cfg))
+    assert back == cfg
+
+
+def test_defaults_follow_helm_values():
+    cfg = load_config("/nonexistent", {})
+    assert (cfg.alias, cfg.shard_config_path, cfg.controller_namespace, cfg.workers) == \
+        ("controller-cluster", "/app/config/shards", "nexus", 2)
+    assert (cfg.failure_rate_base_delay, cfg.failure_rate_max_delay) == (0.03, 5.0)
+
+
+def test_kubeconfig_variants(tmp_path):
+    ca = b"-----BEGIN CERTIFICATE-----\nMIIB\n-----END CERTIFICATE-----\n"
+    (tmp_path / "ca.crt").write_bytes(ca)
+    (tmp_path / "token").write_text("file-token\n")
+    doc = {
+        "current-context": "b",
+        "clusters": [{"name": "c1", "cluster": {"server": "https://a.example:6443/",
+                                                "certificate-authority-data": base64.b64encode(ca).decode()}},
+                     {"name": "c2", "cluster": {"server": "https://b.example", "certificate-authority": "ca.crt",
+                                                "tls-server-name": "kube.b"}}],
+        "users": [{"name": "u1", "user": {"token": "t1"}}, {"name": "u2", "user": {"tokenFile": "token"}}],
+        "contexts": [{"name": "a", "context": {"cluster": "c1", "user": "u1"}},
+                     {"name": "b", "context": {"cluster": "c2", "user": "u2", "namespace": "nexus"}}],
+    }
+    cfg = parse_kubeconfig(doc, base_dir=str(tmp_path))
+    assert cfg.server == "https://b.example" and cfg.ca_data == ca and cfg.tls_server_name == "kube.b"
+    assert cfg.token_file.endswith("token") and cfg.namespace == "nexus"
+    a = parse_kubeconfig(doc, context="a")
+    assert a.server == "https://a.example:6443" and a.token == "t1" and a.ca_data == ca
+    with pytest.raises(ConfigError):
+        parse_kubeconfig(doc, context="missing")
+
+
+async def test_exec_plugin_token_is_cached_and_refreshed(tmp_path):
+    counter = tmp_path / "count"
+    script = tmp_path / "get-token"
+    script.write_text(f"""#!{sys.executable}
+import json, os, sys
+p = {str(counter)!r}
+n = int(open(p).read()) + 1 if os.path.exists(p) else 1
+open(p, "w").write(str(n))
+info = json.loads(os.environ["KUBERNETES_EXEC_INFO"])
+assert info["kind"] == "ExecCredential"
+print(json.dumps({{"apiVersion": "client.authentication.k8s.io/v1", "kind": "ExecCredential",
+                  "status": {{"token": os.environ["TOKEN_PREFIX"] + str(n),
+                             "expirationTimestamp": "2999-01-01T00:00:00Z"}}}}))
+""")
+    script.chmod(script.stat().st_mode | stat.S_IEXEC)
+    kc = tmp_path / "shard.kubeconfig"
+    kc.write_text(render_kubeconfig("http://127.0.0.1:1", "shard", exec_cfg={
+        "apiVersion": "client.authentication.k8s.io/v1", "command": str(script), "args": [],
+        "env": [{"name": "TOKEN_PREFIX", "value": "tok-"}], "provideClusterInfo": True}))
+    cfg = load_kubeconfig(str(kc))
+    creds = CredentialSource(cfg)
+    assert await creds.token() == "tok-1"
+    assert await creds.token() == "tok-1" and creds.exec_runs == 1      # cached until expiry
+    assert await creds.token(force_refresh=True) == "tok-2"
+    # a 401 from the apiserver triggers exactly one refresh and retry
+    srv = FakeApiServer(token="tok-3")
+    url = await srv.start()
+    cfg.server = url
+    client = RestClient(cfg)
+    try:
+        client.creds._token = "tok-2"
+        assert (await client.list(R.SECRETS, "nexus"))["items"] == []
+        assert client.creds.exec_runs == 1 and counter.read_text() == "3"
+    finally:
+        await client.close()
+        await srv.stop()
+
+
+def test_in_cluster_and_build_config(tmp_path, monkeypatch):
+    monkeypatch.delenv("KUBERNETES_SERVICE_HOST", raising=False)
+    with pytest.raises(ConfigError):
+        in_cluster_config()
+    monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "10.0.0.1")
+    monkeypatch.setenv("KUBERNETES_SERVICE_PORT", "443")
+    cfg = build_config("")
+    assert cfg.server == "https://10.0.0.1:443" and cfg.token_file.endswith("/token")
+    kc = tmp_path / "c.kubeconfig"
+    kc.write_text(render_kubeconfig("http://x:1", "c", token="t"))
+    assert build_config(str(kc)).token == "t"
+
+
+def test_shard_discovery_matches_secret_volume_layout(tmp_path):
+    for n in ("kind-nexus-shard-0", "b-cluster", "a-cluster"):
+        (tmp_path / f"{n}.kubeconfig").write_text("x")
+    (tmp_path / "README").write_text("ignored")
+    os.makedirs(tmp_path / "..2024_01_01", exist_ok=True)
+    (tmp_path / "..data").symlink_to(tmp_path / "..2024_01_01")
+    assert [n for n, _ in discover(str(tmp_path))] == ["a-cluster", "b-cluster", "kind-nexus-shard-0"]
+    assert discover(str(tmp_path / "missing")) == []
+
+
+async def test_bearer_token_via_rest_client_against_fake():
+    srv = FakeApiServer(token="abc")
+    url = await srv.start()
+    try:
+        ok = RestClient(ClusterConfig(server=url, token="abc"))
+        assert (await ok.create(R.SECRETS, "nexus", {"metadata": {"name": "x"}, "data": {}}))["kind"] == "Secret"
+        await ok.close()
+        nok = RestClient(ClusterConfig(server=url, username="u", password="p"))
+        with pytest.raises(E.Unauthorized):
+            await nok.get(R.SECRETS, "nexus", "x")
+        await nok.close()
+    finally:
+        await srv.stop()
+
+
+def test_statsd_and_json_logging(capsys):
+    import socket
+
+    from ncc.telemetry.logging import configure_logging
+    from ncc.telemetry.statsd import StatsdClient
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.bind(("127.0.0.1", 0))
+    rx.settimeout(2)
+    c = StatsdClient("nexus_configuration_controller", f"udp://127.0.0.1:{rx.getsockname()[1]}", ["service:ncc"])
+    c.gauge("workqueue_length", 3)
+    assert rx.recv(1024) == b"nexus_configuration_controller.workqueue_length:3|g|#service:ncc"
+    c.close()
+    rx.close()
+    import logging
+    configure_logging("DEBUG", "json")
+    logging.getLogger("ncc.test").info("hello", extra={"shard": "s0"})
+    line = capsys.readouterr().out.strip().splitlines()[-1]
+    rec = json.loads(line)
+    assert rec["msg"] == "hello" and rec["shard"] == "s0" and rec["level"] == "INFO"
+    configure_logging("WARNING", "text")

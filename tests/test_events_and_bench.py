@@ -1,0 +1,84 @@
+"""Event correlator semantics, and the multi-rank benchmark path over gloo (world_size 2, CPU)."""
+import asyncio
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from ncc.api import resources as R
+from ncc.controller.events import SPAM_BURST, BroadcastRecorder, FakeRecorder
+from ncc.fakeapi.storage import ClusterState
+from ncc.testing.fake_client import FakeClient
+from ncc.testing.workload import make_template
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+async def _drain(rec):
+    await asyncio.wait_for(rec._queue.join(), 5)
+
+
+async def test_event_dedup_patches_count():
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False)
+    rec.start()
+    t = client.state.create(R.TEMPLATES, "nexus", make_template(0, "nexus"))
+    for _ in range(3):
+        rec.event(t, "Normal", "Synced", "Resource of type NexusAlgorithmTemplate synced successfully")
+    await _drain(rec)
+    events = client.state.list(R.EVENTS, "nexus")["items"]
+    assert len(events) == 1 and events[0]["count"] == 3 and events[0]["involvedObject"]["kind"] == "NexusAlgorithmTemplate"
+    assert events[0]["source"]["component"] == "nexus-configuration-controller"
+    assert rec.stats["created"] == 1 and rec.stats["patched"] == 2
+    await rec.stop()
+
+
+async def test_event_spam_filter_and_aggregation():
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False)
+    rec.start()
+    t = client.state.create(R.TEMPLATES, "nexus", make_template(0, "nexus"))
+    for i in range(SPAM_BURST + 10):
+        rec.event(t, "Warning", "ErrResourceSyncError", f"failure #{i}")
+    await _drain(rec)
+    assert rec.stats["dropped_spam"] == 10
+    msgs = [e["message"] for e in client.state.list(R.EVENTS, "nexus")["items"]]
+    assert any(m.startswith("(combined from similar events)") for m in msgs)
+    # distinct messages beyond the aggregation threshold collapse into one aggregate event
+    assert len(msgs) <= 10
+    await rec.stop()
+
+
+def test_fake_recorder_formats_like_client_go():
+    r = FakeRecorder()
+    r.event({}, "Warning", "ErrResourceMissing", "msg")
+    assert r.events == ["Warning ErrResourceMissing msg"]
+    silent = FakeRecorder(keep=False)
+    silent.event({}, "Normal", "Synced", "x")
+    assert silent.events == []
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_over_gloo():
+    """The driver's N>1 launch shape: torch.distributed.run, one shard apiserver per rank, rank 0 reports."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["shards"] == 2 and res["scaling"] == "weak"
+    assert res["value"] > 0 and res["p50_latency_ms"] is not None and res["controller_alive"]
