@@ -2,8 +2,10 @@
 """Build the in-tree native extension `ncc/_native*.so` (C++17 + pybind11).
 
 Usage: python native/build.py [--debug] [--sanitize]
-`--sanitize` builds with AddressSanitizer/UBSan for host-side testing (run the tests with
-`LD_PRELOAD=$(g++ -print-file-name=libasan.so)`).
+`--sanitize` builds with AddressSanitizer/UBSan for host-side testing; run the tests with
+  NCC_SKIP_NATIVE_BUILD=1 ASAN_OPTIONS=detect_leaks=0 \
+  LD_PRELOAD="$(g++ -print-file-name=libasan.so) $(g++ -print-file-name=libstdc++.so)" python -m pytest ...
+(libstdc++ must be preloaded too, or ASan's __cxa_throw interceptor cannot resolve the real symbol).
 """
 from __future__ import annotations
 
@@ -27,9 +29,13 @@ def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) ->
     import pybind11
 
     out = target_path()
-    if not debug and not sanitize and os.path.exists(out):
+    flavor = "sanitize" if sanitize else ("debug" if debug else "release")
+    stamp = out + ".flavor"
+    if flavor == "release" and os.path.exists(out) and os.path.exists(stamp):
         so_m = os.path.getmtime(out)
-        if all(os.path.getmtime(s) <= so_m for s in SOURCES + [__file__]):
+        with open(stamp) as f:
+            same = f.read().strip() == flavor
+        if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
     flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"]
@@ -46,6 +52,8 @@ def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) ->
         print(" ".join(shlex.quote(c) for c in cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(flavor)
     return out
 
 

@@ -72,6 +72,7 @@ def _free_port() -> int:
 @pytest.mark.slow
 def test_bench_two_ranks_over_gloo():
     """The driver's N>1 launch shape: torch.distributed.run, one shard apiserver per rank, rank 0 reports."""
+    pytest.importorskip("torch.distributed")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1"]
