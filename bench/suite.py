@@ -1,0 +1,413 @@
+#!/usr/bin/env python
+"""Benchmark suite for the five BASELINE.json configurations, native vs reference-compat mode.
+
+    python bench/suite.py --configs 1,2,3,4,5 --modes native,compat [--scale 1.0] [--out results.json]
+
+Every configuration runs on real processes: one fake kube-apiserver process per cluster
+(controller + N shards) and the controller as `python -m ncc` (which in native mode spawns its
+shard executors).  Propagation latency is measured with server-side probes (`ncc.fakeapi.markers`):
+shard commit time − controller commit time for every object, no client-side watches involved.
+
+  1  1 shard,  10 templates × 1 Secret — cold start, then single-template update latency
+  2  2 shards, 100 templates × (Secret + ConfigMap) — cold start + update-wave throughput
+  3  4 shards, 1 000 templates, steady churn at 10 template updates/s — latency under churn
+  4  8 shards, 10 000 templates + dependents, cold-start adoption of pre-existing shard objects
+     (every template pre-exists unlabelled on every shard, half of them drifted; half of the
+     dependents pre-exist, owned, with stale data)
+  5  8 shards, 1 000 templates, one shard apiserver flapping (down/up every 1.5 s) — healthy-shard
+     latency and the flaky shard's catch-up
+
+Reference-compat mode reproduces the reference controller's scheduling (sequential fail-fast
+shard loop, client-go 5 QPS/10 burst per API group, Event per reconcile, 2 workers).  It is a
+semantic reproduction on the same substrate, not the Go binary.  `--compat-cap N` bounds the
+template count of compat runs whose full size would take hours; capped runs are labelled.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import base64
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from ncc.kube.kubeconfig import render_kubeconfig  # noqa: E402
+from ncc.testing.env import spawn_fakeapi, wait_port_file  # noqa: E402
+from ncc.testing.workload import (configmap_name, make_configmap, make_secret, make_template,  # noqa: E402
+                                  secret_name, template_name)
+
+NS = "nexus"
+MARKERS = ["nexusalgorithmtemplates=spec.container.versionTag", "secrets=data.version", "configmaps=data.version"]
+
+
+def b64(s: str) -> str:
+    return base64.b64encode(s.encode()).decode()
+
+
+def pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, max(0, int(round(q / 100.0 * (len(xs) - 1)))))]
+
+
+def summarize(lat_ms: list) -> dict:
+    if not lat_ms:
+        return {"n": 0}
+    return {"n": len(lat_ms), "p50_ms": round(statistics.median(lat_ms), 2), "p99_ms": round(pct(lat_ms, 99), 2),
+            "max_ms": round(max(lat_ms), 2)}
+
+
+class Topology:
+    def __init__(self, n_shards: int, mode: str, workers: int | None = None, extra_env: dict | None = None):
+        self.n = n_shards
+        self.mode = mode
+        self.workers = workers
+        self.extra_env = extra_env or {}
+        self.work = tempfile.mkdtemp(prefix="ncc-suite-")
+        self.procs: list = []
+        self.controller = None
+        self.session = None
+
+    async def _post(self, url, body, timeout=None):
+        import aiohttp
+        async with self.session.post(url, data=json.dumps(body), headers={"Content-Type": "application/json"},
+                                     timeout=aiohttp.ClientTimeout(total=timeout)) as r:
+            r.raise_for_status()
+            return await r.json()
+
+    async def start_servers(self):
+        import aiohttp
+        self.session = aiohttp.ClientSession()
+        loop = asyncio.get_running_loop()
+        extra = sum((["--marker", m] for m in MARKERS), [])
+        files = []
+        for i in range(self.n):
+            pf = os.path.join(self.work, f"shard-{i}.url")
+            self.procs.append(spawn_fakeapi(f"shard-{i}", pf, extra=extra))
+            files.append(pf)
+        pf = os.path.join(self.work, "controller.url")
+        self.procs.append(spawn_fakeapi("controller", pf))
+        files.append(pf)
+        urls = [await loop.run_in_executor(None, wait_port_file, f, p) for f, p in zip(files, self.procs)]
+        self.shard_urls, self.ctrl_url = urls[:-1], urls[-1]
+        self.shard_dir = os.path.join(self.work, "shards")
+        os.makedirs(self.shard_dir)
+        for i, u in enumerate(self.shard_urls):
+            with open(os.path.join(self.shard_dir, f"shard-{i}.kubeconfig"), "w") as f:
+                f.write(render_kubeconfig(u, f"shard-{i}"))
+        self.ckc = os.path.join(self.work, "controller.kubeconfig")
+        with open(self.ckc, "w") as f:
+            f.write(render_kubeconfig(self.ctrl_url, "controller"))
+
+    def start_controller(self) -> int:
+        env = dict(os.environ)
+        env.update({"NEXUS__CONTROLLER_CONFIG_PATH": self.ckc, "NEXUS__SHARD_CONFIG_PATH": self.shard_dir,
+                    "NEXUS__CONTROLLER_NAMESPACE": NS, "NEXUS__ALIAS": "controller-cluster",
+                    "NEXUS__MODE": self.mode, "NEXUS__LOG_LEVEL": "WARNING",
+                    "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        env["NEXUS__WORKERS"] = str(self.workers or (64 if self.mode == "native" else 2))
+        env.update(self.extra_env)
+        self.log = open(os.path.join(self.work, "controller.log"), "wb")
+        t = time.time_ns()
+        self.controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=self.log,
+                                           stderr=subprocess.STDOUT, cwd=self.work)
+        self.procs.append(self.controller)
+        return t
+
+    async def seed(self, url, items):
+        for k in range(0, len(items), 5000):
+            await self._post(f"{url}/_fake/objects", {"items": items[k:k + 5000]})
+
+    async def apply(self, items) -> int:
+        r = await self._post(f"{self.ctrl_url}/_fake/apply", {"items": items})
+        return r["t1_ns"]
+
+    async def wait(self, i: int, want: list, timeout: float) -> dict:
+        return await self._post(f"{self.shard_urls[i]}/_fake/markers/wait",
+                                {"want": want, "timeout": timeout, "times": True}, timeout=timeout + 30)
+
+    async def fault(self, i: int, body: dict) -> None:
+        await self._post(f"{self.shard_urls[i]}/_fake/faults", body)
+
+    def log_tail(self, n=2000) -> str:
+        try:
+            with open(os.path.join(self.work, "controller.log"), "rb") as f:
+                return f.read()[-n:].decode(errors="replace")
+        except OSError:
+            return ""
+
+    async def stop(self):
+        for p in reversed(self.procs):
+            if p.poll() is None:
+                p.terminate()
+        for p in self.procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        if self.session is not None:
+            await self.session.close()
+        shutil.rmtree(self.work, ignore_errors=True)
+
+
+def objects(T: int, version: int, *, secrets=True, configmaps=True, payload=256) -> list:
+    out = []
+    for i in range(T):
+        out.append(make_template(i, NS, secrets=[secret_name(i)] if secrets else [],
+                                 configmaps=[configmap_name(i)] if configmaps else [], version=f"v{version}"))
+        if secrets:
+            out.append(make_secret(secret_name(i), NS, payload=payload, version=version))
+        if configmaps:
+            out.append(make_configmap(configmap_name(i), NS, payload=payload, version=version))
+    return out
+
+
+def want(T: int, version: int, *, secrets=True, configmaps=True) -> list:
+    w = [{"plural": "nexusalgorithmtemplates", "value": f"v{version}", "count": T}]
+    if secrets:
+        w.append({"plural": "secrets", "value": b64(str(version)), "count": T})
+    if configmaps:
+        w.append({"plural": "configmaps", "value": str(version), "count": T})
+    return w
+
+
+def latencies(r: dict, t0_ns: int) -> list:
+    return [(t - t0_ns) / 1e6 for ts in r["times"].values() for t in ts]
+
+
+async def wave_all(topo: Topology, T: int, version: int, timeout: float, shards=None, **kw) -> tuple:
+    shards = range(topo.n) if shards is None else shards
+    res = await asyncio.gather(*(topo.wait(i, want(T, version, **kw), timeout) for i in shards))
+    return res
+
+
+# ------------------------------------------------------------------------------------------- configs
+async def config_cold_and_waves(n_shards, T, mode, waves, timeout, secrets=True, configmaps=True, label=""):
+    topo = Topology(n_shards, mode)
+    try:
+        await topo.start_servers()
+        await topo.apply(objects(T, 0, secrets=secrets, configmaps=configmaps))
+        t_boot = topo.start_controller()
+        res = await wave_all(topo, T, 0, timeout, secrets=secrets, configmaps=configmaps)
+        ok = all(r["ok"] for r in res)
+        objs_per_shard = T * (1 + secrets + configmaps)
+        out = {"config": label, "mode": mode, "shards": n_shards, "templates": T, "objects_per_wave": objs_per_shard
+               * n_shards, "cold_start": {"ok": ok}}
+        if ok:
+            done = max(max(max(ts) for ts in r["times"].values()) for r in res)
+            cold = (done - t_boot) / 1e9
+            out["cold_start"].update(seconds=round(cold, 3), objects_per_s=round(objs_per_shard * n_shards / cold, 1))
+        else:
+            out["cold_start"]["counts"] = [r["counts"] for r in res]
+            out["log_tail"] = topo.log_tail()
+            return out
+        lat, t_total = [], 0.0
+        for v in range(1, waves + 1):
+            t0 = await topo.apply(objects(T, v, secrets=secrets, configmaps=configmaps))
+            s = time.perf_counter()
+            res = await wave_all(topo, T, v, timeout, secrets=secrets, configmaps=configmaps)
+            t_total += time.perf_counter() - s
+            if not all(r["ok"] for r in res):
+                out["waves"] = {"ok": False, "at_wave": v, "counts": [r["counts"] for r in res]}
+                out["log_tail"] = topo.log_tail()
+                return out
+            for r in res:
+                lat.extend(latencies(r, t0))
+        if waves:
+            out["waves"] = {"ok": True, "waves": waves, "objects_per_s": round(waves * objs_per_shard * n_shards /
+                                                                               t_total, 1), **summarize(lat)}
+        return out
+    finally:
+        await topo.stop()
+
+
+async def config3_churn(mode, T, rate, duration, timeout):
+    topo = Topology(4, mode)
+    try:
+        await topo.start_servers()
+        await topo.apply(objects(T, 0))
+        topo.start_controller()
+        res = await wave_all(topo, T, 0, timeout)
+        out = {"config": "3: 4 shards, churn", "mode": mode, "shards": 4, "templates": T, "rate_per_s": rate,
+               "duration_s": duration, "cold_start_ok": all(r["ok"] for r in res)}
+        if not out["cold_start_ok"]:
+            out["log_tail"] = topo.log_tail()
+            return out
+        n = int(rate * duration)
+        sent = []
+        interval = 1.0 / rate
+        t_start = time.perf_counter()
+        for k in range(n):
+            i = (k * 7919) % T
+            tmpl = make_template(i, NS, secrets=[secret_name(i)], configmaps=[configmap_name(i)], version=f"c{k}")
+            t0 = await topo.apply([tmpl])
+            sent.append((k, t0))
+            delay = t_start + (k + 1) * interval - time.perf_counter()
+            if delay > 0:
+                await asyncio.sleep(delay)
+        lat, missing = [], 0
+        for i in range(4):
+            w = [{"plural": "nexusalgorithmtemplates", "value": f"c{k}", "count": 1} for k, _ in sent]
+            r = await topo.wait(i, w, timeout)
+            for k, t0 in sent:
+                ts = r["times"].get(f"nexusalgorithmtemplates=c{k}") or []
+                if ts:
+                    lat.append((ts[0] - t0) / 1e6)
+                else:
+                    missing += 1
+        out["updates"] = n
+        out["latency"] = summarize(lat)
+        out["missing_after_timeout"] = missing
+        return out
+    finally:
+        await topo.stop()
+
+
+async def config4_adoption(mode, T, timeout):
+    """8 shards with pre-existing objects: every template exists unlabelled (half drifted); half the
+    dependents exist owned by the shard template with stale data."""
+    topo = Topology(8, mode)
+    try:
+        await topo.start_servers()
+        await topo.apply(objects(T, 0))
+        for i in range(8):
+            tmpls, deps = [], []
+            for k in range(T):
+                t = make_template(k, NS, secrets=[secret_name(k)], configmaps=[configmap_name(k)],
+                                  version="stale" if k % 2 else "v0")
+                tmpls.append(t)
+                if k % 2 == 0:
+                    s = make_secret(secret_name(k), NS, version=99)
+                    s["__owner_template__"] = template_name(k)
+                    c = make_configmap(configmap_name(k), NS, version=99)
+                    c["__owner_template__"] = template_name(k)
+                    deps += [s, c]
+            await topo.seed(topo.shard_urls[i], tmpls)
+            await topo.seed(topo.shard_urls[i], deps)
+        t_boot = topo.start_controller()
+        res = await wave_all(topo, T, 0, timeout)
+        ok = all(r["ok"] for r in res)
+        out = {"config": "4: 8 shards, cold-start adoption", "mode": mode, "shards": 8, "templates": T, "ok": ok}
+        if ok:
+            done = max(max(max(ts) for ts in r["times"].values()) for r in res)
+            secs = (done - t_boot) / 1e9
+            out.update(converge_s=round(secs, 3), objects_per_s=round(3 * T * 8 / secs, 1))
+        else:
+            out["counts"] = [r["counts"] for r in res]
+            out["log_tail"] = topo.log_tail()
+        return out
+    finally:
+        await topo.stop()
+
+
+async def config5_flaky(mode, T, timeout, flap=1.5):
+    topo = Topology(8, mode)
+    try:
+        await topo.start_servers()
+        await topo.apply(objects(T, 0))
+        topo.start_controller()
+        res = await wave_all(topo, T, 0, timeout)
+        out = {"config": "5: 8 shards, one flapping", "mode": mode, "shards": 8, "templates": T,
+               "cold_start_ok": all(r["ok"] for r in res)}
+        if not out["cold_start_ok"]:
+            out["log_tail"] = topo.log_tail()
+            return out
+        flaky = 3  # a shard in the middle: sequential compat processing blocks shards 4..7 behind it
+        stop = asyncio.Event()
+
+        async def flapper():
+            down = False
+            while not stop.is_set():
+                down = not down
+                await topo.fault(flaky, {"down": down, "write_only": False})
+                try:
+                    await asyncio.wait_for(stop.wait(), flap)
+                except asyncio.TimeoutError:
+                    pass
+            await topo.fault(flaky, {"down": False})
+
+        fl = asyncio.ensure_future(flapper())
+        t0 = await topo.apply(objects(T, 1))
+        healthy = [i for i in range(8) if i != flaky]
+        res = await asyncio.gather(*(topo.wait(i, want(T, 1), timeout) for i in healthy))
+        lat = [x for r in res for x in latencies(r, t0)]
+        out["healthy_shards"] = {"ok": all(r["ok"] for r in res), **summarize(lat)}
+        if res and all(r["ok"] for r in res):
+            out["healthy_shards"]["converge_s"] = round(
+                (max(max(max(ts) for ts in r["times"].values()) for r in res) - t0) / 1e9, 3)
+        stop.set()
+        await fl
+        r = await topo.wait(flaky, want(T, 1), timeout)
+        out["flaky_shard"] = {"ok": r["ok"], "counts": r["counts"]}
+        if r["ok"]:
+            out["flaky_shard"]["converge_after_recovery_s"] = round(
+                (max(max(ts) for ts in r["times"].values()) - t0) / 1e9, 3)
+        return out
+    finally:
+        await topo.stop()
+
+
+async def run(args) -> list:
+    results = []
+    s = args.scale
+    cap = args.compat_cap
+
+    def size(T, mode):
+        T = max(1, int(T * s))
+        return min(T, cap) if mode == "compat" and cap else T
+
+    for mode in args.modes:
+        for c in args.configs:
+            t = time.perf_counter()
+            if c == 1:
+                r = await config_cold_and_waves(1, size(10, mode), mode, waves=5, timeout=args.timeout,
+                                                configmaps=False, label="1: 1 shard, 10 templates x 1 Secret")
+            elif c == 2:
+                r = await config_cold_and_waves(2, size(100, mode), mode, waves=3, timeout=args.timeout,
+                                                label="2: 2 shards, 100 templates x (Secret+ConfigMap)")
+            elif c == 3:
+                r = await config3_churn(mode, size(1000, mode), rate=10.0, duration=args.churn_seconds,
+                                        timeout=args.timeout)
+            elif c == 4:
+                r = await config4_adoption(mode, size(10000, mode), timeout=args.timeout)
+            elif c == 5:
+                r = await config5_flaky(mode, size(1000, mode), timeout=args.timeout)
+            else:
+                continue
+            r["wall_s"] = round(time.perf_counter() - t, 1)
+            if mode == "compat" and cap:
+                r["compat_capped_templates"] = cap
+            print(json.dumps(r), flush=True)
+            results.append(r)
+    return results
+
+
+def main():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--configs", default="1,2,3,4,5")
+    p.add_argument("--modes", default="native,compat")
+    p.add_argument("--scale", type=float, default=1.0, help="multiply template counts (e.g. 0.1 for a quick run)")
+    p.add_argument("--compat-cap", type=int, default=100, help="max templates for compat runs (0 = no cap)")
+    p.add_argument("--churn-seconds", type=float, default=30.0)
+    p.add_argument("--timeout", type=float, default=600.0)
+    p.add_argument("--out", default="")
+    a = p.parse_args()
+    a.configs = [int(x) for x in a.configs.split(",") if x]
+    a.modes = [m for m in a.modes.split(",") if m]
+    res = asyncio.run(run(a))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -375,6 +375,13 @@ class FakeApiServer:
             n = 0
             for o in body.get("items") or []:
                 rt = R.by_kind(o["kind"])
+                owner = o.pop("__owner_template__", None)
+                if owner:  # seed a dependent owned by an existing template (resolve its live UID)
+                    ns_ = (o.get("metadata") or {}).get("namespace", "")
+                    t = self.state.get(R.TEMPLATES, ns_, owner)
+                    o.setdefault("metadata", {})["ownerReferences"] = [{
+                        "apiVersion": t["apiVersion"], "kind": t["kind"], "name": owner,
+                        "uid": t["metadata"]["uid"]}]
                 try:
                     self.state.create(rt, (o.get("metadata") or {}).get("namespace", ""), o)
                     n += 1
