@@ -177,18 +177,22 @@ class App:
             await self.close()
 
     async def close(self) -> None:
+        log.info("closing (role=%s)", self.options.role)
         if self.pool is not None:
             await self.pool.stop()
         if isinstance(self.recorder, BroadcastRecorder):
             await self.recorder.stop()
         await self.factory.stop()
+        log.debug("controller informers stopped")
         for s in self.shards:
             await s.stop()
+        log.debug("shards stopped")
         await self.client.close()
         if self.ops is not None:
             await self.ops.stop()
         if self.metrics is not None:
             self.metrics.close()
+        log.info("closed (role=%s)", self.options.role)
 
 
 def setup_signal_handler(stop: asyncio.Event) -> None:

@@ -26,6 +26,7 @@ import random
 from dataclasses import dataclass
 from typing import Callable
 
+from ..aio import wait_timeout
 from ..api.objects import ObjectKey, key_of
 from ..api.resources import ResourceType
 from ..kube import errors as E
@@ -101,6 +102,7 @@ class Informer:
         self.relists = 0
         self.events = 0
         self.last_error: BaseException | None = None
+        self._stopping = False
 
     # ------------------------------------------------------------- public API
     def add_event_handler(self, on_add=None, on_update=None, on_delete=None) -> None:
@@ -111,7 +113,7 @@ class Informer:
 
     async def wait_for_sync(self, timeout: float | None = None) -> bool:
         try:
-            await asyncio.wait_for(self._synced.wait(), timeout)
+            await wait_timeout(self._synced.wait(), timeout)
             return True
         except asyncio.TimeoutError:
             return False
@@ -124,15 +126,13 @@ class Informer:
         return self._task
 
     async def stop(self) -> None:
+        self._stopping = True
         for t in (self._task, self._resync_task):
             if t is not None:
                 t.cancel()
-        for t in (self._task, self._resync_task):
-            if t is not None:
-                try:
-                    await t
-                except (asyncio.CancelledError, Exception):  # noqa: BLE001
-                    pass
+        pending = [t for t in (self._task, self._resync_task) if t is not None]
+        if pending:
+            await asyncio.wait(pending, timeout=5.0)
         self._task = self._resync_task = None
 
     # ------------------------------------------------------------- dispatch
@@ -211,7 +211,7 @@ class Informer:
         backoff = 0.8
         rv = ""
         need_list = True
-        while True:
+        while not self._stopping:
             try:
                 if need_list:
                     rv = await self._list()

@@ -20,6 +20,7 @@ import asyncio
 import logging
 import time
 
+from ..aio import wait_timeout
 from ..api import constants as C
 from ..api import resources as R
 from ..api.objects import meta, now_rfc3339
@@ -94,7 +95,7 @@ class BroadcastRecorder(EventRecorder):
         if self._task is None:
             return
         try:
-            await asyncio.wait_for(self._queue.join(), drain_timeout)
+            await wait_timeout(self._queue.join(), drain_timeout)
         except asyncio.TimeoutError:
             pass
         self._task.cancel()

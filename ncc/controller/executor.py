@@ -25,6 +25,7 @@ import socket
 import sys
 
 from .ipc import Channel
+from ..aio import wait_timeout
 
 log = logging.getLogger("ncc.executor")
 
@@ -94,7 +95,7 @@ class ExecutorHandle:
         if self.proc is not None and self.proc.returncode is None:
             try:
                 self.proc.terminate()
-                await asyncio.wait_for(self.proc.wait(), timeout)
+                await wait_timeout(self.proc.wait(), timeout)
             except (ProcessLookupError, asyncio.TimeoutError):
                 try:
                     self.proc.kill()
@@ -118,7 +119,7 @@ class ExecutorPool:
 
     async def wait_ready(self, timeout: float | None = None) -> bool:
         try:
-            await asyncio.wait_for(asyncio.gather(*(h.ready.wait() for h in self.handles)), timeout)
+            await wait_timeout(asyncio.gather(*(h.ready.wait() for h in self.handles)), timeout)
             return True
         except asyncio.TimeoutError:
             return False

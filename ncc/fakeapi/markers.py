@@ -13,6 +13,8 @@ from __future__ import annotations
 import asyncio
 import time
 
+from ..aio import wait_timeout
+
 
 def _extract(obj: dict, path: list[str]):
     cur = obj
@@ -71,7 +73,7 @@ class MarkerTracker:
         fut = asyncio.get_running_loop().create_future()
         self._waiters.append((want, fut))
         try:
-            return await asyncio.wait_for(fut, timeout)
+            return await wait_timeout(fut, timeout)
         except asyncio.TimeoutError:
             return False
 

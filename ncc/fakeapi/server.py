@@ -28,6 +28,7 @@ import time
 from . import httpserver as web
 
 from ..api import resources as R
+from ..aio import wait_timeout
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
 from .markers import MarkerTracker
@@ -279,10 +280,13 @@ class FakeApiServer:
                     wait = min(wait, deadline - now)
                     if wait <= 0:
                         break
-                try:
-                    rec = await asyncio.wait_for(w.queue.get(), max(wait, 0.0))
-                except asyncio.TimeoutError:
-                    rec = False
+                if not w.queue.empty():
+                    rec = w.queue.get_nowait()
+                else:
+                    try:
+                        rec = await wait_timeout(w.queue.get(), max(wait, 0.0))
+                    except asyncio.TimeoutError:
+                        rec = False
                 if rec is None:
                     break
                 chunks = []

@@ -21,6 +21,7 @@ import ssl as _ssl
 from collections import deque
 from urllib.parse import urlsplit
 
+from ..aio import wait_timeout
 from . import errors as E
 
 _CRLF2 = b"\r\n\r\n"
@@ -252,7 +253,7 @@ class ConnectionPool:
             kw["ssl"] = self.ssl
             kw["server_hostname"] = self.server_hostname or self.host
         try:
-            _, proto = await asyncio.wait_for(
+            _, proto = await wait_timeout(
                 loop.create_connection(lambda: _Conn(self), self.host, self.port, **kw), self.connect_timeout)
         except (OSError, asyncio.TimeoutError, _ssl.SSLError) as e:
             raise E.TransportError(f"connect {self.host}:{self.port}: {type(e).__name__}: {e}") from e
@@ -286,8 +287,20 @@ class ConnectionPool:
             lines.append(b"Content-Length: " + str(body_len).encode())
         return b"\r\n".join(lines) + _CRLF2
 
+    @staticmethod
+    def _expire(c: _Conn, what: str) -> None:
+        """Timer callback: fail the in-flight exchange and drop the connection.
+
+        Timeouts are plain loop timers rather than `asyncio.wait_for`, which costs a Task per request
+        and on Python 3.10 can swallow a concurrent cancellation (bpo-42130) — a hang at shutdown."""
+        fut = c.fut
+        if fut is not None and not fut.done():
+            fut.set_exception(E.TransportError(f"{what}: timed out"))
+        c.close()
+
     async def request(self, method: str, target: str, headers: dict, body: bytes | None,
                       timeout: float | None = 30.0) -> _Response:
+        loop = asyncio.get_running_loop()
         async with self._sem:
             for attempt in (0, 1):
                 c = await self._acquire()
@@ -297,52 +310,61 @@ class ConnectionPool:
                                   (0 if method in ("POST", "PUT", "PATCH") else None))
                 if body:
                     data += body
+                fut = c.send(data)
+                timer = loop.call_later(timeout, self._expire, c, f"{method} {target}") if timeout else None
                 try:
-                    return await asyncio.wait_for(c.send(data), timeout)
+                    return await fut
                 except E.TransportError:
                     c.close()
                     # a reused keep-alive connection may have been closed by the server: retry once on a fresh one
-                    if attempt == 0 and reused:
+                    if attempt == 0 and reused and (timer is None or not timer.cancelled()) and not fut.cancelled():
+                        if timer is not None:
+                            timer.cancel()
                         continue
                     raise
-                except asyncio.TimeoutError as e:
-                    c.close()
-                    raise E.TransportError(f"{method} {target}: timeout after {timeout}s") from e
                 except BaseException:
                     c.close()
                     raise
+                finally:
+                    if timer is not None:
+                        timer.cancel()
         raise E.TransportError("unreachable")  # pragma: no cover
 
     async def stream(self, target: str, headers: dict, timeout: float | None = None):
-        """GET with a streaming body; yields complete lines (bytes).  Uses a dedicated connection."""
+        """GET with a streaming body; yields complete lines (bytes).  Uses a dedicated connection.
+
+        `timeout` bounds the whole stream (closing the connection ends it), like a client-side
+        `timeoutSeconds`; waiting itself is a plain Event wait, so cancellation is never swallowed."""
         c = await self._connect()
+        loop = asyncio.get_running_loop()
+        head_timer = loop.call_later(self.connect_timeout + 20, self._expire, c, f"GET {target}")
+        stream_timer = None
         try:
-            resp = await asyncio.wait_for(c.send(self._head("GET", target, headers, None), stream=True),
-                                          self.connect_timeout + 20)
+            resp = await c.send(self._head("GET", target, headers, None), stream=True)
+            head_timer.cancel()
+            if timeout:
+                stream_timer = loop.call_later(timeout, c.close)
             if resp.status >= 300:
                 # drain the (small) error body
                 while not c.stream_done:
                     c.stream_event.clear()
-                    await asyncio.wait_for(c.stream_event.wait(), 10)
+                    await c.stream_event.wait()
                 raw = b"\n".join(c.stream) + bytes(c.linebuf)
                 yield resp, raw
                 return
             yield resp, None
-            loop = asyncio.get_running_loop()
-            deadline = loop.time() + timeout if timeout else None
             while True:
                 while c.stream:
                     yield None, c.stream.popleft()
                     c.resume()
-                if c.stream_done:
+                if c.stream_done or c.closed:
                     return
                 c.stream_event.clear()
-                wait = None if deadline is None else max(0.1, deadline - loop.time())
-                try:
-                    await asyncio.wait_for(c.stream_event.wait(), wait)
-                except asyncio.TimeoutError:
-                    return
+                await c.stream_event.wait()
         finally:
+            head_timer.cancel()
+            if stream_timer is not None:
+                stream_timer.cancel()
             c.close()
 
     def close(self) -> None:

@@ -15,6 +15,7 @@ import asyncio
 from dataclasses import dataclass, field
 from typing import Any, Callable
 
+from ..aio import wait_timeout
 from ..api.objects import deep_copy
 from ..api.resources import ResourceType
 from ..fakeapi.storage import ClusterState
@@ -140,7 +141,7 @@ class FakeClient(KubeClient):
             while True:
                 timeout = None if deadline is None else max(0.0, deadline - loop.time())
                 try:
-                    rec = await asyncio.wait_for(w.queue.get(), timeout)
+                    rec = await wait_timeout(w.queue.get(), timeout)
                 except asyncio.TimeoutError:
                     return
                 if rec is None:
