@@ -23,6 +23,7 @@ from ..api.fingerprint import SLIM_FP, fingerprint
 from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
 from ..api.refs import configmap_names, is_owned_by_uid, ready_condition, secret_names, template_owner_ref
 from ..kube import errors as E
+from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
 
 log = logging.getLogger("ncc.reconcile")
 
@@ -82,6 +83,15 @@ class ReconcileMixin:
     """Reconcile logic; mixed into `Controller` (which provides clients, listers, options)."""
 
     # ============================================================ status (controller.go:428-480)
+    async def _write_status(self, rt, namespace: str, obj: dict, field_manager: str | None = None) -> dict:
+        """UpdateStatus (compat: PUT with the cached resourceVersion, 409 on a concurrent edit) or, in
+        native mode, a JSON merge PATCH of `.status` — the controller owns status, so a spec edit by a
+        user racing with our status write no longer costs a conflict and a retry."""
+        if self.options.patch_writes:
+            return await self.client.patch(rt, namespace, meta(obj).get("name", ""), {"status": obj.get("status")},
+                                           patch_type=PATCH_MERGE, field_manager=field_manager, subresource="status")
+        return await self.client.update_status(rt, namespace, obj, field_manager=field_manager)
+
     async def report_template_init_condition(self, template: dict) -> dict:
         status = template.get("status") or {}
         if not status.get("conditions"):
@@ -89,7 +99,7 @@ class ReconcileMixin:
             new = with_fields(template, status=dict(status, conditions=[
                 ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Algorithm {q(name)} initializing")]))
             self._pass_wrote()
-            res = await self.client.update_status(R.TEMPLATES, meta(template).get("namespace", ""), new,
+            res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""), new,
                                                   field_manager=C.FIELD_MANAGER)
             return self._assume(self.template_informer, res)
         return template
@@ -101,7 +111,7 @@ class ReconcileMixin:
             new = with_fields(workgroup, status=dict(status, conditions=[
                 ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Workgroup {q(name)} initializing")]))
             self._pass_wrote()
-            res = await self.client.update_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""), new,
+            res = await self._write_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""), new,
                                                   field_manager=C.FIELD_MANAGER)
             return self._assume(self.workgroup_informer, res)
         return workgroup
@@ -118,7 +128,7 @@ class ReconcileMixin:
         if new_status != status:
             conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
             self._pass_wrote()
-            res = await self.client.update_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""),
+            res = await self._write_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""),
                                                   with_fields(workgroup, status=new_status),
                                                   field_manager=C.FIELD_MANAGER)
             return self._assume(self.workgroup_informer, res)
@@ -137,7 +147,7 @@ class ReconcileMixin:
         if new_status != status:
             conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
             self._pass_wrote()
-            res = await self.client.update_status(R.TEMPLATES, meta(template).get("namespace", ""),
+            res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""),
                                                   with_fields(template, status=new_status),
                                                   field_manager=C.FIELD_MANAGER)
             return self._assume(self.template_informer, res)
@@ -187,7 +197,12 @@ class ReconcileMixin:
     async def _adopt_one(self, rt, ns, obj, template, nm, informer):
         self._pass_wrote()
         try:
-            res = await self.client.update(rt, ns, obj)
+            if self.options.patch_writes:
+                # strategic merge on ownerReferences (patchMergeKey=uid) appends without a resourceVersion race
+                res = await self.client.patch(rt, ns, nm, {"metadata": {"ownerReferences": [template_owner_ref(template)]}},
+                                              patch_type=PATCH_STRATEGIC, field_manager=C.FIELD_MANAGER)
+            else:
+                res = await self.client.update(rt, ns, obj)
             self._assume(informer, res)
         except Exception as e:  # noqa: BLE001
             self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
