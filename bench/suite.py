@@ -255,9 +255,9 @@ async def config3_churn(mode, T, rate, duration, timeout):
             if delay > 0:
                 await asyncio.sleep(delay)
         lat, missing = [], 0
-        for i in range(4):
-            w = [{"plural": "nexusalgorithmtemplates", "value": f"c{k}", "count": 1} for k, _ in sent]
-            r = await topo.wait(i, w, timeout)
+        w = [{"plural": "nexusalgorithmtemplates", "value": f"c{k}", "count": 1} for k, _ in sent]
+        results = await asyncio.gather(*(topo.wait(i, w, timeout) for i in range(4)))
+        for r in results:
             for k, t0 in sent:
                 ts = r["times"].get(f"nexusalgorithmtemplates=c{k}") or []
                 if ts:
@@ -356,7 +356,23 @@ async def config5_flaky(mode, T, timeout, flap=1.5):
         await topo.stop()
 
 
+async def heartbeat(every: float = 30.0):
+    """Progress lines so a long (compat) run is visibly alive."""
+    t0 = time.perf_counter()
+    while True:
+        await asyncio.sleep(every)
+        print(f"# still running: {time.perf_counter() - t0:.0f}s", flush=True)
+
+
 async def run(args) -> list:
+    hb = asyncio.ensure_future(heartbeat())
+    try:
+        return await _run(args)
+    finally:
+        hb.cancel()
+
+
+async def _run(args) -> list:
     results = []
     s = args.scale
     cap = args.compat_cap
@@ -388,6 +404,9 @@ async def run(args) -> list:
                 r["compat_capped_templates"] = cap
             print(json.dumps(r), flush=True)
             results.append(r)
+            if args.out:  # keep partial results if a later configuration is cut short
+                with open(args.out, "w") as f:
+                    json.dump(results, f, indent=1)
     return results
 
 
