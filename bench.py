@@ -100,6 +100,10 @@ class Dist:
             import torch
             torch.cuda.synchronize()
 
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
     def max(self, x: float) -> float:
         if self.dist is None:
             return x
@@ -210,6 +214,7 @@ async def run(args, d: Dist) -> dict | None:
 
             # ---- cold start (warm-up 0): boot + full fan-out of pre-seeded objects
             r = await converge(0, True)
+            d.barrier()
             cold_local = max(max(v) for v in r["times"].values()) - t_boot
             cold = d.max(cold_local / 1e9)
 
@@ -228,6 +233,7 @@ async def run(args, d: Dist) -> dict | None:
                     t0 = a["t1_ns"]
                 t0 = d.broadcast(t0)
                 r = await converge(step, timed)
+                d.barrier()  # the wave is done only when every shard has converged
                 if timed:
                     for ts in r["times"].values():
                         lat_ms.extend((t - t0) / 1e6 for t in ts)

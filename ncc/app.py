@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import json
 import logging
 import os
 import signal
@@ -146,15 +147,19 @@ class App:
 
     def debug_state(self) -> dict:
         c = self.controller
-        out = {"role": c.role, "queue_depth": len(c.queue), "stats": c.stats, "queue": c.queue.metrics,
-               "shards": {s.name: {"synced": s.has_synced()} for s in c.shards},
-               "events": getattr(self.recorder, "stats", {})}
+        out = c.debug_snapshot()
+        out["events"] = getattr(self.recorder, "stats", {})
         if self.pool is not None:
             out["executors"] = self.pool.stats()
         return out
 
     async def run(self, stop: asyncio.Event) -> None:
         controller = self.controller or await self.build()
+        try:  # `kill -USR1 <pid>` dumps queue/informer state to the log
+            asyncio.get_running_loop().add_signal_handler(
+                signal.SIGUSR1, lambda: log.warning("debug state: %s", json.dumps(self.debug_state(), default=str)))
+        except (NotImplementedError, RuntimeError, ValueError):  # pragma: no cover
+            pass
         if self.ops is not None:
             await self.ops.start(self.cfg.health_bind_address or self.cfg.metrics_bind_address)
         for s in self.shards:

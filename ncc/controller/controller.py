@@ -293,6 +293,29 @@ class Controller(ReconcileMixin):
             out[s] = e[2]
         return out
 
+    def debug_snapshot(self) -> dict:
+        """Queue/informer/shard state for operators (SIGUSR1 dump, /debug/state)."""
+        core = self.queue.core
+
+        def inf(i: Informer) -> dict:
+            return {"synced": i.has_synced(), "objects": len(i.store), "events": i.events, "relists": i.relists,
+                    "last_rv": i.last_rv, "last_error": repr(i.last_error) if i.last_error else None}
+        return {
+            "role": self.role, "stats": dict(self.stats),
+            "queue": {"depth": core.length(), "waiting": core.waiting(), "processing": core.processing(),
+                      **self.queue.metrics},
+            "informers": {n: inf(i) for n, i in (("templates", self.template_informer),
+                                                 ("workgroups", self.workgroup_informer),
+                                                 ("secrets", self.secret_informer),
+                                                 ("configmaps", self.configmap_informer))},
+            "shards": {s.name: {n: inf(i) for n, i in (("templates", s.template_informer),
+                                                       ("workgroups", s.workgroup_informer),
+                                                       ("secrets", s.secret_informer),
+                                                       ("configmaps", s.configmap_informer))}
+                       for s in self.shards},
+            "pending_deletes": len(self._pending_deletes), "shard_state": len(self.shard_state),
+        }
+
     # ================================================================== helpers
     def _assume(self, informer: Informer, res):
         if self.options.assume_writes and isinstance(res, dict):
