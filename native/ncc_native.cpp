@@ -14,6 +14,8 @@
 //    type-tagged scalars) computed by walking the CPython objects directly, ~10x cheaper than
 //    canonical json.dumps + hashing; used for O(1) drift detection on slim shard caches.
 //  * fingerprint_many(list) — batch form (one call per informer relist page).
+//  * scan_event(bytes) — reads type/namespace/name/resourceVersion out of a raw watch-event line
+//    without materialising the object, so informers can recognise echoes of their own writes.
 
 #include <pybind11/pybind11.h>
 
@@ -34,7 +36,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 3
+#define NCC_NATIVE_ABI 4
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -361,6 +363,171 @@ class RateLimitingQueue {
     bool shutting_down_ = false;
 };
 
+
+// ----------------------------------------------------------------------------- watch-event scanner
+// scan_event(line) -> (type, namespace, name, resourceVersion) | None
+//
+// Structural scan of one watch-stream line {"type":..., "object":{..., "metadata":{...}}} that reads
+// only the four strings the informer needs to recognise the echo of its own write, skipping every
+// other value by bracket matching.  No Python objects are built for the (large) spec/data payloads;
+// a full json.loads happens only for events that are not our own echoes.  Any input it does not
+// fully understand (escaped keys or values, malformed JSON) returns None and the caller falls back.
+class Scanner {
+  public:
+    Scanner(const char* p, size_t n) : p_(p), e_(p + n) {}
+
+    bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        if (!expect('{')) return false;
+        bool have_type = false, have_obj = false;
+        if (peek('}')) return false;
+        for (;;) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            if (key == "type") {
+                if (!str(type)) return false;
+                have_type = true;
+            } else if (key == "object") {
+                if (!object_meta(ns, name, rv)) return false;
+                have_obj = true;
+            } else if (!skip_value()) {
+                return false;
+            }
+            if (have_type && have_obj) return true;
+            if (peek(',')) { ++p_; continue; }
+            return false;
+        }
+    }
+
+  private:
+    const char* p_;
+    const char* e_;
+
+    void ws() {
+        while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+    }
+    bool peek(char c) {
+        ws();
+        return p_ < e_ && *p_ == c;
+    }
+    bool expect(char c) {
+        ws();
+        if (p_ >= e_ || *p_ != c) return false;
+        ++p_;
+        return true;
+    }
+    // a string without escapes (anything escaped makes the caller fall back to json.loads)
+    bool str(std::string_view& out) {
+        ws();
+        if (p_ >= e_ || *p_ != '"') return false;
+        const char* s = ++p_;
+        while (p_ < e_ && *p_ != '"') {
+            if (*p_ == '\\') return false;
+            ++p_;
+        }
+        if (p_ >= e_) return false;
+        out = std::string_view(s, static_cast<size_t>(p_ - s));
+        ++p_;
+        return true;
+    }
+    bool skip_string() {
+        if (p_ >= e_ || *p_ != '"') return false;
+        ++p_;
+        while (p_ < e_) {
+            if (*p_ == '\\') {
+                p_ += 2;
+                continue;
+            }
+            if (*p_ == '"') {
+                ++p_;
+                return true;
+            }
+            ++p_;
+        }
+        return false;
+    }
+    bool skip_value() {
+        ws();
+        if (p_ >= e_) return false;
+        char c = *p_;
+        if (c == '"') return skip_string();
+        if (c == '{' || c == '[') {
+            int depth = 0;
+            while (p_ < e_) {
+                char d = *p_;
+                if (d == '"') {
+                    if (!skip_string()) return false;
+                    continue;
+                }
+                if (d == '{' || d == '[') ++depth;
+                else if (d == '}' || d == ']') {
+                    if (--depth == 0) {
+                        ++p_;
+                        return true;
+                    }
+                }
+                ++p_;
+            }
+            return false;
+        }
+        while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n' &&
+               *p_ != '\t' && *p_ != '\r')
+            ++p_;
+        return true;
+    }
+    bool object_meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        if (!expect('{')) return false;
+        bool found = false;
+        if (peek('}')) { ++p_; return false; }
+        for (;;) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            if (key == "metadata") {
+                if (!meta(ns, name, rv)) return false;
+                found = true;
+            } else if (!skip_value()) {
+                return false;
+            }
+            if (peek(',')) { ++p_; continue; }
+            if (!expect('}')) return false;
+            return found;
+        }
+    }
+    bool meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        if (!expect('{')) return false;
+        bool have_name = false, have_rv = false;
+        if (peek('}')) { ++p_; return false; }
+        for (;;) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            if (key == "name") {
+                if (!str(name)) return false;
+                have_name = true;
+            } else if (key == "namespace") {
+                if (!str(ns)) return false;
+            } else if (key == "resourceVersion") {
+                if (!str(rv)) return false;
+                have_rv = true;
+            } else if (!skip_value()) {
+                return false;
+            }
+            if (peek(',')) { ++p_; continue; }
+            if (!expect('}')) return false;
+            return have_name && have_rv;
+        }
+    }
+};
+
+py::object scan_event(py::bytes line) {
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view type, ns, name, rv;
+    Scanner sc(buf, static_cast<size_t>(len));
+    if (!sc.scan(type, ns, name, rv)) return py::none();
+    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
+                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -368,6 +535,8 @@ PYBIND11_MODULE(_native, m) {
     m.attr("ABI_VERSION") = NCC_NATIVE_ABI;
     m.def("fingerprint", &fingerprint, py::arg("obj"), "64-bit structural digest of a JSON-shaped value");
     m.def("fingerprint_many", &fingerprint_many, py::arg("objs"));
+    m.def("scan_event", &scan_event, py::arg("line"),
+          "(type, namespace, name, resourceVersion) of a watch-event line, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")
         .def(py::init<double, double, double, int>(), py::arg("base_delay"), py::arg("max_delay"), py::arg("qps"),
              py::arg("burst"))

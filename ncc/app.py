@@ -198,6 +198,11 @@ class App:
         if self.metrics is not None:
             self.metrics.close()
         log.info("closed (role=%s)", self.options.role)
+        if os.environ.get("NCC_CPU_REPORT"):
+            import resource
+            ru = resource.getrusage(resource.RUSAGE_SELF)
+            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f reconciles=%d", self.options.role, ru.ru_utime,
+                        ru.ru_stime, self.controller.stats["reconciles"])
 
 
 def setup_signal_handler(stop: asyncio.Event) -> None:

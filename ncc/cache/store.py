@@ -133,6 +133,19 @@ class Store:
             return
         self._assumed[key] = (obj, rv, time.monotonic() + self.assume_ttl)
 
+    def confirm(self, key: ObjectKey, resource_version: str) -> dict | None:
+        """The watch delivered exactly the version we assumed: promote it without decoding the event."""
+        a = self._assumed.get(key)
+        if a is None or a[1] != rv_int(resource_version):
+            return None
+        del self._assumed[key]
+        obj = a[0]
+        old = self._items.get(key)
+        self._items[key] = obj
+        if self._indexers:
+            self._index(key, old, obj)
+        return obj
+
     # ------------------------------------------------------------ reads
     def get(self, namespace: str, name: str) -> dict | None:
         key = ObjectKey(namespace, name)

@@ -80,6 +80,9 @@ class Controller(ReconcileMixin):
         self.on_ready = None  # executor role: called once caches are synced and workers run
         self.shard_state: dict[str, dict] = {}  # coordinator role: key -> {shard: (uid, generation, error)}
         self._pending_event: set = set()
+        if o.assume_writes:
+            for inf in (template_informer, workgroup_informer, secret_informer, configmap_informer):
+                inf.echo_fastpath = True
         if o.mode == "native":
             # reverse index template ← referenced Secret/ConfigMap, so dependents map to templates even
             # before adoption has stamped ownerRefs on them

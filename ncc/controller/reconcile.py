@@ -79,6 +79,19 @@ def slim_data(obj: dict) -> dict:
     return out
 
 
+async def gather_all(coros) -> list:
+    """asyncio.gather(..., return_exceptions=True) without Task overhead for the common single case."""
+    coros = list(coros)
+    if len(coros) == 1:
+        try:
+            return [await coros[0]]
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001
+            return [e]
+    return await asyncio.gather(*coros, return_exceptions=True)
+
+
 class ReconcileMixin:
     """Reconcile logic; mixed into `Controller` (which provides clients, listers, options)."""
 
@@ -244,8 +257,7 @@ class ReconcileMixin:
         spec = template.get("spec")
         spec_fp = fingerprint(spec) if self.options.slim_shard_cache else None
         if self.options.concurrent_fanout:
-            results = await asyncio.gather(*(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards),
-                                           return_exceptions=True)
+            results = await gather_all(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards)
             failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
             for r in failures.values():
                 if isinstance(r, asyncio.CancelledError):
@@ -276,8 +288,7 @@ class ReconcileMixin:
             self.secret_lister.get(ns, nm)
         for nm in configmap_names(template):
             self.configmap_lister.get(ns, nm)
-        results = await asyncio.gather(*(self._sync_template_to_shard(template, s, None) for s in self.shards),
-                                       return_exceptions=True)
+        results = await gather_all(self._sync_template_to_shard(template, s, None) for s in self.shards)
         failures = {}
         for s, r in zip(self.shards, results):
             if isinstance(r, asyncio.CancelledError):
@@ -335,8 +346,14 @@ class ReconcileMixin:
             shard_template = await self._write(shard, "create_template", shard.template_informer, R.TEMPLATES,
                                                name, ns, spec, C.FIELD_MANAGER)
         if self.options.concurrent_dependents:
-            await asyncio.gather(self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard),
-                                 self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard))
+            # dependents need the shard template's UID for their ownerRefs, so they go after it — all at once
+            holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) else shard_template
+            jobs = [self._sync_dependent(R.SECRETS, template, shard_template, shard, n) for n in secret_names(holder)]
+            jobs += [self._sync_dependent(R.CONFIGMAPS, template, shard_template, shard, n)
+                     for n in configmap_names(holder)]
+            for r in await gather_all(jobs):
+                if isinstance(r, BaseException):
+                    raise r
         else:
             await self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard)
             await self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard)
@@ -503,8 +520,7 @@ class ReconcileMixin:
                 await self.propagate_workgroup_delete(namespace, name)
             return
         if self.role == "executor":
-            results = await asyncio.gather(*(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards),
-                                           return_exceptions=True)
+            results = await gather_all(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards)
             failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
             self._report(C.KIND_WORKGROUP, namespace, name, workgroup,
                          {s.name: (f"{type(failures[s.name]).__name__}: {failures[s.name]}"[:500]
@@ -517,8 +533,7 @@ class ReconcileMixin:
             await self._coordinator_finish(C.KIND_WORKGROUP, workgroup)
             return
         if self.options.concurrent_fanout:
-            results = await asyncio.gather(*(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards),
-                                           return_exceptions=True)
+            results = await gather_all(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards)
             failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
             if failures:
                 if self.options.shard_failure_isolation:

@@ -218,14 +218,14 @@ class RestClient(KubeClient):
                 body["preconditions"] = preconditions
         return await self.request("DELETE", rt.item_path(namespace, name), body=body)
 
-    async def watch(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
-                    allow_bookmarks=True, label_selector=None) -> AsyncIterator[WatchEvent]:
+    async def watch_raw(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
+                        allow_bookmarks=True, label_selector=None) -> AsyncIterator[bytes]:
+        """The watch stream as raw JSON lines (one event per line), undecoded."""
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": timeout_seconds,
                   "allowWatchBookmarks": "true" if allow_bookmarks else None, "labelSelector": label_selector}
         target = rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items() if v is not None})
         self.stats["watch_streams"] += 1
         headers = await self._headers(None)
-        loads = json.loads
         if self.transport == "fast":
             pool = await self._get_pool()
             stream = pool.stream(target, headers, timeout=(timeout_seconds + 30) if timeout_seconds else None)
@@ -234,13 +234,12 @@ class RestClient(KubeClient):
                     if resp is not None:
                         if resp.status >= 300:
                             try:
-                                st = loads(line) if line else None
+                                st = json.loads(line) if line else None
                             except ValueError:
                                 st = None
                             raise E.from_status(resp.status, st if isinstance(st, dict) else None)
                         continue
-                    ev = loads(line)
-                    yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+                    yield line
             finally:
                 await stream.aclose()
             return
@@ -253,7 +252,7 @@ class RestClient(KubeClient):
                 if resp.status >= 300:
                     raw = await resp.read()
                     try:
-                        st = loads(raw)
+                        st = json.loads(raw)
                     except ValueError:
                         st = None
                     raise E.from_status(resp.status, st if isinstance(st, dict) else None)
@@ -266,13 +265,20 @@ class RestClient(KubeClient):
                     buf = lines.pop()
                     for line in lines:
                         if line:
-                            ev = loads(line)
-                            yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+                            yield line
                 if buf.strip():
-                    ev = loads(buf)
-                    yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
+                    yield buf
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
             raise E.TransportError(f"watch {url}: {type(e).__name__}: {e}") from e
+
+    async def watch(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
+                    allow_bookmarks=True, label_selector=None) -> AsyncIterator[WatchEvent]:
+        loads = json.loads
+        async for line in self.watch_raw(rt, namespace, resource_version=resource_version,
+                                         timeout_seconds=timeout_seconds, allow_bookmarks=allow_bookmarks,
+                                         label_selector=label_selector):
+            ev = loads(line)
+            yield WatchEvent(ev.get("type", ""), ev.get("object") or {})
 
     async def close(self) -> None:
         if self._pool is not None:

@@ -50,6 +50,9 @@ class Shard:
         self.secret_lister = self.secret_informer.lister
         self.configmap_lister = self.configmap_informer.lister
         self.healthy = True  # flipped by the controller's per-shard circuit breaker
+        if assume_writes:
+            for inf in self.factory.informers():
+                inf.echo_fastpath = True
 
     # ---------------------------------------------------------------- lifecycle
     def start(self) -> None:

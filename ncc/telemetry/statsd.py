@@ -7,12 +7,13 @@ default `unix:///var/run/datadog/dsd.socket`, values.yaml:190-192), falling back
 `DD_AGENT_HOST`/`DD_DOGSTATSD_PORT`.  Unified-service tags come from `DD_SERVICE`,
 `DD_VERSION`, `DD_ENV` and origin detection from `DD_ENTITY_ID` (deployment.yaml:85-95).
 
-Sends are fire-and-forget datagrams on a non-blocking socket: a missing agent never slows
-the reconcile loop.  `MemoryMetrics` records values for tests; `MultiMetrics` fans out (e.g.
-to the optional Prometheus exporter).
+Sends are fire-and-forget datagrams on a non-blocking socket, aggregated client-side and
+flushed once a second: a missing agent never slows the reconcile loop.  `MemoryMetrics`
+records values for tests; `MultiMetrics` fans out (e.g. to the optional Prometheus exporter).
 """
 from __future__ import annotations
 
+import asyncio
 import os
 import socket
 import time
@@ -87,14 +88,28 @@ def _format_tags(tags: dict | None, constant: list[str]) -> str:
 
 
 class StatsdClient(Metrics):
-    def __init__(self, namespace: str, url: str | None = None, constant_tags: list[str] | None = None):
+    """DogStatsD over UDP/UDS with client-side aggregation, like datadog-go v5's default client.
+
+    Gauges keep the last value and counts are summed per (name, tags) within a flush interval;
+    histograms are buffered.  Everything goes out as newline-joined packets (≤ `max_packet` bytes)
+    from a loop timer, so a reconcile costs a dict update instead of a syscall."""
+
+    def __init__(self, namespace: str, url: str | None = None, constant_tags: list[str] | None = None,
+                 flush_interval: float = 1.0, max_packet: int = 1432, aggregate: bool = True):
         self.namespace = namespace.rstrip(".") + "." if namespace else ""
         self.url = url or default_url()
         self.constant_tags = list(constant_tags if constant_tags is not None else default_tags())
+        self.flush_interval = flush_interval
+        self.max_packet = max_packet
+        self.aggregate = aggregate
         self.sent = 0
         self.dropped = 0
         self._sock = None
         self._addr = None
+        self._gauges: dict = {}
+        self._counts: dict = {}
+        self._lines: list[str] = []
+        self._timer = None
         self._open()
 
     def _open(self) -> None:
@@ -126,20 +141,72 @@ class StatsdClient(Metrics):
         except OSError:
             self.dropped += 1
 
-    def _emit(self, name: str, value: float, kind: str, tags: dict | None, rate: float) -> None:
+    def _line(self, name: str, value: float, kind: str, tags, rate: float) -> str:
         sr = f"|@{rate}" if rate < 1.0 else ""
-        self._send(f"{self.namespace}{name}:{value:g}|{kind}{sr}{_format_tags(tags, self.constant_tags)}")
+        t = dict(tags) if tags and not isinstance(tags, dict) else tags
+        return f"{self.namespace}{name}:{value:g}|{kind}{sr}{_format_tags(t, self.constant_tags)}"
+
+    def _schedule(self) -> None:
+        if self._timer is not None:
+            return
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            return  # no running loop: buffered until flush()/close()
+        self._timer = loop.call_later(self.flush_interval, self.flush)
+
+    def flush(self) -> None:
+        self._timer = None
+        lines = self._lines
+        self._lines = []
+        for (name, tags), v in self._gauges.items():
+            lines.append(self._line(name, v, "g", tags, 1.0))
+        for (name, tags), v in self._counts.items():
+            lines.append(self._line(name, v, "c", tags, 1.0))
+        self._gauges.clear()
+        self._counts.clear()
+        buf: list[str] = []
+        size = 0
+        for ln in lines:
+            if buf and size + len(ln) + 1 > self.max_packet:
+                self._send("\n".join(buf))
+                buf, size = [], 0
+            buf.append(ln)
+            size += len(ln) + 1
+        if buf:
+            self._send("\n".join(buf))
+
+    @staticmethod
+    def _key(name, tags):
+        return name, (tuple(sorted(tags.items())) if tags else None)
 
     def gauge(self, name, value, tags=None, rate=1.0):
-        self._emit(name, value, "g", tags, rate)
+        if not self.aggregate:
+            self._send(self._line(name, value, "g", tags, rate))
+            return
+        self._gauges[self._key(name, tags)] = value
+        self._schedule()
 
     def count(self, name, value=1, tags=None, rate=1.0):
-        self._emit(name, value, "c", tags, rate)
+        if not self.aggregate:
+            self._send(self._line(name, value, "c", tags, rate))
+            return
+        k = self._key(name, tags)
+        self._counts[k] = self._counts.get(k, 0) + value
+        self._schedule()
 
     def histogram(self, name, value, tags=None, rate=1.0):
-        self._emit(name, value, "h", tags, rate)
+        if not self.aggregate:
+            self._send(self._line(name, value, "h", tags, rate))
+            return
+        self._lines.append(self._line(name, value, "h", tags, rate))
+        self._schedule()
 
     def close(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+        self.flush()
         if self._sock is not None:
             self._sock.close()
             self._sock = None

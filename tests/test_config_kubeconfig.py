@@ -173,7 +173,12 @@ def test_statsd_and_json_logging(capsys):
     rx.settimeout(2)
     c = StatsdClient("nexus_configuration_controller", f"udp://127.0.0.1:{rx.getsockname()[1]}", ["service:ncc"])
     c.gauge("workqueue_length", 3)
-    assert rx.recv(1024) == b"nexus_configuration_controller.workqueue_length:3|g|#service:ncc"
+    c.gauge("workqueue_length", 5)          # aggregated: last value wins within a flush interval
+    c.count("reconciles", 1, {"kind": "template"})
+    c.count("reconciles", 2, {"kind": "template"})
+    c.flush()
+    assert rx.recv(1024) == (b"nexus_configuration_controller.workqueue_length:5|g|#service:ncc\n"
+                             b"nexus_configuration_controller.reconciles:3|c|#service:ncc,kind:template")
     c.close()
     rx.close()
     import logging
