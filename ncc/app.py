@@ -48,7 +48,8 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
               failure_max_delay=cfg.failure_rate_max_delay, rate_limit_qps=float(cfg.rate_limit_elements_per_second),
               rate_limit_burst=cfg.rate_limit_elements_burst, resync_period=cfg.resync_period)
     if cfg.mode == "native":
-        kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout)
+        kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout,
+                  server_side_apply=cfg.server_side_apply)
     opts = ControllerOptions.for_mode(cfg.mode, **kw)
     # expert/ablation overrides: NCC_OPT_<FIELD>=value (e.g. NCC_OPT_COALESCE_WINDOW=0)
     for f, cur in opts.as_dict().items():

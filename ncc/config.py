@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `transport`, `executors`, `max-executors`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `executors`, `max-executors`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
 `metrics-bind-address`, `health-bind-address`, `log-format`.
 """
 from __future__ import annotations
@@ -79,6 +79,7 @@ class AppConfig:
     client_burst: int = 10
     client_pool_size: int = 64
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
+    server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     executors: int = -1              # shard-executor processes; -1 = auto (native: one per shard, ≤ max)
     max_executors: int = 16
     resync_period: float = _dur(30.0)

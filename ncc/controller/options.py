@@ -40,6 +40,7 @@ class ControllerOptions:
     full_resync_period: float = 0.0        # periodic enqueue-all sweep (native replaces informer resync)
     native_queue: bool | None = None       # None: use the C++ queue when built
     coalesce_window: float = 0.0           # seconds to park event-triggered keys so bursts collapse
+    server_side_apply: bool = False       # shard writes as SSA (PATCH apply-patch, force) instead of GET/PUT
     patch_writes: bool = False            # controller.go:434,476,663,686 PUT status/ownerRefs (409-prone)
     role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
 

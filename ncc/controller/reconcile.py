@@ -337,7 +337,11 @@ class ReconcileMixin:
         name = meta(template).get("name", "")
         spec = template.get("spec")
         shard_template = shard.template_lister.try_get(ns, name)
-        if shard_template is not None and not spec_matches(spec, shard_template):
+        if self.options.server_side_apply:
+            if shard_template is None or not spec_matches(spec, shard_template):
+                self._pass_wrote()
+                shard_template = await shard.apply_template(name, ns, spec, C.FIELD_MANAGER)
+        elif shard_template is not None and not spec_matches(spec, shard_template):
             log.debug("Content changed for NexusAlgorithmTemplate %s, updating", name)
             shard_template = await self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
                                                shard_template, spec, C.FIELD_MANAGER)
@@ -418,6 +422,18 @@ class ReconcileMixin:
             return e
 
         shard_obj = shard_lister.try_get(shard_ns, meta(src).get("name", ""))
+        if self.options.server_side_apply:
+            try:
+                if shard_obj is not None:
+                    missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind)  # rogue → error
+                    with_binary = self.options.sync_binary_data and not is_secret
+                    if not missing_owner and data_matches(src, shard_obj, with_binary):
+                        return
+                self._pass_wrote()
+                await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)
+            except Exception as e:  # noqa: BLE001
+                raise fail(e)
+            return
         if shard_obj is None:
             try:
                 shard_obj = await self._write(shard, "create_secret" if is_secret else "create_configmap",
@@ -557,7 +573,11 @@ class ReconcileMixin:
         name = meta(workgroup).get("name", "")
         spec = workgroup.get("spec")
         sw = shard.workgroup_lister.try_get(ns, name)
-        if sw is not None and not spec_matches(spec, sw):
+        if self.options.server_side_apply:
+            if sw is None or not spec_matches(spec, sw):
+                self._pass_wrote()
+                await shard.apply_workgroup(name, ns, spec, C.FIELD_MANAGER)
+        elif sw is not None and not spec_matches(spec, sw):
             await self._write(shard, "update_workgroup", shard.workgroup_informer, R.WORKGROUPS, sw, spec,
                               C.FIELD_MANAGER)
         elif sw is None:

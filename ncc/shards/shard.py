@@ -14,8 +14,8 @@ reference; the object shapes are pinned by the reference's test expectations:
 * `update_secret` / `update_configmap`     — X8f: replace `data` when given, append the owner ref
   when given, preserve everything else (controller_test.go:970-1006, 1085-1087).
 
-Native-mode additions: `assume_writes` publishes every write result into the informer's
-mutation overlay; `sync_binary_data` also carries `ConfigMap.binaryData`; deletes for
+Native-mode additions: `apply_*` server-side-apply variants of the writes; `assume_writes`
+publishes every write result into the informer's mutation overlay; `sync_binary_data` also carries `ConfigMap.binaryData`; deletes for
 workgroups and dependents support the orphan sweep.
 """
 from __future__ import annotations
@@ -25,7 +25,7 @@ from ..api import resources as R
 from ..api.objects import meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
-from ..kube.client import KubeClient
+from ..kube.client import PATCH_APPLY, KubeClient
 
 
 class Shard:
@@ -91,6 +91,18 @@ class Shard:
                                        field_manager=field_manager)
         return self._assume(self.template_informer, res)
 
+    async def apply_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
+        """Server-side apply (create-or-update in one request; no resourceVersion, no 409 races)."""
+        body = {
+            "apiVersion": C.API_VERSION,
+            "kind": C.TEMPLATE_KIND,
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
+            "spec": spec,
+        }
+        res = await self.client.patch(R.TEMPLATES, namespace, name, body, patch_type=PATCH_APPLY,
+                                      field_manager=field_manager, force=True)
+        return self._assume(self.template_informer, res)
+
     async def delete_template(self, obj: dict) -> None:
         m = meta(obj)
         await self.client.delete(R.TEMPLATES, m.get("namespace", ""), m.get("name", ""))
@@ -111,6 +123,17 @@ class Shard:
         obj["spec"] = spec
         res = await self.client.update(R.WORKGROUPS, meta(shard_obj).get("namespace", ""), obj,
                                        field_manager=field_manager)
+        return self._assume(self.workgroup_informer, res)
+
+    async def apply_workgroup(self, name: str, namespace: str, spec, field_manager: str) -> dict:
+        body = {
+            "apiVersion": C.API_VERSION,
+            "kind": C.WORKGROUP_KIND,
+            "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
+            "spec": spec,
+        }
+        res = await self.client.patch(R.WORKGROUPS, namespace, name, body, patch_type=PATCH_APPLY,
+                                      field_manager=field_manager, force=True)
         return self._assume(self.workgroup_informer, res)
 
     async def delete_workgroup(self, obj: dict) -> None:
@@ -180,6 +203,14 @@ class Shard:
         res = await self.client.update(R.CONFIGMAPS, meta(shard_configmap).get("namespace", ""), body,
                                        field_manager=field_manager)
         return self._assume(self.configmap_informer, res)
+
+    async def apply_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str) -> dict:
+        """Apply our view of a dependent: owner labels, our ownerRef (merged by uid with other owners'), payload."""
+        body = self._dependent_body(rt, shard_template, src)
+        m = body["metadata"]
+        res = await self.client.patch(rt, m["namespace"], m["name"], body, patch_type=PATCH_APPLY,
+                                      field_manager=field_manager, force=True)
+        return self._assume(self.secret_informer if rt is R.SECRETS else self.configmap_informer, res)
 
     async def delete_dependent(self, rt: R.ResourceType, obj: dict) -> None:
         m = meta(obj)

@@ -91,8 +91,9 @@ async def test_controller_main_propagates_create_and_update(tmp_path, mode):
         await env.stop()
 
 
-@pytest.mark.parametrize("mode,transport", [("compat", "fast"), ("native", "fast"), ("native", "aiohttp")])
-async def test_dependents_fan_out_and_delete(tmp_path, mode, transport):
+@pytest.mark.parametrize("mode,transport,ssa", [("compat", "fast", False), ("native", "fast", False),
+                                                ("native", "aiohttp", False), ("native", "fast", True)])
+async def test_dependents_fan_out_and_delete(tmp_path, mode, transport, ssa):
     env = await FakeEnvironment(2, str(tmp_path)).start()
     cc = env.controller_client()
     scs = [env.shard_client(i) for i in range(2)]
@@ -101,7 +102,7 @@ async def test_dependents_fan_out_and_delete(tmp_path, mode, transport):
         await cc.create(R.CONFIGMAPS, NS, make_configmap("c0", NS))
         await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=["c0"]))
         await cc.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
-        async with Running(env, mode, transport=transport):
+        async with Running(env, mode, transport=transport, server_side_apply=ssa):
             for sc in scs:
                 st = await wait_for(lambda sc=sc: _get(sc, R.TEMPLATES, "algo-00000"), timeout=3)
                 sec = await wait_for(lambda sc=sc: _get(sc, R.SECRETS, "s0"), timeout=3)

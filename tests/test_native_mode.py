@@ -235,3 +235,41 @@ async def test_coordinator_waits_for_all_shard_reports():
     assert any(e.startswith("Normal Synced") for e in env.recorder.events)
     # a report about an older incarnation (different UID) does not count
     assert ctl.shard_readiness(key, {"metadata": {"uid": "other", "generation": 1}}) is None
+
+
+async def test_server_side_apply_writes():
+    """`server_side_apply`: every shard write is one apply PATCH (no GET/PUT, no resourceVersion);
+    other owners' refs survive, drift is corrected, a rogue (unowned) object still blocks."""
+    env = Env(1, server_side_apply=True)
+    t = env.seed()
+    name = t["metadata"]["name"]
+    ctl = env.build()
+    other = env.sstates[0].create(R.TEMPLATES, NS, make_template(99, NS))
+    sec = make_secret("s", NS, version=42)
+    sec["metadata"]["ownerReferences"] = [{"apiVersion": C.API_VERSION, "kind": C.TEMPLATE_KIND,
+                                           "name": other["metadata"]["name"], "uid": other["metadata"]["uid"]}]
+    env.sstates[0].create(R.SECRETS, NS, sec)
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    writes = env.sclients[0].writes()
+    assert writes and all(a.verb == "patch" for a in writes)
+    live = env.sstates[0].get(R.SECRETS, NS, "s")
+    assert live["data"] == env.cstate.get(R.SECRETS, NS, "s")["data"]
+    assert len(live["metadata"]["ownerReferences"]) == 2
+    assert env.sstates[0].get(R.CONFIGMAPS, NS, "c")["metadata"]["labels"] == C.owner_labels(ALIAS)
+    assert env.cstate.get(R.TEMPLATES, NS, name)["status"]["syncedToClusters"] == ["s0"]
+    # spec drift on the shard is re-applied
+    st = env.sstates[0].get(R.TEMPLATES, NS, name)
+    st["spec"]["container"]["image"] = "drifted"
+    env.sstates[0].update(R.TEMPLATES, NS, st)
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    assert env.sstates[0].get(R.TEMPLATES, NS, name)["spec"] == env.cstate.get(R.TEMPLATES, NS, name)["spec"]
+    # a rogue configmap (no owner refs) is never overwritten
+    env.cstate.create(R.CONFIGMAPS, NS, make_configmap("rogue", NS))
+    env.sstates[0].create(R.CONFIGMAPS, NS, make_configmap("rogue", NS, version=7))
+    t2 = env.cstate.create(R.TEMPLATES, NS, make_template(5, NS, secrets=[], configmaps=["rogue"]))
+    env.refresh()
+    with pytest.raises(Exception):
+        await ctl.sync_template(NS, t2["metadata"]["name"])
+    assert env.sstates[0].get(R.CONFIGMAPS, NS, "rogue")["data"] != env.cstate.get(R.CONFIGMAPS, NS, "rogue")["data"]
