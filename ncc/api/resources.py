@@ -54,8 +54,9 @@ EVENTS = ResourceType("", "v1", "events", "Event")
 NAMESPACES = ResourceType("", "v1", "namespaces", "Namespace", namespaced=False)
 TEMPLATES = ResourceType(C.GROUP, C.VERSION, C.TEMPLATE_PLURAL, C.TEMPLATE_KIND, has_status=True)
 WORKGROUPS = ResourceType(C.GROUP, C.VERSION, C.WORKGROUP_PLURAL, C.WORKGROUP_KIND, has_status=True)
+LEASES = ResourceType("coordination.k8s.io", "v1", "leases", "Lease")  # leader election (ncc/leader.py)
 
-BUILTIN = (SECRETS, CONFIGMAPS, EVENTS, NAMESPACES, TEMPLATES, WORKGROUPS)
+BUILTIN = (SECRETS, CONFIGMAPS, EVENTS, NAMESPACES, TEMPLATES, WORKGROUPS, LEASES)
 
 _BY_KIND = {r.kind: r for r in BUILTIN}
 _BY_PLURAL = {(r.group, r.plural): r for r in BUILTIN}

@@ -34,6 +34,7 @@ from .controller.options import ControllerOptions
 from .kube.client import RateLimitedClient
 from .kube.kubeconfig import build_config
 from .kube.rest import RestClient
+from .leader import LeaderElector, identity_from_env
 from .shards.loader import default_client_factory, discover, load_shards
 from .telemetry.logging import configure_logging
 from .telemetry.statsd import MultiMetrics, StatsdClient
@@ -95,6 +96,9 @@ class App:
         self.metrics = metrics
         self.ops = None
         self.controller: Controller | None = None
+        self.elector: LeaderElector | None = None
+        self._lease_task = None
+        self.lost_leadership = False
 
     async def build(self) -> Controller:
         cfg, o = self.cfg, self.options
@@ -142,9 +146,15 @@ class App:
                                      shard_names=all_names if o.role == "coordinator" else None)
         if cfg.metrics_bind_address or cfg.health_bind_address:
             from .telemetry.http import OpsServer
-            self.ops = OpsServer(ready=lambda: self.controller is not None and self.controller.ready.is_set(),
+            self.ops = OpsServer(ready=self._ready,
                                  prometheus=prom, extra=self.debug_state)
         return self.controller
+
+    def _ready(self) -> bool:
+        """Ready once caches synced and workers run — or while standing by for the leader Lease."""
+        if self.elector is not None and not self.elector.leading:
+            return not self.lost_leadership
+        return self.controller is not None and self.controller.ready.is_set()
 
     def debug_state(self) -> dict:
         c = self.controller
@@ -152,6 +162,9 @@ class App:
         out["events"] = getattr(self.recorder, "stats", {})
         if self.pool is not None:
             out["executors"] = self.pool.stats()
+        if self.elector is not None:
+            out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
+                             "transitions": self.elector.transitions}
         return out
 
     async def run(self, stop: asyncio.Event) -> None:
@@ -163,6 +176,20 @@ class App:
             pass
         if self.ops is not None:
             await self.ops.start(self.cfg.health_bind_address or self.cfg.metrics_bind_address)
+        if self.cfg.leader_elect and self.options.role != "executor":
+            cfg = self.cfg
+            self.elector = LeaderElector(self.client, cfg.leader_election_namespace or cfg.controller_namespace,
+                                         cfg.leader_election_lease_name, identity_from_env(),
+                                         lease_duration=cfg.lease_duration, renew_deadline=cfg.renew_deadline,
+                                         retry_period=cfg.retry_period)
+            if not await self.elector.acquire(stop):
+                await self.close()
+                return
+
+            def lost():
+                self.lost_leadership = True
+                stop.set()
+            self._lease_task = asyncio.ensure_future(self.elector.hold(stop, on_lost=lost))
         for s in self.shards:
             s.start()
         if isinstance(self.recorder, BroadcastRecorder):
@@ -184,6 +211,9 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
+        if self._lease_task is not None:
+            self._lease_task.cancel()
+            await asyncio.gather(self._lease_task, return_exceptions=True)
         if self.pool is not None:
             await self.pool.stop()
         if isinstance(self.recorder, BroadcastRecorder):
@@ -193,6 +223,8 @@ class App:
         for s in self.shards:
             await s.stop()
         log.debug("shards stopped")
+        if self.elector is not None and self.elector.leading:
+            await self.elector.release()
         await self.client.close()
         if self.ops is not None:
             await self.ops.stop()
@@ -234,7 +266,7 @@ async def _amain(cfg: AppConfig) -> int:
         log.error("Error building controller: %s", e)
         return 1
     await app.run(stop)
-    return 0
+    return 1 if app.lost_leadership else 0
 
 
 def main(argv=None) -> int:

@@ -12,7 +12,8 @@ Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
 `client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `executors`, `max-executors`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
-`metrics-bind-address`, `health-bind-address`, `log-format`.
+`metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
+`leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
 from __future__ import annotations
 
@@ -88,6 +89,12 @@ class AppConfig:
     metrics_bind_address: str = ""   # e.g. ":9090" → Prometheus /metrics
     health_bind_address: str = ""    # e.g. ":8081" → /healthz, /readyz
     log_format: str = "json"
+    leader_elect: bool = False       # Lease-based leader election (run >1 replica; ncc/leader.py)
+    leader_election_namespace: str = ""   # default: controller-namespace
+    leader_election_lease_name: str = "nexus-configuration-controller"
+    lease_duration: float = _dur(15.0)
+    renew_deadline: float = _dur(10.0)
+    retry_period: float = _dur(2.0)
 
     @staticmethod
     def key_of(attr: str) -> str:

@@ -188,3 +188,16 @@ def test_statsd_and_json_logging(capsys):
     rec = json.loads(line)
     assert rec["msg"] == "hello" and rec["shard"] == "s0" and rec["level"] == "INFO"
     configure_logging("WARNING", "text")
+
+
+def test_helm_env_names_map_to_config_keys():
+    """Every NEXUS__* variable the chart sets must be a real AppConfig key (no silently ignored settings)."""
+    import re
+    from dataclasses import fields
+    from pathlib import Path
+    tpl = (Path(__file__).parent.parent / "deploy/helm/nexus-configuration-controller/templates/deployment.yaml"
+           ).read_text()
+    names = set(re.findall(r"name: (NEXUS__[A-Z_]+)", tpl))
+    known = {AppConfig.env_of(f.name) for f in fields(AppConfig)}
+    assert names and names <= known, names - known
+    assert {"NEXUS__LEADER_ELECT", "NEXUS__SERVER_SIDE_APPLY", "NEXUS__WORKERS"} <= names

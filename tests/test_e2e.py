@@ -174,3 +174,41 @@ async def test_native_repairs_shard_drift_and_workgroup_delete(tmp_path):
         await cc.close()
         await sc.close()
         await env.stop()
+
+
+async def test_leader_election_failover(tmp_path):
+    """Two replicas with `leader-elect`: only the Lease holder reconciles; the standby takes over when the
+    leader shuts down (released Lease → immediate) and keeps propagating."""
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    kw = dict(leader_elect=True, lease_duration=1.0, renew_deadline=0.6, retry_period=0.1)
+    apps = [App(env.app_config(mode="native", **kw)) for _ in range(2)]
+    stops = [asyncio.Event(), asyncio.Event()]
+    try:
+        await apps[0].build()
+        t0 = asyncio.ensure_future(apps[0].run(stops[0]))
+        await asyncio.wait_for(apps[0].controller.ready.wait(), 10)
+        await apps[1].build()
+        t1 = asyncio.ensure_future(apps[1].run(stops[1]))
+        await asyncio.sleep(0.5)
+        assert apps[0].elector.leading and not apps[1].elector.leading
+        assert not apps[1].controller.ready.is_set() and apps[1]._ready()
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS))
+        await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00000"), timeout=3)
+
+        stops[0].set()
+        await asyncio.wait_for(t0, 15)
+        await asyncio.wait_for(apps[1].controller.ready.wait(), 10)
+        assert apps[1].elector.leading
+        lease = await cc.get(R.LEASES, NS, "nexus-configuration-controller")
+        assert lease["spec"]["holderIdentity"] == apps[1].elector.identity
+        await cc.create(R.TEMPLATES, NS, make_template(1, NS))
+        await wait_for(lambda: _get(sc, R.TEMPLATES, "algo-00001"), timeout=3)
+        stops[1].set()
+        await asyncio.wait_for(t1, 15)
+    finally:
+        for s in stops:
+            s.set()
+        await cc.close()
+        await sc.close()
+        await env.stop()
