@@ -116,15 +116,23 @@ class Dist:
 
 # ------------------------------------------------------------------ workload
 def wave_objects(T: int, version: int, payload: int) -> list:
+    """One wave: per template its Secret, its ConfigMap, then the template itself (dependencies first,
+    as a user rolling out a new config version would)."""
     from ncc.testing.workload import configmap_name, make_configmap, make_secret, make_template, secret_name
     items = []
     for i in range(T):
+        items.append(make_secret(secret_name(i), NS, payload=payload, version=version))
+        items.append(make_configmap(configmap_name(i), NS, payload=payload, version=version))
         items.append(make_template(i, NS, secrets=[secret_name(i)], configmaps=[configmap_name(i)],
                                    version=f"v{version}"))
-        s = make_secret(secret_name(i), NS, payload=payload, version=version)
-        items.append(s)
-        items.append(make_configmap(configmap_name(i), NS, payload=payload, version=version))
     return items
+
+
+def wave_body(T: int, version: int, payload: int) -> bytes:
+    """Pre-encoded /_fake/apply request (generated before the timed region: the load generator's own
+    work is not part of the system under test).  The server commits in slices of 100 objects and lets
+    watches flush in between, like a real apiserver under many concurrent writers."""
+    return json.dumps({"items": wave_objects(T, version, payload), "yield_every": 100}).encode()
 
 
 def want(T: int, version: int) -> list:
@@ -135,10 +143,29 @@ def want(T: int, version: int) -> list:
 
 async def post(session, url, body, timeout=None):
     import aiohttp
-    async with session.post(url, data=json.dumps(body), headers={"Content-Type": "application/json"},
+    data = body if isinstance(body, bytes) else json.dumps(body)
+    async with session.post(url, data=data, headers={"Content-Type": "application/json"},
                             timeout=aiohttp.ClientTimeout(total=timeout)) as r:
         r.raise_for_status()
         return await r.json()
+
+
+def cpu_seconds(named: dict) -> dict:
+    """user+sys CPU seconds per named process; `controller` also reports its executor children."""
+    import psutil
+    out = {}
+    for name, proc in named.items():
+        if proc is None:
+            continue
+        try:
+            p = psutil.Process(proc.pid)
+            t = p.cpu_times()
+            out[name] = t.user + t.system
+            if name == "coordinator":
+                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in p.children(recursive=True))
+        except (psutil.Error, OSError):
+            pass
+    return out
 
 
 def pct(xs, q):
@@ -168,7 +195,7 @@ async def run(args, d: Dist) -> dict | None:
         T = args.templates
         if d.rank == 0:
             cpf = os.path.join(work, "controller.url")
-            procs.append(spawn_fakeapi("controller", cpf))
+            procs.append(spawn_fakeapi("controller", cpf, extra=extra))
             ctrl_url = wait_port_file(cpf, procs[-1])
             shard_dir = os.path.join(work, "shards")
             os.makedirs(shard_dir)
@@ -199,10 +226,18 @@ async def run(args, d: Dist) -> dict | None:
                                               stderr=subprocess.STDOUT, cwd=work)
                 procs.append(controller)
             t_boot = d.broadcast(t_boot if d.rank == 0 else None)
+            named = {"shard-apiserver": procs[0]}
+            if d.rank == 0:
+                named.update({"controller-apiserver": procs[1], "coordinator": controller})
 
-            async def converge(version: int, times: bool):
-                r = await post(session, f"{my_url}/_fake/markers/wait",
-                               {"want": want(T, version), "timeout": args.timeout, "times": times},
+            total = args.warmup + args.steps
+            bodies = {}
+            if d.rank == 0:
+                bodies = {v: wave_body(T, v, args.payload) for v in range(1, total + 1)}
+
+            async def converge(version: int, times: bool, url=my_url):
+                r = await post(session, f"{url}/_fake/markers/wait",
+                               {"want": want(T, version), "timeout": args.timeout, "times": times, "keyed": True},
                                timeout=args.timeout + 30)
                 if not r["ok"]:
                     tail = ""
@@ -215,35 +250,52 @@ async def run(args, d: Dist) -> dict | None:
             # ---- cold start (warm-up 0): boot + full fan-out of pre-seeded objects
             r = await converge(0, True)
             d.barrier()
-            cold_local = max(max(v) for v in r["times"].values()) - t_boot
+            cold_local = max(max(v.values()) for v in r["times"].values()) - t_boot
             cold = d.max(cold_local / 1e9)
 
-            lat_ms: list[float] = []
+            shard_times: list[dict] = []  # per timed wave: {"plural=value": {"ns/name": t_ns}}
+            ctrl_times: list[dict] = []
             t_start = None
-            total = args.warmup + args.steps
             for step in range(1, total + 1):
                 timed = step > args.warmup
                 if step == args.warmup + 1:
                     d.sync()
                     t_start = time.perf_counter()
+                    cpu0 = cpu_seconds(named)
                 t0 = None
                 if d.rank == 0:
-                    a = await post(session, f"{ctrl_url}/_fake/apply",
-                                   {"items": wave_objects(T, step, args.payload)})
-                    t0 = a["t1_ns"]
+                    a = await post(session, f"{ctrl_url}/_fake/apply", bodies.pop(step))
+                    t0 = a["t0_ns"]
+                    if os.environ.get("NCC_BENCH_DEBUG"):
+                        print(f"# wave {step}: apply {(a['t1_ns'] - a['t0_ns']) / 1e6:.1f} ms", file=sys.stderr)
                 t0 = d.broadcast(t0)
                 r = await converge(step, timed)
+                if os.environ.get("NCC_BENCH_DEBUG"):
+                    for plural, ts in r.get("times", {}).items():
+                        ts = sorted(ts.values())
+                        print(f"# wave {step} rank {d.rank} {plural}: first {(ts[0] - t0) / 1e6:.1f} "
+                              f"p50 {(ts[len(ts) // 2] - t0) / 1e6:.1f} last {(ts[-1] - t0) / 1e6:.1f} ms",
+                              file=sys.stderr)
                 d.barrier()  # the wave is done only when every shard has converged
                 if timed:
-                    for ts in r["times"].values():
-                        lat_ms.extend((t - t0) / 1e6 for t in ts)
+                    shard_times.append(r["times"])
+                    if d.rank == 0:  # controller-side commit times of the same objects (already there)
+                        ctrl_times.append((await converge(step, True, ctrl_url))["times"])
             d.sync()
             elapsed = time.perf_counter() - t_start
+            cpu1 = cpu_seconds(named)
+            util = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 3) for k in cpu1}
+            utils = d.all_gather(util)
             elapsed = d.max(elapsed)
-            all_lat = d.all_gather(lat_ms)
+            all_times = d.all_gather(shard_times)
             if d.rank != 0:
                 return None
-            lat = [x for part in all_lat for x in part]
+            lat = []  # per object and shard: shard commit − controller commit of the same version
+            for per_rank in all_times:
+                for wave, ctrl in zip(per_rank, ctrl_times):
+                    for marker, objs in wave.items():
+                        c = ctrl[marker]
+                        lat.extend((t - c[k]) / 1e6 for k, t in objs.items())
             objs = args.steps * 3 * T * d.world
             value = objs / elapsed
             ctrl_alive = controller.poll() is None
@@ -268,6 +320,9 @@ async def run(args, d: Dist) -> dict | None:
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
+                # busy CPU cores per process over the timed steps (rank 0's, plus the busiest shard server)
+                "cpu_cores_busy": dict(utils[0], **{"shard-apiserver-max": max(u.get("shard-apiserver", 0.0)
+                                                                                 for u in utils)}),
             }
     finally:
         for p in reversed(procs):

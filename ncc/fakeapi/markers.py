@@ -77,8 +77,10 @@ class MarkerTracker:
         except asyncio.TimeoutError:
             return False
 
-    def times(self, plural: str, value) -> list[int]:
-        return list(self.first_seen.get((plural, str(value)), {}).values())
+    def times(self, plural: str, value, keyed: bool = False):
+        """Commit times of objects that reached `value`: a list, or {"ns/name": t_ns} when keyed."""
+        b = self.first_seen.get((plural, str(value)), {})
+        return dict(b) if keyed else list(b.values())
 
     def counts(self) -> dict:
         return {f"{p}={v}": len(b) for (p, v), b in self.first_seen.items()}

@@ -345,14 +345,20 @@ class FakeApiServer:
             out = {"ok": ok, "counts": {f"{w['plural']}={w['value']}": len(self.markers.times(w["plural"], w["value"]))
                                         for w in want}}
             if body.get("times"):
-                out["times"] = {f"{w['plural']}={w['value']}": self.markers.times(w["plural"], w["value"])
+                keyed = bool(body.get("keyed"))
+                out["times"] = {f"{w['plural']}={w['value']}": self.markers.times(w["plural"], w["value"], keyed)
                                 for w in want}
             return self._json(out)
         if what == "apply" and request.method == "POST":
             body = await self._body(request)
             t0 = time.time_ns()
             n = 0
+            # yield_every > 0 lets watch streams flush while a large apply is in progress (commits and
+            # watch delivery interleave, as on a real apiserver serving many concurrent writers)
+            yield_every = int(body.get("yield_every") or 0)
             for o in body.get("items") or []:
+                if yield_every and n and n % yield_every == 0:
+                    await asyncio.sleep(0)
                 rt = R.by_kind(o["kind"])
                 m = o.get("metadata") or {}
                 ns = m.get("namespace", "")
