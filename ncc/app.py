@@ -77,6 +77,22 @@ def client_limits(cfg: AppConfig) -> tuple[float, int]:
     return 0.0, cfg.client_burst
 
 
+def cpu_share() -> int:
+    """CPUs this process may run on (cgroup cpuset aware, unlike os.cpu_count())."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover - non-Linux
+        return os.cpu_count() or 1
+
+
+def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
+    """Two key-partitioned executors per shard group when there are ≥ 6 CPUs per group (measured on
+    MI355X hosts: +48% objects/s at one shard; a third executor adds no throughput because every
+    executor decodes the full watch streams), else one."""
+    cpus = cpu_share() if cpus is None else cpus
+    return 2 if cpus >= 6 * max(1, groups) else 1
+
+
 class App:
     """Wires and owns every component of one controller process."""
 
@@ -89,6 +105,7 @@ class App:
         self.shard_filter = shard_filter
         self.pool: ExecutorPool | None = None
         self.n_executors = 0
+        self.per_shard = 1
         qps, burst = client_limits(cfg)
         self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size,
                                                                        cfg.transport)
@@ -126,6 +143,8 @@ class App:
             self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
             if self.n_executors > 0:
                 o.role = "coordinator"
+                self.per_shard = (cfg.executors_per_shard if cfg.executors_per_shard > 0
+                                  else auto_executors_per_shard(self.n_executors))
         if o.role == "coordinator":
             self.shards = []
         else:
@@ -199,11 +218,12 @@ class App:
             env = dict(os.environ)
             env.update(config_to_env(self.cfg))
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
-                                     env=env)
+                                     env=env, per_shard=self.per_shard)
             self.pool.start()
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
-                 "executors=%d workers=%d", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
-                 self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.options.workers)
+                 "executors=%d×%d workers=%d", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
+                 self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
+                 self.options.workers)
         try:
             await controller.run(stop)
         finally:

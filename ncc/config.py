@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `executors`, `max-executors`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -83,6 +83,7 @@ class AppConfig:
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     executors: int = -1              # shard-executor processes; -1 = auto (native: one per shard, ≤ max)
     max_executors: int = 16
+    executors_per_shard: int = -1    # key-partitioned executors per shard group; -1 = auto (app.py)
     resync_period: float = _dur(30.0)
     full_resync_period: float = _dur(600.0)
     shard_sync_timeout: float = _dur(10.0)

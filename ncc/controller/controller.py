@@ -26,6 +26,7 @@ from ..cache.informer import DeletedFinalStateUnknown, Informer
 from ..telemetry.statsd import Metrics, NullMetrics
 from ..workqueue.queue import WorkQueue
 from .events import EventRecorder, FakeRecorder
+from .executor import key_part
 from .options import ControllerOptions
 from .reconcile import ReconcileMixin, spec_matches, data_matches
 
@@ -151,6 +152,9 @@ class Controller(ReconcileMixin):
     def _enqueue_key(self, key: str) -> None:
         """Event-driven enqueue; native mode coalesces bursts (a template and its Secret/ConfigMap
         changing together) into one reconcile by parking the key for `coalesce_window` seconds."""
+        part = self.options.partition
+        if part is not None and key_part(key, part[1]) != part[0]:
+            return  # another executor of this shard group owns the key
         w = self.options.coalesce_window
         if w > 0:
             self.queue.add_after(key, w)

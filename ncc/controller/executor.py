@@ -23,6 +23,7 @@ import logging
 import os
 import socket
 import sys
+import zlib
 
 from .ipc import Channel
 from ..aio import wait_timeout
@@ -39,10 +40,19 @@ def partition(names: list[str], n: int) -> list[list[str]]:
     return parts
 
 
+def key_part(key: str, parts: int) -> int:
+    """Stable key → partition (crc32 of "ns/name"; a template's and its delete's keys agree)."""
+    _, _, nsname = key.partition("/")
+    return zlib.crc32(nsname.encode()) % parts
+
+
 class ExecutorHandle:
-    def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None):
+    def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None,
+                 part: int = 0, parts: int = 1):
         self.index = index
         self.shards = shards
+        self.part = part
+        self.parts = parts
         self.on_message = on_message
         self.env = env
         self.proc: asyncio.subprocess.Process | None = None
@@ -59,7 +69,8 @@ class ExecutorHandle:
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
         self.proc = await asyncio.create_subprocess_exec(
             sys.executable, "-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
-            "--shards", ",".join(self.shards), pass_fds=(child.fileno(),), env=env)
+            "--shards", ",".join(self.shards), "--part", f"{self.part}/{self.parts}",
+            pass_fds=(child.fileno(),), env=env)
         child.close()
         reader, writer = await asyncio.open_connection(sock=parent)
         self.channel = Channel(reader, writer)
@@ -110,8 +121,13 @@ class ExecutorHandle:
 
 
 class ExecutorPool:
-    def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None):
-        self.handles = [ExecutorHandle(i, part, on_message, env) for i, part in enumerate(partition(shard_names, n))]
+    """`n` shard groups × `per_shard` key partitions.  Every executor of a group watches the same shards;
+    each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
+
+    def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1):
+        per_shard = max(1, per_shard)
+        self.handles = [ExecutorHandle(g * per_shard + p, group, on_message, env, p, per_shard)
+                        for g, group in enumerate(partition(shard_names, n)) for p in range(per_shard)]
 
     def start(self) -> None:
         for h in self.handles:
@@ -128,12 +144,12 @@ class ExecutorPool:
         await asyncio.gather(*(h.stop() for h in self.handles))
 
     def stats(self) -> dict:
-        return {h.index: {"shards": h.shards, "restarts": h.restarts,
+        return {h.index: {"shards": h.shards, "part": f"{h.part}/{h.parts}", "restarts": h.restarts,
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
 
 
 # ---------------------------------------------------------------------------------------- executor side
-async def executor_main(fd: int, index: int, shards: list[str]) -> int:
+async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0, 1)) -> int:
     from ..app import App, setup_signal_handler
     from ..config import load_config
 
@@ -144,6 +160,8 @@ async def executor_main(fd: int, index: int, shards: list[str]) -> int:
     stop = asyncio.Event()
     setup_signal_handler(stop)
     app = App(cfg, role="executor", shard_filter=set(shards))
+    if part[1] > 1:
+        app.options.partition = part
     await app.build()
     ctl = app.controller
     ctl.reporter = channel.send
@@ -179,7 +197,10 @@ def main(argv=None) -> int:
     p.add_argument("--fd", type=int, required=True)
     p.add_argument("--index", type=int, default=0)
     p.add_argument("--shards", default="")
+    p.add_argument("--part", default="0/1", help="key partition p/k of this executor within its shard group")
     a = p.parse_args(argv)
+    pi, _, pk = a.part.partition("/")
+    part = (int(pi), int(pk or 1))
     cfg = load_config()
     configure_logging(cfg.log_level, cfg.log_format)
     logging.getLogger().handlers[0].addFilter(lambda r: setattr(r, "executor", a.index) or True)
@@ -189,8 +210,8 @@ def main(argv=None) -> int:
         prof = cProfile.Profile()
         prof.enable()
         try:
-            return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s]))
+            return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s], part))
         finally:
             prof.disable()
             prof.dump_stats(f"{prof_path}.executor{a.index}")
-    return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s]))
+    return asyncio.run(executor_main(a.fd, a.index, [s for s in a.shards.split(",") if s], part))

@@ -43,6 +43,7 @@ class ControllerOptions:
     server_side_apply: bool = False       # shard writes as SSA (PATCH apply-patch, force) instead of GET/PUT
     patch_writes: bool = False            # controller.go:434,476,663,686 PUT status/ownerRefs (409-prone)
     role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
+    partition: tuple | None = None         # executor: (p, k) → reconcile only keys with key_part(key, k) == p
 
     @classmethod
     def compat(cls, **kw) -> "ControllerOptions":

@@ -212,3 +212,36 @@ async def test_leader_election_failover(tmp_path):
         await cc.close()
         await sc.close()
         await env.stop()
+
+
+async def test_partitioned_executors_per_shard(tmp_path):
+    """`executors-per-shard: 2`: two key-partitioned executors serve each shard; every template is synced
+    exactly by its partition's owner and the coordinator still reports Ready for all."""
+    from ncc.controller.executor import key_part
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc = env.controller_client()
+    scs = [env.shard_client(i) for i in range(2)]
+    try:
+        T = 12
+        for i in range(T):
+            await cc.create(R.SECRETS, NS, make_secret(f"s{i}", NS))
+            await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[]))
+        parts = {key_part(f"template/{NS}/algo-{i:05d}", 2) for i in range(T)}
+        assert parts == {0, 1}  # the workload really exercises both partitions
+        async with Running(env, "native", executors_per_shard=2) as app:
+            assert len(app.pool.handles) == 4
+
+            async def all_ready():
+                items = (await cc.list(R.TEMPLATES, NS))["items"]
+                return len(items) == T and all(
+                    (o.get("status") or {}).get("syncedToClusters") == ["shard-0", "shard-1"] and
+                    o["status"]["conditions"][0]["status"] == "True" for o in items)
+            await wait_for(all_ready, timeout=10)
+            for sc in scs:
+                assert len((await sc.list(R.TEMPLATES, NS))["items"]) == T
+                assert len((await sc.list(R.SECRETS, NS))["items"]) == T
+    finally:
+        await cc.close()
+        for sc in scs:
+            await sc.close()
+        await env.stop()
