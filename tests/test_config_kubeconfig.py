@@ -201,3 +201,13 @@ def test_helm_env_names_map_to_config_keys():
     known = {AppConfig.env_of(f.name) for f in fields(AppConfig)}
     assert names and names <= known, names - known
     assert {"NEXUS__LEADER_ELECT", "NEXUS__SERVER_SIDE_APPLY", "NEXUS__WORKERS"} <= names
+
+
+def test_cpu_share_reads_cgroup_quota(tmp_path):
+    from ncc.app import auto_executors_per_shard, cgroup_cpu_quota
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert cgroup_cpu_quota(str(tmp_path)) == 16.0
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert cgroup_cpu_quota(str(tmp_path)) is None
+    assert auto_executors_per_shard(1, cpus=16) == 2 and auto_executors_per_shard(4, cpus=16) == 2 and auto_executors_per_shard(8, cpus=16) == 1
+    assert auto_executors_per_shard(8, cpus=128) == 2
