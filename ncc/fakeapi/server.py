@@ -184,7 +184,7 @@ class FakeApiServer:
                 return self._json(self.state.get(rt, ns or "", name))
             body = await self._body(request) if m != "DELETE" or request.can_read_body else None
             if m == "POST" and name is None:
-                return self._json(self.state.create(rt, ns or "", body), 201)
+                return self._written(self.state.create(rt, ns or "", body, owned=True), 201)
             if m == "PUT" and name is not None:
                 if (body.get("metadata") or {}).get("name") not in (None, name):
                     raise E.BadRequest("the name of the object does not match the name on the URL")
@@ -193,12 +193,12 @@ class FakeApiServer:
                     raise E.NotFound(f"subresource {sub} not found")
                 if sub == "status" and not rt.has_status:
                     raise E.NotFound(f"{rt.plural} has no status subresource")
-                return self._json(self.state.update(rt, ns or "", body, subresource=sub))
+                return self._written(self.state.update(rt, ns or "", body, subresource=sub, owned=True))
             if m == "PATCH" and name is not None:
                 ctype = request.content_type
                 if ctype not in (PATCH_MERGE, PATCH_STRATEGIC, PATCH_JSON, PATCH_APPLY):
                     raise E.ApiError(f"unsupported patch type {ctype}", code=415, reason="UnsupportedMediaType")
-                return self._json(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
+                return self._written(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
             if m == "DELETE" and name is not None:
                 opts = body or {}
                 return self._json(self.state.delete(rt, ns or "", name, preconditions=opts.get("preconditions"),
@@ -225,6 +225,11 @@ class FakeApiServer:
     @staticmethod
     def _json(obj, status: int = 200) -> web.Response:
         return web.Response(status=status, body=_dumps(obj), content_type=_JSON)
+
+    def _written(self, obj, status: int = 200) -> web.Response:
+        """Write response; reuses the watch event's encoding of the same object when there is one."""
+        body = self.state.encoded(obj)
+        return web.Response(status=status, body=body if body is not None else _dumps(obj), content_type=_JSON)
 
     # ------------------------------------------------------------------ discovery
     def _discovery(self, target: str) -> web.Response:
@@ -367,7 +372,7 @@ class FakeApiServer:
                 except E.NotFound:
                     cur = None
                 if cur is None:
-                    self.state.create(rt, ns, o)
+                    self.state.create(rt, ns, o, owned=True)
                 else:
                     new = dict(cur)
                     for k, v in o.items():
@@ -377,7 +382,7 @@ class FakeApiServer:
                     for mk in ("labels", "annotations"):
                         if mk in m:
                             new["metadata"][mk] = m[mk]
-                    self.state.update(rt, ns, new)
+                    self.state.update(rt, ns, new, owned=True)
                 n += 1
             return self._json({"applied": n, "t0_ns": t0, "t1_ns": time.time_ns(), "rv": self.state.rv})
         if what == "objects" and request.method == "POST":
@@ -449,6 +454,17 @@ def main(argv=None) -> None:
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
     p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")
     args = p.parse_args(argv)
+    prof_path = os.environ.get("NCC_FAKEAPI_PROFILE")
+    if prof_path:  # NCC_FAKEAPI_PROFILE=/path/prefix → /path/prefix.<name>
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            asyncio.run(serve(args))
+        finally:
+            prof.disable()
+            prof.dump_stats(f"{prof_path}.{args.name}")
+        return
     asyncio.run(serve(args))
 
 

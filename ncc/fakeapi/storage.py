@@ -40,16 +40,23 @@ RtKey = tuple  # (group, plural)
 
 
 class EventRecord:
-    __slots__ = ("rv", "rt_key", "namespace", "type", "obj", "_line")
+    __slots__ = ("rv", "rt_key", "namespace", "type", "obj", "_line", "_body")
 
     def __init__(self, rv: int, rt_key: RtKey, namespace: str, type_: str, obj: dict):
         self.rv, self.rt_key, self.namespace, self.type, self.obj = rv, rt_key, namespace, type_, obj
         self._line = None
+        self._body = None
+
+    def body(self) -> bytes:
+        """The object's JSON, encoded once for the write response and every watch line."""
+        if self._body is None:
+            self._body = json.dumps(self.obj, separators=(",", ":")).encode()
+        return self._body
 
     def line(self) -> bytes:
         """Serialised watch-stream line, computed once and shared by every watcher."""
         if self._line is None:
-            self._line = json.dumps({"type": self.type, "object": self.obj}, separators=(",", ":")).encode() + b"\n"
+            self._line = b'{"type":"' + self.type.encode() + b'","object":' + self.body() + b"}\n"
         return self._line
 
 
@@ -107,6 +114,7 @@ class ClusterState:
         self._uids: dict[str, tuple] = {}  # uid -> (rt_key, ns, name)
         self._dependents: dict[str, set] = {}  # owner uid -> {(rt_key, ns, name)}
         self.write_hooks: list[Callable[[str, ResourceType, dict], None]] = []
+        self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
 
@@ -134,6 +142,7 @@ class ClusterState:
 
     def _emit(self, rv: int, rt: ResourceType, ns: str, type_: str, obj: dict) -> None:
         rec = EventRecord(rv, (rt.group, rt.plural), ns, type_, obj)
+        self.last_record = rec
         if not self.simple:
             self._history.append(rec)
         for w in tuple(self._watchers):
@@ -209,8 +218,15 @@ class ClusterState:
         return {"apiVersion": rt.api_version, "kind": rt.list_kind, "metadata": lmeta, "items": items}
 
     # ------------------------------------------------------------------ writes
-    def create(self, rt: ResourceType, ns: str, obj: dict) -> dict:
-        obj = deep_copy(obj)
+    def encoded(self, obj: dict) -> bytes | None:
+        """JSON of `obj` if it is the object of the latest write event (already encoded once)."""
+        rec = self.last_record
+        return rec.body() if rec is not None and rec.obj is obj else None
+
+    def create(self, rt: ResourceType, ns: str, obj: dict, *, owned: bool = False) -> dict:
+        """`owned=True`: the caller hands over `obj` (e.g. freshly decoded from a request) — no copy."""
+        if not owned:
+            obj = deep_copy(obj)
         m = obj.setdefault("metadata", {})
         ns = ns if rt.namespaced else ""
         if rt.namespaced:
@@ -246,7 +262,8 @@ class ClusterState:
         self._emit(self.rv, rt, ns, "ADDED", obj)
         return obj
 
-    def update(self, rt: ResourceType, ns: str, obj: dict, *, subresource: str | None = None) -> dict:
+    def update(self, rt: ResourceType, ns: str, obj: dict, *, subresource: str | None = None,
+               owned: bool = False) -> dict:
         ns = ns if rt.namespaced else ""
         m_in = obj.get("metadata") or {}
         name = m_in.get("name", "")
@@ -255,7 +272,7 @@ class ClusterState:
         if cur is None:
             raise _not_found(rt, name)
         if self.simple:
-            new = deep_copy(obj)
+            new = obj if owned else deep_copy(obj)
             b[name] = new
             self.stats["status" if subresource == "status" else "update"] += 1
             self._emit(self.rv, rt, ns, "MODIFIED", new)
@@ -273,7 +290,7 @@ class ClusterState:
                 new.pop("status", None)
             new["metadata"] = dict(cm)
         else:
-            new = deep_copy(obj)
+            new = obj if owned else deep_copy(obj)
             nm = new.setdefault("metadata", {})
             for k in ("uid", "creationTimestamp", "namespace", "name", "generation", "deletionTimestamp"):
                 if k in cm:
