@@ -29,7 +29,7 @@ from .cache.informer import InformerFactory
 from .config import AppConfig, config_to_env, load_config
 from .controller.controller import Controller
 from .controller.events import BroadcastRecorder, FakeRecorder
-from .controller.executor import ExecutorPool
+from .controller.executor import ExecutorPool, partition_filter
 from .controller.options import ControllerOptions
 from .kube.client import RateLimitedClient
 from .kube.kubeconfig import build_config
@@ -159,7 +159,9 @@ class App:
                 client = RateLimitedClient(client, qps, burst)
         self.client = client
         self.factory = InformerFactory(client, cfg.controller_namespace, o.resync_period)
-        infs = {rt: self.factory.informer(rt) for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
+        kf = partition_filter(*o.partition) if o.partition is not None else None
+        infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
+                for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
         all_names = [n for n, _ in discover(cfg.shard_config_path)]
         if o.role == "all" and o.mode == "native" and all_names:
             n = cfg.executors if cfg.executors >= 0 else len(all_names)
@@ -175,7 +177,8 @@ class App:
                                       client_factory=self.client_factory,
                                       resync_period=0.0 if o.watch_shards else o.resync_period,
                                       assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
-                                      slim=o.slim_shard_cache, start=False, names=self.shard_filter)
+                                      slim=o.slim_shard_cache, start=False, names=self.shard_filter,
+                                      key_filter=kf)
         if o.role == "executor":
             self.recorder = FakeRecorder(keep=False)  # executors never write to the controller cluster
         else:

@@ -66,6 +66,9 @@ class Lister:
         return self.store.list(namespace)
 
 
+_OBJECT_EVENTS = frozenset(("ADDED", "MODIFIED", "DELETED"))
+
+
 @dataclass
 class _Handler:
     on_add: Callable | None
@@ -85,8 +88,12 @@ class Informer:
     def __init__(self, client: KubeClient, rt: ResourceType, namespace: str | None, *,
                  resync_period: float = 0.0, transform: Callable[[dict], dict] | None = None,
                  label_selector: str | None = None, page_size: int = 500, watch_timeout: tuple = (300, 600),
-                 name: str = ""):
+                 name: str = "", key_filter: Callable[[str, str], bool] | None = None):
         self.client = client
+        # key_filter(ns, name) → False drops the object before it is decoded/stored (a partitioned
+        # executor skips the other partitions' templates straight off the wire via the native scanner)
+        self.key_filter = key_filter
+        self.filtered = 0
         self.rt = rt
         self.namespace = namespace
         self.resync_period = resync_period
@@ -169,6 +176,11 @@ class Informer:
             token = lm.get("continue")
             if not token:
                 break
+        kf = self.key_filter
+        if kf is not None:
+            dflt = self.namespace or ""
+            items = [o for o in items if kf((o.get("metadata") or {}).get("namespace") or dflt,
+                                            (o.get("metadata") or {}).get("name", ""))]
         added, updated, deleted = self.store.replace(items)
         self.relists += 1
         synced_before = self.has_synced()
@@ -188,7 +200,8 @@ class Informer:
         kw = dict(resource_version=rv, timeout_seconds=random.randint(lo, hi), allow_bookmarks=True,
                   label_selector=self.label_selector)
         scan = None
-        if self.echo_fastpath and hasattr(self.client, "watch_raw"):
+        kf = self.key_filter
+        if (self.echo_fastpath or kf is not None) and hasattr(self.client, "watch_raw"):
             mod = _native.load()
             scan = mod.scan_event if mod is not None else None
         if scan is not None:
@@ -196,8 +209,16 @@ class Informer:
             store = self.store
             default_ns = self.namespace or ""
             async for line in self.client.watch_raw(self.rt, self.namespace, **kw):
-                if store._assumed:
+                sc = None
+                if kf is not None:
                     sc = scan(line)
+                    if sc is not None and sc[0] in _OBJECT_EVENTS and not kf(sc[1] or default_ns, sc[2]):
+                        rv = self.last_rv = sc[3]
+                        self.filtered += 1
+                        continue
+                if store._assumed:
+                    if sc is None:
+                        sc = scan(line)
                     if sc is not None and sc[0] in ("ADDED", "MODIFIED") and \
                             store.confirm(ObjectKey(sc[1] or default_ns, sc[2]), sc[3]) is not None:
                         rv = self.last_rv = sc[3]
@@ -220,6 +241,13 @@ class Informer:
         new_rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
         if t == "BOOKMARK":
             return new_rv
+        kf = self.key_filter
+        if kf is not None:
+            m = obj.get("metadata") or {}
+            if not kf(m.get("namespace") or self.namespace or "", m.get("name", "")):
+                self.filtered += 1
+                self.last_rv = new_rv
+                return new_rv
         self.events += 1
         if t in ("ADDED", "MODIFIED"):
             stored, old = self.store.upsert(obj)

@@ -46,6 +46,12 @@ def key_part(key: str, parts: int) -> int:
     return zlib.crc32(nsname.encode()) % parts
 
 
+def partition_filter(part: int, parts: int):
+    """Informer key filter for partition `part` of `parts` (agrees with `key_part`)."""
+    crc = zlib.crc32
+    return lambda ns, name: crc(f"{ns}/{name}".encode()) % parts == part
+
+
 class ExecutorHandle:
     def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None,
                  part: int = 0, parts: int = 1):

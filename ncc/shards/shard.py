@@ -31,7 +31,7 @@ from ..kube.client import PATCH_APPLY, KubeClient
 class Shard:
     def __init__(self, owner_alias: str, name: str, client: KubeClient, namespace: str, *,
                  resync_period: float = 0.0, assume_writes: bool = False, sync_binary_data: bool = False,
-                 transforms: dict | None = None, informer_kw: dict | None = None):
+                 transforms: dict | None = None, informer_kw: dict | None = None, key_filters: dict | None = None):
         self.owner_alias = owner_alias
         self.name = name
         self.client = client
@@ -40,9 +40,12 @@ class Shard:
         self.sync_binary_data = sync_binary_data
         self.labels = C.owner_labels(owner_alias)
         transforms = transforms or {}
+        kfs = key_filters or {}
         self.factory = InformerFactory(client, namespace, resync_period, **(informer_kw or {}))
-        self.template_informer: Informer = self.factory.informer(R.TEMPLATES, transform=transforms.get(R.TEMPLATES))
-        self.workgroup_informer: Informer = self.factory.informer(R.WORKGROUPS, transform=transforms.get(R.WORKGROUPS))
+        self.template_informer: Informer = self.factory.informer(R.TEMPLATES, transform=transforms.get(R.TEMPLATES),
+                                                                 key_filter=kfs.get(R.TEMPLATES))
+        self.workgroup_informer: Informer = self.factory.informer(R.WORKGROUPS, transform=transforms.get(R.WORKGROUPS),
+                                                                  key_filter=kfs.get(R.WORKGROUPS))
         self.secret_informer: Informer = self.factory.informer(R.SECRETS, transform=transforms.get(R.SECRETS))
         self.configmap_informer: Informer = self.factory.informer(R.CONFIGMAPS, transform=transforms.get(R.CONFIGMAPS))
         self.template_lister = self.template_informer.lister

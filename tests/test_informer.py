@@ -147,3 +147,36 @@ def test_store_indices_and_mutation_overlay():
     assert s.by_index("owner", "u1") == []
     added, updated, deleted = s.replace([make_secret("b", NS)])
     assert [x["metadata"]["name"] for x in added] == ["b"] and [x["metadata"]["name"] for x in deleted] == ["a"]
+
+
+async def test_key_filter_drops_foreign_keys_on_list_and_watch():
+    """Partitioned executors: a key filter keeps other partitions' objects out of the store — off the wire
+    (native scanner, raw watch over HTTP) and on the decoded path (in-memory client)."""
+    for http in (True, False):
+        state = ClusterState()
+        state.create(R.SECRETS, NS, make_secret("keep-0", NS))
+        state.create(R.SECRETS, NS, make_secret("drop-0", NS))
+        srv = None
+        if http:
+            srv = FakeApiServer(state=state)
+            client = RestClient(ClusterConfig(server=await srv.start()))
+        else:
+            client = FakeClient(state, simple=False)
+        inf = Informer(client, R.SECRETS, NS, key_filter=lambda ns, name: ns == NS and name.startswith("keep"))
+        rec = Rec()
+        inf.add_event_handler(rec.add, rec.update, rec.delete)
+        inf.start()
+        assert await inf.wait_for_sync(2)
+        for n in ("drop-1", "keep-1"):
+            state.create(R.SECRETS, NS, make_secret(n, NS))
+        state.delete(R.SECRETS, NS, "drop-0")
+        state.delete(R.SECRETS, NS, "keep-0")
+        await wait_until(lambda: len(rec.log) == 3)
+        assert rec.log == [("add", "keep-0"), ("add", "keep-1"), ("delete", "keep-0")]
+        assert [o["metadata"]["name"] for o in inf.lister.list()] == ["keep-1"]
+        await wait_until(lambda: inf.last_rv == str(state.rv))  # filtered events still advance the RV
+        assert inf.filtered >= 2
+        await inf.stop()
+        if srv is not None:
+            await client.close()
+            await srv.stop()
