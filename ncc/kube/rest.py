@@ -55,6 +55,25 @@ def _ssl_context(cfg: ClusterConfig, exec_cert: tuple | None = None) -> ssl.SSLC
     return ctx
 
 
+_QUERY_CACHE: dict = {}
+
+
+def _query(params: dict) -> str:
+    """"?k=v&…" for the non-None params; memoised (writes repeat the same fieldManager/dryRun sets)."""
+    key = tuple(params.items())
+    try:
+        return _QUERY_CACHE[key]
+    except KeyError:
+        pass
+    except TypeError:  # unhashable value
+        key = None
+    q = {k: v for k, v in params.items() if v is not None}
+    out = ("?" + urlencode(q)) if q else ""
+    if key is not None and len(_QUERY_CACHE) < 4096:
+        _QUERY_CACHE[key] = out
+    return out
+
+
 class RestClient(KubeClient):
     def __init__(self, cfg: ClusterConfig, *, pool_size: int = 64, request_timeout: float = 30.0,
                  max_retries: int = 5, cluster_name: str | None = None, transport: str = "fast"):
@@ -132,9 +151,7 @@ class RestClient(KubeClient):
                       content_type: str = _JSON):
         target = path
         if params:
-            q = {k: v for k, v in params.items() if v is not None}
-            if q:
-                target += "?" + urlencode(q)
+            target += _query(params)
         data = None
         if body is not None:
             data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
