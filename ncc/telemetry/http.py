@@ -72,12 +72,15 @@ class OpsServer:
         self.prometheus = prometheus
         self.extra = extra
         self.app = web.Application()
-        self.app.router.add_get("/healthz", lambda r: web.Response(text="ok"))
+        self.app.router.add_get("/healthz", self._healthz)
         self.app.router.add_get("/readyz", self._readyz)
         self.app.router.add_get("/metrics", self._metrics)
         self.app.router.add_get("/debug/state", self._state)
         self._runner = None
         self.port = None
+
+    async def _healthz(self, _r):
+        return web.Response(text="ok")
 
     async def _readyz(self, _r):
         return web.Response(text="ok") if self.ready() else web.Response(status=503, text="not ready")
