@@ -16,6 +16,8 @@
 //  * fingerprint_many(list) — batch form (one call per informer relist page).
 //  * scan_event(bytes) — reads type/namespace/name/resourceVersion out of a raw watch-event line
 //    without materialising the object, so informers can recognise echoes of their own writes.
+//  * scan_event_owners(bytes) — the same plus ownerReferences names, so a key-partitioned executor
+//    can drop dependents owned only by another partition's templates without decoding them.
 
 #include <pybind11/pybind11.h>
 
@@ -36,7 +38,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 4
+#define NCC_NATIVE_ABI 5
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -376,6 +378,9 @@ class Scanner {
   public:
     Scanner(const char* p, size_t n) : p_(p), e_(p + n) {}
 
+    // owners != nullptr → also collect metadata.ownerReferences[*].name (escaped names → failure)
+    std::vector<std::string_view>* owners = nullptr;
+
     bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
         bool have_type = false, have_obj = false;
@@ -492,6 +497,34 @@ class Scanner {
             return found;
         }
     }
+    // [{"apiVersion":..., "kind":..., "name": "...", "uid": ...}, ...] → owners->push_back(name)
+    bool owner_refs() {
+        ws();
+        if (p_ < e_ && *p_ == 'n') return skip_value();  // null
+        if (!expect('[')) return false;
+        if (peek(']')) { ++p_; return true; }
+        for (;;) {
+            if (!expect('{')) return false;
+            if (!peek('}')) {
+                for (;;) {
+                    std::string_view key;
+                    if (!str(key) || !expect(':')) return false;
+                    if (key == "name") {
+                        std::string_view v;
+                        if (!str(v)) return false;
+                        owners->push_back(v);
+                    } else if (!skip_value()) {
+                        return false;
+                    }
+                    if (peek(',')) { ++p_; continue; }
+                    break;
+                }
+            }
+            if (!expect('}')) return false;
+            if (peek(',')) { ++p_; continue; }
+            return expect(']');
+        }
+    }
     bool meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
         bool have_name = false, have_rv = false;
@@ -507,6 +540,8 @@ class Scanner {
             } else if (key == "resourceVersion") {
                 if (!str(rv)) return false;
                 have_rv = true;
+            } else if (owners != nullptr && key == "ownerReferences") {
+                if (!owner_refs()) return false;
             } else if (!skip_value()) {
                 return false;
             }
@@ -528,6 +563,22 @@ py::object scan_event(py::bytes line) {
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()));
 }
 
+// scan_event_owners(line) -> (type, namespace, name, resourceVersion, (owner names...)) | None
+py::object scan_event_owners(py::bytes line) {
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view type, ns, name, rv;
+    std::vector<std::string_view> owners;
+    Scanner sc(buf, static_cast<size_t>(len));
+    sc.owners = &owners;
+    if (!sc.scan(type, ns, name, rv)) return py::none();
+    py::tuple o(owners.size());
+    for (size_t i = 0; i < owners.size(); ++i) o[i] = py::str(owners[i].data(), owners[i].size());
+    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
+                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -537,6 +588,8 @@ PYBIND11_MODULE(_native, m) {
     m.def("fingerprint_many", &fingerprint_many, py::arg("objs"));
     m.def("scan_event", &scan_event, py::arg("line"),
           "(type, namespace, name, resourceVersion) of a watch-event line, or None");
+    m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
+          "scan_event plus the tuple of metadata.ownerReferences[*].name, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")
         .def(py::init<double, double, double, int>(), py::arg("base_delay"), py::arg("max_delay"), py::arg("qps"),
              py::arg("burst"))

@@ -29,7 +29,7 @@ from .cache.informer import InformerFactory
 from .config import AppConfig, config_to_env, load_config
 from .controller.controller import Controller
 from .controller.events import BroadcastRecorder, FakeRecorder
-from .controller.executor import ExecutorPool, partition_filter
+from .controller.executor import ExecutorPool, partition_filter, partition_owner_filter
 from .controller.options import ControllerOptions
 from .kube.client import RateLimitedClient
 from .kube.kubeconfig import build_config
@@ -178,7 +178,8 @@ class App:
                                       resync_period=0.0 if o.watch_shards else o.resync_period,
                                       assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
                                       slim=o.slim_shard_cache, start=False, names=self.shard_filter,
-                                      key_filter=kf)
+                                      key_filter=kf,
+                                      owner_filter=partition_owner_filter(*o.partition) if o.partition else None)
         if o.role == "executor":
             self.recorder = FakeRecorder(keep=False)  # executors never write to the controller cluster
         else:
@@ -280,6 +281,9 @@ class App:
         if os.environ.get("NCC_CPU_REPORT"):
             import resource
             ru = resource.getrusage(resource.RUSAGE_SELF)
+            infs = [self.factory] + [s.factory for s in self.shards]
+            counts = {i.name: (i.events, getattr(i, "echoes", 0), i.filtered) for f in infs for i in f.informers()}
+            log.warning("informer events/echoes/filtered: %s", counts)
             log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f reconciles=%d", self.options.role, ru.ru_utime,
                         ru.ru_stime, self.controller.stats["reconciles"])
 

@@ -29,7 +29,7 @@ from typing import Callable
 
 from .. import native as _native
 from ..aio import wait_timeout
-from ..api.objects import ObjectKey, key_of
+from ..api.objects import ObjectKey, key_of, rv_int
 from ..api.resources import ResourceType
 from ..kube import errors as E
 from ..kube.client import KubeClient
@@ -88,12 +88,21 @@ class Informer:
     def __init__(self, client: KubeClient, rt: ResourceType, namespace: str | None, *,
                  resync_period: float = 0.0, transform: Callable[[dict], dict] | None = None,
                  label_selector: str | None = None, page_size: int = 500, watch_timeout: tuple = (300, 600),
-                 name: str = "", key_filter: Callable[[str, str], bool] | None = None):
+                 name: str = "", key_filter: Callable[[str, str], bool] | None = None,
+                 owner_filter: Callable[[str, tuple], bool] | None = None):
         self.client = client
-        # key_filter(ns, name) → False drops the object before it is decoded/stored (a partitioned
-        # executor skips the other partitions' templates straight off the wire via the native scanner)
+        # key_filter(ns, name) / owner_filter(ns, owner_names) → False drops the object before it is
+        # decoded/stored (a partitioned executor skips the other partitions' templates, and dependents
+        # owned only by them, straight off the wire via the native scanner).  An object that leaves the
+        # filter (e.g. our ownerRef removed) is dropped from the store.
         self.key_filter = key_filter
+        self.owner_filter = owner_filter
         self.filtered = 0
+        # Writes in flight (`begin_write`/`end_write`): a watch event for such a key may overtake the
+        # write's HTTP response.  It is parked undecoded and, once the response is in, dropped if it is
+        # the write's own echo — the common case — or applied if it is someone else's newer version.
+        self._inflight: dict = {}
+        self._stash: dict = {}
         self.rt = rt
         self.namespace = namespace
         self.resync_period = resync_period
@@ -176,11 +185,9 @@ class Informer:
             token = lm.get("continue")
             if not token:
                 break
-        kf = self.key_filter
-        if kf is not None:
-            dflt = self.namespace or ""
-            items = [o for o in items if kf((o.get("metadata") or {}).get("namespace") or dflt,
-                                            (o.get("metadata") or {}).get("name", ""))]
+        if self.key_filter is not None or self.owner_filter is not None:
+            items = [o for o in items if self._wanted(o.get("metadata") or {})]
+        self._stash.clear()  # the relist is newer than anything parked
         added, updated, deleted = self.store.replace(items)
         self.relists += 1
         synced_before = self.has_synced()
@@ -200,31 +207,47 @@ class Informer:
         kw = dict(resource_version=rv, timeout_seconds=random.randint(lo, hi), allow_bookmarks=True,
                   label_selector=self.label_selector)
         scan = None
-        kf = self.key_filter
-        if (self.echo_fastpath or kf is not None) and hasattr(self.client, "watch_raw"):
+        kf, of = self.key_filter, self.owner_filter
+        if (self.echo_fastpath or kf is not None or of is not None) and hasattr(self.client, "watch_raw"):
             mod = _native.load()
-            scan = mod.scan_event if mod is not None else None
+            if mod is not None:
+                scan = mod.scan_event_owners if of is not None else mod.scan_event
         if scan is not None:
             loads = json.loads
             store = self.store
             default_ns = self.namespace or ""
+            inflight, stash = self._inflight, self._stash
             async for line in self.client.watch_raw(self.rt, self.namespace, **kw):
                 sc = None
-                if kf is not None:
+                if kf is not None or of is not None:
                     sc = scan(line)
-                    if sc is not None and sc[0] in _OBJECT_EVENTS and not kf(sc[1] or default_ns, sc[2]):
-                        rv = self.last_rv = sc[3]
-                        self.filtered += 1
-                        continue
-                if store._assumed:
+                    if sc is not None and sc[0] in _OBJECT_EVENTS:
+                        ns_ = sc[1] or default_ns
+                        if (kf is not None and not kf(ns_, sc[2])) or (of is not None and not of(ns_, sc[4])):
+                            rv = self.last_rv = sc[3]
+                            self._filtered_out(ObjectKey(ns_, sc[2]))
+                            continue
+                if store._assumed or inflight:
                     if sc is None:
                         sc = scan(line)
-                    if sc is not None and sc[0] in ("ADDED", "MODIFIED") and \
-                            store.confirm(ObjectKey(sc[1] or default_ns, sc[2]), sc[3]) is not None:
-                        rv = self.last_rv = sc[3]
-                        self.events += 1
-                        self.echoes += 1
-                        continue
+                    if sc is not None and sc[0] in ("ADDED", "MODIFIED"):
+                        key = ObjectKey(sc[1] or default_ns, sc[2])
+                        if store.confirm(key, sc[3]) is not None:
+                            rv = self.last_rv = sc[3]
+                            self.events += 1
+                            self.echoes += 1
+                            continue
+                        if key in inflight:  # overtook the response of our write: park it
+                            prev = stash.get(key)
+                            if prev is not None:
+                                await self._apply_line(prev[1])
+                            stash[key] = (sc[3], line)
+                            rv = self.last_rv = sc[3]
+                            continue
+                if stash and sc is not None:
+                    prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
+                    if prev is not None:  # keep per-key order
+                        await self._apply_line(prev[1])
                 ev = loads(line)
                 rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
             return rv
@@ -241,13 +264,63 @@ class Informer:
         new_rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
         if t == "BOOKMARK":
             return new_rv
-        kf = self.key_filter
-        if kf is not None:
+        if (self.key_filter is not None or self.owner_filter is not None) and t in _OBJECT_EVENTS:
             m = obj.get("metadata") or {}
-            if not kf(m.get("namespace") or self.namespace or "", m.get("name", "")):
-                self.filtered += 1
+            if not self._wanted(m):
+                self._filtered_out(ObjectKey(m.get("namespace") or self.namespace or "", m.get("name", "")))
                 self.last_rv = new_rv
                 return new_rv
+        await self._apply(t, obj)
+        self.last_rv = new_rv
+        return new_rv
+
+    def _wanted(self, m: dict) -> bool:
+        ns = m.get("namespace") or self.namespace or ""
+        if self.key_filter is not None and not self.key_filter(ns, m.get("name", "")):
+            return False
+        if self.owner_filter is not None:
+            owners = tuple(r.get("name", "") for r in (m.get("ownerReferences") or ()))
+            if not self.owner_filter(ns, owners):
+                return False
+        return True
+
+    def _filtered_out(self, key: ObjectKey) -> None:
+        self.filtered += 1
+        if self.store.get(key.namespace, key.name) is not None:
+            self.store.delete(key)  # left our partition: forget it (no handler dispatch)
+
+    async def _apply_line(self, line: bytes) -> None:
+        ev = json.loads(line)
+        await self._apply(ev.get("type", ""), ev.get("object") or {})
+
+    # ------------------------------------------------------------- write tracking
+    def begin_write(self, key: ObjectKey) -> None:
+        self._inflight[key] = self._inflight.get(key, 0) + 1
+
+    async def end_write(self, key: ObjectKey, obj: dict | None) -> None:
+        """Publish a write result (mutation overlay) and settle a parked watch event for the key."""
+        n = self._inflight.get(key, 0) - 1
+        if n > 0:
+            self._inflight[key] = n
+        else:
+            self._inflight.pop(key, None)
+        if obj is not None:
+            self.store.assume(obj)
+        if n > 0:
+            return
+        parked = self._stash.pop(key, None)
+        if parked is None:
+            return
+        if obj is not None:
+            prv, orv = rv_int(parked[0]), rv_int((obj.get("metadata") or {}).get("resourceVersion"))
+            if prv <= orv:  # our own echo (==) or an older version our write superseded (<)
+                if prv == orv and self.store.confirm(key, parked[0]) is not None:
+                    self.events += 1
+                    self.echoes += 1
+                return
+        await self._apply_line(parked[1])
+
+    async def _apply(self, t: str, obj: dict) -> None:
         self.events += 1
         if t in ("ADDED", "MODIFIED"):
             stored, old = self.store.upsert(obj)
@@ -258,8 +331,6 @@ class Informer:
         elif t == "DELETED":
             old = self.store.delete(obj)
             await self._dispatch_delete(old if old is not None else obj)
-        self.last_rv = new_rv
-        return new_rv
 
     async def _run(self) -> None:
         backoff = 0.8

@@ -52,6 +52,21 @@ def partition_filter(part: int, parts: int):
     return lambda ns, name: crc(f"{ns}/{name}".encode()) % parts == part
 
 
+def partition_owner_filter(part: int, parts: int):
+    """Shard-dependent filter: keep unowned objects (rogue detection needs them) and objects with at
+    least one owner template in this partition; drop those owned only by other partitions' templates."""
+    crc = zlib.crc32
+
+    def keep(ns: str, owners: tuple) -> bool:
+        if not owners:
+            return True
+        for o in owners:
+            if crc(f"{ns}/{o}".encode()) % parts == part:
+                return True
+        return False
+    return keep
+
+
 class ExecutorHandle:
     def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None,
                  part: int = 0, parts: int = 1):

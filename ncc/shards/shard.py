@@ -22,7 +22,7 @@ from __future__ import annotations
 
 from ..api import constants as C
 from ..api import resources as R
-from ..api.objects import meta
+from ..api.objects import ObjectKey, meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
 from ..kube.client import PATCH_APPLY, KubeClient
@@ -31,7 +31,8 @@ from ..kube.client import PATCH_APPLY, KubeClient
 class Shard:
     def __init__(self, owner_alias: str, name: str, client: KubeClient, namespace: str, *,
                  resync_period: float = 0.0, assume_writes: bool = False, sync_binary_data: bool = False,
-                 transforms: dict | None = None, informer_kw: dict | None = None, key_filters: dict | None = None):
+                 transforms: dict | None = None, informer_kw: dict | None = None, key_filters: dict | None = None,
+                 owner_filters: dict | None = None):
         self.owner_alias = owner_alias
         self.name = name
         self.client = client
@@ -46,8 +47,11 @@ class Shard:
                                                                  key_filter=kfs.get(R.TEMPLATES))
         self.workgroup_informer: Informer = self.factory.informer(R.WORKGROUPS, transform=transforms.get(R.WORKGROUPS),
                                                                   key_filter=kfs.get(R.WORKGROUPS))
-        self.secret_informer: Informer = self.factory.informer(R.SECRETS, transform=transforms.get(R.SECRETS))
-        self.configmap_informer: Informer = self.factory.informer(R.CONFIGMAPS, transform=transforms.get(R.CONFIGMAPS))
+        ofs = owner_filters or {}
+        self.secret_informer: Informer = self.factory.informer(R.SECRETS, transform=transforms.get(R.SECRETS),
+                                                               owner_filter=ofs.get(R.SECRETS))
+        self.configmap_informer: Informer = self.factory.informer(R.CONFIGMAPS, transform=transforms.get(R.CONFIGMAPS),
+                                                                  owner_filter=ofs.get(R.CONFIGMAPS))
         self.template_lister = self.template_informer.lister
         self.workgroup_lister = self.workgroup_informer.lister
         self.secret_lister = self.secret_informer.lister
@@ -71,10 +75,19 @@ class Shard:
     async def wait_for_sync(self, timeout: float | None = None) -> bool:
         return await self.factory.wait_for_sync(timeout)
 
-    def _assume(self, informer: Informer, obj):
-        if self.assume_writes and isinstance(obj, dict):
-            informer.store.assume(obj)
-        return obj
+    async def _tracked(self, informer: Informer, namespace: str, name: str, call):
+        """Run one write; publish its result to the informer (mutation overlay) and let the informer
+        settle a watch event that overtook the response (see Informer.begin_write)."""
+        if not self.assume_writes:
+            return await call
+        key = ObjectKey(namespace, name)
+        informer.begin_write(key)
+        res = None
+        try:
+            res = await call
+            return res
+        finally:
+            await informer.end_write(key, res if isinstance(res, dict) else None)
 
     # ---------------------------------------------------------------- templates
     async def create_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
@@ -84,15 +97,16 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        res = await self.client.create(R.TEMPLATES, namespace, obj, field_manager=field_manager)
-        return self._assume(self.template_informer, res)
+        return await self._tracked(self.template_informer, namespace, name,
+                                   self.client.create(R.TEMPLATES, namespace, obj, field_manager=field_manager))
 
     async def update_template(self, shard_obj: dict, spec, field_manager: str) -> dict:
         obj = _strip_slim(dict(shard_obj))
         obj["spec"] = spec
-        res = await self.client.update(R.TEMPLATES, meta(shard_obj).get("namespace", ""), obj,
-                                       field_manager=field_manager)
-        return self._assume(self.template_informer, res)
+        m = meta(shard_obj)
+        return await self._tracked(self.template_informer, m.get("namespace", ""), m.get("name", ""),
+                                   self.client.update(R.TEMPLATES, m.get("namespace", ""), obj,
+                                                      field_manager=field_manager))
 
     async def apply_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
         """Server-side apply (create-or-update in one request; no resourceVersion, no 409 races)."""
@@ -102,9 +116,9 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        res = await self.client.patch(R.TEMPLATES, namespace, name, body, patch_type=PATCH_APPLY,
-                                      field_manager=field_manager, force=True)
-        return self._assume(self.template_informer, res)
+        return await self._tracked(self.template_informer, namespace, name,
+                                   self.client.patch(R.TEMPLATES, namespace, name, body, patch_type=PATCH_APPLY,
+                                                     field_manager=field_manager, force=True))
 
     async def delete_template(self, obj: dict) -> None:
         m = meta(obj)
@@ -118,15 +132,16 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        res = await self.client.create(R.WORKGROUPS, namespace, obj, field_manager=field_manager)
-        return self._assume(self.workgroup_informer, res)
+        return await self._tracked(self.workgroup_informer, namespace, name,
+                                   self.client.create(R.WORKGROUPS, namespace, obj, field_manager=field_manager))
 
     async def update_workgroup(self, shard_obj: dict, spec, field_manager: str) -> dict:
         obj = _strip_slim(dict(shard_obj))
         obj["spec"] = spec
-        res = await self.client.update(R.WORKGROUPS, meta(shard_obj).get("namespace", ""), obj,
-                                       field_manager=field_manager)
-        return self._assume(self.workgroup_informer, res)
+        m = meta(shard_obj)
+        return await self._tracked(self.workgroup_informer, m.get("namespace", ""), m.get("name", ""),
+                                   self.client.update(R.WORKGROUPS, m.get("namespace", ""), obj,
+                                                      field_manager=field_manager))
 
     async def apply_workgroup(self, name: str, namespace: str, spec, field_manager: str) -> dict:
         body = {
@@ -135,9 +150,9 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        res = await self.client.patch(R.WORKGROUPS, namespace, name, body, patch_type=PATCH_APPLY,
-                                      field_manager=field_manager, force=True)
-        return self._assume(self.workgroup_informer, res)
+        return await self._tracked(self.workgroup_informer, namespace, name,
+                                   self.client.patch(R.WORKGROUPS, namespace, name, body, patch_type=PATCH_APPLY,
+                                                     field_manager=field_manager, force=True))
 
     async def delete_workgroup(self, obj: dict) -> None:
         m = meta(obj)
@@ -183,37 +198,43 @@ class Shard:
             obj["metadata"] = m
         return obj
 
+    def _dep_informer(self, rt: R.ResourceType) -> Informer:
+        return self.secret_informer if rt is R.SECRETS else self.configmap_informer
+
+    async def _create_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str):
+        body = self._dependent_body(rt, shard_template, src)
+        m = body["metadata"]
+        return await self._tracked(self._dep_informer(rt), m["namespace"], m["name"],
+                                   self.client.create(rt, m["namespace"], body, field_manager=field_manager))
+
+    async def _update_dependent(self, rt: R.ResourceType, shard_obj: dict, data, new_owner, field_manager: str,
+                                binary_data=None):
+        body = self._updated_dependent(shard_obj, data, new_owner, binary_data)
+        m = meta(shard_obj)
+        return await self._tracked(self._dep_informer(rt), m.get("namespace", ""), m.get("name", ""),
+                                   self.client.update(rt, m.get("namespace", ""), body, field_manager=field_manager))
+
     async def create_secret(self, shard_template: dict, secret: dict, field_manager: str) -> dict:
-        body = self._dependent_body(R.SECRETS, shard_template, secret)
-        res = await self.client.create(R.SECRETS, body["metadata"]["namespace"], body, field_manager=field_manager)
-        return self._assume(self.secret_informer, res)
+        return await self._create_dependent(R.SECRETS, shard_template, secret, field_manager)
 
     async def update_secret(self, shard_secret: dict, data, new_owner: dict | None, field_manager: str) -> dict:
-        body = self._updated_dependent(shard_secret, data, new_owner)
-        res = await self.client.update(R.SECRETS, meta(shard_secret).get("namespace", ""), body,
-                                       field_manager=field_manager)
-        return self._assume(self.secret_informer, res)
+        return await self._update_dependent(R.SECRETS, shard_secret, data, new_owner, field_manager)
 
     async def create_configmap(self, shard_template: dict, configmap: dict, field_manager: str) -> dict:
-        body = self._dependent_body(R.CONFIGMAPS, shard_template, configmap)
-        res = await self.client.create(R.CONFIGMAPS, body["metadata"]["namespace"], body,
-                                       field_manager=field_manager)
-        return self._assume(self.configmap_informer, res)
+        return await self._create_dependent(R.CONFIGMAPS, shard_template, configmap, field_manager)
 
     async def update_configmap(self, shard_configmap: dict, data, new_owner: dict | None, field_manager: str,
                                binary_data=None) -> dict:
-        body = self._updated_dependent(shard_configmap, data, new_owner, binary_data)
-        res = await self.client.update(R.CONFIGMAPS, meta(shard_configmap).get("namespace", ""), body,
-                                       field_manager=field_manager)
-        return self._assume(self.configmap_informer, res)
+        return await self._update_dependent(R.CONFIGMAPS, shard_configmap, data, new_owner, field_manager,
+                                            binary_data)
 
     async def apply_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str) -> dict:
         """Apply our view of a dependent: owner labels, our ownerRef (merged by uid with other owners'), payload."""
         body = self._dependent_body(rt, shard_template, src)
         m = body["metadata"]
-        res = await self.client.patch(rt, m["namespace"], m["name"], body, patch_type=PATCH_APPLY,
-                                      field_manager=field_manager, force=True)
-        return self._assume(self.secret_informer if rt is R.SECRETS else self.configmap_informer, res)
+        return await self._tracked(self._dep_informer(rt), m["namespace"], m["name"],
+                                   self.client.patch(rt, m["namespace"], m["name"], body, patch_type=PATCH_APPLY,
+                                                     field_manager=field_manager, force=True))
 
     async def delete_dependent(self, rt: R.ResourceType, obj: dict) -> None:
         m = meta(obj)

@@ -180,3 +180,59 @@ async def test_key_filter_drops_foreign_keys_on_list_and_watch():
         if srv is not None:
             await client.close()
             await srv.stop()
+
+
+async def test_owner_filter_and_parked_echoes():
+    """Owner filter (partitioned executors) and in-flight write tracking: a watch event that overtakes
+    the response of our own write is parked undecoded and settled by `end_write`."""
+    from ncc.api.objects import ObjectKey
+    state = ClusterState()
+    srv = FakeApiServer(state=state)
+    client = RestClient(ClusterConfig(server=await srv.start()))
+
+    def owned(name, owners):
+        s = make_secret(name, NS)
+        s["metadata"]["ownerReferences"] = [{"apiVersion": "v1", "kind": "NexusAlgorithmTemplate", "name": o,
+                                             "uid": f"u-{o}"} for o in owners]
+        return s
+    try:
+        state.create(R.SECRETS, NS, owned("a", ["mine"]))
+        state.create(R.SECRETS, NS, owned("b", ["other"]))
+        state.create(R.SECRETS, NS, owned("c", []))
+        inf = Informer(client, R.SECRETS, NS, owner_filter=lambda ns, owners: not owners or "mine" in owners)
+        rec = Rec()
+        inf.add_event_handler(rec.add, rec.update, rec.delete)
+        inf.start()
+        assert await inf.wait_for_sync(2)
+        assert sorted(o["metadata"]["name"] for o in inf.lister.list()) == ["a", "c"]
+        state.create(R.SECRETS, NS, owned("d", ["other", "mine"]))
+        cur = state.get(R.SECRETS, NS, "a")
+        state.update(R.SECRETS, NS, dict(cur, metadata=dict(cur["metadata"], ownerReferences=owned(
+            "a", ["other"])["metadata"]["ownerReferences"])))
+        await wait_until(lambda: inf.lister.try_get(NS, "d") is not None and inf.lister.try_get(NS, "a") is None)
+        assert rec.log[-1] == ("add", "d")  # "a" left the partition silently
+
+        # our write's echo overtakes its response: parked, then confirmed without dispatch
+        key = ObjectKey(NS, "c")
+        inf.begin_write(key)
+        cur = state.get(R.SECRETS, NS, "c")
+        res = state.update(R.SECRETS, NS, dict(cur, data={"k": "MQ=="}))
+        await wait_until(lambda: key in inf._stash)
+        n_log, echoes = len(rec.log), inf.echoes
+        await inf.end_write(key, res)
+        assert inf.echoes == echoes + 1 and len(rec.log) == n_log
+        assert inf.lister.get(NS, "c")["data"] == {"k": "MQ=="}
+
+        # a newer foreign write parked behind our (older) response is applied when the write ends
+        inf.begin_write(key)
+        cur = state.get(R.SECRETS, NS, "c")
+        ours = state.update(R.SECRETS, NS, dict(cur, data={"k": "Mg=="}))
+        theirs = state.update(R.SECRETS, NS, dict(ours, data={"k": "Mw=="}))
+        await wait_until(lambda: key in inf._stash and inf._stash[key][0] == theirs["metadata"]["resourceVersion"])
+        await inf.end_write(key, ours)
+        assert inf.lister.get(NS, "c")["data"] == {"k": "Mw=="}
+        assert rec.log[-1] == ("update", "c", False)
+        await inf.stop()
+    finally:
+        await client.close()
+        await srv.stop()
