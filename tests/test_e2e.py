@@ -245,3 +245,58 @@ async def test_partitioned_executors_per_shard(tmp_path):
         for sc in scs:
             await sc.close()
         await env.stop()
+
+
+@pytest.mark.parametrize("executors", [0, -1])
+async def test_native_converges_under_faults(tmp_path, executors):
+    """Failure detection/recovery soak: with 30 % of shard writes failing (5xx), injected latency, and
+    every shard watch dropped mid-run, the native controller still converges every template on every
+    shard (per-key backoff retries, watch resume/relist), and statuses end Ready once faults clear."""
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc = env.controller_client()
+    scs = [env.shard_client(i) for i in range(2)]
+    T = 20
+    try:
+        async with aiohttp_session() as s:
+            for srv in env.shard_servers:
+                async with s.post(srv.url + "/_fake/faults", json={"error_rate": 0.3, "error_code": 503,
+                                                                   "latency_ms": 2, "jitter_ms": 3}) as r:
+                    await r.json()
+            async with Running(env, "native", executors=executors, failure_rate_max_delay=0.2):
+                for i in range(T):
+                    await cc.create(R.SECRETS, NS, make_secret(f"s{i}", NS))
+                    await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[]))
+                await asyncio.sleep(0.3)
+                for srv in env.shard_servers:  # cut every watch stream; informers resume from their last RV
+                    async with s.post(srv.url + "/_fake/faults", json={"drop_watches": True}) as r:
+                        await r.json()
+
+                async def shards_converged():
+                    for sc in scs:
+                        if len((await sc.list(R.TEMPLATES, NS))["items"]) != T:
+                            return False
+                        if len((await sc.list(R.SECRETS, NS))["items"]) != T:
+                            return False
+                    return True
+                await wait_for(shards_converged, timeout=20, interval=0.1)
+                for srv in env.shard_servers:
+                    async with s.post(srv.url + "/_fake/faults", json={"error_rate": 0.0, "latency_ms": 0,
+                                                                       "jitter_ms": 0}) as r:
+                        await r.json()
+
+                async def all_ready():
+                    items = (await cc.list(R.TEMPLATES, NS))["items"]
+                    return len(items) == T and all(
+                        o.get("status", {}).get("conditions", [{}])[0].get("status") == "True" and
+                        o["status"]["syncedToClusters"] == ["shard-0", "shard-1"] for o in items)
+                await wait_for(all_ready, timeout=20, interval=0.1)
+    finally:
+        await cc.close()
+        for sc in scs:
+            await sc.close()
+        await env.stop()
+
+
+def aiohttp_session():
+    import aiohttp
+    return aiohttp.ClientSession()
