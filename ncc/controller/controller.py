@@ -73,7 +73,8 @@ class Controller(ReconcileMixin):
         self._pending_workgroup_deletes: set = set()
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
-        self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0}
+        self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
+                      "reports_pending": 0}
         self.ready = asyncio.Event()
         self.role = o.role
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
@@ -281,10 +282,18 @@ class Controller(ReconcileMixin):
         self.stats["reports"] += 1
         key = msg["k"]
         st = self.shard_state.setdefault(key, {})
+        uid, gen = msg["u"], msg["g"]
         for shard, err in msg["r"].items():
-            st[shard] = (msg["u"], msg["g"], err)
+            st[shard] = (uid, gen, err)
         if msg.get("w"):
             self._pending_event.add(key)
+        # Only a complete set of reports for this object version can change its status: re-evaluate
+        # then, instead of once per executor report (N× fewer coordinator passes at N shards).
+        for s in self.all_shard_names:
+            e = st.get(s)
+            if e is None or e[0] != uid or e[1] < gen:
+                self.stats["reports_pending"] += 1
+                return
         self._enqueue_key(key)
 
     def shard_readiness(self, key: str, obj: dict):
