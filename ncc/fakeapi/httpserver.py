@@ -17,10 +17,14 @@ import json
 from urllib.parse import parse_qsl, unquote
 
 _CRLF2 = b"\r\n\r\n"
+_HEADS: dict = {}
 _REASONS = {200: "OK", 201: "Created", 204: "No Content", 400: "Bad Request", 401: "Unauthorized",
             403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed", 409: "Conflict", 410: "Gone",
             415: "Unsupported Media Type", 422: "Unprocessable Entity", 429: "Too Many Requests",
             500: "Internal Server Error", 503: "Service Unavailable", 504: "Gateway Timeout"}
+
+
+_QUERY_MEMO: dict = {}  # raw query → parsed (write requests repeat e.g. "fieldManager=…"); read-only use
 
 
 class Request:
@@ -38,7 +42,12 @@ class Request:
     @property
     def query(self) -> dict:
         if self._query is None:
-            self._query = dict(parse_qsl(self.raw_query, keep_blank_values=True))
+            q = _QUERY_MEMO.get(self.raw_query)
+            if q is None:
+                q = dict(parse_qsl(self.raw_query, keep_blank_values=True))
+                if len(_QUERY_MEMO) < 1024 and "resourceVersion" not in q and "continue" not in q:
+                    _QUERY_MEMO[self.raw_query] = q
+            self._query = q
         return self._query
 
     @property
@@ -67,6 +76,13 @@ class Response:
         self.headers = headers or {}
 
     def encode(self) -> bytes:
+        if not self.headers:
+            head = _HEADS.get((self.status, self.content_type))
+            if head is None:
+                head = _HEADS[(self.status, self.content_type)] = (
+                    f"HTTP/1.1 {self.status} {_REASONS.get(self.status, 'Status')}\r\n"
+                    f"Content-Type: {self.content_type}\r\nContent-Length: ").encode()
+            return b"%s%d\r\n\r\n%s" % (head, len(self.body), self.body)
         h = [f"HTTP/1.1 {self.status} {_REASONS.get(self.status, 'Status')}", f"Content-Type: {self.content_type}",
              f"Content-Length: {len(self.body)}"]
         for k, v in self.headers.items():
@@ -147,34 +163,47 @@ class _ServerConn(asyncio.Protocol):
             self._next()
 
     def _next(self):
-        buf = self.buf
-        i = buf.find(_CRLF2)
-        if i < 0:
-            if len(buf) > 1 << 20:
+        fast = self.server.fast
+        while True:
+            buf = self.buf
+            i = buf.find(_CRLF2)
+            if i < 0:
+                if len(buf) > 1 << 20:
+                    self.transport.close()
+                return
+            lines = bytes(buf[:i]).split(b"\r\n")
+            try:
+                method, target, _ = lines[0].decode("latin-1").split(" ", 2)
+            except ValueError:
                 self.transport.close()
+                return
+            headers = {}
+            for ln in lines[1:]:
+                k, _, v = ln.partition(b":")
+                headers[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
+            clen = int(headers.get("content-length", "0") or 0)
+            if len(buf) < i + 4 + clen:
+                return  # wait for the full body
+            body = bytes(buf[i + 4:i + 4 + clen])
+            del buf[:i + 4 + clen]
+            req = Request(method, target, headers, body)
+            req._conn = self  # type: ignore[attr-defined]
+            keep = headers.get("connection", "").lower() != "close"
+            if fast is not None:
+                try:
+                    resp = fast(req)
+                except Exception as e:  # noqa: BLE001
+                    resp = Response(500, text=f"internal error: {e}")
+                if resp is not None:  # answered synchronously: no task, keep parsing pipelined requests
+                    self.transport.write(resp.encode())
+                    if not keep:
+                        self.transport.close()
+                        return
+                    continue
+            self.busy = True
+            task = asyncio.ensure_future(self.server.handler(req))
+            task.add_done_callback(lambda t, k=keep: self._done(t, k))
             return
-        lines = bytes(buf[:i]).split(b"\r\n")
-        try:
-            method, target, _ = lines[0].decode("latin-1").split(" ", 2)
-        except ValueError:
-            self.transport.close()
-            return
-        headers = {}
-        for ln in lines[1:]:
-            k, _, v = ln.partition(b":")
-            headers[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
-        clen = int(headers.get("content-length", "0") or 0)
-        if len(buf) < i + 4 + clen:
-            return  # wait for the full body
-        body = bytes(buf[i + 4:i + 4 + clen])
-        del buf[:i + 4 + clen]
-        req = Request(method, target, headers, body)
-        req._conn = self  # type: ignore[attr-defined]
-        self.busy = True
-        keep = headers.get("connection", "").lower() != "close"
-        coro = self.server.handler(req)
-        task = asyncio.ensure_future(coro)
-        task.add_done_callback(lambda t, k=keep: self._done(t, k))
 
     def _done(self, task: asyncio.Task, keep: bool):
         self.busy = False
@@ -194,8 +223,10 @@ class _ServerConn(asyncio.Protocol):
 
 
 class HttpServer:
-    def __init__(self, handler):
+    def __init__(self, handler, fast=None):
+        """`handler(request)` is a coroutine; optional `fast(request)` answers synchronously or returns None."""
         self.handler = handler
+        self.fast = fast
         self._server: asyncio.AbstractServer | None = None
         self._conns: set = set()
         self.port: int | None = None

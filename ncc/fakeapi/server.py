@@ -88,7 +88,7 @@ class FakeApiServer:
         self.state.write_hooks.append(self.markers.on_write)
         self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
         self._streams: set = set()
-        self._http = web.HttpServer(self._dispatch)
+        self._http = web.HttpServer(self._dispatch, fast=self.fast)
         self.port: int | None = None
         self.url: str | None = None
 
@@ -139,11 +139,35 @@ class FakeApiServer:
             raise E.NotFound(f"version {version} of {plural}.{group} not served")
         return rt, ns, name, sub
 
+    def fast(self, request: web.Request):
+        """Synchronous handling of plain CRUD requests — no task, no await — used by the HTTP layer for
+        every request that is not a control endpoint, a watch, or subject to injected latency."""
+        if request.path.startswith("/_fake/"):
+            return None
+        f = self.faults
+        if f.latency_ms or f.jitter_ms:
+            return None
+        if request.method == "GET" and "watch=" in request.raw_query:
+            return None
+        self.requests["total"] += 1
+        return self._core(request)
+
     async def _dispatch(self, request: web.Request) -> web.StreamResponse:
         self.requests["total"] += 1
         path = request.path
         if path.startswith("/_fake/"):
             return await self._control(request, path[len("/_fake/"):])
+        f = self.faults
+        if (f.latency_ms or f.jitter_ms) and path.startswith(("/api/", "/apis/")) and not f.down:
+            await asyncio.sleep((f.latency_ms + random.random() * f.jitter_ms) / 1000.0)
+        r = self._core(request)
+        if isinstance(r, tuple):  # a watch
+            return await self._watch(request, r[1], r[2])
+        return r
+
+    def _core(self, request: web.Request):
+        """Auth, faults, routing and CRUD for one request; returns a Response, or ("watch", rt, ns)."""
+        path = request.path
         if path in ("/healthz", "/readyz", "/livez"):
             return web.Response(text="ok")
         if path == "/version":
@@ -157,8 +181,6 @@ class FakeApiServer:
             f = self.faults
             if f.down:
                 raise E.ServiceUnavailable("the server is currently unable to handle the request")
-            if f.latency_ms or f.jitter_ms:
-                await asyncio.sleep((f.latency_ms + random.random() * f.jitter_ms) / 1000.0)
             mutating = request.method in ("POST", "PUT", "PATCH", "DELETE")
             if f.throttle_rate and random.random() < f.throttle_rate:
                 self.requests["throttled"] += 1
@@ -177,12 +199,12 @@ class FakeApiServer:
             if m == "GET":
                 if name is None:
                     if q.get("watch") in ("1", "true"):
-                        return await self._watch(request, rt, ns)
+                        return ("watch", rt, ns)
                     limit = int(q["limit"]) if q.get("limit") else None
                     return self._json(self.state.list(rt, ns, label_selector=q.get("labelSelector"), limit=limit,
                                                       continue_token=q.get("continue")))
                 return self._json(self.state.get(rt, ns or "", name))
-            body = await self._body(request) if m != "DELETE" or request.can_read_body else None
+            body = self._body(request) if m != "DELETE" or request.can_read_body else None
             if m == "POST" and name is None:
                 return self._written(self.state.create(rt, ns or "", body, owned=True), 201)
             if m == "PUT" and name is not None:
@@ -210,8 +232,9 @@ class FakeApiServer:
         except (ValueError, KeyError, TypeError) as e:
             return _status_response(E.BadRequest(f"bad request: {e}"))
 
-    async def _body(self, request: web.Request):
-        raw = await request.read()
+    @staticmethod
+    def _body(request: web.Request):
+        raw = request.body
         if not raw:
             return {}
         if request.content_type == PATCH_APPLY:
@@ -331,7 +354,7 @@ class FakeApiServer:
                                "state": self.state.stats, "objects": counts, "faults": self.faults.as_dict(),
                                "watchers": len(self.state._watchers)})
         if what == "faults" and request.method == "POST":
-            body = await self._body(request)
+            body = self._body(request)
             self.faults.update(body)
             if body.get("drop_watches") or body.get("down"):
                 self.drop_watches()
@@ -339,12 +362,12 @@ class FakeApiServer:
                 self.state.compact()
             return self._json(self.faults.as_dict())
         if what == "markers" and request.method == "POST":
-            body = await self._body(request)
+            body = self._body(request)
             for plural, path in (body.get("specs") or {}).items():
                 self.markers.add_spec(plural, path)
             return self._json({"specs": {k: ".".join(v) for k, v in self.markers.paths.items()}})
         if what == "markers/wait" and request.method == "POST":
-            body = await self._body(request)
+            body = self._body(request)
             want = body.get("want") or []
             ok = await self.markers.wait(want, float(body.get("timeout", 60)))
             out = {"ok": ok, "counts": {f"{w['plural']}={w['value']}": len(self.markers.times(w["plural"], w["value"]))
@@ -355,7 +378,7 @@ class FakeApiServer:
                                 for w in want}
             return self._json(out)
         if what == "apply" and request.method == "POST":
-            body = await self._body(request)
+            body = self._body(request)
             t0 = time.time_ns()
             n = 0
             # yield_every > 0 lets watch streams flush while a large apply is in progress (commits and
@@ -386,7 +409,7 @@ class FakeApiServer:
                 n += 1
             return self._json({"applied": n, "t0_ns": t0, "t1_ns": time.time_ns(), "rv": self.state.rv})
         if what == "objects" and request.method == "POST":
-            body = await self._body(request)
+            body = self._body(request)
             n = 0
             for o in body.get("items") or []:
                 rt = R.by_kind(o["kind"])

@@ -80,6 +80,7 @@ class Watcher:
         if not self.closed:
             self.closed = True
             self.state._watchers.discard(self)
+            self.state._by_rt.get(self.rt_key, set()).discard(self)
             self.queue.put_nowait(None)
 
 
@@ -111,6 +112,7 @@ class ClusterState:
         self._types: dict[RtKey, ResourceType] = {(rt.group, rt.plural): rt for rt in R.BUILTIN}
         self._history: deque[EventRecord] = deque(maxlen=max(history, 1))
         self._watchers: set[Watcher] = set()
+        self._by_rt: dict[RtKey, set] = {}  # watchers per resource type (emit only scans those)
         self._uids: dict[str, tuple] = {}  # uid -> (rt_key, ns, name)
         self._dependents: dict[str, set] = {}  # owner uid -> {(rt_key, ns, name)}
         self.write_hooks: list[Callable[[str, ResourceType, dict], None]] = []
@@ -145,9 +147,11 @@ class ClusterState:
         self.last_record = rec
         if not self.simple:
             self._history.append(rec)
-        for w in tuple(self._watchers):
-            if w.wants(rec):
-                w.queue.put_nowait(rec)
+        ws = self._by_rt.get(rec.rt_key)
+        if ws:
+            for w in tuple(ws):
+                if w.wants(rec):
+                    w.queue.put_nowait(rec)
         for hook in self.write_hooks:
             hook(type_, rt, obj)
 
@@ -418,6 +422,7 @@ class ClusterState:
                     if rec.rv > since and w.wants(rec):
                         w.queue.put_nowait(rec)
         self._watchers.add(w)
+        self._by_rt.setdefault(w.rt_key, set()).add(w)
         return w
 
     def compact(self) -> None:
