@@ -38,7 +38,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 5
+#define NCC_NATIVE_ABI 6
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -378,8 +378,9 @@ class Scanner {
   public:
     Scanner(const char* p, size_t n) : p_(p), e_(p + n) {}
 
-    // owners != nullptr → also collect metadata.ownerReferences[*].name (escaped names → failure)
+    // owners != nullptr → also collect metadata.ownerReferences[*].name and .uid (escapes → failure)
     std::vector<std::string_view>* owners = nullptr;
+    std::vector<std::string_view>* owner_uids = nullptr;
 
     bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
@@ -505,14 +506,15 @@ class Scanner {
         if (peek(']')) { ++p_; return true; }
         for (;;) {
             if (!expect('{')) return false;
+            std::string_view oname, ouid;
             if (!peek('}')) {
                 for (;;) {
                     std::string_view key;
                     if (!str(key) || !expect(':')) return false;
                     if (key == "name") {
-                        std::string_view v;
-                        if (!str(v)) return false;
-                        owners->push_back(v);
+                        if (!str(oname)) return false;
+                    } else if (key == "uid") {
+                        if (!str(ouid)) return false;
                     } else if (!skip_value()) {
                         return false;
                     }
@@ -521,6 +523,8 @@ class Scanner {
                 }
             }
             if (!expect('}')) return false;
+            owners->push_back(oname);
+            owner_uids->push_back(ouid);
             if (peek(',')) { ++p_; continue; }
             return expect(']');
         }
@@ -563,20 +567,22 @@ py::object scan_event(py::bytes line) {
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()));
 }
 
-// scan_event_owners(line) -> (type, namespace, name, resourceVersion, (owner names...)) | None
+// scan_event_owners(line) -> (type, namespace, name, resourceVersion, (owner names...), (owner uids...)) | None
 py::object scan_event_owners(py::bytes line) {
     char* buf = nullptr;
     Py_ssize_t len = 0;
     if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
     std::string_view type, ns, name, rv;
-    std::vector<std::string_view> owners;
+    std::vector<std::string_view> owners, uids;
     Scanner sc(buf, static_cast<size_t>(len));
     sc.owners = &owners;
+    sc.owner_uids = &uids;
     if (!sc.scan(type, ns, name, rv)) return py::none();
-    py::tuple o(owners.size());
+    py::tuple o(owners.size()), u(uids.size());
     for (size_t i = 0; i < owners.size(); ++i) o[i] = py::str(owners[i].data(), owners[i].size());
+    for (size_t i = 0; i < uids.size(); ++i) u[i] = py::str(uids[i].data(), uids[i].size());
     return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
-                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o);
+                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u);
 }
 
 }  // namespace
@@ -589,7 +595,7 @@ PYBIND11_MODULE(_native, m) {
     m.def("scan_event", &scan_event, py::arg("line"),
           "(type, namespace, name, resourceVersion) of a watch-event line, or None");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
-          "scan_event plus the tuple of metadata.ownerReferences[*].name, or None");
+          "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")
         .def(py::init<double, double, double, int>(), py::arg("base_delay"), py::arg("max_delay"), py::arg("qps"),
              py::arg("burst"))

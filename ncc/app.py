@@ -77,6 +77,10 @@ def client_limits(cfg: AppConfig) -> tuple[float, int]:
     return 0.0, cfg.client_burst
 
 
+def strip_payload(obj: dict) -> dict:
+    return {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
+
+
 def cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> float | None:
     """CPU limit from the cgroup CFS quota (v2 `cpu.max`, v1 `cpu.cfs_quota_us`), None if unlimited.
     A Kubernetes pod's `resources.limits.cpu` lands here, not in the affinity mask."""
@@ -172,6 +176,11 @@ class App:
                                   else auto_executors_per_shard(self.n_executors))
         if o.role == "coordinator":
             self.shards = []
+            # the coordinator adopts and reports; it never copies payloads: keep metadata only and skip
+            # payload-only updates straight off the wire
+            for rt in (R.SECRETS, R.CONFIGMAPS):
+                infs[rt].metadata_only = True
+                infs[rt].store.transform = strip_payload
         else:
             self.shards = load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
                                       client_factory=self.client_factory,
@@ -284,8 +293,8 @@ class App:
             infs = [self.factory] + [s.factory for s in self.shards]
             counts = {i.name: (i.events, getattr(i, "echoes", 0), i.filtered) for f in infs for i in f.informers()}
             log.warning("informer events/echoes/filtered: %s", counts)
-            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f reconciles=%d", self.options.role, ru.ru_utime,
-                        ru.ru_stime, self.controller.stats["reconciles"])
+            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f stats=%s", self.options.role, ru.ru_utime,
+                        ru.ru_stime, self.controller.stats)
 
 
 def setup_signal_handler(stop: asyncio.Event) -> None:

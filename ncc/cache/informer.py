@@ -103,6 +103,10 @@ class Informer:
         # the write's own echo — the common case — or applied if it is someone else's newer version.
         self._inflight: dict = {}
         self._stash: dict = {}
+        # metadata_only: the consumer needs names/ownerReferences, never payloads (the coordinator's view
+        # of Secrets/ConfigMaps).  MODIFIED events that leave the owner list unchanged are skipped without
+        # decoding; stored objects keep metadata only.
+        self.metadata_only = False
         self.rt = rt
         self.namespace = namespace
         self.resync_period = resync_period
@@ -208,10 +212,11 @@ class Informer:
                   label_selector=self.label_selector)
         scan = None
         kf, of = self.key_filter, self.owner_filter
-        if (self.echo_fastpath or kf is not None or of is not None) and hasattr(self.client, "watch_raw"):
+        mo = self.metadata_only
+        if (self.echo_fastpath or kf is not None or of is not None or mo) and hasattr(self.client, "watch_raw"):
             mod = _native.load()
             if mod is not None:
-                scan = mod.scan_event_owners if of is not None else mod.scan_event
+                scan = mod.scan_event_owners if (of is not None or mo) else mod.scan_event
         if scan is not None:
             loads = json.loads
             store = self.store
@@ -226,6 +231,17 @@ class Informer:
                         if (kf is not None and not kf(ns_, sc[2])) or (of is not None and not of(ns_, sc[4])):
                             rv = self.last_rv = sc[3]
                             self._filtered_out(ObjectKey(ns_, sc[2]))
+                            continue
+                if mo:
+                    if sc is None:
+                        sc = scan(line)
+                    if sc is not None and sc[0] == "MODIFIED":
+                        cur = store.get(sc[1] or default_ns, sc[2])
+                        refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
+                        if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
+                                tuple(r.get("uid", "") for r in refs) == sc[5]:
+                            rv = self.last_rv = sc[3]
+                            self.filtered += 1
                             continue
                 if store._assumed or inflight:
                     if sc is None:

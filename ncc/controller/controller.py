@@ -141,6 +141,8 @@ class Controller(ReconcileMixin):
                 and old.get("binaryData") == new.get("binaryData") and old.get("type") == new.get("type") \
                 and template_owner_names(old) == template_owner_names(new):
             return  # e.g. our own adoption PUT: ownerRef UIDs changed, payload did not
+        if self.options.role == "coordinator" and om.get("ownerReferences") == nm.get("ownerReferences"):
+            return  # payload changes are the executors' business; the coordinator only adopts and reports
         self._on_dependent(new, index)
 
     def enqueue_resource(self, obj, kind: str) -> None:

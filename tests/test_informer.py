@@ -236,3 +236,31 @@ async def test_owner_filter_and_parked_echoes():
     finally:
         await client.close()
         await srv.stop()
+
+
+async def test_metadata_only_skips_payload_updates_but_not_owner_changes():
+    state = ClusterState()
+    srv = FakeApiServer(state=state)
+    client = RestClient(ClusterConfig(server=await srv.start()))
+    try:
+        state.create(R.SECRETS, NS, make_secret("s", NS))
+        inf = Informer(client, R.SECRETS, NS, transform=lambda o: {k: v for k, v in o.items() if k != "data"})
+        inf.metadata_only = True
+        rec = Rec()
+        inf.add_event_handler(rec.add, rec.update, rec.delete)
+        inf.start()
+        assert await inf.wait_for_sync(2)
+        cur = state.get(R.SECRETS, NS, "s")
+        cur = state.update(R.SECRETS, NS, dict(cur, data={"k": "MQ=="}))  # payload only → skipped
+        ref = {"apiVersion": "v1", "kind": "NexusAlgorithmTemplate", "name": "t", "uid": "u1"}
+        cur = state.update(R.SECRETS, NS, dict(cur, metadata=dict(cur["metadata"], ownerReferences=[ref])))
+        cur = state.update(R.SECRETS, NS, dict(cur, metadata=dict(cur["metadata"], ownerReferences=[
+            dict(ref, uid="u2")])))  # same owner name, new uid (template re-created) → delivered
+        await wait_until(lambda: inf.last_rv == str(state.rv))
+        assert rec.log == [("add", "s"), ("update", "s", False), ("update", "s", False)]
+        assert inf.lister.get(NS, "s")["metadata"]["ownerReferences"][0]["uid"] == "u2"
+        assert "data" not in inf.lister.get(NS, "s") and inf.filtered == 1
+        await inf.stop()
+    finally:
+        await client.close()
+        await srv.stop()
