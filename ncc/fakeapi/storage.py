@@ -60,13 +60,54 @@ class EventRecord:
         return self._line
 
 
+class Mailbox:
+    """Minimal single-consumer queue (the subset of asyncio.Queue a watch stream uses).  `put_nowait` is a
+    deque append plus, only when the consumer is parked, one future completion — it runs once per event
+    per watcher, so it must stay much cheaper than asyncio.Queue's bookkeeping."""
+    __slots__ = ("_items", "_waiter")
+
+    def __init__(self):
+        self._items: deque = deque()
+        self._waiter: asyncio.Future | None = None
+
+    def put_nowait(self, item) -> None:
+        self._items.append(item)
+        w = self._waiter
+        if w is not None:
+            self._waiter = None
+            if not w.done():
+                w.set_result(None)
+
+    def empty(self) -> bool:
+        return not self._items
+
+    def qsize(self) -> int:
+        return len(self._items)
+
+    def get_nowait(self):
+        if not self._items:
+            raise asyncio.QueueEmpty
+        return self._items.popleft()
+
+    async def get(self):
+        while not self._items:
+            fut = self._waiter = asyncio.get_running_loop().create_future()
+            try:
+                await fut
+            finally:
+                if self._waiter is fut:
+                    self._waiter = None
+        return self._items.popleft()
+
+
 class Watcher:
     def __init__(self, state: "ClusterState", rt_key: RtKey, namespace: str | None, selector: str | None):
         self.state = state
         self.rt_key = rt_key
         self.namespace = namespace or None
         self.match_labels = selectors.parse(selector)
-        self.queue: asyncio.Queue = asyncio.Queue()
+        self.everything = not selector  # no label selector: only the namespace decides
+        self.queue = Mailbox()
         self.closed = False
 
     def wants(self, rec: EventRecord) -> bool:
@@ -150,7 +191,9 @@ class ClusterState:
         ws = self._by_rt.get(rec.rt_key)
         if ws:
             for w in tuple(ws):
-                if w.wants(rec):
+                if w.everything and (not w.namespace or w.namespace == ns):
+                    w.queue.put_nowait(rec)
+                elif w.wants(rec):
                     w.queue.put_nowait(rec)
         for hook in self.write_hooks:
             hook(type_, rt, obj)
