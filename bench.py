@@ -150,8 +150,9 @@ async def post(session, url, body, timeout=None):
         return await r.json()
 
 
-def cpu_seconds(named: dict) -> dict:
-    """user+sys CPU seconds per named process; `controller` also reports its executor children."""
+def cpu_seconds(named: dict, rss: dict | None = None) -> dict:
+    """user+sys CPU seconds per named process; `coordinator` also reports its executor children.
+    With `rss` given, resident memory (MiB) per process is recorded there too."""
     import psutil
     out = {}
     for name, proc in named.items():
@@ -161,8 +162,13 @@ def cpu_seconds(named: dict) -> dict:
             p = psutil.Process(proc.pid)
             t = p.cpu_times()
             out[name] = t.user + t.system
+            if rss is not None:
+                rss[name] = round(p.memory_info().rss / 2**20, 1)
             if name == "coordinator":
-                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in p.children(recursive=True))
+                kids = p.children(recursive=True)
+                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in kids)
+                if rss is not None:
+                    rss["executors"] = round(sum(c.memory_info().rss for c in kids) / 2**20, 1)
         except (psutil.Error, OSError):
             pass
     return out
@@ -283,9 +289,11 @@ async def run(args, d: Dist) -> dict | None:
                         ctrl_times.append((await converge(step, True, ctrl_url))["times"])
             d.sync()
             elapsed = time.perf_counter() - t_start
-            cpu1 = cpu_seconds(named)
+            rss: dict = {}
+            cpu1 = cpu_seconds(named, rss)
             util = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 3) for k in cpu1}
             utils = d.all_gather(util)
+            rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)
             all_times = d.all_gather(shard_times)
             if d.rank != 0:
@@ -323,6 +331,8 @@ async def run(args, d: Dist) -> dict | None:
                 # busy CPU cores per process over the timed steps (rank 0's, plus the busiest shard server)
                 "cpu_cores_busy": dict(utils[0], **{"shard-apiserver-max": max(u.get("shard-apiserver", 0.0)
                                                                                  for u in utils)}),
+                "rss_mib": dict(rsses[0], **{"shard-apiserver-max": max(r.get("shard-apiserver", 0.0)
+                                                                       for r in rsses)}),
             }
     finally:
         for p in reversed(procs):
