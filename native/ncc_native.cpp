@@ -16,8 +16,10 @@
 //  * fingerprint_many(list) — batch form (one call per informer relist page).
 //  * scan_event(bytes) — reads type/namespace/name/resourceVersion out of a raw watch-event line
 //    without materialising the object, so informers can recognise echoes of their own writes.
-//  * scan_event_owners(bytes) — the same plus ownerReferences names, so a key-partitioned executor
-//    can drop dependents owned only by another partition's templates without decoding them.
+//  * scan_event_owners(bytes) — the same plus ownerReferences names/uids, so a key-partitioned
+//    executor can drop dependents owned only by another partition's templates without decoding them.
+//  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
+//    writer can publish its write without decoding the echoed object.
 
 #include <pybind11/pybind11.h>
 
@@ -38,7 +40,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 6
+#define NCC_NATIVE_ABI 7
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -381,6 +383,12 @@ class Scanner {
     // owners != nullptr → also collect metadata.ownerReferences[*].name and .uid (escapes → failure)
     std::vector<std::string_view>* owners = nullptr;
     std::vector<std::string_view>* owner_uids = nullptr;
+    std::string_view* uid = nullptr;  // non-null → also read metadata.uid
+
+    // top-level object {"apiVersion":..., "metadata":{...}, ...} (a write response)
+    bool scan_object(std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        return object_meta(ns, name, rv);
+    }
 
     bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
@@ -544,6 +552,8 @@ class Scanner {
             } else if (key == "resourceVersion") {
                 if (!str(rv)) return false;
                 have_rv = true;
+            } else if (uid != nullptr && key == "uid") {
+                if (!str(*uid)) return false;
             } else if (owners != nullptr && key == "ownerReferences") {
                 if (!owner_refs()) return false;
             } else if (!skip_value()) {
@@ -585,6 +595,19 @@ py::object scan_event_owners(py::bytes line) {
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u);
 }
 
+// scan_object(body) -> (namespace, name, resourceVersion, uid) of a JSON object's metadata | None
+py::object scan_object(py::bytes body) {
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(body.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view ns, name, rv, uid;
+    Scanner sc(buf, static_cast<size_t>(len));
+    sc.uid = &uid;
+    if (!sc.scan_object(ns, name, rv)) return py::none();
+    return py::make_tuple(py::str(ns.data(), ns.size()), py::str(name.data(), name.size()),
+                          py::str(rv.data(), rv.size()), py::str(uid.data(), uid.size()));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -594,6 +617,8 @@ PYBIND11_MODULE(_native, m) {
     m.def("fingerprint_many", &fingerprint_many, py::arg("objs"));
     m.def("scan_event", &scan_event, py::arg("line"),
           "(type, namespace, name, resourceVersion) of a watch-event line, or None");
+    m.def("scan_object", &scan_object, py::arg("body"),
+          "(namespace, name, resourceVersion, uid) from an object's metadata without decoding it, or None");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")

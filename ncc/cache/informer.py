@@ -313,7 +313,7 @@ class Informer:
     def begin_write(self, key: ObjectKey) -> None:
         self._inflight[key] = self._inflight.get(key, 0) + 1
 
-    async def end_write(self, key: ObjectKey, obj: dict | None) -> None:
+    async def end_write(self, key: ObjectKey, obj: dict | None, transformed: bool = False) -> None:
         """Publish a write result (mutation overlay) and settle a parked watch event for the key."""
         n = self._inflight.get(key, 0) - 1
         if n > 0:
@@ -321,7 +321,7 @@ class Informer:
         else:
             self._inflight.pop(key, None)
         if obj is not None:
-            self.store.assume(obj)
+            self.store.assume(obj, transformed)
         if n > 0:
             return
         parked = self._stash.pop(key, None)

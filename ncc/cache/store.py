@@ -115,9 +115,10 @@ class Store:
             self._indices[name] = idx
         return added, updated, deleted
 
-    def assume(self, obj: dict) -> None:
-        """Record a write result we made; visible to `get` until the informer catches up."""
-        if self.transform is not None:
+    def assume(self, obj: dict, transformed: bool = False) -> None:
+        """Record a write result we made; visible to `get` until the informer catches up.
+        `transformed=True`: `obj` is already in stored form (e.g. a slim object built by the writer)."""
+        if self.transform is not None and not transformed:
             obj = self.transform(obj)
         key = key_of(obj)
         rv = rv_int((obj.get("metadata") or {}).get("resourceVersion"))

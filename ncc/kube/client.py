@@ -115,6 +115,18 @@ class RateLimitedClient(KubeClient):
         await self.limiter(rt).wait()
         return await self.inner.patch(rt, namespace, name, body, **kw)
 
+    @property
+    def write_meta(self):
+        """Rate-limited pass-through of the inner client's `write_meta`, or None when it has none."""
+        inner = getattr(self.inner, "write_meta", None)
+        if inner is None:
+            return None
+
+        async def wm(verb, rt, namespace, body, **kw):
+            await self.limiter(rt).wait()
+            return await inner(verb, rt, namespace, body, **kw)
+        return wm
+
     async def delete(self, rt, namespace, name, **kw):
         await self.limiter(rt).wait()
         return await self.inner.delete(rt, namespace, name, **kw)

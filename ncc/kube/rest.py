@@ -22,6 +22,7 @@ from urllib.parse import urlencode
 
 import aiohttp
 
+from .. import native as _native
 from ..api.resources import ResourceType
 from . import errors as E
 from .client import PATCH_MERGE, KubeClient, WatchEvent
@@ -148,7 +149,10 @@ class RestClient(KubeClient):
         return h
 
     async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
-                      content_type: str = _JSON):
+                      content_type: str = _JSON, raw: bool = False):
+        """One API call with auth refresh and Retry-After retries → decoded JSON (or the raw body bytes
+        of a successful response with `raw=True`); non-2xx raises the matching ApiError."""
+        raw_out = raw
         target = path
         if params:
             target += _query(params)
@@ -161,12 +165,14 @@ class RestClient(KubeClient):
             self.stats["requests"] += 1
             headers = await self._headers(content_type if data is not None else None)
             try:
-                status, raw, retry_after = await self._send(method, target, headers, data)
+                status, body_bytes, retry_after = await self._send(method, target, headers, data)
             except E.TransportError:
                 self.stats["errors"] += 1
                 raise
             if status < 300:
-                return json.loads(raw) if raw else None
+                if raw_out:
+                    return bytes(body_bytes)
+                return json.loads(body_bytes) if body_bytes else None
             if status == 401 and self.cfg.exec is not None and not refreshed:
                 refreshed = True
                 await self.creds.token(force_refresh=True)
@@ -182,11 +188,11 @@ class RestClient(KubeClient):
                 continue
             self.stats["errors"] += 1
             try:
-                st = json.loads(raw) if raw else None
+                st = json.loads(body_bytes) if body_bytes else None
             except ValueError:
                 st = None
             err = E.from_status(status, st if isinstance(st, dict) else None,
-                                fallback_message=bytes(raw[:200]).decode(errors="replace"))
+                                fallback_message=bytes(body_bytes[:200]).decode(errors="replace"))
             if retry_after is not None:
                 try:
                     err.retry_after = float(retry_after)
@@ -224,6 +230,29 @@ class RestClient(KubeClient):
             params["force"] = "true" if force else "false"
         return await self.request("PATCH", rt.item_path(namespace, name, subresource), params=params, body=body,
                                   content_type=patch_type)
+
+    async def write_meta(self, verb: str, rt, namespace, body: dict, *, name: str | None = None,
+                         field_manager=None, patch_type=None, force=None) -> tuple:
+        """create/update/patch that returns only (namespace, name, resourceVersion, uid) of the stored object,
+        read from the response by the native scanner instead of decoding it (slim-cache writers publish
+        their own request body; the server's echo of the payload is not needed)."""
+        params = {"fieldManager": field_manager}
+        if verb == "create":
+            method, path = "POST", rt.base_path(namespace)
+        elif verb == "update":
+            method, path = "PUT", rt.item_path(namespace, name or (body.get("metadata") or {}).get("name", ""))
+        else:
+            method, path = "PATCH", rt.item_path(namespace, name)
+            if force is not None:
+                params["force"] = "true" if force else "false"
+        raw = await self.request(method, path, params=params, body=body, raw=True,
+                                 content_type=patch_type if verb == "patch" else _JSON)
+        mod = _native.load()
+        sc = mod.scan_object(raw) if mod is not None else None
+        if sc is None:
+            m = (json.loads(raw) or {}).get("metadata") or {}
+            sc = (m.get("namespace", ""), m.get("name", ""), m.get("resourceVersion", ""), m.get("uid", ""))
+        return sc
 
     async def delete(self, rt, namespace, name, *, propagation_policy=None, preconditions=None):
         body = None

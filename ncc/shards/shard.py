@@ -25,6 +25,7 @@ from ..api import resources as R
 from ..api.objects import ObjectKey, meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
+from .. import native as _native
 from ..kube.client import PATCH_APPLY, KubeClient
 
 
@@ -57,6 +58,8 @@ class Shard:
         self.secret_lister = self.secret_informer.lister
         self.configmap_lister = self.configmap_informer.lister
         self.healthy = True  # flipped by the controller's per-shard circuit breaker
+        # response-light writes need the native scanner and slim caches (see _tracked)
+        self._write_meta = getattr(client, "write_meta", None) if (transforms and _native.load()) else None
         if assume_writes:
             for inf in self.factory.informers():
                 inf.echo_fastpath = True
@@ -75,19 +78,39 @@ class Shard:
     async def wait_for_sync(self, timeout: float | None = None) -> bool:
         return await self.factory.wait_for_sync(timeout)
 
-    async def _tracked(self, informer: Informer, namespace: str, name: str, call):
+    async def _call(self, rt: R.ResourceType, verb: str, namespace: str, name: str, body: dict,
+                    field_manager: str, patch_type=None, force=None):
+        if verb == "create":
+            return await self.client.create(rt, namespace, body, field_manager=field_manager)
+        if verb == "update":
+            return await self.client.update(rt, namespace, body, field_manager=field_manager)
+        return await self.client.patch(rt, namespace, name, body, patch_type=patch_type,
+                                       field_manager=field_manager, force=force)
+
+    async def _tracked(self, informer: Informer, rt: R.ResourceType, verb: str, namespace: str, name: str,
+                       body: dict, field_manager: str, patch_type=None, force=None):
         """Run one write; publish its result to the informer (mutation overlay) and let the informer
-        settle a watch event that overtook the response (see Informer.begin_write)."""
+        settle a watch event that overtook the response (see Informer.begin_write).
+
+        With slim caches, full-object writes (create/update) publish the slim form of the request body
+        with the new resourceVersion/uid read natively from the response — the echoed payload is never
+        decoded.  Partial writes (server-side apply) publish the decoded response."""
         if not self.assume_writes:
-            return await call
+            return await self._call(rt, verb, namespace, name, body, field_manager, patch_type, force)
+        light = self._write_meta is not None and verb != "patch" and informer.store.transform is not None
         key = ObjectKey(namespace, name)
         informer.begin_write(key)
         res = None
         try:
-            res = await call
+            if light:
+                _, _, rv, uid = await self._write_meta(verb, rt, namespace, body, name=name,
+                                                       field_manager=field_manager)
+                res = slim_written(rt, body, rv, uid)
+            else:
+                res = await self._call(rt, verb, namespace, name, body, field_manager, patch_type, force)
             return res
         finally:
-            await informer.end_write(key, res if isinstance(res, dict) else None)
+            await informer.end_write(key, res if isinstance(res, dict) else None, transformed=light)
 
     # ---------------------------------------------------------------- templates
     async def create_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
@@ -97,16 +120,14 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        return await self._tracked(self.template_informer, namespace, name,
-                                   self.client.create(R.TEMPLATES, namespace, obj, field_manager=field_manager))
+        return await self._tracked(self.template_informer, R.TEMPLATES, "create", namespace, name, obj, field_manager)
 
     async def update_template(self, shard_obj: dict, spec, field_manager: str) -> dict:
         obj = _strip_slim(dict(shard_obj))
         obj["spec"] = spec
         m = meta(shard_obj)
-        return await self._tracked(self.template_informer, m.get("namespace", ""), m.get("name", ""),
-                                   self.client.update(R.TEMPLATES, m.get("namespace", ""), obj,
-                                                      field_manager=field_manager))
+        return await self._tracked(self.template_informer, R.TEMPLATES, "update", m.get("namespace", ""),
+                                   m.get("name", ""), obj, field_manager)
 
     async def apply_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
         """Server-side apply (create-or-update in one request; no resourceVersion, no 409 races)."""
@@ -116,9 +137,8 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        return await self._tracked(self.template_informer, namespace, name,
-                                   self.client.patch(R.TEMPLATES, namespace, name, body, patch_type=PATCH_APPLY,
-                                                     field_manager=field_manager, force=True))
+        return await self._tracked(self.template_informer, R.TEMPLATES, "patch", namespace, name, body, field_manager,
+                                   patch_type=PATCH_APPLY, force=True)
 
     async def delete_template(self, obj: dict) -> None:
         m = meta(obj)
@@ -132,16 +152,15 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        return await self._tracked(self.workgroup_informer, namespace, name,
-                                   self.client.create(R.WORKGROUPS, namespace, obj, field_manager=field_manager))
+        return await self._tracked(self.workgroup_informer, R.WORKGROUPS, "create", namespace, name, obj,
+                                   field_manager)
 
     async def update_workgroup(self, shard_obj: dict, spec, field_manager: str) -> dict:
         obj = _strip_slim(dict(shard_obj))
         obj["spec"] = spec
         m = meta(shard_obj)
-        return await self._tracked(self.workgroup_informer, m.get("namespace", ""), m.get("name", ""),
-                                   self.client.update(R.WORKGROUPS, m.get("namespace", ""), obj,
-                                                      field_manager=field_manager))
+        return await self._tracked(self.workgroup_informer, R.WORKGROUPS, "update", m.get("namespace", ""),
+                                   m.get("name", ""), obj, field_manager)
 
     async def apply_workgroup(self, name: str, namespace: str, spec, field_manager: str) -> dict:
         body = {
@@ -150,9 +169,8 @@ class Shard:
             "metadata": {"name": name, "namespace": namespace, "labels": dict(self.labels)},
             "spec": spec,
         }
-        return await self._tracked(self.workgroup_informer, namespace, name,
-                                   self.client.patch(R.WORKGROUPS, namespace, name, body, patch_type=PATCH_APPLY,
-                                                     field_manager=field_manager, force=True))
+        return await self._tracked(self.workgroup_informer, R.WORKGROUPS, "patch", namespace, name, body,
+                                   field_manager, patch_type=PATCH_APPLY, force=True)
 
     async def delete_workgroup(self, obj: dict) -> None:
         m = meta(obj)
@@ -204,15 +222,15 @@ class Shard:
     async def _create_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str):
         body = self._dependent_body(rt, shard_template, src)
         m = body["metadata"]
-        return await self._tracked(self._dep_informer(rt), m["namespace"], m["name"],
-                                   self.client.create(rt, m["namespace"], body, field_manager=field_manager))
+        return await self._tracked(self._dep_informer(rt), rt, "create", m["namespace"], m["name"], body,
+                                   field_manager)
 
     async def _update_dependent(self, rt: R.ResourceType, shard_obj: dict, data, new_owner, field_manager: str,
                                 binary_data=None):
         body = self._updated_dependent(shard_obj, data, new_owner, binary_data)
         m = meta(shard_obj)
-        return await self._tracked(self._dep_informer(rt), m.get("namespace", ""), m.get("name", ""),
-                                   self.client.update(rt, m.get("namespace", ""), body, field_manager=field_manager))
+        return await self._tracked(self._dep_informer(rt), rt, "update", m.get("namespace", ""), m.get("name", ""),
+                                   body, field_manager)
 
     async def create_secret(self, shard_template: dict, secret: dict, field_manager: str) -> dict:
         return await self._create_dependent(R.SECRETS, shard_template, secret, field_manager)
@@ -232,13 +250,33 @@ class Shard:
         """Apply our view of a dependent: owner labels, our ownerRef (merged by uid with other owners'), payload."""
         body = self._dependent_body(rt, shard_template, src)
         m = body["metadata"]
-        return await self._tracked(self._dep_informer(rt), m["namespace"], m["name"],
-                                   self.client.patch(rt, m["namespace"], m["name"], body, patch_type=PATCH_APPLY,
-                                                     field_manager=field_manager, force=True))
+        return await self._tracked(self._dep_informer(rt), rt, "patch", m["namespace"], m["name"], body,
+                                   field_manager, patch_type=PATCH_APPLY, force=True)
 
     async def delete_dependent(self, rt: R.ResourceType, obj: dict) -> None:
         m = meta(obj)
         await self.client.delete(rt, m.get("namespace", ""), m.get("name", ""))
+
+
+_PAYLOAD = {"spec": ("spec", "status"), "data": ("data", "binaryData", "stringData")}
+
+
+def slim_written(rt: R.ResourceType, body: dict, rv: str, uid: str) -> dict:
+    """Slim-cache form of an object we just wrote in full (same shape as reconcile.slim_spec/slim_data)."""
+    from ..api.fingerprint import SLIM_FP, fingerprint
+    is_dep = rt is R.SECRETS or rt is R.CONFIGMAPS
+    drop = _PAYLOAD["data"] if is_dep else _PAYLOAD["spec"]
+    out = {k: v for k, v in body.items() if k not in drop and k != SLIM_FP}
+    m = dict(out.get("metadata") or {})
+    m["resourceVersion"] = rv
+    if uid:
+        m["uid"] = uid
+    out["metadata"] = m
+    if is_dep:
+        out[SLIM_FP] = (fingerprint(body.get("data") or None), fingerprint(body.get("binaryData") or None))
+    else:
+        out[SLIM_FP] = (fingerprint(body.get("spec")),)
+    return out
 
 
 def _strip_slim(obj: dict) -> dict:

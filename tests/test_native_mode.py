@@ -273,3 +273,41 @@ async def test_server_side_apply_writes():
     with pytest.raises(Exception):
         await ctl.sync_template(NS, t2["metadata"]["name"])
     assert env.sstates[0].get(R.CONFIGMAPS, NS, "rogue")["data"] != env.cstate.get(R.CONFIGMAPS, NS, "rogue")["data"]
+
+
+async def test_response_light_writes_match_server_state():
+    """Slim-cache shards publish their own request body (plus the RV/UID scanned from the response): the
+    cached slim object must equal what slim-transforming the server's stored object would give."""
+    from ncc.fakeapi.server import FakeApiServer
+    from ncc.kube.kubeconfig import ClusterConfig
+    from ncc.kube.rest import RestClient
+    from ncc.api.fingerprint import SLIM_FP
+    srv = FakeApiServer(name="s0")
+    client = RestClient(ClusterConfig(server=await srv.start()), cluster_name="s0")
+    slim = {R.TEMPLATES: slim_spec, R.WORKGROUPS: slim_spec, R.SECRETS: slim_data, R.CONFIGMAPS: slim_data}
+    sh = Shard(ALIAS, "s0", client, NS, assume_writes=True, sync_binary_data=True, transforms=slim)
+    try:
+        assert sh._write_meta is not None
+        t = make_template(1, NS)
+        st = await sh.create_template(t["metadata"]["name"], NS, t["spec"], C.FIELD_MANAGER)
+        live = srv.state.get(R.TEMPLATES, NS, t["metadata"]["name"])
+        assert st["metadata"]["uid"] == live["metadata"]["uid"]
+        assert st["metadata"]["resourceVersion"] == live["metadata"]["resourceVersion"]
+        assert st[SLIM_FP] == slim_spec(live)[SLIM_FP] and "spec" not in st
+        sec = await sh.create_secret(st, make_secret("s", NS), C.FIELD_MANAGER)
+        cm = make_configmap("c", NS)
+        cm["binaryData"] = {"b": "AAE="}
+        cmo = await sh.create_configmap(st, cm, C.FIELD_MANAGER)
+        sec2 = await sh.update_secret(sec, {"token": "bmV3"}, None, C.FIELD_MANAGER)
+        for got, rt, nm in ((sec2, R.SECRETS, "s"), (cmo, R.CONFIGMAPS, "c")):
+            live = srv.state.get(rt, NS, nm)
+            want = slim_data(live)
+            assert got[SLIM_FP] == want[SLIM_FP]
+            assert got["metadata"]["resourceVersion"] == live["metadata"]["resourceVersion"]
+            assert got["metadata"]["uid"] == live["metadata"]["uid"]
+            assert got["metadata"]["ownerReferences"] == live["metadata"]["ownerReferences"]
+            assert sh.secret_lister.try_get(NS, "s") is sec2 if rt is R.SECRETS else True
+        assert srv.state.get(R.SECRETS, NS, "s")["data"] == {"token": "bmV3"}
+    finally:
+        await client.close()
+        await srv.stop()
