@@ -72,9 +72,12 @@ class Store:
     def delete(self, obj_or_key) -> dict | None:
         key = obj_or_key if isinstance(obj_or_key, tuple) else key_of(obj_or_key)
         old = self._items.pop(key, None)
-        self._assumed.pop(key, None)
+        rv = -1 if isinstance(obj_or_key, tuple) else \
+            rv_int((obj_or_key.get("metadata") or {}).get("resourceVersion"))
+        a = self._assumed.get(key)
+        if a is not None and not (rv >= 0 and a[1] > rv):
+            del self._assumed[key]  # an overlay newer than the deleted version (we re-created it) survives
         if not isinstance(obj_or_key, tuple):
-            rv = rv_int((obj_or_key.get("metadata") or {}).get("resourceVersion"))
             if rv >= 0:
                 if len(self._tombstones) > 16384:
                     self._tombstones.clear()

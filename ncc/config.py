@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
+`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -81,6 +81,7 @@ class AppConfig:
     client_pool_size: int = 64
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
+    controller_adoption: bool = True  # add template ownerRefs to controller-side Secrets/ConfigMaps (reference)
     executors: int = -1              # shard-executor processes; -1 = auto (native: one per shard, ≤ max)
     max_executors: int = 16
     executors_per_shard: int = -1    # key-partitioned executors per shard group; -1 = auto (app.py)

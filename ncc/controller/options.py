@@ -42,6 +42,10 @@ class ControllerOptions:
     coalesce_window: float = 0.0           # seconds to park event-triggered keys so bursts collapse
     server_side_apply: bool = False       # shard writes as SSA (PATCH apply-patch, force) instead of GET/PUT
     patch_writes: bool = False            # controller.go:434,476,663,686 PUT status/ownerRefs (409-prone)
+    sync_secret_type: bool = False         # controller.go:539 ignores Secret.type (immutable: needs re-create)
+    rogue_event_on_template: bool = False  # controller.go:497 records the event on the *shard* object
+    controller_adoption: bool = True       # controller.go:647-695 adds ownerRefs to controller-side dependents,
+                                           # which makes them GC-deletable with their last template
     role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
     partition: tuple | None = None         # executor: (p, k) → reconcile only keys with key_part(key, k) == p
 
@@ -73,6 +77,8 @@ class ControllerOptions:
             full_resync_period=600.0,
             coalesce_window=0.005,
             patch_writes=True,
+            sync_secret_type=True,
+            rogue_event_on_template=True,
         )
         return replace(base, **kw)
 

@@ -167,7 +167,8 @@ class ReconcileMixin:
         return template
 
     # ============================================================ ownership (controller.go:482-502)
-    def is_missing_ownership(self, obj: dict, owner: dict, kind: str) -> bool:
+    def is_missing_ownership(self, obj: dict, owner: dict, kind: str, template: dict | None = None,
+                             shard_name: str = "") -> bool:
         refs = meta(obj).get("ownerReferences") or []
         if refs:
             owner_uid = meta(owner).get("uid", "") or ""
@@ -176,8 +177,13 @@ class ReconcileMixin:
                     return False
             return True
         msg = C.MESSAGE_RESOURCE_EXISTS.format(q(meta(obj).get("name", "")))
-        # The reference records this against the *shard* object into the controller cluster (controller.go:497).
-        self.recorder.event(obj, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_EXISTS, msg, kind=kind)
+        if self.options.rogue_event_on_template and template is not None:
+            # native: report on the controller-side template the user owns, naming the shard and kind
+            self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_EXISTS,
+                                f"{kind} {msg} (shard {q(shard_name)})", kind=C.TEMPLATE_KIND)
+        else:
+            # The reference records this against the *shard* object into the controller cluster (controller.go:497).
+            self.recorder.event(obj, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_EXISTS, msg, kind=kind)
         raise RogueResourceError(msg)
 
     # ============================================================ adoption (controller.go:647-695)
@@ -196,7 +202,7 @@ class ReconcileMixin:
                     self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
                                         C.MESSAGE_RESOURCE_MISSING.format(q(nm), q(tname)), kind=C.TEMPLATE_KIND)
                     lister.get(ns, nm)  # raises the typed NotFound
-                if not is_owned_by_uid(ref, tuid):
+                if self.options.controller_adoption and not is_owned_by_uid(ref, tuid):
                     m = dict(meta(ref))
                     m["ownerReferences"] = list(m.get("ownerReferences") or []) + [template_owner_ref(template)]
                     args = (rt, ns, with_fields(ref, metadata=m), template, nm, informer)
@@ -425,7 +431,8 @@ class ReconcileMixin:
         if self.options.server_side_apply:
             try:
                 if shard_obj is not None:
-                    missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind)  # rogue → error
+                    missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template,
+                                                              shard.name)  # rogue → error
                     with_binary = self.options.sync_binary_data and not is_secret
                     if not missing_owner and data_matches(src, shard_obj, with_binary):
                         return
@@ -441,9 +448,20 @@ class ReconcileMixin:
             except Exception as e:  # noqa: BLE001
                 raise fail(e)
         try:
-            missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind)
+            missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template, shard.name)
         except RogueResourceError as e:
             raise fail(e)
+        if is_secret and self.options.sync_secret_type and \
+                (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
+            # Secret.type is immutable: replace the shard copy (other owners re-add their refs on their passes)
+            try:
+                self._pass_wrote()
+                await self._delete_one(shard, lambda o: shard.delete_dependent(R.SECRETS, o), shard_obj)
+                shard_obj = await self._write(shard, "create_secret", shard_informer, rt, shard_template, src,
+                                              C.FIELD_MANAGER)
+            except Exception as e:  # noqa: BLE001
+                raise fail(e)
+            return
         with_binary = self.options.sync_binary_data and not is_secret
         differs = not data_matches(src, shard_obj, with_binary)
         update = shard.update_secret if is_secret else shard.update_configmap

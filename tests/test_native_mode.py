@@ -311,3 +311,34 @@ async def test_response_light_writes_match_server_state():
     finally:
         await client.close()
         await srv.stop()
+
+
+async def test_secret_type_change_recreates_shard_copy():
+    env = Env(1)
+    t = env.seed()
+    ctl = env.build()
+    name = t["metadata"]["name"]
+    await ctl.sync_template(NS, name)
+    old_uid = env.sstates[0].get(R.SECRETS, NS, "s")["metadata"]["uid"]
+    src = env.cstate.get(R.SECRETS, NS, "s")
+    env.cstate.update(R.SECRETS, NS, dict(src, type="kubernetes.io/dockerconfigjson"))
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    live = env.sstates[0].get(R.SECRETS, NS, "s")
+    assert live["type"] == "kubernetes.io/dockerconfigjson" and live["metadata"]["uid"] != old_uid
+    st_uid = env.sstates[0].get(R.TEMPLATES, NS, name)["metadata"]["uid"]
+    assert [r["uid"] for r in live["metadata"]["ownerReferences"]] == [st_uid]
+
+
+async def test_rogue_event_on_template_and_adoption_switch():
+    env = Env(1, controller_adoption=False)
+    t = env.seed()
+    env.sstates[0].create(R.CONFIGMAPS, NS, make_configmap("c", NS, version=3))  # rogue: no ownerRefs
+    ctl = env.build()
+    with pytest.raises(ShardSyncError):
+        await ctl.sync_template(NS, t["metadata"]["name"])
+    ev = [e for e in env.recorder.events if "ErrResourceExists" in e]
+    assert ev and "ConfigMap" in ev[0] and 'shard "s0"' in ev[0]
+    # controller-side dependents were not adopted (no GC coupling to the template)
+    assert not env.cstate.get(R.SECRETS, NS, "s")["metadata"].get("ownerReferences")
+    assert not env.cstate.get(R.CONFIGMAPS, NS, "c")["metadata"].get("ownerReferences")
