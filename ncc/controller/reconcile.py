@@ -28,6 +28,15 @@ from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
 log = logging.getLogger("ncc.reconcile")
 
 
+def _write_target(op: str, args: tuple) -> tuple:
+    """(namespace, name) of the object a Shard write op touches, from its positional arguments."""
+    if op in ("create_secret", "create_configmap"):  # (shard_template, src, fm): src's name, template's ns
+        return meta(args[0]).get("namespace", ""), meta(args[1]).get("name", "")
+    if isinstance(args[0], dict):  # update_*(shard_obj, ...)
+        return meta(args[0]).get("namespace", ""), meta(args[0]).get("name", "")
+    return args[1], args[0]  # create_template/create_workgroup(name, ns, ...)
+
+
 class RogueResourceError(Exception):
     """A shard dependent exists without any owner reference (controller.go:494-499)."""
 
@@ -377,11 +386,7 @@ class ReconcileMixin:
             if not self.options.tolerate_write_races:
                 raise
             # Our cache was stale: fetch the live object, publish it, let the caller continue from it.
-            target = args[0]
-            if isinstance(target, dict):
-                ns, nm = meta(target).get("namespace", ""), meta(target).get("name", "")
-            else:
-                nm, ns = args[0], args[1]
+            ns, nm = _write_target(op, args)
             live = await shard.client.get(rt, ns, nm)
             informer.store.assume(live)
             if isinstance(e, E.Conflict) and op.startswith("update"):

@@ -300,3 +300,42 @@ async def test_native_converges_under_faults(tmp_path, executors):
 def aiohttp_session():
     import aiohttp
     return aiohttp.ClientSession()
+
+
+async def test_partitioned_executors_shared_dependents(tmp_path):
+    """Templates in different key partitions sharing one Secret/ConfigMap: each partition's executor adds
+    its own ownerRef (refetch on AlreadyExists/Conflict), and a data change reaches the shard once."""
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    try:
+        T = 12
+        await cc.create(R.SECRETS, NS, make_secret("shared", NS))
+        await cc.create(R.CONFIGMAPS, NS, make_configmap("shared-cm", NS))
+        for i in range(T):
+            await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=["shared"], configmaps=["shared-cm"]))
+        async with Running(env, "native", executors_per_shard=2):
+            async def owned_by_all():
+                uids = {o["metadata"]["uid"] for o in (await sc.list(R.TEMPLATES, NS))["items"]}
+                if len(uids) != T:
+                    return False
+                for rt, nm in ((R.SECRETS, "shared"), (R.CONFIGMAPS, "shared-cm")):
+                    o = await sc.get(rt, NS, nm)
+                    if {r["uid"] for r in o["metadata"].get("ownerReferences") or ()} != uids:
+                        return False
+                return True
+            await wait_for(owned_by_all, timeout=15, interval=0.05)
+            await mutate(cc, R.SECRETS, "shared", lambda o: o.__setitem__("data", {"token": "c2hhcmVk"}))
+
+            async def updated():
+                return (await sc.get(R.SECRETS, NS, "shared")).get("data") == {"token": "c2hhcmVk"}
+            await wait_for(updated, timeout=10)
+
+            async def all_ready():
+                items = (await cc.list(R.TEMPLATES, NS))["items"]
+                return all((o.get("status") or {}).get("conditions", [{}])[0].get("status") == "True"
+                           for o in items)
+            await wait_for(all_ready, timeout=10)
+    finally:
+        await cc.close()
+        await sc.close()
+        await env.stop()

@@ -342,3 +342,14 @@ async def test_rogue_event_on_template_and_adoption_switch():
     # controller-side dependents were not adopted (no GC coupling to the template)
     assert not env.cstate.get(R.SECRETS, NS, "s")["metadata"].get("ownerReferences")
     assert not env.cstate.get(R.CONFIGMAPS, NS, "c")["metadata"].get("ownerReferences")
+
+
+def test_write_target_resolves_the_written_object():
+    from ncc.controller.reconcile import _write_target
+    st = {"metadata": {"name": "algo-1", "namespace": "ns1"}}
+    src = {"metadata": {"name": "sec", "namespace": "ctl"}}
+    assert _write_target("create_secret", (st, src, "fm")) == ("ns1", "sec")
+    assert _write_target("create_configmap", (st, src, "fm")) == ("ns1", "sec")
+    assert _write_target("update_secret", (dict(src), None, None, "fm")) == ("ctl", "sec")
+    assert _write_target("create_template", ("algo-1", "ns1", {}, "fm")) == ("ns1", "algo-1")
+    assert _write_target("update_template", (st, {}, "fm")) == ("ns1", "algo-1")
