@@ -113,11 +113,14 @@ def cpu_share() -> int:
 
 
 def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
-    """Two key-partitioned executors per shard group when there are ≥ 4 CPUs per group (measured on
-    MI355X hosts: +48% objects/s at one shard; a third executor adds no throughput because every
-    executor decodes the full watch streams), else one."""
+    """Key-partitioned executors per shard group: about 3/4 of the CPUs across all executors, 1..3 each.
+
+    Measured on the MI355X host under a 16-CPU quota (profiles/r1/kscan, BENCHMARKS.md): at 4 shards
+    k=3 beat k=2 by ~25 % and k=1 by ~60 %; beyond 3 per shard every executor's share of replicated
+    watch decoding outweighs the split."""
+    import math
     cpus = cpu_share() if cpus is None else cpus
-    return 2 if cpus >= 4 * max(1, groups) else 1
+    return max(1, min(3, math.ceil(0.75 * cpus / max(1, groups))))
 
 
 class App:
