@@ -77,6 +77,19 @@ def client_limits(cfg: AppConfig) -> tuple[float, int]:
     return 0.0, cfg.client_burst
 
 
+def shard_files(path: str) -> dict:
+    """{shard name: sha256 of its kubeconfig} for the shard config directory."""
+    import hashlib
+    out = {}
+    for name, p in discover(path):
+        try:
+            with open(p, "rb") as f:
+                out[name] = hashlib.sha256(f.read()).hexdigest()
+        except OSError:
+            continue
+    return out
+
+
 def strip_payload(obj: dict) -> dict:
     return {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
 
@@ -145,6 +158,8 @@ class App:
         self.controller: Controller | None = None
         self.elector: LeaderElector | None = None
         self._lease_task = None
+        self._reload_task = None
+        self._shard_files: dict = {}
         self.lost_leadership = False
 
     async def build(self) -> Controller:
@@ -170,6 +185,7 @@ class App:
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
         all_names = [n for n, _ in discover(cfg.shard_config_path)]
+        self._shard_files = shard_files(cfg.shard_config_path)
         if o.role == "all" and o.mode == "native" and all_names:
             n = cfg.executors if cfg.executors >= 0 else len(all_names)
             self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
@@ -207,6 +223,48 @@ class App:
             self.ops = OpsServer(ready=self._ready,
                                  prometheus=prom, extra=self.debug_state)
         return self.controller
+
+    async def reload_shards(self) -> dict:
+        """Re-scan the shard kubeconfig directory and apply additions, removals and credential changes
+        without a restart (the reference loads shards once at startup, main.go:73).  Returns the diff."""
+        cfg, ctl = self.cfg, self.controller
+        now = shard_files(cfg.shard_config_path)
+        if self.shard_filter is not None:
+            now = {n: h for n, h in now.items() if n in self.shard_filter}
+        old = self._shard_files
+        removed = sorted(set(old) - set(now))
+        added = sorted(set(now) - set(old))
+        changed = sorted(n for n in set(now) & set(old) if now[n] != old[n])
+        if not (removed or added or changed):
+            return {}
+        log.info("shard set changed: added=%s removed=%s changed=%s", added, removed, changed)
+        if self.options.role == "coordinator":
+            if self.pool is not None:
+                await self.pool.remove_shards(removed + changed)
+                self.pool.add_shards(added + changed)
+            ctl.set_shard_names(sorted(now))
+        else:
+            for n in removed + changed:
+                await ctl.remove_shard(n)
+            o = self.options
+            for shard in load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
+                                     client_factory=self.client_factory,
+                                     resync_period=0.0 if o.watch_shards else o.resync_period,
+                                     assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
+                                     slim=o.slim_shard_cache, start=False, names=set(added + changed)):
+                ctl.add_shard(shard)
+            self.shards = list(ctl.shards)
+        self._shard_files = now
+        ctl.enqueue_all()  # fan everything out to new shards; statuses drop removed ones
+        return {"added": added, "removed": removed, "changed": changed}
+
+    async def _reload_loop(self, period: float) -> None:
+        while True:
+            await asyncio.sleep(period)
+            try:
+                await self.reload_shards()
+            except Exception as e:  # noqa: BLE001 — a bad kubeconfig must not kill the controller
+                log.error("shard reload failed: %s", e)
 
     def _ready(self) -> bool:
         """Ready once caches synced and workers run — or while standing by for the leader Lease."""
@@ -259,6 +317,8 @@ class App:
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
                                      env=env, per_shard=self.per_shard)
             self.pool.start()
+        if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
+            self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
                  "executors=%d×%d workers=%d", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
@@ -270,9 +330,10 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
-        if self._lease_task is not None:
-            self._lease_task.cancel()
-            await asyncio.gather(self._lease_task, return_exceptions=True)
+        for t in (self._lease_task, self._reload_task):
+            if t is not None:
+                t.cancel()
+                await asyncio.gather(t, return_exceptions=True)
         if self.pool is not None:
             await self.pool.stop()
         if isinstance(self.recorder, BroadcastRecorder):

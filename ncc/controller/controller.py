@@ -401,6 +401,34 @@ class Controller(ReconcileMixin):
                 log.exception("worker crashed; restarting in 1s")
                 await asyncio.sleep(1.0)
 
+    # ------------------------------------------------------------------ shard membership (hot reload)
+    def add_shard(self, shard) -> None:
+        """Start serving a new shard (in-process shards; the coordinator uses `set_shard_names`)."""
+        self.shards.append(shard)
+        if self.options.watch_shards:
+            self._register_shard_handlers(shard)
+        shard.start()
+        if shard.name not in self.all_shard_names:
+            self.all_shard_names.append(shard.name)
+
+    async def remove_shard(self, name: str) -> None:
+        for shard in [s for s in self.shards if s.name == name]:
+            self.shards.remove(shard)
+            await shard.stop()
+        if name in self.all_shard_names:
+            self.all_shard_names.remove(name)
+        for st in self.shard_state.values():
+            st.pop(name, None)
+
+    def set_shard_names(self, names: list[str]) -> None:
+        """Coordinator: the shard set changed; statuses are re-derived from the executors' reports."""
+        gone = set(self.all_shard_names) - set(names)
+        self.all_shard_names = list(names)
+        if gone:
+            for st in self.shard_state.values():
+                for n in gone:
+                    st.pop(n, None)
+
     async def wait_for_caches(self) -> bool:
         """Run's cache barrier (controller.go:862-871)."""
         ok = await asyncio.gather(*(i.wait_for_sync() for i in (self.secret_informer, self.configmap_informer,

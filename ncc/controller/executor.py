@@ -146,9 +146,42 @@ class ExecutorPool:
     each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1):
-        per_shard = max(1, per_shard)
-        self.handles = [ExecutorHandle(g * per_shard + p, group, on_message, env, p, per_shard)
-                        for g, group in enumerate(partition(shard_names, n)) for p in range(per_shard)]
+        self.per_shard = max(1, per_shard)
+        self.on_message = on_message
+        self.env = env
+        self._next_index = 0
+        self.handles: list[ExecutorHandle] = []
+        for group in partition(shard_names, n):
+            self._new_group(group)
+
+    def _new_group(self, shards: list[str]) -> list[ExecutorHandle]:
+        hs = [ExecutorHandle(self._next_index + p, list(shards), self.on_message, self.env, p, self.per_shard)
+              for p in range(self.per_shard)]
+        self._next_index += self.per_shard
+        self.handles.extend(hs)
+        return hs
+
+    def add_shards(self, names: list[str]) -> None:
+        """Hot-add: one new executor group per added shard (started immediately)."""
+        for n in names:
+            for h in self._new_group([n]):
+                h.start()
+
+    async def remove_shards(self, names: list[str]) -> None:
+        """Hot-remove: stop every group that serves a removed shard; respawn it for its remaining shards."""
+        gone = set(names)
+        hit = [h for h in self.handles if gone & set(h.shards)]
+        groups = {tuple(h.shards) for h in hit}
+        await asyncio.gather(*(h.stop() for h in hit))
+        self.handles = [h for h in self.handles if h not in hit]
+        for g in groups:
+            rest = [s for s in g if s not in gone]
+            if rest:
+                for h in self._new_group(rest):
+                    h.start()
+
+    def shards(self) -> list[str]:
+        return sorted({s for h in self.handles for s in h.shards})
 
     def start(self) -> None:
         for h in self.handles:

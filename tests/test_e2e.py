@@ -339,3 +339,37 @@ async def test_partitioned_executors_shared_dependents(tmp_path):
         await cc.close()
         await sc.close()
         await env.stop()
+
+
+@pytest.mark.parametrize("executors", [0, -1])
+async def test_shard_hot_reload(tmp_path, executors):
+    """Adding/removing a `<cluster>.kubeconfig` in the shards directory takes effect without a restart
+    (the reference loads shards once at startup, main.go:73)."""
+    import os
+    import shutil
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc, s0, s1 = env.controller_client(), env.shard_client(0), env.shard_client(1)
+    parked = os.path.join(str(tmp_path), "shard-1.kubeconfig.parked")
+    shutil.move(os.path.join(env.shard_dir, "shard-1.kubeconfig"), parked)
+
+    async def status_is(shards):
+        o = await cc.get(R.TEMPLATES, NS, "algo-00000")
+        st = o.get("status") or {}
+        return st.get("syncedToClusters") == shards and st["conditions"][0]["status"] == "True"
+    try:
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=[], configmaps=[]))
+        async with Running(env, "native", executors=executors, shard_reload_period=0) as app:
+            await wait_for(lambda: status_is(["shard-0"]), timeout=5)
+            shutil.move(parked, os.path.join(env.shard_dir, "shard-1.kubeconfig"))
+            diff = await app.reload_shards()
+            assert diff == {"added": ["shard-1"], "removed": [], "changed": []}
+            await wait_for(lambda: _get(s1, R.TEMPLATES, "algo-00000"), timeout=10)
+            await wait_for(lambda: status_is(["shard-0", "shard-1"]), timeout=10)
+            os.remove(os.path.join(env.shard_dir, "shard-0.kubeconfig"))
+            assert (await app.reload_shards())["removed"] == ["shard-0"]
+            await wait_for(lambda: status_is(["shard-1"]), timeout=10)
+            assert await app.reload_shards() == {}
+    finally:
+        for c in (cc, s0, s1):
+            await c.close()
+        await env.stop()
