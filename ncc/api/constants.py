@@ -31,6 +31,11 @@ FIELD_MANAGER = CONTROLLER_AGENT_NAME
 METRIC_NAMESPACE = "nexus_configuration_controller"
 RECONCILE_LATENCY_METRIC = "reconcile_latency"
 WORKQUEUE_LENGTH_METRIC = "workqueue_length"
+# native-mode operational metrics (not in the reference)
+RECONCILE_ERRORS_METRIC = "reconcile_errors"          # count, tag kind
+SHARD_SYNC_ERRORS_METRIC = "shard_sync_errors"        # count, tag shard (coordinator, from executor reports)
+SHARDS_METRIC = "shards"                              # gauge: shards served
+LEADER_METRIC = "leader"                              # gauge 1/0 when leader election is on
 
 # Event reasons, controller.go:60-70
 SUCCESS_SYNCED = "Synced"

@@ -261,10 +261,18 @@ class App:
     async def _reload_loop(self, period: float) -> None:
         while True:
             await asyncio.sleep(period)
+            self._gauges()
             try:
                 await self.reload_shards()
             except Exception as e:  # noqa: BLE001 — a bad kubeconfig must not kill the controller
                 log.error("shard reload failed: %s", e)
+
+    def _gauges(self) -> None:
+        if self.metrics is None or self.controller is None:
+            return
+        self.metrics.gauge(C.SHARDS_METRIC, len(self.controller.all_shard_names))
+        if self.elector is not None:
+            self.metrics.gauge(C.LEADER_METRIC, 1 if self.elector.leading else 0)
 
     def _ready(self) -> bool:
         """Ready once caches synced and workers run — or while standing by for the leader Lease."""

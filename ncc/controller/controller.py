@@ -287,6 +287,8 @@ class Controller(ReconcileMixin):
         uid, gen = msg["u"], msg["g"]
         for shard, err in msg["r"].items():
             st[shard] = (uid, gen, err)
+            if err:
+                self.metrics.count(C.SHARD_SYNC_ERRORS_METRIC, 1, {"shard": shard})
         if msg.get("w"):
             self._pending_event.add(key)
         # Only a complete set of reports for this object version can change its status: re-evaluate
@@ -382,6 +384,8 @@ class Controller(ReconcileMixin):
                 self.stats["errors"] += 1
                 log.info("Error syncing %s; re-queuing for later retry: %s", key, e)
                 self.queue.add_rate_limited(key)
+                if self.options.mode == "native":
+                    self.metrics.count(C.RECONCILE_ERRORS_METRIC, 1, {"kind": kind})
         finally:
             self.metrics.gauge(C.WORKQUEUE_LENGTH_METRIC, depth)
             self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, start)

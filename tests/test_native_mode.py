@@ -353,3 +353,20 @@ def test_write_target_resolves_the_written_object():
     assert _write_target("update_secret", (dict(src), None, None, "fm")) == ("ctl", "sec")
     assert _write_target("create_template", ("algo-1", "ns1", {}, "fm")) == ("ns1", "algo-1")
     assert _write_target("update_template", (st, {}, "fm")) == ("ns1", "algo-1")
+
+
+async def test_operational_metrics():
+    from ncc.telemetry.statsd import MemoryMetrics
+    env = Env(1)
+    t = env.seed()
+    ctl = env.build()
+    ctl.metrics = MemoryMetrics()
+    env.sclients[0].prepend_reactor("create", "*", lambda a: (True, None, E.ServiceUnavailable("down")))
+    ctl.queue.add(make_key(C.KIND_TEMPLATE, NS, t["metadata"]["name"]))
+    assert await ctl.process_next_work_item()
+    v = ctl.metrics.values
+    assert v[C.RECONCILE_ERRORS_METRIC] == [1.0] and v[C.WORKQUEUE_LENGTH_METRIC] and v[C.RECONCILE_LATENCY_METRIC]
+    # coordinator side: an executor report carrying a shard error is counted per shard
+    ctl.on_executor_message(0, {"t": "report", "k": make_key(C.KIND_TEMPLATE, NS, "x"), "u": "u", "g": 1,
+                                "r": {"s0": "ServiceUnavailable: down"}, "w": False})
+    assert v[C.SHARD_SYNC_ERRORS_METRIC] == [1.0]
