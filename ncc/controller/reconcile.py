@@ -54,11 +54,12 @@ class ShardSyncError(Exception):
 
 
 # ---------------------------------------------------------------- equality helpers
-def spec_matches(desired_spec, shard_obj: dict) -> bool:
-    """reflect.DeepEqual(shard.Spec, template.Spec) — O(1) against a slim-cache digest."""
+def spec_matches(desired_spec, shard_obj: dict, desired_fp: int | None = None) -> bool:
+    """reflect.DeepEqual(shard.Spec, template.Spec) — O(1) against a slim-cache digest.  `desired_fp`
+    lets a multi-shard pass fingerprint the desired spec once."""
     fp = shard_obj.get(SLIM_FP)
     if fp is not None:
-        return fingerprint(desired_spec) == fp[0]
+        return (desired_fp if desired_fp is not None else fingerprint(desired_spec)) == fp[0]
     return desired_spec == shard_obj.get("spec")
 
 
@@ -122,7 +123,7 @@ class ReconcileMixin:
                 ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Algorithm {q(name)} initializing")]))
             self._pass_wrote()
             res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""), new,
-                                                  field_manager=C.FIELD_MANAGER)
+                                           field_manager=C.FIELD_MANAGER)
             return self._assume(self.template_informer, res)
         return template
 
@@ -134,7 +135,7 @@ class ReconcileMixin:
                 ready_condition(now_rfc3339(), C.CONDITION_FALSE, f"Workgroup {q(name)} initializing")]))
             self._pass_wrote()
             res = await self._write_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""), new,
-                                                  field_manager=C.FIELD_MANAGER)
+                                           field_manager=C.FIELD_MANAGER)
             return self._assume(self.workgroup_informer, res)
         return workgroup
 
@@ -151,8 +152,7 @@ class ReconcileMixin:
             conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
             self._pass_wrote()
             res = await self._write_status(R.WORKGROUPS, meta(workgroup).get("namespace", ""),
-                                                  with_fields(workgroup, status=new_status),
-                                                  field_manager=C.FIELD_MANAGER)
+                                           with_fields(workgroup, status=new_status), field_manager=C.FIELD_MANAGER)
             return self._assume(self.workgroup_informer, res)
         return workgroup
 
@@ -170,8 +170,7 @@ class ReconcileMixin:
             conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
             self._pass_wrote()
             res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""),
-                                                  with_fields(template, status=new_status),
-                                                  field_manager=C.FIELD_MANAGER)
+                                           with_fields(template, status=new_status), field_manager=C.FIELD_MANAGER)
             return self._assume(self.template_informer, res)
         return template
 
@@ -303,7 +302,8 @@ class ReconcileMixin:
             self.secret_lister.get(ns, nm)
         for nm in configmap_names(template):
             self.configmap_lister.get(ns, nm)
-        results = await gather_all(self._sync_template_to_shard(template, s, None) for s in self.shards)
+        spec_fp = fingerprint(template.get("spec")) if len(self.shards) > 1 and self.options.slim_shard_cache else None
+        results = await gather_all(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards)
         failures = {}
         for s, r in zip(self.shards, results):
             if isinstance(r, asyncio.CancelledError):
@@ -353,10 +353,10 @@ class ReconcileMixin:
         spec = template.get("spec")
         shard_template = shard.template_lister.try_get(ns, name)
         if self.options.server_side_apply:
-            if shard_template is None or not spec_matches(spec, shard_template):
+            if shard_template is None or not spec_matches(spec, shard_template, spec_fp):
                 self._pass_wrote()
                 shard_template = await shard.apply_template(name, ns, spec, C.FIELD_MANAGER)
-        elif shard_template is not None and not spec_matches(spec, shard_template):
+        elif shard_template is not None and not spec_matches(spec, shard_template, spec_fp):
             log.debug("Content changed for NexusAlgorithmTemplate %s, updating", name)
             shard_template = await self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
                                                shard_template, spec, C.FIELD_MANAGER)
