@@ -296,7 +296,8 @@ class ClusterState:
                 raise E.BadRequest("resourceVersion should not be set on objects to be created")
             m["uid"] = str(uuid.uuid4())
             m["creationTimestamp"] = now_rfc3339()
-            m["generation"] = 1
+            if rt.group:  # CRDs carry metadata.generation; core Secrets/ConfigMaps do not
+                m["generation"] = 1
             m["resourceVersion"] = str(self._next_rv())
             obj["apiVersion"] = rt.api_version
             obj["kind"] = rt.kind
@@ -351,7 +352,7 @@ class ClusterState:
                     new["status"] = cur["status"]
                 else:
                     new.pop("status", None)
-            if _content(new) != _content(cur):
+            if rt.group and _content(new) != _content(cur):
                 nm["generation"] = int(cm.get("generation", 1)) + 1
         new["metadata"]["resourceVersion"] = cm.get("resourceVersion")
         if new == cur:
