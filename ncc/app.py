@@ -151,7 +151,7 @@ class App:
         self.per_shard = 1
         qps, burst = client_limits(cfg)
         self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size,
-                                                                       cfg.transport)
+                                                                       cfg.transport, cfg.client_pipeline_depth)
         self._controller_client = controller_client
         self.metrics = metrics
         self.ops = None
@@ -176,6 +176,7 @@ class App:
         if client is None:
             qps, burst = client_limits(cfg)
             client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.client_pool_size,
+                                pipeline_depth=cfg.client_pipeline_depth,
                                 cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)

@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -79,6 +79,7 @@ class AppConfig:
     client_qps: float = 0.0          # 0 = unlimited (compat mode forces client-go's 5/10)
     client_burst: int = 10
     client_pool_size: int = 64
+    client_pipeline_depth: int = 1   # >1: HTTP/1.1-pipeline requests once all pool connections are busy
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     controller_adoption: bool = True  # add template ownerRefs to controller-side Secrets/ConfigMaps (reference)

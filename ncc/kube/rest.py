@@ -77,7 +77,8 @@ def _query(params: dict) -> str:
 
 class RestClient(KubeClient):
     def __init__(self, cfg: ClusterConfig, *, pool_size: int = 64, request_timeout: float = 30.0,
-                 max_retries: int = 5, cluster_name: str | None = None, transport: str = "fast"):
+                 max_retries: int = 5, cluster_name: str | None = None, transport: str = "fast",
+                 pipeline_depth: int = 1):
         if transport not in ("fast", "aiohttp"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -85,6 +86,7 @@ class RestClient(KubeClient):
         self.cfg = cfg
         self.cluster_name = cluster_name or cfg.name or cfg.server
         self.pool_size = pool_size
+        self.pipeline_depth = pipeline_depth
         self.request_timeout = request_timeout
         self.max_retries = max_retries
         self.creds = CredentialSource(cfg)
@@ -114,7 +116,8 @@ class RestClient(KubeClient):
                     ctx = _ssl_context(self.cfg, exec_cert)
                     self._pool = ConnectionPool(self.cfg.server, ssl_context=ctx or None,
                                                 server_hostname=self.cfg.tls_server_name, max_size=self.pool_size,
-                                                connect_timeout=self.request_timeout)
+                                                connect_timeout=self.request_timeout,
+                                                pipeline_depth=self.pipeline_depth)
         return self._pool
 
     async def _send(self, method: str, target: str, headers: dict, data):

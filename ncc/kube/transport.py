@@ -5,7 +5,9 @@ multidict headers, tracing hooks and timers.  A controller that fans every chang
 clusters is bound by exactly that per-request cost, so the default transport speaks the small
 subset of HTTP/1.1 a kube-apiserver needs directly on asyncio transports:
 
-* one TCP (or TLS) connection per in-flight request, reused from an idle pool (keep-alive);
+* keep-alive connections from a bounded pool; with `pipeline_depth > 1`, once every connection is
+  busy further requests are pipelined (HTTP/1.1) onto the least-loaded one, and all requests queued on
+  a connection within one loop iteration go out in a single write;
 * pre-encoded request heads, `Content-Length` bodies;
 * response framing by `Content-Length` or `Transfer-Encoding: chunked`, incremental parsing
   in `data_received` (no per-byte Python loops);
@@ -35,7 +37,8 @@ class _Response:
 
 
 class _Conn(asyncio.Protocol):
-    """One HTTP/1.1 connection; handles one exchange at a time."""
+    """One HTTP/1.1 connection.  Requests are answered in order (`pending` futures, FIFO); a streaming
+    (watch) connection carries exactly one exchange."""
 
     HIGH_WATER = 64
 
@@ -45,10 +48,17 @@ class _Conn(asyncio.Protocol):
         self.buf = bytearray()
         self.closed = False
         self.uses = 0
+        self.pending: deque = deque()
+        self._out: list = []
+        self._flush_handle = None
+        self.stream: deque | None = None
         self._reset()
 
+    @property
+    def fut(self) -> asyncio.Future | None:
+        return self.pending[0] if self.pending else None
+
     def _reset(self):
-        self.fut: asyncio.Future | None = None
         self.head_done = False
         self.status = 0
         self.headers: dict = {}
@@ -57,7 +67,6 @@ class _Conn(asyncio.Protocol):
         self.until_close = False
         self.body = bytearray()
         self.chunk_left = -1  # bytes left in current chunk (-1: expecting size line)
-        self.stream: deque | None = None
         self.stream_event: asyncio.Event | None = None
         self.stream_done = False
         self.linebuf = bytearray()
@@ -70,11 +79,14 @@ class _Conn(asyncio.Protocol):
 
     def connection_lost(self, exc):
         self.closed = True
-        if self.fut is not None and not self.fut.done():
-            if self.until_close and self.head_done:
-                self.fut.set_result(_Response(self.status, self.headers, bytes(self.body)))
-            else:
-                self.fut.set_exception(E.TransportError(f"connection lost: {exc or 'closed by peer'}"))
+        fut = self.fut
+        if fut is not None and not fut.done() and self.until_close and self.head_done:
+            self.pending.popleft()
+            fut.set_result(_Response(self.status, self.headers, bytes(self.body)))
+        while self.pending:
+            f = self.pending.popleft()
+            if not f.done():
+                f.set_exception(E.TransportError(f"connection lost: {exc or 'closed by peer'}"))
         if self.stream is not None:
             self.stream_done = True
             if self.stream_event is not None:
@@ -89,32 +101,43 @@ class _Conn(asyncio.Protocol):
 
     def data_received(self, data: bytes):
         self.buf += data
-        if not self.head_done:
-            i = self.buf.find(_CRLF2)
-            if i < 0:
-                return
-            head = bytes(self.buf[:i])
-            del self.buf[:i + 4]
-            self._parse_head(head)
-        if self.chunked:
-            self._parse_chunks()
-        elif self.clen >= 0:
-            if self.stream is not None:
-                self._feed_stream(bytes(self.buf))
-                self.clen -= len(self.buf)
-                self.buf.clear()
-                if self.clen <= 0:
-                    self._finish()
-            elif len(self.buf) >= self.clen:
+        while True:
+            if not self.head_done:
+                i = self.buf.find(_CRLF2)
+                if i < 0:
+                    return
+                head = bytes(self.buf[:i])
+                del self.buf[:i + 4]
+                self._parse_head(head)
+                if not self.head_done:  # a bodiless response completed inside _parse_head
+                    if self.buf and self.pending:
+                        continue
+                    return
+            if self.chunked:
+                if not self._parse_chunks():
+                    return
+            elif self.clen >= 0:
+                if self.stream is not None:
+                    self._feed_stream(bytes(self.buf))
+                    self.clen -= len(self.buf)
+                    self.buf.clear()
+                    if self.clen <= 0:
+                        self._finish()
+                    return
+                if len(self.buf) < self.clen:
+                    return
                 self.body += self.buf[:self.clen]
                 del self.buf[:self.clen]
                 self._finish()
-        else:  # read until close
-            if self.stream is not None:
-                self._feed_stream(bytes(self.buf))
-            else:
-                self.body += self.buf
-            self.buf.clear()
+            else:  # read until close
+                if self.stream is not None:
+                    self._feed_stream(bytes(self.buf))
+                else:
+                    self.body += self.buf
+                self.buf.clear()
+                return
+            if not self.buf or not self.pending or self.closed:
+                return
 
     def _parse_head(self, head: bytes):
         lines = head.split(b"\r\n")
@@ -143,27 +166,28 @@ class _Conn(asyncio.Protocol):
         if self.clen == 0 and not self.chunked:
             self._finish()
 
-    def _parse_chunks(self):
+    def _parse_chunks(self) -> bool:
+        """Consume complete chunks; True once the terminating chunk (and trailers) were read."""
         buf = self.buf
         while True:
             if self.chunk_left == -1:  # expecting a chunk-size line
                 i = buf.find(b"\r\n")
                 if i < 0:
-                    return
+                    return False
                 size = int(bytes(buf[:i]).split(b";", 1)[0].strip(), 16)
                 del buf[:i + 2]
                 self.chunk_left = size if size else -2
             if self.chunk_left == -2:  # after the last chunk: trailer lines until an empty one
                 j = buf.find(b"\r\n")
                 if j < 0:
-                    return
+                    return False
                 del buf[:j + 2]
                 if j == 0:
                     self._finish()
-                    return
+                    return True
                 continue
             if len(buf) < self.chunk_left + 2:
-                return
+                return False
             data = bytes(buf[:self.chunk_left])
             del buf[:self.chunk_left + 2]
             self.chunk_left = -1
@@ -196,26 +220,41 @@ class _Conn(asyncio.Protocol):
             self.stream_done = True
             self.stream_event.set()
             return
-        fut = self.fut
+        fut = self.pending.popleft() if self.pending else None
         resp = _Response(self.status, self.headers, bytes(self.body))
         keep = self.keep_alive
         self._reset()
-        if keep and not self.closed:
-            self.pool._release(self)
-        else:
-            self.close()
         if fut is not None and not fut.done():
             fut.set_result(resp)
+        if not keep or self.closed:
+            self.close()  # connection_lost fails whatever was pipelined behind this response
+        elif not self.pending:
+            self.pool._release(self)
 
     # ---------------------------------------------------------------- API
     def send(self, data: bytes, stream: bool = False) -> asyncio.Future:
         loop = asyncio.get_running_loop()
-        self.fut = loop.create_future()
+        fut = loop.create_future()
+        self.pending.append(fut)
         if stream:
             self.stream = deque()
             self.stream_event = asyncio.Event()
-        self.transport.write(data)
-        return self.fut
+            self.transport.write(data)
+            return fut
+        if self.pool.pipeline_depth > 1:
+            # requests queued on this connection in the same loop iteration leave in one write
+            self._out.append(data)
+            if self._flush_handle is None:
+                self._flush_handle = loop.call_soon(self._flush)
+        else:
+            self.transport.write(data)
+        return fut
+
+    def _flush(self):
+        self._flush_handle = None
+        out, self._out = self._out, []
+        if out and not self.closed and self.transport is not None:
+            self.transport.write(out[0] if len(out) == 1 else b"".join(out))
 
     def resume(self):
         if self.paused and self.transport is not None and self.stream is not None and \
@@ -232,7 +271,7 @@ class _Conn(asyncio.Protocol):
 
 class ConnectionPool:
     def __init__(self, server: str, *, ssl_context: _ssl.SSLContext | None = None, server_hostname: str | None = None,
-                 max_size: int = 64, connect_timeout: float = 10.0):
+                 max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1):
         u = urlsplit(server)
         self.scheme = u.scheme
         self.host = u.hostname or "127.0.0.1"
@@ -242,8 +281,12 @@ class ConnectionPool:
         self.server_hostname = server_hostname
         self.max_size = max_size
         self.connect_timeout = connect_timeout
+        self.pipeline_depth = max(1, pipeline_depth)
         self._idle: list[_Conn] = []
-        self._sem = asyncio.Semaphore(max_size)
+        self._busy: set = set()  # open connections with requests in flight (pipelining candidates)
+        self._connecting = 0
+        self._wake: asyncio.Future | None = None
+        self._sem = asyncio.Semaphore(max_size * self.pipeline_depth)
         self.opened = 0
 
     async def _connect(self) -> _Conn:
@@ -261,21 +304,46 @@ class ConnectionPool:
         return proto
 
     def _release(self, c: _Conn) -> None:
+        self._busy.discard(c)
         if not c.closed:
             self._idle.append(c)
 
     def _discard(self, c: _Conn) -> None:
+        self._busy.discard(c)
         try:
             self._idle.remove(c)
         except ValueError:
             pass
 
     async def _acquire(self) -> _Conn:
-        while self._idle:
-            c = self._idle.pop()
-            if not c.closed:
-                return c
-        return await self._connect()
+        while True:
+            while self._idle:
+                c = self._idle.pop()
+                if not c.closed:
+                    return c
+            if self.pipeline_depth == 1 or len(self._busy) + self._connecting < self.max_size:
+                break
+            best = None
+            for c in self._busy:
+                if not c.closed and len(c.pending) < self.pipeline_depth and \
+                        (best is None or len(c.pending) < len(best.pending)):
+                    best = c
+            if best is not None:
+                return best
+            if not self._connecting:
+                break  # every connection died: open a fresh one
+            if self._wake is None or self._wake.done():
+                self._wake = asyncio.get_running_loop().create_future()
+            await asyncio.shield(self._wake)  # a connect in progress completes (or fails): pick again
+        self._connecting += 1
+        try:
+            c = await self._connect()
+            self._busy.add(c)
+            return c
+        finally:
+            self._connecting -= 1
+            if self._wake is not None and not self._wake.done():
+                self._wake.set_result(None)
 
     def _head(self, method: str, target: str, headers: dict, body_len: int | None) -> bytes:
         lines = [f"{method} {target} HTTP/1.1".encode()]
@@ -295,6 +363,7 @@ class ConnectionPool:
         and on Python 3.10 can swallow a concurrent cancellation (bpo-42130) — a hang at shutdown."""
         fut = c.fut
         if fut is not None and not fut.done():
+            c.pending.popleft()
             fut.set_exception(E.TransportError(f"{what}: timed out"))
         c.close()
 
@@ -306,6 +375,7 @@ class ConnectionPool:
                 c = await self._acquire()
                 reused = c.uses > 0
                 c.uses += 1
+                self._busy.add(c)
                 data = self._head(method, target, headers, len(body) if body is not None else
                                   (0 if method in ("POST", "PUT", "PATCH") else None))
                 if body:
@@ -368,6 +438,7 @@ class ConnectionPool:
             c.close()
 
     def close(self) -> None:
-        for c in self._idle:
+        for c in list(self._idle) + list(self._busy):
             c.close()
         self._idle.clear()
+        self._busy.clear()

@@ -39,10 +39,10 @@ def discover(shard_config_path: str) -> list[tuple[str, str]]:
 
 
 def default_client_factory(qps: float = 0.0, burst: int = 10, pool_size: int = 64,
-                           transport: str = "fast") -> Callable[[str, str], KubeClient]:
+                           transport: str = "fast", pipeline_depth: int = 1) -> Callable[[str, str], KubeClient]:
     def make(name: str, path: str) -> KubeClient:
         client: KubeClient = RestClient(load_kubeconfig(path, name=name), pool_size=pool_size, cluster_name=name,
-                                        transport=transport)
+                                        transport=transport, pipeline_depth=pipeline_depth)
         if qps > 0:
             client = RateLimitedClient(client, qps, burst)
         return client

@@ -190,3 +190,34 @@ async def test_transport_survives_server_side_close():
     finally:
         await c.close()
         await srv.stop()
+
+
+async def test_pipelined_transport_orders_responses_and_recovers():
+    """pipeline_depth > 1: with both pool connections busy, further requests are pipelined; responses are
+    matched in order (errors included), and a connection the server drops fails over to a fresh one."""
+    srv = FakeApiServer()
+    url = await srv.start()
+    c = RestClient(ClusterConfig(server=url), transport="fast", pool_size=2, pipeline_depth=16)
+    try:
+        res = await asyncio.gather(*(c.create(R.SECRETS, NS, make_secret(f"s{i}", NS)) for i in range(40)))
+        assert [r["metadata"]["name"] for r in res] == [f"s{i}" for i in range(40)]
+        pool = c._pool
+        assert pool.opened <= 2 and srv.state.count(R.SECRETS, NS) == 40
+        # interleaved successes and errors on the same pipelined connections stay matched
+        jobs = []
+        for i in range(40):
+            jobs.append(c.get(R.SECRETS, NS, f"s{i}" if i % 2 == 0 else f"missing{i}"))
+        out = await asyncio.gather(*jobs, return_exceptions=True)
+        for i, r in enumerate(out):
+            if i % 2 == 0:
+                assert r["metadata"]["name"] == f"s{i}"
+            else:
+                assert isinstance(r, E.NotFound)
+        for conn in list(srv._http._conns):
+            conn.transport.close()
+        await asyncio.sleep(0.05)
+        got = await asyncio.gather(*(c.get(R.SECRETS, NS, f"s{i}") for i in range(10)))
+        assert [g["metadata"]["name"] for g in got] == [f"s{i}" for i in range(10)]
+    finally:
+        await c.close()
+        await srv.stop()
