@@ -20,6 +20,7 @@
 //    executor can drop dependents owned only by another partition's templates without decoding them.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
+//  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
 
 #include <pybind11/pybind11.h>
 
@@ -28,6 +29,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -40,7 +42,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 7
+#define NCC_NATIVE_ABI 8
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -595,6 +597,124 @@ py::object scan_event_owners(py::bytes line) {
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u);
 }
 
+
+// ----------------------------------------------------------------------------- JSON encoder
+// dumps(obj) -> bytes: compact JSON (separators "," and ":") of a JSON-shaped Python value, key order
+// preserved.  Non-ASCII text is emitted as UTF-8 (valid JSON; json.loads reads it back identically),
+// so strings need only the quote/backslash/control-character escapes.  Used for request bodies and the
+// fake apiserver's responses and watch lines, where json.dumps was the largest single per-object cost.
+class JsonWriter {
+  public:
+    std::string out;
+
+    void value(PyObject* o, int depth) {
+        if (depth > 512) throw py::value_error("dumps: nesting too deep");
+        if (o == Py_None) {
+            out.append("null", 4);
+        } else if (o == Py_True) {
+            out.append("true", 4);
+        } else if (o == Py_False) {
+            out.append("false", 5);
+        } else if (PyUnicode_Check(o)) {
+            str(o);
+        } else if (PyLong_Check(o)) {
+            int overflow = 0;
+            long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
+            if (overflow) {
+                PyObject* r = PyObject_Str(o);
+                if (!r) throw py::error_already_set();
+                Py_ssize_t n = 0;
+                const char* s = PyUnicode_AsUTF8AndSize(r, &n);
+                out.append(s, static_cast<size_t>(n));
+                Py_DECREF(r);
+            } else {
+                char buf[32];
+                int n = std::snprintf(buf, sizeof buf, "%lld", v);
+                out.append(buf, static_cast<size_t>(n));
+            }
+        } else if (PyFloat_Check(o)) {
+            double d = PyFloat_AS_DOUBLE(o);
+            if (!std::isfinite(d)) throw py::value_error("dumps: out of range float values are not JSON compliant");
+            char* s = PyOS_double_to_string(d, 'r', 0, Py_DTSF_ADD_DOT_0, nullptr);
+            if (!s) throw py::error_already_set();
+            out.append(s);
+            PyMem_Free(s);
+        } else if (PyDict_Check(o)) {
+            out.push_back('{');
+            PyObject *k, *v;
+            Py_ssize_t pos = 0;
+            bool first = true;
+            while (PyDict_Next(o, &pos, &k, &v)) {
+                if (!first) out.push_back(',');
+                first = false;
+                if (PyUnicode_Check(k)) {
+                    str(k);
+                } else {
+                    PyObject* ks = PyObject_Str(k);  // json.dumps coerces int/float/bool keys to strings
+                    if (!ks) throw py::error_already_set();
+                    str(ks);
+                    Py_DECREF(ks);
+                }
+                out.push_back(':');
+                value(v, depth + 1);
+            }
+            out.push_back('}');
+        } else if (PyList_Check(o) || PyTuple_Check(o)) {
+            out.push_back('[');
+            PyObject* seq = o;
+            Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+            PyObject** items = PySequence_Fast_ITEMS(seq);
+            for (Py_ssize_t i = 0; i < n; ++i) {
+                if (i) out.push_back(',');
+                value(items[i], depth + 1);
+            }
+            out.push_back(']');
+        } else {
+            throw py::type_error(std::string("dumps: object of type ") + Py_TYPE(o)->tp_name +
+                                 " is not JSON serializable");
+        }
+    }
+
+  private:
+    void str(PyObject* o) {
+        Py_ssize_t n = 0;
+        const char* s = PyUnicode_AsUTF8AndSize(o, &n);
+        if (!s) throw py::error_already_set();
+        out.push_back('"');
+        const char* run = s;
+        const char* end = s + n;
+        for (const char* p = s; p < end; ++p) {
+            unsigned char c = static_cast<unsigned char>(*p);
+            if (c >= 0x20 && c != '"' && c != '\\') continue;
+            out.append(run, static_cast<size_t>(p - run));
+            run = p + 1;
+            switch (c) {
+                case '"': out.append("\\\"", 2); break;
+                case '\\': out.append("\\\\", 2); break;
+                case '\n': out.append("\\n", 2); break;
+                case '\r': out.append("\\r", 2); break;
+                case '\t': out.append("\\t", 2); break;
+                case '\b': out.append("\\b", 2); break;
+                case '\f': out.append("\\f", 2); break;
+                default: {
+                    char buf[8];
+                    std::snprintf(buf, sizeof buf, "\\u%04x", c);
+                    out.append(buf, 6);
+                }
+            }
+        }
+        out.append(run, static_cast<size_t>(end - run));
+        out.push_back('"');
+    }
+};
+
+py::bytes dumps(py::handle obj) {
+    JsonWriter w;
+    w.out.reserve(1024);
+    w.value(obj.ptr(), 0);
+    return py::bytes(w.out.data(), w.out.size());
+}
+
 // scan_object(body) -> (namespace, name, resourceVersion, uid) of a JSON object's metadata | None
 py::object scan_object(py::bytes body) {
     char* buf = nullptr;
@@ -617,6 +737,7 @@ PYBIND11_MODULE(_native, m) {
     m.def("fingerprint_many", &fingerprint_many, py::arg("objs"));
     m.def("scan_event", &scan_event, py::arg("line"),
           "(type, namespace, name, resourceVersion) of a watch-event line, or None");
+    m.def("dumps", &dumps, py::arg("obj"), "compact JSON bytes of a JSON-shaped value (UTF-8, key order kept)");
     m.def("scan_object", &scan_object, py::arg("body"),
           "(namespace, name, resourceVersion, uid) from an object's metadata without decoding it, or None");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),

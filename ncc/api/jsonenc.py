@@ -1,0 +1,24 @@
+"""Compact JSON encoding for request bodies, responses and watch lines.
+
+Uses the native encoder (`ncc._native.dumps`, ~4x faster than `json.dumps` on Kubernetes objects)
+when the extension is built, else the standard library.  Output is compact (`,`/`:` separators) with
+key order preserved; the native path writes non-ASCII text as UTF-8 instead of `\\u` escapes — both
+are valid JSON and decode identically.
+"""
+from __future__ import annotations
+
+import json
+
+from .. import native as _native
+
+_mod = _native.load()
+_native_dumps = getattr(_mod, "dumps", None) if _mod is not None else None
+
+
+def dumps_bytes(obj) -> bytes:
+    if _native_dumps is not None:
+        try:
+            return _native_dumps(obj)
+        except (TypeError, ValueError):
+            pass  # non-JSON-shaped input (e.g. non-string keys): the stdlib decides
+    return json.dumps(obj, separators=(",", ":")).encode()

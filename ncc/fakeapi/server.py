@@ -28,6 +28,7 @@ import time
 from . import httpserver as web
 
 from ..api import resources as R
+from ..api.jsonenc import dumps_bytes
 from ..aio import wait_timeout
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
@@ -40,7 +41,7 @@ _JSON = "application/json"
 
 
 def _dumps(o) -> bytes:
-    return json.dumps(o, separators=(",", ":")).encode()
+    return dumps_bytes(o)
 
 
 def _status_response(err: E.ApiError) -> web.Response:

@@ -30,6 +30,7 @@ from typing import Callable
 
 from ..api import resources as R
 from ..api import selectors
+from ..api.jsonenc import dumps_bytes
 from ..api.objects import deep_copy, now_rfc3339
 from ..api.patch import apply_patch, json_patch, merge_patch, strategic_merge_patch
 from ..api.resources import ResourceType
@@ -50,7 +51,7 @@ class EventRecord:
     def body(self) -> bytes:
         """The object's JSON, encoded once for the write response and every watch line."""
         if self._body is None:
-            self._body = json.dumps(self.obj, separators=(",", ":")).encode()
+            self._body = dumps_bytes(self.obj)
         return self._body
 
     def line(self) -> bytes:

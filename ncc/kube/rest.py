@@ -23,6 +23,7 @@ from urllib.parse import urlencode
 import aiohttp
 
 from .. import native as _native
+from ..api.jsonenc import dumps_bytes
 from ..api.resources import ResourceType
 from . import errors as E
 from .client import PATCH_MERGE, KubeClient, WatchEvent
@@ -161,7 +162,7 @@ class RestClient(KubeClient):
             target += _query(params)
         data = None
         if body is not None:
-            data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
+            data = body if isinstance(body, (bytes, str)) else dumps_bytes(body)
         refreshed = False
         attempt = 0
         while True:

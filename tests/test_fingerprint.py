@@ -71,3 +71,17 @@ def test_rejects_non_string_keys_and_deep_nesting():
         cur = nxt
     with pytest.raises(ValueError):
         NATIVE.fingerprint(deep)
+
+
+def test_native_json_encoder_roundtrips():
+    """ncc._native.dumps must decode to exactly what json.dumps does (UTF-8 instead of \\u escapes)."""
+    import json
+    from ncc.api.jsonenc import dumps_bytes
+    from ncc.testing.workload import make_secret, make_template
+    cases = [make_secret("s", "ns", payload=700, version=9), make_template(3, "ns", version="v9"),
+             {"a": [1, -2, 2.5, -0.0, 1e300, 1.0, True, False, None], "s": "é☃ \n\t\"\\ \x01 \x1f /",
+              "nested": {"x": {"y": [[], {}]}}, "big": 2 ** 80, "neg": -(2 ** 70)},
+             [], {}, "plain", 7, None]
+    for o in cases:
+        assert json.loads(dumps_bytes(o)) == json.loads(json.dumps(o))
+    assert dumps_bytes({1: "int key"}) == b'{"1":"int key"}'  # stdlib fallback semantics for odd keys
