@@ -22,7 +22,7 @@ import os
 import signal
 import sys
 
-from . import __version__
+from . import __version__, gctune
 from .api import constants as C
 from .api import resources as R
 from .cache.informer import InformerFactory
@@ -159,6 +159,7 @@ class App:
         self.elector: LeaderElector | None = None
         self._lease_task = None
         self._reload_task = None
+        self._gc_task = None
         self._shard_files: dict = {}
         self.lost_leadership = False
 
@@ -326,6 +327,9 @@ class App:
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
                                      env=env, per_shard=self.per_shard)
             self.pool.start()
+        if self.cfg.mode == "native":
+            gctune.tune()
+            self._gc_task = asyncio.ensure_future(gctune.freeze_loop())
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
@@ -339,7 +343,7 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
-        for t in (self._lease_task, self._reload_task):
+        for t in (self._lease_task, self._reload_task, self._gc_task):
             if t is not None:
                 t.cancel()
                 await asyncio.gather(t, return_exceptions=True)

@@ -441,6 +441,9 @@ async def serve(args) -> None:
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ctx.load_cert_chain(args.tls_cert, args.tls_key)
     url = await server.start(args.host, args.port, ctx)
+    from .. import gctune
+    gctune.tune()
+    gc_task = asyncio.ensure_future(gctune.freeze_loop())
     if args.port_file:
         tmp = args.port_file + ".tmp"
         with open(tmp, "w") as f:
@@ -462,6 +465,7 @@ async def serve(args) -> None:
                     return
         asyncio.ensure_future(watch_parent())
     await stop.wait()
+    gc_task.cancel()
     await server.stop()
 
 
