@@ -405,11 +405,35 @@ async def _amain(cfg: AppConfig) -> int:
     return 1 if app.lost_leadership else 0
 
 
+# klog.InitFlags(nil) + flag.Parse() (main.go:36-37): the reference binary accepts klog's flags.  `-v N`
+# maps onto the log level (the reference logs reconcile detail at V(4)); the output-routing flags are
+# accepted and ignored, since logs always go to stdout as structured lines here.
+_KLOG_VALUE_FLAGS = ("log_dir", "log_file", "log_file_max_size", "stderrthreshold", "vmodule", "log_backtrace_at")
+_KLOG_BOOL_FLAGS = ("logtostderr", "alsologtostderr", "add_dir_header", "skip_headers", "skip_log_headers",
+                    "one_output")
+
+
+def _go_style_flags(argv: list) -> list:
+    """Go's flag package takes `-name`, `--name`, `-name=value`; argparse wants `--name` for long names."""
+    out = []
+    for a in argv:
+        if a.startswith("-") and not a.startswith("--") and len(a.split("=", 1)[0]) > 2:
+            a = "-" + a
+        out.append(a)
+    return out
+
+
 def main(argv=None) -> int:
     p = argparse.ArgumentParser(prog="python -m ncc", description="Nexus multi-cluster configuration controller")
     p.add_argument("--config-dir", default=None, help="directory holding appconfig.yaml (default: cwd)")
     p.add_argument("--version", action="store_true")
-    args = p.parse_args(argv)
+    p.add_argument("-v", "--v", type=int, default=None, metavar="N",
+                   help="klog verbosity: N>=4 logs at DEBUG (overrides log-level), N<4 leaves log-level as set")
+    for f in _KLOG_VALUE_FLAGS:
+        p.add_argument(f"--{f}", default=None, help=argparse.SUPPRESS)
+    for f in _KLOG_BOOL_FLAGS:
+        p.add_argument(f"--{f}", nargs="?", const="true", default=None, help=argparse.SUPPRESS)
+    args = p.parse_args(_go_style_flags(list(sys.argv[1:] if argv is None else argv)))
     if args.version:
         print(__version__)
         return 0
@@ -418,6 +442,8 @@ def main(argv=None) -> int:
     except ValueError as e:
         print(f"configuration error: {e}", file=sys.stderr)
         return 1
+    if args.v is not None and args.v >= 4:
+        cfg.log_level = "DEBUG"
     configure_logging(cfg.log_level, cfg.log_format)
     prof_path = os.environ.get("NCC_PROFILE")
     if prof_path:  # host-side profiling of the control loop: NCC_PROFILE=/path/out.prof

@@ -440,6 +440,9 @@ async def serve(args) -> None:
     if args.tls_cert:
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ctx.load_cert_chain(args.tls_cert, args.tls_key)
+        if args.tls_client_ca:  # x509 client auth (kube-apiserver --client-ca-file)
+            ctx.load_verify_locations(cafile=args.tls_client_ca)
+            ctx.verify_mode = ssl.CERT_REQUIRED
     url = await server.start(args.host, args.port, ctx)
     from .. import gctune
     gctune.tune()
@@ -478,6 +481,7 @@ def main(argv=None) -> None:
     p.add_argument("--token")
     p.add_argument("--tls-cert")
     p.add_argument("--tls-key")
+    p.add_argument("--tls-client-ca", help="require client certificates signed by this CA (mutual TLS)")
     p.add_argument("--bookmark-interval", type=float, default=5.0)
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
     p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")

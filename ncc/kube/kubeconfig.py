@@ -157,14 +157,21 @@ def build_config(path: str | None) -> ClusterConfig:
 
 
 def render_kubeconfig(server: str, name: str, *, token: str | None = None, ca_data: bytes | None = None,
-                      insecure: bool = False, namespace: str | None = None, exec_cfg: dict | None = None) -> str:
+                      insecure: bool = False, namespace: str | None = None, exec_cfg: dict | None = None,
+                      client_cert_data: bytes | None = None, client_key_data: bytes | None = None,
+                      tls_server_name: str | None = None) -> str:
     """Write a minimal single-context kubeconfig (used by tests, benches and the Helm README example)."""
     cluster = {"server": server}
     if ca_data:
         cluster["certificate-authority-data"] = base64.b64encode(ca_data).decode()
     if insecure:
         cluster["insecure-skip-tls-verify"] = True
+    if tls_server_name:
+        cluster["tls-server-name"] = tls_server_name
     user: dict = {}
+    if client_cert_data and client_key_data:  # x509 client auth, as in a kind cluster's admin kubeconfig
+        user["client-certificate-data"] = base64.b64encode(client_cert_data).decode()
+        user["client-key-data"] = base64.b64encode(client_key_data).decode()
     if token:
         user["token"] = token
     if exec_cfg:

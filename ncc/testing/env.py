@@ -20,13 +20,15 @@ from ..kube.rest import RestClient
 
 
 def spawn_fakeapi(name: str, port_file: str, *, token: str | None = None, extra: list | None = None,
-                  bookmark_interval: float = 5.0) -> subprocess.Popen:
+                  bookmark_interval: float = 5.0, pki=None) -> subprocess.Popen:
     if os.path.exists(port_file):
         os.remove(port_file)
     cmd = [sys.executable, "-m", "ncc.fakeapi", "--name", name, "--port-file", port_file,
            "--bookmark-interval", str(bookmark_interval), "--parent-pid", str(os.getpid())]
     if token:
         cmd += ["--token", token]
+    if pki is not None:
+        cmd += ["--tls-cert", pki.server_cert, "--tls-key", pki.server_key, "--tls-client-ca", pki.ca_cert]
     cmd += extra or []
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env = dict(os.environ)
@@ -51,7 +53,10 @@ def wait_port_file(path: str, proc: subprocess.Popen | None = None, timeout: flo
 
 class FakeEnvironment:
     def __init__(self, n_shards: int, workdir: str, *, namespace: str = "nexus", token: str | None = None,
-                 subprocesses: bool = False, shard_prefix: str = "shard", bookmark_interval: float = 5.0):
+                 subprocesses: bool = False, shard_prefix: str = "shard", bookmark_interval: float = 5.0,
+                 tls: bool = False, tls_server_name: str | None = None):
+        """`tls=True` serves every apiserver over HTTPS with mutual TLS (a throwaway CA, x509 client auth,
+        like a kind cluster); `tls_server_name` additionally puts `tls-server-name` in the kubeconfigs."""
         self.n_shards = n_shards
         self.workdir = workdir
         self.namespace = namespace
@@ -66,15 +71,22 @@ class FakeEnvironment:
         self.shard_urls: list[str] = []
         self.shard_dir = os.path.join(workdir, "shards")
         self.controller_kubeconfig = os.path.join(workdir, "controller.kubeconfig")
+        self.tls = tls
+        self.tls_server_name = tls_server_name
+        self.pki = None
 
     async def start(self) -> "FakeEnvironment":
         os.makedirs(self.shard_dir, exist_ok=True)
         names = ["controller"] + self.shard_names
+        if self.tls:
+            from .pki import make_pki
+            self.pki = make_pki(os.path.join(self.workdir, "pki"))
         if self.subprocesses:
             files = []
             for n in names:
                 pf = os.path.join(self.workdir, f"{n}.url")
-                self.procs.append(spawn_fakeapi(n, pf, token=self.token, bookmark_interval=self.bookmark_interval))
+                self.procs.append(spawn_fakeapi(n, pf, token=self.token, bookmark_interval=self.bookmark_interval,
+                                                pki=self.pki))
                 files.append(pf)
             urls = [await asyncio.get_running_loop().run_in_executor(None, wait_port_file, f, p)
                     for f, p in zip(files, self.procs)]
@@ -82,18 +94,26 @@ class FakeEnvironment:
             urls = []
             for n in names:
                 s = FakeApiServer(name=n, token=self.token, bookmark_interval=self.bookmark_interval)
-                urls.append(await s.start())
+                urls.append(await s.start(ssl_context=self.pki.server_context() if self.pki else None))
                 if n == "controller":
                     self.controller_server = s
                 else:
                     self.shard_servers.append(s)
         self.controller_url, self.shard_urls = urls[0], urls[1:]
         with open(self.controller_kubeconfig, "w") as f:
-            f.write(render_kubeconfig(self.controller_url, "controller", token=self.token))
+            f.write(self.kubeconfig(self.controller_url, "controller"))
         for n, u in zip(self.shard_names, self.shard_urls):
             with open(os.path.join(self.shard_dir, f"{n}.kubeconfig"), "w") as f:
-                f.write(render_kubeconfig(u, n, token=self.token))
+                f.write(self.kubeconfig(u, n))
         return self
+
+    def kubeconfig(self, url: str, name: str, **kw) -> str:
+        if self.pki is not None:
+            kw.setdefault("ca_data", self.pki.ca_data)
+            kw.setdefault("client_cert_data", self.pki.client_cert_data)
+            kw.setdefault("client_key_data", self.pki.client_key_data)
+            kw.setdefault("tls_server_name", self.tls_server_name)
+        return render_kubeconfig(url, name, token=self.token, **kw)
 
     def app_config(self, mode: str = "native", **kw) -> AppConfig:
         cfg = AppConfig(alias="controller-cluster", controller_config_path=self.controller_kubeconfig,

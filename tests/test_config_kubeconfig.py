@@ -211,3 +211,23 @@ def test_cpu_share_reads_cgroup_quota(tmp_path):
     assert cgroup_cpu_quota(str(tmp_path)) is None
     assert [auto_executors_per_shard(n, cpus=16) for n in (1, 2, 4, 8, 16)] == [3, 3, 3, 2, 1]
     assert auto_executors_per_shard(8, cpus=128) == 3 and auto_executors_per_shard(1, cpus=2) == 2
+
+
+def test_klog_style_flags(monkeypatch, capsys):
+    """main.go:36-37 — klog.InitFlags + flag.Parse: `-v=4` and klog's output flags are accepted, Go style."""
+    import ncc.app as app
+    from ncc.config import AppConfig
+    assert app._go_style_flags(["-v=4", "-logtostderr", "--vmodule=x=2", "-v", "2"]) == \
+        ["-v=4", "--logtostderr", "--vmodule=x=2", "-v", "2"]
+    assert app.main(["-v=4", "-logtostderr=true", "--alsologtostderr", "-stderrthreshold", "INFO", "--version"]) == 0
+    assert capsys.readouterr().out.strip() == app.__version__
+    seen = {}
+
+    async def fake_amain(cfg):
+        seen["level"] = cfg.log_level
+        return 0
+    monkeypatch.setattr(app, "_amain", fake_amain)
+    monkeypatch.setattr(app, "load_config", lambda _d: AppConfig(log_level="INFO"))
+    monkeypatch.setattr(app, "configure_logging", lambda *a, **k: None)
+    assert app.main(["-v=4"]) == 0 and seen["level"] == "DEBUG"
+    assert app.main(["-v", "2"]) == 0 and seen["level"] == "INFO"
