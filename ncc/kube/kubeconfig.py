@@ -18,6 +18,7 @@ import base64
 import datetime as _dt
 import json
 import os
+import time
 from dataclasses import dataclass, field
 
 import yaml
@@ -195,6 +196,28 @@ class CredentialSource:
         self._expiry: float | None = None
         self._lock = asyncio.Lock()
         self.exec_runs = 0
+        self._file_token: str | None = None
+        self._file_read_at = -1e18
+
+    # client-go re-reads a token file at most once a minute (transport.NewCachedFileTokenSource)
+    FILE_TOKEN_PERIOD = 60.0
+
+    def cached_token(self) -> tuple[bool, str | None]:
+        """Synchronous fast path for the per-request Authorization header: (True, token) when no I/O or
+        exec run is needed (static token, a token file read within the last minute, an unexpired exec
+        credential), else (False, None) and the caller awaits `token()`."""
+        cfg = self.cfg
+        if cfg.exec is not None:
+            if (self._token is not None or self._cert is not None) and not self._expired():
+                return True, self._token
+            return False, None
+        if cfg.token:
+            return True, cfg.token
+        if cfg.token_file:
+            if time.monotonic() - self._file_read_at < self.FILE_TOKEN_PERIOD:
+                return True, self._file_token
+            return False, None
+        return True, None
 
     def _expired(self) -> bool:
         if self._expiry is None:
@@ -211,11 +234,14 @@ class CredentialSource:
         if cfg.token:
             return cfg.token
         if cfg.token_file:
-            try:
-                with open(cfg.token_file) as f:  # re-read: projected SA tokens rotate
-                    return f.read().strip()
-            except OSError:
-                return None
+            if force_refresh or time.monotonic() - self._file_read_at >= self.FILE_TOKEN_PERIOD:
+                try:
+                    with open(cfg.token_file) as f:  # re-read periodically: projected SA tokens rotate
+                        self._file_token = f.read().strip()
+                except OSError:
+                    self._file_token = None
+                self._file_read_at = time.monotonic()
+            return self._file_token
         return None
 
     async def exec_client_cert(self) -> tuple | None:

@@ -91,6 +91,7 @@ class RestClient(KubeClient):
         self.request_timeout = request_timeout
         self.max_retries = max_retries
         self.creds = CredentialSource(cfg)
+        self._hdr_cache: dict = {}
         self._session: aiohttp.ClientSession | None = None
         self._session_lock = asyncio.Lock()
         self.stats = {"requests": 0, "retries": 0, "errors": 0, "watch_streams": 0}
@@ -121,12 +122,13 @@ class RestClient(KubeClient):
                                                 pipeline_depth=self.pipeline_depth)
         return self._pool
 
-    async def _send(self, method: str, target: str, headers: dict, data):
-        """One HTTP exchange → (status, raw body, Retry-After header or None)."""
+    async def _send(self, method: str, target: str, headers: dict, data, block: bytes | None = None):
+        """One HTTP exchange → (status, raw body, Retry-After header or None).  `block` is the pre-rendered
+        header section of `headers` (fast transport)."""
         if self.transport == "fast":
-            pool = await self._get_pool()
+            pool = self._pool or await self._get_pool()
             body = data.encode() if isinstance(data, str) else data
-            resp = await pool.request(method, target, headers, body, timeout=self.request_timeout)
+            resp = await pool.request(method, target, headers, body, timeout=self.request_timeout, block=block)
             return resp.status, resp.body, resp.headers.get("retry-after")
         session = await self._get_session()
         try:
@@ -138,10 +140,26 @@ class RestClient(KubeClient):
             raise E.TransportError(f"{method} {target}: {type(e).__name__}: {e}") from e
 
     async def _headers(self, content_type: str | None, refresh: bool = False) -> dict:
+        return self._render_headers(content_type, await self.creds.token(force_refresh=refresh))[0]
+
+    def _headers_now(self, content_type: str | None) -> tuple | None:
+        """(headers, rendered header block) without awaiting when the credential is at hand; memoised per
+        (content type, token), so steady-state requests build no header dict and no header bytes."""
+        hit, tok = self.creds.cached_token()
+        if not hit:
+            return None
+        key = (content_type, tok)
+        got = self._hdr_cache.get(key)
+        if got is None:
+            if len(self._hdr_cache) > 16:  # rotated tokens: keep the cache small
+                self._hdr_cache.clear()
+            got = self._hdr_cache[key] = self._render_headers(content_type, tok)
+        return got
+
+    def _render_headers(self, content_type: str | None, tok: str | None) -> tuple:
         h = {"User-Agent": USER_AGENT, "Accept": _JSON}
         if content_type:
             h["Content-Type"] = content_type
-        tok = await self.creds.token(force_refresh=refresh)
         if tok:
             h["Authorization"] = f"Bearer {tok}"
         elif self.cfg.username is not None:
@@ -150,7 +168,8 @@ class RestClient(KubeClient):
                 f"{self.cfg.username}:{self.cfg.password or ''}".encode()).decode()
         if self.cfg.tls_server_name:
             h["Host"] = self.cfg.tls_server_name
-        return h
+        block = b"".join(f"{k}: {v}\r\n".encode("latin-1") for k, v in h.items())
+        return h, block
 
     async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
                       content_type: str = _JSON, raw: bool = False):
@@ -165,11 +184,14 @@ class RestClient(KubeClient):
             data = body if isinstance(body, (bytes, str)) else dumps_bytes(body)
         refreshed = False
         attempt = 0
+        ctype = content_type if data is not None else None
         while True:
             self.stats["requests"] += 1
-            headers = await self._headers(content_type if data is not None else None)
+            got = None if refreshed else self._headers_now(ctype)
+            if got is None:
+                got = self._render_headers(ctype, await self.creds.token())
             try:
-                status, body_bytes, retry_after = await self._send(method, target, headers, data)
+                status, body_bytes, retry_after = await self._send(method, target, got[0], data, got[1])
             except E.TransportError:
                 self.stats["errors"] += 1
                 raise
@@ -177,7 +199,7 @@ class RestClient(KubeClient):
                 if raw_out:
                     return bytes(body_bytes)
                 return json.loads(body_bytes) if body_bytes else None
-            if status == 401 and self.cfg.exec is not None and not refreshed:
+            if status == 401 and (self.cfg.exec is not None or self.cfg.token_file) and not refreshed:
                 refreshed = True
                 await self.creds.token(force_refresh=True)
                 continue

@@ -52,6 +52,9 @@ class _Conn(asyncio.Protocol):
         self._out: list = []
         self._flush_handle = None
         self.stream: deque | None = None
+        self.deadline: float | None = None  # loop time by which the in-flight exchange must complete
+        self.deadline_what = ""
+        self.timed_out = False
         self._reset()
 
     @property
@@ -286,7 +289,10 @@ class ConnectionPool:
         self._busy: set = set()  # open connections with requests in flight (pipelining candidates)
         self._connecting = 0
         self._wake: asyncio.Future | None = None
-        self._sem = asyncio.Semaphore(max_size * self.pipeline_depth)
+        self._limit = max_size * self.pipeline_depth
+        self._inflight = 0
+        self._slot_waiters: deque = deque()
+        self._sweep_handle = None
         self.opened = 0
 
     async def _connect(self) -> _Conn:
@@ -345,59 +351,112 @@ class ConnectionPool:
             if self._wake is not None and not self._wake.done():
                 self._wake.set_result(None)
 
-    def _head(self, method: str, target: str, headers: dict, body_len: int | None) -> bytes:
-        lines = [f"{method} {target} HTTP/1.1".encode()]
-        if "Host" not in headers:
-            lines.append(b"Host: " + self.host_header)
-        for k, v in headers.items():
-            lines.append(f"{k}: {v}".encode())
-        if body_len is not None:
-            lines.append(b"Content-Length: " + str(body_len).encode())
-        return b"\r\n".join(lines) + _CRLF2
+    def _head(self, method: str, target: str, headers: dict, body_len: int | None, block: bytes | None = None) -> bytes:
+        """Request line + headers.  `block` is the caller's pre-rendered "K: V\r\n" header section (the
+        REST client memoises it per credential), so a steady-state request only formats its target."""
+        if block is None:
+            block = b"".join(f"{k}: {v}\r\n".encode("latin-1") for k, v in headers.items())
+        host = b"" if "Host" in headers else b"Host: " + self.host_header + b"\r\n"
+        clen = b"" if body_len is None else b"Content-Length: %d\r\n" % body_len
+        return b"%s %s HTTP/1.1\r\n%s%s%s\r\n" % (method.encode(), target.encode(), host, block, clen)
 
     @staticmethod
     def _expire(c: _Conn, what: str) -> None:
-        """Timer callback: fail the in-flight exchange and drop the connection.
+        """Fail the in-flight exchange and drop the connection (request timeout).
 
         Timeouts are plain loop timers rather than `asyncio.wait_for`, which costs a Task per request
         and on Python 3.10 can swallow a concurrent cancellation (bpo-42130) — a hang at shutdown."""
         fut = c.fut
+        c.timed_out = True
         if fut is not None and not fut.done():
             c.pending.popleft()
             fut.set_exception(E.TransportError(f"{what}: timed out"))
         c.close()
 
+    # ---- request slots: at most max_size × pipeline_depth exchanges in flight (a counting semaphore
+    # without asyncio.Semaphore's coroutine + waiter bookkeeping on the uncontended path)
+    async def _take_slot(self) -> None:
+        if self._inflight < self._limit and not self._slot_waiters:
+            self._inflight += 1
+            return
+        fut = asyncio.get_running_loop().create_future()
+        self._slot_waiters.append(fut)
+        try:
+            await fut  # the releasing request hands its slot over (no decrement/increment race)
+        except BaseException:
+            if fut.done() and not fut.cancelled():
+                self._give_slot()  # woken, then cancelled before running: pass the slot on
+            else:
+                try:
+                    self._slot_waiters.remove(fut)
+                except ValueError:
+                    pass
+            raise
+
+    def _give_slot(self) -> None:
+        while self._slot_waiters:
+            w = self._slot_waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+                return
+        self._inflight -= 1
+
+    # ---- timeouts: one coarse sweep per second over the busy connections instead of a timer per request
+    def _arm_sweep(self) -> None:
+        if self._sweep_handle is None:
+            self._sweep_handle = asyncio.get_running_loop().call_later(self.SWEEP_PERIOD, self._sweep)
+
+    def _sweep(self) -> None:
+        self._sweep_handle = None
+        now = asyncio.get_running_loop().time()
+        for c in [c for c in self._busy if c.deadline is not None and c.deadline <= now]:
+            if c.fut is not None and not c.fut.done():
+                self._expire(c, c.deadline_what)
+        if self._busy:
+            self._arm_sweep()
+
+    SWEEP_PERIOD = 0.5
+
     async def request(self, method: str, target: str, headers: dict, body: bytes | None,
-                      timeout: float | None = 30.0) -> _Response:
+                      timeout: float | None = 30.0, block: bytes | None = None) -> _Response:
         loop = asyncio.get_running_loop()
-        async with self._sem:
+        await self._take_slot()
+        try:
             for attempt in (0, 1):
                 c = await self._acquire()
                 reused = c.uses > 0
                 c.uses += 1
                 self._busy.add(c)
                 data = self._head(method, target, headers, len(body) if body is not None else
-                                  (0 if method in ("POST", "PUT", "PATCH") else None))
+                                  (0 if method in ("POST", "PUT", "PATCH") else None), block)
                 if body:
                     data += body
                 fut = c.send(data)
-                timer = loop.call_later(timeout, self._expire, c, f"{method} {target}") if timeout else None
+                timer = None
+                if timeout:
+                    if self.pipeline_depth == 1:  # one exchange per connection: the connection carries the deadline
+                        c.deadline, c.deadline_what = loop.time() + timeout, f"{method} {target}"
+                        self._arm_sweep()
+                    else:
+                        timer = loop.call_later(timeout, self._expire, c, f"{method} {target}")
                 try:
                     return await fut
                 except E.TransportError:
                     c.close()
-                    # a reused keep-alive connection may have been closed by the server: retry once on a fresh one
-                    if attempt == 0 and reused and (timer is None or not timer.cancelled()) and not fut.cancelled():
-                        if timer is not None:
-                            timer.cancel()
+                    # a reused keep-alive connection may have been closed by the server: retry once on a fresh
+                    # one (never after a timeout: the server may have acted on the request)
+                    if attempt == 0 and reused and not c.timed_out and not fut.cancelled():
                         continue
                     raise
                 except BaseException:
                     c.close()
                     raise
                 finally:
+                    c.deadline = None
                     if timer is not None:
                         timer.cancel()
+        finally:
+            self._give_slot()
         raise E.TransportError("unreachable")  # pragma: no cover
 
     async def stream(self, target: str, headers: dict, timeout: float | None = None):
@@ -438,6 +497,9 @@ class ConnectionPool:
             c.close()
 
     def close(self) -> None:
+        if self._sweep_handle is not None:
+            self._sweep_handle.cancel()
+            self._sweep_handle = None
         for c in list(self._idle) + list(self._busy):
             c.close()
         self._idle.clear()
