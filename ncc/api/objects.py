@@ -11,7 +11,7 @@ hot-path equivalent of client-go's "NEVER modify objects from the store" rule
 """
 from __future__ import annotations
 
-import datetime as _dt
+import time as _time
 from typing import Any, NamedTuple
 
 Obj = dict
@@ -93,9 +93,16 @@ def with_meta(obj: Obj, **fields: Any) -> Obj:
     return out
 
 
+_TS_CACHE = [-1, ""]
+
+
 def now_rfc3339() -> str:
-    """metav1.Now() serialised: RFC3339 with second precision, UTC."""
-    return _dt.datetime.now(_dt.timezone.utc).replace(microsecond=0).strftime("%Y-%m-%dT%H:%M:%SZ")
+    """metav1.Now() serialised: RFC3339 with second precision, UTC (formatted once per second)."""
+    sec = int(_time.time())
+    if sec != _TS_CACHE[0]:
+        _TS_CACHE[1] = _time.strftime("%Y-%m-%dT%H:%M:%SZ", _time.gmtime(sec))
+        _TS_CACHE[0] = sec
+    return _TS_CACHE[1]
 
 
 def normalize_data(d: Any) -> dict:

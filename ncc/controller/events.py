@@ -85,6 +85,7 @@ class BroadcastRecorder(EventRecorder):
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
         self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
         self._task: asyncio.Task | None = None
+        self._write_meta = getattr(client, "write_meta", None)  # undecoded writes (REST clients)
         self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0}
 
     def start(self) -> None:
@@ -151,11 +152,16 @@ class BroadcastRecorder(EventRecorder):
         ts = now_rfc3339()
         prev = self._seen.get(key)
         ns = ref["namespace"] or "default"
+        wm = self._write_meta
         if prev is not None:
             count = int(prev.get("count", 1)) + 1
             patch = {"count": count, "lastTimestamp": ts, "message": message}
-            res = await self.client.patch(R.EVENTS, ns, prev["metadata"]["name"], patch,
-                                          patch_type=PATCH_STRATEGIC)
+            if wm is not None:  # only the Event's name and count matter here: skip decoding the response
+                await wm("patch", R.EVENTS, ns, patch, name=prev["metadata"]["name"], patch_type=PATCH_STRATEGIC)
+                res = None
+            else:
+                res = await self.client.patch(R.EVENTS, ns, prev["metadata"]["name"], patch,
+                                              patch_type=PATCH_STRATEGIC)
             self._seen[key] = res if isinstance(res, dict) else dict(prev, count=count)
             self.stats["patched"] += 1
             return
@@ -174,7 +180,11 @@ class BroadcastRecorder(EventRecorder):
             "reportingComponent": self.component,
             "reportingInstance": "",
         }
-        res = await self.client.create(R.EVENTS, ns, ev)
+        if wm is not None:
+            await wm("create", R.EVENTS, ns, ev)
+            res = None
+        else:
+            res = await self.client.create(R.EVENTS, ns, ev)
         self._seen[key] = res if isinstance(res, dict) else ev
         if len(self._seen) > 4096:  # LRU-ish bound like client-go's 4096-entry cache
             for k in list(self._seen)[:1024]:
