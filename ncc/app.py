@@ -186,6 +186,14 @@ class App:
         kf = partition_filter(*o.partition) if o.partition is not None else None
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
+        if o.partition is not None and o.controller_adoption:
+            # controller-side Secrets/ConfigMaps owned only by other partitions' templates are dropped before
+            # decoding (adoption stamps every referenced dependent with its templates); one that a template
+            # of this partition references but which is not (yet) owned by it is kept through the reverse index
+            tstore = infs[R.TEMPLATES].store
+            for rt, index in ((R.SECRETS, "secret"), (R.CONFIGMAPS, "configmap")):
+                infs[rt].owner_filter = partition_owner_filter(
+                    *o.partition, referenced=lambda ns, name, i=index: bool(tstore.by_index(i, f"{ns}/{name}")))
         all_names = [n for n, _ in discover(cfg.shard_config_path)]
         self._shard_files = shard_files(cfg.shard_config_path)
         if o.role == "all" and o.mode == "native" and all_names:

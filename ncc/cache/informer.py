@@ -89,9 +89,9 @@ class Informer:
                  resync_period: float = 0.0, transform: Callable[[dict], dict] | None = None,
                  label_selector: str | None = None, page_size: int = 500, watch_timeout: tuple = (300, 600),
                  name: str = "", key_filter: Callable[[str, str], bool] | None = None,
-                 owner_filter: Callable[[str, tuple], bool] | None = None):
+                 owner_filter: Callable[[str, str, tuple], bool] | None = None):
         self.client = client
-        # key_filter(ns, name) / owner_filter(ns, owner_names) → False drops the object before it is
+        # key_filter(ns, name) / owner_filter(ns, name, owner_names) → False drops the object before it is
         # decoded/stored (a partitioned executor skips the other partitions' templates, and dependents
         # owned only by them, straight off the wire via the native scanner).  An object that leaves the
         # filter (e.g. our ownerRef removed) is dropped from the store.
@@ -228,7 +228,7 @@ class Informer:
                     sc = scan(line)
                     if sc is not None and sc[0] in _OBJECT_EVENTS:
                         ns_ = sc[1] or default_ns
-                        if (kf is not None and not kf(ns_, sc[2])) or (of is not None and not of(ns_, sc[4])):
+                        if (kf is not None and not kf(ns_, sc[2])) or (of is not None and not of(ns_, sc[2], sc[4])):
                             rv = self.last_rv = sc[3]
                             self._filtered_out(ObjectKey(ns_, sc[2]))
                             continue
@@ -296,7 +296,7 @@ class Informer:
             return False
         if self.owner_filter is not None:
             owners = tuple(r.get("name", "") for r in (m.get("ownerReferences") or ()))
-            if not self.owner_filter(ns, owners):
+            if not self.owner_filter(ns, m.get("name", ""), owners):
                 return False
         return True
 

@@ -52,18 +52,20 @@ def partition_filter(part: int, parts: int):
     return lambda ns, name: crc(f"{ns}/{name}".encode()) % parts == part
 
 
-def partition_owner_filter(part: int, parts: int):
-    """Shard-dependent filter: keep unowned objects (rogue detection needs them) and objects with at
-    least one owner template in this partition; drop those owned only by other partitions' templates."""
+def partition_owner_filter(part: int, parts: int, referenced=None):
+    """Dependent filter for partition `part` of `parts`: keep unowned objects (rogue detection and not yet
+    adopted references need them), objects with at least one owner template in this partition, and —
+    with `referenced(ns, name)` — objects a template of this partition references; drop the rest (owned
+    only by other partitions' templates) before they are decoded."""
     crc = zlib.crc32
 
-    def keep(ns: str, owners: tuple) -> bool:
+    def keep(ns: str, name: str, owners: tuple) -> bool:
         if not owners:
             return True
         for o in owners:
             if crc(f"{ns}/{o}".encode()) % parts == part:
                 return True
-        return False
+        return referenced is not None and referenced(ns, name)
     return keep
 
 

@@ -299,9 +299,11 @@ class ReconcileMixin:
         ns, name = meta(template).get("namespace", ""), meta(template).get("name", "")
         # the coordinator adopts; an executor only refuses to write when a reference is missing (as adoption would)
         for nm in secret_names(template):
-            self.secret_lister.get(ns, nm)
+            if self.secret_lister.try_get(ns, nm) is None:
+                await self._fetch_filtered(self.secret_informer, R.SECRETS, ns, nm)
         for nm in configmap_names(template):
-            self.configmap_lister.get(ns, nm)
+            if self.configmap_lister.try_get(ns, nm) is None:
+                await self._fetch_filtered(self.configmap_informer, R.CONFIGMAPS, ns, nm)
         spec_fp = fingerprint(template.get("spec")) if len(self.shards) > 1 and self.options.slim_shard_cache else None
         results = await gather_all(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards)
         failures = {}
@@ -315,6 +317,18 @@ class ReconcileMixin:
                                if s.name in failures else None) for s in self.shards})
         if failures:
             raise ShardSyncError(failures)
+
+    async def _fetch_filtered(self, informer, rt, ns: str, name: str) -> None:
+        """A referenced dependent missing from a partition-filtered cache may have been dropped off the wire
+        while it was owned only by other partitions' templates (a template of ours started referencing it
+        since): read it once; from now on the reference keeps its watch events flowing to this cache.
+        NotFound propagates as the missing-reference error it is."""
+        if informer.owner_filter is None:
+            informer.lister.get(ns, name)  # raises the typed NotFound
+            return
+        obj = await self.client.get(rt, ns, name)
+        if informer.lister.try_get(ns, name) is None:  # the watch may have delivered it meanwhile
+            informer.store.upsert(obj)
 
     async def _coordinator_finish(self, kind: str, obj: dict) -> None:
         """Coordinator role: turn the executors' per-shard reports into the status condition."""

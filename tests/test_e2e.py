@@ -373,3 +373,54 @@ async def test_shard_hot_reload(tmp_path, executors):
         for c in (cc, s0, s1):
             await c.close()
         await env.stop()
+
+
+async def test_partition_filter_keeps_newly_referenced_dependent(tmp_path):
+    """Executors drop controller-side Secrets owned only by other partitions' templates before decoding.
+    A template of the *other* partition that starts referencing such a Secret must still sync it (the
+    reverse index keeps it, and a filtered-out reference is fetched once), and later data changes must
+    reach the shard through both partitions."""
+    from ncc.controller.executor import key_part
+    from ncc.controller.executor import partition_owner_filter
+    keep = partition_owner_filter(0, 2, referenced=lambda ns, name: name == "wanted")
+    names = [f"algo-{i:05d}" for i in range(40)]
+    mine = next(n for n in names if key_part(f"template/{NS}/{n}", 2) == 0)
+    other = next(n for n in names if key_part(f"template/{NS}/{n}", 2) == 1)
+    assert keep(NS, "x", ()) and keep(NS, "x", (mine,)) and keep(NS, "wanted", (other,))
+    assert not keep(NS, "x", (other,))
+
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    try:
+        ia, ib = int(mine.split("-")[1]), int(other.split("-")[1])
+        await cc.create(R.SECRETS, NS, make_secret("s-shared", NS))
+        await cc.create(R.TEMPLATES, NS, make_template(ia, NS, secrets=["s-shared"]))
+        async with Running(env, "native", executors_per_shard=2):
+            async def owned(uids):
+                o = await sc.get(R.SECRETS, NS, "s-shared")
+                return {r["uid"] for r in o["metadata"].get("ownerReferences") or ()} == uids
+            await wait_for(lambda: _get(sc, R.TEMPLATES, mine), timeout=5)
+            ua = (await sc.get(R.TEMPLATES, NS, mine))["metadata"]["uid"]
+            await wait_for(lambda: owned({ua}), timeout=5)
+            # now a template of the other partition references the Secret owned only by the first one
+            await cc.create(R.TEMPLATES, NS, make_template(ib, NS, secrets=["s-shared"]))
+            await wait_for(lambda: _get(sc, R.TEMPLATES, other), timeout=5)
+            ub = (await sc.get(R.TEMPLATES, NS, other))["metadata"]["uid"]
+            await wait_for(lambda: owned({ua, ub}), timeout=5)
+            await mutate(cc, R.SECRETS, "s-shared", lambda o: o.__setitem__("data", {"token": "bmV3LXZhbA=="}))
+
+            async def updated():
+                return (await sc.get(R.SECRETS, NS, "s-shared")).get("data") == {"token": "bmV3LXZhbA=="}
+            await wait_for(updated, timeout=5)
+
+            async def both_ready():
+                for n in (mine, other):
+                    st = (await cc.get(R.TEMPLATES, NS, n)).get("status") or {}
+                    if (st.get("conditions") or [{}])[0].get("status") != "True":
+                        return False
+                return True
+            await wait_for(both_ready, timeout=5)
+    finally:
+        await cc.close()
+        await sc.close()
+        await env.stop()

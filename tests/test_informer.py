@@ -199,7 +199,7 @@ async def test_owner_filter_and_parked_echoes():
         state.create(R.SECRETS, NS, owned("a", ["mine"]))
         state.create(R.SECRETS, NS, owned("b", ["other"]))
         state.create(R.SECRETS, NS, owned("c", []))
-        inf = Informer(client, R.SECRETS, NS, owner_filter=lambda ns, owners: not owners or "mine" in owners)
+        inf = Informer(client, R.SECRETS, NS, owner_filter=lambda ns, name, owners: not owners or "mine" in owners)
         rec = Rec()
         inf.add_event_handler(rec.add, rec.update, rec.delete)
         inf.start()
