@@ -18,6 +18,8 @@
 //    without materialising the object, so informers can recognise echoes of their own writes.
 //  * scan_event_owners(bytes) — the same plus ownerReferences names/uids, so a key-partitioned
 //    executor can drop dependents owned only by another partition's templates without decoding them.
+//  * scan_event_part(bytes, parts, ns) — the same plus the crc32 key partition of the object and the
+//    bitmask of its owners' partitions, so the partition test itself builds no Python strings.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
 //  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
@@ -42,7 +44,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 8
+#define NCC_NATIVE_ABI 9
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -597,6 +599,66 @@ py::object scan_event_owners(py::bytes line) {
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u);
 }
 
+// ----------------------------------------------------------------------------- partitions
+// crc32 (IEEE, reflected; identical to zlib.crc32) of "<ns>/<name>": the executors' key → partition map
+// (ncc.controller.executor.key_part), computed here so foreign-partition watch lines are dropped without
+// building Python strings.
+static uint32_t kCrcTable[256];
+static bool crc_table_init() {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        kCrcTable[i] = c;
+    }
+    return true;
+}
+static const bool kCrcReady = crc_table_init();
+
+static uint32_t crc_update(uint32_t c, std::string_view s) {
+    for (unsigned char ch : s) c = kCrcTable[(c ^ ch) & 0xFFu] ^ (c >> 8);
+    return c;
+}
+
+static uint32_t key_crc(std::string_view ns, std::string_view name) {
+    uint32_t c = crc_update(0xFFFFFFFFu, ns);
+    c = crc_update(c, std::string_view("/", 1));
+    return crc_update(c, name) ^ 0xFFFFFFFFu;
+}
+
+// scan_event_part(line, parts, default_ns) -> (type, namespace, name, resourceVersion, (owner names...),
+//     (owner uids...), key_partition, owner_partition_mask) | None
+// key_partition = crc32("ns/name") % parts; bit p of owner_partition_mask is set when some owner
+// template "ns/<owner>" falls in partition p (parts <= 63).  An empty namespace uses `default_ns`.
+py::object scan_event_part(py::bytes line, int parts, const std::string& default_ns) {
+    if (parts < 1 || parts > 63) throw py::value_error("scan_event_part: parts must be in 1..63");
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view type, ns, name, rv;
+    std::vector<std::string_view> owners, uids;
+    Scanner sc(buf, static_cast<size_t>(len));
+    sc.owners = &owners;
+    sc.owner_uids = &uids;
+    if (!sc.scan(type, ns, name, rv)) return py::none();
+    std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
+    const uint32_t up = static_cast<uint32_t>(parts);
+    long long kp = static_cast<long long>(key_crc(kns, name) % up);
+    unsigned long long mask = 0;
+    py::tuple o(owners.size()), u(uids.size());
+    for (size_t i = 0; i < owners.size(); ++i) {
+        mask |= 1ull << (key_crc(kns, owners[i]) % up);
+        o[i] = py::str(owners[i].data(), owners[i].size());
+    }
+    for (size_t i = 0; i < uids.size(); ++i) u[i] = py::str(uids[i].data(), uids[i].size());
+    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
+                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u, kp, mask);
+}
+
+py::int_ key_partition(const std::string& ns, const std::string& name, int parts) {
+    if (parts < 1) throw py::value_error("key_partition: parts must be >= 1");
+    return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));
+}
+
 
 // ----------------------------------------------------------------------------- JSON encoder
 // dumps(obj) -> bytes: compact JSON (separators "," and ":") of a JSON-shaped Python value, key order
@@ -740,6 +802,9 @@ PYBIND11_MODULE(_native, m) {
     m.def("dumps", &dumps, py::arg("obj"), "compact JSON bytes of a JSON-shaped value (UTF-8, key order kept)");
     m.def("scan_object", &scan_object, py::arg("body"),
           "(namespace, name, resourceVersion, uid) from an object's metadata without decoding it, or None");
+    m.def("scan_event_part", &scan_event_part, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
+          "scan_event_owners plus the key partition and the owner-partition bitmask (crc32 % parts)");
+    m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")

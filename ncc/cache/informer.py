@@ -84,6 +84,12 @@ async def _call(fn, *args):
         await r
 
 
+async def _single_lines(lines):
+    """Adapt a line-at-a-time raw watch to the batched loop."""
+    async for line in lines:
+        yield (line,)
+
+
 class Informer:
     def __init__(self, client: KubeClient, rt: ResourceType, namespace: str | None, *,
                  resync_period: float = 0.0, transform: Callable[[dict], dict] | None = None,
@@ -211,61 +217,91 @@ class Informer:
         kw = dict(resource_version=rv, timeout_seconds=random.randint(lo, hi), allow_bookmarks=True,
                   label_selector=self.label_selector)
         scan = None
+        nparts = 0
         kf, of = self.key_filter, self.owner_filter
         mo = self.metadata_only
         if (self.echo_fastpath or kf is not None or of is not None or mo) and hasattr(self.client, "watch_raw"):
             mod = _native.load()
             if mod is not None:
                 scan = mod.scan_event_owners if (of is not None or mo) else mod.scan_event
+                # partition filters (executor key partitions) are evaluated natively: crc32 % parts of the
+                # key and of every owner, so a foreign line costs one scan and two integer tests
+                parts = {getattr(f, "parts", None) for f in (kf, of) if f is not None}
+                if len(parts) == 1 and None not in parts:
+                    nparts = parts.pop()
+                    default_ns_ = self.namespace or ""
+
+                    def scan(line, _s=mod.scan_event_part, _p=nparts, _d=default_ns_):
+                        return _s(line, _p, _d)
+                    kpart = kf.part if kf is not None else None
+                    opart = of.part if of is not None else None
+                    oref = getattr(of, "referenced", None) if of is not None else None
+                    kf = of = None
         if scan is not None:
             loads = json.loads
             store = self.store
             default_ns = self.namespace or ""
             inflight, stash = self._inflight, self._stash
-            async for line in self.client.watch_raw(self.rt, self.namespace, **kw):
-                sc = None
-                if kf is not None or of is not None:
-                    sc = scan(line)
-                    if sc is not None and sc[0] in _OBJECT_EVENTS:
-                        ns_ = sc[1] or default_ns
-                        if (kf is not None and not kf(ns_, sc[2])) or (of is not None and not of(ns_, sc[2], sc[4])):
-                            rv = self.last_rv = sc[3]
-                            self._filtered_out(ObjectKey(ns_, sc[2]))
-                            continue
-                if mo:
-                    if sc is None:
+            batches = getattr(self.client, "watch_raw_batches", None)
+            if batches is not None:
+                source = batches(self.rt, self.namespace, **kw)
+            else:
+                source = _single_lines(self.client.watch_raw(self.rt, self.namespace, **kw))
+            async for lines in source:
+                for line in lines:
+                    sc = None
+                    if nparts:
                         sc = scan(line)
-                    if sc is not None and sc[0] == "MODIFIED":
-                        cur = store.get(sc[1] or default_ns, sc[2])
-                        refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
-                        if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
-                                tuple(r.get("uid", "") for r in refs) == sc[5]:
+                        if sc is not None and sc[0] in _OBJECT_EVENTS and (
+                                (kpart is not None and sc[6] != kpart) or
+                                (opart is not None and sc[4] and not (sc[7] >> opart) & 1 and
+                                 (oref is None or not oref(sc[1] or default_ns, sc[2])))):
                             rv = self.last_rv = sc[3]
-                            self.filtered += 1
+                            self._filtered_out(sc[1] or default_ns, sc[2])
                             continue
-                if store._assumed or inflight:
-                    if sc is None:
+                    elif kf is not None or of is not None:
                         sc = scan(line)
-                    if sc is not None and sc[0] in ("ADDED", "MODIFIED"):
-                        key = ObjectKey(sc[1] or default_ns, sc[2])
-                        if store.confirm(key, sc[3]) is not None:
-                            rv = self.last_rv = sc[3]
-                            self.events += 1
-                            self.echoes += 1
-                            continue
-                        if key in inflight:  # overtook the response of our write: park it
-                            prev = stash.get(key)
-                            if prev is not None:
-                                await self._apply_line(prev[1])
-                            stash[key] = (sc[3], line)
-                            rv = self.last_rv = sc[3]
-                            continue
-                if stash and sc is not None:
-                    prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
-                    if prev is not None:  # keep per-key order
-                        await self._apply_line(prev[1])
-                ev = loads(line)
-                rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
+                        if sc is not None and sc[0] in _OBJECT_EVENTS:
+                            ns_ = sc[1] or default_ns
+                            if (kf is not None and not kf(ns_, sc[2])) or \
+                                    (of is not None and not of(ns_, sc[2], sc[4])):
+                                rv = self.last_rv = sc[3]
+                                self._filtered_out(ns_, sc[2])
+                                continue
+                    if mo:
+                        if sc is None:
+                            sc = scan(line)
+                        if sc is not None and sc[0] == "MODIFIED":
+                            cur = store.get(sc[1] or default_ns, sc[2])
+                            refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
+                            if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
+                                    tuple(r.get("uid", "") for r in refs) == sc[5]:
+                                rv = self.last_rv = sc[3]
+                                self.filtered += 1
+                                continue
+                    if store._assumed or inflight:
+                        if sc is None:
+                            sc = scan(line)
+                        if sc is not None and sc[0] in ("ADDED", "MODIFIED"):
+                            key = ObjectKey(sc[1] or default_ns, sc[2])
+                            if store.confirm(key, sc[3]) is not None:
+                                rv = self.last_rv = sc[3]
+                                self.events += 1
+                                self.echoes += 1
+                                continue
+                            if key in inflight:  # overtook the response of our write: park it
+                                prev = stash.get(key)
+                                if prev is not None:
+                                    await self._apply_line(prev[1])
+                                stash[key] = (sc[3], line)
+                                rv = self.last_rv = sc[3]
+                                continue
+                    if stash and sc is not None:
+                        prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
+                        if prev is not None:  # keep per-key order
+                            await self._apply_line(prev[1])
+                    ev = loads(line)
+                    rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
             return rv
         async for ev in self.client.watch(self.rt, self.namespace, **kw):
             rv = await self._handle(ev.type, ev.object, rv)
@@ -283,7 +319,7 @@ class Informer:
         if (self.key_filter is not None or self.owner_filter is not None) and t in _OBJECT_EVENTS:
             m = obj.get("metadata") or {}
             if not self._wanted(m):
-                self._filtered_out(ObjectKey(m.get("namespace") or self.namespace or "", m.get("name", "")))
+                self._filtered_out(m.get("namespace") or self.namespace or "", m.get("name", ""))
                 self.last_rv = new_rv
                 return new_rv
         await self._apply(t, obj)
@@ -300,10 +336,10 @@ class Informer:
                 return False
         return True
 
-    def _filtered_out(self, key: ObjectKey) -> None:
+    def _filtered_out(self, ns: str, name: str) -> None:
         self.filtered += 1
-        if self.store.get(key.namespace, key.name) is not None:
-            self.store.delete(key)  # left our partition: forget it (no handler dispatch)
+        if self.store.get(ns, name) is not None:
+            self.store.delete(ObjectKey(ns, name))  # left our partition: forget it (no handler dispatch)
 
     async def _apply_line(self, line: bytes) -> None:
         ev = json.loads(line)

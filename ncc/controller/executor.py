@@ -49,7 +49,11 @@ def key_part(key: str, parts: int) -> int:
 def partition_filter(part: int, parts: int):
     """Informer key filter for partition `part` of `parts` (agrees with `key_part`)."""
     crc = zlib.crc32
-    return lambda ns, name: crc(f"{ns}/{name}".encode()) % parts == part
+
+    def keep(ns: str, name: str) -> bool:
+        return crc(f"{ns}/{name}".encode()) % parts == part
+    keep.part, keep.parts = part, parts  # lets informers test the partition natively (scan_event_part)
+    return keep
 
 
 def partition_owner_filter(part: int, parts: int, referenced=None):
@@ -66,6 +70,7 @@ def partition_owner_filter(part: int, parts: int, referenced=None):
             if crc(f"{ns}/{o}".encode()) % parts == part:
                 return True
         return referenced is not None and referenced(ns, name)
+    keep.part, keep.parts, keep.referenced = part, parts, referenced
     return keep
 
 

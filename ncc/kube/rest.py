@@ -293,6 +293,15 @@ class RestClient(KubeClient):
     async def watch_raw(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
                         allow_bookmarks=True, label_selector=None) -> AsyncIterator[bytes]:
         """The watch stream as raw JSON lines (one event per line), undecoded."""
+        async for lines in self.watch_raw_batches(rt, namespace, resource_version=resource_version,
+                                                  timeout_seconds=timeout_seconds, allow_bookmarks=allow_bookmarks,
+                                                  label_selector=label_selector):
+            for line in lines:
+                yield line
+
+    async def watch_raw_batches(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
+                                allow_bookmarks=True, label_selector=None) -> AsyncIterator[list]:
+        """The watch stream as lists of raw JSON lines: everything that arrived in one read, undecoded."""
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": timeout_seconds,
                   "allowWatchBookmarks": "true" if allow_bookmarks else None, "labelSelector": label_selector}
         target = rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items() if v is not None})
@@ -300,18 +309,19 @@ class RestClient(KubeClient):
         headers = await self._headers(None)
         if self.transport == "fast":
             pool = await self._get_pool()
-            stream = pool.stream(target, headers, timeout=(timeout_seconds + 30) if timeout_seconds else None)
+            stream = pool.stream(target, headers, timeout=(timeout_seconds + 30) if timeout_seconds else None,
+                                 batch=True)
             try:
-                async for resp, line in stream:
+                async for resp, lines in stream:
                     if resp is not None:
                         if resp.status >= 300:
                             try:
-                                st = json.loads(line) if line else None
+                                st = json.loads(lines) if lines else None
                             except ValueError:
                                 st = None
                             raise E.from_status(resp.status, st if isinstance(st, dict) else None)
                         continue
-                    yield line
+                    yield lines
             finally:
                 await stream.aclose()
             return
@@ -335,11 +345,11 @@ class RestClient(KubeClient):
                         continue
                     lines = buf.split(b"\n")
                     buf = lines.pop()
-                    for line in lines:
-                        if line:
-                            yield line
+                    lines = [ln for ln in lines if ln]
+                    if lines:
+                        yield lines
                 if buf.strip():
-                    yield buf
+                    yield [buf]
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
             raise E.TransportError(f"watch {url}: {type(e).__name__}: {e}") from e
 

@@ -459,8 +459,10 @@ class ConnectionPool:
             self._give_slot()
         raise E.TransportError("unreachable")  # pragma: no cover
 
-    async def stream(self, target: str, headers: dict, timeout: float | None = None):
-        """GET with a streaming body; yields complete lines (bytes).  Uses a dedicated connection.
+    async def stream(self, target: str, headers: dict, timeout: float | None = None, batch: bool = False):
+        """GET with a streaming body; yields complete lines (bytes) — or, with `batch`, lists of all the
+        lines that arrived together, so the consumer iterates a plain list instead of resuming this
+        generator per line.  Uses a dedicated connection.
 
         `timeout` bounds the whole stream (closing the connection ends it), like a client-side
         `timeoutSeconds`; waiting itself is a plain Event wait, so cancellation is never swallowed."""
@@ -483,9 +485,16 @@ class ConnectionPool:
                 return
             yield resp, None
             while True:
-                while c.stream:
-                    yield None, c.stream.popleft()
-                    c.resume()
+                if batch:
+                    if c.stream:
+                        lines = list(c.stream)
+                        c.stream.clear()
+                        c.resume()
+                        yield None, lines
+                else:
+                    while c.stream:
+                        yield None, c.stream.popleft()
+                        c.resume()
                 if c.stream_done or c.closed:
                     return
                 c.stream_event.clear()
