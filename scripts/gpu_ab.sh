@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) echo "fatal status $1 in $2; stopping"; exit "$1";; esac; }
 python native/build.py > gpurun_out/build.log 2>&1 || exit 1
 (cd ab_old && python native/build.py > ../gpurun_out/build_old.log 2>&1) || exit 1
-for i in 1 2 3; do
+for i in $(seq 1 ${AB_REPS:-3}); do
   (cd ab_old && timeout -k 10 300 python bench.py "$@" > ../gpurun_out/ab_old_$i.json 2>/dev/null); s=$?; fatal $s old$i
   timeout -k 10 300 python bench.py "$@" > gpurun_out/ab_new_$i.json 2>/dev/null; s=$?; fatal $s new$i
 done
