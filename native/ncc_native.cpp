@@ -20,6 +20,7 @@
 //    executor can drop dependents owned only by another partition's templates without decoding them.
 //  * scan_event_part(bytes, parts, ns) — the same plus the crc32 key partition of the object and the
 //    bitmask of its owners' partitions, so the partition test itself builds no Python strings.
+//  * parse_response_head(bytes) — status and the framing headers of an HTTP/1.1 response.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
 //  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
@@ -44,7 +45,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 9
+#define NCC_NATIVE_ABI 10
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -659,6 +660,77 @@ py::int_ key_partition(const std::string& ns, const std::string& name, int parts
     return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));
 }
 
+// ----------------------------------------------------------------------------- HTTP/1.1 response heads
+static std::string_view trim(std::string_view v) {
+    while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+    while (!v.empty() && (v.back() == ' ' || v.back() == '\t' || v.back() == '\r')) v.remove_suffix(1);
+    return v;
+}
+
+static bool ieq(std::string_view a, std::string_view b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); ++i) {
+        char x = a[i], y = b[i];
+        if (x >= 'A' && x <= 'Z') x = static_cast<char>(x - 'A' + 'a');
+        if (x != y) return false;
+    }
+    return true;
+}
+
+static bool icontains(std::string_view hay, std::string_view needle) {
+    if (needle.size() > hay.size()) return false;
+    for (size_t i = 0; i + needle.size() <= hay.size(); ++i)
+        if (ieq(hay.substr(i, needle.size()), needle)) return true;
+    return false;
+}
+
+// parse_response_head(head) -> (status, content_length | -1, chunked, connection_close, retry_after | None)
+// `head` is everything before the blank line.  Only the headers the client acts on are extracted.
+py::object parse_response_head(py::bytes head) {
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(head.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view h(buf, static_cast<size_t>(len));
+    size_t eol = h.find("\r\n");
+    std::string_view first = h.substr(0, eol);
+    size_t sp = first.find(' ');
+    if (sp == std::string_view::npos || first.substr(0, 5) != "HTTP/") throw py::value_error("bad status line");
+    long status = 0;
+    size_t i = sp + 1;
+    int digits = 0;
+    for (; i < first.size() && first[i] >= '0' && first[i] <= '9'; ++i, ++digits) status = status * 10 + (first[i] - '0');
+    if (digits != 3) throw py::value_error("bad status code");
+    long long clen = -1;
+    bool chunked = false, close = false;
+    py::object retry = py::none();
+    size_t pos = eol == std::string_view::npos ? h.size() : eol + 2;
+    while (pos < h.size()) {
+        size_t e = h.find("\r\n", pos);
+        std::string_view line = h.substr(pos, e == std::string_view::npos ? std::string_view::npos : e - pos);
+        pos = e == std::string_view::npos ? h.size() : e + 2;
+        size_t c = line.find(':');
+        if (c == std::string_view::npos) continue;
+        std::string_view k = trim(line.substr(0, c)), v = trim(line.substr(c + 1));
+        if (ieq(k, "content-length")) {
+            long long n = 0;
+            if (v.empty()) throw py::value_error("bad content-length");
+            for (char ch : v) {
+                if (ch < '0' || ch > '9') throw py::value_error("bad content-length");
+                n = n * 10 + (ch - '0');
+                if (n > (1LL << 40)) throw py::value_error("content-length too large");
+            }
+            clen = n;
+        } else if (ieq(k, "transfer-encoding")) {
+            chunked = chunked || icontains(v, "chunked");
+        } else if (ieq(k, "connection")) {
+            close = ieq(v, "close");
+        } else if (ieq(k, "retry-after")) {
+            retry = py::str(v.data(), v.size());
+        }
+    }
+    return py::make_tuple(status, clen, chunked, close, retry);
+}
+
 
 // ----------------------------------------------------------------------------- JSON encoder
 // dumps(obj) -> bytes: compact JSON (separators "," and ":") of a JSON-shaped Python value, key order
@@ -804,6 +876,8 @@ PYBIND11_MODULE(_native, m) {
           "(namespace, name, resourceVersion, uid) from an object's metadata without decoding it, or None");
     m.def("scan_event_part", &scan_event_part, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
           "scan_event_owners plus the key partition and the owner-partition bitmask (crc32 % parts)");
+    m.def("parse_response_head", &parse_response_head, py::arg("head"),
+          "(status, content_length|-1, chunked, connection_close, retry_after|None) of an HTTP/1.1 response head");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");

@@ -1,4 +1,4 @@
-"""Compact JSON encoding for request bodies, responses and watch lines.
+"""Compact JSON encoding (and UTF-8 decoding) for request bodies, responses and watch lines.
 
 Uses the native encoder (`ncc._native.dumps`, ~4x faster than `json.dumps` on Kubernetes objects)
 when the extension is built, else the standard library.  Output is compact (`,`/`:` separators) with
@@ -13,6 +13,15 @@ from .. import native as _native
 
 _mod = _native.load()
 _native_dumps = getattr(_mod, "dumps", None) if _mod is not None else None
+
+
+_decode = json.JSONDecoder().decode
+
+
+def loads_bytes(b):
+    """json.loads for UTF-8 wire bytes (Kubernetes JSON is always UTF-8) without the stdlib's per-call
+    encoding detection."""
+    return _decode(b.decode("utf-8", "surrogatepass") if isinstance(b, (bytes, bytearray, memoryview)) else b)
 
 
 def dumps_bytes(obj) -> bytes:

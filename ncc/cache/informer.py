@@ -29,6 +29,7 @@ from typing import Callable
 
 from .. import native as _native
 from ..aio import wait_timeout
+from ..api.jsonenc import loads_bytes
 from ..api.objects import ObjectKey, key_of, rv_int
 from ..api.resources import ResourceType
 from ..kube import errors as E
@@ -74,14 +75,6 @@ class _Handler:
     on_add: Callable | None
     on_update: Callable | None
     on_delete: Callable | None
-
-
-async def _call(fn, *args):
-    if fn is None:
-        return
-    r = fn(*args)
-    if inspect.isawaitable(r):
-        await r
 
 
 async def _single_lines(lines):
@@ -169,17 +162,31 @@ class Informer:
         self._task = self._resync_task = None
 
     # ------------------------------------------------------------- dispatch
+    # handlers are plain callables; one that returns an awaitable (e.g. the reference-compat inline delete)
+    # is awaited before the next event, like client-go's serial handler delivery
     async def _dispatch_add(self, obj):
         for h in self._handlers:
-            await _call(h.on_add, obj)
+            fn = h.on_add
+            if fn is not None:
+                r = fn(obj)
+                if r is not None and inspect.isawaitable(r):
+                    await r
 
     async def _dispatch_update(self, old, new):
         for h in self._handlers:
-            await _call(h.on_update, old, new)
+            fn = h.on_update
+            if fn is not None:
+                r = fn(old, new)
+                if r is not None and inspect.isawaitable(r):
+                    await r
 
     async def _dispatch_delete(self, obj):
         for h in self._handlers:
-            await _call(h.on_delete, obj)
+            fn = h.on_delete
+            if fn is not None:
+                r = fn(obj)
+                if r is not None and inspect.isawaitable(r):
+                    await r
 
     # ------------------------------------------------------------- reflector
     async def _list(self) -> str:
@@ -238,7 +245,7 @@ class Informer:
                     oref = getattr(of, "referenced", None) if of is not None else None
                     kf = of = None
         if scan is not None:
-            loads = json.loads
+            loads = loads_bytes
             store = self.store
             default_ns = self.namespace or ""
             inflight, stash = self._inflight, self._stash
@@ -342,7 +349,7 @@ class Informer:
             self.store.delete(ObjectKey(ns, name))  # left our partition: forget it (no handler dispatch)
 
     async def _apply_line(self, line: bytes) -> None:
-        ev = json.loads(line)
+        ev = loads_bytes(line)
         await self._apply(ev.get("type", ""), ev.get("object") or {})
 
     # ------------------------------------------------------------- write tracking

@@ -23,10 +23,33 @@ import ssl as _ssl
 from collections import deque
 from urllib.parse import urlsplit
 
+from .. import native as _native
 from ..aio import wait_timeout
 from . import errors as E
 
 _CRLF2 = b"\r\n\r\n"
+
+
+_native_mod = _native.load()
+_parse_native = getattr(_native_mod, "parse_response_head", None) if _native_mod is not None else None
+_NO_HEADERS: dict = {}
+
+
+def _parse_head_py(head: bytes) -> tuple:
+    """(status, content_length | -1, chunked, connection_close, headers) — the pure-Python fallback."""
+    lines = head.split(b"\r\n")
+    parts = lines[0].split(b" ", 2)
+    try:
+        status = int(parts[1])
+    except (IndexError, ValueError) as e:
+        raise E.TransportError(f"malformed response head: {lines[0][:80]!r}") from e
+    h = {}
+    for ln in lines[1:]:
+        k, _, v = ln.partition(b":")
+        h[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
+    clen = int(h["content-length"]) if "content-length" in h else -1
+    return (status, clen, "chunked" in h.get("transfer-encoding", "").lower(),
+            h.get("connection", "").lower() == "close", h)
 
 
 class _Response:
@@ -143,25 +166,25 @@ class _Conn(asyncio.Protocol):
                 return
 
     def _parse_head(self, head: bytes):
-        lines = head.split(b"\r\n")
-        parts = lines[0].split(b" ", 2)
-        self.status = int(parts[1])
-        h = {}
-        for ln in lines[1:]:
-            k, _, v = ln.partition(b":")
-            h[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
-        self.headers = h
+        if _parse_native is not None:
+            try:
+                status, clen, chunked, close, retry = _parse_native(head)
+            except ValueError as e:
+                raise E.TransportError(f"malformed response head: {e}") from e
+            self.headers = _NO_HEADERS if retry is None else {"retry-after": retry}
+        else:
+            status, clen, chunked, close, self.headers = _parse_head_py(head)
+        self.status = status
         self.head_done = True
-        te = h.get("transfer-encoding", "")
-        if "chunked" in te.lower():
+        if chunked:
             self.chunked = True
-        elif "content-length" in h:
-            self.clen = int(h["content-length"])
-        elif self.status in (204, 304) or 100 <= self.status < 200:
+        elif clen >= 0:
+            self.clen = clen
+        elif status in (204, 304) or 100 <= status < 200:
             self.clen = 0
         else:
             self.until_close = True
-        if h.get("connection", "").lower() == "close":
+        if close:
             self.keep_alive = False
         if self.stream is not None and self.fut is not None and not self.fut.done():
             # streaming: hand the status/headers over now, body follows as lines

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 from ..api import constants as C
 from ..api import resources as R
+from ..api.fingerprint import SLIM_FP, fingerprint
 from ..api.objects import ObjectKey, meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
@@ -258,16 +259,16 @@ class Shard:
         await self.client.delete(rt, m.get("namespace", ""), m.get("name", ""))
 
 
-_PAYLOAD = {"spec": ("spec", "status"), "data": ("data", "binaryData", "stringData")}
+_DROP_DEP = frozenset(("data", "binaryData", "stringData", SLIM_FP))
+_DROP_SPEC = frozenset(("spec", "status", SLIM_FP))
 
 
 def slim_written(rt: R.ResourceType, body: dict, rv: str, uid: str) -> dict:
     """Slim-cache form of an object we just wrote in full (same shape as reconcile.slim_spec/slim_data)."""
-    from ..api.fingerprint import SLIM_FP, fingerprint
     is_dep = rt is R.SECRETS or rt is R.CONFIGMAPS
-    drop = _PAYLOAD["data"] if is_dep else _PAYLOAD["spec"]
-    out = {k: v for k, v in body.items() if k not in drop and k != SLIM_FP}
-    m = dict(out.get("metadata") or {})
+    drop = _DROP_DEP if is_dep else _DROP_SPEC
+    out = {k: v for k, v in body.items() if k not in drop}
+    m = dict(out.get("metadata") or ())
     m["resourceVersion"] = rv
     if uid:
         m["uid"] = uid
@@ -281,6 +282,5 @@ def slim_written(rt: R.ResourceType, body: dict, rv: str, uid: str) -> dict:
 
 def _strip_slim(obj: dict) -> dict:
     """Drop the slim-cache digest key before an object is sent back to an apiserver."""
-    from ..api.fingerprint import SLIM_FP
     obj.pop(SLIM_FP, None)
     return obj

@@ -170,3 +170,26 @@ async def test_file_token_is_cached_and_reread_after_period_or_401(tmp_path):
     finally:
         await c.close()
         await srv.stop()
+
+
+@pytest.mark.parametrize("head", [
+    b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: 17",
+    b"HTTP/1.1 201 Created\r\ncontent-length: 0\r\nConnection: close",
+    b"HTTP/1.1 429 Too Many Requests\r\nRetry-After:  3 \r\nTransfer-Encoding: gzip, Chunked",
+    b"HTTP/1.1 204 No Content",
+    b"HTTP/1.0 503 Unavailable\r\nRetry-After: 1\r\nX-Other: a:b:c\r\nCONNECTION: Close",
+])
+def test_native_response_head_parser_matches_python(head):
+    from ncc import native
+    from ncc.kube.transport import _parse_head_py
+    m = native.load(required=True)
+    status, clen, chunked, close, retry = m.parse_response_head(head)
+    ps, pc, pch, pcl, ph = _parse_head_py(head)
+    assert (status, clen, chunked, close, retry) == (ps, pc, pch, pcl, ph.get("retry-after"))
+
+
+@pytest.mark.parametrize("head", [b"garbage", b"HTTP/1.1 2x0 OK", b"HTTP/1.1 200 OK\r\nContent-Length: -5"])
+def test_native_response_head_parser_rejects_malformed(head):
+    from ncc import native
+    with pytest.raises(ValueError):
+        native.load(required=True).parse_response_head(head)
