@@ -82,6 +82,8 @@ class Controller(ReconcileMixin):
         self.on_ready = None  # executor role: called once caches are synced and workers run
         self.shard_state: dict[str, dict] = {}  # coordinator role: key -> {shard: (uid, generation, error)}
         self._pending_event: set = set()
+        # adoption_cache: template key → resourceVersion whose references were last verified as adopted
+        self._adopted: dict[str, str] = {}
         if o.assume_writes:
             for inf in (template_informer, workgroup_informer, secret_informer, configmap_informer):
                 inf.echo_fastpath = True
@@ -114,6 +116,14 @@ class Controller(ReconcileMixin):
                 self._register_shard_handlers(shard)
 
     def _on_crd_update(self, old: dict, new: dict, kind: str) -> None:
+        if self.options.adoption_cache and kind == C.KIND_TEMPLATE:
+            # adoption depends on the references and the dependents' ownerRefs (whose changes arrive as
+            # dependent events): a new template version with the same references stays adopted
+            om, nm = meta(old), meta(new)
+            key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
+            if self._adopted.get(key) == om.get("resourceVersion") and om.get("uid") == nm.get("uid") and \
+                    secret_names(old) == secret_names(new) and configmap_names(old) == configmap_names(new):
+                self._adopted[key] = nm.get("resourceVersion")
         if self.options.generation_filter:
             om, nm = meta(old), meta(new)
             if om.get("resourceVersion") == nm.get("resourceVersion"):
@@ -127,9 +137,25 @@ class Controller(ReconcileMixin):
     def _on_dependent(self, obj, index: str):
         obj = self._unwrap(obj)
         if self.options.mode == "native":
+            # templates referencing the object (reverse index), then owners that no longer reference it
+            # (handleObject's ownerRef walk, controller.go:206-223) — each template enqueued once
             ns, name = meta(obj).get("namespace", "") or "", meta(obj).get("name", "")
+            seen = set()
+            adopted = self._adopted
             for t in self.template_informer.store.by_index(index, f"{ns}/{name}"):
-                self.enqueue_resource(t, C.KIND_TEMPLATE)
+                tn = meta(t).get("name", "")
+                seen.add(tn)
+                key = make_key(C.KIND_TEMPLATE, ns, tn)
+                adopted.pop(key, None)  # the dependent's ownership may have changed: re-check adoption
+                self._enqueue_key(key)
+            if isinstance(obj, dict) and obj.get("kind") != C.TEMPLATE_KIND:
+                for ref in meta(obj).get("ownerReferences") or ():
+                    if ref.get("kind") != C.TEMPLATE_KIND or ref.get("name", "") in seen:
+                        continue
+                    if self.template_lister.try_get(ns, ref.get("name", "")) is None:
+                        return None  # the reference stops at the first orphaned owner (controller.go:215-218)
+                    self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, ref.get("name", "")))
+                return None
         return self.handle_object(obj)
 
     def _on_dependent_update(self, old: dict, new: dict, index: str = "secret") -> None:

@@ -46,6 +46,8 @@ class ControllerOptions:
     rogue_event_on_template: bool = False  # controller.go:497 records the event on the *shard* object
     controller_adoption: bool = True       # controller.go:647-695 adds ownerRefs to controller-side dependents,
                                            # which makes them GC-deletable with their last template
+    adoption_cache: bool = False           # skip re-checking adoption while neither the template nor a
+                                           # dependent's ownership changed since the last check
     role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
     partition: tuple | None = None         # executor: (p, k) → reconcile only keys with key_part(key, k) == p
 
@@ -79,6 +81,7 @@ class ControllerOptions:
             patch_writes=True,
             sync_secret_type=True,
             rogue_event_on_template=True,
+            adoption_cache=True,
         )
         return replace(base, **kw)
 

@@ -115,6 +115,15 @@ class ReconcileMixin:
                                            patch_type=PATCH_MERGE, field_manager=field_manager, subresource="status")
         return await self.client.update_status(rt, namespace, obj, field_manager=field_manager)
 
+    def _carry_adoption(self, old: dict, new):
+        """Our own status write changes only the template's status: keep its adoption mark (adoption_cache)."""
+        if self.options.adoption_cache and isinstance(new, dict):
+            om, nm = meta(old), meta(new)
+            key = f"{C.KIND_TEMPLATE}/{om.get('namespace', '')}/{om.get('name', '')}"
+            if self._adopted.get(key) == om.get("resourceVersion"):
+                self._adopted[key] = nm.get("resourceVersion")
+        return new
+
     async def report_template_init_condition(self, template: dict) -> dict:
         status = template.get("status") or {}
         if not status.get("conditions"):
@@ -124,7 +133,7 @@ class ReconcileMixin:
             self._pass_wrote()
             res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""), new,
                                            field_manager=C.FIELD_MANAGER)
-            return self._assume(self.template_informer, res)
+            return self._carry_adoption(template, self._assume(self.template_informer, res))
         return template
 
     async def report_workgroup_init_condition(self, workgroup: dict) -> dict:
@@ -171,7 +180,7 @@ class ReconcileMixin:
             self._pass_wrote()
             res = await self._write_status(R.TEMPLATES, meta(template).get("namespace", ""),
                                            with_fields(template, status=new_status), field_manager=C.FIELD_MANAGER)
-            return self._assume(self.template_informer, res)
+            return self._carry_adoption(template, self._assume(self.template_informer, res))
         return template
 
     # ============================================================ ownership (controller.go:482-502)
@@ -252,6 +261,7 @@ class ReconcileMixin:
         if template is None:
             log.debug("NexusAlgorithmTemplate %s/%s referenced by item in work queue no longer exists",
                       namespace, name)
+            self._adopted.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
             if self.role == "coordinator":
                 self.shard_state.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
                 self._pending_event.discard(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
@@ -262,7 +272,14 @@ class ReconcileMixin:
             await self._executor_sync_template(template)
             return
         template = await self.report_template_init_condition(template)
-        await self.adopt_references(template)
+        if self.options.adoption_cache:
+            key = f"{C.KIND_TEMPLATE}/{namespace}/{name}"
+            rv = meta(template).get("resourceVersion")
+            if self._adopted.get(key) != rv:
+                await self.adopt_references(template)
+                self._adopted[key] = rv
+        else:
+            await self.adopt_references(template)
         if self.role == "coordinator":
             await self._coordinator_finish(C.KIND_TEMPLATE, template)
             return

@@ -154,8 +154,9 @@ class WorkQueue:
         """Next key, or None once the queue is shut down and drained of ready keys."""
         loop = asyncio.get_event_loop()
         while True:
-            if self.core.promote(time.monotonic()):
-                self._wake(len(self._waiters))
+            n = self.core.promote(time.monotonic())
+            if n > 1:
+                self._wake(n - 1)  # this caller takes one of the promoted keys; wake one waiter per other
             key = self.core.try_get()
             if key is not None:
                 self._handed_out(key)

@@ -370,3 +370,47 @@ async def test_operational_metrics():
     ctl.on_executor_message(0, {"t": "report", "k": make_key(C.KIND_TEMPLATE, NS, "x"), "u": "u", "g": 1,
                                 "r": {"s0": "ServiceUnavailable: down"}, "w": False})
     assert v[C.SHARD_SYNC_ERRORS_METRIC] == [1.0]
+
+
+async def test_adoption_cache_rechecks_after_dependent_events():
+    """adoption_cache: a second pass over the same template version skips the adoption check, but a
+    dependent event (e.g. the Secret re-created without our ownerRef) invalidates it."""
+    env = Env(1)
+    t = env.seed()
+    name, key = t["metadata"]["name"], make_key(C.KIND_TEMPLATE, NS, t["metadata"]["name"])
+    ctl = env.build()
+    await ctl.sync_template(NS, name)
+    assert env.cstate.get(R.SECRETS, NS, "s")["metadata"]["ownerReferences"][0]["name"] == name
+    env.refresh()
+    cur = ctl.template_lister.get(NS, name)
+    assert ctl._adopted[key] == cur["metadata"]["resourceVersion"]
+    calls = []
+    orig = ctl.adopt_references
+
+    async def spy(tpl):
+        calls.append(tpl["metadata"]["name"])
+        return await orig(tpl)
+    ctl.adopt_references = spy
+    await ctl.sync_template(NS, name)
+    assert calls == []  # unchanged template version, no dependent event: no re-check
+
+    # the Secret is replaced by one without ownerRefs; its informer event invalidates the cache
+    env.cstate.delete(R.SECRETS, NS, "s")
+    fresh = env.cstate.create(R.SECRETS, NS, make_secret("s", NS))
+    env.refresh()
+    ctl._on_dependent(fresh, "secret")
+    assert key not in ctl._adopted
+    await ctl.sync_template(NS, name)
+    assert calls == [name]
+    assert env.cstate.get(R.SECRETS, NS, "s")["metadata"]["ownerReferences"][0]["name"] == name
+
+    # a new template version with the same references inherits the adoption mark
+    old = ctl.template_lister.get(NS, name)
+    new = dict(old, metadata=dict(old["metadata"], resourceVersion="999999"))
+    ctl._adopted[key] = old["metadata"]["resourceVersion"]
+    ctl._on_crd_update(old, new, C.KIND_TEMPLATE)
+    assert ctl._adopted[key] == "999999"
+    changed = dict(new, metadata=dict(new["metadata"], resourceVersion="1000000"),
+                   spec=dict(new["spec"], runtimeEnvironment={"mappedEnvironmentVariables": []}))
+    ctl._on_crd_update(new, changed, C.KIND_TEMPLATE)
+    assert ctl._adopted[key] == "999999"  # references changed: the new version is not marked
