@@ -75,36 +75,43 @@ class BroadcastRecorder(EventRecorder):
     """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
 
     def __init__(self, client: KubeClient, component: str = C.CONTROLLER_AGENT_NAME, *, spam_filter: bool = True,
-                 log_events: bool = True):
+                 log_events: bool = True, writers: int = 1):
         self.client = client
         self.component = component
         self.spam_filter = spam_filter
         self.log_events = log_events
-        self._queue: asyncio.Queue = asyncio.Queue(maxsize=BUFFER)
+        # client-go writes through one sink goroutine; with `writers` > 1 events are spread over that many
+        # writer tasks by involved object, so each object's events (and their dedup PATCHes) stay ordered
+        self.writers = max(1, writers)
+        self._queues: list[asyncio.Queue] = [asyncio.Queue(maxsize=max(1, BUFFER // self.writers))
+                                             for _ in range(self.writers)]
+        self._queue = self._queues[0]
         self._buckets: dict[tuple, TokenBucket] = {}
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
         self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
-        self._task: asyncio.Task | None = None
+        self._tasks: list[asyncio.Task] = []
         self._write_meta = getattr(client, "write_meta", None)  # undecoded writes (REST clients)
         self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0}
 
     def start(self) -> None:
-        if self._task is None:
-            self._task = asyncio.ensure_future(self._run())
+        if not self._tasks:
+            self._tasks = [asyncio.ensure_future(self._run(q)) for q in self._queues]
 
     async def stop(self, drain_timeout: float = 1.0) -> None:
-        if self._task is None:
+        if not self._tasks:
             return
         try:
-            await wait_timeout(self._queue.join(), drain_timeout)
+            await wait_timeout(asyncio.gather(*(q.join() for q in self._queues)), drain_timeout)
         except asyncio.TimeoutError:
             pass
-        self._task.cancel()
-        try:
-            await self._task
-        except (asyncio.CancelledError, Exception):  # noqa: BLE001
-            pass
-        self._task = None
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+        self._tasks = []
 
     def event(self, obj, event_type, reason, message, kind=None):
         self.stats["recorded"] += 1
@@ -112,8 +119,10 @@ class BroadcastRecorder(EventRecorder):
         if self.log_events:
             log.info("Event occurred", extra={"object": f"{ref['namespace']}/{ref['name']}", "kind": ref["kind"],
                                               "type": event_type, "reason": reason, "message": message})
+        q = self._queue if self.writers == 1 else \
+            self._queues[hash((ref["namespace"], ref["name"], ref["kind"])) % self.writers]
         try:
-            self._queue.put_nowait((ref, event_type, reason, message, time.monotonic()))
+            q.put_nowait((ref, event_type, reason, message, time.monotonic()))
         except asyncio.QueueFull:
             self.stats["dropped_full"] += 1
 
@@ -191,9 +200,9 @@ class BroadcastRecorder(EventRecorder):
                 del self._seen[k]
         self.stats["created"] += 1
 
-    async def _run(self) -> None:
+    async def _run(self, queue: asyncio.Queue) -> None:
         while True:
-            ref, event_type, reason, message, _t = await self._queue.get()
+            ref, event_type, reason, message, _t = await queue.get()
             try:
                 for attempt in range(3):
                     try:
@@ -208,4 +217,4 @@ class BroadcastRecorder(EventRecorder):
                         else:
                             await asyncio.sleep(0.1 * (attempt + 1))
             finally:
-                self._queue.task_done()
+                queue.task_done()

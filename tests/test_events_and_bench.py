@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 async def _drain(rec):
-    await asyncio.wait_for(rec._queue.join(), 5)
+    await asyncio.wait_for(asyncio.gather(*(q.join() for q in rec._queues)), 5)
 
 
 async def test_event_dedup_patches_count():
@@ -49,6 +49,23 @@ async def test_event_spam_filter_and_aggregation():
     assert any(m.startswith("(combined from similar events)") for m in msgs)
     # distinct messages beyond the aggregation threshold collapse into one aggregate event
     assert len(msgs) <= 10
+    await rec.stop()
+
+
+async def test_event_writers_keep_per_object_order():
+    """Several writer tasks: each object's events stay on one writer, so dedup PATCHes count correctly."""
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False, writers=4)
+    rec.start()
+    ts = [client.state.create(R.TEMPLATES, "nexus", make_template(i, "nexus")) for i in range(12)]
+    for _ in range(5):
+        for t in ts:
+            rec.event(t, "Normal", "Synced", "Resource of type NexusAlgorithmTemplate synced successfully")
+    await _drain(rec)
+    events = client.state.list(R.EVENTS, "nexus")["items"]
+    assert len(events) == 12 and all(e["count"] == 5 for e in events)
+    assert rec.stats["created"] == 12 and rec.stats["patched"] == 48
+    assert sum(1 for q in rec._queues if q.qsize() == 0) == 4
     await rec.stop()
 
 
