@@ -74,7 +74,7 @@ class Controller(ReconcileMixin):
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
-                      "reports_pending": 0}
+                      "reports_pending": 0, "early_passes_skipped": 0}
         self.ready = asyncio.Event()
         self.role = o.role
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
@@ -132,6 +132,16 @@ class Controller(ReconcileMixin):
                     and om.get("labels") == nm.get("labels") and om.get("annotations") == nm.get("annotations") \
                     and old.get("spec") == new.get("spec"):
                 return  # status-only change (typically our own status write)
+        if self.role == "coordinator" and self.options.adoption_cache:
+            # A new version of an initialised, adopted object has nothing to do here until every shard has
+            # reported on it, and the last report enqueues it: skip the early pass.
+            nm = meta(new)
+            key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
+            if (new.get("status") or {}).get("conditions") and \
+                    (kind != C.KIND_TEMPLATE or self._adopted.get(key) == nm.get("resourceVersion")) and \
+                    self.shard_readiness(key, new) is None:
+                self.stats["early_passes_skipped"] += 1
+                return
         self.enqueue_resource(new, kind)
 
     def _on_dependent(self, obj, index: str):

@@ -414,3 +414,39 @@ async def test_adoption_cache_rechecks_after_dependent_events():
                    spec=dict(new["spec"], runtimeEnvironment={"mappedEnvironmentVariables": []}))
     ctl._on_crd_update(new, changed, C.KIND_TEMPLATE)
     assert ctl._adopted[key] == "999999"  # references changed: the new version is not marked
+
+
+async def test_coordinator_skips_early_pass_until_reports_complete():
+    """A spec update of an initialised, adopted template is not reconciled by the coordinator on its
+    informer event (nothing to do before the executors report); the last report enqueues it — and if
+    every report is already in when the event arrives, the event enqueues it."""
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build(role="coordinator")
+    name = t["metadata"]["name"]
+    key = make_key(C.KIND_TEMPLATE, NS, name)
+    await ctl.sync_template(NS, name)
+    env.refresh()
+    old = ctl.template_lister.get(NS, name)
+    ctl._on_crd_update(old, old, C.KIND_TEMPLATE)  # resync: filtered
+    assert len(ctl.queue) == 0 and ctl.queue.core.waiting() == 0
+    new = dict(old, metadata=dict(old["metadata"], resourceVersion="900", generation=old["metadata"]["generation"] + 1),
+               spec=dict(old["spec"], container=dict(old["spec"]["container"], versionTag="v-next")))
+    ctl._on_crd_update(old, new, C.KIND_TEMPLATE)
+    assert ctl.stats["early_passes_skipped"] == 1 and ctl.queue.core.waiting() == 0 and len(ctl.queue) == 0
+    m = new["metadata"]
+    for i in range(2):
+        ctl.on_executor_message(i, {"t": "report", "k": key, "u": m["uid"], "g": m["generation"],
+                                    "r": {f"s{i}": None}, "w": True})
+    assert ctl.queue.core.waiting() + len(ctl.queue) == 1  # the last report enqueued it
+    # reports already complete for the next version: the informer event itself enqueues
+    ctl.queue.shutdown()
+    ctl2 = env.build(role="coordinator")
+    ctl2._adopted[key] = new["metadata"]["resourceVersion"]
+    newer = dict(new, metadata=dict(m, resourceVersion="901", generation=m["generation"] + 1))
+    for i in range(2):
+        ctl2.on_executor_message(i, {"t": "report", "k": key, "u": m["uid"], "g": m["generation"] + 1,
+                                     "r": {f"s{i}": None}, "w": True})
+    before = ctl2.queue.core.waiting() + len(ctl2.queue)
+    ctl2._on_crd_update(new, newer, C.KIND_TEMPLATE)
+    assert ctl2.stats["early_passes_skipped"] == 0 and ctl2.queue.core.waiting() + len(ctl2.queue) >= before
