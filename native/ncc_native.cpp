@@ -20,7 +20,8 @@
 //    executor can drop dependents owned only by another partition's templates without decoding them.
 //  * scan_event_part(bytes, parts, ns) — the same plus the crc32 key partition of the object and the
 //    bitmask of its owners' partitions, so the partition test itself builds no Python strings.
-//  * parse_response_head(bytes) — status and the framing headers of an HTTP/1.1 response.
+//  * parse_response_head(bytes) / parse_request_head(bytes) — HTTP/1.1 heads for the client transport
+//    and the fake apiserver.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
 //  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
@@ -45,7 +46,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 10
+#define NCC_NATIVE_ABI 11
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -731,6 +732,56 @@ py::object parse_response_head(py::bytes head) {
     return py::make_tuple(status, clen, chunked, close, retry);
 }
 
+// parse_request_head(head) -> (method, target, {lower-cased header name: value}) of an HTTP/1.1 request
+// head (everything before the blank line); used by the fake apiserver's HTTP server.
+py::object parse_request_head(py::bytes head) {
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(head.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view h(buf, static_cast<size_t>(len));
+    size_t eol = h.find("\r\n");
+    std::string_view first = h.substr(0, eol);
+    size_t s1 = first.find(' ');
+    size_t s2 = s1 == std::string_view::npos ? s1 : first.find(' ', s1 + 1);
+    if (s1 == std::string_view::npos || s2 == std::string_view::npos || s1 == 0 || s2 == s1 + 1)
+        throw py::value_error("bad request line");
+    std::string_view method = first.substr(0, s1), target = first.substr(s1 + 1, s2 - s1 - 1);
+    py::dict headers;
+    std::string key;
+    size_t pos = eol == std::string_view::npos ? h.size() : eol + 2;
+    while (pos < h.size()) {
+        size_t e = h.find("\r\n", pos);
+        std::string_view line = h.substr(pos, e == std::string_view::npos ? std::string_view::npos : e - pos);
+        pos = e == std::string_view::npos ? h.size() : e + 2;
+        size_t c = line.find(':');
+        if (c == std::string_view::npos) continue;
+        std::string_view k = trim(line.substr(0, c)), v = trim(line.substr(c + 1));
+        key.assign(k.data(), k.size());
+        for (auto& ch : key)
+            if (ch >= 'A' && ch <= 'Z') ch = static_cast<char>(ch - 'A' + 'a');
+        // latin-1 like the pure-Python server: every byte maps to one code point
+        PyObject* ks = PyUnicode_DecodeLatin1(key.data(), static_cast<Py_ssize_t>(key.size()), nullptr);
+        PyObject* vs = PyUnicode_DecodeLatin1(v.data(), static_cast<Py_ssize_t>(v.size()), nullptr);
+        if (ks == nullptr || vs == nullptr) {
+            Py_XDECREF(ks);
+            Py_XDECREF(vs);
+            throw py::error_already_set();
+        }
+        int rc = PyDict_SetItem(headers.ptr(), ks, vs);
+        Py_DECREF(ks);
+        Py_DECREF(vs);
+        if (rc != 0) throw py::error_already_set();
+    }
+    PyObject* ms = PyUnicode_DecodeLatin1(method.data(), static_cast<Py_ssize_t>(method.size()), nullptr);
+    PyObject* ts = PyUnicode_DecodeLatin1(target.data(), static_cast<Py_ssize_t>(target.size()), nullptr);
+    if (ms == nullptr || ts == nullptr) {
+        Py_XDECREF(ms);
+        Py_XDECREF(ts);
+        throw py::error_already_set();
+    }
+    return py::make_tuple(py::reinterpret_steal<py::object>(ms), py::reinterpret_steal<py::object>(ts), headers);
+}
+
 
 // ----------------------------------------------------------------------------- JSON encoder
 // dumps(obj) -> bytes: compact JSON (separators "," and ":") of a JSON-shaped Python value, key order
@@ -878,6 +929,8 @@ PYBIND11_MODULE(_native, m) {
           "scan_event_owners plus the key partition and the owner-partition bitmask (crc32 % parts)");
     m.def("parse_response_head", &parse_response_head, py::arg("head"),
           "(status, content_length|-1, chunked, connection_close, retry_after|None) of an HTTP/1.1 response head");
+    m.def("parse_request_head", &parse_request_head, py::arg("head"),
+          "(method, target, {lower-cased name: value}) of an HTTP/1.1 request head");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");

@@ -16,6 +16,8 @@ import asyncio
 import json
 from urllib.parse import parse_qsl, unquote
 
+from .. import native as _native
+
 _CRLF2 = b"\r\n\r\n"
 _HEADS: dict = {}
 _REASONS = {200: "OK", 201: "Created", 204: "No Content", 400: "Bad Request", 401: "Unauthorized",
@@ -171,17 +173,12 @@ class _ServerConn(asyncio.Protocol):
                 if len(buf) > 1 << 20:
                     self.transport.close()
                 return
-            lines = bytes(buf[:i]).split(b"\r\n")
             try:
-                method, target, _ = lines[0].decode("latin-1").split(" ", 2)
+                method, target, headers = _parse_head(bytes(buf[:i]))
+                clen = int(headers.get("content-length", "0") or 0)
             except ValueError:
                 self.transport.close()
                 return
-            headers = {}
-            for ln in lines[1:]:
-                k, _, v = ln.partition(b":")
-                headers[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
-            clen = int(headers.get("content-length", "0") or 0)
             if len(buf) < i + 4 + clen:
                 return  # wait for the full body
             body = bytes(buf[i + 4:i + 4 + clen])
@@ -220,6 +217,21 @@ class _ServerConn(asyncio.Protocol):
             return
         if self.buf:
             self._next()
+
+
+def _parse_head_py(head: bytes) -> tuple:
+    lines = head.split(b"\r\n")
+    method, target, _ = lines[0].decode("latin-1").split(" ", 2)
+    headers = {}
+    for ln in lines[1:]:
+        k, sep, v = ln.partition(b":")
+        if sep:  # a line without a colon is not a header
+            headers[k.strip().lower().decode("latin-1")] = v.strip().decode("latin-1")
+    return method, target, headers
+
+
+_native_mod = _native.load()
+_parse_head = getattr(_native_mod, "parse_request_head", None) or _parse_head_py
 
 
 class HttpServer:

@@ -28,7 +28,7 @@ import time
 from . import httpserver as web
 
 from ..api import resources as R
-from ..api.jsonenc import dumps_bytes
+from ..api.jsonenc import dumps_bytes, loads_bytes
 from ..aio import wait_timeout
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
@@ -240,11 +240,11 @@ class FakeApiServer:
             return {}
         if request.content_type == PATCH_APPLY:
             try:
-                return json.loads(raw)
+                return loads_bytes(raw)
             except ValueError:
                 import yaml
                 return yaml.safe_load(raw)
-        return json.loads(raw)
+        return loads_bytes(raw)
 
     @staticmethod
     def _json(obj, status: int = 200) -> web.Response:

@@ -193,3 +193,16 @@ def test_native_response_head_parser_rejects_malformed(head):
     from ncc import native
     with pytest.raises(ValueError):
         native.load(required=True).parse_response_head(head)
+
+
+def test_native_request_head_parser_matches_python():
+    from ncc import native
+    from ncc.fakeapi.httpserver import _parse_head_py
+    m = native.load(required=True)
+    for head in (b"PUT /api/v1/namespaces/n/secrets/a?fieldManager=x HTTP/1.1\r\nHost: h:1\r\nContent-Length: 12",
+                 b"GET /apis/x/y?watch=1 HTTP/1.1\r\nAuthorization:  Bearer t \r\nX-Odd: a: b\r\nNoColonLine",
+                 b"DELETE /a HTTP/1.1"):
+        assert m.parse_request_head(head) == _parse_head_py(head)
+    for bad in (b"GARBAGE", b"GET /only-two", b" / HTTP/1.1"):
+        with pytest.raises(ValueError):
+            m.parse_request_head(bad)
