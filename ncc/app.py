@@ -50,7 +50,8 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
               rate_limit_burst=cfg.rate_limit_elements_burst, resync_period=cfg.resync_period)
     if cfg.mode == "native":
         kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout,
-                  server_side_apply=cfg.server_side_apply, controller_adoption=cfg.controller_adoption)
+                  server_side_apply=cfg.server_side_apply, controller_adoption=cfg.controller_adoption,
+                  coalesce_window=cfg.coalesce_window)
     opts = ControllerOptions.for_mode(cfg.mode, **kw)
     # expert/ablation overrides: NCC_OPT_<FIELD>=value (e.g. NCC_OPT_COALESCE_WINDOW=0)
     for f, cur in opts.as_dict().items():

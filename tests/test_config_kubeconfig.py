@@ -231,3 +231,16 @@ def test_klog_style_flags(monkeypatch, capsys):
     monkeypatch.setattr(app, "configure_logging", lambda *a, **k: None)
     assert app.main(["-v=4"]) == 0 and seen["level"] == "DEBUG"
     assert app.main(["-v", "2"]) == 0 and seen["level"] == "INFO"
+
+
+def test_coalesce_window_key_reaches_native_options(monkeypatch):
+    from ncc.app import options_from_config
+    from ncc.config import AppConfig
+    assert AppConfig().coalesce_window == 0.002
+    monkeypatch.setenv("NEXUS__COALESCE_WINDOW", "7ms")
+    from ncc.config import load_config
+    cfg = load_config(None)
+    assert cfg.coalesce_window == 0.007
+    assert options_from_config(cfg).coalesce_window == 0.007
+    cfg.mode = "compat"
+    assert options_from_config(cfg).coalesce_window == 0.0  # reference: every event enqueues at once
