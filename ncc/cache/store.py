@@ -26,6 +26,7 @@ class Store:
         self._items: dict[ObjectKey, dict] = {}
         self._indexers: dict[str, IndexFunc] = {}
         self._indices: dict[str, dict[str, set]] = {}
+        self._index_vals: dict[str, dict[ObjectKey, tuple]] = {}  # indexer → key → its current values
         self._assumed: dict[ObjectKey, tuple[dict, int, float]] = {}
         self._tombstones: dict[ObjectKey, int] = {}  # key -> RV of the observed delete
         self.transform = transform
@@ -35,24 +36,38 @@ class Store:
     def add_indexer(self, name: str, fn: IndexFunc) -> None:
         self._indexers[name] = fn
         idx: dict[str, set] = {}
+        vals: dict[ObjectKey, tuple] = {}
         for k, o in self._items.items():
-            for v in fn(o):
+            vs = tuple(fn(o))
+            if vs:
+                vals[k] = vs
+            for v in vs:
                 idx.setdefault(v, set()).add(k)
         self._indices[name] = idx
+        self._index_vals[name] = vals
 
     def _index(self, key: ObjectKey, old: dict | None, new: dict | None) -> None:
+        """Move `key` between index buckets.  Each key's current index values are remembered, so an update
+        that leaves them unchanged (the common case: a spec edit keeps the references) touches no set."""
         for name, fn in self._indexers.items():
+            vals = self._index_vals[name]
+            ov = vals.get(key, ())
+            nv = tuple(fn(new)) if new is not None else ()
+            if ov == nv:
+                continue
             idx = self._indices[name]
-            if old is not None:
-                for v in fn(old):
-                    s = idx.get(v)
-                    if s is not None:
-                        s.discard(key)
-                        if not s:
-                            del idx[v]
-            if new is not None:
-                for v in fn(new):
-                    idx.setdefault(v, set()).add(key)
+            for v in ov:
+                s = idx.get(v)
+                if s is not None:
+                    s.discard(key)
+                    if not s:
+                        del idx[v]
+            for v in nv:
+                idx.setdefault(v, set()).add(key)
+            if nv:
+                vals[key] = nv
+            else:
+                vals.pop(key, None)
 
     def by_index(self, name: str, value: str) -> list[dict]:
         return [self._items[k] for k in self._indices.get(name, {}).get(value, ()) if k in self._items]
@@ -112,10 +127,15 @@ class Store:
                     del self._assumed[k]
         for name, fn in self._indexers.items():
             idx: dict[str, set] = {}
+            vals: dict[ObjectKey, tuple] = {}
             for k, o in new_items.items():
-                for v in fn(o):
+                vs = tuple(fn(o))
+                if vs:
+                    vals[k] = vs
+                for v in vs:
                     idx.setdefault(v, set()).add(k)
             self._indices[name] = idx
+            self._index_vals[name] = vals
         return added, updated, deleted
 
     def assume(self, obj: dict, transformed: bool = False) -> None:

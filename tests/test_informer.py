@@ -264,3 +264,26 @@ async def test_metadata_only_skips_payload_updates_but_not_owner_changes():
     finally:
         await client.close()
         await srv.stop()
+
+
+def test_store_index_tracks_value_changes_and_relists():
+    from ncc.cache.store import Store
+    from ncc.testing.workload import make_template
+    st = Store()
+    st.add_indexer("secret", lambda t: [f"nexus/{n}" for n in
+                                        [e.get("secretRef", {}).get("name") for e in
+                                         t["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"]] if n])
+    t = make_template(0, "nexus", secrets=["a"])
+    st.upsert(t)
+    assert [o["metadata"]["name"] for o in st.by_index("secret", "nexus/a")] == ["algo-00000"]
+    t2 = make_template(0, "nexus", secrets=["a"], version="v9")  # same references: buckets untouched
+    st.upsert(t2)
+    assert st.by_index("secret", "nexus/a")[0]["spec"]["container"]["versionTag"] == "v9"
+    st.upsert(make_template(0, "nexus", secrets=["b"]))  # moved to another bucket
+    assert st.by_index("secret", "nexus/a") == [] and len(st.by_index("secret", "nexus/b")) == 1
+    st.upsert(make_template(0, "nexus", secrets=[]))  # no references left
+    assert st.by_index("secret", "nexus/b") == [] and st._index_vals["secret"] == {}
+    st.replace([make_template(1, "nexus", secrets=["c"])])
+    assert len(st.by_index("secret", "nexus/c")) == 1
+    st.delete(make_template(1, "nexus", secrets=["c"]))
+    assert st.by_index("secret", "nexus/c") == [] and st._index_vals["secret"] == {}
