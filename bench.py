@@ -219,10 +219,9 @@ async def run(args, d: Dist) -> dict | None:
                             "NEXUS__CONTROLLER_NAMESPACE": NS, "NEXUS__ALIAS": "controller-cluster",
                             "NEXUS__MODE": args.mode, "NEXUS__LOG_LEVEL": "WARNING",
                             "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
-                if args.workers:
+                if args.workers:  # native: per-process workers (otherwise the config's native-workers default)
                     env["NEXUS__WORKERS"] = str(args.workers)
-                elif args.mode == "native":
-                    env["NEXUS__WORKERS"] = "64"
+                    env["NEXUS__NATIVE_WORKERS"] = str(args.workers)
                 for kv in args.extra_env:
                     k, _, v = kv.partition("=")
                     env[k] = v

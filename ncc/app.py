@@ -49,6 +49,9 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
               failure_max_delay=cfg.failure_rate_max_delay, rate_limit_qps=float(cfg.rate_limit_elements_per_second),
               rate_limit_burst=cfg.rate_limit_elements_burst, resync_period=cfg.resync_period)
     if cfg.mode == "native":
+        # the reference's `workers` (Helm default 2) sized sequential Go reconciles; a native process hides
+        # shard RTTs behind cheap coroutines, so it runs at least `native-workers`
+        kw["workers"] = max(cfg.workers, cfg.native_workers)
         kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout,
                   server_side_apply=cfg.server_side_apply, controller_adoption=cfg.controller_adoption,
                   coalesce_window=cfg.coalesce_window)

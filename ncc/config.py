@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `native-workers`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -70,6 +70,8 @@ class AppConfig:
     controller_namespace: str = "nexus"
     log_level: str = "INFO"
     workers: int = 2
+    native_workers: int = 32         # native: reconcile workers per process (coordinator, each executor);
+                                     # `workers` raises it when larger (box sweep: 16–32 best, 64 worse)
     failure_rate_base_delay: float = _dur(0.030)
     failure_rate_max_delay: float = _dur(5.0)
     rate_limit_elements_per_second: int = 50

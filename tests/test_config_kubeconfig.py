@@ -244,3 +244,15 @@ def test_coalesce_window_key_reaches_native_options(monkeypatch):
     assert options_from_config(cfg).coalesce_window == 0.007
     cfg.mode = "compat"
     assert options_from_config(cfg).coalesce_window == 0.0  # reference: every event enqueues at once
+
+
+def test_native_workers_floor():
+    from ncc.app import options_from_config
+    from ncc.config import AppConfig
+    cfg = AppConfig(mode="native")  # reference default workers=2
+    assert options_from_config(cfg).workers == 32
+    cfg.workers = 64
+    assert options_from_config(cfg).workers == 64
+    cfg.native_workers, cfg.workers = 8, 2
+    assert options_from_config(cfg).workers == 8
+    assert options_from_config(AppConfig(mode="compat")).workers == 2  # reference semantics
