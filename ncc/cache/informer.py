@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import asyncio
 import inspect
-import json
 import logging
 import random
 from dataclasses import dataclass
