@@ -53,6 +53,8 @@ def parse_args(argv=None):
     p.add_argument("--timeout", type=float, default=600.0, help="per-wave convergence timeout (s)")
     p.add_argument("--keep", action="store_true", help="keep the work directory")
     p.add_argument("--extra-env", action="append", default=[], help="KEY=VAL passed to the controller process")
+    p.add_argument("--shards-per-rank", type=int, default=1,
+                   help="experiments only: shard apiservers hosted per rank (the driver contract is 1)")
     return p.parse_args(argv)
 
 
@@ -192,10 +194,14 @@ async def run(args, d: Dist) -> dict | None:
     procs = []
     try:
         extra = sum((["--marker", m] for m in MARKERS), [])
-        pf = os.path.join(work, "shard.url")
-        procs.append(spawn_fakeapi(f"shard-{d.rank}", pf, extra=extra))
-        my_url = wait_port_file(pf, procs[-1])
-        urls = d.all_gather(my_url)
+        S = max(1, args.shards_per_rank)
+        my_urls = []
+        for j in range(S):
+            pf = os.path.join(work, f"shard{j}.url")
+            procs.append(spawn_fakeapi(f"shard-{d.rank * S + j}", pf, extra=extra))
+            my_urls.append(wait_port_file(pf, procs[-1]))
+        my_url = my_urls[0]
+        urls = [u for us in d.all_gather(my_urls) for u in us]
         ctrl_url = None
         controller = None
         T = args.templates
@@ -203,6 +209,7 @@ async def run(args, d: Dist) -> dict | None:
             cpf = os.path.join(work, "controller.url")
             procs.append(spawn_fakeapi("controller", cpf, extra=extra))
             ctrl_url = wait_port_file(cpf, procs[-1])
+            ctrl_proc = procs[-1]
             shard_dir = os.path.join(work, "shards")
             os.makedirs(shard_dir)
             for i, u in enumerate(urls):
@@ -233,15 +240,22 @@ async def run(args, d: Dist) -> dict | None:
             t_boot = d.broadcast(t_boot if d.rank == 0 else None)
             named = {"shard-apiserver": procs[0]}
             if d.rank == 0:
-                named.update({"controller-apiserver": procs[1], "coordinator": controller})
+                named.update({"controller-apiserver": ctrl_proc, "coordinator": controller})
 
             total = args.warmup + args.steps
             bodies = {}
             if d.rank == 0:
                 bodies = {v: wave_body(T, v, args.payload) for v in range(1, total + 1)}
 
-            async def converge(version: int, times: bool, url=my_url):
-                r = await post(session, f"{url}/_fake/markers/wait",
+            async def converge(version: int, times: bool, url=None):
+                if url is None and S > 1:  # every shard this rank hosts; times keyed per shard
+                    rs = await asyncio.gather(*(converge(version, times, u) for u in my_urls))
+                    merged = {}
+                    for j, r in enumerate(rs):
+                        for marker, objs in (r.get("times") or {}).items():
+                            merged.setdefault(marker, {}).update({f"{j}:{k}": t for k, t in objs.items()})
+                    return {"ok": True, "times": merged}
+                r = await post(session, f"{url or my_url}/_fake/markers/wait",
                                {"want": want(T, version), "timeout": args.timeout, "times": times, "keyed": True},
                                timeout=args.timeout + 30)
                 if not r["ok"]:
@@ -302,8 +316,8 @@ async def run(args, d: Dist) -> dict | None:
                 for wave, ctrl in zip(per_rank, ctrl_times):
                     for marker, objs in wave.items():
                         c = ctrl[marker]
-                        lat.extend((t - c[k]) / 1e6 for k, t in objs.items())
-            objs = args.steps * 3 * T * d.world
+                        lat.extend((t - c[k.split(":", 1)[-1]]) / 1e6 for k, t in objs.items())
+            objs = args.steps * 3 * T * d.world * S
             value = objs / elapsed
             ctrl_alive = controller.poll() is None
             return {
@@ -321,11 +335,11 @@ async def run(args, d: Dist) -> dict | None:
                 "data": "synthetic (fake kube-apiservers, random NexusAlgorithmTemplate/Secret/ConfigMap objects)",
                 "config": {"model": "NexusAlgorithmTemplate fan-out (1 Secret + 1 ConfigMap each)",
                            "global_batch": T, "seq_len": 3, "parallelism": f"shards{d.world}",
-                           "templates": T, "shards": d.world, "mode": args.mode, "payload_bytes": args.payload},
+                           "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
                 "cold_start_s": round(cold, 3),
-                "cold_start_objects_per_s": round(3 * T * d.world / cold, 1) if cold > 0 else None,
+                "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
                 # busy CPU cores per process over the timed steps (rank 0's, plus the busiest shard server)
                 "cpu_cores_busy": dict(utils[0], **{"shard-apiserver-max": max(u.get("shard-apiserver", 0.0)
