@@ -29,7 +29,7 @@ from .cache.informer import InformerFactory
 from .config import AppConfig, config_to_env, load_config
 from .controller.controller import Controller
 from .controller.events import BroadcastRecorder, FakeRecorder
-from .controller.executor import ExecutorPool, partition_filter, partition_owner_filter
+from .controller.executor import CoordinatorPartitions, ExecutorPool, partition_filter, partition_owner_filter
 from .controller.options import ControllerOptions
 from .kube.client import RateLimitedClient
 from .kube.kubeconfig import build_config
@@ -140,6 +140,28 @@ def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
     return max(1, min(3, math.ceil(0.75 * cpus / max(1, groups))))
 
 
+def auto_coordinator_partitions(groups: int, per_shard: int, cpus: int | None = None) -> int:
+    """Coordinator processes: one per executor key partition once there are ≥ 4 shard groups and CPUs to spare
+    (≥ 32 per extra coordinator).  At 8 shards one coordinator spends ~210 µs per template pass on the box
+    (profiles/r1/session2/spr_8.json), which caps a single process near 110k objects/s."""
+    cpus = cpu_share() if cpus is None else cpus
+    if groups < 4:
+        return 1
+    return max(1, min(per_shard, cpus // 32))
+
+
+def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int) -> tuple | None:
+    """(p, C) for this coordinator process, or None when the coordinator is not split."""
+    env = os.environ.get("NCC_COORDINATOR_PART")
+    if env:  # a child started by CoordinatorPartitions
+        pi, _, pk = env.partition("/")
+        p, c = int(pi), int(pk)
+        return (p, c) if c > 1 else None
+    c = cfg.coordinator_partitions if cfg.coordinator_partitions > 0 else \
+        auto_coordinator_partitions(groups, per_shard)
+    return (0, c) if c > 1 else None
+
+
 class App:
     """Wires and owns every component of one controller process."""
 
@@ -166,6 +188,8 @@ class App:
         self._gc_task = None
         self._shard_files: dict = {}
         self.lost_leadership = False
+        self.coord_part: tuple | None = None  # (p, C) when the coordinator role is split over C processes
+        self.partitions: CoordinatorPartitions | None = None  # children for partitions 1..C-1 (parent only)
 
     async def build(self) -> Controller:
         cfg, o = self.cfg, self.options
@@ -187,6 +211,18 @@ class App:
                 client = RateLimitedClient(client, qps, burst)
         self.client = client
         self.factory = InformerFactory(client, cfg.controller_namespace, o.resync_period)
+        all_names = [n for n, _ in discover(cfg.shard_config_path)]
+        self._shard_files = shard_files(cfg.shard_config_path)
+        if o.role == "all" and o.mode == "native" and all_names:
+            n = cfg.executors if cfg.executors >= 0 else len(all_names)
+            self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
+            if self.n_executors > 0:
+                o.role = "coordinator"
+                self.per_shard = (cfg.executors_per_shard if cfg.executors_per_shard > 0
+                                  else auto_executors_per_shard(self.n_executors))
+                self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard)
+                if self.coord_part is not None:
+                    o.partition = self.coord_part  # this coordinator's share of the template keys
         kf = partition_filter(*o.partition) if o.partition is not None else None
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
@@ -198,15 +234,6 @@ class App:
             for rt, index in ((R.SECRETS, "secret"), (R.CONFIGMAPS, "configmap")):
                 infs[rt].owner_filter = partition_owner_filter(
                     *o.partition, referenced=lambda ns, name, i=index: bool(tstore.by_index(i, f"{ns}/{name}")))
-        all_names = [n for n, _ in discover(cfg.shard_config_path)]
-        self._shard_files = shard_files(cfg.shard_config_path)
-        if o.role == "all" and o.mode == "native" and all_names:
-            n = cfg.executors if cfg.executors >= 0 else len(all_names)
-            self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
-            if self.n_executors > 0:
-                o.role = "coordinator"
-                self.per_shard = (cfg.executors_per_shard if cfg.executors_per_shard > 0
-                                  else auto_executors_per_shard(self.n_executors))
         if o.role == "coordinator":
             self.shards = []
             # the coordinator adopts and reports; it never copies payloads: keep metadata only and skip
@@ -295,7 +322,8 @@ class App:
         """Ready once caches synced and workers run — or while standing by for the leader Lease."""
         if self.elector is not None and not self.elector.leading:
             return not self.lost_leadership
-        return self.controller is not None and self.controller.ready.is_set()
+        return self.controller is not None and self.controller.ready.is_set() and \
+            (self.partitions is None or self.partitions.ready())
 
     def debug_state(self) -> dict:
         c = self.controller
@@ -303,6 +331,8 @@ class App:
         out["events"] = getattr(self.recorder, "stats", {})
         if self.pool is not None:
             out["executors"] = self.pool.stats()
+        if self.partitions is not None:
+            out["coordinator_partitions"] = self.partitions.stats()
         if self.elector is not None:
             out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
                              "transitions": self.elector.transitions}
@@ -339,9 +369,14 @@ class App:
         if self.options.role == "coordinator":
             env = dict(os.environ)
             env.update(config_to_env(self.cfg))
+            env.pop("NCC_COORDINATOR_PART", None)
+            part, parts = self.coord_part or (0, 1)
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
-                                     env=env, per_shard=self.per_shard)
+                                     env=env, per_shard=self.per_shard, part_base=part, part_stride=parts)
             self.pool.start()
+            if parts > 1 and part == 0 and not os.environ.get("NCC_COORDINATOR_PART"):
+                self.partitions = CoordinatorPartitions(parts, env)
+                self.partitions.start()
         if self.cfg.mode == "native":
             gctune.tune()
             self._gc_task = asyncio.ensure_future(gctune.freeze_loop())
@@ -362,6 +397,8 @@ class App:
             if t is not None:
                 t.cancel()
                 await asyncio.gather(t, return_exceptions=True)
+        if self.partitions is not None:
+            await self.partitions.stop()
         if self.pool is not None:
             await self.pool.stop()
         if isinstance(self.recorder, BroadcastRecorder):
@@ -407,7 +444,7 @@ def setup_signal_handler(stop: asyncio.Event) -> None:
             pass
 
 
-async def _amain(cfg: AppConfig) -> int:
+async def _amain(cfg: AppConfig, control_fd: int | None = None) -> int:
     stop = asyncio.Event()
     setup_signal_handler(stop)
     app = App(cfg)
@@ -416,7 +453,27 @@ async def _amain(cfg: AppConfig) -> int:
     except Exception as e:  # noqa: BLE001
         log.error("Error building controller: %s", e)
         return 1
-    await app.run(stop)
+    watcher = None
+    if control_fd is not None:
+        # a coordinator partition started by its parent: report readiness; the parent closing the channel
+        # (or dying) ends this process
+        import socket
+
+        from .controller.ipc import Channel
+        reader, writer = await asyncio.open_connection(sock=socket.socket(fileno=control_fd))
+        channel = Channel(reader, writer)
+        app.controller.on_ready = lambda: channel.send({"t": "ready"})
+
+        async def watch_parent():
+            while await channel.recv() is not None:
+                pass
+            stop.set()
+        watcher = asyncio.ensure_future(watch_parent())
+    try:
+        await app.run(stop)
+    finally:
+        if watcher is not None:
+            watcher.cancel()
     return 1 if app.lost_leadership else 0
 
 
@@ -442,6 +499,7 @@ def main(argv=None) -> int:
     p = argparse.ArgumentParser(prog="python -m ncc", description="Nexus multi-cluster configuration controller")
     p.add_argument("--config-dir", default=None, help="directory holding appconfig.yaml (default: cwd)")
     p.add_argument("--version", action="store_true")
+    p.add_argument("--control-fd", type=int, default=None, help=argparse.SUPPRESS)  # coordinator partitions
     p.add_argument("-v", "--v", type=int, default=None, metavar="N",
                    help="klog verbosity: N>=4 logs at DEBUG (overrides log-level), N<4 leaves log-level as set")
     for f in _KLOG_VALUE_FLAGS:
@@ -465,9 +523,10 @@ def main(argv=None) -> int:
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+        part = os.environ.get("NCC_COORDINATOR_PART", "").replace("/", "of")
         try:
-            return asyncio.run(_amain(cfg))
+            return asyncio.run(_amain(cfg, args.control_fd))
         finally:
             prof.disable()
-            prof.dump_stats(prof_path)
-    return asyncio.run(_amain(cfg))
+            prof.dump_stats(prof_path + (f".coordinator{part}" if part else ""))
+    return asyncio.run(_amain(cfg, args.control_fd))

@@ -76,7 +76,9 @@ def partition_owner_filter(part: int, parts: int, referenced=None):
 
 class ExecutorHandle:
     def __init__(self, index: int, shards: list[str], on_message, env: dict | None = None,
-                 part: int = 0, parts: int = 1):
+                 part: int = 0, parts: int = 1, argv: list | None = None, what: str = "executor"):
+        self.argv = argv  # child command after `python`; default: the shard executor
+        self.what = what
         self.index = index
         self.shards = shards
         self.part = part
@@ -95,10 +97,12 @@ class ExecutorHandle:
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(self.env or os.environ)
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
-        self.proc = await asyncio.create_subprocess_exec(
-            sys.executable, "-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
-            "--shards", ",".join(self.shards), "--part", f"{self.part}/{self.parts}",
-            pass_fds=(child.fileno(),), env=env)
+        if self.argv is not None:
+            args = [*self.argv, "--control-fd", str(child.fileno())]
+        else:
+            args = ["-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
+                    "--shards", ",".join(self.shards), "--part", f"{self.part}/{self.parts}"]
+        self.proc = await asyncio.create_subprocess_exec(sys.executable, *args, pass_fds=(child.fileno(),), env=env)
         child.close()
         reader, writer = await asyncio.open_connection(sock=parent)
         self.channel = Channel(reader, writer)
@@ -121,8 +125,8 @@ class ExecutorHandle:
             if self._stopping:
                 return
             self.restarts += 1
-            log.error("executor %d (shards %s) exited with %s; restarting in %.1fs", self.index, self.shards, rc,
-                      backoff)
+            log.error("%s %d (shards %s) exited with %s; restarting in %.1fs", self.what, self.index, self.shards,
+                      rc, backoff)
             await asyncio.sleep(backoff)
             backoff = min(backoff * 2, 30.0)
 
@@ -152,8 +156,14 @@ class ExecutorPool:
     """`n` shard groups × `per_shard` key partitions.  Every executor of a group watches the same shards;
     each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
 
-    def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1):
+    def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
+                 part_base: int = 0, part_stride: int = 1):
+        """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
+        mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
+        keys are exactly a share of this coordinator's."""
         self.per_shard = max(1, per_shard)
+        self.part_base = part_base
+        self.part_stride = max(1, part_stride)
         self.on_message = on_message
         self.env = env
         self._next_index = 0
@@ -162,8 +172,9 @@ class ExecutorPool:
             self._new_group(group)
 
     def _new_group(self, shards: list[str]) -> list[ExecutorHandle]:
-        hs = [ExecutorHandle(self._next_index + p, list(shards), self.on_message, self.env, p, self.per_shard)
-              for p in range(self.per_shard)]
+        hs = [ExecutorHandle(self._next_index + j, list(shards), self.on_message, self.env,
+                             self.part_base + self.part_stride * j, self.part_stride * self.per_shard)
+              for j in range(self.per_shard)]
         self._next_index += self.per_shard
         self.handles.extend(hs)
         return hs
@@ -206,6 +217,39 @@ class ExecutorPool:
 
     def stats(self) -> dict:
         return {h.index: {"shards": h.shards, "part": f"{h.part}/{h.parts}", "restarts": h.restarts,
+                          "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
+
+
+class CoordinatorPartitions:
+    """Child coordinator processes for key partitions 1..C-1 (partition 0 is the parent itself).
+
+    Each child is a full native-mode coordinator (`python -m ncc`) restricted to the template keys
+    ≡ p mod C: it watches the controller cluster with that key filter, adopts, writes status and Events
+    for its keys, and runs its own shard executors (global partitions p + C·j).  The parent holds the
+    leader Lease and the ops endpoints; children exit when the parent's control channel closes."""
+
+    def __init__(self, parts: int, env: dict):
+        self.parts = parts
+        self.handles = []
+        for p in range(1, parts):
+            e = dict(env)
+            e.update({"NCC_COORDINATOR_PART": f"{p}/{parts}", "NEXUS__LEADER_ELECT": "False",
+                      "NEXUS__METRICS_BIND_ADDRESS": "", "NEXUS__HEALTH_BIND_ADDRESS": ""})
+            self.handles.append(ExecutorHandle(p, [], lambda i, m: None, e, p, parts, argv=["-m", "ncc"],
+                                               what="coordinator partition"))
+
+    def start(self) -> None:
+        for h in self.handles:
+            h.start()
+
+    def ready(self) -> bool:
+        return all(h.ready.is_set() for h in self.handles)
+
+    async def stop(self) -> None:
+        await asyncio.gather(*(h.stop() for h in self.handles))
+
+    def stats(self) -> dict:
+        return {h.index: {"part": f"{h.part}/{h.parts}", "restarts": h.restarts, "ready": h.ready.is_set(),
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
 
 

@@ -215,6 +215,14 @@ class ReconcileMixin:
                                              self.configmap_informer)):
             for nm in names:
                 ref = lister.try_get(ns, nm)
+                if ref is None and informer.owner_filter is not None:
+                    # a partitioned coordinator may have dropped it off the wire (owned only by other
+                    # partitions' templates when it arrived): read it once
+                    try:
+                        await self._fetch_filtered(informer, rt, ns, nm)
+                    except E.NotFound:
+                        pass
+                    ref = lister.try_get(ns, nm)
                 if ref is None:
                     self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
                                         C.MESSAGE_RESOURCE_MISSING.format(q(nm), q(tname)), kind=C.TEMPLATE_KIND)

@@ -223,7 +223,7 @@ def test_klog_style_flags(monkeypatch, capsys):
     assert capsys.readouterr().out.strip() == app.__version__
     seen = {}
 
-    async def fake_amain(cfg):
+    async def fake_amain(cfg, control_fd=None):
         seen["level"] = cfg.log_level
         return 0
     monkeypatch.setattr(app, "_amain", fake_amain)

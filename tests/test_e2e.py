@@ -424,3 +424,73 @@ async def test_partition_filter_keeps_newly_referenced_dependent(tmp_path):
         await cc.close()
         await sc.close()
         await env.stop()
+
+
+async def test_partitioned_coordinators(tmp_path):
+    """coordinator-partitions=2: the template keys are split between the parent coordinator and one child
+    coordinator process, each with its own executors.  Every template still becomes Ready, shared
+    dependents are adopted by all their templates, and a killed child is restarted and resumes its keys."""
+    import os
+    import signal
+    from ncc.controller.executor import key_part
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc = env.controller_client()
+    scs = [env.shard_client(i) for i in range(2)]
+    T = 12
+    try:
+        await cc.create(R.SECRETS, NS, make_secret("shared", NS))
+        for i in range(T):
+            await cc.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
+            await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=["shared"], configmaps=[f"c{i}"]))
+        parts = {key_part(f"template/{NS}/algo-{i:05d}", 2) for i in range(T)}
+        assert parts == {0, 1}, "the workload must exercise both coordinator partitions"
+        async with Running(env, "native", coordinator_partitions=2, executors_per_shard=2) as app:
+            assert app.coord_part == (0, 2) and app.partitions is not None
+
+            async def all_ready(tag=None):
+                items = (await cc.list(R.TEMPLATES, NS))["items"]
+                if len(items) != T:
+                    return False
+                for o in items:
+                    st = o.get("status") or {}
+                    if (st.get("conditions") or [{}])[0].get("status") != "True" or \
+                            st.get("syncedToClusters") != ["shard-0", "shard-1"]:
+                        return False
+                    if tag and o["spec"]["container"]["versionTag"] != tag:
+                        return False
+                return True
+            await wait_for(all_ready, timeout=20, interval=0.05)
+            await wait_for(lambda: asyncio.sleep(0, app._ready()), timeout=10)
+            owners = {r["name"] for r in (await cc.get(R.SECRETS, NS, "shared"))["metadata"]["ownerReferences"]}
+            assert owners == {f"algo-{i:05d}" for i in range(T)}
+            for sc in scs:
+                uids = {o["metadata"]["uid"] for o in (await sc.list(R.TEMPLATES, NS))["items"]}
+                sec = await sc.get(R.SECRETS, NS, "shared")
+                assert {r["uid"] for r in sec["metadata"]["ownerReferences"]} == uids and len(uids) == T
+            events = (await cc.list(R.EVENTS, NS))["items"]
+            assert {e["involvedObject"]["name"] for e in events if e["reason"] == C.SUCCESS_SYNCED} == \
+                {f"algo-{i:05d}" for i in range(T)}
+
+            # kill the child coordinator: it is restarted and keeps serving its partition
+            child = app.partitions.handles[0]
+            old_pid = child.proc.pid
+            os.kill(old_pid, signal.SIGKILL)
+            await wait_for(lambda: asyncio.sleep(0, child.proc is not None and child.proc.pid != old_pid
+                                                 and child.ready.is_set()), timeout=20, interval=0.05)
+            for i in range(T):
+                await mutate(cc, R.TEMPLATES, f"algo-{i:05d}",
+                             lambda o: o["spec"]["container"].__setitem__("versionTag", "v-part"))
+
+            async def propagated():
+                for sc in scs:
+                    for o in (await sc.list(R.TEMPLATES, NS))["items"]:
+                        if o["spec"]["container"]["versionTag"] != "v-part":
+                            return False
+                return True
+            await wait_for(propagated, timeout=20, interval=0.05)
+            await wait_for(lambda: all_ready("v-part"), timeout=20, interval=0.05)
+    finally:
+        await cc.close()
+        for sc in scs:
+            await sc.close()
+        await env.stop()
