@@ -256,3 +256,28 @@ def test_native_workers_floor():
     cfg.native_workers, cfg.workers = 8, 2
     assert options_from_config(cfg).workers == 8
     assert options_from_config(AppConfig(mode="compat")).workers == 2  # reference semantics
+
+
+def test_coordinator_partition_rules(monkeypatch):
+    from ncc.app import auto_coordinator_partitions, coordinator_partition
+    from ncc.config import AppConfig
+    assert auto_coordinator_partitions(2, 3, cpus=256) == 1        # few shards: one coordinator
+    assert auto_coordinator_partitions(8, 3, cpus=16) == 1         # the 16-CPU box: CPU-bound anyway
+    assert auto_coordinator_partitions(8, 3, cpus=64) == 2
+    assert auto_coordinator_partitions(8, 3, cpus=256) == 3        # capped by executors per shard
+    monkeypatch.delenv("NCC_COORDINATOR_PART", raising=False)
+    assert coordinator_partition(AppConfig(coordinator_partitions=1), 8, 3) is None
+    assert coordinator_partition(AppConfig(coordinator_partitions=3), 1, 1) == (0, 3)
+    monkeypatch.setenv("NCC_COORDINATOR_PART", "2/3")
+    assert coordinator_partition(AppConfig(coordinator_partitions=1), 8, 3) == (2, 3)  # a child
+
+
+def test_executor_pool_global_partitions():
+    from ncc.controller.executor import ExecutorPool, key_part
+    pool = ExecutorPool(["s0", "s1"], 2, lambda i, m: None, per_shard=2, part_base=1, part_stride=3)
+    assert [(h.shards, h.part, h.parts) for h in pool.handles] == \
+        [(["s0"], 1, 6), (["s0"], 4, 6), (["s1"], 1, 6), (["s1"], 4, 6)]
+    # every key of executor partition q of 6 belongs to coordinator partition q % 3
+    for i in range(200):
+        k = f"template/nexus/algo-{i:05d}"
+        assert key_part(k, 6) % 3 == key_part(k, 3)
