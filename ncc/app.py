@@ -223,6 +223,8 @@ class App:
                 self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard)
                 if self.coord_part is not None:
                     o.partition = self.coord_part  # this coordinator's share of the template keys
+                    # the k executors per shard are shared out among the C coordinators (k/C each, at least 1)
+                    self.per_shard = max(1, self.per_shard // self.coord_part[1])
         kf = partition_filter(*o.partition) if o.partition is not None else None
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}

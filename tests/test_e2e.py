@@ -494,3 +494,21 @@ async def test_partitioned_coordinators(tmp_path):
         for sc in scs:
             await sc.close()
         await env.stop()
+
+
+def test_partitioned_coordinators_share_the_executors(tmp_path, monkeypatch):
+    """C coordinators split the k executors per shard between them instead of each running k."""
+    import asyncio as aio
+    from ncc.app import App
+    monkeypatch.delenv("NCC_COORDINATOR_PART", raising=False)
+
+    async def go():
+        env = await FakeEnvironment(4, str(tmp_path)).start()
+        try:
+            app = App(env.app_config(mode="native", coordinator_partitions=2, executors_per_shard=4))
+            await app.build()
+            assert app.coord_part == (0, 2) and app.per_shard == 2 and app.n_executors == 4
+            await app.factory.stop()
+        finally:
+            await env.stop()
+    aio.run(go())
