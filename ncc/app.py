@@ -141,13 +141,15 @@ def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
 
 
 def auto_coordinator_partitions(groups: int, per_shard: int, cpus: int | None = None) -> int:
-    """Coordinator processes: one per executor key partition once there are ≥ 4 shard groups and CPUs to spare
-    (≥ 32 per extra coordinator).  At 8 shards one coordinator spends ~210 µs per template pass on the box
-    (profiles/r1/session2/spr_8.json), which caps a single process near 110k objects/s."""
+    """Coordinator processes: one per executor key partition (C = k, so each coordinator keeps one executor
+    per shard) once there are ≥ 4 shard groups and ≥ 32 CPUs per coordinator; otherwise one.  At 8 shards
+    one coordinator spends ~210 µs per template pass on the box (profiles/r1/session2/spr_8.json), which caps
+    a single process near 110k objects/s; on a CPU-bound host extra processes only cost
+    (profiles/r1/session2/coord_partitions_*)."""
     cpus = cpu_share() if cpus is None else cpus
-    if groups < 4:
+    if groups < 4 or per_shard < 2 or cpus // 32 < per_shard:
         return 1
-    return max(1, min(per_shard, cpus // 32))
+    return per_shard
 
 
 def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int) -> tuple | None:

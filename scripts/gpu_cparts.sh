@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) echo "fatal status $1 in $2; stopping"; exit "$1";; esac; }
 python native/build.py > gpurun_out/build.log 2>&1 || exit 1
-for r in 1 2; do for C in 1 2 3; do
+for r in 1 2; do for C in 1 2; do
   timeout -k 10 300 python bench.py --shards-per-rank 8 --extra-env NEXUS__COORDINATOR_PARTITIONS=$C \
     > gpurun_out/cp_${C}_$r.json 2>gpurun_out/cp_${C}_$r.err; s=$?; fatal $s c$C
   python -c "

@@ -263,8 +263,9 @@ def test_coordinator_partition_rules(monkeypatch):
     from ncc.config import AppConfig
     assert auto_coordinator_partitions(2, 3, cpus=256) == 1        # few shards: one coordinator
     assert auto_coordinator_partitions(8, 3, cpus=16) == 1         # the 16-CPU box: CPU-bound anyway
-    assert auto_coordinator_partitions(8, 3, cpus=64) == 2
-    assert auto_coordinator_partitions(8, 3, cpus=256) == 3        # capped by executors per shard
+    assert auto_coordinator_partitions(8, 3, cpus=64) == 1         # C must divide k: not enough CPUs for 3
+    assert auto_coordinator_partitions(8, 3, cpus=128) == 3        # one coordinator per executor partition
+    assert auto_coordinator_partitions(8, 2, cpus=256) == 2
     monkeypatch.delenv("NCC_COORDINATOR_PART", raising=False)
     assert coordinator_partition(AppConfig(coordinator_partitions=1), 8, 3) is None
     assert coordinator_partition(AppConfig(coordinator_partitions=3), 1, 1) == (0, 3)
