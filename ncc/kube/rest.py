@@ -20,7 +20,22 @@ import tempfile
 from typing import AsyncIterator
 from urllib.parse import urlencode
 
-import aiohttp
+
+class _LazyModule:
+    """Import on first attribute access: aiohttp costs ~0.2 s of process start-up and only the optional
+    `transport: aiohttp` path uses it (every executor process starts with this module)."""
+
+    def __init__(self, name: str):
+        self._name = name
+
+    def __getattr__(self, attr):
+        import importlib
+        mod = importlib.import_module(self._name)
+        globals()[self._name] = mod
+        return getattr(mod, attr)
+
+
+aiohttp = _LazyModule("aiohttp")
 
 from .. import native as _native
 from ..api.jsonenc import dumps_bytes, loads_bytes
