@@ -450,52 +450,67 @@ class ReconcileMixin:
             for n in names:
                 await self._sync_dependent(rt, template, shard_template, shard, n)
 
+    def _dependent_failed(self, template: dict, dep_name: str, e: BaseException) -> BaseException:
+        """Warning ErrResourceSyncError on the template (controller.go:525,546,557); returns `e` to raise."""
+        self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
+                            C.MESSAGE_RESOURCE_OPERATION_FAILED.format(q(dep_name), q(meta(template).get("name", "")),
+                                                                      e), kind=C.TEMPLATE_KIND)
+        return e
+
+    async def _put_dependent(self, shard, rt, src: dict, obj: dict, data, owner, with_binary: bool):
+        """UpdateSecret / UpdateConfigMap (X8f) of a shard dependent, race-tolerant in native mode."""
+        is_secret = rt is R.SECRETS
+        args = (obj, data, owner, C.FIELD_MANAGER)
+        if with_binary:
+            args = args + (normalize_data(src.get("binaryData")),)
+        if self.options.tolerate_write_races:
+            informer = shard.secret_informer if is_secret else shard.configmap_informer
+            return await self._write(shard, "update_secret" if is_secret else "update_configmap", informer, rt,
+                                     *args)
+        self._pass_wrote()
+        return await (shard.update_secret if is_secret else shard.update_configmap)(*args)
+
     async def _sync_dependent(self, rt, template: dict, shard_template: dict, shard, dep_name: str) -> None:
         is_secret = rt is R.SECRETS
         kind = rt.kind
-        tname = meta(template).get("name", "")
-        ns = meta(template).get("namespace", "")
+        tm = meta(template)
+        ns = tm.get("namespace", "")
         lister = self.secret_lister if is_secret else self.configmap_lister
-        shard_lister = shard.secret_lister if is_secret else shard.configmap_lister
-        shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
         src = lister.try_get(ns, dep_name)
         if src is None:
             self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
-                                C.MESSAGE_RESOURCE_MISSING.format(q(dep_name), q(tname)), kind=C.TEMPLATE_KIND)
+                                C.MESSAGE_RESOURCE_MISSING.format(q(dep_name), q(tm.get("name", ""))),
+                                kind=C.TEMPLATE_KIND)
             lister.get(ns, dep_name)  # raises NotFound
         shard_ns = meta(shard_template).get("namespace", "")
-
-        def fail(e: BaseException):
-            self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
-                                C.MESSAGE_RESOURCE_OPERATION_FAILED.format(q(dep_name), q(tname), e),
-                                kind=C.TEMPLATE_KIND)
-            return e
-
+        shard_lister = shard.secret_lister if is_secret else shard.configmap_lister
         shard_obj = shard_lister.try_get(shard_ns, meta(src).get("name", ""))
-        if self.options.server_side_apply:
+        opts = self.options
+        with_binary = opts.sync_binary_data and not is_secret
+        if opts.server_side_apply:
             try:
                 if shard_obj is not None:
                     missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template,
                                                               shard.name)  # rogue → error
-                    with_binary = self.options.sync_binary_data and not is_secret
                     if not missing_owner and data_matches(src, shard_obj, with_binary):
                         return
                 self._pass_wrote()
                 await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise fail(e)
+                raise self._dependent_failed(template, dep_name, e)
             return
+        shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
         if shard_obj is None:
             try:
                 shard_obj = await self._write(shard, "create_secret" if is_secret else "create_configmap",
                                               shard_informer, rt, shard_template, src, C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise fail(e)
+                raise self._dependent_failed(template, dep_name, e)
         try:
             missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template, shard.name)
         except RogueResourceError as e:
-            raise fail(e)
-        if is_secret and self.options.sync_secret_type and \
+            raise self._dependent_failed(template, dep_name, e)
+        if is_secret and opts.sync_secret_type and \
                 (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
             # Secret.type is immutable: replace the shard copy (other owners re-add their refs on their passes)
             try:
@@ -504,37 +519,26 @@ class ReconcileMixin:
                 shard_obj = await self._write(shard, "create_secret", shard_informer, rt, shard_template, src,
                                               C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise fail(e)
+                raise self._dependent_failed(template, dep_name, e)
             return
-        with_binary = self.options.sync_binary_data and not is_secret
         differs = not data_matches(src, shard_obj, with_binary)
-        update = shard.update_secret if is_secret else shard.update_configmap
-        op = "update_secret" if is_secret else "update_configmap"
-
-        async def put(obj, data, owner):
-            args = (obj, data, owner, C.FIELD_MANAGER)
-            if with_binary:
-                args = args + (normalize_data(src.get("binaryData")),)
-            if self.options.tolerate_write_races:
-                return await self._write(shard, op, shard_informer, rt, *args)
-            self._pass_wrote()
-            return await update(*args)
-
         try:
-            if self.options.single_put_dependents or SLIM_FP in shard_obj:
+            slim = SLIM_FP in shard_obj
+            if opts.single_put_dependents or slim:
                 if differs or missing_owner:
-                    await put(shard_obj, normalize_data(src.get("data")) if (differs or SLIM_FP in shard_obj)
-                              else None, shard_template if missing_owner else None)
+                    await self._put_dependent(shard, rt, src, shard_obj,
+                                              normalize_data(src.get("data")) if (differs or slim) else None,
+                                              shard_template if missing_owner else None, with_binary)
             else:
                 if differs:
                     log.debug("Content changed for %s %s, updating", kind, dep_name)
-                    await put(shard_obj, src.get("data"), None)
+                    await self._put_dependent(shard, rt, src, shard_obj, src.get("data"), None, with_binary)
                 if missing_owner:
                     log.debug("Ownership missing for %s %s, updating", kind, dep_name)
                     # The reference re-uses the pre-update object here (controller.go:552,614).
-                    await put(shard_obj, None, shard_template)
+                    await self._put_dependent(shard, rt, src, shard_obj, None, shard_template, with_binary)
         except Exception as e:  # noqa: BLE001
-            raise fail(e)
+            raise self._dependent_failed(template, dep_name, e)
 
     async def propagate_template_delete(self, namespace: str, name: str) -> None:
         """Level-triggered shard delete (native `queued_deletes`): retried through the queue."""
