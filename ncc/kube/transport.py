@@ -126,6 +126,19 @@ class _Conn(asyncio.Protocol):
         pass
 
     def data_received(self, data: bytes):
+        if not self.buf and not self.head_done and self.stream is None and self.pending:
+            # fast path: a whole API response in one read (the common case) is framed straight from `data`
+            i = data.find(_CRLF2)
+            if i >= 0:
+                self._parse_head(data[:i])
+                if self.head_done and not self.chunked and 0 <= self.clen <= len(data) - i - 4:
+                    end = i + 4 + self.clen
+                    self.body = data[i + 4:end]
+                    self._finish()
+                    if end < len(data) and self.pending and not self.closed:
+                        self.data_received(data[end:])  # pipelined responses behind it
+                    return
+                data = data[i + 4:]  # head consumed (or a bodiless response finished): general path
         self.buf += data
         while True:
             if not self.head_done:
@@ -509,7 +522,7 @@ class ConnectionPool:
             yield resp, None
             while True:
                 if batch:
-                    if c.stream:
+                    while c.stream:  # lines may arrive while the consumer works on a batch: drain them all
                         lines = list(c.stream)
                         c.stream.clear()
                         c.resume()

@@ -206,3 +206,56 @@ def test_native_request_head_parser_matches_python():
     for bad in (b"GARBAGE", b"GET /only-two", b" / HTTP/1.1"):
         with pytest.raises(ValueError):
             m.parse_request_head(bad)
+
+
+async def test_pipelined_responses_in_one_read_and_split_reads():
+    """Several responses in one TCP read (pipelining) and a response split over reads both frame right."""
+    from ncc.kube.transport import _Conn
+
+    class _Pool:
+        pipeline_depth = 4
+
+        def _release(self, c):
+            pass
+
+        def _discard(self, c):
+            pass
+
+    loop = asyncio.get_running_loop()
+    c = _Conn(_Pool())
+    futs = [loop.create_future() for _ in range(3)]
+    c.pending.extend(futs)
+    r = lambda b: b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n%s" % (len(b), b)  # noqa: E731
+    c.data_received(r(b'{"a":1}') + r(b"") + r(b'{"c":3}')[:20])
+    assert futs[0].result().body == b'{"a":1}' and futs[1].result().body == b"" and not futs[2].done()
+    c.data_received(r(b'{"c":3}')[20:])
+    assert futs[2].result().body == b'{"c":3}'
+
+
+async def test_watch_batches_drain_lines_that_arrive_during_processing():
+    """Lines that arrive while the consumer is busy with a batch are delivered before the stream ends."""
+    async def handler(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n")
+        for i in range(5):
+            line = b'{"n":%d}\n' % i
+            writer.write(b"%x\r\n%s\r\n" % (len(line), line))
+            await writer.drain()
+            await asyncio.sleep(0.01)
+        writer.write(b"0\r\n\r\n")
+        await writer.drain()
+        writer.close()
+    srv = await asyncio.start_server(handler, "127.0.0.1", 0)
+    url = f"http://127.0.0.1:{srv.sockets[0].getsockname()[1]}"
+    pool = ConnectionPool(url)
+    got = []
+    try:
+        async for resp, lines in pool.stream("/w?watch=1", {}, batch=True):
+            if resp is not None:
+                continue
+            got.extend(lines)
+            await asyncio.sleep(0.05)  # slow consumer: later lines and the end of the stream arrive meanwhile
+        assert got == [b'{"n":%d}' % i for i in range(5)]
+    finally:
+        pool.close()
+        srv.close()
