@@ -188,13 +188,17 @@ class Informer:
                     await r
 
     # ------------------------------------------------------------- reflector
-    async def _list(self) -> str:
+    async def _list(self, resource_version: str | None = None) -> str:
+        """LIST (paginated).  Like client-go's reflector, the first page asks for `resourceVersion` — "0" on
+        a cold start, i.e. anything the apiserver's watch cache holds, instead of a quorum read of every page
+        from etcd; "" (consistent) after the watch expired (410 Gone)."""
         items: list[dict] = []
         token = None
         rv = ""
         while True:
             resp = await self.client.list(self.rt, self.namespace, label_selector=self.label_selector,
-                                          limit=self.page_size, continue_token=token)
+                                          limit=self.page_size, continue_token=token,
+                                          resource_version=resource_version if token is None else None)
             items.extend(resp.get("items") or ())
             lm = resp.get("metadata") or {}
             rv = lm.get("resourceVersion", rv)
@@ -394,10 +398,11 @@ class Informer:
         backoff = 0.8
         rv = ""
         need_list = True
+        list_rv = "0"  # cold start: served from the apiserver's watch cache
         while not self._stopping:
             try:
                 if need_list:
-                    rv = await self._list()
+                    rv = await self._list(list_rv)
                     self.last_rv = rv
                     need_list = False
                 rv = await self._watch(self.last_rv or rv)  # resume after the last event we processed
@@ -406,6 +411,7 @@ class Informer:
                 raise
             except E.Gone:
                 need_list = True
+                list_rv = ""  # our resourceVersion is too old for the cache: consistent read
                 log.debug("%s: watch expired, relisting", self.name)
             except Exception as e:  # noqa: BLE001 — transport errors, 5xx, etc.
                 self.last_error = e
@@ -414,6 +420,7 @@ class Informer:
                 backoff = min(backoff * 2, 30.0)
                 if not isinstance(e, E.TransportError):
                     need_list = True
+                    list_rv = self.last_rv or "0"  # not older than what we have seen
 
     async def _resync_loop(self) -> None:
         while True:

@@ -287,3 +287,41 @@ def test_store_index_tracks_value_changes_and_relists():
     assert len(st.by_index("secret", "nexus/c")) == 1
     st.delete(make_template(1, "nexus", secrets=["c"]))
     assert st.by_index("secret", "nexus/c") == [] and st._index_vals["secret"] == {}
+
+
+async def test_list_resource_version_semantics():
+    """Reflector semantics: cold-start LIST at resourceVersion "0" (watch cache), continuation pages carry
+    only the token, and after 410 Gone the relist is a consistent read ("")."""
+    import asyncio as aio
+    from ncc.cache.informer import Informer
+    from ncc.kube import errors as E2
+
+    calls = []
+
+    class Client:
+        cluster_name = "c"
+        watches = 0
+
+        async def list(self, rt, ns, *, label_selector=None, limit=None, continue_token=None,
+                       resource_version=None):
+            calls.append((resource_version, continue_token))
+            if continue_token is None and len(calls) == 1:
+                return {"items": [], "metadata": {"resourceVersion": "5", "continue": "page2"}}
+            return {"items": [], "metadata": {"resourceVersion": "5"}}
+
+        async def watch(self, rt, ns, **kw):
+            Client.watches += 1
+            if Client.watches == 1:
+                raise E2.Gone("expired")
+            await aio.sleep(3600)
+            yield  # pragma: no cover
+
+    inf = Informer(Client(), R.SECRETS, "nexus")
+    task = aio.ensure_future(inf._run())
+    for _ in range(200):
+        if len(calls) >= 3:
+            break
+        await aio.sleep(0.01)
+    task.cancel()
+    await aio.gather(task, return_exceptions=True)
+    assert calls[:3] == [("0", None), (None, "page2"), ("", None)]
