@@ -32,6 +32,7 @@ class MarkerTracker:
         self.paths = {plural: path.split(".") for plural, path in (specs or {}).items()}
         self.first_seen: dict[tuple, dict] = {}  # (plural, value) -> {name: t_ns}
         self._waiters: list[tuple[list, asyncio.Future]] = []
+        self._thresholds: dict[tuple, set] = {}  # (plural, value) -> counts some waiter needs
 
     def add_spec(self, plural: str, path: str) -> None:
         self.paths[plural] = path.split(".")
@@ -46,11 +47,15 @@ class MarkerTracker:
         if v is None:
             return
         m = obj.get("metadata") or {}
-        bucket = self.first_seen.setdefault((rt.plural, str(v)), {})
+        bk = (rt.plural, str(v))
+        bucket = self.first_seen.get(bk)
+        if bucket is None:
+            bucket = self.first_seen[bk] = {}
         key = f"{m.get('namespace', '')}/{m.get('name', '')}"
         if key not in bucket:
             bucket[key] = time.time_ns()
-            if self._waiters:
+            # re-evaluate waiters only when this write completes one of their counts
+            if self._waiters and len(bucket) in self._thresholds.get(bk, ()):
                 self._check()
 
     def satisfied(self, want: list) -> bool:
@@ -66,12 +71,16 @@ class MarkerTracker:
             else:
                 keep.append((want, fut))
         self._waiters = keep
+        if not keep:
+            self._thresholds.clear()
 
     async def wait(self, want: list, timeout: float) -> bool:
         if self.satisfied(want):
             return True
         fut = asyncio.get_running_loop().create_future()
         self._waiters.append((want, fut))
+        for w in want:
+            self._thresholds.setdefault((w["plural"], str(w["value"])), set()).add(int(w["count"]))
         try:
             return await wait_timeout(fut, timeout)
         except asyncio.TimeoutError:

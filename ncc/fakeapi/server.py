@@ -80,6 +80,7 @@ class FakeApiServer:
     def __init__(self, state: ClusterState | None = None, *, name: str = "fake", token: str | None = None,
                  bookmark_interval: float = 5.0):
         self.state = state or ClusterState(name)
+        self._routes: dict = {}  # path -> parsed route (see _parse)
         self.name = name
         self.token = token
         self.bookmark_interval = bookmark_interval
@@ -107,7 +108,18 @@ class FakeApiServer:
 
     # ------------------------------------------------------------------ routing
     def _parse(self, path: str):
-        """→ (rt, namespace, name, subresource) or a special-route string."""
+        """→ (rt, namespace, name, subresource) or a special-route string; memoised per path (writes
+        repeat the same object paths wave after wave)."""
+        hit = self._routes.get(path)
+        if hit is not None:
+            return hit
+        out = self._parse_uncached(path)
+        if len(self._routes) > 65536:
+            self._routes.clear()
+        self._routes[path] = out
+        return out
+
+    def _parse_uncached(self, path: str):
         parts = [p for p in path.split("/") if p]
         if not parts:
             return "root"
