@@ -103,6 +103,8 @@ class FakeApiServer:
         self.state.close_watchers()
         await self._http.stop()
 
+    WATCH_COALESCE_S = 0.0005  # see _watch
+
     def drop_watches(self) -> None:
         self.state.close_watchers()
 
@@ -312,6 +314,7 @@ class FakeApiServer:
         loop = asyncio.get_running_loop()
         deadline = loop.time() + timeout if timeout else None
         last_bookmark = loop.time()
+        last_write = 0.0
         try:
             while True:
                 now = loop.time()
@@ -329,6 +332,10 @@ class FakeApiServer:
                         rec = False
                 if rec is None:
                     break
+                if rec is not False and loop.time() - last_write < self.WATCH_COALESCE_S:
+                    # under sustained load, let a few more events join this write (one syscall and one
+                    # consumer wake-up per batch instead of per event); an isolated event goes out at once
+                    await asyncio.sleep(self.WATCH_COALESCE_S)
                 chunks = []
                 if rec is not False:
                     chunks.append(rec.line())
@@ -345,6 +352,7 @@ class FakeApiServer:
                     last_bookmark = loop.time()
                 if chunks:
                     await resp.write(b"".join(chunks))
+                    last_write = loop.time()
                 if rec is None:
                     break
         except (ConnectionResetError, asyncio.CancelledError):
