@@ -13,6 +13,7 @@ Citations (reference snapshot, /root/reference):
   * owner labels            controller_test.go:183-188 (nexus-core shards.OwnerLabels)
   * group/version/plurals   .helm/templates/cluster-role-template-editor.yaml:25-36
 """
+import functools
 
 GROUP = "science.sneaksanddata.com"
 VERSION = "v1"
@@ -71,8 +72,10 @@ CONDITION_TRUE = "True"
 CONDITION_FALSE = "False"
 
 
+@functools.lru_cache(maxsize=65536)
 def go_quote(s: str) -> str:
-    """Render a string the way Go's fmt `%q` verb does for printable ASCII input."""
+    """Render a string the way Go's fmt `%q` verb does for printable ASCII input (memoised: status and
+    Event messages quote the same object names on every pass)."""
     out = ['"']
     for ch in s:
         if ch == '"':
