@@ -2,8 +2,10 @@
 
 The extension (sources in `native/`, built in-tree by `python native/build.py` or
 `__graft_entry__.build()`) provides the hot runtime primitives the reference gets from
-compiled client-go: the rate-limited exclusive-key work queue and structural fingerprints
-used for O(1) drift detection.
+compiled client-go — the rate-limited exclusive-key work queue and structural fingerprints
+used for O(1) drift detection — plus the per-object hot spots of
+this runtime: watch-line/response scanners with crc32 key partitions, a compact JSON encoder
+and HTTP/1.1 head parsers (see the header of native/ncc_native.cpp).
 
 `load(required=False)` returns the module or None.  Set `NCC_REQUIRE_NATIVE=1` (the GPU-box
 test tier does) to turn a missing or stale build into a hard ImportError instead of a silent
