@@ -259,3 +259,30 @@ async def test_watch_batches_drain_lines_that_arrive_during_processing():
     finally:
         pool.close()
         srv.close()
+
+
+def test_native_parsers_survive_arbitrary_bytes():
+    """Random and truncated inputs: the C++ parsers return or raise ValueError, never crash."""
+    from hypothesis import given, settings, strategies as st
+    from ncc import native
+    m = native.load(required=True)
+    good_resp = b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\nRetry-After: 1"
+    good_req = b"PUT /api/v1/namespaces/n/secrets/a HTTP/1.1\r\nContent-Length: 3"
+    good_line = (b'{"type":"MODIFIED","object":{"metadata":{"name":"s","namespace":"n","resourceVersion":"7",'
+                 b'"ownerReferences":[{"name":"t","uid":"u"}]}}}')
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.binary(max_size=200), st.integers(0, 200))
+    def check(blob, cut):
+        for fn in (m.parse_response_head, m.parse_request_head):
+            for data in (blob, good_resp[:cut] + blob, good_req[:cut] + blob):
+                try:
+                    fn(data)
+                except ValueError:
+                    pass
+        for data in (blob, good_line[:cut], good_line[:cut] + blob):
+            r = m.scan_event_part(data, 3, "n")
+            assert r is None or len(r) == 8
+            m.scan_event_owners(data)
+            m.scan_object(data)
+    check()
