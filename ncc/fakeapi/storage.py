@@ -360,9 +360,12 @@ class ClusterState:
             self.stats["noop_update"] += 1
             return cur
         new["metadata"]["resourceVersion"] = str(self._next_rv())
-        self._index_owners(rt, cur, False)
+        same_owners = (cm.get("ownerReferences") == new["metadata"].get("ownerReferences"))
+        if not same_owners:
+            self._index_owners(rt, cur, False)
         b[name] = new
-        self._index_owners(rt, new, True)
+        if not same_owners:
+            self._index_owners(rt, new, True)
         self.stats["status" if subresource == "status" else "update"] += 1
         self._emit(self.rv, rt, ns, "MODIFIED", new)
         return new
