@@ -286,3 +286,54 @@ def test_native_parsers_survive_arbitrary_bytes():
             m.scan_event_owners(data)
             m.scan_object(data)
     check()
+
+
+async def test_write_meta_fast_path_errors_and_retries():
+    """write_meta's direct-to-pool path: a 2xx is scanned natively; a 409 raises Conflict; a 429 with
+    Retry-After is retried through the general exchange loop."""
+    from ncc.api import resources as R
+    seq = []
+
+    async def handler(method, target, hdrs, body):
+        seq.append((method, target))
+        n = len(seq)
+        if n == 1:
+            return 200, b'{"metadata":{"namespace":"n","name":"a","resourceVersion":"7","uid":"u1"}}'
+        if n == 2:
+            return 409, b'{"kind":"Status","code":409,"reason":"Conflict","message":"modified"}'
+        if n == 3:
+            return 429, b'{"kind":"Status","code":429}'
+        return 201, b'{"metadata":{"namespace":"n","name":"b","resourceVersion":"9","uid":"u2"}}'
+
+    class RetrySrv(_Server):
+        async def _conn(self, reader, writer):
+            try:
+                while True:
+                    head = await reader.readuntil(b"\r\n\r\n")
+                    lines = head.decode("latin-1").split("\r\n")
+                    method, target, _ = lines[0].split(" ", 2)
+                    hdrs = {ln.partition(":")[0].strip().lower(): ln.partition(":")[2].strip() for ln in lines[1:] if ln}
+                    body = await reader.readexactly(int(hdrs.get("content-length", "0")))
+                    status, out = await self.handler(method, target, hdrs, body)
+                    extra = b"Retry-After: 0\r\n" if status == 429 else b""
+                    writer.write(b"HTTP/1.1 %d X\r\n%sContent-Length: %d\r\n\r\n%s" % (status, extra, len(out), out))
+                    await writer.drain()
+            except (asyncio.IncompleteReadError, ConnectionError):
+                pass
+            finally:
+                writer.close()
+
+    srv = RetrySrv(handler)
+    url = await srv.start()
+    c = RestClient(ClusterConfig(server=url))
+    try:
+        await c._get_pool()
+        assert await c.write_meta("update", R.SECRETS, "n", {"metadata": {"name": "a"}}, name="a") == \
+            ("n", "a", "7", "u1")
+        with pytest.raises(E.Conflict):
+            await c.write_meta("update", R.SECRETS, "n", {"metadata": {"name": "a"}}, name="a")
+        assert await c.write_meta("create", R.SECRETS, "n", {"metadata": {"name": "b"}}) == ("n", "b", "9", "u2")
+        assert [m for m, _ in seq] == ["PUT", "PUT", "POST", "POST"] and c.stats["retries"] == 1
+    finally:
+        await c.close()
+        await srv.stop()
