@@ -319,6 +319,9 @@ async def run(args, d: Dist) -> dict | None:
                         lat.extend((t - c[k.split(":", 1)[-1]]) / 1e6 for k, t in objs.items())
             objs = args.steps * 3 * T * d.world * S
             value = objs / elapsed
+            from ncc.app import auto_coordinator_partitions, auto_executors_per_shard, cpu_share
+            groups = d.world * S  # the controller's automatic sizing on this host (same rule, same cgroup)
+            k = auto_executors_per_shard(groups)
             ctrl_alive = controller.poll() is None
             return {
                 "metric": METRIC,
@@ -341,6 +344,9 @@ async def run(args, d: Dist) -> dict | None:
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
+                "controller_sizing": {"cpus": cpu_share(), "executors_per_shard": k,
+                                      "coordinator_partitions": auto_coordinator_partitions(groups, k),
+                                      "overrides": [kv for kv in args.extra_env if kv.startswith("NEXUS__")]},
                 # busy CPU cores per process over the timed steps (rank 0's, plus the busiest shard server)
                 "cpu_cores_busy": dict(utils[0], **{"shard-apiserver-max": max(u.get("shard-apiserver", 0.0)
                                                                                  for u in utils)}),
