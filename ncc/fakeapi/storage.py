@@ -144,7 +144,7 @@ def _content(obj: dict) -> dict:
 
 
 class ClusterState:
-    def __init__(self, name: str = "cluster", *, simple: bool = False, history: int = 500_000,
+    def __init__(self, name: str = "cluster", *, simple: bool = False, history: int = 100_000,
                  status_subresource: bool = True):
         self.name = name
         self.simple = simple
