@@ -78,8 +78,11 @@ class Faults:
 
 class FakeApiServer:
     def __init__(self, state: ClusterState | None = None, *, name: str = "fake", token: str | None = None,
-                 bookmark_interval: float = 5.0):
+                 bookmark_interval: float = 5.0, crd_dir: str | None = None):
         self.state = state or ClusterState(name)
+        if crd_dir:  # validate custom-resource writes against these CRDs' schemas (422 Invalid)
+            from ..api.schema import load_crds
+            self.state.crds.update(load_crds(crd_dir))
         self._routes: dict = {}  # path -> parsed route (see _parse)
         self.name = name
         self.token = token
@@ -451,7 +454,8 @@ class FakeApiServer:
 
 async def serve(args) -> None:
     logging.basicConfig(level=logging.WARNING)
-    server = FakeApiServer(name=args.name, token=args.token, bookmark_interval=args.bookmark_interval)
+    server = FakeApiServer(name=args.name, token=args.token, bookmark_interval=args.bookmark_interval,
+                           crd_dir=args.crd_dir)
     for m in args.marker:
         plural, _, path = m.partition("=")
         server.markers.add_spec(plural, path)
@@ -501,6 +505,7 @@ def main(argv=None) -> None:
     p.add_argument("--tls-cert")
     p.add_argument("--tls-key")
     p.add_argument("--tls-client-ca", help="require client certificates signed by this CA (mutual TLS)")
+    p.add_argument("--crd-dir", help="validate custom-resource writes against the CRDs in this directory")
     p.add_argument("--bookmark-interval", type=float, default=5.0)
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
     p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")

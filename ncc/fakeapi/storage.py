@@ -158,6 +158,7 @@ class ClusterState:
         self._uids: dict[str, tuple] = {}  # uid -> (rt_key, ns, name)
         self._dependents: dict[str, set] = {}  # owner uid -> {(rt_key, ns, name)}
         self.write_hooks: list[Callable[[str, ResourceType, dict], None]] = []
+        self.crds: dict = {}  # (group, plural) -> CRD: writes of those kinds are schema-validated (422)
         self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
@@ -183,6 +184,19 @@ class ClusterState:
     def _next_rv(self) -> int:
         self.rv += 1
         return self.rv
+
+    def _validate(self, rt: ResourceType, obj: dict) -> None:
+        """Structural-schema validation of a custom resource write, as the apiserver does (422 Invalid)."""
+        crd = self.crds.get((rt.group, rt.plural))
+        if crd is None:
+            return
+        from ..api.schema import validate_object
+        errs = validate_object(crd, obj, rt.version)
+        if errs:
+            name = (obj.get("metadata") or {}).get("name", "")
+            raise E.Invalid(f'{rt.kind}.{rt.group} "{name}" is invalid: [{", ".join(errs)}]',
+                            details={"name": name, "group": rt.group, "kind": rt.kind,
+                                     "causes": [{"message": e} for e in errs]})
 
     def _emit(self, rv: int, rt: ResourceType, ns: str, type_: str, obj: dict) -> None:
         rec = EventRecord(rv, (rt.group, rt.plural), ns, type_, obj)
@@ -292,6 +306,8 @@ class ClusterState:
         if name in b:
             gr = f"{rt.plural}.{rt.group}" if rt.group else rt.plural
             raise E.AlreadyExists(f'{gr} "{name}" already exists', details={"name": name, "kind": rt.plural})
+        if self.crds:
+            self._validate(rt, obj)
         if not self.simple:
             if m.get("resourceVersion"):
                 raise E.BadRequest("resourceVersion should not be set on objects to be created")
@@ -356,6 +372,8 @@ class ClusterState:
             if rt.group and _content(new) != _content(cur):
                 nm["generation"] = int(cm.get("generation", 1)) + 1
         new["metadata"]["resourceVersion"] = cm.get("resourceVersion")
+        if self.crds:
+            self._validate(rt, new)
         if new == cur:
             self.stats["noop_update"] += 1
             return cur

@@ -54,9 +54,11 @@ def wait_port_file(path: str, proc: subprocess.Popen | None = None, timeout: flo
 class FakeEnvironment:
     def __init__(self, n_shards: int, workdir: str, *, namespace: str = "nexus", token: str | None = None,
                  subprocesses: bool = False, shard_prefix: str = "shard", bookmark_interval: float = 5.0,
-                 tls: bool = False, tls_server_name: str | None = None):
+                 tls: bool = False, tls_server_name: str | None = None, crd_dir: str | None = "default"):
         """`tls=True` serves every apiserver over HTTPS with mutual TLS (a throwaway CA, x509 client auth,
-        like a kind cluster); `tls_server_name` additionally puts `tls-server-name` in the kubeconfigs."""
+        like a kind cluster); `tls_server_name` additionally puts `tls-server-name` in the kubeconfigs.
+        `crd_dir` ("default": the repository's deploy/crds) makes the apiservers validate custom-resource
+        writes against the shipped CRD schemas, as a real apiserver does; None disables it."""
         self.n_shards = n_shards
         self.workdir = workdir
         self.namespace = namespace
@@ -73,6 +75,11 @@ class FakeEnvironment:
         self.controller_kubeconfig = os.path.join(workdir, "controller.kubeconfig")
         self.tls = tls
         self.tls_server_name = tls_server_name
+        if crd_dir == "default":
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            crd_dir = os.path.join(root, "deploy", "crds")
+            crd_dir = crd_dir if os.path.isdir(crd_dir) else None
+        self.crd_dir = crd_dir
         self.pki = None
 
     async def start(self) -> "FakeEnvironment":
@@ -86,14 +93,16 @@ class FakeEnvironment:
             for n in names:
                 pf = os.path.join(self.workdir, f"{n}.url")
                 self.procs.append(spawn_fakeapi(n, pf, token=self.token, bookmark_interval=self.bookmark_interval,
-                                                pki=self.pki))
+                                                pki=self.pki,
+                                                extra=["--crd-dir", self.crd_dir] if self.crd_dir else None))
                 files.append(pf)
             urls = [await asyncio.get_running_loop().run_in_executor(None, wait_port_file, f, p)
                     for f, p in zip(files, self.procs)]
         else:
             urls = []
             for n in names:
-                s = FakeApiServer(name=n, token=self.token, bookmark_interval=self.bookmark_interval)
+                s = FakeApiServer(name=n, token=self.token, bookmark_interval=self.bookmark_interval,
+                                  crd_dir=self.crd_dir)
                 urls.append(await s.start(ssl_context=self.pki.server_context() if self.pki else None))
                 if n == "controller":
                     self.controller_server = s
