@@ -130,14 +130,16 @@ def cpu_share() -> int:
 
 
 def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
-    """Key-partitioned executors per shard group: about 3/4 of the CPUs across all executors, 1..3 each.
+    """Key-partitioned executors per shard group: one per CPU share of the group, 1..4.
 
-    Measured on the MI355X host under a 16-CPU quota (profiles/r1/kscan, BENCHMARKS.md): at 4 shards
-    k=3 beat k=2 by ~25 % and k=1 by ~60 %; beyond 3 per shard every executor's share of replicated
-    watch decoding outweighs the split."""
+    Measured on the MI355X host under a 16-CPU quota, 3 runs each (profiles/r1/session2/kgrid_rep/):
+    N=1 k=3/4/5 25.2k/26.4k/26.8k, N=2 41.8k/46.1k/41.9k, N=4 72.4k/71.0k/74.8k objects/s, with p50 latency
+    falling as k grows.  Since other partitions' lines are dropped natively before decoding, an extra
+    executor costs little; past 4 the gain is within noise (the previous round's tree, which decoded every
+    controller-side dependent in every executor, peaked at k=3: profiles/r1/kscan)."""
     import math
     cpus = cpu_share() if cpus is None else cpus
-    return max(1, min(3, math.ceil(0.75 * cpus / max(1, groups))))
+    return max(1, min(4, math.ceil(cpus / max(1, groups))))
 
 
 def auto_coordinator_partitions(groups: int, per_shard: int, cpus: int | None = None) -> int:

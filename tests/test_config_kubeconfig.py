@@ -209,8 +209,8 @@ def test_cpu_share_reads_cgroup_quota(tmp_path):
     assert cgroup_cpu_quota(str(tmp_path)) == 16.0
     (tmp_path / "cpu.max").write_text("max 100000\n")
     assert cgroup_cpu_quota(str(tmp_path)) is None
-    assert [auto_executors_per_shard(n, cpus=16) for n in (1, 2, 4, 8, 16)] == [3, 3, 3, 2, 1]
-    assert auto_executors_per_shard(8, cpus=128) == 3 and auto_executors_per_shard(1, cpus=2) == 2
+    assert [auto_executors_per_shard(n, cpus=16) for n in (1, 2, 4, 8, 16)] == [4, 4, 4, 2, 1]
+    assert auto_executors_per_shard(8, cpus=128) == 4 and auto_executors_per_shard(1, cpus=2) == 2
 
 
 def test_klog_style_flags(monkeypatch, capsys):
