@@ -41,6 +41,28 @@ def configmap_names(template: Obj, unique: bool = False) -> list[str]:
     return _dedupe(out) if unique else out
 
 
+def dependent_names(template: Obj) -> tuple[list[str], list[str]]:
+    """(`secret_names`, `configmap_names`) in one walk over the mapped environment."""
+    secrets: list[str] = []
+    configmaps: list[str] = []
+    for ef in _mapped_env(template):
+        if ef:
+            ref = ef.get("secretRef")
+            if ref is not None:
+                secrets.append(ref.get("name", ""))
+            ref = ef.get("configMapRef")
+            if ref is not None:
+                configmaps.append(ref.get("name", ""))
+    return secrets, configmaps
+
+
+def same_references(old: Obj, new: Obj) -> bool:
+    """True when two template versions reference the same Secrets and ConfigMaps (in order).  Identical
+    mapped-environment lists, the common case of a version bump, are recognised by one C-level compare."""
+    a, b = _mapped_env(old), _mapped_env(new)
+    return a == b or dependent_names(old) == dependent_names(new)
+
+
 def _dedupe(xs: list[str]) -> list[str]:
     seen: set[str] = set()
     out = []

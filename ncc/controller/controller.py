@@ -21,7 +21,7 @@ import time
 
 from ..api import constants as C
 from ..api.objects import ObjectKey, meta
-from ..api.refs import configmap_names, secret_names, template_owner_names
+from ..api.refs import configmap_names, same_references, secret_names, template_owner_names
 from ..cache.informer import DeletedFinalStateUnknown, Informer
 from ..telemetry.statsd import Metrics, NullMetrics
 from ..workqueue.queue import WorkQueue
@@ -122,7 +122,7 @@ class Controller(ReconcileMixin):
             om, nm = meta(old), meta(new)
             key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
             if self._adopted.get(key) == om.get("resourceVersion") and om.get("uid") == nm.get("uid") and \
-                    secret_names(old) == secret_names(new) and configmap_names(old) == configmap_names(new):
+                    same_references(old, new):
                 self._adopted[key] = nm.get("resourceVersion")
         if self.options.generation_filter:
             om, nm = meta(old), meta(new)

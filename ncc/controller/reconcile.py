@@ -21,7 +21,8 @@ from ..api import resources as R
 from ..api.constants import go_quote as q
 from ..api.fingerprint import SLIM_FP, fingerprint
 from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
-from ..api.refs import configmap_names, is_owned_by_uid, ready_condition, secret_names, template_owner_ref
+from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready_condition, secret_names,
+                        template_owner_ref)
 from ..kube import errors as E
 from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
 
@@ -306,15 +307,15 @@ class ReconcileMixin:
                     raise next(iter(failures.values()))
                 ok = [n for n in shard_names if n not in failures]
                 await self.report_template_synced_condition(
-                    template, secret_names(template), configmap_names(template), ok, ready=False,
+                    template, *dependent_names(template), ok, ready=False,
                     message=f"Algorithm {q(name)} failed to sync to shards: {', '.join(sorted(failures))}")
                 raise ShardSyncError(failures)
         else:
             for shard in self.shards:
                 await self._sync_template_to_shard(template, shard, spec_fp)
 
-        template = await self.report_template_synced_condition(template, secret_names(template),
-                                                               configmap_names(template), shard_names)
+        template = await self.report_template_synced_condition(template, *dependent_names(template),
+                                                               shard_names)
         if self.options.event_on_noop or self._last_pass_wrote():
             self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
                                 C.MESSAGE_RESOURCE_SYNCED.format("NexusAlgorithmTemplate"), kind=C.TEMPLATE_KIND)
@@ -369,13 +370,13 @@ class ReconcileMixin:
             what = f"Algorithm {q(name)}" if is_template else f"Workgroup {q(name)}"
             msg = f"{what} failed to sync to shards: {', '.join(failures)}"
             if is_template:
-                await self.report_template_synced_condition(obj, secret_names(obj), configmap_names(obj), ok,
+                await self.report_template_synced_condition(obj, *dependent_names(obj), ok,
                                                             ready=False, message=msg)
             else:
                 await self.report_workgroup_synced_condition(obj, ready=False, message=msg)
             return
         if is_template:
-            obj = await self.report_template_synced_condition(obj, secret_names(obj), configmap_names(obj), ok)
+            obj = await self.report_template_synced_condition(obj, *dependent_names(obj), ok)
         else:
             obj = await self.report_workgroup_synced_condition(obj)
         if key in self._pending_event or self._last_pass_wrote() or self.options.event_on_noop:
