@@ -324,10 +324,11 @@ class ReconcileMixin:
         """Executor role: fan out to this process's shards only and report to the coordinator."""
         ns, name = meta(template).get("namespace", ""), meta(template).get("name", "")
         # the coordinator adopts; an executor only refuses to write when a reference is missing (as adoption would)
-        for nm in secret_names(template):
+        secrets, configmaps = dependent_names(template)
+        for nm in secrets:
             if self.secret_lister.try_get(ns, nm) is None:
                 await self._fetch_filtered(self.secret_informer, R.SECRETS, ns, nm)
-        for nm in configmap_names(template):
+        for nm in configmaps:
             if self.configmap_lister.try_get(ns, nm) is None:
                 await self._fetch_filtered(self.configmap_informer, R.CONFIGMAPS, ns, nm)
         spec_fp = fingerprint(template.get("spec")) if len(self.shards) > 1 and self.options.slim_shard_cache else None
@@ -407,9 +408,9 @@ class ReconcileMixin:
         if self.options.concurrent_dependents:
             # dependents need the shard template's UID for their ownerRefs, so they go after it — all at once
             holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) else shard_template
-            jobs = [self._sync_dependent(R.SECRETS, template, shard_template, shard, n) for n in secret_names(holder)]
-            jobs += [self._sync_dependent(R.CONFIGMAPS, template, shard_template, shard, n)
-                     for n in configmap_names(holder)]
+            secrets, configmaps = dependent_names(holder)
+            jobs = [self._sync_dependent(R.SECRETS, template, shard_template, shard, n) for n in secrets]
+            jobs += [self._sync_dependent(R.CONFIGMAPS, template, shard_template, shard, n) for n in configmaps]
             for r in await gather_all(jobs):
                 if isinstance(r, BaseException):
                     raise r
