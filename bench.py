@@ -37,6 +37,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "objects synced/sec + p50 controller->shard latency at 1/2/4/8 shards"
 NS = "nexus"
+# bench mode -> controller environment
+MODES = {"native": {"NEXUS__MODE": "native"},
+         "compat": {"NEXUS__MODE": "compat"},
+         "compat-unthrottled": {"NEXUS__MODE": "compat", "NEXUS__CLIENT_QPS": "-1"}}
 MARKERS = ["nexusalgorithmtemplates=spec.container.versionTag", "secrets=data.version", "configmaps=data.version"]
 
 
@@ -48,11 +52,17 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--templates", type=int, default=1000)
     p.add_argument("--payload", type=int, default=512, help="bytes per Secret/ConfigMap payload")
-    p.add_argument("--mode", default="native", choices=["native", "compat"])
+    p.add_argument("--mode", default="native", choices=list(MODES),
+                   help="native | compat (reference semantics incl. client-go's 5 QPS/10 burst) | "
+                        "compat-unthrottled (reference semantics without the client-side limiter)")
     p.add_argument("--workers", type=int, default=0, help="controller workers (0 = mode default)")
     p.add_argument("--timeout", type=float, default=600.0, help="per-wave convergence timeout (s)")
     p.add_argument("--keep", action="store_true", help="keep the work directory")
     p.add_argument("--extra-env", action="append", default=[], help="KEY=VAL passed to the controller process")
+    p.add_argument("--shard-latency-ms", type=float, default=0.0,
+                   help="added to every request a shard apiserver serves (emulates controller->shard RTT)")
+    p.add_argument("--shard-jitter-ms", type=float, default=0.0,
+                   help="uniform extra delay 0..J ms per shard request, on top of --shard-latency-ms")
     p.add_argument("--shards-per-rank", type=int, default=1,
                    help="experiments only: shard apiservers hosted per rank (the driver contract is 1)")
     return p.parse_args(argv)
@@ -143,6 +153,16 @@ def want(T: int, version: int) -> list:
             {"plural": "configmaps", "value": str(version), "count": T}]
 
 
+async def set_shard_latency(urls: list, latency_ms: float, jitter_ms: float) -> None:
+    """Drive the fake apiservers' fault hook (ncc/fakeapi/server.py `Faults`): every API request a shard
+    serves is delayed by latency + U(0, jitter) ms before it is processed, so each controller->shard write
+    pays a network round trip as it would against a remote cluster."""
+    import aiohttp
+    async with aiohttp.ClientSession() as session:
+        for u in urls:
+            await post(session, f"{u}/_fake/faults", {"latency_ms": latency_ms, "jitter_ms": jitter_ms})
+
+
 async def post(session, url, body, timeout=None):
     import aiohttp
     data = body if isinstance(body, bytes) else json.dumps(body)
@@ -201,6 +221,8 @@ async def run(args, d: Dist) -> dict | None:
             procs.append(spawn_fakeapi(f"shard-{d.rank * S + j}", pf, extra=extra))
             my_urls.append(wait_port_file(pf, procs[-1]))
         my_url = my_urls[0]
+        if args.shard_latency_ms or args.shard_jitter_ms:
+            await set_shard_latency(my_urls, args.shard_latency_ms, args.shard_jitter_ms)
         urls = [u for us in d.all_gather(my_urls) for u in us]
         ctrl_url = None
         controller = None
@@ -224,8 +246,9 @@ async def run(args, d: Dist) -> dict | None:
                 env = dict(os.environ)
                 env.update({"NEXUS__CONTROLLER_CONFIG_PATH": ckc, "NEXUS__SHARD_CONFIG_PATH": shard_dir,
                             "NEXUS__CONTROLLER_NAMESPACE": NS, "NEXUS__ALIAS": "controller-cluster",
-                            "NEXUS__MODE": args.mode, "NEXUS__LOG_LEVEL": "WARNING",
+                            "NEXUS__LOG_LEVEL": "WARNING",
                             "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+                env.update(MODES[args.mode])
                 if args.workers:  # native: per-process workers (otherwise the config's native-workers default)
                     env["NEXUS__WORKERS"] = str(args.workers)
                     env["NEXUS__NATIVE_WORKERS"] = str(args.workers)
@@ -319,6 +342,10 @@ async def run(args, d: Dist) -> dict | None:
                         lat.extend((t - c[k.split(":", 1)[-1]]) / 1e6 for k, t in objs.items())
             objs = args.steps * 3 * T * d.world * S
             value = objs / elapsed
+            # controller CPU (coordinator + every executor, all on rank 0) per synced object over the timed
+            # waves: the cost of the system under test, independent of how fast the fake apiservers are
+            ctl_cpu = {k: cpu1.get(k, 0.0) - cpu0.get(k, 0.0) for k in ("coordinator", "executors")}
+            us_per_obj = {k: round(v * 1e6 / objs, 1) for k, v in ctl_cpu.items()}
             from ncc.app import auto_coordinator_partitions, auto_executors_per_shard, cpu_share
             groups = d.world * S  # the controller's automatic sizing on this host (same rule, same cgroup)
             k = auto_executors_per_shard(groups)
@@ -334,13 +361,16 @@ async def run(args, d: Dist) -> dict | None:
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": None,
-                "dtype": "bf16",
+                "dtype": "n/a",  # a control plane: no tensor arithmetic, so no numeric precision to report
                 "data": "synthetic (fake kube-apiservers, random NexusAlgorithmTemplate/Secret/ConfigMap objects)",
                 "config": {"model": "NexusAlgorithmTemplate fan-out (1 Secret + 1 ConfigMap each)",
                            "global_batch": T, "seq_len": 3, "parallelism": f"shards{d.world}",
-                           "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload},
+                           "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload,
+                           "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
+                "controller_cpu_us_per_object": round(sum(ctl_cpu.values()) * 1e6 / objs, 1),
+                "controller_cpu_us_per_object_split": us_per_obj,
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,

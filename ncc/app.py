@@ -74,8 +74,13 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
 
 
 def client_limits(cfg: AppConfig) -> tuple[float, int]:
+    """(qps, burst) of the client-side token bucket; qps 0 = no limiter.  `client-qps` > 0 sets it,
+    < 0 switches it off in every mode (the "compat-unthrottled" baseline: reference scheduling without
+    client-go's default 5 QPS / burst 10), 0 keeps the mode default."""
     if cfg.client_qps > 0:
         return cfg.client_qps, cfg.client_burst
+    if cfg.client_qps < 0:
+        return 0.0, cfg.client_burst
     if cfg.mode == "compat":
         return COMPAT_QPS, COMPAT_BURST
     return 0.0, cfg.client_burst
@@ -192,6 +197,8 @@ class App:
         self._gc_task = None
         self._shard_files: dict = {}
         self.lost_leadership = False
+        self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
+        self.standby_was_warm = False  # caches had synced before this replica acquired the Lease
         self.coord_part: tuple | None = None  # (p, C) when the coordinator role is split over C processes
         self.partitions: CoordinatorPartitions | None = None  # children for partitions 1..C-1 (parent only)
 
@@ -353,35 +360,68 @@ class App:
             pass
         if self.ops is not None:
             await self.ops.start(self.cfg.health_bind_address or self.cfg.metrics_bind_address)
+        if self.gate is None and os.environ.get("NCC_GATED") == "1":
+            self.gate = asyncio.Event()  # a child pre-spawned by a warm standby: {"t": "go"} opens it
         if self.cfg.leader_elect and self.options.role != "executor":
             cfg = self.cfg
             self.elector = LeaderElector(self.client, cfg.leader_election_namespace or cfg.controller_namespace,
                                          cfg.leader_election_lease_name, identity_from_env(),
                                          lease_duration=cfg.lease_duration, renew_deadline=cfg.renew_deadline,
                                          retry_period=cfg.retry_period)
-            if not await self.elector.acquire(stop):
-                await self.close()
-                return
+            self.gate = asyncio.Event()
+        # Everything read-only starts now — informers on every cluster, shard executors (their workers gated
+        # while this replica stands by) — so a standby that acquires the Lease only has to open the gates.
+        self._start_components(controller)
+        run = asyncio.ensure_future(controller.run(stop, gate=self.gate))
+        try:
+            if self.elector is not None:
+                acquire = asyncio.ensure_future(self.elector.acquire(stop))
+                done, _ = await asyncio.wait({acquire, run}, return_when=asyncio.FIRST_COMPLETED)
+                if acquire not in done or not acquire.result():
+                    acquire.cancel()
+                    stop.set()
+                    await run
+                    return
+                self.standby_was_warm = controller.caches_synced.is_set() and \
+                    (self.pool is None or self.pool.all_synced())
 
-            def lost():
-                self.lost_leadership = True
-                stop.set()
-            self._lease_task = asyncio.ensure_future(self.elector.hold(stop, on_lost=lost))
+                def lost():
+                    self.lost_leadership = True
+                    # stop writing before the Lease can expire into another replica's hands: cancel the
+                    # workers and kill the executors now instead of letting them drain
+                    controller.abort_workers()
+                    for group in (self.pool, self.partitions):
+                        if group is not None:
+                            group.kill()
+                    stop.set()
+                self._lease_task = asyncio.ensure_future(self.elector.hold(stop, on_lost=lost))
+                self.open_gate()
+            await run
+        finally:
+            if not run.done():
+                run.cancel()
+                await asyncio.gather(run, return_exceptions=True)
+            await self.close()
+
+    def _start_components(self, controller: Controller) -> None:
         for s in self.shards:
             s.start()
         if isinstance(self.recorder, BroadcastRecorder):
             self.recorder.start()
         self.factory.start()
+        gated = self.gate is not None and not self.gate.is_set()
         if self.options.role == "coordinator":
             env = dict(os.environ)
             env.update(config_to_env(self.cfg))
             env.pop("NCC_COORDINATOR_PART", None)
+            env.pop("NCC_GATED", None)
             part, parts = self.coord_part or (0, 1)
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
-                                     env=env, per_shard=self.per_shard, part_base=part, part_stride=parts)
+                                     env=env, per_shard=self.per_shard, part_base=part, part_stride=parts,
+                                     gated=gated)
             self.pool.start()
             if parts > 1 and part == 0 and not os.environ.get("NCC_COORDINATOR_PART"):
-                self.partitions = CoordinatorPartitions(parts, env)
+                self.partitions = CoordinatorPartitions(parts, env, gated=gated)
                 self.partitions.start()
         if self.cfg.mode == "native":
             gctune.tune()
@@ -389,13 +429,19 @@ class App:
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
-                 "executors=%d×%d workers=%d", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
+                 "executors=%d×%d workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
-                 self.options.workers)
-        try:
-            await controller.run(stop)
-        finally:
-            await self.close()
+                 self.options.workers, " (standing by)" if gated else "")
+
+    def open_gate(self) -> None:
+        """Leading now (or released by the parent): start reconciling here and in every child process."""
+        if self.gate is None or self.gate.is_set():
+            return
+        log.info("gate open: starting workers (role=%s)", self.options.role)
+        for group in (self.pool, self.partitions):
+            if group is not None:
+                group.open_gate()
+        self.gate.set()
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
@@ -471,8 +517,12 @@ async def _amain(cfg: AppConfig, control_fd: int | None = None) -> int:
         app.controller.on_ready = lambda: channel.send({"t": "ready"})
 
         async def watch_parent():
-            while await channel.recv() is not None:
-                pass
+            while True:
+                batch = await channel.recv()
+                if batch is None:
+                    break
+                if any(isinstance(m, dict) and m.get("t") == "go" for m in batch):
+                    app.open_gate()  # the parent acquired the Lease
             stop.set()
         watcher = asyncio.ensure_future(watch_parent())
     try:

@@ -78,7 +78,7 @@ class AppConfig:
     rate_limit_elements_burst: int = 300
     # ---- framework extensions ----
     mode: str = "native"
-    client_qps: float = 0.0          # 0 = unlimited (compat mode forces client-go's 5/10)
+    client_qps: float = 0.0          # 0 = mode default (compat: client-go's 5/10, native: none); < 0 = none
     client_burst: int = 10
     client_pool_size: int = 64
     client_pipeline_depth: int = 1   # >1: HTTP/1.1-pipeline requests once all pool connections are busy

@@ -75,11 +75,13 @@ class Controller(ReconcileMixin):
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
                       "reports_pending": 0, "early_passes_skipped": 0}
-        self.ready = asyncio.Event()
+        self.ready = asyncio.Event()  # workers running
+        self.caches_synced = asyncio.Event()  # controller (and shard) caches synced
         self.role = o.role
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
         self.reporter = None  # executor role: callable(msg) sending results to the coordinator
         self.on_ready = None  # executor role: called once caches are synced and workers run
+        self.on_synced = None  # executor role: called once caches are synced (before a gate opens)
         self.shard_state: dict[str, dict] = {}  # coordinator role: key -> {shard: (uid, generation, error)}
         self._pending_event: set = set()
         # adoption_cache: template key → resourceVersion whose references were last verified as adopted
@@ -530,24 +532,47 @@ class Controller(ReconcileMixin):
             if self.options.orphan_sweep:
                 self.sweep_orphans()
 
-    async def run(self, stop: asyncio.Event, workers: int | None = None) -> None:
-        """Run (controller.go:851-884): cache barrier, workers, block until `stop`."""
+    async def run(self, stop: asyncio.Event, workers: int | None = None, gate: asyncio.Event | None = None) -> None:
+        """Run (controller.go:851-884): cache barrier, workers, block until `stop`.
+
+        With `gate` (a warm standby under leader election, or an executor pre-spawned for one) the caches
+        sync and keys queue up as usual, but the workers start only once the gate opens."""
         log.info("Starting NexusAlgorithmTemplate controller")
         log.info("Waiting for informer caches to sync")
         sync = asyncio.ensure_future(self.wait_for_caches())
-        stopper = asyncio.ensure_future(stop.wait())
-        done, _ = await asyncio.wait({sync, stopper}, return_when=asyncio.FIRST_COMPLETED)
-        if stopper in done:
-            sync.cancel()
-            await self.shutdown()
+        if not await self._until(sync, stop):
             return
-        stopper.cancel()
         if not sync.result():
             raise RuntimeError("failed to wait for caches to sync")
+        self.caches_synced.set()
+        if self.on_synced is not None:
+            self.on_synced()
+        if gate is not None and not gate.is_set():
+            log.info("Caches synced; standing by until this replica leads")
+            if not await self._until(asyncio.ensure_future(gate.wait()), stop):
+                return
         self.start_workers(workers)
         await stop.wait()
         log.info("Shutting down workers")
         await self.shutdown()
+
+    async def _until(self, fut: asyncio.Future, stop: asyncio.Event) -> bool:
+        """Wait for `fut` unless `stop` comes first (then shut down and return False)."""
+        stopper = asyncio.ensure_future(stop.wait())
+        done, _ = await asyncio.wait({fut, stopper}, return_when=asyncio.FIRST_COMPLETED)
+        if fut not in done:
+            fut.cancel()
+            await self.shutdown()
+            return False
+        stopper.cancel()
+        return True
+
+    def abort_workers(self) -> None:
+        """Leadership lost: cancel every worker now — a reconcile must not keep writing while another
+        replica may already hold the Lease."""
+        self.queue.shutdown()
+        for t in self._workers + self._aux:
+            t.cancel()
 
     async def shutdown(self) -> None:
         self.queue.shutdown()

@@ -87,8 +87,11 @@ class ExecutorHandle:
         self.env = env
         self.proc: asyncio.subprocess.Process | None = None
         self.channel: Channel | None = None
-        self.ready = asyncio.Event()
+        self.ready = asyncio.Event()  # workers running
+        self.synced = asyncio.Event()  # caches synced (a gated child reports this before it may run)
         self.restarts = 0
+        self.gated = False  # spawned for a warm standby: workers wait for {"t": "go"}
+        self.gate_open = False
         self._task: asyncio.Task | None = None
         self._stopping = False
 
@@ -102,23 +105,52 @@ class ExecutorHandle:
         else:
             args = ["-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
                     "--shards", ",".join(self.shards), "--part", f"{self.part}/{self.parts}"]
+        gated = self.gated and not self.gate_open
+        if gated:
+            env["NCC_GATED"] = "1"
+        else:
+            env.pop("NCC_GATED", None)
         self.proc = await asyncio.create_subprocess_exec(sys.executable, *args, pass_fds=(child.fileno(),), env=env)
         child.close()
         reader, writer = await asyncio.open_connection(sock=parent)
         self.channel = Channel(reader, writer)
+        if gated and self.gate_open:  # the gate opened while this child was being spawned
+            self.channel.send({"t": "go"})
+
+    def open_gate(self) -> None:
+        """This replica leads now: let the (already running, caches synced) child start its workers."""
+        if self.gate_open:
+            return
+        self.gate_open = True
+        if self.channel is not None:
+            self.channel.send({"t": "go"})
+
+    def kill(self) -> None:
+        """Leadership lost: stop the child at once (SIGKILL), without letting it drain its writes."""
+        self._stopping = True
+        if self.proc is not None and self.proc.returncode is None:
+            try:
+                self.proc.kill()
+            except ProcessLookupError:
+                pass
 
     async def _run(self) -> None:
         backoff = 1.0
         while not self._stopping:
             self.ready.clear()
+            self.synced.clear()
             await self._spawn()
             while True:
                 batch = await self.channel.recv()
                 if batch is None:
                     break
                 for msg in batch:
-                    if msg.get("t") == "ready":
+                    t = msg.get("t")
+                    if t == "ready":
                         self.ready.set()
+                        self.synced.set()
+                    elif t == "synced":
+                        self.synced.set()
                     self.on_message(self.index, msg)
             rc = await self.proc.wait()
             self.channel.close()
@@ -157,7 +189,7 @@ class ExecutorPool:
     each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
-                 part_base: int = 0, part_stride: int = 1):
+                 part_base: int = 0, part_stride: int = 1, gated: bool = False):
         """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
         mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
         keys are exactly a share of this coordinator's."""
@@ -166,6 +198,8 @@ class ExecutorPool:
         self.part_stride = max(1, part_stride)
         self.on_message = on_message
         self.env = env
+        self.gated = gated
+        self.gate_open = not gated
         self._next_index = 0
         self.handles: list[ExecutorHandle] = []
         for group in partition(shard_names, n):
@@ -175,6 +209,8 @@ class ExecutorPool:
         hs = [ExecutorHandle(self._next_index + j, list(shards), self.on_message, self.env,
                              self.part_base + self.part_stride * j, self.part_stride * self.per_shard)
               for j in range(self.per_shard)]
+        for h in hs:
+            h.gated, h.gate_open = self.gated, self.gate_open
         self._next_index += self.per_shard
         self.handles.extend(hs)
         return hs
@@ -215,6 +251,18 @@ class ExecutorPool:
     async def stop(self) -> None:
         await asyncio.gather(*(h.stop() for h in self.handles))
 
+    def open_gate(self) -> None:
+        self.gate_open = True
+        for h in self.handles:
+            h.open_gate()
+
+    def all_synced(self) -> bool:
+        return all(h.synced.is_set() for h in self.handles)
+
+    def kill(self) -> None:
+        for h in self.handles:
+            h.kill()
+
     def stats(self) -> dict:
         return {h.index: {"shards": h.shards, "part": f"{h.part}/{h.parts}", "restarts": h.restarts,
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
@@ -228,15 +276,16 @@ class CoordinatorPartitions:
     for its keys, and runs its own shard executors (global partitions p + C·j).  The parent holds the
     leader Lease and the ops endpoints; children exit when the parent's control channel closes."""
 
-    def __init__(self, parts: int, env: dict):
+    def __init__(self, parts: int, env: dict, gated: bool = False):
         self.parts = parts
         self.handles = []
         for p in range(1, parts):
             e = dict(env)
             e.update({"NCC_COORDINATOR_PART": f"{p}/{parts}", "NEXUS__LEADER_ELECT": "False",
                       "NEXUS__METRICS_BIND_ADDRESS": "", "NEXUS__HEALTH_BIND_ADDRESS": ""})
-            self.handles.append(ExecutorHandle(p, [], lambda i, m: None, e, p, parts, argv=["-m", "ncc"],
-                                               what="coordinator partition"))
+            h = ExecutorHandle(p, [], lambda i, m: None, e, p, parts, argv=["-m", "ncc"], what="coordinator partition")
+            h.gated = gated
+            self.handles.append(h)
 
     def start(self) -> None:
         for h in self.handles:
@@ -244,6 +293,14 @@ class CoordinatorPartitions:
 
     def ready(self) -> bool:
         return all(h.ready.is_set() for h in self.handles)
+
+    def open_gate(self) -> None:
+        for h in self.handles:
+            h.open_gate()
+
+    def kill(self) -> None:
+        for h in self.handles:
+            h.kill()
 
     async def stop(self) -> None:
         await asyncio.gather(*(h.stop() for h in self.handles))
@@ -271,13 +328,19 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
     ctl = app.controller
     ctl.reporter = channel.send
     ctl.on_ready = lambda: channel.send({"t": "ready", "i": index})
+    ctl.on_synced = lambda: channel.send({"t": "synced", "i": index})
 
     async def watch_parent():
-        # the coordinator closing its end (or dying) ends this executor
+        # {"t": "go"} opens the gate of an executor pre-spawned by a warm standby; the coordinator closing
+        # its end (or dying) ends this executor
         while True:
-            if await channel.recv() is None:
+            batch = await channel.recv()
+            if batch is None:
                 stop.set()
                 return
+            for msg in batch:
+                if isinstance(msg, dict) and msg.get("t") == "go":
+                    app.open_gate()
 
     wp = asyncio.ensure_future(watch_parent())
     try:

@@ -21,8 +21,8 @@ from ..api import resources as R
 from ..api.constants import go_quote as q
 from ..api.fingerprint import SLIM_FP, fingerprint
 from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
-from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready_condition, secret_names,
-                        template_owner_ref)
+from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready_condition, same_references,
+                        secret_names, template_owner_ref)
 from ..kube import errors as E
 from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
 
@@ -117,12 +117,20 @@ class ReconcileMixin:
         return await self.client.update_status(rt, namespace, obj, field_manager=field_manager)
 
     def _carry_adoption(self, old: dict, new):
-        """Our own status write changes only the template's status: keep its adoption mark (adoption_cache)."""
+        """Keep a template's adoption mark (adoption_cache) across our own status write.
+
+        A status write changes only `.status` — but native mode sends it as a merge PATCH without a
+        resourceVersion precondition, so the response may already carry a user's spec edit made after our
+        read (e.g. a new secretRef).  The mark moves to the response's version only when that version
+        references the same Secrets/ConfigMaps; otherwise it is dropped and the next pass re-adopts."""
         if self.options.adoption_cache and isinstance(new, dict):
             om, nm = meta(old), meta(new)
             key = f"{C.KIND_TEMPLATE}/{om.get('namespace', '')}/{om.get('name', '')}"
             if self._adopted.get(key) == om.get("resourceVersion"):
-                self._adopted[key] = nm.get("resourceVersion")
+                if om.get("uid") == nm.get("uid") and same_references(old, new):
+                    self._adopted[key] = nm.get("resourceVersion")
+                else:
+                    self._adopted.pop(key, None)
         return new
 
     async def report_template_init_condition(self, template: dict) -> dict:
@@ -285,8 +293,13 @@ class ReconcileMixin:
             key = f"{C.KIND_TEMPLATE}/{namespace}/{name}"
             rv = meta(template).get("resourceVersion")
             if self._adopted.get(key) != rv:
+                # A dependent event during the awaits below (our ownerRef removed, the Secret re-created)
+                # pops this token in `_on_dependent`; the mark is stored only if nothing invalidated it.
+                token = object()
+                self._adopted[key] = token
                 await self.adopt_references(template)
-                self._adopted[key] = rv
+                if self._adopted.get(key) is token:
+                    self._adopted[key] = rv
         else:
             await self.adopt_references(template)
         if self.role == "coordinator":

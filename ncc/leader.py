@@ -3,17 +3,19 @@
 The reference supports a single replica only: its Helm chart pins `replicas: 1` with the
 `Recreate` strategy ("NCC only supports single replica", .helm/templates/deployment.yaml:15-19)
 and there is no leader election (SURVEY.md §5.3 "HA: none").  With `leader-elect: true` this
-framework runs N replicas: one holds the Lease and reconciles, the others wait warm-standby
-(process up, probes answering) and take over within `lease-duration` of the leader dying, or
-immediately when the leader releases the Lease on a clean shutdown.
+framework runs N replicas: one holds the Lease and reconciles, the others wait as warm standbys —
+controller and shard informers listed and watching, shard executors spawned with their caches
+synced, only the reconcile workers gated (`App.run`) — and take over within `lease-duration` of
+the leader dying, or immediately when the leader releases the Lease on a clean shutdown.
 
 Semantics follow the usual Kubernetes controller pattern:
 * expiry is judged on the *local* clock from when this candidate last saw the Lease record change
   (holder / renewTime), never by comparing wall clocks across machines;
 * every acquire/renew is an optimistic-concurrency PUT (resourceVersion), so two candidates can
   never both win — the loser gets 409 and keeps waiting;
-* the leader renews every `retry-period`; if it cannot renew for `renew-deadline` it stops
-  leading (the app then exits non-zero so its replacement starts from a clean slate);
+* the leader renews every `retry-period`, each attempt bounded by the rest of the renew deadline; if
+  it cannot renew for `renew-deadline` it stops leading: workers are cancelled and executors killed at
+  once (no draining writes), and the app exits non-zero so its replacement starts from a clean slate;
 * release on shutdown empties `holderIdentity` so a standby takes over without waiting.
 """
 from __future__ import annotations
@@ -147,12 +149,24 @@ class LeaderElector:
                 return False
 
     async def hold(self, stop: asyncio.Event | None = None, on_lost=None) -> None:
-        """Renew every `retry_period` until `stop`; give up after `renew_deadline` without a renewal."""
+        """Renew every `retry_period` until `stop`; give up after `renew_deadline` without a renewal.
+
+        Each renew attempt is itself bounded by what is left of the renew deadline (client-go bounds it
+        with RenewDeadline the same way): a renew stuck in a slow request or Retry-After back-off must not
+        outlive the deadline, or a standby could take the expired Lease while this replica still writes."""
         last_ok = self.clock()
         while True:
             if await self._sleep(self.retry_period, stop):
                 return
-            if await self.try_acquire_or_renew():
+            budget = self.renew_deadline - (self.clock() - last_ok)
+            ok = False
+            if budget > 0:
+                try:
+                    ok = await asyncio.wait_for(self.try_acquire_or_renew(), timeout=budget)
+                except asyncio.TimeoutError:
+                    log.warning("lease %s/%s: renew did not finish within the renew deadline", self.namespace,
+                                self.name)
+            if ok:
                 last_ok = self.clock()
                 continue
             if not self.leading or self.clock() - last_ok >= self.renew_deadline:

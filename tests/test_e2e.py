@@ -214,6 +214,57 @@ async def test_leader_election_failover(tmp_path):
         await env.stop()
 
 
+async def test_warm_standby_takes_over_within_lease_duration(tmp_path):
+    """A standby lists/watches every cluster and pre-spawns its executors (workers gated) before it holds
+    the Lease.  When the leader dies without releasing the Lease, the first shard write of a new template
+    version lands within lease-duration + 1 s, with 1k templates in the caches."""
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    lease = 2.0
+    kw = dict(leader_elect=True, lease_duration=lease, renew_deadline=1.2, retry_period=0.2)
+    for i in range(1000):
+        env.controller_server.state.create(R.TEMPLATES, NS, make_template(i, NS))
+    apps = [App(env.app_config(mode="native", **kw)) for _ in range(2)]
+    stops = [asyncio.Event(), asyncio.Event()]
+    try:
+        await apps[0].build()
+        t0 = asyncio.ensure_future(apps[0].run(stops[0]))
+        await asyncio.wait_for(apps[0].controller.ready.wait(), 10)
+        await wait_for(lambda: asyncio.sleep(0, env.shard_servers[0].state.count(R.TEMPLATES) == 1000),
+                       timeout=30)
+        await apps[1].build()
+        t1 = asyncio.ensure_future(apps[1].run(stops[1]))
+        # the standby is warm: its caches and its executors' caches synced while it does not lead
+        await asyncio.wait_for(apps[1].controller.caches_synced.wait(), 10)
+        await wait_for(lambda: asyncio.sleep(0, apps[1].pool is not None and apps[1].pool.all_synced()), timeout=20)
+        assert not apps[1].elector.leading and not apps[1].controller.ready.is_set()
+
+        async def no_release():
+            return False
+        apps[0].elector.release = no_release  # the leader dies: its Lease is left to expire
+        stops[0].set()
+        await asyncio.wait_for(t0, 15)
+        loop = asyncio.get_running_loop()
+        t_dead = loop.time()
+        await mutate(cc, R.TEMPLATES, "algo-00007", lambda o: o["spec"]["container"].__setitem__("versionTag", "v-new"))
+
+        async def propagated():
+            st = await sc.get(R.TEMPLATES, NS, "algo-00007")
+            return st["spec"]["container"]["versionTag"] == "v-new"
+        await wait_for(propagated, timeout=lease + 5, interval=0.01)
+        took = loop.time() - t_dead
+        assert apps[1].elector.leading and apps[1].standby_was_warm
+        assert took < lease + 1.0, f"takeover to first shard write took {took:.2f}s"
+        stops[1].set()
+        await asyncio.wait_for(t1, 15)
+    finally:
+        for s in stops:
+            s.set()
+        await cc.close()
+        await sc.close()
+        await env.stop()
+
+
 async def test_partitioned_executors_per_shard(tmp_path):
     """`executors-per-shard: 2`: two key-partitioned executors serve each shard; every template is synced
     exactly by its partition's owner and the coordinator still reports Ready for all."""

@@ -75,3 +75,24 @@ async def test_hold_reports_loss_after_renew_deadline():
     lost = asyncio.Event()
     await asyncio.wait_for(a.hold(None, on_lost=lost.set), 2.0)
     assert lost.is_set() and not a.leading
+
+
+async def test_hold_bounds_a_hanging_renew_by_the_renew_deadline():
+    """ADVICE r1: a renew that hangs (slow apiserver, Retry-After back-off) must not outlive renew_deadline;
+    otherwise a standby could take the expired Lease while this replica still believes it leads."""
+    st = ClusterState("c")
+    client = FakeClient(st, simple=False)
+    a = LeaderElector(client, NS, "ncc", "a", lease_duration=0.5, renew_deadline=0.3, retry_period=0.05)
+    assert await a.acquire()
+    orig_get = client.get
+
+    async def hanging_get(*args, **kw):
+        await asyncio.sleep(30)
+        return await orig_get(*args, **kw)
+    client.get = hanging_get
+    lost = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    t0 = loop.time()
+    await asyncio.wait_for(a.hold(None, on_lost=lost.set), 2.0)
+    assert lost.is_set() and not a.leading
+    assert loop.time() - t0 < 0.5  # gave up inside the lease duration, not after the hung request

@@ -450,3 +450,59 @@ async def test_coordinator_skips_early_pass_until_reports_complete():
     before = ctl2.queue.core.waiting() + len(ctl2.queue)
     ctl2._on_crd_update(new, newer, C.KIND_TEMPLATE)
     assert ctl2.stats["early_passes_skipped"] == 0 and ctl2.queue.core.waiting() + len(ctl2.queue) >= before
+
+
+async def test_status_patch_racing_a_spec_edit_drops_the_adoption_mark():
+    """native status writes are merge PATCHes without a resourceVersion precondition, so the
+    response can carry a user's spec edit made after our read.  If that edit adds a reference, the adoption
+    mark must not move to the response's version: the next pass adopts the new Secret."""
+    env = Env(1)
+    t = env.seed()
+    name, key = t["metadata"]["name"], make_key(C.KIND_TEMPLATE, NS, t["metadata"]["name"])
+    ctl = env.build()
+    await ctl.sync_template(NS, name)
+    env.refresh()
+    cur = ctl.template_lister.get(NS, name)
+    assert ctl._adopted[key] == cur["metadata"]["resourceVersion"]
+    env.cstate.create(R.SECRETS, NS, make_secret("s-new", NS))
+    # the user adds a secretRef between our read and our status PATCH
+    orig_patch = env.cclient.patch
+
+    async def racing_patch(rt, ns, nm, body, **kw):
+        if rt is R.TEMPLATES and kw.get("subresource") == "status":
+            live = env.cstate.get(R.TEMPLATES, NS, name)
+            spec = dict(live["spec"])
+            rte = dict(spec["runtimeEnvironment"])
+            rte["mappedEnvironmentVariables"] = list(rte["mappedEnvironmentVariables"]) + [
+                {"secretRef": {"name": "s-new"}}]
+            spec["runtimeEnvironment"] = rte
+            env.cstate.update(R.TEMPLATES, NS, dict(live, spec=spec))
+        return await orig_patch(rt, ns, nm, body, **kw)
+    env.cclient.patch = racing_patch
+    stale = dict(cur, status=dict(cur["status"], syncedToClusters=[]))  # forces a status write
+    res = await ctl.report_template_synced_condition(stale, ["s"], ["c"], ["s0"])
+    env.cclient.patch = orig_patch
+    assert [e["secretRef"]["name"] for e in res["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"]
+            if e.get("secretRef")] == ["s", "s-new"]
+    assert ctl._adopted.get(key) != res["metadata"]["resourceVersion"]
+    env.refresh()
+    await ctl.sync_template(NS, name)
+    owners = env.cstate.get(R.SECRETS, NS, "s-new")["metadata"].get("ownerReferences") or []
+    assert [o["name"] for o in owners] == [name]
+
+
+async def test_adoption_mark_not_stored_when_invalidated_during_adoption():
+    """a dependent event that arrives while `adopt_references` is awaiting must win over the
+    mark the pass would store afterwards."""
+    env = Env(1)
+    t = env.seed()
+    name, key = t["metadata"]["name"], make_key(C.KIND_TEMPLATE, NS, t["metadata"]["name"])
+    ctl = env.build()
+    orig = ctl.adopt_references
+
+    async def adopt_then_event(tpl):
+        await orig(tpl)
+        ctl._on_dependent(env.cstate.get(R.SECRETS, NS, "s"), "secret")  # e.g. our ownerRef removed
+    ctl.adopt_references = adopt_then_event
+    await ctl.sync_template(NS, name)
+    assert key not in ctl._adopted

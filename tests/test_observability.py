@@ -225,7 +225,8 @@ async def test_executor_restarts_after_crash(tmp_path):
 
 
 async def test_executor_protocol_in_process(tmp_path, monkeypatch):
-    """`executor_main` driven in-process over a socketpair: ready → per-shard report → clean exit on EOF."""
+    """`executor_main` driven in-process over a socketpair: synced → ready → per-shard report → clean exit
+    on EOF."""
     from ncc.config import config_to_env
     from ncc.controller.executor import executor_main
     env = await FakeEnvironment(1, str(tmp_path), subprocesses=True, token="t0k").start()
@@ -244,7 +245,7 @@ async def test_executor_protocol_in_process(tmp_path, monkeypatch):
         while loop.time() < end and not any(m.get("t") == "report" for m in msgs):
             batch = await asyncio.wait_for(ch.recv(), 15)
             msgs.extend(batch or [])
-        assert msgs[0] == {"t": "ready", "i": 0}
+        assert msgs[:2] == [{"t": "synced", "i": 0}, {"t": "ready", "i": 0}]
         rep = next(m for m in msgs if m.get("t") == "report")
         assert rep["k"] == f"template/{NS}/algo-00001" and rep["r"] == {"shard-0": None} and rep["w"] is True
         ch.close()  # the coordinator going away ends the executor
