@@ -325,6 +325,13 @@ async def run(args, d: Dist) -> dict | None:
                         ctrl_times.append((await converge(step, True, ctrl_url))["times"])
             d.sync()
             elapsed = time.perf_counter() - t_start
+            ctrl_api = None
+            if d.rank == 0:  # LIST/WATCH load the controller put on its own cluster (watch relay: 1 each per kind)
+                import aiohttp as _aiohttp
+                async with session.get(f"{ctrl_url}/_fake/stats", timeout=_aiohttp.ClientTimeout(total=30)) as r:
+                    st = await r.json()
+                ctrl_api = {"lists": st["state"]["list"], "watches": st["state"]["watch"],
+                            "requests": st["requests"]["total"]}
             rss: dict = {}
             cpu1 = cpu_seconds(named, rss)
             util = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 3) for k in cpu1}
@@ -374,6 +381,7 @@ async def run(args, d: Dist) -> dict | None:
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
+                "controller_apiserver_load": ctrl_api,
                 "controller_sizing": {"cpus": cpu_share(), "executors_per_shard": k,
                                       "coordinator_partitions": auto_coordinator_partitions(groups, k),
                                       "overrides": [kv for kv in args.extra_env if kv.startswith("NEXUS__")]},

@@ -46,7 +46,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 11
+#define NCC_NATIVE_ABI 12
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -656,6 +656,31 @@ py::object scan_event_part(py::bytes line, int parts, const std::string& default
                           py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u, kp, mask);
 }
 
+// relay_scan(line, parts, default_ns) -> (type_code, namespace, name, key_partition, owner_partition_mask,
+//     n_owners) | None.  The coordinator's watch relay (ncc/controller/relay.py) routes every controller-side
+// watch line to the executors whose key partitions need it with this one call: type_code 0 ADDED,
+// 1 MODIFIED, 2 DELETED, 3 anything else (BOOKMARK, ERROR); `namespace` is already defaulted.
+py::object relay_scan(py::bytes line, int parts, const std::string& default_ns) {
+    if (parts < 1 || parts > 63) throw py::value_error("relay_scan: parts must be in 1..63");
+    char* buf = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
+    std::string_view type, ns, name, rv;
+    std::vector<std::string_view> owners, uids;
+    Scanner sc(buf, static_cast<size_t>(len));
+    sc.owners = &owners;
+    sc.owner_uids = &uids;
+    if (!sc.scan(type, ns, name, rv)) return py::none();
+    int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
+    std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
+    const uint32_t up = static_cast<uint32_t>(parts);
+    long long kp = static_cast<long long>(key_crc(kns, name) % up);
+    unsigned long long mask = 0;
+    for (const auto& o : owners) mask |= 1ull << (key_crc(kns, o) % up);
+    return py::make_tuple(code, py::str(kns.data(), kns.size()), py::str(name.data(), name.size()), kp, mask,
+                          static_cast<long long>(owners.size()));
+}
+
 py::int_ key_partition(const std::string& ns, const std::string& name, int parts) {
     if (parts < 1) throw py::value_error("key_partition: parts must be >= 1");
     return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));
@@ -931,6 +956,8 @@ PYBIND11_MODULE(_native, m) {
           "(status, content_length|-1, chunked, connection_close, retry_after|None) of an HTTP/1.1 response head");
     m.def("parse_request_head", &parse_request_head, py::arg("head"),
           "(method, target, {lower-cased name: value}) of an HTTP/1.1 request head");
+    m.def("relay_scan", &relay_scan, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
+          "(type_code, namespace, name, key_partition, owner_partition_mask, n_owners) of a watch line");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");

@@ -198,6 +198,8 @@ class App:
         self._shard_files: dict = {}
         self.lost_leadership = False
         self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
+        self.relay = None  # coordinator: WatchRelay feeding the executors
+        self.relay_feeds: list | None = None  # executor: per-kind feeds from the coordinator's relay
         self.standby_was_warm = False  # caches had synced before this replica acquired the Lease
         self.coord_part: tuple | None = None  # (p, C) when the coordinator role is split over C processes
         self.partitions: CoordinatorPartitions | None = None  # children for partitions 1..C-1 (parent only)
@@ -247,6 +249,13 @@ class App:
             for rt, index in ((R.SECRETS, "secret"), (R.CONFIGMAPS, "configmap")):
                 infs[rt].owner_filter = partition_owner_filter(
                     *o.partition, referenced=lambda ns, name, i=index: bool(tstore.by_index(i, f"{ns}/{name}")))
+        if o.role == "executor" and os.environ.get("NCC_RELAY") == "1":
+            # the coordinator lists and watches the controller cluster for us (ncc/controller/relay.py)
+            from .controller.relay import KINDS, RelayFeed
+            self.relay_feeds = []
+            for rt in KINDS:
+                infs[rt].feed = RelayFeed()
+                self.relay_feeds.append(infs[rt].feed)
         if o.role == "coordinator":
             self.shards = []
             # the coordinator adopts and reports; it never copies payloads: keep metadata only and skip
@@ -346,6 +355,8 @@ class App:
             out["executors"] = self.pool.stats()
         if self.partitions is not None:
             out["coordinator_partitions"] = self.partitions.stats()
+        if self.relay is not None:
+            out["watch_relay"] = dict(self.relay.stats)
         if self.elector is not None:
             out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
                              "transitions": self.elector.transitions}
@@ -404,6 +415,14 @@ class App:
             await self.close()
 
     def _start_components(self, controller: Controller) -> None:
+        if self.options.role == "coordinator" and self.cfg.watch_relay and self.n_executors > 0:
+            from . import native as _native
+            if _native.load() is not None and hasattr(self.client, "watch_raw"):
+                from .controller.relay import KINDS, WatchRelay
+                infs = {R.TEMPLATES: controller.template_informer, R.WORKGROUPS: controller.workgroup_informer,
+                        R.SECRETS: controller.secret_informer, R.CONFIGMAPS: controller.configmap_informer}
+                self.relay = WatchRelay([infs[rt] for rt in KINDS], controller.template_informer.store,
+                                        self.cfg.controller_namespace)
         for s in self.shards:
             s.start()
         if isinstance(self.recorder, BroadcastRecorder):
@@ -415,10 +434,12 @@ class App:
             env.update(config_to_env(self.cfg))
             env.pop("NCC_COORDINATOR_PART", None)
             env.pop("NCC_GATED", None)
+            env.pop("NCC_RELAY", None)
             part, parts = self.coord_part or (0, 1)
+            exec_env = dict(env, NCC_RELAY="1") if self.relay is not None else env
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
-                                     env=env, per_shard=self.per_shard, part_base=part, part_stride=parts,
-                                     gated=gated)
+                                     env=exec_env, per_shard=self.per_shard, part_base=part, part_stride=parts,
+                                     gated=gated, relay=self.relay)
             self.pool.start()
             if parts > 1 and part == 0 and not os.environ.get("NCC_COORDINATOR_PART"):
                 self.partitions = CoordinatorPartitions(parts, env, gated=gated)

@@ -128,6 +128,10 @@ class Informer:
         # and promoted without json decoding or handler dispatch (the writer already acted on them).
         self.echo_fastpath = False
         self.echoes = 0
+        # Watch relay (ncc/controller/relay.py): `tap` sees every raw line and listing this informer takes in
+        # (the coordinator forwarding them); `feed` replaces LIST/WATCH by what a coordinator forwards.
+        self.tap = None
+        self.feed = None
 
     # ------------------------------------------------------------- public API
     def add_event_handler(self, on_add=None, on_update=None, on_delete=None) -> None:
@@ -205,6 +209,13 @@ class Informer:
             token = lm.get("continue")
             if not token:
                 break
+        if self.tap is not None:
+            self.tap.on_list(items)
+        await self._replace_items(items)
+        return rv
+
+    async def _replace_items(self, items: list) -> None:
+        """Swap in a complete listing (LIST, or a relayed snapshot) and deliver the differences."""
         if self.key_filter is not None or self.owner_filter is not None:
             items = [o for o in items if self._wanted(o.get("metadata") or {})]
         self._stash.clear()  # the relist is newer than anything parked
@@ -219,102 +230,119 @@ class Informer:
         if synced_before:
             for o in deleted:
                 await self._dispatch_delete(DeletedFinalStateUnknown(key_of(o), o))
-        return rv
+
+    def _line_ctx(self, force: bool = False):
+        """Scanner state for the raw-line path, or None when lines must be decoded one by one (no native
+        module, or nothing to gain: no filters, no echo promotion, no metadata-only skipping).  `force`
+        asks for the raw path whenever the native module is there (a relayed feed is raw lines anyway)."""
+        kf, of = self.key_filter, self.owner_filter
+        mo = self.metadata_only
+        if not (force or self.echo_fastpath or kf is not None or of is not None or mo):
+            return None
+        mod = _native.load()
+        if mod is None:
+            return None
+        scan = mod.scan_event_owners if (of is not None or mo) else mod.scan_event
+        nparts = 0
+        kpart = opart = oref = None
+        # partition filters (executor key partitions) are evaluated natively: crc32 % parts of the key and
+        # of every owner, so a foreign line costs one scan and two integer tests
+        parts = {getattr(f, "parts", None) for f in (kf, of) if f is not None}
+        if len(parts) == 1 and None not in parts:
+            nparts = parts.pop()
+            default_ns_ = self.namespace or ""
+
+            def scan(line, _s=mod.scan_event_part, _p=nparts, _d=default_ns_):
+                return _s(line, _p, _d)
+            kpart = kf.part if kf is not None else None
+            opart = of.part if of is not None else None
+            oref = getattr(of, "referenced", None) if of is not None else None
+            kf = of = None
+        return (scan, nparts, kpart, opart, oref, kf, of, mo)
 
     async def _watch(self, rv: str) -> str:
         """Consume one watch stream; returns the last RV seen.  Raises Gone to force a relist."""
         lo, hi = self.watch_timeout
         kw = dict(resource_version=rv, timeout_seconds=random.randint(lo, hi), allow_bookmarks=True,
                   label_selector=self.label_selector)
-        scan = None
-        nparts = 0
-        kf, of = self.key_filter, self.owner_filter
-        mo = self.metadata_only
-        if (self.echo_fastpath or kf is not None or of is not None or mo) and hasattr(self.client, "watch_raw"):
-            mod = _native.load()
-            if mod is not None:
-                scan = mod.scan_event_owners if (of is not None or mo) else mod.scan_event
-                # partition filters (executor key partitions) are evaluated natively: crc32 % parts of the
-                # key and of every owner, so a foreign line costs one scan and two integer tests
-                parts = {getattr(f, "parts", None) for f in (kf, of) if f is not None}
-                if len(parts) == 1 and None not in parts:
-                    nparts = parts.pop()
-                    default_ns_ = self.namespace or ""
-
-                    def scan(line, _s=mod.scan_event_part, _p=nparts, _d=default_ns_):
-                        return _s(line, _p, _d)
-                    kpart = kf.part if kf is not None else None
-                    opart = of.part if of is not None else None
-                    oref = getattr(of, "referenced", None) if of is not None else None
-                    kf = of = None
-        if scan is not None:
-            loads = loads_bytes
-            store = self.store
-            default_ns = self.namespace or ""
-            inflight, stash = self._inflight, self._stash
+        ctx = self._line_ctx(force=self.tap is not None) if hasattr(self.client, "watch_raw") else None
+        if ctx is not None:
             batches = getattr(self.client, "watch_raw_batches", None)
             if batches is not None:
                 source = batches(self.rt, self.namespace, **kw)
             else:
                 source = _single_lines(self.client.watch_raw(self.rt, self.namespace, **kw))
+            tap = self.tap
             async for lines in source:
-                for line in lines:
-                    sc = None
-                    if nparts:
-                        sc = scan(line)
-                        if sc is not None and sc[0] in _OBJECT_EVENTS and (
-                                (kpart is not None and sc[6] != kpart) or
-                                (opart is not None and sc[4] and not (sc[7] >> opart) & 1 and
-                                 (oref is None or not oref(sc[1] or default_ns, sc[2])))):
-                            rv = self.last_rv = sc[3]
-                            self._filtered_out(sc[1] or default_ns, sc[2])
-                            continue
-                    elif kf is not None or of is not None:
-                        sc = scan(line)
-                        if sc is not None and sc[0] in _OBJECT_EVENTS:
-                            ns_ = sc[1] or default_ns
-                            if (kf is not None and not kf(ns_, sc[2])) or \
-                                    (of is not None and not of(ns_, sc[2], sc[4])):
-                                rv = self.last_rv = sc[3]
-                                self._filtered_out(ns_, sc[2])
-                                continue
-                    if mo:
-                        if sc is None:
-                            sc = scan(line)
-                        if sc is not None and sc[0] == "MODIFIED":
-                            cur = store.get(sc[1] or default_ns, sc[2])
-                            refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
-                            if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
-                                    tuple(r.get("uid", "") for r in refs) == sc[5]:
-                                rv = self.last_rv = sc[3]
-                                self.filtered += 1
-                                continue
-                    if store._assumed or inflight:
-                        if sc is None:
-                            sc = scan(line)
-                        if sc is not None and sc[0] in ("ADDED", "MODIFIED"):
-                            key = ObjectKey(sc[1] or default_ns, sc[2])
-                            if store.confirm(key, sc[3]) is not None:
-                                rv = self.last_rv = sc[3]
-                                self.events += 1
-                                self.echoes += 1
-                                continue
-                            if key in inflight:  # overtook the response of our write: park it
-                                prev = stash.get(key)
-                                if prev is not None:
-                                    await self._apply_line(prev[1])
-                                stash[key] = (sc[3], line)
-                                rv = self.last_rv = sc[3]
-                                continue
-                    if stash and sc is not None:
-                        prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
-                        if prev is not None:  # keep per-key order
-                            await self._apply_line(prev[1])
-                    ev = loads(line)
-                    rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
+                if tap is not None:
+                    tap.on_lines(lines)
+                rv = await self._consume(lines, ctx, rv)
             return rv
         async for ev in self.client.watch(self.rt, self.namespace, **kw):
             rv = await self._handle(ev.type, ev.object, rv)
+        return rv
+
+    async def _consume(self, lines, ctx, rv: str) -> str:
+        """Apply one batch of raw watch lines (see `_line_ctx`); returns the last RV seen."""
+        scan, nparts, kpart, opart, oref, kf, of, mo = ctx
+        loads = loads_bytes
+        store = self.store
+        default_ns = self.namespace or ""
+        inflight, stash = self._inflight, self._stash
+        for line in lines:
+            sc = None
+            if nparts:
+                sc = scan(line)
+                if sc is not None and sc[0] in _OBJECT_EVENTS and (
+                        (kpart is not None and sc[6] != kpart) or
+                        (opart is not None and sc[4] and not (sc[7] >> opart) & 1 and
+                         (oref is None or not oref(sc[1] or default_ns, sc[2])))):
+                    rv = self.last_rv = sc[3]
+                    self._filtered_out(sc[1] or default_ns, sc[2])
+                    continue
+            elif kf is not None or of is not None:
+                sc = scan(line)
+                if sc is not None and sc[0] in _OBJECT_EVENTS:
+                    ns_ = sc[1] or default_ns
+                    if (kf is not None and not kf(ns_, sc[2])) or \
+                            (of is not None and not of(ns_, sc[2], sc[4])):
+                        rv = self.last_rv = sc[3]
+                        self._filtered_out(ns_, sc[2])
+                        continue
+            if mo:
+                if sc is None:
+                    sc = scan(line)
+                if sc is not None and sc[0] == "MODIFIED":
+                    cur = store.get(sc[1] or default_ns, sc[2])
+                    refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
+                    if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
+                            tuple(r.get("uid", "") for r in refs) == sc[5]:
+                        rv = self.last_rv = sc[3]
+                        self.filtered += 1
+                        continue
+            if store._assumed or inflight:
+                if sc is None:
+                    sc = scan(line)
+                if sc is not None and sc[0] in ("ADDED", "MODIFIED"):
+                    key = ObjectKey(sc[1] or default_ns, sc[2])
+                    if store.confirm(key, sc[3]) is not None:
+                        rv = self.last_rv = sc[3]
+                        self.events += 1
+                        self.echoes += 1
+                        continue
+                    if key in inflight:  # overtook the response of our write: park it
+                        prev = stash.get(key)
+                        if prev is not None:
+                            await self._apply_line(prev[1])
+                        stash[key] = (sc[3], line)
+                        rv = self.last_rv = sc[3]
+                        continue
+            if stash and sc is not None:
+                prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
+                if prev is not None:  # keep per-key order
+                    await self._apply_line(prev[1])
+            ev = loads(line)
+            rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
         return rv
 
     async def _handle(self, t: str, obj: dict, rv: str) -> str:
@@ -394,7 +422,34 @@ class Informer:
             old = self.store.delete(obj)
             await self._dispatch_delete(old if old is not None else obj)
 
+    async def _run_feed(self) -> None:
+        """Relay mode (an executor under a coordinator's watch relay, ncc/controller/relay.py): the
+        coordinator is the only process listing and watching the controller cluster; it forwards a snapshot
+        of every kind once (and again after each of its relists) and then the raw watch lines this
+        executor's key partition needs."""
+        ctx = self._line_ctx(force=True)
+        feed = self.feed
+        while not self._stopping:
+            what, lines = await feed.get()
+            if what == "s":
+                loads = loads_bytes
+                items = []
+                for line in lines:
+                    ev = loads(line)
+                    if ev.get("type") in ("ADDED", "MODIFIED"):
+                        items.append(ev.get("object") or {})
+                await self._replace_items(items)
+            elif ctx is not None:
+                self.last_rv = await self._consume(lines, ctx, self.last_rv)
+            else:
+                for line in lines:
+                    ev = loads_bytes(line)
+                    self.last_rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, self.last_rv)
+
     async def _run(self) -> None:
+        if self.feed is not None:
+            await self._run_feed()
+            return
         backoff = 0.8
         rv = ""
         need_list = True

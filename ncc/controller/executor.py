@@ -26,6 +26,7 @@ import sys
 import zlib
 
 from .ipc import Channel
+from .relay import deliver
 from ..aio import wait_timeout
 
 log = logging.getLogger("ncc.executor")
@@ -92,6 +93,8 @@ class ExecutorHandle:
         self.restarts = 0
         self.gated = False  # spawned for a warm standby: workers wait for {"t": "go"}
         self.gate_open = False
+        self.on_spawn = None  # callable(handle) once the channel to a (re)started child is up (watch relay)
+        self.on_exit = None  # callable(handle) when that child has gone
         self._task: asyncio.Task | None = None
         self._stopping = False
 
@@ -116,6 +119,8 @@ class ExecutorHandle:
         self.channel = Channel(reader, writer)
         if gated and self.gate_open:  # the gate opened while this child was being spawned
             self.channel.send({"t": "go"})
+        if self.on_spawn is not None:
+            self.on_spawn(self)
 
     def open_gate(self) -> None:
         """This replica leads now: let the (already running, caches synced) child start its workers."""
@@ -152,6 +157,8 @@ class ExecutorHandle:
                     elif t == "synced":
                         self.synced.set()
                     self.on_message(self.index, msg)
+            if self.on_exit is not None:
+                self.on_exit(self)
             rc = await self.proc.wait()
             self.channel.close()
             if self._stopping:
@@ -189,7 +196,7 @@ class ExecutorPool:
     each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
-                 part_base: int = 0, part_stride: int = 1, gated: bool = False):
+                 part_base: int = 0, part_stride: int = 1, gated: bool = False, relay=None):
         """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
         mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
         keys are exactly a share of this coordinator's."""
@@ -198,6 +205,7 @@ class ExecutorPool:
         self.part_stride = max(1, part_stride)
         self.on_message = on_message
         self.env = env
+        self.relay = relay  # coordinator's WatchRelay: executors get the controller cluster from it
         self.gated = gated
         self.gate_open = not gated
         self._next_index = 0
@@ -211,6 +219,8 @@ class ExecutorPool:
               for j in range(self.per_shard)]
         for h in hs:
             h.gated, h.gate_open = self.gated, self.gate_open
+            if self.relay is not None:
+                h.on_spawn, h.on_exit = self.relay.attach, self.relay.detach
         self._next_index += self.per_shard
         self.handles.extend(hs)
         return hs
@@ -329,6 +339,7 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
     ctl.reporter = channel.send
     ctl.on_ready = lambda: channel.send({"t": "ready", "i": index})
     ctl.on_synced = lambda: channel.send({"t": "synced", "i": index})
+    feeds = app.relay_feeds  # controller informers fed by the coordinator's watch relay (or None)
 
     async def watch_parent():
         # {"t": "go"} opens the gate of an executor pre-spawned by a warm standby; the coordinator closing
@@ -339,7 +350,11 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
                 stop.set()
                 return
             for msg in batch:
-                if isinstance(msg, dict) and msg.get("t") == "go":
+                if not isinstance(msg, dict):
+                    continue
+                if feeds is not None and deliver(feeds, msg):
+                    continue
+                if msg.get("t") == "go":
                     app.open_gate()
 
     wp = asyncio.ensure_future(watch_parent())

@@ -563,3 +563,53 @@ def test_partitioned_coordinators_share_the_executors(tmp_path, monkeypatch):
         finally:
             await env.stop()
     aio.run(go())
+
+
+async def test_watch_relay_one_list_and_watch_per_kind_and_relist(tmp_path):
+    """Native mode with 2 shards × 2 executors: the controller apiserver serves one LIST and one WATCH per
+    kind (the coordinator's; executors are fed by its watch relay).  After a 410 relist of the coordinator
+    (watch history compacted while the apiserver was unreachable), executors get a fresh snapshot: a
+    template changed and one deleted during the gap both reach the shards, with no executor LIST."""
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(1)
+    st = env.controller_server.state
+    for i in range(20):
+        st.create(R.SECRETS, NS, make_secret(f"s{i}", NS))
+        st.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
+        st.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[f"c{i}"]))
+    try:
+        async with Running(env, "native", executors_per_shard=2) as app:
+            assert app.relay is not None and len(app.pool.handles) == 4
+
+            async def all_synced():
+                return all(s.state.count(R.TEMPLATES) == 20 and s.state.count(R.SECRETS) == 20
+                           for s in env.shard_servers)
+            await wait_for(all_synced, timeout=20)
+            assert st.stats["list"] == 4 and st.stats["watch"] == 4, st.stats
+
+            srv = env.controller_server
+            srv.faults.update({"down": True})
+            srv.drop_watches()
+            cur = st.get(R.TEMPLATES, NS, "algo-00003")
+            upd = dict(cur, spec=dict(cur["spec"], container=dict(cur["spec"]["container"], versionTag="v-gap")))
+            st.update(R.TEMPLATES, NS, upd)
+            st.delete(R.TEMPLATES, NS, "algo-00004")
+            st.compact()
+            srv.faults.update({"down": False})
+
+            async def caught_up():
+                t = await sc.get(R.TEMPLATES, NS, "algo-00003")
+                if t["spec"]["container"]["versionTag"] != "v-gap":
+                    return False
+                try:
+                    await sc.get(R.TEMPLATES, NS, "algo-00004")
+                    return False
+                except E.NotFound:
+                    return True
+            await wait_for(caught_up, timeout=20)
+            assert st.stats["list"] == 8, st.stats  # one relist per kind, by the coordinator only
+            assert app.relay.stats["snapshots"] >= 8
+    finally:
+        await cc.close()
+        await sc.close()
+        await env.stop()
