@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Build the in-tree native extension `ncc/_native*.so` (C++17 + pybind11).
+"""Build the in-tree native code: the extension `ncc/_native*.so` (C++17 + pybind11) and the native
+shard executor `ncc/bin/ncc-executor` (C++20 coroutines + epoll + OpenSSL, sources in native/executor/).
 
 Usage: python native/build.py [--debug] [--sanitize]
 `--sanitize` builds with AddressSanitizer/UBSan for host-side testing; run the tests with
@@ -25,7 +26,48 @@ def target_path() -> str:
     return os.path.join(ROOT, "ncc", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+EXECUTOR_DIR = os.path.join(HERE, "executor")
+EXECUTOR_MAIN = os.path.join(EXECUTOR_DIR, "executor.cpp")
+
+
+def executor_path() -> str:
+    return os.path.join(ROOT, "ncc", "bin", "ncc-executor")
+
+
+def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
+    """The native shard executor (one translation unit; headers alongside)."""
+    out = executor_path()
+    flavor = "sanitize" if sanitize else ("debug" if debug else "release")
+    stamp = out + ".flavor"
+    sources = [os.path.join(EXECUTOR_DIR, f) for f in sorted(os.listdir(EXECUTOR_DIR))
+               if f.endswith((".cpp", ".hpp"))]
+    if os.path.exists(out) and os.path.exists(stamp):
+        with open(stamp) as f:
+            same = f.read().strip() == flavor
+        if same and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in sources + [__file__]):
+            return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-std=c++20", "-fcoroutines", "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"]
+    if debug or sanitize:
+        flags += ["-O1", "-fno-omit-frame-pointer"]
+    else:
+        flags += ["-O2", "-DNDEBUG"]
+    if sanitize:
+        flags += ["-fsanitize=address,undefined"]
+    tmp = out + ".tmp"
+    cmd = [cxx, *flags, EXECUTOR_MAIN, "-o", tmp, "-lssl", "-lcrypto"]
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(flavor)
+    return out
+
+
 def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
+    build_executor(debug, sanitize, verbose)
     import pybind11
 
     out = target_path()

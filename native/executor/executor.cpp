@@ -1,0 +1,1522 @@
+// ncc-executor: the native shard executor (native mode's data plane).
+//
+// One process per shard group and key partition, spawned and supervised by the coordinator
+// (ncc/controller/executor.py) exactly like the Python executor (`python -m ncc.executor`) it
+// replaces, and speaking the same socketpair protocol (ncc/controller/ipc.py, msgpack frames):
+//
+//   coordinator -> executor   {"t":"cfg","c":<json>}   shards (resolved credentials) + options
+//                             {"t":"s"|"w","k":kind,"l":[raw watch line...]}  watch relay
+//                                (ncc/controller/relay.py): the controller cluster's objects
+//                             {"t":"go"}   warm standby acquired the Lease: start the workers
+//                             {"t":"cred","s":shard,"token":...}   refreshed exec credential
+//   executor -> coordinator   {"t":"synced","i":n}, {"t":"ready","i":n}
+//                             {"t":"report","k":key,"u":uid,"g":generation,"r":{shard:error|nil},"w":wrote}
+//                             {"t":"need","k":kind,"n":"ns/name"}   a referenced dependent not yet relayed
+//
+// Reconcile semantics are those of the Python executor role (ncc/controller/reconcile.py,
+// `_executor_sync_template`/`_sync_template_to_shard`/`_sync_dependent`, native options), which in
+// turn follow the reference's templateSyncHandler / syncSecretsToShard / syncConfigMapsToShard /
+// workgroupSyncHandler (controller.go:504-626, 697-845) with native-mode scheduling:
+//   * every shard concurrently, failures isolated per shard and reported;
+//   * the template first (its shard UID is needed for the dependents' ownerRefs), then all of its
+//     Secrets/ConfigMaps concurrently; one PUT per dependent (data + ownerRef together);
+//   * rogue shard objects (no ownerRefs) refused; Secret.type changes re-create the shard copy;
+//     ConfigMap.binaryData synced; 409 races resolved by re-reading the live object;
+//   * queued, retried deletes of templates/workgroups that left the controller cluster; an orphan
+//     sweep by the configuration-owner label; shard-side drift repaired from the shard watches.
+// The shard caches hold the *server's* answer to every write (never the request body), and a
+// per-object memo of "the version our last write produced and the spec/data it was meant to carry"
+// keeps a server that rewrites what we send (CRD defaulting, pruning, mutating webhooks) from
+// triggering a write loop.
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <csignal>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <set>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "http.hpp"
+#include "json.hpp"
+#include "loop.hpp"
+#include "msgpack.hpp"
+
+namespace ncc {
+
+// ------------------------------------------------------------------------------------ constants
+constexpr const char* kApiVersion = "science.sneaksanddata.com/v1";
+constexpr const char* kTemplateKind = "NexusAlgorithmTemplate";
+constexpr const char* kWorkgroupKind = "NexusAlgorithmWorkgroup";
+constexpr const char* kFieldManagerQuery = "?fieldManager=nexus-configuration-controller";
+constexpr const char* kLabelApp = "science.sneaksanddata.com/controller-app";
+constexpr const char* kLabelOwner = "science.sneaksanddata.com/configuration-owner";
+constexpr const char* kAgent = "nexus-configuration-controller";
+
+enum Kind { TEMPLATES = 0, WORKGROUPS = 1, SECRETS = 2, CONFIGMAPS = 3 };
+constexpr const char* kPlural[] = {"nexusalgorithmtemplates", "nexusalgorithmworkgroups", "secrets", "configmaps"};
+
+inline std::string base_path(int k, const std::string& ns) {
+    if (k < 2) return std::string("/apis/science.sneaksanddata.com/v1/namespaces/") + ns + "/" + kPlural[k];
+    return "/api/v1/namespaces/" + ns + "/" + kPlural[k];
+}
+inline std::string item_path(int k, const std::string& ns, const std::string& name) {
+    return base_path(k, ns) + "/" + name;
+}
+
+// crc32 (zlib) of "ns/name": the key -> partition map shared with ncc.controller.executor.key_part
+static uint32_t g_crc[256];
+static void crc_init() {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        g_crc[i] = c;
+    }
+}
+static uint32_t crc32(std::string_view s) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (unsigned char ch : s) c = g_crc[(c ^ ch) & 0xFF] ^ (c >> 8);
+    return c ^ 0xFFFFFFFFu;
+}
+
+struct Options {
+    int index = 0;
+    int part = 0, parts = 1;
+    std::string ns = "nexus";
+    std::string alias = "controller-cluster";
+    int workers = 256;
+    int pool_size = 64;
+    double request_timeout = 30;
+    double coalesce = 0.002;
+    double base_delay = 0.03, max_delay = 5.0;
+    double qps = 50, burst = 300;
+    double shard_sync_timeout = 10;
+    double full_resync = 600;
+    bool sync_binary_data = true;
+    bool sync_secret_type = true;
+    bool orphan_sweep = true;
+    bool propagate_workgroup_deletes = true;
+    int log_level = 30;  // Python logging levels
+    bool gated = false;
+};
+static Options g_opt;
+
+static void log_at(int level, const char* fmt, ...) {
+    if (level < g_opt.log_level) return;
+    char msg[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    std::string m;
+    write_string(m, msg);
+    const char* lv = level >= 40 ? "ERROR" : level >= 30 ? "WARNING" : level >= 20 ? "INFO" : "DEBUG";
+    std::fprintf(stderr, "{\"level\":\"%s\",\"logger\":\"ncc.executor.native\",\"executor\":%d,\"message\":%s}\n", lv,
+                 g_opt.index, m.c_str());
+    std::fflush(stderr);
+}
+#define LOG_ERROR(...) log_at(40, __VA_ARGS__)
+#define LOG_WARN(...) log_at(30, __VA_ARGS__)
+#define LOG_INFO(...) log_at(20, __VA_ARGS__)
+#define LOG_DEBUG(...) log_at(10, __VA_ARGS__)
+
+// A reconcile failure with the Python exception class name the reports carry.
+struct NamedError : std::runtime_error {
+    std::string kind;
+    NamedError(std::string k, const std::string& m) : std::runtime_error(m), kind(std::move(k)) {}
+};
+
+static std::string describe(const std::exception_ptr& ep) {
+    try {
+        std::rethrow_exception(ep);
+    } catch (const ApiError& e) {
+        return std::string(e.kind()) + ": " + e.what();
+    } catch (const NamedError& e) {
+        return e.kind + ": " + e.what();
+    } catch (const TransportError& e) {
+        return std::string("TransportError: ") + e.what();
+    } catch (const std::exception& e) {
+        return std::string("Error: ") + e.what();
+    } catch (...) {
+        return "Error: unknown";
+    }
+}
+
+// ------------------------------------------------------------------------------------ objects
+static const Value* meta_of(const Value& o) { return o.get("metadata"); }
+static std::string mget(const Value& o, std::string_view k) {
+    const Value* m = meta_of(o);
+    return m ? std::string(m->sget(k)) : std::string();
+}
+static long long rv_num(std::string_view rv) {
+    if (rv.empty()) return -1;
+    long long v = 0;
+    for (char c : rv) {
+        if (c < '0' || c > '9') return -1;
+        v = v * 10 + (c - '0');
+    }
+    return v;
+}
+static std::vector<std::string> template_owner_names(const Value& o) {
+    std::vector<std::string> out;
+    const Value* m = meta_of(o);
+    const Value* refs = m ? m->get("ownerReferences") : nullptr;
+    if (refs && refs->is_arr())
+        for (const auto& r : refs->a)
+            if (r.sget("kind") == kTemplateKind) out.emplace_back(r.sget("name"));
+    return out;
+}
+// GetSecretNames() / GetConfigMapNames(): spec.runtimeEnvironment.mappedEnvironmentVariables[*]
+static void dependent_names(const Value& tpl, std::vector<std::string>& secrets, std::vector<std::string>& cms) {
+    const Value* spec = tpl.get("spec");
+    const Value* rte = spec ? spec->get("runtimeEnvironment") : nullptr;
+    const Value* mev = rte ? rte->get("mappedEnvironmentVariables") : nullptr;
+    if (!mev || !mev->is_arr()) return;
+    for (const auto& ef : mev->a) {
+        if (!ef.is_obj()) continue;
+        const Value* s = ef.get("secretRef");
+        if (s && !s->is_null()) secrets.emplace_back(s->sget("name"));
+        const Value* c = ef.get("configMapRef");
+        if (c && !c->is_null()) cms.emplace_back(c->sget("name"));
+    }
+}
+
+// Controller-side object as relayed by the coordinator (immutable once stored).
+struct CtlObj {
+    Value obj;
+    std::string ns, name, uid, rv;
+    long long generation = 0;
+    bool has_generation = false;
+    uint64_t fp_spec = 0, fp_data = 0, fp_bin = 0, fp_labels = 0, fp_ann = 0;
+    std::string type;  // Secret.type ("" = Opaque)
+    std::vector<std::string> secrets, configmaps;  // templates
+    std::vector<std::string> owners;               // NexusAlgorithmTemplate owner names (dependents)
+};
+using CtlPtr = std::shared_ptr<const CtlObj>;
+
+static CtlPtr make_ctl(int kind, Value obj) {
+    auto c = std::make_shared<CtlObj>();
+    const Value* m = meta_of(obj);
+    if (m) {
+        c->ns = std::string(m->sget("namespace"));
+        c->name = std::string(m->sget("name"));
+        c->uid = std::string(m->sget("uid"));
+        c->rv = std::string(m->sget("resourceVersion"));
+        const Value* g = m->get("generation");
+        if (g && g->t == Value::NUM) {
+            c->generation = std::atoll(g->s.c_str());
+            c->has_generation = true;
+        }
+        c->fp_labels = fp_opt(m->get("labels"));
+        c->fp_ann = fp_opt(m->get("annotations"));
+    }
+    if (c->ns.empty()) c->ns = g_opt.ns;
+    if (kind < 2) {
+        const Value* spec = obj.get("spec");
+        c->fp_spec = spec ? fingerprint(*spec) : fingerprint(Value());
+        if (kind == TEMPLATES) dependent_names(obj, c->secrets, c->configmaps);
+    } else {
+        c->fp_data = fp_opt(obj.get("data"));
+        c->fp_bin = fp_opt(obj.get("binaryData"));
+        c->type = std::string(obj.sget("type"));
+        c->owners = template_owner_names(obj);
+    }
+    c->obj = std::move(obj);
+    return c;
+}
+
+// Slim shard-side object: everything but the payloads, plus their fingerprints.
+struct ShardObj {
+    Value rest;  // the object without spec/status/data/binaryData/stringData (re-sent on PUT)
+    std::string ns, name, uid;
+    long long rv = -1;
+    uint64_t fp_spec = 0, fp_data = 0, fp_bin = 0;
+    std::string type;
+    bool has_owner_refs = false;
+    std::vector<std::pair<std::string, std::string>> template_owners;  // (name, uid) of template owners
+    std::vector<std::string> all_owner_names;
+    std::string label_app, label_owner;
+};
+using ShardPtr = std::shared_ptr<const ShardObj>;
+
+static ShardPtr make_shard_obj(int kind, Value obj) {
+    auto s = std::make_shared<ShardObj>();
+    const Value* m = meta_of(obj);
+    if (m) {
+        s->ns = std::string(m->sget("namespace"));
+        s->name = std::string(m->sget("name"));
+        s->uid = std::string(m->sget("uid"));
+        s->rv = rv_num(m->sget("resourceVersion"));
+        const Value* refs = m->get("ownerReferences");
+        if (refs && refs->is_arr() && !refs->a.empty()) {
+            s->has_owner_refs = true;
+            for (const auto& r : refs->a) {
+                s->all_owner_names.emplace_back(r.sget("name"));
+                if (r.sget("kind") == kTemplateKind) s->template_owners.emplace_back(r.sget("name"), r.sget("uid"));
+            }
+        }
+        const Value* labels = m->get("labels");
+        if (labels) {
+            s->label_app = std::string(labels->sget(kLabelApp));
+            s->label_owner = std::string(labels->sget(kLabelOwner));
+        }
+    }
+    if (s->ns.empty()) s->ns = g_opt.ns;
+    if (kind < 2) {
+        const Value* spec = obj.get("spec");
+        s->fp_spec = spec ? fingerprint(*spec) : fingerprint(Value());
+        obj.erase("spec");
+        obj.erase("status");
+    } else {
+        s->fp_data = fp_opt(obj.get("data"));
+        s->fp_bin = fp_opt(obj.get("binaryData"));
+        s->type = std::string(obj.sget("type"));
+        obj.erase("data");
+        obj.erase("binaryData");
+        obj.erase("stringData");
+    }
+    s->rest = std::move(obj);
+    return s;
+}
+
+static bool is_ours(const ShardObj& s) { return s.label_owner == g_opt.alias && s.label_app == kAgent; }
+
+static std::string key_of(const std::string& ns, const std::string& name) { return ns + "/" + name; }
+static bool in_partition(const std::string& ns, const std::string& name) {
+    return g_opt.parts <= 1 || static_cast<int>(crc32(key_of(ns, name)) % g_opt.parts) == g_opt.part;
+}
+
+// ------------------------------------------------------------------------------------ channel
+class Channel {
+public:
+    explicit Channel(int fd) : fd_(fd) {
+        int fl = fcntl(fd_, F_GETFL);
+        fcntl(fd_, F_SETFL, fl | O_NONBLOCK);
+        loop().add_fd(fd_);
+        spawn(writer(), "channel writer");
+    }
+    // Queue one message (an encoded msgpack map); frames are coalesced per loop iteration.
+    void send(std::string msg) {
+        pending_.push_back(std::move(msg));
+        if (!flush_scheduled_) {
+            flush_scheduled_ = true;
+            loop().call_soon([this] { flush(); });
+        }
+    }
+    bool closed() const { return closed_; }
+
+    // Next batch of messages; empty on EOF.
+    Task<std::vector<mp::Obj>> recv() {
+        while (true) {
+            if (in_.size() - pos_ >= 4) {
+                const unsigned char* p = reinterpret_cast<const unsigned char*>(in_.data() + pos_);
+                uint32_t n = (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3];
+                bool batch = (n & 0x80000000u) != 0;
+                n &= 0x7FFFFFFFu;
+                if (in_.size() - pos_ >= 4 + n) {
+                    std::string body = in_.substr(pos_ + 4, n);
+                    pos_ += 4 + n;
+                    if (pos_ > (1 << 20)) {
+                        in_.erase(0, pos_);
+                        pos_ = 0;
+                    }
+                    mp::Obj o = mp::decode(body);
+                    std::vector<mp::Obj> out;
+                    if (batch && o.t == mp::Obj::ARR)
+                        out = std::move(o.a);
+                    else
+                        out.push_back(std::move(o));
+                    co_return out;
+                }
+            }
+            char buf[1 << 16];
+            ssize_t r = ::recv(fd_, buf, sizeof buf, 0);
+            if (r > 0) {
+                in_.append(buf, static_cast<size_t>(r));
+                continue;
+            }
+            if (r == 0) {
+                closed_ = true;
+                co_return std::vector<mp::Obj>{};
+            }
+            if (errno == EAGAIN || errno == EWOULDBLOCK) {
+                co_await loop().readable(fd_);
+                continue;
+            }
+            if (errno == EINTR) continue;
+            closed_ = true;
+            co_return std::vector<mp::Obj>{};
+        }
+    }
+
+    // Write out everything queued (bounded wait) — used before exiting.
+    Task<void> drain(double timeout) {
+        flush();
+        double end = now_s() + timeout;
+        while (!out_.empty() && !closed_ && now_s() < end) co_await loop().sleep(0.005);
+    }
+
+private:
+    int fd_;
+    bool closed_ = false;
+    bool flush_scheduled_ = false;
+    std::vector<std::string> pending_;
+    std::string in_;
+    size_t pos_ = 0;
+    std::string out_;
+    Event has_out_;
+
+    void flush() {
+        flush_scheduled_ = false;
+        if (pending_.empty()) return;
+        std::string body;
+        bool batch = pending_.size() > 1;
+        if (batch) {
+            mp::Encoder e;
+            e.array(pending_.size());
+            body = std::move(e.out);
+            for (auto& m : pending_) body += m;
+        } else {
+            body = std::move(pending_[0]);
+        }
+        pending_.clear();
+        uint32_t n = static_cast<uint32_t>(body.size()) | (batch ? 0x80000000u : 0u);
+        char hdr[4] = {static_cast<char>(n >> 24), static_cast<char>(n >> 16), static_cast<char>(n >> 8),
+                       static_cast<char>(n)};
+        out_.append(hdr, 4);
+        out_ += body;
+        has_out_.set();
+    }
+
+    Task<void> writer() {
+        size_t off = 0;
+        while (true) {
+            if (off >= out_.size()) {
+                out_.clear();
+                off = 0;
+                has_out_.clear();
+                co_await has_out_.wait();
+                continue;
+            }
+            ssize_t r = ::send(fd_, out_.data() + off, out_.size() - off, MSG_NOSIGNAL);
+            if (r > 0) {
+                off += static_cast<size_t>(r);
+                if (off > (1 << 20)) {
+                    out_.erase(0, off);
+                    off = 0;
+                }
+                continue;
+            }
+            if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+                co_await loop().writable(fd_);
+                continue;
+            }
+            if (r < 0 && errno == EINTR) continue;
+            closed_ = true;
+            out_.clear();
+            co_return;
+        }
+    }
+};
+static Channel* g_chan = nullptr;
+
+static void send_simple(const char* t) {
+    mp::Encoder e;
+    e.map(2);
+    e.str("t");
+    e.str(t);
+    e.str("i");
+    e.integer(g_opt.index);
+    g_chan->send(std::move(e.out));
+}
+
+// ------------------------------------------------------------------------------------ work queue
+// client-go's rate-limiting queue semantics (as ncc/workqueue + native/ncc_native.cpp RateLimitingQueue):
+// dedup of queued keys, a key is never processed twice at once (re-added keys wait for `done`),
+// delayed adds, per-key exponential failure backoff max'ed with a token bucket for AddRateLimited.
+class WorkQueue {
+public:
+    void add(const std::string& key) {
+        if (shutdown_) return;
+        if (dirty_.count(key)) return;
+        dirty_.insert(key);
+        if (processing_.count(key)) return;
+        queue_.push_back(key);
+        wake();
+    }
+    void add_after(const std::string& key, double delay) {
+        if (shutdown_) return;
+        if (delay <= 0) {
+            add(key);
+            return;
+        }
+        double at = now_s() + delay;
+        auto it = waiting_.find(key);
+        if (it != waiting_.end() && it->second <= at) return;
+        waiting_[key] = at;
+        spawn(delayed(key, at), "delayed add");
+    }
+    void add_rate_limited(const std::string& key) {
+        int f = failures_[key]++;
+        double exp_delay = std::min(g_opt.base_delay * std::pow(2.0, f), g_opt.max_delay);
+        double now = now_s();
+        tokens_ = std::min(g_opt.burst, tokens_ + (now - last_) * g_opt.qps);
+        last_ = now;
+        tokens_ -= 1.0;
+        double bucket = tokens_ < 0 ? -tokens_ / g_opt.qps : 0.0;
+        add_after(key, std::max(exp_delay, bucket));
+    }
+    void forget(const std::string& key) { failures_.erase(key); }
+    void done(const std::string& key) {
+        processing_.erase(key);
+        if (dirty_.count(key)) {
+            queue_.push_back(key);
+            wake();
+        }
+    }
+    size_t length() const { return queue_.size(); }
+    void shutdown() {
+        shutdown_ = true;
+        for (auto h : getters_) loop().post(h);
+        getters_.clear();
+    }
+
+    struct GetAwait {
+        WorkQueue* q;
+        bool await_ready() { return !q->queue_.empty() || q->shutdown_; }
+        void await_suspend(std::coroutine_handle<> h) { q->getters_.push_back(h); }
+        void await_resume() {}
+    };
+    // Next key to process ("" after shutdown).
+    Task<std::string> get() {
+        while (queue_.empty() && !shutdown_) co_await GetAwait{this};
+        if (shutdown_) co_return std::string();
+        std::string k = std::move(queue_.front());
+        queue_.pop_front();
+        processing_.insert(k);
+        dirty_.erase(k);
+        co_return k;
+    }
+
+private:
+    std::deque<std::string> queue_;
+    std::unordered_set<std::string> dirty_, processing_;
+    std::unordered_map<std::string, double> waiting_;
+    std::unordered_map<std::string, int> failures_;
+    std::deque<std::coroutine_handle<>> getters_;
+    double tokens_ = 300, last_ = now_s();
+    bool shutdown_ = false;
+
+    void wake() {
+        if (!getters_.empty()) {
+            loop().post(getters_.front());
+            getters_.pop_front();
+        }
+    }
+    Task<void> delayed(std::string key, double at) {
+        co_await loop().sleep(std::max(0.0, at - now_s()));
+        auto it = waiting_.find(key);
+        if (it == waiting_.end() || it->second > at + 1e-9) co_return;  // superseded by an earlier/later add
+        waiting_.erase(it);
+        add(key);
+    }
+};
+
+// ------------------------------------------------------------------------------------ state
+struct Shard;
+struct Executor;
+static Executor* g_ex = nullptr;
+
+struct Informer {
+    Shard* shard = nullptr;
+    int kind = 0;
+    std::unordered_map<std::string, ShardPtr> store;
+    bool synced = false;
+    Event synced_ev;
+    std::string last_rv;
+    long long events = 0, relists = 0;
+};
+
+struct Memo {  // the version our last write produced, and the fingerprints it was meant to carry
+    long long rv = -1;
+    uint64_t fp_a = 0, fp_b = 0;
+};
+
+struct Shard {
+    std::string name;
+    std::unique_ptr<Client> client;
+    Informer inf[4];
+    std::unordered_map<std::string, Memo> memo[4];
+    bool synced() const {
+        for (const auto& i : inf)
+            if (!i.synced) return false;
+        return true;
+    }
+    ShardPtr get(int k, const std::string& key) const {
+        auto it = inf[k].store.find(key);
+        return it == inf[k].store.end() ? nullptr : it->second;
+    }
+};
+
+struct PassState {
+    bool wrote = false;
+};
+
+static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const ShardPtr& cur, bool deleted);
+static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool deleted);
+
+struct Executor {
+    std::vector<std::unique_ptr<Shard>> shards;
+    std::unordered_map<std::string, CtlPtr> ctl[4];
+    bool ctl_synced[4] = {false, false, false, false};
+    Event ctl_synced_ev;
+    std::unordered_map<std::string, std::set<std::string>> refs[2];  // dep key -> template keys (secret, configmap)
+    std::unordered_set<std::string> pending_deletes[2];              // templates, workgroups
+    WorkQueue queue;
+    Event gate;
+    Event stop_ev;
+    std::unordered_map<std::string, double> needed;  // dependent keys asked from the coordinator
+    long long stats_reconciles = 0, stats_errors = 0, stats_writes = 0;
+
+    CtlPtr cget(int k, const std::string& key) const {
+        auto it = ctl[k].find(key);
+        return it == ctl[k].end() ? nullptr : it->second;
+    }
+
+    void enqueue(int kind, const std::string& ns, const std::string& name) {
+        if (!in_partition(ns, name)) return;
+        std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
+        if (g_opt.coalesce > 0)
+            queue.add_after(key, g_opt.coalesce);
+        else
+            queue.add(key);
+    }
+};
+
+// ------------------------------------------------------------------------------------ controller side
+static void index_template(const CtlPtr& old, const CtlPtr& cur) {
+    Executor& ex = *g_ex;
+    const CtlObj* o = old.get();
+    const CtlObj* c = cur.get();
+    const CtlObj* any = c ? c : o;
+    std::string tkey = key_of(any->ns, any->name);
+    for (int i = 0; i < 2; ++i) {
+        const std::vector<std::string>* ov = o ? (i == 0 ? &o->secrets : &o->configmaps) : nullptr;
+        const std::vector<std::string>* nv = c ? (i == 0 ? &c->secrets : &c->configmaps) : nullptr;
+        if (ov && nv && *ov == *nv) continue;
+        if (ov)
+            for (const auto& n : *ov) {
+                auto it = ex.refs[i].find(key_of(any->ns, n));
+                if (it != ex.refs[i].end()) {
+                    it->second.erase(tkey);
+                    if (it->second.empty()) ex.refs[i].erase(it);
+                }
+            }
+        if (nv)
+            for (const auto& n : *nv) ex.refs[i][key_of(any->ns, n)].insert(tkey);
+    }
+}
+
+// Apply one relayed controller-side event.
+static void ctl_apply(int kind, const std::string& type, Value obj) {
+    Executor& ex = *g_ex;
+    CtlPtr cur = make_ctl(kind, std::move(obj));
+    std::string key = key_of(cur->ns, cur->name);
+    auto& store = ex.ctl[kind];
+    auto it = store.find(key);
+    CtlPtr old = it == store.end() ? nullptr : it->second;
+    if (type == "DELETED") {
+        if (it != store.end()) store.erase(it);
+        if (kind == TEMPLATES) index_template(old ? old : cur, nullptr);
+        on_ctl_event(kind, old ? old : cur, nullptr, true);
+        return;
+    }
+    store[key] = cur;
+    if (kind == TEMPLATES) index_template(old, cur);
+    if (kind >= 2) ex.needed.erase(key);
+    on_ctl_event(kind, old, cur, false);
+}
+
+static void ctl_snapshot(int kind, std::vector<Value> objs) {
+    Executor& ex = *g_ex;
+    auto& store = ex.ctl[kind];
+    std::unordered_map<std::string, CtlPtr> fresh;
+    for (auto& o : objs) {
+        CtlPtr c = make_ctl(kind, std::move(o));
+        fresh[key_of(c->ns, c->name)] = c;
+    }
+    bool was_synced = ex.ctl_synced[kind];
+    std::vector<std::pair<CtlPtr, CtlPtr>> changes;  // (old, new); new null = deleted
+    for (auto& kv : fresh) {
+        auto it = store.find(kv.first);
+        changes.emplace_back(it == store.end() ? nullptr : it->second, kv.second);
+    }
+    for (auto& kv : store)
+        if (!fresh.count(kv.first)) changes.emplace_back(kv.second, nullptr);
+    store = std::move(fresh);
+    if (kind == TEMPLATES) {
+        ex.refs[0].clear();
+        ex.refs[1].clear();
+        for (auto& kv : store) index_template(nullptr, kv.second);
+    }
+    ex.ctl_synced[kind] = true;
+    for (auto& ch : changes) {
+        if (ch.second)
+            on_ctl_event(kind, ch.first, ch.second, false);
+        else if (was_synced)
+            on_ctl_event(kind, ch.first, nullptr, true);
+    }
+    if (ex.ctl_synced[0] && ex.ctl_synced[1] && ex.ctl_synced[2] && ex.ctl_synced[3]) ex.ctl_synced_ev.set();
+}
+
+// templates referencing the dependent, then template owners that no longer reference it
+// (handleObject's ownerRef walk, controller.go:206-223; native: reverse index first)
+static void on_dependent(int kind, const CtlObj& obj) {
+    Executor& ex = *g_ex;
+    std::set<std::string> seen;
+    auto it = ex.refs[kind == SECRETS ? 0 : 1].find(key_of(obj.ns, obj.name));
+    if (it != ex.refs[kind == SECRETS ? 0 : 1].end()) {
+        for (const auto& tkey : it->second) {
+            std::string tname = tkey.substr(tkey.find('/') + 1);
+            seen.insert(tname);
+            ex.enqueue(TEMPLATES, obj.ns, tname);
+        }
+    }
+    for (const auto& owner : obj.owners) {
+        if (seen.count(owner)) continue;
+        if (!ex.cget(TEMPLATES, key_of(obj.ns, owner))) return;  // stops at the first orphaned owner
+        ex.enqueue(TEMPLATES, obj.ns, owner);
+    }
+}
+
+static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool deleted) {
+    Executor& ex = *g_ex;
+    if (kind == TEMPLATES || kind == WORKGROUPS) {
+        const CtlObj& o = deleted ? *old : *cur;
+        if (deleted) {
+            if (kind == TEMPLATES || g_opt.propagate_workgroup_deletes) {
+                if (in_partition(o.ns, o.name)) ex.pending_deletes[kind].insert(key_of(o.ns, o.name));
+                ex.enqueue(kind, o.ns, o.name);
+            }
+            return;
+        }
+        if (old) {  // generation filter: skip resyncs and status-only changes (our coordinator's writes)
+            if (old->rv == cur->rv) return;
+            if (old->has_generation && old->generation == cur->generation && old->fp_labels == cur->fp_labels &&
+                old->fp_ann == cur->fp_ann && old->fp_spec == cur->fp_spec)
+                return;
+        }
+        ex.enqueue(kind, o.ns, o.name);
+        return;
+    }
+    if (deleted || !old) {
+        on_dependent(kind, deleted ? *old : *cur);
+        return;
+    }
+    if (old->rv == cur->rv) return;
+    if (old->fp_data == cur->fp_data && old->fp_bin == cur->fp_bin && old->type == cur->type &&
+        old->owners == cur->owners)
+        return;  // e.g. the coordinator's adoption write: ownerRef UIDs changed, payload did not
+    on_dependent(kind, *cur);
+}
+
+// ------------------------------------------------------------------------------------ shard side
+static bool spec_in_sync(const Shard& sh, int kind, const ShardObj& so, uint64_t desired) {
+    if (so.fp_spec == desired) return true;
+    auto it = sh.memo[kind].find(key_of(so.ns, so.name));
+    // the server rewrote what we sent (defaulting / pruning / a mutating webhook): the version our own
+    // write produced counts as in sync, or every pass would write again
+    return it != sh.memo[kind].end() && it->second.rv == so.rv && it->second.fp_a == desired;
+}
+static bool data_in_sync(const Shard& sh, int kind, const ShardObj& so, const CtlObj& src) {
+    bool with_bin = kind == CONFIGMAPS && g_opt.sync_binary_data;
+    if (so.fp_data == src.fp_data && (!with_bin || so.fp_bin == src.fp_bin)) return true;
+    auto it = sh.memo[kind].find(key_of(so.ns, so.name));
+    return it != sh.memo[kind].end() && it->second.rv == so.rv && it->second.fp_a == src.fp_data &&
+           (!with_bin || it->second.fp_b == src.fp_bin);
+}
+
+static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const ShardPtr& cur, bool deleted) {
+    Executor& ex = *g_ex;
+    if (!deleted && !old) return;  // adds are not drift (the reference only repairs on update/delete)
+    const ShardObj& o = deleted ? *old : *cur;
+    if (kind == TEMPLATES || kind == WORKGROUPS) {
+        CtlPtr c = ex.cget(kind, key_of(o.ns, o.name));
+        if (!c) return;
+        if (deleted || !spec_in_sync(sh, kind, o, c->fp_spec)) ex.enqueue(kind, o.ns, o.name);
+        return;
+    }
+    CtlPtr src = ex.cget(kind, key_of(o.ns, o.name));
+    if (!src) return;
+    if (!deleted && data_in_sync(sh, kind, o, *src)) return;
+    std::vector<std::string> owners;
+    for (const auto& p : o.template_owners) owners.push_back(p.first);
+    if (owners.empty()) owners = src->owners;
+    for (const auto& n : owners)
+        if (ex.cget(TEMPLATES, key_of(o.ns, n))) ex.enqueue(TEMPLATES, o.ns, n);
+}
+
+// Keep a shard object in this executor's cache?  Templates/workgroups of our key partition; dependents
+// without owners or with an owner template in our partition (others' are dropped, as in the Python
+// executor's partition filters).
+static bool wanted(int kind, const ShardObj& s) {
+    if (g_opt.parts <= 1) return true;
+    if (kind < 2) return in_partition(s.ns, s.name);
+    if (s.all_owner_names.empty()) return true;
+    for (const auto& n : s.all_owner_names)
+        if (in_partition(s.ns, n)) return true;
+    return false;
+}
+
+// Store a shard object version unless we already hold a newer one (our write's response and its watch
+// echo arrive in either order).
+static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch) {
+    Informer& inf = sh.inf[kind];
+    std::string key = key_of(so->ns, so->name);
+    auto it = inf.store.find(key);
+    ShardPtr old = it == inf.store.end() ? nullptr : it->second;
+    if (old && so->rv >= 0 && old->rv >= so->rv) return;
+    if (!wanted(kind, *so)) {
+        if (old) inf.store.erase(it);
+        return;
+    }
+    inf.store[key] = so;
+    if (dispatch) on_shard_event(sh, kind, old, so, false);
+}
+
+static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
+    Value ev = parse(line);
+    std::string type(ev.sget("type"));
+    Value* obj = ev.get("object");
+    if (obj == nullptr) return;
+    Informer& inf = sh.inf[kind];
+    ++inf.events;
+    if (type == "ERROR") {
+        std::string body = dumps(*obj);
+        ApiError e = api_error(200, body);
+        throw e;
+    }
+    std::string rv = mget(*obj, "resourceVersion");
+    if (type == "BOOKMARK") {
+        if (!rv.empty()) inf.last_rv = rv;
+        return;
+    }
+    ShardPtr so = make_shard_obj(kind, std::move(*obj));
+    if (!rv.empty()) inf.last_rv = rv;
+    if (type == "DELETED") {
+        std::string key = key_of(so->ns, so->name);
+        auto it = inf.store.find(key);
+        if (it == inf.store.end()) return;
+        ShardPtr old = it->second;
+        inf.store.erase(it);
+        on_shard_event(sh, kind, old, nullptr, true);
+        return;
+    }
+    shard_upsert(sh, kind, so, true);
+}
+
+static Task<void> shard_list(Shard& sh, int kind, std::string list_rv) {
+    Informer& inf = sh.inf[kind];
+    std::unordered_map<std::string, ShardPtr> fresh;
+    std::string token, rv;
+    bool first = true;
+    while (true) {
+        std::string target = base_path(kind, g_opt.ns) + "?limit=500";
+        if (first && !list_rv.empty()) target += "&resourceVersion=" + list_rv;
+        if (!token.empty()) target += "&continue=" + token;
+        first = false;
+        Response r = co_await sh.client->request("GET", target, nullptr);
+        if (r.status >= 300) throw api_error(r.status, r.body);
+        Value lst = parse(r.body);
+        Value* items = lst.get("items");
+        if (items && items->is_arr())
+            for (auto& it : items->a) {
+                ShardPtr so = make_shard_obj(kind, std::move(it));
+                if (wanted(kind, *so)) fresh[key_of(so->ns, so->name)] = so;
+            }
+        const Value* lm = lst.get("metadata");
+        rv = lm ? std::string(lm->sget("resourceVersion")) : rv;
+        token = lm ? std::string(lm->sget("continue")) : std::string();
+        if (token.empty()) break;
+    }
+    bool was_synced = inf.synced;
+    std::vector<std::pair<ShardPtr, ShardPtr>> changes;
+    for (auto& kv : fresh) {
+        auto it = inf.store.find(kv.first);
+        if (it != inf.store.end()) changes.emplace_back(it->second, kv.second);
+    }
+    std::vector<ShardPtr> gone;
+    for (auto& kv : inf.store)
+        if (!fresh.count(kv.first)) gone.push_back(kv.second);
+    inf.store = std::move(fresh);
+    inf.last_rv = rv;
+    ++inf.relists;
+    inf.synced = true;
+    inf.synced_ev.set();
+    for (auto& ch : changes) on_shard_event(sh, kind, ch.first, ch.second, false);
+    if (was_synced)
+        for (auto& g : gone) on_shard_event(sh, kind, g, nullptr, true);
+}
+
+static std::mt19937_64 g_rng(12345);
+static double jitter() { return std::uniform_real_distribution<double>(0.0, 1.0)(g_rng); }
+
+static Task<void> shard_watch(Shard& sh, int kind) {
+    Informer& inf = sh.inf[kind];
+    int timeout = 300 + static_cast<int>(jitter() * 300);
+    std::string target = base_path(kind, g_opt.ns) + "?watch=1&resourceVersion=" + inf.last_rv +
+                         "&timeoutSeconds=" + std::to_string(timeout) + "&allowWatchBookmarks=true";
+    co_await sh.client->stream(
+        target,
+        [&sh, kind](std::vector<std::string>& lines) {
+            for (const auto& l : lines) shard_apply_line(sh, kind, l);
+        },
+        timeout + 30.0);
+}
+
+// Reflector loop (list -> watch -> re-watch; 410 -> consistent relist; errors back off 0.8 s..30 s).
+static Task<void> shard_informer(Shard* shp, int kind) {
+    Shard& sh = *shp;
+    double backoff = 0.8;
+    bool need_list = true;
+    std::string list_rv = "0";
+    while (!g_ex->stop_ev.is_set()) {
+        bool gone = false, transport = false, failed = false;
+        std::string err;
+        try {
+            if (need_list) {
+                co_await shard_list(sh, kind, list_rv);
+                need_list = false;
+            }
+            co_await shard_watch(sh, kind);
+            backoff = 0.8;
+        } catch (const ApiError& e) {
+            if (e.code == 410) {
+                gone = true;
+            } else {
+                failed = true;
+                err = describe(std::current_exception());
+            }
+        } catch (const TransportError& e) {
+            failed = transport = true;
+            err = e.what();
+        } catch (const std::exception& e) {
+            failed = true;
+            err = e.what();
+        }
+        if (gone) {
+            need_list = true;
+            list_rv = "";
+            continue;
+        }
+        if (failed) {
+            LOG_DEBUG("shard %s %s: list/watch failed: %s; retry in %.2fs", sh.name.c_str(), kPlural[kind],
+                      err.c_str(), backoff);
+            co_await loop().sleep(backoff * (1 + jitter() * 0.2));
+            backoff = std::min(backoff * 2, 30.0);
+            if (!transport) {
+                need_list = true;
+                list_rv = sh.inf[kind].last_rv.empty() ? "0" : sh.inf[kind].last_rv;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ writes
+static Value owner_labels() {
+    Value l = Value::object();
+    l.set(kLabelApp, Value::str(kAgent));
+    l.set(kLabelOwner, Value::str(g_opt.alias));
+    return l;
+}
+static Value owner_ref(const std::string& name, const std::string& uid) {
+    Value r = Value::object();
+    r.set("apiVersion", Value::str(kApiVersion));
+    r.set("kind", Value::str(kTemplateKind));
+    r.set("name", Value::str(name));
+    r.set("uid", Value::str(uid));
+    return r;
+}
+
+// One write; the server's answer goes into the cache (and the memo of what we meant to write).
+static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const std::string& ns,
+                                  const std::string& name, const Value& body, PassState* pass, uint64_t want_a,
+                                  uint64_t want_b) {
+    pass->wrote = true;
+    ++g_ex->stats_writes;
+    std::string target =
+        (std::string(method) == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) + kFieldManagerQuery;
+    std::string data = dumps(body);
+    Response r = co_await sh.client->request(method, target, &data);
+    if (r.status >= 300) throw api_error(r.status, r.body);
+    ShardPtr so = make_shard_obj(kind, parse(r.body));
+    sh.memo[kind][key_of(so->ns, so->name)] = Memo{so->rv, want_a, want_b};
+    shard_upsert(sh, kind, so, false);
+    co_return so;
+}
+
+static Task<ShardPtr> shard_get_live(Shard& sh, int kind, const std::string& ns, const std::string& name) {
+    Response r = co_await sh.client->request("GET", item_path(kind, ns, name), nullptr);
+    if (r.status >= 300) throw api_error(r.status, r.body);
+    ShardPtr so = make_shard_obj(kind, parse(r.body));
+    shard_upsert(sh, kind, so, false);
+    co_return so;
+}
+
+static Task<void> shard_delete(Shard& sh, int kind, const std::string& ns, const std::string& name) {
+    Response r = co_await sh.client->request("DELETE", item_path(kind, ns, name), nullptr);
+    if (r.status >= 300 && r.status != 404) throw api_error(r.status, r.body);
+}
+
+// create-or-update of a template/workgroup (native `_write`: AlreadyExists/Conflict -> re-read the live
+// object; a Conflict on update is retried once from it)
+static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj& want, PassState* pass) {
+    const Value* spec = want.obj.get("spec");
+    bool update = cur != nullptr;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        Value body;
+        if (update) {
+            body = cur->rest;
+        } else {
+            body = Value::object();
+            body.set("apiVersion", Value::str(kApiVersion));
+            body.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
+            Value m = Value::object();
+            m.set("name", Value::str(want.name));
+            m.set("namespace", Value::str(want.ns));
+            m.set("labels", owner_labels());
+            body.set("metadata", std::move(m));
+        }
+        body.set("spec", spec ? *spec : Value());
+        bool race = false, exists = false;
+        try {
+            co_return co_await shard_write(sh, kind, update ? "PUT" : "POST", want.ns, want.name, body, pass,
+                                           want.fp_spec, 0);
+        } catch (const ApiError& e) {
+            if (e.conflict() || e.already_exists()) {
+                race = true;
+                exists = e.already_exists();
+            } else {
+                throw;
+            }
+        }
+        if (!race) break;
+        ShardPtr live = co_await shard_get_live(sh, kind, want.ns, want.name);
+        if (exists || attempt == 1) co_return live;
+        cur = live;  // Conflict on update: once more from the live version
+    }
+    co_return cur;
+}
+
+static Task<void> sync_dependent(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep, PassState* pass) {
+    Shard& sh = *shp;
+    Executor& ex = *g_ex;
+    CtlPtr src = ex.cget(kind, key_of(tpl->ns, dep));
+    if (!src) throw ApiError(404, "NotFound", std::string(kPlural[kind]) + " \"" + dep + "\" not found");
+    const std::string& shard_ns = st->ns;
+    bool is_secret = kind == SECRETS;
+    bool with_bin = !is_secret && g_opt.sync_binary_data;
+    ShardPtr so = sh.get(kind, key_of(shard_ns, dep));
+    auto create_body = [&]() {
+        Value body = Value::object();
+        body.set("apiVersion", Value::str("v1"));
+        body.set("kind", Value::str(is_secret ? "Secret" : "ConfigMap"));
+        Value m = Value::object();
+        m.set("name", Value::str(dep));
+        m.set("namespace", Value::str(shard_ns));
+        m.set("labels", owner_labels());
+        Value refs = Value::array();
+        refs.a.push_back(owner_ref(st->name, st->uid));
+        m.set("ownerReferences", std::move(refs));
+        body.set("metadata", std::move(m));
+        const Value* data = src->obj.get("data");
+        if (data && !data->is_null()) body.set("data", *data);
+        if (is_secret) {
+            if (!src->type.empty()) body.set("type", Value::str(src->type));
+        } else if (with_bin) {
+            const Value* bin = src->obj.get("binaryData");
+            if (bin && !bin->is_null()) body.set("binaryData", *bin);
+        }
+        return body;
+    };
+    auto create = [&]() -> Task<ShardPtr> {
+        bool exists = false;
+        try {
+            co_return co_await shard_write(sh, kind, "POST", shard_ns, dep, create_body(), pass, src->fp_data,
+                                           src->fp_bin);
+        } catch (const ApiError& e) {
+            if (!e.already_exists()) throw;
+            exists = true;
+        }
+        (void)exists;
+        co_return co_await shard_get_live(sh, kind, shard_ns, dep);
+    };
+    if (!so) so = co_await create();
+    // isMissingOwnership (controller.go:482-502): no ownerRefs at all = a rogue object we refuse to touch
+    if (!so->has_owner_refs)
+        throw NamedError("RogueResourceError", "Resource \"" + dep +
+                                                   "\" already exists and is not managed by any Machine "
+                                                   "Learning Algorithm");
+    bool missing_owner = true;
+    for (const auto& o : so->template_owners)
+        if (o.second == st->uid) missing_owner = false;
+    if (is_secret && g_opt.sync_secret_type &&
+        (src->type.empty() ? std::string("Opaque") : src->type) != (so->type.empty() ? std::string("Opaque") : so->type)) {
+        // Secret.type is immutable: replace the shard copy (other owners re-add their refs on their passes)
+        pass->wrote = true;
+        co_await shard_delete(sh, kind, shard_ns, dep);
+        sh.inf[kind].store.erase(key_of(shard_ns, dep));
+        co_await create();
+        co_return;
+    }
+    bool differs = !data_in_sync(sh, kind, *so, *src);
+    if (!differs && !missing_owner) co_return;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        Value body = so->rest;
+        const Value* data = src->obj.get("data");
+        body.set("data", (data && !data->is_null()) ? *data : Value::object());
+        if (with_bin) {
+            const Value* bin = src->obj.get("binaryData");
+            if (bin && !bin->is_null() && !bin->empty_container())
+                body.set("binaryData", *bin);
+            else
+                body.erase("binaryData");
+        }
+        if (missing_owner) {
+            Value* m = body.get("metadata");
+            if (m == nullptr) m = &body.set("metadata", Value::object());
+            Value* refs = m->get("ownerReferences");
+            if (refs == nullptr || !refs->is_arr()) refs = &m->set("ownerReferences", Value::array());
+            refs->a.push_back(owner_ref(st->name, st->uid));
+        }
+        bool conflict = false;
+        try {
+            co_await shard_write(sh, kind, "PUT", shard_ns, dep, body, pass, src->fp_data, src->fp_bin);
+            co_return;
+        } catch (const ApiError& e) {
+            if (!e.conflict() || attempt == 1) throw;
+            conflict = true;
+        }
+        if (conflict) {
+            so = co_await shard_get_live(sh, kind, shard_ns, dep);
+            missing_owner = true;
+            for (const auto& o : so->template_owners)
+                if (o.second == st->uid) missing_owner = false;
+            if (!so->has_owner_refs) throw NamedError("RogueResourceError", "Resource \"" + dep + "\" lost its owners");
+            if (data_in_sync(sh, kind, *so, *src) && !missing_owner) co_return;
+        }
+    }
+}
+
+static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass) {
+    Shard& sh = *shp;
+    if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
+    std::string key = key_of(tpl->ns, tpl->name);
+    ShardPtr st = sh.get(TEMPLATES, key);
+    if (!st || !spec_in_sync(sh, TEMPLATES, *st, tpl->fp_spec)) st = co_await write_crd(sh, TEMPLATES, st, *tpl, pass);
+    std::vector<Task<void>> jobs;
+    for (const auto& n : tpl->secrets) jobs.push_back(sync_dependent(shp, SECRETS, tpl, st, n, pass));
+    for (const auto& n : tpl->configmaps) jobs.push_back(sync_dependent(shp, CONFIGMAPS, tpl, st, n, pass));
+    auto errs = co_await when_all(std::move(jobs));
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+}
+
+static Task<void> sync_workgroup_to_shard(Shard* shp, CtlPtr wg, PassState* pass) {
+    Shard& sh = *shp;
+    if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
+    ShardPtr sw = sh.get(WORKGROUPS, key_of(wg->ns, wg->name));
+    if (!sw || !spec_in_sync(sh, WORKGROUPS, *sw, wg->fp_spec)) co_await write_crd(sh, WORKGROUPS, sw, *wg, pass);
+}
+
+static void report(const std::string& key, const CtlObj& obj, const std::vector<std::pair<std::string, std::string>>& results,
+                   bool wrote) {
+    mp::Encoder e;
+    e.map(6);
+    e.str("t");
+    e.str("report");
+    e.str("k");
+    e.str(key);
+    e.str("u");
+    e.str(obj.uid);
+    e.str("g");
+    e.integer(obj.generation);
+    e.str("r");
+    e.map(results.size());
+    for (const auto& r : results) {
+        e.str(r.first);
+        if (r.second.empty())
+            e.nil();
+        else
+            e.str(r.second.substr(0, 500));
+    }
+    e.str("w");
+    e.boolean(wrote);
+    g_chan->send(std::move(e.out));
+}
+
+static void ask_coordinator(int kind, const std::string& key) {
+    Executor& ex = *g_ex;
+    double now = now_s();
+    auto it = ex.needed.find(key);
+    if (it != ex.needed.end() && now - it->second < 1.0) return;
+    ex.needed[key] = now;
+    mp::Encoder e;
+    e.map(3);
+    e.str("t");
+    e.str("need");
+    e.str("k");
+    e.integer(kind);
+    e.str("n");
+    e.str(key);
+    g_chan->send(std::move(e.out));
+}
+
+static Task<void> propagate_delete(int kind, std::string ns, std::string name) {
+    Executor& ex = *g_ex;
+    std::string key = key_of(ns, name);
+    bool explicit_ = ex.pending_deletes[kind].count(key) > 0;
+    std::vector<Task<void>> jobs;
+    for (auto& sp : ex.shards) {
+        Shard& sh = *sp;
+        ShardPtr so = sh.get(kind, key);
+        if (!so) continue;
+        if (!explicit_ && !is_ours(*so)) continue;
+        if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
+        jobs.push_back(shard_delete(sh, kind, ns, name));
+    }
+    auto errs = co_await when_all(std::move(jobs));
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+    ex.pending_deletes[kind].erase(key);
+}
+
+static Task<void> sync_object(int kind, std::string ns, std::string name) {
+    Executor& ex = *g_ex;
+    std::string key = key_of(ns, name);
+    CtlPtr obj = ex.cget(kind, key);
+    if (!obj) {
+        if (kind == TEMPLATES || g_opt.propagate_workgroup_deletes) co_await propagate_delete(kind, ns, name);
+        co_return;
+    }
+    if (kind == TEMPLATES) {
+        // the coordinator adopts; an executor only refuses to write while a reference is missing
+        for (int k = SECRETS; k <= CONFIGMAPS; ++k)
+            for (const auto& n : (k == SECRETS ? obj->secrets : obj->configmaps)) {
+                std::string dk = key_of(ns, n);
+                if (!ex.cget(k, dk)) {
+                    ask_coordinator(k, dk);
+                    throw ApiError(404, "NotFound", std::string(kPlural[k]) + " \"" + n + "\" not found");
+                }
+            }
+    }
+    PassState pass;
+    std::vector<Task<void>> jobs;
+    for (auto& sp : ex.shards)
+        jobs.push_back(kind == TEMPLATES ? sync_template_to_shard(sp.get(), obj, &pass)
+                                         : sync_workgroup_to_shard(sp.get(), obj, &pass));
+    auto errs = co_await when_all(std::move(jobs));
+    std::vector<std::pair<std::string, std::string>> results;
+    bool failed = false;
+    std::string first;
+    for (size_t i = 0; i < ex.shards.size(); ++i) {
+        std::string msg = errs[i] ? describe(errs[i]) : std::string();
+        if (errs[i]) {
+            failed = true;
+            if (first.empty()) first = ex.shards[i]->name + ": " + msg;
+        }
+        results.emplace_back(ex.shards[i]->name, msg);
+    }
+    report(std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key, *obj, results, pass.wrote);
+    if (failed) throw NamedError("ShardSyncError", first);
+}
+
+static Task<void> worker() {
+    Executor& ex = *g_ex;
+    while (true) {
+        std::string key = co_await ex.queue.get();
+        if (key.empty()) co_return;
+        size_t a = key.find('/');
+        size_t b = key.find('/', a + 1);
+        std::string kind = key.substr(0, a), ns = key.substr(a + 1, b - a - 1), name = key.substr(b + 1);
+        ++ex.stats_reconciles;
+        bool ok = true;
+        std::string err;
+        try {
+            co_await sync_object(kind == "template" ? TEMPLATES : WORKGROUPS, ns, name);
+        } catch (const std::exception&) {
+            ok = false;
+            err = describe(std::current_exception());
+        }
+        if (ok) {
+            ex.queue.forget(key);
+        } else {
+            ++ex.stats_errors;
+            LOG_INFO("Error syncing %s; re-queuing for later retry: %s", key.c_str(), err.c_str());
+            ex.queue.add_rate_limited(key);
+        }
+        ex.queue.done(key);
+    }
+}
+
+static void sweep_orphans() {
+    Executor& ex = *g_ex;
+    for (auto& sp : ex.shards) {
+        for (int kind : {TEMPLATES, WORKGROUPS}) {
+            if (kind == WORKGROUPS && !g_opt.propagate_workgroup_deletes) continue;
+            for (auto& kv : sp->inf[kind].store)
+                if (is_ours(*kv.second) && !ex.cget(kind, kv.first)) ex.enqueue(kind, kv.second->ns, kv.second->name);
+        }
+    }
+}
+
+static void enqueue_all() {
+    Executor& ex = *g_ex;
+    for (int kind : {TEMPLATES, WORKGROUPS})
+        for (auto& kv : ex.ctl[kind]) ex.enqueue(kind, kv.second->ns, kv.second->name);
+}
+
+static Task<void> full_resync_loop() {
+    while (!g_ex->stop_ev.is_set()) {
+        co_await loop().sleep(g_opt.full_resync);
+        enqueue_all();
+        if (g_opt.orphan_sweep) sweep_orphans();
+    }
+}
+
+static Task<bool> wait_event(Event& ev, double timeout) {
+    double end = now_s() + timeout;
+    while (!ev.is_set()) {
+        if (now_s() >= end) co_return false;
+        co_await loop().sleep(std::min(0.01, std::max(0.0, end - now_s())));
+    }
+    co_return true;
+}
+
+static Task<void> wait_shard_synced(Shard* sh, double timeout) {
+    double end = now_s() + timeout;
+    for (auto& inf : sh->inf) {
+        double left = end - now_s();
+        if (left <= 0 || !(co_await wait_event(inf.synced_ev, left))) {
+            LOG_WARN("shard %s did not sync within %.1fs; continuing without it for now", sh->name.c_str(), timeout);
+            co_return;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ config / main
+static Credentials creds_of(const Value& s) {
+    Credentials c;
+    c.server = std::string(s.sget("server"));
+    c.ca_pem = std::string(s.sget("ca_pem"));
+    const Value* ins = s.get("insecure");
+    c.insecure = ins && ins->t == Value::BOOL && ins->b;
+    c.tls_server_name = std::string(s.sget("tls_server_name"));
+    c.cert_pem = std::string(s.sget("cert_pem"));
+    c.key_pem = std::string(s.sget("key_pem"));
+    c.token = std::string(s.sget("token"));
+    c.token_file = std::string(s.sget("token_file"));
+    c.username = std::string(s.sget("username"));
+    c.password = std::string(s.sget("password"));
+    return c;
+}
+
+static double num(const Value& o, const char* k, double d) {
+    const Value* v = o.get(k);
+    if (v && v->t == Value::NUM) return std::atof(v->s.c_str());
+    if (v && v->t == Value::BOOL) return v->b ? 1.0 : 0.0;
+    return d;
+}
+
+static void configure(const Value& c) {
+    Options& o = g_opt;
+    o.ns = std::string(c.sget("namespace"));
+    o.alias = std::string(c.sget("alias"));
+    o.workers = static_cast<int>(num(c, "workers", o.workers));
+    o.pool_size = static_cast<int>(num(c, "pool_size", o.pool_size));
+    o.request_timeout = num(c, "request_timeout", o.request_timeout);
+    o.coalesce = num(c, "coalesce_window", o.coalesce);
+    o.base_delay = num(c, "failure_base_delay", o.base_delay);
+    o.max_delay = num(c, "failure_max_delay", o.max_delay);
+    o.qps = num(c, "rate_limit_qps", o.qps);
+    o.burst = num(c, "rate_limit_burst", o.burst);
+    o.shard_sync_timeout = num(c, "shard_sync_timeout", o.shard_sync_timeout);
+    o.full_resync = num(c, "full_resync_period", o.full_resync);
+    o.sync_binary_data = num(c, "sync_binary_data", 1) != 0;
+    o.sync_secret_type = num(c, "sync_secret_type", 1) != 0;
+    o.orphan_sweep = num(c, "orphan_sweep", 1) != 0;
+    o.propagate_workgroup_deletes = num(c, "propagate_workgroup_deletes", 1) != 0;
+    o.log_level = static_cast<int>(num(c, "log_level", o.log_level));
+    if (o.full_resync <= 0) o.full_resync = 1e9;
+    Executor& ex = *g_ex;
+    const Value* shards = c.get("shards");
+    if (shards && shards->is_arr())
+        for (const auto& s : shards->a) {
+            auto sh = std::make_unique<Shard>();
+            sh->name = std::string(s.sget("name"));
+            sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout);
+            for (int k = 0; k < 4; ++k) {
+                sh->inf[k].shard = sh.get();
+                sh->inf[k].kind = k;
+            }
+            ex.shards.push_back(std::move(sh));
+        }
+}
+
+static void handle_message(const mp::Obj& m) {
+    Executor& ex = *g_ex;
+    std::string_view t = m.sget("t");
+    if (t == "w" || t == "s") {
+        int kind = static_cast<int>(m.iget("k"));
+        const mp::Obj* lines = m.get("l");
+        if (kind < 0 || kind > 3 || lines == nullptr || lines->t != mp::Obj::ARR) return;
+        if (t == "s") {
+            std::vector<Value> objs;
+            objs.reserve(lines->a.size());
+            for (const auto& l : lines->a) {
+                Value ev = parse(l.s);
+                Value* o = ev.get("object");
+                std::string_view type = ev.sget("type");
+                if (o && (type == "ADDED" || type == "MODIFIED")) objs.push_back(std::move(*o));
+            }
+            ctl_snapshot(kind, std::move(objs));
+        } else {
+            for (const auto& l : lines->a) {
+                Value ev = parse(l.s);
+                std::string type(ev.sget("type"));
+                Value* o = ev.get("object");
+                if (o && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) ctl_apply(kind, type, std::move(*o));
+            }
+        }
+    } else if (t == "go") {
+        ex.gate.set();
+    } else if (t == "cred") {
+        std::string_view shard = m.sget("s");
+        for (auto& sp : ex.shards)
+            if (sp->name == shard) sp->client->set_token(std::string(m.sget("token")));
+    }
+}
+
+static Task<void> reader(Event* configured) {
+    Executor& ex = *g_ex;
+    while (true) {
+        std::vector<mp::Obj> batch = co_await g_chan->recv();
+        if (batch.empty() && g_chan->closed()) break;
+        for (const auto& m : batch) {
+            if (m.sget("t") == "cfg") {
+                if (!configured->is_set()) {
+                    configure(parse(m.sget("c")));
+                    configured->set();
+                }
+                continue;
+            }
+            try {
+                handle_message(m);
+            } catch (const std::exception& e) {
+                LOG_ERROR("bad message from the coordinator: %s", e.what());
+            }
+        }
+    }
+    ex.stop_ev.set();  // the coordinator closing its end (or dying) ends this executor
+}
+
+static Task<void> run_main() {
+    Executor& ex = *g_ex;
+    Event configured;
+    spawn(reader(&configured), "channel reader");
+    co_await configured.wait();
+    for (auto& sp : ex.shards)
+        for (int k = 0; k < 4; ++k) spawn(shard_informer(sp.get(), k), "shard informer");
+    co_await ex.ctl_synced_ev.wait();
+    std::vector<Task<void>> waits;
+    for (auto& sp : ex.shards) waits.push_back(wait_shard_synced(sp.get(), g_opt.shard_sync_timeout));
+    co_await when_all(std::move(waits));
+    send_simple("synced");
+    if (g_opt.gated) co_await ex.gate.wait();
+    for (int i = 0; i < g_opt.workers; ++i) spawn(worker(), "worker");
+    if (g_opt.orphan_sweep) sweep_orphans();
+    spawn(full_resync_loop(), "full resync");
+    send_simple("ready");
+    LOG_INFO("native executor %d ready: %zu shard(s), partition %d/%d, %d workers", g_opt.index, ex.shards.size(),
+             g_opt.part, g_opt.parts, g_opt.workers);
+    co_await ex.stop_ev.wait();
+    ex.queue.shutdown();
+    co_await g_chan->drain(2.0);
+    loop().stop();
+}
+
+static int g_sigpipe[2] = {-1, -1};
+static void on_signal(int) {
+    char c = 1;
+    (void)!write(g_sigpipe[1], &c, 1);
+}
+static Task<void> signal_watch() {
+    while (true) {
+        char c;
+        ssize_t r = ::read(g_sigpipe[0], &c, 1);
+        if (r > 0) break;
+        if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+            co_await loop().readable(g_sigpipe[0]);
+            continue;
+        }
+        if (r < 0 && errno == EINTR) continue;
+        co_return;
+    }
+    g_ex->stop_ev.set();
+}
+
+}  // namespace ncc
+
+int main(int argc, char** argv) {
+    using namespace ncc;
+    int fd = -1;
+    for (int i = 1; i + 1 < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "--fd") fd = std::atoi(argv[++i]);
+        else if (a == "--index") g_opt.index = std::atoi(argv[++i]);
+        else if (a == "--part") {
+            std::string p = argv[++i];
+            size_t sl = p.find('/');
+            g_opt.part = std::atoi(p.substr(0, sl).c_str());
+            g_opt.parts = sl == std::string::npos ? 1 : std::atoi(p.c_str() + sl + 1);
+        }
+    }
+    if (argc > 1 && std::string(argv[1]) == "--version") {
+        std::puts("ncc-executor 1");
+        return 0;
+    }
+    if (fd < 0) {
+        std::fprintf(stderr, "usage: ncc-executor --fd N --index I --part p/k\n");
+        return 2;
+    }
+    crc_init();
+    const char* gated = std::getenv("NCC_GATED");
+    g_opt.gated = gated != nullptr && std::string(gated) == "1";
+    ::signal(SIGPIPE, SIG_IGN);
+    Loop lp;
+    g_loop = &lp;
+    Executor ex;
+    g_ex = &ex;
+    if (pipe2(g_sigpipe, O_NONBLOCK | O_CLOEXEC) == 0) {
+        lp.add_fd(g_sigpipe[0]);
+        ::signal(SIGTERM, on_signal);
+        ::signal(SIGINT, on_signal);
+        spawn(signal_watch(), "signals");
+    }
+    Channel chan(fd);
+    g_chan = &chan;
+    spawn(run_main(), "main");
+    try {
+        lp.run();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "ncc-executor: fatal: %s\n", e.what());
+        return 1;
+    }
+    std::fflush(stderr);
+    std::_Exit(0);  // skip destructors of still-suspended coroutines
+}

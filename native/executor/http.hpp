@@ -1,0 +1,740 @@
+// HTTP/1.1 client for kube-apiservers: keep-alive connection pool, TLS (OpenSSL, CA / client
+// certificate / insecure / tls-server-name), bearer and basic auth, chunked watch streams,
+// Retry-After retries and request deadlines.  The native twin of ncc/kube/transport.py +
+// ncc/kube/rest.py for the executor's shard clusters.
+#pragma once
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstring>
+#include <map>
+#include <fstream>
+#include <memory>
+#include <set>
+#include <sstream>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "json.hpp"
+#include "loop.hpp"
+
+namespace ncc {
+
+struct TransportError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+// A non-2xx answer with a Kubernetes Status body (reason/message), like ncc.kube.errors.ApiError.
+struct ApiError : std::runtime_error {
+    int code;
+    std::string reason;
+    ApiError(int c, std::string r, const std::string& msg) : std::runtime_error(msg), code(c), reason(std::move(r)) {}
+    // the Python class name the coordinator sees in reports (ncc/kube/errors.py)
+    const char* kind() const {
+        if (reason == "AlreadyExists") return "AlreadyExists";
+        if (reason == "Gone" || code == 410) return "Gone";
+        switch (code) {
+            case 400: return "BadRequest";
+            case 401: return "Unauthorized";
+            case 403: return "Forbidden";
+            case 404: return "NotFound";
+            case 409: return "Conflict";
+            case 422: return "Invalid";
+            case 429: return "TooManyRequests";
+            case 503: return "ServiceUnavailable";
+            default: return code >= 500 ? "InternalError" : "ApiError";
+        }
+    }
+    bool not_found() const { return code == 404; }
+    bool already_exists() const { return code == 409 && reason == "AlreadyExists"; }
+    bool conflict() const { return code == 409 && reason != "AlreadyExists"; }
+};
+
+inline ApiError api_error(int status, const std::string& body) {
+    std::string reason, message;
+    try {
+        Value st = parse(body);
+        reason = std::string(st.sget("reason"));
+        message = std::string(st.sget("message"));
+        if (status == 200) {  // an in-stream watch ERROR carries its own code
+            const Value* c = st.get("code");
+            if (c != nullptr && c->t == Value::NUM) status = std::atoi(c->s.c_str());
+        }
+    } catch (const std::exception&) {
+        message = body.substr(0, 200);
+    }
+    if (reason.empty()) {
+        switch (status) {
+            case 404: reason = "NotFound"; break;
+            case 409: reason = "Conflict"; break;
+            case 410: reason = "Gone"; break;
+            default: break;
+        }
+    }
+    return ApiError(status, reason, message.empty() ? ("HTTP " + std::to_string(status)) : message);
+}
+
+struct Credentials {
+    std::string server;
+    std::string ca_pem;
+    bool insecure = false;
+    std::string tls_server_name;
+    std::string cert_pem, key_pem;
+    std::string token, token_file;
+    std::string username, password;
+};
+
+struct Url {
+    bool tls = false;
+    std::string host;
+    int port = 0;
+    std::string prefix;  // path prefix of the server URL (e.g. a proxy path), no trailing '/'
+};
+
+inline Url parse_url(const std::string& s) {
+    Url u;
+    std::string rest;
+    if (s.rfind("https://", 0) == 0) {
+        u.tls = true;
+        rest = s.substr(8);
+    } else if (s.rfind("http://", 0) == 0) {
+        rest = s.substr(7);
+    } else {
+        throw std::runtime_error("unsupported server URL " + s);
+    }
+    size_t slash = rest.find('/');
+    std::string hostport = rest.substr(0, slash);
+    if (slash != std::string::npos) u.prefix = rest.substr(slash);
+    while (!u.prefix.empty() && u.prefix.back() == '/') u.prefix.pop_back();
+    if (!hostport.empty() && hostport[0] == '[') {  // [v6]:port
+        size_t rb = hostport.find(']');
+        u.host = hostport.substr(1, rb - 1);
+        if (rb + 1 < hostport.size() && hostport[rb + 1] == ':') u.port = std::atoi(hostport.c_str() + rb + 2);
+    } else {
+        size_t colon = hostport.rfind(':');
+        if (colon != std::string::npos) {
+            u.host = hostport.substr(0, colon);
+            u.port = std::atoi(hostport.c_str() + colon + 1);
+        } else {
+            u.host = hostport;
+        }
+    }
+    if (u.port == 0) u.port = u.tls ? 443 : 80;
+    return u;
+}
+
+inline bool is_ip(const std::string& h) {
+    in6_addr a6;
+    in_addr a4;
+    return inet_pton(AF_INET, h.c_str(), &a4) == 1 || inet_pton(AF_INET6, h.c_str(), &a6) == 1;
+}
+
+// ------------------------------------------------------------------------------------ TLS context
+inline std::string ssl_errors() {
+    std::string out;
+    unsigned long e;
+    char buf[256];
+    while ((e = ERR_get_error()) != 0) {
+        ERR_error_string_n(e, buf, sizeof buf);
+        if (!out.empty()) out += "; ";
+        out += buf;
+    }
+    return out.empty() ? "unknown TLS error" : out;
+}
+
+inline SSL_CTX* make_ssl_ctx(const Credentials& c) {
+    SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+    if (ctx == nullptr) throw std::runtime_error("SSL_CTX_new: " + ssl_errors());
+    SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+    SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+    if (c.insecure) {
+        SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
+    } else {
+        SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+        if (!c.ca_pem.empty()) {
+            X509_STORE* store = SSL_CTX_get_cert_store(ctx);
+            BIO* bio = BIO_new_mem_buf(c.ca_pem.data(), static_cast<int>(c.ca_pem.size()));
+            int n = 0;
+            while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+                X509_STORE_add_cert(store, x);
+                X509_free(x);
+                ++n;
+            }
+            BIO_free(bio);
+            ERR_clear_error();
+            if (n == 0) throw std::runtime_error("certificate-authority-data holds no certificate");
+        } else {
+            SSL_CTX_set_default_verify_paths(ctx);
+        }
+    }
+    if (!c.cert_pem.empty() && !c.key_pem.empty()) {
+        BIO* bio = BIO_new_mem_buf(c.cert_pem.data(), static_cast<int>(c.cert_pem.size()));
+        X509* leaf = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+        if (leaf == nullptr || SSL_CTX_use_certificate(ctx, leaf) != 1)
+            throw std::runtime_error("client certificate: " + ssl_errors());
+        X509_free(leaf);
+        while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) SSL_CTX_add_extra_chain_cert(ctx, x);
+        ERR_clear_error();
+        BIO_free(bio);
+        bio = BIO_new_mem_buf(c.key_pem.data(), static_cast<int>(c.key_pem.size()));
+        EVP_PKEY* key = PEM_read_bio_PrivateKey(bio, nullptr, nullptr, nullptr);
+        BIO_free(bio);
+        if (key == nullptr || SSL_CTX_use_PrivateKey(ctx, key) != 1)
+            throw std::runtime_error("client key: " + ssl_errors());
+        EVP_PKEY_free(key);
+    }
+    return ctx;
+}
+
+// ------------------------------------------------------------------------------------ connection
+class Conn {
+public:
+    int fd = -1;
+    SSL* ssl = nullptr;
+    std::string buf;  // received, not yet consumed
+    size_t pos = 0;
+    double deadline = 0;  // request deadline (pool sweep shuts the socket down when passed)
+    bool reused = false;
+
+    ~Conn() { close(); }
+    void close() {
+        if (ssl != nullptr) {
+            SSL_free(ssl);
+            ssl = nullptr;
+        }
+        if (fd >= 0) {
+            loop().del_fd(fd);
+            ::close(fd);
+            fd = -1;
+        }
+    }
+    void abort() {  // wake a pending read/write with an error (deadline sweep)
+        if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
+    }
+
+    Task<void> connect(const Url& u, SSL_CTX* ctx, const std::string& server_name) {
+        addrinfo hints{};
+        hints.ai_family = AF_UNSPEC;
+        hints.ai_socktype = SOCK_STREAM;
+        addrinfo* res = nullptr;
+        std::string port = std::to_string(u.port);
+        int rc = getaddrinfo(u.host.c_str(), port.c_str(), &hints, &res);
+        if (rc != 0 || res == nullptr) throw TransportError("resolve " + u.host + ": " + gai_strerror(rc));
+        fd = ::socket(res->ai_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+        if (fd < 0) {
+            freeaddrinfo(res);
+            throw TransportError("socket() failed");
+        }
+        int one = 1;
+        setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        loop().add_fd(fd);
+        rc = ::connect(fd, res->ai_addr, res->ai_addrlen);
+        freeaddrinfo(res);
+        if (rc != 0 && errno != EINPROGRESS) throw TransportError("connect " + u.host + ": " + std::strerror(errno));
+        if (rc != 0) {
+            co_await loop().writable(fd);
+            int err = 0;
+            socklen_t len = sizeof err;
+            getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
+            if (err != 0) throw TransportError("connect " + u.host + ":" + port + ": " + std::strerror(err));
+        }
+        if (ctx != nullptr) {
+            ssl = SSL_new(ctx);
+            SSL_set_fd(ssl, fd);
+            const std::string& name = server_name.empty() ? u.host : server_name;
+            if (!is_ip(name)) SSL_set_tlsext_host_name(ssl, name.c_str());
+            X509_VERIFY_PARAM* vp = SSL_get0_param(ssl);
+            if (is_ip(name))
+                X509_VERIFY_PARAM_set1_ip_asc(vp, name.c_str());
+            else
+                X509_VERIFY_PARAM_set1_host(vp, name.c_str(), 0);
+            while (true) {
+                int r = SSL_connect(ssl);
+                if (r == 1) break;
+                int e = SSL_get_error(ssl, r);
+                if (e == SSL_ERROR_WANT_READ) {
+                    co_await loop().readable(fd);
+                } else if (e == SSL_ERROR_WANT_WRITE) {
+                    co_await loop().writable(fd);
+                } else {
+                    throw TransportError("TLS handshake with " + u.host + ": " + ssl_errors());
+                }
+            }
+        }
+    }
+
+    // Read more bytes into `buf`; throws on EOF/error.
+    Task<void> fill() {
+        if (pos > 0 && pos == buf.size()) {
+            buf.clear();
+            pos = 0;
+        } else if (pos > 65536) {
+            buf.erase(0, pos);
+            pos = 0;
+        }
+        char tmp[65536];
+        while (true) {
+            if (fd < 0) throw TransportError("connection closed");
+            if (ssl != nullptr) {
+                int r = SSL_read(ssl, tmp, sizeof tmp);
+                if (r > 0) {
+                    buf.append(tmp, static_cast<size_t>(r));
+                    co_return;
+                }
+                int e = SSL_get_error(ssl, r);
+                if (e == SSL_ERROR_WANT_READ) {
+                    co_await loop().readable(fd);
+                } else if (e == SSL_ERROR_WANT_WRITE) {
+                    co_await loop().writable(fd);
+                } else if (e == SSL_ERROR_ZERO_RETURN) {
+                    throw TransportError("connection closed by peer");
+                } else {
+                    throw TransportError("TLS read: " + ssl_errors());
+                }
+            } else {
+                ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+                if (r > 0) {
+                    buf.append(tmp, static_cast<size_t>(r));
+                    co_return;
+                }
+                if (r == 0) throw TransportError("connection closed by peer");
+                if (errno == EAGAIN || errno == EWOULDBLOCK) {
+                    co_await loop().readable(fd);
+                } else if (errno != EINTR) {
+                    throw TransportError(std::string("recv: ") + std::strerror(errno));
+                }
+            }
+        }
+    }
+
+    Task<void> write_all(const std::string& data) {
+        size_t off = 0;
+        while (off < data.size()) {
+            if (fd < 0) throw TransportError("connection closed");
+            if (ssl != nullptr) {
+                int r = SSL_write(ssl, data.data() + off, static_cast<int>(data.size() - off));
+                if (r > 0) {
+                    off += static_cast<size_t>(r);
+                    continue;
+                }
+                int e = SSL_get_error(ssl, r);
+                if (e == SSL_ERROR_WANT_WRITE) {
+                    co_await loop().writable(fd);
+                } else if (e == SSL_ERROR_WANT_READ) {
+                    co_await loop().readable(fd);
+                } else {
+                    throw TransportError("TLS write: " + ssl_errors());
+                }
+            } else {
+                ssize_t r = ::send(fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
+                if (r > 0) {
+                    off += static_cast<size_t>(r);
+                    continue;
+                }
+                if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+                    co_await loop().writable(fd);
+                } else if (r < 0 && errno != EINTR) {
+                    throw TransportError(std::string("send: ") + std::strerror(errno));
+                }
+            }
+        }
+    }
+
+    // Next line terminated by CRLF (without it).
+    Task<std::string> read_line() {
+        while (true) {
+            size_t i = buf.find("\r\n", pos);
+            if (i != std::string::npos) {
+                std::string line = buf.substr(pos, i - pos);
+                pos = i + 2;
+                co_return line;
+            }
+            co_await fill();
+        }
+    }
+    Task<std::string> read_exact(size_t n) {
+        while (buf.size() - pos < n) co_await fill();
+        std::string out = buf.substr(pos, n);
+        pos += n;
+        co_return out;
+    }
+};
+
+struct Head {
+    int status = 0;
+    long long content_length = -1;
+    bool chunked = false;
+    bool close = false;
+    std::string retry_after;
+};
+
+inline bool ieq_prefix(std::string_view line, std::string_view name) {
+    if (line.size() <= name.size() || line[name.size()] != ':') return false;
+    for (size_t i = 0; i < name.size(); ++i)
+        if (std::tolower(static_cast<unsigned char>(line[i])) != name[i]) return false;
+    return true;
+}
+inline std::string header_value(std::string_view line, size_t name_len) {
+    std::string_view v = line.substr(name_len + 1);
+    while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+    while (!v.empty() && (v.back() == ' ' || v.back() == '\t')) v.remove_suffix(1);
+    return std::string(v);
+}
+
+inline Task<Head> read_head(Conn& c) {
+    Head h;
+    std::string status_line = co_await c.read_line();
+    if (status_line.rfind("HTTP/1.", 0) != 0 || status_line.size() < 12)
+        throw TransportError("malformed status line");
+    h.status = std::atoi(status_line.c_str() + 9);
+    if (status_line.compare(0, 8, "HTTP/1.0") == 0) h.close = true;
+    while (true) {
+        std::string line = co_await c.read_line();
+        if (line.empty()) break;
+        if (ieq_prefix(line, "content-length")) {
+            h.content_length = std::atoll(header_value(line, 14).c_str());
+        } else if (ieq_prefix(line, "transfer-encoding")) {
+            std::string v = header_value(line, 17);
+            std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+            h.chunked = v.find("chunked") != std::string::npos;
+        } else if (ieq_prefix(line, "connection")) {
+            std::string v = header_value(line, 10);
+            std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+            if (v == "close") h.close = true;
+        } else if (ieq_prefix(line, "retry-after")) {
+            h.retry_after = header_value(line, 11);
+        }
+    }
+    co_return h;
+}
+
+// Next chunk of a chunked body; "" marks the end (trailers consumed).
+inline Task<std::string> read_chunk(Conn& c) {
+    std::string size_line = co_await c.read_line();
+    size_t n = std::strtoul(size_line.c_str(), nullptr, 16);
+    if (n == 0) {
+        while (true) {
+            std::string t = co_await c.read_line();
+            if (t.empty()) break;
+        }
+        co_return std::string();
+    }
+    std::string data = co_await c.read_exact(n);
+    co_await c.read_exact(2);  // CRLF
+    co_return data;
+}
+
+inline Task<std::string> read_body(Conn& c, const Head& h) {
+    if (h.chunked) {
+        std::string body;
+        while (true) {
+            std::string ch = co_await read_chunk(c);
+            if (ch.empty()) break;
+            body += ch;
+        }
+        co_return body;
+    }
+    if (h.content_length >= 0) co_return co_await c.read_exact(static_cast<size_t>(h.content_length));
+    if (h.status == 204 || h.status == 304) co_return std::string();
+    // no length: read to EOF
+    std::string body;
+    try {
+        while (true) co_await c.fill();
+    } catch (const TransportError&) {
+    }
+    body = c.buf.substr(c.pos);
+    c.pos = c.buf.size();
+    co_return body;
+}
+
+struct Response {
+    int status = 0;
+    std::string body;
+    std::string retry_after;
+};
+
+// ------------------------------------------------------------------------------------ client
+class Client {
+public:
+    Client(Credentials creds, int pool_size, double request_timeout)
+        : creds_(std::move(creds)), max_(std::max(1, pool_size)), timeout_(request_timeout) {
+        url_ = parse_url(creds_.server);
+        if (url_.tls) ctx_ = make_ssl_ctx(creds_);
+        host_ = creds_.tls_server_name.empty()
+                    ? (url_.host.find(':') != std::string::npos ? "[" + url_.host + "]" : url_.host) + ":" +
+                          std::to_string(url_.port)
+                    : creds_.tls_server_name;
+        token_ = creds_.token;
+        reload_token(true);
+        spawn(sweep(), "request-deadline sweep");
+    }
+    ~Client() {
+        closed_ = true;
+        idle_.clear();
+        if (ctx_ != nullptr) SSL_CTX_free(ctx_);
+    }
+    void set_token(std::string t) {
+        token_ = std::move(t);
+        hdr_.clear();
+    }
+    const std::string& prefix() const { return url_.prefix; }
+    std::map<std::string, long long> stats;
+
+    // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
+    // token once on 401, and re-send once on a fresh connection when a reused keep-alive connection died
+    // before any byte of the response arrived.
+    Task<Response> request(const std::string& method, const std::string& target, const std::string* body,
+                           const char* content_type = "application/json") {
+        int attempt = 0;
+        bool refreshed = false;
+        while (true) {
+            Response r = co_await exchange(method, target, body, content_type);
+            if (r.status == 401 && !creds_.token_file.empty() && !refreshed) {
+                refreshed = true;
+                reload_token(true);
+                continue;
+            }
+            if ((r.status == 429 || r.status == 500 || r.status == 502 || r.status == 503 || r.status == 504) &&
+                !r.retry_after.empty() && attempt < 5) {
+                ++attempt;
+                double d = std::atof(r.retry_after.c_str());
+                co_await loop().sleep(std::min(d > 0 ? d : 1.0, 10.0));
+                continue;
+            }
+            co_return r;
+        }
+    }
+
+    // A watch stream: `on_lines` gets every complete line of one read; returns at the end of the stream.
+    template <class F>
+    Task<void> stream(const std::string& target, F on_lines, double idle_timeout) {
+        auto conn = std::make_unique<Conn>();
+        co_await conn->connect(url_, ctx_, creds_.tls_server_name);
+        // a silent dead peer must not hold the watch forever: the deadline sweep aborts the stream
+        // when nothing (events or bookmarks) arrived for `idle_timeout` seconds
+        conn->deadline = now_s() + idle_timeout;
+        struct Guard {
+            Client* cl;
+            Conn* c;
+            ~Guard() { cl->busy_.erase(c); }
+        } guard{this, conn.get()};
+        busy_.insert(conn.get());
+        co_await conn->write_all(render("GET", target, nullptr, nullptr));
+        Head h = co_await read_head(*conn);
+        if (h.status >= 300) {
+            std::string b = co_await read_body(*conn, h);
+            throw api_error(h.status, b);
+        }
+        std::string pending;
+        std::vector<std::string> lines;
+        while (true) {
+            std::string chunk;
+            if (h.chunked) {
+                chunk = co_await read_chunk(*conn);
+                if (chunk.empty()) break;
+            } else {
+                try {
+                    co_await conn->fill();
+                } catch (const TransportError&) {
+                    break;
+                }
+                chunk = conn->buf.substr(conn->pos);
+                conn->pos = conn->buf.size();
+            }
+            conn->deadline = now_s() + idle_timeout;
+            pending += chunk;
+            size_t start = 0, nl;
+            while ((nl = pending.find('\n', start)) != std::string::npos) {
+                if (nl > start) lines.emplace_back(pending, start, nl - start);
+                start = nl + 1;
+            }
+            pending.erase(0, start);
+            if (!lines.empty()) {
+                on_lines(lines);
+                lines.clear();
+            }
+        }
+        if (!pending.empty()) {
+            lines.push_back(pending);
+            on_lines(lines);
+        }
+    }
+
+private:
+    Credentials creds_;
+    Url url_;
+    SSL_CTX* ctx_ = nullptr;
+    std::string host_;
+    int max_;
+    double timeout_;
+    int open_ = 0;
+    bool closed_ = false;
+    std::string token_;
+    double token_read_at_ = -1e9;
+    std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
+    std::vector<std::unique_ptr<Conn>> idle_;
+    std::set<Conn*> busy_;
+    std::deque<std::coroutine_handle<>> waiters_;
+
+    void reload_token(bool force) {
+        if (creds_.token_file.empty()) return;
+        double now = now_s();
+        if (!force && now - token_read_at_ < 60.0) return;
+        std::ifstream f(creds_.token_file);
+        if (f) {
+            std::stringstream ss;
+            ss << f.rdbuf();
+            std::string t = ss.str();
+            while (!t.empty() && (t.back() == '\n' || t.back() == '\r' || t.back() == ' ')) t.pop_back();
+            if (t != token_) set_token(t);
+        }
+        token_read_at_ = now;
+    }
+
+    const std::string& headers(const char* content_type) {
+        reload_token(false);
+        std::string key = content_type ? content_type : "";
+        auto it = hdr_.find(key);
+        if (it != hdr_.end()) return it->second;
+        std::string h = "Host: " + host_ + "\r\nUser-Agent: nexus-configuration-controller/ncc-executor (linux/amd64)"
+                        "\r\nAccept: application/json\r\n";
+        if (content_type != nullptr) h += std::string("Content-Type: ") + content_type + "\r\n";
+        if (!token_.empty()) {
+            h += "Authorization: Bearer " + token_ + "\r\n";
+        } else if (!creds_.username.empty()) {
+            std::string up = creds_.username + ":" + creds_.password;
+            std::string b64(4 * ((up.size() + 2) / 3) + 1, '\0');
+            int n = EVP_EncodeBlock(reinterpret_cast<unsigned char*>(&b64[0]),
+                                    reinterpret_cast<const unsigned char*>(up.data()), static_cast<int>(up.size()));
+            b64.resize(static_cast<size_t>(n));
+            h += "Authorization: Basic " + b64 + "\r\n";
+        }
+        return hdr_[key] = h;
+    }
+
+    std::string render(const char* method, const std::string& target, const std::string* body,
+                       const char* content_type) {
+        std::string req;
+        req.reserve(256 + (body ? body->size() : 0));
+        req += method;
+        req += ' ';
+        req += url_.prefix;
+        req += target;
+        req += " HTTP/1.1\r\n";
+        req += headers(body ? content_type : nullptr);
+        if (body != nullptr) {
+            req += "Content-Length: " + std::to_string(body->size()) + "\r\n\r\n";
+            req += *body;
+        } else {
+            req += "\r\n";
+        }
+        return req;
+    }
+
+    Task<std::unique_ptr<Conn>> acquire() {
+        while (true) {
+            if (!idle_.empty()) {
+                auto c = std::move(idle_.back());
+                idle_.pop_back();
+                c->reused = true;
+                co_return c;
+            }
+            if (open_ < max_) {
+                ++open_;
+                auto c = std::make_unique<Conn>();
+                try {
+                    co_await c->connect(url_, ctx_, creds_.tls_server_name);
+                } catch (...) {
+                    --open_;
+                    wake_one();
+                    throw;
+                }
+                co_return c;
+            }
+            struct Park {
+                Client* cl;
+                bool await_ready() { return false; }
+                void await_suspend(std::coroutine_handle<> h) { cl->waiters_.push_back(h); }
+                void await_resume() {}
+            };
+            co_await Park{this};
+        }
+    }
+    void wake_one() {
+        if (!waiters_.empty()) {
+            loop().post(waiters_.front());
+            waiters_.pop_front();
+        }
+    }
+    void release(std::unique_ptr<Conn> c, bool reuse) {
+        if (reuse && !closed_ && c->fd >= 0) {
+            idle_.push_back(std::move(c));
+        } else {
+            --open_;
+            c.reset();
+        }
+        wake_one();
+    }
+
+    Task<Response> exchange(const std::string& method, const std::string& target, const std::string* body,
+                            const char* content_type) {
+        std::string req = render(method.c_str(), target, body, content_type);
+        for (int tries = 0;; ++tries) {
+            auto c = co_await acquire();
+            bool reused = c->reused;
+            size_t before = 0;
+            c->deadline = now_s() + timeout_;
+            busy_.insert(c.get());
+            Response r;
+            bool ok = false, keep = false;
+            std::string err;
+            try {
+                co_await c->write_all(req);
+                before = c->buf.size() - c->pos;
+                Head h = co_await read_head(*c);
+                r.body = co_await read_body(*c, h);
+                r.status = h.status;
+                r.retry_after = h.retry_after;
+                keep = !h.close;
+                ok = true;
+            } catch (const TransportError& e) {
+                err = e.what();
+            }
+            busy_.erase(c.get());
+            bool timed_out = !ok && now_s() >= c->deadline;
+            release(std::move(c), ok && keep);
+            if (ok) {
+                ++stats["requests"];
+                co_return r;
+            }
+            ++stats["errors"];
+            if (timed_out) throw TransportError(method + " " + target + ": request timed out");
+            if (reused && before == 0 && tries == 0) continue;  // stale keep-alive connection: once more, fresh
+            throw TransportError(method + " " + target + ": " + err);
+        }
+    }
+
+    Task<void> sweep() {
+        while (!closed_) {
+            co_await loop().sleep(0.5);
+            double now = now_s();
+            for (Conn* c : busy_)
+                if (c->deadline > 0 && now >= c->deadline) c->abort();
+        }
+    }
+};
+
+}  // namespace ncc

@@ -1,0 +1,450 @@
+// JSON DOM for the native shard executor: parse, serialise, structural 64-bit fingerprints.
+//
+// The executor keeps every controller-side object it needs (templates, workgroups, Secrets,
+// ConfigMaps) and a slim copy of every shard object as `Value` trees.  Members keep their wire
+// order (a PUT re-sends shard metadata exactly as read); numbers keep their text.  Fingerprints
+// are order-independent for objects and number-canonical (1 == 1.0), so "is the shard copy's spec
+// the template's spec" — reflect.DeepEqual in the reference (controller.go:795-802) — is one
+// integer compare.
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+namespace ncc {
+
+struct JsonError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+struct Value {
+    enum Type : uint8_t { NUL, BOOL, NUM, STR, ARR, OBJ };
+    Type t = NUL;
+    bool b = false;
+    std::string s;  // string value, or the number's text
+    std::vector<Value> a;
+    std::vector<std::pair<std::string, Value>> o;
+
+    Value() = default;
+    static Value str(std::string v) {
+        Value x;
+        x.t = STR;
+        x.s = std::move(v);
+        return x;
+    }
+    static Value object() {
+        Value x;
+        x.t = OBJ;
+        return x;
+    }
+    static Value array() {
+        Value x;
+        x.t = ARR;
+        return x;
+    }
+    static Value boolean(bool v) {
+        Value x;
+        x.t = BOOL;
+        x.b = v;
+        return x;
+    }
+    static Value number(long long v) {
+        Value x;
+        x.t = NUM;
+        x.s = std::to_string(v);
+        return x;
+    }
+
+    bool is_obj() const { return t == OBJ; }
+    bool is_arr() const { return t == ARR; }
+    bool is_str() const { return t == STR; }
+    bool is_null() const { return t == NUL; }
+
+    const Value* get(std::string_view k) const {
+        if (t != OBJ) return nullptr;
+        for (const auto& kv : o)
+            if (kv.first == k) return &kv.second;
+        return nullptr;
+    }
+    Value* get(std::string_view k) {
+        if (t != OBJ) return nullptr;
+        for (auto& kv : o)
+            if (kv.first == k) return &kv.second;
+        return nullptr;
+    }
+    // string member or "" (absent / not a string)
+    std::string_view sget(std::string_view k) const {
+        const Value* v = get(k);
+        return (v != nullptr && v->t == STR) ? std::string_view(v->s) : std::string_view();
+    }
+    Value& set(std::string_view k, Value v) {
+        if (t != OBJ) {
+            t = OBJ;
+            o.clear();
+        }
+        for (auto& kv : o)
+            if (kv.first == k) {
+                kv.second = std::move(v);
+                return kv.second;
+            }
+        o.emplace_back(std::string(k), std::move(v));
+        return o.back().second;
+    }
+    void erase(std::string_view k) {
+        if (t != OBJ) return;
+        for (auto it = o.begin(); it != o.end(); ++it)
+            if (it->first == k) {
+                o.erase(it);
+                return;
+            }
+    }
+    bool empty_container() const { return (t == OBJ && o.empty()) || (t == ARR && a.empty()); }
+};
+
+// ------------------------------------------------------------------------------------ parse
+class Parser {
+public:
+    Parser(const char* p, size_t n) : p_(p), e_(p + n) {}
+
+    Value parse() {
+        Value v;
+        value(v, 0);
+        ws();
+        if (p_ != e_) throw JsonError("trailing characters");
+        return v;
+    }
+
+private:
+    const char* p_;
+    const char* e_;
+
+    void ws() {
+        while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+    }
+    [[noreturn]] void fail(const char* what) { throw JsonError(what); }
+
+    void value(Value& v, int depth) {
+        if (depth > 200) fail("nesting too deep");
+        ws();
+        if (p_ >= e_) fail("unexpected end");
+        char c = *p_;
+        if (c == '{') {
+            ++p_;
+            v.t = Value::OBJ;
+            ws();
+            if (p_ < e_ && *p_ == '}') {
+                ++p_;
+                return;
+            }
+            while (true) {
+                ws();
+                if (p_ >= e_ || *p_ != '"') fail("expected key");
+                std::string key;
+                string(key);
+                ws();
+                if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+                ++p_;
+                v.o.emplace_back(std::move(key), Value());
+                value(v.o.back().second, depth + 1);
+                ws();
+                if (p_ < e_ && *p_ == ',') {
+                    ++p_;
+                    continue;
+                }
+                if (p_ < e_ && *p_ == '}') {
+                    ++p_;
+                    return;
+                }
+                fail("expected ',' or '}'");
+            }
+        }
+        if (c == '[') {
+            ++p_;
+            v.t = Value::ARR;
+            ws();
+            if (p_ < e_ && *p_ == ']') {
+                ++p_;
+                return;
+            }
+            while (true) {
+                v.a.emplace_back();
+                value(v.a.back(), depth + 1);
+                ws();
+                if (p_ < e_ && *p_ == ',') {
+                    ++p_;
+                    continue;
+                }
+                if (p_ < e_ && *p_ == ']') {
+                    ++p_;
+                    return;
+                }
+                fail("expected ',' or ']'");
+            }
+        }
+        if (c == '"') {
+            v.t = Value::STR;
+            string(v.s);
+            return;
+        }
+        if (c == 't' && e_ - p_ >= 4 && std::memcmp(p_, "true", 4) == 0) {
+            p_ += 4;
+            v.t = Value::BOOL;
+            v.b = true;
+            return;
+        }
+        if (c == 'f' && e_ - p_ >= 5 && std::memcmp(p_, "false", 5) == 0) {
+            p_ += 5;
+            v.t = Value::BOOL;
+            v.b = false;
+            return;
+        }
+        if (c == 'n' && e_ - p_ >= 4 && std::memcmp(p_, "null", 4) == 0) {
+            p_ += 4;
+            v.t = Value::NUL;
+            return;
+        }
+        if (c == '-' || (c >= '0' && c <= '9')) {
+            const char* s = p_;
+            ++p_;
+            while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' ||
+                               *p_ == '+' || *p_ == '-'))
+                ++p_;
+            v.t = Value::NUM;
+            v.s.assign(s, static_cast<size_t>(p_ - s));
+            return;
+        }
+        fail("unexpected character");
+    }
+
+    static int hex(char c) {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    }
+    unsigned u4() {
+        if (e_ - p_ < 4) fail("short \\u escape");
+        unsigned v = 0;
+        for (int i = 0; i < 4; ++i) {
+            int h = hex(p_[i]);
+            if (h < 0) fail("bad \\u escape");
+            v = (v << 4) | static_cast<unsigned>(h);
+        }
+        p_ += 4;
+        return v;
+    }
+    static void utf8(std::string& out, unsigned cp) {
+        if (cp < 0x80) {
+            out.push_back(static_cast<char>(cp));
+        } else if (cp < 0x800) {
+            out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+        } else if (cp < 0x10000) {
+            out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+        } else {
+            out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+        }
+    }
+    void string(std::string& out) {
+        ++p_;  // opening quote
+        const char* run = p_;
+        while (true) {
+            if (p_ >= e_) fail("unterminated string");
+            char c = *p_;
+            if (c == '"') {
+                out.append(run, static_cast<size_t>(p_ - run));
+                ++p_;
+                return;
+            }
+            if (c == '\\') {
+                out.append(run, static_cast<size_t>(p_ - run));
+                ++p_;
+                if (p_ >= e_) fail("bad escape");
+                char x = *p_++;
+                switch (x) {
+                    case '"': out.push_back('"'); break;
+                    case '\\': out.push_back('\\'); break;
+                    case '/': out.push_back('/'); break;
+                    case 'b': out.push_back('\b'); break;
+                    case 'f': out.push_back('\f'); break;
+                    case 'n': out.push_back('\n'); break;
+                    case 'r': out.push_back('\r'); break;
+                    case 't': out.push_back('\t'); break;
+                    case 'u': {
+                        unsigned cp = u4();
+                        if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+                            p_ += 2;
+                            unsigned lo = u4();
+                            if (lo >= 0xDC00 && lo < 0xE000) {
+                                cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                            } else {
+                                utf8(out, 0xFFFD);
+                                cp = lo;
+                            }
+                        }
+                        utf8(out, cp);
+                        break;
+                    }
+                    default: fail("bad escape");
+                }
+                run = p_;
+                continue;
+            }
+            ++p_;
+        }
+    }
+};
+
+inline Value parse(std::string_view text) { return Parser(text.data(), text.size()).parse(); }
+
+// ------------------------------------------------------------------------------------ serialise
+inline void write_string(std::string& out, std::string_view s) {
+    static const char* hexd = "0123456789abcdef";
+    out.push_back('"');
+    const char* run = s.data();
+    const char* end = s.data() + s.size();
+    for (const char* p = run; p < end; ++p) {
+        unsigned char c = static_cast<unsigned char>(*p);
+        if (c >= 0x20 && c != '"' && c != '\\') continue;
+        out.append(run, static_cast<size_t>(p - run));
+        switch (c) {
+            case '"': out.append("\\\""); break;
+            case '\\': out.append("\\\\"); break;
+            case '\n': out.append("\\n"); break;
+            case '\r': out.append("\\r"); break;
+            case '\t': out.append("\\t"); break;
+            case '\b': out.append("\\b"); break;
+            case '\f': out.append("\\f"); break;
+            default:
+                out.append("\\u00");
+                out.push_back(hexd[c >> 4]);
+                out.push_back(hexd[c & 15]);
+        }
+        run = p + 1;
+    }
+    out.append(run, static_cast<size_t>(end - run));
+    out.push_back('"');
+}
+
+inline void dump(std::string& out, const Value& v) {
+    switch (v.t) {
+        case Value::NUL: out.append("null"); break;
+        case Value::BOOL: out.append(v.b ? "true" : "false"); break;
+        case Value::NUM: out.append(v.s); break;
+        case Value::STR: write_string(out, v.s); break;
+        case Value::ARR: {
+            out.push_back('[');
+            bool first = true;
+            for (const auto& x : v.a) {
+                if (!first) out.push_back(',');
+                first = false;
+                dump(out, x);
+            }
+            out.push_back(']');
+            break;
+        }
+        case Value::OBJ: {
+            out.push_back('{');
+            bool first = true;
+            for (const auto& kv : v.o) {
+                if (!first) out.push_back(',');
+                first = false;
+                write_string(out, kv.first);
+                out.push_back(':');
+                dump(out, kv.second);
+            }
+            out.push_back('}');
+            break;
+        }
+    }
+}
+
+inline std::string dumps(const Value& v) {
+    std::string out;
+    out.reserve(256);
+    dump(out, v);
+    return out;
+}
+
+// ------------------------------------------------------------------------------------ fingerprints
+inline uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+inline uint64_t hash_bytes(std::string_view s, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ULL;
+    uint64_t h = seed ^ (s.size() * m);
+    const char* p = s.data();
+    size_t n = s.size();
+    while (n >= 8) {
+        uint64_t k;
+        std::memcpy(&k, p, 8);
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+        p += 8;
+        n -= 8;
+    }
+    uint64_t tail = 0;
+    for (size_t i = 0; i < n; ++i) tail |= static_cast<uint64_t>(static_cast<unsigned char>(p[i])) << (8 * i);
+    h ^= tail;
+    h *= m;
+    return fmix64(h);
+}
+
+inline uint64_t fingerprint(const Value& v) {
+    switch (v.t) {
+        case Value::NUL: return 0x9e3779b97f4a7c15ULL;
+        case Value::BOOL: return fmix64(v.b ? 0x1234567ULL : 0x7654321ULL);
+        case Value::NUM: {
+            char* end = nullptr;
+            double d = std::strtod(v.s.c_str(), &end);
+            if (std::isfinite(d) && d == std::floor(d) && std::fabs(d) < 9.0e15)
+                return fmix64(static_cast<uint64_t>(static_cast<long long>(d)) ^ 0x3333ULL);
+            uint64_t bits;
+            std::memcpy(&bits, &d, 8);
+            return fmix64(bits ^ 0x4444ULL);
+        }
+        case Value::STR: return hash_bytes(v.s, 0x5555ULL);
+        case Value::ARR: {
+            uint64_t h = 0x6666ULL + v.a.size();
+            for (const auto& x : v.a) h = fmix64(h * 31 + fingerprint(x));
+            return h;
+        }
+        case Value::OBJ: {
+            uint64_t acc = 0x7777ULL + v.o.size();
+            for (const auto& kv : v.o)  // commutative: member order does not matter
+                acc += fmix64(hash_bytes(kv.first, 0x8888ULL) ^ (fingerprint(kv.second) * 0x9E3779B97F4A7C15ULL));
+            return fmix64(acc);
+        }
+    }
+    return 0;
+}
+
+// fingerprint(x or None): absent, null and empty maps are one value (a nil Go map == an empty one)
+inline uint64_t fp_opt(const Value* v) {
+    static const Value null_value;
+    if (v == nullptr || v->t == Value::NUL || v->empty_container()) return fingerprint(null_value);
+    return fingerprint(*v);
+}
+
+}  // namespace ncc

@@ -1,0 +1,351 @@
+// Single-threaded epoll reactor + C++20 coroutines for the native shard executor.
+//
+// One process per shard group, one thread, no locks: the same concurrency model as the Python
+// executor's asyncio loop, without its per-await cost.  `Task<T>` is a lazy coroutine awaited by
+// its parent (symmetric transfer), `spawn` detaches one, `when_all` joins several; sockets are
+// registered edge-triggered and awaited through `readable`/`writable`; `sleep` uses a timer heap.
+#pragma once
+
+#include <sys/epoll.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <coroutine>
+#include <cstdio>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <queue>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace ncc {
+
+inline double now_s() {
+    using namespace std::chrono;
+    return duration_cast<duration<double>>(steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------------------------ Task
+template <class T>
+class Task;
+
+namespace detail {
+struct FinalAwaiter {
+    bool await_ready() noexcept { return false; }
+    template <class P>
+    std::coroutine_handle<> await_suspend(std::coroutine_handle<P> h) noexcept {
+        auto c = h.promise().cont;
+        return c ? c : std::noop_coroutine();
+    }
+    void await_resume() noexcept {}
+};
+struct PromiseBase {
+    std::coroutine_handle<> cont;
+    std::exception_ptr exc;
+    std::suspend_always initial_suspend() noexcept { return {}; }
+    FinalAwaiter final_suspend() noexcept { return {}; }
+    void unhandled_exception() { exc = std::current_exception(); }
+};
+}  // namespace detail
+
+template <class T>
+class [[nodiscard]] Task {
+public:
+    struct promise_type : detail::PromiseBase {
+        std::optional<T> value;
+        Task get_return_object() { return Task(std::coroutine_handle<promise_type>::from_promise(*this)); }
+        void return_value(T v) { value.emplace(std::move(v)); }
+    };
+    Task() = default;
+    explicit Task(std::coroutine_handle<promise_type> h) : h_(h) {}
+    Task(Task&& o) noexcept : h_(std::exchange(o.h_, {})) {}
+    Task& operator=(Task&& o) noexcept {
+        if (this != &o) {
+            if (h_) h_.destroy();
+            h_ = std::exchange(o.h_, {});
+        }
+        return *this;
+    }
+    Task(const Task&) = delete;
+    ~Task() {
+        if (h_) h_.destroy();
+    }
+    bool await_ready() const noexcept { return false; }
+    std::coroutine_handle<> await_suspend(std::coroutine_handle<> c) noexcept {
+        h_.promise().cont = c;
+        return h_;
+    }
+    T await_resume() {
+        if (h_.promise().exc) std::rethrow_exception(h_.promise().exc);
+        return std::move(*h_.promise().value);
+    }
+
+private:
+    std::coroutine_handle<promise_type> h_;
+};
+
+template <>
+class [[nodiscard]] Task<void> {
+public:
+    struct promise_type : detail::PromiseBase {
+        Task get_return_object() { return Task(std::coroutine_handle<promise_type>::from_promise(*this)); }
+        void return_void() {}
+    };
+    Task() = default;
+    explicit Task(std::coroutine_handle<promise_type> h) : h_(h) {}
+    Task(Task&& o) noexcept : h_(std::exchange(o.h_, {})) {}
+    Task& operator=(Task&& o) noexcept {
+        if (this != &o) {
+            if (h_) h_.destroy();
+            h_ = std::exchange(o.h_, {});
+        }
+        return *this;
+    }
+    Task(const Task&) = delete;
+    ~Task() {
+        if (h_) h_.destroy();
+    }
+    bool await_ready() const noexcept { return false; }
+    std::coroutine_handle<> await_suspend(std::coroutine_handle<> c) noexcept {
+        h_.promise().cont = c;
+        return h_;
+    }
+    void await_resume() {
+        if (h_.promise().exc) std::rethrow_exception(h_.promise().exc);
+    }
+
+private:
+    std::coroutine_handle<promise_type> h_;
+};
+
+// ------------------------------------------------------------------------------------ Loop
+class Loop {
+public:
+    Loop() {
+        ep_ = epoll_create1(EPOLL_CLOEXEC);
+        if (ep_ < 0) throw std::runtime_error("epoll_create1 failed");
+    }
+    ~Loop() { ::close(ep_); }
+
+    struct FdState {
+        std::coroutine_handle<> reader, writer;
+        bool readable = false, writable = false;
+    };
+
+    void add_fd(int fd) {
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLOUT | EPOLLET | EPOLLRDHUP;
+        ev.data.fd = fd;
+        fds_[fd] = FdState{};
+        if (epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev) != 0) throw std::runtime_error("epoll_ctl ADD failed");
+    }
+    void del_fd(int fd) {
+        epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+        auto it = fds_.find(fd);
+        if (it != fds_.end()) {
+            // wake anyone still parked on the fd: their next syscall fails and raises
+            if (it->second.reader) post(it->second.reader);
+            if (it->second.writer) post(it->second.writer);
+            fds_.erase(it);
+        }
+    }
+
+    struct IoAwait {
+        Loop* loop;
+        int fd;
+        bool write;
+        bool await_ready() {
+            auto it = loop->fds_.find(fd);
+            if (it == loop->fds_.end()) return true;
+            bool& flag = write ? it->second.writable : it->second.readable;
+            if (flag) {
+                flag = false;  // consumed: the caller retries its syscall
+                return true;
+            }
+            return false;
+        }
+        void await_suspend(std::coroutine_handle<> h) {
+            auto& st = loop->fds_[fd];
+            (write ? st.writer : st.reader) = h;
+        }
+        void await_resume() {}
+    };
+    // Await the socket becoming readable/writable after a syscall returned EAGAIN (edge-triggered).
+    IoAwait readable(int fd) { return IoAwait{this, fd, false}; }
+    IoAwait writable(int fd) { return IoAwait{this, fd, true}; }
+
+    struct SleepAwait {
+        Loop* loop;
+        double until;
+        bool await_ready() { return until <= now_s(); }
+        void await_suspend(std::coroutine_handle<> h) { loop->timers_.push(Timer{until, loop->seq_++, h}); }
+        void await_resume() {}
+    };
+    SleepAwait sleep(double seconds) { return SleepAwait{this, now_s() + seconds}; }
+
+    void post(std::coroutine_handle<> h) { ready_.push_back(h); }
+    void call_soon(std::function<void()> fn) { calls_.push_back(std::move(fn)); }
+    void stop() { stopped_ = true; }
+    bool stopped() const { return stopped_; }
+
+    void run() {
+        epoll_event evs[256];
+        while (!stopped_) {
+            while (!ready_.empty() || !calls_.empty()) {
+                while (!ready_.empty()) {
+                    auto h = ready_.front();
+                    ready_.pop_front();
+                    h.resume();
+                }
+                while (!calls_.empty()) {
+                    auto fn = std::move(calls_.front());
+                    calls_.pop_front();
+                    fn();
+                }
+                if (stopped_) return;
+            }
+            int timeout_ms = -1;
+            double now = now_s();
+            if (!timers_.empty()) {
+                double dt = timers_.top().at - now;
+                timeout_ms = dt <= 0 ? 0 : static_cast<int>(dt * 1000.0) + 1;
+            }
+            int n = epoll_wait(ep_, evs, 256, timeout_ms);
+            if (n < 0 && errno != EINTR) throw std::runtime_error("epoll_wait failed");
+            for (int i = 0; i < n; ++i) {
+                auto it = fds_.find(evs[i].data.fd);
+                if (it == fds_.end()) continue;
+                uint32_t e = evs[i].events;
+                FdState& st = it->second;
+                if (e & (EPOLLIN | EPOLLHUP | EPOLLERR | EPOLLRDHUP)) {
+                    st.readable = true;
+                    if (st.reader) {
+                        auto h = std::exchange(st.reader, {});
+                        st.readable = false;
+                        ready_.push_back(h);
+                    }
+                }
+                if (e & (EPOLLOUT | EPOLLHUP | EPOLLERR)) {
+                    st.writable = true;
+                    if (st.writer) {
+                        auto h = std::exchange(st.writer, {});
+                        st.writable = false;
+                        ready_.push_back(h);
+                    }
+                }
+            }
+            now = now_s();
+            while (!timers_.empty() && timers_.top().at <= now) {
+                ready_.push_back(timers_.top().h);
+                timers_.pop();
+            }
+        }
+    }
+
+private:
+    struct Timer {
+        double at;
+        uint64_t seq;
+        std::coroutine_handle<> h;
+        bool operator>(const Timer& o) const { return at != o.at ? at > o.at : seq > o.seq; }
+    };
+    int ep_;
+    bool stopped_ = false;
+    uint64_t seq_ = 0;
+    std::unordered_map<int, FdState> fds_;
+    std::deque<std::coroutine_handle<>> ready_;
+    std::deque<std::function<void()>> calls_;
+    std::priority_queue<Timer, std::vector<Timer>, std::greater<Timer>> timers_;
+};
+
+inline Loop* g_loop = nullptr;
+inline Loop& loop() { return *g_loop; }
+
+// ------------------------------------------------------------------------------------ Event
+// Level-triggered flag with waiters (asyncio.Event).
+class Event {
+public:
+    bool is_set() const { return set_; }
+    void set() {
+        set_ = true;
+        for (auto h : waiters_) loop().post(h);
+        waiters_.clear();
+    }
+    void clear() { set_ = false; }
+    struct Await {
+        Event* ev;
+        bool await_ready() { return ev->set_; }
+        void await_suspend(std::coroutine_handle<> h) { ev->waiters_.push_back(h); }
+        void await_resume() {}
+    };
+    Await wait() { return Await{this}; }
+
+private:
+    bool set_ = false;
+    std::vector<std::coroutine_handle<>> waiters_;
+};
+
+// ------------------------------------------------------------------------------------ spawn / when_all
+struct Detached {
+    struct promise_type {
+        Detached get_return_object() { return {}; }
+        std::suspend_never initial_suspend() noexcept { return {}; }
+        std::suspend_never final_suspend() noexcept { return {}; }
+        void return_void() {}
+        void unhandled_exception() { std::terminate(); }
+    };
+};
+
+inline Detached spawn_impl(Task<void> t, const char* what) {
+    try {
+        co_await t;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "{\"level\":\"error\",\"msg\":\"%s task failed: %s\"}\n", what, e.what());
+    }
+}
+inline void spawn(Task<void> t, const char* what = "background") { spawn_impl(std::move(t), what); }
+
+namespace detail {
+struct JoinState {
+    size_t left = 0;
+    Event done;
+    std::vector<std::exception_ptr> errs;
+};
+inline Detached join_one(Task<void> t, std::shared_ptr<JoinState> st, size_t i) {
+    try {
+        co_await t;
+    } catch (...) {
+        st->errs[i] = std::current_exception();
+    }
+    if (--st->left == 0) st->done.set();
+}
+}  // namespace detail
+
+// Run every task concurrently; returns one exception_ptr per task (null on success).
+inline Task<std::vector<std::exception_ptr>> when_all(std::vector<Task<void>> tasks) {
+    std::vector<std::exception_ptr> out(tasks.size());
+    if (tasks.empty()) co_return out;
+    if (tasks.size() == 1) {
+        try {
+            co_await tasks[0];
+        } catch (...) {
+            out[0] = std::current_exception();
+        }
+        co_return out;
+    }
+    auto st = std::make_shared<detail::JoinState>();
+    st->left = tasks.size();
+    st->errs.resize(tasks.size());
+    for (size_t i = 0; i < tasks.size(); ++i) detail::join_one(std::move(tasks[i]), st, i);
+    co_await st->done.wait();
+    co_return std::move(st->errs);
+}
+
+}  // namespace ncc

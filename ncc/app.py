@@ -199,6 +199,8 @@ class App:
         self.lost_leadership = False
         self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
         self.relay = None  # coordinator: WatchRelay feeding the executors
+        self.executor_impl = ""  # coordinator: "native" (ncc/bin/ncc-executor) or "python" shard executors
+        self._cred_task = None
         self.relay_feeds: list | None = None  # executor: per-kind feeds from the coordinator's relay
         self.standby_was_warm = False  # caches had synced before this replica acquired the Lease
         self.coord_part: tuple | None = None  # (p, C) when the coordinator role is split over C processes
@@ -357,6 +359,8 @@ class App:
             out["coordinator_partitions"] = self.partitions.stats()
         if self.relay is not None:
             out["watch_relay"] = dict(self.relay.stats)
+        if self.executor_impl:
+            out["executor_impl"] = self.executor_impl
         if self.elector is not None:
             out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
                              "transitions": self.elector.transitions}
@@ -437,9 +441,17 @@ class App:
             env.pop("NCC_RELAY", None)
             part, parts = self.coord_part or (0, 1)
             exec_env = dict(env, NCC_RELAY="1") if self.relay is not None else env
+            from .controller.native_executor import NativeExecutorConfig, choose
+            use_native, why = choose(self.cfg, self.options, self.relay is not None)
+            self.executor_impl = "native" if use_native else "python"
+            if not use_native:
+                log.debug("Python shard executors: %s", why)
+            native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
                                      env=exec_env, per_shard=self.per_shard, part_base=part, part_stride=parts,
-                                     gated=gated, relay=self.relay)
+                                     gated=gated, relay=self.relay, native_config=native_cfg)
+            if native_cfg is not None:
+                self._cred_task = asyncio.ensure_future(native_cfg.refresh_loop(self.pool))
             self.pool.start()
             if parts > 1 and part == 0 and not os.environ.get("NCC_COORDINATOR_PART"):
                 self.partitions = CoordinatorPartitions(parts, env, gated=gated)
@@ -450,9 +462,9 @@ class App:
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
-                 "executors=%d×%d workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
+                 "executors=%d×%d (%s) workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
-                 self.options.workers, " (standing by)" if gated else "")
+                 self.executor_impl or "in-process", self.options.workers, " (standing by)" if gated else "")
 
     def open_gate(self) -> None:
         """Leading now (or released by the parent): start reconciling here and in every child process."""
@@ -466,7 +478,7 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
-        for t in (self._lease_task, self._reload_task, self._gc_task):
+        for t in (self._lease_task, self._reload_task, self._gc_task, self._cred_task):
             if t is not None:
                 t.cancel()
                 await asyncio.gather(t, return_exceptions=True)

@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `native-workers`, `coordinator-partitions`, `watch-relay`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -89,6 +89,8 @@ class AppConfig:
     max_executors: int = 16
     executors_per_shard: int = -1    # key-partitioned executors per shard group; -1 = auto (app.py)
     coordinator_partitions: int = -1  # native: coordinator processes splitting the template keys; -1 = auto
+    executor_impl: str = "auto"      # native: shard executors as ncc/bin/ncc-executor (C++) when built and
+                                     # supported ("auto"), always "native", or "python"
     watch_relay: bool = True         # native: executors get the controller cluster from the coordinator's
                                      # LIST/WATCH (ncc/controller/relay.py) instead of their own
     resync_period: float = _dur(30.0)

@@ -95,6 +95,11 @@ class ExecutorHandle:
         self.gate_open = False
         self.on_spawn = None  # callable(handle) once the channel to a (re)started child is up (watch relay)
         self.on_exit = None  # callable(handle) when that child has gone
+        self.on_need = None  # callable(handle, msg): the child asks for a controller object (watch relay)
+        # native shard executor (ncc/bin/ncc-executor): `config` renders its first message ({"t": "cfg"})
+        self.native = False
+        self.binary: str | None = None
+        self.config = None
         self._task: asyncio.Task | None = None
         self._stopping = False
 
@@ -103,9 +108,16 @@ class ExecutorHandle:
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(self.env or os.environ)
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
-        if self.argv is not None:
+        first = None
+        if self.native:
+            program = self.binary
+            args = ["--fd", str(child.fileno()), "--index", str(self.index), "--part", f"{self.part}/{self.parts}"]
+            first = {"t": "cfg", "c": await self.config.render(self)}
+        elif self.argv is not None:
+            program = sys.executable
             args = [*self.argv, "--control-fd", str(child.fileno())]
         else:
+            program = sys.executable
             args = ["-m", "ncc.executor", "--fd", str(child.fileno()), "--index", str(self.index),
                     "--shards", ",".join(self.shards), "--part", f"{self.part}/{self.parts}"]
         gated = self.gated and not self.gate_open
@@ -113,10 +125,12 @@ class ExecutorHandle:
             env["NCC_GATED"] = "1"
         else:
             env.pop("NCC_GATED", None)
-        self.proc = await asyncio.create_subprocess_exec(sys.executable, *args, pass_fds=(child.fileno(),), env=env)
+        self.proc = await asyncio.create_subprocess_exec(program, *args, pass_fds=(child.fileno(),), env=env)
         child.close()
         reader, writer = await asyncio.open_connection(sock=parent)
         self.channel = Channel(reader, writer)
+        if first is not None:
+            self.channel.send(first)
         if gated and self.gate_open:  # the gate opened while this child was being spawned
             self.channel.send({"t": "go"})
         if self.on_spawn is not None:
@@ -156,6 +170,10 @@ class ExecutorHandle:
                         self.synced.set()
                     elif t == "synced":
                         self.synced.set()
+                    elif t == "need":
+                        if self.on_need is not None:
+                            self.on_need(self, msg)
+                        continue
                     self.on_message(self.index, msg)
             if self.on_exit is not None:
                 self.on_exit(self)
@@ -196,7 +214,8 @@ class ExecutorPool:
     each reconciles only the keys of its partition (`key_part`), so one busy shard can use several cores."""
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
-                 part_base: int = 0, part_stride: int = 1, gated: bool = False, relay=None):
+                 part_base: int = 0, part_stride: int = 1, gated: bool = False, relay=None,
+                 native_config=None):
         """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
         mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
         keys are exactly a share of this coordinator's."""
@@ -206,6 +225,7 @@ class ExecutorPool:
         self.on_message = on_message
         self.env = env
         self.relay = relay  # coordinator's WatchRelay: executors get the controller cluster from it
+        self.native_config = native_config  # NativeExecutorConfig: run ncc/bin/ncc-executor instead of Python
         self.gated = gated
         self.gate_open = not gated
         self._next_index = 0
@@ -220,7 +240,10 @@ class ExecutorPool:
         for h in hs:
             h.gated, h.gate_open = self.gated, self.gate_open
             if self.relay is not None:
-                h.on_spawn, h.on_exit = self.relay.attach, self.relay.detach
+                h.on_spawn, h.on_exit, h.on_need = self.relay.attach, self.relay.detach, self.relay.on_need
+            if self.native_config is not None:
+                from .native_executor import binary_path
+                h.native, h.binary, h.config = True, binary_path(), self.native_config
         self._next_index += self.per_shard
         self.handles.extend(hs)
         return hs
@@ -275,6 +298,7 @@ class ExecutorPool:
 
     def stats(self) -> dict:
         return {h.index: {"shards": h.shards, "part": f"{h.part}/{h.parts}", "restarts": h.restarts,
+                          "impl": "native" if h.native else "python",
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
 
 

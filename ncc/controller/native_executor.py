@@ -1,0 +1,126 @@
+"""Coordinator-side support for the native shard executor (`ncc/bin/ncc-executor`, native/executor/).
+
+The C++ executor is a drop-in for the Python executor process (`python -m ncc.executor`): same
+supervision (`ExecutorHandle`), same socketpair protocol, same reports.  It never talks to the
+controller cluster — the coordinator's watch relay feeds it (ncc/controller/relay.py) — so the
+coordinator hands it everything else it needs as the first message on the channel:
+
+    {"t": "cfg", "c": "<json>"}   options + per-shard connection details with *resolved* credentials
+
+Kubeconfig parsing, `tokenFile` paths and `exec` credential plugins (EKS `aws eks get-token`) stay in
+Python (ncc/kube/kubeconfig.py): the executor receives the server URL, CA / client certificate PEMs,
+and a bearer token; exec tokens are refreshed here and pushed as `{"t": "cred"}` messages.
+
+`executor-impl: auto` (default) picks the native executor whenever the binary is built and the
+configuration is one it implements (native mode with the watch relay, PUT-based writes); otherwise
+the Python executor runs.  Server-side apply (`server-side-apply: true`) stays on the Python path.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+
+from ..kube.kubeconfig import CredentialSource, load_kubeconfig
+from ..shards.loader import discover
+
+log = logging.getLogger("ncc.executor")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "WARN": 30, "ERROR": 40, "CRITICAL": 50}
+
+
+def binary_path() -> str | None:
+    p = os.environ.get("NCC_EXECUTOR_BINARY") or os.path.join(ROOT, "ncc", "bin", "ncc-executor")
+    return p if os.path.isfile(p) and os.access(p, os.X_OK) else None
+
+
+def choose(cfg, options, relay_active: bool) -> tuple[bool, str]:
+    """(use the native executor?, why not)."""
+    # NCC_EXECUTOR_IMPL overrides the config (lets a test run / CI job pin either implementation)
+    impl = (os.environ.get("NCC_EXECUTOR_IMPL") or cfg.executor_impl or "auto").lower()
+    if impl == "python":
+        return False, "executor-impl: python"
+    reasons = []
+    if binary_path() is None:
+        reasons.append("ncc/bin/ncc-executor is not built (python native/build.py)")
+    if not relay_active:
+        reasons.append("the watch relay is off")
+    if options.server_side_apply:
+        reasons.append("server-side-apply is implemented by the Python executor only")
+    if reasons:
+        if impl == "native":
+            log.warning("executor-impl: native requested but unavailable (%s); using the Python executor",
+                        "; ".join(reasons))
+        return False, "; ".join(reasons)
+    return True, ""
+
+
+class NativeExecutorConfig:
+    """Renders the `cfg` message of one executor and keeps exec-plugin tokens fresh."""
+
+    def __init__(self, cfg, options):
+        self.cfg = cfg
+        self.options = options
+        self.paths = dict(discover(cfg.shard_config_path))
+        self.creds: dict[str, CredentialSource] = {}
+        self.tokens: dict[str, str | None] = {}
+
+    def _source(self, name: str) -> CredentialSource:
+        src = self.creds.get(name)
+        if src is None:
+            self.paths = dict(discover(self.cfg.shard_config_path))
+            cc = load_kubeconfig(self.paths[name], name=name)
+            src = self.creds[name] = CredentialSource(cc)
+        return src
+
+    async def shard_entry(self, name: str) -> dict:
+        src = self._source(name)
+        cc = src.cfg
+        token = await src.token() if (cc.exec is not None or cc.token) else None
+        self.tokens[name] = token
+        cert, key = cc.client_cert_data, cc.client_key_data
+        exec_cert = await src.exec_client_cert()
+        if exec_cert:
+            cert, key = exec_cert
+        return {"name": name, "server": cc.server, "ca_pem": (cc.ca_data or b"").decode(), "insecure": cc.insecure,
+                "tls_server_name": cc.tls_server_name or "", "cert_pem": (cert or b"").decode(),
+                "key_pem": (key or b"").decode(), "token": token or "",
+                "token_file": cc.token_file if (cc.token_file and not cc.token and cc.exec is None) else "",
+                "username": cc.username or "", "password": cc.password or ""}
+
+    async def render(self, handle) -> str:
+        o, cfg = self.options, self.cfg
+        shards = [await self.shard_entry(n) for n in handle.shards]
+        doc = {
+            "namespace": cfg.controller_namespace, "alias": cfg.alias,
+            "workers": max(256, 4 * cfg.client_pool_size), "pool_size": cfg.client_pool_size,
+            "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
+            "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,
+            "rate_limit_qps": o.rate_limit_qps, "rate_limit_burst": o.rate_limit_burst,
+            "shard_sync_timeout": o.wait_for_shards_timeout if o.wait_for_shards_timeout is not None else 3600.0,
+            "full_resync_period": o.full_resync_period, "sync_binary_data": o.sync_binary_data,
+            "sync_secret_type": o.sync_secret_type, "orphan_sweep": o.orphan_sweep,
+            "propagate_workgroup_deletes": o.propagate_workgroup_deletes,
+            "log_level": _LEVELS.get(str(cfg.log_level).upper(), 30), "shards": shards,
+        }
+        return json.dumps(doc)
+
+    async def refresh_loop(self, pool, period: float = 30.0) -> None:
+        """Push rotated exec-plugin tokens to the executors serving each shard."""
+        while True:
+            await asyncio.sleep(period)
+            for name, src in list(self.creds.items()):
+                if src.cfg.exec is None:
+                    continue
+                try:
+                    tok = await src.token()
+                except Exception as e:  # noqa: BLE001
+                    log.warning("refreshing the credential of shard %s: %s", name, e)
+                    continue
+                if tok and tok != self.tokens.get(name):
+                    self.tokens[name] = tok
+                    for h in pool.handles:
+                        if h.native and name in h.shards and h.channel is not None:
+                            h.channel.send({"t": "cred", "s": name, "token": tok})

@@ -121,6 +121,19 @@ class WatchRelay:
             if ok:
                 self._send_snapshot(k, [handle])
 
+    def on_need(self, handle, msg: dict) -> None:
+        """An executor misses a controller object it needs (e.g. a dependent routed elsewhere while another
+        partition's template owned it, before one of this partition's templates referenced it): send the
+        latest line of it, if the object exists."""
+        kind = msg.get("k")
+        ns, _, name = str(msg.get("n", "")).partition("/")
+        if not isinstance(kind, int) or not 0 <= kind < len(KINDS):
+            return
+        line = self.raw[kind].get((ns, name))
+        if line is not None:
+            self._send(handle, {"t": "w", "k": kind, "l": [line]})
+            self.stats["needs_served"] = self.stats.get("needs_served", 0) + 1
+
     def detach(self, handle) -> None:
         if handle in self.handles:
             self.handles.remove(handle)

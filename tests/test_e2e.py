@@ -565,11 +565,13 @@ def test_partitioned_coordinators_share_the_executors(tmp_path, monkeypatch):
     aio.run(go())
 
 
-async def test_watch_relay_one_list_and_watch_per_kind_and_relist(tmp_path):
+@pytest.mark.parametrize("impl", ["native", "python"])
+async def test_watch_relay_one_list_and_watch_per_kind_and_relist(tmp_path, impl, monkeypatch):
     """Native mode with 2 shards × 2 executors: the controller apiserver serves one LIST and one WATCH per
     kind (the coordinator's; executors are fed by its watch relay).  After a 410 relist of the coordinator
     (watch history compacted while the apiserver was unreachable), executors get a fresh snapshot: a
     template changed and one deleted during the gap both reach the shards, with no executor LIST."""
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
     env = await FakeEnvironment(2, str(tmp_path)).start()
     cc, sc = env.controller_client(), env.shard_client(1)
     st = env.controller_server.state
@@ -578,13 +580,15 @@ async def test_watch_relay_one_list_and_watch_per_kind_and_relist(tmp_path):
         st.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
         st.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[f"c{i}"]))
     try:
-        async with Running(env, "native", executors_per_shard=2) as app:
-            assert app.relay is not None and len(app.pool.handles) == 4
+        async with Running(env, "native", executors_per_shard=2, executor_impl=impl) as app:
+            assert app.relay is not None and len(app.pool.handles) == 4 and app.executor_impl == impl
 
             async def all_synced():
                 return all(s.state.count(R.TEMPLATES) == 20 and s.state.count(R.SECRETS) == 20
                            for s in env.shard_servers)
             await wait_for(all_synced, timeout=20)
+            await wait_for(lambda: asyncio.sleep(0, st.stats["watch"] >= 4), timeout=5)
+            await asyncio.sleep(0.2)
             assert st.stats["list"] == 4 and st.stats["watch"] == 4, st.stats
 
             srv = env.controller_server
