@@ -255,6 +255,7 @@ async def run(args, d: Dist) -> dict | None:
                 for kv in args.extra_env:
                     k, _, v = kv.partition("=")
                     env[k] = v
+                env["NCC_TOPOLOGY_FILE"] = os.path.join(work, "topology.json")
                 log = open(os.path.join(work, "controller.log"), "wb")
                 t_boot = time.time_ns()
                 controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=log,
@@ -326,6 +327,10 @@ async def run(args, d: Dist) -> dict | None:
             d.sync()
             elapsed = time.perf_counter() - t_start
             ctrl_api = None
+            ctrl_state = {}
+            if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
+                with open(os.path.join(work, "topology.json")) as f:
+                    ctrl_state["sizing"] = json.load(f)
             if d.rank == 0:  # LIST/WATCH load the controller put on its own cluster (watch relay: 1 each per kind)
                 import aiohttp as _aiohttp
                 async with session.get(f"{ctrl_url}/_fake/stats", timeout=_aiohttp.ClientTimeout(total=30)) as r:
@@ -353,9 +358,8 @@ async def run(args, d: Dist) -> dict | None:
             # waves: the cost of the system under test, independent of how fast the fake apiservers are
             ctl_cpu = {k: cpu1.get(k, 0.0) - cpu0.get(k, 0.0) for k in ("coordinator", "executors")}
             us_per_obj = {k: round(v * 1e6 / objs, 1) for k, v in ctl_cpu.items()}
-            from ncc.app import auto_coordinator_partitions, auto_executors_per_shard, cpu_share
-            groups = d.world * S  # the controller's automatic sizing on this host (same rule, same cgroup)
-            k = auto_executors_per_shard(groups)
+            from ncc.app import cpu_share
+            sizing = ctrl_state.get("sizing") or {}
             ctrl_alive = controller.poll() is None
             return {
                 "metric": METRIC,
@@ -382,9 +386,8 @@ async def run(args, d: Dist) -> dict | None:
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
                 "controller_apiserver_load": ctrl_api,
-                "controller_sizing": {"cpus": cpu_share(), "executors_per_shard": k,
-                                      "coordinator_partitions": auto_coordinator_partitions(groups, k),
-                                      "overrides": [kv for kv in args.extra_env if kv.startswith("NEXUS__")]},
+                "controller_sizing": {"cpus": cpu_share(), **sizing,
+                                      "overrides": [kv for kv in args.extra_env if kv.startswith(("NEXUS__", "NCC_"))]},
                 # busy CPU cores per process over the timed steps (rank 0's, plus the busiest shard server)
                 "cpu_cores_busy": dict(utils[0], **{"shard-apiserver-max": max(u.get("shard-apiserver", 0.0)
                                                                                  for u in utils)}),

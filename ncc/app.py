@@ -125,7 +125,11 @@ def cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> float | None:
 
 
 def cpu_share() -> int:
-    """CPUs this process may really use: the affinity mask capped by the cgroup CPU quota."""
+    """CPUs this process may really use: the affinity mask capped by the cgroup CPU quota.
+    `NCC_CPU_SHARE=<n>` overrides it (rehearsing a large host's automatic sizing on a small one)."""
+    forced = os.environ.get("NCC_CPU_SHARE")
+    if forced:
+        return max(1, int(forced))
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):  # pragma: no cover - non-Linux
@@ -159,15 +163,40 @@ def auto_coordinator_partitions(groups: int, per_shard: int, cpus: int | None = 
     return per_shard
 
 
-def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int) -> tuple | None:
+def auto_sizing(groups: int, cpus: int | None = None, native: bool = False) -> tuple[int, int]:
+    """(executors per shard k, coordinator processes C) chosen automatically for `groups` shard groups.
+
+    Python executors: k = one per CPU share of a group (1..4), C = k once there are ≥ 4 groups and
+    ≥ 32 CPUs per coordinator (see the two functions above).
+
+    Native executors (ncc/bin/ncc-executor): k = 1.  One C++ process per shard costs ~24 µs of CPU per
+    synced object on the MI355X host and keeps up with a shard apiserver on its own
+    (profiles/r2/native_executor_box/: k=1 28.2k objects/s at 52 µs/object in total vs k=4 28.8k at
+    73 µs); extra partitions would only re-parse the same shard watch streams.  The coordinator then
+    carries the per-template work (status, adoption, Events, reports): C = one per 32 CPUs, up to 4,
+    once there are ≥ 4 shard groups."""
+    cpus = cpu_share() if cpus is None else cpus
+    if not native:
+        k = auto_executors_per_shard(groups, cpus)
+        return k, auto_coordinator_partitions(groups, k, cpus)
+    if groups < 4:
+        return 1, 1
+    return 1, max(1, min(4, cpus // 32))
+
+
+def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int, native: bool = False) -> tuple | None:
     """(p, C) for this coordinator process, or None when the coordinator is not split."""
     env = os.environ.get("NCC_COORDINATOR_PART")
     if env:  # a child started by CoordinatorPartitions
         pi, _, pk = env.partition("/")
         p, c = int(pi), int(pk)
         return (p, c) if c > 1 else None
-    c = cfg.coordinator_partitions if cfg.coordinator_partitions > 0 else \
-        auto_coordinator_partitions(groups, per_shard)
+    if cfg.coordinator_partitions > 0:
+        c = cfg.coordinator_partitions
+    elif native:
+        c = auto_sizing(groups, native=True)[1]
+    else:
+        c = auto_coordinator_partitions(groups, per_shard)
     return (0, c) if c > 1 else None
 
 
@@ -233,9 +262,11 @@ class App:
             self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
             if self.n_executors > 0:
                 o.role = "coordinator"
+                from .controller.native_executor import choose
+                native = choose(cfg, o, relay_active=cfg.watch_relay, quiet=True)[0]
                 self.per_shard = (cfg.executors_per_shard if cfg.executors_per_shard > 0
-                                  else auto_executors_per_shard(self.n_executors))
-                self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard)
+                                  else auto_sizing(self.n_executors, native=native)[0])
+                self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard, native)
                 if self.coord_part is not None:
                     o.partition = self.coord_part  # this coordinator's share of the template keys
                     # the k executors per shard are shared out among the C coordinators (k/C each, at least 1)
@@ -461,10 +492,23 @@ class App:
             self._gc_task = asyncio.ensure_future(gctune.freeze_loop())
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
+        topo_file = os.environ.get("NCC_TOPOLOGY_FILE")
+        if topo_file and self.options.role == "coordinator" and not os.environ.get("NCC_COORDINATOR_PART"):
+            with open(topo_file + ".tmp", "w") as f:  # for benchmarks / operators: what auto-sizing picked
+                json.dump(self.topology(), f)
+            os.replace(topo_file + ".tmp", topo_file)
         log.info("nexus-configuration-controller %s starting: mode=%s role=%s alias=%s namespace=%s shards=%s "
                  "executors=%d×%d (%s) workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
                  self.executor_impl or "in-process", self.options.workers, " (standing by)" if gated else "")
+
+    def topology(self) -> dict:
+        """The process layout this coordinator chose (automatic sizing or overrides)."""
+        parts = self.coord_part[1] if self.coord_part else 1
+        return {"shard_groups": self.n_executors, "executors_per_shard": self.per_shard * parts,
+                "coordinator_partitions": parts, "executor_impl": self.executor_impl or "in-process",
+                "executor_processes": len(self.pool.handles) if self.pool is not None else 0,
+                "watch_relay": self.relay is not None}
 
     def open_gate(self) -> None:
         """Leading now (or released by the parent): start reconciling here and in every child process."""

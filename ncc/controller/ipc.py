@@ -21,7 +21,12 @@ class Channel:
 
     def send(self, msg) -> None:
         """Queue a message; frames are coalesced and written on the next loop iteration."""
-        self._pending.append(msg)
+        self.send_packed(msgpack.packb(msg, use_bin_type=True))
+
+    def send_packed(self, packed: bytes) -> None:
+        """Queue an already msgpack-encoded message (the watch relay encodes a batch once for every
+        executor it goes to)."""
+        self._pending.append(packed)
         if self._flush_handle is None:
             self._flush_handle = asyncio.get_running_loop().call_soon(self._flush)
 
@@ -30,8 +35,14 @@ class Channel:
         if not self._pending or self.writer.is_closing():
             self._pending.clear()
             return
-        body = msgpack.packb(self._pending if len(self._pending) > 1 else self._pending[0], use_bin_type=True)
-        batch = len(self._pending) > 1
+        n = len(self._pending)
+        batch = n > 1
+        if batch:  # a msgpack array of the queued messages
+            head = bytes((0x90 | n,)) if n < 16 else (b"\xdc" + n.to_bytes(2, "big") if n < 65536
+                                                     else b"\xdd" + n.to_bytes(4, "big"))
+            body = head + b"".join(self._pending)
+        else:
+            body = self._pending[0]
         self._pending = []
         self.writer.write(_HDR.pack(len(body) | (0x80000000 if batch else 0)) + body)
         self.sent += 1

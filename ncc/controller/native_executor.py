@@ -36,8 +36,9 @@ def binary_path() -> str | None:
     return p if os.path.isfile(p) and os.access(p, os.X_OK) else None
 
 
-def choose(cfg, options, relay_active: bool) -> tuple[bool, str]:
-    """(use the native executor?, why not)."""
+def choose(cfg, options, relay_active: bool, quiet: bool = False) -> tuple[bool, str]:
+    """(use the native executor?, why not).  `relay_active`: the coordinator's watch relay feeds the
+    executors (a precondition: the native executor has no controller-cluster client)."""
     # NCC_EXECUTOR_IMPL overrides the config (lets a test run / CI job pin either implementation)
     impl = (os.environ.get("NCC_EXECUTOR_IMPL") or cfg.executor_impl or "auto").lower()
     if impl == "python":
@@ -50,7 +51,7 @@ def choose(cfg, options, relay_active: bool) -> tuple[bool, str]:
     if options.server_side_apply:
         reasons.append("server-side-apply is implemented by the Python executor only")
     if reasons:
-        if impl == "native":
+        if impl == "native" and not quiet:
             log.warning("executor-impl: native requested but unavailable (%s); using the Python executor",
                         "; ".join(reasons))
         return False, "; ".join(reasons)
@@ -95,7 +96,9 @@ class NativeExecutorConfig:
         shards = [await self.shard_entry(n) for n in handle.shards]
         doc = {
             "namespace": cfg.controller_namespace, "alias": cfg.alias,
-            "workers": max(256, 4 * cfg.client_pool_size), "pool_size": cfg.client_pool_size,
+            # one C++ process per shard carries all of its concurrency: like client-go's HTTP/2 connection
+            # (up to 250 concurrent streams) it keeps ≥ 256 requests in flight per shard
+            "workers": 4 * max(256, cfg.client_pool_size), "pool_size": max(256, cfg.client_pool_size),
             "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
             "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,
             "rate_limit_qps": o.rate_limit_qps, "rate_limit_burst": o.rate_limit_burst,

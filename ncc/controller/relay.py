@@ -30,6 +30,8 @@ import asyncio
 import logging
 from collections import deque
 
+import msgpack
+
 from .. import native as _native
 from ..api import resources as R
 from ..api.jsonenc import dumps_bytes
@@ -177,8 +179,7 @@ class WatchRelay:
         self.stats["snapshots"] += len(handles)
         lines = list(self.raw[kind].values())
         if self.parts <= 1 or self._mod is None:
-            for h in handles:
-                self._send(h, {"t": "s", "k": kind, "l": lines})
+            self._send_all(handles, {"t": "s", "k": kind, "l": lines})
             return
         per: dict = {id(h): [] for h in handles}
         for line in lines:
@@ -213,8 +214,7 @@ class WatchRelay:
                     raw[(sc[1], sc[2])] = line
                 keep.append(line)
             if keep:
-                for h in handles:
-                    self._send(h, {"t": "w", "k": kind, "l": keep})
+                self._send_all(handles, {"t": "w", "k": kind, "l": keep})
                 self.stats["lines_out"] += len(keep) * len(handles)
             return
         per: dict = {}
@@ -247,6 +247,15 @@ class WatchRelay:
         for h, ls in per.values():
             self._send(h, {"t": "w", "k": kind, "l": ls})
             self.stats["lines_out"] += len(ls)
+
+    def _send_all(self, handles: list, msg: dict) -> None:
+        """One encoding of `msg` for every executor it goes to."""
+        packed = msgpack.packb(msg, use_bin_type=True)
+        for h in handles:
+            ch = h.channel
+            if ch is not None:
+                ch.send_packed(packed)
+                self.stats["frames"] += 1
 
     def _send(self, handle, msg: dict) -> None:
         ch = handle.channel

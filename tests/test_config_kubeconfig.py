@@ -282,3 +282,17 @@ def test_executor_pool_global_partitions():
     for i in range(200):
         k = f"template/nexus/algo-{i:05d}"
         assert key_part(k, 6) % 3 == key_part(k, 3)
+
+
+def test_native_auto_sizing_and_cpu_override(monkeypatch):
+    """Native executors: one per shard; coordinator processes one per 32 CPUs (≤ 4) from 4 shards up.
+    NCC_CPU_SHARE rehearses a large host's sizing on a small one."""
+    from ncc.app import auto_sizing, cpu_share
+    assert auto_sizing(1, cpus=16, native=True) == (1, 1)
+    assert auto_sizing(4, cpus=16, native=True) == (1, 1)
+    assert auto_sizing(8, cpus=64, native=True) == (1, 2)
+    assert auto_sizing(8, cpus=128, native=True) == (1, 4)
+    assert auto_sizing(8, cpus=512, native=True) == (1, 4)
+    assert auto_sizing(8, cpus=128, native=False) == (4, 4)  # Python executors: k = C = 4
+    monkeypatch.setenv("NCC_CPU_SHARE", "128")
+    assert cpu_share() == 128
