@@ -814,6 +814,7 @@ static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
         if (it == inf.store.end()) return;
         ShardPtr old = it->second;
         inf.store.erase(it);
+        sh.memo[kind].erase(key);
         on_shard_event(sh, kind, old, nullptr, true);
         return;
     }
@@ -852,7 +853,10 @@ static Task<void> shard_list(Shard& sh, int kind, std::string list_rv) {
     }
     std::vector<ShardPtr> gone;
     for (auto& kv : inf.store)
-        if (!fresh.count(kv.first)) gone.push_back(kv.second);
+        if (!fresh.count(kv.first)) {
+            gone.push_back(kv.second);
+            sh.memo[kind].erase(kv.first);
+        }
     inf.store = std::move(fresh);
     inf.last_rv = rv;
     ++inf.relists;
@@ -955,7 +959,14 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
     Response r = co_await sh.client->request(method, target, &data);
     if (r.status >= 300) throw api_error(r.status, r.body);
     ShardPtr so = make_shard_obj(kind, parse(r.body));
-    sh.memo[kind][key_of(so->ns, so->name)] = Memo{so->rv, want_a, want_b};
+    // remember the intent only when the server stored something else (keeps the memo as small as the set
+    // of rewritten objects)
+    bool with_bin = kind == CONFIGMAPS && g_opt.sync_binary_data;
+    bool rewritten = kind < 2 ? so->fp_spec != want_a : (so->fp_data != want_a || (with_bin && so->fp_bin != want_b));
+    if (rewritten)
+        sh.memo[kind][key_of(so->ns, so->name)] = Memo{so->rv, want_a, want_b};
+    else
+        sh.memo[kind].erase(key_of(so->ns, so->name));
     shard_upsert(sh, kind, so, false);
     co_return so;
 }

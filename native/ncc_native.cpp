@@ -25,6 +25,8 @@
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
 //  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
+//  * members_equal(a, b, keys) — byte equality of named top-level members of two JSON objects, so a
+//    slim-cache writer sees whether the server rewrote its payload without decoding the response.
 
 #include <pybind11/pybind11.h>
 
@@ -46,7 +48,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 12
+#define NCC_NATIVE_ABI 13
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -394,6 +396,24 @@ class Scanner {
     // top-level object {"apiVersion":..., "metadata":{...}, ...} (a write response)
     bool scan_object(std::string_view& ns, std::string_view& name, std::string_view& rv) {
         return object_meta(ns, name, rv);
+    }
+
+    // raw JSON of the top-level members named in `keys` (out[i].data() == nullptr: absent)
+    bool members(const std::vector<std::string>& keys, std::vector<std::string_view>& out) {
+        out.assign(keys.size(), std::string_view());
+        if (!expect('{')) return false;
+        if (peek('}')) { ++p_; return true; }
+        for (;;) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            ws();
+            const char* s = p_;
+            if (!skip_value()) return false;
+            for (size_t i = 0; i < keys.size(); ++i)
+                if (key == keys[i]) out[i] = std::string_view(s, static_cast<size_t>(p_ - s));
+            if (peek(',')) { ++p_; continue; }
+            return expect('}');
+        }
     }
 
     bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
@@ -938,6 +958,28 @@ py::object scan_object(py::bytes body) {
                           py::str(rv.data(), rv.size()), py::str(uid.data(), uid.size()));
 }
 
+// members_equal(a, b, keys) -> True iff every top-level member named in `keys` has byte-identical raw
+// JSON in both objects (or is absent from both).  False when either is not a JSON object this scanner
+// reads (e.g. escaped keys): the caller then decodes.  A slim writer compares its request body with the
+// write response this way to see whether the server rewrote the payload (defaulting, pruning, webhooks).
+bool members_equal(py::bytes a, py::bytes b, py::sequence key_seq) {
+    std::vector<std::string> keys;
+    for (auto k : key_seq) keys.push_back(k.cast<std::string>());
+    char* pa = nullptr;
+    char* pb = nullptr;
+    Py_ssize_t na = 0, nb = 0;
+    if (PyBytes_AsStringAndSize(a.ptr(), &pa, &na) != 0 || PyBytes_AsStringAndSize(b.ptr(), &pb, &nb) != 0)
+        throw py::error_already_set();
+    std::vector<std::string_view> ma, mb;
+    Scanner sa(pa, static_cast<size_t>(na)), sb(pb, static_cast<size_t>(nb));
+    if (!sa.members(keys, ma) || !sb.members(keys, mb)) return false;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        if ((ma[i].data() == nullptr) != (mb[i].data() == nullptr)) return false;
+        if (ma[i].data() != nullptr && ma[i] != mb[i]) return false;
+    }
+    return true;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -959,6 +1001,8 @@ PYBIND11_MODULE(_native, m) {
     m.def("relay_scan", &relay_scan, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
           "(type_code, namespace, name, key_partition, owner_partition_mask, n_owners) of a watch line");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
+    m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
+          "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")

@@ -18,6 +18,11 @@ import json
 from .. import native as _native
 
 SLIM_FP = "__ncc_fp__"  # key under which slim-cache transforms store content digests
+# On a slim object published from our own write whose stored payload differs from what we sent (the
+# server defaulted, pruned or a webhook mutated it): the digests of what we sent.  That version counts as
+# in sync for exactly that intent; any later version (a new watch event, a relist) replaces the object
+# and the mark with it, so drift made by others is still seen.
+SLIM_WROTE = "__ncc_wrote__"
 
 
 def _py_fingerprint(v) -> int:

@@ -12,6 +12,7 @@ are reported, which on a real apiserver would be pruned (or rejected with strict
 """
 from __future__ import annotations
 
+import copy
 import os
 
 import yaml
@@ -79,6 +80,59 @@ def _walk(s: dict, v, path: str, errs: list) -> None:
     elif isinstance(v, list) and isinstance(s.get("items"), dict):
         for i, item in enumerate(v):
             _walk(s["items"], item, f"{path}[{i}]", errs)
+
+
+def default_and_prune(s: dict, v):
+    """Apply a structural schema's `default`s to missing properties and drop unknown fields of
+    non-preserving objects, in place — what a kube-apiserver does to every custom-resource body it
+    decodes (before validation).  Returns `v`."""
+    if isinstance(v, dict):
+        props = s.get("properties") or {}
+        addl = s.get("additionalProperties")
+        keep_unknown = addl is True or s.get("x-kubernetes-preserve-unknown-fields", False) or \
+            (not props and addl is None and not s.get("type"))
+        for k in list(v):
+            if k in props:
+                default_and_prune(props[k], v[k])
+            elif isinstance(addl, dict):
+                default_and_prune(addl, v[k])
+            elif not keep_unknown:
+                del v[k]
+        for k, sub in props.items():
+            if k not in v and "default" in sub:
+                v[k] = copy.deepcopy(sub["default"])
+                default_and_prune(sub, v[k])
+    elif isinstance(v, list) and isinstance(s.get("items"), dict):
+        for item in v:
+            default_and_prune(s["items"], item)
+    return v
+
+
+def version_schema(crd: dict, version: str | None = None) -> dict | None:
+    vers = (crd.get("spec") or {}).get("versions") or []
+    v = next((x for x in vers if version is None or x.get("name") == version), None)
+    if v is None:
+        return None
+    return ((v.get("schema") or {}).get("openAPIV3Schema")) or {}
+
+
+def default_and_prune_object(crd: dict, obj: dict, version: str | None = None) -> dict:
+    """default_and_prune of a custom resource's top-level fields but metadata/apiVersion/kind, in place."""
+    schema = version_schema(crd, version)
+    if schema is None:
+        return obj
+    props = schema.get("properties") or {}
+    for k in list(obj):
+        if k in ("metadata", "apiVersion", "kind"):
+            continue
+        if k in props:
+            default_and_prune(props[k], obj[k])
+        elif not schema.get("x-kubernetes-preserve-unknown-fields", False):
+            del obj[k]
+    for k, sub in props.items():
+        if k not in obj and "default" in sub:
+            obj[k] = default_and_prune(sub, copy.deepcopy(sub["default"]))
+    return obj
 
 
 def validate_object(crd: dict, obj: dict, version: str | None = None) -> list[str]:

@@ -19,7 +19,7 @@ import logging
 from ..api import constants as C
 from ..api import resources as R
 from ..api.constants import go_quote as q
-from ..api.fingerprint import SLIM_FP, fingerprint
+from ..api.fingerprint import SLIM_FP, SLIM_WROTE, fingerprint
 from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
 from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready_condition, same_references,
                         secret_names, template_owner_ref)
@@ -60,7 +60,11 @@ def spec_matches(desired_spec, shard_obj: dict, desired_fp: int | None = None) -
     lets a multi-shard pass fingerprint the desired spec once."""
     fp = shard_obj.get(SLIM_FP)
     if fp is not None:
-        return (desired_fp if desired_fp is not None else fingerprint(desired_spec)) == fp[0]
+        want = desired_fp if desired_fp is not None else fingerprint(desired_spec)
+        if want == fp[0]:
+            return True
+        wrote = shard_obj.get(SLIM_WROTE)  # the server rewrote our last write of exactly this spec
+        return wrote is not None and wrote[0] == want
     return desired_spec == shard_obj.get("spec")
 
 
@@ -68,9 +72,12 @@ def data_matches(src: dict, shard_obj: dict, with_binary: bool) -> bool:
     """reflect.DeepEqual(src.Data, shard.Data) (+ binaryData in native mode)."""
     fp = shard_obj.get(SLIM_FP)
     if fp is not None:
-        if fingerprint(src.get("data") or None) != fp[0]:
-            return False
-        return (not with_binary) or fingerprint(src.get("binaryData") or None) == fp[1]
+        want = (fingerprint(src.get("data") or None),
+                fingerprint(src.get("binaryData") or None) if with_binary else None)
+        for got in (fp, shard_obj.get(SLIM_WROTE)):  # as stored, or as our last write of it meant it
+            if got is not None and got[0] == want[0] and (not with_binary or got[1] == want[1]):
+                return True
+        return False
     if normalize_data(src.get("data")) != normalize_data(shard_obj.get("data")):
         return False
     return (not with_binary) or normalize_data(src.get("binaryData")) == normalize_data(shard_obj.get("binaryData"))

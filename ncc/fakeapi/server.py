@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import json
 import logging
 import os
 import random
@@ -375,6 +376,7 @@ class FakeApiServer:
             counts = {f"{g or 'core'}/{p}": self.state.count(rt) for (g, p), rt in self.state._types.items()}
             return self._json({"name": self.name, "rv": self.state.rv, "requests": self.requests,
                                "state": self.state.stats, "objects": counts, "faults": self.faults.as_dict(),
+                               "admission": self.state.admission.as_dict(),
                                "watchers": len(self.state._watchers)})
         if what == "faults" and request.method == "POST":
             body = self._body(request)
@@ -384,6 +386,9 @@ class FakeApiServer:
             if body.get("compact"):
                 self.state.compact()
             return self._json(self.faults.as_dict())
+        if what == "admission" and request.method == "POST":
+            self.state.admission.update(self._body(request))
+            return self._json(self.state.admission.as_dict())
         if what == "markers" and request.method == "POST":
             body = self._body(request)
             for plural, path in (body.get("specs") or {}).items():
@@ -459,6 +464,12 @@ async def serve(args) -> None:
     for m in args.marker:
         plural, _, path = m.partition("=")
         server.markers.add_spec(plural, path)
+    sets: dict = {}
+    for a in args.admission_set:  # plural=dotted.path=<json value>
+        plural, _, rest = a.partition("=")
+        path, _, value = rest.partition("=")
+        sets.setdefault(plural, {})[path] = json.loads(value)
+    server.state.admission.update({"prune_defaults": args.prune_defaults, "sets": sets})
     ctx = None
     if args.tls_cert:
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
@@ -506,6 +517,10 @@ def main(argv=None) -> None:
     p.add_argument("--tls-key")
     p.add_argument("--tls-client-ca", help="require client certificates signed by this CA (mutual TLS)")
     p.add_argument("--crd-dir", help="validate custom-resource writes against the CRDs in this directory")
+    p.add_argument("--prune-defaults", action="store_true",
+                   help="apply the --crd-dir schemas' defaults and prune unknown fields on writes (as an apiserver)")
+    p.add_argument("--admission-set", action="append", default=[], metavar="PLURAL=PATH=JSON",
+                   help="mutating-webhook stand-in: write this field into every create/update (repeatable)")
     p.add_argument("--bookmark-interval", type=float, default=5.0)
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
     p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")

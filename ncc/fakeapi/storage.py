@@ -36,6 +36,7 @@ from ..api.patch import apply_patch, json_patch, merge_patch, strategic_merge_pa
 from ..api.resources import ResourceType
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+from .admission import Admission
 
 RtKey = tuple  # (group, plural)
 
@@ -159,6 +160,7 @@ class ClusterState:
         self._dependents: dict[str, set] = {}  # owner uid -> {(rt_key, ns, name)}
         self.write_hooks: list[Callable[[str, ResourceType, dict], None]] = []
         self.crds: dict = {}  # (group, plural) -> CRD: writes of those kinds are schema-validated (422)
+        self.admission = Admission()  # server-side mutation of write bodies (defaulting/pruning, webhooks)
         self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
@@ -306,6 +308,8 @@ class ClusterState:
         if name in b:
             gr = f"{rt.plural}.{rt.group}" if rt.group else rt.plural
             raise E.AlreadyExists(f'{gr} "{name}" already exists', details={"name": name, "kind": rt.plural})
+        if self.admission.active:
+            self.admission.admit(rt, obj, self.crds.get((rt.group, rt.plural)))
         if self.crds:
             self._validate(rt, obj)
         if not self.simple:
@@ -369,6 +373,8 @@ class ClusterState:
                     new["status"] = cur["status"]
                 else:
                     new.pop("status", None)
+            if self.admission.active:
+                self.admission.admit(rt, new, self.crds.get((rt.group, rt.plural)))
             if rt.group and _content(new) != _content(cur):
                 nm["generation"] = int(cm.get("generation", 1)) + 1
         new["metadata"]["resourceVersion"] = cm.get("resourceVersion")

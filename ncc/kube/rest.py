@@ -92,6 +92,7 @@ def _query(params: dict) -> str:
 
 
 _scan_object = getattr(_native.load(), "scan_object", None)
+_members_equal = getattr(_native.load(), "members_equal", None)
 
 
 class RestClient(KubeClient):
@@ -284,10 +285,15 @@ class RestClient(KubeClient):
                                   content_type=patch_type)
 
     async def write_meta(self, verb: str, rt, namespace, body: dict, *, name: str | None = None,
-                         field_manager=None, patch_type=None, force=None) -> tuple:
+                         field_manager=None, patch_type=None, force=None, verify: tuple | None = None) -> tuple:
         """create/update/patch that returns only (namespace, name, resourceVersion, uid) of the stored object,
         read from the response by the native scanner instead of decoding it (slim-cache writers publish
-        their own request body; the server's echo of the payload is not needed)."""
+        their own request body; the server's echo of the payload is not needed).
+
+        `verify=(member, ...)` appends a fifth element: None when those top-level members of the response
+        are byte-identical to the request's (the server stored what we sent), else the decoded response —
+        the server rewrote the payload (CRD defaulting or pruning, a mutating webhook, or merely another
+        encoding of the same JSON) and the caller must publish what was stored, not what it sent."""
         params = {"fieldManager": field_manager}
         if verb == "create":
             method, path = "POST", rt.base_path(namespace)
@@ -314,11 +320,15 @@ class RestClient(KubeClient):
                 method, target, data, ctype, True, first=(resp.status, resp.body, resp.headers.get("retry-after")))
         else:
             raw = await self._exchange(method, target, data, ctype, True)
+        raw = bytes(raw) if not isinstance(raw, bytes) else raw
+        stored = None
+        if verify is not None and (_members_equal is None or not _members_equal(data, raw, verify)):
+            stored = json.loads(raw)
         sc = _scan_object(raw) if _scan_object is not None else None
         if sc is None:
-            m = (json.loads(raw) or {}).get("metadata") or {}
+            m = ((stored if stored is not None else json.loads(raw)) or {}).get("metadata") or {}
             sc = (m.get("namespace", ""), m.get("name", ""), m.get("resourceVersion", ""), m.get("uid", ""))
-        return sc
+        return sc if verify is None else sc + (stored,)
 
     async def delete(self, rt, namespace, name, *, propagation_policy=None, preconditions=None):
         body = None

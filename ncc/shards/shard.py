@@ -22,7 +22,7 @@ from __future__ import annotations
 
 from ..api import constants as C
 from ..api import resources as R
-from ..api.fingerprint import SLIM_FP, fingerprint
+from ..api.fingerprint import SLIM_FP, SLIM_WROTE, fingerprint
 from ..api.objects import ObjectKey, meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
@@ -59,6 +59,7 @@ class Shard:
         self.secret_lister = self.secret_informer.lister
         self.configmap_lister = self.configmap_informer.lister
         self.healthy = True  # flipped by the controller's per-shard circuit breaker
+        self.server_rewrites = 0  # writes whose stored payload differed from the request (see _tracked)
         # response-light writes need the native scanner and slim caches (see _tracked)
         self._write_meta = getattr(client, "write_meta", None) if (transforms and _native.load()) else None
         if assume_writes:
@@ -95,23 +96,37 @@ class Shard:
 
         With slim caches, full-object writes (create/update) publish the slim form of the request body
         with the new resourceVersion/uid read natively from the response — the echoed payload is never
-        decoded.  Partial writes (server-side apply) publish the decoded response."""
+        decoded — as long as the response's payload members are byte-identical to the request's.  When
+        the server stored something else (CRD defaulting/pruning, a mutating webhook), the response is
+        decoded and published as stored, marked with the digests of what we sent (SLIM_WROTE) so that
+        version is not rewritten on every pass.  Partial writes (server-side apply) publish the decoded
+        response, marked the same way when it differs from the applied payload."""
         if not self.assume_writes:
             return await self._call(rt, verb, namespace, name, body, field_manager, patch_type, force)
-        light = self._write_meta is not None and verb != "patch" and informer.store.transform is not None
+        transform = informer.store.transform
+        light = self._write_meta is not None and verb != "patch" and transform is not None
         key = ObjectKey(namespace, name)
         informer.begin_write(key)
         res = None
+        transformed = light
         try:
             if light:
-                _, _, rv, uid = await self._write_meta(verb, rt, namespace, body, name=name,
-                                                       field_manager=field_manager)
-                res = slim_written(rt, body, rv, uid)
+                _, _, rv, uid, stored = await self._write_meta(verb, rt, namespace, body, name=name,
+                                                               field_manager=field_manager,
+                                                               verify=_PAYLOAD_MEMBERS[rt.plural])
+                if stored is None:
+                    res = slim_written(rt, body, rv, uid)
+                else:
+                    self.server_rewrites += 1
+                    res = _mark_intent(rt, transform(stored), body)
             else:
                 res = await self._call(rt, verb, namespace, name, body, field_manager, patch_type, force)
+                if transform is not None and isinstance(res, dict):
+                    res = _mark_intent(rt, transform(res), body)
+                    transformed = True
             return res
         finally:
-            await informer.end_write(key, res if isinstance(res, dict) else None, transformed=light)
+            await informer.end_write(key, res if isinstance(res, dict) else None, transformed=transformed)
 
     # ---------------------------------------------------------------- templates
     async def create_template(self, name: str, namespace: str, spec, field_manager: str) -> dict:
@@ -259,8 +274,27 @@ class Shard:
         await self.client.delete(rt, m.get("namespace", ""), m.get("name", ""))
 
 
-_DROP_DEP = frozenset(("data", "binaryData", "stringData", SLIM_FP))
-_DROP_SPEC = frozenset(("spec", "status", SLIM_FP))
+_DROP_DEP = frozenset(("data", "binaryData", "stringData", SLIM_FP, SLIM_WROTE))
+_DROP_SPEC = frozenset(("spec", "status", SLIM_FP, SLIM_WROTE))
+# top-level members whose bytes must come back unchanged for a write to be published from its request body
+_PAYLOAD_MEMBERS = {R.TEMPLATES.plural: ("spec",), R.WORKGROUPS.plural: ("spec",),
+                    R.SECRETS.plural: ("data", "binaryData", "type"), R.CONFIGMAPS.plural: ("data", "binaryData")}
+
+
+def _payload_fp(rt: R.ResourceType, obj: dict) -> tuple:
+    if rt is R.SECRETS or rt is R.CONFIGMAPS:
+        return (fingerprint(obj.get("data") or None), fingerprint(obj.get("binaryData") or None))
+    return (fingerprint(obj.get("spec")),)
+
+
+def _mark_intent(rt: R.ResourceType, slim: dict, body: dict) -> dict:
+    """A slim object as the server stored it; when its payload differs from the request body's, remember
+    the digests of what we sent (see SLIM_WROTE)."""
+    if SLIM_FP in slim:
+        sent = _payload_fp(rt, body)
+        if sent != tuple(slim[SLIM_FP]):
+            slim[SLIM_WROTE] = sent
+    return slim
 
 
 def slim_written(rt: R.ResourceType, body: dict, rv: str, uid: str) -> dict:
@@ -273,14 +307,12 @@ def slim_written(rt: R.ResourceType, body: dict, rv: str, uid: str) -> dict:
     if uid:
         m["uid"] = uid
     out["metadata"] = m
-    if is_dep:
-        out[SLIM_FP] = (fingerprint(body.get("data") or None), fingerprint(body.get("binaryData") or None))
-    else:
-        out[SLIM_FP] = (fingerprint(body.get("spec")),)
+    out[SLIM_FP] = _payload_fp(rt, body)
     return out
 
 
 def _strip_slim(obj: dict) -> dict:
     """Drop the slim-cache digest key before an object is sent back to an apiserver."""
     obj.pop(SLIM_FP, None)
+    obj.pop(SLIM_WROTE, None)
     return obj
