@@ -187,13 +187,32 @@ def cpu_seconds(named: dict, rss: dict | None = None) -> dict:
             if rss is not None:
                 rss[name] = round(p.memory_info().rss / 2**20, 1)
             if name == "coordinator":
-                kids = p.children(recursive=True)
-                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in kids)
+                # children: shard executors (ncc-executor / -m ncc.executor) and, on large hosts, the
+                # coordinator partitions (-m ncc), whose cost is the coordinator's
+                ex, co = [], []
+                for c in p.children(recursive=True):
+                    try:
+                        cmd = " ".join(c.cmdline())
+                    except (psutil.Error, OSError):
+                        continue
+                    (ex if ("ncc-executor" in cmd or "ncc.executor" in cmd) else co).append(c)
+                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in ex)
+                out[name] += sum(sum(c.cpu_times()[:2]) for c in co)
                 if rss is not None:
-                    rss["executors"] = round(sum(c.memory_info().rss for c in kids) / 2**20, 1)
+                    rss["executors"] = round(sum(c.memory_info().rss for c in ex) / 2**20, 1)
+                    rss[name] += round(sum(c.memory_info().rss for c in co) / 2**20, 1)
         except (psutil.Error, OSError):
             pass
     return out
+
+
+def child_pids(proc) -> set:
+    """PIDs of every process under the controller (coordinator partitions, executors)."""
+    import psutil
+    try:
+        return {c.pid for c in psutil.Process(proc.pid).children(recursive=True)}
+    except (psutil.Error, OSError):
+        return set()
 
 
 def pct(xs, q):
@@ -305,6 +324,7 @@ async def run(args, d: Dist) -> dict | None:
                     d.sync()
                     t_start = time.perf_counter()
                     cpu0 = cpu_seconds(named)
+                    kids0 = child_pids(controller) if controller is not None else set()
                 t0 = None
                 if d.rank == 0:
                     a = await post(session, f"{ctrl_url}/_fake/apply", bodies.pop(step))
@@ -339,6 +359,7 @@ async def run(args, d: Dist) -> dict | None:
                             "requests": st["requests"]["total"]}
             rss: dict = {}
             cpu1 = cpu_seconds(named, rss)
+            kids1 = child_pids(controller) if controller is not None else set()
             util = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 3) for k in cpu1}
             utils = d.all_gather(util)
             rsses = d.all_gather(rss)
@@ -385,6 +406,8 @@ async def run(args, d: Dist) -> dict | None:
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,
+                # processes under the controller over the timed waves; a restarted child shows as replaced
+                "controller_children": {"start": len(kids0), "end": len(kids1), "replaced": len(kids0 - kids1)},
                 "controller_apiserver_load": ctrl_api,
                 "controller_sizing": {"cpus": cpu_share(), **sizing,
                                       "overrides": [kv for kv in args.extra_env if kv.startswith(("NEXUS__", "NCC_"))]},

@@ -100,3 +100,35 @@ def test_bench_two_ranks_over_gloo():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["shards"] == 2 and res["scaling"] == "weak"
     assert res["value"] > 0 and res["p50_latency_ms"] is not None and res["controller_alive"]
+
+
+@pytest.mark.slow
+def test_bench_eight_ranks_auto_sized_topology():
+    """The driver's N=8 launch on a large host, rehearsed here: NCC_CPU_SHARE=128 makes the automatic
+    sizing pick what it would on an 8-GPU node with ≥128 CPUs (ncc/app.py `auto_sizing`: native executors,
+    k=1 per shard, C=4 coordinator partitions → 3 partition children + 4×8 executors under the controller).
+    Every wave must converge with no process restarted and the controller alive."""
+    pytest.importorskip("torch.distributed")
+    from ncc.app import auto_sizing
+    from ncc.controller.native_executor import binary_path
+    native = binary_path() is not None
+    k, c = auto_sizing(8, cpus=128, native=native)
+    env = dict(os.environ, NCC_CPU_SHARE="128")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--templates", "40", "--steps", "2", "--warmup", "1", "--timeout", "120"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 8 and res["config"]["shards"] == 8 and res["controller_alive"]
+    sz = res["controller_sizing"]
+    per_coord = max(1, k // c)  # each coordinator partition keeps its share of the k executors per shard
+    assert sz["cpus"] == 128 and sz["coordinator_partitions"] == c and sz["executors_per_shard"] == per_coord * c
+    assert sz["executor_impl"] == ("native" if native else "python")
+    want_children = (c - 1) + c * 8 * per_coord
+    ch = res["controller_children"]
+    assert ch == {"start": want_children, "end": want_children, "replaced": 0}, (ch, sz)
+    assert res["value"] > 0 and res["p50_latency_ms"] is not None
+    print(json.dumps(res))
