@@ -22,6 +22,11 @@ ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "ncc_native.cpp")]
 
 
+def _werror() -> list:
+    """NCC_WERROR=1 (the CI lint job): warnings fail the build."""
+    return ["-Werror"] if os.environ.get("NCC_WERROR") == "1" else []
+
+
 def target_path() -> str:
     return os.path.join(ROOT, "ncc", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -48,7 +53,7 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
             return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
-    flags = ["-std=c++20", "-fcoroutines", "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"]
+    flags = ["-std=c++20", "-fcoroutines", "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"] + _werror()
     if debug or sanitize:
         flags += ["-O1", "-fno-omit-frame-pointer"]
     else:
@@ -80,7 +85,8 @@ def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) ->
         if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
-    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra",
+             "-Wno-unused-parameter"] + _werror()
     if debug or sanitize:
         flags += ["-O1", "-g", "-fno-omit-frame-pointer"]
     else:

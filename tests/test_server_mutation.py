@@ -24,7 +24,7 @@ from ncc.api import resources as R
 from ncc.api.fingerprint import SLIM_FP, SLIM_WROTE, fingerprint
 from ncc.api.schema import default_and_prune, default_and_prune_object
 from ncc.fakeapi.admission import Admission
-from test_e2e import NS, Running, _get, mutate, wait_for
+from test_e2e import NS, Running, mutate, wait_for
 from ncc.testing.env import FakeEnvironment
 from ncc.testing.workload import make_configmap, make_secret, make_template
 
