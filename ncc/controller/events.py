@@ -41,6 +41,14 @@ class EventRecorder:
         raise NotImplementedError
 
 
+def _bound(cache: dict, limit: int = 4096) -> None:
+    """Keep a correlator cache within client-go's 4096 entries (maxLruCacheEntries): past the limit the
+    oldest quarter goes (insertion order), so a controller that has seen many objects does not grow."""
+    if len(cache) > limit:
+        for k in list(cache)[:limit // 4]:
+            del cache[k]
+
+
 class FakeRecorder(EventRecorder):
     """client-go record.FakeRecorder: with `keep=False` events are discarded (as in the reference tests)."""
 
@@ -134,6 +142,7 @@ class BroadcastRecorder(EventRecorder):
         b = self._buckets.get(k)
         if b is None:
             b = self._buckets[k] = TokenBucket(SPAM_QPS, SPAM_BURST, now=now)
+            _bound(self._buckets)
         return b.reserve(now) <= 0.0 or self._refund(b)
 
     @staticmethod
@@ -148,6 +157,7 @@ class BroadcastRecorder(EventRecorder):
             msgs, first = set(), now
         msgs.add(message)
         self._similar[akey] = (msgs, first)
+        _bound(self._similar)
         if len(msgs) >= AGGREGATE_MAX_EVENTS:
             return "(combined from similar events): " + message, akey
         return message, akey + (message,)
@@ -195,9 +205,7 @@ class BroadcastRecorder(EventRecorder):
         else:
             res = await self.client.create(R.EVENTS, ns, ev)
         self._seen[key] = res if isinstance(res, dict) else ev
-        if len(self._seen) > 4096:  # LRU-ish bound like client-go's 4096-entry cache
-            for k in list(self._seen)[:1024]:
-                del self._seen[k]
+        _bound(self._seen)
         self.stats["created"] += 1
 
     async def _run(self, queue: asyncio.Queue) -> None:

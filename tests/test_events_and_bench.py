@@ -69,6 +69,24 @@ async def test_event_writers_keep_per_object_order():
     await rec.stop()
 
 
+async def test_event_correlator_caches_are_bounded():
+    """client-go keeps its correlator state in 4096-entry LRUs; so do we (no growth with object count)."""
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False, writers=4)
+    rec.start()
+    for i in range(5000):
+        rec.event({"kind": "NexusAlgorithmTemplate", "apiVersion": "science.sneaksanddata.com/v1",
+                   "metadata": {"name": f"t{i}", "namespace": "nexus", "uid": f"u{i}"}},
+                  "Normal", "Synced", "synced")
+        if i % 500 == 499:
+            await _drain(rec)
+    await _drain(rec)
+    assert rec.stats["created"] == 5000
+    for cache in (rec._buckets, rec._similar, rec._seen):
+        assert 0 < len(cache) <= 4096
+    await rec.stop()
+
+
 def test_fake_recorder_formats_like_client_go():
     r = FakeRecorder()
     r.event({}, "Warning", "ErrResourceMissing", "msg")
