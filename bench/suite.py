@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Benchmark suite for the five BASELINE.json configurations, native vs reference-compat mode.
 
-    python bench/suite.py --configs 1,2,3,4,5 --modes native,compat [--scale 1.0] [--out results.json]
+    python bench/suite.py --configs 1,2,3,4,5 --modes native,compat-unthrottled,compat [--scale 1.0] [--out results.json]
 
 Every configuration runs on real processes: one fake kube-apiserver process per cluster
 (controller + N shards) and the controller as `python -m ncc` (which in native mode spawns its
@@ -19,8 +19,10 @@ shard commit time − controller commit time for every object, no client-side wa
 
 Reference-compat mode reproduces the reference controller's scheduling (sequential fail-fast
 shard loop, client-go 5 QPS/10 burst per API group, Event per reconcile, 2 workers).  It is a
-semantic reproduction on the same substrate, not the Go binary.  `--compat-cap N` bounds the
-template count of compat runs whose full size would take hours; capped runs are labelled.
+semantic reproduction on the same substrate, not the Go binary.  `compat-unthrottled` is the same
+scheduling without the client-side 5/10 limiter, separating the gain of native mode's concurrency
+and executors from the gain of removing the throttle.  `--compat-cap N` / `--unthrottled-cap N`
+bound the template count of runs whose full size would take hours; capped runs are labelled.
 """
 from __future__ import annotations
 
@@ -46,6 +48,10 @@ from ncc.testing.workload import (configmap_name, make_configmap, make_secret, m
 
 NS = "nexus"
 MARKERS = ["nexusalgorithmtemplates=spec.container.versionTag", "secrets=data.version", "configmaps=data.version"]
+# suite mode -> controller environment (same table as bench.py's MODES)
+MODE_ENV = {"native": {"NEXUS__MODE": "native"},
+            "compat": {"NEXUS__MODE": "compat"},
+            "compat-unthrottled": {"NEXUS__MODE": "compat", "NEXUS__CLIENT_QPS": "-1"}}
 
 
 def b64(s: str) -> str:
@@ -112,8 +118,9 @@ class Topology:
         env = dict(os.environ)
         env.update({"NEXUS__CONTROLLER_CONFIG_PATH": self.ckc, "NEXUS__SHARD_CONFIG_PATH": self.shard_dir,
                     "NEXUS__CONTROLLER_NAMESPACE": NS, "NEXUS__ALIAS": "controller-cluster",
-                    "NEXUS__MODE": self.mode, "NEXUS__LOG_LEVEL": "WARNING",
+                    "NEXUS__LOG_LEVEL": "WARNING",
                     "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        env.update(MODE_ENV[self.mode])
         env["NEXUS__WORKERS"] = str(self.workers or (64 if self.mode == "native" else 2))
         env.update(self.extra_env)
         self.log = open(os.path.join(self.work, "controller.log"), "wb")
@@ -393,7 +400,8 @@ async def _run(args) -> list:
 
     def size(T, mode):
         T = max(1, int(T * s))
-        return min(T, cap) if mode == "compat" and cap else T
+        c = {"compat": cap, "compat-unthrottled": args.unthrottled_cap}.get(mode, 0)
+        return min(T, c) if c else T
 
     for mode in args.modes:
         for c in args.configs:
@@ -414,8 +422,9 @@ async def _run(args) -> list:
             else:
                 continue
             r["wall_s"] = round(time.perf_counter() - t, 1)
-            if mode == "compat" and cap:
-                r["compat_capped_templates"] = cap
+            c = {"compat": cap, "compat-unthrottled": args.unthrottled_cap}.get(mode, 0)
+            if c:
+                r["compat_capped_templates"] = c
             print(json.dumps(r), flush=True)
             results.append(r)
             if args.out:  # keep partial results if a later configuration is cut short
@@ -427,9 +436,11 @@ async def _run(args) -> list:
 def main():
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--configs", default="1,2,3,4,5")
-    p.add_argument("--modes", default="native,compat")
+    p.add_argument("--modes", default="native,compat-unthrottled,compat")
     p.add_argument("--scale", type=float, default=1.0, help="multiply template counts (e.g. 0.1 for a quick run)")
     p.add_argument("--compat-cap", type=int, default=100, help="max templates for compat runs (0 = no cap)")
+    p.add_argument("--unthrottled-cap", type=int, default=1000,
+                   help="max templates for compat-unthrottled runs (0 = no cap)")
     p.add_argument("--churn-seconds", type=float, default=30.0)
     p.add_argument("--timeout", type=float, default=600.0)
     p.add_argument("--out", default="")
