@@ -410,7 +410,7 @@ async def _run(args) -> list:
                 r = await config_cold_and_waves(1, size(10, mode), mode, waves=5, timeout=args.timeout,
                                                 configmaps=False, label="1: 1 shard, 10 templates x 1 Secret")
             elif c == 2:
-                r = await config_cold_and_waves(2, size(100, mode), mode, waves=3, timeout=args.timeout,
+                r = await config_cold_and_waves(2, size(100, mode), mode, waves=10, timeout=args.timeout,
                                                 label="2: 2 shards, 100 templates x (Secret+ConfigMap)")
             elif c == 3:
                 r = await config3_churn(mode, size(1000, mode), rate=10.0, duration=args.churn_seconds,

@@ -42,6 +42,10 @@
 #include <unordered_map>
 #include <unordered_set>
 
+#ifdef NCC_GPROF
+extern "C" void _mcleanup(void);
+#endif
+
 #include "http.hpp"
 #include "json.hpp"
 #include "loop.hpp"
@@ -588,10 +592,17 @@ struct Executor {
         return it == ctl[k].end() ? nullptr : it->second;
     }
 
+    // Event-driven enqueue.  Inside a burst (another event less than one coalesce window ago) the key is
+    // parked for the window, so a template and its Secret/ConfigMap changing together reconcile once; an
+    // isolated change after a quiet window goes straight to the workers and pays no coalescing delay.
+    double last_event = -1e18;
     void enqueue(int kind, const std::string& ns, const std::string& name) {
         if (!in_partition(ns, name)) return;
         std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
-        if (g_opt.coalesce > 0)
+        double now = now_s();
+        bool burst = now - last_event < g_opt.coalesce;
+        last_event = now;
+        if (g_opt.coalesce > 0 && burst)
             queue.add_after(key, g_opt.coalesce);
         else
             queue.add(key);
@@ -1529,5 +1540,8 @@ int main(int argc, char** argv) {
         return 1;
     }
     std::fflush(stderr);
+#ifdef NCC_GPROF
+    _mcleanup();  // profiling builds (-pg): write gmon.out before skipping the exit handlers
+#endif
     std::_Exit(0);  // skip destructors of still-suspended coroutines
 }

@@ -71,6 +71,7 @@ class Controller(ReconcileMixin):
                                         qps=o.rate_limit_qps, burst=o.rate_limit_burst, native=o.native_queue)
         self._pending_deletes: set = set()
         self._pending_workgroup_deletes: set = set()
+        self._last_event = float("-inf")  # monotonic time of the last event-driven enqueue (coalescing)
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
@@ -192,15 +193,21 @@ class Controller(ReconcileMixin):
 
     def _enqueue_key(self, key: str) -> None:
         """Event-driven enqueue; native mode coalesces bursts (a template and its Secret/ConfigMap
-        changing together) into one reconcile by parking the key for `coalesce_window` seconds."""
+        changing together) into one reconcile by parking the key for `coalesce_window` seconds.  Only
+        inside a burst — another event less than one window ago: an isolated change after a quiet window
+        is reconciled at once and pays no coalescing delay."""
         part = self.options.partition
         if part is not None and key_part(key, part[1]) != part[0]:
             return  # another executor of this shard group owns the key
         w = self.options.coalesce_window
         if w > 0:
-            self.queue.add_after(key, w)
-        else:
-            self.queue.add(key)
+            now = time.monotonic()
+            burst = now - self._last_event < w
+            self._last_event = now
+            if burst:
+                self.queue.add_after(key, w)
+                return
+        self.queue.add(key)
 
     def _unwrap(self, obj):
         if isinstance(obj, DeletedFinalStateUnknown):
