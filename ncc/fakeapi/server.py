@@ -12,6 +12,10 @@ Test/bench control endpoints (not part of the Kubernetes API):
                         "down", "drop_watches", "compact"} — fault injection for the
                        retry/backoff benchmark (BASELINE.json config 5)
   POST /_fake/objects  bulk create `{"items": [...]}` without per-request overhead (bench seeding)
+  POST /_fake/apply    `{"items": [...], "yield_every": n}` create-or-update a wave of user changes,
+                       committed in slices of n with watch delivery in between; `{"staged": id}`
+                       commits a body sent earlier to
+  POST /_fake/stage    `{"id": id, "items": [...], ...}` (decoded ahead of a timed apply)
 """
 from __future__ import annotations
 
@@ -90,6 +94,7 @@ class FakeApiServer:
         self.bookmark_interval = bookmark_interval
         self.faults = Faults()
         self.markers = MarkerTracker()
+        self.staged: dict[str, dict] = {}  # /_fake/stage: pre-decoded apply bodies by id
         self.state.write_hooks.append(self.markers.on_write)
         self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
         self._streams: set = set()
@@ -405,8 +410,16 @@ class FakeApiServer:
                 out["times"] = {f"{w['plural']}={w['value']}": self.markers.times(w["plural"], w["value"], keyed)
                                 for w in want}
             return self._json(out)
+        if what == "stage" and request.method == "POST":
+            # a load generator's apply body, decoded ahead of time and committed later by
+            # {"staged": id} — so a timed apply measures commits, not the decoding of the request
+            body = self._body(request)
+            self.staged[str(body["id"])] = body
+            return self._json({"staged": str(body["id"]), "items": len(body.get("items") or [])})
         if what == "apply" and request.method == "POST":
             body = self._body(request)
+            if "staged" in body:
+                body = self.staged.pop(str(body["staged"]))
             t0 = time.time_ns()
             n = 0
             # yield_every > 0 lets watch streams flush while a large apply is in progress (commits and
