@@ -567,6 +567,8 @@ struct Shard {
     }
 };
 
+constexpr double kDependentHold = 5.0;  // coalesce windows a dependent-triggered pass waits in a burst
+
 struct PassState {
     bool wrote = false;
 };
@@ -595,15 +597,18 @@ struct Executor {
     // Event-driven enqueue.  Inside a burst (another event less than one coalesce window ago) the key is
     // parked for the window, so a template and its Secret/ConfigMap changing together reconcile once; an
     // isolated change after a quiet window goes straight to the workers and pays no coalescing delay.
+    // A pass triggered by a dependent is parked `hold` windows: users roll a new configuration out
+    // dependents first, and the template's own event (relayed over another watch stream, so often a
+    // loop iteration later) pulls the pass in to one window — one pass instead of two.
     double last_event = -1e18;
-    void enqueue(int kind, const std::string& ns, const std::string& name) {
+    void enqueue(int kind, const std::string& ns, const std::string& name, double hold = 1.0) {
         if (!in_partition(ns, name)) return;
         std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
         double now = now_s();
         bool burst = now - last_event < g_opt.coalesce;
         last_event = now;
         if (g_opt.coalesce > 0 && burst)
-            queue.add_after(key, g_opt.coalesce);
+            queue.add_after(key, g_opt.coalesce * hold);
         else
             queue.add(key);
     }
@@ -695,13 +700,13 @@ static void on_dependent(int kind, const CtlObj& obj) {
         for (const auto& tkey : it->second) {
             std::string tname = tkey.substr(tkey.find('/') + 1);
             seen.insert(tname);
-            ex.enqueue(TEMPLATES, obj.ns, tname);
+            ex.enqueue(TEMPLATES, obj.ns, tname, kDependentHold);
         }
     }
     for (const auto& owner : obj.owners) {
         if (seen.count(owner)) continue;
         if (!ex.cget(TEMPLATES, key_of(obj.ns, owner))) return;  // stops at the first orphaned owner
-        ex.enqueue(TEMPLATES, obj.ns, owner);
+        ex.enqueue(TEMPLATES, obj.ns, owner, kDependentHold);
     }
 }
 
