@@ -36,13 +36,28 @@ inline double now_s() {
 template <class T>
 class Task;
 
+// Stack guard for symmetric transfer.  A finished task resumes its awaiter by symmetric transfer, which
+// is a tail call only when the compiler makes it one: at -O0/-O1 or under ASan GCC emits a nested call, so
+// a worker whose awaits keep completing synchronously (queue never empty, nothing to write) grows the
+// stack without bound.  Past kMaxNest bytes below the loop's frame the continuation is posted to the
+// loop instead, which unwinds the stack; release builds never get near it.
+inline char* g_stack_base = nullptr;                  // set by Loop::run
+inline void (*g_post)(std::coroutine_handle<>) = nullptr;  // Loop::post of the running loop
+constexpr std::ptrdiff_t kMaxNest = 256 * 1024;
+
 namespace detail {
 struct FinalAwaiter {
     bool await_ready() noexcept { return false; }
     template <class P>
     std::coroutine_handle<> await_suspend(std::coroutine_handle<P> h) noexcept {
         auto c = h.promise().cont;
-        return c ? c : std::noop_coroutine();
+        if (!c) return std::noop_coroutine();
+        char probe;
+        if (g_stack_base != nullptr && g_post != nullptr && g_stack_base - &probe > kMaxNest) {
+            g_post(c);
+            return std::noop_coroutine();
+        }
+        return c;
     }
     void await_resume() noexcept {}
 };
@@ -126,6 +141,8 @@ private:
 };
 
 // ------------------------------------------------------------------------------------ Loop
+inline void g_loop_post(std::coroutine_handle<> h);
+
 class Loop {
 public:
     Loop() {
@@ -196,6 +213,9 @@ public:
     bool stopped() const { return stopped_; }
 
     void run() {
+        char base;
+        g_stack_base = &base;
+        g_post = &g_loop_post;
         epoll_event evs[256];
         while (!stopped_) {
             while (!ready_.empty() || !calls_.empty()) {
@@ -267,6 +287,7 @@ private:
 
 inline Loop* g_loop = nullptr;
 inline Loop& loop() { return *g_loop; }
+inline void g_loop_post(std::coroutine_handle<> h) { g_loop->post(h); }
 
 // ------------------------------------------------------------------------------------ Event
 // Level-triggered flag with waiters (asyncio.Event).
