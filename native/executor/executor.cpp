@@ -567,7 +567,12 @@ struct Shard {
     }
 };
 
-constexpr double kDependentHold = 5.0;  // coalesce windows a dependent-triggered pass waits in a burst
+constexpr double kDependentHold = 5.0;
+// enqueues by cause (NCC_CPU_REPORT diagnostics): template/workgroup event, dependent event, shard-side
+// template drift, shard-side dependent drift, failure retry, orphan sweep, full resync, delete
+enum EnqCause { ENQ_OBJECT, ENQ_DEPENDENT, ENQ_SHARD_OBJECT, ENQ_SHARD_DEPENDENT, ENQ_RETRY, ENQ_SWEEP, ENQ_RESYNC,
+                ENQ_DELETE, ENQ_N };
+static long long g_enq[ENQ_N] = {};  // coalesce windows a dependent-triggered pass waits in a burst
 
 struct PassState {
     bool wrote = false;
@@ -700,12 +705,14 @@ static void on_dependent(int kind, const CtlObj& obj) {
         for (const auto& tkey : it->second) {
             std::string tname = tkey.substr(tkey.find('/') + 1);
             seen.insert(tname);
+            ++g_enq[ENQ_DEPENDENT];
             ex.enqueue(TEMPLATES, obj.ns, tname, kDependentHold);
         }
     }
     for (const auto& owner : obj.owners) {
         if (seen.count(owner)) continue;
         if (!ex.cget(TEMPLATES, key_of(obj.ns, owner))) return;  // stops at the first orphaned owner
+        ++g_enq[ENQ_DEPENDENT];
         ex.enqueue(TEMPLATES, obj.ns, owner, kDependentHold);
     }
 }
@@ -717,6 +724,7 @@ static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool de
         if (deleted) {
             if (kind == TEMPLATES || g_opt.propagate_workgroup_deletes) {
                 if (in_partition(o.ns, o.name)) ex.pending_deletes[kind].insert(key_of(o.ns, o.name));
+                ++g_enq[ENQ_DELETE];
                 ex.enqueue(kind, o.ns, o.name);
             }
             return;
@@ -727,6 +735,7 @@ static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool de
                 old->fp_ann == cur->fp_ann && old->fp_spec == cur->fp_spec)
                 return;
         }
+        ++g_enq[ENQ_OBJECT];
         ex.enqueue(kind, o.ns, o.name);
         return;
     }
@@ -764,7 +773,10 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     if (kind == TEMPLATES || kind == WORKGROUPS) {
         CtlPtr c = ex.cget(kind, key_of(o.ns, o.name));
         if (!c) return;
-        if (deleted || !spec_in_sync(sh, kind, o, c->fp_spec)) ex.enqueue(kind, o.ns, o.name);
+        if (deleted || !spec_in_sync(sh, kind, o, c->fp_spec)) {
+            ++g_enq[ENQ_SHARD_OBJECT];
+            ex.enqueue(kind, o.ns, o.name);
+        }
         return;
     }
     CtlPtr src = ex.cget(kind, key_of(o.ns, o.name));
@@ -774,7 +786,10 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     for (const auto& p : o.template_owners) owners.push_back(p.first);
     if (owners.empty()) owners = src->owners;
     for (const auto& n : owners)
-        if (ex.cget(TEMPLATES, key_of(o.ns, n))) ex.enqueue(TEMPLATES, o.ns, n);
+        if (ex.cget(TEMPLATES, key_of(o.ns, n))) {
+            ++g_enq[ENQ_SHARD_DEPENDENT];
+            ex.enqueue(TEMPLATES, o.ns, n);
+        }
 }
 
 // Keep a shard object in this executor's cache?  Templates/workgroups of our key partition; dependents
@@ -1285,6 +1300,7 @@ static Task<void> worker() {
         } else {
             ++ex.stats_errors;
             LOG_INFO("Error syncing %s; re-queuing for later retry: %s", key.c_str(), err.c_str());
+            ++g_enq[ENQ_RETRY];
             ex.queue.add_rate_limited(key);
         }
         ex.queue.done(key);
@@ -1297,7 +1313,10 @@ static void sweep_orphans() {
         for (int kind : {TEMPLATES, WORKGROUPS}) {
             if (kind == WORKGROUPS && !g_opt.propagate_workgroup_deletes) continue;
             for (auto& kv : sp->inf[kind].store)
-                if (is_ours(*kv.second) && !ex.cget(kind, kv.first)) ex.enqueue(kind, kv.second->ns, kv.second->name);
+                if (is_ours(*kv.second) && !ex.cget(kind, kv.first)) {
+                    ++g_enq[ENQ_SWEEP];
+                    ex.enqueue(kind, kv.second->ns, kv.second->name);
+                }
         }
     }
 }
@@ -1305,7 +1324,10 @@ static void sweep_orphans() {
 static void enqueue_all() {
     Executor& ex = *g_ex;
     for (int kind : {TEMPLATES, WORKGROUPS})
-        for (auto& kv : ex.ctl[kind]) ex.enqueue(kind, kv.second->ns, kv.second->name);
+        for (auto& kv : ex.ctl[kind]) {
+            ++g_enq[ENQ_RESYNC];
+            ex.enqueue(kind, kv.second->ns, kv.second->name);
+        }
 }
 
 static Task<void> full_resync_loop() {
@@ -1472,6 +1494,12 @@ static Task<void> run_main() {
     LOG_INFO("native executor %d ready: %zu shard(s), partition %d/%d, %d workers", g_opt.index, ex.shards.size(),
              g_opt.part, g_opt.parts, g_opt.workers);
     co_await ex.stop_ev.wait();
+    if (std::getenv("NCC_CPU_REPORT"))
+        LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld enqueues: object=%lld dependent=%lld "
+                 "shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",
+                 ex.stats_reconciles, ex.stats_writes, ex.stats_errors, g_enq[ENQ_OBJECT], g_enq[ENQ_DEPENDENT],
+                 g_enq[ENQ_SHARD_OBJECT], g_enq[ENQ_SHARD_DEPENDENT], g_enq[ENQ_RETRY], g_enq[ENQ_SWEEP],
+                 g_enq[ENQ_RESYNC], g_enq[ENQ_DELETE]);
     ex.queue.shutdown();
     co_await g_chan->drain(2.0);
     loop().stop();
