@@ -48,7 +48,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 13
+#define NCC_NATIVE_ABI 14
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -285,6 +285,12 @@ class RateLimitingQueue {
     size_t waiting() {
         std::lock_guard<std::mutex> g(mu_);
         return waiting_ready_.size();
+    }
+
+    // Queued, being processed or waiting for a delayed add: a worker pass for the key is pending or running.
+    bool busy(const std::string& key) {
+        std::lock_guard<std::mutex> g(mu_);
+        return dirty_.count(key) || processing_.count(key) || waiting_ready_.count(key);
     }
 
     // RateLimiting: MaxOf(ItemExponentialFailure(base, max), Bucket(qps, burst))
@@ -1020,6 +1026,7 @@ PYBIND11_MODULE(_native, m) {
         .def("promote", &RateLimitingQueue::promote)
         .def("next_ready_in", &RateLimitingQueue::next_ready_in)
         .def("waiting", &RateLimitingQueue::waiting)
+        .def("busy", &RateLimitingQueue::busy)
         .def("add_rate_limited", &RateLimitingQueue::add_rate_limited)
         .def("forget", &RateLimitingQueue::forget)
         .def("num_requeues", &RateLimitingQueue::num_requeues);

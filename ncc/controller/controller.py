@@ -75,7 +75,9 @@ class Controller(ReconcileMixin):
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
-                      "reports_pending": 0, "early_passes_skipped": 0}
+                      "reports_pending": 0, "early_passes_skipped": 0, "inline_finishes": 0}
+        self._inline_keys: set = set()  # coordinator: keys with a complete report set, finished in one batch
+        self._inline_timer = None
         self.ready = asyncio.Event()  # workers running
         self.caches_synced = asyncio.Event()  # controller (and shard) caches synced
         self.role = o.role
@@ -199,15 +201,21 @@ class Controller(ReconcileMixin):
         part = self.options.partition
         if part is not None and key_part(key, part[1]) != part[0]:
             return  # another executor of this shard group owns the key
+        delay = self._coalesce_delay()
+        if delay > 0:
+            self.queue.add_after(key, delay)
+        else:
+            self.queue.add(key)
+
+    def _coalesce_delay(self) -> float:
+        """The coalesce window inside a burst (another event less than one window ago), else 0."""
         w = self.options.coalesce_window
-        if w > 0:
-            now = time.monotonic()
-            burst = now - self._last_event < w
-            self._last_event = now
-            if burst:
-                self.queue.add_after(key, w)
-                return
-        self.queue.add(key)
+        if w <= 0:
+            return 0.0
+        now = time.monotonic()
+        burst = now - self._last_event < w
+        self._last_event = now
+        return w if burst else 0.0
 
     def _unwrap(self, obj):
         if isinstance(obj, DeletedFinalStateUnknown):
@@ -343,7 +351,29 @@ class Controller(ReconcileMixin):
             if e is None or e[0] != uid or e[1] < gen:
                 self.stats["reports_pending"] += 1
                 return
-        self._enqueue_key(key)
+        if not self.options.inline_finish:
+            self._enqueue_key(key)
+            return
+        # Complete: finish it in the next batch (coalesced like any event-driven enqueue); keys that need a
+        # real pass go to the work queue from there.
+        self._inline_keys.add(key)
+        if self._inline_timer is None:
+            delay = self._coalesce_delay()
+            loop = asyncio.get_running_loop()
+            self._inline_timer = loop.call_later(delay, self._flush_inline) if delay > 0 else \
+                loop.call_soon(self._flush_inline)
+
+    def _flush_inline(self) -> None:
+        self._inline_timer = None
+        keys, self._inline_keys = self._inline_keys, set()
+        for key in keys:
+            try:
+                done = self.finish_inline(key)
+            except Exception:  # noqa: BLE001 — the queued pass will hit (and report) the same problem
+                log.exception("inline finish of %s failed; queueing a pass", key)
+                done = False
+            if not done:
+                self.queue.add(key)
 
     def shard_readiness(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else {shard: error|None}."""

@@ -48,6 +48,8 @@ class ControllerOptions:
                                            # which makes them GC-deletable with their last template
     adoption_cache: bool = False           # skip re-checking adoption while neither the template nor a
                                            # dependent's ownership changed since the last check
+    inline_finish: bool = False            # coordinator: a complete report set that only needs the Synced
+                                           # Event is finished without a queued pass (reconcile.finish_inline)
     role: str = "all"                      # all | coordinator | executor (see ncc/controller/executor.py)
     partition: tuple | None = None         # executor: (p, k) → reconcile only keys with key_part(key, k) == p
 
@@ -82,6 +84,7 @@ class ControllerOptions:
             sync_secret_type=True,
             rogue_event_on_template=True,
             adoption_cache=True,
+            inline_finish=True,
         )
         return replace(base, **kw)
 

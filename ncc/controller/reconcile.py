@@ -181,8 +181,10 @@ class ReconcileMixin:
             return self._assume(self.workgroup_informer, res)
         return workgroup
 
-    async def report_template_synced_condition(self, template: dict, secrets: list, configmaps: list, shards: list,
-                                               ready: bool = True, message: str | None = None) -> dict:
+    @staticmethod
+    def _template_synced_status(template: dict, secrets: list, configmaps: list, shards: list, ready: bool = True,
+                                message: str | None = None) -> tuple:
+        """(current status, status after a synced report, its conditions list) — equal statuses mean no write."""
         status = template.get("status") or {}
         conds = list(status.get("conditions") or [])
         name = meta(template).get("name", "")
@@ -191,6 +193,12 @@ class ReconcileMixin:
                                    C.CONDITION_TRUE if ready else C.CONDITION_FALSE, msg)
         new_status = dict(status, conditions=conds, syncedSecrets=list(secrets),
                           syncedConfigurations=list(configmaps), syncedToClusters=list(shards))
+        return status, new_status, conds
+
+    async def report_template_synced_condition(self, template: dict, secrets: list, configmaps: list, shards: list,
+                                               ready: bool = True, message: str | None = None) -> dict:
+        status, new_status, conds = self._template_synced_status(template, secrets, configmaps, shards, ready,
+                                                                 message)
         if new_status != status:
             conds[0] = dict(conds[0], lastTransitionTime=now_rfc3339())
             self._pass_wrote()
@@ -405,6 +413,39 @@ class ReconcileMixin:
             kind_name = C.TEMPLATE_KIND if is_template else C.WORKGROUP_KIND
             self.recorder.event(obj, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
                                 C.MESSAGE_RESOURCE_SYNCED.format(kind_name), kind=kind_name)
+
+    def finish_inline(self, key: str) -> bool:
+        """Coordinator: the pass a complete set of executor reports would run, done synchronously when it can
+        only end in the `Synced` Event — the template exists, is initialised and adopted at this version, every
+        shard succeeded and the status already says so.  Saves the queue round trip, the worker hand-off and
+        the pass preamble for the common case.  False (nothing done) when a real pass is needed: a status or
+        adoption write, a failure to report, a deletion, or a pass already queued or running for the key."""
+        if not self.ready.is_set() or self.queue.shutting_down() or self.queue.busy(key) or \
+                not self.options.adoption_cache:
+            return False  # workers not running (standby, shutdown, lost Lease): nothing may be written
+        kind, ns, name = key.split("/", 2)
+        if kind != C.KIND_TEMPLATE:
+            return False
+        template = self.template_lister.try_get(ns, name)
+        if template is None:
+            return False
+        status = template.get("status") or {}
+        if not status.get("conditions") or self._adopted.get(key) != meta(template).get("resourceVersion"):
+            return False
+        results = self.shard_readiness(key, template)
+        if results is None or any(results.values()):
+            return False
+        ok = [s for s in self.all_shard_names if not results[s]]
+        status, new_status, _ = self._template_synced_status(template, *dependent_names(template), ok)
+        if new_status != status:
+            return False
+        self.stats["reconciles"] += 1
+        self.stats["inline_finishes"] += 1
+        if key in self._pending_event or self.options.event_on_noop:
+            self._pending_event.discard(key)
+            self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND), kind=C.TEMPLATE_KIND)
+        return True
 
     async def _sync_template_to_shard(self, template: dict, shard, spec_fp) -> None:
         if self.options.wait_for_shards_timeout is not None and not shard.has_synced():

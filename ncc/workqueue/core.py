@@ -183,6 +183,10 @@ class PyRateLimitingQueue:
     def waiting(self) -> int:
         return len(self._waiting_ready)
 
+    def busy(self, key: str) -> bool:
+        """Queued, being processed or waiting for a delayed add: a worker pass for the key is pending or running."""
+        return key in self._dirty or key in self._processing or key in self._waiting_ready
+
     # -- RateLimiting -----------------------------------------------------------
     def add_rate_limited(self, key: str, now: float) -> float:
         d = self.limiter.when(key, now)

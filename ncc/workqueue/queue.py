@@ -123,6 +123,9 @@ class WorkQueue:
             self._mark(key)
             self._wake(1)
 
+    def busy(self, key: str) -> bool:
+        return self.core.busy(key)
+
     def __len__(self) -> int:
         return self.core.length()
 

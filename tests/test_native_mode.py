@@ -438,7 +438,10 @@ async def test_coordinator_skips_early_pass_until_reports_complete():
     for i in range(2):
         ctl.on_executor_message(i, {"t": "report", "k": key, "u": m["uid"], "g": m["generation"],
                                     "r": {f"s{i}": None}, "w": True})
-    assert ctl.queue.core.waiting() + len(ctl.queue) == 1  # the last report enqueued it
+    assert ctl._inline_keys == {key}  # the last report completed the set: finished in the next batch
+    ctl._inline_timer.cancel()
+    ctl._flush_inline()  # workers not started: no inline finish, a queued pass instead
+    assert ctl.queue.core.waiting() + len(ctl.queue) == 1 and ctl.stats["inline_finishes"] == 0
     # reports already complete for the next version: the informer event itself enqueues
     ctl.queue.shutdown()
     ctl2 = env.build(role="coordinator")
@@ -450,6 +453,51 @@ async def test_coordinator_skips_early_pass_until_reports_complete():
     before = ctl2.queue.core.waiting() + len(ctl2.queue)
     ctl2._on_crd_update(new, newer, C.KIND_TEMPLATE)
     assert ctl2.stats["early_passes_skipped"] == 0 and ctl2.queue.core.waiting() + len(ctl2.queue) >= before
+
+
+async def test_coordinator_finishes_complete_reports_inline():
+    """A complete report set for an initialised, adopted template whose status already says Ready only needs
+    the Synced Event: it is recorded without a queued pass.  Anything else (a status change, a failed shard,
+    a pass already queued) goes through the work queue."""
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build(role="coordinator")
+    name = t["metadata"]["name"]
+    key = make_key(C.KIND_TEMPLATE, NS, name)
+    ctl.ready.set()  # workers "running"
+
+    def report(gen, errs=(None, None), wrote=True):
+        cur = ctl.template_lister.get(NS, name)["metadata"]
+        for i in range(2):
+            ctl.on_executor_message(i, {"t": "report", "k": key, "u": cur["uid"], "g": gen,
+                                        "r": {f"s{i}": errs[i]}, "w": wrote})
+        ctl._inline_timer.cancel()
+        ctl._flush_inline()
+
+    await ctl.sync_template(NS, name)  # initialising status + adoption; no reports yet
+    env.refresh()
+    gen = ctl.template_lister.get(NS, name)["metadata"]["generation"]
+    report(gen)  # status still "initializing": a real pass must write Ready
+    assert len(ctl.queue) == 1 and ctl.stats["inline_finishes"] == 0
+    assert ctl.queue.try_get() == key
+    await ctl.sync_template(NS, name)
+    ctl.queue.done(key)
+    env.refresh()
+    cur = ctl.template_lister.get(NS, name)
+    assert cur["status"]["conditions"][0]["status"] == C.CONDITION_TRUE
+    # a new version: the adoption mark follows it, every shard reports success, the status stays Ready
+    spec = dict(cur["spec"], container=dict(cur["spec"]["container"], versionTag="v-next"))
+    new = env.cstate.update(R.TEMPLATES, NS, dict(cur, spec=spec))
+    ctl._on_crd_update(cur, new, C.KIND_TEMPLATE)
+    env.refresh()
+    events = len(env.recorder.events)
+    report(new["metadata"]["generation"])
+    assert ctl.stats["inline_finishes"] == 1 and len(ctl.queue) == 0 and ctl.queue.core.waiting() == 0
+    assert env.recorder.events[events:] == [f"{C.EVENT_TYPE_NORMAL} {C.SUCCESS_SYNCED} "
+                                            f"{C.MESSAGE_RESOURCE_SYNCED.format('NexusAlgorithmTemplate')}"]
+    # a shard failure changes the status: queued
+    report(new["metadata"]["generation"], errs=(None, "ApiError: boom"))
+    assert ctl.stats["inline_finishes"] == 1 and len(ctl.queue) == 1
 
 
 async def test_status_patch_racing_a_spec_edit_drops_the_adoption_mark():

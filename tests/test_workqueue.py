@@ -28,6 +28,20 @@ def test_dedup_and_fifo(make):
     assert q.try_get() == "a" and q.try_get() == "b" and q.try_get() is None
 
 
+def test_busy_covers_queued_processing_and_waiting(make):
+    q = make(0.01, 1.0, 10.0, 10)
+    assert not q.busy("a")
+    q.add("a")
+    assert q.busy("a")
+    assert q.try_get() == "a"
+    assert q.busy("a")  # processing
+    q.done("a")
+    assert not q.busy("a")
+    q.add_after("b", 0.5, 0.0)
+    assert q.busy("b")  # waiting for its delayed add
+    assert q.promote(1.0) == 1 and q.busy("b")
+
+
 def test_exclusive_processing_requeues_on_done(make):
     q = make(0.01, 1.0, 10.0, 100)
     q.add("a")
@@ -125,6 +139,7 @@ def test_native_matches_python_reference(seq):
         assert py.length() == nat.length()
         assert py.num_requeues(key) == nat.num_requeues(key)
         assert py.next_ready_in(now) == pytest.approx(nat.next_ready_in(now))
+        assert all(py.busy(k) == nat.busy(k) for k in "abcd")
 
 
 @pytest.mark.parametrize("native_core", [False] + ([True] if NATIVE is not None else []))
