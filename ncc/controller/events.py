@@ -12,6 +12,11 @@ This module re-creates the parts of client-go `tools/record` that shape the API 
   Event instead of creating a new one;
 * bounded retries of failed sink writes.
 
+The correlator runs when an event is recorded, as client-go's broadcaster does on receipt.  With
+`coalesce=True` (native mode) an event identical to one still waiting for its writer is folded into it:
+one write then carries both (`count` + n).  The Event object ends up the same — count, last
+timestamp, message — with fewer API writes when a burst outruns the writers.
+
 `FakeRecorder` mirrors client-go's: it keeps "Type Reason Message" strings (or drops them).
 """
 from __future__ import annotations
@@ -83,7 +88,7 @@ class BroadcastRecorder(EventRecorder):
     """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
 
     def __init__(self, client: KubeClient, component: str = C.CONTROLLER_AGENT_NAME, *, spam_filter: bool = True,
-                 log_events: bool = True, writers: int = 1):
+                 log_events: bool = True, writers: int = 1, coalesce: bool = False):
         self.client = client
         self.component = component
         self.spam_filter = spam_filter
@@ -94,12 +99,15 @@ class BroadcastRecorder(EventRecorder):
         self._queues: list[asyncio.Queue] = [asyncio.Queue(maxsize=max(1, BUFFER // self.writers))
                                              for _ in range(self.writers)]
         self._queue = self._queues[0]
+        self.coalesce = coalesce
+        self._pending: dict[tuple, list] = {}  # coalesce: correlation key -> queued entry [.., n]
         self._buckets: dict[tuple, TokenBucket] = {}
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
         self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
         self._tasks: list[asyncio.Task] = []
         self._write_meta = getattr(client, "write_meta", None)  # undecoded writes (REST clients)
-        self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0}
+        self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0,
+                      "merged": 0}
 
     def start(self) -> None:
         if not self._tasks:
@@ -127,12 +135,28 @@ class BroadcastRecorder(EventRecorder):
         if self.log_events:
             log.info("Event occurred", extra={"object": f"{ref['namespace']}/{ref['name']}", "kind": ref["kind"],
                                               "type": event_type, "reason": reason, "message": message})
+        now = time.monotonic()
+        if not self._allow(ref, now):
+            self.stats["dropped_spam"] += 1
+            return
+        message, key = self._aggregate(ref, event_type, reason, message, now)
+        if self.coalesce:
+            entry = self._pending.get(key)
+            if entry is not None:
+                entry[4] += 1
+                entry[0], entry[3] = ref, message  # the latest involvedObject and message go out with the write
+                self.stats["merged"] += 1
+                return
         q = self._queue if self.writers == 1 else \
             self._queues[hash((ref["namespace"], ref["name"], ref["kind"])) % self.writers]
+        entry = [ref, event_type, reason, message, 1, key]
         try:
-            q.put_nowait((ref, event_type, reason, message, time.monotonic()))
+            q.put_nowait(entry)
         except asyncio.QueueFull:
             self.stats["dropped_full"] += 1
+            return
+        if self.coalesce:
+            self._pending[key] = entry
 
     # ------------------------------------------------------------------ correlator
     def _allow(self, ref: dict, now: float) -> bool:
@@ -162,18 +186,14 @@ class BroadcastRecorder(EventRecorder):
             return "(combined from similar events): " + message, akey
         return message, akey + (message,)
 
-    async def _write(self, ref, event_type, reason, message) -> None:
-        now = time.monotonic()
-        if not self._allow(ref, now):
-            self.stats["dropped_spam"] += 1
-            return
-        message, key = self._aggregate(ref, event_type, reason, message, now)
+    async def _write(self, ref, event_type, reason, message, n: int, key: tuple) -> None:
+        """One sink write for `n` correlated occurrences of an event (n > 1 only when coalescing)."""
         ts = now_rfc3339()
         prev = self._seen.get(key)
         ns = ref["namespace"] or "default"
         wm = self._write_meta
         if prev is not None:
-            count = int(prev.get("count", 1)) + 1
+            count = int(prev.get("count", 1)) + n
             patch = {"count": count, "lastTimestamp": ts, "message": message}
             if wm is not None:  # only the Event's name and count matter here: skip decoding the response
                 await wm("patch", R.EVENTS, ns, patch, name=prev["metadata"]["name"], patch_type=PATCH_STRATEGIC)
@@ -194,7 +214,7 @@ class BroadcastRecorder(EventRecorder):
             "source": {"component": self.component},
             "firstTimestamp": ts,
             "lastTimestamp": ts,
-            "count": 1,
+            "count": n,
             "type": event_type,
             "reportingComponent": self.component,
             "reportingInstance": "",
@@ -210,11 +230,14 @@ class BroadcastRecorder(EventRecorder):
 
     async def _run(self, queue: asyncio.Queue) -> None:
         while True:
-            ref, event_type, reason, message, _t = await queue.get()
+            entry = await queue.get()
+            if self.coalesce and self._pending.get(entry[5]) is entry:
+                del self._pending[entry[5]]  # from here on, a repeat queues a write of its own
+            ref, event_type, reason, message, n, key = entry
             try:
                 for attempt in range(3):
                     try:
-                        await self._write(ref, event_type, reason, message)
+                        await self._write(ref, event_type, reason, message, n, key)
                         break
                     except asyncio.CancelledError:
                         raise

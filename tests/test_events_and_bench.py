@@ -36,6 +36,31 @@ async def test_event_dedup_patches_count():
     await rec.stop()
 
 
+async def test_event_coalescing_folds_pending_repeats():
+    """Native mode: repeats of an event still waiting for its writer ride on that write (count + n); the
+    Event object ends up exactly as with one write per occurrence."""
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False, writers=4, coalesce=True)
+    t = client.state.create(R.TEMPLATES, "nexus", make_template(0, "nexus"))
+    other = client.state.create(R.TEMPLATES, "nexus", make_template(1, "nexus"))
+    msg = "Resource of type NexusAlgorithmTemplate synced successfully"
+    for _ in range(3):
+        rec.event(t, "Normal", "Synced", msg)
+    rec.event(other, "Normal", "Synced", msg)
+    rec.event(t, "Warning", "ErrResourceSyncError", "boom")  # a different event is not folded
+    rec.start()
+    await _drain(rec)
+    rec.event(t, "Normal", "Synced", msg)  # written already: a repeat PATCHes the count
+    await _drain(rec)
+    events = {(e["involvedObject"]["name"], e["reason"]): e for e in client.state.list(R.EVENTS, "nexus")["items"]}
+    assert events[(t["metadata"]["name"], "Synced")]["count"] == 4
+    assert events[(other["metadata"]["name"], "Synced")]["count"] == 1
+    assert events[(t["metadata"]["name"], "ErrResourceSyncError")]["count"] == 1
+    assert rec.stats["merged"] == 2 and rec.stats["created"] == 3 and rec.stats["patched"] == 1
+    assert not rec._pending
+    await rec.stop()
+
+
 async def test_event_spam_filter_and_aggregation():
     client = FakeClient(ClusterState(), simple=False)
     rec = BroadcastRecorder(client, log_events=False)
