@@ -310,7 +310,8 @@ class App:
             # native: 4 writer tasks (per-object order kept) so Event traffic keeps up with fan-out rates;
             # compat: client-go's single sink goroutine
             self.recorder = BroadcastRecorder(client, log_events=log.isEnabledFor(logging.DEBUG),
-                                              writers=4 if o.mode == "native" else 1, coalesce=o.mode == "native")
+                                              writers=4 if o.mode == "native" else 1,
+                                              coalesce=o.mode == "native" and os.environ.get("NCC_EVENT_COALESCE") != "0")
         self.controller = Controller(alias=cfg.alias, namespace=cfg.controller_namespace, client=client,
                                      shards=self.shards, template_informer=infs[R.TEMPLATES],
                                      workgroup_informer=infs[R.WORKGROUPS], secret_informer=infs[R.SECRETS],
