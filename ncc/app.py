@@ -23,6 +23,7 @@ import signal
 import sys
 
 from . import __version__, gctune
+from . import native as native_ext
 from .api import constants as C
 from .api import resources as R
 from .cache.informer import InformerFactory
@@ -296,6 +297,11 @@ class App:
             for rt in (R.SECRETS, R.CONFIGMAPS):
                 infs[rt].metadata_only = True
                 infs[rt].store.transform = strip_payload
+            # ...nor template specs beyond their references: templates arrive slim (metadata, status, the
+            # Secret/ConfigMap references and a digest of the spec; `_native.template_event_slim`)
+            mod = native_ext.load()
+            if mod is not None and os.environ.get("NCC_SLIM_TEMPLATES") != "0":
+                infs[R.TEMPLATES].slim_decode = mod.template_event_slim
         else:
             self.shards = load_shards(cfg.alias, cfg.shard_config_path, cfg.controller_namespace,
                                       client_factory=self.client_factory,

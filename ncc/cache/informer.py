@@ -28,7 +28,7 @@ from typing import Callable
 
 from .. import native as _native
 from ..aio import wait_timeout
-from ..api.jsonenc import loads_bytes
+from ..api.jsonenc import loads_fast
 from ..api.objects import ObjectKey, key_of, rv_int
 from ..api.resources import ResourceType
 from ..kube import errors as E
@@ -132,6 +132,9 @@ class Informer:
         # (the coordinator forwarding them); `feed` replaces LIST/WATCH by what a coordinator forwards.
         self.tap = None
         self.feed = None
+        # Optional native decoder for watch lines returning (type, object) or None (then the full decode):
+        # the coordinator's template informer keeps slim templates (`_native.template_event_slim`).
+        self.slim_decode = None
 
     # ------------------------------------------------------------- public API
     def add_event_handler(self, on_add=None, on_update=None, on_delete=None) -> None:
@@ -237,7 +240,7 @@ class Informer:
         asks for the raw path whenever the native module is there (a relayed feed is raw lines anyway)."""
         kf, of = self.key_filter, self.owner_filter
         mo = self.metadata_only
-        if not (force or self.echo_fastpath or kf is not None or of is not None or mo):
+        if not (force or self.echo_fastpath or kf is not None or of is not None or mo or self.slim_decode):
             return None
         mod = _native.load()
         if mod is None:
@@ -285,7 +288,8 @@ class Informer:
     async def _consume(self, lines, ctx, rv: str) -> str:
         """Apply one batch of raw watch lines (see `_line_ctx`); returns the last RV seen."""
         scan, nparts, kpart, opart, oref, kf, of, mo = ctx
-        loads = loads_bytes
+        loads = loads_fast
+        slim = self.slim_decode
         store = self.store
         default_ns = self.namespace or ""
         inflight, stash = self._inflight, self._stash
@@ -341,6 +345,10 @@ class Informer:
                 prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
                 if prev is not None:  # keep per-key order
                     await self._apply_line(prev[1])
+            sl = slim(line) if slim is not None else None
+            if sl is not None:
+                rv = await self._handle(sl[0], sl[1], rv)
+                continue
             ev = loads(line)
             rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
         return rv
@@ -380,7 +388,11 @@ class Informer:
             self.store.delete(ObjectKey(ns, name))  # left our partition: forget it (no handler dispatch)
 
     async def _apply_line(self, line: bytes) -> None:
-        ev = loads_bytes(line)
+        sl = self.slim_decode(line) if self.slim_decode is not None else None
+        if sl is not None:
+            await self._apply(sl[0], sl[1])
+            return
+        ev = loads_fast(line)
         await self._apply(ev.get("type", ""), ev.get("object") or {})
 
     # ------------------------------------------------------------- write tracking
@@ -432,7 +444,7 @@ class Informer:
         while not self._stopping:
             what, lines = await feed.get()
             if what == "s":
-                loads = loads_bytes
+                loads = loads_fast
                 items = []
                 for line in lines:
                     ev = loads(line)
@@ -443,7 +455,7 @@ class Informer:
                 self.last_rv = await self._consume(lines, ctx, self.last_rv)
             else:
                 for line in lines:
-                    ev = loads_bytes(line)
+                    ev = loads_fast(line)
                     self.last_rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, self.last_rv)
 
     async def _run(self) -> None:

@@ -38,7 +38,7 @@ class _LazyModule:
 aiohttp = _LazyModule("aiohttp")
 
 from .. import native as _native
-from ..api.jsonenc import dumps_bytes, loads_bytes
+from ..api.jsonenc import dumps_bytes, loads_fast
 from ..api.resources import ResourceType
 from . import errors as E
 from .client import PATCH_MERGE, KubeClient, WatchEvent
@@ -225,7 +225,7 @@ class RestClient(KubeClient):
             if status < 300:
                 if raw_out:
                     return bytes(body_bytes)
-                return loads_bytes(body_bytes) if body_bytes else None
+                return loads_fast(body_bytes) if body_bytes else None
             if status == 401 and (self.cfg.exec is not None or self.cfg.token_file) and not refreshed:
                 refreshed = True
                 await self.creds.token(force_refresh=True)
@@ -405,7 +405,7 @@ class RestClient(KubeClient):
 
     async def watch(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
                     allow_bookmarks=True, label_selector=None) -> AsyncIterator[WatchEvent]:
-        loads = loads_bytes
+        loads = loads_fast
         async for line in self.watch_raw(rt, namespace, resource_version=resource_version,
                                          timeout_seconds=timeout_seconds, allow_bookmarks=allow_bookmarks,
                                          label_selector=label_selector):

@@ -85,3 +85,78 @@ def test_native_json_encoder_roundtrips():
     for o in cases:
         assert json.loads(dumps_bytes(o)) == json.loads(json.dumps(o))
     assert dumps_bytes({1: "int key"}) == b'{"1":"int key"}'  # stdlib fallback semantics for odd keys
+
+
+# ----------------------------------------------------------------------------- native JSON decoding
+def _same(a, b) -> bool:
+    """Equal values and equal types (1 vs 1.0 and -0.0 vs 0.0 count as different)."""
+    if type(a) is not type(b):
+        return False
+    if isinstance(a, float):
+        return str(a) == str(b)  # also tells -0.0 from 0.0, and nan == nan
+    if isinstance(a, list):
+        return len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict):
+        return list(a) == list(b) and all(_same(a[k], b[k]) for k in a)
+    return a == b
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+@settings(max_examples=400, deadline=None)
+@given(json_values, st.booleans())
+def test_native_loads_matches_stdlib(v, ascii_only):
+    """`_native.loads` decodes what json.dumps writes (escaped or raw UTF-8) to exactly json.loads' value."""
+    text = json.dumps(v, ensure_ascii=ascii_only)
+    assert _same(NATIVE.loads(text.encode("utf-8", "surrogatepass")), json.loads(text))
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+@settings(max_examples=400, deadline=None)
+@given(st.binary(max_size=64))
+def test_native_loads_on_arbitrary_bytes(raw):
+    """Malformed input gives None (the caller falls back to the stdlib); accepted input decodes as json does."""
+    v = NATIVE.loads(raw)
+    if v is None:
+        return
+    assert _same(v, json.loads(raw.decode("utf-8", "surrogatepass")))
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+def test_native_loads_edge_cases():
+    from ncc.api.jsonenc import loads_fast
+    for text in ['"\\ud83d\\ude00 \\u00e9 \\ud800 x"', "[1e400, -1e400, -0.0, 0, -0, 123456789012345678901234]",
+                 '{"a": {"a": {"a": []}}, "b": "\\"\\\\\\/\\b\\f\\n\\r\\t"}', " [ ] ", "\"\"", "NaN"]:
+        assert _same(loads_fast(text.encode("utf-8", "surrogatepass")), json.loads(text))
+    for bad in [b"[1,]", b"{\"a\" 1}", b"01", b"[1] x", b"\"\x01\"", b"tru", b"-", b"1.", b"{\"a\":1,}"]:
+        assert NATIVE.loads(bad) is None
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+def test_template_event_slim_keeps_what_the_coordinator_reads():
+    """The coordinator's slim templates: metadata (without managedFields) and status decoded, the spec reduced
+    to its Secret/ConfigMap references and a digest of the raw spec (same spec <=> same digest)."""
+    from ncc.api.refs import dependent_names, same_references
+    from ncc.testing.workload import make_template
+    t = make_template(4, "nexus", secrets=["s1", "s2"], configmaps=["c1"], version="v1")
+    t["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"].insert(1, {"prefix": "X_", "secretRef": None})
+    t["metadata"].update(uid="u-4", resourceVersion="77", generation=3,
+                         managedFields=[{"manager": "kubectl", "fieldsV1": {"f:spec": {}}}])
+    t["status"] = {"conditions": [{"type": "Ready", "status": "True", "message": "Algorithm \"é\" ready"}],
+                   "syncedSecrets": ["s1", "s2"]}
+    line = json.dumps({"type": "MODIFIED", "object": t}).encode()
+    typ, slim = NATIVE.template_event_slim(line)
+    assert typ == "MODIFIED" and slim["kind"] == t["kind"] and slim["apiVersion"] == t["apiVersion"]
+    assert slim["status"] == t["status"]
+    assert slim["metadata"] == {k: v for k, v in t["metadata"].items() if k != "managedFields"}
+    assert dependent_names(slim) == dependent_names(t) == (["s1", "s2"], ["c1"])
+    assert same_references(slim, t)
+    again = NATIVE.template_event_slim(json.dumps({"object": t, "type": "MODIFIED"}).encode())[1]
+    assert again["spec"] == slim["spec"]
+    t["spec"]["container"]["versionTag"] = "v2"
+    changed = NATIVE.template_event_slim(json.dumps({"type": "MODIFIED", "object": t}).encode())[1]
+    assert changed["spec"] != slim["spec"] and dependent_names(changed) == dependent_names(slim)
+    no_env = dict(t, spec={"container": {}})
+    assert dependent_names(NATIVE.template_event_slim(json.dumps({"type": "ADDED", "object": no_env}).encode())[1]) \
+        == ([], [])
+    for bad in [b"", b"{}", b'{"type": "ADDED"}', b'{"type": "ADDED", "object": {"spec": [}}', line[:-1]]:
+        assert NATIVE.template_event_slim(bad) is None
