@@ -121,33 +121,35 @@ class Controller(ReconcileMixin):
                 self._register_shard_handlers(shard)
 
     def _on_crd_update(self, old: dict, new: dict, kind: str) -> None:
-        if self.options.adoption_cache and kind == C.KIND_TEMPLATE:
+        o = self.options
+        om, nm = old.get("metadata") or {}, new.get("metadata") or {}
+        nrv = nm.get("resourceVersion")
+        key = None
+        if o.adoption_cache and kind == C.KIND_TEMPLATE:
             # adoption depends on the references and the dependents' ownerRefs (whose changes arrive as
             # dependent events): a new template version with the same references stays adopted
-            om, nm = meta(old), meta(new)
             key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
             if self._adopted.get(key) == om.get("resourceVersion") and om.get("uid") == nm.get("uid") and \
                     same_references(old, new):
-                self._adopted[key] = nm.get("resourceVersion")
-        if self.options.generation_filter:
-            om, nm = meta(old), meta(new)
-            if om.get("resourceVersion") == nm.get("resourceVersion"):
+                self._adopted[key] = nrv
+        if o.generation_filter:
+            if om.get("resourceVersion") == nrv:
                 return  # informer resync: nothing changed
-            if om.get("generation") == nm.get("generation") and om.get("generation") is not None \
-                    and om.get("labels") == nm.get("labels") and om.get("annotations") == nm.get("annotations") \
-                    and old.get("spec") == new.get("spec"):
+            gen = om.get("generation")
+            if gen is not None and gen == nm.get("generation") and om.get("labels") == nm.get("labels") \
+                    and om.get("annotations") == nm.get("annotations") and old.get("spec") == new.get("spec"):
                 return  # status-only change (typically our own status write)
-        if self.role == "coordinator" and self.options.adoption_cache:
+        if self.role == "coordinator" and o.adoption_cache:
             # A new version of an initialised, adopted object has nothing to do here until every shard has
             # reported on it, and the last report enqueues it: skip the early pass.
-            nm = meta(new)
-            key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
+            if key is None:
+                key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
             if (new.get("status") or {}).get("conditions") and \
-                    (kind != C.KIND_TEMPLATE or self._adopted.get(key) == nm.get("resourceVersion")) and \
+                    (kind != C.KIND_TEMPLATE or self._adopted.get(key) == nrv) and \
                     self.shard_readiness(key, new) is None:
                 self.stats["early_passes_skipped"] += 1
                 return
-        self.enqueue_resource(new, kind)
+        self._enqueue_key(key or make_key(kind, nm.get("namespace", "") or "", nm.get("name", "")))
 
     def _on_dependent(self, obj, index: str):
         obj = self._unwrap(obj)
@@ -377,9 +379,11 @@ class Controller(ReconcileMixin):
 
     def shard_readiness(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else {shard: error|None}."""
-        m = meta(obj)
+        st = self.shard_state.get(key)
+        if st is None:
+            return None
+        m = obj.get("metadata") or {}
         uid, gen = m.get("uid", ""), int(m.get("generation") or 0)
-        st = self.shard_state.get(key) or {}
         out = {}
         for s in self.all_shard_names:
             e = st.get(s)

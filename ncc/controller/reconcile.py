@@ -430,14 +430,19 @@ class ReconcileMixin:
         if template is None:
             return False
         status = template.get("status") or {}
-        if not status.get("conditions") or self._adopted.get(key) != meta(template).get("resourceVersion"):
+        conds = status.get("conditions")
+        if not conds or self._adopted.get(key) != (template.get("metadata") or {}).get("resourceVersion"):
             return False
         results = self.shard_readiness(key, template)
         if results is None or any(results.values()):
             return False
-        ok = [s for s in self.all_shard_names if not results[s]]
-        status, new_status, _ = self._template_synced_status(template, *dependent_names(template), ok)
-        if new_status != status:
+        # report_template_synced_condition would leave the status as it is (no write) exactly when the Ready
+        # condition and the three synced lists already hold what it would set
+        secrets, configmaps = dependent_names(template)
+        c0 = conds[0]
+        if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE, f"Algorithm {q(name)} ready") \
+                or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
+                or status.get("syncedToClusters") != self.all_shard_names:
             return False
         self.stats["reconciles"] += 1
         self.stats["inline_finishes"] += 1

@@ -554,3 +554,30 @@ async def test_adoption_mark_not_stored_when_invalidated_during_adoption():
     ctl.adopt_references = adopt_then_event
     await ctl.sync_template(NS, name)
     assert key not in ctl._adopted
+
+
+async def test_inline_finish_agrees_with_the_status_pass():
+    """finish_inline's "status would not change" test is report_template_synced_condition's own decision."""
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build(role="coordinator")
+    ctl.ready.set()
+    name = t["metadata"]["name"]
+    key = make_key(C.KIND_TEMPLATE, NS, name)
+    base = ctl.template_lister.get(NS, name)
+    good = {"conditions": [{"type": "Ready", "status": "True", "lastTransitionTime": "2026-01-01T00:00:00Z",
+                            "reason": C.CONDITION_READY_REASON, "message": f'Algorithm "{name}" ready'}],
+            "syncedSecrets": ["s"], "syncedConfigurations": ["c"], "syncedToClusters": ["s0", "s1"]}
+    variants = [good, dict(good, syncedToClusters=["s0"]), dict(good, syncedSecrets=[]),
+                {k: v for k, v in good.items() if k != "syncedConfigurations"},
+                dict(good, conditions=[dict(good["conditions"][0], status="False")]),
+                dict(good, conditions=[dict(good["conditions"][0], message="other")]),
+                dict(good, conditions=good["conditions"] + [{"type": "Other"}]), dict(good, extra=1)]
+    for st in variants:
+        obj = dict(base, status=st)
+        ctl.template_informer.store.upsert(obj)
+        ctl._adopted[key] = obj["metadata"]["resourceVersion"]
+        m = obj["metadata"]
+        ctl.shard_state[key] = {s: (m["uid"], int(m.get("generation") or 0), None) for s in ("s0", "s1")}
+        old, new, _ = ctl._template_synced_status(obj, ["s"], ["c"], ["s0", "s1"])
+        assert ctl.finish_inline(key) == (old == new), st
