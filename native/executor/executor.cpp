@@ -567,7 +567,7 @@ struct Shard {
     }
 };
 
-constexpr double kDependentHold = 5.0;
+static double kDependentHold = 5.0;  // NCC_DEPENDENT_HOLD overrides
 // enqueues by cause (NCC_CPU_REPORT diagnostics): template/workgroup event, dependent event, shard-side
 // template drift, shard-side dependent drift, failure retry, orphan sweep, full resync, delete
 enum EnqCause { ENQ_OBJECT, ENQ_DEPENDENT, ENQ_SHARD_OBJECT, ENQ_SHARD_DEPENDENT, ENQ_RETRY, ENQ_SWEEP, ENQ_RESYNC,
@@ -1550,6 +1550,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     crc_init();
+    if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
     const char* gated = std::getenv("NCC_GATED");
     g_opt.gated = gated != nullptr && std::string(gated) == "1";
     ::signal(SIGPIPE, SIG_IGN);
