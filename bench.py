@@ -176,11 +176,13 @@ async def post(session, url, body, timeout=None):
         return await r.json()
 
 
-def cpu_seconds(named: dict, rss: dict | None = None) -> dict:
+def cpu_seconds(named: dict, rss: dict | None = None, sys_out: dict | None = None) -> dict:
     """user+sys CPU seconds per named process; `coordinator` also reports its executor children.
-    With `rss` given, resident memory (MiB) per process is recorded there too."""
+    With `rss` given, resident memory (MiB) per process is recorded there too; with `sys_out`, the
+    kernel-mode part of the CPU seconds."""
     import psutil
     out = {}
+    sys_out = {} if sys_out is None else sys_out
     for name, proc in named.items():
         if proc is None:
             continue
@@ -188,6 +190,7 @@ def cpu_seconds(named: dict, rss: dict | None = None) -> dict:
             p = psutil.Process(proc.pid)
             t = p.cpu_times()
             out[name] = t.user + t.system
+            sys_out[name] = t.system
             if rss is not None:
                 rss[name] = round(p.memory_info().rss / 2**20, 1)
             if name == "coordinator":
@@ -200,8 +203,12 @@ def cpu_seconds(named: dict, rss: dict | None = None) -> dict:
                     except (psutil.Error, OSError):
                         continue
                     (ex if ("ncc-executor" in cmd or "ncc.executor" in cmd) else co).append(c)
-                out["executors"] = sum(sum(c.cpu_times()[:2]) for c in ex)
-                out[name] += sum(sum(c.cpu_times()[:2]) for c in co)
+                ext = [c.cpu_times() for c in ex]
+                cot = [c.cpu_times() for c in co]
+                out["executors"] = sum(t.user + t.system for t in ext)
+                sys_out["executors"] = sum(t.system for t in ext)
+                out[name] += sum(t.user + t.system for t in cot)
+                sys_out[name] += sum(t.system for t in cot)
                 if rss is not None:
                     rss["executors"] = round(sum(c.memory_info().rss for c in ex) / 2**20, 1)
                     rss[name] += round(sum(c.memory_info().rss for c in co) / 2**20, 1)
@@ -329,7 +336,8 @@ async def run(args, d: Dist) -> dict | None:
                 if step == args.warmup + 1:
                     d.sync()
                     t_start = time.perf_counter()
-                    cpu0 = cpu_seconds(named)
+                    sys0: dict = {}
+                    cpu0 = cpu_seconds(named, sys_out=sys0)
                     kids0 = child_pids(controller) if controller is not None else set()
                 t0 = None
                 if d.rank == 0:
@@ -349,7 +357,8 @@ async def run(args, d: Dist) -> dict | None:
             d.sync()
             elapsed = time.perf_counter() - t_start
             rss: dict = {}
-            cpu1 = cpu_seconds(named, rss)
+            sys1: dict = {}
+            cpu1 = cpu_seconds(named, rss, sys1)
             ctrl_api = None
             ctrl_state = {}
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
@@ -411,6 +420,9 @@ async def run(args, d: Dist) -> dict | None:
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
                 "controller_cpu_us_per_object": round(sum(ctl_cpu.values()) * 1e6 / objs, 1),
                 "controller_cpu_us_per_object_split": us_per_obj,
+                # kernel-mode share of that CPU (syscalls, the loopback TCP stack) per process
+                "controller_cpu_sys_share": {k: round((sys1.get(k, 0.0) - sys0.get(k, 0.0)) / v, 3)
+                                             for k, v in ctl_cpu.items() if v > 0},
                 "cold_start_s": round(cold, 3),
                 "cold_start_objects_per_s": round(3 * T * d.world * S / cold, 1) if cold > 0 else None,
                 "controller_alive": ctrl_alive,

@@ -46,6 +46,9 @@
 extern "C" void _mcleanup(void);
 #endif
 
+#ifndef NCC_SYSTEM_MALLOC
+#include "alloc.hpp"
+#endif
 #include "http.hpp"
 #include "json.hpp"
 #include "loop.hpp"
