@@ -59,7 +59,8 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
     else:
         flags += ["-O2", "-DNDEBUG"]
     if sanitize:
-        flags += ["-fsanitize=address,undefined"]
+        # ASan must see every heap allocation: keep malloc instead of the executor's pool allocator
+        flags += ["-fsanitize=address,undefined", "-DNCC_SYSTEM_MALLOC"]
     tmp = out + ".tmp"
     cmd = [cxx, *flags, EXECUTOR_MAIN, "-o", tmp, "-lssl", "-lcrypto"]
     if verbose:
