@@ -378,6 +378,127 @@ inline std::string dumps(const Value& v) {
     return out;
 }
 
+// ------------------------------------------------------------------------------------ scanning
+// type / metadata.namespace / .name / .resourceVersion of a raw watch line without building a DOM, so
+// the echo of the executor's own write (already cached from the write's response) costs one scan.  Any
+// escape in the strings read, or anything unexpected, returns false (the caller parses the line).
+class EventScanner {
+public:
+    EventScanner(std::string_view line) : p_(line.data()), e_(line.data() + line.size()) {}
+    bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        if (!expect('{')) return false;
+        bool have_type = false, have_meta = false;
+        while (true) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            if (key == "type") {
+                if (!str(type)) return false;
+                have_type = true;
+            } else if (key == "object") {
+                if (!object_meta(ns, name, rv)) return false;
+                have_meta = true;
+            } else if (!skip()) {
+                return false;
+            }
+            if (have_type && have_meta) return true;
+            if (!expect(',')) return false;
+        }
+    }
+
+private:
+    const char* p_;
+    const char* e_;
+    void ws() {
+        while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+    }
+    bool expect(char c) {
+        ws();
+        if (p_ >= e_ || *p_ != c) return false;
+        ++p_;
+        return true;
+    }
+    bool str(std::string_view& out) {
+        ws();
+        if (p_ >= e_ || *p_ != '"') return false;
+        const char* s = ++p_;
+        while (p_ < e_ && *p_ != '"') {
+            if (*p_ == '\\') return false;
+            ++p_;
+        }
+        if (p_ >= e_) return false;
+        out = std::string_view(s, static_cast<size_t>(p_ - s));
+        ++p_;
+        return true;
+    }
+    bool skip_str() {
+        ++p_;
+        while (p_ < e_) {
+            if (*p_ == '\\') {
+                p_ += 2;
+                continue;
+            }
+            if (*p_++ == '"') return true;
+        }
+        return false;
+    }
+    bool skip() {
+        ws();
+        if (p_ >= e_) return false;
+        if (*p_ == '"') return skip_str();
+        if (*p_ == '{' || *p_ == '[') {
+            int depth = 0;
+            while (p_ < e_) {
+                char c = *p_;
+                if (c == '"') {
+                    if (!skip_str()) return false;
+                    continue;
+                }
+                if (c == '{' || c == '[') ++depth;
+                if (c == '}' || c == ']') {
+                    if (--depth == 0) {
+                        ++p_;
+                        return true;
+                    }
+                }
+                ++p_;
+            }
+            return false;
+        }
+        const char* s = p_;
+        while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n') ++p_;
+        return p_ > s;
+    }
+    bool object_meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
+        if (!expect('{')) return false;
+        while (true) {
+            std::string_view key;
+            if (!str(key) || !expect(':')) return false;
+            if (key == "metadata") {
+                if (!expect('{')) return false;
+                bool have_name = false, have_rv = false;
+                while (true) {
+                    std::string_view k;
+                    if (!str(k) || !expect(':')) return false;
+                    if (k == "name") {
+                        if (!str(name)) return false;
+                        have_name = true;
+                    } else if (k == "namespace") {
+                        if (!str(ns)) return false;
+                    } else if (k == "resourceVersion") {
+                        if (!str(rv)) return false;
+                        have_rv = true;
+                    } else if (!skip()) {
+                        return false;
+                    }
+                    if (expect(',')) continue;
+                    return expect('}') && have_name && have_rv;
+                }
+            }
+            if (!skip() || !expect(',')) return false;
+        }
+    }
+};
+
 // ------------------------------------------------------------------------------------ fingerprints
 inline uint64_t fmix64(uint64_t k) {
     k ^= k >> 33;
