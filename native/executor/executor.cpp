@@ -179,8 +179,8 @@ static std::vector<std::string> template_owner_names(const Value& o) {
     return out;
 }
 // GetSecretNames() / GetConfigMapNames(): spec.runtimeEnvironment.mappedEnvironmentVariables[*]
-static void dependent_names(const Value& tpl, std::vector<std::string>& secrets, std::vector<std::string>& cms) {
-    const Value* spec = tpl.get("spec");
+// (`spec`: the template's spec, or a view of it holding at least runtimeEnvironment)
+static void dependent_names(const Value* spec, std::vector<std::string>& secrets, std::vector<std::string>& cms) {
     const Value* rte = spec ? spec->get("runtimeEnvironment") : nullptr;
     const Value* mev = rte ? rte->get("mappedEnvironmentVariables") : nullptr;
     if (!mev || !mev->is_arr()) return;
@@ -193,9 +193,16 @@ static void dependent_names(const Value& tpl, std::vector<std::string>& secrets,
     }
 }
 
-// Controller-side object as relayed by the coordinator (immutable once stored).
+// Payload members: kept as raw JSON text (fingerprinted, re-sent verbatim), never decoded into a DOM.
+static const std::string_view kPayloadKeys[2][3] = {{"spec", "status", ""}, {"data", "binaryData", "stringData"}};
+static const std::string_view* payload_keys(int kind) { return kPayloadKeys[kind < 2 ? 0 : 1]; }
+static size_t payload_count(int kind) { return kind < 2 ? 2 : 3; }
+static bool raw_null(std::string_view raw) { return raw.empty() || raw == "null"; }
+
+// Controller-side object as relayed by the coordinator (immutable once stored).  The payload the shard
+// copy gets (templates/workgroups: spec; Secrets/ConfigMaps: data, binaryData) is kept as its raw JSON.
 struct CtlObj {
-    Value obj;
+    std::string spec_raw, data_raw, bin_raw;
     std::string ns, name, uid, rv;
     long long generation = 0;
     bool has_generation = false;
@@ -206,7 +213,8 @@ struct CtlObj {
 };
 using CtlPtr = std::shared_ptr<const CtlObj>;
 
-static CtlPtr make_ctl(int kind, Value obj) {
+// `obj`: the object without its payload members; `raw`: their text (payload_keys order, empty = absent)
+static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) {
     auto c = std::make_shared<CtlObj>();
     const Value* m = meta_of(obj);
     if (m) {
@@ -224,16 +232,21 @@ static CtlPtr make_ctl(int kind, Value obj) {
     }
     if (c->ns.empty()) c->ns = g_opt.ns;
     if (kind < 2) {
-        const Value* spec = obj.get("spec");
-        c->fp_spec = spec ? fingerprint(*spec) : fingerprint(Value());
-        if (kind == TEMPLATES) dependent_names(obj, c->secrets, c->configmaps);
+        c->spec_raw.assign(raw[0]);
+        c->fp_spec = raw[0].empty() ? fingerprint(Value()) : fingerprint_text(raw[0]);
+        if (kind == TEMPLATES && !raw_null(raw[0])) {
+            static const std::string_view rte[1] = {"runtimeEnvironment"};
+            Value view = Parser(raw[0].data(), raw[0].size()).parse_only(rte, 1);
+            dependent_names(&view, c->secrets, c->configmaps);
+        }
     } else {
-        c->fp_data = fp_opt(obj.get("data"));
-        c->fp_bin = fp_opt(obj.get("binaryData"));
+        c->data_raw.assign(raw[0]);
+        c->bin_raw.assign(raw[1]);
+        c->fp_data = fp_opt_text(raw[0]);
+        c->fp_bin = fp_opt_text(raw[1]);
         c->type = std::string(obj.sget("type"));
         c->owners = template_owner_names(obj);
     }
-    c->obj = std::move(obj);
     return c;
 }
 
@@ -251,7 +264,8 @@ struct ShardObj {
 };
 using ShardPtr = std::shared_ptr<const ShardObj>;
 
-static ShardPtr make_shard_obj(int kind, Value obj) {
+// `raw` (optional): the payload members' text when `obj` was parsed without them (parse_split)
+static ShardPtr make_shard_obj(int kind, Value obj, const std::string_view* raw = nullptr) {
     auto s = std::make_shared<ShardObj>();
     const Value* m = meta_of(obj);
     if (m) {
@@ -274,7 +288,15 @@ static ShardPtr make_shard_obj(int kind, Value obj) {
         }
     }
     if (s->ns.empty()) s->ns = g_opt.ns;
-    if (kind < 2) {
+    if (raw != nullptr) {  // payloads never decoded
+        if (kind < 2) {
+            s->fp_spec = raw[0].empty() ? fingerprint(Value()) : fingerprint_text(raw[0]);
+        } else {
+            s->fp_data = fp_opt_text(raw[0]);
+            s->fp_bin = fp_opt_text(raw[1]);
+            s->type = std::string(obj.sget("type"));
+        }
+    } else if (kind < 2) {
         const Value* spec = obj.get("spec");
         s->fp_spec = spec ? fingerprint(*spec) : fingerprint(Value());
         obj.erase("spec");
@@ -289,6 +311,13 @@ static ShardPtr make_shard_obj(int kind, Value obj) {
     }
     s->rest = std::move(obj);
     return s;
+}
+
+// A write/GET response body straight into the slim form, payloads fingerprinted from their text.
+static ShardPtr shard_obj_from_body(int kind, std::string_view body) {
+    std::string_view raw[3];
+    Value rest = Parser(body.data(), body.size()).parse_split(payload_keys(kind), payload_count(kind), raw);
+    return make_shard_obj(kind, std::move(rest), raw);
 }
 
 static bool is_ours(const ShardObj& s) { return s.label_owner == g_opt.alias && s.label_app == kAgent; }
@@ -647,9 +676,8 @@ static void index_template(const CtlPtr& old, const CtlPtr& cur) {
 }
 
 // Apply one relayed controller-side event.
-static void ctl_apply(int kind, const std::string& type, Value obj) {
+static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
     Executor& ex = *g_ex;
-    CtlPtr cur = make_ctl(kind, std::move(obj));
     std::string key = key_of(cur->ns, cur->name);
     auto& store = ex.ctl[kind];
     auto it = store.find(key);
@@ -666,14 +694,11 @@ static void ctl_apply(int kind, const std::string& type, Value obj) {
     on_ctl_event(kind, old, cur, false);
 }
 
-static void ctl_snapshot(int kind, std::vector<Value> objs) {
+static void ctl_snapshot(int kind, std::vector<CtlPtr> objs) {
     Executor& ex = *g_ex;
     auto& store = ex.ctl[kind];
     std::unordered_map<std::string, CtlPtr> fresh;
-    for (auto& o : objs) {
-        CtlPtr c = make_ctl(kind, std::move(o));
-        fresh[key_of(c->ns, c->name)] = c;
-    }
+    for (auto& c : objs) fresh[key_of(c->ns, c->name)] = c;
     bool was_synced = ex.ctl_synced[kind];
     std::vector<std::pair<CtlPtr, CtlPtr>> changes;  // (old, new); new null = deleted
     for (auto& kv : fresh) {
@@ -838,23 +863,22 @@ static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
             }
         }
     }
-    Value ev = parse(line);
-    std::string type(ev.sget("type"));
-    Value* obj = ev.get("object");
-    if (obj == nullptr) return;
+    std::string type;
+    std::string_view raw[3];
+    Value obj = Parser(line.data(), line.size()).parse_event_split(type, payload_keys(kind), payload_count(kind), raw);
+    if (!obj.is_obj()) return;
     Informer& inf = sh.inf[kind];
     ++inf.events;
-    if (type == "ERROR") {
-        std::string body = dumps(*obj);
-        ApiError e = api_error(200, body);
+    if (type == "ERROR") {  // a Status object: no payload members were split off
+        ApiError e = api_error(200, dumps(obj));
         throw e;
     }
-    std::string rv = mget(*obj, "resourceVersion");
+    std::string rv = mget(obj, "resourceVersion");
     if (type == "BOOKMARK") {
         if (!rv.empty()) inf.last_rv = rv;
         return;
     }
-    ShardPtr so = make_shard_obj(kind, std::move(*obj));
+    ShardPtr so = make_shard_obj(kind, std::move(obj), raw);
     if (!rv.empty()) inf.last_rv = rv;
     if (type == "DELETED") {
         std::string key = key_of(so->ns, so->name);
@@ -996,17 +1020,17 @@ static Value owner_ref(const std::string& name, const std::string& uid) {
 }
 
 // One write; the server's answer goes into the cache (and the memo of what we meant to write).
+// `data`: the request body (rendered with dumps_with: cached metadata + the raw controller-side payload)
 static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const std::string& ns,
-                                  const std::string& name, const Value& body, PassState* pass, uint64_t want_a,
+                                  const std::string& name, std::string data, PassState* pass, uint64_t want_a,
                                   uint64_t want_b) {
     pass->wrote = true;
     ++g_ex->stats_writes;
     std::string target =
         (std::string(method) == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) + kFieldManagerQuery;
-    std::string data = dumps(body);
     Response r = co_await sh.client->request(method, target, &data);
     if (r.status >= 300) throw api_error(r.status, r.body);
-    ShardPtr so = make_shard_obj(kind, parse(r.body));
+    ShardPtr so = shard_obj_from_body(kind, r.body);
     // remember the intent only when the server stored something else (keeps the memo as small as the set
     // of rewritten objects)
     bool with_bin = kind == CONFIGMAPS && g_opt.sync_binary_data;
@@ -1022,7 +1046,7 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
 static Task<ShardPtr> shard_get_live(Shard& sh, int kind, const std::string& ns, const std::string& name) {
     Response r = co_await sh.client->request("GET", item_path(kind, ns, name), nullptr);
     if (r.status >= 300) throw api_error(r.status, r.body);
-    ShardPtr so = make_shard_obj(kind, parse(r.body));
+    ShardPtr so = shard_obj_from_body(kind, r.body);
     shard_upsert(sh, kind, so, false);
     co_return so;
 }
@@ -1035,27 +1059,27 @@ static Task<void> shard_delete(Shard& sh, int kind, const std::string& ns, const
 // create-or-update of a template/workgroup (native `_write`: AlreadyExists/Conflict -> re-read the live
 // object; a Conflict on update is retried once from it)
 static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj& want, PassState* pass) {
-    const Value* spec = want.obj.get("spec");
+    std::string_view spec = want.spec_raw.empty() ? std::string_view("null") : std::string_view(want.spec_raw);
     bool update = cur != nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        Value body;
+        std::string body;
         if (update) {
-            body = cur->rest;
+            body = dumps_with(cur->rest, {{"spec", spec}});
         } else {
-            body = Value::object();
-            body.set("apiVersion", Value::str(kApiVersion));
-            body.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
+            Value head = Value::object();
+            head.set("apiVersion", Value::str(kApiVersion));
+            head.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
             Value m = Value::object();
             m.set("name", Value::str(want.name));
             m.set("namespace", Value::str(want.ns));
             m.set("labels", owner_labels());
-            body.set("metadata", std::move(m));
+            head.set("metadata", std::move(m));
+            body = dumps_with(head, {{"spec", spec}});
         }
-        body.set("spec", spec ? *spec : Value());
         bool race = false, exists = false;
         try {
-            co_return co_await shard_write(sh, kind, update ? "PUT" : "POST", want.ns, want.name, body, pass,
-                                           want.fp_spec, 0);
+            co_return co_await shard_write(sh, kind, update ? "PUT" : "POST", want.ns, want.name, std::move(body),
+                                           pass, want.fp_spec, 0);
         } catch (const ApiError& e) {
             if (e.conflict() || e.already_exists()) {
                 race = true;
@@ -1093,15 +1117,11 @@ static Task<void> sync_dependent(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, 
         refs.a.push_back(owner_ref(st->name, st->uid));
         m.set("ownerReferences", std::move(refs));
         body.set("metadata", std::move(m));
-        const Value* data = src->obj.get("data");
-        if (data && !data->is_null()) body.set("data", *data);
-        if (is_secret) {
-            if (!src->type.empty()) body.set("type", Value::str(src->type));
-        } else if (with_bin) {
-            const Value* bin = src->obj.get("binaryData");
-            if (bin && !bin->is_null()) body.set("binaryData", *bin);
-        }
-        return body;
+        if (is_secret && !src->type.empty()) body.set("type", Value::str(src->type));
+        std::string_view data = raw_null(src->data_raw) ? std::string_view() : std::string_view(src->data_raw);
+        std::string_view bin = (!is_secret && with_bin && !raw_null(src->bin_raw)) ? std::string_view(src->bin_raw)
+                                                                                    : std::string_view();
+        return dumps_with(body, {{"data", data}, {"binaryData", bin}});
     };
     auto create = [&]() -> Task<ShardPtr> {
         bool exists = false;
@@ -1136,26 +1156,28 @@ static Task<void> sync_dependent(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, 
     bool differs = !data_in_sync(sh, kind, *so, *src);
     if (!differs && !missing_owner) co_return;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        Value body = so->rest;
-        const Value* data = src->obj.get("data");
-        body.set("data", (data && !data->is_null()) ? *data : Value::object());
-        if (with_bin) {
-            const Value* bin = src->obj.get("binaryData");
-            if (bin && !bin->is_null() && !bin->empty_container())
-                body.set("binaryData", *bin);
-            else
-                body.erase("binaryData");
-        }
+        std::string_view data = raw_null(src->data_raw) ? std::string_view("{}") : std::string_view(src->data_raw);
+        // binaryData: the source's when it has any; otherwise the member is dropped ("" = drop; without
+        // binaryData sync the shard copy's own member is kept as it is)
+        std::string_view bin;
+        bool touch_bin = with_bin;
+        if (with_bin && !raw_is_empty(src->bin_raw)) bin = src->bin_raw;
+        std::string body;
         if (missing_owner) {
-            Value* m = body.get("metadata");
-            if (m == nullptr) m = &body.set("metadata", Value::object());
+            Value copy = so->rest;
+            Value* m = copy.get("metadata");
+            if (m == nullptr) m = &copy.set("metadata", Value::object());
             Value* refs = m->get("ownerReferences");
             if (refs == nullptr || !refs->is_arr()) refs = &m->set("ownerReferences", Value::array());
             refs->a.push_back(owner_ref(st->name, st->uid));
+            body = touch_bin ? dumps_with(copy, {{"data", data}, {"binaryData", bin}}) : dumps_with(copy, {{"data", data}});
+        } else {
+            body = touch_bin ? dumps_with(so->rest, {{"data", data}, {"binaryData", bin}})
+                             : dumps_with(so->rest, {{"data", data}});
         }
         bool conflict = false;
         try {
-            co_await shard_write(sh, kind, "PUT", shard_ns, dep, body, pass, src->fp_data, src->fp_bin);
+            co_await shard_write(sh, kind, "PUT", shard_ns, dep, std::move(body), pass, src->fp_data, src->fp_bin);
             co_return;
         } catch (const ApiError& e) {
             if (!e.conflict() || attempt == 1) throw;
@@ -1441,22 +1463,23 @@ static void handle_message(const mp::Obj& m) {
         int kind = static_cast<int>(m.iget("k"));
         const mp::Obj* lines = m.get("l");
         if (kind < 0 || kind > 3 || lines == nullptr || lines->t != mp::Obj::ARR) return;
+        std::string type;
+        std::string_view raw[3];
         if (t == "s") {
-            std::vector<Value> objs;
+            std::vector<CtlPtr> objs;
             objs.reserve(lines->a.size());
             for (const auto& l : lines->a) {
-                Value ev = parse(l.s);
-                Value* o = ev.get("object");
-                std::string_view type = ev.sget("type");
-                if (o && (type == "ADDED" || type == "MODIFIED")) objs.push_back(std::move(*o));
+                Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
+                                                                            payload_count(kind), raw);
+                if (o.is_obj() && (type == "ADDED" || type == "MODIFIED")) objs.push_back(make_ctl(kind, o, raw));
             }
             ctl_snapshot(kind, std::move(objs));
         } else {
             for (const auto& l : lines->a) {
-                Value ev = parse(l.s);
-                std::string type(ev.sget("type"));
-                Value* o = ev.get("object");
-                if (o && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) ctl_apply(kind, type, std::move(*o));
+                Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
+                                                                            payload_count(kind), raw);
+                if (o.is_obj() && (type == "ADDED" || type == "MODIFIED" || type == "DELETED"))
+                    ctl_apply(kind, type, make_ctl(kind, o, raw));
             }
         }
     } else if (t == "go") {
@@ -1568,6 +1591,32 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && std::string(argv[1]) == "--version") {
         std::puts("ncc-executor 1");
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "--json-selftest") {
+        // one JSON text per stdin line -> "<fingerprint of the DOM> <streaming fingerprint> <split render>"
+        // (tests/test_native_executor_json.py compares them and the render against the input)
+        std::string line;
+        char buf[1 << 16];
+        while (std::fgets(buf, sizeof buf, stdin) != nullptr) {
+            line.assign(buf);
+            while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+            try {
+                Value v = parse(line);
+                uint64_t a = fingerprint(v), b = fingerprint_text(line);
+                std::string render = "-";
+                if (v.is_obj()) {
+                    static const std::string_view keys[2] = {"spec", "data"};
+                    std::string_view raw[2];
+                    Value rest = Parser(line.data(), line.size()).parse_split(keys, 2, raw);
+                    render = dumps_with(rest, {{"spec", raw[0]}, {"data", raw[1]}});
+                }
+                std::printf("%llu %llu %s\n", static_cast<unsigned long long>(a), static_cast<unsigned long long>(b),
+                            render.c_str());
+            } catch (const std::exception& e) {
+                std::printf("error %s\n", e.what());
+            }
+        }
         return 0;
     }
     if (fd < 0) {

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cmath>
+#include <initializer_list>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -121,14 +122,279 @@ public:
         return v;
     }
 
+    // A top-level object whose members named in `keys` are kept as raw JSON text (`raw[i]`, empty when
+    // absent) instead of being decoded: the payloads (spec, data, ...) the executor only fingerprints
+    // and re-sends verbatim.  Returns the object without them.
+    Value parse_split(const std::string_view* keys, size_t n, std::string_view* raw) {
+        Value v;
+        object_split(v, keys, n, raw);
+        ws();
+        if (p_ != e_) fail("trailing characters");
+        return v;
+    }
+    // A watch event {"type": ..., "object": {...}} with the object split as in parse_split.
+    Value parse_event_split(std::string& type, const std::string_view* keys, size_t n, std::string_view* raw) {
+        Value obj;
+        bool have_obj = false;
+        ws();
+        if (p_ >= e_ || *p_ != '{') fail("expected an event object");
+        ++p_;
+        while (true) {
+            ws();
+            if (p_ >= e_ || *p_ != '"') fail("expected key");
+            std::string key;
+            string(key);
+            ws();
+            if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+            ++p_;
+            ws();
+            if (key == "type") {
+                if (p_ >= e_ || *p_ != '"') fail("expected the event type");
+                type.clear();
+                string(type);
+            } else if (key == "object" && p_ < e_ && *p_ == '{') {
+                object_split(obj, keys, n, raw);
+                have_obj = true;
+            } else {
+                skip(0);
+            }
+            ws();
+            if (p_ < e_ && *p_ == ',') {
+                ++p_;
+                continue;
+            }
+            if (p_ < e_ && *p_ == '}') {
+                ++p_;
+                break;
+            }
+            fail("expected ',' or '}'");
+        }
+        ws();
+        if (p_ != e_) fail("trailing characters");
+        if (!have_obj) obj = Value();
+        return obj;
+    }
+    // A top-level object with only the members named in `keys` decoded (the rest skipped).
+    Value parse_only(const std::string_view* keys, size_t n) {
+        Value v;
+        ws();
+        if (p_ >= e_ || *p_ != '{') fail("expected an object");
+        ++p_;
+        v.t = Value::OBJ;
+        ws();
+        if (p_ < e_ && *p_ == '}') {
+            ++p_;
+            return v;
+        }
+        while (true) {
+            ws();
+            if (p_ >= e_ || *p_ != '"') fail("expected key");
+            std::string key;
+            string(key);
+            ws();
+            if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+            ++p_;
+            size_t i = 0;
+            while (i < n && keys[i] != key) ++i;
+            if (i < n) {
+                v.o.emplace_back(std::move(key), Value());
+                value(v.o.back().second, 1);
+            } else {
+                skip(0);
+            }
+            ws();
+            if (p_ < e_ && *p_ == ',') {
+                ++p_;
+                continue;
+            }
+            if (p_ < e_ && *p_ == '}') {
+                ++p_;
+                break;
+            }
+            fail("expected ',' or '}'");
+        }
+        ws();
+        if (p_ != e_) fail("trailing characters");
+        return v;
+    }
+    // fingerprint() of the JSON text without building it (same decoding, same hash)
+    uint64_t fingerprint_text() {
+        uint64_t h = fp(0);
+        ws();
+        if (p_ != e_) fail("trailing characters");
+        return h;
+    }
+
 private:
     const char* p_;
     const char* e_;
+    std::string tmp_;
 
     void ws() {
         while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
     }
     [[noreturn]] void fail(const char* what) { throw JsonError(what); }
+
+    void object_split(Value& v, const std::string_view* keys, size_t n, std::string_view* raw) {
+        for (size_t i = 0; i < n; ++i) raw[i] = std::string_view();
+        ws();
+        if (p_ >= e_ || *p_ != '{') fail("expected an object");
+        ++p_;
+        v.t = Value::OBJ;
+        ws();
+        if (p_ < e_ && *p_ == '}') {
+            ++p_;
+            return;
+        }
+        while (true) {
+            ws();
+            if (p_ >= e_ || *p_ != '"') fail("expected key");
+            std::string key;
+            string(key);
+            ws();
+            if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+            ++p_;
+            ws();
+            size_t i = 0;
+            while (i < n && keys[i] != key) ++i;
+            if (i < n) {
+                const char* s = p_;
+                skip(0);
+                raw[i] = std::string_view(s, static_cast<size_t>(p_ - s));
+            } else {
+                v.o.emplace_back(std::move(key), Value());
+                value(v.o.back().second, 1);
+            }
+            ws();
+            if (p_ < e_ && *p_ == ',') {
+                ++p_;
+                continue;
+            }
+            if (p_ < e_ && *p_ == '}') {
+                ++p_;
+                return;
+            }
+            fail("expected ',' or '}'");
+        }
+    }
+    // Skip one value (strings decoded into tmp_, which also validates their escapes).
+    void skip(int depth) {
+        if (depth > 200) fail("nesting too deep");
+        ws();
+        if (p_ >= e_) fail("unexpected end");
+        char c = *p_;
+        if (c == '"') {
+            tmp_.clear();
+            string(tmp_);
+            return;
+        }
+        if (c == '{' || c == '[') {
+            char close = c == '{' ? '}' : ']';
+            ++p_;
+            ws();
+            if (p_ < e_ && *p_ == close) {
+                ++p_;
+                return;
+            }
+            while (true) {
+                if (c == '{') {
+                    ws();
+                    if (p_ >= e_ || *p_ != '"') fail("expected key");
+                    tmp_.clear();
+                    string(tmp_);
+                    ws();
+                    if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+                    ++p_;
+                }
+                skip(depth + 1);
+                ws();
+                if (p_ < e_ && *p_ == ',') {
+                    ++p_;
+                    continue;
+                }
+                if (p_ < e_ && *p_ == close) {
+                    ++p_;
+                    return;
+                }
+                fail("expected ',' or a closing bracket");
+            }
+        }
+        Value scalar;
+        value(scalar, depth);
+    }
+    uint64_t fp(int depth) {
+        if (depth > 200) fail("nesting too deep");
+        ws();
+        if (p_ >= e_) fail("unexpected end");
+        char c = *p_;
+        if (c == '"') {
+            tmp_.clear();
+            string(tmp_);
+            return hash_str(tmp_);
+        }
+        if (c == '{') {
+            ++p_;
+            uint64_t acc = 0, count = 0;
+            ws();
+            if (p_ < e_ && *p_ == '}') {
+                ++p_;
+                return fp_object(acc, 0);
+            }
+            while (true) {
+                ws();
+                if (p_ >= e_ || *p_ != '"') fail("expected key");
+                tmp_.clear();
+                string(tmp_);
+                uint64_t kh = hash_key(tmp_);
+                ws();
+                if (p_ >= e_ || *p_ != ':') fail("expected ':'");
+                ++p_;
+                acc += fp_member(kh, fp(depth + 1));
+                ++count;
+                ws();
+                if (p_ < e_ && *p_ == ',') {
+                    ++p_;
+                    continue;
+                }
+                if (p_ < e_ && *p_ == '}') {
+                    ++p_;
+                    return fp_object(acc, count);
+                }
+                fail("expected ',' or '}'");
+            }
+        }
+        if (c == '[') {
+            ++p_;
+            std::vector<uint64_t> items;
+            ws();
+            if (p_ < e_ && *p_ == ']') {
+                ++p_;
+                return fp_array(items);
+            }
+            while (true) {
+                items.push_back(fp(depth + 1));
+                ws();
+                if (p_ < e_ && *p_ == ',') {
+                    ++p_;
+                    continue;
+                }
+                if (p_ < e_ && *p_ == ']') {
+                    ++p_;
+                    return fp_array(items);
+                }
+                fail("expected ',' or ']'");
+            }
+        }
+        Value scalar;
+        value(scalar, depth);
+        return fp_scalar(scalar);
+    }
+    static uint64_t hash_str(std::string_view s);
+    static uint64_t hash_key(std::string_view s);
+    static uint64_t fp_member(uint64_t key_hash, uint64_t value_fp);
+    static uint64_t fp_object(uint64_t acc, uint64_t count);
+    static uint64_t fp_array(const std::vector<uint64_t>& items);
+    static uint64_t fp_scalar(const Value& v);
 
     void value(Value& v, int depth) {
         if (depth > 200) fail("nesting too deep");
@@ -559,6 +825,82 @@ inline uint64_t fingerprint(const Value& v) {
         }
     }
     return 0;
+}
+
+// The streaming form (Parser::fingerprint_text) composes the same pieces.
+inline uint64_t Parser::hash_str(std::string_view s) { return hash_bytes(s, 0x5555ULL); }
+inline uint64_t Parser::hash_key(std::string_view s) { return hash_bytes(s, 0x8888ULL); }
+inline uint64_t Parser::fp_member(uint64_t kh, uint64_t vf) { return fmix64(kh ^ (vf * 0x9E3779B97F4A7C15ULL)); }
+inline uint64_t Parser::fp_object(uint64_t acc, uint64_t count) { return fmix64(acc + 0x7777ULL + count); }
+inline uint64_t Parser::fp_array(const std::vector<uint64_t>& items) {
+    uint64_t h = 0x6666ULL + items.size();
+    for (uint64_t x : items) h = fmix64(h * 31 + x);
+    return h;
+}
+inline uint64_t Parser::fp_scalar(const Value& v) { return fingerprint(v); }
+
+inline uint64_t fingerprint_text(std::string_view text) { return Parser(text.data(), text.size()).fingerprint_text(); }
+
+// fp_opt of raw text: absent, null and empty maps/arrays are one value (a nil Go map == an empty one)
+inline bool raw_is_empty(std::string_view raw) {
+    size_t i = 0, n = raw.size();
+    while (i < n && (raw[i] == ' ' || raw[i] == '\n' || raw[i] == '\r' || raw[i] == '\t')) ++i;
+    if (i >= n) return true;
+    if (raw.substr(i, 4) == "null") return true;
+    if (raw[i] != '{' && raw[i] != '[') return false;
+    char close = raw[i] == '{' ? '}' : ']';
+    ++i;
+    while (i < n && (raw[i] == ' ' || raw[i] == '\n' || raw[i] == '\r' || raw[i] == '\t')) ++i;
+    return i < n && raw[i] == close;
+}
+inline uint64_t fp_opt_text(std::string_view raw) {
+    return raw_is_empty(raw) ? fingerprint(Value()) : fingerprint_text(raw);
+}
+
+// dumps(base) with the members named in `over` written as the given raw JSON text (replacing a member of
+// that name, or appended after base's members); an empty text drops the member.
+inline std::string dumps_with(const Value& base, std::initializer_list<std::pair<std::string_view, std::string_view>> over) {
+    std::string out;
+    out.reserve(512);
+    out.push_back('{');
+    bool first = true;
+    auto member = [&](std::string_view k) {
+        if (!first) out.push_back(',');
+        first = false;
+        write_string(out, k);
+        out.push_back(':');
+    };
+    std::vector<bool> done(over.size(), false);
+    if (base.t == Value::OBJ)
+        for (const auto& kv : base.o) {
+            size_t i = 0;
+            bool replaced = false;
+            for (const auto& ov : over) {
+                if (ov.first == kv.first) {
+                    done[i] = true;
+                    replaced = true;
+                    if (!ov.second.empty()) {
+                        member(kv.first);
+                        out.append(ov.second);
+                    }
+                    break;
+                }
+                ++i;
+            }
+            if (replaced) continue;
+            member(kv.first);
+            dump(out, kv.second);
+        }
+    size_t i = 0;
+    for (const auto& ov : over) {
+        if (!done[i] && !ov.second.empty()) {
+            member(ov.first);
+            out.append(ov.second);
+        }
+        ++i;
+    }
+    out.push_back('}');
+    return out;
 }
 
 // fingerprint(x or None): absent, null and empty maps are one value (a nil Go map == an empty one)
