@@ -31,6 +31,9 @@ class Store:
         self._tombstones: dict[ObjectKey, int] = {}  # key -> RV of the observed delete
         self.transform = transform
         self.assume_ttl = assume_ttl
+        # index_guard(obj): a cheap projection of everything the indexers read; an update that leaves it
+        # equal skips the indexers altogether (templates: the mapped environment, i.e. the references)
+        self.index_guard: Callable[[dict], object] | None = None
 
     # ------------------------------------------------------------ indices
     def add_indexer(self, name: str, fn: IndexFunc) -> None:
@@ -49,6 +52,9 @@ class Store:
     def _index(self, key: ObjectKey, old: dict | None, new: dict | None) -> None:
         """Move `key` between index buckets.  Each key's current index values are remembered, so an update
         that leaves them unchanged (the common case: a spec edit keeps the references) touches no set."""
+        g = self.index_guard
+        if g is not None and old is not None and new is not None and g(old) == g(new):
+            return
         for name, fn in self._indexers.items():
             vals = self._index_vals[name]
             ov = vals.get(key, ())

@@ -99,6 +99,10 @@ class Controller(ReconcileMixin):
                 "secret", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in secret_names(t)])
             self.template_informer.store.add_indexer(
                 "configmap", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in configmap_names(t)])
+            # both indices read only the namespace and the mapped environment
+            self.template_informer.store.index_guard = \
+                lambda t: (meta(t).get("namespace"), ((t.get("spec") or {}).get("runtimeEnvironment") or {})
+                           .get("mappedEnvironmentVariables"))
         self._register_handlers()
 
     # ================================================================== handlers
