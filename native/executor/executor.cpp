@@ -575,7 +575,7 @@ struct Informer {
     bool synced = false;
     Event synced_ev;
     std::string last_rv;
-    long long events = 0, relists = 0, echoes = 0;
+    long long events = 0, relists = 0, echoes = 0, foreign = 0;
 };
 
 struct Memo {  // the version our last write produced, and the fingerprints it was meant to carry
@@ -849,13 +849,39 @@ static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch)
 }
 
 static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
-    {  // the echo of our own write, whose response is already cached: nothing to decode
+    {  // nothing to decode: the echo of our own write (its response is already cached), or an object of
+       // another executor's key partition (several executors share a shard's watch streams)
         std::string_view type, ns, name, rv;
-        if (EventScanner(line).scan(type, ns, name, rv) && (type == "ADDED" || type == "MODIFIED")) {
+        std::vector<std::string_view> owners;
+        EventScanner sc(line);
+        if (kind >= 2 && g_opt.parts > 1) sc.owners = &owners;
+        if (sc.scan(type, ns, name, rv) && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) {
             Informer& inf = sh.inf[kind];
-            auto it = inf.store.find(key_of(ns.empty() ? g_opt.ns : std::string(ns), std::string(name)));
+            std::string sns = ns.empty() ? g_opt.ns : std::string(ns);
+            std::string key = key_of(sns, std::string(name));
+            auto it = inf.store.find(key);
             long long r = rv_num(rv);
-            if (it != inf.store.end() && r >= 0 && it->second->rv >= r) {
+            bool mine = true;
+            if (g_opt.parts > 1) {
+                if (kind < 2) {
+                    mine = in_partition(sns, std::string(name));
+                } else if (!owners.empty()) {
+                    mine = false;
+                    for (auto o : owners)
+                        if (in_partition(sns, std::string(o))) mine = true;
+                }
+            }
+            if (!mine) {
+                ++inf.events;
+                ++inf.foreign;
+                inf.last_rv = std::string(rv);
+                if (it != inf.store.end()) {  // it left our partition (as shard_upsert does for !wanted)
+                    inf.store.erase(it);
+                    sh.memo[kind].erase(key);
+                }
+                return;
+            }
+            if (type != "DELETED" && it != inf.store.end() && r >= 0 && it->second->rv >= r) {
                 ++inf.events;
                 ++inf.echoes;
                 inf.last_rv = std::string(rv);
@@ -1534,14 +1560,16 @@ static Task<void> run_main() {
     LOG_INFO("native executor %d ready: %zu shard(s), partition %d/%d, %d workers", g_opt.index, ex.shards.size(),
              g_opt.part, g_opt.parts, g_opt.workers);
     co_await ex.stop_ev.wait();
-    long long echoes = 0, shard_events = 0;
+    long long echoes = 0, shard_events = 0, foreign = 0;
     for (auto& sp : ex.shards)
         for (int k = 0; k < 4; ++k) {
             echoes += sp->inf[k].echoes;
             shard_events += sp->inf[k].events;
+            foreign += sp->inf[k].foreign;
         }
     if (std::getenv("NCC_CPU_REPORT"))
-        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld", shard_events, echoes);
+        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld", shard_events,
+                 echoes, foreign);
     if (std::getenv("NCC_CPU_REPORT"))
         LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld enqueues: object=%lld dependent=%lld "
                  "shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",

@@ -651,6 +651,8 @@ inline std::string dumps(const Value& v) {
 class EventScanner {
 public:
     EventScanner(std::string_view line) : p_(line.data()), e_(line.data() + line.size()) {}
+    // non-null: also collect metadata.ownerReferences[*].name (the partition of a shard dependent)
+    std::vector<std::string_view>* owners = nullptr;
     bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
         bool have_type = false, have_meta = false;
@@ -734,6 +736,37 @@ private:
         while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n') ++p_;
         return p_ > s;
     }
+    bool owner_names() {
+        ws();
+        if (e_ - p_ >= 4 && std::memcmp(p_, "null", 4) == 0) {
+            p_ += 4;
+            return true;
+        }
+        if (!expect('[')) return false;
+        ws();
+        if (p_ < e_ && *p_ == ']') {
+            ++p_;
+            return true;
+        }
+        while (true) {
+            if (!expect('{')) return false;
+            while (true) {
+                std::string_view k, v;
+                if (!str(k) || !expect(':')) return false;
+                if (k == "name") {
+                    if (!str(v)) return false;
+                    owners->push_back(v);
+                } else if (!skip()) {
+                    return false;
+                }
+                if (expect(',')) continue;
+                if (!expect('}')) return false;
+                break;
+            }
+            if (expect(',')) continue;
+            return expect(']');
+        }
+    }
     bool object_meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
         if (!expect('{')) return false;
         while (true) {
@@ -753,6 +786,8 @@ private:
                     } else if (k == "resourceVersion") {
                         if (!str(rv)) return false;
                         have_rv = true;
+                    } else if (owners != nullptr && k == "ownerReferences") {
+                        if (!owner_names()) return false;
                     } else if (!skip()) {
                         return false;
                     }
