@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import time
 
 from ..api import constants as C
 from ..api import resources as R
@@ -446,6 +447,7 @@ class ReconcileMixin:
             return False
         self.stats["reconciles"] += 1
         self.stats["inline_finishes"] += 1
+        self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())  # a reconcile, done in place
         if key in self._pending_event or self.options.event_on_noop:
             self._pending_event.discard(key)
             self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
