@@ -631,18 +631,22 @@ struct Executor {
         return it == ctl[k].end() ? nullptr : it->second;
     }
 
-    // Event-driven enqueue.  Inside a burst (another event less than one coalesce window ago) the key is
-    // parked for the window, so a template and its Secret/ConfigMap changing together reconcile once; an
-    // isolated change after a quiet window goes straight to the workers and pays no coalescing delay.
+    // Event-driven enqueue.  Inside a burst — a run of more than kBurstMin events, each less than one
+    // coalesce window after the previous — the key is parked for the window, so a template and its
+    // Secret/ConfigMap changing together reconcile once.  An isolated change, or a small batch, goes straight
+    // to the workers and pays no coalescing delay (an extra pass there costs nothing that matters).
     // A pass triggered by a dependent is parked `hold` windows: users roll a new configuration out
     // dependents first, and the template's own event (relayed over another watch stream, so often a
     // loop iteration later) pulls the pass in to one window — one pass instead of two.
+    static constexpr int kBurstMin = 32;
     double last_event = -1e18;
+    int run_len = 0;
     void enqueue(int kind, const std::string& ns, const std::string& name, double hold = 1.0) {
         if (!in_partition(ns, name)) return;
         std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
         double now = now_s();
-        bool burst = now - last_event < g_opt.coalesce;
+        run_len = now - last_event < g_opt.coalesce ? run_len + 1 : 1;
+        bool burst = run_len > kBurstMin;
         last_event = now;
         if (g_opt.coalesce > 0 && burst)
             queue.add_after(key, g_opt.coalesce * hold);

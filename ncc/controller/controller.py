@@ -72,6 +72,7 @@ class Controller(ReconcileMixin):
         self._pending_deletes: set = set()
         self._pending_workgroup_deletes: set = set()
         self._last_event = float("-inf")  # monotonic time of the last event-driven enqueue (coalescing)
+        self._run_len = 0  # events in the current run (coalescing)
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
@@ -213,15 +214,18 @@ class Controller(ReconcileMixin):
         else:
             self.queue.add(key)
 
+    BURST_MIN = 32  # events in a run (each < one window after the previous) before coalescing starts
+
     def _coalesce_delay(self) -> float:
-        """The coalesce window inside a burst (another event less than one window ago), else 0."""
+        """The coalesce window inside a burst — a run of more than BURST_MIN events, each less than one window
+        after the previous — else 0: an isolated change or a small batch is reconciled at once."""
         w = self.options.coalesce_window
         if w <= 0:
             return 0.0
         now = time.monotonic()
-        burst = now - self._last_event < w
+        self._run_len = self._run_len + 1 if now - self._last_event < w else 1
         self._last_event = now
-        return w if burst else 0.0
+        return w if self._run_len > self.BURST_MIN else 0.0
 
     def _unwrap(self, obj):
         if isinstance(obj, DeletedFinalStateUnknown):
