@@ -226,7 +226,7 @@ async def config_cold_and_waves(n_shards, T, mode, waves, timeout, secrets=True,
             out["cold_start"]["counts"] = [r["counts"] for r in res]
             out["log_tail"] = topo.log_tail()
             return out
-        lat, t_total = [], 0.0
+        lat, t_total, wave_max = [], 0.0, []
         for v in range(1, waves + 1):
             t0 = await topo.apply(objects(T, v, secrets=secrets, configmaps=configmaps))
             s = time.perf_counter()
@@ -236,11 +236,13 @@ async def config_cold_and_waves(n_shards, T, mode, waves, timeout, secrets=True,
                 out["waves"] = {"ok": False, "at_wave": v, "counts": [r["counts"] for r in res]}
                 out["log_tail"] = topo.log_tail()
                 return out
-            for r in res:
-                lat.extend(latencies(r, t0))
+            wl = [x for r in res for x in latencies(r, t0)]
+            wave_max.append(round(max(wl), 1))
+            lat.extend(wl)
         if waves:
             out["waves"] = {"ok": True, "waves": waves, "objects_per_s": round(waves * objs_per_shard * n_shards /
-                                                                               t_total, 1), **summarize(lat)}
+                                                                               t_total, 1), **summarize(lat),
+                            "max_ms_per_wave": wave_max}
         return out
     finally:
         await topo.stop()

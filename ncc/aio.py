@@ -10,17 +10,33 @@ from __future__ import annotations
 import asyncio
 
 
+def _retrieve(fut: asyncio.Future) -> None:
+    """Mark the outcome of an abandoned future as seen (a cancelled gather() finishes with a CancelledError
+    *exception*, which asyncio would otherwise log as never retrieved)."""
+    if not fut.cancelled():
+        fut.exception()
+
+
+def _abandon(task: asyncio.Future) -> None:
+    task.cancel()
+    task.add_done_callback(_retrieve)
+
+
 async def wait_timeout(aw, timeout: float | None):
     """Await `aw` with a timeout (raises asyncio.TimeoutError); cancellation-safe."""
     task = asyncio.ensure_future(aw)
     if timeout is None:
-        return await task
+        try:
+            return await task
+        except asyncio.CancelledError:
+            _abandon(task)
+            raise
     try:
         done, _ = await asyncio.wait({task}, timeout=timeout)
     except asyncio.CancelledError:
-        task.cancel()
+        _abandon(task)
         raise
     if not done:
-        task.cancel()
+        _abandon(task)
         raise asyncio.TimeoutError()
     return task.result()
