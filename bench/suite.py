@@ -151,6 +151,21 @@ class Topology:
         return await self._post(f"{self.shard_urls[i]}/_fake/markers/wait",
                                 {"want": want, "timeout": timeout, "times": True}, timeout=timeout + 30)
 
+    async def settle(self, T: int, timeout: float, quiet: float = 0.3) -> bool:
+        """Wait until all T templates report Ready on the controller cluster, then `quiet` seconds more."""
+        deadline = time.monotonic() + timeout
+        url = f"{self.ctrl_url}/apis/science.sneaksanddata.com/v1/namespaces/{NS}/nexusalgorithmtemplates"
+        while time.monotonic() < deadline:
+            async with self.session.get(url) as r:
+                items = (await r.json()).get("items") or []
+            ready = sum(1 for t in items if any(c.get("type") == "Ready" and c.get("status") == "True"
+                                                for c in ((t.get("status") or {}).get("conditions") or ())))
+            if ready >= T:
+                await asyncio.sleep(quiet)
+                return True
+            await asyncio.sleep(0.05)
+        return False
+
     async def fault(self, i: int, body: dict) -> None:
         await self._post(f"{self.shard_urls[i]}/_fake/faults", body)
 
@@ -226,6 +241,9 @@ async def config_cold_and_waves(n_shards, T, mode, waves, timeout, secrets=True,
             out["cold_start"]["counts"] = [r["counts"] for r in res]
             out["log_tail"] = topo.log_tail()
             return out
+        # the update waves measure steady state: let the cold start settle first (every template Ready on the
+        # controller cluster, i.e. the coordinator's status writes done), as bench.py's warm-up waves do
+        await topo.settle(T, timeout)
         lat, t_total, wave_max = [], 0.0, []
         for v in range(1, waves + 1):
             t0 = await topo.apply(objects(T, v, secrets=secrets, configmaps=configmaps))
