@@ -64,6 +64,8 @@ def parse_args(argv=None):
                    help="added to every request a shard apiserver serves (emulates controller->shard RTT)")
     p.add_argument("--shard-jitter-ms", type=float, default=0.0,
                    help="uniform extra delay 0..J ms per shard request, on top of --shard-latency-ms")
+    p.add_argument("--tls", action="store_true",
+                   help="every apiserver serves HTTPS with x509 client auth (throwaway CA), as kind/EKS clusters do")
     p.add_argument("--shards-per-rank", type=int, default=1,
                    help="experiments only: shard apiservers hosted per rank (the driver contract is 1)")
     return p.parse_args(argv)
@@ -157,14 +159,22 @@ def want(T: int, version: int) -> list:
             {"plural": "configmaps", "value": str(version), "count": T}]
 
 
-async def set_shard_latency(urls: list, latency_ms: float, jitter_ms: float) -> None:
+async def set_shard_latency(urls: list, latency_ms: float, jitter_ms: float, ssl_ctx=None) -> None:
     """Drive the fake apiservers' fault hook (ncc/fakeapi/server.py `Faults`): every API request a shard
     serves is delayed by latency + U(0, jitter) ms before it is processed, so each controller->shard write
     pays a network round trip as it would against a remote cluster."""
     import aiohttp
-    async with aiohttp.ClientSession() as session:
+    async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=ssl_ctx) if ssl_ctx else None) as session:
         for u in urls:
             await post(session, f"{u}/_fake/faults", {"latency_ms": latency_ms, "jitter_ms": jitter_ms})
+
+
+def client_ssl(pki):
+    """The load generator's own client context for the HTTPS apiservers (their CA, the client certificate)."""
+    import ssl
+    ctx = ssl.create_default_context(cafile=pki.ca_cert)
+    ctx.load_cert_chain(pki.client_cert, pki.client_key)
+    return ctx
 
 
 async def post(session, url, body, timeout=None):
@@ -242,35 +252,48 @@ async def run(args, d: Dist) -> dict | None:
 
     work = tempfile.mkdtemp(prefix=f"ncc-bench-r{d.rank}-")
     procs = []
+    pki = ssl_ctx = None
     try:
+        if args.tls:  # one CA for the job (all ranks are on one node): rank 0 makes it, the others read it
+            from ncc.testing.pki import PKI, make_pki
+            pdir = None
+            if d.rank == 0:
+                pdir = make_pki(os.path.join(work, "pki")).dir
+            pdir = d.broadcast(pdir)
+            j_ = lambda n: os.path.join(pdir, n)  # noqa: E731
+            pki = PKI(pdir, j_("ca.crt"), j_("server.crt"), j_("server.key"), j_("client.crt"), j_("client.key"))
+            ssl_ctx = client_ssl(pki)
         extra = sum((["--marker", m] for m in MARKERS), [])
         S = max(1, args.shards_per_rank)
         my_urls = []
         for j in range(S):
             pf = os.path.join(work, f"shard{j}.url")
-            procs.append(spawn_fakeapi(f"shard-{d.rank * S + j}", pf, extra=extra))
+            procs.append(spawn_fakeapi(f"shard-{d.rank * S + j}", pf, extra=extra, pki=pki))
             my_urls.append(wait_port_file(pf, procs[-1]))
         my_url = my_urls[0]
         if args.shard_latency_ms or args.shard_jitter_ms:
-            await set_shard_latency(my_urls, args.shard_latency_ms, args.shard_jitter_ms)
+            await set_shard_latency(my_urls, args.shard_latency_ms, args.shard_jitter_ms, ssl_ctx)
         urls = [u for us in d.all_gather(my_urls) for u in us]
         ctrl_url = None
         controller = None
         T = args.templates
         if d.rank == 0:
             cpf = os.path.join(work, "controller.url")
-            procs.append(spawn_fakeapi("controller", cpf, extra=extra))
+            procs.append(spawn_fakeapi("controller", cpf, extra=extra, pki=pki))
             ctrl_url = wait_port_file(cpf, procs[-1])
             ctrl_proc = procs[-1]
             shard_dir = os.path.join(work, "shards")
             os.makedirs(shard_dir)
+            tls = dict(ca_data=pki.ca_data, client_cert_data=pki.client_cert_data,
+                       client_key_data=pki.client_key_data) if pki is not None else {}
             for i, u in enumerate(urls):
                 with open(os.path.join(shard_dir, f"shard-{i}.kubeconfig"), "w") as f:
-                    f.write(render_kubeconfig(u, f"shard-{i}"))
+                    f.write(render_kubeconfig(u, f"shard-{i}", **tls))
             ckc = os.path.join(work, "controller.kubeconfig")
             with open(ckc, "w") as f:
-                f.write(render_kubeconfig(ctrl_url, "controller"))
-        async with aiohttp.ClientSession() as session:
+                f.write(render_kubeconfig(ctrl_url, "controller", **tls))
+        connector = aiohttp.TCPConnector(ssl=ssl_ctx) if ssl_ctx is not None else None
+        async with aiohttp.ClientSession(connector=connector) as session:
             if d.rank == 0:
                 await post(session, f"{ctrl_url}/_fake/apply", {"items": wave_objects(T, 0, args.payload)})
                 env = dict(os.environ)
@@ -415,7 +438,8 @@ async def run(args, d: Dist) -> dict | None:
                 "config": {"model": "NexusAlgorithmTemplate fan-out (1 Secret + 1 ConfigMap each)",
                            "global_batch": T, "seq_len": 3, "parallelism": f"shards{d.world}",
                            "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload,
-                           "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms},
+                           "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms,
+                           "tls": bool(args.tls)},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
                 "controller_cpu_us_per_object": round(sum(ctl_cpu.values()) * 1e6 / objs, 1),
