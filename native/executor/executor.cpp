@@ -29,6 +29,7 @@
 // keeps a server that rewrites what we send (CRD defaulting, pruning, mutating webhooks) from
 // triggering a write loop.
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -1656,6 +1657,13 @@ int main(int argc, char** argv) {
         return 2;
     }
     crc_init();
+    {  // soft RLIMIT_NOFILE up to the hard limit (256 connections per shard plus watch streams), as Go does
+        struct rlimit rl;
+        if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur < rl.rlim_max) {
+            rl.rlim_cur = rl.rlim_max == RLIM_INFINITY ? (1u << 20) : std::min<rlim_t>(rl.rlim_max, 1u << 20);
+            setrlimit(RLIMIT_NOFILE, &rl);
+        }
+    }
     if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
     const char* gated = std::getenv("NCC_GATED");
     g_opt.gated = gated != nullptr && std::string(gated) == "1";

@@ -647,6 +647,8 @@ def main(argv=None) -> int:
     for f in _KLOG_BOOL_FLAGS:
         p.add_argument(f"--{f}", nargs="?", const="true", default=None, help=argparse.SUPPRESS)
     args = p.parse_args(_go_style_flags(list(sys.argv[1:] if argv is None else argv)))
+    from .proclimits import raise_nofile_limit
+    raise_nofile_limit()
     if args.version:
         print(__version__)
         return 0

@@ -395,6 +395,8 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
 
 
 def main(argv=None) -> int:
+    from ..proclimits import raise_nofile_limit
+    raise_nofile_limit()
     import argparse
 
     from ..config import load_config

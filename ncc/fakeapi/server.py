@@ -520,6 +520,8 @@ async def serve(args) -> None:
 
 
 def main(argv=None) -> None:
+    from ..proclimits import raise_nofile_limit
+    raise_nofile_limit()
     p = argparse.ArgumentParser(prog="python -m ncc.fakeapi", description="in-process fake kube-apiserver")
     p.add_argument("--name", default="fake")
     p.add_argument("--host", default="127.0.0.1")

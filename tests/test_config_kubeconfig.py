@@ -296,3 +296,17 @@ def test_native_auto_sizing_and_cpu_override(monkeypatch):
     assert auto_sizing(8, cpus=128, native=False) == (4, 4)  # Python executors: k = C = 4
     monkeypatch.setenv("NCC_CPU_SHARE", "128")
     assert cpu_share() == 128
+
+
+def test_nofile_limit_raised_to_hard(monkeypatch):
+    """Every ncc process lifts its soft RLIMIT_NOFILE to the hard limit (as the Go runtime does)."""
+    import resource
+
+    from ncc.proclimits import raise_nofile_limit
+    calls = []
+    monkeypatch.setattr(resource, "getrlimit", lambda r: (1024, 65536))
+    monkeypatch.setattr(resource, "setrlimit", lambda r, v: calls.append(v))
+    assert raise_nofile_limit() == 65536 and calls == [(65536, 65536)]
+    monkeypatch.setattr(resource, "getrlimit", lambda r: (65536, 65536))
+    calls.clear()
+    assert raise_nofile_limit() == 65536 and calls == []
