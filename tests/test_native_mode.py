@@ -581,3 +581,20 @@ async def test_inline_finish_agrees_with_the_status_pass():
         ctl.shard_state[key] = {s: (m["uid"], int(m.get("generation") or 0), None) for s in ("s0", "s1")}
         old, new, _ = ctl._template_synced_status(obj, ["s"], ["c"], ["s0", "s1"])
         assert ctl.finish_inline(key) == (old == new), st
+
+
+def test_coalescing_starts_only_inside_a_burst(monkeypatch):
+    """Small batches and isolated changes are reconciled at once; only a run of more than BURST_MIN events,
+    each less than one window after the previous, is parked for the coalesce window."""
+    import ncc.controller.controller as ctl_mod
+    env = Env(1, coalesce_window=0.002)
+    ctl = env.build()
+    now = [100.0]
+    monkeypatch.setattr(ctl_mod.time, "monotonic", lambda: now[0])
+    delays = []
+    for _ in range(ctl.BURST_MIN + 3):
+        now[0] += 0.0001
+        delays.append(ctl._coalesce_delay())
+    assert delays[:ctl.BURST_MIN] == [0.0] * ctl.BURST_MIN and delays[ctl.BURST_MIN:] == [0.002] * 3
+    now[0] += 0.01  # a quiet window ends the run
+    assert ctl._coalesce_delay() == 0.0
