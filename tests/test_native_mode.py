@@ -587,7 +587,8 @@ def test_coalescing_starts_only_inside_a_burst(monkeypatch):
     """Small batches and isolated changes are reconciled at once; only a run of more than BURST_MIN events,
     each less than one window after the previous, is parked for the coalesce window."""
     import ncc.controller.controller as ctl_mod
-    env = Env(1, coalesce_window=0.002)
+    env = Env(1)
+    env.opts.coalesce_window = 0.002
     ctl = env.build()
     now = [100.0]
     monkeypatch.setattr(ctl_mod.time, "monotonic", lambda: now[0])
