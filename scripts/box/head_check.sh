@@ -4,6 +4,7 @@
 set -o pipefail
 out=${1:-gpurun_out/head}
 mkdir -p $out
+echo "ulimit -n: $(ulimit -n) / hard $(ulimit -Hn); nproc $(nproc)"
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || exit $?
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit $?
 tail -1 $out/smoke.log
