@@ -39,9 +39,10 @@ def executor_path() -> str:
     return os.path.join(ROOT, "ncc", "bin", "ncc-executor")
 
 
-def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
-    """The native shard executor (one translation unit; headers alongside)."""
-    out = executor_path()
+def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False, out: str | None = None) -> str:
+    """The native shard executor (one translation unit; headers alongside); `out` overrides the in-tree
+    path (setup.py builds it into the wheel's ncc/bin/)."""
+    out = out or executor_path()
     flavor = "sanitize" if sanitize else ("debug" if debug else "release")
     stamp = out + ".flavor"
     sources = [os.path.join(EXECUTOR_DIR, f) for f in sorted(os.listdir(EXECUTOR_DIR))

@@ -1,11 +1,33 @@
-"""Packaging hook for the C++ runtime extension `ncc._native` (sources in native/).
+"""Packaging hook for the native code: the C++ runtime extension `ncc._native` (sources in native/) and
+the native shard executor `ncc/bin/ncc-executor` (native/executor/, C++20 + OpenSSL).
 
-`pip install .` / `python -m build` compile it with the same flags as `python native/build.py`, which
-remains the in-tree development build (it is what CI, `__graft_entry__.build()` and the tests use).
+`pip install .` / `python -m build` compile both with the same flags as `python native/build.py`, which
+remains the in-tree development build (it is what CI, `__graft_entry__.build()` and the tests use).  The
+executor needs g++ with C++20 coroutines and the OpenSSL headers (libssl-dev); without them the package
+still installs and native mode runs the Python executor (`executor-impl: auto`).
 """
-from pybind11.setup_helpers import Pybind11Extension
+import os
+import sys
+
+from pybind11.setup_helpers import Pybind11Extension, build_ext
 from setuptools import setup
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class BuildWithExecutor(build_ext):
+    def run(self):
+        super().run()
+        sys.path.insert(0, os.path.join(HERE, "native"))
+        import build as native_build  # native/build.py
+        out = os.path.join(self.build_lib, "ncc", "bin", "ncc-executor")
+        try:
+            native_build.build_executor(out=out)
+        except Exception as e:  # noqa: BLE001 — the Python executor remains
+            print(f"warning: native shard executor not built ({e}); native mode will use the Python executor")
+
 
 setup(ext_modules=[Pybind11Extension(
     "ncc._native", ["native/ncc_native.cpp"], cxx_std=17,
-    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"])])
+    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"])],
+    cmdclass={"build_ext": BuildWithExecutor})
