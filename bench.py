@@ -354,6 +354,7 @@ async def run(args, d: Dist) -> dict | None:
             shard_times: list[dict] = []  # per timed wave: {"plural=value": {"ns/name": t_ns}}
             ctrl_times: list[dict] = []
             t_start = None
+            t0s: dict = {}
             debug = bool(os.environ.get("NCC_BENCH_DEBUG"))
             for step in range(1, total + 1):
                 if step == args.warmup + 1:
@@ -368,7 +369,7 @@ async def run(args, d: Dist) -> dict | None:
                     t0 = a["t0_ns"]
                     if debug:
                         print(f"# wave {step}: apply {(a['t1_ns'] - a['t0_ns']) / 1e6:.1f} ms", file=sys.stderr)
-                t0 = d.broadcast(t0)
+                t0 = t0s[step] = d.broadcast(t0)
                 r = await converge(step, debug)
                 if debug:
                     for plural, ts in r.get("times", {}).items():
@@ -401,6 +402,14 @@ async def run(args, d: Dist) -> dict | None:
                 shard_times.append((await converge(step, True))["times"])
                 if d.rank == 0:  # controller-side commit times of the same objects
                     ctrl_times.append((await converge(step, True, ctrl_url))["times"])
+                    if debug:  # per kind: controller commits vs shard commits, ms after the wave's apply
+                        for plural, ts in ctrl_times[-1].items():
+                            c = sorted(ts.values())
+                            sh = shard_times[-1].get(plural, {})
+                            lt = sorted(t - ts[k.split(":", 1)[-1]] for k, t in sh.items())
+                            print(f"# wave {step} {plural}: controller {(c[0] - t0s[step]) / 1e6:.1f}.."
+                                  f"{(c[-1] - t0s[step]) / 1e6:.1f} ms, latency p50 {lt[len(lt) // 2] / 1e6:.1f} "
+                                  f"max {lt[-1] / 1e6:.1f} ms", file=sys.stderr)
             utils = d.all_gather(util)
             rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)

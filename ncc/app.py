@@ -22,7 +22,7 @@ import os
 import signal
 import sys
 
-from . import __version__, gctune
+from . import __version__, gctune, loopmon
 from . import native as native_ext
 from .api import constants as C
 from .api import resources as R
@@ -225,6 +225,7 @@ class App:
         self._lease_task = None
         self._reload_task = None
         self._gc_task = None
+        self._lag_task = None
         self._shard_files: dict = {}
         self.lost_leadership = False
         self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
@@ -497,6 +498,7 @@ class App:
         if self.cfg.mode == "native":
             gctune.tune()
             self._gc_task = asyncio.ensure_future(gctune.freeze_loop())
+        self._lag_task = loopmon.start(self.options.role)
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
         topo_file = os.environ.get("NCC_TOPOLOGY_FILE")
@@ -529,7 +531,7 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
-        for t in (self._lease_task, self._reload_task, self._gc_task, self._cred_task):
+        for t in (self._lease_task, self._reload_task, self._gc_task, self._cred_task, self._lag_task):
             if t is not None:
                 t.cancel()
                 await asyncio.gather(t, return_exceptions=True)

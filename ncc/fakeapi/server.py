@@ -493,7 +493,14 @@ async def serve(args) -> None:
     url = await server.start(args.host, args.port, ctx)
     from .. import gctune
     gctune.tune()
-    gc_task = asyncio.ensure_future(gctune.freeze_loop())
+    # A test server that keeps what it allocates: freeze every second, never scan the survivors (gctune);
+    # NCC_FAKEAPI_GC=collect restores the controller processes' policy (collect + freeze every 5 s) for A/B runs
+    if os.environ.get("NCC_FAKEAPI_GC") == "collect":
+        gc_task = asyncio.ensure_future(gctune.freeze_loop())
+    else:
+        gc_task = asyncio.ensure_future(gctune.freeze_loop(1.0, collect=False))
+    from .. import loopmon
+    lag_task = loopmon.start(f"fakeapi:{args.name}")
     if args.port_file:
         tmp = args.port_file + ".tmp"
         with open(tmp, "w") as f:
@@ -516,6 +523,8 @@ async def serve(args) -> None:
         asyncio.ensure_future(watch_parent())
     await stop.wait()
     gc_task.cancel()
+    if lag_task is not None:
+        lag_task.cancel()
     await server.stop()
 
 
