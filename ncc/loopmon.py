@@ -5,13 +5,15 @@ that came more than `threshold` ms late: the loop was blocked (a long callback, 
 descheduled).  Each stall, and each GC pass longer than the threshold, is one JSON line — process, wall-clock end of the stall, its length, and the
 cyclic-GC time spent inside it — appended to `NCC_LOOP_LAG_FILE` (default: stderr).  The wall clock is
 `time.time_ns()`, the clock the fake apiservers stamp commits with, so stalls line up with a bench wave's
-per-object timings.
+per-object timings.  `NCC_LOOP_LAG_DEBUG=1` also runs the loop in asyncio debug mode (slower) and writes
+asyncio's "Executing <callback> took N seconds" reports past the threshold, which name the callback.
 """
 from __future__ import annotations
 
 import asyncio
 import gc
 import json
+import logging
 import os
 import sys
 import time
@@ -38,10 +40,27 @@ class _GcClock:
                                        "end_ns": time.time_ns()}) + "\n")
 
 
+class _JsonLines(logging.Handler):
+    def __init__(self, name: str, out):
+        super().__init__(logging.WARNING)
+        self.name_, self.out = name, out
+
+    def emit(self, record: logging.LogRecord) -> None:
+        self.out.write(json.dumps({"asyncio": record.getMessage()[:500], "process": self.name_,
+                                   "end_ns": time.time_ns()}) + "\n")
+
+
 async def _monitor(name: str, threshold_ms: float, path: str | None) -> None:
     out = open(path, "a", buffering=1) if path else sys.stderr
     gcc = _GcClock(name, threshold_ms, out)
     gc.callbacks.append(gcc)
+    handler = None
+    if os.environ.get("NCC_LOOP_LAG_DEBUG") == "1":
+        loop = asyncio.get_running_loop()
+        loop.set_debug(True)
+        loop.slow_callback_duration = threshold_ms / 1e3
+        handler = _JsonLines(name, out)
+        logging.getLogger("asyncio").addHandler(handler)
     try:
         last, gc_last = time.perf_counter(), 0.0
         while True:
@@ -55,6 +74,8 @@ async def _monitor(name: str, threshold_ms: float, path: str | None) -> None:
             last, gc_last = now, gcc.total
     finally:
         gc.callbacks.remove(gcc)
+        if handler is not None:
+            logging.getLogger("asyncio").removeHandler(handler)
         if path:
             out.close()
 
