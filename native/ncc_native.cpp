@@ -30,8 +30,10 @@
 //  * loads(bytes) — JSON decoder straight into CPython objects.
 //  * template_event_slim(line) — a template watch line decoded into the coordinator's slim form
 //    (metadata without managedFields, status, and a spec reduced to its references + raw digest).
+//  * ReportTable — the coordinator's fold of shard-executor reports, fed raw IPC frames.
 
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <Python.h>
 
@@ -51,7 +53,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 15
+#define NCC_NATIVE_ABI 16
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -1546,7 +1548,10 @@ py::object loads(py::bytes data) {
         o = nullptr;
     }
     if (o == nullptr) {
-        if (PyErr_Occurred()) throw py::error_already_set();
+        // invalid UTF-8 inside a string is malformed input too: None, and the caller's stdlib fallback
+        // reports it
+        if (PyErr_Occurred() && !PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) throw py::error_already_set();
+        PyErr_Clear();
         return py::none();
     }
     return py::reinterpret_steal<py::object>(o);
@@ -1564,6 +1569,357 @@ py::object template_event_slim(py::bytes line) {
     return py::reinterpret_steal<py::object>(o);
 }
 
+
+// ----------------------------------------------------------------------------- executor reports
+// The coordinator folds every shard executor's per-pass reports into "which shards have reported on which
+// version of each object" (ncc/controller/reports.py is the Python twin and the specification).  At 8
+// shards that is 8 reports per template and wave; decoding them into dicts and folding them in Python was
+// a third of the coordinator's CPU.  ReportTable.feed takes a raw IPC frame (ncc/controller/ipc.py: one
+// msgpack message, or an array of them), folds the reports natively and hands back only what Python acts
+// on: the keys whose report set became complete, the keys whose pass wrote, the failing shards, and every
+// other message decoded.
+
+class MpReader {
+  public:
+    MpReader(const char* p, size_t n) : p_(reinterpret_cast<const uint8_t*>(p)), e_(p_ + n) {}
+    bool at_end() const { return p_ == e_; }
+
+    [[noreturn]] static void fail() { throw py::value_error("msgpack: malformed frame"); }
+    void need(size_t n) const {
+        if (static_cast<size_t>(e_ - p_) < n) fail();
+    }
+    uint8_t peek() const {
+        need(1);
+        return *p_;
+    }
+    uint64_t be(int n) {
+        need(static_cast<size_t>(n));
+        uint64_t v = 0;
+        for (int k = 0; k < n; ++k) v = (v << 8) | p_[k];
+        p_ += n;
+        return v;
+    }
+    // container headers: false (nothing consumed) when the next value is not of that kind
+    bool map_len(size_t& n) {
+        uint8_t c = peek();
+        if ((c & 0xf0) == 0x80) { ++p_; n = c & 0x0f; return true; }
+        if (c == 0xde) { ++p_; n = be(2); return true; }
+        if (c == 0xdf) { ++p_; n = be(4); return true; }
+        return false;
+    }
+    bool arr_len(size_t& n) {
+        uint8_t c = peek();
+        if ((c & 0xf0) == 0x90) { ++p_; n = c & 0x0f; return true; }
+        if (c == 0xdc) { ++p_; n = be(2); return true; }
+        if (c == 0xdd) { ++p_; n = be(4); return true; }
+        return false;
+    }
+    bool str(std::string_view& out) {  // str or bin
+        uint8_t c = peek();
+        size_t n;
+        if ((c & 0xe0) == 0xa0) { ++p_; n = c & 0x1f; }
+        else if (c == 0xd9 || c == 0xc4) { ++p_; n = be(1); }
+        else if (c == 0xda || c == 0xc5) { ++p_; n = be(2); }
+        else if (c == 0xdb || c == 0xc6) { ++p_; n = be(4); }
+        else return false;
+        need(n);
+        out = std::string_view(reinterpret_cast<const char*>(p_), n);
+        p_ += n;
+        return true;
+    }
+    bool integer(int64_t& v) {
+        uint8_t c = peek();
+        if (c <= 0x7f) { ++p_; v = c; return true; }
+        if (c >= 0xe0) { ++p_; v = static_cast<int8_t>(c); return true; }
+        switch (c) {
+            case 0xcc: ++p_; v = static_cast<int64_t>(be(1)); return true;
+            case 0xcd: ++p_; v = static_cast<int64_t>(be(2)); return true;
+            case 0xce: ++p_; v = static_cast<int64_t>(be(4)); return true;
+            case 0xcf: ++p_; v = static_cast<int64_t>(be(8)); return true;
+            case 0xd0: ++p_; v = static_cast<int8_t>(be(1)); return true;
+            case 0xd1: ++p_; v = static_cast<int16_t>(be(2)); return true;
+            case 0xd2: ++p_; v = static_cast<int32_t>(be(4)); return true;
+            case 0xd3: ++p_; v = static_cast<int64_t>(be(8)); return true;
+            default: return false;
+        }
+    }
+    bool nil() {
+        if (peek() != 0xc0) return false;
+        ++p_;
+        return true;
+    }
+    // Python truthiness of the next value, consuming it (nil/false/0/""/empty containers are false)
+    bool truthy() {
+        uint8_t c = peek();
+        if (c == 0xc0 || c == 0xc2) { ++p_; return false; }
+        if (c == 0xc3) { ++p_; return true; }
+        int64_t i;
+        if (integer(i)) return i != 0;
+        std::string_view s;
+        if (str(s)) return !s.empty();
+        size_t n;
+        const uint8_t* at = p_;
+        if (map_len(n) || arr_len(n)) {
+            p_ = at;
+            skip();
+            return n != 0;
+        }
+        skip();  // floats
+        return true;
+    }
+    void skip(int depth = 0) {
+        if (depth > 64) fail();
+        size_t n;
+        std::string_view s;
+        int64_t i;
+        if (map_len(n)) {
+            for (size_t k = 0; k < 2 * n; ++k) skip(depth + 1);
+        } else if (arr_len(n)) {
+            for (size_t k = 0; k < n; ++k) skip(depth + 1);
+        } else if (str(s) || integer(i) || nil()) {
+        } else {
+            uint8_t c = peek();
+            if (c == 0xc2 || c == 0xc3) { ++p_; }
+            else if (c == 0xca) { ++p_; be(4); }
+            else if (c == 0xcb) { ++p_; be(8); }
+            else fail();
+        }
+    }
+    // generic decode into a new reference (msgpack -> Python, as msgpack.unpackb(raw=False) does)
+    PyObject* value(int depth = 0) {
+        if (depth > 64) fail();
+        size_t n;
+        std::string_view s;
+        int64_t i;
+        uint8_t c = peek();
+        if (map_len(n)) {
+            PyObject* d = PyDict_New();
+            if (d == nullptr) throw py::error_already_set();
+            for (size_t k = 0; k < n; ++k) {
+                PyObject* kk = nullptr;
+                PyObject* vv = nullptr;
+                try {
+                    kk = value(depth + 1);
+                    vv = value(depth + 1);
+                } catch (...) {
+                    Py_XDECREF(kk);
+                    Py_DECREF(d);
+                    throw;
+                }
+                int rc = PyDict_SetItem(d, kk, vv);
+                Py_DECREF(kk);
+                Py_DECREF(vv);
+                if (rc != 0) { Py_DECREF(d); throw py::error_already_set(); }
+            }
+            return d;
+        }
+        if (arr_len(n)) {
+            PyObject* l = PyList_New(static_cast<Py_ssize_t>(n));
+            if (l == nullptr) throw py::error_already_set();
+            for (size_t k = 0; k < n; ++k) {
+                try {
+                    PyList_SET_ITEM(l, static_cast<Py_ssize_t>(k), value(depth + 1));
+                } catch (...) {
+                    for (size_t j = k; j < n; ++j) { Py_INCREF(Py_None); PyList_SET_ITEM(l, static_cast<Py_ssize_t>(j), Py_None); }
+                    Py_DECREF(l);
+                    throw;
+                }
+            }
+            return l;
+        }
+        if ((c & 0xe0) == 0xa0 || c == 0xd9 || c == 0xda || c == 0xdb) {
+            str(s);
+            PyObject* o = PyUnicode_DecodeUTF8(s.data(), static_cast<Py_ssize_t>(s.size()), "strict");
+            if (o == nullptr) throw py::error_already_set();
+            return o;
+        }
+        if (c == 0xc4 || c == 0xc5 || c == 0xc6) {
+            str(s);
+            return PyBytes_FromStringAndSize(s.data(), static_cast<Py_ssize_t>(s.size()));
+        }
+        if (c == 0xcf) {  // uint64: may not fit int64
+            ++p_;
+            return PyLong_FromUnsignedLongLong(be(8));
+        }
+        if (integer(i)) return PyLong_FromLongLong(i);
+        if (nil()) Py_RETURN_NONE;
+        if (c == 0xc2) { ++p_; Py_RETURN_FALSE; }
+        if (c == 0xc3) { ++p_; Py_RETURN_TRUE; }
+        if (c == 0xca) {
+            ++p_;
+            uint32_t u = static_cast<uint32_t>(be(4));
+            float f;
+            std::memcpy(&f, &u, 4);
+            return PyFloat_FromDouble(f);
+        }
+        if (c == 0xcb) {
+            ++p_;
+            uint64_t u = be(8);
+            double d;
+            std::memcpy(&d, &u, 8);
+            return PyFloat_FromDouble(d);
+        }
+        fail();
+    }
+    const uint8_t* pos() const { return p_; }
+    void seek(const uint8_t* q) { p_ = q; }
+
+  private:
+    const uint8_t* p_;
+    const uint8_t* e_;
+};
+
+class ReportTable {
+  public:
+    struct Slot {
+        std::string shard;
+        std::string uid;
+        int64_t gen = 0;
+        std::string err;  // empty: success (an empty error string is falsy in the Python twin too)
+    };
+
+    void set_shards(const std::vector<std::string>& shards) { shards_ = shards; }
+    std::vector<std::string> shards() const { return shards_; }
+    size_t size() const { return state_.size(); }
+    void pop(const std::string& key) { state_.erase(key); }
+    void drop_shards(const std::vector<std::string>& names) {
+        for (auto& kv : state_) {
+            auto& v = kv.second;
+            v.erase(std::remove_if(v.begin(), v.end(), [&](const Slot& s) {
+                        return std::find(names.begin(), names.end(), s.shard) != names.end();
+                    }), v.end());
+        }
+    }
+
+    // feed(frame body, batch) -> (complete keys, wrote keys, failing shards, other messages, reports, pending)
+    py::tuple feed(py::bytes body, bool batch) {
+        std::string_view v = bytes_view(body);
+        MpReader r(v.data(), v.size());
+        py::list complete, wrote, errors, others;
+        int64_t reports = 0, pending = 0;
+        size_t n = 1;
+        if (batch && !r.arr_len(n)) MpReader::fail();
+        for (size_t k = 0; k < n; ++k) {
+            const uint8_t* start = r.pos();
+            int rc = report(r, complete, wrote, errors);
+            if (rc < 0) {  // not a report: decode it for Python
+                r.seek(start);
+                others.append(py::reinterpret_steal<py::object>(r.value()));
+                continue;
+            }
+            ++reports;
+            if (rc == 0) ++pending;
+        }
+        if (!r.at_end()) MpReader::fail();
+        return py::make_tuple(complete, wrote, errors, others, reports, pending);
+    }
+
+    // readiness(key, uid, generation) -> None while some shard has not reported on this version, else
+    // {shard: error | None} in shard order
+    py::object readiness(const std::string& key, const std::string& uid, int64_t gen) const {
+        auto it = state_.find(key);
+        if (it == state_.end()) return py::none();
+        py::dict out;
+        for (const auto& s : shards_) {
+            const Slot* e = find(it->second, s);
+            if (e == nullptr || e->uid != uid || e->gen < gen) return py::none();
+            if (e->err.empty())
+                out[py::str(s)] = py::none();
+            else
+                out[py::str(s)] = py::str(e->err);
+        }
+        return std::move(out);
+    }
+
+  private:
+    static const Slot* find(const std::vector<Slot>& v, std::string_view shard) {
+        for (const auto& s : v)
+            if (s.shard == shard) return &s;
+        return nullptr;
+    }
+
+    // One message at the reader.  -1: not a report (nothing folded; the caller rewinds), 0: folded, some
+    // shard still to report on this version, 1: folded and complete.
+    int report(MpReader& r, py::list& complete, py::list& wrote, py::list& errors) {
+        size_t n;
+        if (!r.map_len(n)) return -1;
+        const uint8_t* body = r.pos();
+        // first pass: is it {"t": "report", ...}?  (key order is the sender's)
+        bool is_report = false;
+        for (size_t k = 0; k < n; ++k) {
+            std::string_view key, val;
+            if (!r.str(key)) return -1;
+            if (key == "t") {
+                if (!r.str(val)) return -1;
+                is_report = val == "report";
+                break;
+            }
+            r.skip();
+        }
+        if (!is_report) return -1;
+        r.seek(body);
+        std::string_view rkey, uid;
+        int64_t gen = 0;
+        bool w = false, have_k = false;
+        const uint8_t* results = nullptr;
+        for (size_t k = 0; k < n; ++k) {
+            std::string_view key;
+            if (!r.str(key)) MpReader::fail();
+            if (key == "k") {
+                if (!r.str(rkey)) MpReader::fail();
+                have_k = true;
+            } else if (key == "u") {
+                if (!r.str(uid)) MpReader::fail();
+            } else if (key == "g") {
+                if (!r.integer(gen) && !r.nil()) MpReader::fail();
+            } else if (key == "w") {
+                w = r.truthy();
+            } else if (key == "r") {
+                results = r.pos();
+                r.skip();
+            } else {
+                r.skip();
+            }
+        }
+        if (!have_k || results == nullptr) MpReader::fail();
+        const uint8_t* end = r.pos();
+        std::string skey(rkey);
+        auto& slots = state_[skey];
+        r.seek(results);
+        size_t m;
+        if (!r.map_len(m)) MpReader::fail();
+        bool changed = false;
+        for (size_t k = 0; k < m; ++k) {
+            std::string_view shard, err;
+            if (!r.str(shard)) MpReader::fail();
+            if (!r.nil() && !r.str(err)) MpReader::fail();
+            Slot* s = const_cast<Slot*>(find(slots, shard));
+            if (s == nullptr) {
+                slots.push_back(Slot{std::string(shard), {}, 0, {}});
+                s = &slots.back();
+                changed = true;
+            } else if (!changed && (s->uid != uid || s->gen != gen || s->err != err)) {
+                changed = true;
+            }
+            s->uid.assign(uid.data(), uid.size());
+            s->gen = gen;
+            s->err.assign(err.data(), err.size());
+            if (!err.empty()) errors.append(py::str(shard.data(), shard.size()));
+        }
+        r.seek(end);
+        py::str pkey(skey);
+        if (w) wrote.append(pkey);
+        for (const auto& sh : shards_) {
+            const Slot* e = find(slots, sh);
+            if (e == nullptr || e->uid != uid || e->gen < gen) return 0;
+        }
+        if (changed || w) complete.append(pkey);  // a repeat of a complete set changes nothing
+        return 1;
+    }
+
+    std::vector<std::string> shards_;
+    std::unordered_map<std::string, std::vector<Slot>> state_;
+};
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -1611,4 +1967,15 @@ PYBIND11_MODULE(_native, m) {
         .def("add_rate_limited", &RateLimitingQueue::add_rate_limited)
         .def("forget", &RateLimitingQueue::forget)
         .def("num_requeues", &RateLimitingQueue::num_requeues);
+    py::class_<ReportTable>(m, "ReportTable")
+        .def(py::init<>())
+        .def("set_shards", &ReportTable::set_shards, py::arg("shards"))
+        .def("shards", &ReportTable::shards)
+        .def("feed", &ReportTable::feed, py::arg("body"), py::arg("batch"),
+             "fold a raw executor IPC frame: (complete keys, wrote keys, failing shards, other messages, "
+             "reports, pending)")
+        .def("readiness", &ReportTable::readiness, py::arg("key"), py::arg("uid"), py::arg("generation"))
+        .def("pop", &ReportTable::pop, py::arg("key"))
+        .def("drop_shards", &ReportTable::drop_shards, py::arg("names"))
+        .def("__len__", &ReportTable::size);
 }

@@ -488,7 +488,8 @@ class App:
             native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
                                      env=exec_env, per_shard=self.per_shard, part_base=part, part_stride=parts,
-                                     gated=gated, relay=self.relay, native_config=native_cfg)
+                                     gated=gated, relay=self.relay, native_config=native_cfg,
+                                     on_frame=controller.on_executor_frame)
             if native_cfg is not None:
                 self._cred_task = asyncio.ensure_future(native_cfg.refresh_loop(self.pool))
             self.pool.start()

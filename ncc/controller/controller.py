@@ -19,6 +19,8 @@ import contextvars
 import logging
 import time
 
+import msgpack
+
 from ..api import constants as C
 from ..api.objects import ObjectKey, meta
 from ..api.refs import configmap_names, same_references, secret_names, template_owner_names
@@ -28,6 +30,7 @@ from ..workqueue.queue import WorkQueue
 from .events import EventRecorder, FakeRecorder
 from .executor import key_part
 from .options import ControllerOptions
+from .reports import make_report_table
 from .reconcile import ReconcileMixin, spec_matches, data_matches
 
 log = logging.getLogger("ncc.controller")
@@ -76,17 +79,18 @@ class Controller(ReconcileMixin):
         self._workers: list[asyncio.Task] = []
         self._aux: list[asyncio.Task] = []
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
-                      "reports_pending": 0, "early_passes_skipped": 0, "inline_finishes": 0}
+                      "reports_pending": 0, "early_passes_skipped": 0, "inline_finishes": 0, "inline_superseded": 0}
         self._inline_keys: set = set()  # coordinator: keys with a complete report set, finished in one batch
         self._inline_timer = None
         self.ready = asyncio.Event()  # workers running
         self.caches_synced = asyncio.Event()  # controller (and shard) caches synced
         self.role = o.role
+        # coordinator role: key -> {shard: (uid, generation, error)} of the executors' reports (native table)
+        self.reports = make_report_table()
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
         self.reporter = None  # executor role: callable(msg) sending results to the coordinator
         self.on_ready = None  # executor role: called once caches are synced and workers run
         self.on_synced = None  # executor role: called once caches are synced (before a gate opens)
-        self.shard_state: dict[str, dict] = {}  # coordinator role: key -> {shard: (uid, generation, error)}
         self._pending_event: set = set()
         # adoption_cache: template key → resourceVersion whose references were last verified as adopted
         self._adopted: dict[str, str] = {}
@@ -105,6 +109,16 @@ class Controller(ReconcileMixin):
                 lambda t: (meta(t).get("namespace"), ((t.get("spec") or {}).get("runtimeEnvironment") or {})
                            .get("mappedEnvironmentVariables"))
         self._register_handlers()
+
+    @property
+    def all_shard_names(self) -> list[str]:
+        return self._all_shard_names
+
+    @all_shard_names.setter
+    def all_shard_names(self, names) -> None:
+        # the report table decides completeness against this list: assign a new list, never mutate in place
+        self._all_shard_names = list(names)
+        self.reports.set_shards(self._all_shard_names)
 
     # ================================================================== handlers
     def _register_handlers(self) -> None:
@@ -341,26 +355,28 @@ class Controller(ReconcileMixin):
                        "g": int(m.get("generation") or 0), "r": results, "w": self._last_pass_wrote()})
 
     def on_executor_message(self, index: int, msg: dict) -> None:
-        """Coordinator: fold an executor report into `shard_state` and re-evaluate that object."""
-        if msg.get("t") != "report":
-            return
-        self.stats["reports"] += 1
-        key = msg["k"]
-        st = self.shard_state.setdefault(key, {})
-        uid, gen = msg["u"], msg["g"]
-        for shard, err in msg["r"].items():
-            st[shard] = (uid, gen, err)
-            if err:
-                self.metrics.count(C.SHARD_SYNC_ERRORS_METRIC, 1, {"shard": shard})
-        if msg.get("w"):
-            self._pending_event.add(key)
+        """Coordinator: fold one decoded executor message (tests, and executors without raw frames)."""
+        if isinstance(msg, dict) and msg.get("t") == "report":
+            self.on_executor_frame(index, msgpack.packb(msg, use_bin_type=True), False)
+
+    def on_executor_frame(self, index: int, body: bytes, batch: bool) -> list:
+        """Coordinator: fold a raw IPC frame of executor `index` into the report table and re-evaluate
+        the objects whose report set it completed.  Returns the frame's other messages, decoded."""
+        complete, wrote, errors, others, reports, pending = self.reports.feed(body, batch)
+        st = self.stats
+        st["reports"] += reports
+        st["reports_pending"] += pending
+        for shard in errors:
+            self.metrics.count(C.SHARD_SYNC_ERRORS_METRIC, 1, {"shard": shard})
+        if wrote:
+            self._pending_event.update(wrote)
         # Only a complete set of reports for this object version can change its status: re-evaluate
         # then, instead of once per executor report (N× fewer coordinator passes at N shards).
-        for s in self.all_shard_names:
-            e = st.get(s)
-            if e is None or e[0] != uid or e[1] < gen:
-                self.stats["reports_pending"] += 1
-                return
+        for key in complete:
+            self._reports_complete(key)
+        return others
+
+    def _reports_complete(self, key: str) -> None:
         if not self.options.inline_finish:
             self._enqueue_key(key)
             return
@@ -387,18 +403,8 @@ class Controller(ReconcileMixin):
 
     def shard_readiness(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else {shard: error|None}."""
-        st = self.shard_state.get(key)
-        if st is None:
-            return None
         m = obj.get("metadata") or {}
-        uid, gen = m.get("uid", ""), int(m.get("generation") or 0)
-        out = {}
-        for s in self.all_shard_names:
-            e = st.get(s)
-            if e is None or e[0] != uid or e[1] < gen:
-                return None
-            out[s] = e[2]
-        return out
+        return self.reports.readiness(key, m.get("uid", ""), int(m.get("generation") or 0))
 
     def debug_snapshot(self) -> dict:
         """Queue/informer/shard state for operators (SIGUSR1 dump, /debug/state)."""
@@ -420,7 +426,7 @@ class Controller(ReconcileMixin):
                                                        ("secrets", s.secret_informer),
                                                        ("configmaps", s.configmap_informer))}
                        for s in self.shards},
-            "pending_deletes": len(self._pending_deletes), "shard_state": len(self.shard_state),
+            "pending_deletes": len(self._pending_deletes), "shard_state": len(self.reports),
         }
 
     # ================================================================== helpers
@@ -500,25 +506,22 @@ class Controller(ReconcileMixin):
             self._register_shard_handlers(shard)
         shard.start()
         if shard.name not in self.all_shard_names:
-            self.all_shard_names.append(shard.name)
+            self.all_shard_names = self.all_shard_names + [shard.name]
 
     async def remove_shard(self, name: str) -> None:
         for shard in [s for s in self.shards if s.name == name]:
             self.shards.remove(shard)
             await shard.stop()
         if name in self.all_shard_names:
-            self.all_shard_names.remove(name)
-        for st in self.shard_state.values():
-            st.pop(name, None)
+            self.all_shard_names = [s for s in self.all_shard_names if s != name]
+        self.reports.drop_shards([name])
 
     def set_shard_names(self, names: list[str]) -> None:
         """Coordinator: the shard set changed; statuses are re-derived from the executors' reports."""
         gone = set(self.all_shard_names) - set(names)
         self.all_shard_names = list(names)
         if gone:
-            for st in self.shard_state.values():
-                for n in gone:
-                    st.pop(n, None)
+            self.reports.drop_shards(sorted(gone))
 
     async def wait_for_caches(self) -> bool:
         """Run's cache barrier (controller.go:862-871)."""

@@ -85,6 +85,8 @@ class ExecutorHandle:
         self.part = part
         self.parts = parts
         self.on_message = on_message
+        # coordinator: folds raw frames (reports) natively and returns the other messages, decoded
+        self.on_frame = None
         self.env = env
         self.proc: asyncio.subprocess.Process | None = None
         self.channel: Channel | None = None
@@ -160,9 +162,17 @@ class ExecutorHandle:
             self.synced.clear()
             await self._spawn()
             while True:
-                batch = await self.channel.recv()
-                if batch is None:
-                    break
+                if self.on_frame is not None:
+                    frames = await self.channel.recv_frames()
+                    if frames is None:
+                        break
+                    batch = []
+                    for body, is_batch in frames:
+                        batch += self.on_frame(self.index, body, is_batch)
+                else:
+                    batch = await self.channel.recv()
+                    if batch is None:
+                        break
                 for msg in batch:
                     t = msg.get("t")
                     if t == "ready":
@@ -215,7 +225,7 @@ class ExecutorPool:
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
                  part_base: int = 0, part_stride: int = 1, gated: bool = False, relay=None,
-                 native_config=None):
+                 native_config=None, on_frame=None):
         """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
         mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
         keys are exactly a share of this coordinator's."""
@@ -223,6 +233,7 @@ class ExecutorPool:
         self.part_base = part_base
         self.part_stride = max(1, part_stride)
         self.on_message = on_message
+        self.on_frame = on_frame  # raw-frame report folding (Controller.on_executor_frame)
         self.env = env
         self.relay = relay  # coordinator's WatchRelay: executors get the controller cluster from it
         self.native_config = native_config  # NativeExecutorConfig: run ncc/bin/ncc-executor instead of Python
@@ -239,6 +250,7 @@ class ExecutorPool:
               for j in range(self.per_shard)]
         for h in hs:
             h.gated, h.gate_open = self.gated, self.gate_open
+            h.on_frame = self.on_frame
             if self.relay is not None:
                 h.on_spawn, h.on_exit, h.on_need = self.relay.attach, self.relay.detach, self.relay.on_need
             if self.native_config is not None:

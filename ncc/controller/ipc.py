@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import asyncio
+import collections
 import struct
 
 import msgpack
@@ -18,6 +19,9 @@ class Channel:
         self._flush_handle: asyncio.Handle | None = None
         self.sent = 0
         self.received = 0
+        self._rbuf = bytearray()  # bytes read but not yet framed
+        self._rpos = 0
+        self._frames: collections.deque = collections.deque()  # framed, not yet handed out (recv_raw)
 
     def send(self, msg) -> None:
         """Queue a message; frames are coalesced and written on the next loop iteration."""
@@ -53,22 +57,62 @@ class Channel:
 
     async def recv(self) -> list | None:
         """Next batch of messages (list), or None at EOF."""
-        try:
-            hdr = await self.reader.readexactly(_HDR.size)
-        except (asyncio.IncompleteReadError, ConnectionError):
+        raw = await self.recv_raw()
+        if raw is None:
             return None
-        (n,) = _HDR.unpack(hdr)
-        batch = bool(n & 0x80000000)
-        n &= 0x7FFFFFFF
-        if n > MAX_FRAME:
-            raise ValueError(f"frame too large: {n}")
-        try:
-            body = await self.reader.readexactly(n)
-        except (asyncio.IncompleteReadError, ConnectionError):
-            return None
-        self.received += 1
+        body, batch = raw
         msg = msgpack.unpackb(body, raw=False)
         return msg if batch else [msg]
+
+    async def recv_raw(self) -> tuple[bytes, bool] | None:
+        """Next frame undecoded: (msgpack body, whether it is an array of messages), or None at EOF."""
+        if not self._frames:
+            frames = await self.recv_frames()
+            if frames is None:
+                return None
+            self._frames.extend(frames)
+        return self._frames.popleft()
+
+    async def recv_frames(self) -> list | None:
+        """Every complete frame that has arrived, undecoded ([(body, batch), ...], at least one), or None at
+        EOF.  One read per call instead of two awaited `readexactly` per frame: a coordinator at 8 shards
+        receives ~70k small report frames per 8 waves."""
+        if self._frames:
+            out = list(self._frames)
+            self._frames.clear()
+            return out
+        buf = self._rbuf
+        while True:
+            out = []
+            pos, end = self._rpos, len(buf)
+            with memoryview(buf) as mv:  # released before the buffer is resized below
+                while end - pos >= 4:
+                    (n,) = _HDR.unpack_from(buf, pos)
+                    batch = bool(n & 0x80000000)
+                    n &= 0x7FFFFFFF
+                    if n > MAX_FRAME:
+                        raise ValueError(f"frame too large: {n}")
+                    if end - pos - 4 < n:
+                        break
+                    out.append((bytes(mv[pos + 4:pos + 4 + n]), batch))
+                    pos += 4 + n
+            if pos == end:
+                buf.clear()
+                pos = 0
+            elif pos > (1 << 16):
+                del buf[:pos]
+                pos = 0
+            self._rpos = pos
+            if out:
+                self.received += len(out)
+                return out
+            try:
+                data = await self.reader.read(1 << 18)
+            except ConnectionError:
+                data = b""
+            if not data:
+                return None
+            buf += data
 
     def close(self) -> None:
         try:

@@ -1,0 +1,106 @@
+"""The coordinator's fold of shard-executor reports.
+
+Every executor pass over a template (or workgroup) ends in one report to the coordinator:
+`{"t": "report", "k": key, "u": uid, "g": generation, "r": {shard: error | None}, "w": wrote}`.  The coordinator
+keeps, per object key and shard, the last reported (uid, generation, error) and derives the status condition
+once *every* shard has reported on the current version (`readiness`).  This is the native mode's version of
+the reference's sequential shard loop outcome (`/root/reference/controller.go:790-831`, one error aborts the
+loop; here each shard's error is kept and listed).
+
+`ReportTable` is the specification and the fallback; `ncc._native.ReportTable` (native/ncc_native.cpp) is
+the implementation the coordinator uses.  Both are fed raw IPC frames (`ipc.Channel.recv_raw`: one msgpack
+message, or an array of them), so at 8 shards the 8 reports per template and wave are folded without
+materialising a dict per report.  tests/test_reports.py drives the two in lock-step.
+
+`feed(body, batch)` returns `(complete, wrote, errors, others, reports, pending)`:
+- `complete`: keys whose report leaves a complete set for the reported version, when the report changed a
+  per-shard result or wrote (a repeat of an already complete set with nothing new is not a completion: at 8
+  shards each executor's second, dependent-triggered pass would otherwise re-evaluate the template ~5 times
+  per wave);
+- `wrote`: keys of reports whose pass wrote something (the next status pass records the `Synced` Event);
+- `errors`: the failing shard of every failed per-shard result (a metric count each);
+- `others`: every non-report message, decoded;
+- `reports` / `pending`: reports folded, and how many of them left the set incomplete.
+"""
+from __future__ import annotations
+
+import msgpack
+
+from .. import native
+
+
+class ReportTable:
+    def __init__(self) -> None:
+        self._shards: list[str] = []
+        self._state: dict[str, dict[str, tuple]] = {}
+
+    def set_shards(self, shards) -> None:
+        self._shards = list(shards)
+
+    def shards(self) -> list[str]:
+        return list(self._shards)
+
+    def __len__(self) -> int:
+        return len(self._state)
+
+    def pop(self, key: str) -> None:
+        self._state.pop(key, None)
+
+    def drop_shards(self, names) -> None:
+        for st in self._state.values():
+            for n in names:
+                st.pop(n, None)
+
+    def feed(self, body: bytes, batch: bool) -> tuple:
+        msgs = msgpack.unpackb(body, raw=False)
+        if not batch:
+            msgs = [msgs]
+        elif not isinstance(msgs, list):
+            raise ValueError("msgpack: malformed frame")
+        complete, wrote, errors, others = [], [], [], []
+        reports = pending = 0
+        for msg in msgs:
+            if not isinstance(msg, dict) or msg.get("t") != "report":
+                others.append(msg)
+                continue
+            reports += 1
+            key, uid, gen = msg["k"], msg.get("u", ""), int(msg.get("g") or 0)
+            st = self._state.setdefault(key, {})
+            changed = False
+            for shard, err in msg["r"].items():
+                e = (uid, gen, err or None)
+                changed = changed or st.get(shard) != e
+                st[shard] = e
+                if err:
+                    errors.append(shard)
+            if msg.get("w"):
+                wrote.append(key)
+            for s in self._shards:
+                e = st.get(s)
+                if e is None or e[0] != uid or e[1] < gen:
+                    pending += 1
+                    break
+            else:
+                if changed or msg.get("w"):
+                    complete.append(key)
+        return complete, wrote, errors, others, reports, pending
+
+    def readiness(self, key: str, uid: str, generation: int):
+        st = self._state.get(key)
+        if st is None:
+            return None
+        out = {}
+        for s in self._shards:
+            e = st.get(s)
+            if e is None or e[0] != uid or e[1] < generation:
+                return None
+            out[s] = e[2]
+        return out
+
+
+def make_report_table():
+    """The native table when the extension is loaded, else the Python one."""
+    m = native.load()
+    if m is not None and hasattr(m, "ReportTable"):
+        return m.ReportTable()
+    return ReportTable()

@@ -1,4 +1,5 @@
 """Native-mode behaviours that deliberately differ from the reference."""
+import msgpack
 import pytest
 
 from ncc.api import constants as C
@@ -495,9 +496,26 @@ async def test_coordinator_finishes_complete_reports_inline():
     assert ctl.stats["inline_finishes"] == 1 and len(ctl.queue) == 0 and ctl.queue.core.waiting() == 0
     assert env.recorder.events[events:] == [f"{C.EVENT_TYPE_NORMAL} {C.SUCCESS_SYNCED} "
                                             f"{C.MESSAGE_RESOURCE_SYNCED.format('NexusAlgorithmTemplate')}"]
+    # a complete set for this version whose flush finds the next version already cached (adopted, not yet
+    # reported): nothing to do and nothing queued; the next version's reports bring the key back
+    newer = env.cstate.update(R.TEMPLATES, NS, dict(new, spec=dict(spec, container=dict(spec["container"],
+                                                                                         versionTag="v-3"))))
+    ctl._on_crd_update(new, newer, C.KIND_TEMPLATE)
+    assert ctl.stats["early_passes_skipped"] >= 1
+    for i in range(2):
+        ctl.on_executor_message(i, {"t": "report", "k": key, "u": new["metadata"]["uid"],
+                                    "g": new["metadata"]["generation"], "r": {f"s{i}": None}, "w": True})
+    env.refresh()  # the cache moves to `newer` before the batch is flushed
+    ctl._inline_timer.cancel()
+    ctl._flush_inline()
+    assert ctl.stats["inline_superseded"] == 1 and len(ctl.queue) == 0 and ctl.queue.core.waiting() == 0
+    events = len(env.recorder.events)
+    report(newer["metadata"]["generation"])
+    assert ctl.stats["inline_finishes"] == 2 and len(ctl.queue) == 0
+    assert len(env.recorder.events) == events + 1  # the pending Synced Event went out with the newer version
     # a shard failure changes the status: queued
-    report(new["metadata"]["generation"], errs=(None, "ApiError: boom"))
-    assert ctl.stats["inline_finishes"] == 1 and len(ctl.queue) == 1
+    report(newer["metadata"]["generation"], errs=(None, "ApiError: boom"))
+    assert ctl.stats["inline_finishes"] == 2 and len(ctl.queue) == 1
 
 
 async def test_status_patch_racing_a_spec_edit_drops_the_adoption_mark():
@@ -578,7 +596,8 @@ async def test_inline_finish_agrees_with_the_status_pass():
         ctl.template_informer.store.upsert(obj)
         ctl._adopted[key] = obj["metadata"]["resourceVersion"]
         m = obj["metadata"]
-        ctl.shard_state[key] = {s: (m["uid"], int(m.get("generation") or 0), None) for s in ("s0", "s1")}
+        ctl.reports.feed(msgpack.packb({"t": "report", "k": key, "u": m["uid"], "g": int(m.get("generation") or 0),
+                                        "r": {"s0": None, "s1": None}, "w": False}), False)
         old, new, _ = ctl._template_synced_status(obj, ["s"], ["c"], ["s0", "s1"])
         assert ctl.finish_inline(key) == (old == new), st
 

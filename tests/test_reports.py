@@ -1,0 +1,138 @@
+"""The coordinator's report table: the native ReportTable (native/ncc_native.cpp) against its Python twin
+(ncc/controller/reports.py), driven in lock-step with arbitrary report streams, frames and shard-set
+changes; plus the raw-frame path through ipc.Channel and Controller.on_executor_frame."""
+import asyncio
+import socket
+
+import msgpack
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from ncc import native
+from ncc.controller.ipc import Channel
+from ncc.controller.reports import ReportTable
+
+NATIVE = native.load()
+
+SHARDS = ["s0", "s1", "s2"]
+KEYS = ["NexusAlgorithmTemplate/ns/a", "NexusAlgorithmTemplate/ns/b", "NexusAlgorithmWorkgroup/ns/w"]
+
+report = st.fixed_dictionaries({
+    "t": st.just("report"), "k": st.sampled_from(KEYS), "u": st.sampled_from(["u1", "u2"]),
+    "g": st.integers(0, 4), "r": st.dictionaries(st.sampled_from(SHARDS + ["gone"]),
+                                                 st.one_of(st.none(), st.just(""), st.sampled_from(["boom", "409"])),
+                                                 min_size=1, max_size=3),
+    "w": st.booleans()})
+other = st.one_of(
+    st.fixed_dictionaries({"t": st.sampled_from(["ready", "synced"]), "i": st.integers(0, 1 << 40)}),
+    st.fixed_dictionaries({"t": st.just("need"), "k": st.integers(0, 3), "n": st.text(max_size=8)}),
+    st.fixed_dictionaries({"t": st.just("x"), "f": st.floats(allow_nan=False), "b": st.binary(max_size=4),
+                           "l": st.lists(st.one_of(st.none(), st.booleans(), st.integers(-(1 << 63), (1 << 64) - 1)),
+                                         max_size=3)}))
+op = st.one_of(
+    st.tuples(st.just("feed"), st.lists(st.one_of(report, report, other), min_size=1, max_size=5)),
+    st.tuples(st.just("shards"), st.lists(st.sampled_from(SHARDS), unique=True, max_size=3)),
+    st.tuples(st.just("drop"), st.lists(st.sampled_from(SHARDS), max_size=2)),
+    st.tuples(st.just("pop"), st.sampled_from(KEYS)))
+
+
+def frame(msgs: list) -> tuple[bytes, bool]:
+    if len(msgs) == 1:
+        return msgpack.packb(msgs[0], use_bin_type=True), False
+    return msgpack.packb(msgs, use_bin_type=True), True
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+@settings(max_examples=300, deadline=None)
+@given(st.lists(op, max_size=25))
+def test_native_report_table_matches_python(ops):
+    py, nat = ReportTable(), NATIVE.ReportTable()
+    for t in (py, nat):
+        t.set_shards(SHARDS[:2])
+    for kind, arg in ops:
+        if kind == "feed":
+            body, batch = frame(arg)
+            assert nat.feed(body, batch) == py.feed(body, batch)
+        elif kind == "shards":
+            py.set_shards(arg), nat.set_shards(arg)
+            assert nat.shards() == py.shards() == arg
+        elif kind == "drop":
+            py.drop_shards(arg), nat.drop_shards(arg)
+        else:
+            py.pop(arg), nat.pop(arg)
+        assert len(nat) == len(py)
+        for k in KEYS:
+            for u in ("u1", "u2"):
+                for g in range(5):
+                    assert nat.readiness(k, u, g) == py.readiness(k, u, g)
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=48), st.booleans())
+def test_native_report_table_rejects_malformed_frames(raw, batch):
+    """Arbitrary bytes either fold like the Python twin or raise (ValueError for a malformed frame, what
+    msgpack raises for undecodable content: bad UTF-8, an unhashable map key); never crash."""
+    nat, py = NATIVE.ReportTable(), ReportTable()
+    nat.set_shards(SHARDS), py.set_shards(SHARDS)
+    try:
+        got = nat.feed(raw, batch)
+    except (ValueError, UnicodeDecodeError, TypeError):
+        return
+    try:
+        want = py.feed(raw, batch)
+    except Exception:  # noqa: BLE001 — msgpack is laxer about some inputs the native table refuses
+        return
+    if got[4] or want[4]:  # only well-formed reports are compared
+        assert got[:3] == want[:3]
+
+
+def test_report_table_completion_and_readiness():
+    t = (NATIVE.ReportTable if NATIVE is not None else ReportTable)()
+    t.set_shards(["a", "b"])
+    k = "NexusAlgorithmTemplate/ns/x"
+    assert t.feed(*frame([{"t": "report", "k": k, "u": "u", "g": 2, "r": {"a": None}, "w": True}])) == \
+        ([], [k], [], [], 1, 1)
+    assert t.readiness(k, "u", 2) is None
+    got = t.feed(*frame([{"t": "report", "k": k, "u": "u", "g": 2, "r": {"b": "boom"}, "w": False},
+                         {"t": "need", "k": 1, "n": "ns/s"}]))
+    assert got == ([k], [], ["b"], [{"t": "need", "k": 1, "n": "ns/s"}], 1, 0)
+    assert t.readiness(k, "u", 2) == {"a": None, "b": "boom"}
+    assert t.readiness(k, "u", 3) is None and t.readiness(k, "other", 2) is None
+    # a repeat of a complete set with nothing new is not a completion; a changed result or a write is
+    rep = {"t": "report", "k": k, "u": "u", "g": 2, "r": {"a": None}, "w": False}
+    assert t.feed(*frame([rep])) == ([], [], [], [], 1, 0)
+    assert t.feed(*frame([dict(rep, w=True)])) == ([k], [k], [], [], 1, 0)
+    assert t.feed(*frame([dict(rep, r={"b": None})])) == ([k], [], [], [], 1, 0)
+    assert t.readiness(k, "u", 2) == {"a": None, "b": None}
+    t.set_shards(["a", "b", "c"])  # a shard added: not complete until it reports
+    assert t.readiness(k, "u", 2) is None
+    t.drop_shards(["c"])
+    t.set_shards(["a", "b"])
+    assert t.readiness(k, "u", 2) == {"a": None, "b": None}
+    t.pop(k)
+    assert t.readiness(k, "u", 2) is None and len(t) == 0
+
+
+async def test_channel_raw_frames_fold_through_the_controller_path():
+    """Frames written by Channel.send (single and coalesced batches) arrive undecoded via recv_raw and fold
+    exactly as their decoded messages would."""
+    a, b = socket.socketpair()
+    ra, wa = await asyncio.open_connection(sock=a)
+    rb, wb = await asyncio.open_connection(sock=b)
+    tx, rx = Channel(ra, wa), Channel(rb, wb)
+    t = (NATIVE.ReportTable if NATIVE is not None else ReportTable)()
+    t.set_shards(["s0"])
+    tx.send({"t": "report", "k": "K/ns/a", "u": "u", "g": 1, "r": {"s0": None}, "w": True})
+    await tx.drain()
+    body, batch = await rx.recv_raw()
+    assert not batch and t.feed(body, batch)[:2] == (["K/ns/a"], ["K/ns/a"])
+    tx.send({"t": "ready", "i": 0})
+    tx.send({"t": "report", "k": "K/ns/b", "u": "u", "g": 1, "r": {"s0": "boom"}, "w": False})
+    await tx.drain()
+    body, batch = await rx.recv_raw()
+    assert batch and t.feed(body, batch) == (["K/ns/b"], [], ["s0"], [{"t": "ready", "i": 0}], 1, 0)
+    tx.close()
+    assert await rx.recv_raw() is None
+    rx.close()
