@@ -1600,19 +1600,25 @@ class MpReader {
         return v;
     }
     // container headers: false (nothing consumed) when the next value is not of that kind
+    // (a container cannot hold more elements than there are bytes left: one byte each at least, so a
+    // corrupt length fails here instead of sizing a huge list)
     bool map_len(size_t& n) {
         uint8_t c = peek();
-        if ((c & 0xf0) == 0x80) { ++p_; n = c & 0x0f; return true; }
-        if (c == 0xde) { ++p_; n = be(2); return true; }
-        if (c == 0xdf) { ++p_; n = be(4); return true; }
-        return false;
+        if ((c & 0xf0) == 0x80) { ++p_; n = c & 0x0f; }
+        else if (c == 0xde) { ++p_; n = be(2); }
+        else if (c == 0xdf) { ++p_; n = be(4); }
+        else return false;
+        if (n > static_cast<size_t>(e_ - p_) / 2) fail();
+        return true;
     }
     bool arr_len(size_t& n) {
         uint8_t c = peek();
-        if ((c & 0xf0) == 0x90) { ++p_; n = c & 0x0f; return true; }
-        if (c == 0xdc) { ++p_; n = be(2); return true; }
-        if (c == 0xdd) { ++p_; n = be(4); return true; }
-        return false;
+        if ((c & 0xf0) == 0x90) { ++p_; n = c & 0x0f; }
+        else if (c == 0xdc) { ++p_; n = be(2); }
+        else if (c == 0xdd) { ++p_; n = be(4); }
+        else return false;
+        if (n > static_cast<size_t>(e_ - p_)) fail();
+        return true;
     }
     bool str(std::string_view& out) {  // str or bin
         uint8_t c = peek();
@@ -1792,26 +1798,40 @@ class ReportTable {
     }
 
     // feed(frame body, batch) -> (complete keys, wrote keys, failing shards, other messages, reports, pending)
-    py::tuple feed(py::bytes body, bool batch) {
-        std::string_view v = bytes_view(body);
-        MpReader r(v.data(), v.size());
+    struct Folded {
         py::list complete, wrote, errors, others;
         int64_t reports = 0, pending = 0;
-        size_t n = 1;
-        if (batch && !r.arr_len(n)) MpReader::fail();
-        for (size_t k = 0; k < n; ++k) {
-            const uint8_t* start = r.pos();
-            int rc = report(r, complete, wrote, errors);
-            if (rc < 0) {  // not a report: decode it for Python
-                r.seek(start);
-                others.append(py::reinterpret_steal<py::object>(r.value()));
-                continue;
-            }
-            ++reports;
-            if (rc == 0) ++pending;
+    };
+
+    py::tuple feed(py::bytes body, bool batch) {
+        std::string_view v = bytes_view(body);
+        Folded f;
+        fold_frame(v.data(), v.size(), batch, f);
+        return py::make_tuple(f.complete, f.wrote, f.errors, f.others, f.reports, f.pending);
+    }
+
+    // feed_stream(buffer, start) -> (complete, wrote, errors, others, reports, pending, end): every complete
+    // frame (4-byte big-endian length, high bit = batch, then the msgpack body) in buffer[start:], folded;
+    // `end` is the offset of the first byte not consumed (a partial frame's header or body).
+    py::tuple feed_stream(py::buffer buf, size_t start) {
+        py::buffer_info info = buf.request();
+        if (info.ndim != 1 || info.itemsize != 1) throw py::value_error("feed_stream: a byte buffer is required");
+        const char* p = static_cast<const char*>(info.ptr);
+        size_t len = static_cast<size_t>(info.size);
+        if (start > len) throw py::value_error("feed_stream: start past the end");
+        Folded f;
+        size_t pos = start;
+        while (len - pos >= 4) {
+            const auto* h = reinterpret_cast<const uint8_t*>(p + pos);
+            uint32_t n = (uint32_t(h[0]) << 24) | (uint32_t(h[1]) << 16) | (uint32_t(h[2]) << 8) | uint32_t(h[3]);
+            bool batch = (n & 0x80000000u) != 0;
+            n &= 0x7fffffffu;
+            if (n > kMaxFrame) throw py::value_error("frame too large: " + std::to_string(n));
+            if (len - pos - 4 < n) break;
+            fold_frame(p + pos + 4, n, batch, f);
+            pos += 4 + n;
         }
-        if (!r.at_end()) MpReader::fail();
-        return py::make_tuple(complete, wrote, errors, others, reports, pending);
+        return py::make_tuple(f.complete, f.wrote, f.errors, f.others, f.reports, f.pending, pos);
     }
 
     // readiness(key, uid, generation) -> None while some shard has not reported on this version, else
@@ -1831,7 +1851,41 @@ class ReportTable {
         return std::move(out);
     }
 
+    // ready_ok(key, uid, generation) -> None while some shard has not reported on this version, else
+    // whether every shard succeeded (readiness() without building the dict)
+    py::object ready_ok(const std::string& key, const std::string& uid, int64_t gen) const {
+        auto it = state_.find(key);
+        if (it == state_.end()) return py::none();
+        bool ok = true;
+        for (const auto& s : shards_) {
+            const Slot* e = find(it->second, s);
+            if (e == nullptr || e->uid != uid || e->gen < gen) return py::none();
+            ok = ok && e->err.empty();
+        }
+        return py::bool_(ok);
+    }
+
   private:
+    static constexpr uint32_t kMaxFrame = 64u * 1024 * 1024;  // ipc.MAX_FRAME
+
+    void fold_frame(const char* p, size_t len, bool batch, Folded& f) {
+        MpReader r(p, len);
+        size_t n = 1;
+        if (batch && !r.arr_len(n)) MpReader::fail();
+        for (size_t k = 0; k < n; ++k) {
+            const uint8_t* at = r.pos();
+            int rc = report(r, f.complete, f.wrote, f.errors);
+            if (rc < 0) {  // not a report: decode it for Python
+                r.seek(at);
+                f.others.append(py::reinterpret_steal<py::object>(r.value()));
+                continue;
+            }
+            ++f.reports;
+            if (rc == 0) ++f.pending;
+        }
+        if (!r.at_end()) MpReader::fail();
+    }
+
     static const Slot* find(const std::vector<Slot>& v, std::string_view shard) {
         for (const auto& s : v)
             if (s.shard == shard) return &s;
@@ -1974,7 +2028,10 @@ PYBIND11_MODULE(_native, m) {
         .def("feed", &ReportTable::feed, py::arg("body"), py::arg("batch"),
              "fold a raw executor IPC frame: (complete keys, wrote keys, failing shards, other messages, "
              "reports, pending)")
+        .def("feed_stream", &ReportTable::feed_stream, py::arg("buffer"), py::arg("start"),
+             "fold every complete frame of a byte stream from `start`: feed()'s tuple + the end offset")
         .def("readiness", &ReportTable::readiness, py::arg("key"), py::arg("uid"), py::arg("generation"))
+        .def("ready_ok", &ReportTable::ready_ok, py::arg("key"), py::arg("uid"), py::arg("generation"))
         .def("pop", &ReportTable::pop, py::arg("key"))
         .def("drop_shards", &ReportTable::drop_shards, py::arg("names"))
         .def("__len__", &ReportTable::size);

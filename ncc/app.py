@@ -489,7 +489,7 @@ class App:
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
                                      env=exec_env, per_shard=self.per_shard, part_base=part, part_stride=parts,
                                      gated=gated, relay=self.relay, native_config=native_cfg,
-                                     on_frame=controller.on_executor_frame)
+                                     on_stream=controller.on_executor_stream)
             if native_cfg is not None:
                 self._cred_task = asyncio.ensure_future(native_cfg.refresh_loop(self.pool))
             self.pool.start()

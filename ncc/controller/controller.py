@@ -81,6 +81,8 @@ class Controller(ReconcileMixin):
         self.stats = {"reconciles": 0, "errors": 0, "template": 0, "workgroup": 0, "reports": 0,
                       "reports_pending": 0, "early_passes_skipped": 0, "inline_finishes": 0, "inline_superseded": 0}
         self._inline_keys: set = set()  # coordinator: keys with a complete report set, finished in one batch
+        # key -> (template object, shard-name list) whose status finish_inline found final (identity memo)
+        self._inline_status_ok: dict = {}
         self._inline_timer = None
         self.ready = asyncio.Event()  # workers running
         self.caches_synced = asyncio.Event()  # controller (and shard) caches synced
@@ -165,7 +167,7 @@ class Controller(ReconcileMixin):
                 key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
             if (new.get("status") or {}).get("conditions") and \
                     (kind != C.KIND_TEMPLATE or self._adopted.get(key) == nrv) and \
-                    self.shard_readiness(key, new) is None:
+                    self.shard_ready_ok(key, new) is None:
                 self.stats["early_passes_skipped"] += 1
                 return
         self._enqueue_key(key or make_key(kind, nm.get("namespace", "") or "", nm.get("name", "")))
@@ -363,6 +365,17 @@ class Controller(ReconcileMixin):
         """Coordinator: fold a raw IPC frame of executor `index` into the report table and re-evaluate
         the objects whose report set it completed.  Returns the frame's other messages, decoded."""
         complete, wrote, errors, others, reports, pending = self.reports.feed(body, batch)
+        self._folded(complete, wrote, errors, reports, pending)
+        return others
+
+    def on_executor_stream(self, index: int, buf, start: int) -> tuple[list, int]:
+        """Coordinator: fold every complete frame of executor `index`'s byte stream from `start` (ipc.py
+        framing, parsed natively).  Returns (the other messages, decoded; the offset after the last frame)."""
+        complete, wrote, errors, others, reports, pending, end = self.reports.feed_stream(buf, start)
+        self._folded(complete, wrote, errors, reports, pending)
+        return others, end
+
+    def _folded(self, complete: list, wrote: list, errors: list, reports: int, pending: int) -> None:
         st = self.stats
         st["reports"] += reports
         st["reports_pending"] += pending
@@ -374,7 +387,6 @@ class Controller(ReconcileMixin):
         # then, instead of once per executor report (N× fewer coordinator passes at N shards).
         for key in complete:
             self._reports_complete(key)
-        return others
 
     def _reports_complete(self, key: str) -> None:
         if not self.options.inline_finish:
@@ -400,6 +412,11 @@ class Controller(ReconcileMixin):
                 done = False
             if not done:
                 self.queue.add(key)
+
+    def shard_ready_ok(self, key: str, obj: dict):
+        """None while some shard has not reported on this object version, else whether all succeeded."""
+        m = obj.get("metadata") or {}
+        return self.reports.ready_ok(key, m.get("uid", ""), int(m.get("generation") or 0))
 
     def shard_readiness(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else {shard: error|None}."""

@@ -85,8 +85,9 @@ class ExecutorHandle:
         self.part = part
         self.parts = parts
         self.on_message = on_message
-        # coordinator: folds raw frames (reports) natively and returns the other messages, decoded
-        self.on_frame = None
+        # coordinator: callable(index, buffer, start) -> (other messages, end) folding the raw frame stream
+        # (reports) natively
+        self.on_stream = None
         self.env = env
         self.proc: asyncio.subprocess.Process | None = None
         self.channel: Channel | None = None
@@ -162,13 +163,10 @@ class ExecutorHandle:
             self.synced.clear()
             await self._spawn()
             while True:
-                if self.on_frame is not None:
-                    frames = await self.channel.recv_frames()
-                    if frames is None:
+                if self.on_stream is not None:
+                    batch = await self.channel.recv_folded(self._fold)
+                    if batch is None:
                         break
-                    batch = []
-                    for body, is_batch in frames:
-                        batch += self.on_frame(self.index, body, is_batch)
                 else:
                     batch = await self.channel.recv()
                     if batch is None:
@@ -196,6 +194,9 @@ class ExecutorHandle:
                       rc, backoff)
             await asyncio.sleep(backoff)
             backoff = min(backoff * 2, 30.0)
+
+    def _fold(self, buf, start: int):
+        return self.on_stream(self.index, buf, start)
 
     def start(self) -> None:
         self._task = asyncio.ensure_future(self._run())
@@ -225,7 +226,7 @@ class ExecutorPool:
 
     def __init__(self, shard_names: list[str], n: int, on_message, env: dict | None = None, per_shard: int = 1,
                  part_base: int = 0, part_stride: int = 1, gated: bool = False, relay=None,
-                 native_config=None, on_frame=None):
+                 native_config=None, on_stream=None):
         """With partitioned coordinators (`part_stride` = C > 1, this coordinator owning keys ≡ `part_base`
         mod C), executor j of a group takes the global key partition part_base + C·j of C·per_shard, so its
         keys are exactly a share of this coordinator's."""
@@ -233,7 +234,7 @@ class ExecutorPool:
         self.part_base = part_base
         self.part_stride = max(1, part_stride)
         self.on_message = on_message
-        self.on_frame = on_frame  # raw-frame report folding (Controller.on_executor_frame)
+        self.on_stream = on_stream  # raw-stream report folding (Controller.on_executor_stream)
         self.env = env
         self.relay = relay  # coordinator's WatchRelay: executors get the controller cluster from it
         self.native_config = native_config  # NativeExecutorConfig: run ncc/bin/ncc-executor instead of Python
@@ -250,7 +251,7 @@ class ExecutorPool:
               for j in range(self.per_shard)]
         for h in hs:
             h.gated, h.gate_open = self.gated, self.gate_open
-            h.on_frame = self.on_frame
+            h.on_stream = self.on_stream
             if self.relay is not None:
                 h.on_spawn, h.on_exit, h.on_need = self.relay.attach, self.relay.detach, self.relay.on_need
             if self.native_config is not None:

@@ -114,6 +114,34 @@ class Channel:
                 return None
             buf += data
 
+    async def recv_folded(self, fold) -> list | None:
+        """Read what has arrived and fold it in place: `fold(buffer, start) -> (messages, end)` consumes the
+        complete frames of `buffer[start:]` (the coordinator's native report table parses the framing itself)
+        and returns the messages it did not fold.  Returns them after each read (possibly none), or None at
+        EOF.  Not to be mixed with recv/recv_raw on one channel."""
+        try:
+            data = await self.reader.read(1 << 18)
+        except ConnectionError:
+            data = b""
+        if not data:
+            return None
+        if self._rpos < len(self._rbuf):  # a partial frame is waiting
+            self._rbuf += data
+            src, start = self._rbuf, self._rpos
+        else:
+            src, start = data, 0
+        msgs, end = fold(src, start)
+        if end >= len(src):
+            self._rbuf, self._rpos = bytearray(), 0
+        elif src is data:
+            self._rbuf, self._rpos = bytearray(data[end:]), 0
+        elif end > (1 << 16):
+            del self._rbuf[:end]
+            self._rpos = 0
+        else:
+            self._rpos = end
+        return msgs
+
     def close(self) -> None:
         try:
             self.writer.close()

@@ -297,6 +297,7 @@ class ReconcileMixin:
             self._adopted.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
             if self.role == "coordinator":
                 self.reports.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
+                self._inline_status_ok.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
                 self._pending_event.discard(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
             elif self.options.queued_deletes:
                 await self.propagate_template_delete(namespace, name)
@@ -434,23 +435,29 @@ class ReconcileMixin:
         conds = status.get("conditions")
         if not conds or self._adopted.get(key) != (template.get("metadata") or {}).get("resourceVersion"):
             return False
-        results = self.shard_readiness(key, template)
-        if results is None:
+        ok = self.shard_ready_ok(key, template)
+        if ok is None:
             # A newer version (the next wave) reached the cache between the last report and this flush.  It is
             # initialised and adopted, so the pass would stop at the readiness check, exactly as the early pass
             # `_on_crd_update` skips: the new version's last report brings the key back.
             self.stats["inline_superseded"] += 1
             return True
-        if any(results.values()):
+        if not ok:
             return False
         # report_template_synced_condition would leave the status as it is (no write) exactly when the Ready
-        # condition and the three synced lists already hold what it would set
-        secrets, configmaps = dependent_names(template)
-        c0 = conds[0]
-        if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE, f"Algorithm {q(name)} ready") \
-                or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
-                or status.get("syncedToClusters") != self.all_shard_names:
-            return False
+        # condition and the three synced lists already hold what it would set.  That depends only on the
+        # cached template object and the shard list, so a repeat for the same two objects skips the check.
+        shards = self.all_shard_names
+        memo = self._inline_status_ok.get(key)
+        if memo is None or memo[0] is not template or memo[1] is not shards:
+            secrets, configmaps = dependent_names(template)
+            c0 = conds[0]
+            if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE,
+                                     f"Algorithm {q(name)} ready") \
+                    or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
+                    or status.get("syncedToClusters") != shards:
+                return False
+            self._inline_status_ok[key] = (template, shards)
         self.stats["reconciles"] += 1
         self.stats["inline_finishes"] += 1
         self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())  # a reconcile, done in place

@@ -27,6 +27,7 @@ from __future__ import annotations
 import msgpack
 
 from .. import native
+from .ipc import _HDR, MAX_FRAME
 
 
 class ReportTable:
@@ -85,6 +86,30 @@ class ReportTable:
                     complete.append(key)
         return complete, wrote, errors, others, reports, pending
 
+    def feed_stream(self, buffer, start: int) -> tuple:
+        """Every complete frame of `buffer[start:]` (ipc.py framing) folded: feed()'s tuple + the offset of the
+        first byte not consumed."""
+        complete, wrote, errors, others = [], [], [], []
+        reports = pending = 0
+        pos, end = start, len(buffer)
+        while end - pos >= 4:
+            (n,) = _HDR.unpack_from(buffer, pos)
+            batch = bool(n & 0x80000000)
+            n &= 0x7FFFFFFF
+            if n > MAX_FRAME:
+                raise ValueError(f"frame too large: {n}")
+            if end - pos - 4 < n:
+                break
+            r = self.feed(bytes(buffer[pos + 4:pos + 4 + n]), batch)
+            complete += r[0]
+            wrote += r[1]
+            errors += r[2]
+            others += r[3]
+            reports += r[4]
+            pending += r[5]
+            pos += 4 + n
+        return complete, wrote, errors, others, reports, pending, pos
+
     def readiness(self, key: str, uid: str, generation: int):
         st = self._state.get(key)
         if st is None:
@@ -96,6 +121,12 @@ class ReportTable:
                 return None
             out[s] = e[2]
         return out
+
+
+    def ready_ok(self, key: str, uid: str, generation: int):
+        """None while some shard has not reported on this version, else whether every shard succeeded."""
+        r = self.readiness(key, uid, generation)
+        return None if r is None else not any(r.values())
 
 
 def make_report_table():

@@ -600,6 +600,14 @@ async def test_inline_finish_agrees_with_the_status_pass():
                                         "r": {"s0": None, "s1": None}, "w": False}), False)
         old, new, _ = ctl._template_synced_status(obj, ["s"], ["c"], ["s0", "s1"])
         assert ctl.finish_inline(key) == (old == new), st
+        assert ctl.finish_inline(key) == (old == new), st  # again: the memoised check agrees
+    # the memo follows the shard list: a new list re-checks (and a status naming the old set needs a pass)
+    obj = dict(base, status=good)
+    ctl.template_informer.store.upsert(obj)
+    ctl._adopted[key] = obj["metadata"]["resourceVersion"]
+    assert ctl.finish_inline(key)
+    ctl.all_shard_names = ["s0"]
+    assert not ctl.finish_inline(key)
 
 
 def test_coalescing_starts_only_inside_a_burst(monkeypatch):

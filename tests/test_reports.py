@@ -66,6 +66,7 @@ def test_native_report_table_matches_python(ops):
             for u in ("u1", "u2"):
                 for g in range(5):
                     assert nat.readiness(k, u, g) == py.readiness(k, u, g)
+                    assert nat.ready_ok(k, u, g) == py.ready_ok(k, u, g)
 
 
 @pytest.mark.skipif(NATIVE is None, reason="native extension not built")
@@ -88,6 +89,45 @@ def test_native_report_table_rejects_malformed_frames(raw, batch):
         assert got[:3] == want[:3]
 
 
+def framed(frames: list) -> bytes:
+    out = b""
+    for msgs in frames:
+        body, batch = frame(msgs)
+        out += (len(body) | (0x80000000 if batch else 0)).to_bytes(4, "big")
+        out += body
+    return out
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.lists(st.one_of(report, other), min_size=1, max_size=4), min_size=1, max_size=6),
+       st.lists(st.integers(0, 400), max_size=5))
+def test_native_feed_stream_matches_python_at_any_split(frames, cuts):
+    """A frame stream cut into arbitrary reads folds the same natively and in Python, and as a whole."""
+    data = framed(frames)
+    cuts = sorted({min(c, len(data)) for c in cuts} | {len(data)})
+    results = []
+    for t in (NATIVE.ReportTable(), ReportTable()):
+        t.set_shards(SHARDS[:2])
+        buf, pos, got, prev = bytearray(), 0, [[], [], [], [], 0, 0], 0
+        for c in cuts:  # what Channel.recv_folded does with each read
+            buf += data[prev:c]
+            prev = c
+            r = t.feed_stream(buf, pos)
+            for i in range(4):
+                got[i] += r[i]
+            got[4] += r[4]
+            got[5] += r[5]
+            pos = r[6]
+        assert pos == len(buf)
+        results.append(got)
+    assert results[0] == results[1]
+    whole = NATIVE.ReportTable()
+    whole.set_shards(SHARDS[:2])
+    r = whole.feed_stream(data, 0)
+    assert list(r[:4]) == results[0][:4] and r[4:6] == tuple(results[0][4:6]) and r[6] == len(data)
+
+
 def test_report_table_completion_and_readiness():
     t = (NATIVE.ReportTable if NATIVE is not None else ReportTable)()
     t.set_shards(["a", "b"])
@@ -98,14 +138,14 @@ def test_report_table_completion_and_readiness():
     got = t.feed(*frame([{"t": "report", "k": k, "u": "u", "g": 2, "r": {"b": "boom"}, "w": False},
                          {"t": "need", "k": 1, "n": "ns/s"}]))
     assert got == ([k], [], ["b"], [{"t": "need", "k": 1, "n": "ns/s"}], 1, 0)
-    assert t.readiness(k, "u", 2) == {"a": None, "b": "boom"}
-    assert t.readiness(k, "u", 3) is None and t.readiness(k, "other", 2) is None
+    assert t.readiness(k, "u", 2) == {"a": None, "b": "boom"} and t.ready_ok(k, "u", 2) is False
+    assert t.readiness(k, "u", 3) is None and t.readiness(k, "other", 2) is None and t.ready_ok(k, "u", 3) is None
     # a repeat of a complete set with nothing new is not a completion; a changed result or a write is
     rep = {"t": "report", "k": k, "u": "u", "g": 2, "r": {"a": None}, "w": False}
     assert t.feed(*frame([rep])) == ([], [], [], [], 1, 0)
     assert t.feed(*frame([dict(rep, w=True)])) == ([k], [k], [], [], 1, 0)
     assert t.feed(*frame([dict(rep, r={"b": None})])) == ([k], [], [], [], 1, 0)
-    assert t.readiness(k, "u", 2) == {"a": None, "b": None}
+    assert t.readiness(k, "u", 2) == {"a": None, "b": None} and t.ready_ok(k, "u", 2) is True
     t.set_shards(["a", "b", "c"])  # a shard added: not complete until it reports
     assert t.readiness(k, "u", 2) is None
     t.drop_shards(["c"])
@@ -133,6 +173,26 @@ async def test_channel_raw_frames_fold_through_the_controller_path():
     await tx.drain()
     body, batch = await rx.recv_raw()
     assert batch and t.feed(body, batch) == (["K/ns/b"], [], ["s0"], [{"t": "ready", "i": 0}], 1, 0)
+    # the folding path: frames cut across reads are folded once complete; other messages come back decoded
+    t2 = (NATIVE.ReportTable if NATIVE is not None else ReportTable)()
+    t2.set_shards(["s0"])
+    seen = []
+
+    def fold(buf, start):
+        r = t2.feed_stream(buf, start)
+        seen.extend(r[0])
+        return r[3], r[6]
+    data = framed([[{"t": "report", "k": "K/ns/c", "u": "u", "g": 1, "r": {"s0": None}, "w": False}],
+                   [{"t": "synced", "i": 3}]])
+    wa.write(data[:7])
+    await wa.drain()
+    assert await rx.recv_folded(fold) == [] and seen == []
+    wa.write(data[7:])
+    await wa.drain()
+    got = []
+    while not got:
+        got = await rx.recv_folded(fold)
+    assert got == [{"t": "synced", "i": 3}] and seen == ["K/ns/c"]
     tx.close()
-    assert await rx.recv_raw() is None
+    assert await rx.recv_folded(fold) is None
     rx.close()
