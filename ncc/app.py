@@ -173,16 +173,23 @@ def auto_sizing(groups: int, cpus: int | None = None, native: bool = False) -> t
     Native executors (ncc/bin/ncc-executor): k = 1.  One C++ process per shard costs ~24 µs of CPU per
     synced object on the MI355X host and keeps up with a shard apiserver on its own
     (profiles/r2/native_executor_box/: k=1 28.2k objects/s at 52 µs/object in total vs k=4 28.8k at
-    73 µs); extra partitions would only re-parse the same shard watch streams.  The coordinator then
-    carries the per-template work (status, adoption, Events, reports): C = one per 32 CPUs, up to 4,
-    once there are ≥ 4 shard groups."""
+    73 µs); extra partitions would only re-parse the same shard watch streams.
+
+    The coordinator carries the per-template work (status, adoption, Events, reports).  One process keeps
+    up with ~140-160k objects/s whether it serves 4 or 8 shards (box: N=4 134k at 0.93 cores,
+    profiles/r2/sweep_r2e/; 8 shards on one rank 159k at 0.94 cores, profiles/r2/prof8/), i.e. with about
+    4 shards at a shard apiserver's ~36k objects/s.  But every coordinator partition brings its own
+    executor per shard, and each shard apiserver then serves C watch streams per kind: on one shard C=2
+    costs 12-17 % and C=4 about 25 % of the throughput (profiles/r2/c_on_one_shard/).  So C = one per 4
+    shard groups (N=8: 2), and only with 32 CPUs per coordinator, up to 4."""
+    import math
     cpus = cpu_share() if cpus is None else cpus
     if not native:
         k = auto_executors_per_shard(groups, cpus)
         return k, auto_coordinator_partitions(groups, k, cpus)
     if groups < 4:
         return 1, 1
-    return 1, max(1, min(4, cpus // 32))
+    return 1, max(1, min(4, cpus // 32, math.ceil(groups / 4)))
 
 
 def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int, native: bool = False) -> tuple | None:

@@ -149,7 +149,8 @@ def test_bench_two_ranks_over_gloo():
 def test_bench_eight_ranks_auto_sized_topology():
     """The driver's N=8 launch on a large host, rehearsed here: NCC_CPU_SHARE=128 makes the automatic
     sizing pick what it would on an 8-GPU node with ≥128 CPUs (ncc/app.py `auto_sizing`: native executors,
-    k=1 per shard, C=4 coordinator partitions → 3 partition children + 4×8 executors under the controller).
+    k=1 per shard, C=2 coordinator partitions (one per 4 shards) → 1 partition child + 2×8 executors under the
+    controller).
     Every wave must converge with no process restarted and the controller alive."""
     pytest.importorskip("torch.distributed")
     from ncc.app import auto_sizing
