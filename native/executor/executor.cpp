@@ -8,6 +8,7 @@
 //                             {"t":"s"|"w","k":kind,"l":[raw watch line...]}  watch relay
 //                                (ncc/controller/relay.py): the controller cluster's objects
 //                             {"t":"go"}   warm standby acquired the Lease: start the workers
+//                             {"t":"resync","p":p,"n":C}   pass again over the keys of coordinator partition p
 //                             {"t":"cred","s":shard,"token":...}   refreshed exec credential
 //   executor -> coordinator   {"t":"synced","i":n}, {"t":"ready","i":n}
 //                             {"t":"report","k":key,"u":uid,"g":generation,"r":{shard:error|nil},"w":wrote}
@@ -1515,6 +1516,17 @@ static void handle_message(const mp::Obj& m) {
         }
     } else if (t == "go") {
         ex.gate.set();
+    } else if (t == "resync") {
+        // a coordinator partition (re)started and has no report state: pass over its keys again so every
+        // shard reports on them (in-sync keys cost no write)
+        long long part = m.iget("p"), parts = m.iget("n", 1);
+        if (parts < 1 || part < 0 || part >= parts) return;
+        for (int kind : {TEMPLATES, WORKGROUPS})
+            for (auto& kv : ex.ctl[kind])
+                if (static_cast<long long>(crc32(key_of(kv.second->ns, kv.second->name)) % parts) == part) {
+                    ++g_enq[ENQ_RESYNC];
+                    ex.enqueue(kind, kv.second->ns, kv.second->name);
+                }
     } else if (t == "cred") {
         std::string_view shard = m.sget("s");
         for (auto& sp : ex.shards)

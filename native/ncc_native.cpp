@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <queue>
 #include <string>
@@ -1785,6 +1786,24 @@ class ReportTable {
     };
 
     void set_shards(const std::vector<std::string>& shards) { shards_ = shards; }
+    // This coordinator owns the keys of partition `part` of `parts`; reports on other keys are not folded but
+    // kept, raw, for take_forwards() (the parent coordinator relays them to the partition's process).
+    void set_partition(int part, int parts) {
+        if (parts < 1 || part < 0 || part >= parts) throw py::value_error("set_partition: 0 <= part < parts");
+        part_ = part;
+        parts_ = parts;
+    }
+    // {partition: [raw msgpack report message, ...]} collected since the last call
+    py::dict take_forwards() {
+        py::dict out;
+        for (auto& kv : forwards_) {
+            py::list l;
+            for (auto& m : kv.second) l.append(py::bytes(m));
+            out[py::int_(kv.first)] = l;
+        }
+        forwards_.clear();
+        return out;
+    }
     std::vector<std::string> shards() const { return shards_; }
     size_t size() const { return state_.size(); }
     void pop(const std::string& key) { state_.erase(key); }
@@ -1880,6 +1899,7 @@ class ReportTable {
                 f.others.append(py::reinterpret_steal<py::object>(r.value()));
                 continue;
             }
+            if (rc == 2) continue;  // forwarded
             ++f.reports;
             if (rc == 0) ++f.pending;
         }
@@ -1895,6 +1915,7 @@ class ReportTable {
     // One message at the reader.  -1: not a report (nothing folded; the caller rewinds), 0: folded, some
     // shard still to report on this version, 1: folded and complete.
     int report(MpReader& r, py::list& complete, py::list& wrote, py::list& errors) {
+        const uint8_t* msg = r.pos();
         size_t n;
         if (!r.map_len(n)) return -1;
         const uint8_t* body = r.pos();
@@ -1937,6 +1958,15 @@ class ReportTable {
         }
         if (!have_k || results == nullptr) MpReader::fail();
         const uint8_t* end = r.pos();
+        if (parts_ > 1) {  // ipc key "kind/ns/name": its partition is crc32("ns/name") % C (executor.key_part)
+            size_t slash = rkey.find('/');
+            std::string_view nsname = slash == std::string_view::npos ? std::string_view() : rkey.substr(slash + 1);
+            int p = static_cast<int>((crc_update(0xFFFFFFFFu, nsname) ^ 0xFFFFFFFFu) % static_cast<uint32_t>(parts_));
+            if (p != part_) {  // another coordinator partition's key: hand its raw bytes on, unfolded
+                forwards_[p].emplace_back(reinterpret_cast<const char*>(msg), static_cast<size_t>(end - msg));
+                return 2;
+            }
+        }
         std::string skey(rkey);
         auto& slots = state_[skey];
         r.seek(results);
@@ -1973,6 +2003,8 @@ class ReportTable {
 
     std::vector<std::string> shards_;
     std::unordered_map<std::string, std::vector<Slot>> state_;
+    int part_ = 0, parts_ = 1;
+    std::map<int, std::vector<std::string>> forwards_;
 };
 }  // namespace
 
@@ -2033,6 +2065,8 @@ PYBIND11_MODULE(_native, m) {
         .def("readiness", &ReportTable::readiness, py::arg("key"), py::arg("uid"), py::arg("generation"))
         .def("ready_ok", &ReportTable::ready_ok, py::arg("key"), py::arg("uid"), py::arg("generation"))
         .def("pop", &ReportTable::pop, py::arg("key"))
+        .def("set_partition", &ReportTable::set_partition, py::arg("part"), py::arg("parts"))
+        .def("take_forwards", &ReportTable::take_forwards)
         .def("drop_shards", &ReportTable::drop_shards, py::arg("names"))
         .def("__len__", &ReportTable::size);
 }

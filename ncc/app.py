@@ -278,8 +278,9 @@ class App:
                 self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard, native)
                 if self.coord_part is not None:
                     o.partition = self.coord_part  # this coordinator's share of the template keys
-                    # the k executors per shard are shared out among the C coordinators (k/C each, at least 1)
-                    self.per_shard = max(1, self.per_shard // self.coord_part[1])
+                    if os.environ.get("NCC_COORDINATOR_PART"):
+                        # a child: the parent's executors serve every key; it relays this partition's reports
+                        self.n_executors = 0
         kf = partition_filter(*o.partition) if o.partition is not None else None
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
@@ -479,7 +480,7 @@ class App:
             self.recorder.start()
         self.factory.start()
         gated = self.gate is not None and not self.gate.is_set()
-        if self.options.role == "coordinator":
+        if self.options.role == "coordinator" and self.n_executors > 0:
             env = dict(os.environ)
             env.update(config_to_env(self.cfg))
             env.pop("NCC_COORDINATOR_PART", None)
@@ -493,15 +494,23 @@ class App:
             if not use_native:
                 log.debug("Python shard executors: %s", why)
             native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
+            # One executor group per shard group serves every template key, whatever the number of coordinator
+            # partitions: a shard apiserver then serves one executor's watches, not C of them
+            # (profiles/r2/c_on_one_shard/: C executors on one shard cost it 12-25 %).
             self.pool = ExecutorPool(controller.all_shard_names, self.n_executors, controller.on_executor_message,
-                                     env=exec_env, per_shard=self.per_shard, part_base=part, part_stride=parts,
-                                     gated=gated, relay=self.relay, native_config=native_cfg,
-                                     on_stream=controller.on_executor_stream)
+                                     env=exec_env, per_shard=self.per_shard, gated=gated, relay=self.relay,
+                                     native_config=native_cfg, on_stream=controller.on_executor_stream)
             if native_cfg is not None:
                 self._cred_task = asyncio.ensure_future(native_cfg.refresh_loop(self.pool))
             self.pool.start()
-            if parts > 1 and part == 0 and not os.environ.get("NCC_COORDINATOR_PART"):
-                self.partitions = CoordinatorPartitions(parts, env, gated=gated)
+            if parts > 1 and part == 0:
+                # the children own keys ≡ p mod C: their executor reports are forwarded raw by the report table,
+                # and a child that comes up (or back) gets every executor to pass over its keys again
+                pool = self.pool
+                self.partitions = CoordinatorPartitions(
+                    parts, env, gated=gated, on_child_ready=lambda p: pool.resync_partition(p, parts))
+                controller.reports.set_partition(0, parts)
+                controller.forward_reports = self.partitions.forward
                 self.partitions.start()
         if self.cfg.mode == "native":
             gctune.tune()
@@ -522,7 +531,7 @@ class App:
     def topology(self) -> dict:
         """The process layout this coordinator chose (automatic sizing or overrides)."""
         parts = self.coord_part[1] if self.coord_part else 1
-        return {"shard_groups": self.n_executors, "executors_per_shard": self.per_shard * parts,
+        return {"shard_groups": self.n_executors, "executors_per_shard": self.per_shard,
                 "coordinator_partitions": parts, "executor_impl": self.executor_impl or "in-process",
                 "executor_processes": len(self.pool.handles) if self.pool is not None else 0,
                 "watch_relay": self.relay is not None}
@@ -609,10 +618,14 @@ async def _amain(cfg: AppConfig, control_fd: int | None = None) -> int:
         reader, writer = await asyncio.open_connection(sock=socket.socket(fileno=control_fd))
         channel = Channel(reader, writer)
         app.controller.on_ready = lambda: channel.send({"t": "ready"})
+        ctl = app.controller
+
+        def fold(buf, start):  # executor reports on this partition's keys, forwarded raw by the parent
+            return ctl.on_executor_stream(-1, buf, start)
 
         async def watch_parent():
             while True:
-                batch = await channel.recv()
+                batch = await channel.recv_folded(fold)
                 if batch is None:
                     break
                 if any(isinstance(m, dict) and m.get("t") == "go" for m in batch):

@@ -89,6 +89,9 @@ class Controller(ReconcileMixin):
         self.role = o.role
         # coordinator role: key -> {shard: (uid, generation, error)} of the executors' reports (native table)
         self.reports = make_report_table()
+        # parent of partitioned coordinators: callable(partition, [raw report message, ...]) relaying the
+        # reports on other partitions' keys (the report table sets them aside)
+        self.forward_reports = None
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
         self.reporter = None  # executor role: callable(msg) sending results to the coordinator
         self.on_ready = None  # executor role: called once caches are synced and workers run
@@ -376,6 +379,9 @@ class Controller(ReconcileMixin):
         return others, end
 
     def _folded(self, complete: list, wrote: list, errors: list, reports: int, pending: int) -> None:
+        if self.forward_reports is not None:
+            for part, msgs in self.reports.take_forwards().items():
+                self.forward_reports(part, msgs)
         st = self.stats
         st["reports"] += reports
         st["reports_pending"] += pending
@@ -588,11 +594,14 @@ class Controller(ReconcileMixin):
                         n += 1
         return n
 
-    def enqueue_all(self) -> None:
-        for t in self.template_lister.list():
-            self.enqueue_resource(t, C.KIND_TEMPLATE)
-        for w in self.workgroup_lister.list():
-            self.enqueue_resource(w, C.KIND_WORKGROUP)
+    def enqueue_all(self, part: tuple | None = None) -> None:
+        """Every template and workgroup (only the keys of partition `part` = (p, C) when given)."""
+        for lister, kind in ((self.template_lister, C.KIND_TEMPLATE), (self.workgroup_lister, C.KIND_WORKGROUP)):
+            for obj in lister.list():
+                m = meta(obj)
+                key = make_key(kind, m.get("namespace", "") or "", m.get("name", ""))
+                if part is None or key_part(key, part[1]) == part[0]:
+                    self._enqueue_key(key)
 
     async def _full_resync_loop(self) -> None:
         while True:

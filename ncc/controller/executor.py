@@ -261,6 +261,13 @@ class ExecutorPool:
         self.handles.extend(hs)
         return hs
 
+    def resync_partition(self, part: int, parts: int) -> None:
+        """Every executor passes over the keys of coordinator partition `part` of `parts` again (that
+        partition's process came up and holds no report state)."""
+        for h in self.handles:
+            if h.channel is not None:
+                h.channel.send({"t": "resync", "p": part, "n": parts})
+
     def add_shards(self, names: list[str]) -> None:
         """Hot-add: one new executor group per added shard (started immediately)."""
         for n in names:
@@ -318,21 +325,40 @@ class ExecutorPool:
 class CoordinatorPartitions:
     """Child coordinator processes for key partitions 1..C-1 (partition 0 is the parent itself).
 
-    Each child is a full native-mode coordinator (`python -m ncc`) restricted to the template keys
-    ≡ p mod C: it watches the controller cluster with that key filter, adopts, writes status and Events
-    for its keys, and runs its own shard executors (global partitions p + C·j).  The parent holds the
-    leader Lease and the ops endpoints; children exit when the parent's control channel closes."""
+    Each child is a native-mode coordinator (`python -m ncc`) restricted to the template keys ≡ p mod C: it
+    watches the controller cluster with that key filter, adopts, writes status and Events for its keys.  It
+    runs no executors: the parent's executors serve every key, and the parent's report table hands the
+    reports on the child's keys to `forward`, which relays them raw over the child's control channel.  The
+    parent holds the leader Lease and the ops endpoints; children exit when that channel closes."""
 
-    def __init__(self, parts: int, env: dict, gated: bool = False):
+    def __init__(self, parts: int, env: dict, gated: bool = False, on_child_ready=None):
         self.parts = parts
         self.handles = []
+        self.on_child_ready = on_child_ready  # callable(p): child p is up (again) and needs every report
+        self.forwarded = 0
         for p in range(1, parts):
             e = dict(env)
             e.update({"NCC_COORDINATOR_PART": f"{p}/{parts}", "NEXUS__LEADER_ELECT": "False",
                       "NEXUS__METRICS_BIND_ADDRESS": "", "NEXUS__HEALTH_BIND_ADDRESS": ""})
-            h = ExecutorHandle(p, [], lambda i, m: None, e, p, parts, argv=["-m", "ncc"], what="coordinator partition")
+            h = ExecutorHandle(p, [], self._on_child_message, e, p, parts, argv=["-m", "ncc"],
+                               what="coordinator partition")
             h.gated = gated
             self.handles.append(h)
+
+    def _on_child_message(self, index: int, msg) -> None:
+        if isinstance(msg, dict) and msg.get("t") == "ready" and self.on_child_ready is not None:
+            self.on_child_ready(index)
+
+    def forward(self, part: int, msgs: list) -> None:
+        """Executor reports (raw msgpack messages) on partition `part`'s keys, to its process."""
+        if not 1 <= part < self.parts:
+            return
+        ch = self.handles[part - 1].channel
+        if ch is None:
+            return  # restarting: it is resynced once it reports ready
+        for m in msgs:
+            ch.send_packed(m)
+        self.forwarded += len(msgs)
 
     def start(self) -> None:
         for h in self.handles:
@@ -393,6 +419,8 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
                     continue
                 if msg.get("t") == "go":
                     app.open_gate()
+                elif msg.get("t") == "resync" and app.controller is not None:
+                    app.controller.enqueue_all(part=(int(msg.get("p", 0)), int(msg.get("n", 1))))
 
     wp = asyncio.ensure_future(watch_parent())
     try:

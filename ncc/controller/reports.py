@@ -24,6 +24,8 @@ materialising a dict per report.  tests/test_reports.py drives the two in lock-s
 """
 from __future__ import annotations
 
+import zlib
+
 import msgpack
 
 from .. import native
@@ -34,6 +36,20 @@ class ReportTable:
     def __init__(self) -> None:
         self._shards: list[str] = []
         self._state: dict[str, dict[str, tuple]] = {}
+        self._part, self._parts = 0, 1
+        self._forwards: dict[int, list] = {}
+
+    def set_partition(self, part: int, parts: int) -> None:
+        """This coordinator owns the keys of partition `part` of `parts` (executor.key_part); reports on other
+        keys are not folded but kept, as msgpack messages, for `take_forwards` (the parent coordinator relays
+        them to the partition's process)."""
+        if parts < 1 or not 0 <= part < parts:
+            raise ValueError("set_partition: 0 <= part < parts")
+        self._part, self._parts = part, parts
+
+    def take_forwards(self) -> dict:
+        out, self._forwards = self._forwards, {}
+        return out
 
     def set_shards(self, shards) -> None:
         self._shards = list(shards)
@@ -64,8 +80,13 @@ class ReportTable:
             if not isinstance(msg, dict) or msg.get("t") != "report":
                 others.append(msg)
                 continue
-            reports += 1
             key, uid, gen = msg["k"], msg.get("u", ""), int(msg.get("g") or 0)
+            if self._parts > 1:
+                p = zlib.crc32(key.partition("/")[2].encode()) % self._parts
+                if p != self._part:
+                    self._forwards.setdefault(p, []).append(msgpack.packb(msg, use_bin_type=True))
+                    continue
+            reports += 1
             st = self._state.setdefault(key, {})
             changed = False
             for shard, err in msg["r"].items():

@@ -479,8 +479,9 @@ async def test_partition_filter_keeps_newly_referenced_dependent(tmp_path):
 
 async def test_partitioned_coordinators(tmp_path):
     """coordinator-partitions=2: the template keys are split between the parent coordinator and one child
-    coordinator process, each with its own executors.  Every template still becomes Ready, shared
-    dependents are adopted by all their templates, and a killed child is restarted and resumes its keys."""
+    coordinator process; the parent's executors serve both, and the reports on the child's keys are
+    forwarded to it.  Every template still becomes Ready, shared dependents are adopted by all their
+    templates, and a killed child is restarted, resynced and resumes its keys."""
     import os
     import signal
     from ncc.controller.executor import key_part
@@ -497,6 +498,7 @@ async def test_partitioned_coordinators(tmp_path):
         assert parts == {0, 1}, "the workload must exercise both coordinator partitions"
         async with Running(env, "native", coordinator_partitions=2, executors_per_shard=2) as app:
             assert app.coord_part == (0, 2) and app.partitions is not None
+            assert len(app.pool.handles) == 2 * 2 and app.topology()["executor_processes"] == 4
 
             async def all_ready(tag=None):
                 items = (await cc.list(R.TEMPLATES, NS))["items"]
@@ -521,6 +523,7 @@ async def test_partitioned_coordinators(tmp_path):
             events = (await cc.list(R.EVENTS, NS))["items"]
             assert {e["involvedObject"]["name"] for e in events if e["reason"] == C.SUCCESS_SYNCED} == \
                 {f"algo-{i:05d}" for i in range(T)}
+            assert app.partitions.forwarded > 0  # the child's statuses came from forwarded reports
 
             # kill the child coordinator: it is restarted and keeps serving its partition
             child = app.partitions.handles[0]
@@ -548,7 +551,8 @@ async def test_partitioned_coordinators(tmp_path):
 
 
 def test_partitioned_coordinators_share_the_executors(tmp_path, monkeypatch):
-    """C coordinators split the k executors per shard between them instead of each running k."""
+    """C coordinators share one set of executors (the parent's: k per shard, every key) instead of each
+    running its own: a shard apiserver serves k executors' watches whatever C is."""
     import asyncio as aio
     from ncc.app import App
     monkeypatch.delenv("NCC_COORDINATOR_PART", raising=False)
@@ -558,7 +562,7 @@ def test_partitioned_coordinators_share_the_executors(tmp_path, monkeypatch):
         try:
             app = App(env.app_config(mode="native", coordinator_partitions=2, executors_per_shard=4))
             await app.build()
-            assert app.coord_part == (0, 2) and app.per_shard == 2 and app.n_executors == 4
+            assert app.coord_part == (0, 2) and app.per_shard == 4 and app.n_executors == 4
             await app.factory.stop()
         finally:
             await env.stop()

@@ -149,8 +149,8 @@ def test_bench_two_ranks_over_gloo():
 def test_bench_eight_ranks_auto_sized_topology():
     """The driver's N=8 launch on a large host, rehearsed here: NCC_CPU_SHARE=128 makes the automatic
     sizing pick what it would on an 8-GPU node with ≥128 CPUs (ncc/app.py `auto_sizing`: native executors,
-    k=1 per shard, C=2 coordinator partitions (one per 4 shards) → 1 partition child + 2×8 executors under the
-    controller).
+    k=1 per shard, C=2 coordinator partitions (one per 4 shards) sharing the executors → 1 partition child +
+    8 executors under the controller).
     Every wave must converge with no process restarted and the controller alive."""
     pytest.importorskip("torch.distributed")
     from ncc.app import auto_sizing
@@ -168,10 +168,10 @@ def test_bench_eight_ranks_auto_sized_topology():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 8 and res["config"]["shards"] == 8 and res["controller_alive"]
     sz = res["controller_sizing"]
-    per_coord = max(1, k // c)  # each coordinator partition keeps its share of the k executors per shard
-    assert sz["cpus"] == 128 and sz["coordinator_partitions"] == c and sz["executors_per_shard"] == per_coord * c
+    # the C coordinators share the parent's k executors per shard
+    assert sz["cpus"] == 128 and sz["coordinator_partitions"] == c and sz["executors_per_shard"] == k
     assert sz["executor_impl"] == ("native" if native else "python")
-    want_children = (c - 1) + c * 8 * per_coord
+    want_children = (c - 1) + 8 * k
     ch = res["controller_children"]
     assert ch == {"start": want_children, "end": want_children, "replaced": 0}, (ch, sz)
     assert res["value"] > 0 and res["p50_latency_ms"] is not None

@@ -34,7 +34,8 @@ op = st.one_of(
     st.tuples(st.just("feed"), st.lists(st.one_of(report, report, other), min_size=1, max_size=5)),
     st.tuples(st.just("shards"), st.lists(st.sampled_from(SHARDS), unique=True, max_size=3)),
     st.tuples(st.just("drop"), st.lists(st.sampled_from(SHARDS), max_size=2)),
-    st.tuples(st.just("pop"), st.sampled_from(KEYS)))
+    st.tuples(st.just("pop"), st.sampled_from(KEYS)),
+    st.tuples(st.just("part"), st.integers(1, 3).flatmap(lambda c: st.tuples(st.integers(0, c - 1), st.just(c)))))
 
 
 def frame(msgs: list) -> tuple[bytes, bool]:
@@ -54,6 +55,11 @@ def test_native_report_table_matches_python(ops):
         if kind == "feed":
             body, batch = frame(arg)
             assert nat.feed(body, batch) == py.feed(body, batch)
+            fn, fp = nat.take_forwards(), py.take_forwards()
+            assert {p: [msgpack.unpackb(m) for m in ms] for p, ms in fn.items()} == \
+                {p: [msgpack.unpackb(m) for m in ms] for p, ms in fp.items()}
+        elif kind == "part":
+            py.set_partition(*arg), nat.set_partition(*arg)
         elif kind == "shards":
             py.set_shards(arg), nat.set_shards(arg)
             assert nat.shards() == py.shards() == arg
