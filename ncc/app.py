@@ -153,8 +153,8 @@ def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
 
 
 def auto_coordinator_partitions(groups: int, per_shard: int, cpus: int | None = None) -> int:
-    """Coordinator processes: one per executor key partition (C = k, so each coordinator keeps one executor
-    per shard) once there are ≥ 4 shard groups and ≥ 32 CPUs per coordinator; otherwise one.  At 8 shards
+    """Coordinator processes (Python executors): one per executor key partition (C = k) once there are ≥ 4
+    shard groups and ≥ 32 CPUs per coordinator; otherwise one.  The coordinators share the k executors.  At 8 shards
     one coordinator spends ~210 µs per template pass on the box (profiles/r1/session2/spr_8.json), which caps
     a single process near 110k objects/s; on a CPU-bound host extra processes only cost
     (profiles/r1/session2/coord_partitions_*)."""
