@@ -178,10 +178,10 @@ def auto_sizing(groups: int, cpus: int | None = None, native: bool = False) -> t
     The coordinator carries the per-template work (status, adoption, Events, reports).  One process keeps
     up with ~140-160k objects/s whether it serves 4 or 8 shards (box: N=4 134k at 0.93 cores,
     profiles/r2/sweep_r2e/; 8 shards on one rank 159k at 0.94 cores, profiles/r2/prof8/), i.e. with about
-    4 shards at a shard apiserver's ~36k objects/s.  But every coordinator partition brings its own
-    executor per shard, and each shard apiserver then serves C watch streams per kind: on one shard C=2
-    costs 12-17 % and C=4 about 25 % of the throughput (profiles/r2/c_on_one_shard/).  So C = one per 4
-    shard groups (N=8: 2), and only with 32 CPUs per coordinator, up to 4."""
+    4 shards at a shard apiserver's ~36k objects/s.  The partitions share the executors, so they cost the
+    shards next to nothing (profiles/r2/c_on_one_shard_shared/); they cost CPU.  So C = one per 4 shard
+    groups (N=8: 2), with 8 CPUs per coordinator, up to 4: 8 shards on one rank of the 16-CPU box ran
+    141k/179k objects/s at C=1, 156k/214k at C=2, 150k/197k at C=4 (profiles/r2/spr8_c_shared/)."""
     import math
     cpus = cpu_share() if cpus is None else cpus
     if not native:
@@ -189,7 +189,7 @@ def auto_sizing(groups: int, cpus: int | None = None, native: bool = False) -> t
         return k, auto_coordinator_partitions(groups, k, cpus)
     if groups < 4:
         return 1, 1
-    return 1, max(1, min(4, cpus // 32, math.ceil(groups / 4)))
+    return 1, max(1, min(4, cpus // 8, math.ceil(groups / 4)))
 
 
 def coordinator_partition(cfg: AppConfig, groups: int, per_shard: int, native: bool = False) -> tuple | None:

@@ -295,7 +295,8 @@ def test_native_auto_sizing_and_cpu_override(monkeypatch):
     assert auto_sizing(4, cpus=512, native=True) == (1, 1)
     assert auto_sizing(8, cpus=512, native=True) == (1, 2)
     assert auto_sizing(16, cpus=512, native=True) == (1, 4)
-    assert auto_sizing(32, cpus=96, native=True) == (1, 3)  # capped by 32 CPUs per coordinator
+    assert auto_sizing(32, cpus=24, native=True) == (1, 3)  # capped by 8 CPUs per coordinator
+    assert auto_sizing(8, cpus=16, native=True) == (1, 2) and auto_sizing(8, cpus=8, native=True) == (1, 1)
     assert auto_sizing(8, cpus=128, native=False) == (4, 4)  # Python executors: k = C = 4
     monkeypatch.setenv("NCC_CPU_SHARE", "128")
     assert cpu_share() == 128
