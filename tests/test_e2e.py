@@ -477,7 +477,8 @@ async def test_partition_filter_keeps_newly_referenced_dependent(tmp_path):
         await env.stop()
 
 
-async def test_partitioned_coordinators(tmp_path):
+@pytest.mark.parametrize("impl", ["native", "python"])
+async def test_partitioned_coordinators(tmp_path, impl, monkeypatch):
     """coordinator-partitions=2: the template keys are split between the parent coordinator and one child
     coordinator process; the parent's executors serve both, and the reports on the child's keys are
     forwarded to it.  Every template still becomes Ready, shared dependents are adopted by all their
@@ -496,8 +497,10 @@ async def test_partitioned_coordinators(tmp_path):
             await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=["shared"], configmaps=[f"c{i}"]))
         parts = {key_part(f"template/{NS}/algo-{i:05d}", 2) for i in range(T)}
         assert parts == {0, 1}, "the workload must exercise both coordinator partitions"
-        async with Running(env, "native", coordinator_partitions=2, executors_per_shard=2) as app:
-            assert app.coord_part == (0, 2) and app.partitions is not None
+        monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+        async with Running(env, "native", coordinator_partitions=2, executors_per_shard=2,
+                           executor_impl=impl) as app:
+            assert app.coord_part == (0, 2) and app.partitions is not None and app.executor_impl == impl
             assert len(app.pool.handles) == 2 * 2 and app.topology()["executor_processes"] == 4
 
             async def all_ready(tag=None):
