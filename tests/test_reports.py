@@ -134,6 +134,22 @@ def test_native_feed_stream_matches_python_at_any_split(frames, cuts):
     assert list(r[:4]) == results[0][:4] and r[4:6] == tuple(results[0][4:6]) and r[6] == len(data)
 
 
+def test_feed_stream_bounds():
+    """A frame header past the 64 MiB cap is an error, a partial header or body is left for the next read,
+    and `start` past the end is refused."""
+    for t in ([NATIVE.ReportTable()] if NATIVE is not None else []) + [ReportTable()]:
+        with pytest.raises(ValueError):
+            t.feed_stream(b"\x7f\xff\xff\xff" + b"x" * 8, 0)
+        body = msgpack.packb({"t": "ready", "i": 1})
+        data = len(body).to_bytes(4, "big") + body
+        assert t.feed_stream(data[:3], 0)[6] == 0 and t.feed_stream(data[:-1], 0)[6] == 0
+        assert t.feed_stream(data, 0)[3] == [{"t": "ready", "i": 1}] and t.feed_stream(data, 0)[6] == len(data)
+        assert t.feed_stream(b"pad" + data, 3)[6] == 3 + len(data)
+    if NATIVE is not None:
+        with pytest.raises(ValueError):
+            NATIVE.ReportTable().feed_stream(b"abc", 4)
+
+
 def test_report_table_completion_and_readiness():
     t = (NATIVE.ReportTable if NATIVE is not None else ReportTable)()
     t.set_shards(["a", "b"])
