@@ -217,6 +217,8 @@ def cpu_seconds(named: dict, rss: dict | None = None, sys_out: dict | None = Non
                 cot = [c.cpu_times() for c in co]
                 out["executors"] = sum(t.user + t.system for t in ext)
                 sys_out["executors"] = sum(t.system for t in ext)
+                if cot:  # partitioned: the parent alone too (it relays and routes every key's reports)
+                    out["coordinator-parent"] = out[name]
                 out[name] += sum(t.user + t.system for t in cot)
                 sys_out[name] += sum(t.system for t in cot)
                 if rss is not None:
