@@ -51,6 +51,8 @@ def main(argv=None) -> int:
     ap.add_argument("--total", type=float, default=75.0)
     ap.add_argument("--exempt", action="append", default=list(DEFAULT_EXEMPT))
     ap.add_argument("--report-only", action="store_true")
+    ap.add_argument("--show-missing", action="append", default=[], metavar="FILE",
+                    help="print the unexecuted line ranges of FILE (repo-relative, e.g. ncc/fakeapi/server.py)")
     ap.add_argument("pytest_args", nargs="*", default=["tests", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider"])
     a = ap.parse_args(argv)
 
@@ -82,6 +84,7 @@ def main(argv=None) -> int:
         return int(rc)
 
     rows = []
+    missing: dict[str, list[int]] = {}
     pkg_tot: dict[str, list[int]] = defaultdict(lambda: [0, 0])
     tot = [0, 0]
     for dirpath, _, files in os.walk(PKG):
@@ -97,6 +100,8 @@ def main(argv=None) -> int:
             pkg = os.path.dirname(rel)
             exempt = rel in a.exempt
             rows.append((rel, got, len(exe), exempt))
+            if rel in a.show_missing:
+                missing[rel] = sorted(exe - hits.get(path, set()))
             if not exempt:
                 pkg_tot[pkg][0] += got
                 pkg_tot[pkg][1] += len(exe)
@@ -118,6 +123,15 @@ def main(argv=None) -> int:
         print(f"package {pkg:44s} {pct:6.1f}%")
     total = 100.0 * tot[0] / max(tot[1], 1)
     print(f"\nTOTAL {total:.1f}%  ({tot[0]}/{tot[1]} lines)")
+    for rel, ls in missing.items():
+        spans, start = [], None
+        for i, ln in enumerate(ls):
+            if start is None:
+                start = ln
+            if i + 1 == len(ls) or ls[i + 1] != ln + 1:
+                spans.append(f"{start}" if start == ln else f"{start}-{ln}")
+                start = None
+        print(f"missing {rel}: {', '.join(spans)}")
     if total < a.total:
         bad.append(f"total {total:.1f}%")
     if bad and not a.report_only:

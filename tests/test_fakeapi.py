@@ -221,3 +221,77 @@ async def test_pipelined_transport_orders_responses_and_recovers():
     finally:
         await c.close()
         await srv.stop()
+
+
+async def test_control_endpoints_stage_apply_markers_and_seeding():
+    """The load generator's control plane (bench.py, bench/suite.py drive it from other processes): marker
+    probes, staged and direct applies, seeding of owned dependents, admission/fault switches and stats."""
+    import aiohttp
+    srv = FakeApiServer(name="ctl")
+    url = await srv.start()
+    try:
+        async with aiohttp.ClientSession() as s:
+            async def post(what, body):
+                async with s.post(f"{url}/_fake/{what}", json=body) as r:
+                    return r.status, await r.json()
+            st, out = await post("markers", {"specs": {"secrets": "data.version"}})
+            assert st == 200 and out["specs"]["secrets"] == "data.version"
+            sec = make_secret("m0", NS, version=1)
+            st, out = await post("stage", {"id": 7, "items": [sec], "yield_every": 1})
+            assert out == {"staged": "7", "items": 1}
+            st, out = await post("apply", {"staged": 7})
+            assert out["applied"] == 1 and out["t1_ns"] >= out["t0_ns"] and "7" not in srv.staged
+            # a second apply updates in place, keeping metadata the server owns
+            uid = srv.state.get(R.SECRETS, NS, "m0")["metadata"]["uid"]
+            sec2 = make_secret("m0", NS, version=2)
+            sec2["metadata"]["labels"] = {"wave": "2"}
+            st, out = await post("apply", {"items": [sec2, make_configmap("c0", NS)], "yield_every": 1})
+            cur = srv.state.get(R.SECRETS, NS, "m0")
+            assert out["applied"] == 2 and cur["metadata"]["uid"] == uid and cur["metadata"]["labels"] == {"wave": "2"}
+            st, out = await post("markers/wait", {"want": [{"plural": "secrets", "value": sec2["data"]["version"],
+                                                            "count": 1}], "timeout": 5, "times": True, "keyed": True})
+            assert out["ok"] and list(out["counts"].values()) == [1] and "times" in out
+            # seeding: a dependent owned by an existing template resolves the template's live UID
+            t = srv.state.create(R.TEMPLATES, NS, make_template(3, NS))
+            dep = make_secret("owned", NS)
+            dep["__owner_template__"] = t["metadata"]["name"]
+            st, out = await post("objects", {"items": [dep, make_secret("m0", NS)]})
+            assert out["created"] == 1  # m0 exists already: skipped
+            refs = srv.state.get(R.SECRETS, NS, "owned")["metadata"]["ownerReferences"]
+            assert refs[0]["uid"] == t["metadata"]["uid"]
+            st, out = await post("admission", {"prune_defaults": False, "sets": {}})
+            assert st == 200
+            st, out = await post("faults", {"compact": True})
+            assert st == 200
+            async with s.get(f"{url}/_fake/stats") as r:
+                stats = await r.json()
+            assert stats["name"] == "ctl" and stats["objects"]["core/secrets"] == 2
+            async with s.post(f"{url}/_fake/nope", json={}) as r:
+                assert r.status == 404
+    finally:
+        await srv.stop()
+
+
+async def test_serve_entrypoint_exits_when_parent_is_gone(tmp_path):
+    """`python -m ncc.fakeapi` as spawned by tests and benches, run in-process: markers, an admission field
+    set, the port file, and the exit once the parent PID disappears."""
+    import argparse
+    import gc
+    import subprocess
+    import sys
+
+    from ncc.fakeapi.server import serve
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    pf = tmp_path / "url"
+    args = argparse.Namespace(name="served", token=None, bookmark_interval=5.0, crd_dir=None, host="127.0.0.1",
+                              port=0, port_file=str(pf), tls_cert=None, tls_key=None, tls_client_ca=None,
+                              prune_defaults=False, admission_set=['secrets=metadata.labels.hook="on"'],
+                              parent_pid=dead.pid, marker=["secrets=data.version"])
+    thresholds = gc.get_threshold()
+    try:
+        await asyncio.wait_for(serve(args), timeout=15)
+    finally:
+        gc.set_threshold(*thresholds)
+        gc.unfreeze()
+    assert pf.read_text().startswith("http://127.0.0.1:")
