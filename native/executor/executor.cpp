@@ -36,6 +36,7 @@
 #include <unistd.h>
 
 #include <csignal>
+#include <optional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -140,9 +141,54 @@ struct NamedError : std::runtime_error {
     NamedError(std::string k, const std::string& m) : std::runtime_error(m), kind(std::move(k)) {}
 };
 
+// A failed step tagged with the shard object it concerns (a dependent's failure inside a template pass).
+struct ObjectError : std::runtime_error {
+    std::string cls, kind, name;
+    int code;
+    ObjectError(std::string c, std::string k, std::string n, int h, const std::string& m)
+        : std::runtime_error(m), cls(std::move(c)), kind(std::move(k)), name(std::move(n)), code(h) {}
+};
+
+// The typed failure a report carries per shard (ncc/controller/failures.py): class, object kind and name,
+// HTTP code, message.
+struct Failure {
+    std::string cls, kind, name, msg;
+    int code = 0;
+};
+
+static Failure failure_of(const std::exception_ptr& ep, const std::string& kind, const std::string& name) {
+    Failure f{"", kind, name, "", 0};
+    try {
+        std::rethrow_exception(ep);
+    } catch (const ObjectError& e) {
+        f = Failure{e.cls, e.kind, e.name, e.what(), e.code};
+    } catch (const ApiError& e) {
+        f.cls = e.kind();
+        f.code = e.code;
+        f.msg = e.what();
+    } catch (const NamedError& e) {
+        f.cls = e.kind;
+        f.msg = e.what();
+        if (e.kind == "ShardNotReadyError") f.kind.clear(), f.name.clear();
+    } catch (const TransportError& e) {
+        f.cls = "TransportError";
+        f.msg = e.what();
+    } catch (const std::exception& e) {
+        f.cls = "Error";
+        f.msg = e.what();
+    } catch (...) {
+        f.cls = "Error";
+        f.msg = "unknown";
+    }
+    if (f.msg.size() > 500) f.msg.resize(500);
+    return f;
+}
+
 static std::string describe(const std::exception_ptr& ep) {
     try {
         std::rethrow_exception(ep);
+    } catch (const ObjectError& e) {
+        return e.kind + " \"" + e.name + "\": " + e.cls + ": " + e.what();
     } catch (const ApiError& e) {
         return std::string(e.kind()) + ": " + e.what();
     } catch (const NamedError& e) {
@@ -1128,11 +1174,30 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
     co_return cur;
 }
 
+static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep,
+                                       PassState* pass);
+
+// syncSecretsToShard / syncConfigMapsToShard for one dependent: a failure is tagged with the dependent, so the
+// coordinator can record the reference's Warning Events for it (controller.go:497,525-557,587-619)
 static Task<void> sync_dependent(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep, PassState* pass) {
+    std::exception_ptr err;
+    try {
+        co_await sync_dependent_steps(shp, kind, tpl, st, dep, pass);
+    } catch (...) {
+        err = std::current_exception();
+    }
+    if (err) {
+        Failure f = failure_of(err, kind == SECRETS ? "Secret" : "ConfigMap", dep);
+        throw ObjectError(f.cls, f.kind, f.name, f.code, f.msg);
+    }
+}
+
+static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep,
+                                       PassState* pass) {
     Shard& sh = *shp;
     Executor& ex = *g_ex;
     CtlPtr src = ex.cget(kind, key_of(tpl->ns, dep));
-    if (!src) throw ApiError(404, "NotFound", std::string(kPlural[kind]) + " \"" + dep + "\" not found");
+    if (!src) throw NamedError("ReferenceMissing", std::string(kPlural[kind]) + " \"" + dep + "\" not found");
     const std::string& shard_ns = st->ns;
     bool is_secret = kind == SECRETS;
     bool with_bin = !is_secret && g_opt.sync_binary_data;
@@ -1247,8 +1312,8 @@ static Task<void> sync_workgroup_to_shard(Shard* shp, CtlPtr wg, PassState* pass
     if (!sw || !spec_in_sync(sh, WORKGROUPS, *sw, wg->fp_spec)) co_await write_crd(sh, WORKGROUPS, sw, *wg, pass);
 }
 
-static void report(const std::string& key, const CtlObj& obj, const std::vector<std::pair<std::string, std::string>>& results,
-                   bool wrote) {
+static void report(const std::string& key, const CtlObj& obj,
+                   const std::vector<std::pair<std::string, std::optional<Failure>>>& results, bool wrote) {
     mp::Encoder e;
     e.map(6);
     e.str("t");
@@ -1263,10 +1328,22 @@ static void report(const std::string& key, const CtlObj& obj, const std::vector<
     e.map(results.size());
     for (const auto& r : results) {
         e.str(r.first);
-        if (r.second.empty())
+        if (!r.second) {
             e.nil();
-        else
-            e.str(r.second.substr(0, 500));
+            continue;
+        }
+        const Failure& f = *r.second;
+        e.map(5);
+        e.str("c");
+        e.str(f.cls);
+        e.str("k");
+        e.str(f.kind);
+        e.str("n");
+        e.str(f.name);
+        e.str("h");
+        e.integer(f.code);
+        e.str("m");
+        e.str(f.msg);
     }
     e.str("w");
     e.boolean(wrote);
@@ -1334,16 +1411,18 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
         jobs.push_back(kind == TEMPLATES ? sync_template_to_shard(sp.get(), obj, &pass)
                                          : sync_workgroup_to_shard(sp.get(), obj, &pass));
     auto errs = co_await when_all(std::move(jobs));
-    std::vector<std::pair<std::string, std::string>> results;
+    std::vector<std::pair<std::string, std::optional<Failure>>> results;
     bool failed = false;
     std::string first;
+    const char* obj_kind = kind == TEMPLATES ? kTemplateKind : kWorkgroupKind;
     for (size_t i = 0; i < ex.shards.size(); ++i) {
-        std::string msg = errs[i] ? describe(errs[i]) : std::string();
+        std::optional<Failure> f;
         if (errs[i]) {
+            f = failure_of(errs[i], obj_kind, name);
+            if (!failed) first = ex.shards[i]->name + ": " + describe(errs[i]);
             failed = true;
-            if (first.empty()) first = ex.shards[i]->name + ": " + msg;
         }
-        results.emplace_back(ex.shards[i]->name, msg);
+        results.emplace_back(ex.shards[i]->name, std::move(f));
     }
     report(std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key, *obj, results, pass.wrote);
     if (failed) throw NamedError("ShardSyncError", first);

@@ -54,7 +54,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 16
+#define NCC_NATIVE_ABI 17
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -1782,7 +1782,9 @@ class ReportTable {
         std::string shard;
         std::string uid;
         int64_t gen = 0;
-        std::string err;  // empty: success (an empty error string is falsy in the Python twin too)
+        // the reported failure as its raw msgpack value (a typed failure map, ncc/controller/failures.py, or
+        // a free-form string); empty: success (nil, or an empty string, which is falsy in the Python twin too)
+        std::string err;
     };
 
     void set_shards(const std::vector<std::string>& shards) { shards_ = shards; }
@@ -1862,10 +1864,12 @@ class ReportTable {
         for (const auto& s : shards_) {
             const Slot* e = find(it->second, s);
             if (e == nullptr || e->uid != uid || e->gen < gen) return py::none();
-            if (e->err.empty())
+            if (e->err.empty()) {
                 out[py::str(s)] = py::none();
-            else
-                out[py::str(s)] = py::str(e->err);
+            } else {
+                MpReader er(e->err.data(), e->err.size());
+                out[py::str(s)] = py::reinterpret_steal<py::object>(er.value());
+            }
         }
         return std::move(out);
     }
@@ -1974,9 +1978,15 @@ class ReportTable {
         if (!r.map_len(m)) MpReader::fail();
         bool changed = false;
         for (size_t k = 0; k < m; ++k) {
-            std::string_view shard, err;
+            std::string_view shard, err, text;
             if (!r.str(shard)) MpReader::fail();
-            if (!r.nil() && !r.str(err)) MpReader::fail();
+            const uint8_t* v = r.pos();
+            if (!r.nil()) {
+                bool is_str = r.str(text);
+                if (!is_str) r.skip();  // a typed failure map (or any other value): kept raw
+                if (!is_str || !text.empty())  // an empty string is a success
+                    err = std::string_view(reinterpret_cast<const char*>(v), static_cast<size_t>(r.pos() - v));
+            }
             Slot* s = const_cast<Slot*>(find(slots, shard));
             if (s == nullptr) {
                 slots.push_back(Slot{std::string(shard), {}, 0, {}});

@@ -94,9 +94,14 @@ class Controller(ReconcileMixin):
         self.forward_reports = None
         self.all_shard_names = list(shard_names) if shard_names is not None else [s.name for s in self.shards]
         self.reporter = None  # executor role: callable(msg) sending results to the coordinator
+        # executor role with the watch relay: callable(kind index, "ns/name") asking the coordinator for a
+        # controller object this executor has not received (see `_executor_fetch_reference`)
+        self.need = None
         self.on_ready = None  # executor role: called once caches are synced and workers run
         self.on_synced = None  # executor role: called once caches are synced (before a gate opens)
         self._pending_event: set = set()
+        # coordinator: template key -> {shard: signature of the failure whose Warning Events were recorded}
+        self._failure_events: dict[str, dict] = {}
         # adoption_cache: template key → resourceVersion whose references were last verified as adopted
         self._adopted: dict[str, str] = {}
         if o.assume_writes:

@@ -403,14 +403,41 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
     ctl.on_ready = lambda: channel.send({"t": "ready", "i": index})
     ctl.on_synced = lambda: channel.send({"t": "synced", "i": index})
     feeds = app.relay_feeds  # controller informers fed by the coordinator's watch relay (or None)
+    if feeds is not None:
+        asked: dict = {}
+
+        def need(kind: int, key: str) -> None:  # at most once a second per object, like the C++ executor
+            now = asyncio.get_running_loop().time()
+            if now - asked.get(key, -1e9) >= 1.0:
+                if len(asked) > 4096:
+                    _prune()
+                asked[key] = now
+                channel.send({"t": "need", "k": kind, "n": key})
+        ctl.need = need
+
+        def _prune():  # keep the memo small: forget requests older than a minute
+            now = asyncio.get_running_loop().time()
+            for k in [k for k, t in asked.items() if now - t > 60.0]:
+                del asked[k]
 
     async def watch_parent():
         # {"t": "go"} opens the gate of an executor pre-spawned by a warm standby; the coordinator closing
-        # its end (or dying) ends this executor
+        # its end (or dying) ends this executor — and so does a channel it cannot read any more (a malformed
+        # or oversized frame): an executor cut off from the relay would reconcile from a stale cache, so it
+        # exits and the coordinator respawns it with a fresh snapshot
+        try:
+            await _watch_parent()
+        except Exception:  # noqa: BLE001
+            log.exception("executor %d: channel to the coordinator failed; exiting", index)
+            exit_code[0] = 1
+        stop.set()
+
+    exit_code = [0]
+
+    async def _watch_parent():
         while True:
             batch = await channel.recv()
             if batch is None:
-                stop.set()
                 return
             for msg in batch:
                 if not isinstance(msg, dict):
@@ -432,7 +459,7 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
         except Exception:  # noqa: BLE001
             pass
         channel.close()
-    return 0
+    return exit_code[0]
 
 
 def main(argv=None) -> int:

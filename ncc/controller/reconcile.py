@@ -26,6 +26,7 @@ from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready
                         secret_names, template_owner_ref)
 from ..kube import errors as E
 from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
+from . import failures as F
 
 log = logging.getLogger("ncc.reconcile")
 
@@ -109,6 +110,13 @@ async def gather_all(coros) -> list:
         except Exception as e:  # noqa: BLE001
             return [e]
     return await asyncio.gather(*coros, return_exceptions=True)
+
+
+def _shard_failure(e: BaseException, kind: str, name: str) -> dict:
+    """Typed failure of one shard's step: a dependent's tag wins; a shard that has not synced names no object."""
+    if isinstance(e, ShardNotReadyError):
+        return F.from_exception(e)
+    return F.from_exception(e, kind, name)
 
 
 class ReconcileMixin:
@@ -297,6 +305,7 @@ class ReconcileMixin:
             self._adopted.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
             if self.role == "coordinator":
                 self.reports.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
+                self._failure_events.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
                 self._inline_status_ok.pop(f"{C.KIND_TEMPLATE}/{namespace}/{name}", None)
                 self._pending_event.discard(f"{C.KIND_TEMPLATE}/{namespace}/{name}")
             elif self.options.queued_deletes:
@@ -338,7 +347,8 @@ class ReconcileMixin:
                 ok = [n for n in shard_names if n not in failures]
                 await self.report_template_synced_condition(
                     template, *dependent_names(template), ok, ready=False,
-                    message=f"Algorithm {q(name)} failed to sync to shards: {', '.join(sorted(failures))}")
+                    message=F.status_message(f"Algorithm {q(name)}", {
+                        s: _shard_failure(e, C.TEMPLATE_KIND, name) for s, e in failures.items()}))
                 raise ShardSyncError(failures)
         else:
             for shard in self.shards:
@@ -355,12 +365,12 @@ class ReconcileMixin:
         ns, name = meta(template).get("namespace", ""), meta(template).get("name", "")
         # the coordinator adopts; an executor only refuses to write when a reference is missing (as adoption would)
         secrets, configmaps = dependent_names(template)
-        for nm in secrets:
-            if self.secret_lister.try_get(ns, nm) is None:
-                await self._fetch_filtered(self.secret_informer, R.SECRETS, ns, nm)
-        for nm in configmaps:
-            if self.configmap_lister.try_get(ns, nm) is None:
-                await self._fetch_filtered(self.configmap_informer, R.CONFIGMAPS, ns, nm)
+        for rt, names, lister, informer in ((R.SECRETS, secrets, self.secret_lister, self.secret_informer),
+                                            (R.CONFIGMAPS, configmaps, self.configmap_lister,
+                                             self.configmap_informer)):
+            for nm in names:
+                if lister.try_get(ns, nm) is None:
+                    await self._executor_fetch_reference(informer, rt, ns, nm, template)
         spec_fp = fingerprint(template.get("spec")) if len(self.shards) > 1 and self.options.slim_shard_cache else None
         results = await gather_all(self._sync_template_to_shard(template, s, spec_fp) for s in self.shards)
         failures = {}
@@ -370,10 +380,24 @@ class ReconcileMixin:
             if isinstance(r, BaseException):
                 failures[s.name] = r
         self._report(C.KIND_TEMPLATE, ns, name, template,
-                     {s.name: (f"{type(failures[s.name]).__name__}: {failures[s.name]}"[:500]
-                               if s.name in failures else None) for s in self.shards})
+                     {s.name: (_shard_failure(failures[s.name], C.TEMPLATE_KIND, name) if s.name in failures else None)
+                      for s in self.shards})
         if failures:
             raise ShardSyncError(failures)
+
+    async def _executor_fetch_reference(self, informer, rt, ns: str, nm: str, template: dict) -> None:
+        """A referenced Secret/ConfigMap this executor has not received: with the watch relay, ask the
+        coordinator for it (it may have been routed to another partition while only other partitions'
+        templates owned it) as the C++ executor does; otherwise read it once.  The pass then fails without a
+        report and retries with backoff: the coordinator's adoption pass, which reads its own cache, is the
+        authority on a missing reference (ErrResourceMissing), and a relay that is a line behind must not flap
+        the status to Ready=False."""
+        if self.need is not None:
+            self.need(2 if rt is R.SECRETS else 3, f"{ns}/{nm}")
+        try:
+            await self._fetch_filtered(informer, rt, ns, nm)
+        except E.NotFound as e:
+            raise F.mark(e, rt.kind, nm, F.REFERENCE_MISSING)
 
     async def _fetch_filtered(self, informer, rt, ns: str, name: str) -> None:
         """A referenced dependent missing from a partition-filtered cache may have been dropped off the wire
@@ -394,18 +418,20 @@ class ReconcileMixin:
         results = self.shard_readiness(key, obj)
         if results is None:
             return  # some shard has not reported on this version yet; its report re-enqueues the key
-        failures = sorted(s for s, e in results.items() if e)
+        failures = {s: F.normalize(e) for s, e in results.items() if e}
         ok = [s for s in self.all_shard_names if not results[s]]
         is_template = kind == C.KIND_TEMPLATE
         if failures:
             what = f"Algorithm {q(name)}" if is_template else f"Workgroup {q(name)}"
-            msg = f"{what} failed to sync to shards: {', '.join(failures)}"
+            msg = F.status_message(what, failures)
             if is_template:
+                self._record_failure_events(key, obj, failures)
                 await self.report_template_synced_condition(obj, *dependent_names(obj), ok,
                                                             ready=False, message=msg)
             else:
                 await self.report_workgroup_synced_condition(obj, ready=False, message=msg)
             return
+        self._failure_events.pop(key, None)
         if is_template:
             obj = await self.report_template_synced_condition(obj, *dependent_names(obj), ok)
         else:
@@ -415,6 +441,24 @@ class ReconcileMixin:
             kind_name = C.TEMPLATE_KIND if is_template else C.WORKGROUP_KIND
             self.recorder.event(obj, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
                                 C.MESSAGE_RESOURCE_SYNCED.format(kind_name), kind=kind_name)
+
+    def _record_failure_events(self, key: str, template: dict, failures: dict) -> None:
+        """Coordinator: the Warning Events the in-process reconcile records where a shard write fails
+        (controller.go:497,525-557,587-619), from the executors' typed failures.  Recorded once per distinct
+        failure and shard: a backoff retry that fails the same way again changes nothing to announce (the
+        report table does not even complete a repeat of an identical report set), and the memo also covers
+        a set that completes again because *another* shard's result changed."""
+        seen = self._failure_events.setdefault(key, {})
+        for shard in sorted(failures):
+            f = failures[shard]
+            sig = F.signature(f)
+            if seen.get(shard) == sig:
+                continue
+            seen[shard] = sig
+            for etype, reason, message in F.events(f, meta(template).get("name", ""), shard):
+                self.recorder.event(template, etype, reason, message, kind=C.TEMPLATE_KIND)
+        for shard in [s for s in seen if s not in failures]:
+            del seen[shard]
 
     def finish_inline(self, key: str) -> bool:
         """Coordinator: the pass a complete set of executor reports would run, done synchronously when it can
@@ -533,8 +577,10 @@ class ReconcileMixin:
             for n in names:
                 await self._sync_dependent(rt, template, shard_template, shard, n)
 
-    def _dependent_failed(self, template: dict, dep_name: str, e: BaseException) -> BaseException:
-        """Warning ErrResourceSyncError on the template (controller.go:525,546,557); returns `e` to raise."""
+    def _dependent_failed(self, template: dict, kind: str, dep_name: str, e: BaseException) -> BaseException:
+        """Warning ErrResourceSyncError on the template (controller.go:525,546,557); returns `e` to raise,
+        tagged with the dependent it concerns (the typed failure an executor reports, `failures.py`)."""
+        F.mark(e, kind, dep_name)
         self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_SYNC_ERROR,
                             C.MESSAGE_RESOURCE_OPERATION_FAILED.format(q(dep_name), q(meta(template).get("name", "")),
                                                                       e), kind=C.TEMPLATE_KIND)
@@ -564,7 +610,10 @@ class ReconcileMixin:
             self.recorder.event(template, C.EVENT_TYPE_WARNING, C.ERR_RESOURCE_MISSING,
                                 C.MESSAGE_RESOURCE_MISSING.format(q(dep_name), q(tm.get("name", ""))),
                                 kind=C.TEMPLATE_KIND)
-            lister.get(ns, dep_name)  # raises NotFound
+            try:
+                lister.get(ns, dep_name)  # raises NotFound
+            except E.NotFound as e:
+                raise F.mark(e, kind, dep_name, F.REFERENCE_MISSING)
         shard_ns = meta(shard_template).get("namespace", "")
         shard_lister = shard.secret_lister if is_secret else shard.configmap_lister
         shard_obj = shard_lister.try_get(shard_ns, meta(src).get("name", ""))
@@ -580,7 +629,7 @@ class ReconcileMixin:
                 self._pass_wrote()
                 await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise self._dependent_failed(template, dep_name, e)
+                raise self._dependent_failed(template, kind, dep_name, e)
             return
         shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
         if shard_obj is None:
@@ -588,11 +637,11 @@ class ReconcileMixin:
                 shard_obj = await self._write(shard, "create_secret" if is_secret else "create_configmap",
                                               shard_informer, rt, shard_template, src, C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise self._dependent_failed(template, dep_name, e)
+                raise self._dependent_failed(template, kind, dep_name, e)
         try:
             missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template, shard.name)
         except RogueResourceError as e:
-            raise self._dependent_failed(template, dep_name, e)
+            raise self._dependent_failed(template, kind, dep_name, e)
         if is_secret and opts.sync_secret_type and \
                 (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
             # Secret.type is immutable: replace the shard copy (other owners re-add their refs on their passes)
@@ -602,7 +651,7 @@ class ReconcileMixin:
                 shard_obj = await self._write(shard, "create_secret", shard_informer, rt, shard_template, src,
                                               C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
-                raise self._dependent_failed(template, dep_name, e)
+                raise self._dependent_failed(template, kind, dep_name, e)
             return
         differs = not data_matches(src, shard_obj, with_binary)
         try:
@@ -621,7 +670,7 @@ class ReconcileMixin:
                     # The reference re-uses the pre-update object here (controller.go:552,614).
                     await self._put_dependent(shard, rt, src, shard_obj, None, shard_template, with_binary)
         except Exception as e:  # noqa: BLE001
-            raise self._dependent_failed(template, dep_name, e)
+            raise self._dependent_failed(template, kind, dep_name, e)
 
     async def propagate_template_delete(self, namespace: str, name: str) -> None:
         """Level-triggered shard delete (native `queued_deletes`): retried through the queue."""
@@ -688,7 +737,7 @@ class ReconcileMixin:
             results = await gather_all(self._sync_workgroup_to_shard(workgroup, s) for s in self.shards)
             failures = {s.name: r for s, r in zip(self.shards, results) if isinstance(r, BaseException)}
             self._report(C.KIND_WORKGROUP, namespace, name, workgroup,
-                         {s.name: (f"{type(failures[s.name]).__name__}: {failures[s.name]}"[:500]
+                         {s.name: (_shard_failure(failures[s.name], C.WORKGROUP_KIND, name)
                                    if s.name in failures else None) for s in self.shards})
             if failures:
                 raise ShardSyncError(failures)
@@ -704,7 +753,8 @@ class ReconcileMixin:
                 if self.options.shard_failure_isolation:
                     await self.report_workgroup_synced_condition(
                         workgroup, ready=False,
-                        message=f"Workgroup {q(name)} failed to sync to shards: {', '.join(sorted(failures))}")
+                        message=F.status_message(f"Workgroup {q(name)}", {
+                            s: _shard_failure(e, C.WORKGROUP_KIND, name) for s, e in failures.items()}))
                     raise ShardSyncError(failures)
                 raise next(iter(failures.values()))
         else:

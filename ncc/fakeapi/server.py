@@ -9,8 +9,11 @@ paths, namespaced and cluster-wide, `GET` (get / list / `?watch=1`), `POST`, `PU
 Test/bench control endpoints (not part of the Kubernetes API):
   GET  /_fake/stats    request counters and object counts
   POST /_fake/faults   {"latency_ms", "jitter_ms", "error_rate", "error_code", "throttle_rate",
-                        "down", "drop_watches", "compact"} — fault injection for the
-                       retry/backoff benchmark (BASELINE.json config 5)
+                        "down", "drop_watches", "compact", "rules"} — fault injection for the
+                       retry/backoff benchmark (BASELINE.json config 5) and for targeted tests:
+                       `rules` = [{"method", "resource", "name", "code", "reason", "count"}, ...] fail
+                       the matching requests ("*" or absent = any; `count` answers, -1 = until cleared)
+  GET  /_fake/writes   the mutating requests served so far ([method, plural, name, subresource, status])
   POST /_fake/objects  bulk create `{"items": [...]}` without per-request overhead (bench seeding)
   POST /_fake/apply    `{"items": [...], "yield_every": n}` create-or-update a wave of user changes,
                        committed in slices of n with watch delivery in between; `{"staged": id}`
@@ -65,8 +68,28 @@ class Faults:
         self.throttle_rate = 0.0
         self.down = False
         self.write_only = True  # error_rate applies to mutating requests only
+        self.rules: list[dict] = []  # targeted failures (see the module docstring)
+
+    def match(self, method: str, plural: str, name: str | None) -> tuple | None:
+        """(error, after) of the targeted rule this request matches, or None.  `after`: the request is
+        served and *then* answered with the error (a lost response, or a concurrent writer that won the
+        race: the object changed, the client is told it conflicted)."""
+        for r in self.rules:
+            if r.get("count", -1) == 0:
+                continue
+            if r.get("method", "*") not in ("*", method) or r.get("resource", "*") not in ("*", plural) or \
+                    r.get("name", "*") not in ("*", name):
+                continue
+            if r.get("count", -1) > 0:
+                r["count"] -= 1
+            err = E.from_status(int(r.get("code", 500)), {"reason": r.get("reason", ""),
+                                                          "message": r.get("message", "injected fault")})
+            return err, bool(r.get("after"))
+        return None
 
     def update(self, d: dict) -> None:
+        if "rules" in d:
+            self.rules = [dict(r) for r in d["rules"] or ()]
         for k in ("latency_ms", "jitter_ms", "error_rate", "throttle_rate"):
             if k in d:
                 setattr(self, k, float(d[k]))
@@ -97,6 +120,9 @@ class FakeApiServer:
         self.staged: dict[str, dict] = {}  # /_fake/stage: pre-decoded apply bodies by id
         self.state.write_hooks.append(self.markers.on_write)
         self.requests = {"total": 0, "watch_streams": 0, "errors_injected": 0, "throttled": 0}
+        # (method, plural, name, subresource, status) of every mutating request (tests count writes per object)
+        self.writes: list[tuple] = []
+        self.record_writes = False  # in-process test servers turn it on (FakeEnvironment)
         self._streams: set = set()
         self._http = web.HttpServer(self._dispatch, fast=self.fast)
         self.port: int | None = None
@@ -189,6 +215,18 @@ class FakeApiServer:
         return r
 
     def _core(self, request: web.Request):
+        """`_serve` plus the write log."""
+        r = self._serve(request)
+        if self.record_writes and request.method in ("POST", "PUT", "PATCH", "DELETE") and \
+                not isinstance(r, tuple) and request.path.startswith(("/api/", "/apis/")):
+            target = self._routes.get(request.path)
+            if isinstance(target, tuple) and len(target) == 4:
+                self.writes.append((request.method, target[0].plural, target[2], target[3], r.status))
+                if len(self.writes) > 100000:
+                    del self.writes[:50000]
+        return r
+
+    def _serve(self, request: web.Request):
         """Auth, faults, routing and CRUD for one request; returns a Response, or ("watch", rt, ns)."""
         path = request.path
         if path in ("/healthz", "/readyz", "/livez"):
@@ -217,43 +255,57 @@ class FakeApiServer:
             if target[0] == "resources":
                 return self._resource_list(target[1], target[2])
             rt, ns, name, sub = target
-            q = request.query
             m = request.method
-            if m == "GET":
-                if name is None:
-                    if q.get("watch") in ("1", "true"):
-                        return ("watch", rt, ns)
-                    limit = int(q["limit"]) if q.get("limit") else None
-                    return self._json(self.state.list(rt, ns, label_selector=q.get("labelSelector"), limit=limit,
-                                                      continue_token=q.get("continue")))
-                return self._json(self.state.get(rt, ns or "", name))
-            body = self._body(request) if m != "DELETE" or request.can_read_body else None
-            if m == "POST" and name is None:
-                return self._written(self.state.create(rt, ns or "", body, owned=True), 201)
-            if m == "PUT" and name is not None:
-                if (body.get("metadata") or {}).get("name") not in (None, name):
-                    raise E.BadRequest("the name of the object does not match the name on the URL")
-                body.setdefault("metadata", {})["name"] = name
-                if sub not in (None, "status"):
-                    raise E.NotFound(f"subresource {sub} not found")
-                if sub == "status" and not rt.has_status:
-                    raise E.NotFound(f"{rt.plural} has no status subresource")
-                return self._written(self.state.update(rt, ns or "", body, subresource=sub, owned=True))
-            if m == "PATCH" and name is not None:
-                ctype = request.content_type
-                if ctype not in (PATCH_MERGE, PATCH_STRATEGIC, PATCH_JSON, PATCH_APPLY):
-                    raise E.ApiError(f"unsupported patch type {ctype}", code=415, reason="UnsupportedMediaType")
-                return self._written(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
-            if m == "DELETE" and name is not None:
-                opts = body or {}
-                return self._json(self.state.delete(rt, ns or "", name, preconditions=opts.get("preconditions"),
-                                                    propagation_policy=opts.get("propagationPolicy")
-                                                    or q.get("propagationPolicy")))
-            raise E.MethodNotAllowed(f"method {m} not allowed on {path}")
+            if f.rules:
+                if m == "POST" and name is None:  # a create names its object in the body
+                    name = ((self._body(request) or {}).get("metadata") or {}).get("name")
+                hit = f.match(m, rt.plural, name)
+                if hit is not None:
+                    self.requests["errors_injected"] += 1
+                    if not hit[1]:
+                        raise hit[0]
+                    self._crud(request, path, rt, ns, target[2], sub)  # served, then answered with the error
+                    raise hit[0]
+            return self._crud(request, path, rt, ns, target[2], sub)
         except E.ApiError as e:
             return _status_response(e)
         except (ValueError, KeyError, TypeError) as e:
             return _status_response(E.BadRequest(f"bad request: {e}"))
+
+    def _crud(self, request: web.Request, path: str, rt, ns, name, sub):
+        q = request.query
+        m = request.method
+        if m == "GET":
+            if name is None:
+                if q.get("watch") in ("1", "true"):
+                    return ("watch", rt, ns)
+                limit = int(q["limit"]) if q.get("limit") else None
+                return self._json(self.state.list(rt, ns, label_selector=q.get("labelSelector"), limit=limit,
+                                                  continue_token=q.get("continue")))
+            return self._json(self.state.get(rt, ns or "", name))
+        body = self._body(request) if m != "DELETE" or request.can_read_body else None
+        if m == "POST" and name is None:
+            return self._written(self.state.create(rt, ns or "", body, owned=True), 201)
+        if m == "PUT" and name is not None:
+            if (body.get("metadata") or {}).get("name") not in (None, name):
+                raise E.BadRequest("the name of the object does not match the name on the URL")
+            body.setdefault("metadata", {})["name"] = name
+            if sub not in (None, "status"):
+                raise E.NotFound(f"subresource {sub} not found")
+            if sub == "status" and not rt.has_status:
+                raise E.NotFound(f"{rt.plural} has no status subresource")
+            return self._written(self.state.update(rt, ns or "", body, subresource=sub, owned=True))
+        if m == "PATCH" and name is not None:
+            ctype = request.content_type
+            if ctype not in (PATCH_MERGE, PATCH_STRATEGIC, PATCH_JSON, PATCH_APPLY):
+                raise E.ApiError(f"unsupported patch type {ctype}", code=415, reason="UnsupportedMediaType")
+            return self._written(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
+        if m == "DELETE" and name is not None:
+            opts = body or {}
+            return self._json(self.state.delete(rt, ns or "", name, preconditions=opts.get("preconditions"),
+                                                propagation_policy=opts.get("propagationPolicy")
+                                                or q.get("propagationPolicy")))
+        raise E.MethodNotAllowed(f"method {m} not allowed on {path}")
 
     @staticmethod
     def _body(request: web.Request):
@@ -383,6 +435,8 @@ class FakeApiServer:
                                "state": self.state.stats, "objects": counts, "faults": self.faults.as_dict(),
                                "admission": self.state.admission.as_dict(),
                                "watchers": len(self.state._watchers)})
+        if what == "writes":
+            return self._json({"writes": [list(w) for w in self.writes]})
         if what == "faults" and request.method == "POST":
             body = self._body(request)
             self.faults.update(body)

@@ -242,6 +242,10 @@ class ClusterState:
             raise _not_found(rt, name)
         return obj
 
+    def try_get(self, rt: ResourceType, ns: str, name: str) -> dict | None:
+        """The stored object, or None (tests; not counted as a request)."""
+        return self._bucket(rt, ns if rt.namespaced else "").get(name)
+
     def list(self, rt: ResourceType, ns: str | None, *, label_selector: str | None = None,
              limit: int | None = None, continue_token: str | None = None) -> dict:
         self.stats["list"] += 1

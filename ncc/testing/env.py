@@ -103,6 +103,7 @@ class FakeEnvironment:
             for n in names:
                 s = FakeApiServer(name=n, token=self.token, bookmark_interval=self.bookmark_interval,
                                   crd_dir=self.crd_dir)
+                s.record_writes = True
                 urls.append(await s.start(ssl_context=self.pki.server_context() if self.pki else None))
                 if n == "controller":
                     self.controller_server = s

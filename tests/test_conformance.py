@@ -1,0 +1,434 @@
+"""One conformance suite for the three implementations of the shard-side reconcile semantics.
+
+The same scenarios run against the whole controller (`App` over real HTTP to in-process fake apiservers), in
+each topology native mode can take:
+
+* ``inprocess`` — `executors: 0`: one process reconciles every shard (`ncc/controller/reconcile.py`, role "all");
+* ``python``    — the coordinator plus Python shard executors (`python -m ncc.executor`, role "executor");
+* ``native``    — the coordinator plus the C++ shard executor (`ncc/bin/ncc-executor`, native/executor/).
+
+What each scenario pins is the reference's behaviour (`/root/reference/controller.go:482-626,697-845`) with the
+native-mode changes documented in SURVEY.md Appendix B: rogue shard dependents refused with the Warning
+Events of `:497,525-557`; one PUT for data + ownerRef; Secret.type changes re-create the shard copy;
+ConfigMap.binaryData synced; per-shard failure isolation; deletes queued and retried; the orphan sweep;
+missing references refused; AlreadyExists/Conflict races resolved by re-reading; shard drift repaired; a
+shard watch that expired (410) relisted.
+"""
+import asyncio
+import os
+
+import pytest
+
+from ncc.api import constants as C
+from ncc.api import resources as R
+from ncc.app import App
+from ncc.controller.native_executor import binary_path
+from ncc.kube import errors as E
+from ncc.testing.env import FakeEnvironment
+from ncc.testing.workload import make_configmap, make_secret, make_template, make_workgroup
+
+NS = "nexus"
+T0 = "algo-00000"
+IMPLS = ["inprocess", "python", "native"]
+
+
+@pytest.fixture(params=IMPLS)
+def impl(request, monkeypatch):
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+    if request.param == "native" and binary_path() is None:
+        pytest.skip("ncc/bin/ncc-executor is not built")
+    return request.param
+
+
+def impl_config(impl: str) -> dict:
+    kw = dict(failure_rate_max_delay=0.2, full_resync_period=0)
+    if impl == "inprocess":
+        return dict(kw, executors=0)
+    return dict(kw, executor_impl=impl)
+
+
+async def wait_for(pred, timeout=8.0, interval=0.02):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    last = None
+    while loop.time() < end:
+        try:
+            last = await pred()
+            if last:
+                return last
+        except E.NotFound:
+            pass
+        await asyncio.sleep(interval)
+    raise AssertionError(f"condition not met within {timeout}s (last={last!r})")
+
+
+async def mutate(client, rt, name, fn, attempts=20):
+    for _ in range(attempts):
+        cur = await client.get(rt, NS, name)
+        fn(cur)
+        try:
+            return await client.update(rt, NS, cur)
+        except E.Conflict:
+            await asyncio.sleep(0.01)
+    raise AssertionError(f"could not update {name}")
+
+
+class Cluster:
+    """A FakeEnvironment, its clients, and a running controller in the topology under test."""
+
+    def __init__(self, tmp_path, impl: str, n_shards: int = 2, **cfg):
+        self.tmp_path, self.impl, self.n_shards, self.cfg = str(tmp_path), impl, n_shards, cfg
+        self.stop = asyncio.Event()
+
+    async def __aenter__(self):
+        self.env = await FakeEnvironment(self.n_shards, self.tmp_path).start()
+        self.cc = self.env.controller_client()
+        self.sc = [self.env.shard_client(i) for i in range(self.n_shards)]
+        self.cstate = self.env.controller_server.state
+        self.sstates = [s.state for s in self.env.shard_servers]
+        return self
+
+    async def start(self):
+        self.app = App(self.env.app_config(mode="native", **impl_config(self.impl), **self.cfg))
+        await self.app.build()
+        self.task = asyncio.ensure_future(self.app.run(self.stop))
+        await asyncio.wait_for(self.app.controller.ready.wait(), 15)
+        if self.impl == "inprocess":
+            assert self.app.pool is None
+        else:
+            assert self.app.executor_impl == self.impl, "the scenario must run the implementation it names"
+            await wait_for(lambda: asyncio.sleep(0, self.app.pool.all_synced()), timeout=15)
+        return self.app
+
+    async def __aexit__(self, *exc):
+        self.stop.set()
+        if hasattr(self, "task"):
+            await asyncio.wait_for(self.task, 20)
+        for c in [self.cc] + self.sc:
+            await c.close()
+        await self.env.stop()
+
+    # ------------------------------------------------------------------ helpers
+    def seed(self, i=0, secrets=("s0",), configmaps=("c0",)):
+        for s in secrets:
+            if self.cstate.try_get(R.SECRETS, NS, s) is None:
+                self.cstate.create(R.SECRETS, NS, make_secret(s, NS))
+        for c in configmaps:
+            if self.cstate.try_get(R.CONFIGMAPS, NS, c) is None:
+                self.cstate.create(R.CONFIGMAPS, NS, make_configmap(c, NS))
+        return self.cstate.create(R.TEMPLATES, NS, make_template(i, NS, secrets=list(secrets),
+                                                                 configmaps=list(configmaps)))
+
+    def status(self, name=T0) -> dict:
+        return self.cstate.get(R.TEMPLATES, NS, name).get("status") or {}
+
+    async def ready(self, name=T0, shards=None) -> dict:
+        shards = shards if shards is not None else self.env.shard_names
+
+        async def ok():
+            st = self.status(name)
+            c = (st.get("conditions") or [{}])[0]
+            return c.get("status") == "True" and st.get("syncedToClusters") == shards and st
+        return await wait_for(ok)
+
+    async def not_ready(self, name=T0, *needles) -> str:
+        async def ok():
+            c = (self.status(name).get("conditions") or [{}])[0]
+            msg = c.get("message") or ""
+            return c.get("status") == "False" and all(n in msg for n in needles) and msg
+        return await wait_for(ok)
+
+    def events(self, reason=None, name=T0) -> list:
+        return [e for e in self.cstate.list(R.EVENTS, NS)["items"]
+                if e["involvedObject"]["name"] == name and (reason is None or e["reason"] == reason)]
+
+    async def wait_events(self, reason, name=T0, n=1) -> list:
+        return await wait_for(lambda: asyncio.sleep(0, len(self.events(reason, name)) >= n and
+                                                    self.events(reason, name)))
+
+    def writes(self, shard: int, plural: str, name: str) -> list:
+        return [w for w in self.env.shard_servers[shard].writes if w[1] == plural and w[2] == name]
+
+    def rules(self, shard: int, rules: list) -> None:
+        self.env.shard_servers[shard].faults.update({"rules": rules})
+
+
+# ---------------------------------------------------------------------------------------------- scenarios
+async def test_fanout_status_and_synced_event(tmp_path, impl):
+    async with Cluster(tmp_path, impl) as cl:
+        cl.seed()
+        cl.cstate.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        await cl.start()
+        st = await cl.ready()
+        assert st["syncedSecrets"] == ["s0"] and st["syncedConfigurations"] == ["c0"]
+        for s in cl.sstates:
+            t = s.get(R.TEMPLATES, NS, T0)
+            assert t["metadata"]["labels"] == C.owner_labels("controller-cluster")
+            for rt, nm in ((R.SECRETS, "s0"), (R.CONFIGMAPS, "c0")):
+                dep = s.get(rt, NS, nm)
+                assert [r["uid"] for r in dep["metadata"]["ownerReferences"]] == [t["metadata"]["uid"]]
+                assert dep["data"] == cl.cstate.get(rt, NS, nm)["data"]
+        await wait_for(lambda: asyncio.sleep(0, all(s.try_get(R.WORKGROUPS, NS, "mi355x") for s in cl.sstates)))
+        await cl.wait_events(C.SUCCESS_SYNCED)
+        owners = cl.cstate.get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+        assert [o["name"] for o in owners] == [T0]  # controller-side adoption (controller.go:647-695)
+
+
+async def test_rogue_dependent_warning_events_and_status(tmp_path, impl):
+    """A shard Secret without ownerRefs is refused on that shard only; the template gets the reference's
+    Warning ErrResourceExists (naming kind and shard) and ErrResourceSyncError, and a Ready=False status
+    naming the shard, the dependent and the reason.  Removing the rogue object lets the template converge."""
+    async with Cluster(tmp_path, impl) as cl:
+        rogue = make_secret("s0", NS, version=7)
+        cl.sstates[0].create(R.SECRETS, NS, rogue)
+        cl.seed()
+        await cl.start()
+        msg = await cl.not_ready(T0, "shard-0", 'Secret "s0"', "RogueResourceError", "already exists")
+        assert "shard-1" not in msg.split("(")[0]
+        exists = await cl.wait_events(C.ERR_RESOURCE_EXISTS)
+        assert exists[0]["type"] == C.EVENT_TYPE_WARNING
+        assert "Secret" in exists[0]["message"] and 'shard "shard-0"' in exists[0]["message"]
+        assert exists[0]["involvedObject"]["kind"] == C.TEMPLATE_KIND
+        sync_err = await cl.wait_events(C.ERR_RESOURCE_SYNC_ERROR)
+        assert sync_err[0]["message"].startswith(
+            'Synchronization/update of a resource "s0" referenced by NexusAlgorithmTemplate "algo-00000" failed '
+            'with a fatal error Resource "s0" already exists')
+        assert cl.status()["syncedToClusters"] == ["shard-1"]
+        assert cl.sstates[0].get(R.SECRETS, NS, "s0")["data"] == rogue["data"]  # never overwritten
+        assert cl.sstates[1].get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+        # the operator removes the rogue object: the next retry creates ours and the template becomes Ready
+        cl.sstates[0].delete(R.SECRETS, NS, "s0")
+        await cl.ready()
+        assert cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+
+
+async def test_single_put_for_data_and_owner(tmp_path, impl):
+    """A shard dependent owned by another template with stale data gets one PUT carrying both the new data and
+    the appended ownerRef (the reference issues two, the second on a stale object: controller.go:539-560)."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        other = cl.sstates[0].create(R.TEMPLATES, NS, make_template(99, NS))
+        sec = make_secret("s0", NS, version=42)
+        sec["metadata"]["ownerReferences"] = [{"apiVersion": C.API_VERSION, "kind": C.TEMPLATE_KIND,
+                                               "name": other["metadata"]["name"], "uid": other["metadata"]["uid"]}]
+        cl.sstates[0].create(R.SECRETS, NS, sec)
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        live = cl.sstates[0].get(R.SECRETS, NS, "s0")
+        assert live["data"] == cl.cstate.get(R.SECRETS, NS, "s0")["data"]
+        assert [r["name"] for r in live["metadata"]["ownerReferences"]] == ["algo-00099", T0]
+        writes = cl.writes(0, "secrets", "s0")
+        assert [w[0] for w in writes] == ["PUT"], writes
+
+
+async def test_secret_type_change_recreates_shard_copy(tmp_path, impl):
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        old_uid = cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]["uid"]
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o.__setitem__("type", "kubernetes.io/dockerconfigjson"))
+
+        async def recreated():
+            live = cl.sstates[0].try_get(R.SECRETS, NS, "s0")
+            return live is not None and live.get("type") == "kubernetes.io/dockerconfigjson" and \
+                live["metadata"]["uid"] != old_uid and live
+        live = await wait_for(recreated)
+        st_uid = cl.sstates[0].get(R.TEMPLATES, NS, T0)["metadata"]["uid"]
+        assert [r["uid"] for r in live["metadata"]["ownerReferences"]] == [st_uid]
+        assert live["data"] == cl.cstate.get(R.SECRETS, NS, "s0")["data"]
+
+
+async def test_configmap_binary_data_synced(tmp_path, impl):
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cm = make_configmap("c0", NS)
+        cm["binaryData"] = {"blob": "AAEC"}
+        cl.cstate.create(R.CONFIGMAPS, NS, cm)
+        cl.seed(secrets=())
+        await cl.start()
+        await cl.ready()
+        assert cl.sstates[0].get(R.CONFIGMAPS, NS, "c0")["binaryData"] == {"blob": "AAEC"}
+        await mutate(cl.cc, R.CONFIGMAPS, "c0", lambda o: o.__setitem__("binaryData", {"blob": "AwQF"}))
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.CONFIGMAPS, NS, "c0").get("binaryData") ==
+                                             {"blob": "AwQF"}))
+        await mutate(cl.cc, R.CONFIGMAPS, "c0", lambda o: o.pop("binaryData"))
+        await wait_for(lambda: asyncio.sleep(0, not cl.sstates[0].get(R.CONFIGMAPS, NS, "c0").get("binaryData")))
+
+
+async def test_failure_isolation_names_shard_and_reason(tmp_path, impl):
+    """A shard that rejects every create does not hold up the other: that one is synced, the status names the
+    failing shard and the API error; when the shard recovers the template converges."""
+    async with Cluster(tmp_path, impl) as cl:
+        cl.rules(1, [{"method": "POST", "code": 503, "message": "shard-1 is down for maintenance"}])
+        cl.seed()
+        await cl.start()
+        await cl.not_ready(T0, "shard-1", "ServiceUnavailable", "down for maintenance")
+        assert cl.status()["syncedToClusters"] == ["shard-0"]
+        assert cl.sstates[0].try_get(R.SECRETS, NS, "s0") is not None
+        assert cl.sstates[1].count(R.TEMPLATES) == 0
+        assert cl.events(C.ERR_RESOURCE_EXISTS) == []  # a template write failure records no Event (:795-831)
+        cl.rules(1, [])
+        await cl.ready()
+
+
+async def test_dependent_write_failure_records_sync_error(tmp_path, impl):
+    """A dependent whose write fails (403 here) gets Warning ErrResourceSyncError with the API error text."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.rules(0, [{"method": "POST", "resource": "configmaps", "code": 403,
+                      "message": "configmaps is forbidden: quota exceeded"}])
+        cl.seed()
+        await cl.start()
+        await cl.not_ready(T0, "shard-0", 'ConfigMap "c0"', "Forbidden", "quota exceeded")
+        ev = await cl.wait_events(C.ERR_RESOURCE_SYNC_ERROR)
+        assert '"c0"' in ev[0]["message"] and "quota exceeded" in ev[0]["message"]
+        assert cl.events(C.ERR_RESOURCE_EXISTS) == []
+        cl.rules(0, [])
+        await cl.ready()
+
+
+async def test_queued_delete_is_retried(tmp_path, impl):
+    """A template delete that fails on one shard is retried until it succeeds there (the reference drops it
+    after the first error, controller.go:195-205)."""
+    async with Cluster(tmp_path, impl) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        cl.rules(1, [{"method": "DELETE", "resource": "nexusalgorithmtemplates", "code": 500}])
+        await cl.cc.delete(R.TEMPLATES, NS, T0)
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].try_get(R.TEMPLATES, NS, T0) is None))
+        await wait_for(lambda: asyncio.sleep(0, len(cl.writes(1, "nexusalgorithmtemplates", T0)) >= 3))
+        assert cl.sstates[1].try_get(R.TEMPLATES, NS, T0) is not None
+        cl.rules(1, [])
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[1].try_get(R.TEMPLATES, NS, T0) is None))
+        # shard GC collects the dependents that only it owned
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[1].try_get(R.SECRETS, NS, "s0") is None))
+
+
+async def test_orphan_sweep_removes_only_our_objects(tmp_path, impl):
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        mine = make_template(5, NS)
+        mine["metadata"]["labels"] = C.owner_labels("controller-cluster")
+        cl.sstates[0].create(R.TEMPLATES, NS, mine)
+        cl.sstates[0].create(R.TEMPLATES, NS, make_template(6, NS))  # someone else's
+        wg = make_workgroup("old-pool", NS)
+        wg["metadata"]["labels"] = C.owner_labels("controller-cluster")
+        cl.sstates[0].create(R.WORKGROUPS, NS, wg)
+        await cl.start()
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].try_get(R.TEMPLATES, NS, "algo-00005") is None))
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].try_get(R.WORKGROUPS, NS, "old-pool") is None))
+        assert cl.sstates[0].try_get(R.TEMPLATES, NS, "algo-00006") is not None
+
+
+async def test_missing_reference_is_refused_until_it_exists(tmp_path, impl):
+    async with Cluster(tmp_path, impl) as cl:
+        cl.cstate.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["later"]))
+        await cl.start()
+        ev = await cl.wait_events(C.ERR_RESOURCE_MISSING)
+        assert ev[0]["message"] == ('Resource "later" referenced by NexusAlgorithmTemplate "algo-00000" is missing '
+                                    'in the controller cluster')
+        await asyncio.sleep(0.3)
+        assert all(s.count(R.TEMPLATES) == 0 for s in cl.sstates)  # nothing written while a reference is missing
+        await cl.cc.create(R.SECRETS, NS, make_secret("later", NS))
+        await cl.ready()
+        assert all(s.try_get(R.SECRETS, NS, "later") is not None for s in cl.sstates)
+
+
+async def test_write_races_resolved_by_rereading(tmp_path, impl):
+    """A create answered AlreadyExists and an update answered Conflict — both after the server applied the
+    request, as when a concurrent writer won — are resolved from the live object, without a failed pass
+    surfacing in the status."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        await cl.wait_events(C.SUCCESS_SYNCED)
+        cl.rules(0, [{"method": "PUT", "resource": "secrets", "name": "s0", "code": 409, "reason": "Conflict",
+                      "after": True, "count": 1},
+                     {"method": "POST", "resource": "configmaps", "name": "c1", "code": 409,
+                      "reason": "AlreadyExists", "after": True, "count": 1}])
+        cl.cstate.create(R.CONFIGMAPS, NS, make_configmap("c1", NS))
+
+        def edit(o):
+            o["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"].append({"configMapRef": {"name": "c1"}})
+        await mutate(cl.cc, R.TEMPLATES, T0, edit)
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o.__setitem__("data", {"token": "cmFjZQ=="}))
+
+        async def converged():
+            sec = cl.sstates[0].get(R.SECRETS, NS, "s0")
+            cm = cl.sstates[0].try_get(R.CONFIGMAPS, NS, "c1")
+            return sec["data"] == {"token": "cmFjZQ=="} and cm is not None and cm["metadata"].get("ownerReferences")
+        await wait_for(converged)
+        assert cl.env.shard_servers[0].faults.rules[0]["count"] == 0 and cl.env.shard_servers[0].faults.rules[1][
+            "count"] == 0, "both races must have been provoked"
+        st = await cl.ready()
+        assert st["syncedConfigurations"] == ["c0", "c1"]
+
+
+async def test_shard_drift_repaired(tmp_path, impl):
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        await mutate(cl.sc[0], R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("versionTag", "bad"))
+        await mutate(cl.sc[0], R.SECRETS, "s0", lambda o: o.__setitem__("data", {"token": "dGFtcGVyZWQ="}))
+        await cl.sc[0].delete(R.CONFIGMAPS, NS, "c0")
+        want = cl.cstate.get(R.SECRETS, NS, "s0")["data"]
+
+        async def repaired():
+            t = cl.sstates[0].get(R.TEMPLATES, NS, T0)
+            cm = cl.sstates[0].try_get(R.CONFIGMAPS, NS, "c0")
+            return t["spec"]["container"]["versionTag"] == "v1.0.0" and cm is not None and \
+                cl.sstates[0].get(R.SECRETS, NS, "s0")["data"] == want
+        await wait_for(repaired)
+
+
+async def test_shard_watch_expiry_relists_and_repairs(tmp_path, impl):
+    """The shard apiserver goes away, its objects change meanwhile and its watch history is compacted: the
+    shard informers' resume gets 410 Gone, they relist, and the drift that happened during the gap is
+    repaired (client-go's reflector relist; the C++ executor's `shard_informer`)."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        srv, st = cl.env.shard_servers[0], cl.sstates[0]
+        lists_before = st.stats["list"]
+        srv.faults.update({"down": True})
+        srv.drop_watches()
+        t = st.get(R.TEMPLATES, NS, T0)
+        st.update(R.TEMPLATES, NS, dict(t, spec=dict(t["spec"], container=dict(t["spec"]["container"],
+                                                                               versionTag="gap"))))
+        st.delete(R.CONFIGMAPS, NS, "c0")
+        st.compact()
+        await asyncio.sleep(0.3)
+        srv.faults.update({"down": False})
+
+        async def repaired():
+            t = st.get(R.TEMPLATES, NS, T0)
+            return t["spec"]["container"]["versionTag"] == "v1.0.0" and st.try_get(R.CONFIGMAPS, NS, "c0")
+        await wait_for(repaired, timeout=15)
+        # every shard informer relists after its expired watch (each on its own backoff schedule)
+        await wait_for(lambda: asyncio.sleep(0, st.stats["list"] >= lists_before + 4), timeout=15)
+
+
+async def test_workgroup_fanout_update_and_delete(tmp_path, impl):
+    async with Cluster(tmp_path, impl) as cl:
+        cl.cstate.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        await cl.start()
+        await wait_for(lambda: asyncio.sleep(0, all(s.try_get(R.WORKGROUPS, NS, "mi355x") for s in cl.sstates)))
+
+        async def wg_ready():
+            c = ((cl.cstate.get(R.WORKGROUPS, NS, "mi355x").get("status") or {}).get("conditions") or [{}])[0]
+            return c.get("status") == "True"
+        await wait_for(wg_ready)
+        await mutate(cl.cc, R.WORKGROUPS, "mi355x", lambda o: o["spec"].__setitem__("description", "v2"))
+        await wait_for(lambda: asyncio.sleep(0, all(s.get(R.WORKGROUPS, NS, "mi355x")["spec"]["description"] == "v2"
+                                                    for s in cl.sstates)))
+        await cl.cc.delete(R.WORKGROUPS, NS, "mi355x")
+        await wait_for(lambda: asyncio.sleep(0, all(s.try_get(R.WORKGROUPS, NS, "mi355x") is None
+                                                    for s in cl.sstates)))
+
+
+def test_every_implementation_is_exercised():
+    """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
+    if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
+        assert binary_path() is not None

@@ -18,10 +18,16 @@ NATIVE = native.load()
 SHARDS = ["s0", "s1", "s2"]
 KEYS = ["NexusAlgorithmTemplate/ns/a", "NexusAlgorithmTemplate/ns/b", "NexusAlgorithmWorkgroup/ns/w"]
 
+# typed failures (ncc/controller/failures.py): kept raw by the native table, decoded back by readiness()
+failure = st.fixed_dictionaries({"c": st.sampled_from(["RogueResourceError", "Conflict", "TransportError"]),
+                                 "k": st.sampled_from(["", "Secret", "NexusAlgorithmTemplate"]),
+                                 "n": st.sampled_from(["", "s0"]), "h": st.integers(0, 600),
+                                 "m": st.text(max_size=6)})
 report = st.fixed_dictionaries({
     "t": st.just("report"), "k": st.sampled_from(KEYS), "u": st.sampled_from(["u1", "u2"]),
     "g": st.integers(0, 4), "r": st.dictionaries(st.sampled_from(SHARDS + ["gone"]),
-                                                 st.one_of(st.none(), st.just(""), st.sampled_from(["boom", "409"])),
+                                                 st.one_of(st.none(), st.just(""), st.sampled_from(["boom", "409"]),
+                                                           failure),
                                                  min_size=1, max_size=3),
     "w": st.booleans()})
 other = st.one_of(
