@@ -6,7 +6,8 @@
 //
 //   coordinator -> executor   {"t":"cfg","c":<json>}   shards (resolved credentials) + options
 //                             {"t":"s"|"w","k":kind,"l":[raw watch line...]}  watch relay
-//                                (ncc/controller/relay.py): the controller cluster's objects
+//                                (ncc/controller/relay.py): the controller cluster's objects; a listing
+//                                ("s") may come in chunks, all but the last with "more": true
 //                             {"t":"go"}   warm standby acquired the Lease: start the workers
 //                             {"t":"resync","p":p,"n":C}   pass again over the keys of coordinator partition p
 //                             {"t":"cred","s":shard,"token":...}   refreshed exec credential
@@ -672,6 +673,7 @@ struct Executor {
     Event gate;
     Event stop_ev;
     std::unordered_map<std::string, double> needed;  // dependent keys asked from the coordinator
+    std::vector<CtlPtr> partial_snapshot[4];          // chunks of a listing still arriving (per kind)
     long long stats_reconciles = 0, stats_errors = 0, stats_writes = 0;
 
     CtlPtr cget(int k, const std::string& key) const {
@@ -1488,20 +1490,11 @@ static Task<void> full_resync_loop() {
     }
 }
 
-static Task<bool> wait_event(Event& ev, double timeout) {
-    double end = now_s() + timeout;
-    while (!ev.is_set()) {
-        if (now_s() >= end) co_return false;
-        co_await loop().sleep(std::min(0.01, std::max(0.0, end - now_s())));
-    }
-    co_return true;
-}
-
 static Task<void> wait_shard_synced(Shard* sh, double timeout) {
     double end = now_s() + timeout;
     for (auto& inf : sh->inf) {
         double left = end - now_s();
-        if (left <= 0 || !(co_await wait_event(inf.synced_ev, left))) {
+        if (left <= 0 || !(co_await inf.synced_ev.wait_for(left))) {
             LOG_WARN("shard %s did not sync within %.1fs; continuing without it for now", sh->name.c_str(), timeout);
             co_return;
         }
@@ -1577,14 +1570,18 @@ static void handle_message(const mp::Obj& m) {
         std::string type;
         std::string_view raw[3];
         if (t == "s") {
-            std::vector<CtlPtr> objs;
-            objs.reserve(lines->a.size());
+            // a large listing arrives in chunks: every one but the last carries "more" (relay.py)
+            std::vector<CtlPtr>& objs = ex.partial_snapshot[kind];
+            objs.reserve(objs.size() + lines->a.size());
             for (const auto& l : lines->a) {
                 Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
                                                                             payload_count(kind), raw);
                 if (o.is_obj() && (type == "ADDED" || type == "MODIFIED")) objs.push_back(make_ctl(kind, o, raw));
             }
+            const mp::Obj* more = m.get("more");
+            if (more != nullptr && more->t == mp::Obj::BOOL && more->b) return;
             ctl_snapshot(kind, std::move(objs));
+            objs = std::vector<CtlPtr>();
         } else {
             for (const auto& l : lines->a) {
                 Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
@@ -1638,7 +1635,7 @@ static Task<void> reader(Event* configured) {
 
 static Task<void> run_main() {
     Executor& ex = *g_ex;
-    Event configured;
+    static Event configured;
     spawn(reader(&configured), "channel reader");
     co_await configured.wait();
     for (auto& sp : ex.shards)
@@ -1655,6 +1652,12 @@ static Task<void> run_main() {
     send_simple("ready");
     LOG_INFO("native executor %d ready: %zu shard(s), partition %d/%d, %d workers", g_opt.index, ex.shards.size(),
              g_opt.part, g_opt.parts, g_opt.workers);
+}
+
+// The coordinator closing the channel (or dying), or a signal, ends the executor — at any point, including
+// while it still waits for a shard's caches.
+static Task<void> shutdown_watch() {
+    Executor& ex = *g_ex;
     co_await ex.stop_ev.wait();
     long long echoes = 0, shard_events = 0, foreign = 0;
     for (auto& sp : ex.shards)
@@ -1664,8 +1667,8 @@ static Task<void> run_main() {
             foreign += sp->inf[k].foreign;
         }
     if (std::getenv("NCC_CPU_REPORT"))
-        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld", shard_events,
-                 echoes, foreign);
+        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu",
+                 shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()));
     if (std::getenv("NCC_CPU_REPORT"))
         LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld enqueues: object=%lld dependent=%lld "
                  "shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",
@@ -1771,6 +1774,7 @@ int main(int argc, char** argv) {
     }
     Channel chan(fd);
     g_chan = &chan;
+    spawn(shutdown_watch(), "shutdown");
     spawn(run_main(), "main");
     try {
         lp.run();

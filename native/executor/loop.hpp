@@ -202,10 +202,14 @@ public:
         Loop* loop;
         double until;
         bool await_ready() { return until <= now_s(); }
-        void await_suspend(std::coroutine_handle<> h) { loop->timers_.push(Timer{until, loop->seq_++, h}); }
+        void await_suspend(std::coroutine_handle<> h) { loop->timers_.push(Timer{until, loop->seq_++, h, {}}); }
         void await_resume() {}
     };
     SleepAwait sleep(double seconds) { return SleepAwait{this, now_s() + seconds}; }
+    // Run `fn` on the loop at (or after) time `at`.
+    void call_at(double at, std::function<void()> fn) { timers_.push(Timer{at, seq_++, {}, std::move(fn)}); }
+    // epoll_wait returns so far (idle-loop diagnostics: an executor with nothing to do must not wake up)
+    uint64_t wakeups() const { return wakeups_; }
 
     void post(std::coroutine_handle<> h) { ready_.push_back(h); }
     void call_soon(std::function<void()> fn) { calls_.push_back(std::move(fn)); }
@@ -238,6 +242,7 @@ public:
                 timeout_ms = dt <= 0 ? 0 : static_cast<int>(dt * 1000.0) + 1;
             }
             int n = epoll_wait(ep_, evs, 256, timeout_ms);
+            ++wakeups_;
             if (n < 0 && errno != EINTR) throw std::runtime_error("epoll_wait failed");
             for (int i = 0; i < n; ++i) {
                 auto it = fds_.find(evs[i].data.fd);
@@ -263,7 +268,11 @@ public:
             }
             now = now_s();
             while (!timers_.empty() && timers_.top().at <= now) {
-                ready_.push_back(timers_.top().h);
+                const Timer& t = timers_.top();
+                if (t.h)
+                    ready_.push_back(t.h);
+                else
+                    calls_.push_back(t.fn);
                 timers_.pop();
             }
         }
@@ -273,12 +282,14 @@ private:
     struct Timer {
         double at;
         uint64_t seq;
-        std::coroutine_handle<> h;
+        std::coroutine_handle<> h;  // resumed at `at`; or, when null,
+        std::function<void()> fn;   // called at `at`
         bool operator>(const Timer& o) const { return at != o.at ? at > o.at : seq > o.seq; }
     };
     int ep_;
     bool stopped_ = false;
     uint64_t seq_ = 0;
+    uint64_t wakeups_ = 0;
     std::unordered_map<int, FdState> fds_;
     std::deque<std::coroutine_handle<>> ready_;
     std::deque<std::function<void()>> calls_;
@@ -290,7 +301,7 @@ inline Loop& loop() { return *g_loop; }
 inline void g_loop_post(std::coroutine_handle<> h) { g_loop->post(h); }
 
 // ------------------------------------------------------------------------------------ Event
-// Level-triggered flag with waiters (asyncio.Event).
+// Level-triggered flag with waiters (asyncio.Event), optionally with a deadline (`wait_for`).
 class Event {
 public:
     bool is_set() const { return set_; }
@@ -298,6 +309,8 @@ public:
         set_ = true;
         for (auto h : waiters_) loop().post(h);
         waiters_.clear();
+        for (auto& w : timed_) w->fire(true);
+        timed_.clear();
     }
     void clear() { set_ = false; }
     struct Await {
@@ -308,9 +321,38 @@ public:
     };
     Await wait() { return Await{this}; }
 
+    // One waiter with a deadline: resumed once, by whichever comes first — set() (result true) or the
+    // deadline timer (false).  The timer holds the node until it fires, so nothing dangles either way.
+    struct TimedWaiter {
+        std::coroutine_handle<> h;
+        bool done = false, result = false;
+        void fire(bool r) {
+            if (done) return;
+            done = true;
+            result = r;
+            loop().post(h);
+        }
+    };
+    struct TimedAwait {
+        Event* ev;
+        double timeout;
+        std::shared_ptr<TimedWaiter> node = std::make_shared<TimedWaiter>();
+        bool await_ready() { return ev->set_ || timeout <= 0; }
+        void await_suspend(std::coroutine_handle<> h) {
+            node->h = h;
+            ev->timed_.push_back(node);
+            loop().call_at(now_s() + timeout, [n = node] { n->fire(false); });
+        }
+        bool await_resume() { return ev->set_ || node->result; }
+    };
+    // co_await ev.wait_for(seconds) -> whether the event is set (false: the deadline passed first).  No
+    // polling: the waiter sleeps until set() or its single deadline timer.
+    TimedAwait wait_for(double timeout) { return TimedAwait{this, timeout}; }
+
 private:
     bool set_ = false;
     std::vector<std::coroutine_handle<>> waiters_;
+    std::vector<std::shared_ptr<TimedWaiter>> timed_;
 };
 
 // ------------------------------------------------------------------------------------ spawn / when_all

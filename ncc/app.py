@@ -239,6 +239,8 @@ class App:
         self.relay = None  # coordinator: WatchRelay feeding the executors
         self.executor_impl = ""  # coordinator: "native" (ncc/bin/ncc-executor) or "python" shard executors
         self._cred_task = None
+        self.native_cfg = None  # coordinator with C++ executors: NativeExecutorConfig (renders their config)
+        self._relay_ok = False  # coordinator: the watch relay can run (decided once, in build)
         self.relay_feeds: list | None = None  # executor: per-kind feeds from the coordinator's relay
         self.standby_was_warm = False  # caches had synced before this replica acquired the Lease
         self.coord_part: tuple | None = None  # (p, C) when the coordinator role is split over C processes
@@ -263,6 +265,9 @@ class App:
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)
         self.client = client
+        # the watch relay needs the native extension and a transport that hands out raw watch lines: decided
+        # here, once, for both the sizing below and the choice of executor implementation
+        self._relay_ok = bool(cfg.watch_relay) and native_ext.load() is not None and hasattr(client, "watch_raw")
         self.factory = InformerFactory(client, cfg.controller_namespace, o.resync_period)
         all_names = [n for n, _ in discover(cfg.shard_config_path)]
         self._shard_files = shard_files(cfg.shard_config_path)
@@ -272,7 +277,7 @@ class App:
             if self.n_executors > 0:
                 o.role = "coordinator"
                 from .controller.native_executor import choose
-                native = choose(cfg, o, relay_active=cfg.watch_relay, quiet=True)[0]
+                native = choose(cfg, o, relay_active=self._relay_ok, quiet=True)[0]
                 self.per_shard = (cfg.executors_per_shard if cfg.executors_per_shard > 0
                                   else auto_sizing(self.n_executors, native=native)[0])
                 self.coord_part = coordinator_partition(cfg, self.n_executors, self.per_shard, native)
@@ -356,6 +361,8 @@ class App:
         if self.options.role == "coordinator":
             if self.pool is not None:
                 await self.pool.remove_shards(removed + changed)
+                if self.native_cfg is not None:
+                    self.native_cfg.forget(removed + changed)
                 self.pool.add_shards(added + changed)
             ctl.set_shard_names(sorted(now))
         else:
@@ -466,14 +473,12 @@ class App:
             await self.close()
 
     def _start_components(self, controller: Controller) -> None:
-        if self.options.role == "coordinator" and self.cfg.watch_relay and self.n_executors > 0:
-            from . import native as _native
-            if _native.load() is not None and hasattr(self.client, "watch_raw"):
-                from .controller.relay import KINDS, WatchRelay
-                infs = {R.TEMPLATES: controller.template_informer, R.WORKGROUPS: controller.workgroup_informer,
-                        R.SECRETS: controller.secret_informer, R.CONFIGMAPS: controller.configmap_informer}
-                self.relay = WatchRelay([infs[rt] for rt in KINDS], controller.template_informer.store,
-                                        self.cfg.controller_namespace)
+        if self.options.role == "coordinator" and self._relay_ok and self.n_executors > 0:
+            from .controller.relay import KINDS, WatchRelay
+            infs = {R.TEMPLATES: controller.template_informer, R.WORKGROUPS: controller.workgroup_informer,
+                    R.SECRETS: controller.secret_informer, R.CONFIGMAPS: controller.configmap_informer}
+            self.relay = WatchRelay([infs[rt] for rt in KINDS], controller.template_informer.store,
+                                    self.cfg.controller_namespace)
         for s in self.shards:
             s.start()
         if isinstance(self.recorder, BroadcastRecorder):
@@ -493,7 +498,7 @@ class App:
             self.executor_impl = "native" if use_native else "python"
             if not use_native:
                 log.debug("Python shard executors: %s", why)
-            native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
+            native_cfg = self.native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
             # One executor group per shard group serves every template key, whatever the number of coordinator
             # partitions: a shard apiserver then serves one executor's watches, not C of them
             # (profiles/r2/c_on_one_shard/: C executors on one shard cost it 12-25 %).

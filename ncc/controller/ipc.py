@@ -9,6 +9,7 @@ import msgpack
 
 _HDR = struct.Struct(">I")
 MAX_FRAME = 64 * 1024 * 1024
+FRAME_BUDGET = 16 * 1024 * 1024  # coalesce queued messages into frames of about this size at most
 
 
 class Channel:
@@ -39,15 +40,27 @@ class Channel:
         if not self._pending or self.writer.is_closing():
             self._pending.clear()
             return
-        n = len(self._pending)
+        pending, self._pending = self._pending, []
+        group, size = [], 0
+        for m in pending:  # one frame per FRAME_BUDGET bytes: a frame never approaches the MAX_FRAME cap
+            if group and size + len(m) > FRAME_BUDGET:
+                self._write_frame(group)
+                group, size = [], 0
+            group.append(m)
+            size += len(m)
+        self._write_frame(group)
+
+    def _write_frame(self, msgs: list) -> None:
+        n = len(msgs)
         batch = n > 1
         if batch:  # a msgpack array of the queued messages
             head = bytes((0x90 | n,)) if n < 16 else (b"\xdc" + n.to_bytes(2, "big") if n < 65536
                                                      else b"\xdd" + n.to_bytes(4, "big"))
-            body = head + b"".join(self._pending)
+            body = head + b"".join(msgs)
         else:
-            body = self._pending[0]
-        self._pending = []
+            body = msgs[0]
+        if len(body) > MAX_FRAME:
+            raise ValueError(f"message too large for one frame: {len(body)} bytes")
         self.writer.write(_HDR.pack(len(body) | (0x80000000 if batch else 0)) + body)
         self.sent += 1
 

@@ -58,6 +58,15 @@ def choose(cfg, options, relay_active: bool, quiet: bool = False) -> tuple[bool,
     return True, ""
 
 
+def _file_digest(path: str) -> str:
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return ""
+
+
 class NativeExecutorConfig:
     """Renders the `cfg` message of one executor and keeps exec-plugin tokens fresh."""
 
@@ -67,14 +76,29 @@ class NativeExecutorConfig:
         self.paths = dict(discover(cfg.shard_config_path))
         self.creds: dict[str, CredentialSource] = {}
         self.tokens: dict[str, str | None] = {}
+        self.digests: dict[str, str] = {}  # sha256 of the kubeconfig each cached CredentialSource came from
 
     def _source(self, name: str) -> CredentialSource:
+        """The shard's credentials, re-read when its kubeconfig file changed since they were loaded (a rotated
+        CA, server or client certificate must reach the next executor spawned for it)."""
+        self.paths = dict(discover(self.cfg.shard_config_path))
+        path = self.paths[name]
+        digest = _file_digest(path)
         src = self.creds.get(name)
-        if src is None:
-            self.paths = dict(discover(self.cfg.shard_config_path))
-            cc = load_kubeconfig(self.paths[name], name=name)
+        if src is None or self.digests.get(name) != digest:
+            cc = load_kubeconfig(path, name=name)
             src = self.creds[name] = CredentialSource(cc)
+            self.digests[name] = digest
+            self.tokens.pop(name, None)
         return src
+
+    def forget(self, names) -> None:
+        """Drop what is cached for shards that were removed or changed (App.reload_shards): their next
+        executor re-reads the kubeconfig, and the token refresher stops serving removed shards."""
+        for n in names:
+            self.creds.pop(n, None)
+            self.tokens.pop(n, None)
+            self.digests.pop(n, None)
 
     async def shard_entry(self, name: str) -> dict:
         src = self._source(name)

@@ -45,11 +45,12 @@ _DEP_INDEX = {2: "secret", 3: "configmap"}
 
 class RelayFeed:
     """Executor side: the queue an informer in relay mode consumes (`Informer.feed`)."""
-    __slots__ = ("_items", "_waiter")
+    __slots__ = ("_items", "_waiter", "partial")
 
     def __init__(self):
         self._items: deque = deque()
         self._waiter: asyncio.Future | None = None
+        self.partial: list = []  # lines of a chunked snapshot still arriving
 
     def put(self, what: str, lines: list) -> None:
         self._items.append((what, lines))
@@ -71,12 +72,39 @@ class RelayFeed:
 
 
 def deliver(feeds: list, msg: dict) -> bool:
-    """Executor side: hand a relay message to the feed of its kind; False if `msg` is no relay message."""
+    """Executor side: hand a relay message to the feed of its kind; False if `msg` is no relay message.  A
+    listing that came in chunks (all but the last with "more") is handed over whole, as one snapshot."""
     t = msg.get("t")
     if t not in ("s", "w"):
         return False
-    feeds[msg["k"]].put(t, msg["l"])
+    feed = feeds[msg["k"]]
+    if t == "s":
+        if msg.get("more"):
+            feed.partial.extend(msg["l"])
+            return True
+        if feed.partial:
+            lines, feed.partial = feed.partial + list(msg["l"]), []
+            feed.put("s", lines)
+            return True
+    feed.put(t, msg["l"])
     return True
+
+
+SNAPSHOT_CHUNK = 4 << 20  # bytes of watch lines per snapshot message (frames stay far below ipc.MAX_FRAME)
+
+
+def snapshot_messages(kind: int, lines: list, chunk: int | None = None) -> list:
+    """A listing as relay messages of at most ~`chunk` bytes each ("more" on all but the last)."""
+    chunk = SNAPSHOT_CHUNK if chunk is None else chunk
+    out, cur, size = [], [], 0
+    for line in lines:
+        if cur and size + len(line) > chunk:
+            out.append({"t": "s", "k": kind, "l": cur, "more": True})
+            cur, size = [], 0
+        cur.append(line)
+        size += len(line)
+    out.append({"t": "s", "k": kind, "l": cur})
+    return out
 
 
 class _Tap:
@@ -179,7 +207,8 @@ class WatchRelay:
         self.stats["snapshots"] += len(handles)
         lines = list(self.raw[kind].values())
         if self.parts <= 1 or self._mod is None:
-            self._send_all(handles, {"t": "s", "k": kind, "l": lines})
+            for msg in snapshot_messages(kind, lines):
+                self._send_all(handles, msg)
             return
         per: dict = {id(h): [] for h in handles}
         for line in lines:
@@ -191,7 +220,8 @@ class WatchRelay:
                 if mask == -1 or (mask >> h.part) & 1:
                     per[id(h)].append(line)
         for h in handles:
-            self._send(h, {"t": "s", "k": kind, "l": per[id(h)]})
+            for msg in snapshot_messages(kind, per[id(h)]):
+                self._send(h, msg)
 
     def on_lines(self, kind: int, lines: list) -> None:
         handles = self.handles

@@ -432,3 +432,34 @@ def test_every_implementation_is_exercised():
     """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
     if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
         assert binary_path() is not None
+
+
+async def test_chunked_relay_snapshot_and_frames(tmp_path, impl, monkeypatch):
+    """a listing larger than one IPC frame may hold goes to the executors in chunks ("more") and in
+    several frames; both executors reassemble it into one snapshot (forced here with tiny chunk and frame
+    budgets, so every line is its own message and every few messages their own frame)."""
+    if impl == "inprocess":
+        pytest.skip("no relay without executors")
+    from ncc.controller import ipc, relay
+    monkeypatch.setattr(relay, "SNAPSHOT_CHUNK", 256)
+    monkeypatch.setattr(ipc, "FRAME_BUDGET", 4096)
+    async with Cluster(tmp_path, impl) as cl:
+        for i in range(12):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        assert cl.app.relay is not None
+        for i in range(12):
+            await cl.ready(f"algo-{i:05d}")
+        assert all(s.count(R.SECRETS) == 12 and s.count(R.CONFIGMAPS) == 12 for s in cl.sstates)
+
+
+def test_snapshot_messages_and_deliver_reassemble():
+    from ncc.controller.relay import RelayFeed, deliver, snapshot_messages
+    lines = [b"x" * 100 for _ in range(10)]
+    msgs = snapshot_messages(2, lines, chunk=250)
+    assert [len(m["l"]) for m in msgs] == [2, 2, 2, 2, 2] and [bool(m.get("more")) for m in msgs] == [True] * 4 + [False]
+    feeds = [RelayFeed() for _ in range(4)]
+    for m in msgs:
+        assert deliver(feeds, m)
+    assert list(feeds[2]._items) == [("s", lines)] and feeds[2].partial == []
+    assert snapshot_messages(1, []) == [{"t": "s", "k": 1, "l": []}]

@@ -624,3 +624,32 @@ async def test_watch_relay_one_list_and_watch_per_kind_and_relist(tmp_path, impl
         await cc.close()
         await sc.close()
         await env.stop()
+
+
+async def test_reload_with_changed_kubeconfig_reaches_native_executor(tmp_path, monkeypatch):
+    """a shard whose kubeconfig changes (a rotated CA, a moved server) gets a C++ executor
+    configured from the *new* file — the coordinator's credential cache must not hand it the old one."""
+    import os
+    import shutil
+    from ncc.controller.native_executor import binary_path
+    if binary_path() is None:
+        pytest.skip("ncc/bin/ncc-executor is not built")
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+    env = await FakeEnvironment(2, str(tmp_path)).start()
+    cc = env.controller_client()
+    parked = os.path.join(str(tmp_path), "shard-1.kubeconfig.parked")
+    shutil.move(os.path.join(env.shard_dir, "shard-1.kubeconfig"), parked)
+    try:
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=[], configmaps=[]))
+        async with Running(env, "native", executor_impl="native", shard_reload_period=0) as app:
+            assert app.executor_impl == "native"
+            await wait_for(lambda: asyncio.sleep(0, env.shard_servers[0].state.count(R.TEMPLATES) == 1), timeout=10)
+            assert env.shard_servers[1].state.count(R.TEMPLATES) == 0
+            with open(os.path.join(env.shard_dir, "shard-0.kubeconfig"), "w") as f:
+                f.write(env.kubeconfig(env.shard_urls[1], "shard-0"))  # "shard-0" now lives on server 1
+            assert await app.reload_shards() == {"added": [], "removed": [], "changed": ["shard-0"]}
+            await wait_for(lambda: asyncio.sleep(0, env.shard_servers[1].state.count(R.TEMPLATES) == 1), timeout=15)
+            assert app.native_cfg.creds["shard-0"].cfg.server == env.shard_urls[1]
+    finally:
+        await cc.close()
+        await env.stop()

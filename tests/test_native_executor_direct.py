@@ -1,0 +1,124 @@
+"""The C++ shard executor (`ncc/bin/ncc-executor`) driven directly over its socketpair protocol
+(native/executor/executor.cpp header comment): no coordinator, the test plays it.
+
+* An idle executor whose shard is unreachable sleeps: it waits for the shard caches with a timed Event
+  wait (loop.hpp `Event::wait_for`), not a polling loop, so it makes no periodic wake-ups.
+* A pass over a template reports one typed failure per shard (ncc/controller/failures.py): a rogue shard
+  Secret comes back as {c: RogueResourceError, k: Secret, n: <name>, h: 0, m: <reference message>}.
+"""
+import asyncio
+import json
+import os
+import re
+import socket
+
+import pytest
+
+from ncc.api import resources as R
+from ncc.controller.ipc import Channel
+from ncc.controller.native_executor import binary_path
+from ncc.fakeapi.server import FakeApiServer
+from ncc.testing.workload import make_secret, make_template
+
+pytestmark = pytest.mark.skipif(binary_path() is None, reason="ncc/bin/ncc-executor is not built")
+NS = "nexus"
+
+
+def cfg(shards: list, **kw) -> dict:
+    doc = {"namespace": NS, "alias": "controller-cluster", "workers": 8, "pool_size": 8, "request_timeout": 5.0,
+           "coalesce_window": 0.0, "failure_base_delay": 0.05, "failure_max_delay": 0.2, "rate_limit_qps": 50,
+           "rate_limit_burst": 300, "shard_sync_timeout": 30.0, "full_resync_period": 0, "log_level": 30,
+           "shards": shards}
+    doc.update(kw)
+    return {"t": "cfg", "c": json.dumps(doc)}
+
+
+def line(obj: dict) -> bytes:
+    return json.dumps({"type": "ADDED", "object": obj}).encode()
+
+
+class Executor:
+    def __init__(self, config: dict, env: dict | None = None):
+        self.config, self.env = config, env
+
+    async def __aenter__(self):
+        parent, child = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        env = dict(os.environ, **(self.env or {}))
+        self.proc = await asyncio.create_subprocess_exec(
+            binary_path(), "--fd", str(child.fileno()), "--index", "0", "--part", "0/1", pass_fds=(child.fileno(),),
+            env=env, stderr=asyncio.subprocess.PIPE)
+        child.close()
+        reader, writer = await asyncio.open_connection(sock=parent)
+        self.ch = Channel(reader, writer)
+        self.ch.send(self.config)
+        return self
+
+    def snapshot(self, kind: int, objs: list) -> None:
+        self.ch.send({"t": "s", "k": kind, "l": [line(o) for o in objs]})
+
+    async def next_message(self, t: str, timeout: float = 10.0) -> dict:
+        async def go():
+            while True:
+                batch = await self.ch.recv()
+                assert batch is not None, "executor closed the channel"
+                for m in batch:
+                    if m.get("t") == t:
+                        return m
+        return await asyncio.wait_for(go(), timeout)
+
+    async def close(self) -> str:
+        self.ch.close()
+        _, err = await asyncio.wait_for(self.proc.communicate(), 10)
+        return err.decode(errors="replace")
+
+    async def __aexit__(self, *exc):
+        if self.proc.returncode is None:
+            self.proc.kill()
+            await self.proc.wait()
+
+
+async def test_idle_executor_with_unreachable_shard_does_not_poll():
+    with socket.socket() as s:  # a port nothing listens on
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    shard = {"name": "dead", "server": f"http://127.0.0.1:{port}"}
+    async with Executor(cfg([shard]), env={"NCC_CPU_REPORT": "1"}) as ex:
+        for k in range(4):
+            ex.snapshot(k, [])
+        # the controller side is synced; the executor now waits (up to 30 s) for the dead shard's caches
+        await asyncio.sleep(2.0)
+        assert ex.proc.returncode is None
+        err = await ex.close()
+    m = re.search(r"loop_wakeups=(\d+)", err)
+    assert m, err[-2000:]
+    # a 10 ms polling wait would have woken ~200 times in 2 s; the reflectors' reconnect backoff (0.8 s, 1.6 s...
+    # for 4 informers) accounts for a handful
+    print(m.group(0))
+    assert int(m.group(1)) < 60, m.group(0)
+
+
+async def test_rogue_dependent_report_is_typed():
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        rogue = make_secret("s0", NS, version=3)
+        srv.state.create(R.SECRETS, NS, rogue)
+        tpl = make_template(0, NS, secrets=["s0"])
+        tpl["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        sec = make_secret("s0", NS)
+        sec["metadata"].update(uid="u-s", resourceVersion="11")
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, [tpl]), (1, []), (2, [sec]), (3, [])):
+                ex.snapshot(k, objs)
+            await ex.next_message("ready")
+            rep = await ex.next_message("report")
+            assert rep["k"] == "template/nexus/algo-00000" and rep["u"] == "u-0" and rep["g"] == 1
+            f = rep["r"]["shard-0"]
+            assert f == {"c": "RogueResourceError", "k": "Secret", "n": "s0", "h": 0,
+                         "m": 'Resource "s0" already exists and is not managed by any Machine Learning Algorithm'}
+            assert srv.state.get(R.SECRETS, NS, "s0")["data"] == rogue["data"]  # refused, not overwritten
+            # the shard template itself was written: only the dependent failed
+            assert srv.state.get(R.TEMPLATES, NS, "algo-00000")["spec"] == tpl["spec"]
+            await ex.close()
+    finally:
+        await srv.stop()
