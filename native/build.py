@@ -39,11 +39,13 @@ def executor_path() -> str:
     return os.path.join(ROOT, "ncc", "bin", "ncc-executor")
 
 
-def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False, out: str | None = None) -> str:
+def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False, out: str | None = None,
+                   coverage: bool = False) -> str:
     """The native shard executor (one translation unit; headers alongside); `out` overrides the in-tree
-    path (setup.py builds it into the wheel's ncc/bin/)."""
+    path (setup.py builds it into the wheel's ncc/bin/).  `coverage`: gcov instrumentation (the executor
+    flushes its counters on exit; scripts/cpp_coverage.py gates the line coverage)."""
     out = out or executor_path()
-    flavor = "sanitize" if sanitize else ("debug" if debug else "release")
+    flavor = "coverage" if coverage else ("sanitize" if sanitize else ("debug" if debug else "release"))
     stamp = out + ".flavor"
     sources = [os.path.join(EXECUTOR_DIR, f) for f in sorted(os.listdir(EXECUTOR_DIR))
                if f.endswith((".cpp", ".hpp"))]
@@ -55,7 +57,9 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
     flags = ["-std=c++20", "-fcoroutines", "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"] + _werror()
-    if debug or sanitize:
+    if coverage:
+        flags += ["-O0", "--coverage", "-DNCC_COVERAGE", "-DNCC_SYSTEM_MALLOC"]
+    elif debug or sanitize:
         flags += ["-O1", "-fno-omit-frame-pointer"]
     else:
         flags += ["-O2", "-DNDEBUG"]
@@ -126,6 +130,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--sanitize", action="store_true")
+    ap.add_argument("--executor-coverage", action="store_true",
+                    help="rebuild only ncc/bin/ncc-executor with gcov instrumentation (scripts/cpp_coverage.py)")
     a = ap.parse_args()
+    if a.executor_coverage:
+        print(build_executor(coverage=True, verbose=True))
+        sys.exit(0)
     print(build(a.debug, a.sanitize, verbose=True))
     sys.exit(0)

@@ -49,6 +49,9 @@
 #ifdef NCC_GPROF
 extern "C" void _mcleanup(void);
 #endif
+#ifdef NCC_COVERAGE
+extern "C" void __gcov_dump(void);
+#endif
 
 #ifndef NCC_SYSTEM_MALLOC
 #include "alloc.hpp"
@@ -1785,6 +1788,9 @@ int main(int argc, char** argv) {
     std::fflush(stderr);
 #ifdef NCC_GPROF
     _mcleanup();  // profiling builds (-pg): write gmon.out before skipping the exit handlers
+#endif
+#ifdef NCC_COVERAGE
+    __gcov_dump();  // coverage builds: write the .gcda counters before skipping the exit handlers
 #endif
     std::_Exit(0);  // skip destructors of still-suspended coroutines
 }
