@@ -68,6 +68,9 @@ def parse_args(argv=None):
                    help="every apiserver serves HTTPS with x509 client auth (throwaway CA), as kind/EKS clusters do")
     p.add_argument("--shards-per-rank", type=int, default=1,
                    help="experiments only: shard apiservers hosted per rank (the driver contract is 1)")
+    p.add_argument("--stages", action="store_true",
+                   help="trace where each object's latency goes (controller commit -> coordinator relay -> "
+                        "executor receive -> executor dequeue -> shard commit) and report p50/p99 per stage")
     return p.parse_args(argv)
 
 
@@ -246,6 +249,81 @@ def pct(xs, q):
     return xs[k]
 
 
+# ------------------------------------------------------------------ latency stages (--stages)
+KIND_INDEX = {"nexusalgorithmtemplates": 0, "secrets": 2, "configmaps": 3}
+STAGES = ("relay", "ipc", "queue", "write")
+
+
+def _first_at_or_after(ts: list, t: int):
+    import bisect
+    i = bisect.bisect_left(ts, t)
+    return ts[i] if i < len(ts) else None
+
+
+def stage_breakdown(trace_dir: str, ctrl_times: list, shard_waves: list) -> dict | None:
+    """Per object of the timed waves on shard 0: controller commit -> coordinator relay (`relay`) -> executor
+    receive (`ipc`) -> executor worker dequeue of the owning template key (`queue`: coalescing and work-queue
+    wait) -> shard commit (`write`: the pass up to the shard apiserver committing the object).  p50/p99 per
+    stage, and the mean stage split of the slowest 1 % of objects (who owns the p99)."""
+    import glob as _glob
+    relay: dict = {}
+    recv: dict = {}
+    deq: dict = {}
+    for f in _glob.glob(os.path.join(trace_dir, "relay-*.tsv")):
+        with open(f) as fh:
+            for ln in fh:
+                k, key, t = ln.rstrip("\n").split("\t")
+                relay.setdefault((int(k), key), []).append(int(t))
+    ex_files = sorted(_glob.glob(os.path.join(trace_dir, "executor-0-*.tsv")))
+    if not relay or not ex_files:
+        return None
+    for f in ex_files:
+        with open(f) as fh:
+            for ln in fh:
+                w, k, key, t = ln.rstrip("\n").split("\t")
+                if w == "r":
+                    recv.setdefault((int(k), key), []).append(int(t))
+                else:
+                    deq.setdefault(key, []).append(int(t))
+    for dct in (relay, recv, deq):
+        for v in dct.values():
+            v.sort()
+    rows = []
+    for ctrl, wave in zip(ctrl_times, shard_waves):
+        for marker, objs in wave.items():
+            plural = marker.split("=", 1)[0]
+            kind = KIND_INDEX.get(plural)
+            if kind is None:
+                continue
+            c = ctrl[marker]
+            for k, t_s in objs.items():
+                key = k.split(":", 1)[-1]
+                t_c = c.get(key)
+                if t_c is None:
+                    continue
+                t_r = _first_at_or_after(relay.get((kind, key), []), t_c)
+                t_e = _first_at_or_after(recv.get((kind, key), []), t_r if t_r is not None else t_c)
+                name = key.split("/", 1)[-1]
+                owner = name if kind == 0 else name.rsplit("-", 1)[0]  # workload: <template>-secret/-config
+                t_q = _first_at_or_after(deq.get(f"template/{key.split('/', 1)[0]}/{owner}", []),
+                                         t_e if t_e is not None else t_c)
+                if None in (t_r, t_e, t_q) or not (t_c <= t_r <= t_e <= t_q <= t_s):
+                    continue
+                rows.append((t_s - t_c, t_r - t_c, t_e - t_r, t_q - t_e, t_s - t_q))
+    if not rows:
+        return None
+    out = {"objects": len(rows)}
+    for i, name in enumerate(("total",) + STAGES):
+        xs = [r[i] / 1e6 for r in rows]
+        out[name] = {"p50_ms": round(pct(xs, 50), 2), "p99_ms": round(pct(xs, 99), 2)}
+    rows.sort()
+    tail = rows[-max(1, len(rows) // 100):]
+    out["p99_tail_mean_ms"] = {name: round(sum(r[i + 1] for r in tail) / len(tail) / 1e6, 2)
+                               for i, name in enumerate(STAGES)}
+    out["p99_owner"] = max(out["p99_tail_mean_ms"], key=out["p99_tail_mean_ms"].get)
+    return out
+
+
 # ------------------------------------------------------------------ main
 async def run(args, d: Dist) -> dict | None:
     import aiohttp
@@ -311,6 +389,9 @@ async def run(args, d: Dist) -> dict | None:
                     k, _, v = kv.partition("=")
                     env[k] = v
                 env["NCC_TOPOLOGY_FILE"] = os.path.join(work, "topology.json")
+                if args.stages:
+                    env["NCC_TRACE_STAGES"] = os.path.join(work, "trace")
+                    os.makedirs(env["NCC_TRACE_STAGES"], exist_ok=True)
                 log = open(os.path.join(work, "controller.log"), "wb")
                 t_boot = time.time_ns()
                 controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=log,
@@ -426,6 +507,14 @@ async def run(args, d: Dist) -> dict | None:
                         lat.extend((t - c[k.split(":", 1)[-1]]) / 1e6 for k, t in objs.items())
             objs = args.steps * 3 * T * d.world * S
             value = objs / elapsed
+            stages = None
+            if args.stages:
+                controller.terminate()  # the relay and the executors write their traces on shutdown
+                try:
+                    controller.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    pass
+                stages = stage_breakdown(os.path.join(work, "trace"), ctrl_times, all_times[0])
             # controller CPU (coordinator + every executor, all on rank 0) per synced object over the timed
             # waves: the cost of the system under test, independent of how fast the fake apiservers are
             ctl_cpu = {k: cpu1.get(k, 0.0) - cpu0.get(k, 0.0) for k in ("coordinator", "executors")}
@@ -471,6 +560,7 @@ async def run(args, d: Dist) -> dict | None:
                                                                                  for u in utils)}),
                 "rss_mib": dict(rsses[0], **{"shard-apiserver-max": max(r.get("shard-apiserver", 0.0)
                                                                        for r in rsses)}),
+                **({"stages": stages} if stages is not None else {}),
             }
     finally:
         for p in reversed(procs):

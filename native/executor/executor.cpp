@@ -32,10 +32,12 @@
 // triggering a write loop.
 #include <fcntl.h>
 #include <sys/resource.h>
+#include <sys/stat.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <csignal>
 #include <optional>
 #include <cstdarg>
@@ -652,6 +654,34 @@ struct Shard {
 };
 
 static double kDependentHold = 5.0;  // NCC_DEPENDENT_HOLD overrides
+
+// NCC_TRACE_STAGES=<dir>: wall-clock times of every relayed controller object received ("r", kind) and of
+// every key a worker dequeues ("q"), written to <dir>/executor-<index>.tsv on exit (bench.py --stages)
+struct TraceRec {
+    char what;
+    int kind;
+    std::string key;
+    long long t_ns;
+};
+static std::vector<TraceRec>* g_trace = nullptr;
+static long long wall_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+static void trace(char what, int kind, const std::string& key) {
+    if (g_trace != nullptr) g_trace->push_back(TraceRec{what, kind, key, wall_ns()});
+}
+static void dump_trace() {
+    const char* dir = std::getenv("NCC_TRACE_STAGES");
+    if (g_trace == nullptr || dir == nullptr) return;
+    ::mkdir(dir, 0755);
+    std::string path = std::string(dir) + "/executor-" + std::to_string(g_opt.index) + "-" + std::to_string(getpid()) +
+                       ".tsv";
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (f == nullptr) return;
+    for (const auto& r : *g_trace) std::fprintf(f, "%c\t%d\t%s\t%lld\n", r.what, r.kind, r.key.c_str(), r.t_ns);
+    std::fclose(f);
+}
 // enqueues by cause (NCC_CPU_REPORT diagnostics): template/workgroup event, dependent event, shard-side
 // template drift, shard-side dependent drift, failure retry, orphan sweep, full resync, delete
 enum EnqCause { ENQ_OBJECT, ENQ_DEPENDENT, ENQ_SHARD_OBJECT, ENQ_SHARD_DEPENDENT, ENQ_RETRY, ENQ_SWEEP, ENQ_RESYNC,
@@ -746,6 +776,7 @@ static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
         return;
     }
     store[key] = cur;
+    trace('r', kind, key);
     if (kind == TEMPLATES) index_template(old, cur);
     if (kind >= 2) ex.needed.erase(key);
     on_ctl_event(kind, old, cur, false);
@@ -1438,6 +1469,7 @@ static Task<void> worker() {
     while (true) {
         std::string key = co_await ex.queue.get();
         if (key.empty()) co_return;
+        trace('q', 0, key);
         size_t a = key.find('/');
         size_t b = key.find('/', a + 1);
         std::string kind = key.substr(0, a), ns = key.substr(a + 1, b - a - 1), name = key.substr(b + 1);
@@ -1679,6 +1711,7 @@ static Task<void> shutdown_watch() {
                  g_enq[ENQ_SHARD_OBJECT], g_enq[ENQ_SHARD_DEPENDENT], g_enq[ENQ_RETRY], g_enq[ENQ_SWEEP],
                  g_enq[ENQ_RESYNC], g_enq[ENQ_DELETE]);
     ex.queue.shutdown();
+    dump_trace();
     co_await g_chan->drain(2.0);
     loop().stop();
 }
@@ -1762,6 +1795,10 @@ int main(int argc, char** argv) {
         }
     }
     if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
+    if (std::getenv("NCC_TRACE_STAGES") != nullptr) {
+        g_trace = new std::vector<TraceRec>();
+        g_trace->reserve(1 << 20);
+    }
     const char* gated = std::getenv("NCC_GATED");
     g_opt.gated = gated != nullptr && std::string(gated) == "1";
     ::signal(SIGPIPE, SIG_IGN);

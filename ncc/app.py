@@ -561,6 +561,8 @@ class App:
             await self.partitions.stop()
         if self.pool is not None:
             await self.pool.stop()
+        if self.relay is not None:
+            self.relay.dump_trace()
         if isinstance(self.recorder, BroadcastRecorder):
             await self.recorder.stop()
         await self.factory.stop()

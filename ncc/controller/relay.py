@@ -28,6 +28,8 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
+import time
 from collections import deque
 
 import msgpack
@@ -138,6 +140,9 @@ class WatchRelay:
         self._by_part: dict[int, list] = {}
         self._mod = _native.load()
         self.stats = {"lines_in": 0, "lines_out": 0, "snapshots": 0, "frames": 0}
+        # NCC_TRACE_STAGES=<dir>: record when each watch line was relayed (bench.py --stages joins it with the
+        # apiservers' commit times and the executors' receive/dequeue times: where does an object's latency go?)
+        self.trace: list | None = [] if os.environ.get("NCC_TRACE_STAGES") else None
         for k, inf in enumerate(informers):
             inf.tap = _Tap(self, k)
 
@@ -232,6 +237,12 @@ class WatchRelay:
         scan = mod.relay_scan
         parts, ns = self.parts, self.namespace
         self.stats["lines_in"] += len(lines)
+        if self.trace is not None:
+            now = time.time_ns()
+            for line in lines:
+                sc = scan(line, 1, ns)
+                if sc is not None and sc[0] < 2:
+                    self.trace.append((kind, sc[1], sc[2], now))
         if parts <= 1:
             keep = []
             for line in lines:
@@ -277,6 +288,16 @@ class WatchRelay:
         for h, ls in per.values():
             self._send(h, {"t": "w", "k": kind, "l": ls})
             self.stats["lines_out"] += len(ls)
+
+    def dump_trace(self) -> None:
+        """Write the relay trace (kind, namespace, name, wall-clock ns per relayed line) under NCC_TRACE_STAGES."""
+        d = os.environ.get("NCC_TRACE_STAGES")
+        if not d or self.trace is None:
+            return
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"relay-{os.getpid()}.tsv"), "w") as f:
+            for kind, ns, name, t in self.trace:
+                f.write(f"{kind}\t{ns}/{name}\t{t}\n")
 
     def _send_all(self, handles: list, msg: dict) -> None:
         """One encoding of `msg` for every executor it goes to."""
