@@ -570,6 +570,8 @@ public:
         }
     }
     size_t length() const { return queue_.size(); }
+    // a pass over `key` is pending (added while queued or processing): the next one will see the latest state
+    bool dirty(const std::string& key) const { return dirty_.count(key) > 0 && !shutdown_; }
     void shutdown() {
         shutdown_ = true;
         for (auto h : getters_) loop().post(h);
@@ -707,7 +709,8 @@ struct Executor {
     Event stop_ev;
     std::unordered_map<std::string, double> needed;  // dependent keys asked from the coordinator
     std::vector<CtlPtr> partial_snapshot[4];          // chunks of a listing still arriving (per kind)
-    long long stats_reconciles = 0, stats_errors = 0, stats_writes = 0;
+    long long stats_reconciles = 0, stats_errors = 0, stats_writes = 0, stats_reports_skipped = 0;
+    std::unordered_set<std::string> carry_wrote;  // keys whose unreported (superseded) pass wrote
 
     CtlPtr cget(int k, const std::string& key) const {
         auto it = ctl[k].find(key);
@@ -1213,6 +1216,10 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
 static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep,
                                        PassState* pass);
 
+static Task<void> update_crd(Shard* shp, int kind, ShardPtr cur, CtlPtr want, PassState* pass) {
+    co_await write_crd(*shp, kind, cur, *want, pass);
+}
+
 // syncSecretsToShard / syncConfigMapsToShard for one dependent: a failure is tagged with the dependent, so the
 // coordinator can record the reference's Warning Events for it (controller.go:497,525-557,587-619)
 static Task<void> sync_dependent(Shard* shp, int kind, CtlPtr tpl, ShardPtr st, std::string dep, PassState* pass) {
@@ -1332,8 +1339,14 @@ static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass
     if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
     std::string key = key_of(tpl->ns, tpl->name);
     ShardPtr st = sh.get(TEMPLATES, key);
-    if (!st || !spec_in_sync(sh, TEMPLATES, *st, tpl->fp_spec)) st = co_await write_crd(sh, TEMPLATES, st, *tpl, pass);
     std::vector<Task<void>> jobs;
+    if (!st) {
+        st = co_await write_crd(sh, TEMPLATES, st, *tpl, pass);  // the dependents' ownerRefs need its UID
+    } else if (!spec_in_sync(sh, TEMPLATES, *st, tpl->fp_spec)) {
+        // an update keeps the shard template's UID: its dependents go out alongside it, not one round trip
+        // later (the reference's loop is strictly sequential, controller.go:790-831)
+        jobs.push_back(update_crd(shp, TEMPLATES, st, tpl, pass));
+    }
     for (const auto& n : tpl->secrets) jobs.push_back(sync_dependent(shp, SECRETS, tpl, st, n, pass));
     for (const auto& n : tpl->configmaps) jobs.push_back(sync_dependent(shp, CONFIGMAPS, tpl, st, n, pass));
     auto errs = co_await when_all(std::move(jobs));
@@ -1447,6 +1460,18 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
         jobs.push_back(kind == TEMPLATES ? sync_template_to_shard(sp.get(), obj, &pass)
                                          : sync_workgroup_to_shard(sp.get(), obj, &pass));
     auto errs = co_await when_all(std::move(jobs));
+    std::string qkey = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key;
+    if (ex.queue.dirty(qkey)) {
+        // a newer version (or a dependent) re-queued the key while this pass ran: the next pass reports on
+        // the version it sees, carrying this pass's writes — a report on a version the coordinator may already
+        // have moved past would only cost it a fold and a superseded finish
+        if (pass.wrote) ex.carry_wrote.insert(qkey);
+        ++ex.stats_reports_skipped;
+        for (auto& e : errs)
+            if (e) std::rethrow_exception(e);
+        co_return;
+    }
+    if (ex.carry_wrote.erase(qkey) > 0) pass.wrote = true;
     std::vector<std::pair<std::string, std::optional<Failure>>> results;
     bool failed = false;
     std::string first;
@@ -1460,7 +1485,7 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
         }
         results.emplace_back(ex.shards[i]->name, std::move(f));
     }
-    report(std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key, *obj, results, pass.wrote);
+    report(qkey, *obj, results, pass.wrote);
     if (failed) throw NamedError("ShardSyncError", first);
 }
 
@@ -1705,9 +1730,10 @@ static Task<void> shutdown_watch() {
         LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu",
                  shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()));
     if (std::getenv("NCC_CPU_REPORT"))
-        LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld enqueues: object=%lld dependent=%lld "
-                 "shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",
-                 ex.stats_reconciles, ex.stats_writes, ex.stats_errors, g_enq[ENQ_OBJECT], g_enq[ENQ_DEPENDENT],
+        LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld reports_skipped=%lld enqueues: object=%lld "
+                 "dependent=%lld shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",
+                 ex.stats_reconciles, ex.stats_writes, ex.stats_errors, ex.stats_reports_skipped, g_enq[ENQ_OBJECT],
+                 g_enq[ENQ_DEPENDENT],
                  g_enq[ENQ_SHARD_OBJECT], g_enq[ENQ_SHARD_DEPENDENT], g_enq[ENQ_RETRY], g_enq[ENQ_SWEEP],
                  g_enq[ENQ_RESYNC], g_enq[ENQ_DELETE]);
     ex.queue.shutdown();

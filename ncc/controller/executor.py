@@ -25,7 +25,7 @@ import socket
 import sys
 import zlib
 
-from .ipc import Channel
+from .ipc import Channel, RawChannel
 from .relay import deliver
 from ..aio import wait_timeout
 
@@ -130,8 +130,13 @@ class ExecutorHandle:
             env.pop("NCC_GATED", None)
         self.proc = await asyncio.create_subprocess_exec(program, *args, pass_fds=(child.fileno(),), env=env)
         child.close()
-        reader, writer = await asyncio.open_connection(sock=parent)
-        self.channel = Channel(reader, writer)
+        if self.on_stream is not None:
+            # reports are folded natively straight off the socket (no stream reader, no task wake-up per frame)
+            self._eof = asyncio.Event()
+            self.channel = RawChannel(parent, self._fold, self._dispatch, self._eof.set)
+        else:
+            reader, writer = await asyncio.open_connection(sock=parent)
+            self.channel = Channel(reader, writer)
         if first is not None:
             self.channel.send(first)
         if gated and self.gate_open:  # the gate opened while this child was being spawned
@@ -162,27 +167,14 @@ class ExecutorHandle:
             self.ready.clear()
             self.synced.clear()
             await self._spawn()
-            while True:
-                if self.on_stream is not None:
-                    batch = await self.channel.recv_folded(self._fold)
-                    if batch is None:
-                        break
-                else:
+            if isinstance(self.channel, RawChannel):
+                await self._eof.wait()  # messages are dispatched from the channel's read callback
+            else:
+                while True:
                     batch = await self.channel.recv()
                     if batch is None:
                         break
-                for msg in batch:
-                    t = msg.get("t")
-                    if t == "ready":
-                        self.ready.set()
-                        self.synced.set()
-                    elif t == "synced":
-                        self.synced.set()
-                    elif t == "need":
-                        if self.on_need is not None:
-                            self.on_need(self, msg)
-                        continue
-                    self.on_message(self.index, msg)
+                    self._dispatch(batch)
             if self.on_exit is not None:
                 self.on_exit(self)
             rc = await self.proc.wait()
@@ -194,6 +186,22 @@ class ExecutorHandle:
                       rc, backoff)
             await asyncio.sleep(backoff)
             backoff = min(backoff * 2, 30.0)
+
+    def _dispatch(self, batch: list) -> None:
+        for msg in batch:
+            if not isinstance(msg, dict):
+                continue
+            t = msg.get("t")
+            if t == "ready":
+                self.ready.set()
+                self.synced.set()
+            elif t == "synced":
+                self.synced.set()
+            elif t == "need":
+                if self.on_need is not None:
+                    self.on_need(self, msg)
+                continue
+            self.on_message(self.index, msg)
 
     def _fold(self, buf, start: int):
         return self.on_stream(self.index, buf, start)

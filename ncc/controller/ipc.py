@@ -12,6 +12,178 @@ MAX_FRAME = 64 * 1024 * 1024
 FRAME_BUDGET = 16 * 1024 * 1024  # coalesce queued messages into frames of about this size at most
 
 
+def frames(msgs: list):
+    """Encoded messages → framed bytes: one frame per FRAME_BUDGET bytes of messages (a msgpack array when it
+    holds several), so a frame never approaches the MAX_FRAME cap."""
+    group, size = [], 0
+    for m in msgs:
+        if group and size + len(m) > FRAME_BUDGET:
+            yield _frame(group)
+            group, size = [], 0
+        group.append(m)
+        size += len(m)
+    if group:
+        yield _frame(group)
+
+
+def _frame(msgs: list) -> bytes:
+    n = len(msgs)
+    batch = n > 1
+    if batch:  # a msgpack array of the queued messages
+        head = bytes((0x90 | n,)) if n < 16 else (b"\xdc" + n.to_bytes(2, "big") if n < 65536
+                                                 else b"\xdd" + n.to_bytes(4, "big"))
+        body = head + b"".join(msgs)
+    else:
+        body = msgs[0]
+    if len(body) > MAX_FRAME:
+        raise ValueError(f"message too large for one frame: {len(body)} bytes")
+    return _HDR.pack(len(body) | (0x80000000 if batch else 0)) + body
+
+
+class RawChannel:
+    """The coordinator's end of an executor socketpair, without asyncio streams.
+
+    Executors report after every pass; at 8 shards the coordinator takes in tens of thousands of small
+    frames per second.  Through a StreamReader each read costs a protocol callback, a buffer copy, a reader
+    task wake-up and a resume.  Here the socket's readability callback reads what has arrived and hands it
+    straight to `fold(buffer, start) -> (other messages, end)` (the native report table parses the framing
+    and folds the reports in place); `on_messages(list)` gets whatever it did not fold, `on_eof()` the end
+    of the stream.  Writes use the same frames as `Channel`, sent from the loop directly (the relay's lines,
+    `go`/`resync`/`cred`), buffered only while the socket is full."""
+
+    def __init__(self, sock, fold, on_messages, on_eof):
+        sock.setblocking(False)
+        self.sock = sock
+        self._fd = sock.fileno()
+        self._loop = asyncio.get_running_loop()
+        self._fold, self._on_messages, self._on_eof = fold, on_messages, on_eof
+        self._rbuf = bytearray()
+        self._rpos = 0
+        self._pending: list = []
+        self._flush_handle: asyncio.Handle | None = None
+        self._out = bytearray()
+        self._writing = False
+        self._drained: asyncio.Future | None = None
+        self._closed = False
+        self.sent = 0
+        self.received = 0
+        self._loop.add_reader(self._fd, self._on_readable)
+
+    # ------------------------------------------------------------------ read side
+    def _on_readable(self) -> None:
+        try:
+            data = self.sock.recv(1 << 18)
+        except (BlockingIOError, InterruptedError):
+            return
+        except OSError:
+            data = b""
+        if not data:
+            self._eof()
+            return
+        self.received += 1
+        if self._rpos < len(self._rbuf):  # a partial frame is waiting
+            self._rbuf += data
+            src, start = self._rbuf, self._rpos
+        else:
+            src, start = data, 0
+        try:
+            msgs, end = self._fold(src, start)
+        except Exception:  # noqa: BLE001 — a corrupt stream: drop the executor (the handle restarts it)
+            import logging
+            logging.getLogger("ncc.ipc").exception("bad frame from a shard executor; closing its channel")
+            self._eof()
+            return
+        if end >= len(src):
+            self._rbuf, self._rpos = bytearray(), 0
+        elif src is data:
+            self._rbuf, self._rpos = bytearray(data[end:]), 0
+        elif end > (1 << 16):
+            del self._rbuf[:end]
+            self._rpos = 0
+        else:
+            self._rpos = end
+        if msgs:
+            self._on_messages(msgs)
+
+    def _eof(self) -> None:
+        if self._closed:
+            return
+        self.close()
+        self._on_eof()
+
+    # ------------------------------------------------------------------ write side
+    def send(self, msg) -> None:
+        self.send_packed(msgpack.packb(msg, use_bin_type=True))
+
+    def send_packed(self, packed: bytes) -> None:
+        if self._closed:
+            return
+        self._pending.append(packed)
+        if self._flush_handle is None:
+            self._flush_handle = self._loop.call_soon(self._flush)
+
+    def _flush(self) -> None:
+        self._flush_handle = None
+        if self._closed or not self._pending:
+            self._pending.clear()
+            return
+        pending, self._pending = self._pending, []
+        for frame in frames(pending):
+            self._out += frame
+            self.sent += 1
+        self._write()
+
+    def _write(self) -> None:
+        while self._out:
+            try:
+                n = self.sock.send(self._out)
+            except (BlockingIOError, InterruptedError):
+                break
+            except OSError:
+                self._out.clear()
+                self._eof()
+                return
+            del self._out[:n]
+        if self._out and not self._writing:
+            self._writing = True
+            self._loop.add_writer(self._fd, self._on_writable)
+        elif not self._out:
+            if self._writing:
+                self._writing = False
+                self._loop.remove_writer(self._fd)
+            if self._drained is not None and not self._drained.done():
+                self._drained.set_result(None)
+
+    def _on_writable(self) -> None:
+        self._write()
+
+    async def drain(self) -> None:
+        self._flush()
+        if self._out and not self._closed:
+            self._drained = self._loop.create_future()
+            await self._drained
+
+    def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        if self._flush_handle is not None:
+            self._flush_handle.cancel()
+            self._flush_handle = None
+        try:
+            self._loop.remove_reader(self._fd)
+            if self._writing:
+                self._loop.remove_writer(self._fd)
+        except (ValueError, OSError):
+            pass
+        if self._drained is not None and not self._drained.done():
+            self._drained.set_result(None)
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
 class Channel:
     def __init__(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
         self.reader = reader
@@ -41,28 +213,9 @@ class Channel:
             self._pending.clear()
             return
         pending, self._pending = self._pending, []
-        group, size = [], 0
-        for m in pending:  # one frame per FRAME_BUDGET bytes: a frame never approaches the MAX_FRAME cap
-            if group and size + len(m) > FRAME_BUDGET:
-                self._write_frame(group)
-                group, size = [], 0
-            group.append(m)
-            size += len(m)
-        self._write_frame(group)
-
-    def _write_frame(self, msgs: list) -> None:
-        n = len(msgs)
-        batch = n > 1
-        if batch:  # a msgpack array of the queued messages
-            head = bytes((0x90 | n,)) if n < 16 else (b"\xdc" + n.to_bytes(2, "big") if n < 65536
-                                                     else b"\xdd" + n.to_bytes(4, "big"))
-            body = head + b"".join(msgs)
-        else:
-            body = msgs[0]
-        if len(body) > MAX_FRAME:
-            raise ValueError(f"message too large for one frame: {len(body)} bytes")
-        self.writer.write(_HDR.pack(len(body) | (0x80000000 if batch else 0)) + body)
-        self.sent += 1
+        for frame in frames(pending):
+            self.writer.write(frame)
+            self.sent += 1
 
     async def drain(self) -> None:
         self._flush()

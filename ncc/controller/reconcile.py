@@ -518,24 +518,33 @@ class ReconcileMixin:
         name = meta(template).get("name", "")
         spec = template.get("spec")
         shard_template = shard.template_lister.try_get(ns, name)
+        update = None
         if self.options.server_side_apply:
             if shard_template is None or not spec_matches(spec, shard_template, spec_fp):
                 self._pass_wrote()
                 shard_template = await shard.apply_template(name, ns, spec, C.FIELD_MANAGER)
         elif shard_template is not None and not spec_matches(spec, shard_template, spec_fp):
             log.debug("Content changed for NexusAlgorithmTemplate %s, updating", name)
-            shard_template = await self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
-                                               shard_template, spec, C.FIELD_MANAGER)
+            update = self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
+                                 shard_template, spec, C.FIELD_MANAGER)
+            if not self.options.concurrent_dependents:
+                shard_template = await update
+                update = None
+            # native: an update keeps the shard template's UID, so its dependents go out alongside it
+            # instead of one round trip later (controller.go:790-831 is strictly sequential)
         elif shard_template is None:
             log.debug("Algorithm %s not found in shard %s, creating", name, shard.name)
             shard_template = await self._write(shard, "create_template", shard.template_informer, R.TEMPLATES,
                                                name, ns, spec, C.FIELD_MANAGER)
         if self.options.concurrent_dependents:
             # dependents need the shard template's UID for their ownerRefs, so they go after it — all at once
-            holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) else shard_template
+            holder = template if (update is not None or SLIM_FP in shard_template or shard_template.get("spec") is None) \
+                else shard_template  # a shard template still being updated carries the old references
             secrets, configmaps = dependent_names(holder)
             jobs = [self._sync_dependent(R.SECRETS, template, shard_template, shard, n) for n in secrets]
             jobs += [self._sync_dependent(R.CONFIGMAPS, template, shard_template, shard, n) for n in configmaps]
+            if update is not None:
+                jobs.insert(0, update)
             for r in await gather_all(jobs):
                 if isinstance(r, BaseException):
                     raise r
