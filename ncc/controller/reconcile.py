@@ -490,10 +490,12 @@ class ReconcileMixin:
             return False
         # report_template_synced_condition would leave the status as it is (no write) exactly when the Ready
         # condition and the three synced lists already hold what it would set.  That depends only on the
-        # cached template object and the shard list, so a repeat for the same two objects skips the check.
+        # status, the references and the shard list: a new template version (the next wave) with an equal
+        # status and equal references reuses the last verdict (two C-level compares instead of the rebuild).
         shards = self.all_shard_names
+        refs = ((template.get("spec") or {}).get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
         memo = self._inline_status_ok.get(key)
-        if memo is None or memo[0] is not template or memo[1] is not shards:
+        if memo is None or memo[2] is not shards or memo[0] != status or memo[1] != refs:
             secrets, configmaps = dependent_names(template)
             c0 = conds[0]
             if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE,
@@ -501,7 +503,7 @@ class ReconcileMixin:
                     or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
                     or status.get("syncedToClusters") != shards:
                 return False
-            self._inline_status_ok[key] = (template, shards)
+            self._inline_status_ok[key] = (status, refs, shards)
         self.stats["reconciles"] += 1
         self.stats["inline_finishes"] += 1
         self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())  # a reconcile, done in place
