@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `event-repeat-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -99,6 +99,8 @@ class AppConfig:
     shard_reload_period: float = _dur(30.0)  # native: re-scan shard-config-path for added/removed/changed shards
     coalesce_window: float = _dur(0.002)  # native: park event-triggered keys this long so a template and its
                                           # Secret/ConfigMap changing together reconcile once
+    event_repeat_window: float = _dur(1.0)  # native: repeats of an Event already written are folded into one
+                                            # count PATCH per window (first occurrences go out at once)
     metrics_bind_address: str = ""   # e.g. ":9090" → Prometheus /metrics
     health_bind_address: str = ""    # e.g. ":8081" → /healthz, /readyz
     log_format: str = "json"

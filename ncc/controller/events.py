@@ -15,7 +15,11 @@ This module re-creates the parts of client-go `tools/record` that shape the API 
 The correlator runs when an event is recorded, as client-go's broadcaster does on receipt.  With
 `coalesce=True` (native mode) an event identical to one still waiting for its writer is folded into it:
 one write then carries both (`count` + n).  The Event object ends up the same — count, last
-timestamp, message — with fewer API writes when a burst outruns the writers.
+timestamp, message — with fewer API writes when a burst outruns the writers.  With `repeat_window` > 0
+(native mode, `event-repeat-window`) a repeat of an event that has already been written is held for up to
+that long and folded with the repeats that follow it: a template synced on every wave of a rollout costs one
+count PATCH per window instead of one per pass (a first occurrence, and every Warning that is new, still goes
+out at once).
 
 `FakeRecorder` mirrors client-go's: it keeps "Type Reason Message" strings (or drops them).
 """
@@ -88,7 +92,7 @@ class BroadcastRecorder(EventRecorder):
     """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
 
     def __init__(self, client: KubeClient, component: str = C.CONTROLLER_AGENT_NAME, *, spam_filter: bool = True,
-                 log_events: bool = True, writers: int = 1, coalesce: bool = False):
+                 log_events: bool = True, writers: int = 1, coalesce: bool = False, repeat_window: float = 0.0):
         self.client = client
         self.component = component
         self.spam_filter = spam_filter
@@ -101,6 +105,9 @@ class BroadcastRecorder(EventRecorder):
         self._queue = self._queues[0]
         self.coalesce = coalesce
         self._pending: dict[tuple, list] = {}  # coalesce: correlation key -> queued entry [.., n]
+        self.repeat_window = repeat_window if coalesce else 0.0
+        self._deferred: dict[tuple, list] = {}  # repeat_window: correlation key -> held entry [.., n]
+        self._flush_timer = None
         self._buckets: dict[tuple, TokenBucket] = {}
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
         self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
@@ -114,6 +121,13 @@ class BroadcastRecorder(EventRecorder):
             self._tasks = [asyncio.ensure_future(self._run(q)) for q in self._queues]
 
     async def stop(self, drain_timeout: float = 1.0) -> None:
+        if self._flush_timer is not None:
+            self._flush_timer.cancel()
+            self._flush_timer = None
+        if self._deferred and self._tasks:
+            for entry in self._deferred.values():  # held repeats still go out (up to the buffers' room)
+                self._enqueue(entry, held=True)
+            self._deferred.clear()
         if not self._tasks:
             return
         try:
@@ -141,22 +155,48 @@ class BroadcastRecorder(EventRecorder):
             return
         message, key = self._aggregate(ref, event_type, reason, message, now)
         if self.coalesce:
-            entry = self._pending.get(key)
+            entry = self._pending.get(key) or self._deferred.get(key)
             if entry is not None:
                 entry[4] += 1
                 entry[0], entry[3] = ref, message  # the latest involvedObject and message go out with the write
                 self.stats["merged"] += 1
                 return
+            if self.repeat_window > 0 and key in self._seen:
+                # a repeat of an Event already written: held, and folded with those that follow it
+                self._deferred[key] = [ref, event_type, reason, message, 1, key]
+                if self._flush_timer is None:
+                    self._flush_timer = asyncio.get_running_loop().call_later(self.repeat_window,
+                                                                              self._flush_deferred)
+                return
+        self._enqueue([ref, event_type, reason, message, 1, key])
+
+    def _flush_deferred(self) -> None:
+        """Hand the held repeats to the writers — as many as their buffers take now (a held repeat is never
+        dropped for a full buffer: the rest waits for the next, short, round)."""
+        self._flush_timer = None
+        room = sum(q.maxsize - q.qsize() for q in self._queues)
+        for key in list(self._deferred)[:max(0, room)]:
+            if self._enqueue(self._deferred[key], held=True):
+                del self._deferred[key]
+        if self._deferred:
+            self._flush_timer = asyncio.get_running_loop().call_later(0.01, self._flush_deferred)
+
+    def _enqueue(self, entry: list, held: bool = False) -> bool:
+        """Queue for its object's writer; False when that buffer is full (a new event is then dropped, as
+        client-go drops on a full broadcaster buffer; a held repeat stays held)."""
+        ref, key = entry[0], entry[5]
         q = self._queue if self.writers == 1 else \
             self._queues[hash((ref["namespace"], ref["name"], ref["kind"])) % self.writers]
-        entry = [ref, event_type, reason, message, 1, key]
+        if held and q.full():
+            return False
         try:
             q.put_nowait(entry)
         except asyncio.QueueFull:
             self.stats["dropped_full"] += 1
-            return
+            return False
         if self.coalesce:
             self._pending[key] = entry
+        return True
 
     # ------------------------------------------------------------------ correlator
     def _allow(self, ref: dict, now: float) -> bool:

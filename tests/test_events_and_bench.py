@@ -176,3 +176,40 @@ def test_bench_eight_ranks_auto_sized_topology():
     assert ch == {"start": want_children, "end": want_children, "replaced": 0}, (ch, sz)
     assert res["value"] > 0 and res["p50_latency_ms"] is not None
     print(json.dumps(res))
+
+
+async def test_event_repeat_window_folds_repeats_of_written_events():
+    """Native mode `event-repeat-window`: the first occurrence is written at once; repeats of an Event already
+    written are held for the window and go out as one count PATCH — the Event ends up with the same count."""
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False, writers=4, coalesce=True, repeat_window=0.05)
+    rec.start()
+    t = client.state.create(R.TEMPLATES, "nexus", make_template(0, "nexus"))
+    msg = "Resource of type NexusAlgorithmTemplate synced successfully"
+    rec.event(t, "Normal", "Synced", msg)
+    await _drain(rec)
+    assert rec.stats["created"] == 1
+    for _ in range(5):  # repeats within one window
+        rec.event(t, "Normal", "Synced", msg)
+    rec.event(t, "Warning", "ErrResourceSyncError", "boom")  # a new event is not held
+    await _drain(rec)
+    assert rec.stats["patched"] == 0 and rec.stats["created"] == 2
+    await asyncio.sleep(0.1)
+    await _drain(rec)
+    events = {e["reason"]: e for e in client.state.list(R.EVENTS, "nexus")["items"]}
+    assert events["Synced"]["count"] == 6 and rec.stats["patched"] == 1
+    # many held repeats are never dropped for a full writer buffer
+    ts = [client.state.create(R.TEMPLATES, "nexus", make_template(i, "nexus")) for i in range(1, 1600)]
+    for k in range(0, len(ts), 200):  # first occurrences, at a pace the writers keep up with
+        for o in ts[k:k + 200]:
+            rec.event(o, "Normal", "Synced", msg)
+        await _drain(rec)
+    assert rec.stats["dropped_full"] == 0
+    for o in ts:  # then one burst of repeats: more than the writers' buffers hold
+        rec.event(o, "Normal", "Synced", msg)
+    await asyncio.sleep(0.5)
+    await _drain(rec)
+    await rec.stop()
+    counts = [e["count"] for e in client.state.list(R.EVENTS, "nexus")["items"] if e["reason"] == "Synced"]
+    assert len(counts) == 1600 and sorted(counts)[:1599] == [2] * 1599, rec.stats
+    assert rec.stats["dropped_full"] == 0
