@@ -178,7 +178,7 @@ class Store:
 
     # ------------------------------------------------------------ reads
     def get(self, namespace: str, name: str) -> dict | None:
-        key = ObjectKey(namespace, name)
+        key = (namespace, name)  # hashes and compares equal to ObjectKey(namespace, name), built faster
         cur = self._items.get(key)
         if self._assumed:
             a = self._assumed.get(key)

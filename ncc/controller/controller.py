@@ -153,16 +153,17 @@ class Controller(ReconcileMixin):
         o = self.options
         om, nm = old.get("metadata") or {}, new.get("metadata") or {}
         nrv = nm.get("resourceVersion")
+        orv = om.get("resourceVersion")
         key = None
         if o.adoption_cache and kind == C.KIND_TEMPLATE:
             # adoption depends on the references and the dependents' ownerRefs (whose changes arrive as
             # dependent events): a new template version with the same references stays adopted
-            key = make_key(kind, nm.get("namespace", "") or "", nm.get("name", ""))
-            if self._adopted.get(key) == om.get("resourceVersion") and om.get("uid") == nm.get("uid") and \
-                    same_references(old, new):
-                self._adopted[key] = nrv
+            key = f"{kind}/{nm.get('namespace') or ''}/{nm.get('name', '')}"
+            adopted = self._adopted
+            if adopted.get(key) == orv and om.get("uid") == nm.get("uid") and same_references(old, new):
+                adopted[key] = nrv
         if o.generation_filter:
-            if om.get("resourceVersion") == nrv:
+            if orv == nrv:
                 return  # informer resync: nothing changed
             gen = om.get("generation")
             if gen is not None and gen == nm.get("generation") and om.get("labels") == nm.get("labels") \
@@ -427,7 +428,7 @@ class Controller(ReconcileMixin):
     def shard_ready_ok(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else whether all succeeded."""
         m = obj.get("metadata") or {}
-        return self.reports.ready_ok(key, m.get("uid", ""), int(m.get("generation") or 0))
+        return self.reports.ready_ok(key, m.get("uid") or "", m.get("generation") or 0)
 
     def shard_readiness(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else {shard: error|None}."""

@@ -216,12 +216,12 @@ class BroadcastRecorder(EventRecorder):
 
     def _aggregate(self, ref: dict, event_type: str, reason: str, message: str, now: float) -> tuple[str, tuple]:
         akey = (self.component, ref["kind"], ref["namespace"], ref["name"], ref["uid"], event_type, reason)
-        msgs, first = self._similar.get(akey, (set(), now))
-        if now - first > AGGREGATE_INTERVAL_S:
-            msgs, first = set(), now
+        hit = self._similar.get(akey)
+        if hit is None or now - hit[1] > AGGREGATE_INTERVAL_S:
+            hit = self._similar[akey] = (set(), now)
+            _bound(self._similar)
+        msgs = hit[0]
         msgs.add(message)
-        self._similar[akey] = (msgs, first)
-        _bound(self._similar)
         if len(msgs) >= AGGREGATE_MAX_EVENTS:
             return "(combined from similar events): " + message, akey
         return message, akey + (message,)

@@ -472,14 +472,15 @@ class ReconcileMixin:
         kind, ns, name = key.split("/", 2)
         if kind != C.KIND_TEMPLATE:
             return False
-        template = self.template_lister.try_get(ns, name)
+        template = self.template_informer.store.get(ns, name)
         if template is None:
             return False
         status = template.get("status") or {}
         conds = status.get("conditions")
-        if not conds or self._adopted.get(key) != (template.get("metadata") or {}).get("resourceVersion"):
+        m = template.get("metadata") or {}
+        if not conds or self._adopted.get(key) != m.get("resourceVersion"):
             return False
-        ok = self.shard_ready_ok(key, template)
+        ok = self.reports.ready_ok(key, m.get("uid") or "", m.get("generation") or 0)
         if ok is None:
             # A newer version (the next wave) reached the cache between the last report and this flush.  It is
             # initialised and adopted, so the pass would stop at the readiness check, exactly as the early pass
