@@ -382,6 +382,8 @@ static bool in_partition(const std::string& ns, const std::string& name) {
 }
 
 // ------------------------------------------------------------------------------------ channel
+static double g_flush_interval = 0.001;  // NCC_REPORT_FLUSH_MS overrides (0: every loop iteration)
+
 class Channel {
 public:
     explicit Channel(int fd) : fd_(fd) {
@@ -390,12 +392,19 @@ public:
         loop().add_fd(fd_);
         spawn(writer(), "channel writer");
     }
-    // Queue one message (an encoded msgpack map); frames are coalesced per loop iteration.
+    // Queue one message (an encoded msgpack map).  Frames are coalesced per loop iteration, and under load
+    // to at most one per `g_flush_interval`: a busy executor reports after every pass, and at 8 shards the
+    // coordinator's cost is per frame (a wake-up and a read), not per report.  The first message after a
+    // quiet interval still goes out on the next loop iteration.
     void send(std::string msg) {
         pending_.push_back(std::move(msg));
         if (!flush_scheduled_) {
             flush_scheduled_ = true;
-            loop().call_soon([this] { flush(); });
+            double due = last_flush_ + g_flush_interval;
+            if (g_flush_interval <= 0 || now_s() >= due)
+                loop().call_soon([this] { flush(); });
+            else
+                loop().call_at(due, [this] { flush(); });
         }
     }
     bool closed() const { return closed_; }
@@ -455,6 +464,7 @@ private:
     int fd_;
     bool closed_ = false;
     bool flush_scheduled_ = false;
+    double last_flush_ = 0;
     std::vector<std::string> pending_;
     std::string in_;
     size_t pos_ = 0;
@@ -463,6 +473,7 @@ private:
 
     void flush() {
         flush_scheduled_ = false;
+        last_flush_ = now_s();
         if (pending_.empty()) return;
         std::string body;
         bool batch = pending_.size() > 1;
@@ -1821,6 +1832,7 @@ int main(int argc, char** argv) {
         }
     }
     if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
+    if (const char* f = std::getenv("NCC_REPORT_FLUSH_MS")) g_flush_interval = std::max(0.0, std::atof(f) / 1000.0);
     if (std::getenv("NCC_TRACE_STAGES") != nullptr) {
         g_trace = new std::vector<TraceRec>();
         g_trace->reserve(1 << 20);
