@@ -309,14 +309,19 @@ def stage_breakdown(trace_dir: str, ctrl_times: list, shard_waves: list) -> dict
                                          t_e if t_e is not None else t_c)
                 if None in (t_r, t_e, t_q) or not (t_c <= t_r <= t_e <= t_q <= t_s):
                     continue
-                rows.append((t_s - t_c, t_r - t_c, t_e - t_r, t_q - t_e, t_s - t_q))
+                rows.append((t_s - t_c, t_r - t_c, t_e - t_r, t_q - t_e, t_s - t_q, plural))
     if not rows:
         return None
     out = {"objects": len(rows)}
     for i, name in enumerate(("total",) + STAGES):
         xs = [r[i] / 1e6 for r in rows]
         out[name] = {"p50_ms": round(pct(xs, 50), 2), "p99_ms": round(pct(xs, 99), 2)}
-    rows.sort()
+    by_kind = {}
+    for r in rows:
+        by_kind.setdefault(r[5], []).append(r[0] / 1e6)
+    out["total_by_kind"] = {k: {"p50_ms": round(pct(v, 50), 2), "p99_ms": round(pct(v, 99), 2)}
+                            for k, v in sorted(by_kind.items())}
+    rows.sort(key=lambda r: r[0])
     tail = rows[-max(1, len(rows) // 100):]
     out["p99_tail_mean_ms"] = {name: round(sum(r[i + 1] for r in tail) / len(tail) / 1e6, 2)
                                for i, name in enumerate(STAGES)}
