@@ -38,6 +38,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <x86intrin.h>
 #include <csignal>
 #include <optional>
 #include <cstdarg>
@@ -140,6 +141,22 @@ static void log_at(int level, const char* fmt, ...) {
 #define LOG_WARN(...) log_at(30, __VA_ARGS__)
 #define LOG_INFO(...) log_at(20, __VA_ARGS__)
 #define LOG_DEBUG(...) log_at(10, __VA_ARGS__)
+
+// NCC_CPU_REPORT: CPU cycles per phase of the data plane (rdtsc; reported as shares of the process's CPU)
+enum Phase { PH_RELAY, PH_SHARD_LINE, PH_RESPONSE, PH_BODY, PH_CHANNEL_IN, PH_N };
+static const char* kPhaseName[PH_N] = {"relay_in", "shard_watch", "write_response", "write_body", "channel_read"};
+static unsigned long long g_phase[PH_N] = {};
+static bool g_phases_on = false;
+static long long g_scan_hits = 0, g_scan_misses = 0;  // write responses read without / with a DOM
+struct PhaseTimer {
+    int ph;
+    unsigned long long t0;
+    explicit PhaseTimer(int p) : ph(p), t0(g_phases_on ? __rdtsc() : 0) {}
+    ~PhaseTimer() {
+        if (g_phases_on) g_phase[ph] += __rdtsc() - t0;
+    }
+};
+
 
 // A reconcile failure with the Python exception class name the reports carry.
 struct NamedError : std::runtime_error {
@@ -306,7 +323,7 @@ static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) 
 
 // Slim shard-side object: everything but the payloads, plus their fingerprints.
 struct ShardObj {
-    Value rest;  // the object without spec/status/data/binaryData/stringData (re-sent on PUT)
+    std::string rest;  // JSON text of the object without spec/status/data/binaryData/stringData (re-sent on PUT)
     std::string ns, name, uid;
     long long rv = -1;
     uint64_t fp_spec = 0, fp_data = 0, fp_bin = 0;
@@ -363,12 +380,111 @@ static ShardPtr make_shard_obj(int kind, Value obj, const std::string_view* raw 
         obj.erase("binaryData");
         obj.erase("stringData");
     }
-    s->rest = std::move(obj);
+    s->rest = dumps(obj);
+    return s;
+}
+
+// metadata fields of a shard object from its raw text (no DOM); false: anything unexpected (an escaped
+// string, a non-string where a string belongs) — the caller parses the object instead
+static bool scan_meta(ShardObj& s, std::string_view meta) {
+    RawCursor c(meta);
+    return c.members([&](std::string_view k, std::string_view v) {
+        RawCursor vc(v);
+        std::string_view t;
+        if (k == "name" || k == "namespace" || k == "uid" || k == "resourceVersion") {
+            if (!vc.str(t)) return v == "null";
+            if (k == "name") s.name.assign(t);
+            else if (k == "namespace") s.ns.assign(t);
+            else if (k == "uid") s.uid.assign(t);
+            else s.rv = rv_num(t);
+            return true;
+        }
+        if (k == "labels") {
+            if (v == "null") return true;
+            return vc.members([&](std::string_view lk, std::string_view lv) {
+                RawCursor x(lv);
+                std::string_view val;
+                if (lk == kLabelApp || lk == kLabelOwner) {
+                    if (!x.str(val)) return false;
+                    (lk == kLabelApp ? s.label_app : s.label_owner).assign(val);
+                }
+                return true;
+            });
+        }
+        if (k == "ownerReferences") {
+            if (v == "null") return true;
+            return vc.elements([&](std::string_view ref) {
+                std::string_view rk, rn, ru;
+                RawCursor rc(ref);
+                bool ok = rc.members([&](std::string_view fk, std::string_view fv) {
+                    RawCursor f(fv);
+                    if (fk == "kind") return f.str(rk);
+                    if (fk == "name") return f.str(rn);
+                    if (fk == "uid") return f.str(ru);
+                    return true;
+                });
+                if (!ok) return false;
+                s.has_owner_refs = true;
+                s.all_owner_names.emplace_back(rn);
+                if (rk == kTemplateKind) s.template_owners.emplace_back(std::string(rn), std::string(ru));
+                return true;
+            });
+        }
+        return true;
+    });
+}
+
+// A write response straight into the slim form without a DOM: the non-payload members are copied as text
+// (the next PUT's body), the metadata fields read in place, the payloads fingerprinted from their text.
+static ShardPtr shard_obj_scan(int kind, std::string_view body) {
+    auto s = std::make_shared<ShardObj>();
+    const std::string_view* keys = payload_keys(kind);
+    size_t nk = payload_count(kind);
+    std::string_view raw[3];
+    std::string& rest = s->rest;
+    rest.reserve(body.size());
+    rest.push_back('{');
+    bool first = true;
+    bool ok = RawCursor(body).members([&](std::string_view k, std::string_view v) {
+        for (size_t i = 0; i < nk; ++i)
+            if (k == keys[i]) {
+                raw[i] = v;
+                return true;
+            }
+        if (!first) rest.push_back(',');
+        first = false;
+        rest.push_back('"');
+        rest.append(k);
+        rest.append("\":");
+        rest.append(v);
+        if (k == "metadata") return scan_meta(*s, v);
+        if (k == "type" && kind >= 2) {  // Secret.type
+            std::string_view t;
+            if (!RawCursor(v).str(t)) return v == "null";
+            s->type.assign(t);
+        }
+        return true;
+    });
+    if (!ok) return nullptr;
+    rest.push_back('}');
+    if (s->ns.empty()) s->ns = g_opt.ns;
+    if (kind < 2) {
+        s->fp_spec = raw[0].empty() ? fingerprint(Value()) : fingerprint_text(raw[0]);
+    } else {
+        s->fp_data = fp_opt_text(raw[0]);
+        s->fp_bin = fp_opt_text(raw[1]);
+    }
     return s;
 }
 
 // A write/GET response body straight into the slim form, payloads fingerprinted from their text.
 static ShardPtr shard_obj_from_body(int kind, std::string_view body) {
+    PhaseTimer pt(PH_RESPONSE);
+    if (ShardPtr fast = shard_obj_scan(kind, body)) {
+        ++g_scan_hits;
+        return fast;
+    }
+    ++g_scan_misses;
     std::string_view raw[3];
     Value rest = Parser(body.data(), body.size()).parse_split(payload_keys(kind), payload_count(kind), raw);
     return make_shard_obj(kind, std::move(rest), raw);
@@ -424,6 +540,7 @@ public:
                         in_.erase(0, pos_);
                         pos_ = 0;
                     }
+                    PhaseTimer pt(PH_CHANNEL_IN);
                     mp::Obj o = mp::decode(body);
                     std::vector<mp::Obj> out;
                     if (batch && o.t == mp::Obj::ARR)
@@ -667,6 +784,7 @@ struct Shard {
 };
 
 static double kDependentHold = 5.0;  // NCC_DEPENDENT_HOLD overrides
+
 
 // NCC_TRACE_STAGES=<dir>: wall-clock times of every relayed controller object received ("r", kind) and of
 // every key a worker dequeues ("q"), written to <dir>/executor-<index>.tsv on exit (bench.py --stages)
@@ -951,6 +1069,7 @@ static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch)
 }
 
 static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
+    PhaseTimer pt(PH_SHARD_LINE);
     {  // nothing to decode: the echo of our own write (its response is already cached), or an object of
        // another executor's key partition (several executors share a shard's watch streams)
         std::string_view type, ns, name, rv;
@@ -1192,8 +1311,10 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
     for (int attempt = 0; attempt < 2; ++attempt) {
         std::string body;
         if (update) {
-            body = dumps_with(cur->rest, {{"spec", spec}});
+            PhaseTimer pt(PH_BODY);
+            body = splice_members(cur->rest, {{"spec", spec}});
         } else {
+            PhaseTimer pt(PH_BODY);
             Value head = Value::object();
             head.set("apiVersion", Value::str(kApiVersion));
             head.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
@@ -1315,7 +1436,8 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         if (with_bin && !raw_is_empty(src->bin_raw)) bin = src->bin_raw;
         std::string body;
         if (missing_owner) {
-            Value copy = so->rest;
+            PhaseTimer pt(PH_BODY);
+            Value copy = parse(so->rest);
             Value* m = copy.get("metadata");
             if (m == nullptr) m = &copy.set("metadata", Value::object());
             Value* refs = m->get("ownerReferences");
@@ -1323,8 +1445,9 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
             refs->a.push_back(owner_ref(st->name, st->uid));
             body = touch_bin ? dumps_with(copy, {{"data", data}, {"binaryData", bin}}) : dumps_with(copy, {{"data", data}});
         } else {
-            body = touch_bin ? dumps_with(so->rest, {{"data", data}, {"binaryData", bin}})
-                             : dumps_with(so->rest, {{"data", data}});
+            PhaseTimer pt(PH_BODY);
+            body = touch_bin ? splice_members(so->rest, {{"data", data}, {"binaryData", bin}})
+                             : splice_members(so->rest, {{"data", data}});
         }
         bool conflict = false;
         try {
@@ -1632,6 +1755,7 @@ static void configure(const Value& c) {
 }
 
 static void handle_message(const mp::Obj& m) {
+    PhaseTimer pt(PH_RELAY);
     Executor& ex = *g_ex;
     std::string_view t = m.sget("t");
     if (t == "w" || t == "s") {
@@ -1740,6 +1864,25 @@ static Task<void> shutdown_watch() {
     if (std::getenv("NCC_CPU_REPORT"))
         LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu",
                  shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()));
+    if (g_phases_on) {
+        // cycles -> seconds: calibrate the TSC against the steady clock
+        unsigned long long c0 = __rdtsc();
+        double w0 = now_s();
+        while (now_s() - w0 < 0.02) {
+        }
+        double hz = static_cast<double>(__rdtsc() - c0) / (now_s() - w0);
+        struct rusage ru;
+        getrusage(RUSAGE_SELF, &ru);
+        double user = ru.ru_utime.tv_sec + ru.ru_utime.tv_usec / 1e6, sys = ru.ru_stime.tv_sec + ru.ru_stime.tv_usec / 1e6;
+        std::string parts;
+        for (int i = 0; i < PH_N; ++i) {
+            char b[96];
+            std::snprintf(b, sizeof b, " %s=%.3fs", kPhaseName[i], static_cast<double>(g_phase[i]) / hz);
+            parts += b;
+        }
+        LOG_WARN("executor cpu user=%.3fs sys=%.3fs phases:%s response_scan=%lld/%lld", user, sys, parts.c_str(),
+                 g_scan_hits, g_scan_hits + g_scan_misses);
+    }
     if (std::getenv("NCC_CPU_REPORT"))
         LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld reports_skipped=%lld enqueues: object=%lld "
                  "dependent=%lld shard_object=%lld shard_dependent=%lld retry=%lld sweep=%lld resync=%lld delete=%lld",
@@ -1819,6 +1962,41 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "--shardobj-selftest") {
+        // one JSON object per stdin line -> per kind (template, secret): whether the DOM-free scan took it, and
+        // the slim fields + rest text from the scan and from the DOM path (tests/test_native_executor_json.py)
+        auto fields = [](const ShardPtr& o) {
+            if (!o) return std::string("-");
+            std::string f = o->ns + "|" + o->name + "|" + o->uid + "|" + std::to_string(o->rv) + "|" +
+                            std::to_string(o->fp_spec) + "|" + std::to_string(o->fp_data) + "|" +
+                            std::to_string(o->fp_bin) + "|" + o->type + "|" + (o->has_owner_refs ? "1" : "0") + "|" +
+                            o->label_app + "|" + o->label_owner + "|";
+            for (const auto& t : o->template_owners) f += t.first + "/" + t.second + ",";
+            f += "|";
+            for (const auto& n : o->all_owner_names) f += n + ",";
+            return f;
+        };
+        std::string line;
+        std::vector<char> buf(1 << 20);
+        while (std::fgets(buf.data(), static_cast<int>(buf.size()), stdin) != nullptr) {
+            line.assign(buf.data());
+            while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+            for (int kind : {TEMPLATES, SECRETS}) {
+                ShardPtr fast = shard_obj_scan(kind, line);
+                ShardPtr slow;
+                try {
+                    std::string_view raw[3];
+                    Value rest = Parser(line.data(), line.size()).parse_split(payload_keys(kind), payload_count(kind), raw);
+                    slow = make_shard_obj(kind, std::move(rest), raw);
+                } catch (const std::exception&) {
+                }
+                std::string a = fields(fast), b = fields(slow);
+                std::printf("%d\t%d\t%s\t%s\n", fast ? 1 : 0, a == b ? 1 : 0, fast ? fast->rest.c_str() : "-",
+                            slow ? slow->rest.c_str() : "-");
+            }
+        }
+        return 0;
+    }
     if (fd < 0) {
         std::fprintf(stderr, "usage: ncc-executor --fd N --index I --part p/k\n");
         return 2;
@@ -1833,6 +2011,7 @@ int main(int argc, char** argv) {
     }
     if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
     if (const char* f = std::getenv("NCC_REPORT_FLUSH_MS")) g_flush_interval = std::max(0.0, std::atof(f) / 1000.0);
+    g_phases_on = std::getenv("NCC_CPU_REPORT") != nullptr;
     if (std::getenv("NCC_TRACE_STAGES") != nullptr) {
         g_trace = new std::vector<TraceRec>();
         g_trace->reserve(1 << 20);

@@ -491,7 +491,7 @@ public:
         hdr_.clear();
     }
     const std::string& prefix() const { return url_.prefix; }
-    std::map<std::string, long long> stats;
+    long long requests = 0, request_errors = 0;  // completed exchanges / transport failures
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
     // token once on 401, and re-send once on a fresh connection when a reused keep-alive connection died
@@ -717,10 +717,10 @@ private:
             bool timed_out = !ok && now_s() >= c->deadline;
             release(std::move(c), ok && keep);
             if (ok) {
-                ++stats["requests"];
+                ++requests;
                 co_return r;
             }
-            ++stats["errors"];
+            ++request_errors;
             if (timed_out) throw TransportError(method + " " + target + ": request timed out");
             if (reused && before == 0 && tries == 0) continue;  // stale keep-alive connection: once more, fresh
             throw TransportError(method + " " + target + ": " + err);

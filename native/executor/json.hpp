@@ -18,6 +18,8 @@
 #include <string_view>
 #include <utility>
 #include <vector>
+#include <charconv>
+#include <system_error>
 
 namespace ncc {
 
@@ -327,11 +329,7 @@ private:
         ws();
         if (p_ >= e_) fail("unexpected end");
         char c = *p_;
-        if (c == '"') {
-            tmp_.clear();
-            string(tmp_);
-            return hash_str(tmp_);
-        }
+        if (c == '"') return hash_str(str_view());
         if (c == '{') {
             ++p_;
             uint64_t acc = 0, count = 0;
@@ -343,9 +341,7 @@ private:
             while (true) {
                 ws();
                 if (p_ >= e_ || *p_ != '"') fail("expected key");
-                tmp_.clear();
-                string(tmp_);
-                uint64_t kh = hash_key(tmp_);
+                uint64_t kh = hash_key(str_view());
                 ws();
                 if (p_ >= e_ || *p_ != ':') fail("expected ':'");
                 ++p_;
@@ -365,14 +361,15 @@ private:
         }
         if (c == '[') {
             ++p_;
-            std::vector<uint64_t> items;
+            uint64_t h = kArraySeed, count = 0;
             ws();
             if (p_ < e_ && *p_ == ']') {
                 ++p_;
-                return fp_array(items);
+                return fp_array_end(h, 0);
             }
             while (true) {
-                items.push_back(fp(depth + 1));
+                h = fp_array_step(h, fp(depth + 1));
+                ++count;
                 ws();
                 if (p_ < e_ && *p_ == ',') {
                     ++p_;
@@ -380,21 +377,56 @@ private:
                 }
                 if (p_ < e_ && *p_ == ']') {
                     ++p_;
-                    return fp_array(items);
+                    return fp_array_end(h, count);
                 }
                 fail("expected ',' or ']'");
             }
         }
-        Value scalar;
-        value(scalar, depth);
-        return fp_scalar(scalar);
+        if (c == 't' && e_ - p_ >= 4 && std::memcmp(p_, "true", 4) == 0) {
+            p_ += 4;
+            return fp_bool(true);
+        }
+        if (c == 'f' && e_ - p_ >= 5 && std::memcmp(p_, "false", 5) == 0) {
+            p_ += 5;
+            return fp_bool(false);
+        }
+        if (c == 'n' && e_ - p_ >= 4 && std::memcmp(p_, "null", 4) == 0) {
+            p_ += 4;
+            return kNullFp;
+        }
+        const char* s = p_;
+        while (p_ < e_ && (*p_ == '-' || *p_ == '+' || *p_ == '.' || *p_ == 'e' || *p_ == 'E' ||
+                           (*p_ >= '0' && *p_ <= '9')))
+            ++p_;
+        if (p_ == s || !(c == '-' || (c >= '0' && c <= '9'))) fail("unexpected character");
+        return fp_number(std::string_view(s, static_cast<size_t>(p_ - s)));
+    }
+    // the next string's content: a view of the text when it has no escape sequence, else decoded into tmp_
+    std::string_view str_view() {
+        const char* s = p_ + 1;
+        const char* q = s;
+        while (q < e_ && *q != '"' && *q != '\\') ++q;
+        if (q < e_ && *q == '"') {
+            p_ = q + 1;
+            return std::string_view(s, static_cast<size_t>(q - s));
+        }
+        tmp_.clear();
+        string(tmp_);
+        return tmp_;
     }
     static uint64_t hash_str(std::string_view s);
     static uint64_t hash_key(std::string_view s);
     static uint64_t fp_member(uint64_t key_hash, uint64_t value_fp);
     static uint64_t fp_object(uint64_t acc, uint64_t count);
-    static uint64_t fp_array(const std::vector<uint64_t>& items);
-    static uint64_t fp_scalar(const Value& v);
+public:
+    static constexpr uint64_t kArraySeed = 0x6666ULL;
+    static constexpr uint64_t kNullFp = 0x9e3779b97f4a7c15ULL;
+    static uint64_t fp_array_step(uint64_t h, uint64_t item);
+    static uint64_t fp_array_end(uint64_t h, uint64_t count);
+    static uint64_t fp_bool(bool b);
+    static uint64_t fp_number(std::string_view text);
+
+private:
 
     void value(Value& v, int depth) {
         if (depth > 200) fail("nesting too deep");
@@ -800,6 +832,135 @@ private:
     }
 };
 
+// ------------------------------------------------------------------------------------ raw members
+// A cursor over JSON text for reading a few members without building a DOM.  Strings are returned as views
+// of the text, so one with an escape sequence is refused (`str` returns false) and the caller falls back to
+// the parser.
+struct RawCursor {
+    const char* p;
+    const char* e;
+    RawCursor(std::string_view t) : p(t.data()), e(t.data() + t.size()) {}
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+    }
+    bool at(char c) {
+        ws();
+        return p < e && *p == c;
+    }
+    bool expect(char c) {
+        if (!at(c)) return false;
+        ++p;
+        return true;
+    }
+    bool str(std::string_view& out) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        const char* s = ++p;
+        while (p < e && *p != '"') {
+            if (*p == '\\') return false;
+            ++p;
+        }
+        if (p >= e) return false;
+        out = std::string_view(s, static_cast<size_t>(p - s));
+        ++p;
+        return true;
+    }
+    bool skip_str() {
+        ++p;
+        while (p < e) {
+            if (*p == '\\') {
+                p += 2;
+                continue;
+            }
+            if (*p++ == '"') return true;
+        }
+        return false;
+    }
+    // skip one value; `span` gets its text
+    bool value(std::string_view& span) {
+        ws();
+        if (p >= e) return false;
+        const char* s = p;
+        if (*p == '"') {
+            if (!skip_str()) return false;
+        } else if (*p == '{' || *p == '[') {
+            int depth = 0;
+            bool done = false;
+            while (p < e) {
+                char c = *p;
+                if (c == '"') {
+                    if (!skip_str()) return false;
+                    continue;
+                }
+                if (c == '{' || c == '[') ++depth;
+                if ((c == '}' || c == ']') && --depth == 0) {
+                    ++p;
+                    done = true;
+                    break;
+                }
+                ++p;
+            }
+            if (!done) return false;
+        } else {
+            while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' &&
+                   *p != '\t')
+                ++p;
+            if (p == s) return false;
+        }
+        span = std::string_view(s, static_cast<size_t>(p - s));
+        return true;
+    }
+    // the members of an object (the cursor at its '{'): fn(key, value text) for each; false when malformed
+    // or a key carries an escape
+    template <class Fn>
+    bool members(Fn&& fn) {
+        if (!expect('{')) return false;
+        if (expect('}')) return true;
+        while (true) {
+            std::string_view k, v;
+            if (!str(k) || !expect(':') || !value(v)) return false;
+            if (!fn(k, v)) return false;
+            if (expect(',')) continue;
+            return expect('}');
+        }
+    }
+    template <class Fn>
+    bool elements(Fn&& fn) {
+        if (!expect('[')) return false;
+        if (expect(']')) return true;
+        while (true) {
+            std::string_view v;
+            if (!value(v)) return false;
+            if (!fn(v)) return false;
+            if (expect(',')) continue;
+            return expect(']');
+        }
+    }
+};
+
+// `{...}` text of a JSON object with the given members appended (each as raw JSON; an empty text adds
+// nothing).  For objects kept as text without those members (the shard cache), this is dumps_with.
+inline std::string splice_members(std::string_view obj, std::initializer_list<std::pair<std::string_view, std::string_view>> add) {
+    std::string out;
+    out.reserve(obj.size() + 64);
+    size_t end = obj.rfind('}');
+    if (end == std::string_view::npos) end = obj.size();
+    out.append(obj.substr(0, end));
+    size_t i = end;
+    while (i > 0 && (obj[i - 1] == ' ' || obj[i - 1] == '\n' || obj[i - 1] == '\r' || obj[i - 1] == '\t')) --i;
+    bool empty = i > 0 && obj[i - 1] == '{';
+    for (const auto& m : add) {
+        if (m.second.empty()) continue;
+        if (!empty) out.push_back(',');
+        empty = false;
+        write_string(out, m.first);
+        out.push_back(':');
+        out.append(m.second);
+    }
+    out.push_back('}');
+    return out;
+}
+
 // ------------------------------------------------------------------------------------ fingerprints
 inline uint64_t fmix64(uint64_t k) {
     k ^= k >> 33;
@@ -833,24 +994,32 @@ inline uint64_t hash_bytes(std::string_view s, uint64_t seed) {
     return fmix64(h);
 }
 
+// fingerprint of a JSON number's text: integral values (1 == 1.0) hash as integers
+inline uint64_t fp_number_text(std::string_view text) {
+    long long iv = 0;
+    auto [ip, iec] = std::from_chars(text.data(), text.data() + text.size(), iv);
+    if (iec == std::errc() && ip == text.data() + text.size() && iv > -9000000000000000LL && iv < 9000000000000000LL)
+        return fmix64(static_cast<uint64_t>(iv) ^ 0x3333ULL);
+    double d = 0;
+    std::string z(text);
+    d = std::strtod(z.c_str(), nullptr);
+    if (std::isfinite(d) && d == std::floor(d) && std::fabs(d) < 9.0e15)
+        return fmix64(static_cast<uint64_t>(static_cast<long long>(d)) ^ 0x3333ULL);
+    uint64_t bits;
+    std::memcpy(&bits, &d, 8);
+    return fmix64(bits ^ 0x4444ULL);
+}
+
 inline uint64_t fingerprint(const Value& v) {
     switch (v.t) {
-        case Value::NUL: return 0x9e3779b97f4a7c15ULL;
-        case Value::BOOL: return fmix64(v.b ? 0x1234567ULL : 0x7654321ULL);
-        case Value::NUM: {
-            char* end = nullptr;
-            double d = std::strtod(v.s.c_str(), &end);
-            if (std::isfinite(d) && d == std::floor(d) && std::fabs(d) < 9.0e15)
-                return fmix64(static_cast<uint64_t>(static_cast<long long>(d)) ^ 0x3333ULL);
-            uint64_t bits;
-            std::memcpy(&bits, &d, 8);
-            return fmix64(bits ^ 0x4444ULL);
-        }
+        case Value::NUL: return Parser::kNullFp;
+        case Value::BOOL: return Parser::fp_bool(v.b);
+        case Value::NUM: return fp_number_text(v.s);
         case Value::STR: return hash_bytes(v.s, 0x5555ULL);
         case Value::ARR: {
-            uint64_t h = 0x6666ULL + v.a.size();
-            for (const auto& x : v.a) h = fmix64(h * 31 + fingerprint(x));
-            return h;
+            uint64_t h = Parser::kArraySeed;
+            for (const auto& x : v.a) h = Parser::fp_array_step(h, fingerprint(x));
+            return Parser::fp_array_end(h, v.a.size());
         }
         case Value::OBJ: {
             uint64_t acc = 0x7777ULL + v.o.size();
@@ -867,12 +1036,10 @@ inline uint64_t Parser::hash_str(std::string_view s) { return hash_bytes(s, 0x55
 inline uint64_t Parser::hash_key(std::string_view s) { return hash_bytes(s, 0x8888ULL); }
 inline uint64_t Parser::fp_member(uint64_t kh, uint64_t vf) { return fmix64(kh ^ (vf * 0x9E3779B97F4A7C15ULL)); }
 inline uint64_t Parser::fp_object(uint64_t acc, uint64_t count) { return fmix64(acc + 0x7777ULL + count); }
-inline uint64_t Parser::fp_array(const std::vector<uint64_t>& items) {
-    uint64_t h = 0x6666ULL + items.size();
-    for (uint64_t x : items) h = fmix64(h * 31 + x);
-    return h;
-}
-inline uint64_t Parser::fp_scalar(const Value& v) { return fingerprint(v); }
+inline uint64_t Parser::fp_array_step(uint64_t h, uint64_t item) { return fmix64(h * 31 + item); }
+inline uint64_t Parser::fp_array_end(uint64_t h, uint64_t count) { return fmix64(h ^ (count * 0xA0761D6478BD642FULL)); }
+inline uint64_t Parser::fp_bool(bool b) { return fmix64(b ? 0x1234567ULL : 0x7654321ULL); }
+inline uint64_t Parser::fp_number(std::string_view text) { return fp_number_text(text); }
 
 inline uint64_t fingerprint_text(std::string_view text) { return Parser(text.data(), text.size()).fingerprint_text(); }
 

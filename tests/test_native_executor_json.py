@@ -54,3 +54,49 @@ def test_fingerprint_text_semantics():
     assert fps[0] == fps[1]  # member order and 1 == 1.0 do not matter
     assert fps[2] == fps[3]  # escapes decode to the same string
     assert len({fps[4], fps[5], fps[6]}) == 3
+
+
+names = st.text(alphabet=st.characters(min_codepoint=32, max_codepoint=0x2FF), max_size=8)
+owner_ref = st.fixed_dictionaries({"apiVersion": st.just("science.sneaksanddata.com/v1"),
+                                   "kind": st.sampled_from(["NexusAlgorithmTemplate", "Other"]),
+                                   "name": names, "uid": names})
+shard_objs = st.fixed_dictionaries(
+    {"metadata": st.fixed_dictionaries(
+        {"name": names, "resourceVersion": st.integers(0, 10**9).map(str)},
+        optional={"namespace": names, "uid": names, "ownerReferences": st.none() | st.lists(owner_ref, max_size=3),
+                  "labels": st.none() | st.dictionaries(
+                      st.sampled_from(["science.sneaksanddata.com/controller-app",
+                                       "science.sneaksanddata.com/configuration-owner", "x"]), names, max_size=3),
+                  "annotations": st.dictionaries(names, names, max_size=2)})},
+    optional={"spec": values, "status": values, "data": st.none() | st.dictionaries(names, names, max_size=3),
+              "binaryData": st.none() | st.dictionaries(names, names, max_size=2), "type": st.none() | names,
+              "apiVersion": st.just("v1"), "kind": st.sampled_from(["Secret", "ConfigMap", "NexusAlgorithmTemplate"])})
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.lists(shard_objs, min_size=1, max_size=15), st.booleans())
+def test_shard_object_scan_matches_the_dom_path(objs, ascii_only):
+    """The executor reads write responses without a DOM (`shard_obj_scan`): for every object it accepts, the
+    slim fields and fingerprints equal the DOM path's and the kept text is the same object without its
+    payloads; anything it refuses (escaped strings) takes the DOM path."""
+    texts = [json.dumps(o, ensure_ascii=ascii_only) for o in objs]
+    out = subprocess.run([EXE, "--shardobj-selftest"], input="\n".join(texts) + "\n", capture_output=True,
+                         text=True, timeout=60, check=True).stdout.split("\n")[:-1]
+    assert len(out) == 2 * len(texts)
+    for i, line in enumerate(out):
+        fast, same, rest_fast, rest_slow = line.split("\t")
+        if fast == "1":
+            assert same == "1", (texts[i // 2], line)
+            assert json.loads(rest_fast) == json.loads(rest_slow)
+
+
+
+def test_plain_shard_object_takes_the_scan_path():
+    obj = {"apiVersion": "v1", "kind": "Secret", "type": "Opaque", "data": {"k": "dg=="},
+           "metadata": {"name": "s0", "namespace": "nexus", "uid": "u1", "resourceVersion": "42",
+                        "labels": {"science.sneaksanddata.com/controller-app": "nexus-configuration-controller"},
+                        "ownerReferences": [{"apiVersion": "science.sneaksanddata.com/v1",
+                                             "kind": "NexusAlgorithmTemplate", "name": "t", "uid": "tu"}]}}
+    out = subprocess.run([EXE, "--shardobj-selftest"], input=json.dumps(obj) + "\n", capture_output=True, text=True,
+                         timeout=60, check=True).stdout.split("\n")[:-1]
+    assert [line.split("\t")[:2] for line in out] == [["1", "1"], ["1", "1"]]
