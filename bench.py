@@ -260,7 +260,7 @@ def _first_at_or_after(ts: list, t: int):
     return ts[i] if i < len(ts) else None
 
 
-def stage_breakdown(trace_dir: str, ctrl_times: list, shard_waves: list) -> dict | None:
+def stage_breakdown(trace_dir: str, ctrl_times: list, shard_waves: list, executor: int = 0) -> dict | None:
     """Per object of the timed waves on shard 0: controller commit -> coordinator relay (`relay`) -> executor
     receive (`ipc`) -> executor worker dequeue of the owning template key (`queue`: coalescing and work-queue
     wait) -> shard commit (`write`: the pass up to the shard apiserver committing the object).  p50/p99 per
@@ -274,7 +274,7 @@ def stage_breakdown(trace_dir: str, ctrl_times: list, shard_waves: list) -> dict
             for ln in fh:
                 k, key, t = ln.rstrip("\n").split("\t")
                 relay.setdefault((int(k), key), []).append(int(t))
-    ex_files = sorted(_glob.glob(os.path.join(trace_dir, "executor-0-*.tsv")))
+    ex_files = sorted(_glob.glob(os.path.join(trace_dir, f"executor-{executor}-*.tsv")))
     if not relay or not ex_files:
         return None
     for f in ex_files:

@@ -73,7 +73,9 @@ def summarize(lat_ms: list) -> dict:
 
 
 class Topology:
-    def __init__(self, n_shards: int, mode: str, workers: int | None = None, extra_env: dict | None = None):
+    def __init__(self, n_shards: int, mode: str, workers: int | None = None, extra_env: dict | None = None,
+                 stages: bool = False):
+        self.stages = stages  # trace where latency goes (bench.py --stages): controller markers + NCC_TRACE_STAGES
         self.n = n_shards
         self.mode = mode
         self.workers = workers
@@ -101,7 +103,7 @@ class Topology:
             self.procs.append(spawn_fakeapi(f"shard-{i}", pf, extra=extra))
             files.append(pf)
         pf = os.path.join(self.work, "controller.url")
-        self.procs.append(spawn_fakeapi("controller", pf))
+        self.procs.append(spawn_fakeapi("controller", pf, extra=extra if self.stages else None))
         files.append(pf)
         urls = [await loop.run_in_executor(None, wait_port_file, f, p) for f, p in zip(files, self.procs)]
         self.shard_urls, self.ctrl_url = urls[:-1], urls[-1]
@@ -123,6 +125,9 @@ class Topology:
         env.update(MODE_ENV[self.mode])
         env["NEXUS__WORKERS"] = str(self.workers or (64 if self.mode == "native" else 2))
         env.update(self.extra_env)
+        if self.stages:
+            env["NCC_TRACE_STAGES"] = os.path.join(self.work, "trace")
+            os.makedirs(env["NCC_TRACE_STAGES"], exist_ok=True)
         self.log = open(os.path.join(self.work, "controller.log"), "wb")
         t = time.time_ns()
         self.controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=self.log,
@@ -147,9 +152,25 @@ class Topology:
         r = await self._post(f"{self.ctrl_url}/_fake/apply", {"items": items})
         return r["t1_ns"]
 
-    async def wait(self, i: int, want: list, timeout: float) -> dict:
-        return await self._post(f"{self.shard_urls[i]}/_fake/markers/wait",
-                                {"want": want, "timeout": timeout, "times": True}, timeout=timeout + 30)
+    async def wait(self, i: int, want: list, timeout: float, keyed: bool = False) -> dict:
+        url = self.ctrl_url if i < 0 else self.shard_urls[i]
+        return await self._post(f"{url}/_fake/markers/wait",
+                                {"want": want, "timeout": timeout, "times": True, "keyed": keyed}, timeout=timeout + 30)
+
+    async def stage_breakdown(self, T: int, version: int, shards: list, timeout: float) -> dict:
+        """bench.py's per-stage latency split of one wave, per shard (the controller is stopped to flush its
+        traces: call last)."""
+        sys.path.insert(0, ROOT)
+        from bench import stage_breakdown
+        ctrl = (await self.wait(-1, want(T, version), timeout, keyed=True))["times"]
+        waves = {i: (await self.wait(i, want(T, version), timeout, keyed=True))["times"] for i in shards}
+        self.controller.terminate()
+        try:
+            self.controller.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            pass
+        return {f"shard-{i}": stage_breakdown(os.path.join(self.work, "trace"), [ctrl], [w], executor=i)
+                for i, w in waves.items()}
 
     async def settle(self, T: int, timeout: float, quiet: float = 0.3) -> bool:
         """Wait until all T templates report Ready on the controller cluster, then `quiet` seconds more."""
@@ -350,8 +371,8 @@ async def config4_adoption(mode, T, timeout):
         await topo.stop()
 
 
-async def config5_flaky(mode, T, timeout, flap=1.5):
-    topo = Topology(8, mode)
+async def config5_flaky(mode, T, timeout, flap=1.5, stages=False):
+    topo = Topology(8, mode, stages=stages and mode == "native")
     try:
         await topo.start_servers()
         await topo.apply(objects(T, 0))
@@ -392,6 +413,10 @@ async def config5_flaky(mode, T, timeout, flap=1.5):
         if r["ok"]:
             out["flaky_shard"]["converge_after_recovery_s"] = round(
                 (max(max(ts) for ts in r["times"].values()) - t0) / 1e9, 3)
+        if topo.stages:
+            bd = await topo.stage_breakdown(T, 1, [healthy[0], healthy[-1]], timeout)
+            out["stages"] = {k: {s: v[s] for s in ("total", "relay", "ipc", "queue", "write", "p99_owner")}
+                             for k, v in bd.items() if v}
         return out
     finally:
         await topo.stop()
@@ -438,7 +463,7 @@ async def _run(args) -> list:
             elif c == 4:
                 r = await config4_adoption(mode, size(10000, mode), timeout=args.timeout)
             elif c == 5:
-                r = await config5_flaky(mode, size(1000, mode), timeout=args.timeout)
+                r = await config5_flaky(mode, size(1000, mode), timeout=args.timeout, stages=args.stages)
             else:
                 continue
             r["wall_s"] = round(time.perf_counter() - t, 1)
@@ -464,6 +489,8 @@ def main():
     p.add_argument("--churn-seconds", type=float, default=30.0)
     p.add_argument("--timeout", type=float, default=600.0)
     p.add_argument("--out", default="")
+    p.add_argument("--stages", action="store_true",
+                   help="config 5, native: per-stage latency split of the healthy shards' wave (bench.py --stages)")
     a = p.parse_args()
     a.configs = [int(x) for x in a.configs.split(",") if x]
     a.modes = [m for m in a.modes.split(",") if m]
