@@ -413,9 +413,17 @@ class Controller(ReconcileMixin):
             self._inline_timer = loop.call_later(delay, self._flush_inline) if delay > 0 else \
                 loop.call_soon(self._flush_inline)
 
+    INLINE_BATCH = 256  # keys finished per loop iteration: a wave's worth of completions must not hold up
+    #                     the loop (the watch lines the relay forwards wait behind it)
+
     def _flush_inline(self) -> None:
         self._inline_timer = None
-        keys, self._inline_keys = self._inline_keys, set()
+        pending = self._inline_keys
+        if len(pending) > self.INLINE_BATCH:
+            keys = [pending.pop() for _ in range(self.INLINE_BATCH)]
+            self._inline_timer = asyncio.get_running_loop().call_soon(self._flush_inline)
+        else:
+            keys, self._inline_keys = pending, set()
         for key in keys:
             try:
                 done = self.finish_inline(key)
