@@ -271,11 +271,16 @@ class Informer:
         ctx = self._line_ctx(force=self.tap is not None) if hasattr(self.client, "watch_raw") else None
         if ctx is not None:
             batches = getattr(self.client, "watch_raw_batches", None)
-            if batches is not None:
+            tap = self.tap
+            if batches is not None and tap is not None and getattr(self.client, "supports_line_tap", False):
+                # the relay gets every line straight off the socket: an executor is not kept waiting while
+                # this coordinator works through the batches before it (BENCHMARKS.md, latency stages)
+                source = batches(self.rt, self.namespace, on_lines=tap.on_lines, **kw)
+                tap = None
+            elif batches is not None:
                 source = batches(self.rt, self.namespace, **kw)
             else:
                 source = _single_lines(self.client.watch_raw(self.rt, self.namespace, **kw))
-            tap = self.tap
             async for lines in source:
                 if tap is not None:
                     tap.on_lines(lines)

@@ -349,9 +349,13 @@ class RestClient(KubeClient):
             for line in lines:
                 yield line
 
+    supports_line_tap = True  # watch_raw_batches(on_lines=...)
+
     async def watch_raw_batches(self, rt: ResourceType, namespace, *, resource_version=None, timeout_seconds=None,
-                                allow_bookmarks=True, label_selector=None) -> AsyncIterator[list]:
-        """The watch stream as lists of raw JSON lines: everything that arrived in one read, undecoded."""
+                                allow_bookmarks=True, label_selector=None, on_lines=None) -> AsyncIterator[list]:
+        """The watch stream as lists of raw JSON lines: everything that arrived in one read, undecoded.
+        `on_lines(lines)` sees every line first — with the fast transport as soon as it is read off the
+        socket, whatever the consumer of this generator is doing."""
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": timeout_seconds,
                   "allowWatchBookmarks": "true" if allow_bookmarks else None, "labelSelector": label_selector}
         target = rt.base_path(namespace) + "?" + urlencode({k: v for k, v in params.items() if v is not None})
@@ -360,7 +364,7 @@ class RestClient(KubeClient):
         if self.transport == "fast":
             pool = await self._get_pool()
             stream = pool.stream(target, headers, timeout=(timeout_seconds + 30) if timeout_seconds else None,
-                                 batch=True)
+                                 batch=True, on_lines=on_lines)
             try:
                 async for resp, lines in stream:
                     if resp is not None:
@@ -397,8 +401,12 @@ class RestClient(KubeClient):
                     buf = lines.pop()
                     lines = [ln for ln in lines if ln]
                     if lines:
+                        if on_lines is not None:
+                            on_lines(lines)
                         yield lines
                 if buf.strip():
+                    if on_lines is not None:
+                        on_lines([buf])
                     yield [buf]
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError, asyncio.TimeoutError, OSError) as e:
             raise E.TransportError(f"watch {url}: {type(e).__name__}: {e}") from e

@@ -64,6 +64,9 @@ class _Conn(asyncio.Protocol):
     (watch) connection carries exactly one exchange."""
 
     HIGH_WATER = 64
+    # a tapped stream (the watch relay's) keeps reading while its consumer works through a burst: the tap
+    # must see lines as they arrive, so the buffer may hold a whole wave (lines are ~1 KB)
+    TAPPED_HIGH_WATER = 1 << 16
 
     def __init__(self, pool: "ConnectionPool"):
         self.pool = pool
@@ -75,6 +78,9 @@ class _Conn(asyncio.Protocol):
         self._out: list = []
         self._flush_handle = None
         self.stream: deque | None = None
+        # streams: callable(lines) seeing every complete line as it arrives, before the consumer does (the
+        # coordinator's watch relay forwards lines from here, whatever its informer is busy with)
+        self.line_tap = None
         self.deadline: float | None = None  # loop time by which the in-flight exchange must complete
         self.deadline_what = ""
         self.timed_out = False
@@ -243,18 +249,30 @@ class _Conn(asyncio.Protocol):
         parts = lb.split(b"\n")
         tail = parts.pop()
         self.linebuf = bytearray(tail)
-        for p in parts:
-            if p:
-                self.stream.append(bytes(p))
+        lines = [bytes(p) for p in parts if p]
+        if self.line_tap is not None and lines:
+            self._tap(lines)
+        self.stream.extend(lines)
         self.stream_event.set()
-        if len(self.stream) > self.HIGH_WATER and not self.paused and self.transport is not None:
+        if len(self.stream) > (self.HIGH_WATER if self.line_tap is None else self.TAPPED_HIGH_WATER) and \
+                not self.paused and self.transport is not None:
             self.paused = True
             self.transport.pause_reading()
+
+    def _tap(self, lines: list) -> None:
+        try:
+            self.line_tap(lines)
+        except Exception:  # noqa: BLE001 — a tap must not break the stream its consumer reads
+            import logging
+            logging.getLogger("ncc.transport").exception("watch line tap failed")
 
     def _finish(self):
         if self.stream is not None:
             if self.linebuf.strip():
-                self.stream.append(bytes(self.linebuf))
+                line = bytes(self.linebuf)
+                if self.line_tap is not None:
+                    self._tap([line])
+                self.stream.append(line)
                 self.linebuf = bytearray()
             self.stream_done = True
             self.stream_event.set()
@@ -296,8 +314,9 @@ class _Conn(asyncio.Protocol):
             self.transport.write(out[0] if len(out) == 1 else b"".join(out))
 
     def resume(self):
+        hw = self.HIGH_WATER if self.line_tap is None else self.TAPPED_HIGH_WATER
         if self.paused and self.transport is not None and self.stream is not None and \
-                len(self.stream) < self.HIGH_WATER // 2:
+                len(self.stream) < hw // 2:
             self.paused = False
             self.transport.resume_reading()
 
@@ -495,13 +514,16 @@ class ConnectionPool:
             self._give_slot()
         raise E.TransportError("unreachable")  # pragma: no cover
 
-    async def stream(self, target: str, headers: dict, timeout: float | None = None, batch: bool = False):
+    async def stream(self, target: str, headers: dict, timeout: float | None = None, batch: bool = False,
+                     on_lines=None):
         """GET with a streaming body; yields complete lines (bytes) — or, with `batch`, lists of all the
         lines that arrived together, so the consumer iterates a plain list instead of resuming this
         generator per line.  Uses a dedicated connection.
 
         `timeout` bounds the whole stream (closing the connection ends it), like a client-side
-        `timeoutSeconds`; waiting itself is a plain Event wait, so cancellation is never swallowed."""
+        `timeoutSeconds`; waiting itself is a plain Event wait, so cancellation is never swallowed.
+        `on_lines(lines)` (a successful stream only) sees every line as soon as it is read off the socket,
+        before the consumer of this generator gets it."""
         c = await self._connect()
         loop = asyncio.get_running_loop()
         head_timer = loop.call_later(self.connect_timeout + 20, self._expire, c, f"GET {target}")
@@ -519,6 +541,10 @@ class ConnectionPool:
                 raw = b"\n".join(c.stream) + bytes(c.linebuf)
                 yield resp, raw
                 return
+            if on_lines is not None:
+                if c.stream:
+                    on_lines(list(c.stream))  # lines that came in with the response head
+                c.line_tap = on_lines
             yield resp, None
             while True:
                 if batch:
