@@ -143,8 +143,10 @@ static void log_at(int level, const char* fmt, ...) {
 #define LOG_DEBUG(...) log_at(10, __VA_ARGS__)
 
 // NCC_CPU_REPORT: CPU cycles per phase of the data plane (rdtsc; reported as shares of the process's CPU)
-enum Phase { PH_RELAY, PH_SHARD_LINE, PH_RESPONSE, PH_BODY, PH_CHANNEL_IN, PH_N };
-static const char* kPhaseName[PH_N] = {"relay_in", "shard_watch", "write_response", "write_body", "channel_read"};
+// relay_decode is the part of relay_in spent reading the lines (the rest: stores, indexes, enqueues)
+enum Phase { PH_RELAY, PH_SHARD_LINE, PH_RESPONSE, PH_BODY, PH_CHANNEL_IN, PH_RELAY_DECODE, PH_N };
+static const char* kPhaseName[PH_N] = {"relay_in", "shard_watch", "write_response", "write_body", "channel_read",
+                                       "relay_decode"};
 static unsigned long long g_phase[PH_N] = {};
 static bool g_phases_on = false;
 static long long g_scan_hits = 0, g_scan_misses = 0;  // write responses read without / with a DOM
@@ -264,6 +266,35 @@ static void dependent_names(const Value* spec, std::vector<std::string>& secrets
     }
 }
 
+// dependent_names of spec.runtimeEnvironment's raw text; false when the scan cannot read it in place (the
+// caller parses)
+static bool dependent_names_rte(std::string_view rte, std::vector<std::string>& secrets, std::vector<std::string>& cms) {
+    auto is_obj = [](std::string_view v) { return !v.empty() && v[0] == '{'; };
+    auto ref = [&](std::string_view r, std::vector<std::string>& out) {
+        if (r == "null") return true;
+        std::string_view name;
+        if (is_obj(r) && !RawCursor(r).members([&](std::string_view k, std::string_view v) {
+                if (k == "name" && !v.empty() && v[0] == '"') return RawCursor(v).str(name);
+                return true;
+            }))
+            return false;
+        out.emplace_back(name);
+        return true;
+    };
+    if (!is_obj(rte)) return true;
+    return RawCursor(rte).members([&](std::string_view k, std::string_view mev) {
+        if (k != "mappedEnvironmentVariables" || mev.empty() || mev[0] != '[') return true;
+        return RawCursor(mev).elements([&](std::string_view ef) {
+            if (!is_obj(ef)) return true;
+            return RawCursor(ef).members([&](std::string_view fk, std::string_view fv) {
+                if (fk == "secretRef") return ref(fv, secrets);
+                if (fk == "configMapRef") return ref(fv, cms);
+                return true;
+            });
+        });
+    });
+}
+
 // Payload members: kept as raw JSON text (fingerprinted, re-sent verbatim), never decoded into a DOM.
 static const std::string_view kPayloadKeys[2][3] = {{"spec", "status", ""}, {"data", "binaryData", "stringData"}};
 static const std::string_view* payload_keys(int kind) { return kPayloadKeys[kind < 2 ? 0 : 1]; }
@@ -317,6 +348,137 @@ static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) 
         c->fp_bin = fp_opt_text(raw[1]);
         c->type = std::string(obj.sget("type"));
         c->owners = template_owner_names(obj);
+    }
+    return c;
+}
+
+// A relayed watch line straight into a CtlObj without a DOM of its metadata (make_ctl's result for the same
+// line); nullptr when the scan meets anything it does not read in place (an escaped string...): the caller
+// parses the line instead.  `type` gets the event type.
+static CtlPtr ctl_scan(int kind, std::string_view line, std::string& type) {
+    PhaseTimer pt(PH_RELAY_DECODE);
+    auto c = std::make_shared<CtlObj>();
+    const std::string_view* keys = payload_keys(kind);
+    size_t nk = payload_count(kind);
+    std::string_view raw[3];
+    bool have_obj = false;
+    auto meta = [&](std::string_view mk, RawCursor& x) {
+        std::string_view mv;
+        if (!x.value(mv)) return false;
+        std::string_view t;
+        if (mk == "name" || mk == "namespace" || mk == "uid" || mk == "resourceVersion") {
+            if (!RawCursor(mv).str(t)) return mv == "null";
+            (mk == "name" ? c->name : mk == "namespace" ? c->ns : mk == "uid" ? c->uid : c->rv).assign(t);
+            return true;
+        }
+        if (mk == "generation") {
+            if (mv.empty() || !(mv[0] == '-' || (mv[0] >= '0' && mv[0] <= '9'))) return mv == "null";
+            c->generation = std::atoll(std::string(mv).c_str());
+            c->has_generation = true;
+            return true;
+        }
+        if (mk == "labels") {
+            c->fp_labels = fp_opt_text(mv);
+            return true;
+        }
+        if (mk == "annotations") {
+            c->fp_ann = fp_opt_text(mv);
+            return true;
+        }
+        if (mk == "ownerReferences" && kind >= 2) {
+            if (mv == "null") return true;
+            return RawCursor(mv).elements([&](std::string_view ref) {
+                std::string_view rk, rn;
+                bool ok = RawCursor(ref).members([&](std::string_view fk, std::string_view fv) {
+                    if (fk == "kind") return RawCursor(fv).str(rk);
+                    if (fk == "name") return RawCursor(fv).str(rn);
+                    return true;
+                });
+                if (ok && rk == kTemplateKind) c->owners.emplace_back(rn);
+                return ok;
+            });
+        }
+        return true;
+    };
+    uint64_t fps[3] = {0, 0, 0};
+    std::string_view rte;  // templates: spec.runtimeEnvironment
+    auto object = [&](std::string_view k, RawCursor& x) {
+        if (k == "metadata") return x.walk(meta);
+        for (size_t i = 0; i < nk; ++i)
+            if (k == keys[i]) {  // fingerprinted as it is skipped: one pass over the payload
+                x.ws();
+                const char* s = x.p;
+                if (kind == TEMPLATES && i == 0 && x.at('{')) {
+                    // the spec member by member (fingerprint's object formula), keeping runtimeEnvironment's span
+                    uint64_t acc = 0, count = 0;
+                    bool spec_ok = x.walk([&](std::string_view sk, RawCursor& y) {
+                        y.ws();
+                        const char* vs = y.p;
+                        const char* end = nullptr;
+                        uint64_t vf = Parser(vs, static_cast<size_t>(y.e - vs)).fingerprint_prefix(&end);
+                        if (sk == "runtimeEnvironment") rte = std::string_view(vs, static_cast<size_t>(end - vs));
+                        acc += Parser::fp_member(Parser::hash_key(sk), vf);
+                        ++count;
+                        y.p = end;
+                        return true;
+                    });
+                    if (!spec_ok) return false;
+                    fps[0] = Parser::fp_object(acc, count);
+                    raw[0] = std::string_view(s, static_cast<size_t>(x.p - s));
+                    return true;
+                }
+                const char* end = nullptr;
+                fps[i] = Parser(s, static_cast<size_t>(x.e - s)).fingerprint_prefix(&end);
+                raw[i] = std::string_view(s, static_cast<size_t>(end - s));
+                x.p = end;
+                return true;
+            }
+        std::string_view v;
+        if (!x.value(v)) return false;
+        if (k == "type" && kind >= 2) {
+            std::string_view t;
+            if (!RawCursor(v).str(t)) return v == "null";
+            c->type.assign(t);
+        }
+        return true;
+    };
+    static const uint64_t kNoMap = fp_opt(nullptr);
+    c->fp_labels = c->fp_ann = kNoMap;
+    auto event = [&](std::string_view k, RawCursor& x) {
+        if (k == "object") {
+            have_obj = true;
+            return x.walk(object);
+        }
+        std::string_view v;
+        if (!x.value(v)) return false;
+        if (k == "type") {
+            std::string_view t;
+            if (!RawCursor(v).str(t)) return false;
+            type.assign(t);
+        }
+        return true;
+    };
+    bool ok = false;
+    try {
+        ok = RawCursor(line).walk(event);
+    } catch (const JsonError&) {
+        return nullptr;  // a malformed payload: the parser path reports it
+    }
+    if (!ok || !have_obj) return nullptr;
+    if (kind == TEMPLATES && !raw_null(raw[0]) && raw[0][0] != '{') return nullptr;  // the parser's error path
+    if (c->ns.empty()) c->ns = g_opt.ns;
+    if (kind < 2) {
+        c->spec_raw.assign(raw[0]);
+        c->fp_spec = raw[0].empty() ? fingerprint(Value()) : fps[0];
+        if (kind == TEMPLATES && !raw_null(raw[0])) {
+            if (!dependent_names_rte(rte, c->secrets, c->configmaps)) return nullptr;
+        }
+    } else {
+        static const uint64_t kNullFp = fingerprint(Value());
+        c->data_raw.assign(raw[0]);
+        c->bin_raw.assign(raw[1]);
+        c->fp_data = raw_is_empty(raw[0]) ? kNullFp : fps[0];
+        c->fp_bin = raw_is_empty(raw[1]) ? kNullFp : fps[1];
     }
     return c;
 }
@@ -1769,6 +1931,10 @@ static void handle_message(const mp::Obj& m) {
             std::vector<CtlPtr>& objs = ex.partial_snapshot[kind];
             objs.reserve(objs.size() + lines->a.size());
             for (const auto& l : lines->a) {
+                if (CtlPtr fast = ctl_scan(kind, l.s, type)) {
+                    if (type == "ADDED" || type == "MODIFIED") objs.push_back(std::move(fast));
+                    continue;
+                }
                 Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
                                                                             payload_count(kind), raw);
                 if (o.is_obj() && (type == "ADDED" || type == "MODIFIED")) objs.push_back(make_ctl(kind, o, raw));
@@ -1779,6 +1945,10 @@ static void handle_message(const mp::Obj& m) {
             objs = std::vector<CtlPtr>();
         } else {
             for (const auto& l : lines->a) {
+                if (CtlPtr fast = ctl_scan(kind, l.s, type)) {
+                    if (type == "ADDED" || type == "MODIFIED" || type == "DELETED") ctl_apply(kind, type, fast);
+                    continue;
+                }
                 Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
                                                                             payload_count(kind), raw);
                 if (o.is_obj() && (type == "ADDED" || type == "MODIFIED" || type == "DELETED"))
@@ -1962,6 +2132,44 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "--decode-bench") {
+        // relayed watch lines (one per stdin line, kind argv[2]): ns per line of the scan and of the parser path
+        int kind = argc > 2 ? std::atoi(argv[2]) : TEMPLATES;
+        std::vector<std::string> lines;
+        static char buf[1 << 20];
+        while (std::fgets(buf, sizeof buf, stdin) != nullptr) {
+            std::string line(buf);
+            while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+            lines.push_back(std::move(line));
+        }
+        if (lines.empty()) return 1;
+        size_t sink = 0;
+        auto run = [&](bool scan) {
+            double best = 1e30;
+            for (int rep = 0; rep < 5; ++rep) {
+                double t0 = now_s();
+                for (const auto& l : lines) {
+                    std::string type;
+                    CtlPtr c;
+                    if (scan) {
+                        c = ctl_scan(kind, l, type);
+                    } else {
+                        std::string_view raw[3];
+                        Value o = Parser(l.data(), l.size()).parse_event_split(type, payload_keys(kind),
+                                                                              payload_count(kind), raw);
+                        c = make_ctl(kind, o, raw);
+                    }
+                    sink += c ? c->name.size() : 0;
+                }
+                best = std::min(best, now_s() - t0);
+            }
+            return best / static_cast<double>(lines.size()) * 1e9;
+        };
+        double dom = run(false), scan = run(true);
+        std::printf("{\"lines\": %zu, \"parser_ns\": %.0f, \"scan_ns\": %.0f, \"sink\": %zu}\n", lines.size(), dom,
+                    scan, sink);
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "--shardobj-selftest") {
         // one JSON object per stdin line -> per kind (template, secret): whether the DOM-free scan took it, and
         // the slim fields + rest text from the scan and from the DOM path (tests/test_native_executor_json.py)
@@ -1982,6 +2190,41 @@ int main(int argc, char** argv) {
             line.assign(buf.data());
             while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
             for (int kind : {TEMPLATES, SECRETS}) {
+                if (line.rfind("{\"type\"", 0) == 0) {  // a watch event: the relayed-line scan vs make_ctl
+                    std::string t1, t2;
+                    CtlPtr fast, slow;
+                    try {
+                        fast = ctl_scan(kind, line, t1);
+                    } catch (const std::exception&) {
+                        std::printf("-1\t0\t-\t-\n");
+                        continue;
+                    }
+                    try {
+                        std::string_view raw[3];
+                        Value o = Parser(line.data(), line.size()).parse_event_split(t2, payload_keys(kind),
+                                                                                    payload_count(kind), raw);
+                        if (o.is_obj()) slow = make_ctl(kind, o, raw);
+                    } catch (const std::exception&) {
+                    }
+                    auto cf = [](const CtlPtr& o, const std::string& t) {
+                        if (!o) return std::string("-");
+                        std::string f = t + "|" + o->ns + "|" + o->name + "|" + o->uid + "|" + o->rv + "|" +
+                                        std::to_string(o->generation) + (o->has_generation ? "g" : "") + "|" +
+                                        std::to_string(o->fp_spec) + "|" + std::to_string(o->fp_data) + "|" +
+                                        std::to_string(o->fp_bin) + "|" + std::to_string(o->fp_labels) + "|" +
+                                        std::to_string(o->fp_ann) + "|" + o->type + "|" + o->spec_raw + "|" +
+                                        o->data_raw + "|" + o->bin_raw + "|";
+                        for (const auto& n : o->secrets) f += n + ",";
+                        f += "|";
+                        for (const auto& n : o->configmaps) f += n + ",";
+                        f += "|";
+                        for (const auto& n : o->owners) f += n + ",";
+                        return f;
+                    };
+                    std::string a = cf(fast, t1), b = cf(slow, t2);
+                    std::printf("%d\t%d\t-\t-\n", fast ? 1 : 0, a == b ? 1 : 0);
+                    continue;
+                }
                 ShardPtr fast = shard_obj_scan(kind, line);
                 ShardPtr slow;
                 try {

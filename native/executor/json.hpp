@@ -20,8 +20,69 @@
 #include <vector>
 #include <charconv>
 #include <system_error>
+#include <emmintrin.h>
 
 namespace ncc {
+
+// ------------------------------------------------------------------------------------ byte search
+// 16 bytes per step (SSE2, part of every x86-64): JSON text is mostly string content and structure-free runs.
+// The first '"' or '\\' in [p, e), or e.
+inline const char* find_quote(const char* p, const char* e) {
+    const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\');
+    while (e - p >= 16) {
+        __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+        int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, b)));
+        if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
+        p += 16;
+    }
+    while (p < e && *p != '"' && *p != '\\') ++p;
+    return p;
+}
+// The first '"', '{', '}', '[' or ']' in [p, e), or e ('[' | 0x20 == '{', ']' | 0x20 == '}').
+inline const char* find_structural(const char* p, const char* e) {
+    const __m128i q = _mm_set1_epi8('"'), lo = _mm_set1_epi8(0x20), open = _mm_set1_epi8('{'),
+                  close = _mm_set1_epi8('}');
+    while (e - p >= 16) {
+        __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+        __m128i f = _mm_or_si128(x, lo);
+        int m = _mm_movemask_epi8(
+            _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_or_si128(_mm_cmpeq_epi8(f, open), _mm_cmpeq_epi8(f, close))));
+        if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
+        p += 16;
+    }
+    while (p < e && *p != '"' && (*p | 0x20) != '{' && (*p | 0x20) != '}') ++p;
+    return p;
+}
+// Past the string whose opening quote is at p (escapes skipped, not checked); nullptr when unterminated.
+inline const char* skip_string_text(const char* p, const char* e) {
+    ++p;
+    while (true) {
+        p = find_quote(p, e);
+        if (p >= e) return nullptr;
+        if (*p == '"') return p + 1;
+        p += 2;  // the escaped character
+    }
+}
+// Past the object or array whose bracket is at p; nullptr when unbalanced.
+inline const char* skip_container_text(const char* p, const char* e) {
+    int depth = 0;
+    while (true) {
+        p = find_structural(p, e);
+        if (p >= e) return nullptr;
+        char c = *p;
+        if (c == '"') {
+            p = skip_string_text(p, e);
+            if (p == nullptr) return nullptr;
+            continue;
+        }
+        if ((c | 0x20) == '{') {
+            ++depth;
+        } else if (--depth == 0) {
+            return p + 1;
+        }
+        ++p;
+    }
+}
 
 struct JsonError : std::runtime_error {
     using std::runtime_error::runtime_error;
@@ -219,6 +280,12 @@ public:
         if (p_ != e_) fail("trailing characters");
         return v;
     }
+    // fingerprint() of the value at the start of the text; `end` gets the position just past it
+    uint64_t fingerprint_prefix(const char** end) {
+        uint64_t h = fp(0);
+        *end = p_;
+        return h;
+    }
     // fingerprint() of the JSON text without building it (same decoding, same hash)
     uint64_t fingerprint_text() {
         uint64_t h = fp(0);
@@ -286,8 +353,7 @@ private:
         if (p_ >= e_) fail("unexpected end");
         char c = *p_;
         if (c == '"') {
-            tmp_.clear();
-            string(tmp_);
+            str_view();  // validates escapes only when there are any
             return;
         }
         if (c == '{' || c == '[') {
@@ -404,8 +470,7 @@ private:
     // the next string's content: a view of the text when it has no escape sequence, else decoded into tmp_
     std::string_view str_view() {
         const char* s = p_ + 1;
-        const char* q = s;
-        while (q < e_ && *q != '"' && *q != '\\') ++q;
+        const char* q = find_quote(s, e_);
         if (q < e_ && *q == '"') {
             p_ = q + 1;
             return std::string_view(s, static_cast<size_t>(q - s));
@@ -415,10 +480,11 @@ private:
         return tmp_;
     }
     static uint64_t hash_str(std::string_view s);
+public:
+    // the pieces fingerprint() composes (a caller walking an object itself combines its members with them)
     static uint64_t hash_key(std::string_view s);
     static uint64_t fp_member(uint64_t key_hash, uint64_t value_fp);
     static uint64_t fp_object(uint64_t acc, uint64_t count);
-public:
     static constexpr uint64_t kArraySeed = 0x6666ULL;
     static constexpr uint64_t kNullFp = 0x9e3779b97f4a7c15ULL;
     static uint64_t fp_array_step(uint64_t h, uint64_t item);
@@ -600,7 +666,7 @@ private:
                 run = p_;
                 continue;
             }
-            ++p_;
+            p_ = find_quote(p_, e_);
         }
     }
 };
@@ -720,49 +786,28 @@ private:
     bool str(std::string_view& out) {
         ws();
         if (p_ >= e_ || *p_ != '"') return false;
-        const char* s = ++p_;
-        while (p_ < e_ && *p_ != '"') {
-            if (*p_ == '\\') return false;
-            ++p_;
-        }
-        if (p_ >= e_) return false;
-        out = std::string_view(s, static_cast<size_t>(p_ - s));
-        ++p_;
+        const char* s = p_ + 1;
+        const char* q = find_quote(s, e_);
+        if (q >= e_ || *q != '"') return false;
+        out = std::string_view(s, static_cast<size_t>(q - s));
+        p_ = q + 1;
         return true;
     }
     bool skip_str() {
-        ++p_;
-        while (p_ < e_) {
-            if (*p_ == '\\') {
-                p_ += 2;
-                continue;
-            }
-            if (*p_++ == '"') return true;
-        }
-        return false;
+        const char* q = skip_string_text(p_, e_);
+        if (q == nullptr) return false;
+        p_ = q;
+        return true;
     }
     bool skip() {
         ws();
         if (p_ >= e_) return false;
         if (*p_ == '"') return skip_str();
         if (*p_ == '{' || *p_ == '[') {
-            int depth = 0;
-            while (p_ < e_) {
-                char c = *p_;
-                if (c == '"') {
-                    if (!skip_str()) return false;
-                    continue;
-                }
-                if (c == '{' || c == '[') ++depth;
-                if (c == '}' || c == ']') {
-                    if (--depth == 0) {
-                        ++p_;
-                        return true;
-                    }
-                }
-                ++p_;
-            }
-            return false;
+            const char* q = skip_container_text(p_, e_);
+            if (q == nullptr) return false;
+            p_ = q;
+            return true;
         }
         const char* s = p_;
         while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n') ++p_;
@@ -855,26 +900,18 @@ struct RawCursor {
     bool str(std::string_view& out) {
         ws();
         if (p >= e || *p != '"') return false;
-        const char* s = ++p;
-        while (p < e && *p != '"') {
-            if (*p == '\\') return false;
-            ++p;
-        }
-        if (p >= e) return false;
-        out = std::string_view(s, static_cast<size_t>(p - s));
-        ++p;
+        const char* s = p + 1;
+        const char* q = find_quote(s, e);
+        if (q >= e || *q != '"') return false;
+        out = std::string_view(s, static_cast<size_t>(q - s));
+        p = q + 1;
         return true;
     }
     bool skip_str() {
-        ++p;
-        while (p < e) {
-            if (*p == '\\') {
-                p += 2;
-                continue;
-            }
-            if (*p++ == '"') return true;
-        }
-        return false;
+        const char* q = skip_string_text(p, e);
+        if (q == nullptr) return false;
+        p = q;
+        return true;
     }
     // skip one value; `span` gets its text
     bool value(std::string_view& span) {
@@ -884,23 +921,9 @@ struct RawCursor {
         if (*p == '"') {
             if (!skip_str()) return false;
         } else if (*p == '{' || *p == '[') {
-            int depth = 0;
-            bool done = false;
-            while (p < e) {
-                char c = *p;
-                if (c == '"') {
-                    if (!skip_str()) return false;
-                    continue;
-                }
-                if (c == '{' || c == '[') ++depth;
-                if ((c == '}' || c == ']') && --depth == 0) {
-                    ++p;
-                    done = true;
-                    break;
-                }
-                ++p;
-            }
-            if (!done) return false;
+            const char* q = skip_container_text(p, e);
+            if (q == nullptr) return false;
+            p = q;
         } else {
             while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' &&
                    *p != '\t')
@@ -920,6 +943,20 @@ struct RawCursor {
             std::string_view k, v;
             if (!str(k) || !expect(':') || !value(v)) return false;
             if (!fn(k, v)) return false;
+            if (expect(',')) continue;
+            return expect('}');
+        }
+    }
+    // members() reading in place: fn(key, *this) consumes the member's value itself (value(), str(), a
+    // nested walk()...), so a member the caller descends into is not skipped first
+    template <class Fn>
+    bool walk(Fn&& fn) {
+        if (!expect('{')) return false;
+        if (expect('}')) return true;
+        while (true) {
+            std::string_view k;
+            if (!str(k) || !expect(':')) return false;
+            if (!fn(k, *this)) return false;
             if (expect(',')) continue;
             return expect('}');
         }

@@ -100,3 +100,43 @@ def test_plain_shard_object_takes_the_scan_path():
     out = subprocess.run([EXE, "--shardobj-selftest"], input=json.dumps(obj) + "\n", capture_output=True, text=True,
                          timeout=60, check=True).stdout.split("\n")[:-1]
     assert [line.split("\t")[:2] for line in out] == [["1", "1"], ["1", "1"]]
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from(["ADDED", "MODIFIED", "DELETED"]), shard_objs,
+                          st.none() | st.integers(0, 50),
+                          st.lists(st.sampled_from(["s1", "s2"]), max_size=2),
+                          st.lists(st.sampled_from(["c1"]), max_size=1)), min_size=1, max_size=15),
+       st.booleans())
+def test_relayed_line_scan_matches_the_dom_path(events, ascii_only):
+    """The executor reads relayed controller-side watch lines without a DOM of their metadata (`ctl_scan`):
+    every field of the resulting object — keys, resourceVersion, generation, label/annotation and payload
+    fingerprints, raw payloads, references, owners — equals what the parser path builds."""
+    texts = []
+    for typ, obj, gen, secs, cms in events:
+        obj = json.loads(json.dumps(obj))
+        if gen is not None:
+            obj["metadata"]["generation"] = gen
+        if isinstance(obj.get("spec"), dict) or "spec" not in obj:
+            obj["spec"] = {"runtimeEnvironment": {"mappedEnvironmentVariables": [
+                {"secretRef": {"name": n}} for n in secs] + [{"configMapRef": {"name": n}} for n in cms]}}
+        texts.append(json.dumps({"type": typ, "object": obj}, ensure_ascii=ascii_only))
+    out = subprocess.run([EXE, "--shardobj-selftest"], input="\n".join(texts) + "\n", capture_output=True,
+                         text=True, timeout=60, check=True).stdout.split("\n")[:-1]
+    assert len(out) == 2 * len(texts)
+    for i, line in enumerate(out):
+        fast, same = line.split("\t")[:2]
+        assert fast != "-1", (texts[i // 2], line)  # the scan never raises on a line the parser reads
+        if fast == "1":
+            assert same == "1", (texts[i // 2], line)
+
+
+def test_plain_relayed_line_takes_the_scan_path():
+    ev = {"type": "MODIFIED", "object": {
+        "apiVersion": "science.sneaksanddata.com/v1", "kind": "NexusAlgorithmTemplate",
+        "metadata": {"name": "t", "namespace": "nexus", "uid": "u", "resourceVersion": "7", "generation": 3,
+                     "labels": {"a": "b"}},
+        "spec": {"runtimeEnvironment": {"mappedEnvironmentVariables": [{"secretRef": {"name": "s"}}]}}}}
+    out = subprocess.run([EXE, "--shardobj-selftest"], input=json.dumps(ev) + "\n", capture_output=True, text=True,
+                         timeout=60, check=True).stdout.split("\n")[:-1]
+    assert [line.split("\t")[:2] for line in out] == [["1", "1"], ["1", "1"]]
