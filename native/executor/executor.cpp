@@ -603,16 +603,25 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body) {
     const std::string_view* keys = payload_keys(kind);
     size_t nk = payload_count(kind);
     std::string_view raw[3];
+    uint64_t fps[3] = {0, 0, 0};
     std::string& rest = s->rest;
     rest.reserve(body.size());
     rest.push_back('{');
     bool first = true;
-    bool ok = RawCursor(body).members([&](std::string_view k, std::string_view v) {
+    bool ok = false;
+    auto member = [&](std::string_view k, RawCursor& x) {
         for (size_t i = 0; i < nk; ++i)
-            if (k == keys[i]) {
-                raw[i] = v;
+            if (k == keys[i]) {  // fingerprinted as it is skipped
+                x.ws();
+                const char* b = x.p;
+                const char* end = nullptr;
+                fps[i] = Parser(b, static_cast<size_t>(x.e - b)).fingerprint_prefix(&end);
+                raw[i] = std::string_view(b, static_cast<size_t>(end - b));
+                x.p = end;
                 return true;
             }
+        std::string_view v;
+        if (!x.value(v)) return false;
         if (!first) rest.push_back(',');
         first = false;
         rest.push_back('"');
@@ -626,15 +635,21 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body) {
             s->type.assign(t);
         }
         return true;
-    });
+    };
+    try {
+        ok = RawCursor(body).walk(member);
+    } catch (const JsonError&) {
+        return nullptr;  // a malformed payload: the parser path reports it
+    }
     if (!ok) return nullptr;
     rest.push_back('}');
     if (s->ns.empty()) s->ns = g_opt.ns;
+    static const uint64_t kNullFp = fingerprint(Value());
     if (kind < 2) {
-        s->fp_spec = raw[0].empty() ? fingerprint(Value()) : fingerprint_text(raw[0]);
+        s->fp_spec = raw[0].empty() ? kNullFp : fps[0];
     } else {
-        s->fp_data = fp_opt_text(raw[0]);
-        s->fp_bin = fp_opt_text(raw[1]);
+        s->fp_data = raw_is_empty(raw[0]) ? kNullFp : fps[0];
+        s->fp_bin = raw_is_empty(raw[1]) ? kNullFp : fps[1];
     }
     return s;
 }
@@ -2129,6 +2144,17 @@ int main(int argc, char** argv) {
             } catch (const std::exception& e) {
                 std::printf("error %s\n", e.what());
             }
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "--skip-selftest") {
+        // one JSON container per stdin line (trailing text allowed) -> the byte offset just past it, or -1
+        static char buf[1 << 20];
+        while (std::fgets(buf, sizeof buf, stdin) != nullptr) {
+            std::string_view line(buf);
+            while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.remove_suffix(1);
+            const char* end = skip_container_text(line.data(), line.data() + line.size());
+            std::printf("%lld\n", end ? static_cast<long long>(end - line.data()) : -1LL);
         }
         return 0;
     }

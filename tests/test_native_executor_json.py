@@ -140,3 +140,27 @@ def test_plain_relayed_line_takes_the_scan_path():
     out = subprocess.run([EXE, "--shardobj-selftest"], input=json.dumps(ev) + "\n", capture_output=True, text=True,
                          timeout=60, check=True).stdout.split("\n")[:-1]
     assert [line.split("\t")[:2] for line in out] == [["1", "1"], ["1", "1"]]
+
+
+_json_leaf = st.none() | st.booleans() | st.integers() | st.text(alphabet=st.sampled_from(
+    list('ab"\\{}[]:, é中') + ["\n"]), max_size=90)
+_json_tree = st.recursive(_json_leaf, lambda kids: st.lists(kids, max_size=6) |
+                          st.dictionaries(st.text(alphabet='ab"\\{[', max_size=8), kids, max_size=6), max_leaves=40)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.tuples(_json_tree.filter(lambda v: isinstance(v, (list, dict))), st.booleans(),
+                          st.sampled_from(["", ",\"x\":1}", "]]", " {\"a\":[1]}"])), min_size=1, max_size=20))
+def test_container_skip_matches_a_json_decoder(cases):
+    """skip_container_text (json.hpp: 64-byte blocks of quote/backslash/bracket bit masks, byte by byte
+    where a block has a backslash) ends each container exactly where a JSON decoder does: strings full of
+    brackets, quotes and backslashes, values straddling block edges, trailing text after the container."""
+    lines, want = [], []
+    for value, compact, tail in cases:
+        text = json.dumps(value, ensure_ascii=False, separators=(",", ":") if compact else None)
+        _, end = json.JSONDecoder().raw_decode(text + tail)
+        lines.append(text + tail)
+        want.append(len((text + tail)[:end].encode()))
+    out = subprocess.run([EXE, "--skip-selftest"], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                         timeout=60, check=True).stdout.split()
+    assert [int(x) for x in out] == want
