@@ -164,3 +164,14 @@ def test_container_skip_matches_a_json_decoder(cases):
     out = subprocess.run([EXE, "--skip-selftest"], input="\n".join(lines) + "\n", capture_output=True, text=True,
                          timeout=60, check=True).stdout.split()
     assert [int(x) for x in out] == want
+
+
+def test_decode_bench_reads_both_paths():
+    """`ncc-executor --decode-bench KIND` (the relayed-line decode microbenchmark) reports a time per line
+    for the parser path and the scan path over the same lines."""
+    ev = {"type": "ADDED", "object": {"metadata": {"name": "s", "namespace": "nexus", "resourceVersion": "1"},
+                                      "data": {"k": "dg=="}}}
+    out = subprocess.run([EXE, "--decode-bench", "2"], input=json.dumps(ev) + "\n", capture_output=True, text=True,
+                         timeout=60, check=True).stdout
+    d = json.loads(out)
+    assert d["lines"] == 1 and d["parser_ns"] > 0 and d["scan_ns"] > 0
