@@ -33,6 +33,8 @@
 #include <fcntl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/time.h>
+#include <ucontext.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -990,6 +992,63 @@ static void dump_trace() {
     for (const auto& r : *g_trace) std::fprintf(f, "%c\t%d\t%s\t%lld\n", r.what, r.kind, r.key.c_str(), r.t_ns);
     std::fclose(f);
 }
+// NCC_SAMPLE_PROFILE=<dir>: a sampling CPU profiler.  SIGPROF fires every `NCC_SAMPLE_US` (default 500) µs of
+// the process's CPU time and records the interrupted instruction's address; on exit the process's
+// executable mappings and the addresses go to <dir>/executor-<index>-<pid>.samples
+// (scripts/executor_profile.py maps them to functions of the executable and its shared libraries, inlined
+// ones included, with addr2line).  Unlike -pg it needs no rebuild and attributes time in coroutine frames and
+// inlined code correctly; time in the kernel lands on the libc system-call wrapper that entered it.
+// Each sample also keeps the word at the top of the stack: in a frameless leaf (memcpy, a system-call
+// wrapper) that is the return address, i.e. the caller.
+static constexpr size_t kMaxSamples = 1 << 20;
+static uintptr_t* g_samples = nullptr;  // pairs: pc, top-of-stack word
+static volatile size_t g_nsamples = 0;
+static void on_sigprof(int, siginfo_t*, void* ucv) {
+    auto* uc = static_cast<ucontext_t*>(ucv);
+    size_t n = g_nsamples;
+    if (n < kMaxSamples) {
+        g_samples[2 * n] = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
+        g_samples[2 * n + 1] = *reinterpret_cast<const uintptr_t*>(uc->uc_mcontext.gregs[REG_RSP]);
+        g_nsamples = n + 1;
+    }
+}
+static void start_sampling() {
+    if (std::getenv("NCC_SAMPLE_PROFILE") == nullptr) return;
+    g_samples = new uintptr_t[2 * kMaxSamples];
+    struct sigaction sa {};
+    sa.sa_sigaction = on_sigprof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGPROF, &sa, nullptr);
+    long us = 500;
+    if (const char* v = std::getenv("NCC_SAMPLE_US")) us = std::max(50L, std::atol(v));
+    struct itimerval it {};
+    it.it_interval.tv_sec = us / 1000000;
+    it.it_interval.tv_usec = us % 1000000;
+    it.it_value = it.it_interval;
+    setitimer(ITIMER_PROF, &it, nullptr);
+}
+static void dump_samples() {
+    const char* dir = std::getenv("NCC_SAMPLE_PROFILE");
+    if (g_samples == nullptr || dir == nullptr) return;
+    struct itimerval off {};
+    setitimer(ITIMER_PROF, &off, nullptr);
+    ::mkdir(dir, 0755);
+    std::string path = std::string(dir) + "/executor-" + std::to_string(g_opt.index) + "-" + std::to_string(getpid()) +
+                       ".samples";
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (f == nullptr) return;
+    if (FILE* maps = std::fopen("/proc/self/maps", "r")) {  // "# map <start>-<end> <perms> <offset> ... <path>"
+        char line[4096];
+        while (std::fgets(line, sizeof line, maps) != nullptr)
+            if (std::strstr(line, " r-xp ") != nullptr) std::fprintf(f, "# map %s", line);
+        std::fclose(maps);
+    }
+    for (size_t i = 0; i < g_nsamples; ++i)
+        std::fprintf(f, "%zx %zx\n", static_cast<size_t>(g_samples[2 * i]), static_cast<size_t>(g_samples[2 * i + 1]));
+    std::fclose(f);
+}
+
 // enqueues by cause (NCC_CPU_REPORT diagnostics): template/workgroup event, dependent event, shard-side
 // template drift, shard-side dependent drift, failure retry, orphan sweep, full resync, delete
 enum EnqCause { ENQ_OBJECT, ENQ_DEPENDENT, ENQ_SHARD_OBJECT, ENQ_SHARD_DEPENDENT, ENQ_RETRY, ENQ_SWEEP, ENQ_RESYNC,
@@ -2281,6 +2340,7 @@ int main(int argc, char** argv) {
     if (const char* h = std::getenv("NCC_DEPENDENT_HOLD")) kDependentHold = std::max(1.0, std::atof(h));
     if (const char* f = std::getenv("NCC_REPORT_FLUSH_MS")) g_flush_interval = std::max(0.0, std::atof(f) / 1000.0);
     g_phases_on = std::getenv("NCC_CPU_REPORT") != nullptr;
+    start_sampling();
     if (std::getenv("NCC_TRACE_STAGES") != nullptr) {
         g_trace = new std::vector<TraceRec>();
         g_trace->reserve(1 << 20);
@@ -2308,6 +2368,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "ncc-executor: fatal: %s\n", e.what());
         return 1;
     }
+    dump_samples();
     std::fflush(stderr);
 #ifdef NCC_GPROF
     _mcleanup();  // profiling builds (-pg): write gmon.out before skipping the exit handlers

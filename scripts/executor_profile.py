@@ -1,0 +1,155 @@
+#!/usr/bin/env python
+"""Where the C++ shard executor spends its CPU: symbolizes the executor's own sampling profile.
+
+Run anything that starts executors with `NCC_SAMPLE_PROFILE=<dir>` (optionally `NCC_SAMPLE_US`, default
+500 µs of CPU between samples); each executor writes `<dir>/executor-<index>-<pid>.samples` on exit: the
+offset, in the executable, of the instruction each SIGPROF interrupted (native/executor/executor.cpp
+`start_sampling`).  This maps the offsets to functions with `addr2line -i` and prints these views:
+
+* self — the innermost function at the sample, inlined functions counted as themselves;
+* frame — the function whose machine code it is (what an inlined helper was inlined into; coroutine bodies
+  show up as their own frames);
+* line — the hottest source lines;
+* library code by caller — time in libc/libstdc++ leaves (memcpy, system-call wrappers) by the executor's
+  call site (the return address on top of the stack at the sample).
+
+    NCC_SAMPLE_PROFILE=/tmp/prof python bench.py --steps 20 --warmup 5
+    python scripts/executor_profile.py /tmp/prof [--binary ncc/bin/ncc-executor] [--top 30]
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import glob
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_samples(paths: list[str]) -> collections.Counter:
+    """((module, address in the module's file), (module, address) of the top-of-stack word, or None when it
+    is not code) -> samples, over every process's file."""
+    counts: collections.Counter = collections.Counter()
+    for p in paths:
+        files = sorted(glob.glob(os.path.join(p, "*.samples"))) if os.path.isdir(p) else [p]
+        for f in files:
+            maps = []  # (start, end, file offset, path)
+            raw: collections.Counter = collections.Counter()
+            with open(f) as fh:
+                for line in fh:
+                    if line.startswith("# map "):
+                        parts = line[6:].split()
+                        lo, hi = (int(x, 16) for x in parts[0].split("-"))
+                        maps.append((lo, hi, int(parts[2], 16), parts[5] if len(parts) > 5 else "[anon]"))
+                    elif line.strip():
+                        words = line.split()
+                        raw[(int(words[0], 16), int(words[1], 16) if len(words) > 1 else 0)] += 1
+
+            def where(addr):
+                for lo, hi, off, path in maps:
+                    if lo <= addr < hi:
+                        return path, addr - lo + off
+                return None
+
+            for (pc, top), n in raw.items():
+                counts[(where(pc) or ("[unknown]", pc), where(top))] += n
+    return counts
+
+
+def short(fn: str, width: int = 110) -> str:
+    fn = re.sub(r"std::__cxx11::basic_string<char, std::char_traits<char>, std::allocator<char> >", "std::string", fn)
+    fn = re.sub(r"std::basic_string_view<char, std::char_traits<char> >", "std::string_view", fn)
+    return fn if len(fn) <= width else fn[:width - 3] + "..."
+
+
+def symbolize(binary: str, addrs: list[int]) -> dict[int, list[tuple[str, str]]]:
+    """address -> inline chain [(function, file:line)], innermost first."""
+    out: dict[int, list[tuple[str, str]]] = {}
+    chunk = 20000
+    for lo in range(0, len(addrs), chunk):
+        batch = addrs[lo:lo + chunk]
+        r = subprocess.run(["addr2line", "-a", "-f", "-C", "-i", "-e", binary], input="\n".join(f"{a:x}" for a in batch),
+                           capture_output=True, text=True, check=True)
+        cur = None
+        lines = r.stdout.splitlines()
+        i = 0
+        while i < len(lines):
+            line = lines[i]
+            if line.startswith("0x"):
+                cur = int(line, 16)
+                out[cur] = []
+                i += 1
+                continue
+            fn = line
+            loc = lines[i + 1] if i + 1 < len(lines) else "??:0"
+            out[cur].append((fn, os.path.relpath(loc, ROOT) if loc.startswith(ROOT) else loc))
+            i += 2
+    return out
+
+
+def report(counts: collections.Counter, binary: str, top: int) -> str:
+    total = sum(counts.values())
+    if not total:
+        return "no samples"
+    chains = {}
+    modules: collections.Counter = collections.Counter()
+    wanted = collections.defaultdict(set)
+    for (pc, tos), n in counts.items():
+        modules[os.path.basename(pc[0])] += n
+        wanted[pc[0]].add(pc[1])
+        if tos is not None and pc[0] != os.path.realpath(binary) and tos[0] == os.path.realpath(binary):
+            wanted[tos[0]].add(tos[1])
+    for path, addrs in wanted.items():
+        if os.path.isfile(path):
+            for a, chain in symbolize(path, sorted(addrs)).items():
+                chains[(path, a)] = chain
+    self_c: collections.Counter = collections.Counter()
+    frame_c: collections.Counter = collections.Counter()
+    line_c: collections.Counter = collections.Counter()
+    lib_c: collections.Counter = collections.Counter()
+    for (pc, tos), n in counts.items():
+        path = pc[0]
+        chain = chains.get(pc) or [("??", "??:0")]
+        ours = os.path.realpath(path) == os.path.realpath(binary)
+        tag = "" if ours else f"  [{os.path.basename(path)}]"
+        self_c[chain[0][0] + tag] += n
+        frame_c[chain[-1][0] + tag] += n
+        line_c[f"{chain[0][1].split(' ')[0]}  ({short(chain[0][0], 50)}){tag}"] += n
+        if not ours:  # a leaf in a library: its caller is the return address on top of the stack
+            caller = chains.get(tos) if tos is not None else None
+            who = f"{caller[0][1].split(' ')[0]} ({short(caller[-1][0], 60)})" if caller else "?"
+            lib_c[f"{chain[0][0]}{tag}  <-  {who}"] += n
+    out = [f"{total} samples"]
+    out.append("\n== module")
+    for name, n in modules.most_common():
+        out.append(f"{100.0 * n / total:6.2f}%  {n:7d}  {name}")
+    for title, c in (("self (innermost function, inlined code counted as itself)", self_c),
+                     ("frame (the function whose code ran: inlined helpers folded into their caller)", frame_c),
+                     ("line", line_c),
+                     ("library code by caller (the executor's call site that entered it)", lib_c)):
+        out.append(f"\n== {title}")
+        for name, n in c.most_common(top):
+            out.append(f"{100.0 * n / total:6.2f}%  {n:7d}  {short(name)}")
+    return "\n".join(out)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("paths", nargs="+", help="NCC_SAMPLE_PROFILE directories or .samples files")
+    ap.add_argument("--binary", default=os.path.join(ROOT, "ncc", "bin", "ncc-executor"))
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    text = report(load_samples(a.paths), a.binary, a.top)
+    print(text)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(text + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -122,3 +122,36 @@ async def test_rogue_dependent_report_is_typed():
             await ex.close()
     finally:
         await srv.stop()
+
+
+async def test_sampling_profile_is_written_and_symbolized(tmp_path):
+    """NCC_SAMPLE_PROFILE: the executor samples its own CPU (SIGPROF) and writes the executable mappings and
+    the sampled addresses on exit; scripts/executor_profile.py maps them to functions."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "executor_profile", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                         "executor_profile.py"))
+    prof = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(prof)
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        tpl = make_template(0, NS, secrets=["s0"])
+        tpl["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        sec = make_secret("s0", NS)
+        sec["metadata"].update(uid="u-s", resourceVersion="11")
+        async with Executor(cfg([{"name": "shard-0", "server": url}]),
+                            env={"NCC_SAMPLE_PROFILE": str(tmp_path), "NCC_SAMPLE_US": "50"}) as ex:
+            for k, objs in ((0, [tpl]), (1, []), (2, [sec]), (3, [])):
+                ex.snapshot(k, objs)
+            await ex.next_message("report")
+            await ex.close()
+    finally:
+        await srv.stop()
+    files = list(tmp_path.glob("executor-0-*.samples"))
+    assert len(files) == 1
+    text = files[0].read_text()
+    assert "# map " in text and "ncc-executor" in text
+    counts = prof.load_samples([str(tmp_path)])
+    out = prof.report(counts, binary_path(), 10)
+    assert out.split()[0].isdigit() and "== self" in out if counts else out == "no samples"
