@@ -2009,9 +2009,13 @@ static void handle_message(const mp::Obj& m) {
                     if (type == "ADDED" || type == "MODIFIED") objs.push_back(std::move(fast));
                     continue;
                 }
-                Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
-                                                                            payload_count(kind), raw);
-                if (o.is_obj() && (type == "ADDED" || type == "MODIFIED")) objs.push_back(make_ctl(kind, o, raw));
+                try {
+                    Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
+                                                                                payload_count(kind), raw);
+                    if (o.is_obj() && (type == "ADDED" || type == "MODIFIED")) objs.push_back(make_ctl(kind, o, raw));
+                } catch (const std::exception& e) {  // one bad line costs that object, not the rest of the batch
+                    LOG_ERROR("unreadable relayed line (kind %d): %s", kind, e.what());
+                }
             }
             const mp::Obj* more = m.get("more");
             if (more != nullptr && more->t == mp::Obj::BOOL && more->b) return;
@@ -2023,10 +2027,16 @@ static void handle_message(const mp::Obj& m) {
                     if (type == "ADDED" || type == "MODIFIED" || type == "DELETED") ctl_apply(kind, type, fast);
                     continue;
                 }
-                Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
-                                                                            payload_count(kind), raw);
-                if (o.is_obj() && (type == "ADDED" || type == "MODIFIED" || type == "DELETED"))
-                    ctl_apply(kind, type, make_ctl(kind, o, raw));
+                CtlPtr parsed;
+                try {
+                    Value o = Parser(l.s.data(), l.s.size()).parse_event_split(type, payload_keys(kind),
+                                                                                payload_count(kind), raw);
+                    if (o.is_obj() && (type == "ADDED" || type == "MODIFIED" || type == "DELETED"))
+                        parsed = make_ctl(kind, o, raw);
+                } catch (const std::exception& e) {  // one bad line costs that object, not the rest of the batch
+                    LOG_ERROR("unreadable relayed line (kind %d): %s", kind, e.what());
+                }
+                if (parsed) ctl_apply(kind, type, parsed);
             }
         }
     } else if (t == "go") {

@@ -155,3 +155,28 @@ async def test_sampling_profile_is_written_and_symbolized(tmp_path):
     counts = prof.load_samples([str(tmp_path)])
     out = prof.report(counts, binary_path(), 10)
     assert out.split()[0].isdigit() and "== self" in out if counts else out == "no samples"
+
+
+async def test_unreadable_relayed_line_costs_only_itself():
+    """A relayed watch batch with an unreadable line: the executor logs it and applies the rest of the batch
+    (the template after it is still synced and reported)."""
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        t0 = make_template(0, NS)
+        t0["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        t1 = make_template(1, NS)
+        t1["metadata"].update(uid="u-1", resourceVersion="11", generation=1)
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, [t0]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            assert (await ex.next_message("report"))["k"] == "template/nexus/algo-00000"
+            ex.ch.send({"t": "w", "k": 0, "l": [b'{"type":"ADDED","object":{"metadata":{"name":"x"},"spec":{,}}}',
+                                                 line(t1)]})
+            rep = await ex.next_message("report")
+            assert rep["k"] == "template/nexus/algo-00001" and rep["r"]["shard-0"] is None
+            assert srv.state.get(R.TEMPLATES, NS, "algo-00001") is not None
+            err = await ex.close()
+        assert "unreadable relayed line" in err
+    finally:
+        await srv.stop()
