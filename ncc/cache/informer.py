@@ -36,6 +36,7 @@ from ..kube.client import KubeClient
 from .store import Store
 
 log = logging.getLogger("ncc.informer")
+_UNREADABLE = (ValueError, AttributeError, TypeError)  # a relayed line that is not a JSON watch event
 
 
 @dataclass(frozen=True)
@@ -452,16 +453,33 @@ class Informer:
                 loads = loads_fast
                 items = []
                 for line in lines:
-                    ev = loads(line)
+                    try:
+                        ev = loads(line)
+                        ev.get("type")
+                    except (ValueError, AttributeError) as e:
+                        log.error("%s: unreadable relayed line skipped: %s", self.name, e)
+                        continue
                     if ev.get("type") in ("ADDED", "MODIFIED"):
                         items.append(ev.get("object") or {})
                 await self._replace_items(items)
-            elif ctx is not None:
-                self.last_rv = await self._consume(lines, ctx, self.last_rv)
-            else:
+                continue
+            try:
+                await self._feed_lines(lines, ctx)
+            except _UNREADABLE:
+                # an unreadable line costs that object, not the rest of its batch: again line by line
                 for line in lines:
-                    ev = loads_fast(line)
-                    self.last_rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, self.last_rv)
+                    try:
+                        await self._feed_lines([line], ctx)
+                    except _UNREADABLE as e:
+                        log.error("%s: unreadable relayed line skipped: %s", self.name, e)
+
+    async def _feed_lines(self, lines: list, ctx) -> None:
+        if ctx is not None:
+            self.last_rv = await self._consume(lines, ctx, self.last_rv)
+            return
+        for line in lines:
+            ev = loads_fast(line)
+            self.last_rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, self.last_rv)
 
     async def _run(self) -> None:
         if self.feed is not None:

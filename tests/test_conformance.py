@@ -463,3 +463,29 @@ def test_snapshot_messages_and_deliver_reassemble():
         assert deliver(feeds, m)
     assert list(feeds[2]._items) == [("s", lines)] and feeds[2].partial == []
     assert snapshot_messages(1, []) == [{"t": "s", "k": 1, "l": []}]
+
+
+async def test_python_feed_skips_an_unreadable_line():
+    """The Python executor's relay feed: an unreadable line (in a snapshot or a watch batch) is logged and
+    skipped; the other lines of its batch still reach the cache (the C++ executor's twin is in
+    tests/test_native_executor_direct.py)."""
+    import json
+    from ncc.cache.informer import Informer
+    from ncc.controller.relay import RelayFeed
+    inf = Informer(None, R.SECRETS, "nexus", name="secrets")
+    inf.feed = RelayFeed()
+    task = asyncio.ensure_future(inf._run_feed())
+
+    def ev(name):
+        return json.dumps({"type": "ADDED", "object": make_secret(name, "nexus")}).encode()
+    try:
+        inf.feed.put("s", [b"{bad", ev("s1"), b"[1]"])
+        inf.feed.put("w", [b"[1]", ev("s2"), b'{"type": "ADDED", "object": {,}}', ev("s3")])
+        for _ in range(200):
+            if inf.store.get("nexus", "s3") is not None:
+                break
+            await asyncio.sleep(0.01)
+        assert [inf.store.get("nexus", n) is not None for n in ("s1", "s2", "s3")] == [True, True, True]
+        assert not task.done()
+    finally:
+        task.cancel()
