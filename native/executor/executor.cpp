@@ -42,6 +42,7 @@
 #include <chrono>
 #include <x86intrin.h>
 #include <csignal>
+#include <functional>
 #include <optional>
 #include <cstdarg>
 #include <cstdio>
@@ -2212,6 +2213,94 @@ int main(int argc, char** argv) {
                             render.c_str());
             } catch (const std::exception& e) {
                 std::printf("error %s\n", e.what());
+            }
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "--msgpack-selftest") {
+        // one hex-encoded msgpack value per stdin line -> "<decoded value as JSON>\t<hex of its re-encoding>"
+        // (maps as [[key, value], ...], bin as {"bin": "<hex>"}; "-" when the value holds a type the
+        // executor never sends: float, bin), or "error" (tests/test_native_executor_json.py)
+        static char buf[1 << 20];
+        std::function<void(std::string&, const mp::Obj&)> render = [&](std::string& out, const mp::Obj& o) {
+            char num[64];
+            switch (o.t) {
+                case mp::Obj::NIL: out += "null"; break;
+                case mp::Obj::BOOL: out += o.b ? "true" : "false"; break;
+                case mp::Obj::INT: out += std::to_string(o.i); break;
+                case mp::Obj::FLOAT: std::snprintf(num, sizeof num, "%.17g", o.d); out += num; break;
+                case mp::Obj::STR: write_string(out, o.s); break;
+                case mp::Obj::BIN: {
+                    out += "{\"bin\":\"";
+                    for (unsigned char ch : o.s) {
+                        std::snprintf(num, sizeof num, "%02x", ch);
+                        out += num;
+                    }
+                    out += "\"}";
+                    break;
+                }
+                case mp::Obj::ARR:
+                    out += '[';
+                    for (size_t k = 0; k < o.a.size(); ++k) {
+                        if (k) out += ',';
+                        render(out, o.a[k]);
+                    }
+                    out += ']';
+                    break;
+                case mp::Obj::MAP:
+                    out += '[';
+                    for (size_t k = 0; k < o.m.size(); ++k) {
+                        if (k) out += ',';
+                        out += '[';
+                        render(out, o.m[k].first);
+                        out += ',';
+                        render(out, o.m[k].second);
+                        out += ']';
+                    }
+                    out += ']';
+                    break;
+            }
+        };
+        std::function<bool(mp::Encoder&, const mp::Obj&)> encode = [&](mp::Encoder& en, const mp::Obj& o) {
+            switch (o.t) {
+                case mp::Obj::NIL: en.nil(); return true;
+                case mp::Obj::BOOL: en.boolean(o.b); return true;
+                case mp::Obj::INT: en.integer(o.i); return true;
+                case mp::Obj::STR: en.str(o.s); return true;
+                case mp::Obj::ARR:
+                    en.array(o.a.size());
+                    for (const auto& x : o.a)
+                        if (!encode(en, x)) return false;
+                    return true;
+                case mp::Obj::MAP:
+                    en.map(o.m.size());
+                    for (const auto& kv : o.m)
+                        if (!encode(en, kv.first) || !encode(en, kv.second)) return false;
+                    return true;
+                default: return false;
+            }
+        };
+        while (std::fgets(buf, sizeof buf, stdin) != nullptr) {
+            std::string hex(buf), body;
+            while (!hex.empty() && (hex.back() == '\n' || hex.back() == '\r')) hex.pop_back();
+            for (size_t k = 0; k + 1 < hex.size(); k += 2) body.push_back(static_cast<char>(std::stoi(hex.substr(k, 2), nullptr, 16)));
+            try {
+                mp::Obj o = mp::decode(body);
+                std::string out;
+                render(out, o);
+                mp::Encoder en;
+                std::string re = "-";
+                if (encode(en, o)) {
+                    re.clear();
+                    for (unsigned char ch : en.out) {
+                        char h[3];
+                        std::snprintf(h, sizeof h, "%02x", ch);
+                        re += h;
+                    }
+                }
+                std::printf("%s\t%s\n", out.c_str(), re.c_str());
+            } catch (const std::exception&) {
+                std::printf("error\n");
             }
         }
         return 0;

@@ -113,6 +113,9 @@ def main(argv=None) -> int:
         tot = sum(r[1] for r in rows)
         hits = sum(r[2] for r in rows)
         report.append(f"{'total':<36} {tot:>7} {hits:>7} {100.0 * hits / max(tot, 1):>6.1f}%")
+        for name, total, hit, missing in rows:
+            if missing and not name.endswith("executor.cpp"):
+                report.append(f"{os.path.basename(name)} unexecuted lines: {ranges(missing)}")
         if gate is None:
             report.append("executor.cpp: no coverage data")
             ok = False

@@ -175,3 +175,51 @@ def test_decode_bench_reads_both_paths():
                          timeout=60, check=True).stdout
     d = json.loads(out)
     assert d["lines"] == 1 and d["parser_ns"] > 0 and d["scan_ns"] > 0
+
+
+_mp_leaf = (st.none() | st.booleans() | st.integers(-(2 ** 63), 2 ** 63 - 1) |
+            st.floats(allow_nan=False, allow_infinity=False, min_value=-1e38, max_value=1e38) |
+            st.text(max_size=300) | st.binary(max_size=300))
+_mp_tree = st.recursive(_mp_leaf, lambda kids: st.lists(kids, max_size=20) |
+                        st.dictionaries(st.text(max_size=6), kids, max_size=20), max_leaves=60)
+
+
+def _mp_expect(v):
+    if isinstance(v, dict):
+        return [[k, _mp_expect(x)] for k, x in v.items()]
+    if isinstance(v, list):
+        return [_mp_expect(x) for x in v]
+    if isinstance(v, bytes):
+        return {"bin": v.hex()}
+    return v
+
+
+def _mp_encodable(v):
+    if isinstance(v, dict):
+        return all(_mp_encodable(x) for x in v.values())
+    if isinstance(v, list):
+        return all(_mp_encodable(x) for x in v)
+    return not isinstance(v, (float, bytes))
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(_mp_tree, st.booleans()), min_size=1, max_size=10))
+def test_msgpack_decoder_and_encoder_against_msgpack(values):
+    """The executor's msgpack layer (native/executor/msgpack.hpp, the socketpair protocol) against the Python
+    msgpack package: every width of int/str/bin/array/map, single and double floats, and nesting decode to
+    the same value; what the executor itself sends (no floats, no bin) re-encodes to bytes msgpack reads back
+    as the same value."""
+    import msgpack
+    blobs = [msgpack.packb(v, use_bin_type=True, use_single_float=single) for v, single in values]
+    blobs.append(b"\xc1")  # never used: an error, not a crash
+    out = subprocess.run([EXE, "--msgpack-selftest"], input="\n".join(b.hex() for b in blobs) + "\n",
+                         capture_output=True, text=True, timeout=60, check=True).stdout.split("\n")[:-1]
+    assert len(out) == len(blobs) and out[-1] == "error"
+    for (v, single), line in zip(values, out):
+        rendered, re = line.split("\t")
+        want = msgpack.unpackb(msgpack.packb(v, use_single_float=single), raw=False) if single else v
+        assert json.loads(rendered) == _mp_expect(want)
+        if _mp_encodable(v):
+            assert msgpack.unpackb(bytes.fromhex(re), raw=False, strict_map_key=False) == v
+        else:
+            assert re == "-"
