@@ -42,20 +42,37 @@ struct ApiError : std::runtime_error {
     int code;
     std::string reason;
     ApiError(int c, std::string r, const std::string& msg) : std::runtime_error(msg), code(c), reason(std::move(r)) {}
-    // the Python class name the coordinator sees in reports (ncc/kube/errors.py)
+    // the Python class name the coordinator sees in reports: ncc/kube/errors.py `from_status` — the class of
+    // the Status reason when its code agrees, else the class of the HTTP code, else ApiError
     const char* kind() const {
-        if (reason == "AlreadyExists") return "AlreadyExists";
-        if (reason == "Gone" || code == 410) return "Gone";
+        struct ByReason {
+            const char* reason;
+            int code;
+            const char* cls;
+        };
+        static const ByReason by_reason[] = {
+            {"BadRequest", 400, "BadRequest"}, {"Unauthorized", 401, "Unauthorized"}, {"Forbidden", 403, "Forbidden"},
+            {"NotFound", 404, "NotFound"}, {"MethodNotAllowed", 405, "MethodNotAllowed"},
+            {"AlreadyExists", 409, "AlreadyExists"}, {"Conflict", 409, "Conflict"}, {"Expired", 410, "Gone"},
+            {"Invalid", 422, "Invalid"}, {"TooManyRequests", 429, "TooManyRequests"},
+            {"InternalError", 500, "InternalError"}, {"ServiceUnavailable", 503, "ServiceUnavailable"},
+            {"Timeout", 504, "Timeout"}};
+        for (const auto& r : by_reason)
+            if (reason == r.reason && (r.code == code || code == 0)) return r.cls;
         switch (code) {
             case 400: return "BadRequest";
             case 401: return "Unauthorized";
             case 403: return "Forbidden";
             case 404: return "NotFound";
-            case 409: return "Conflict";
+            case 405: return "MethodNotAllowed";
+            case 409: return reason == "AlreadyExists" ? "AlreadyExists" : "Conflict";
+            case 410: return "Gone";
             case 422: return "Invalid";
             case 429: return "TooManyRequests";
+            case 500: return "InternalError";
             case 503: return "ServiceUnavailable";
-            default: return code >= 500 ? "InternalError" : "ApiError";
+            case 504: return "Timeout";
+            default: return "ApiError";
         }
     }
     bool not_found() const { return code == 404; }

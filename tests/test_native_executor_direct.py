@@ -180,3 +180,30 @@ async def test_unreadable_relayed_line_costs_only_itself():
         assert "unreadable relayed line" in err
     finally:
         await srv.stop()
+
+
+@pytest.mark.parametrize("code,reason", [(400, ""), (401, ""), (403, ""), (405, ""), (422, "Invalid"), (429, ""),
+                                         (500, ""), (502, ""), (503, ""), (504, ""), (418, ""), (500, "Forbidden")])
+async def test_failure_class_matches_the_python_client(code, reason):
+    """A shard answering a write with an error status: the C++ executor's report names the failure with the
+    class the Python client (ncc/kube/errors.py `from_status`) gives the same response, so status messages
+    and Events read the same under either executor."""
+    from ncc.kube import errors as E
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        srv.faults.update({"rules": [{"method": m, "resource": "nexusalgorithmtemplates", "code": code,
+                                      "reason": reason, "count": 1} for m in ("POST", "PUT", "PATCH")]})
+        tpl = make_template(0, NS)
+        tpl["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, [tpl]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            rep = await ex.next_message("report")
+            await ex.close()
+    finally:
+        await srv.stop()
+    wire = E.from_status(code, {"reason": reason, "message": "injected fault"})  # what the fake server sends
+    want = type(E.from_status(code, {"reason": wire.reason, "message": str(wire)})).__name__
+    f = rep["r"]["shard-0"]
+    assert f["c"] == want and f["h"] == code, f
