@@ -207,3 +207,46 @@ async def test_failure_class_matches_the_python_client(code, reason):
     want = type(E.from_status(code, {"reason": wire.reason, "message": str(wire)})).__name__
     f = rep["r"]["shard-0"]
     assert f["c"] == want and f["h"] == code, f
+
+
+@pytest.mark.skipif(__import__("shutil").which("openssl") is None, reason="openssl CLI needed to mint test certificates")
+@pytest.mark.parametrize("case", ["ok", "wrong-ca", "no-client-cert", "insecure-skip", "server-name-ok",
+                                  "server-name-wrong"])
+async def test_tls_shard_connections(tmp_path, case):
+    """The C++ executor's OpenSSL client against a mutual-TLS shard apiserver (the Python client's twin is
+    tests/test_tls.py): verification against the kubeconfig CA, the client certificate, insecure-skip-tls-verify
+    and tls-server-name.  A refused handshake is a TransportError failure in the report, not a crash."""
+    from ncc.testing.env import FakeEnvironment
+    from ncc.testing.pki import make_pki
+    env = await FakeEnvironment(1, str(tmp_path), tls=True).start()
+    try:
+        pki = env.pki
+        shard = {"name": "shard-0", "server": env.shard_urls[0], "ca_pem": pki.ca_data.decode(),
+                 "cert_pem": pki.client_cert_data.decode(), "key_pem": pki.client_key_data.decode()}
+        other = make_pki(str(tmp_path / "other")) if case in ("wrong-ca", "insecure-skip") else None
+        if case == "wrong-ca":
+            shard["ca_pem"] = other.ca_data.decode()
+        elif case == "no-client-cert":
+            shard["cert_pem"] = shard["key_pem"] = ""
+        elif case == "insecure-skip":
+            shard.update(ca_pem=other.ca_data.decode(), insecure=True)
+        elif case == "server-name-ok":
+            shard["tls_server_name"] = "kube.test"
+        elif case == "server-name-wrong":
+            shard["tls_server_name"] = "not-in-the-cert.example"
+        tpl = make_template(0, NS)
+        tpl["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        ok = case in ("ok", "insecure-skip", "server-name-ok")
+        async with Executor(cfg([shard], shard_sync_timeout=1.0)) as ex:
+            for k, objs in ((0, [tpl]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            rep = await ex.next_message("report", timeout=15)
+            err = await ex.close()
+        f = rep["r"]["shard-0"]
+        if ok:
+            assert f is None, (f, err[-2000:])
+            assert env.shard_servers[0].state.get(R.TEMPLATES, NS, "algo-00000") is not None
+        else:
+            assert f is not None and f["c"] in ("TransportError", "ShardNotReadyError"), f
+    finally:
+        await env.stop()
