@@ -11,8 +11,10 @@ Test/bench control endpoints (not part of the Kubernetes API):
   POST /_fake/faults   {"latency_ms", "jitter_ms", "error_rate", "error_code", "throttle_rate",
                         "down", "drop_watches", "compact", "rules"} — fault injection for the
                        retry/backoff benchmark (BASELINE.json config 5) and for targeted tests:
-                       `rules` = [{"method", "resource", "name", "code", "reason", "count"}, ...] fail
-                       the matching requests ("*" or absent = any; `count` answers, -1 = until cleared)
+                       `rules` = [{"method", "resource", "name", "code", "reason", "count",
+                       "retry_after", "after"}, ...] fail the matching requests ("*" or absent = any;
+                       `count` answers, -1 = until cleared; `retry_after` seconds go out as a Retry-After
+                       header; `after`: serve the request, then answer with the error)
   GET  /_fake/writes   the mutating requests served so far ([method, plural, name, subresource, status])
   POST /_fake/objects  bulk create `{"items": [...]}` without per-request overhead (bench seeding)
   POST /_fake/apply    `{"items": [...], "yield_every": n}` create-or-update a wave of user changes,
@@ -84,6 +86,8 @@ class Faults:
                 r["count"] -= 1
             err = E.from_status(int(r.get("code", 500)), {"reason": r.get("reason", ""),
                                                           "message": r.get("message", "injected fault")})
+            if r.get("retry_after") is not None:  # answered with a Retry-After header
+                err.retry_after = float(r["retry_after"])
             return err, bool(r.get("after"))
         return None
 

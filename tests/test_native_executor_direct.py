@@ -250,3 +250,54 @@ async def test_tls_shard_connections(tmp_path, case):
             assert f is not None and f["c"] in ("TransportError", "ShardNotReadyError"), f
     finally:
         await env.stop()
+
+
+async def test_retry_after_is_honoured():
+    """A 429 with Retry-After: the C++ client waits and sends the request again (at most 5 times, ≤ 10 s
+    each); the pass succeeds and no failure is reported."""
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        srv.faults.update({"rules": [{"method": "POST", "resource": "nexusalgorithmtemplates", "code": 429,
+                                      "retry_after": 1, "count": 2}]})
+        tpl = make_template(0, NS)
+        tpl["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, [tpl]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            t0 = asyncio.get_running_loop().time()
+            rep = await ex.next_message("report", timeout=20)
+            waited = asyncio.get_running_loop().time() - t0
+            await ex.close()
+        assert rep["r"]["shard-0"] is None and waited >= 1.9
+        assert srv.state.get(R.TEMPLATES, NS, "algo-00000") is not None
+        assert srv.faults.rules[0]["count"] == 0
+    finally:
+        await srv.stop()
+
+
+async def test_token_file_is_reread_on_401(tmp_path):
+    """A rotated bound service-account token: the shard starts answering 401 to the old token; the client
+    re-reads its token file once and retries with the new token (no failure reported)."""
+    srv = FakeApiServer(name="shard-0", token="t1")
+    url = await srv.start()
+    tok = tmp_path / "token"
+    tok.write_text("t1\n")
+    try:
+        t0 = make_template(0, NS)
+        t0["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        t1 = make_template(1, NS)
+        t1["metadata"].update(uid="u-1", resourceVersion="11", generation=1)
+        async with Executor(cfg([{"name": "shard-0", "server": url, "token_file": str(tok)}])) as ex:
+            for k, objs in ((0, [t0]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            assert (await ex.next_message("report"))["r"]["shard-0"] is None
+            srv.token = "t2"  # rotation: the server now wants the new token, which the file holds
+            tok.write_text("t2\n")
+            ex.ch.send({"t": "w", "k": 0, "l": [line(t1)]})
+            rep = await ex.next_message("report", timeout=15)
+            await ex.close()
+        assert rep["k"] == "template/nexus/algo-00001" and rep["r"]["shard-0"] is None, rep
+        assert srv.state.get(R.TEMPLATES, NS, "algo-00001") is not None
+    finally:
+        await srv.stop()
