@@ -428,6 +428,39 @@ async def test_workgroup_fanout_update_and_delete(tmp_path, impl):
                                                     for s in cl.sstates)))
 
 
+async def test_updates_and_new_references_propagate(tmp_path, impl):
+    """Controller-side changes reach every shard: a template spec change, Secret/ConfigMap payload changes,
+    and a reference added to the template (the new dependent is created on the shards, owned by the template,
+    listed in the status); the template stays Ready throughout."""
+    async with Cluster(tmp_path, impl) as cl:
+        cl.seed()
+        cl.cstate.create(R.SECRETS, NS, make_secret("s1", NS, version=5))
+        await cl.start()
+        await cl.ready()
+        await mutate(cl.cc, R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("versionTag", "v9"))
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o["data"].__setitem__("extra", "eA=="))
+        await mutate(cl.cc, R.CONFIGMAPS, "c0", lambda o: o["data"].__setitem__("extra", "x"))
+
+        async def propagated():
+            return all(s.get(R.TEMPLATES, NS, T0)["spec"]["container"]["versionTag"] == "v9" and
+                       s.get(R.SECRETS, NS, "s0")["data"].get("extra") == "eA==" and
+                       s.get(R.CONFIGMAPS, NS, "c0")["data"].get("extra") == "x" for s in cl.sstates)
+        await wait_for(propagated)
+
+        def add_ref(o):
+            o["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"].append({"secretRef": {"name": "s1"}})
+        await mutate(cl.cc, R.TEMPLATES, T0, add_ref)
+
+        async def new_dep():
+            st = cl.status()
+            return sorted(st.get("syncedSecrets") or []) == ["s0", "s1"] and all(
+                s.try_get(R.SECRETS, NS, "s1") is not None and
+                [r["name"] for r in s.get(R.SECRETS, NS, "s1")["metadata"]["ownerReferences"]] == [T0] and
+                s.get(R.SECRETS, NS, "s1")["data"] == cl.cstate.get(R.SECRETS, NS, "s1")["data"] for s in cl.sstates)
+        await wait_for(new_dep)
+        await cl.ready()
+
+
 def test_every_implementation_is_exercised():
     """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
     if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
