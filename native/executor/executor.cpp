@@ -315,12 +315,14 @@ struct CtlObj {
     std::string type;  // Secret.type ("" = Opaque)
     std::vector<std::string> secrets, configmaps;  // templates
     std::vector<std::string> owners;               // NexusAlgorithmTemplate owner names (dependents)
+    double recv_at = 0;                            // when this version reached the executor (now_s)
 };
 using CtlPtr = std::shared_ptr<const CtlObj>;
 
 // `obj`: the object without its payload members; `raw`: their text (payload_keys order, empty = absent)
 static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) {
     auto c = std::make_shared<CtlObj>();
+    c->recv_at = now_s();
     const Value* m = meta_of(obj);
     if (m) {
         c->ns = std::string(m->sget("namespace"));
@@ -361,6 +363,7 @@ static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) 
 static CtlPtr ctl_scan(int kind, std::string_view line, std::string& type) {
     PhaseTimer pt(PH_RELAY_DECODE);
     auto c = std::make_shared<CtlObj>();
+    c->recv_at = now_s();
     const std::string_view* keys = payload_keys(kind);
     size_t nk = payload_count(kind);
     std::string_view raw[3];
@@ -1182,6 +1185,14 @@ static void ctl_snapshot(int kind, std::vector<CtlPtr> objs) {
 
 // templates referencing the dependent, then template owners that no longer reference it
 // (handleObject's ownerRef walk, controller.go:206-223; native: reverse index first)
+// The hold of a pass a dependent's event triggers: `kDependentHold` windows wait for the template's own event
+// (users roll dependents out first), unless that event already came (the template changed within the
+// hold): then the dependent is the follower and waits one window like any event in a burst.
+static double dependent_hold(const std::string& tkey) {
+    CtlPtr t = g_ex->cget(TEMPLATES, tkey);
+    return t && now_s() - t->recv_at < g_opt.coalesce * kDependentHold ? 1.0 : kDependentHold;
+}
+
 static void on_dependent(int kind, const CtlObj& obj) {
     Executor& ex = *g_ex;
     std::set<std::string> seen;
@@ -1191,14 +1202,15 @@ static void on_dependent(int kind, const CtlObj& obj) {
             std::string tname = tkey.substr(tkey.find('/') + 1);
             seen.insert(tname);
             ++g_enq[ENQ_DEPENDENT];
-            ex.enqueue(TEMPLATES, obj.ns, tname, kDependentHold);
+            ex.enqueue(TEMPLATES, obj.ns, tname, dependent_hold(tkey));
         }
     }
     for (const auto& owner : obj.owners) {
         if (seen.count(owner)) continue;
-        if (!ex.cget(TEMPLATES, key_of(obj.ns, owner))) return;  // stops at the first orphaned owner
+        std::string tkey = key_of(obj.ns, owner);
+        if (!ex.cget(TEMPLATES, tkey)) return;  // stops at the first orphaned owner
         ++g_enq[ENQ_DEPENDENT];
-        ex.enqueue(TEMPLATES, obj.ns, owner, kDependentHold);
+        ex.enqueue(TEMPLATES, obj.ns, owner, dependent_hold(tkey));
     }
 }
 
