@@ -881,6 +881,7 @@ public:
         }
     }
     size_t length() const { return queue_.size(); }
+    size_t load() const { return queue_.size() + processing_.size() + waiting_.size(); }  // keys with work pending
     // a pass over `key` is pending (added while queued or processing): the next one will see the latest state
     bool dirty(const std::string& key) const { return dirty_.count(key) > 0 && !shutdown_; }
     void shutdown() {
@@ -1087,7 +1088,8 @@ struct Executor {
     }
 
     // Event-driven enqueue.  Inside a burst — a run of more than kBurstMin events, each less than one
-    // coalesce window after the previous — the key is parked for the window, so a template and its
+    // coalesce window after the previous, while at least kBurstMin keys have work pending (back-to-back
+    // small batches make a run but no load) — the key is parked for the window, so a template and its
     // Secret/ConfigMap changing together reconcile once.  An isolated change, or a small batch, goes straight
     // to the workers and pays no coalescing delay (an extra pass there costs nothing that matters).
     // A pass triggered by a dependent is parked `hold` windows: users roll a new configuration out
@@ -1101,7 +1103,7 @@ struct Executor {
         std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
         double now = now_s();
         run_len = now - last_event < g_opt.coalesce ? run_len + 1 : 1;
-        bool burst = run_len > kBurstMin;
+        bool burst = run_len > kBurstMin && queue.load() >= static_cast<size_t>(kBurstMin);
         last_event = now;
         if (g_opt.coalesce > 0 && burst)
             queue.add_after(key, g_opt.coalesce * hold);

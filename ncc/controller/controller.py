@@ -243,14 +243,20 @@ class Controller(ReconcileMixin):
 
     def _coalesce_delay(self) -> float:
         """The coalesce window inside a burst — a run of more than BURST_MIN events, each less than one window
-        after the previous — else 0: an isolated change or a small batch is reconciled at once."""
+        after the previous, while at least BURST_MIN keys are queued, running or parked — else 0: an isolated
+        change or a small batch is reconciled at once (back-to-back small batches too: a run alone is not
+        load)."""
         w = self.options.coalesce_window
         if w <= 0:
             return 0.0
         now = time.monotonic()
         self._run_len = self._run_len + 1 if now - self._last_event < w else 1
         self._last_event = now
-        return w if self._run_len > self.BURST_MIN else 0.0
+        if self._run_len <= self.BURST_MIN:
+            return 0.0
+        core = self.queue.core
+        load = len(self._inline_keys) + core.length() + core.processing() + core.waiting()
+        return w if load >= self.BURST_MIN else 0.0
 
     def _unwrap(self, obj):
         if isinstance(obj, DeletedFinalStateUnknown):

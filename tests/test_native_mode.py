@@ -612,17 +612,26 @@ async def test_inline_finish_agrees_with_the_status_pass():
 
 def test_coalescing_starts_only_inside_a_burst(monkeypatch):
     """Small batches and isolated changes are reconciled at once; only a run of more than BURST_MIN events,
-    each less than one window after the previous, is parked for the coalesce window."""
+    each less than one window after the previous, while BURST_MIN keys have work pending, is parked for the
+    coalesce window.  Back-to-back small batches make a run but no load: no coalescing."""
     import ncc.controller.controller as ctl_mod
     env = Env(1)
     env.opts.coalesce_window = 0.002
     ctl = env.build()
     now = [100.0]
     monkeypatch.setattr(ctl_mod.time, "monotonic", lambda: now[0])
-    delays = []
-    for _ in range(ctl.BURST_MIN + 3):
-        now[0] += 0.0001
-        delays.append(ctl._coalesce_delay())
-    assert delays[:ctl.BURST_MIN] == [0.0] * ctl.BURST_MIN and delays[ctl.BURST_MIN:] == [0.002] * 3
+
+    def run(n):
+        out = []
+        for _ in range(n):
+            now[0] += 0.0001
+            out.append(ctl._coalesce_delay())
+        return out
+    assert run(ctl.BURST_MIN + 3) == [0.0] * (ctl.BURST_MIN + 3)  # a long run over an idle queue
     now[0] += 0.01  # a quiet window ends the run
+    for i in range(ctl.BURST_MIN):
+        ctl.queue.add(f"template/nexus/t{i}")
+    delays = run(ctl.BURST_MIN + 3)
+    assert delays[:ctl.BURST_MIN] == [0.0] * ctl.BURST_MIN and delays[ctl.BURST_MIN:] == [0.002] * 3
+    now[0] += 0.01
     assert ctl._coalesce_delay() == 0.0
