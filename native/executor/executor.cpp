@@ -1976,6 +1976,7 @@ static void configure(const Value& c) {
     o.alias = std::string(c.sget("alias"));
     o.workers = static_cast<int>(num(c, "workers", o.workers));
     o.pool_size = static_cast<int>(num(c, "pool_size", o.pool_size));
+    if (const char* ps = std::getenv("NCC_POOL_SIZE")) o.pool_size = std::max(1, std::atoi(ps));  // experiments
     o.request_timeout = num(c, "request_timeout", o.request_timeout);
     o.coalesce = num(c, "coalesce_window", o.coalesce);
     o.base_delay = num(c, "failure_base_delay", o.base_delay);
