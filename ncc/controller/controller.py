@@ -470,7 +470,21 @@ class Controller(ReconcileMixin):
                                                        ("configmaps", s.configmap_informer))}
                        for s in self.shards},
             "pending_deletes": len(self._pending_deletes), "shard_state": len(self.reports),
+            "failing": self.failing_by_shard(),
         }
+
+    def failing_by_shard(self, limit: int = 100) -> dict:
+        """Coordinator: the objects whose last complete report set failed, per shard — template key, failure
+        class, the object the shard refused (kind/name), HTTP code and message (ncc/controller/failures.py);
+        at most `limit` per shard.  The operator's per-shard view of what the Warning Events announced."""
+        out: dict = {}
+        for key in sorted(self._failure_events):
+            for shard, (_sig, f) in sorted(self._failure_events[key].items()):
+                lst = out.setdefault(shard, [])
+                if len(lst) < limit:
+                    lst.append({"key": key, "class": f.get("c", ""), "kind": f.get("k", ""), "name": f.get("n", ""),
+                                "code": f.get("h", 0), "message": f.get("m", "")})
+        return out
 
     # ================================================================== helpers
     def _assume(self, informer: Informer, res):

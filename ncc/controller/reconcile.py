@@ -448,13 +448,13 @@ class ReconcileMixin:
         failure and shard: a backoff retry that fails the same way again changes nothing to announce (the
         report table does not even complete a repeat of an identical report set), and the memo also covers
         a set that completes again because *another* shard's result changed."""
-        seen = self._failure_events.setdefault(key, {})
+        seen = self._failure_events.setdefault(key, {})  # shard -> (signature, failure): also /debug/state
         for shard in sorted(failures):
             f = failures[shard]
             sig = F.signature(f)
-            if seen.get(shard) == sig:
+            if seen.get(shard, (None,))[0] == sig:
                 continue
-            seen[shard] = sig
+            seen[shard] = (sig, f)
             for etype, reason, message in F.events(f, meta(template).get("name", ""), shard):
                 self.recorder.event(template, etype, reason, message, kind=C.TEMPLATE_KIND)
         for shard in [s for s in seen if s not in failures]:

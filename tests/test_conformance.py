@@ -196,10 +196,17 @@ async def test_rogue_dependent_warning_events_and_status(tmp_path, impl):
         assert cl.status()["syncedToClusters"] == ["shard-1"]
         assert cl.sstates[0].get(R.SECRETS, NS, "s0")["data"] == rogue["data"]  # never overwritten
         assert cl.sstates[1].get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+        if impl != "inprocess":  # the coordinator's per-shard view (/debug/state "failing")
+            failing = cl.app.debug_state()["failing"]
+            assert list(failing) == ["shard-0"]
+            f = failing["shard-0"][0]
+            assert (f["key"], f["class"], f["kind"], f["name"]) == (f"template/{NS}/{T0}", "RogueResourceError",
+                                                                    "Secret", "s0")
         # the operator removes the rogue object: the next retry creates ours and the template becomes Ready
         cl.sstates[0].delete(R.SECRETS, NS, "s0")
         await cl.ready()
         assert cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+        assert cl.app.debug_state()["failing"] == {}
 
 
 async def test_single_put_for_data_and_owner(tmp_path, impl):
