@@ -37,6 +37,7 @@ RECONCILE_ERRORS_METRIC = "reconcile_errors"          # count, tag kind
 SHARD_SYNC_ERRORS_METRIC = "shard_sync_errors"        # count, tag shard (coordinator, from executor reports)
 SHARDS_METRIC = "shards"                              # gauge: shards served
 LEADER_METRIC = "leader"                              # gauge 1/0 when leader election is on
+SHARD_FAILING_METRIC = "shard_failing_objects"        # gauge, tag shard: templates whose last sync there failed
 
 # Event reasons, controller.go:60-70
 SUCCESS_SYNCED = "Synced"

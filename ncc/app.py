@@ -394,6 +394,8 @@ class App:
         if self.metrics is None or self.controller is None:
             return
         self.metrics.gauge(C.SHARDS_METRIC, len(self.controller.all_shard_names))
+        for shard, n in self.controller.failing_counts().items():
+            self.metrics.gauge(C.SHARD_FAILING_METRIC, n, {"shard": shard})
         if self.elector is not None:
             self.metrics.gauge(C.LEADER_METRIC, 1 if self.elector.leading else 0)
 

@@ -473,6 +473,14 @@ class Controller(ReconcileMixin):
             "failing": self.failing_by_shard(),
         }
 
+    def failing_counts(self) -> dict:
+        """Per shard served, how many templates' last sync there failed (0 for the healthy ones)."""
+        counts = {s: 0 for s in self.all_shard_names}
+        for per_shard in self._failure_events.values():
+            for shard in per_shard:
+                counts[shard] = counts.get(shard, 0) + 1
+        return counts
+
     def failing_by_shard(self, limit: int = 100) -> dict:
         """Coordinator: the objects whose last complete report set failed, per shard — template key, failure
         class, the object the shard refused (kind/name), HTTP code and message (ncc/controller/failures.py);

@@ -202,6 +202,7 @@ async def test_rogue_dependent_warning_events_and_status(tmp_path, impl):
             f = failing["shard-0"][0]
             assert (f["key"], f["class"], f["kind"], f["name"]) == (f"template/{NS}/{T0}", "RogueResourceError",
                                                                     "Secret", "s0")
+            assert cl.app.controller.failing_counts() == {"shard-0": 1, "shard-1": 0}
         # the operator removes the rogue object: the next retry creates ours and the template becomes Ready
         cl.sstates[0].delete(R.SECRETS, NS, "s0")
         await cl.ready()
