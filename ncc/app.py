@@ -587,8 +587,8 @@ class App:
             infs = [self.factory] + [s.factory for s in self.shards]
             counts = {i.name: (i.events, getattr(i, "echoes", 0), i.filtered) for f in infs for i in f.informers()}
             log.warning("informer events/echoes/filtered: %s", counts)
-            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f stats=%s", self.options.role, ru.ru_utime,
-                        ru.ru_stime, self.controller.stats)
+            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f stats=%s events=%s", self.options.role, ru.ru_utime,
+                        ru.ru_stime, self.controller.stats, getattr(self.recorder, "stats", {}))
 
 
 def setup_signal_handler(stop: asyncio.Event) -> None:

@@ -284,7 +284,7 @@ class BroadcastRecorder(EventRecorder):
                     except Exception as e:  # noqa: BLE001
                         if attempt == 2:
                             self.stats["failed"] += 1
-                            log.debug("unable to write event: %r", e)
+                            log.warning("unable to write event: %r", e)
                         else:
                             await asyncio.sleep(0.1 * (attempt + 1))
             finally:
