@@ -17,6 +17,7 @@ from __future__ import annotations
 import asyncio
 import contextvars
 import logging
+import os
 import time
 
 import msgpack
@@ -419,8 +420,9 @@ class Controller(ReconcileMixin):
             self._inline_timer = loop.call_later(delay, self._flush_inline) if delay > 0 else \
                 loop.call_soon(self._flush_inline)
 
-    INLINE_BATCH = 256  # keys finished per loop iteration: a wave's worth of completions must not hold up
-    #                     the loop (the watch lines the relay forwards wait behind it)
+    # keys finished per loop iteration: a wave's worth of completions must not hold up the loop (the watch
+    # lines the relay forwards wait behind it); NCC_INLINE_BATCH overrides (experiments)
+    INLINE_BATCH = int(os.environ.get("NCC_INLINE_BATCH", "256"))
 
     def _flush_inline(self) -> None:
         self._inline_timer = None
