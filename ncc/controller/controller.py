@@ -422,7 +422,7 @@ class Controller(ReconcileMixin):
 
     # keys finished per loop iteration: a wave's worth of completions must not hold up the loop (the watch
     # lines the relay forwards wait behind it); NCC_INLINE_BATCH overrides (experiments)
-    INLINE_BATCH = int(os.environ.get("NCC_INLINE_BATCH", "16"))
+    INLINE_BATCH = int(os.environ.get("NCC_INLINE_BATCH", "256"))
 
     def _flush_inline(self) -> None:
         self._inline_timer = None
