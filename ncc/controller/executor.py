@@ -31,6 +31,8 @@ from ..aio import wait_timeout
 
 log = logging.getLogger("ncc.executor")
 
+EXIT_GRACE_S = 10.0  # how long a child may take to exit once its channel has closed
+
 
 def partition(names: list[str], n: int) -> list[list[str]]:
     """Round-robin shard → executor assignment (stable for a given shard list)."""
@@ -177,7 +179,13 @@ class ExecutorHandle:
                     self._dispatch(batch)
             if self.on_exit is not None:
                 self.on_exit(self)
-            rc = await self.proc.wait()
+            try:  # the channel is gone: a child that does not exit on its own (wedged) is killed
+                rc = await asyncio.wait_for(self.proc.wait(), EXIT_GRACE_S)
+            except asyncio.TimeoutError:
+                log.error("%s %d (shards %s) did not exit after its channel closed; killing it", self.what,
+                          self.index, self.shards)
+                self.proc.kill()
+                rc = await self.proc.wait()
             self.channel.close()
             if self._stopping:
                 return

@@ -3,13 +3,21 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import logging
+import os
 import struct
 
 import msgpack
 
 _HDR = struct.Struct(">I")
+log = logging.getLogger("ncc.ipc")
+
 MAX_FRAME = 64 * 1024 * 1024
 FRAME_BUDGET = 16 * 1024 * 1024  # coalesce queued messages into frames of about this size at most
+# A peer that stops reading (an executor wedged or stopped) must not grow the coordinator's memory without
+# bound: past this many unsent bytes the channel is closed as if the peer had gone (it is respawned with a
+# fresh snapshot), as an apiserver terminates a watcher that cannot keep up.
+MAX_BACKLOG = int(os.environ.get("NCC_IPC_MAX_BACKLOG", str(512 << 20)))
 
 
 def frames(msgs: list):
@@ -132,6 +140,10 @@ class RawChannel:
             self._out += frame
             self.sent += 1
         self._write()
+        if len(self._out) > MAX_BACKLOG and not self._closed:
+            log.error("peer is not reading (%d MiB unsent): closing the channel", len(self._out) >> 20)
+            self._out.clear()
+            self._eof()
 
     def _write(self) -> None:
         while self._out:

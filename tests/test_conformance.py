@@ -530,3 +530,26 @@ async def test_python_feed_skips_an_unreadable_line():
         assert not task.done()
     finally:
         task.cancel()
+
+
+async def test_raw_channel_closes_on_a_peer_that_stops_reading(monkeypatch):
+    """The coordinator's end of an executor channel gives up on a peer that does not read: past MAX_BACKLOG
+    unsent bytes it closes and reports EOF (the pool then respawns the executor), instead of buffering the
+    relayed lines without bound."""
+    import socket
+    from ncc.controller import ipc
+    monkeypatch.setattr(ipc, "MAX_BACKLOG", 1 << 20)
+    a, b = socket.socketpair()
+    eof = asyncio.Event()
+    ch = ipc.RawChannel(a, lambda buf, start: ([], start), lambda msgs: None, eof.set)
+    try:
+        for _ in range(64):  # 64 x 64 KiB messages, nobody reads `b`
+            ch.send({"t": "w", "k": 0, "l": [b"x" * (64 << 10)]})
+            await asyncio.sleep(0)
+            if eof.is_set():
+                break
+        await asyncio.wait_for(eof.wait(), 2)
+        ch.send({"t": "w"})  # a closed channel drops sends
+    finally:
+        ch.close()
+        b.close()
