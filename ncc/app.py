@@ -330,9 +330,12 @@ class App:
             # native: 4 writer tasks (per-object order kept) so Event traffic keeps up with fan-out rates;
             # compat: client-go's single sink goroutine
             native_events = o.mode == "native" and os.environ.get("NCC_EVENT_COALESCE") != "0"
+            tstore, wstore = infs[R.TEMPLATES].store, infs[R.WORKGROUPS].store
             self.recorder = BroadcastRecorder(client, log_events=log.isEnabledFor(logging.DEBUG),
                                               writers=4 if o.mode == "native" else 1, coalesce=native_events,
-                                              repeat_window=cfg.event_repeat_window if native_events else 0.0)
+                                              repeat_window=cfg.event_repeat_window if native_events else 0.0,
+                                              cache_limit=(lambda: 2 * (len(tstore) + len(wstore)))
+                                              if o.mode == "native" else 4096)
         self.controller = Controller(alias=cfg.alias, namespace=cfg.controller_namespace, client=client,
                                      shards=self.shards, template_informer=infs[R.TEMPLATES],
                                      workgroup_informer=infs[R.WORKGROUPS], secret_informer=infs[R.SECRETS],

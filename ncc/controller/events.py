@@ -50,10 +50,19 @@ class EventRecorder:
         raise NotImplementedError
 
 
-def _bound(cache: dict, limit: int = 4096) -> None:
-    """Keep a correlator cache within client-go's 4096 entries (maxLruCacheEntries): past the limit the
-    oldest quarter goes (insertion order), so a controller that has seen many objects does not grow."""
-    if len(cache) > limit:
+CACHE_LIMIT = 4096  # client-go's maxLruCacheEntries
+
+
+def _bound(cache: dict, limit=CACHE_LIMIT) -> None:
+    """Keep a correlator cache within `limit` entries (client-go: 4096, maxLruCacheEntries): past the limit
+    the oldest quarter goes (insertion order), so a controller that has seen many objects does not grow.
+    `limit` may be a callable, evaluated only when the cache is over the default."""
+    n = len(cache)
+    if n <= CACHE_LIMIT:
+        return
+    if callable(limit):
+        limit = max(CACHE_LIMIT, int(limit()))
+    if n > limit:
         for k in list(cache)[:limit // 4]:
             del cache[k]
 
@@ -92,8 +101,13 @@ class BroadcastRecorder(EventRecorder):
     """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
 
     def __init__(self, client: KubeClient, component: str = C.CONTROLLER_AGENT_NAME, *, spam_filter: bool = True,
-                 log_events: bool = True, writers: int = 1, coalesce: bool = False, repeat_window: float = 0.0):
+                 log_events: bool = True, writers: int = 1, coalesce: bool = False, repeat_window: float = 0.0,
+                 cache_limit=CACHE_LIMIT):
         self.client = client
+        # correlator cache size: client-go's 4096 (an int), or a callable re-read when a cache is trimmed —
+        # native mode sizes it to the objects the controller manages, so a repeat stays a count PATCH
+        # instead of becoming a new Event once more than 4096 objects emit events
+        self.cache_limit = cache_limit
         self.component = component
         self.spam_filter = spam_filter
         self.log_events = log_events
@@ -110,7 +124,7 @@ class BroadcastRecorder(EventRecorder):
         self._flush_timer = None
         self._buckets: dict[tuple, TokenBucket] = {}
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
-        self._seen: dict[tuple, dict] = {}  # full key -> last Event object written
+        self._seen: dict[tuple, list] = {}  # full key -> [name, count] of the Event last written
         self._tasks: list[asyncio.Task] = []
         self._write_meta = getattr(client, "write_meta", None)  # undecoded writes (REST clients)
         self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0,
@@ -206,7 +220,7 @@ class BroadcastRecorder(EventRecorder):
         b = self._buckets.get(k)
         if b is None:
             b = self._buckets[k] = TokenBucket(SPAM_QPS, SPAM_BURST, now=now)
-            _bound(self._buckets)
+            _bound(self._buckets, self.cache_limit)
         return b.reserve(now) <= 0.0 or self._refund(b)
 
     @staticmethod
@@ -219,7 +233,7 @@ class BroadcastRecorder(EventRecorder):
         hit = self._similar.get(akey)
         if hit is None or now - hit[1] > AGGREGATE_INTERVAL_S:
             hit = self._similar[akey] = (set(), now)
-            _bound(self._similar)
+            _bound(self._similar, self.cache_limit)
         msgs = hit[0]
         msgs.add(message)
         if len(msgs) >= AGGREGATE_MAX_EVENTS:
@@ -232,16 +246,16 @@ class BroadcastRecorder(EventRecorder):
         prev = self._seen.get(key)
         ns = ref["namespace"] or "default"
         wm = self._write_meta
-        if prev is not None:
-            count = int(prev.get("count", 1)) + n
+        if prev is not None:  # [name, count]: only these matter for the count PATCH
+            count = prev[1] + n
             patch = {"count": count, "lastTimestamp": ts, "message": message}
-            if wm is not None:  # only the Event's name and count matter here: skip decoding the response
-                await wm("patch", R.EVENTS, ns, patch, name=prev["metadata"]["name"], patch_type=PATCH_STRATEGIC)
-                res = None
+            if wm is not None:  # skip decoding the response
+                await wm("patch", R.EVENTS, ns, patch, name=prev[0], patch_type=PATCH_STRATEGIC)
             else:
-                res = await self.client.patch(R.EVENTS, ns, prev["metadata"]["name"], patch,
-                                              patch_type=PATCH_STRATEGIC)
-            self._seen[key] = res if isinstance(res, dict) else dict(prev, count=count)
+                res = await self.client.patch(R.EVENTS, ns, prev[0], patch, patch_type=PATCH_STRATEGIC)
+                if isinstance(res, dict):
+                    count = int(res.get("count", count))
+            prev[1] = count
             self.stats["patched"] += 1
             return
         ev = {
@@ -264,8 +278,10 @@ class BroadcastRecorder(EventRecorder):
             res = None
         else:
             res = await self.client.create(R.EVENTS, ns, ev)
-        self._seen[key] = res if isinstance(res, dict) else ev
-        _bound(self._seen)
+        done = res if isinstance(res, dict) else ev
+        self._seen[key] = [(done.get("metadata") or {}).get("name", ev["metadata"]["name"]),
+                           int(done.get("count", n))]
+        _bound(self._seen, self.cache_limit)
         self.stats["created"] += 1
 
     async def _run(self, queue: asyncio.Queue) -> None:

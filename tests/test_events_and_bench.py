@@ -112,6 +112,27 @@ async def test_event_correlator_caches_are_bounded():
     await rec.stop()
 
 
+async def test_native_correlator_cache_follows_the_object_count():
+    """Native mode sizes the correlator caches to the objects managed (a callable limit): with 5000 objects
+    emitting events, each object's repeat is still a count PATCH of its first Event, not a new Event."""
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False, writers=4, cache_limit=lambda: 2 * 5000)
+    rec.start()
+
+    def obj(i):
+        return {"kind": "NexusAlgorithmTemplate", "apiVersion": "science.sneaksanddata.com/v1",
+                "metadata": {"name": f"t{i}", "namespace": "nexus", "uid": f"u{i}"}}
+    for rnd in range(2):
+        for i in range(5000):
+            rec.event(obj(i), "Normal", "Synced", "synced")
+            if i % 500 == 499:
+                await _drain(rec)
+        await _drain(rec)
+    assert rec.stats["created"] == 5000 and rec.stats["patched"] == 5000
+    assert len(rec._seen) == 5000
+    await rec.stop()
+
+
 def test_fake_recorder_formats_like_client_go():
     r = FakeRecorder()
     r.event({}, "Warning", "ErrResourceMissing", "msg")
