@@ -717,14 +717,13 @@ public:
                 bool batch = (n & 0x80000000u) != 0;
                 n &= 0x7FFFFFFFu;
                 if (in_.size() - pos_ >= 4 + n) {
-                    std::string body = in_.substr(pos_ + 4, n);
+                    PhaseTimer pt(PH_CHANNEL_IN);
+                    mp::Obj o = mp::decode(std::string_view(in_).substr(pos_ + 4, n));  // straight from the buffer
                     pos_ += 4 + n;
                     if (pos_ > (1 << 20)) {
                         in_.erase(0, pos_);
                         pos_ = 0;
                     }
-                    PhaseTimer pt(PH_CHANNEL_IN);
-                    mp::Obj o = mp::decode(body);
                     std::vector<mp::Obj> out;
                     if (batch && o.t == mp::Obj::ARR)
                         out = std::move(o.a);

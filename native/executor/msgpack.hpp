@@ -134,7 +134,7 @@ struct Decoder {
     }
 };
 
-inline Obj decode(const std::string& body) {
+inline Obj decode(std::string_view body) {
     Decoder d{reinterpret_cast<const unsigned char*>(body.data()),
               reinterpret_cast<const unsigned char*>(body.data()) + body.size()};
     Obj o;
