@@ -23,3 +23,22 @@ def test_checker_finds_and_fixes_a_stale_reference(tmp_path):
     assert len(problems) == 2 and "defined at line" in problems[0]
     assert doc_refs.check(str(doc), fix=False) == []
     assert f"`ncc/app.py:{good[0]}` `main`" in doc.read_text()
+
+
+def test_every_environment_variable_is_documented():
+    """docs/ENVIRONMENT.md lists every NCC_* variable (or compile-time macro) the sources read."""
+    import re
+    names = set()
+    for base in ("ncc", "native", "bench", "scripts"):
+        for dirpath, _dirs, files in os.walk(os.path.join(ROOT, base)):
+            for f in files:
+                if f.endswith((".py", ".cpp", ".hpp")):
+                    with open(os.path.join(dirpath, f), errors="replace") as fh:
+                        names.update(re.findall(r"NCC_[A-Z][A-Z_]*[A-Z]", fh.read()))
+    with open(os.path.join(ROOT, "bench.py")) as fh:
+        names.update(re.findall(r"NCC_[A-Z][A-Z_]*[A-Z]", fh.read()))
+    with open(os.path.join(ROOT, "docs", "ENVIRONMENT.md")) as fh:
+        doc = fh.read()
+    documented = set(re.findall(r"NCC_[A-Z][A-Z_]*[A-Z]", doc))
+    missing = {n for n in names if n not in documented and not any(n.startswith(p) for p in ("NCC_OPT_",))}
+    assert not missing, sorted(missing)
