@@ -469,6 +469,40 @@ async def test_updates_and_new_references_propagate(tmp_path, impl):
         await cl.ready()
 
 
+async def test_other_namespaces_are_ignored(tmp_path, impl):
+    """Only the controller namespace is watched (main.go:70-71): a template in another namespace is never
+    synced, while the one in the controller namespace is."""
+    async with Cluster(tmp_path, impl) as cl:
+        cl.cstate.create(R.SECRETS, "elsewhere", make_secret("s0", "elsewhere"))
+        cl.cstate.create(R.TEMPLATES, "elsewhere", make_template(7, "elsewhere", secrets=["s0"], configmaps=[]))
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        await asyncio.sleep(0.2)
+        for s in cl.sstates:
+            assert s.list(R.TEMPLATES, "elsewhere")["items"] == [] and s.list(R.SECRETS, "elsewhere")["items"] == []
+        assert not (cl.cstate.get(R.TEMPLATES, "elsewhere", "algo-00007").get("status") or {}).get("conditions")
+
+
+async def test_deleted_reference_turns_the_template_not_ready_until_restored(tmp_path, impl):
+    """A referenced Secret deleted on the controller cluster: the template's next pass reports the missing
+    reference (the reference's Warning ErrResourceMissing; its status is left as it was, controller.go:649-653);
+    re-creating the Secret syncs the new data and version everywhere and the template is Ready."""
+    async with Cluster(tmp_path, impl) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        await cl.cc.delete(R.SECRETS, NS, "s0")
+        await mutate(cl.cc, R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("versionTag", "v2"))
+        ev = await cl.wait_events(C.ERR_RESOURCE_MISSING)
+        assert '"s0"' in ev[0]["message"]
+        await cl.cc.create(R.SECRETS, NS, make_secret("s0", NS, version=3))
+        await cl.ready()
+        await wait_for(lambda: asyncio.sleep(0, all(
+            s.get(R.SECRETS, NS, "s0")["data"] == cl.cstate.get(R.SECRETS, NS, "s0")["data"] and
+            s.get(R.TEMPLATES, NS, T0)["spec"]["container"]["versionTag"] == "v2" for s in cl.sstates)))
+
+
 def test_every_implementation_is_exercised():
     """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
     if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
