@@ -368,8 +368,9 @@ async def test_write_races_resolved_by_rereading(tmp_path, impl):
         await wait_for(converged)
         assert cl.env.shard_servers[0].faults.rules[0]["count"] == 0 and cl.env.shard_servers[0].faults.rules[1][
             "count"] == 0, "both races must have been provoked"
-        st = await cl.ready()
-        assert st["syncedConfigurations"] == ["c0", "c1"]
+        # the status follows the new template version once its reports are in (not necessarily by now)
+        await wait_for(lambda: asyncio.sleep(0, cl.status().get("syncedConfigurations") == ["c0", "c1"]))
+        await cl.ready()
 
 
 async def test_shard_drift_repaired(tmp_path, impl):
