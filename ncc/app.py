@@ -525,7 +525,10 @@ class App:
                 self.partitions.start()
         if self.cfg.mode == "native":
             gctune.tune()
-            self._gc_task = asyncio.ensure_future(gctune.freeze_loop())
+            # NCC_GC_FREEZE="<period>,<generation collected first, or none>" (experiments; default "1,none")
+            period, _, gen = os.environ.get("NCC_GC_FREEZE", "1,none").partition(",")
+            self._gc_task = asyncio.ensure_future(
+                gctune.freeze_loop(float(period), collect=None if gen in ("", "none") else int(gen)))
         self._lag_task = loopmon.start(self.options.role)
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))
@@ -590,8 +593,9 @@ class App:
             infs = [self.factory] + [s.factory for s in self.shards]
             counts = {i.name: (i.events, getattr(i, "echoes", 0), i.filtered) for f in infs for i in f.informers()}
             log.warning("informer events/echoes/filtered: %s", counts)
-            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f stats=%s events=%s", self.options.role, ru.ru_utime,
-                        ru.ru_stime, self.controller.stats, getattr(self.recorder, "stats", {}))
+            log.warning("cpu report role=%s user_s=%.3f sys_s=%.3f stats=%s events=%s gc=%s", self.options.role,
+                        ru.ru_utime, ru.ru_stime, self.controller.stats, getattr(self.recorder, "stats", {}),
+                        gctune.STATS)
 
 
 def setup_signal_handler(stop: asyncio.Event) -> None:

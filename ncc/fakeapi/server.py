@@ -550,13 +550,13 @@ async def serve(args) -> None:
             ctx.verify_mode = ssl.CERT_REQUIRED
     url = await server.start(args.host, args.port, ctx)
     from .. import gctune
-    gctune.tune()
+    gctune.tune(account=False)
     # A test server that keeps what it allocates: freeze every second, never scan the survivors (gctune);
-    # NCC_FAKEAPI_GC=collect restores the controller processes' policy (collect + freeze every 5 s) for A/B runs
+    # NCC_FAKEAPI_GC=collect restores the round-2 controller policy (generation-1 pass + freeze every 5 s)
     if os.environ.get("NCC_FAKEAPI_GC") == "collect":
-        gc_task = asyncio.ensure_future(gctune.freeze_loop())
+        gc_task = asyncio.ensure_future(gctune.freeze_loop(5.0, collect=1))
     else:
-        gc_task = asyncio.ensure_future(gctune.freeze_loop(1.0, collect=False))
+        gc_task = asyncio.ensure_future(gctune.freeze_loop(1.0, collect=None))
     from .. import loopmon
     lag_task = loopmon.start(f"fakeapi:{args.name}")
     if args.port_file:

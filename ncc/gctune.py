@@ -11,24 +11,51 @@ from __future__ import annotations
 
 import asyncio
 import gc
+import time
 
 THRESHOLDS = (50_000, 20, 100)
+STATS = {"passes": 0, "collected": 0, "seconds": 0.0, "max_seconds": 0.0}  # freeze_loop's own passes
 
 
-def tune(thresholds: tuple = THRESHOLDS) -> None:
+_auto = {"t0": 0.0}
+
+
+def _on_gc(phase: str, info: dict) -> None:
+    """Time every collection the interpreter runs (automatic ones included), per generation."""
+    if phase == "start":
+        _auto["t0"] = time.perf_counter()
+        return
+    dt = time.perf_counter() - _auto["t0"]
+    g = info.get("generation", 0)
+    STATS[f"gen{g}_n"] = STATS.get(f"gen{g}_n", 0) + 1
+    STATS[f"gen{g}_s"] = round(STATS.get(f"gen{g}_s", 0.0) + dt, 4)
+    STATS[f"gen{g}_max_s"] = round(max(STATS.get(f"gen{g}_max_s", 0.0), dt), 4)
+
+
+def tune(thresholds: tuple = THRESHOLDS, account: bool = True) -> None:
     gc.set_threshold(*thresholds)
     gc.freeze()
+    if account and _on_gc not in gc.callbacks:
+        gc.callbacks.append(_on_gc)
 
 
-async def freeze_loop(period: float = 5.0, collect: bool = True) -> None:
-    """Collect young garbage, then freeze the survivors, every `period` seconds.
+async def freeze_loop(period: float = 1.0, collect: int | None = None) -> None:
+    """Collect young garbage of generations up to `collect` (None: no pass of our own), then freeze the
+    survivors, every `period` seconds.
 
-    `collect=False` freezes without the generation-1 pass.  That pass scans every young survivor, and in a
-    process that retains most of what it allocates (the fake apiserver's store and watch history: ~1M
-    containers in 5 s at bench rates) it found nothing to free and stopped the loop for 130-240 ms.
-    Freezing instead keeps the cycles that died after surviving a generation-0 pass."""
+    The controller processes default to freezing every second with no pass of their own: the automatic
+    generation-0 collections (every 50 000 container allocations) still reclaim cycles that die young, and
+    everything that survived one is frozen unscanned.  The round-2 policy, a generation-1 pass every 5 s,
+    scans every young survivor: in the coordinator at 20 000 templates it found nothing to free in a whole
+    run and stopped the loop for up to 250-300 ms each time; an explicit generation-0 pass every second
+    found nothing either and cost 1.2 s of CPU per run (BENCHMARKS.md)."""
     while True:
         await asyncio.sleep(period)
-        if collect:
-            gc.collect(1)
+        if collect is not None:
+            t0 = time.perf_counter()
+            STATS["collected"] += gc.collect(collect)
+            dt = time.perf_counter() - t0
+            STATS["passes"] += 1
+            STATS["seconds"] += dt
+            STATS["max_seconds"] = max(STATS["max_seconds"], dt)
         gc.freeze()

@@ -41,17 +41,20 @@ def test_monitor_reports_blocked_loop_and_gc_pass(monkeypatch, tmp_path):
 
 
 def test_freeze_loop_without_collect_only_freezes(monkeypatch):
+    """The controllers' default freezes without a pass of its own; `collect=<generation>` runs that pass first
+    and accounts for it in gctune.STATS."""
     calls = []
-    monkeypatch.setattr(gctune.gc, "collect", lambda gen=2: calls.append(("collect", gen)))
+    monkeypatch.setattr(gctune.gc, "collect", lambda gen=2: calls.append(("collect", gen)) or 0)
     monkeypatch.setattr(gctune.gc, "freeze", lambda: calls.append(("freeze",)))
 
-    async def main(collect):
-        t = asyncio.ensure_future(gctune.freeze_loop(0.01, collect=collect))
+    async def main(**kw):
+        t = asyncio.ensure_future(gctune.freeze_loop(0.01, **kw))
         await asyncio.sleep(0.035)
         t.cancel()
         await asyncio.gather(t, return_exceptions=True)
-    asyncio.run(main(False))
+    asyncio.run(main())
     assert calls and all(c == ("freeze",) for c in calls)
     calls.clear()
-    asyncio.run(main(True))
-    assert ("collect", 1) in calls and ("freeze",) in calls
+    passes = gctune.STATS["passes"]
+    asyncio.run(main(collect=1))
+    assert ("collect", 1) in calls and ("freeze",) in calls and gctune.STATS["passes"] > passes
