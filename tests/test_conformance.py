@@ -504,6 +504,25 @@ async def test_deleted_reference_turns_the_template_not_ready_until_restored(tmp
             s.get(R.TEMPLATES, NS, T0)["spec"]["container"]["versionTag"] == "v2" for s in cl.sstates)))
 
 
+async def test_one_executor_serving_several_shards(tmp_path, impl):
+    """`executors: 1` with three shards: one executor process serves them all.  A refusal on one shard
+    stays on that shard (the others sync and are listed in the status), and clears when the rogue object
+    goes."""
+    if impl == "inprocess":
+        pytest.skip("no executors")
+    async with Cluster(tmp_path, impl, n_shards=3, executors=1) as cl:
+        cl.sstates[1].create(R.SECRETS, NS, make_secret("s0", NS, version=9))
+        cl.seed()
+        await cl.start()
+        assert cl.app.n_executors == 1
+        await cl.not_ready(T0, "shard-1", "RogueResourceError")
+        await wait_for(lambda: asyncio.sleep(0, cl.status().get("syncedToClusters") == ["shard-0", "shard-2"]))
+        for i in (0, 2):
+            assert cl.sstates[i].get(R.SECRETS, NS, "s0")["metadata"]["ownerReferences"]
+        cl.sstates[1].delete(R.SECRETS, NS, "s0")
+        await cl.ready()
+
+
 def test_every_implementation_is_exercised():
     """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
     if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
