@@ -1,0 +1,165 @@
+"""Randomised chaos against the native topology, checked against a model of the end state.
+
+A seeded sequence of user changes — template spec updates, Secret/ConfigMap payload updates, new templates
+(some sharing an existing dependent), template deletes — runs while the shards misbehave: a share of their
+writes fail (503), watch streams are cut, the watch history is compacted (resumes get 410 and relist),
+and executor processes are killed (the pool respawns them with a fresh snapshot).  Once the faults clear,
+every shard must hold exactly what the controller cluster implies:
+
+* every controller template, with the same spec, Ready with every shard listed;
+* every dependent a template references, with the controller's payload and an ownerRef to the shard copy
+  of each template that references it;
+* no copy of a deleted template (queued, retried deletes), and no dependent that only it owned (shard GC).
+
+Runs for the in-process topology and for the Python and C++ executors (executor kills only where there
+are executors).  NCC_CHAOS_STEPS / NCC_CHAOS_SEEDS / NCC_CHAOS_KILLS scale a run up for exploration.
+"""
+import asyncio
+import os
+import random
+
+import pytest
+
+from ncc.api import constants as C
+from ncc.api import resources as R
+from ncc.testing.workload import make_configmap, make_secret, make_template
+
+from test_conformance import NS, Cluster, mutate, wait_for
+
+pytestmark = pytest.mark.skipif(os.environ.get("NCC_SKIP_CHAOS") == "1", reason="NCC_SKIP_CHAOS=1")
+# NCC_CHAOS_STEPS / NCC_CHAOS_SEEDS / NCC_CHAOS_KILLS scale the run up for exploration
+STEPS = int(os.environ.get("NCC_CHAOS_STEPS", "40"))
+SEEDS = int(os.environ.get("NCC_CHAOS_SEEDS", "5"))
+MAX_KILLS = int(os.environ.get("NCC_CHAOS_KILLS", "2"))
+
+
+def _deps(t: dict) -> tuple[list, list]:
+    mev = t["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"]
+    return ([e["secretRef"]["name"] for e in mev if e.get("secretRef")],
+            [e["configMapRef"]["name"] for e in mev if e.get("configMapRef")])
+
+
+def _converged(cl) -> str:
+    """'' when every shard matches the model, else the first difference found."""
+    shards = cl.env.shard_names
+    templates = {t["metadata"]["name"]: t for t in cl.cstate.list(R.TEMPLATES, NS)["items"]}
+    for name, t in templates.items():
+        st = t.get("status") or {}
+        c = (st.get("conditions") or [{}])[0]
+        if c.get("status") != "True" or st.get("syncedToClusters") != shards:
+            return f"{name}: status {c.get('status')} {st.get('syncedToClusters')}"
+    for i, s in enumerate(cl.sstates):
+        ours = {t["metadata"]["name"]: t for t in s.list(R.TEMPLATES, NS)["items"]}
+        if set(ours) != set(templates):
+            return f"shard {i}: templates {sorted(set(ours) ^ set(templates))} differ"
+        want_owners: dict = {}
+        for name, t in templates.items():
+            if ours[name]["spec"] != t["spec"]:
+                return f"shard {i}: {name} spec differs"
+            secrets, cms = _deps(t)
+            for rt, names in ((R.SECRETS, secrets), (R.CONFIGMAPS, cms)):
+                for n in names:
+                    want_owners.setdefault((rt.plural, n), set()).add(ours[name]["metadata"]["uid"])
+        for (plural, n), uids in want_owners.items():
+            rt = R.SECRETS if plural == "secrets" else R.CONFIGMAPS
+            live = s.try_get(rt, NS, n)
+            if live is None:
+                return f"shard {i}: {plural}/{n} missing"
+            if live.get("data") != cl.cstate.get(rt, NS, n).get("data"):
+                return f"shard {i}: {plural}/{n} data differs"
+            have = {r["uid"] for r in live["metadata"].get("ownerReferences") or ()}
+            if not uids <= have:
+                return f"shard {i}: {plural}/{n} owners {sorted(have)} lack {sorted(uids - have)}"
+        for rt in (R.SECRETS, R.CONFIGMAPS):
+            for o in s.list(rt, NS)["items"]:
+                if (rt.plural, o["metadata"]["name"]) not in want_owners:
+                    live_owners = {r["uid"] for r in o["metadata"].get("ownerReferences") or ()}
+                    if live_owners & {t["metadata"]["uid"] for t in ours.values()}:
+                        return f"shard {i}: {rt.plural}/{o['metadata']['name']} owned but unreferenced"
+                    if live_owners:
+                        return f"shard {i}: {rt.plural}/{o['metadata']['name']} left behind by a deleted template"
+    return ""
+
+
+@pytest.mark.parametrize("impl", ["inprocess", "python", "native"])
+@pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
+async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
+    from ncc.controller.native_executor import binary_path
+    if impl == "native" and binary_path() is None:
+        pytest.skip("ncc/bin/ncc-executor is not built")
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+    rnd = random.Random(seed)
+    async with Cluster(tmp_path, impl, n_shards=2) as cl:
+        live = []
+        for i in range(6):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+            live.append(f"algo-{i:05d}")
+        await cl.start()
+        next_id, kills, version = 6, 0, 0
+        ops: dict = {}
+        for _step in range(STEPS):
+            version += 1
+            op = rnd.choices(["spec", "secret", "configmap", "create", "delete", "fault", "kill"],
+                             weights=[5, 4, 3, 2, 2, 3, 1])[0]
+            ops[op] = ops.get(op, 0) + 1
+            if op == "spec" and live:
+                name = rnd.choice(live)
+                await mutate(cl.cc, R.TEMPLATES, name,
+                             lambda o, v=version: o["spec"]["container"].__setitem__("versionTag", f"v{v}"))
+            elif op in ("secret", "configmap"):
+                rt = R.SECRETS if op == "secret" else R.CONFIGMAPS
+                names = [o["metadata"]["name"] for o in cl.cstate.list(rt, NS)["items"]]
+                if names:
+                    n = rnd.choice(names)
+                    val = f"v{version}" if rt is R.CONFIGMAPS else "djk="
+                    await mutate(cl.cc, rt, n, lambda o, k=f"k{version}", v=val: o.setdefault("data", {})
+                                 .__setitem__(k, v))
+            elif op == "create":
+                i = next_id
+                next_id += 1
+                shared = rnd.random() < 0.3 and live
+                sec = f"s{rnd.randrange(next_id - 1)}" if shared else f"s{i}"
+                if cl.cstate.try_get(R.SECRETS, NS, sec) is None:
+                    await cl.cc.create(R.SECRETS, NS, make_secret(sec, NS))
+                await cl.cc.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
+                await cl.cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[sec], configmaps=[f"c{i}"]))
+                live.append(f"algo-{i:05d}")
+            elif op == "delete" and len(live) > 2:
+                name = live.pop(rnd.randrange(len(live)))
+                await cl.cc.delete(R.TEMPLATES, NS, name)
+            elif op == "fault":
+                srv = rnd.choice(cl.env.shard_servers)
+                kind = rnd.choice(["errors", "drop", "compact"])
+                if kind == "errors":
+                    srv.faults.update({"error_rate": 0.2, "error_code": 503})
+                elif kind == "drop":
+                    srv.drop_watches()
+                else:
+                    srv.state.compact()
+                    srv.drop_watches()
+            elif op == "kill" and kills < MAX_KILLS and cl.app.pool is not None:
+                h = rnd.choice(cl.app.pool.handles)
+                if h.proc is not None and h.proc.returncode is None:
+                    h.proc.kill()  # a crash: the pool respawns it (not `h.kill()`, which stops it for good)
+                    kills += 1
+            await asyncio.sleep(rnd.uniform(0, 0.03))
+        for srv in cl.env.shard_servers:
+            srv.faults.update({"error_rate": 0.0})
+        print(f"seed {seed} {impl}: ops {ops}, executor kills {kills}, templates {len(live)}")
+        last = ""
+
+        async def done():
+            nonlocal last
+            last = _converged(cl)
+            return last == ""
+        try:
+            await wait_for(done, timeout=45, interval=0.2)
+        except AssertionError:
+            raise AssertionError(f"seed {seed} ({impl}) did not converge: {last}") from None
+        # the model check sees a difference (and the controller repairs it): drift on one shard copy
+        name = live[0]
+        await mutate(cl.sc[0], R.TEMPLATES, name, lambda o: o["spec"]["container"].__setitem__("versionTag", "drift"))
+        assert "spec differs" in _converged(cl)
+        await wait_for(done, timeout=15, interval=0.1)
+        rogue = [e for e in cl.cstate.list(R.EVENTS, NS)["items"] if e["reason"] == C.ERR_RESOURCE_EXISTS]
+        assert rogue == []  # nothing here is a rogue object
