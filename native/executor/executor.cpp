@@ -955,6 +955,7 @@ struct Shard {
     std::unique_ptr<Client> client;
     Informer inf[4];
     std::unordered_map<std::string, Memo> memo[4];
+    Event answering;  // set when a write or read was answered (< 500): reflectors in an outage backoff retry
     bool synced() const {
         for (const auto& i : inf)
             if (!i.synced) return false;
@@ -1452,14 +1453,18 @@ static Task<void> shard_watch(Shard& sh, int kind) {
         timeout + 30.0);
 }
 
-// Reflector loop (list -> watch -> re-watch; 410 -> consistent relist; errors back off 0.8 s..30 s).
+// Reflector loop (list -> watch -> re-watch; 410 -> consistent relist; errors back off 0.8 s..30 s, as
+// client-go's reflector).  After an outage (transport error or 5xx) the backoff can reach 30 s; when the
+// workers' own requests to the shard are answered again (`Shard::answering`), the sleeping reflector
+// retries at once — once per outage, so an endpoint that keeps failing while writes succeed (RBAC on watch,
+// say) still backs off.
 static Task<void> shard_informer(Shard* shp, int kind) {
     Shard& sh = *shp;
     double backoff = 0.8;
-    bool need_list = true;
+    bool need_list = true, woken = false;
     std::string list_rv = "0";
     while (!g_ex->stop_ev.is_set()) {
-        bool gone = false, transport = false, failed = false;
+        bool gone = false, transport = false, failed = false, outage = false;
         std::string err;
         try {
             if (need_list) {
@@ -1468,15 +1473,17 @@ static Task<void> shard_informer(Shard* shp, int kind) {
             }
             co_await shard_watch(sh, kind);
             backoff = 0.8;
+            woken = false;
         } catch (const ApiError& e) {
             if (e.code == 410) {
                 gone = true;
             } else {
                 failed = true;
+                outage = e.code >= 500;
                 err = describe(std::current_exception());
             }
         } catch (const TransportError& e) {
-            failed = transport = true;
+            failed = transport = outage = true;
             err = e.what();
         } catch (const std::exception& e) {
             failed = true;
@@ -1490,7 +1497,13 @@ static Task<void> shard_informer(Shard* shp, int kind) {
         if (failed) {
             LOG_DEBUG("shard %s %s: list/watch failed: %s; retry in %.2fs", sh.name.c_str(), kPlural[kind],
                       err.c_str(), backoff);
-            co_await loop().sleep(backoff * (1 + jitter() * 0.2));
+            double wait = backoff * (1 + jitter() * 0.2);
+            if (outage && !woken) {
+                sh.answering.clear();
+                if (co_await sh.answering.wait_for(wait)) woken = true;  // the shard answers again
+            } else {
+                co_await loop().sleep(wait);
+            }
             backoff = std::min(backoff * 2, 30.0);
             if (!transport) {
                 need_list = true;
@@ -1501,6 +1514,11 @@ static Task<void> shard_informer(Shard* shp, int kind) {
 }
 
 // ------------------------------------------------------------------------------------ writes
+// An answer below 500 means the shard's apiserver is serving: wake reflectors waiting out an outage backoff.
+static void note_answer(Shard& sh, int status) {
+    if (status > 0 && status < 500 && !sh.answering.is_set()) sh.answering.set();
+}
+
 static Value owner_labels() {
     Value l = Value::object();
     l.set(kLabelApp, Value::str(kAgent));
@@ -1526,6 +1544,7 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
     std::string target =
         (std::string(method) == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) + kFieldManagerQuery;
     Response r = co_await sh.client->request(method, target, &data);
+    note_answer(sh, r.status);
     if (r.status >= 300) throw api_error(r.status, r.body);
     ShardPtr so = shard_obj_from_body(kind, r.body);
     // remember the intent only when the server stored something else (keeps the memo as small as the set
@@ -1542,6 +1561,7 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
 
 static Task<ShardPtr> shard_get_live(Shard& sh, int kind, const std::string& ns, const std::string& name) {
     Response r = co_await sh.client->request("GET", item_path(kind, ns, name), nullptr);
+    note_answer(sh, r.status);
     if (r.status >= 300) throw api_error(r.status, r.body);
     ShardPtr so = shard_obj_from_body(kind, r.body);
     shard_upsert(sh, kind, so, false);
@@ -1550,6 +1570,7 @@ static Task<ShardPtr> shard_get_live(Shard& sh, int kind, const std::string& ns,
 
 static Task<void> shard_delete(Shard& sh, int kind, const std::string& ns, const std::string& name) {
     Response r = co_await sh.client->request("DELETE", item_path(kind, ns, name), nullptr);
+    note_answer(sh, r.status);
     if (r.status >= 300 && r.status != 404) throw api_error(r.status, r.body);
 }
 

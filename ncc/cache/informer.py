@@ -102,6 +102,9 @@ class Informer:
         # the write's own echo — the common case — or applied if it is someone else's newer version.
         self._inflight: dict = {}
         self._stash: dict = {}
+        # set by the owner when the apiserver answers its other requests again (ncc/shards/shard.py): a
+        # list/watch waiting out an outage backoff retries at once, once per outage
+        self.answering: asyncio.Event | None = None
         # metadata_only: the consumer needs names/ownerReferences, never payloads (the coordinator's view
         # of Secrets/ConfigMaps).  MODIFIED events that leave the owner list unchanged are skipped without
         # decoding; stored objects keep metadata only.
@@ -488,6 +491,7 @@ class Informer:
         backoff = 0.8
         rv = ""
         need_list = True
+        woken = False
         list_rv = "0"  # cold start: served from the apiserver's watch cache
         while not self._stopping:
             try:
@@ -497,6 +501,7 @@ class Informer:
                     need_list = False
                 rv = await self._watch(self.last_rv or rv)  # resume after the last event we processed
                 backoff = 0.8
+                woken = False
             except asyncio.CancelledError:
                 raise
             except E.Gone:
@@ -506,7 +511,18 @@ class Informer:
             except Exception as e:  # noqa: BLE001 — transport errors, 5xx, etc.
                 self.last_error = e
                 log.debug("%s: list/watch failed: %r; retry in %.2fs", self.name, e, backoff)
-                await asyncio.sleep(backoff * (1 + random.random() * 0.2))
+                wait = backoff * (1 + random.random() * 0.2)
+                outage = isinstance(e, E.TransportError) or (isinstance(e, E.ApiError) and (e.code or 0) >= 500)
+                ans = self.answering
+                if outage and ans is not None and not woken:
+                    ans.clear()  # the owner's next answered request ends the wait (once per outage)
+                    try:
+                        await asyncio.wait_for(ans.wait(), wait)
+                        woken = True
+                    except asyncio.TimeoutError:
+                        pass
+                else:
+                    await asyncio.sleep(wait)
                 backoff = min(backoff * 2, 30.0)
                 if not isinstance(e, E.TransportError):
                     need_list = True

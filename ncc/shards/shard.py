@@ -20,6 +20,8 @@ workgroups and dependents support the orphan sweep.
 """
 from __future__ import annotations
 
+import asyncio
+
 from ..api import constants as C
 from ..api import resources as R
 from ..api.fingerprint import SLIM_FP, SLIM_WROTE, fingerprint
@@ -27,6 +29,7 @@ from ..api.objects import ObjectKey, meta
 from ..api.refs import template_owner_ref
 from ..cache.informer import Informer, InformerFactory
 from .. import native as _native
+from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, KubeClient
 
 
@@ -65,6 +68,9 @@ class Shard:
         if assume_writes:
             for inf in self.factory.informers():
                 inf.echo_fastpath = True
+        self.answering = asyncio.Event()
+        for inf in self.factory.informers():
+            inf.answering = self.answering
 
     # ---------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -89,8 +95,29 @@ class Shard:
         return await self.client.patch(rt, namespace, name, body, patch_type=patch_type,
                                        field_manager=field_manager, force=force)
 
+    def _answered(self) -> None:
+        """The shard's apiserver answered a request (< 500): its informers waiting out an outage backoff
+        retry at once (see Informer.answering)."""
+        if not self.answering.is_set():
+            self.answering.set()
+
+    async def _answer_tracking(self, coro):
+        try:
+            res = await coro
+        except E.ApiError as e:
+            if 0 < (e.code or 0) < 500:
+                self._answered()
+            raise
+        self._answered()
+        return res
+
     async def _tracked(self, informer: Informer, rt: R.ResourceType, verb: str, namespace: str, name: str,
                        body: dict, field_manager: str, patch_type=None, force=None):
+        return await self._answer_tracking(self._tracked_write(informer, rt, verb, namespace, name, body,
+                                                               field_manager, patch_type, force))
+
+    async def _tracked_write(self, informer: Informer, rt: R.ResourceType, verb: str, namespace: str, name: str,
+                             body: dict, field_manager: str, patch_type=None, force=None):
         """Run one write; publish its result to the informer (mutation overlay) and let the informer
         settle a watch event that overtook the response (see Informer.begin_write).
 
@@ -158,7 +185,7 @@ class Shard:
 
     async def delete_template(self, obj: dict) -> None:
         m = meta(obj)
-        await self.client.delete(R.TEMPLATES, m.get("namespace", ""), m.get("name", ""))
+        await self._answer_tracking(self.client.delete(R.TEMPLATES, m.get("namespace", ""), m.get("name", "")))
 
     # ---------------------------------------------------------------- workgroups
     async def create_workgroup(self, name: str, namespace: str, spec, field_manager: str) -> dict:
@@ -190,7 +217,7 @@ class Shard:
 
     async def delete_workgroup(self, obj: dict) -> None:
         m = meta(obj)
-        await self.client.delete(R.WORKGROUPS, m.get("namespace", ""), m.get("name", ""))
+        await self._answer_tracking(self.client.delete(R.WORKGROUPS, m.get("namespace", ""), m.get("name", "")))
 
     # ---------------------------------------------------------------- dependents
     def _dependent_body(self, rt: R.ResourceType, shard_template: dict, src: dict) -> dict:
@@ -271,7 +298,7 @@ class Shard:
 
     async def delete_dependent(self, rt: R.ResourceType, obj: dict) -> None:
         m = meta(obj)
-        await self.client.delete(rt, m.get("namespace", ""), m.get("name", ""))
+        await self._answer_tracking(self.client.delete(rt, m.get("namespace", ""), m.get("name", "")))
 
 
 _DROP_DEP = frozenset(("data", "binaryData", "stringData", SLIM_FP, SLIM_WROTE))

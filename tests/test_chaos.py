@@ -163,11 +163,9 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
             raise AssertionError(f"seed {seed} ({impl}) did not converge: {last}") from None
         rogue = [e for e in cl.cstate.list(R.EVENTS, NS)["items"] if e["reason"] == C.ERR_RESOURCE_EXISTS]
         assert rogue == []  # nothing here is a rogue object
-        # the model check sees a difference (and the controller repairs it): drift on one shard copy.  Only
-        # without a "down" episode: after one, a shard watch may sit in its reconnect backoff (client-go's
-        # 0.8 s doubling to 30 s) well after the shard is back, and drift is seen when it reconnects.
-        if downs:
-            return
+        # the model check sees a difference (and the controller repairs it): drift on one shard copy.  After
+        # a "down" episode too: a shard watch in its reconnect backoff (client-go's 0.8 s doubling to 30 s)
+        # retries as soon as the shard answers the executor's writes again.
         name = live[0]
         await mutate(cl.sc[0], R.TEMPLATES, name, lambda o: o["spec"]["container"].__setitem__("versionTag", "drift"))
         assert "spec differs" in _converged(cl)

@@ -130,6 +130,29 @@ async def test_informer_recovers_from_transport_errors():
     await srv.stop()
 
 
+async def test_answering_ends_an_outage_backoff_once():
+    """After an outage the list/watch backoff grows towards 30 s.  When the owner's other requests are
+    answered again (`Informer.answering`, set by ncc/shards/shard.py), the sleeping informer retries at once
+    — only once per outage, so an endpoint that keeps failing still backs off."""
+    srv = FakeApiServer()
+    url = await srv.start()
+    client = RestClient(ClusterConfig(server=url))
+    inf = Informer(client, R.SECRETS, NS)
+    inf.answering = asyncio.Event()
+    srv.faults.update({"down": True, "write_only": False})
+    inf.start()
+    await asyncio.sleep(2.0)  # failures at 0, ~0.8, ~2.4 s: the next wait is ~3.2 s
+    assert not inf.has_synced()
+    srv.faults.update({"down": False})
+    t0 = asyncio.get_running_loop().time()
+    inf.answering.set()  # e.g. a shard write succeeded
+    assert await inf.wait_for_sync(1.0)
+    assert asyncio.get_running_loop().time() - t0 < 1.0
+    await inf.stop()
+    await client.close()
+    await srv.stop()
+
+
 def test_store_indices_and_mutation_overlay():
     s = Store()
     s.add_indexer("owner", lambda o: [r["uid"] for r in o["metadata"].get("ownerReferences", [])])

@@ -301,3 +301,44 @@ async def test_token_file_is_reread_on_401(tmp_path):
         assert srv.state.get(R.TEMPLATES, NS, "algo-00001") is not None
     finally:
         await srv.stop()
+
+
+async def test_answered_write_ends_the_reflectors_outage_backoff():
+    """The C++ reflectors back off up to 30 s after a shard outage (client-go's schedule).  A write the shard
+    answers again wakes them at once (`Shard::answering`), so shard-side drift right after the outage is
+    repaired without waiting out the backoff."""
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        t0 = make_template(0, NS)
+        t0["metadata"].update(uid="u-0", resourceVersion="10", generation=1)
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, [t0]), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            assert (await ex.next_message("report"))["r"]["shard-0"] is None
+            srv.faults.update({"down": True, "write_only": False})
+            srv.drop_watches()
+            await asyncio.sleep(3.5)  # reflector failures at ~0, 0.8, 2.4 s: the current wait is ~3.2-6.4 s
+            srv.faults.update({"down": False})
+            t1 = make_template(1, NS)
+            t1["metadata"].update(uid="u-1", resourceVersion="11", generation=1)
+            ex.ch.send({"t": "w", "k": 0, "l": [line(t1)]})
+            assert (await ex.next_message("report", timeout=15))["r"]["shard-0"] is None
+            await asyncio.sleep(0.3)  # the woken reflectors relist and watch again
+            from ncc.kube.kubeconfig import ClusterConfig
+            from ncc.kube.rest import RestClient
+            client = RestClient(ClusterConfig(server=url))  # through the API: the watch streams see it
+            live = await client.get(R.TEMPLATES, NS, "algo-00000")
+            live["spec"]["container"]["versionTag"] = "drift"
+            await client.update(R.TEMPLATES, NS, live)
+            await client.close()
+            loop = asyncio.get_running_loop()
+            end = loop.time() + 1.5
+            while loop.time() < end:
+                if srv.state.get(R.TEMPLATES, NS, "algo-00000")["spec"]["container"]["versionTag"] != "drift":
+                    break
+                await asyncio.sleep(0.02)
+            assert srv.state.get(R.TEMPLATES, NS, "algo-00000")["spec"] == t0["spec"], "drift not repaired"
+            await ex.close()
+    finally:
+        await srv.stop()
