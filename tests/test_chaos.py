@@ -1,7 +1,8 @@
 """Randomised chaos against the native topology, checked against a model of the end state.
 
 A seeded sequence of user changes — template spec updates, Secret/ConfigMap payload updates, new templates
-(some sharing an existing dependent), template deletes — runs while the shards misbehave: a share of their
+(some sharing an existing dependent), templates pointed at another Secret, a referenced ConfigMap deleted
+and re-created, template deletes — runs while the shards misbehave: a share of their
 writes fail (503), a shard apiserver goes down and comes back, watch streams are cut, the watch history is
 compacted (resumes get 410 and relist), and executor processes are killed (the pool respawns them with a fresh snapshot).  Once the faults clear,
 every shard must hold exactly what the controller cluster implies:
@@ -70,13 +71,14 @@ def _converged(cl) -> str:
             have = {r["uid"] for r in live["metadata"].get("ownerReferences") or ()}
             if not uids <= have:
                 return f"shard {i}: {plural}/{n} owners {sorted(have)} lack {sorted(uids - have)}"
+        live_uids = {t["metadata"]["uid"] for t in ours.values()}
         for rt in (R.SECRETS, R.CONFIGMAPS):
             for o in s.list(rt, NS)["items"]:
                 if (rt.plural, o["metadata"]["name"]) not in want_owners:
-                    live_owners = {r["uid"] for r in o["metadata"].get("ownerReferences") or ()}
-                    if live_owners & {t["metadata"]["uid"] for t in ours.values()}:
-                        return f"shard {i}: {rt.plural}/{o['metadata']['name']} owned but unreferenced"
-                    if live_owners:
+                    # no longer referenced: kept while a live template still owns it (the reference never
+                    # removes ownerRefs), collected by the shard's GC once all its owners are gone
+                    owners = {r["uid"] for r in o["metadata"].get("ownerReferences") or ()}
+                    if owners and not owners & live_uids:
                         return f"shard {i}: {rt.plural}/{o['metadata']['name']} left behind by a deleted template"
     return ""
 
@@ -99,8 +101,8 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
         ops: dict = {}
         for _step in range(STEPS):
             version += 1
-            op = rnd.choices(["spec", "secret", "configmap", "create", "delete", "fault", "kill"],
-                             weights=[5, 4, 3, 2, 2, 3, 1])[0]
+            op = rnd.choices(["spec", "secret", "configmap", "create", "delete", "fault", "kill", "reref",
+                              "recreate"], weights=[5, 4, 3, 2, 2, 3, 1, 2, 1])[0]
             ops[op] = ops.get(op, 0) + 1
             if op == "spec" and live:
                 name = rnd.choice(live)
@@ -124,6 +126,27 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
                 await cl.cc.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
                 await cl.cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[sec], configmaps=[f"c{i}"]))
                 live.append(f"algo-{i:05d}")
+            elif op == "reref" and live:
+                # point a template at another Secret (an existing one, or a new one)
+                name = rnd.choice(live)
+                names = [o["metadata"]["name"] for o in cl.cstate.list(R.SECRETS, NS)["items"]]
+                target = rnd.choice(names) if names and rnd.random() < 0.5 else f"sx{version}"
+                if cl.cstate.try_get(R.SECRETS, NS, target) is None:
+                    await cl.cc.create(R.SECRETS, NS, make_secret(target, NS))
+
+                def reref(o, target=target):
+                    mev = o["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"]
+                    o["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"] = \
+                        [e for e in mev if not e.get("secretRef")] + [{"secretRef": {"name": target}}]
+                await mutate(cl.cc, R.TEMPLATES, name, reref)
+            elif op == "recreate":
+                # a referenced ConfigMap deleted and created again (its references go missing meanwhile)
+                names = [o["metadata"]["name"] for o in cl.cstate.list(R.CONFIGMAPS, NS)["items"]]
+                if names:
+                    n = rnd.choice(names)
+                    await cl.cc.delete(R.CONFIGMAPS, NS, n)
+                    await asyncio.sleep(rnd.uniform(0, 0.05))
+                    await cl.cc.create(R.CONFIGMAPS, NS, make_configmap(n, NS, version=version))
             elif op == "delete" and len(live) > 2:
                 name = live.pop(rnd.randrange(len(live)))
                 await cl.cc.delete(R.TEMPLATES, NS, name)
