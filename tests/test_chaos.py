@@ -83,15 +83,19 @@ def _converged(cl) -> str:
     return ""
 
 
-@pytest.mark.parametrize("impl", ["inprocess", "python", "native"])
+@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2"])
 @pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
-async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
+async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatch):
+    """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
+    the kills then also hit the child coordinator."""
     from ncc.controller.native_executor import binary_path
+    impl, _, parts = topology.partition("-c")
     if impl == "native" and binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
     rnd = random.Random(seed)
-    async with Cluster(tmp_path, impl, n_shards=2) as cl:
+    extra = {"coordinator_partitions": int(parts)} if parts else {}
+    async with Cluster(tmp_path, impl, n_shards=2, **extra) as cl:
         live = []
         for i in range(6):
             cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
@@ -166,14 +170,14 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
                     srv.state.compact()
                     srv.drop_watches()
             elif op == "kill" and kills < MAX_KILLS and cl.app.pool is not None:
-                h = rnd.choice(cl.app.pool.handles)
+                h = rnd.choice(cl.app.pool.handles + (cl.app.partitions.handles if cl.app.partitions else []))
                 if h.proc is not None and h.proc.returncode is None:
                     h.proc.kill()  # a crash: the pool respawns it (not `h.kill()`, which stops it for good)
                     kills += 1
             await asyncio.sleep(rnd.uniform(0, 0.03))
         for srv in cl.env.shard_servers:
             srv.faults.update({"error_rate": 0.0, "down": False})
-        print(f"seed {seed} {impl}: ops {ops}, executor kills {kills}, templates {len(live)}")
+        print(f"seed {seed} {topology}: ops {ops}, process kills {kills}, templates {len(live)}")
         last = ""
 
         async def done():
@@ -183,7 +187,7 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
         try:
             await wait_for(done, timeout=45, interval=0.2)
         except AssertionError:
-            raise AssertionError(f"seed {seed} ({impl}) did not converge: {last}") from None
+            raise AssertionError(f"seed {seed} ({topology}) did not converge: {last}") from None
         rogue = [e for e in cl.cstate.list(R.EVENTS, NS)["items"] if e["reason"] == C.ERR_RESOURCE_EXISTS]
         assert rogue == []  # nothing here is a rogue object
         # the model check sees a difference (and the controller repairs it): drift on one shard copy.  After
@@ -195,4 +199,4 @@ async def test_chaos_converges_to_the_model(tmp_path, impl, seed, monkeypatch):
         try:
             await wait_for(done, timeout=15, interval=0.1)
         except AssertionError:
-            raise AssertionError(f"seed {seed} ({impl}): drift on shard-0 not repaired: {last}") from None
+            raise AssertionError(f"seed {seed} ({topology}): drift on shard-0 not repaired: {last}") from None
