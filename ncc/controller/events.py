@@ -43,6 +43,7 @@ SPAM_QPS = 1.0 / 300.0
 AGGREGATE_MAX_EVENTS = 10
 AGGREGATE_INTERVAL_S = 600.0
 BUFFER = 1000
+WARNING_OVERFLOW = 16384  # native: Warnings held past a full buffer (beyond this they are dropped too)
 
 
 class EventRecorder:
@@ -128,7 +129,7 @@ class BroadcastRecorder(EventRecorder):
         self._tasks: list[asyncio.Task] = []
         self._write_meta = getattr(client, "write_meta", None)  # undecoded writes (REST clients)
         self.stats = {"recorded": 0, "dropped_spam": 0, "dropped_full": 0, "created": 0, "patched": 0, "failed": 0,
-                      "merged": 0}
+                      "merged": 0, "warnings_held": 0}
 
     def start(self) -> None:
         if not self._tasks:
@@ -197,7 +198,9 @@ class BroadcastRecorder(EventRecorder):
 
     def _enqueue(self, entry: list, held: bool = False) -> bool:
         """Queue for its object's writer; False when that buffer is full (a new event is then dropped, as
-        client-go drops on a full broadcaster buffer; a held repeat stays held)."""
+        client-go drops on a full broadcaster buffer; a held repeat stays held).  With coalescing (native
+        mode) a Warning is not dropped for a full buffer: it waits in the held set and goes out with the
+        next flush — a burst of `Synced` Events must not swallow the one that reports a failure."""
         ref, key = entry[0], entry[5]
         q = self._queue if self.writers == 1 else \
             self._queues[hash((ref["namespace"], ref["name"], ref["kind"])) % self.writers]
@@ -206,6 +209,12 @@ class BroadcastRecorder(EventRecorder):
         try:
             q.put_nowait(entry)
         except asyncio.QueueFull:
+            if self.coalesce and entry[1] == C.EVENT_TYPE_WARNING and len(self._deferred) < WARNING_OVERFLOW:
+                self._deferred[key] = entry
+                self.stats["warnings_held"] += 1
+                if self._flush_timer is None:
+                    self._flush_timer = asyncio.get_running_loop().call_later(0.01, self._flush_deferred)
+                return False
             self.stats["dropped_full"] += 1
             return False
         if self.coalesce:

@@ -133,6 +133,39 @@ async def test_native_correlator_cache_follows_the_object_count():
     await rec.stop()
 
 
+async def test_warning_is_held_not_dropped_when_the_buffer_is_full():
+    """Native mode: a flood of `Synced` Events fills the writers' buffer (client-go drops past it, and so do
+    we for Normal events), but a Warning recorded meanwhile is held and written once there is room."""
+    client = FakeClient(ClusterState(), simple=False)
+    gate = asyncio.Event()
+    real_create = client.create
+
+    async def slow_create(rt, ns, body, **kw):
+        await gate.wait()
+        return await real_create(rt, ns, body, **kw)
+    client.create = slow_create
+    rec = BroadcastRecorder(client, log_events=False, writers=1, coalesce=True, repeat_window=1.0)
+    rec._write_meta = None  # through client.create
+    rec.start()
+
+    def obj(i):
+        return {"kind": "NexusAlgorithmTemplate", "apiVersion": "science.sneaksanddata.com/v1",
+                "metadata": {"name": f"t{i}", "namespace": "nexus", "uid": f"u{i}"}}
+    for i in range(1100):  # one blocked in the writer, 1000 buffered, the rest dropped
+        rec.event(obj(i), "Normal", "Synced", "synced")
+        await asyncio.sleep(0) if i == 0 else None
+    assert rec.stats["dropped_full"] > 0
+    rec.event(obj(5000), "Warning", "ErrResourceExists", "Secret already exists")
+    assert rec.stats["warnings_held"] == 1
+    gate.set()
+    for _ in range(500):
+        if any(e["reason"] == "ErrResourceExists" for e in client.state.list(R.EVENTS, "nexus")["items"]):
+            break
+        await asyncio.sleep(0.01)
+    assert any(e["reason"] == "ErrResourceExists" for e in client.state.list(R.EVENTS, "nexus")["items"])
+    await rec.stop()
+
+
 def test_fake_recorder_formats_like_client_go():
     r = FakeRecorder()
     r.event({}, "Warning", "ErrResourceMissing", "msg")
