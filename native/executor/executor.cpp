@@ -11,7 +11,7 @@
 //                             {"t":"go"}   warm standby acquired the Lease: start the workers
 //                             {"t":"resync","p":p,"n":C}   pass again over the keys of coordinator partition p
 //                             {"t":"cred","s":shard,"token":...}   refreshed exec credential
-//   executor -> coordinator   {"t":"synced","i":n}, {"t":"ready","i":n}
+//   executor -> coordinator   {"t":"synced","i":n}, {"t":"ready","i":n}, {"t":"status",...} (every 5 s)
 //                             {"t":"report","k":key,"u":uid,"g":generation,"r":{shard:error|nil},"w":wrote}
 //                             {"t":"need","k":kind,"n":"ns/name"}   a referenced dependent not yet relayed
 //
@@ -825,6 +825,12 @@ private:
 };
 static Channel* g_chan = nullptr;
 
+// {"t":"status","i":n,"s":{shard:{plural:[synced, watching, events, relists, last error]}},"q":queued,
+// "r":passes,"w":writes,"e":errors} every NCC_STATUS_S (5) seconds: the coordinator's /debug/state shows
+// each executor's view of its shards (is the watch up, what failed last).
+static void send_status();
+static Task<void> status_loop();
+
 static void send_simple(const char* t) {
     mp::Encoder e;
     e.map(2);
@@ -940,6 +946,8 @@ struct Informer {
     int kind = 0;
     std::unordered_map<std::string, ShardPtr> store;
     bool synced = false;
+    bool watching = false;   // a watch request is open (status reports)
+    std::string last_error;  // the last list/watch failure, "" once a watch succeeds again
     Event synced_ev;
     std::string last_rv;
     long long events = 0, relists = 0, echoes = 0, foreign = 0;
@@ -1471,7 +1479,10 @@ static Task<void> shard_informer(Shard* shp, int kind) {
                 co_await shard_list(sh, kind, list_rv);
                 need_list = false;
             }
+            sh.inf[kind].watching = true;
+            sh.inf[kind].last_error.clear();
             co_await shard_watch(sh, kind);
+            sh.inf[kind].watching = false;
             backoff = 0.8;
             woken = false;
         } catch (const ApiError& e) {
@@ -1494,7 +1505,9 @@ static Task<void> shard_informer(Shard* shp, int kind) {
             list_rv = "";
             continue;
         }
+        sh.inf[kind].watching = false;
         if (failed) {
+            sh.inf[kind].last_error = err.substr(0, 300);
             LOG_DEBUG("shard %s %s: list/watch failed: %s; retry in %.2fs", sh.name.c_str(), kPlural[kind],
                       err.c_str(), backoff);
             double wait = backoff * (1 + jitter() * 0.2);
@@ -2125,6 +2138,7 @@ static Task<void> run_main() {
     co_await configured.wait();
     for (auto& sp : ex.shards)
         for (int k = 0; k < 4; ++k) spawn(shard_informer(sp.get(), k), "shard informer");
+    spawn(status_loop(), "status");
     co_await ex.ctl_synced_ev.wait();
     std::vector<Task<void>> waits;
     for (auto& sp : ex.shards) waits.push_back(wait_shard_synced(sp.get(), g_opt.shard_sync_timeout));
@@ -2137,6 +2151,51 @@ static Task<void> run_main() {
     send_simple("ready");
     LOG_INFO("native executor %d ready: %zu shard(s), partition %d/%d, %d workers", g_opt.index, ex.shards.size(),
              g_opt.part, g_opt.parts, g_opt.workers);
+}
+
+static void send_status() {
+    Executor& ex = *g_ex;
+    mp::Encoder e;
+    e.map(7);
+    e.str("t");
+    e.str("status");
+    e.str("i");
+    e.integer(g_opt.index);
+    e.str("s");
+    e.map(ex.shards.size());
+    for (const auto& sp : ex.shards) {
+        e.str(sp->name);
+        e.map(4);
+        for (int k = 0; k < 4; ++k) {
+            const Informer& inf = sp->inf[k];
+            e.str(kPlural[k]);
+            e.array(5);
+            e.boolean(inf.synced);
+            e.boolean(inf.watching);
+            e.integer(inf.events);
+            e.integer(inf.relists);
+            e.str(inf.last_error);
+        }
+    }
+    e.str("q");
+    e.integer(static_cast<long long>(ex.queue.load()));
+    e.str("r");
+    e.integer(ex.stats_reconciles);
+    e.str("w");
+    e.integer(ex.stats_writes);
+    e.str("e");
+    e.integer(ex.stats_errors);
+    g_chan->send(std::move(e.out));
+}
+
+static Task<void> status_loop() {
+    Executor& ex = *g_ex;
+    double period = 5.0;
+    if (const char* v = std::getenv("NCC_STATUS_S")) period = std::max(0.05, std::atof(v));
+    while (!ex.stop_ev.is_set()) {
+        send_status();
+        co_await ex.stop_ev.wait_for(period);
+    }
 }
 
 // The coordinator closing the channel (or dying), or a signal, ends the executor — at any point, including

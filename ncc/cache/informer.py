@@ -105,6 +105,7 @@ class Informer:
         # set by the owner when the apiserver answers its other requests again (ncc/shards/shard.py): a
         # list/watch waiting out an outage backoff retries at once, once per outage
         self.answering: asyncio.Event | None = None
+        self.watching = False  # a watch request is open (executor status)
         # metadata_only: the consumer needs names/ownerReferences, never payloads (the coordinator's view
         # of Secrets/ConfigMaps).  MODIFIED events that leave the owner list unchanged are skipped without
         # decoding; stored objects keep metadata only.
@@ -499,7 +500,12 @@ class Informer:
                     rv = await self._list(list_rv)
                     self.last_rv = rv
                     need_list = False
-                rv = await self._watch(self.last_rv or rv)  # resume after the last event we processed
+                self.watching = True
+                self.last_error = None
+                try:
+                    rv = await self._watch(self.last_rv or rv)  # resume after the last event we processed
+                finally:
+                    self.watching = False
                 backoff = 0.8
                 woken = False
             except asyncio.CancelledError:

@@ -23,6 +23,7 @@ import logging
 import os
 import socket
 import sys
+import time
 import zlib
 
 from .ipc import Channel, RawChannel
@@ -96,6 +97,7 @@ class ExecutorHandle:
         self.ready = asyncio.Event()  # workers running
         self.synced = asyncio.Event()  # caches synced (a gated child reports this before it may run)
         self.restarts = 0
+        self.status: dict | None = None  # the executor's last {"t": "status"} (status_view), for /debug/state
         self.gated = False  # spawned for a warm standby: workers wait for {"t": "go"}
         self.gate_open = False
         self.on_spawn = None  # callable(handle) once the channel to a (re)started child is up (watch relay)
@@ -208,6 +210,9 @@ class ExecutorHandle:
             elif t == "need":
                 if self.on_need is not None:
                     self.on_need(self, msg)
+                continue
+            elif t == "status":
+                self.status = status_view(msg)
                 continue
             self.on_message(self.index, msg)
 
@@ -335,7 +340,8 @@ class ExecutorPool:
     def stats(self) -> dict:
         return {h.index: {"shards": h.shards, "part": f"{h.part}/{h.parts}", "restarts": h.restarts,
                           "impl": "native" if h.native else "python",
-                          "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
+                          "alive": h.proc is not None and h.proc.returncode is None, "status": h.status}
+                for h in self.handles}
 
 
 class CoordinatorPartitions:
@@ -397,6 +403,32 @@ class CoordinatorPartitions:
     def stats(self) -> dict:
         return {h.index: {"part": f"{h.part}/{h.parts}", "restarts": h.restarts, "ready": h.ready.is_set(),
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
+
+
+def status_view(msg: dict) -> dict:
+    """An executor's periodic status message ({"t": "status", "s": {shard: {plural: [synced, watching,
+    events, relists, last error]}}, "q", "r", "w", "e"}) as /debug/state shows it."""
+    shards = {}
+    for shard, kinds in (msg.get("s") or {}).items():
+        shards[shard] = {plural: {"synced": bool(v[0]), "watching": bool(v[1]), "events": v[2], "relists": v[3],
+                                  "last_error": v[4] or None}
+                         for plural, v in (kinds or {}).items() if isinstance(v, (list, tuple)) and len(v) >= 5}
+    return {"shards": shards, "queued": msg.get("q"), "passes": msg.get("r"), "writes": msg.get("w"),
+            "errors": msg.get("e"), "at": time.time()}
+
+
+def status_message(index: int, shards: list, stats: dict) -> dict:
+    """The Python executor's status message, the same shape as the C++ executor's (`send_status`)."""
+    out = {}
+    for sh in shards:
+        kinds = {}
+        for inf in sh.factory.informers():
+            err = inf.last_error if not inf.watching else None
+            kinds[inf.rt.plural] = [inf.has_synced(), inf.watching, inf.events, inf.relists,
+                                    repr(err)[:300] if err is not None else ""]
+        out[sh.name] = kinds
+    return {"t": "status", "i": index, "s": out, "q": stats.get("queued"), "r": stats.get("reconciles"),
+            "w": stats.get("writes"), "e": stats.get("errors")}
 
 
 # ---------------------------------------------------------------------------------------- executor side
@@ -465,11 +497,23 @@ async def executor_main(fd: int, index: int, shards: list[str], part: tuple = (0
                 elif msg.get("t") == "resync" and app.controller is not None:
                     app.controller.enqueue_all(part=(int(msg.get("p", 0)), int(msg.get("n", 1))))
 
+    async def send_status():
+        period = float(os.environ.get("NCC_STATUS_S", "5"))
+        while True:
+            c = app.controller
+            st = dict(c.stats) if c is not None else {}
+            if c is not None:
+                st["queued"] = len(c.queue)
+            channel.send(status_message(index, app.shards, st))
+            await asyncio.sleep(period)
+
     wp = asyncio.ensure_future(watch_parent())
+    sp = asyncio.ensure_future(send_status())
     try:
         await app.run(stop)
     finally:
         wp.cancel()
+        sp.cancel()
         try:
             await channel.drain()
         except Exception:  # noqa: BLE001

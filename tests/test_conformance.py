@@ -607,3 +607,35 @@ async def test_raw_channel_closes_on_a_peer_that_stops_reading(monkeypatch):
     finally:
         ch.close()
         b.close()
+
+
+async def test_executor_status_in_debug_state(tmp_path, impl, monkeypatch):
+    """Every executor reports its shards' watch state every NCC_STATUS_S seconds; /debug/state shows it per
+    executor — synced, watching, events, relists and the last list/watch error (a shard that is down)."""
+    if impl == "inprocess":
+        pytest.skip("no executors")
+    monkeypatch.setenv("NCC_STATUS_S", "0.1")
+    async with Cluster(tmp_path, impl) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+
+        def status():
+            ex = cl.app.debug_state()["executors"]
+            return {s: st for h in ex.values() if h.get("status") for s, st in h["status"]["shards"].items()}
+
+        async def all_watching():
+            st = status()
+            return sorted(st) == ["shard-0", "shard-1"] and all(
+                k["synced"] and k["watching"] for s in st.values() for k in s.values()) and st
+        st = await wait_for(all_watching)
+        assert st["shard-0"]["nexusalgorithmtemplates"]["events"] >= 0
+        cl.env.shard_servers[1].faults.update({"down": True, "write_only": False})
+        cl.env.shard_servers[1].drop_watches()
+
+        async def down_seen():
+            st = status().get("shard-1") or {}
+            return st and all(not k["watching"] and k["last_error"] for k in st.values())
+        await wait_for(down_seen, timeout=10)
+        assert all(k["watching"] for k in status()["shard-0"].values())
+        cl.env.shard_servers[1].faults.update({"down": False})

@@ -245,6 +245,9 @@ async def test_executor_protocol_in_process(tmp_path, monkeypatch):
         while loop.time() < end and not any(m.get("t") == "report" for m in msgs):
             batch = await asyncio.wait_for(ch.recv(), 15)
             msgs.extend(batch or [])
+        status = [m for m in msgs if m.get("t") == "status"]  # periodic, from the start (shape: status_view)
+        assert status and set(status[0]["s"]) == {"shard-0"}
+        msgs = [m for m in msgs if m.get("t") != "status"]
         assert msgs[:2] == [{"t": "synced", "i": 0}, {"t": "ready", "i": 0}]
         rep = next(m for m in msgs if m.get("t") == "report")
         assert rep["k"] == f"template/{NS}/algo-00001" and rep["r"] == {"shard-0": None} and rep["w"] is True
