@@ -82,7 +82,7 @@ async def test_idle_executor_with_unreachable_shard_does_not_poll():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     shard = {"name": "dead", "server": f"http://127.0.0.1:{port}"}
-    async with Executor(cfg([shard]), env={"NCC_CPU_REPORT": "1"}) as ex:
+    async with Executor(cfg([shard]), env={"NCC_CPU_REPORT": "1", "NCC_STATUS_S": "5"}) as ex:
         for k in range(4):
             ex.snapshot(k, [])
         # the controller side is synced; the executor now waits (up to 30 s) for the dead shard's caches
