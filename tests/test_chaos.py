@@ -40,16 +40,17 @@ def _deps(t: dict) -> tuple[list, list]:
             [e["configMapRef"]["name"] for e in mev if e.get("configMapRef")])
 
 
-def _converged(cl) -> str:
-    """'' when every shard matches the model, else the first difference found."""
-    shards = cl.env.shard_names
+def _converged(cl, active=None) -> str:
+    """'' when every (active) shard matches the model, else the first difference found."""
+    active = sorted(active if active is not None else range(len(cl.sstates)))
+    shards = [cl.env.shard_names[i] for i in active]
     templates = {t["metadata"]["name"]: t for t in cl.cstate.list(R.TEMPLATES, NS)["items"]}
     for name, t in templates.items():
         st = t.get("status") or {}
         c = (st.get("conditions") or [{}])[0]
         if c.get("status") != "True" or st.get("syncedToClusters") != shards:
             return f"{name}: status {c.get('status')} {st.get('syncedToClusters')}"
-    for i, s in enumerate(cl.sstates):
+    for i, s in ((i, cl.sstates[i]) for i in active):
         ours = {t["metadata"]["name"]: t for t in s.list(R.TEMPLATES, NS)["items"]}
         if set(ours) != set(templates):
             return f"shard {i}: templates {sorted(set(ours) ^ set(templates))} differ"
@@ -83,19 +84,28 @@ def _converged(cl) -> str:
     return ""
 
 
-@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2"])
+@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload"])
 @pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
 async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatch):
     """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
     the kills then also hit the child coordinator."""
     from ncc.controller.native_executor import binary_path
-    impl, _, parts = topology.partition("-c")
+    reload = topology.endswith("-reload")
+    impl, _, parts = topology.replace("-reload", "").partition("-c")
     if impl == "native" and binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
     rnd = random.Random(seed)
     extra = {"coordinator_partitions": int(parts)} if parts else {}
-    async with Cluster(tmp_path, impl, n_shards=2, **extra) as cl:
+    if reload:  # a third shard whose kubeconfig comes and goes (hot reload of the shards directory)
+        extra["shard_reload_period"] = 0
+    async with Cluster(tmp_path, impl, n_shards=3 if reload else 2, **extra) as cl:
+        active = {0, 1, 2}
+        if reload:
+            kc = os.path.join(cl.env.shard_dir, "shard-2.kubeconfig")
+            parked = os.path.join(str(tmp_path), "shard-2.kubeconfig.parked")
+            os.replace(kc, parked)
+            active = {0, 1}
         live = []
         for i in range(6):
             cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
@@ -106,7 +116,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         for _step in range(STEPS):
             version += 1
             op = rnd.choices(["spec", "secret", "configmap", "create", "delete", "fault", "kill", "reref",
-                              "recreate"], weights=[5, 4, 3, 2, 2, 3, 1, 2, 1])[0]
+                              "recreate", "reshard"], weights=[5, 4, 3, 2, 2, 3, 1, 2, 1, 2 if reload else 0])[0]
             ops[op] = ops.get(op, 0) + 1
             if op == "spec" and live:
                 name = rnd.choice(live)
@@ -151,6 +161,14 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
                     await cl.cc.delete(R.CONFIGMAPS, NS, n)
                     await asyncio.sleep(rnd.uniform(0, 0.05))
                     await cl.cc.create(R.CONFIGMAPS, NS, make_configmap(n, NS, version=version))
+            elif op == "reshard":  # shard-2 joins or leaves
+                if 2 in active:
+                    os.replace(kc, parked)
+                    active.discard(2)
+                else:
+                    os.replace(parked, kc)
+                    active.add(2)
+                await cl.app.reload_shards()
             elif op == "delete" and len(live) > 2:
                 name = live.pop(rnd.randrange(len(live)))
                 await cl.cc.delete(R.TEMPLATES, NS, name)
@@ -182,7 +200,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
 
         async def done():
             nonlocal last
-            last = _converged(cl)
+            last = _converged(cl, active)
             return last == ""
         try:
             await wait_for(done, timeout=45, interval=0.2)
@@ -195,7 +213,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         # retries as soon as the shard answers the executor's writes again.
         name = live[0]
         await mutate(cl.sc[0], R.TEMPLATES, name, lambda o: o["spec"]["container"].__setitem__("versionTag", "drift"))
-        assert "spec differs" in _converged(cl)
+        assert "spec differs" in _converged(cl, active)
         try:
             await wait_for(done, timeout=15, interval=0.1)
         except AssertionError:
