@@ -100,7 +100,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
     if reload:  # a third shard whose kubeconfig comes and goes (hot reload of the shards directory)
         extra["shard_reload_period"] = 0
     async with Cluster(tmp_path, impl, n_shards=3 if reload else 2, **extra) as cl:
-        active = {0, 1, 2}
+        active = set(range(len(cl.sstates)))
         if reload:
             kc = os.path.join(cl.env.shard_dir, "shard-2.kubeconfig")
             parked = os.path.join(str(tmp_path), "shard-2.kubeconfig.parked")
