@@ -74,6 +74,9 @@ constexpr const char* kApiVersion = "science.sneaksanddata.com/v1";
 constexpr const char* kTemplateKind = "NexusAlgorithmTemplate";
 constexpr const char* kWorkgroupKind = "NexusAlgorithmWorkgroup";
 constexpr const char* kFieldManagerQuery = "?fieldManager=nexus-configuration-controller";
+// server-side apply (`server-side-apply: true`): the controller is the sole manager of what it applies
+constexpr const char* kApplyQuery = "?fieldManager=nexus-configuration-controller&force=true";
+constexpr const char* kApplyType = "application/apply-patch+yaml";
 constexpr const char* kLabelApp = "science.sneaksanddata.com/controller-app";
 constexpr const char* kLabelOwner = "science.sneaksanddata.com/configuration-owner";
 constexpr const char* kAgent = "nexus-configuration-controller";
@@ -121,6 +124,7 @@ struct Options {
     bool sync_secret_type = true;
     bool orphan_sweep = true;
     bool propagate_workgroup_deletes = true;
+    bool server_side_apply = false;  // shard writes as one apply PATCH (create-or-update) instead of POST/PUT
     int log_level = 30;  // Python logging levels
     bool gated = false;
 };
@@ -1554,9 +1558,11 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
                                   uint64_t want_b) {
     pass->wrote = true;
     ++g_ex->stats_writes;
-    std::string target =
-        (std::string(method) == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) + kFieldManagerQuery;
-    Response r = co_await sh.client->request(method, target, &data);
+    std::string_view m(method);
+    bool apply = m == "PATCH";  // the only PATCH this executor sends is a server-side apply
+    std::string target = (m == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) +
+                         (apply ? kApplyQuery : kFieldManagerQuery);
+    Response r = co_await sh.client->request(method, target, &data, apply ? kApplyType : "application/json");
     note_answer(sh, r.status);
     if (r.status >= 300) throw api_error(r.status, r.body);
     ShardPtr so = shard_obj_from_body(kind, r.body);
@@ -1589,8 +1595,30 @@ static Task<void> shard_delete(Shard& sh, int kind, const std::string& ns, const
 
 // create-or-update of a template/workgroup (native `_write`: AlreadyExists/Conflict -> re-read the live
 // object; a Conflict on update is retried once from it)
+static Value crd_head(int kind, const CtlObj& want) {
+    Value head = Value::object();
+    head.set("apiVersion", Value::str(kApiVersion));
+    head.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
+    Value m = Value::object();
+    m.set("name", Value::str(want.name));
+    m.set("namespace", Value::str(want.ns));
+    m.set("labels", owner_labels());
+    head.set("metadata", std::move(m));
+    return head;
+}
+
 static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj& want, PassState* pass) {
     std::string_view spec = want.spec_raw.empty() ? std::string_view("null") : std::string_view(want.spec_raw);
+    if (g_opt.server_side_apply) {
+        // Shard.apply_template / apply_workgroup: one apply creates or updates; it carries no
+        // resourceVersion, so there is no AlreadyExists/Conflict race to resolve
+        std::string body;
+        {
+            PhaseTimer pt(PH_BODY);
+            body = dumps_with(crd_head(kind, want), {{"spec", spec}});
+        }
+        co_return co_await shard_write(sh, kind, "PATCH", want.ns, want.name, std::move(body), pass, want.fp_spec, 0);
+    }
     bool update = cur != nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
         std::string body;
@@ -1599,15 +1627,7 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
             body = splice_members(cur->rest, {{"spec", spec}});
         } else {
             PhaseTimer pt(PH_BODY);
-            Value head = Value::object();
-            head.set("apiVersion", Value::str(kApiVersion));
-            head.set("kind", Value::str(kind == TEMPLATES ? kTemplateKind : kWorkgroupKind));
-            Value m = Value::object();
-            m.set("name", Value::str(want.name));
-            m.set("namespace", Value::str(want.ns));
-            m.set("labels", owner_labels());
-            head.set("metadata", std::move(m));
-            body = dumps_with(head, {{"spec", spec}});
+            body = dumps_with(crd_head(kind, want), {{"spec", spec}});
         }
         bool race = false, exists = false;
         try {
@@ -1691,6 +1711,31 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         (void)exists;
         co_return co_await shard_get_live(sh, kind, shard_ns, dep);
     };
+    if (g_opt.server_side_apply) {
+        // Shard.apply_dependent: refuse a rogue copy, skip one in sync that already carries our ownerRef,
+        // otherwise apply our view (the server unions the ownerRefs by uid, so other owners' stay)
+        if (so) {
+            if (!so->has_owner_refs)
+                throw NamedError("RogueResourceError", "Resource \"" + dep +
+                                                           "\" already exists and is not managed by any Machine "
+                                                           "Learning Algorithm");
+            bool ours = false;
+            for (const auto& o : so->template_owners)
+                if (o.second == st->uid) ours = true;
+            bool type_changed = is_secret && g_opt.sync_secret_type &&
+                                (src->type.empty() ? std::string("Opaque") : src->type) !=
+                                    (so->type.empty() ? std::string("Opaque") : so->type);
+            if (type_changed) {  // Secret.type is immutable: an apply cannot change it, so replace the copy
+                pass->wrote = true;
+                co_await shard_delete(sh, kind, shard_ns, dep);
+                sh.inf[kind].store.erase(key_of(shard_ns, dep));
+            } else if (ours && data_in_sync(sh, kind, *so, *src)) {
+                co_return;
+            }
+        }
+        co_await shard_write(sh, kind, "PATCH", shard_ns, dep, create_body(), pass, src->fp_data, src->fp_bin);
+        co_return;
+    }
     if (!so) so = co_await create();
     // isMissingOwnership (controller.go:482-502): no ownerRefs at all = a rogue object we refuse to touch
     if (!so->has_owner_refs)
@@ -2022,6 +2067,7 @@ static void configure(const Value& c) {
     o.sync_secret_type = num(c, "sync_secret_type", 1) != 0;
     o.orphan_sweep = num(c, "orphan_sweep", 1) != 0;
     o.propagate_workgroup_deletes = num(c, "propagate_workgroup_deletes", 1) != 0;
+    o.server_side_apply = num(c, "server_side_apply", 0) != 0;
     o.log_level = static_cast<int>(num(c, "log_level", o.log_level));
     if (o.full_resync <= 0) o.full_resync = 1e9;
     Executor& ex = *g_ex;

@@ -12,8 +12,8 @@ Python (ncc/kube/kubeconfig.py): the executor receives the server URL, CA / clie
 and a bearer token; exec tokens are refreshed here and pushed as `{"t": "cred"}` messages.
 
 `executor-impl: auto` (default) picks the native executor whenever the binary is built and the
-configuration is one it implements (native mode with the watch relay, PUT-based writes); otherwise
-the Python executor runs.  Server-side apply (`server-side-apply: true`) stays on the Python path.
+configuration is one it implements (native mode with the watch relay; POST/PUT writes, or server-side
+apply with `server-side-apply: true`); otherwise the Python executor runs.
 """
 from __future__ import annotations
 
@@ -48,8 +48,6 @@ def choose(cfg, options, relay_active: bool, quiet: bool = False) -> tuple[bool,
         reasons.append("ncc/bin/ncc-executor is not built (python native/build.py)")
     if not relay_active:
         reasons.append("the watch relay is off")
-    if options.server_side_apply:
-        reasons.append("server-side-apply is implemented by the Python executor only")
     if reasons:
         if impl == "native" and not quiet:
             log.warning("executor-impl: native requested but unavailable (%s); using the Python executor",
@@ -129,7 +127,7 @@ class NativeExecutorConfig:
             "shard_sync_timeout": o.wait_for_shards_timeout if o.wait_for_shards_timeout is not None else 3600.0,
             "full_resync_period": o.full_resync_period, "sync_binary_data": o.sync_binary_data,
             "sync_secret_type": o.sync_secret_type, "orphan_sweep": o.orphan_sweep,
-            "propagate_workgroup_deletes": o.propagate_workgroup_deletes,
+            "propagate_workgroup_deletes": o.propagate_workgroup_deletes, "server_side_apply": o.server_side_apply,
             "log_level": _LEVELS.get(str(cfg.log_level).upper(), 30), "shards": shards,
         }
         return json.dumps(doc)

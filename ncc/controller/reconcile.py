@@ -636,7 +636,12 @@ class ReconcileMixin:
                 if shard_obj is not None:
                     missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template,
                                                               shard.name)  # rogue → error
-                    if not missing_owner and data_matches(src, shard_obj, with_binary):
+                    if is_secret and opts.sync_secret_type and \
+                            (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
+                        # Secret.type is immutable, so an apply cannot change it: replace the copy
+                        self._pass_wrote()
+                        await self._delete_one(shard, lambda o: shard.delete_dependent(R.SECRETS, o), shard_obj)
+                    elif not missing_owner and data_matches(src, shard_obj, with_binary):
                         return
                 self._pass_wrote()
                 await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)

@@ -523,6 +523,44 @@ async def test_one_executor_serving_several_shards(tmp_path, impl):
         await cl.ready()
 
 
+async def test_server_side_apply(tmp_path, impl):
+    """`server-side-apply: true` (Shard.apply_*; the C++ executor implements it too): every shard write is
+    one apply PATCH.  Fan-out, a spec update, another owner's ref kept (the server unions ownerRefs by uid),
+    a rogue copy refused with the reference's Warning Events, a Secret.type change replacing the copy."""
+    async with Cluster(tmp_path, impl, n_shards=2, server_side_apply=True) as cl:
+        other = cl.sstates[0].create(R.TEMPLATES, NS, make_template(99, NS))
+        shared = make_secret("s0", NS, version=42)
+        shared["metadata"]["ownerReferences"] = [{"apiVersion": C.API_VERSION, "kind": C.TEMPLATE_KIND,
+                                                  "name": other["metadata"]["name"], "uid": other["metadata"]["uid"]}]
+        cl.sstates[0].create(R.SECRETS, NS, shared)
+        cl.sstates[1].create(R.CONFIGMAPS, NS, make_configmap("c1", NS, version=3))  # rogue on shard-1
+        cl.seed()
+        cl.seed(1, secrets=("s0",), configmaps=("c1",))
+        cl.cstate.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        await cl.start()
+        await cl.ready()
+        t1 = "algo-00001"
+        await cl.not_ready(t1, "shard-1", 'ConfigMap "c1"', "RogueResourceError")
+        await cl.wait_events(C.ERR_RESOURCE_EXISTS, name=t1)
+        assert cl.sstates[1].get(R.CONFIGMAPS, NS, "c1")["data"] != cl.cstate.get(R.CONFIGMAPS, NS, "c1")["data"]
+        live = cl.sstates[0].get(R.SECRETS, NS, "s0")
+        assert live["data"] == cl.cstate.get(R.SECRETS, NS, "s0")["data"]
+        uids = {r["uid"] for r in live["metadata"]["ownerReferences"]}
+        assert other["metadata"]["uid"] in uids and cl.sstates[0].get(R.TEMPLATES, NS, T0)["metadata"]["uid"] in uids
+        await wait_for(lambda: asyncio.sleep(0, all(s.try_get(R.WORKGROUPS, NS, "mi355x") for s in cl.sstates)))
+        await mutate(cl.cc, R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("image", "img:v2"))
+        await wait_for(lambda: asyncio.sleep(0, all(
+            s.get(R.TEMPLATES, NS, T0)["spec"]["container"]["image"] == "img:v2" for s in cl.sstates)))
+        old_uid = cl.sstates[1].get(R.SECRETS, NS, "s0")["metadata"]["uid"]
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o.__setitem__("type", "kubernetes.io/dockerconfigjson"))
+        await wait_for(lambda: asyncio.sleep(0, (lambda x: x is not None and x.get("type") ==
+                                                 "kubernetes.io/dockerconfigjson" and x["metadata"]["uid"] != old_uid)(
+            cl.sstates[1].try_get(R.SECRETS, NS, "s0"))))
+        for i in range(2):
+            writes = [w for w in cl.env.shard_servers[i].writes if w[0] not in ("GET",)]
+            assert writes and {w[0] for w in writes} <= {"PATCH", "DELETE"}, writes
+
+
 def test_every_implementation_is_exercised():
     """The suite must not silently shrink to one topology: the C++ executor is built in this tree."""
     if os.environ.get("NCC_SKIP_NATIVE_BUILD") != "1":
