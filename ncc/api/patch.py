@@ -7,7 +7,8 @@
 * A single-manager approximation of server-side apply: fields present in the applied
   configuration replace the live ones; labels/annotations are merged; ownerReferences are
   unioned by uid.  This matches real SSA for a controller that is the sole manager of the
-  fields it applies (which is how native mode uses it).
+  fields it applies (which is how native mode uses it).  The fake apiserver's storage also removes a
+  top-level field its applier set before and omits now (`ClusterState.patch`), as real SSA does.
 """
 from __future__ import annotations
 

@@ -33,6 +33,8 @@ from ..api import selectors
 from ..api.jsonenc import dumps_bytes
 from ..api.objects import deep_copy, now_rfc3339
 from ..api.patch import apply_patch, json_patch, merge_patch, strategic_merge_patch
+
+_APPLY_ALWAYS = frozenset(("apiVersion", "kind", "metadata"))  # never removed by an apply that omits them
 from ..api.resources import ResourceType
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
@@ -162,6 +164,10 @@ class ClusterState:
         self.crds: dict = {}  # (group, plural) -> CRD: writes of those kinds are schema-validated (422)
         self.admission = Admission()  # server-side mutation of write bodies (defaulting/pruning, webhooks)
         self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
+        # server-side apply: the top-level fields each object's applier set last time (by uid).  A field it
+        # applied before and omits now is removed, as a real apiserver does from managedFields — without
+        # this a dropped ConfigMap.binaryData would stay on the object for ever
+        self._applied: dict[str, frozenset] = {}
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
 
@@ -404,11 +410,18 @@ class ClusterState:
         ns = ns if rt.namespaced else ""
         cur = self._bucket(rt, ns).get(name)
         if patch_type == PATCH_APPLY:
+            fields = frozenset(k for k in body if k not in _APPLY_ALWAYS)
             if cur is None:
                 body = dict(body)
                 body.setdefault("metadata", {}).setdefault("name", name)
-                return self.create(rt, ns, body)
+                out = self.create(rt, ns, body)
+                self._applied[out["metadata"].get("uid", "")] = fields
+                return out
             new = apply_patch(cur, body)
+            uid = cur["metadata"].get("uid", "")
+            for k in self._applied.get(uid, frozenset()) - fields:
+                new.pop(k, None)
+            self._applied[uid] = fields
         else:
             if cur is None:
                 raise _not_found(rt, name)
@@ -445,6 +458,8 @@ class ClusterState:
                 raise _conflict(rt, name)
         del b[name]
         self.stats["delete"] += 1
+        if self._applied:
+            self._applied.pop(cm.get("uid", ""), None)
         if self.simple:
             self._emit(self.rv, rt, ns, "DELETED", cur)
             return cur

@@ -247,8 +247,11 @@ async def test_secret_type_change_recreates_shard_copy(tmp_path, impl):
         assert live["data"] == cl.cstate.get(R.SECRETS, NS, "s0")["data"]
 
 
-async def test_configmap_binary_data_synced(tmp_path, impl):
-    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+@pytest.mark.parametrize("ssa", [False, True], ids=["put", "apply"])
+async def test_configmap_binary_data_synced(tmp_path, impl, ssa):
+    """binaryData follows the source, including its removal (with server-side apply the server drops a field
+    its applier stopped applying; the shard copy must not keep it, or drift repair would re-apply for ever)."""
+    async with Cluster(tmp_path, impl, n_shards=1, server_side_apply=ssa) as cl:
         cm = make_configmap("c0", NS)
         cm["binaryData"] = {"blob": "AAEC"}
         cl.cstate.create(R.CONFIGMAPS, NS, cm)
@@ -261,6 +264,9 @@ async def test_configmap_binary_data_synced(tmp_path, impl):
                                              {"blob": "AwQF"}))
         await mutate(cl.cc, R.CONFIGMAPS, "c0", lambda o: o.pop("binaryData"))
         await wait_for(lambda: asyncio.sleep(0, not cl.sstates[0].get(R.CONFIGMAPS, NS, "c0").get("binaryData")))
+        n = len(cl.writes(0, "configmaps", "c0"))
+        await asyncio.sleep(0.5)
+        assert len(cl.writes(0, "configmaps", "c0")) == n, "the shard copy is rewritten in a loop"
 
 
 async def test_failure_isolation_names_shard_and_reason(tmp_path, impl):

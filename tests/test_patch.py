@@ -80,3 +80,25 @@ def test_apply_patch_single_manager():
     assert out["metadata"]["labels"] == {"keep": "y", "app": "x"} and out["metadata"]["annotations"] == {"a": "1"}
     assert [r["uid"] for r in out["metadata"]["ownerReferences"]] == ["u1", "u2"]
     assert out["data"] == {"k": "bmV3"} and out["type"] == "Opaque" and out["metadata"]["name"] == "s"
+
+
+def test_apply_removes_fields_its_applier_stopped_applying():
+    """The fake apiserver's apply: a top-level field the applier set before and omits now is removed (real
+    SSA does this from managedFields); fields set by a PUT, and re-created objects, start from scratch."""
+    from ncc.api import resources as R
+    from ncc.fakeapi.storage import ClusterState
+    from ncc.kube.client import PATCH_APPLY
+
+    st = ClusterState("shard")
+    body = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "c", "namespace": "ns"},
+            "data": {"a": "1"}, "binaryData": {"b": "AAE="}}
+    st.patch(R.CONFIGMAPS, "ns", "c", body, PATCH_APPLY)
+    slim = {k: v for k, v in body.items() if k != "binaryData"}
+    out = st.patch(R.CONFIGMAPS, "ns", "c", slim, PATCH_APPLY)
+    assert "binaryData" not in out and out["data"] == {"a": "1"}
+    cur = st.get(R.CONFIGMAPS, "ns", "c")
+    cur["binaryData"] = {"x": "AA=="}  # set by an update, not by the applier: an apply leaves it alone
+    st.update(R.CONFIGMAPS, "ns", cur)
+    assert st.patch(R.CONFIGMAPS, "ns", "c", slim, PATCH_APPLY)["binaryData"] == {"x": "AA=="}
+    st.delete(R.CONFIGMAPS, "ns", "c")
+    assert st._applied == {}
