@@ -759,8 +759,7 @@ public:
     // Write out everything queued (bounded wait) — used before exiting.
     Task<void> drain(double timeout) {
         flush();
-        double end = now_s() + timeout;
-        while (!out_.empty() && !closed_ && now_s() < end) co_await loop().sleep(0.005);
+        if (!out_.empty() && !closed_) co_await drained_.wait_for(timeout);
     }
 
 private:
@@ -773,6 +772,7 @@ private:
     size_t pos_ = 0;
     std::string out_;
     Event has_out_;
+    Event drained_;  // set while nothing is waiting to be written (or the channel is closed)
 
     void flush() {
         flush_scheduled_ = false;
@@ -794,6 +794,7 @@ private:
                        static_cast<char>(n)};
         out_.append(hdr, 4);
         out_ += body;
+        drained_.clear();
         has_out_.set();
     }
 
@@ -804,6 +805,7 @@ private:
                 out_.clear();
                 off = 0;
                 has_out_.clear();
+                drained_.set();
                 co_await has_out_.wait();
                 continue;
             }
@@ -823,6 +825,7 @@ private:
             if (r < 0 && errno == EINTR) continue;
             closed_ = true;
             out_.clear();
+            drained_.set();
             co_return;
         }
     }

@@ -496,7 +496,6 @@ public:
                     : creds_.tls_server_name;
         token_ = creds_.token;
         reload_token(true);
-        spawn(sweep(), "request-deadline sweep");
     }
     ~Client() {
         closed_ = true;
@@ -548,7 +547,7 @@ public:
             Conn* c;
             ~Guard() { cl->busy_.erase(c); }
         } guard{this, conn.get()};
-        busy_.insert(conn.get());
+        track(conn.get());
         co_await conn->write_all(render("GET", target, nullptr, nullptr));
         Head h = co_await read_head(*conn);
         if (h.status >= 300) {
@@ -599,6 +598,7 @@ private:
     double timeout_;
     int open_ = 0;
     bool closed_ = false;
+    bool sweeping_ = false;  // a sweep() is running
     std::string token_;
     double token_read_at_ = -1e9;
     std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
@@ -714,7 +714,7 @@ private:
             bool reused = c->reused;
             size_t before = 0;
             c->deadline = now_s() + timeout_;
-            busy_.insert(c.get());
+            track(c.get());
             Response r;
             bool ok = false, keep = false;
             std::string err;
@@ -744,13 +744,24 @@ private:
         }
     }
 
+    // A connection in use (request or watch stream) is under the deadline sweep, which runs only while
+    // there is one: an executor whose shard is unreachable or idle is not woken twice a second for nothing.
+    void track(Conn* c) {
+        busy_.insert(c);
+        if (!sweeping_) {
+            sweeping_ = true;
+            spawn(sweep(), "request-deadline sweep");
+        }
+    }
+
     Task<void> sweep() {
-        while (!closed_) {
+        while (!closed_ && !busy_.empty()) {
             co_await loop().sleep(0.5);
             double now = now_s();
             for (Conn* c : busy_)
                 if (c->deadline > 0 && now >= c->deadline) c->abort();
         }
+        sweeping_ = false;
     }
 };
 
