@@ -84,14 +84,15 @@ def _converged(cl, active=None) -> str:
     return ""
 
 
-@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload"])
+@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload", "native-ssa"])
 @pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
 async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatch):
     """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
-    the kills then also hit the child coordinator."""
+    the kills then also hit the child coordinator.  `native-ssa`: shard writes by server-side apply."""
     from ncc.controller.native_executor import binary_path
     reload = topology.endswith("-reload")
-    impl, _, parts = topology.replace("-reload", "").partition("-c")
+    ssa = topology.endswith("-ssa")
+    impl, _, parts = topology.replace("-reload", "").replace("-ssa", "").partition("-c")
     if impl == "native" and binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
@@ -99,6 +100,8 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
     extra = {"coordinator_partitions": int(parts)} if parts else {}
     if reload:  # a third shard whose kubeconfig comes and goes (hot reload of the shards directory)
         extra["shard_reload_period"] = 0
+    if ssa:
+        extra["server_side_apply"] = True
     async with Cluster(tmp_path, impl, n_shards=3 if reload else 2, **extra) as cl:
         active = set(range(len(cl.sstates)))
         if reload:
