@@ -125,6 +125,7 @@ struct Options {
     bool orphan_sweep = true;
     bool propagate_workgroup_deletes = true;
     bool server_side_apply = false;  // shard writes as one apply PATCH (create-or-update) instead of POST/PUT
+    bool sync_dependent_metadata = false;  // shard Secrets/ConfigMaps carry the source's labels/annotations
     int log_level = 30;  // Python logging levels
     bool gated = false;
 };
@@ -312,6 +313,7 @@ static bool raw_null(std::string_view raw) { return raw.empty() || raw == "null"
 // copy gets (templates/workgroups: spec; Secrets/ConfigMaps: data, binaryData) is kept as its raw JSON.
 struct CtlObj {
     std::string spec_raw, data_raw, bin_raw;
+    std::string labels_raw, ann_raw;  // dependents with sync_dependent_metadata: metadata.labels/annotations
     std::string ns, name, uid, rv;
     long long generation = 0;
     bool has_generation = false;
@@ -340,6 +342,10 @@ static CtlPtr make_ctl(int kind, const Value& obj, const std::string_view* raw) 
         }
         c->fp_labels = fp_opt(m->get("labels"));
         c->fp_ann = fp_opt(m->get("annotations"));
+        if (kind >= 2 && g_opt.sync_dependent_metadata) {
+            if (const Value* l = m->get("labels")) c->labels_raw = dumps(*l);
+            if (const Value* a = m->get("annotations")) c->ann_raw = dumps(*a);
+        }
     }
     if (c->ns.empty()) c->ns = g_opt.ns;
     if (kind < 2) {
@@ -389,10 +395,12 @@ static CtlPtr ctl_scan(int kind, std::string_view line, std::string& type) {
         }
         if (mk == "labels") {
             c->fp_labels = fp_opt_text(mv);
+            if (kind >= 2 && g_opt.sync_dependent_metadata) c->labels_raw.assign(mv);
             return true;
         }
         if (mk == "annotations") {
             c->fp_ann = fp_opt_text(mv);
+            if (kind >= 2 && g_opt.sync_dependent_metadata) c->ann_raw.assign(mv);
             return true;
         }
         if (mk == "ownerReferences" && kind >= 2) {
@@ -1259,7 +1267,8 @@ static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool de
     }
     if (old->rv == cur->rv) return;
     if (old->fp_data == cur->fp_data && old->fp_bin == cur->fp_bin && old->type == cur->type &&
-        old->owners == cur->owners)
+        old->owners == cur->owners &&
+        (!g_opt.sync_dependent_metadata || (old->fp_labels == cur->fp_labels && old->fp_ann == cur->fp_ann)))
         return;  // e.g. the coordinator's adoption write: ownerRef UIDs changed, payload did not
     on_dependent(kind, *cur);
 }
@@ -1280,6 +1289,98 @@ static bool data_in_sync(const Shard& sh, int kind, const ShardObj& so, const Ct
            (!with_bin || it->second.fp_b == src.fp_bin);
 }
 
+// sync_dependent_metadata (Shard.dependent_metadata): the labels and annotations a shard copy of `src`
+// carries — the source's labels under the owner labels (they mark the copy as ours), its annotations without
+// kubectl's last-applied record, and kSyncedMetadata naming the source's keys.  A copy is in sync when it
+// carries all of them (keys others added on the shard are left alone); a key removed at the source changes
+// kSyncedMetadata, and the next write drops the keys it named before and the source no longer has.
+constexpr const char* kLastApplied = "kubectl.kubernetes.io/last-applied-configuration";
+constexpr const char* kSyncedMetadata = "science.sneaksanddata.com/synced-metadata";
+static Value owner_labels();
+static std::pair<Value, Value> desired_metadata(const CtlObj& src) {
+    Value labels = Value::object(), ann = Value::object();
+    if (!raw_null(src.labels_raw)) {
+        Value l = parse(src.labels_raw);
+        if (l.is_obj()) labels = std::move(l);
+    }
+    std::vector<std::string> lkeys, akeys;
+    Value owner = owner_labels();
+    for (const auto& kv : labels.o)
+        if (owner.get(kv.first) == nullptr) lkeys.push_back(kv.first);
+    for (auto& kv : owner.o) labels.set(kv.first, std::move(kv.second));
+    if (!raw_null(src.ann_raw)) {
+        Value a = parse(src.ann_raw);
+        if (a.is_obj()) {
+            a.erase(kLastApplied);
+            a.erase(kSyncedMetadata);
+            ann = std::move(a);
+        }
+    }
+    for (const auto& kv : ann.o) akeys.push_back(kv.first);
+    std::sort(lkeys.begin(), lkeys.end());
+    std::sort(akeys.begin(), akeys.end());
+    std::string v = "labels=";
+    for (size_t i = 0; i < lkeys.size(); ++i) v += (i ? "," : "") + lkeys[i];
+    v += ";annotations=";
+    for (size_t i = 0; i < akeys.size(); ++i) v += (i ? "," : "") + akeys[i];
+    ann.set(kSyncedMetadata, Value::str(v));
+    return {std::move(labels), std::move(ann)};
+}
+static bool carries(const Value* have, const Value& want) {
+    for (const auto& kv : want.o) {
+        const Value* h = have != nullptr && have->is_obj() ? have->get(kv.first) : nullptr;
+        if (h == nullptr || fingerprint(*h) != fingerprint(kv.second)) return false;
+    }
+    return true;
+}
+static bool meta_in_sync(const ShardObj& so, const CtlObj& src) {
+    auto [labels, ann] = desired_metadata(src);
+    Value rest = parse(so.rest);
+    const Value* m = meta_of(rest);
+    return m != nullptr && carries(m->get("labels"), labels) && carries(m->get("annotations"), ann);
+}
+// the keys a kSyncedMetadata value names for `what` ("labels" / "annotations")
+static std::vector<std::string> synced_keys(const Value* ann, std::string_view what) {
+    std::vector<std::string> out;
+    const Value* v = ann != nullptr && ann->is_obj() ? ann->get(kSyncedMetadata) : nullptr;
+    if (v == nullptr || !v->is_str()) return out;
+    std::string_view s = v->s;
+    while (!s.empty()) {
+        size_t semi = s.find(';');
+        std::string_view part = s.substr(0, semi);
+        size_t eq = part.find('=');
+        if (eq != std::string_view::npos && part.substr(0, eq) == what) {
+            std::string_view keys = part.substr(eq + 1);
+            while (!keys.empty()) {
+                size_t comma = keys.find(',');
+                if (comma) out.emplace_back(keys.substr(0, comma));
+                if (comma == std::string_view::npos) break;
+                keys.remove_prefix(comma + 1);
+            }
+        }
+        if (semi == std::string_view::npos) break;
+        s.remove_prefix(semi + 1);
+    }
+    return out;
+}
+// metadata `m` of a copy about to be written: keys synced before and gone at the source dropped, the
+// desired ones set, the rest kept (merge_synced_metadata)
+static void set_metadata(Value& m, const CtlObj& src) {
+    auto [labels, ann] = desired_metadata(src);
+    const Value* have_ann = m.get("annotations");
+    std::vector<std::string> prev_l = synced_keys(have_ann, "labels"), prev_a = synced_keys(have_ann, "annotations");
+    auto merge = [&](const char* k, Value& want, const std::vector<std::string>& prev) {
+        Value out = Value::object();
+        if (const Value* have = m.get(k); have != nullptr && have->is_obj())
+            for (const auto& kv : have->o)
+                if (std::find(prev.begin(), prev.end(), kv.first) == prev.end()) out.set(kv.first, kv.second);
+        for (auto& kv : want.o) out.set(kv.first, std::move(kv.second));
+        m.set(k, std::move(out));
+    };
+    merge("labels", labels, prev_l);
+    merge("annotations", ann, prev_a);
+}
+
 static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const ShardPtr& cur, bool deleted) {
     Executor& ex = *g_ex;
     if (!deleted && !old) return;  // adds are not drift (the reference only repairs on update/delete)
@@ -1295,7 +1396,8 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     }
     CtlPtr src = ex.cget(kind, key_of(o.ns, o.name));
     if (!src) return;
-    if (!deleted && data_in_sync(sh, kind, o, *src)) return;
+    if (!deleted && data_in_sync(sh, kind, o, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(o, *src)))
+        return;
     std::vector<std::string> owners;
     for (const auto& p : o.template_owners) owners.push_back(p.first);
     if (owners.empty()) owners = src->owners;
@@ -1692,6 +1794,7 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         m.set("name", Value::str(dep));
         m.set("namespace", Value::str(shard_ns));
         m.set("labels", owner_labels());
+        if (g_opt.sync_dependent_metadata) set_metadata(m, *src);
         Value refs = Value::array();
         refs.a.push_back(owner_ref(st->name, st->uid));
         m.set("ownerReferences", std::move(refs));
@@ -1732,7 +1835,8 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
                 pass->wrote = true;
                 co_await shard_delete(sh, kind, shard_ns, dep);
                 sh.inf[kind].store.erase(key_of(shard_ns, dep));
-            } else if (ours && data_in_sync(sh, kind, *so, *src)) {
+            } else if (ours && data_in_sync(sh, kind, *so, *src) &&
+                       (!g_opt.sync_dependent_metadata || meta_in_sync(*so, *src))) {
                 co_return;
             }
         }
@@ -1758,7 +1862,8 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         co_return;
     }
     bool differs = !data_in_sync(sh, kind, *so, *src);
-    if (!differs && !missing_owner) co_return;
+    bool meta_differs = g_opt.sync_dependent_metadata && !meta_in_sync(*so, *src);
+    if (!differs && !missing_owner && !meta_differs) co_return;
     for (int attempt = 0; attempt < 2; ++attempt) {
         std::string_view data = raw_null(src->data_raw) ? std::string_view("{}") : std::string_view(src->data_raw);
         // binaryData: the source's when it has any; otherwise the member is dropped ("" = drop; without
@@ -1767,14 +1872,17 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         bool touch_bin = with_bin;
         if (with_bin && !raw_is_empty(src->bin_raw)) bin = src->bin_raw;
         std::string body;
-        if (missing_owner) {
+        if (missing_owner || meta_differs) {
             PhaseTimer pt(PH_BODY);
             Value copy = parse(so->rest);
             Value* m = copy.get("metadata");
             if (m == nullptr) m = &copy.set("metadata", Value::object());
-            Value* refs = m->get("ownerReferences");
-            if (refs == nullptr || !refs->is_arr()) refs = &m->set("ownerReferences", Value::array());
-            refs->a.push_back(owner_ref(st->name, st->uid));
+            if (missing_owner) {
+                Value* refs = m->get("ownerReferences");
+                if (refs == nullptr || !refs->is_arr()) refs = &m->set("ownerReferences", Value::array());
+                refs->a.push_back(owner_ref(st->name, st->uid));
+            }
+            if (meta_differs) set_metadata(*m, *src);
             body = touch_bin ? dumps_with(copy, {{"data", data}, {"binaryData", bin}}) : dumps_with(copy, {{"data", data}});
         } else {
             PhaseTimer pt(PH_BODY);
@@ -1795,7 +1903,8 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
             for (const auto& o : so->template_owners)
                 if (o.second == st->uid) missing_owner = false;
             if (!so->has_owner_refs) throw NamedError("RogueResourceError", "Resource \"" + dep + "\" lost its owners");
-            if (data_in_sync(sh, kind, *so, *src) && !missing_owner) co_return;
+            meta_differs = g_opt.sync_dependent_metadata && !meta_in_sync(*so, *src);
+            if (data_in_sync(sh, kind, *so, *src) && !missing_owner && !meta_differs) co_return;
         }
     }
 }
@@ -2071,6 +2180,7 @@ static void configure(const Value& c) {
     o.orphan_sweep = num(c, "orphan_sweep", 1) != 0;
     o.propagate_workgroup_deletes = num(c, "propagate_workgroup_deletes", 1) != 0;
     o.server_side_apply = num(c, "server_side_apply", 0) != 0;
+    o.sync_dependent_metadata = num(c, "sync_dependent_metadata", 0) != 0;
     o.log_level = static_cast<int>(num(c, "log_level", o.log_level));
     if (o.full_resync <= 0) o.full_resync = 1e9;
     Executor& ex = *g_ex;

@@ -103,3 +103,32 @@ def owner_labels(alias: str) -> dict:
         LABEL_CONTROLLER_APP: CONTROLLER_AGENT_NAME,
         LABEL_CONFIGURATION_OWNER: alias,
     }
+
+
+# kubectl's client-side-apply record: never copied to shard dependents (`sync-dependent-metadata`)
+LAST_APPLIED_ANNOTATION = "kubectl.kubernetes.io/last-applied-configuration"
+# on a shard dependent with `sync-dependent-metadata`: which of its label/annotation keys came from the source,
+# so a key removed at the source is removed from the copy, and keys others add to the copy are left alone
+SYNCED_METADATA_ANNOTATION = "science.sneaksanddata.com/synced-metadata"
+
+
+def synced_metadata_value(labels, annotations) -> str:
+    return f"labels={','.join(sorted(labels))};annotations={','.join(sorted(annotations))}"
+
+
+def parse_synced_metadata(value) -> tuple[set, set]:
+    """(label keys, annotation keys) named by a SYNCED_METADATA_ANNOTATION value (empty sets if absent)."""
+    out = {"labels": set(), "annotations": set()}
+    for part in (value or "").split(";"):
+        k, _, v = part.partition("=")
+        if k in out and v:
+            out[k] = set(v.split(","))
+    return out["labels"], out["annotations"]
+
+
+def merge_synced_metadata(have: dict, want: dict, previous: set) -> dict:
+    """A copy's labels/annotations after a sync: keys we synced before and the source no longer has are
+    dropped, the desired ones set, everything else (added on the shard by others) kept."""
+    out = {k: v for k, v in (have or {}).items() if k not in previous}
+    out.update(want)
+    return out

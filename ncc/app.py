@@ -55,6 +55,7 @@ def options_from_config(cfg: AppConfig) -> ControllerOptions:
         kw["workers"] = max(cfg.workers, cfg.native_workers)
         kw.update(full_resync_period=cfg.full_resync_period, wait_for_shards_timeout=cfg.shard_sync_timeout,
                   server_side_apply=cfg.server_side_apply, controller_adoption=cfg.controller_adoption,
+                  sync_dependent_metadata=cfg.sync_dependent_metadata,
                   coalesce_window=cfg.coalesce_window)
     opts = ControllerOptions.for_mode(cfg.mode, **kw)
     # expert/ablation overrides: NCC_OPT_<FIELD>=value (e.g. NCC_OPT_COALESCE_WINDOW=0)
@@ -321,6 +322,7 @@ class App:
                                       client_factory=self.client_factory,
                                       resync_period=0.0 if o.watch_shards else o.resync_period,
                                       assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
+                                      sync_metadata=o.sync_dependent_metadata,
                                       slim=o.slim_shard_cache, start=False, names=self.shard_filter,
                                       key_filter=kf,
                                       owner_filter=partition_owner_filter(*o.partition) if o.partition else None)
@@ -377,6 +379,7 @@ class App:
                                      client_factory=self.client_factory,
                                      resync_period=0.0 if o.watch_shards else o.resync_period,
                                      assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
+                                     sync_metadata=o.sync_dependent_metadata,
                                      slim=o.slim_shard_cache, start=False, names=set(added + changed)):
                 ctl.add_shard(shard)
             self.shards = list(ctl.shards)

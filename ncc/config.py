@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `event-repeat-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `sync-dependent-metadata`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `event-repeat-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -84,6 +84,8 @@ class AppConfig:
     client_pipeline_depth: int = 1   # >1: HTTP/1.1-pipeline requests once all pool connections are busy
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
+    sync_dependent_metadata: bool = False  # native mode: shard Secrets/ConfigMaps carry the source's labels
+                                           # and annotations (plus the owner labels)
     controller_adoption: bool = True  # add template ownerRefs to controller-side Secrets/ConfigMaps (reference)
     executors: int = -1              # shard-executor processes; -1 = auto (native: one per shard, ≤ max)
     max_executors: int = 16

@@ -213,7 +213,9 @@ class Controller(ReconcileMixin):
             return
         if self.options.dependent_data_filter and old.get("data") == new.get("data") \
                 and old.get("binaryData") == new.get("binaryData") and old.get("type") == new.get("type") \
-                and template_owner_names(old) == template_owner_names(new):
+                and template_owner_names(old) == template_owner_names(new) \
+                and (not self.options.sync_dependent_metadata or
+                     (om.get("labels"), om.get("annotations")) == (nm.get("labels"), nm.get("annotations"))):
             return  # e.g. our own adoption PUT: ownerRef UIDs changed, payload did not
         if self.options.role == "coordinator" and om.get("ownerReferences") == nm.get("ownerReferences"):
             return  # payload changes are the executors' business; the coordinator only adopts and reports
@@ -340,6 +342,8 @@ class Controller(ReconcileMixin):
             if deleted or not spec_matches(ctl.get("spec"), obj):
                 self._enqueue_key(make_key(C.KIND_WORKGROUP, ns, name))
 
+        sync_meta = self.options.sync_dependent_metadata
+
         def dependent_changed(lister, with_binary):
             def h(old, new=None):
                 obj = self._unwrap(new if new is not None else old)
@@ -348,7 +352,8 @@ class Controller(ReconcileMixin):
                 src = lister.try_get(ns, name)
                 if src is None:
                     return
-                if not deleted and data_matches(src, obj, with_binary):
+                if not deleted and data_matches(src, obj, with_binary) and \
+                        (not sync_meta or shard.dependent_metadata_matches(src, obj)):
                     return
                 for owner in template_owner_names(obj) or template_owner_names(src):
                     if self.template_lister.try_get(ns, owner) is not None:

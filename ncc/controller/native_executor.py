@@ -128,6 +128,7 @@ class NativeExecutorConfig:
             "full_resync_period": o.full_resync_period, "sync_binary_data": o.sync_binary_data,
             "sync_secret_type": o.sync_secret_type, "orphan_sweep": o.orphan_sweep,
             "propagate_workgroup_deletes": o.propagate_workgroup_deletes, "server_side_apply": o.server_side_apply,
+            "sync_dependent_metadata": o.sync_dependent_metadata,
             "log_level": _LEVELS.get(str(cfg.log_level).upper(), 30), "shards": shards,
         }
         return json.dumps(doc)

@@ -43,6 +43,8 @@ class ControllerOptions:
     server_side_apply: bool = False       # shard writes as SSA (PATCH apply-patch, force) instead of GET/PUT
     patch_writes: bool = False            # controller.go:434,476,663,686 PUT status/ownerRefs (409-prone)
     sync_secret_type: bool = False         # controller.go:539 ignores Secret.type (immutable: needs re-create)
+    sync_dependent_metadata: bool = False  # controller.go:539,600 copy neither labels nor annotations of
+                                           # dependents (opt-in in native mode too: GitOps tracking labels)
     rogue_event_on_template: bool = False  # controller.go:497 records the event on the *shard* object
     controller_adoption: bool = True       # controller.go:647-695 adds ownerRefs to controller-side dependents,
                                            # which makes them GC-deletable with their last template

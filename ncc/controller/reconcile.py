@@ -604,6 +604,8 @@ class ReconcileMixin:
         args = (obj, data, owner, C.FIELD_MANAGER)
         if with_binary:
             args = args + (normalize_data(src.get("binaryData")),)
+        if self.options.sync_dependent_metadata and data is not None:
+            args = args + ((None,) if not is_secret and not with_binary else ()) + (shard.dependent_metadata(src),)
         if self.options.tolerate_write_races:
             informer = shard.secret_informer if is_secret else shard.configmap_informer
             return await self._write(shard, "update_secret" if is_secret else "update_configmap", informer, rt,
@@ -641,7 +643,8 @@ class ReconcileMixin:
                         # Secret.type is immutable, so an apply cannot change it: replace the copy
                         self._pass_wrote()
                         await self._delete_one(shard, lambda o: shard.delete_dependent(R.SECRETS, o), shard_obj)
-                    elif not missing_owner and data_matches(src, shard_obj, with_binary):
+                    elif not missing_owner and data_matches(src, shard_obj, with_binary) and \
+                            (not opts.sync_dependent_metadata or shard.dependent_metadata_matches(src, shard_obj)):
                         return
                 self._pass_wrote()
                 await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)
@@ -671,6 +674,8 @@ class ReconcileMixin:
                 raise self._dependent_failed(template, kind, dep_name, e)
             return
         differs = not data_matches(src, shard_obj, with_binary)
+        if opts.sync_dependent_metadata and not differs and not shard.dependent_metadata_matches(src, shard_obj):
+            differs = True  # labels/annotations only: one PUT carries them (with the unchanged data)
         try:
             slim = SLIM_FP in shard_obj
             if opts.single_put_dependents or slim:

@@ -164,10 +164,10 @@ class ClusterState:
         self.crds: dict = {}  # (group, plural) -> CRD: writes of those kinds are schema-validated (422)
         self.admission = Admission()  # server-side mutation of write bodies (defaulting/pruning, webhooks)
         self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
-        # server-side apply: the top-level fields each object's applier set last time (by uid).  A field it
-        # applied before and omits now is removed, as a real apiserver does from managedFields — without
-        # this a dropped ConfigMap.binaryData would stay on the object for ever
-        self._applied: dict[str, frozenset] = {}
+        # server-side apply: the top-level fields, labels and annotations each object's applier set last time
+        # (by uid).  One it applied before and omits now is removed, as a real apiserver does from
+        # managedFields — without this a dropped ConfigMap.binaryData would stay on the object for ever
+        self._applied: dict[str, tuple] = {}
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
 
@@ -410,7 +410,9 @@ class ClusterState:
         ns = ns if rt.namespaced else ""
         cur = self._bucket(rt, ns).get(name)
         if patch_type == PATCH_APPLY:
-            fields = frozenset(k for k in body if k not in _APPLY_ALWAYS)
+            bm = body.get("metadata") or {}
+            fields = (frozenset(k for k in body if k not in _APPLY_ALWAYS), frozenset(bm.get("labels") or ()),
+                      frozenset(bm.get("annotations") or ()))
             if cur is None:
                 body = dict(body)
                 body.setdefault("metadata", {}).setdefault("name", name)
@@ -419,8 +421,19 @@ class ClusterState:
                 return out
             new = apply_patch(cur, body)
             uid = cur["metadata"].get("uid", "")
-            for k in self._applied.get(uid, frozenset()) - fields:
-                new.pop(k, None)
+            prev = self._applied.get(uid)
+            if prev is not None:
+                for k in prev[0] - fields[0]:
+                    new.pop(k, None)
+                for i, mk in ((1, "labels"), (2, "annotations")):
+                    gone = prev[i] - fields[i]
+                    if gone and new["metadata"].get(mk):
+                        kept = {k: v for k, v in new["metadata"][mk].items() if k not in gone}
+                        new["metadata"] = dict(new["metadata"])
+                        if kept:
+                            new["metadata"][mk] = kept
+                        else:
+                            new["metadata"].pop(mk, None)
             self._applied[uid] = fields
         else:
             if cur is None:

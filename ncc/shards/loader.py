@@ -51,7 +51,8 @@ def default_client_factory(qps: float = 0.0, burst: int = 10, pool_size: int = 6
 
 def load_shards(alias: str, shard_config_path: str, namespace: str, *,
                 client_factory: Callable[[str, str], KubeClient] | None = None, resync_period: float = 0.0,
-                assume_writes: bool = False, sync_binary_data: bool = False, slim: bool = False,
+                assume_writes: bool = False, sync_binary_data: bool = False, sync_metadata: bool = False,
+                slim: bool = False,
                 start: bool = True, names: set | None = None, key_filter=None, owner_filter=None) -> list[Shard]:
     from ..controller.reconcile import slim_data, slim_spec
     make = client_factory or default_client_factory()
@@ -63,7 +64,7 @@ def load_shards(alias: str, shard_config_path: str, namespace: str, *,
             continue
         client = make(name, path)
         shard = Shard(alias, name, client, namespace, resync_period=resync_period, assume_writes=assume_writes,
-                      sync_binary_data=sync_binary_data, transforms=transforms,
+                      sync_binary_data=sync_binary_data, sync_metadata=sync_metadata, transforms=transforms,
                       key_filters={R.TEMPLATES: key_filter, R.WORKGROUPS: key_filter} if key_filter else None,
                       owner_filters={R.SECRETS: owner_filter, R.CONFIGMAPS: owner_filter} if owner_filter else None)
         if start:

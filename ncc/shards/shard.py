@@ -36,7 +36,7 @@ from ..kube.client import PATCH_APPLY, KubeClient
 class Shard:
     def __init__(self, owner_alias: str, name: str, client: KubeClient, namespace: str, *,
                  resync_period: float = 0.0, assume_writes: bool = False, sync_binary_data: bool = False,
-                 transforms: dict | None = None, informer_kw: dict | None = None, key_filters: dict | None = None,
+                 sync_metadata: bool = False, transforms: dict | None = None, informer_kw: dict | None = None, key_filters: dict | None = None,
                  owner_filters: dict | None = None):
         self.owner_alias = owner_alias
         self.name = name
@@ -44,6 +44,7 @@ class Shard:
         self.namespace = namespace
         self.assume_writes = assume_writes
         self.sync_binary_data = sync_binary_data
+        self.sync_metadata = sync_metadata  # dependents carry the source's labels/annotations too
         self.labels = C.owner_labels(owner_alias)
         transforms = transforms or {}
         kfs = key_filters or {}
@@ -220,6 +221,29 @@ class Shard:
         await self._answer_tracking(self.client.delete(R.WORKGROUPS, m.get("namespace", ""), m.get("name", "")))
 
     # ---------------------------------------------------------------- dependents
+    def dependent_metadata(self, src: dict) -> tuple[dict, dict]:
+        """(labels, annotations) a shard copy of `src` carries with `sync_metadata`: the source's labels under
+        the owner labels (which mark the copy as ours), its annotations without kubectl's last-applied
+        configuration, and SYNCED_METADATA_ANNOTATION naming the source's keys."""
+        m = meta(src)
+        src_labels = m.get("labels") or {}
+        labels = dict(src_labels)
+        labels.update(self.labels)
+        ann = {k: v for k, v in (m.get("annotations") or {}).items()
+               if k not in (C.LAST_APPLIED_ANNOTATION, C.SYNCED_METADATA_ANNOTATION)}
+        ann[C.SYNCED_METADATA_ANNOTATION] = C.synced_metadata_value(
+            (k for k in src_labels if k not in self.labels), ann)
+        return labels, ann
+
+    def dependent_metadata_matches(self, src: dict, shard_obj: dict) -> bool:
+        """The copy carries every label/annotation the source gives it (keys others added are left alone;
+        a key removed at the source changes SYNCED_METADATA_ANNOTATION)."""
+        labels, ann = self.dependent_metadata(src)
+        sm = meta(shard_obj)
+        have_l, have_a = sm.get("labels") or {}, sm.get("annotations") or {}
+        return all(have_l.get(k) == v for k, v in labels.items()) and \
+            all(have_a.get(k) == v for k, v in ann.items())
+
     def _dependent_body(self, rt: R.ResourceType, shard_template: dict, src: dict) -> dict:
         obj = {
             "apiVersion": "v1",
@@ -231,6 +255,11 @@ class Shard:
                 "ownerReferences": [template_owner_ref(shard_template)],
             },
         }
+        if self.sync_metadata:
+            labels, ann = self.dependent_metadata(src)
+            obj["metadata"]["labels"] = labels
+            if ann:
+                obj["metadata"]["annotations"] = ann
         if src.get("data") is not None:
             obj["data"] = src["data"]
         if rt is R.SECRETS:
@@ -240,8 +269,16 @@ class Shard:
             obj["binaryData"] = src["binaryData"]
         return obj
 
-    def _updated_dependent(self, shard_obj: dict, data, new_owner: dict | None, binary_data=None) -> dict:
+    def _updated_dependent(self, shard_obj: dict, data, new_owner: dict | None, binary_data=None,
+                           metadata: tuple | None = None) -> dict:
         obj = _strip_slim(dict(shard_obj))
+        if metadata is not None:  # (labels, annotations) from dependent_metadata
+            m = dict(meta(obj))
+            have_ann = m.get("annotations") or {}
+            prev_l, prev_a = C.parse_synced_metadata(have_ann.get(C.SYNCED_METADATA_ANNOTATION))
+            m["labels"] = C.merge_synced_metadata(m.get("labels"), metadata[0], prev_l)
+            m["annotations"] = C.merge_synced_metadata(have_ann, metadata[1], prev_a)
+            obj["metadata"] = m
         if data is not None:
             obj["data"] = data
         if binary_data is not None:
@@ -250,7 +287,7 @@ class Shard:
             else:
                 obj.pop("binaryData", None)
         if new_owner is not None:
-            m = dict(meta(shard_obj))
+            m = dict(meta(obj))
             refs = list(m.get("ownerReferences") or [])
             new_ref = template_owner_ref(new_owner)
             if not any(r.get("uid") == new_ref["uid"] and r.get("kind") == new_ref["kind"] for r in refs):
@@ -269,8 +306,8 @@ class Shard:
                                    field_manager)
 
     async def _update_dependent(self, rt: R.ResourceType, shard_obj: dict, data, new_owner, field_manager: str,
-                                binary_data=None):
-        body = self._updated_dependent(shard_obj, data, new_owner, binary_data)
+                                binary_data=None, metadata=None):
+        body = self._updated_dependent(shard_obj, data, new_owner, binary_data, metadata)
         m = meta(shard_obj)
         return await self._tracked(self._dep_informer(rt), rt, "update", m.get("namespace", ""), m.get("name", ""),
                                    body, field_manager)
@@ -278,16 +315,18 @@ class Shard:
     async def create_secret(self, shard_template: dict, secret: dict, field_manager: str) -> dict:
         return await self._create_dependent(R.SECRETS, shard_template, secret, field_manager)
 
-    async def update_secret(self, shard_secret: dict, data, new_owner: dict | None, field_manager: str) -> dict:
-        return await self._update_dependent(R.SECRETS, shard_secret, data, new_owner, field_manager)
+    async def update_secret(self, shard_secret: dict, data, new_owner: dict | None, field_manager: str,
+                            metadata: tuple | None = None) -> dict:
+        return await self._update_dependent(R.SECRETS, shard_secret, data, new_owner, field_manager,
+                                            metadata=metadata)
 
     async def create_configmap(self, shard_template: dict, configmap: dict, field_manager: str) -> dict:
         return await self._create_dependent(R.CONFIGMAPS, shard_template, configmap, field_manager)
 
     async def update_configmap(self, shard_configmap: dict, data, new_owner: dict | None, field_manager: str,
-                               binary_data=None) -> dict:
+                               binary_data=None, metadata: tuple | None = None) -> dict:
         return await self._update_dependent(R.CONFIGMAPS, shard_configmap, data, new_owner, field_manager,
-                                            binary_data)
+                                            binary_data, metadata)
 
     async def apply_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str) -> dict:
         """Apply our view of a dependent: owner labels, our ownerRef (merged by uid with other owners'), payload."""

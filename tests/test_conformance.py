@@ -15,6 +15,7 @@ missing references refused; AlreadyExists/Conflict races resolved by re-reading;
 shard watch that expired (410) relisted.
 """
 import asyncio
+import copy as copy_mod
 import os
 
 import pytest
@@ -565,6 +566,65 @@ async def test_server_side_apply(tmp_path, impl):
         for i in range(2):
             writes = [w for w in cl.env.shard_servers[i].writes if w[0] not in ("GET",)]
             assert writes and {w[0] for w in writes} <= {"PATCH", "DELETE"}, writes
+
+
+@pytest.mark.parametrize("ssa", [False, True], ids=["put", "apply"])
+async def test_dependent_labels_and_annotations_synced(tmp_path, impl, ssa):
+    """`sync-dependent-metadata: true` (the reference copies neither): a shard copy carries
+    the source's labels under the owner labels and its annotations without kubectl's last-applied record.
+    A key removed at the source is removed from the copy; keys added on the shard by others stay."""
+    async with Cluster(tmp_path, impl, n_shards=1, sync_dependent_metadata=True, server_side_apply=ssa) as cl:
+        sec = make_secret("s0", NS)
+        sec["metadata"]["labels"] = {"team": "ml", "tier": "gold"}
+        sec["metadata"]["annotations"] = {"note": "v1", C.LAST_APPLIED_ANNOTATION: '{"big": "blob"}'}
+        cl.cstate.create(R.SECRETS, NS, sec)
+        cl.seed(configmaps=())
+        await cl.start()
+        await cl.ready()
+        copy = copy_mod.deepcopy(cl.sstates[0].get(R.SECRETS, NS, "s0"))
+        assert copy["metadata"]["labels"] == dict({"team": "ml", "tier": "gold"},
+                                                  **C.owner_labels("controller-cluster"))
+        ann = copy["metadata"]["annotations"]
+        assert ann["note"] == "v1" and C.LAST_APPLIED_ANNOTATION not in ann
+        # a label added on the shard by someone else is left alone
+        copy["metadata"]["labels"]["shard-local"] = "x"
+        cl.sstates[0].update(R.SECRETS, NS, copy)
+
+        def change(o):
+            o["metadata"]["labels"] = {"team": "ai"}
+            o["metadata"]["annotations"] = {"reviewed": "yes"}
+        await mutate(cl.cc, R.SECRETS, "s0", change)
+
+        def synced():
+            m = cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]
+            lab, ann = m.get("labels") or {}, m.get("annotations") or {}
+            return lab.get("team") == "ai" and "tier" not in lab and ann.get("reviewed") == "yes" and \
+                "note" not in ann and m
+        m = await wait_for(lambda: asyncio.sleep(0, synced()))
+        assert m["labels"]["shard-local"] == "x"
+        assert m["labels"][C.LABEL_CONFIGURATION_OWNER] == "controller-cluster"
+        # label drift on the shard copy is repaired
+        live = copy_mod.deepcopy(cl.sstates[0].get(R.SECRETS, NS, "s0"))
+        live["metadata"]["labels"]["team"] = "drifted"
+        cl.sstates[0].update(R.SECRETS, NS, live)
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]["labels"]
+                                             .get("team") == "ai"))
+        n = len(cl.writes(0, "secrets", "s0"))
+        await asyncio.sleep(0.5)
+        assert len(cl.writes(0, "secrets", "s0")) == n, "the shard copy is rewritten in a loop"
+
+
+async def test_dependent_metadata_not_synced_by_default(tmp_path, impl):
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        sec = make_secret("s0", NS)
+        sec["metadata"]["labels"] = {"team": "ml"}
+        sec["metadata"]["annotations"] = {"note": "v1"}
+        cl.cstate.create(R.SECRETS, NS, sec)
+        cl.seed(configmaps=())
+        await cl.start()
+        await cl.ready()
+        m = cl.sstates[0].get(R.SECRETS, NS, "s0")["metadata"]
+        assert m["labels"] == C.owner_labels("controller-cluster") and not m.get("annotations")
 
 
 def test_every_implementation_is_exercised():
