@@ -40,7 +40,7 @@ def _deps(t: dict) -> tuple[list, list]:
             [e["configMapRef"]["name"] for e in mev if e.get("configMapRef")])
 
 
-def _converged(cl, active=None) -> str:
+def _converged(cl, active=None, meta_sync: bool = False) -> str:
     """'' when every (active) shard matches the model, else the first difference found."""
     active = sorted(active if active is not None else range(len(cl.sstates)))
     shards = [cl.env.shard_names[i] for i in active]
@@ -67,8 +67,16 @@ def _converged(cl, active=None) -> str:
             live = s.try_get(rt, NS, n)
             if live is None:
                 return f"shard {i}: {plural}/{n} missing"
-            if live.get("data") != cl.cstate.get(rt, NS, n).get("data"):
+            src = cl.cstate.get(rt, NS, n)
+            if live.get("data") != src.get("data"):
                 return f"shard {i}: {plural}/{n} data differs"
+            if meta_sync:  # sync-dependent-metadata: the copy carries the source's labels and annotations
+                for mk in ("labels", "annotations"):
+                    want, have = src["metadata"].get(mk) or {}, dict(live["metadata"].get(mk) or {})
+                    for k in list(C.owner_labels("controller-cluster")) + [C.SYNCED_METADATA_ANNOTATION]:
+                        have.pop(k, None)  # ours, not the source's (nothing else writes the copies here)
+                    if have != want:
+                        return f"shard {i}: {plural}/{n} {mk} {have} != {want}"
             have = {r["uid"] for r in live["metadata"].get("ownerReferences") or ()}
             if not uids <= have:
                 return f"shard {i}: {plural}/{n} owners {sorted(have)} lack {sorted(uids - have)}"
@@ -84,15 +92,18 @@ def _converged(cl, active=None) -> str:
     return ""
 
 
-@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload", "native-ssa"])
+@pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload", "native-ssa",
+                                      "native-meta"])
 @pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
 async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatch):
     """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
-    the kills then also hit the child coordinator.  `native-ssa`: shard writes by server-side apply."""
+    the kills then also hit the child coordinator.  `native-ssa`: shard writes by server-side apply.
+    `native-meta`: sync-dependent-metadata, with source labels/annotations changed along the way."""
     from ncc.controller.native_executor import binary_path
     reload = topology.endswith("-reload")
     ssa = topology.endswith("-ssa")
-    impl, _, parts = topology.replace("-reload", "").replace("-ssa", "").partition("-c")
+    meta_sync = topology.endswith("-meta")
+    impl, _, parts = topology.replace("-reload", "").replace("-ssa", "").replace("-meta", "").partition("-c")
     if impl == "native" and binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
@@ -102,6 +113,8 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         extra["shard_reload_period"] = 0
     if ssa:
         extra["server_side_apply"] = True
+    if meta_sync:
+        extra["sync_dependent_metadata"] = True
     async with Cluster(tmp_path, impl, n_shards=3 if reload else 2, **extra) as cl:
         active = set(range(len(cl.sstates)))
         if reload:
@@ -119,7 +132,8 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         for _step in range(STEPS):
             version += 1
             op = rnd.choices(["spec", "secret", "configmap", "create", "delete", "fault", "kill", "reref",
-                              "recreate", "reshard"], weights=[5, 4, 3, 2, 2, 3, 1, 2, 1, 2 if reload else 0])[0]
+                              "recreate", "reshard", "relabel"],
+                             weights=[5, 4, 3, 2, 2, 3, 1, 2, 1, 2 if reload else 0, 3 if meta_sync else 0])[0]
             ops[op] = ops.get(op, 0) + 1
             if op == "spec" and live:
                 name = rnd.choice(live)
@@ -164,6 +178,20 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
                     await cl.cc.delete(R.CONFIGMAPS, NS, n)
                     await asyncio.sleep(rnd.uniform(0, 0.05))
                     await cl.cc.create(R.CONFIGMAPS, NS, make_configmap(n, NS, version=version))
+            elif op == "relabel":  # a source's labels/annotations change (a key set, changed or removed)
+                rt = rnd.choice([R.SECRETS, R.CONFIGMAPS])
+                names = [o["metadata"]["name"] for o in cl.cstate.list(rt, NS)["items"]]
+                if names:
+                    mk, key = rnd.choice(["labels", "annotations"]), rnd.choice(["team", "tier", "note"])
+
+                    def relabel(o, mk=mk, key=key, v=f"v{version}", drop=rnd.random() < 0.4):
+                        d = o["metadata"].setdefault(mk, {}) or {}
+                        if drop:
+                            d.pop(key, None)
+                        else:
+                            d[key] = v
+                        o["metadata"][mk] = d
+                    await mutate(cl.cc, rt, rnd.choice(names), relabel)
             elif op == "reshard":  # shard-2 joins or leaves
                 if 2 in active:
                     os.replace(kc, parked)
@@ -203,7 +231,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
 
         async def done():
             nonlocal last
-            last = _converged(cl, active)
+            last = _converged(cl, active, meta_sync)
             return last == ""
         try:
             await wait_for(done, timeout=45, interval=0.2)
