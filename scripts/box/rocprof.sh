@@ -8,4 +8,4 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -- python3 bench.py --steps 5 --warmup 2 \
   > "$out/bench.json" 2> "$out/rocprof.err" || exit $?
 python scripts/box/summarize.py "$out/bench.json"
-find "$out/trace" -type f | head -20
+if [ -d "$out/trace" ]; then find "$out/trace" -type f; else echo "no trace files: no kernel dispatches were recorded"; fi
