@@ -614,6 +614,44 @@ async def test_dependent_labels_and_annotations_synced(tmp_path, impl, ssa):
         assert len(cl.writes(0, "secrets", "s0")) == n, "the shard copy is rewritten in a loop"
 
 
+async def test_takeover_of_objects_the_reference_wrote_needs_no_shard_writes(tmp_path, impl):
+    """docs/MIGRATION.md: replacing a running reference deployment.  Shard objects exactly as the reference
+    left them (owner labels, ownerRefs to the shard template, the same spec and data) are adopted from the
+    caches: the templates turn Ready without a single shard write."""
+    from ncc.api.refs import template_owner_ref
+    async with Cluster(tmp_path, impl, n_shards=2) as cl:
+        for i in range(3):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        cl.cstate.create(R.WORKGROUPS, NS, make_workgroup("mi355x", NS))
+        labels = C.owner_labels("controller-cluster")
+        for st in cl.sstates:
+            for t in cl.cstate.list(R.TEMPLATES, NS)["items"]:
+                copy = {"apiVersion": C.API_VERSION, "kind": C.TEMPLATE_KIND,
+                        "metadata": {"name": t["metadata"]["name"], "namespace": NS, "labels": dict(labels)},
+                        "spec": copy_mod.deepcopy(t["spec"])}
+                shard_t = st.create(R.TEMPLATES, NS, copy)
+                n = t["metadata"]["name"][-1]
+                for rt, dep in ((R.SECRETS, f"s{int(n)}"), (R.CONFIGMAPS, f"c{int(n)}")):
+                    src = cl.cstate.get(rt, NS, dep)
+                    obj = {"apiVersion": "v1", "kind": rt.kind, "data": copy_mod.deepcopy(src["data"]),
+                           "metadata": {"name": dep, "namespace": NS, "labels": dict(labels),
+                                        "ownerReferences": [template_owner_ref(shard_t)]}}
+                    if rt is R.SECRETS and src.get("type"):
+                        obj["type"] = src["type"]
+                    st.create(rt, NS, obj)
+            wg = cl.cstate.get(R.WORKGROUPS, NS, "mi355x")
+            st.create(R.WORKGROUPS, NS, {"apiVersion": C.API_VERSION, "kind": C.WORKGROUP_KIND,
+                                         "metadata": {"name": "mi355x", "namespace": NS, "labels": dict(labels)},
+                                         "spec": copy_mod.deepcopy(wg["spec"])})
+        await cl.start()
+        for i in range(3):
+            await cl.ready(f"algo-{i:05d}")
+        await asyncio.sleep(0.3)
+        for i in range(2):
+            writes = [w for w in cl.env.shard_servers[i].writes if w[0] in ("POST", "PUT", "PATCH", "DELETE")]
+            assert writes == [], writes
+
+
 async def test_dependent_metadata_not_synced_by_default(tmp_path, impl):
     async with Cluster(tmp_path, impl, n_shards=1) as cl:
         sec = make_secret("s0", NS)
