@@ -512,6 +512,8 @@ struct ShardObj {
     std::vector<std::pair<std::string, std::string>> template_owners;  // (name, uid) of template owners
     std::vector<std::string> all_owner_names;
     std::string label_app, label_owner;
+    // sync_dependent_metadata: metadata.labels / annotations, parsed from `rest` on first use (meta_in_sync)
+    mutable std::unique_ptr<std::pair<Value, Value>> meta_maps;
 };
 using ShardPtr = std::shared_ptr<const ShardObj>;
 
@@ -1334,10 +1336,17 @@ static bool carries(const Value* have, const Value& want) {
     return true;
 }
 static bool meta_in_sync(const ShardObj& so, const CtlObj& src) {
+    if (!so.meta_maps) {
+        auto maps = std::make_unique<std::pair<Value, Value>>();
+        Value rest = parse(so.rest);
+        if (Value* m = rest.get("metadata")) {
+            if (Value* l = m->get("labels")) maps->first = std::move(*l);
+            if (Value* a = m->get("annotations")) maps->second = std::move(*a);
+        }
+        so.meta_maps = std::move(maps);
+    }
     auto [labels, ann] = desired_metadata(src);
-    Value rest = parse(so.rest);
-    const Value* m = meta_of(rest);
-    return m != nullptr && carries(m->get("labels"), labels) && carries(m->get("annotations"), ann);
+    return carries(&so.meta_maps->first, labels) && carries(&so.meta_maps->second, ann);
 }
 // the keys a kSyncedMetadata value names for `what` ("labels" / "annotations")
 static std::vector<std::string> synced_keys(const Value* ann, std::string_view what) {
