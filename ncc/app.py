@@ -682,6 +682,9 @@ def main(argv=None) -> int:
     p = argparse.ArgumentParser(prog="python -m ncc", description="Nexus multi-cluster configuration controller")
     p.add_argument("--config-dir", default=None, help="directory holding appconfig.yaml (default: cwd)")
     p.add_argument("--version", action="store_true")
+    p.add_argument("--check-shards", action="store_true",
+                   help="preflight: list every kind on the controller cluster and each shard, print one JSON line "
+                        "per cluster and exit (0: all answered)")
     p.add_argument("--control-fd", type=int, default=None, help=argparse.SUPPRESS)  # coordinator partitions
     p.add_argument("-v", "--v", type=int, default=None, metavar="N",
                    help="klog verbosity: N>=4 logs at DEBUG (overrides log-level), N<4 leaves log-level as set")
@@ -703,6 +706,9 @@ def main(argv=None) -> int:
     if args.v is not None and args.v >= 4:
         cfg.log_level = "DEBUG"
     configure_logging(cfg.log_level, cfg.log_format)
+    if args.check_shards:
+        from .preflight import run as preflight
+        return preflight(cfg)
     prof_path = os.environ.get("NCC_PROFILE")
     if prof_path:  # host-side profiling of the control loop: NCC_PROFILE=/path/out.prof
         import cProfile

@@ -1,0 +1,66 @@
+"""`python -m ncc --check-shards`: a preflight for a deployment (docs/MIGRATION.md, step 2).
+
+Loads the controller cluster's kubeconfig and every `<cluster>.kubeconfig` in `shard-config-path` exactly as
+the controller does (credentials, `exec` plugins, CA), then LISTs each kind the controller reads and writes
+in `controller-namespace` on each cluster.  One JSON line per cluster, then a summary line; exit status 0 when
+every cluster answered every list.  A missing CRD shows up as NotFound, missing RBAC as Forbidden, a wrong
+server or CA as TransportError — before the controller starts and waits for caches that never sync.  Write
+permissions are not probed (that would need writes, or SelfSubjectAccessReviews the reference never needed).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+
+from .api import resources as R
+from .kube import errors as E
+from .kube.kubeconfig import build_config, load_kubeconfig
+from .kube.rest import RestClient
+from .shards.loader import discover
+
+KINDS = (R.TEMPLATES, R.WORKGROUPS, R.SECRETS, R.CONFIGMAPS)
+
+
+async def check_cluster(name: str, client, namespace: str, timeout: float = 10.0) -> dict:
+    kinds = {}
+    for rt in KINDS:
+        try:
+            await asyncio.wait_for(client.list(rt, namespace, limit=1), timeout)
+            kinds[rt.plural] = "ok"
+        except asyncio.TimeoutError:
+            kinds[rt.plural] = f"TransportError: no answer within {timeout:g}s"
+        except E.ApiError as e:
+            kinds[rt.plural] = f"{type(e).__name__} ({e.code}): {e.message}"[:300]
+        except Exception as e:  # noqa: BLE001 - transport and TLS failures
+            kinds[rt.plural] = f"{type(e).__name__}: {e}"[:300]
+    return {"cluster": name, "ok": all(v == "ok" for v in kinds.values()), "kinds": kinds}
+
+
+async def check(cfg, timeout: float = 10.0) -> list[dict]:
+    out = []
+    targets = [("controller", lambda: build_config(cfg.controller_config_path))]
+    targets += [(name, (lambda p=path, n=name: load_kubeconfig(p, name=n)))
+                for name, path in discover(cfg.shard_config_path)]
+    for name, make_cfg in targets:
+        try:
+            client = RestClient(make_cfg(), pool_size=2, cluster_name=name)
+        except Exception as e:  # noqa: BLE001 - an unreadable kubeconfig
+            out.append({"cluster": name, "ok": False, "error": f"{type(e).__name__}: {e}"[:300]})
+            continue
+        try:
+            out.append(await check_cluster(name, client, cfg.controller_namespace, timeout))
+        finally:
+            await client.close()
+    return out
+
+
+def run(cfg, print_fn=print) -> int:
+    results = asyncio.run(check(cfg))
+    for r in results:
+        print_fn(json.dumps(r, sort_keys=True))
+    shards = [r for r in results if r["cluster"] != "controller"]
+    ok = all(r["ok"] for r in results) and bool(shards)
+    print_fn(json.dumps({"summary": "ok" if ok else "failed", "clusters": len(results), "shards": len(shards),
+                         "failing": [r["cluster"] for r in results if not r["ok"]]
+                         + ([] if shards else ["(no *.kubeconfig in shard-config-path)"])}))
+    return 0 if ok else 1
