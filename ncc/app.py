@@ -700,8 +700,11 @@ def main(argv=None) -> int:
         return 0
     try:
         cfg = load_config(args.config_dir)
-    except ValueError as e:
+    except (ValueError, OSError) as e:
         print(f"configuration error: {e}", file=sys.stderr)
+        return 1
+    except Exception as e:  # noqa: BLE001 - a malformed appconfig.yaml (yaml.YAMLError)
+        print(f"configuration error: {type(e).__name__}: {e}", file=sys.stderr)
         return 1
     if args.v is not None and args.v >= 4:
         cfg.log_level = "DEBUG"

@@ -40,3 +40,11 @@ def test_check_shards_flag_exit_status(tmp_path, monkeypatch, capsys):
     assert app.main(["--config-dir", str(tmp_path), "-check-shards"]) == 1
     lines = [json.loads(x) for x in capsys.readouterr().out.strip().splitlines()]
     assert lines[-1]["summary"] == "failed" and lines[-1]["shards"] == 0
+
+
+def test_malformed_appconfig_is_a_configuration_error(tmp_path, capsys):
+    from ncc import app
+    (tmp_path / "appconfig.yaml").write_text("alias: a: b\n")
+    assert app.main(["--config-dir", str(tmp_path), "--version"]) == 0  # --version needs no config
+    assert app.main(["--config-dir", str(tmp_path), "--check-shards"]) == 1
+    assert "configuration error" in capsys.readouterr().err
