@@ -23,15 +23,23 @@ KINDS = (R.TEMPLATES, R.WORKGROUPS, R.SECRETS, R.CONFIGMAPS)
 
 async def check_cluster(name: str, client, namespace: str, timeout: float = 10.0) -> dict:
     kinds = {}
+    unreachable = False
     for rt in KINDS:
+        if unreachable:  # one timeout or connection failure is enough: do not wait again per kind
+            kinds[rt.plural] = "skipped (cluster unreachable)"
+            continue
         try:
             await asyncio.wait_for(client.list(rt, namespace, limit=1), timeout)
             kinds[rt.plural] = "ok"
         except asyncio.TimeoutError:
             kinds[rt.plural] = f"TransportError: no answer within {timeout:g}s"
+            unreachable = True
+        except E.TransportError as e:
+            kinds[rt.plural] = f"TransportError: {e}"[:300]
+            unreachable = True
         except E.ApiError as e:
             kinds[rt.plural] = f"{type(e).__name__} ({e.code}): {e.message}"[:300]
-        except Exception as e:  # noqa: BLE001 - transport and TLS failures
+        except Exception as e:  # noqa: BLE001 - TLS and other client-side failures
             kinds[rt.plural] = f"{type(e).__name__}: {e}"[:300]
     return {"cluster": name, "ok": all(v == "ok" for v in kinds.values()), "kinds": kinds}
 

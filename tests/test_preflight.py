@@ -48,3 +48,22 @@ def test_malformed_appconfig_is_a_configuration_error(tmp_path, capsys):
     assert app.main(["--config-dir", str(tmp_path), "--version"]) == 0  # --version needs no config
     assert app.main(["--config-dir", str(tmp_path), "--check-shards"]) == 1
     assert "configuration error" in capsys.readouterr().err
+
+
+async def test_unreachable_cluster_is_reported_once(tmp_path):
+    import socket
+
+    from ncc.preflight import check_cluster
+    from ncc.kube.kubeconfig import ClusterConfig
+    from ncc.kube.rest import RestClient
+    with socket.socket() as s:  # a port nothing listens on
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    client = RestClient(ClusterConfig(server=f"http://127.0.0.1:{port}"), pool_size=1, cluster_name="dead")
+    try:
+        r = await check_cluster("dead", client, "nexus", timeout=2.0)
+    finally:
+        await client.close()
+    assert not r["ok"]
+    first, *rest = r["kinds"].values()
+    assert first.startswith("TransportError") and all(v.startswith("skipped") for v in rest), r
