@@ -113,7 +113,8 @@ struct Options {
     std::string ns = "nexus";
     std::string alias = "controller-cluster";
     int workers = 256;
-    int pool_size = 64;
+    int pool_size = 256;
+    FlowLimits flow;  // client-side flow control per shard (http.hpp): AIMD limit, client-qps bucket
     double request_timeout = 30;
     double coalesce = 0.002;
     double base_delay = 0.03, max_delay = 5.0;
@@ -2176,6 +2177,12 @@ static void configure(const Value& c) {
     o.workers = static_cast<int>(num(c, "workers", o.workers));
     o.pool_size = static_cast<int>(num(c, "pool_size", o.pool_size));
     if (const char* ps = std::getenv("NCC_POOL_SIZE")) o.pool_size = std::max(1, std::atoi(ps));  // experiments
+    o.flow.qps = num(c, "client_qps", 0);
+    o.flow.burst = num(c, "client_burst", 10);
+    o.flow.adaptive = num(c, "adaptive_concurrency", 1) != 0;
+    o.flow.initial = num(c, "initial_concurrency", o.flow.initial);
+    o.flow.latency_s = num(c, "overload_latency", o.flow.latency_s);
+    if (const char* v = std::getenv("NCC_AIMD")) o.flow.adaptive = std::atoi(v) != 0;  // experiments
     o.request_timeout = num(c, "request_timeout", o.request_timeout);
     o.coalesce = num(c, "coalesce_window", o.coalesce);
     o.base_delay = num(c, "failure_base_delay", o.base_delay);
@@ -2198,7 +2205,7 @@ static void configure(const Value& c) {
         for (const auto& s : shards->a) {
             auto sh = std::make_unique<Shard>();
             sh->name = std::string(s.sget("name"));
-            sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout);
+            sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout, o.flow);
             for (int k = 0; k < 4; ++k) {
                 sh->inf[k].shard = sh.get();
                 sh->inf[k].kind = k;
@@ -2333,7 +2340,7 @@ static void send_status() {
     e.map(ex.shards.size());
     for (const auto& sp : ex.shards) {
         e.str(sp->name);
-        e.map(4);
+        e.map(5);
         for (int k = 0; k < 4; ++k) {
             const Informer& inf = sp->inf[k];
             e.str(kPlural[k]);
@@ -2344,6 +2351,18 @@ static void send_status() {
             e.integer(inf.relists);
             e.str(inf.last_error);
         }
+        // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms]
+        const Client& cl = *sp->client;
+        e.str("flow");
+        e.array(8);
+        e.integer(static_cast<long long>(cl.limit()));
+        e.integer(cl.inflight());
+        e.integer(cl.flow.max_inflight);
+        e.integer(cl.flow.rejected);
+        e.integer(cl.flow.overloads);
+        e.integer(cl.flow.cuts);
+        e.integer(cl.flow.gated);
+        e.integer(static_cast<long long>(cl.flow.qps_wait_s * 1000));
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

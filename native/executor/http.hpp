@@ -483,11 +483,42 @@ struct Response {
     std::string retry_after;
 };
 
+// Client-side flow control of one shard apiserver.  A real apiserver admits a bounded number of requests
+// (max-in-flight, API Priority and Fairness seats with bounded queues) and answers the rest 429 +
+// Retry-After; it also serves kubelets, the scheduler and the GPU operator.  Instead of a fixed number of
+// requests in flight, the client keeps an adaptive limit (AIMD, as TCP's congestion window):
+//   * slow start from `initial`: +1 per success (doubling per round trip) until the first overload signal;
+//   * then +1/limit per success (one per window of `limit` requests) while at least half the limit is used;
+//   * ×`beta` on an overload signal — 429, 503, a request timeout, or a response slower than `latency_s` and
+//     8× the fastest seen — at most once per window (only requests sent after the last cut count);
+//   * never above `cap` (client-pool-size: also the most connections) nor below 1.
+// `qps`/`burst` (client-qps / client-burst) add client-go's token bucket (/root/reference/main.go:52-68
+// leaves it at client-go's default of 5 QPS / burst 10; native mode has none unless configured).
+struct FlowLimits {
+    int cap = 256;
+    double initial = 32;
+    double beta = 0.7;
+    double latency_s = 1.0;
+    bool adaptive = true;
+    double qps = 0, burst = 0;
+};
+
+struct FlowStats {
+    long long overloads = 0, cuts = 0, gated = 0, rejected = 0;  // rejected: 429 answers
+    int max_inflight = 0;
+    double qps_wait_s = 0;
+};
+
 // ------------------------------------------------------------------------------------ client
 class Client {
 public:
-    Client(Credentials creds, int pool_size, double request_timeout)
-        : creds_(std::move(creds)), max_(std::max(1, pool_size)), timeout_(request_timeout) {
+    Client(Credentials creds, int pool_size, double request_timeout, FlowLimits fl = FlowLimits())
+        : creds_(std::move(creds)), max_(std::max(1, pool_size)), timeout_(request_timeout), fl_(fl) {
+        fl_.cap = max_;
+        limit_ = fl_.adaptive ? std::clamp(fl_.initial, 1.0, static_cast<double>(max_)) : max_;
+        slow_start_ = fl_.adaptive && limit_ < max_;
+        tokens_ = fl_.burst > 0 ? fl_.burst : 1.0;
+        tokens_at_ = now_s();
         url_ = parse_url(creds_.server);
         if (url_.tls) ctx_ = make_ssl_ctx(creds_);
         host_ = creds_.tls_server_name.empty()
@@ -508,6 +539,9 @@ public:
     }
     const std::string& prefix() const { return url_.prefix; }
     long long requests = 0, request_errors = 0;  // completed exchanges / transport failures
+    FlowStats flow;
+    double limit() const { return limit_; }
+    int inflight() const { return inflight_; }
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
     // token once on 401, and re-send once on a fresh connection when a reused keep-alive connection died
@@ -596,6 +630,14 @@ private:
     std::string host_;
     int max_;
     double timeout_;
+    FlowLimits fl_;
+    double limit_ = 1;
+    bool slow_start_ = false;
+    int inflight_ = 0, woken_ = 0;
+    uint64_t sent_seq_ = 0, cut_seq_ = 0;
+    double min_latency_ = 1e9;
+    double tokens_ = 0, tokens_at_ = 0;
+    std::deque<std::coroutine_handle<>> gate_;
     int open_ = 0;
     bool closed_ = false;
     bool sweeping_ = false;  // a sweep() is running
@@ -706,11 +748,79 @@ private:
         wake_one();
     }
 
+    // Wait for a client-qps token and a slot under the concurrency limit; returns the request's sequence
+    // number (a cut applies once per window: only to requests sent after the previous cut).
+    Task<uint64_t> admit() {
+        if (fl_.qps > 0) {  // reservation: the token is taken now, the wait is for when it is due
+            double now = now_s();
+            tokens_ = std::min(std::max(fl_.burst, 1.0), tokens_ + (now - tokens_at_) * fl_.qps);
+            tokens_at_ = now;
+            tokens_ -= 1.0;
+            if (tokens_ < 0) {
+                double wait = -tokens_ / fl_.qps;
+                flow.qps_wait_s += wait;
+                co_await loop().sleep(wait);
+            }
+        }
+        struct Park {
+            Client* cl;
+            bool await_ready() { return false; }
+            void await_suspend(std::coroutine_handle<> h) { cl->gate_.push_back(h); }
+            void await_resume() { --cl->woken_; }
+        };
+        bool parked = false;
+        while (inflight_ >= static_cast<int>(limit_)) {
+            if (!parked) ++flow.gated;
+            parked = true;
+            co_await Park{this};
+        }
+        ++inflight_;
+        flow.max_inflight = std::max(flow.max_inflight, inflight_);
+        co_return ++sent_seq_;
+    }
+    // A request admitted as `seq` finished: `status` (0: transport failure), after `latency` seconds.
+    void finish(uint64_t seq, int status, double latency, bool timed_out) {
+        int used = inflight_--;
+        if (status == 429) ++flow.rejected;
+        if (fl_.adaptive) {
+            bool overload = status == 429 || status == 503 || timed_out ||
+                            (status > 0 && latency > fl_.latency_s && latency > 8 * min_latency_);
+            if (overload) {
+                ++flow.overloads;
+                if (seq > cut_seq_) {
+                    limit_ = std::max(1.0, limit_ * fl_.beta);
+                    slow_start_ = false;
+                    cut_seq_ = sent_seq_;
+                    ++flow.cuts;
+                }
+            } else if (status > 0 && status < 500) {
+                min_latency_ = std::min(min_latency_, latency);
+                if (used >= limit_ / 2)
+                    limit_ = std::min(static_cast<double>(max_), limit_ + (slow_start_ ? 1.0 : 1.0 / limit_));
+                if (limit_ >= max_) slow_start_ = false;
+            }
+        }
+        int room = static_cast<int>(limit_) - inflight_ - woken_;
+        while (room-- > 0 && !gate_.empty()) {
+            loop().post(gate_.front());
+            gate_.pop_front();
+            ++woken_;
+        }
+    }
+
     Task<Response> exchange(const std::string& method, const std::string& target, const std::string* body,
                             const char* content_type) {
         std::string req = render(method.c_str(), target, body, content_type);
         for (int tries = 0;; ++tries) {
-            auto c = co_await acquire();
+            uint64_t seq = co_await admit();
+            double t0 = now_s();
+            std::unique_ptr<Conn> c;
+            try {
+                c = co_await acquire();
+            } catch (...) {
+                finish(seq, 0, now_s() - t0, false);
+                throw;
+            }
             bool reused = c->reused;
             size_t before = 0;
             c->deadline = now_s() + timeout_;
@@ -733,6 +843,7 @@ private:
             busy_.erase(c.get());
             bool timed_out = !ok && now_s() >= c->deadline;
             release(std::move(c), ok && keep);
+            finish(seq, ok ? r.status : 0, now_s() - t0, timed_out);
             if (ok) {
                 ++requests;
                 co_return r;

@@ -223,7 +223,7 @@ class App:
         self.n_executors = 0
         self.per_shard = 1
         qps, burst = client_limits(cfg)
-        self.client_factory = client_factory or default_client_factory(qps, burst, cfg.client_pool_size,
+        self.client_factory = client_factory or default_client_factory(qps, burst, cfg.pool_size(),
                                                                        cfg.transport, cfg.client_pipeline_depth)
         self._controller_client = controller_client
         self.metrics = metrics
@@ -260,7 +260,7 @@ class App:
         client = self._controller_client
         if client is None:
             qps, burst = client_limits(cfg)
-            client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.client_pool_size,
+            client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.pool_size(),
                                 pipeline_depth=cfg.client_pipeline_depth,
                                 cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
@@ -424,6 +424,8 @@ class App:
             out["watch_relay"] = dict(self.relay.stats)
         if self.executor_impl:
             out["executor_impl"] = self.executor_impl
+        if self._gc_task is not None:
+            out["gc"] = dict(gctune.STATS)
         if self.elector is not None:
             out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
                              "transitions": self.elector.transitions}
@@ -528,10 +530,15 @@ class App:
                 self.partitions.start()
         if self.cfg.mode == "native":
             gctune.tune()
-            # NCC_GC_FREEZE="<period>,<generation collected first, or none>" (experiments; default "1,none")
+            # NCC_GC_FREEZE="<period>,<generation collected first, or none>" (experiments; default "1,none":
+            # freeze every second, after a generation-0 pass when no automatic one ran since the last freeze);
+            # NCC_GC_FULL_S: unfreeze + full collection this often, at an idle moment when there is one
             period, _, gen = os.environ.get("NCC_GC_FREEZE", "1,none").partition(",")
-            self._gc_task = asyncio.ensure_future(
-                gctune.freeze_loop(float(period), collect=None if gen in ("", "none") else int(gen)))
+            queue = self.controller.queue
+            self._gc_task = asyncio.ensure_future(gctune.freeze_loop(
+                float(period), collect=None if gen in ("", "none", "blind") else int(gen),
+                full_period=float(os.environ.get("NCC_GC_FULL_S", "300")), idle=queue.idle,
+                young=gen != "blind"))
         self._lag_task = loopmon.start(self.options.role)
         if self.cfg.mode == "native" and self.options.role != "executor" and self.cfg.shard_reload_period > 0:
             self._reload_task = asyncio.ensure_future(self._reload_loop(self.cfg.shard_reload_period))

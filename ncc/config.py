@@ -80,7 +80,8 @@ class AppConfig:
     mode: str = "native"
     client_qps: float = 0.0          # 0 = mode default (compat: client-go's 5/10, native: none); < 0 = none
     client_burst: int = 10
-    client_pool_size: int = 64
+    client_pool_size: int = 0        # connections (= most requests in flight) per cluster; 0 = auto: 64 for
+                                     # the Python clients, 256 for the C++ executor's shard clients
     client_pipeline_depth: int = 1   # >1: HTTP/1.1-pipeline requests once all pool connections are busy
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
@@ -112,6 +113,10 @@ class AppConfig:
     lease_duration: float = _dur(15.0)
     renew_deadline: float = _dur(10.0)
     retry_period: float = _dur(2.0)
+
+    def pool_size(self) -> int:
+        """client-pool-size for the Python transport (0 = its default of 64)."""
+        return self.client_pool_size if self.client_pool_size > 0 else 64
 
     @staticmethod
     def key_of(attr: str) -> str:

@@ -405,16 +405,31 @@ class CoordinatorPartitions:
                           "alive": h.proc is not None and h.proc.returncode is None} for h in self.handles}
 
 
+# per shard in a C++ executor's status: its client's adaptive concurrency limit and what drove it
+# (native/executor/http.hpp `Client::finish`)
+FLOW_FIELDS = ("limit", "inflight", "max_inflight", "rejected_429", "overload_signals", "cuts", "gated",
+               "qps_wait_ms")
+
+
 def status_view(msg: dict) -> dict:
     """An executor's periodic status message ({"t": "status", "s": {shard: {plural: [synced, watching,
     events, relists, last error]}}, "q", "r", "w", "e"}) as /debug/state shows it."""
-    shards = {}
+    shards, flow = {}, {}
     for shard, kinds in (msg.get("s") or {}).items():
         shards[shard] = {plural: {"synced": bool(v[0]), "watching": bool(v[1]), "events": v[2], "relists": v[3],
                                   "last_error": v[4] or None}
-                         for plural, v in (kinds or {}).items() if isinstance(v, (list, tuple)) and len(v) >= 5}
-    return {"shards": shards, "queued": msg.get("q"), "passes": msg.get("r"), "writes": msg.get("w"),
-            "errors": msg.get("e"), "at": time.time()}
+                         for plural, v in (kinds or {}).items()
+                         if plural != "flow" and isinstance(v, (list, tuple)) and len(v) >= 5}
+        fl = (kinds or {}).get("flow")
+        if isinstance(fl, (list, tuple)) and len(fl) >= 8:  # the C++ executor's client-side flow control
+            flow[shard] = dict(zip(FLOW_FIELDS, fl))
+    out = {"shards": shards, "queued": msg.get("q"), "passes": msg.get("r"), "writes": msg.get("w"),
+           "errors": msg.get("e"), "at": time.time()}
+    if flow:
+        out["flow"] = flow
+    if isinstance(msg.get("gc"), dict):  # the Python executor's collector passes (ncc/gctune.py)
+        out["gc"] = msg["gc"]
+    return out
 
 
 def status_message(index: int, shards: list, stats: dict) -> dict:
@@ -427,8 +442,9 @@ def status_message(index: int, shards: list, stats: dict) -> dict:
             kinds[inf.rt.plural] = [inf.has_synced(), inf.watching, inf.events, inf.relists,
                                     repr(err)[:300] if err is not None else ""]
         out[sh.name] = kinds
+    from .. import gctune
     return {"t": "status", "i": index, "s": out, "q": stats.get("queued"), "r": stats.get("reconciles"),
-            "w": stats.get("writes"), "e": stats.get("errors")}
+            "w": stats.get("writes"), "e": stats.get("errors"), "gc": dict(gctune.STATS)}
 
 
 # ---------------------------------------------------------------------------------------- executor side

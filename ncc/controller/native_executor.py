@@ -28,6 +28,8 @@ from ..shards.loader import discover
 log = logging.getLogger("ncc.executor")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# connections (and the most requests in flight) per shard when `client-pool-size` is 0 (auto)
+DEFAULT_POOL_SIZE = 256
 _LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "WARN": 30, "ERROR": 40, "CRITICAL": 50}
 
 
@@ -114,13 +116,18 @@ class NativeExecutorConfig:
                 "username": cc.username or "", "password": cc.password or ""}
 
     async def render(self, handle) -> str:
+        from ..app import client_limits
         o, cfg = self.options, self.cfg
         shards = [await self.shard_entry(n) for n in handle.shards]
+        qps, burst = client_limits(cfg)
+        pool = cfg.client_pool_size if cfg.client_pool_size > 0 else DEFAULT_POOL_SIZE
         doc = {
             "namespace": cfg.controller_namespace, "alias": cfg.alias,
             # one C++ process per shard carries all of its concurrency: like client-go's HTTP/2 connection
-            # (up to 250 concurrent streams) it keeps ≥ 256 requests in flight per shard
-            "workers": 4 * max(256, cfg.client_pool_size), "pool_size": max(256, cfg.client_pool_size),
+            # (up to 250 concurrent streams) up to `pool` requests in flight per shard, under an adaptive
+            # limit (http.hpp `Client`: slow start, AIMD on 429/503/timeouts) and the client-qps bucket
+            "workers": 4 * max(DEFAULT_POOL_SIZE, pool), "pool_size": pool,
+            "client_qps": qps, "client_burst": burst,
             "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
             "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,
             "rate_limit_qps": o.rate_limit_qps, "rate_limit_burst": o.rate_limit_burst,

@@ -135,15 +135,21 @@ class _ServerConn(asyncio.Protocol):
         self.buf = bytearray()
         self.closed = False
         self.busy = False
+        self.api = False  # served a request other than a watch (connection statistics)
         self._drain: asyncio.Future | None = None
 
     def connection_made(self, transport):
         self.transport = transport
-        self.server._conns.add(self)
+        srv = self.server
+        srv._conns.add(self)
+        srv.accepted += 1
 
     def connection_lost(self, exc):
         self.closed = True
-        self.server._conns.discard(self)
+        srv = self.server
+        srv._conns.discard(self)
+        if self.api:
+            srv.api_conns -= 1
         if self._drain is not None and not self._drain.done():
             self._drain.set_result(None)
 
@@ -185,6 +191,12 @@ class _ServerConn(asyncio.Protocol):
             del buf[:i + 4 + clen]
             req = Request(method, target, headers, body)
             req._conn = self  # type: ignore[attr-defined]
+            if not self.api and "watch=" not in target:
+                self.api = True
+                srv = self.server
+                srv.api_conns += 1
+                if srv.api_conns > srv.max_api_conns:
+                    srv.max_api_conns = srv.api_conns
             keep = headers.get("connection", "").lower() != "close"
             if fast is not None:
                 try:
@@ -242,6 +254,12 @@ class HttpServer:
         self._server: asyncio.AbstractServer | None = None
         self._conns: set = set()
         self.port: int | None = None
+        self.accepted = 0  # connections accepted so far
+        self.api_conns = self.max_api_conns = 0  # open connections that served a non-watch request; the most at once
+
+    def conn_stats(self) -> dict:
+        return {"open": len(self._conns), "accepted": self.accepted, "api_open": self.api_conns,
+                "api_max": self.max_api_conns}
 
     async def start(self, host: str, port: int, ssl_context=None) -> int:
         loop = asyncio.get_running_loop()

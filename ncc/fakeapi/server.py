@@ -9,13 +9,16 @@ paths, namespaced and cluster-wide, `GET` (get / list / `?watch=1`), `POST`, `PU
 Test/bench control endpoints (not part of the Kubernetes API):
   GET  /_fake/stats    request counters and object counts
   POST /_fake/faults   {"latency_ms", "jitter_ms", "error_rate", "error_code", "throttle_rate",
-                        "down", "drop_watches", "compact", "rules"} — fault injection for the
+                        "down", "drop_watches", "compact", "rules", and the request-admission model
+                        "max_mutating_inflight", "apf_seats", "apf_queue", "apf_queue_wait_s",
+                        "service_ms", "read_service_ms" (ncc/fakeapi/flowcontrol.py)} — fault injection for the
                        retry/backoff benchmark (BASELINE.json config 5) and for targeted tests:
                        `rules` = [{"method", "resource", "name", "code", "reason", "count",
                        "retry_after", "after"}, ...] fail the matching requests ("*" or absent = any;
                        `count` answers, -1 = until cleared; `retry_after` seconds go out as a Retry-After
                        header; `after`: serve the request, then answer with the error)
-  GET  /_fake/writes   the mutating requests served so far ([method, plural, name, subresource, status])
+  GET  /_fake/writes   the mutating requests served so far ([method, plural, name, subresource, status,
+                       monotonic time])
   POST /_fake/objects  bulk create `{"items": [...]}` without per-request overhead (bench seeding)
   POST /_fake/apply    `{"items": [...], "yield_every": n}` create-or-update a wave of user changes,
                        committed in slices of n with watch delivery in between; `{"staged": id}`
@@ -41,6 +44,7 @@ from ..api.jsonenc import dumps_bytes, loads_bytes
 from ..aio import wait_timeout
 from ..kube import errors as E
 from ..kube.client import PATCH_APPLY, PATCH_JSON, PATCH_MERGE, PATCH_STRATEGIC
+from .flowcontrol import FlowControl
 from .markers import MarkerTracker
 from .storage import ClusterState
 
@@ -71,6 +75,13 @@ class Faults:
         self.down = False
         self.write_only = True  # error_rate applies to mutating requests only
         self.rules: list[dict] = []  # targeted failures (see the module docstring)
+        # request admission (flowcontrol.py): 0 = off
+        self.max_mutating_inflight = 0
+        self.apf_seats = 0
+        self.apf_queue = 50
+        self.apf_queue_wait_s = 15.0
+        self.service_ms = 0.0
+        self.read_service_ms = 0.0
 
     def match(self, method: str, plural: str, name: str | None) -> tuple | None:
         """(error, after) of the targeted rule this request matches, or None.  `after`: the request is
@@ -94,9 +105,13 @@ class Faults:
     def update(self, d: dict) -> None:
         if "rules" in d:
             self.rules = [dict(r) for r in d["rules"] or ()]
-        for k in ("latency_ms", "jitter_ms", "error_rate", "throttle_rate"):
+        for k in ("latency_ms", "jitter_ms", "error_rate", "throttle_rate", "apf_queue_wait_s", "service_ms",
+                  "read_service_ms"):
             if k in d:
                 setattr(self, k, float(d[k]))
+        for k in ("max_mutating_inflight", "apf_seats", "apf_queue"):
+            if k in d:
+                setattr(self, k, int(d[k]))
         if "error_code" in d:
             self.error_code = int(d["error_code"])
         if "down" in d:
@@ -120,6 +135,7 @@ class FakeApiServer:
         self.token = token
         self.bookmark_interval = bookmark_interval
         self.faults = Faults()
+        self.flow = FlowControl()
         self.markers = MarkerTracker()
         self.staged: dict[str, dict] = {}  # /_fake/stage: pre-decoded apply bodies by id
         self.state.write_hooks.append(self.markers.on_write)
@@ -198,7 +214,7 @@ class FakeApiServer:
         if request.path.startswith("/_fake/"):
             return None
         f = self.faults
-        if f.latency_ms or f.jitter_ms:
+        if f.latency_ms or f.jitter_ms or FlowControl.active(f):
             return None
         if request.method == "GET" and "watch=" in request.raw_query:
             return None
@@ -211,8 +227,21 @@ class FakeApiServer:
         if path.startswith("/_fake/"):
             return await self._control(request, path[len("/_fake/"):])
         f = self.faults
-        if (f.latency_ms or f.jitter_ms) and path.startswith(("/api/", "/apis/")) and not f.down:
+        api = path.startswith(("/api/", "/apis/"))
+        if (f.latency_ms or f.jitter_ms) and api and not f.down:
             await asyncio.sleep((f.latency_ms + random.random() * f.jitter_ms) / 1000.0)
+        if api and FlowControl.active(f) and not f.down and \
+                not (request.method == "GET" and "watch=" in request.raw_query):
+            mutating = request.method in ("POST", "PUT", "PATCH", "DELETE")
+            err = await self.flow.admit(f, mutating)
+            if err is not None:
+                self.requests["throttled"] += 1
+                return _status_response(err)
+            try:
+                await self.flow.hold(f, mutating)
+                return self._core(request)
+            finally:
+                self.flow.release(mutating)
         r = self._core(request)
         if isinstance(r, tuple):  # a watch
             return await self._watch(request, r[1], r[2])
@@ -225,7 +254,8 @@ class FakeApiServer:
                 not isinstance(r, tuple) and request.path.startswith(("/api/", "/apis/")):
             target = self._routes.get(request.path)
             if isinstance(target, tuple) and len(target) == 4:
-                self.writes.append((request.method, target[0].plural, target[2], target[3], r.status))
+                self.writes.append((request.method, target[0].plural, target[2], target[3], r.status,
+                                    time.monotonic()))
                 if len(self.writes) > 100000:
                     del self.writes[:50000]
         return r
@@ -438,7 +468,8 @@ class FakeApiServer:
             return self._json({"name": self.name, "rv": self.state.rv, "requests": self.requests,
                                "state": self.state.stats, "objects": counts, "faults": self.faults.as_dict(),
                                "admission": self.state.admission.as_dict(),
-                               "watchers": len(self.state._watchers)})
+                               "watchers": len(self.state._watchers), "connections": self._http.conn_stats(),
+                               "flow": self.flow.stats()})
         if what == "writes":
             return self._json({"writes": [list(w) for w in self.writes]})
         if what == "faults" and request.method == "POST":
@@ -554,9 +585,9 @@ async def serve(args) -> None:
     # A test server that keeps what it allocates: freeze every second, never scan the survivors (gctune);
     # NCC_FAKEAPI_GC=collect restores the round-2 controller policy (generation-1 pass + freeze every 5 s)
     if os.environ.get("NCC_FAKEAPI_GC") == "collect":
-        gc_task = asyncio.ensure_future(gctune.freeze_loop(5.0, collect=1))
+        gc_task = asyncio.ensure_future(gctune.freeze_loop(5.0, collect=1, full_period=0))
     else:
-        gc_task = asyncio.ensure_future(gctune.freeze_loop(1.0, collect=None))
+        gc_task = asyncio.ensure_future(gctune.freeze_loop(1.0, full_period=0, young=False))
     from .. import loopmon
     lag_task = loopmon.start(f"fakeapi:{args.name}")
     if args.port_file:

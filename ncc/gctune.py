@@ -4,8 +4,23 @@ Cached Kubernetes objects are acyclic JSON dicts, so CPython's cyclic collector 
 caches: a full (gen-2) pass over a 30k-object store costs ~10-25 ms and lands at random points of a
 propagation wave as a latency tail.  `tune()` raises the allocation thresholds and periodically moves
 everything that survived into the permanent generation (`gc.freeze()`), so collections only look at
-recent garbage.  Reference counting still frees objects immediately; only cycles created before a
-freeze and later abandoned are kept (the asyncio machinery creates few, and they are short-lived).
+recent garbage.  Reference counting still frees acyclic objects immediately.
+
+Cycles are the catch: `gc.freeze()` moves *every* tracked object into the permanent generation, an
+unreachable cycle included, and nothing there is ever collected again.  A failing reconcile makes such
+cycles (exception -> traceback -> frame -> locals -> exception), so a controller retrying against a dead
+shard for hours must not freeze them.  The freeze therefore happens only where the young generations
+are empty — at the end of a generation-1 (or 2) collection (the `gc.callbacks` "stop" hook), so everything
+frozen has survived two scans (an exception cycle of a pass in flight survives one now and then):
+
+* every `period` seconds a freeze becomes due; a busy process's next automatic generation-1 collection
+  (one per 20 generation-0 ones) performs it;
+* a process with no such collection within a period gets a generation-1 pass of our own, cheap because
+  what it scans is what was allocated and survived since the previous freeze;
+* every `full_period` seconds, preferably when the controller is idle, everything is unfrozen and
+  collected, then frozen again: a cycle that was still alive when a collection froze it is reclaimed there.
+
+Each pass is timed and counted in `STATS` (shown in `/debug/state` and the `NCC_CPU_REPORT` line).
 """
 from __future__ import annotations
 
@@ -14,48 +29,114 @@ import gc
 import time
 
 THRESHOLDS = (50_000, 20, 100)
-STATS = {"passes": 0, "collected": 0, "seconds": 0.0, "max_seconds": 0.0}  # freeze_loop's own passes
+# freeze_loop's own passes: "young" (generation-1 before a due freeze), "full" (unfreeze + full collection),
+# and the explicit `collect` passes of the NCC_GC_FREEZE experiment knob
+STATS = {"passes": 0, "collected": 0, "seconds": 0.0, "max_seconds": 0.0,
+         "young_n": 0, "young_collected": 0, "young_s": 0.0,
+         "full_n": 0, "full_collected": 0, "full_s": 0.0, "full_max_s": 0.0, "frozen": 0}
 
-
-_auto = {"t0": 0.0}
+_auto = {"t0": 0.0, "gen1_runs": 0, "freeze_due": False}
 
 
 def _on_gc(phase: str, info: dict) -> None:
-    """Time every collection the interpreter runs (automatic ones included), per generation."""
+    """Count every collection the interpreter runs (automatic ones included), time them per generation, and
+    perform a due freeze at the end of a generation-1 or -2 collection, when the young generations are empty."""
     if phase == "start":
         _auto["t0"] = time.perf_counter()
         return
-    dt = time.perf_counter() - _auto["t0"]
     g = info.get("generation", 0)
+    if g >= 1:
+        _auto["gen1_runs"] += 1  # passes that empty generations 0 and 1
+    dt = time.perf_counter() - _auto["t0"]
     STATS[f"gen{g}_n"] = STATS.get(f"gen{g}_n", 0) + 1
     STATS[f"gen{g}_s"] = round(STATS.get(f"gen{g}_s", 0.0) + dt, 4)
     STATS[f"gen{g}_max_s"] = round(max(STATS.get(f"gen{g}_max_s", 0.0), dt), 4)
+    if g >= 1 and _auto["freeze_due"]:
+        _auto["freeze_due"] = False
+        gc.freeze()
+        STATS["freezes"] = STATS.get("freezes", 0) + 1
 
 
 def tune(thresholds: tuple = THRESHOLDS, account: bool = True) -> None:
     gc.set_threshold(*thresholds)
+    gc.unfreeze()
+    gc.collect()  # start-up garbage (imports, config parsing) is not frozen
     gc.freeze()
-    if account and _on_gc not in gc.callbacks:
+    if account and _on_gc not in gc.callbacks:  # the young-pass rule of freeze_loop needs the counter
         gc.callbacks.append(_on_gc)
 
 
-async def freeze_loop(period: float = 1.0, collect: int | None = None) -> None:
-    """Collect young garbage of generations up to `collect` (None: no pass of our own), then freeze the
-    survivors, every `period` seconds.
+def _timed_collect(gen: int | None) -> tuple[int, float]:
+    t0 = time.perf_counter()
+    n = gc.collect() if gen is None else gc.collect(gen)
+    return n, time.perf_counter() - t0
 
-    The controller processes default to freezing every second with no pass of their own: the automatic
-    generation-0 collections (every 50 000 container allocations) still reclaim cycles that die young, and
-    everything that survived one is frozen unscanned.  The round-2 policy, a generation-1 pass every 5 s,
-    scans every young survivor: in the coordinator at 20 000 templates it found nothing to free in a whole
-    run and stopped the loop for up to 250-300 ms each time; an explicit generation-0 pass every second
-    found nothing either and cost 1.2 s of CPU per run (BENCHMARKS.md)."""
+
+def young_then_freeze(seen_gen1_runs: int) -> int:
+    """One tick of the freeze policy: make a freeze due (the next generation-1 collection performs it); if one
+    is still due from the previous tick and no such collection ran since `seen_gen1_runs`, run a
+    generation-1 pass of our own, which performs it.  Returns the collection counter for the next tick."""
+    if _auto["freeze_due"] and _auto["gen1_runs"] == seen_gen1_runs:
+        n, dt = _timed_collect(1)
+        STATS["young_n"] += 1
+        STATS["young_collected"] += n
+        STATS["young_s"] = round(STATS["young_s"] + dt, 4)
+        if _auto["freeze_due"]:  # no collection hook installed (tune(account=False)): freeze here
+            _auto["freeze_due"] = False
+            gc.freeze()
+    else:
+        _auto["freeze_due"] = True
+    return _auto["gen1_runs"]
+
+
+def full_collect() -> int:
+    """Collect every generation, then unfreeze, collect again and freeze the survivors.  Returns (and
+    accounts in STATS["full_collected"]) what the second pass found: unreachable objects the freezes had
+    kept — the first pass's are young garbage that was never frozen (STATS["full_pending"])."""
+    pending, dt0 = _timed_collect(None)
+    gc.unfreeze()
+    n, dt = _timed_collect(None)
+    dt += dt0
+    _auto["freeze_due"] = False
+    gc.freeze()
+    STATS["full_n"] += 1
+    STATS["full_pending"] = STATS.get("full_pending", 0) + pending
+    STATS["full_collected"] += n
+    STATS["full_s"] = round(STATS["full_s"] + dt, 4)
+    STATS["full_max_s"] = round(max(STATS["full_max_s"], dt), 4)
+    STATS["frozen"] = gc.get_freeze_count()
+    return n
+
+
+async def freeze_loop(period: float = 1.0, collect: int | None = None, full_period: float = 300.0,
+                      idle=None, young: bool = True) -> None:
+    """Every `period` seconds: collect young garbage (see the module doc; or, with `collect`, always a pass
+    over generations up to `collect` — the NCC_GC_FREEZE experiment knob), then freeze the survivors.
+
+    Every `full_period` seconds (0: never) a full collection over the unfrozen heap.  With `idle` (a callable:
+    is the controller's queue drained?) it waits for an idle moment, for at most another `full_period`.
+
+    `young=False, full_period=0` is the fake apiservers' policy: a test server keeps what it allocates, so it
+    freezes every second and never scans (ncc/fakeapi/server.py)."""
+    seen = _auto["gen1_runs"]
+    last_full = time.monotonic()
     while True:
         await asyncio.sleep(period)
         if collect is not None:
-            t0 = time.perf_counter()
-            STATS["collected"] += gc.collect(collect)
-            dt = time.perf_counter() - t0
+            n, dt = _timed_collect(collect)
+            STATS["collected"] += n
             STATS["passes"] += 1
             STATS["seconds"] += dt
             STATS["max_seconds"] = max(STATS["max_seconds"], dt)
-        gc.freeze()
+            gc.freeze()
+            seen = _auto["gen1_runs"]
+        elif young:
+            seen = young_then_freeze(seen)
+        else:
+            gc.freeze()
+        if full_period > 0:
+            waited = time.monotonic() - last_full
+            if waited >= full_period and (idle is None or waited >= 2 * full_period or idle()):
+                full_collect()
+                seen = _auto["gen1_runs"]
+                last_full = time.monotonic()

@@ -129,6 +129,10 @@ class WorkQueue:
     def __len__(self) -> int:
         return self.core.length()
 
+    def idle(self) -> bool:
+        """Nothing queued and nothing being processed (delayed retries may still be pending)."""
+        return self.core.length() == 0 and not self._started
+
     def shutdown(self) -> None:
         self.core.shutdown()
         if self._timer is not None:

@@ -90,7 +90,7 @@ class Cluster:
         return self
 
     async def start(self):
-        self.app = App(self.env.app_config(mode="native", **impl_config(self.impl), **self.cfg))
+        self.app = App(self.env.app_config(mode="native", **dict(impl_config(self.impl), **self.cfg)))
         await self.app.build()
         self.task = asyncio.ensure_future(self.app.run(self.stop))
         await asyncio.wait_for(self.app.controller.ready.wait(), 15)

@@ -295,3 +295,59 @@ async def test_serve_entrypoint_exits_when_parent_is_gone(tmp_path):
         gc.set_threshold(*thresholds)
         gc.unfreeze()
     assert pf.read_text().startswith("http://127.0.0.1:")
+
+
+async def test_request_admission_seats_queue_inflight_and_service_time():
+    """The APF / max-in-flight model (ncc/fakeapi/flowcontrol.py): requests beyond the seats wait in a bounded
+    FIFO queue, a full queue, an expired wait or too many mutating requests are answered 429 with
+    `Retry-After: 1`, and a write holds its seat for the service time."""
+    import json as _json
+    import time as _time
+
+    import aiohttp
+
+    srv = FakeApiServer(name="apf")
+    url = await srv.start()
+    path = f"{url}/api/v1/namespaces/{NS}/secrets"
+
+    async def burst(session, n, tag):
+        async def one(i):
+            async with session.post(path, data=_json.dumps(make_secret(f"{tag}{i}", NS)),
+                                    headers={"Content-Type": "application/json"}) as r:
+                await r.read()
+                return r.status, r.headers.get("Retry-After")
+        return await asyncio.gather(*(one(i) for i in range(n)))
+
+    try:
+        async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0)) as session:
+            srv.faults.update({"apf_seats": 2, "apf_queue": 2, "service_ms": 100})
+            t0 = _time.monotonic()
+            res = await burst(session, 10, "a")
+            took = _time.monotonic() - t0
+            assert sorted(s for s, _ in res) == [201] * 4 + [429] * 6
+            assert all(ra == "1" for s, ra in res if s == 429)
+            assert 0.19 <= took < 1.5  # two seats, four writes of 100 ms each: two rounds
+            st = srv.flow.stats()
+            assert st["admitted"] == 4 and st["queued"] == 2 and st["rejected_queue_full"] == 6
+            assert st["max_executing"] == 2 and st["executing"] == 0 and st["waiting"] == 0
+            assert sum(b[1] for b in st["by_second"]) == 10 and sum(b[2] for b in st["by_second"]) == 6
+            # an expired wait for a seat is a 429 too
+            srv.faults.update({"apf_seats": 1, "apf_queue": 5, "apf_queue_wait_s": 0.05, "service_ms": 200})
+            res = await burst(session, 3, "b")
+            assert sorted(s for s, _ in res) == [201, 429, 429]
+            assert srv.flow.stats()["rejected_queue_wait"] == 2 and srv.flow.executing == 0
+            # max-mutating-inflight without APF
+            srv.faults.update({"apf_seats": 0, "max_mutating_inflight": 1, "service_ms": 100})
+            res = await burst(session, 3, "c")
+            assert sorted(s for s, _ in res) == [201, 429, 429]
+            assert srv.flow.stats()["rejected_inflight"] == 2 and srv.flow.mutating == 0
+            # reads are not mutating: not limited by max_mutating_inflight
+            async with session.get(path) as r:
+                assert r.status == 200
+            srv.faults.update({"max_mutating_inflight": 0, "service_ms": 0})
+            async with session.get(f"{url}/_fake/stats") as r:
+                stats = await r.json()
+            assert stats["flow"]["admitted"] >= 6 and stats["connections"]["api_max"] >= 1
+            assert stats["requests"]["throttled"] == 10
+    finally:
+        await srv.stop()

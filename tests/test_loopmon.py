@@ -40,21 +40,52 @@ def test_monitor_reports_blocked_loop_and_gc_pass(monkeypatch, tmp_path):
     assert any(r.get("gc_pause_ms") is not None and r["generation"] == 0 for r in rows)
 
 
-def test_freeze_loop_without_collect_only_freezes(monkeypatch):
-    """The controllers' default freezes without a pass of its own; `collect=<generation>` runs that pass first
-    and accounts for it in gctune.STATS."""
+def test_freeze_loop_policies(monkeypatch):
+    """The controllers' default: every tick a freeze becomes due, performed at the end of the next
+    generation-1 collection (young generations empty: cycles abandoned by failing passes are not frozen
+    unscanned), or by a generation-1 pass of our own when none ran within a tick; every `full_period` an
+    unfreeze + full collection.  `young=False` (the fake apiservers) only freezes; `collect=<generation>`
+    always runs that pass first.  Each pass is accounted in gctune.STATS."""
     calls = []
     monkeypatch.setattr(gctune.gc, "collect", lambda gen=2: calls.append(("collect", gen)) or 0)
     monkeypatch.setattr(gctune.gc, "freeze", lambda: calls.append(("freeze",)))
+    monkeypatch.setattr(gctune.gc, "unfreeze", lambda: calls.append(("unfreeze",)))
+    monkeypatch.setattr(gctune.gc, "get_freeze_count", lambda: 0)
+    monkeypatch.setitem(gctune._auto, "freeze_due", False)
 
     async def main(**kw):
         t = asyncio.ensure_future(gctune.freeze_loop(0.01, **kw))
         await asyncio.sleep(0.035)
         t.cancel()
         await asyncio.gather(t, return_exceptions=True)
-    asyncio.run(main())
+    asyncio.run(main(young=False, full_period=0))
     assert calls and all(c == ("freeze",) for c in calls)
     calls.clear()
+    young = gctune.STATS["young_n"]
+    asyncio.run(main(full_period=0))  # quiet process: no collection ran, so a generation-1 pass of ours
+    assert calls[:2] == [("collect", 1), ("freeze",)] and ("unfreeze",) not in calls
+    assert gctune.STATS["young_n"] > young
+    calls.clear()
+    # a generation-1 collection ran since the last tick: the freeze is left due, for the next one to perform
+    gctune._auto["freeze_due"] = False
+    seen = gctune._auto["gen1_runs"]
+    gctune._auto["gen1_runs"] += 1
+    assert gctune.young_then_freeze(seen) == seen + 1 and calls == [] and gctune._auto["freeze_due"]
+    gctune._on_gc("start", {"generation": 0})
+    gctune._on_gc("stop", {"generation": 0})  # a generation-0 pass leaves generation 1 as it was: no freeze
+    assert calls == [] and gctune._auto["freeze_due"]
+    gctune._on_gc("start", {"generation": 1})
+    gctune._on_gc("stop", {"generation": 1})
+    assert calls == [("freeze",)] and not gctune._auto["freeze_due"]
+    calls.clear()
+    full = gctune.STATS["full_n"]
+    asyncio.run(main(full_period=0.015, idle=lambda: True))
+    assert ("unfreeze",) in calls and ("collect", 2) in calls and gctune.STATS["full_n"] > full
+    calls.clear()
+    full = gctune.STATS["full_n"]
+    asyncio.run(main(full_period=0.03, idle=lambda: False))  # busy: waits for idle, at most another period
+    assert gctune.STATS["full_n"] == full
+    calls.clear()
     passes = gctune.STATS["passes"]
-    asyncio.run(main(collect=1))
+    asyncio.run(main(collect=1, full_period=0))
     assert ("collect", 1) in calls and ("freeze",) in calls and gctune.STATS["passes"] > passes

@@ -1,0 +1,112 @@
+"""The controller's memory stays bounded through a long shard outage (BASELINE.json config 5).
+
+The reference retries a failing template forever (`AddRateLimited`, /root/reference/controller.go:405-411).
+Every failing pass leaves reference cycles behind (exception -> traceback -> frame -> locals), which only
+the cyclic collector frees.  Native mode freezes the heap every second (ncc/gctune.py); a freeze must never
+move such a cycle into the permanent generation unscanned, or it is kept for the life of the process.
+These tests run thousands of failing passes against a shard that refuses every write, in the two
+topologies whose reconciles are Python (in-process, and the Python shard executors), and check what is
+left: the unreachable objects a full collection finds, and the resident memory of the executor.
+"""
+import asyncio
+import gc
+import os
+
+import psutil
+import pytest
+
+from ncc import gctune
+from ncc.testing.workload import make_configmap, make_secret, make_template
+from tests.test_conformance import NS, Cluster, wait_for
+
+FAST_RETRY = dict(failure_rate_base_delay=0.001, failure_rate_max_delay=0.003,
+                  rate_limit_elements_per_second=100000, rate_limit_elements_burst=100000)
+TEMPLATES = 20
+
+
+def seed(cl):
+    for i in range(TEMPLATES):
+        cl.cstate.create(R_SECRETS, NS, make_secret(f"s{i}", NS))
+        cl.cstate.create(R_CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
+        cl.cstate.create(R_TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[f"c{i}"]))
+
+
+from ncc.api import resources as R  # noqa: E402
+
+R_SECRETS, R_CONFIGMAPS, R_TEMPLATES = R.SECRETS, R.CONFIGMAPS, R.TEMPLATES
+
+
+async def test_inprocess_failing_passes_leave_no_frozen_garbage(tmp_path, monkeypatch):
+    """5 000+ failing passes in the in-process topology with the full collection switched off: the freezes
+    ran only at the end of collections, so what they kept unreachable is bounded by the failing passes
+    that happened to be in flight at a freeze, not by the number of passes (round 3's policy froze every
+    young cycle: ~1.5 unreachable objects per failing pass)."""
+    monkeypatch.setenv("NCC_GC_FULL_S", "0")
+    gc.unfreeze()  # what earlier tests in this process froze and dropped is not this test's
+    gc.collect()
+    if os.environ.get("NCC_GC_OLD_POLICY"):  # A/B: freeze whatever is there, every tick (round 3)
+        monkeypatch.setattr(gctune, "young_then_freeze", lambda seen: gc.freeze() or seen)
+    try:
+        async with Cluster(tmp_path, "inprocess", **FAST_RETRY) as cl:
+            seed(cl)
+            cl.env.shard_servers[1].faults.update({"error_rate": 1.0, "error_code": 500})
+            await cl.start()
+            stats = cl.app.controller.stats
+
+            async def enough():
+                return stats.get("errors", 0) >= 5000
+            await wait_for(enough, timeout=120, interval=0.2)
+            await asyncio.sleep(1.2)  # at least one more freeze
+            passes = stats.get("errors", 0)
+            gc.collect()  # garbage that is not frozen: the young generation's pending cycles (no leak)
+            gc.unfreeze()
+            leaked = gc.collect()  # what the freezes had kept
+            gc.freeze()
+            freezes = gctune.STATS.get("freezes", 0)
+        assert leaked <= 1500, f"{leaked} unreachable objects frozen after {passes} failing passes ({freezes} freezes)"
+    finally:
+        gc.unfreeze()
+        gc.collect()
+        gc.set_threshold(700, 10, 10)
+
+
+async def test_python_executor_memory_bounded_through_failing_passes(tmp_path, monkeypatch):
+    """The same outage with Python shard executors: their full collections (every second here) find a small
+    constant each time, and an executor's resident memory stops growing once its caches are warm."""
+    monkeypatch.setenv("NCC_GC_FULL_S", "1")
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    try:
+        async with Cluster(tmp_path, "python", **FAST_RETRY) as cl:
+            seed(cl)
+            cl.env.shard_servers[1].faults.update({"error_rate": 1.0, "error_code": 500})
+            await cl.start()
+
+            def status():
+                return [h["status"] for h in cl.app.debug_state()["executors"].values() if h.get("status")]
+
+            def executor_procs():
+                me = psutil.Process(os.getpid())
+                return [c for c in me.children(recursive=True) if "ncc.executor" in " ".join(c.cmdline())]
+
+            async def failing(n):
+                st = status()
+                return st and sum(s.get("errors") or 0 for s in st) >= n
+            await wait_for(lambda: failing(2000), timeout=120, interval=0.2)
+            rss = [sum(p.memory_info().rss for p in executor_procs())]
+            for n in (8000, 14000, 20000):
+                await wait_for(lambda: failing(n), timeout=180, interval=0.2)
+                rss.append(sum(p.memory_info().rss for p in executor_procs()))
+            st = status()
+            g = [s["gc"] for s in st if s.get("gc")]
+            assert g and all(x["full_n"] >= 2 for x in g), g
+            per_pass = max(x["full_collected"] / x["full_n"] for x in g)
+            assert per_pass <= 1500, g  # what the freezes kept: failing passes in flight at a freeze
+            grow = [(b - a) / 2**20 for a, b in zip(rss, rss[1:])]
+            assert grow[-1] < 8, f"executors' resident memory still growing: {grow} MiB per 6000 failing passes"
+    finally:
+        gc.unfreeze()
+        gc.collect()
+        gc.set_threshold(700, 10, 10)
+
+
+pytestmark = pytest.mark.timeout(400)
