@@ -232,6 +232,104 @@ def cpu_seconds(named: dict, rss: dict | None = None, sys_out: dict | None = Non
     return out
 
 
+# ------------------------------------------------------------------ host (box speed vs code speed)
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def cgroup_cpu() -> dict:
+    """The job's CPU quota and its throttling counters (cgroup v2 `cpu.max` / `cpu.stat`, or v1 equivalents)."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            out["quota_cpus"] = None if q == "max" else round(int(q) / int(p), 2)
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for ln in f:
+                k, v = ln.split()
+                if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec"):
+                    out[k] = int(v)
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            out["quota_cpus"] = None if q < 0 else round(q / p, 2)
+            with open("/sys/fs/cgroup/cpu/cpu.stat") as f:
+                for ln in f:
+                    k, v = ln.split()
+                    if k == "throttled_time":
+                        out["throttled_usec"] = int(v) // 1000
+                    elif k in ("nr_periods", "nr_throttled"):
+                        out[k] = int(v)
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+def calibrate() -> dict:
+    """Fixed work timed on this box: a pure-Python loop (dict/str work like the coordinator's) and the C++
+    executor's own `--calibrate` (relayed-line scan, fingerprint, render, crc32).  A slow box shows here
+    before it shows in objects/s."""
+    def py_loop():
+        d = {}
+        for i in range(200_000):
+            k = "nexus/algo-%05d" % (i % 1000)
+            d[k] = d.get(k, 0) + len(k)
+        return d
+    best = 1e9
+    for _ in range(5):
+        t0 = time.perf_counter()
+        py_loop()
+        best = min(best, time.perf_counter() - t0)
+    out = {"python_loop_ms": round(best * 1000, 2)}
+    exe = os.path.join(ROOT, "ncc", "bin", "ncc-executor")
+    if os.path.exists(exe):
+        try:
+            r = subprocess.run([exe, "--calibrate"], capture_output=True, text=True, timeout=60)
+            c = json.loads(r.stdout.strip().splitlines()[-1])
+            out.update({f"cpp_{k}": v for k, v in c.items() if k.endswith("_ns")})
+        except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+            pass
+    return out
+
+
+def ctx_switches(named: dict) -> dict:
+    """Voluntary / involuntary context switches per named process (executors summed under the coordinator)."""
+    import psutil
+    out = {}
+    for name, proc in named.items():
+        if proc is None:
+            continue
+        try:
+            p = psutil.Process(proc.pid)
+            c = p.num_ctx_switches()
+            out[name] = [c.voluntary, c.involuntary]
+            if name == "coordinator":
+                ex = [0, 0]
+                for k in p.children(recursive=True):
+                    try:
+                        if "ncc-executor" in " ".join(k.cmdline()) or "ncc.executor" in " ".join(k.cmdline()):
+                            kc = k.num_ctx_switches()
+                            ex[0] += kc.voluntary
+                            ex[1] += kc.involuntary
+                    except (psutil.Error, OSError):
+                        pass
+                out["executors"] = ex
+        except (psutil.Error, OSError):
+            pass
+    return out
+
+
 def child_pids(proc) -> set:
     """PIDs of every process under the controller (coordinator partitions, executors)."""
     import psutil
@@ -446,6 +544,9 @@ async def run(args, d: Dist) -> dict | None:
             debug = bool(os.environ.get("NCC_BENCH_DEBUG"))
             for step in range(1, total + 1):
                 if step == args.warmup + 1:
+                    cg0 = cgroup_cpu()
+                    cs0 = ctx_switches(named)
+                    load0 = os.getloadavg()
                     d.sync()
                     t_start = time.perf_counter()
                     sys0: dict = {}
@@ -471,6 +572,9 @@ async def run(args, d: Dist) -> dict | None:
             rss: dict = {}
             sys1: dict = {}
             cpu1 = cpu_seconds(named, rss, sys1)
+            cg1 = cgroup_cpu()
+            cs1 = ctx_switches(named)
+            load1 = os.getloadavg()
             ctrl_api = None
             ctrl_state = {}
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
@@ -499,6 +603,21 @@ async def run(args, d: Dist) -> dict | None:
                                   f"{(c[-1] - t0s[step]) / 1e6:.1f} ms, latency p50 {lt[len(lt) // 2] / 1e6:.1f} "
                                   f"max {lt[-1] / 1e6:.1f} ms", file=sys.stderr)
             utils = d.all_gather(util)
+            # the shard apiserver's CPU per object it committed (the substrate's cost; every rank's shard
+            # apiserver commits 3·T·steps objects per hosted shard)
+            sub = (cpu1.get("shard-apiserver", 0.0) - cpu0.get("shard-apiserver", 0.0)) * 1e6 / (args.steps * 3 * T)
+            subs = d.all_gather(sub)
+            host = None
+            if d.rank == 0:
+                host = {"cpu_model": cpu_model(), "cpus": os.cpu_count(), "cgroup": cg1,
+                        "throttled_usec": (cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0))
+                        if "throttled_usec" in cg1 else None,
+                        "nr_throttled": (cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0))
+                        if "nr_throttled" in cg1 else None,
+                        "loadavg": [round(x, 2) for x in load0] + [round(x, 2) for x in load1],
+                        "ctx_switches": {k: [v[0] - cs0.get(k, [0, 0])[0], v[1] - cs0.get(k, [0, 0])[1]]
+                                         for k, v in cs1.items()},
+                        "calibration": calibrate()}
             rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)
             all_times = d.all_gather(shard_times)
@@ -524,6 +643,8 @@ async def run(args, d: Dist) -> dict | None:
             # waves: the cost of the system under test, independent of how fast the fake apiservers are
             ctl_cpu = {k: cpu1.get(k, 0.0) - cpu0.get(k, 0.0) for k in ("coordinator", "executors")}
             us_per_obj = {k: round(v * 1e6 / objs, 1) for k, v in ctl_cpu.items()}
+            substrate = sum(subs) / len(subs) / S if subs else None
+            ctl_us = sum(ctl_cpu.values()) * 1e6 / objs
             from ncc.app import cpu_share
             sizing = ctrl_state.get("sizing") or {}
             ctrl_alive = controller.poll() is None
@@ -547,8 +668,15 @@ async def run(args, d: Dist) -> dict | None:
                            "tls": bool(args.tls)},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
-                "controller_cpu_us_per_object": round(sum(ctl_cpu.values()) * 1e6 / objs, 1),
+                "controller_cpu_us_per_object": round(ctl_us, 1),
                 "controller_cpu_us_per_object_split": us_per_obj,
+                # the same for the fake shard apiserver (the substrate, mean over ranks), and the box-invariant
+                # ratio: controller CPU per synced object over the substrate's CPU per committed object
+                "substrate_us_per_object": round(substrate, 1) if substrate else None,
+                "controller_to_substrate": round(ctl_us / substrate, 3) if substrate else None,
+                "controller_to_substrate_split": {k: round(v / substrate, 3) for k, v in us_per_obj.items()}
+                if substrate else None,
+                "host": host,
                 # kernel-mode share of that CPU (syscalls, the loopback TCP stack) per process
                 "controller_cpu_sys_share": {k: round((sys1.get(k, 0.0) - sys0.get(k, 0.0)) / v, 3)
                                              for k, v in ctl_cpu.items() if v > 0},

@@ -40,7 +40,9 @@
 #include <unistd.h>
 
 #include <chrono>
+#if defined(__x86_64__)
 #include <x86intrin.h>
+#endif
 #include <csignal>
 #include <functional>
 #include <optional>
@@ -158,13 +160,23 @@ static const char* kPhaseName[PH_N] = {"relay_in", "shard_watch", "write_respons
                                        "relay_decode"};
 static unsigned long long g_phase[PH_N] = {};
 static bool g_phases_on = false;
+// phase timer ticks: the TSC on x86_64, the steady clock's nanoseconds elsewhere (aarch64 builds)
+static inline unsigned long long ticks() {
+#if defined(__x86_64__)
+    return __rdtsc();
+#else
+    return static_cast<unsigned long long>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+            .count());
+#endif
+}
 static long long g_scan_hits = 0, g_scan_misses = 0;  // write responses read without / with a DOM
 struct PhaseTimer {
     int ph;
     unsigned long long t0;
-    explicit PhaseTimer(int p) : ph(p), t0(g_phases_on ? __rdtsc() : 0) {}
+    explicit PhaseTimer(int p) : ph(p), t0(g_phases_on ? ticks() : 0) {}
     ~PhaseTimer() {
-        if (g_phases_on) g_phase[ph] += __rdtsc() - t0;
+        if (g_phases_on) g_phase[ph] += ticks() - t0;
     }
 };
 
@@ -1034,6 +1046,7 @@ static void dump_trace() {
 static constexpr size_t kMaxSamples = 1 << 20;
 static uintptr_t* g_samples = nullptr;  // pairs: pc, top-of-stack word
 static volatile size_t g_nsamples = 0;
+#if defined(__x86_64__)
 static void on_sigprof(int, siginfo_t*, void* ucv) {
     auto* uc = static_cast<ucontext_t*>(ucv);
     size_t n = g_nsamples;
@@ -1043,8 +1056,13 @@ static void on_sigprof(int, siginfo_t*, void* ucv) {
         g_nsamples = n + 1;
     }
 }
+#endif
 static void start_sampling() {
     if (std::getenv("NCC_SAMPLE_PROFILE") == nullptr) return;
+#if !defined(__x86_64__)
+    LOG_WARN("NCC_SAMPLE_PROFILE: the sampling profiler reads x86_64 registers; not available on this build");
+    return;
+#else
     g_samples = new uintptr_t[2 * kMaxSamples];
     struct sigaction sa {};
     sa.sa_sigaction = on_sigprof;
@@ -1058,6 +1076,7 @@ static void start_sampling() {
     it.it_interval.tv_usec = us % 1000000;
     it.it_value = it.it_interval;
     setitimer(ITIMER_PROF, &it, nullptr);
+#endif
 }
 static void dump_samples() {
     const char* dir = std::getenv("NCC_SAMPLE_PROFILE");
@@ -2401,12 +2420,12 @@ static Task<void> shutdown_watch() {
         LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu",
                  shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()));
     if (g_phases_on) {
-        // cycles -> seconds: calibrate the TSC against the steady clock
-        unsigned long long c0 = __rdtsc();
+        // ticks -> seconds: calibrate the TSC against the steady clock
+        unsigned long long c0 = ticks();
         double w0 = now_s();
         while (now_s() - w0 < 0.02) {
         }
-        double hz = static_cast<double>(__rdtsc() - c0) / (now_s() - w0);
+        double hz = static_cast<double>(ticks() - c0) / (now_s() - w0);
         struct rusage ru;
         getrusage(RUSAGE_SELF, &ru);
         double user = ru.ru_utime.tv_sec + ru.ru_utime.tv_usec / 1e6, sys = ru.ru_stime.tv_sec + ru.ru_stime.tv_usec / 1e6;
@@ -2595,6 +2614,49 @@ int main(int argc, char** argv) {
             const char* end = skip_container_text(line.data(), line.data() + line.size());
             std::printf("%lld\n", end ? static_cast<long long>(end - line.data()) : -1LL);
         }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "--calibrate") {
+        // fixed work for telling box speed from code speed (bench.py's "host" block): the relayed-line scan
+        // of a synthetic ~1 KB template line, a streaming fingerprint and a body render, and a crc32 loop;
+        // best of 7 rounds, ns per operation
+        crc_init();
+        std::string spec = "{\"container\":{\"image\":\"algo\",\"registry\":\"registry.example.com\",\"versionTag\":\"v1\","
+                           "\"serviceAccountName\":\"sa\"},\"computeResources\":{\"cpuLimit\":\"1000m\",\"memoryLimit\":\"2000Mi\","
+                           "\"customResources\":{\"amd.com/gpu\":\"1\"}},\"command\":\"python\",\"args\":[\"main.py\",\"--x\",\"1\"],"
+                           "\"runtimeEnvironment\":{\"environmentVariables\":[{\"name\":\"A\",\"value\":\"0123456789abcdef\"}],"
+                           "\"mappedEnvironmentVariables\":[{\"secretRef\":{\"name\":\"algo-secret\"}},"
+                           "{\"configMapRef\":{\"name\":\"algo-config\"}}],\"annotations\":{\"a\":\"b\"},"
+                           "\"deadlineSeconds\":120,\"maximumRetries\":3},\"errorHandlingBehaviour\":{\"transientExitCodes\":[1,2],"
+                           "\"fatalExitCodes\":[3]},\"workgroupRef\":{\"name\":\"wg\",\"group\":\"science.sneaksanddata.com\","
+                           "\"kind\":\"NexusAlgorithmWorkgroup\"}}";
+        std::string line = "{\"type\":\"MODIFIED\",\"object\":{\"apiVersion\":\"science.sneaksanddata.com/v1\","
+                           "\"kind\":\"NexusAlgorithmTemplate\",\"metadata\":{\"name\":\"algo-00001\",\"namespace\":\"nexus\","
+                           "\"uid\":\"0b7c7a54-1f1e-4c7e-9d1a-5f6c2b9e8a01\",\"resourceVersion\":\"123456\",\"generation\":7,"
+                           "\"creationTimestamp\":\"2025-01-01T00:00:00Z\"},\"spec\":" + spec + ",\"status\":{\"conditions\":[]}}}";
+        size_t sink = 0;
+        auto best = [&](int n, const std::function<void()>& fn) {
+            double b = 1e30;
+            for (int rep = 0; rep < 7; ++rep) {
+                double t0 = now_s();
+                for (int i = 0; i < n; ++i) fn();
+                b = std::min(b, now_s() - t0);
+            }
+            return b / n * 1e9;
+        };
+        double scan = best(20000, [&] {
+            std::string type;
+            CtlPtr c = ctl_scan(TEMPLATES, line, type);
+            sink += c ? c->spec_raw.size() : 0;
+        });
+        double fp = best(20000, [&] { sink += fingerprint_text(spec) & 1; });
+        Value head = Value::object();
+        head.set("apiVersion", Value::str(kApiVersion));
+        double render = best(20000, [&] { sink += dumps_with(head, {{"spec", spec}}).size(); });
+        std::string kb(1024, 'x');
+        double crc = best(20000, [&] { sink += crc32(kb) & 1; });
+        std::printf("{\"ctl_scan_ns\": %.0f, \"fingerprint_ns\": %.0f, \"render_ns\": %.0f, \"crc32_kb_ns\": %.0f, "
+                    "\"line_bytes\": %zu, \"sink\": %zu}\n", scan, fp, render, crc, line.size(), sink);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "--decode-bench") {

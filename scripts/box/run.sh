@@ -1,0 +1,85 @@
+#!/bin/bash
+# The one box runner (replaces the per-session gpu_*.sh scripts of rounds 1-3).  Every step runs under its
+# own time limit and the first failure ends the call.  Results go to gpurun_out/<out>/.
+#
+#   bash scripts/box/run.sh <out> tier                   GPU tier (pytest -m gpu) + smoke
+#   bash scripts/box/run.sh <out> bench <n> [ARGS...]    the driver's bench shape n times; ARGS are bench.py
+#                                                        flags or KEY=VAL environment for the controller
+#   bash scripts/box/run.sh <out> ab <n> "<A>" "<B>"     A/B in alternation, n pairs; A and B are
+#                                                        space-separated KEY=VAL lists ("-" = none)
+#   bash scripts/box/run.sh <out> suite [suite.py args]  the five BASELINE.json configurations
+#   bash scripts/box/run.sh <out> prof                   rocprofv3 --kernel-trace --stats over a short bench,
+#                                                        and the C++ executor's own sampling profile
+#
+# e.g.  gpurun -- 'bash scripts/box/run.sh r4a tier && bash scripts/box/run.sh r4a bench 3'
+set -o pipefail
+out=gpurun_out/$1
+what=$2
+shift 2
+mkdir -p "$out"
+
+summary() {  # one line per bench result
+  python3 - "$1" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+h = d.get("host") or {}
+c = h.get("calibration") or {}
+print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99", d["p99_latency_ms"],
+      "ctl_us", d["controller_cpu_us_per_object"], d["controller_cpu_us_per_object_split"],
+      "substrate_us", d.get("substrate_us_per_object"), "ratio", d.get("controller_to_substrate"),
+      "coord_cores", d["cpu_cores_busy"].get("coordinator"), "py_loop_ms", c.get("python_loop_ms"),
+      "cpp_scan_ns", c.get("cpp_ctl_scan_ns"), "throttled_us", h.get("throttled_usec"), flush=True)
+EOF
+}
+
+bench_once() {  # <file> [ARGS...]
+  local f=$1; shift
+  local envs=() flags=()
+  for a in "$@"; do  # KEY=VAL: environment (bench.py passes it on to the controller); anything else: a flag
+    if [[ "$a" == *=* && "$a" != -* ]]; then envs+=("$a"); else flags+=("$a"); fi
+  done
+  env "${envs[@]}" timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 "${flags[@]}" \
+    > "$f.json" 2> "$f.err" || return $?
+  summary "$f.json"
+}
+
+case "$what" in
+  tier)
+    timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1 || { tail -30 "$out/pytest_gpu.log"; exit 1; }
+    timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
+      || { tail -30 "$out/smoke.log"; exit 1; }
+    tail -1 "$out/pytest_gpu.log"; tail -1 "$out/smoke.log"
+    ;;
+  bench)
+    n=$1; shift
+    for i in $(seq 1 "$n"); do bench_once "$out/bench_$i" "$@" || exit $?; done
+    ;;
+  ab)
+    n=$1; a=$2; b=$3
+    [ "$a" = "-" ] && a=""
+    [ "$b" = "-" ] && b=""
+    for i in $(seq 1 "$n"); do
+      # shellcheck disable=SC2086
+      bench_once "$out/a_$i" $a || exit $?
+      # shellcheck disable=SC2086
+      bench_once "$out/b_$i" $b || exit $?
+    done
+    ;;
+  suite)
+    timeout -k 10 900 python3 bench/suite.py --modes native --out "$out/suite.json" "$@" > "$out/suite.log" 2>&1 \
+      || { tail -30 "$out/suite.log"; exit 1; }
+    cut -c 1-300 "$out/suite.log" | tail -14
+    ;;
+  prof)
+    export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/rocprof" -o bench -- \
+      python3 bench.py --steps 5 --warmup 2 > "$out/rocprof_bench.json" 2> "$out/rocprof.err" || exit $?
+    NCC_SAMPLE_PROFILE="$PWD/$out/samples" NCC_SAMPLE_US=200 timeout -k 10 300 python3 bench.py --steps 20 \
+      --warmup 5 > "$out/sampled_bench.json" 2> "$out/sampled_bench.err" || exit $?
+    python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
+    summary "$out/sampled_bench.json"
+    ;;
+  *)
+    echo "unknown preset $what" >&2; exit 2;;
+esac

@@ -43,3 +43,6 @@ def test_bench_contract_single_shard():
               "vs_baseline", "dtype", "data", "config"):
         assert k in res
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["controller_alive"]
+    # the data plane that ran is the C++ shard executor, not the Python fallback
+    assert res["controller_sizing"]["executor_impl"] == "native", res["controller_sizing"]
+    assert res["controller_to_substrate"] and res["host"]["calibration"].get("cpp_ctl_scan_ns"), res["host"]
