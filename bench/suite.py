@@ -16,6 +16,11 @@ shard commit time − controller commit time for every object, no client-side wa
      dependents pre-exist, owned, with stale data)
   5  8 shards, 1 000 templates, one shard apiserver flapping (down/up every 1.5 s) — healthy-shard
      latency and the flaky shard's catch-up
+  6  8 shards behind apiservers that admit like a real one (ncc/fakeapi/flowcontrol.py: 50 APF seats, a
+     50-deep queue, 200 mutating requests in flight, 5 ms per write), 10 000-template cold start — does the
+     data plane converge without a 429 storm, and how close to the seats ÷ service-time bound?
+  7  config 6 with the adaptive concurrency limit off (NCC_AIMD=0: a fixed 256 requests in flight per shard,
+     round 3's data plane) — the storm it replaces
 
 Reference-compat mode reproduces the reference controller's scheduling (sequential fail-fast
 shard loop, client-go 5 QPS/10 burst per API group, Event per reconcile, 2 workers).  It is a
@@ -422,6 +427,63 @@ async def config5_flaky(mode, T, timeout, flap=1.5, stages=False):
         await topo.stop()
 
 
+APF = {"apf_seats": 50, "apf_queue": 50, "max_mutating_inflight": 200, "service_ms": 5.0, "apf_queue_wait_s": 15.0}
+
+
+async def config6_admission(mode, T, timeout, aimd=True, admission=None):
+    """8 shards whose apiservers admit requests as a real one does (APF seats + bounded queue, max mutating
+    in flight, a service time per write), cold start of T templates.  Reports convergence (every template
+    Ready), the share of shard requests answered 429 after the first second, and the shard write rate
+    against the seats ÷ service-time bound."""
+    adm = dict(APF, **(admission or {}))
+    topo = Topology(8, mode, extra_env=None if aimd else {"NCC_AIMD": "0"})
+    try:
+        await topo.start_servers()
+        for i in range(8):
+            await topo.fault(i, adm)
+        await topo.apply(objects(T, 0))
+        t_boot = topo.start_controller()
+        res = await wave_all(topo, T, 0, timeout)
+        ok = all(r["ok"] for r in res)
+        label = "6: 8 shards, admission-limited apiservers, cold start" if aimd else \
+            "7: config 6 with a fixed 256 in flight (NCC_AIMD=0)"
+        out = {"config": label, "mode": mode, "shards": 8, "templates": T, "admission": adm, "ok": ok}
+        if not ok:
+            out["counts"] = [r["counts"] for r in res]
+            out["log_tail"] = topo.log_tail()
+            return out
+        done = max(max(max(ts) for ts in r["times"].values()) for r in res)
+        out["converge_s"] = round((done - t_boot) / 1e9, 3)
+        out["all_ready"] = await topo.settle(T, timeout, quiet=0.0)
+        bound = adm["apf_seats"] / (adm["service_ms"] / 1000.0)
+        shares, rates, flows = [], [], []
+        for i, r in enumerate(res):
+            ts = sorted(t for v in r["times"].values() for t in v)
+            span = (ts[-1] - ts[0]) / 1e9 if len(ts) > 1 else 0.0
+            rates.append(len(ts) / span if span > 0 else 0.0)
+            async with topo.session.get(f"{topo.shard_urls[i]}/_fake/stats") as resp:
+                fl = (await resp.json())["flow"]
+            by = fl["by_second"]
+            first = by[0][0] if by else 0
+            req = sum(b[1] for b in by if b[0] > first)
+            rej = sum(b[2] for b in by if b[0] > first)
+            shares.append(rej / req if req else 0.0)
+            flows.append({k: fl[k] for k in ("admitted", "rejected", "rejected_queue_full", "rejected_inflight",
+                                             "rejected_queue_wait", "max_executing", "max_queued", "wait_max_s")})
+            flows[-1]["requests"] = sum(b[1] for b in by)
+        out.update(
+            rejected_share_after_first_second={"max": round(max(shares), 4), "mean": round(sum(shares) / 8, 4)},
+            rejected_total=sum(f["rejected"] for f in flows),
+            requests_total=sum(f["requests"] for f in flows),
+            shard_writes_per_s={"min": round(min(rates), 1), "mean": round(sum(rates) / 8, 1)},
+            bound_writes_per_s=round(bound, 1),
+            of_bound={"min": round(min(rates) / bound, 3), "mean": round(sum(rates) / 8 / bound, 3)},
+            per_shard_flow=flows)
+        return out
+    finally:
+        await topo.stop()
+
+
 async def heartbeat(every: float = 30.0):
     """Progress lines so a long (compat) run is visibly alive."""
     t0 = time.perf_counter()
@@ -464,6 +526,8 @@ async def _run(args) -> list:
                 r = await config4_adoption(mode, size(10000, mode), timeout=args.timeout)
             elif c == 5:
                 r = await config5_flaky(mode, size(1000, mode), timeout=args.timeout, stages=args.stages)
+            elif c in (6, 7) and mode == "native":
+                r = await config6_admission(mode, size(10000, mode), timeout=args.timeout, aimd=c == 6)
             else:
                 continue
             r["wall_s"] = round(time.perf_counter() - t, 1)

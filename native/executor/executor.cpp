@@ -1410,6 +1410,27 @@ static void set_metadata(Value& m, const CtlObj& src) {
     merge("annotations", ann, prev_a);
 }
 
+// A shard Secret/ConfigMap in sync, unless a referencing template whose shard copy exists lost its ownerRef on
+// it (another writer replaced the list: two creating applies at once, a user's edit): that template's pass
+// puts it back — or shard GC could delete the copy with the other owners.
+static void repair_lost_owners(Shard& sh, int kind, const ShardObj& o) {
+    Executor& ex = *g_ex;
+    auto& idx = ex.refs[kind == SECRETS ? 0 : 1];
+    auto it = idx.find(key_of(o.ns, o.name));
+    if (it == idx.end()) return;
+    for (const auto& tkey : it->second) {
+        ShardPtr st = sh.get(TEMPLATES, tkey);
+        if (!st) continue;
+        bool owned = false;
+        for (const auto& p : o.template_owners)
+            if (p.second == st->uid) owned = true;
+        if (!owned) {
+            ++g_enq[ENQ_SHARD_DEPENDENT];
+            ex.enqueue(TEMPLATES, o.ns, tkey.substr(tkey.find('/') + 1));
+        }
+    }
+}
+
 static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const ShardPtr& cur, bool deleted) {
     Executor& ex = *g_ex;
     if (!deleted && !old) return;  // adds are not drift (the reference only repairs on update/delete)
@@ -1425,8 +1446,10 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     }
     CtlPtr src = ex.cget(kind, key_of(o.ns, o.name));
     if (!src) return;
-    if (!deleted && data_in_sync(sh, kind, o, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(o, *src)))
+    if (!deleted && data_in_sync(sh, kind, o, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(o, *src))) {
+        repair_lost_owners(sh, kind, o);
         return;
+    }
     std::vector<std::string> owners;
     for (const auto& p : o.template_owners) owners.push_back(p.first);
     if (owners.empty()) owners = src->owners;
@@ -1815,7 +1838,11 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
     bool is_secret = kind == SECRETS;
     bool with_bin = !is_secret && g_opt.sync_binary_data;
     ShardPtr so = sh.get(kind, key_of(shard_ns, dep));
-    auto create_body = [&]() {
+    // `live`: with server-side apply, the shard copy whose template ownerRefs the applied configuration keeps
+    // (every template's pass applies with the same field manager, and an apply drops the ownerRef entries its
+    // manager applied before and omits now — applying only ours would take the other owners' refs off a
+    // shared Secret/ConfigMap, and shard GC would delete it with this template)
+    auto create_body = [&](const ShardObj* live = nullptr) {
         Value body = Value::object();
         body.set("apiVersion", Value::str("v1"));
         body.set("kind", Value::str(is_secret ? "Secret" : "ConfigMap"));
@@ -1825,6 +1852,12 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         m.set("labels", owner_labels());
         if (g_opt.sync_dependent_metadata) set_metadata(m, *src);
         Value refs = Value::array();
+        if (live != nullptr) {
+            for (const auto& o : live->template_owners)
+                if (o.second != st->uid) refs.a.push_back(owner_ref(o.first, o.second));
+            // a precondition: an apply over a stale view would drop refs applied since (409 instead)
+            if (live->rv >= 0) m.set("resourceVersion", Value::str(std::to_string(live->rv)));
+        }
         refs.a.push_back(owner_ref(st->name, st->uid));
         m.set("ownerReferences", std::move(refs));
         body.set("metadata", std::move(m));
@@ -1847,29 +1880,46 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         co_return co_await shard_get_live(sh, kind, shard_ns, dep);
     };
     if (g_opt.server_side_apply) {
-        // Shard.apply_dependent: refuse a rogue copy, skip one in sync that already carries our ownerRef,
-        // otherwise apply our view (the server unions the ownerRefs by uid, so other owners' stay)
-        if (so) {
-            if (!so->has_owner_refs)
-                throw NamedError("RogueResourceError", "Resource \"" + dep +
-                                                           "\" already exists and is not managed by any Machine "
-                                                           "Learning Algorithm");
-            bool ours = false;
-            for (const auto& o : so->template_owners)
-                if (o.second == st->uid) ours = true;
-            bool type_changed = is_secret && g_opt.sync_secret_type &&
-                                (src->type.empty() ? std::string("Opaque") : src->type) !=
-                                    (so->type.empty() ? std::string("Opaque") : so->type);
-            if (type_changed) {  // Secret.type is immutable: an apply cannot change it, so replace the copy
-                pass->wrote = true;
-                co_await shard_delete(sh, kind, shard_ns, dep);
-                sh.inf[kind].store.erase(key_of(shard_ns, dep));
-            } else if (ours && data_in_sync(sh, kind, *so, *src) &&
-                       (!g_opt.sync_dependent_metadata || meta_in_sync(*so, *src))) {
-                co_return;
+        // Shard.apply_dependent / reconcile.py `_sync_dependent`: every template's pass applies with the same
+        // field manager, and an apply drops the ownerRef entries its manager applied before and omits now.  So
+        // an apply over a known copy carries that copy's template ownerRefs and its resourceVersion (a
+        // concurrent change -> 409 -> once more from the live copy).  A ref lost anyway (two passes creating
+        // the same copy at once from empty caches) is repaired from the shard watch (on_shard_event).  A rogue
+        // copy is refused; one in sync that already carries our ownerRef is skipped.
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            if (so) {
+                if (!so->has_owner_refs)
+                    throw NamedError("RogueResourceError", "Resource \"" + dep +
+                                                               "\" already exists and is not managed by any Machine "
+                                                               "Learning Algorithm");
+                bool ours = false;
+                for (const auto& o : so->template_owners)
+                    if (o.second == st->uid) ours = true;
+                bool type_changed = is_secret && g_opt.sync_secret_type &&
+                                    (src->type.empty() ? std::string("Opaque") : src->type) !=
+                                        (so->type.empty() ? std::string("Opaque") : so->type);
+                if (type_changed) {  // Secret.type is immutable: an apply cannot change it, so replace the copy
+                    pass->wrote = true;
+                    co_await shard_delete(sh, kind, shard_ns, dep);
+                    sh.inf[kind].store.erase(key_of(shard_ns, dep));
+                    so = nullptr;
+                } else if (ours && data_in_sync(sh, kind, *so, *src) &&
+                           (!g_opt.sync_dependent_metadata || meta_in_sync(*so, *src))) {
+                    co_return;
+                }
             }
+            bool conflict = false;
+            try {
+                ShardPtr w = co_await shard_write(sh, kind, "PATCH", shard_ns, dep, create_body(so.get()), pass,
+                                                  src->fp_data, src->fp_bin);
+                if (!so) repair_lost_owners(sh, kind, *w);  // applied without a view of the copy: refs may be gone
+                co_return;
+            } catch (const ApiError& e) {
+                if (!e.conflict() || attempt == 1) throw;
+                conflict = true;
+            }
+            if (conflict) so = co_await shard_get_live(sh, kind, shard_ns, dep);
         }
-        co_await shard_write(sh, kind, "PATCH", shard_ns, dep, create_body(), pass, src->fp_data, src->fp_bin);
         co_return;
     }
     if (!so) so = co_await create();

@@ -4,11 +4,11 @@
   approximated by merge patch except that `metadata.ownerReferences` lists are merged by
   `uid`, which is the only strategic list this controller relies on.
 * RFC 6902 JSON patch (`add`/`remove`/`replace`/`test`/`copy`/`move`).
-* A single-manager approximation of server-side apply: fields present in the applied
-  configuration replace the live ones; labels/annotations are merged; ownerReferences are
-  unioned by uid.  This matches real SSA for a controller that is the sole manager of the
-  fields it applies (which is how native mode uses it).  The fake apiserver's storage also removes a
-  top-level field its applier set before and omits now (`ClusterState.patch`), as real SSA does.
+* An approximation of server-side apply: fields present in the applied configuration replace the
+  live ones; labels/annotations are merged; ownerReferences are unioned by uid.  The fake apiserver's
+  storage (`ClusterState.patch`) also tracks what each field manager applied and removes a top-level
+  field, label, annotation or ownerReference entry the same manager applied before and omits now
+  (an ownerReference another manager also applies stays), as real SSA does from managedFields.
 """
 from __future__ import annotations
 

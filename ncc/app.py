@@ -324,8 +324,7 @@ class App:
                                       assume_writes=o.assume_writes, sync_binary_data=o.sync_binary_data,
                                       sync_metadata=o.sync_dependent_metadata,
                                       slim=o.slim_shard_cache, start=False, names=self.shard_filter,
-                                      key_filter=kf,
-                                      owner_filter=partition_owner_filter(*o.partition) if o.partition else None)
+                                      key_filter=kf, owner_filter=self._shard_owner_filter(infs))
         if o.role == "executor":
             self.recorder = FakeRecorder(keep=False)  # executors never write to the controller cluster
         else:
@@ -551,6 +550,21 @@ class App:
                  "executors=%d×%d (%s) workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
                  self.executor_impl or "in-process", self.options.workers, " (standing by)" if gated else "")
+
+    def _shard_owner_filter(self, infs: dict):
+        """A partitioned executor's filter for shard Secrets/ConfigMaps: owned by one of its partition's
+        templates, unowned, or referenced by one of them — a copy another partition's template owns is still
+        one this partition writes to (with server-side apply it must see the other owners' refs, which an
+        apply without them would drop)."""
+        o = self.options
+        if o.partition is None:
+            return None
+        tstore = infs[R.TEMPLATES].store
+
+        def referenced(ns: str, name: str) -> bool:
+            key = f"{ns}/{name}"
+            return bool(tstore.by_index("secret", key) or tstore.by_index("configmap", key))
+        return partition_owner_filter(*o.partition, referenced=referenced)
 
     def topology(self) -> dict:
         """The process layout this coordinator chose (automatic sizing or overrides)."""

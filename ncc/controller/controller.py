@@ -321,6 +321,19 @@ class Controller(ReconcileMixin):
                 return
 
     # ------------------------------------------------------------ shard-side drift watch (native)
+    def repair_lost_owners(self, shard, index: str, obj: dict) -> None:
+        """A shard Secret/ConfigMap in sync, unless a referencing template whose shard copy exists lost its
+        ownerRef on it (another writer replaced the list: two creating applies at once, a user's edit): that
+        template's pass puts it back — or shard GC could delete the copy with the other owners."""
+        m = meta(obj)
+        ns, name = m.get("namespace", ""), m.get("name", "")
+        uids = {r.get("uid") for r in m.get("ownerReferences") or ()}
+        for t in self.template_informer.store.by_index(index, f"{ns}/{name}"):
+            tn = meta(t).get("name", "")
+            st = shard.template_lister.try_get(ns, tn)
+            if st is not None and meta(st).get("uid") not in uids:
+                self._enqueue_key(make_key(C.KIND_TEMPLATE, ns, tn))
+
     def _register_shard_handlers(self, shard) -> None:
         def template_changed(old, new=None):
             obj = self._unwrap(new if new is not None else old)
@@ -344,7 +357,7 @@ class Controller(ReconcileMixin):
 
         sync_meta = self.options.sync_dependent_metadata
 
-        def dependent_changed(lister, with_binary):
+        def dependent_changed(lister, with_binary, index):
             def h(old, new=None):
                 obj = self._unwrap(new if new is not None else old)
                 deleted = new is None
@@ -354,6 +367,7 @@ class Controller(ReconcileMixin):
                     return
                 if not deleted and data_matches(src, obj, with_binary) and \
                         (not sync_meta or shard.dependent_metadata_matches(src, obj)):
+                    self.repair_lost_owners(shard, index, obj)
                     return
                 for owner in template_owner_names(obj) or template_owner_names(src):
                     if self.template_lister.try_get(ns, owner) is not None:
@@ -362,11 +376,11 @@ class Controller(ReconcileMixin):
 
         shard.template_informer.add_event_handler(on_update=template_changed, on_delete=template_changed)
         shard.workgroup_informer.add_event_handler(on_update=workgroup_changed, on_delete=workgroup_changed)
-        shard.secret_informer.add_event_handler(on_update=dependent_changed(self.secret_lister, False),
-                                                on_delete=dependent_changed(self.secret_lister, False))
+        shard.secret_informer.add_event_handler(on_update=dependent_changed(self.secret_lister, False, "secret"),
+                                                on_delete=dependent_changed(self.secret_lister, False, "secret"))
         shard.configmap_informer.add_event_handler(
-            on_update=dependent_changed(self.configmap_lister, self.options.sync_binary_data),
-            on_delete=dependent_changed(self.configmap_lister, self.options.sync_binary_data))
+            on_update=dependent_changed(self.configmap_lister, self.options.sync_binary_data, "configmap"),
+            on_delete=dependent_changed(self.configmap_lister, self.options.sync_binary_data, "configmap"))
 
     # ================================================================== coordinator / executor plumbing
     def _report(self, kind: str, namespace: str, name: str, obj: dict, results: dict) -> None:

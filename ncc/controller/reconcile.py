@@ -633,29 +633,48 @@ class ReconcileMixin:
         shard_obj = shard_lister.try_get(shard_ns, meta(src).get("name", ""))
         opts = self.options
         with_binary = opts.sync_binary_data and not is_secret
+        shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
+        create = "create_secret" if is_secret else "create_configmap"
         if opts.server_side_apply:
+            # Every template's pass applies with the same field manager, and an apply drops the ownerRef entries
+            # its manager applied before and omits now.  So an apply over a known copy carries that copy's
+            # template ownerRefs and its resourceVersion (a concurrent change → 409 → once more from the live
+            # copy).  A ref lost anyway — two passes creating the same copy at once from empty caches — is
+            # repaired from the shard watch (Controller._register_shard_handlers).
             try:
-                if shard_obj is not None:
-                    missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template,
-                                                              shard.name)  # rogue → error
-                    if is_secret and opts.sync_secret_type and \
-                            (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
-                        # Secret.type is immutable, so an apply cannot change it: replace the copy
-                        self._pass_wrote()
-                        await self._delete_one(shard, lambda o: shard.delete_dependent(R.SECRETS, o), shard_obj)
-                    elif not missing_owner and data_matches(src, shard_obj, with_binary) and \
-                            (not opts.sync_dependent_metadata or shard.dependent_metadata_matches(src, shard_obj)):
+                for attempt in range(2):
+                    if shard_obj is not None:
+                        missing_owner = self.is_missing_ownership(shard_obj, shard_template, kind, template,
+                                                                  shard.name)  # rogue → error
+                        if is_secret and opts.sync_secret_type and \
+                                (src.get("type") or "Opaque") != (shard_obj.get("type") or "Opaque"):
+                            # Secret.type is immutable, so an apply cannot change it: replace the copy
+                            self._pass_wrote()
+                            await self._delete_one(shard, lambda o: shard.delete_dependent(R.SECRETS, o), shard_obj)
+                            shard_obj = None
+                        elif not missing_owner and data_matches(src, shard_obj, with_binary) and \
+                                (not opts.sync_dependent_metadata or shard.dependent_metadata_matches(src, shard_obj)):
+                            return
+                    self._pass_wrote()
+                    try:
+                        res = await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER, live=shard_obj)
+                        if shard_obj is None and isinstance(res, dict):
+                            # applied without a view of the copy: if it existed, refs may have been dropped
+                            self.repair_lost_owners(shard, "secret" if is_secret else "configmap", res)
                         return
-                self._pass_wrote()
-                await shard.apply_dependent(rt, shard_template, src, C.FIELD_MANAGER)
+                    except E.Conflict:
+                        if attempt:
+                            raise
+                    live = await shard.client.get(rt, shard_ns, dep_name)
+                    shard_informer.store.assume(live)
+                    shard_obj = shard_informer.store.get(shard_ns, dep_name) or live
             except Exception as e:  # noqa: BLE001
                 raise self._dependent_failed(template, kind, dep_name, e)
             return
-        shard_informer = shard.secret_informer if is_secret else shard.configmap_informer
         if shard_obj is None:
             try:
-                shard_obj = await self._write(shard, "create_secret" if is_secret else "create_configmap",
-                                              shard_informer, rt, shard_template, src, C.FIELD_MANAGER)
+                shard_obj = await self._write(shard, create, shard_informer, rt, shard_template, src,
+                                              C.FIELD_MANAGER)
             except Exception as e:  # noqa: BLE001
                 raise self._dependent_failed(template, kind, dep_name, e)
         try:

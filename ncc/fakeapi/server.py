@@ -333,7 +333,8 @@ class FakeApiServer:
             ctype = request.content_type
             if ctype not in (PATCH_MERGE, PATCH_STRATEGIC, PATCH_JSON, PATCH_APPLY):
                 raise E.ApiError(f"unsupported patch type {ctype}", code=415, reason="UnsupportedMediaType")
-            return self._written(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub))
+            return self._written(self.state.patch(rt, ns or "", name, body, ctype, subresource=sub,
+                                                  manager=q.get("fieldManager", "")))
         if m == "DELETE" and name is not None:
             opts = body or {}
             return self._json(self.state.delete(rt, ns or "", name, preconditions=opts.get("preconditions"),

@@ -164,10 +164,12 @@ class ClusterState:
         self.crds: dict = {}  # (group, plural) -> CRD: writes of those kinds are schema-validated (422)
         self.admission = Admission()  # server-side mutation of write bodies (defaulting/pruning, webhooks)
         self.last_record: EventRecord | None = None  # lets the HTTP layer reuse the event's encoding
-        # server-side apply: the top-level fields, labels and annotations each object's applier set last time
-        # (by uid).  One it applied before and omits now is removed, as a real apiserver does from
-        # managedFields — without this a dropped ConfigMap.binaryData would stay on the object for ever
-        self._applied: dict[str, tuple] = {}
+        # server-side apply: the top-level fields, labels, annotations and ownerReferences (by uid) each field
+        # manager applied last time, per object uid.  What a manager applied before and omits now is removed,
+        # as a real apiserver does from managedFields — without this a dropped ConfigMap.binaryData would stay
+        # on the object for ever.  ownerReferences is a list-map keyed by uid: an entry another manager also
+        # applies stays (it is co-owned)
+        self._applied: dict[str, dict[str, tuple]] = {}
         self.stats = {"create": 0, "update": 0, "status": 0, "delete": 0, "patch": 0, "get": 0, "list": 0,
                       "watch": 0, "conflict": 0, "noop_update": 0, "gc_delete": 0}
 
@@ -405,24 +407,32 @@ class ClusterState:
         return new
 
     def patch(self, rt: ResourceType, ns: str, name: str, body, patch_type: str, *,
-              subresource: str | None = None) -> dict:
+              subresource: str | None = None, manager: str = "") -> dict:
         self.stats["patch"] += 1
         ns = ns if rt.namespaced else ""
         cur = self._bucket(rt, ns).get(name)
         if patch_type == PATCH_APPLY:
             bm = body.get("metadata") or {}
             fields = (frozenset(k for k in body if k not in _APPLY_ALWAYS), frozenset(bm.get("labels") or ()),
-                      frozenset(bm.get("annotations") or ()))
+                      frozenset(bm.get("annotations") or ()),
+                      frozenset(r.get("uid") for r in bm.get("ownerReferences") or () if isinstance(r, dict)))
             if cur is None:
                 body = dict(body)
                 body.setdefault("metadata", {}).setdefault("name", name)
                 out = self.create(rt, ns, body)
-                self._applied[out["metadata"].get("uid", "")] = fields
+                self._applied[out["metadata"].get("uid", "")] = {manager: fields}
                 return out
             new = apply_patch(cur, body)
             uid = cur["metadata"].get("uid", "")
-            prev = self._applied.get(uid)
+            managers = self._applied.setdefault(uid, {})
+            prev = managers.get(manager)
             if prev is not None:
+                gone_refs = {r for r in prev[3] - fields[3]
+                             if not any(r in f[3] for m, f in managers.items() if m != manager)}
+                if gone_refs and new["metadata"].get("ownerReferences"):
+                    new["metadata"] = dict(new["metadata"])
+                    new["metadata"]["ownerReferences"] = [r for r in new["metadata"]["ownerReferences"]
+                                                          if r.get("uid") not in gone_refs]
                 for k in prev[0] - fields[0]:
                     new.pop(k, None)
                 for i, mk in ((1, "labels"), (2, "annotations")):
@@ -434,7 +444,7 @@ class ClusterState:
                             new["metadata"][mk] = kept
                         else:
                             new["metadata"].pop(mk, None)
-            self._applied[uid] = fields
+            managers[manager] = fields
         else:
             if cur is None:
                 raise _not_found(rt, name)

@@ -328,10 +328,25 @@ class Shard:
         return await self._update_dependent(R.CONFIGMAPS, shard_configmap, data, new_owner, field_manager,
                                             binary_data, metadata)
 
-    async def apply_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str) -> dict:
-        """Apply our view of a dependent: owner labels, our ownerRef (merged by uid with other owners'), payload."""
+    async def apply_dependent(self, rt: R.ResourceType, shard_template: dict, src: dict, field_manager: str,
+                              live: dict | None = None) -> dict:
+        """Apply our view of a dependent: owner labels, payload, and the template ownerRefs — those the live
+        shard copy carries, then ours — with the live copy's resourceVersion as a precondition.  Every
+        template's pass applies with the same field manager, and SSA drops an ownerRef entry its manager
+        applied before and omits now: applying only our own would take the other templates' refs off a
+        shared Secret/ConfigMap (and shard GC would delete it with us); applying over a stale view would do
+        the same, hence the precondition (409 on a concurrent change)."""
         body = self._dependent_body(rt, shard_template, src)
         m = body["metadata"]
+        if live is not None:
+            if meta(live).get("resourceVersion"):
+                m["resourceVersion"] = meta(live)["resourceVersion"]
+            ours = m["ownerReferences"][0]
+            refs = [r for r in (meta(live).get("ownerReferences") or ())
+                    if r.get("kind") == C.TEMPLATE_KIND and r.get("uid") != ours.get("uid")]
+            if refs:
+                m["ownerReferences"] = [{"apiVersion": r.get("apiVersion", ours["apiVersion"]), "kind": C.TEMPLATE_KIND,
+                                         "name": r.get("name", ""), "uid": r.get("uid", "")} for r in refs] + [ours]
         return await self._tracked(self._dep_informer(rt), rt, "patch", m["namespace"], m["name"], body,
                                    field_manager, patch_type=PATCH_APPLY, force=True)
 

@@ -568,6 +568,42 @@ async def test_server_side_apply(tmp_path, impl):
             assert writes and {w[0] for w in writes} <= {"PATCH", "DELETE"}, writes
 
 
+async def test_server_side_apply_shared_dependent_keeps_every_owner(tmp_path, impl):
+    """Two templates share a Secret and a ConfigMap under `server-side-apply: true`.  Every pass applies with
+    the same field manager, and a real apiserver drops an ownerRef entry its manager applied before and omits
+    now (the fake tracks applied ownerRefs per manager, as managedFields do): each apply must carry the other
+    template's ref too.  Otherwise the shared copy ends up owned by whichever template applied
+    last, and deleting that template lets shard GC delete the copy the other still uses."""
+    async with Cluster(tmp_path, impl, n_shards=1, server_side_apply=True) as cl:
+        cl.seed(0)
+        cl.seed(1)  # the same s0 / c0
+        await cl.start()
+        await cl.ready()
+        await cl.ready("algo-00001")
+        s = cl.sstates[0]
+
+        def owners(rt, name):
+            return sorted(r["name"] for r in s.get(rt, NS, name)["metadata"]["ownerReferences"])
+        for rt, name in ((R.SECRETS, "s0"), (R.CONFIGMAPS, "c0")):
+            await wait_for(lambda: asyncio.sleep(0, owners(rt, name) == [T0, "algo-00001"]))
+        # new data: both templates' passes re-apply the copies; both refs stay
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o["data"].__setitem__("version", "OTk="))
+        await mutate(cl.cc, R.CONFIGMAPS, "c0", lambda o: o["data"].__setitem__("version", "99"))
+        for rt, name in ((R.SECRETS, "s0"), (R.CONFIGMAPS, "c0")):
+            await wait_for(lambda: asyncio.sleep(0, s.get(rt, NS, name)["data"] == cl.cstate.get(rt, NS, name)["data"]))
+        await asyncio.sleep(0.3)  # every pass the change triggered has applied
+        for rt, name in ((R.SECRETS, "s0"), (R.CONFIGMAPS, "c0")):
+            assert owners(rt, name) == [T0, "algo-00001"], (rt.plural, s.get(rt, NS, name)["metadata"])
+        # the first template goes: its shard copy is deleted, GC strips its ref, the shared copies stay
+        await cl.cc.delete(R.TEMPLATES, NS, T0)
+        await wait_for(lambda: asyncio.sleep(0, s.try_get(R.TEMPLATES, NS, T0) is None))
+        for rt, name in ((R.SECRETS, "s0"), (R.CONFIGMAPS, "c0")):
+            await wait_for(lambda: asyncio.sleep(0, (lambda o: o is not None and [r["name"] for r in o["metadata"][
+                "ownerReferences"]] == ["algo-00001"])(s.try_get(rt, NS, name))))
+        await asyncio.sleep(0.3)
+        assert s.try_get(R.SECRETS, NS, "s0") is not None and s.try_get(R.CONFIGMAPS, NS, "c0") is not None
+
+
 @pytest.mark.parametrize("ssa", [False, True], ids=["put", "apply"])
 async def test_dependent_labels_and_annotations_synced(tmp_path, impl, ssa):
     """`sync-dependent-metadata: true` (the reference copies neither): a shard copy carries
