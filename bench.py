@@ -492,6 +492,14 @@ async def run(args, d: Dist) -> dict | None:
                     k, _, v = kv.partition("=")
                     env[k] = v
                 env["NCC_TOPOLOGY_FILE"] = os.path.join(work, "topology.json")
+                # the ops port: /debug/state after the timed waves (each executor's client flow control, the
+                # coordinator's GC passes); executors report their state every second
+                import socket as _socket
+                with _socket.socket() as _s:
+                    _s.bind(("127.0.0.1", 0))
+                    ops_port = _s.getsockname()[1]
+                env.setdefault("NEXUS__HEALTH_BIND_ADDRESS", f"127.0.0.1:{ops_port}")
+                env.setdefault("NCC_STATUS_S", "1")
                 if args.stages:
                     env["NCC_TRACE_STAGES"] = os.path.join(work, "trace")
                     os.makedirs(env["NCC_TRACE_STAGES"], exist_ok=True)
@@ -580,6 +588,19 @@ async def run(args, d: Dist) -> dict | None:
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
                 with open(os.path.join(work, "topology.json")) as f:
                     ctrl_state["sizing"] = json.load(f)
+            debug = None
+            if d.rank == 0:
+                try:
+                    await asyncio.sleep(1.2)  # one more status message from every executor, after the waves
+                    async with session.get(f"http://{env['NEXUS__HEALTH_BIND_ADDRESS']}/debug/state",
+                                           timeout=aiohttp.ClientTimeout(total=10)) as r:
+                        st = await r.json()
+                    flow = {}
+                    for h in (st.get("executors") or {}).values():
+                        flow.update((h.get("status") or {}).get("flow") or {})
+                    debug = {"executor_flow": flow, "coordinator_gc": st.get("gc")}
+                except Exception as e:  # noqa: BLE001 — diagnostics only
+                    debug = {"error": repr(e)[:200]}
             if d.rank == 0:  # LIST/WATCH load the controller put on its own cluster (watch relay: 1 each per kind)
                 import aiohttp as _aiohttp
                 async with session.get(f"{ctrl_url}/_fake/stats", timeout=_aiohttp.ClientTimeout(total=30)) as r:
@@ -677,6 +698,9 @@ async def run(args, d: Dist) -> dict | None:
                 "controller_to_substrate_split": {k: round(v / substrate, 3) for k, v in us_per_obj.items()}
                 if substrate else None,
                 "host": host,
+                # per shard: the C++ executor's adaptive concurrency limit at the end, the most requests in flight,
+                # 429s and overload signals seen (native/executor/http.hpp); the coordinator's GC passes
+                "controller_state": debug,
                 # kernel-mode share of that CPU (syscalls, the loopback TCP stack) per process
                 "controller_cpu_sys_share": {k: round((sys1.get(k, 0.0) - sys0.get(k, 0.0)) / v, 3)
                                              for k, v in ctl_cpu.items() if v > 0},

@@ -813,14 +813,16 @@ private:
         std::string req = render(method.c_str(), target, body, content_type);
         for (int tries = 0;; ++tries) {
             uint64_t seq = co_await admit();
-            double t0 = now_s();
             std::unique_ptr<Conn> c;
             try {
                 c = co_await acquire();
             } catch (...) {
-                finish(seq, 0, now_s() - t0, false);
+                finish(seq, 0, 0, false);
                 throw;
             }
+            // the server's latency: from the request on an open connection to its response (a connect is not
+            // the apiserver's queue — a SYN retransmitted under an accept storm alone takes a second)
+            double t0 = now_s();
             bool reused = c->reused;
             size_t before = 0;
             c->deadline = now_s() + timeout_;
