@@ -116,6 +116,7 @@ struct Options {
     std::string alias = "controller-cluster";
     int workers = 256;
     int pool_size = 256;
+    int pipeline_depth = 1;  // requests per connection (HTTP/1.1 pipelining); in flight ≤ pool_size × depth
     FlowLimits flow;  // client-side flow control per shard (http.hpp): AIMD limit, client-qps bucket
     double request_timeout = 30;
     double coalesce = 0.002;
@@ -2246,6 +2247,8 @@ static void configure(const Value& c) {
     o.workers = static_cast<int>(num(c, "workers", o.workers));
     o.pool_size = static_cast<int>(num(c, "pool_size", o.pool_size));
     if (const char* ps = std::getenv("NCC_POOL_SIZE")) o.pool_size = std::max(1, std::atoi(ps));  // experiments
+    o.pipeline_depth = std::max(1, static_cast<int>(num(c, "pipeline_depth", o.pipeline_depth)));
+    if (const char* v = std::getenv("NCC_PIPELINE_DEPTH")) o.pipeline_depth = std::max(1, std::atoi(v));  // experiments
     o.flow.qps = num(c, "client_qps", 0);
     o.flow.burst = num(c, "client_burst", 10);
     o.flow.adaptive = num(c, "adaptive_concurrency", 1) != 0;
@@ -2274,7 +2277,8 @@ static void configure(const Value& c) {
         for (const auto& s : shards->a) {
             auto sh = std::make_unique<Shard>();
             sh->name = std::string(s.sget("name"));
-            sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout, o.flow);
+            sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout, o.flow,
+                                                  o.pipeline_depth);
             for (int k = 0; k < 4; ++k) {
                 sh->inf[k].shard = sh.get();
                 sh->inf[k].kind = k;
@@ -2420,10 +2424,11 @@ static void send_status() {
             e.integer(inf.relists);
             e.str(inf.last_error);
         }
-        // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms]
+        // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
+        // connections, write batches, requests]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(8);
+        e.array(11);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2432,6 +2437,9 @@ static void send_status() {
         e.integer(cl.flow.cuts);
         e.integer(cl.flow.gated);
         e.integer(static_cast<long long>(cl.flow.qps_wait_s * 1000));
+        e.integer(cl.connections());
+        e.integer(cl.sends);
+        e.integer(cl.requests);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

@@ -224,7 +224,7 @@ public:
     std::string buf;  // received, not yet consumed
     size_t pos = 0;
     double deadline = 0;  // request deadline (pool sweep shuts the socket down when passed)
-    bool reused = false;
+    bool drained = false;  // the last recv returned less than it asked for: the socket had nothing more
 
     ~Conn() { close(); }
     void close() {
@@ -303,6 +303,8 @@ public:
             pos = 0;
         }
         char tmp[65536];
+        // the socket was drained and no edge came since: wait for one instead of a recv that returns EAGAIN
+        if (ssl == nullptr && drained && fd >= 0 && !loop().readable_now(fd)) co_await loop().readable(fd);
         while (true) {
             if (fd < 0) throw TransportError("connection closed");
             if (ssl != nullptr) {
@@ -325,6 +327,7 @@ public:
                 ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
                 if (r > 0) {
                     buf.append(tmp, static_cast<size_t>(r));
+                    drained = static_cast<size_t>(r) < sizeof tmp;
                     co_return;
                 }
                 if (r == 0) throw TransportError("connection closed by peer");
@@ -492,10 +495,12 @@ struct Response {
 //   * ×`beta` on an overload signal — 429, 503, a request timeout, or a response slower than `latency_s` and
 //     8× the fastest seen — at most once per window (only requests sent after the last cut count);
 //   * never above `cap` (client-pool-size: also the most connections) nor below 1.
-// `qps`/`burst` (client-qps / client-burst) add client-go's token bucket (/root/reference/main.go:52-68
-// leaves it at client-go's default of 5 QPS / burst 10; native mode has none unless configured).
+// `qps`/`burst` (client-qps / client-burst) add client-go's token bucket, one per API group client as
+// client-go has one per clientset — the core group (Secrets, ConfigMaps) and science.sneaksanddata.com
+// (templates, workgroups) — (/root/reference/main.go:52-68 leaves it at client-go's default of 5 QPS /
+// burst 10; native mode has none unless configured).
 struct FlowLimits {
-    int cap = 256;
+    int cap = 256;     // the most requests in flight: connections × pipeline depth
     double initial = 32;
     double beta = 0.7;
     double latency_s = 1.0;
@@ -512,13 +517,15 @@ struct FlowStats {
 // ------------------------------------------------------------------------------------ client
 class Client {
 public:
-    Client(Credentials creds, int pool_size, double request_timeout, FlowLimits fl = FlowLimits())
-        : creds_(std::move(creds)), max_(std::max(1, pool_size)), timeout_(request_timeout), fl_(fl) {
-        fl_.cap = max_;
-        limit_ = fl_.adaptive ? std::clamp(fl_.initial, 1.0, static_cast<double>(max_)) : max_;
-        slow_start_ = fl_.adaptive && limit_ < max_;
-        tokens_ = fl_.burst > 0 ? fl_.burst : 1.0;
-        tokens_at_ = now_s();
+    // `pool_size` keep-alive connections, each carrying up to `depth` pipelined requests
+    Client(Credentials creds, int pool_size, double request_timeout, FlowLimits fl = FlowLimits(), int depth = 1)
+        : creds_(std::move(creds)), max_(std::max(1, pool_size)), depth_(std::max(1, depth)),
+          timeout_(request_timeout), fl_(fl) {
+        fl_.cap = max_ * depth_;
+        limit_ = fl_.adaptive ? std::clamp(fl_.initial, 1.0, static_cast<double>(fl_.cap)) : fl_.cap;
+        slow_start_ = fl_.adaptive && limit_ < fl_.cap;
+        tokens_[0] = tokens_[1] = std::max(fl_.burst, 1.0);
+        tokens_at_[0] = tokens_at_[1] = now_s();
         url_ = parse_url(creds_.server);
         if (url_.tls) ctx_ = make_ssl_ctx(creds_);
         host_ = creds_.tls_server_name.empty()
@@ -530,7 +537,7 @@ public:
     }
     ~Client() {
         closed_ = true;
-        idle_.clear();
+        pipes_.clear();
         if (ctx_ != nullptr) SSL_CTX_free(ctx_);
     }
     void set_token(std::string t) {
@@ -542,6 +549,8 @@ public:
     FlowStats flow;
     double limit() const { return limit_; }
     int inflight() const { return inflight_; }
+    int connections() const { return static_cast<int>(pipes_.size()); }
+    long long sends = 0;  // write batches (requests issued in one loop iteration go out together)
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
     // token once on 401, and re-send once on a fresh connection when a reused keep-alive connection died
@@ -629,6 +638,7 @@ private:
     SSL_CTX* ctx_ = nullptr;
     std::string host_;
     int max_;
+    int depth_;
     double timeout_;
     FlowLimits fl_;
     double limit_ = 1;
@@ -636,17 +646,33 @@ private:
     int inflight_ = 0, woken_ = 0;
     uint64_t sent_seq_ = 0, cut_seq_ = 0;
     double min_latency_ = 1e9;
-    double tokens_ = 0, tokens_at_ = 0;
+    double tokens_[2] = {0, 0}, tokens_at_[2] = {0, 0};  // per API group: core, named groups
     std::deque<std::coroutine_handle<>> gate_;
-    int open_ = 0;
     bool closed_ = false;
     bool sweeping_ = false;  // a sweep() is running
     std::string token_;
     double token_read_at_ = -1e9;
     std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
-    std::vector<std::unique_ptr<Conn>> idle_;
     std::set<Conn*> busy_;
-    std::deque<std::coroutine_handle<>> waiters_;
+
+    // One keep-alive connection carrying up to `depth_` pipelined requests (HTTP/1.1: the server answers in
+    // request order; Go's net/http, i.e. kube-apiserver, serves them one after the other).  Requests issued in
+    // one loop iteration go out in one send; the responses one read brings are parsed without another.
+    struct Waiter {
+        std::coroutine_handle<> h;
+        Response r;
+        double deadline = 0;
+        bool done = false, ok = false, timed_out = false;
+        std::string err;
+    };
+    struct Pipe {
+        Conn c;
+        std::deque<Waiter*> pending;  // written or queued, awaiting their responses in order
+        std::string out;              // rendered requests not yet written
+        bool connected = false, broken = false, flush_posted = false, writing = false, reading = false;
+    };
+    using PipePtr = std::shared_ptr<Pipe>;
+    std::vector<PipePtr> pipes_;
 
     void reload_token(bool force) {
         if (creds_.token_file.empty()) return;
@@ -703,61 +729,136 @@ private:
         return req;
     }
 
-    Task<std::unique_ptr<Conn>> acquire() {
-        while (true) {
-            if (!idle_.empty()) {
-                auto c = std::move(idle_.back());
-                idle_.pop_back();
-                c->reused = true;
-                co_return c;
-            }
-            if (open_ < max_) {
-                ++open_;
-                auto c = std::make_unique<Conn>();
-                try {
-                    co_await c->connect(url_, ctx_, creds_.tls_server_name);
-                } catch (...) {
-                    --open_;
-                    wake_one();
-                    throw;
+    // The connection a request goes on: an idle one; else a new one while fewer than `max_` are open; else the
+    // least loaded one below `depth_` (the admission gate keeps the requests in flight ≤ max_ × depth_).
+    PipePtr pick() {
+        PipePtr best;
+        for (auto& p : pipes_) {
+            if (p->broken || static_cast<int>(p->pending.size()) >= depth_) continue;
+            if (!best || p->pending.size() < best->pending.size()) best = p;
+            if (best->pending.empty()) break;
+        }
+        if ((!best || !best->pending.empty()) && static_cast<int>(pipes_.size()) < max_) {
+            best = std::make_shared<Pipe>();
+            pipes_.push_back(best);
+            spawn(open_pipe(best), "connect");
+        }
+        if (!best)  // cannot happen under the gate; rather one request deeper than none at all
+            for (auto& p : pipes_)
+                if (!p->broken && (!best || p->pending.size() < best->pending.size())) best = p;
+        return best;
+    }
+    Task<void> open_pipe(PipePtr p) {
+        try {
+            co_await p->c.connect(url_, ctx_, creds_.tls_server_name);
+        } catch (const std::exception& e) {
+            break_pipe(p, e.what());
+            co_return;
+        }
+        if (p->broken) co_return;
+        p->connected = true;
+        kick(p);
+    }
+    // Start what a pipe with queued requests needs: a write of everything queued at the end of this loop
+    // iteration, and a reader for the responses.
+    void kick(const PipePtr& p) {
+        if (!p->connected || p->broken) return;
+        if (!p->out.empty() && !p->flush_posted && !p->writing) {
+            p->flush_posted = true;
+            loop().call_soon([this, p] {
+                p->flush_posted = false;
+                if (!p->writing && !p->broken && !p->out.empty()) {
+                    p->writing = true;
+                    spawn(write_pipe(p), "pipe writer");
                 }
-                co_return c;
+            });
+        }
+        if (!p->pending.empty() && !p->reading) {
+            p->reading = true;
+            spawn(read_pipe(p), "pipe reader");
+        }
+    }
+    Task<void> write_pipe(PipePtr p) {
+        while (!p->out.empty() && !p->broken) {
+            std::string data;
+            data.swap(p->out);
+            ++sends;
+            try {
+                co_await p->c.write_all(data);
+            } catch (const std::exception& e) {
+                break_pipe(p, e.what());
             }
-            struct Park {
-                Client* cl;
-                bool await_ready() { return false; }
-                void await_suspend(std::coroutine_handle<> h) { cl->waiters_.push_back(h); }
-                void await_resume() {}
-            };
-            co_await Park{this};
         }
+        p->writing = false;
     }
-    void wake_one() {
-        if (!waiters_.empty()) {
-            loop().post(waiters_.front());
-            waiters_.pop_front();
+    Task<void> read_pipe(PipePtr p) {
+        busy_.insert(&p->c);
+        if (!sweeping_) {
+            sweeping_ = true;
+            spawn(sweep(), "request-deadline sweep");
         }
+        while (!p->pending.empty() && !p->broken) {
+            Waiter* w = p->pending.front();
+            p->c.deadline = w->deadline;  // the sweep aborts the connection when its oldest request is overdue
+            bool close = false;
+            try {
+                Head h = co_await read_head(p->c);
+                w->r.body = co_await read_body(p->c, h);
+                w->r.status = h.status;
+                w->r.retry_after = std::move(h.retry_after);
+                close = h.close;
+            } catch (const std::exception& e) {
+                break_pipe(p, e.what());
+                break;
+            }
+            p->pending.pop_front();
+            w->ok = true;
+            complete(w);
+            if (close) {  // the server closes after this answer: the requests behind it go again, elsewhere
+                break_pipe(p, "connection closed by the server");
+                break;
+            }
+        }
+        busy_.erase(&p->c);
+        p->reading = false;
     }
-    void release(std::unique_ptr<Conn> c, bool reuse) {
-        if (reuse && !closed_ && c->fd >= 0) {
-            idle_.push_back(std::move(c));
-        } else {
-            --open_;
-            c.reset();
+    void complete(Waiter* w) {
+        w->done = true;
+        if (w->h) loop().post(w->h);
+    }
+    // A connection failed: every request on it fails (each re-sent once by `exchange`, unless overdue).
+    void break_pipe(const PipePtr& p, const std::string& err) {
+        if (p->broken) return;
+        p->broken = true;
+        double now = now_s();
+        for (Waiter* w : p->pending) {
+            w->err = err;
+            w->timed_out = now >= w->deadline;
+            complete(w);
         }
-        wake_one();
+        p->pending.clear();
+        p->out.clear();
+        busy_.erase(&p->c);
+        p->c.close();
+        for (size_t i = 0; i < pipes_.size(); ++i)
+            if (pipes_[i] == p) {
+                pipes_[i] = pipes_.back();
+                pipes_.pop_back();
+                break;
+            }
     }
 
     // Wait for a client-qps token and a slot under the concurrency limit; returns the request's sequence
     // number (a cut applies once per window: only to requests sent after the previous cut).
-    Task<uint64_t> admit() {
+    Task<uint64_t> admit(int group) {
         if (fl_.qps > 0) {  // reservation: the token is taken now, the wait is for when it is due
             double now = now_s();
-            tokens_ = std::min(std::max(fl_.burst, 1.0), tokens_ + (now - tokens_at_) * fl_.qps);
-            tokens_at_ = now;
-            tokens_ -= 1.0;
-            if (tokens_ < 0) {
-                double wait = -tokens_ / fl_.qps;
+            double& tokens = tokens_[group];
+            tokens = std::min(std::max(fl_.burst, 1.0), tokens + (now - tokens_at_[group]) * fl_.qps);
+            tokens_at_[group] = now;
+            tokens -= 1.0;
+            if (tokens < 0) {
+                double wait = -tokens / fl_.qps;
                 flow.qps_wait_s += wait;
                 co_await loop().sleep(wait);
             }
@@ -796,8 +897,8 @@ private:
             } else if (status > 0 && status < 500) {
                 min_latency_ = std::min(min_latency_, latency);
                 if (used >= limit_ / 2)
-                    limit_ = std::min(static_cast<double>(max_), limit_ + (slow_start_ ? 1.0 : 1.0 / limit_));
-                if (limit_ >= max_) slow_start_ = false;
+                    limit_ = std::min(static_cast<double>(fl_.cap), limit_ + (slow_start_ ? 1.0 : 1.0 / limit_));
+                if (limit_ >= fl_.cap) slow_start_ = false;
             }
         }
         int room = static_cast<int>(limit_) - inflight_ - woken_;
@@ -811,49 +912,41 @@ private:
     Task<Response> exchange(const std::string& method, const std::string& target, const std::string* body,
                             const char* content_type) {
         std::string req = render(method.c_str(), target, body, content_type);
+        int group = target.rfind("/apis/", 0) == 0 ? 1 : 0;
         for (int tries = 0;; ++tries) {
-            uint64_t seq = co_await admit();
-            std::unique_ptr<Conn> c;
-            try {
-                c = co_await acquire();
-            } catch (...) {
+            uint64_t seq = co_await admit(group);
+            if (closed_) {
                 finish(seq, 0, 0, false);
-                throw;
+                throw TransportError("client closed");
             }
-            // the server's latency: from the request on an open connection to its response (a connect is not
-            // the apiserver's queue — a SYN retransmitted under an accept storm alone takes a second)
+            PipePtr p = pick();
+            Waiter w;
+            // the server's latency: from the request on its connection to the response (a connect is not the
+            // apiserver's queue — a SYN retransmitted under an accept storm alone takes a second)
             double t0 = now_s();
-            bool reused = c->reused;
-            size_t before = 0;
-            c->deadline = now_s() + timeout_;
-            track(c.get());
-            Response r;
-            bool ok = false, keep = false;
-            std::string err;
-            try {
-                co_await c->write_all(req);
-                before = c->buf.size() - c->pos;
-                Head h = co_await read_head(*c);
-                r.body = co_await read_body(*c, h);
-                r.status = h.status;
-                r.retry_after = h.retry_after;
-                keep = !h.close;
-                ok = true;
-            } catch (const TransportError& e) {
-                err = e.what();
-            }
-            busy_.erase(c.get());
-            bool timed_out = !ok && now_s() >= c->deadline;
-            release(std::move(c), ok && keep);
-            finish(seq, ok ? r.status : 0, now_s() - t0, timed_out);
-            if (ok) {
+            w.deadline = t0 + timeout_;
+            p->out += req;
+            p->pending.push_back(&w);
+            kick(p);
+            struct Suspend {
+                Waiter* w;
+                bool await_ready() { return w->done; }
+                void await_suspend(std::coroutine_handle<> h) { w->h = h; }
+                void await_resume() {}
+            };
+            co_await Suspend{&w};
+            finish(seq, w.ok ? w.r.status : 0, now_s() - t0, w.timed_out);
+            if (w.ok) {
                 ++requests;
-                co_return r;
+                co_return std::move(w.r);
             }
             ++request_errors;
-            if (timed_out) throw TransportError(method + " " + target + ": request timed out");
-            if (reused && before == 0 && tries == 0) continue;  // stale keep-alive connection: once more, fresh
-            throw TransportError(method + " " + target + ": " + err);
+            if (w.timed_out) throw TransportError(method + " " + target + ": request timed out");
+            // the connection went away under it (a stale keep-alive connection, or another request on it
+            // failed): once more on another.  Every write here is safe to repeat — a create answers
+            // AlreadyExists, an update with a resourceVersion Conflict, an apply and a delete are idempotent.
+            if (tries == 0) continue;
+            throw TransportError(method + " " + target + ": " + w.err);
         }
     }
 

@@ -196,6 +196,13 @@ public:
     };
     // Await the socket becoming readable/writable after a syscall returned EAGAIN (edge-triggered).
     IoAwait readable(int fd) { return IoAwait{this, fd, false}; }
+    // Has an edge been reported for `fd` since it was last consumed?  (A reader whose last recv drained the
+    // socket can wait for the next edge without first trying a recv that would return EAGAIN: every new
+    // arrival of data raises an edge.)  Unknown descriptors count as readable: the next syscall fails.
+    bool readable_now(int fd) const {
+        auto it = fds_.find(fd);
+        return it == fds_.end() || it->second.readable;
+    }
     IoAwait writable(int fd) { return IoAwait{this, fd, true}; }
 
     struct SleepAwait {

@@ -224,7 +224,7 @@ class App:
         self.per_shard = 1
         qps, burst = client_limits(cfg)
         self.client_factory = client_factory or default_client_factory(qps, burst, cfg.pool_size(),
-                                                                       cfg.transport, cfg.client_pipeline_depth)
+                                                                       cfg.transport, cfg.pipeline_depth())
         self._controller_client = controller_client
         self.metrics = metrics
         self.ops = None
@@ -261,7 +261,7 @@ class App:
         if client is None:
             qps, burst = client_limits(cfg)
             client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.pool_size(),
-                                pipeline_depth=cfg.client_pipeline_depth,
+                                pipeline_depth=cfg.pipeline_depth(),
                                 cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)

@@ -80,9 +80,10 @@ class AppConfig:
     mode: str = "native"
     client_qps: float = 0.0          # 0 = mode default (compat: client-go's 5/10, native: none); < 0 = none
     client_burst: int = 10
-    client_pool_size: int = 0        # connections (= most requests in flight) per cluster; 0 = auto: 64 for
-                                     # the Python clients, 256 for the C++ executor's shard clients
-    client_pipeline_depth: int = 1   # >1: HTTP/1.1-pipeline requests once all pool connections are busy
+    client_pool_size: int = 0        # keep-alive connections per cluster; 0 = auto: 64 for the Python clients,
+                                     # 256 for the C++ executor's shard clients
+    client_pipeline_depth: int = 0   # HTTP/1.1-pipelined requests per connection (in flight ≤ pool × depth);
+                                     # 0 = auto: 1 (no pipelining)
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     sync_dependent_metadata: bool = False  # native mode: shard Secrets/ConfigMaps carry the source's labels
@@ -117,6 +118,10 @@ class AppConfig:
     def pool_size(self) -> int:
         """client-pool-size for the Python transport (0 = its default of 64)."""
         return self.client_pool_size if self.client_pool_size > 0 else 64
+
+    def pipeline_depth(self) -> int:
+        """client-pipeline-depth for the Python transport (0 = its default of 1: no pipelining)."""
+        return self.client_pipeline_depth if self.client_pipeline_depth > 0 else 1
 
     @staticmethod
     def key_of(attr: str) -> str:

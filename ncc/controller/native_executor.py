@@ -28,8 +28,14 @@ from ..shards.loader import discover
 log = logging.getLogger("ncc.executor")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-# connections (and the most requests in flight) per shard when `client-pool-size` is 0 (auto)
+# keep-alive connections per shard, and pipelined requests on each, when `client-pool-size` /
+# `client-pipeline-depth` are 0 (auto): 256 requests in flight at most.  No pipelining by default: an
+# HTTP/1.1 server (kube-apiserver's Go net/http) serves one connection's requests one after the other, so
+# only connections give a shard apiserver requests to run concurrently (APF seats, etcd round trips); and on
+# the bench, 32 connections × 8 coalesced only 1.3 requests per write (BENCHMARKS.md).  Pipelining pays for a
+# far-away shard, where the round trip rather than the apiserver bounds a connection.
 DEFAULT_POOL_SIZE = 256
+DEFAULT_PIPELINE_DEPTH = 1
 _LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "WARN": 30, "ERROR": 40, "CRITICAL": 50}
 
 
@@ -121,13 +127,15 @@ class NativeExecutorConfig:
         shards = [await self.shard_entry(n) for n in handle.shards]
         qps, burst = client_limits(cfg)
         pool = cfg.client_pool_size if cfg.client_pool_size > 0 else DEFAULT_POOL_SIZE
+        depth = cfg.client_pipeline_depth if cfg.client_pipeline_depth > 0 else DEFAULT_PIPELINE_DEPTH
         doc = {
             "namespace": cfg.controller_namespace, "alias": cfg.alias,
             # one C++ process per shard carries all of its concurrency: like client-go's HTTP/2 connection
-            # (up to 250 concurrent streams) up to `pool` requests in flight per shard, under an adaptive
-            # limit (http.hpp `Client`: slow start, AIMD on 429/503/timeouts) and the client-qps bucket
-            "workers": 4 * max(DEFAULT_POOL_SIZE, pool), "pool_size": pool,
-            "client_qps": qps, "client_burst": burst,
+            # (up to 250 concurrent streams) up to pool × depth requests in flight per shard, pipelined on
+            # `pool` keep-alive connections, under an adaptive limit (http.hpp `Client`: slow start, AIMD on
+            # 429/503/timeouts) and the client-qps bucket
+            "workers": 4 * max(DEFAULT_POOL_SIZE * DEFAULT_PIPELINE_DEPTH, pool * depth), "pool_size": pool,
+            "pipeline_depth": depth, "client_qps": qps, "client_burst": burst,
             "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
             "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,
             "rate_limit_qps": o.rate_limit_qps, "rate_limit_burst": o.rate_limit_burst,

@@ -136,5 +136,17 @@ class RateLimitedClient(KubeClient):
         async for ev in self.inner.watch(rt, namespace, **kw):
             yield ev
 
+    def __getattr__(self, name):
+        """The inner client's extensions: raw watch streams (the watch relay's — a token per stream opened,
+        as `watch`), and anything else read-only (`stats`, `supports_line_tap`, ...)."""
+        inner = getattr(self.inner, name)  # AttributeError when the inner client has none (hasattr → False)
+        if name in ("watch_raw", "watch_raw_batches"):
+            async def raw(rt, namespace, **kw):
+                await self.limiter(rt).wait()
+                async for x in inner(rt, namespace, **kw):
+                    yield x
+            return raw
+        return inner
+
     async def close(self):
         await self.inner.close()

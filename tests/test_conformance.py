@@ -568,6 +568,65 @@ async def test_server_side_apply(tmp_path, impl):
             assert writes and {w[0] for w in writes} <= {"PATCH", "DELETE"}, writes
 
 
+@pytest.mark.parametrize("pipelined", [False, True], ids=["keepalive", "pipelined"])
+async def test_client_qps_and_pool_size_are_honoured(tmp_path, impl, pipelined):
+    """`client-qps` / `client-burst` (client-go's token bucket, /root/reference/main.go:52) and
+    `client-pool-size` bound what one shard client sends: with qps 20, burst 5 no one-second window holds more
+    than 25 writes of one API group (client-go has a bucket per clientset: the core group's Secrets/ConfigMaps
+    and the science group's templates), and a pool of 4 never has more than 4 connections open to the shard
+    — also with HTTP/1.1 pipelining (`client-pipeline-depth: 4`), which stacks requests on those 4 instead
+    of opening more.  One executor per shard, so the limits apply to one client."""
+    if impl == "inprocess":
+        pytest.skip("the in-process topology's shard clients are the Python executor's (covered there)")
+    extra = dict(client_qps=20, client_burst=5, client_pool_size=4, executors_per_shard=1)
+    if pipelined:
+        extra["client_pipeline_depth"] = 4
+    async with Cluster(tmp_path, impl, n_shards=1, **extra) as cl:
+        for i in range(15):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        t0 = asyncio.get_running_loop().time()
+        for i in range(15):
+            await wait_for(lambda i=i: asyncio.sleep(0, cl.sstates[0].try_get(R.CONFIGMAPS, NS, f"c{i}")),
+                           timeout=20)
+        took = asyncio.get_running_loop().time() - t0
+        writes = [w for w in cl.env.shard_servers[0].writes if w[0] in ("POST", "PUT", "PATCH")]
+        assert len(writes) >= 45  # 15 templates, Secrets, ConfigMaps
+        for group in (("secrets", "configmaps"), ("nexusalgorithmtemplates",)):
+            times = sorted(w[5] for w in writes if w[1] in group)
+            worst = max(sum(1 for t in times if a <= t < a + 1.0) for a in times)
+            assert worst <= 25, f"{worst} {group} writes in one second at client-qps 20 / burst 5"
+        assert took >= (30 - 25) / 20 * 0.9, took  # the core group's bucket did hold its 30 writes back
+        conns = cl.env.shard_servers[0]._http.conn_stats()
+        assert conns["api_max"] <= 4, conns
+
+
+async def test_pipelined_shard_writes_on_few_connections(tmp_path, impl, monkeypatch):
+    """`client-pipeline-depth: 8` on `client-pool-size: 2`: 40 templates with their Secrets and ConfigMaps go out
+    on two connections, HTTP/1.1-pipelined (the server answers in order); everything converges, and the C++
+    executor's status shows requests coalesced into fewer writes than requests."""
+    if impl == "inprocess":
+        pytest.skip("the shard clients under test are the executors'")
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, impl, n_shards=1, client_pool_size=2, client_pipeline_depth=8,
+                       executors_per_shard=1) as cl:
+        for i in range(40):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        for i in range(40):
+            await cl.ready(f"algo-{i:05d}")
+        conns = cl.env.shard_servers[0]._http.conn_stats()
+        assert conns["api_max"] <= 2, conns
+        if impl == "native":
+            async def flow():
+                ex = cl.app.debug_state()["executors"]
+                fl = [h["status"]["flow"]["shard-0"] for h in ex.values() if (h.get("status") or {}).get("flow")]
+                return fl and fl[0]["requests"] >= 120 and fl[0]
+            fl = await wait_for(flow)
+            assert fl["connections"] <= 2 and fl["max_inflight"] > 2, fl
+            assert fl["write_batches"] < fl["requests"], fl
+
+
 async def test_server_side_apply_shared_dependent_keeps_every_owner(tmp_path, impl):
     """Two templates share a Secret and a ConfigMap under `server-side-apply: true`.  Every pass applies with
     the same field manager, and a real apiserver drops an ownerRef entry its manager applied before and omits
