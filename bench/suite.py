@@ -129,6 +129,13 @@ class Topology:
                     "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
         env.update(MODE_ENV[self.mode])
         env["NEXUS__WORKERS"] = str(self.workers or (64 if self.mode == "native" else 2))
+        # the ops port, for /debug/state (each C++ executor's client flow control); status every second
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            self.ops = f"127.0.0.1:{sk.getsockname()[1]}"
+        env["NEXUS__HEALTH_BIND_ADDRESS"] = self.ops
+        env.setdefault("NCC_STATUS_S", "1")
         env.update(self.extra_env)
         if self.stages:
             env["NCC_TRACE_STAGES"] = os.path.join(self.work, "trace")
@@ -139,6 +146,19 @@ class Topology:
                                            stderr=subprocess.STDOUT, cwd=self.work)
         self.procs.append(self.controller)
         return t
+
+    async def executor_flow(self) -> dict:
+        """{shard: the C++ executor's client flow-control state} from the coordinator's /debug/state."""
+        try:
+            await asyncio.sleep(1.2)  # a status message from every executor after what was measured
+            async with self.session.get(f"http://{self.ops}/debug/state") as r:
+                st = await r.json()
+        except Exception as e:  # noqa: BLE001 — diagnostics only
+            return {"error": repr(e)[:200]}
+        out = {}
+        for h in (st.get("executors") or {}).values():
+            out.update((h.get("status") or {}).get("flow") or {})
+        return out
 
     async def shard_writes(self) -> int:
         """Writes (create/update/patch, incl. no-op updates) the shard apiservers have served so far."""
@@ -478,7 +498,7 @@ async def config6_admission(mode, T, timeout, aimd=True, admission=None):
             shard_writes_per_s={"min": round(min(rates), 1), "mean": round(sum(rates) / 8, 1)},
             bound_writes_per_s=round(bound, 1),
             of_bound={"min": round(min(rates) / bound, 3), "mean": round(sum(rates) / 8 / bound, 3)},
-            per_shard_flow=flows)
+            per_shard_flow=flows, executor_flow=await topo.executor_flow())
         return out
     finally:
         await topo.stop()

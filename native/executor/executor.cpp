@@ -2425,10 +2425,10 @@ static void send_status() {
             e.str(inf.last_error);
         }
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
-        // connections, write batches, requests]
+        // connections, write batches, requests, slow starts left on rising latency]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(11);
+        e.array(12);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2440,6 +2440,7 @@ static void send_status() {
         e.integer(cl.connections());
         e.integer(cl.sends);
         e.integer(cl.requests);
+        e.integer(cl.flow.hystart);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

@@ -490,7 +490,10 @@ struct Response {
 // (max-in-flight, API Priority and Fairness seats with bounded queues) and answers the rest 429 +
 // Retry-After; it also serves kubelets, the scheduler and the GPU operator.  Instead of a fixed number of
 // requests in flight, the client keeps an adaptive limit (AIMD, as TCP's congestion window):
-//   * slow start from `initial`: +1 per success (doubling per round trip) until the first overload signal;
+//   * slow start from `initial`: +1 per success (doubling per round trip) until the first overload signal,
+//     or until responses come back slower than 2× the fastest of their kind plus 2 ms (HyStart: the server
+//     has started to queue them — leave before the queue overflows into 429s, each of which costs a
+//     Retry-After);
 //   * then +1/limit per success (one per window of `limit` requests) while at least half the limit is used;
 //   * ×`beta` on an overload signal — 429, 503, a request timeout, or a response slower than `latency_s` and
 //     8× the fastest seen — at most once per window (only requests sent after the last cut count);
@@ -510,6 +513,7 @@ struct FlowLimits {
 
 struct FlowStats {
     long long overloads = 0, cuts = 0, gated = 0, rejected = 0;  // rejected: 429 answers
+    long long hystart = 0;  // slow starts left on rising latency
     int max_inflight = 0;
     double qps_wait_s = 0;
 };
@@ -646,6 +650,7 @@ private:
     int inflight_ = 0, woken_ = 0;
     uint64_t sent_seq_ = 0, cut_seq_ = 0;
     double min_latency_ = 1e9;
+    double min_class_[2] = {1e9, 1e9};  // the fastest read / write seen
     double tokens_[2] = {0, 0}, tokens_at_[2] = {0, 0};  // per API group: core, named groups
     std::deque<std::coroutine_handle<>> gate_;
     bool closed_ = false;
@@ -880,7 +885,8 @@ private:
         co_return ++sent_seq_;
     }
     // A request admitted as `seq` finished: `status` (0: transport failure), after `latency` seconds.
-    void finish(uint64_t seq, int status, double latency, bool timed_out) {
+    // `cls`: 0 reads, 1 writes (their latencies differ: a write waits for etcd).
+    void finish(uint64_t seq, int status, double latency, bool timed_out, int cls = 1) {
         int used = inflight_--;
         if (status == 429) ++flow.rejected;
         if (fl_.adaptive) {
@@ -896,6 +902,12 @@ private:
                 }
             } else if (status > 0 && status < 500) {
                 min_latency_ = std::min(min_latency_, latency);
+                double& floor = min_class_[cls];
+                floor = std::min(floor, latency);
+                if (slow_start_ && latency > 2 * floor + 0.002) {
+                    slow_start_ = false;  // queueing began: additive increase from here
+                    ++flow.hystart;
+                }
                 if (used >= limit_ / 2)
                     limit_ = std::min(static_cast<double>(fl_.cap), limit_ + (slow_start_ ? 1.0 : 1.0 / limit_));
                 if (limit_ >= fl_.cap) slow_start_ = false;
@@ -935,7 +947,7 @@ private:
                 void await_resume() {}
             };
             co_await Suspend{&w};
-            finish(seq, w.ok ? w.r.status : 0, now_s() - t0, w.timed_out);
+            finish(seq, w.ok ? w.r.status : 0, now_s() - t0, w.timed_out, method == "GET" ? 0 : 1);
             if (w.ok) {
                 ++requests;
                 co_return std::move(w.r);

@@ -20,6 +20,10 @@ knobs set (`POST /_fake/faults`) it behaves like such a server:
 Watches are long-running requests and, as on a real apiserver, exempt.  `stats()` counts what was
 admitted, queued and rejected, and per wall-clock second how many requests arrived and how many were
 rejected (bench/suite.py computes the 429 share after the first second of a cold start from it).
+
+The model is callback-driven (no task or coroutine per request: `FakeApiServer.fast` hands the HTTP layer a
+`Deferred` answered from a timer), so the substrate's own CPU does not become the bound the benchmark
+compares the client against.
 """
 from __future__ import annotations
 
@@ -34,7 +38,7 @@ class FlowControl:
     def __init__(self):
         self.executing = 0
         self.mutating = 0  # admitted mutating requests, queued or executing
-        self._queue: deque = deque()  # futures of requests waiting for a seat, FIFO
+        self._queue: deque = deque()  # [granted callback, mutating, t_enqueued, live] of requests waiting for a seat
         self.counters = {"admitted": 0, "queued": 0, "rejected": 0, "rejected_inflight": 0,
                          "rejected_queue_full": 0, "rejected_queue_wait": 0, "max_executing": 0,
                          "max_queued": 0, "max_mutating": 0, "wait_max_s": 0.0}
@@ -44,76 +48,86 @@ class FlowControl:
     def active(f) -> bool:
         return bool(f.apf_seats or f.max_mutating_inflight or f.service_ms or f.read_service_ms)
 
-    def _reject(self, why: str) -> E.ApiError:
-        self.counters["rejected"] += 1
-        self.counters["rejected_" + why] += 1
-        self.by_second[self._sec][1] += 1
-        return E.TooManyRequests("too many requests, please try again later", retry_after=1)
-
-    async def admit(self, f, mutating: bool) -> E.ApiError | None:
-        """Hold a seat for one request (None), or the 429 to answer it with."""
-        sec = self._sec = int(time.time())
+    def _slot(self) -> list:
+        sec = int(time.time())
         slot = self.by_second.get(sec)
         if slot is None:
             slot = self.by_second[sec] = [0, 0]
             if len(self.by_second) > 3600:
                 for k in sorted(self.by_second)[:1800]:
                     del self.by_second[k]
-        slot[0] += 1
+        return slot
+
+    def _reject(self, why: str) -> E.ApiError:
+        self.counters["rejected"] += 1
+        self.counters["rejected_" + why] += 1
+        self._slot()[1] += 1
+        return E.TooManyRequests("too many requests, please try again later", retry_after=1)
+
+    def _granted(self, mutating: bool, queued: bool) -> None:
         c = self.counters
+        c["admitted"] += 1
+        c["max_executing"] = max(c["max_executing"], self.executing)
+        c["max_mutating"] = max(c["max_mutating"], self.mutating)
+
+    def admit(self, f, mutating: bool, granted) -> E.ApiError | None:
+        """Admit one request: the 429 to answer it with, or None — then `granted()` is called once it holds a
+        seat (at once, or when one frees up)."""
+        self._slot()[0] += 1
         if mutating and f.max_mutating_inflight and self.mutating >= f.max_mutating_inflight:
             return self._reject("inflight")
         if f.apf_seats and (self.executing >= f.apf_seats or self._queue):
             if len(self._queue) >= max(0, int(f.apf_queue)):
                 return self._reject("queue_full")
-            fut = asyncio.get_running_loop().create_future()
-            self._queue.append(fut)
+            entry = [granted, mutating, time.monotonic(), True]
+            self._queue.append(entry)
+            c = self.counters
             c["queued"] += 1
             c["max_queued"] = max(c["max_queued"], len(self._queue))
             if mutating:
                 self.mutating += 1
-            t0 = time.monotonic()
-            try:
-                await asyncio.wait_for(asyncio.shield(fut), f.apf_queue_wait_s)
-            except asyncio.TimeoutError:
-                if fut.done() and not fut.cancelled():  # the seat came as the wait ran out: give it back
-                    self._seat_freed()
-                else:
-                    fut.cancel()
-                if mutating:
-                    self.mutating -= 1
-                self._sec = int(time.time())
-                self.by_second.setdefault(self._sec, [0, 0])
-                return self._reject("queue_wait")
-            c["wait_max_s"] = max(c["wait_max_s"], round(time.monotonic() - t0, 4))
-            # the releasing request handed its seat over (`executing` already counts it)
-        else:
-            self.executing += 1
-            if mutating:
-                self.mutating += 1
-        c["admitted"] += 1
-        c["max_executing"] = max(c["max_executing"], self.executing)
-        c["max_mutating"] = max(c["max_mutating"], self.mutating)
+            asyncio.get_running_loop().call_later(f.apf_queue_wait_s, self._expire, entry)
+            return None
+        self.executing += 1
+        if mutating:
+            self.mutating += 1
+        self._granted(mutating, False)
+        granted()
         return None
 
+    def _expire(self, entry: list) -> None:
+        """A queued request's wait ran out: take it out of the queue and answer 429."""
+        if not entry[3]:
+            return  # it got its seat
+        entry[3] = False
+        try:
+            self._queue.remove(entry)
+        except ValueError:
+            pass
+        if entry[1]:
+            self.mutating -= 1
+        entry[0](self._reject("queue_wait"))
+
     def release(self, mutating: bool) -> None:
+        """An admitted request finished: its seat passes to the longest waiter."""
         if mutating:
             self.mutating -= 1
-        self._seat_freed()
-
-    def _seat_freed(self) -> None:
         while self._queue:
-            fut = self._queue.popleft()
-            if not fut.done():
-                fut.set_result(None)  # the seat passes to the longest waiter
-                return
+            entry = self._queue.popleft()
+            if not entry[3]:
+                continue
+            entry[3] = False
+            c = self.counters
+            c["wait_max_s"] = max(c["wait_max_s"], round(time.monotonic() - entry[2], 4))
+            self._granted(entry[1], True)
+            entry[0]()
+            return
         self.executing -= 1
 
-    async def hold(self, f, mutating: bool) -> None:
+    @staticmethod
+    def service_s(f, mutating: bool) -> float:
         """The seat holding time of an admitted request (etcd's commit latency stand-in)."""
-        ms = f.service_ms if mutating else f.read_service_ms
-        if ms > 0:
-            await asyncio.sleep(ms / 1000.0)
+        return (f.service_ms if mutating else f.read_service_ms) / 1000.0
 
     def stats(self) -> dict:
         return dict(self.counters, executing=self.executing, waiting=len(self._queue), mutating=self.mutating,

@@ -92,6 +92,24 @@ class Response:
         return ("\r\n".join(h) + "\r\n\r\n").encode() + self.body
 
 
+class Deferred:
+    """A response `fast` handlers answer later, from a callback (no task): the connection waits for it."""
+    __slots__ = ("response", "_cb")
+
+    def __init__(self):
+        self.response = None
+        self._cb = None
+
+    def resolve(self, response: Response) -> None:
+        self.response = response
+        cb, self._cb = self._cb, None
+        if cb is not None:
+            cb(response)
+
+    def then(self, cb) -> None:
+        self._cb = cb
+
+
 def json_response(obj, status: int = 200) -> Response:
     return Response(status=status, body=json.dumps(obj, separators=(",", ":")).encode())
 
@@ -203,6 +221,12 @@ class _ServerConn(asyncio.Protocol):
                     resp = fast(req)
                 except Exception as e:  # noqa: BLE001
                     resp = Response(500, text=f"internal error: {e}")
+                if isinstance(resp, Deferred):
+                    if resp.response is None:  # answered later from a callback: wait for it, in order
+                        self.busy = True
+                        resp.then(lambda r, k=keep: self._deferred_done(r, k))
+                        return
+                    resp = resp.response
                 if resp is not None:  # answered synchronously: no task, keep parsing pipelined requests
                     self.transport.write(resp.encode())
                     if not keep:
@@ -213,6 +237,17 @@ class _ServerConn(asyncio.Protocol):
             task = asyncio.ensure_future(self.server.handler(req))
             task.add_done_callback(lambda t, k=keep: self._done(t, k))
             return
+
+    def _deferred_done(self, resp: Response, keep: bool) -> None:
+        self.busy = False
+        if self.closed:
+            return
+        self.transport.write(resp.encode())
+        if not keep:
+            self.transport.close()
+            return
+        if self.buf:
+            self._next()
 
     def _done(self, task: asyncio.Task, keep: bool):
         self.busy = False

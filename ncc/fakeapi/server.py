@@ -214,12 +214,46 @@ class FakeApiServer:
         if request.path.startswith("/_fake/"):
             return None
         f = self.faults
-        if f.latency_ms or f.jitter_ms or FlowControl.active(f):
+        if f.latency_ms or f.jitter_ms:
             return None
         if request.method == "GET" and "watch=" in request.raw_query:
             return None
         self.requests["total"] += 1
+        if FlowControl.active(f) and not f.down and request.path.startswith(("/api/", "/apis/")):
+            return self._admitted(request)
         return self._core(request)
+
+    def _admitted(self, request: web.Request):
+        """Serve a request through the admission model (flowcontrol.py): a 429 at once, or a Deferred answered
+        once it held a seat for its service time."""
+        f = self.faults
+        mutating = request.method in ("POST", "PUT", "PATCH", "DELETE")
+        d = web.Deferred()
+
+        def run():
+            try:
+                resp = self._core(request)
+            except Exception as e:  # noqa: BLE001
+                resp = web.Response(500, text=f"internal error: {e}")
+            finally:
+                self.flow.release(mutating)
+            d.resolve(resp)
+
+        def granted(err=None):
+            if err is not None:  # its wait for a seat ran out
+                self.requests["throttled"] += 1
+                d.resolve(_status_response(err))
+                return
+            delay = FlowControl.service_s(f, mutating)
+            if delay > 0:
+                asyncio.get_running_loop().call_later(delay, run)
+            else:
+                run()
+        err = self.flow.admit(f, mutating, granted)
+        if err is not None:
+            self.requests["throttled"] += 1
+            return _status_response(err)
+        return d
 
     async def _dispatch(self, request: web.Request) -> web.StreamResponse:
         self.requests["total"] += 1
@@ -232,16 +266,14 @@ class FakeApiServer:
             await asyncio.sleep((f.latency_ms + random.random() * f.jitter_ms) / 1000.0)
         if api and FlowControl.active(f) and not f.down and \
                 not (request.method == "GET" and "watch=" in request.raw_query):
-            mutating = request.method in ("POST", "PUT", "PATCH", "DELETE")
-            err = await self.flow.admit(f, mutating)
-            if err is not None:
-                self.requests["throttled"] += 1
-                return _status_response(err)
-            try:
-                await self.flow.hold(f, mutating)
-                return self._core(request)
-            finally:
-                self.flow.release(mutating)
+            d = self._admitted(request)
+            if not isinstance(d, web.Deferred):
+                return d
+            if d.response is None:
+                fut = asyncio.get_running_loop().create_future()
+                d.then(fut.set_result)
+                return await fut
+            return d.response
         r = self._core(request)
         if isinstance(r, tuple):  # a watch
             return await self._watch(request, r[1], r[2])
