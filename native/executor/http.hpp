@@ -340,8 +340,26 @@ public:
         }
     }
 
-    Task<void> write_all(const std::string& data) {
+    // Send what the socket takes now, without suspending (plain TCP; TLS goes through write_all): the bytes
+    // written, or -1 when the connection failed.  The common case — a request that fits the socket buffer — then
+    // costs no coroutine frame.
+    ssize_t try_send(const char* p, size_t n) {
+        if (fd < 0 || ssl != nullptr) return 0;
         size_t off = 0;
+        while (off < n) {
+            ssize_t r = ::send(fd, p + off, n - off, MSG_NOSIGNAL);
+            if (r > 0) {
+                off += static_cast<size_t>(r);
+                continue;
+            }
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+            return -1;
+        }
+        return static_cast<ssize_t>(off);
+    }
+
+    Task<void> write_all(const std::string& data, size_t off = 0) {
         while (off < data.size()) {
             if (fd < 0) throw TransportError("connection closed");
             if (ssl != nullptr) {
@@ -414,6 +432,61 @@ inline std::string header_value(std::string_view line, size_t name_len) {
     return std::string(v);
 }
 
+struct Response {
+    int status = 0;
+    std::string body;
+    std::string retry_after;
+};
+
+// A response already complete in the connection's buffer, parsed in place (no coroutine, no per-line
+// strings): the usual case, as an apiserver's answer arrives in one read.  NEED_MORE: read more first;
+// SLOW: chunked or without a length — the coroutine readers below take it from the start.
+enum class Parsed { DONE, NEED_MORE, SLOW };
+inline Parsed parse_buffered(Conn& c, Response& r, bool& close) {
+    const std::string& b = c.buf;
+    size_t hend = b.find("\r\n\r\n", c.pos);
+    if (hend == std::string::npos) return Parsed::NEED_MORE;
+    std::string_view head(b.data() + c.pos, hend - c.pos);
+    size_t eol = head.find("\r\n");
+    std::string_view status_line = head.substr(0, eol);
+    if (status_line.substr(0, 7) != "HTTP/1." || status_line.size() < 12) throw TransportError("malformed status line");
+    int status = 0;
+    for (size_t i = 9; i < 12; ++i) status = status * 10 + (status_line[i] - '0');
+    bool http10 = status_line.substr(0, 8) == "HTTP/1.0";
+    long long length = -1;
+    bool chunked = false, conn_close = http10;
+    std::string retry_after;
+    while (eol != std::string_view::npos) {
+        size_t next = head.find("\r\n", eol + 2);
+        std::string_view line = head.substr(eol + 2, next == std::string_view::npos ? std::string_view::npos : next - eol - 2);
+        eol = next;
+        if (ieq_prefix(line, "content-length")) {
+            length = std::atoll(header_value(line, 14).c_str());
+        } else if (ieq_prefix(line, "transfer-encoding")) {
+            chunked = true;  // chunked (or another coding): the slow path
+        } else if (ieq_prefix(line, "connection")) {
+            std::string v = header_value(line, 10);
+            std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+            if (v == "close") conn_close = true;
+        } else if (ieq_prefix(line, "retry-after")) {
+            retry_after = header_value(line, 11);
+        }
+    }
+    if (chunked) return Parsed::SLOW;
+    if (length < 0) {
+        if (status != 204 && status != 304) return Parsed::SLOW;
+        length = 0;
+    }
+    size_t body_at = hend + 4;
+    if (b.size() - body_at < static_cast<size_t>(length)) return Parsed::NEED_MORE;
+    r.status = status;
+    r.body.assign(b, body_at, static_cast<size_t>(length));
+    r.retry_after = std::move(retry_after);
+    close = conn_close;
+    c.pos = body_at + static_cast<size_t>(length);
+    return Parsed::DONE;
+}
+
 inline Task<Head> read_head(Conn& c) {
     Head h;
     std::string status_line = co_await c.read_line();
@@ -480,11 +553,6 @@ inline Task<std::string> read_body(Conn& c, const Head& h) {
     co_return body;
 }
 
-struct Response {
-    int status = 0;
-    std::string body;
-    std::string retry_after;
-};
 
 // Client-side flow control of one shard apiserver.  A real apiserver admits a bounded number of requests
 // (max-in-flight, API Priority and Fairness seats with bounded queues) and answers the rest 429 +
@@ -542,6 +610,7 @@ public:
     ~Client() {
         closed_ = true;
         pipes_.clear();
+        idle_.clear();
         if (ctx_ != nullptr) SSL_CTX_free(ctx_);
     }
     void set_token(std::string t) {
@@ -553,7 +622,7 @@ public:
     FlowStats flow;
     double limit() const { return limit_; }
     int inflight() const { return inflight_; }
-    int connections() const { return static_cast<int>(pipes_.size()); }
+    int connections() const { return depth_ > 1 ? static_cast<int>(pipes_.size()) : open_; }
     long long sends = 0;  // write batches (requests issued in one loop iteration go out together)
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
@@ -563,8 +632,14 @@ public:
                            const char* content_type = "application/json") {
         int attempt = 0;
         bool refreshed = false;
+        int group = target.rfind("/apis/", 0) == 0 ? 1 : 0;
         while (true) {
-            Response r = co_await exchange(method, target, body, content_type);
+            std::string req = render(method.c_str(), target, body, content_type);
+            Response r;  // (no co_await inside a conditional expression: GCC 11 mishandles its temporaries)
+            if (depth_ == 1)
+                r = co_await exchange_direct(method, target, req, group);
+            else
+                r = co_await exchange(method, target, req, group);
             if (r.status == 401 && !creds_.token_file.empty() && !refreshed) {
                 refreshed = true;
                 reload_token(true);
@@ -654,6 +729,9 @@ private:
     double tokens_[2] = {0, 0}, tokens_at_[2] = {0, 0};  // per API group: core, named groups
     std::deque<std::coroutine_handle<>> gate_;
     bool closed_ = false;
+    int open_ = 0;                                 // connections of the direct path (depth 1)
+    std::vector<std::unique_ptr<Conn>> idle_;      // its idle keep-alive connections
+    std::deque<std::coroutine_handle<>> waiters_;  // requests waiting for one of them
     bool sweeping_ = false;  // a sweep() is running
     std::string token_;
     double token_read_at_ = -1e9;
@@ -807,11 +885,19 @@ private:
             p->c.deadline = w->deadline;  // the sweep aborts the connection when its oldest request is overdue
             bool close = false;
             try {
-                Head h = co_await read_head(p->c);
-                w->r.body = co_await read_body(p->c, h);
-                w->r.status = h.status;
-                w->r.retry_after = std::move(h.retry_after);
-                close = h.close;
+                while (true) {
+                    Parsed st = parse_buffered(p->c, w->r, close);
+                    if (st == Parsed::DONE) break;
+                    if (st == Parsed::SLOW) {
+                        Head h = co_await read_head(p->c);
+                        w->r.body = co_await read_body(p->c, h);
+                        w->r.status = h.status;
+                        w->r.retry_after = std::move(h.retry_after);
+                        close = h.close;
+                        break;
+                    }
+                    co_await p->c.fill();
+                }
             } catch (const std::exception& e) {
                 break_pipe(p, e.what());
                 break;
@@ -855,6 +941,22 @@ private:
 
     // Wait for a client-qps token and a slot under the concurrency limit; returns the request's sequence
     // number (a cut applies once per window: only to requests sent after the previous cut).
+    // admit() without suspending, when a token and a slot are there now (and nobody waits before us)
+    bool try_admit(int group, uint64_t& seq) {
+        if (!gate_.empty() || inflight_ >= static_cast<int>(limit_)) return false;
+        if (fl_.qps > 0) {
+            double now = now_s();
+            double& tokens = tokens_[group];
+            double t = std::min(std::max(fl_.burst, 1.0), tokens + (now - tokens_at_[group]) * fl_.qps);
+            if (t < 1.0) return false;
+            tokens = t - 1.0;
+            tokens_at_[group] = now;
+        }
+        ++inflight_;
+        flow.max_inflight = std::max(flow.max_inflight, inflight_);
+        seq = ++sent_seq_;
+        return true;
+    }
     Task<uint64_t> admit(int group) {
         if (fl_.qps > 0) {  // reservation: the token is taken now, the wait is for when it is due
             double now = now_s();
@@ -921,12 +1023,125 @@ private:
         }
     }
 
-    Task<Response> exchange(const std::string& method, const std::string& target, const std::string* body,
-                            const char* content_type) {
-        std::string req = render(method.c_str(), target, body, content_type);
-        int group = target.rfind("/apis/", 0) == 0 ? 1 : 0;
+    // ---- depth 1: one request per connection at a time, written and read by the requesting coroutine
+    Task<std::unique_ptr<Conn>> acquire() {
+        while (true) {
+            if (!idle_.empty()) {
+                auto c = std::move(idle_.back());
+                idle_.pop_back();
+                co_return c;
+            }
+            if (open_ < max_) {
+                ++open_;
+                auto c = std::make_unique<Conn>();
+                try {
+                    co_await c->connect(url_, ctx_, creds_.tls_server_name);
+                } catch (...) {
+                    --open_;
+                    wake_one();
+                    throw;
+                }
+                co_return c;
+            }
+            struct Park {
+                Client* cl;
+                bool await_ready() { return false; }
+                void await_suspend(std::coroutine_handle<> h) { cl->waiters_.push_back(h); }
+                void await_resume() {}
+            };
+            co_await Park{this};
+        }
+    }
+    void wake_one() {
+        if (!waiters_.empty()) {
+            loop().post(waiters_.front());
+            waiters_.pop_front();
+        }
+    }
+    void release(std::unique_ptr<Conn> c, bool reuse) {
+        if (reuse && !closed_ && c->fd >= 0) {
+            idle_.push_back(std::move(c));
+        } else {
+            --open_;
+            c.reset();
+        }
+        wake_one();
+    }
+    Task<Response> exchange_direct(const std::string& method, const std::string& target, const std::string& req,
+                                   int group) {
         for (int tries = 0;; ++tries) {
-            uint64_t seq = co_await admit(group);
+            uint64_t seq;
+            if (!try_admit(group, seq)) seq = co_await admit(group);
+            std::unique_ptr<Conn> c;
+            if (!idle_.empty()) {
+                c = std::move(idle_.back());
+                idle_.pop_back();
+            } else {
+                try {
+                    c = co_await acquire();
+                } catch (...) {
+                    finish(seq, 0, 0, false);
+                    throw;
+                }
+            }
+            // the server's latency: from the request on an open connection to its response (a connect is not
+            // the apiserver's queue — a SYN retransmitted under an accept storm alone takes a second)
+            double t0 = now_s();
+            c->deadline = t0 + timeout_;
+            track(c.get());
+            Response r;
+            bool ok = false, keep = false, got = false;
+            std::string err;
+            try {
+                ++sends;
+                ssize_t n = c->try_send(req.data(), req.size());
+                if (n < 0) throw TransportError(std::string("send: ") + std::strerror(errno));
+                if (static_cast<size_t>(n) < req.size()) co_await c->write_all(req, static_cast<size_t>(n));
+                bool close = false;
+                while (true) {
+                    Parsed st = parse_buffered(*c, r, close);
+                    if (st == Parsed::DONE) break;
+                    if (st == Parsed::SLOW) {
+                        Head h = co_await read_head(*c);
+                        got = true;
+                        r.body = co_await read_body(*c, h);
+                        r.status = h.status;
+                        r.retry_after = std::move(h.retry_after);
+                        close = h.close;
+                        break;
+                    }
+                    if (c->buf.size() > c->pos) got = true;  // part of the answer is here
+                    co_await c->fill();
+                }
+                got = true;
+                keep = !close;
+                ok = true;
+            } catch (const TransportError& e) {
+                err = e.what();
+            }
+            busy_.erase(c.get());
+            bool timed_out = !ok && now_s() >= c->deadline;
+            release(std::move(c), ok && keep);
+            finish(seq, ok ? r.status : 0, now_s() - t0, timed_out, method == "GET" ? 0 : 1);
+            if (ok) {
+                ++requests;
+                co_return r;
+            }
+            ++request_errors;
+            if (timed_out) throw TransportError(method + " " + target + ": request timed out");
+            // a stale keep-alive connection (or one that broke before the answer began): once more, fresh —
+            // every write here is safe to repeat (see exchange)
+            if (!got && tries == 0) continue;
+            throw TransportError(method + " " + target + ": " + err);
+        }
+    }
+
+    // ---- depth > 1: pipelined on shared connections (Pipe)
+    Task<Response> exchange(const std::string& method, const std::string& target, const std::string& req,
+                            int group) {
+        for (int tries = 0;; ++tries) {
+            uint64_t seq;
+            if (!try_admit(group, seq)) seq = co_await admit(group);
             if (closed_) {
                 finish(seq, 0, 0, false);
                 throw TransportError("client closed");
