@@ -1007,6 +1007,7 @@ struct Shard {
 };
 
 static double kDependentHold = 5.0;  // NCC_DEPENDENT_HOLD overrides
+static constexpr double kMaxReportSkip = 0.25;  // a key skips reports of superseded passes for at most this long
 
 
 // NCC_TRACE_STAGES=<dir>: wall-clock times of every relayed controller object received ("r", kind) and of
@@ -1127,6 +1128,7 @@ struct Executor {
     std::vector<CtlPtr> partial_snapshot[4];          // chunks of a listing still arriving (per kind)
     long long stats_reconciles = 0, stats_errors = 0, stats_writes = 0, stats_reports_skipped = 0;
     std::unordered_set<std::string> carry_wrote;  // keys whose unreported (superseded) pass wrote
+    std::unordered_map<std::string, double> skipping_since;  // keys whose reports are being skipped: since when
 
     CtlPtr cget(int k, const std::string& key) const {
         auto it = ctl[k].find(key);
@@ -2095,6 +2097,7 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
     std::string key = key_of(ns, name);
     CtlPtr obj = ex.cget(kind, key);
     if (!obj) {
+        ex.skipping_since.erase(std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key);
         if (kind == TEMPLATES || g_opt.propagate_workgroup_deletes) co_await propagate_delete(kind, ns, name);
         co_return;
     }
@@ -2119,13 +2122,20 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
     if (ex.queue.dirty(qkey)) {
         // a newer version (or a dependent) re-queued the key while this pass ran: the next pass reports on
         // the version it sees, carrying this pass's writes — a report on a version the coordinator may already
-        // have moved past would only cost it a fold and a superseded finish
-        if (pass.wrote) ex.carry_wrote.insert(qkey);
-        ++ex.stats_reports_skipped;
-        for (auto& e : errs)
-            if (e) std::rethrow_exception(e);
-        co_return;
+        // have moved past would only cost it a fold and a superseded finish.  Not for ever, though: under a
+        // steady stream of events every pass would be superseded and the status never advance, so a key
+        // reports at least every kMaxReportSkip seconds
+        double now = now_s();
+        auto [it, fresh] = ex.skipping_since.try_emplace(qkey, now);
+        if (fresh || now - it->second < kMaxReportSkip) {
+            if (pass.wrote) ex.carry_wrote.insert(qkey);
+            ++ex.stats_reports_skipped;
+            for (auto& e : errs)
+                if (e) std::rethrow_exception(e);
+            co_return;
+        }
     }
+    ex.skipping_since.erase(qkey);
     if (ex.carry_wrote.erase(qkey) > 0) pass.wrote = true;
     std::vector<std::pair<std::string, std::optional<Failure>>> results;
     bool failed = false;

@@ -7,6 +7,8 @@
 #                                                        flags or KEY=VAL environment for the controller
 #   bash scripts/box/run.sh <out> ab <n> "<A>" "<B>"     A/B in alternation, n pairs; A and B are
 #                                                        space-separated KEY=VAL lists ("-" = none)
+#   bash scripts/box/run.sh <out> abtree <n> <dir>       this tree against another built tree (<dir>, e.g. an
+#                                                        `abtree_*` copy shipped with the call), n pairs
 #   bash scripts/box/run.sh <out> suite [suite.py args]  the five BASELINE.json configurations
 #   bash scripts/box/run.sh <out> prof                   rocprofv3 --kernel-trace --stats over a short bench,
 #                                                        and the C++ executor's own sampling profile
@@ -64,6 +66,13 @@ case "$what" in
       bench_once "$out/a_$i" $a || exit $?
       # shellcheck disable=SC2086
       bench_once "$out/b_$i" $b || exit $?
+    done
+    ;;
+  abtree)
+    n=$1; other=$2
+    for i in $(seq 1 "$n"); do
+      bench_once "$out/head_$i" || exit $?
+      (cd "$other" && bench_once "$OLDPWD/$out/other_$i") || exit $?
     done
     ;;
   suite)

@@ -15,6 +15,7 @@ missing references refused; AlreadyExists/Conflict races resolved by re-reading;
 shard watch that expired (410) relisted.
 """
 import asyncio
+import base64
 import copy as copy_mod
 import os
 
@@ -625,6 +626,63 @@ async def test_pipelined_shard_writes_on_few_connections(tmp_path, impl, monkeyp
             fl = await wait_for(flow)
             assert fl["connections"] <= 2 and fl["max_inflight"] > 2, fl
             assert fl["write_batches"] < fl["requests"], fl
+
+
+async def test_rejected_template_update_does_not_hold_back_dependents(tmp_path, impl):
+    """A deliberate native-mode deviation (documented in README "Modes"): once the shard template
+    exists its UID is known, so a spec update goes out alongside the Secret/ConfigMap writes instead of before
+    them (the reference's loop is strictly sequential, /root/reference/controller.go:790-831: a failed
+    UpdateTemplate stops the pass before any dependent is written).  When the shard refuses the template
+    update (422), the new dependent data is on the shard all the same, and the status reports the template's
+    failure — Ready=False naming shard and reason — until the update goes through."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        cl.rules(0, [{"method": "PUT", "resource": "nexusalgorithmtemplates", "code": 422, "reason": "Invalid",
+                      "count": -1}])
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o["data"].__setitem__("version", "djc="))
+        await mutate(cl.cc, R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("versionTag", "v7"))
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.SECRETS, NS, "s0")["data"]["version"] == "djc="))
+        await cl.not_ready(T0, "shard-0", "Invalid")
+        assert cl.sstates[0].get(R.TEMPLATES, NS, T0)["spec"]["container"]["versionTag"] != "v7"
+        cl.rules(0, [])
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.TEMPLATES, NS, T0)["spec"]["container"]
+                                             ["versionTag"] == "v7"))
+        await cl.ready()
+
+
+async def test_status_advances_under_a_steady_stream_of_dependent_events(tmp_path, impl):
+    """A pass superseded by an event that arrived while it ran may skip its report (the next pass reports,
+    carrying its writes) — but not for ever: with a Secret changing every few milliseconds every
+    pass is superseded, and the template's Ready condition must still move from False to True once the
+    shard stops failing, while the stream goes on."""
+    async with Cluster(tmp_path, impl, n_shards=1) as cl:
+        cl.seed()
+        cl.rules(0, [{"method": m, "resource": "nexusalgorithmtemplates", "code": 500, "count": -1}
+                     for m in ("POST", "PUT", "PATCH")])
+        await cl.start()
+        await cl.not_ready(T0, "shard-0")
+        # every shard round trip now takes 100 ms, so each pass outlasts the gap between two Secret events
+        cl.env.shard_servers[0].faults.update({"latency_ms": 100})
+        stop = asyncio.Event()
+
+        async def stream():
+            k = 0
+            while not stop.is_set():
+                k += 1
+                await mutate(cl.cc, R.SECRETS, "s0", lambda o, k=k: o["data"].__setitem__(
+                    "tick", base64.b64encode(str(k).encode()).decode()))
+                await asyncio.sleep(0.003)
+        task = asyncio.ensure_future(stream())
+        try:
+            await asyncio.sleep(0.3)
+            cl.rules(0, [])
+            await cl.ready()  # while the Secret keeps changing
+            assert not task.done()
+        finally:
+            stop.set()
+            await task
 
 
 async def test_server_side_apply_shared_dependent_keeps_every_owner(tmp_path, impl):
