@@ -2435,10 +2435,10 @@ static void send_status() {
             e.str(inf.last_error);
         }
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
-        // connections, write batches, requests, slow starts left on rising latency]
+        // connections, write batches, requests, slow starts left on rising latency, increases held back]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(12);
+        e.array(13);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2451,6 +2451,7 @@ static void send_status() {
         e.integer(cl.sends);
         e.integer(cl.requests);
         e.integer(cl.flow.hystart);
+        e.integer(cl.flow.held);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

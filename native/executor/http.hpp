@@ -562,7 +562,11 @@ inline Task<std::string> read_body(Conn& c, const Head& h) {
 //     or until responses come back slower than 2× the fastest of their kind plus 2 ms (HyStart: the server
 //     has started to queue them — leave before the queue overflows into 429s, each of which costs a
 //     Retry-After);
-//   * then +1/limit per success (one per window of `limit` requests) while at least half the limit is used;
+//   * then +1/limit per success (one per window of `limit` requests) while at least half the limit is used
+//     and responses come back within 1.5× the fastest of their kind plus 1 ms; slower ones hold the limit
+//     (TCP Vegas' idea: the server queues them — more in flight would only lengthen its queue until it
+//     overflows into 429s, each costing a Retry-After).  The fastest is remembered per 30 s window, so a
+//     lasting change of round trip moves it;
 //   * ×`beta` on an overload signal — 429, 503, a request timeout, or a response slower than `latency_s` and
 //     8× the fastest seen — at most once per window (only requests sent after the last cut count);
 //   * never above `cap` (client-pool-size: also the most connections) nor below 1.
@@ -582,6 +586,7 @@ struct FlowLimits {
 struct FlowStats {
     long long overloads = 0, cuts = 0, gated = 0, rejected = 0;  // rejected: 429 answers
     long long hystart = 0;  // slow starts left on rising latency
+    long long held = 0;     // successes that did not raise the limit: their response was queued
     int max_inflight = 0;
     double qps_wait_s = 0;
 };
@@ -725,7 +730,9 @@ private:
     int inflight_ = 0, woken_ = 0;
     uint64_t sent_seq_ = 0, cut_seq_ = 0;
     double min_latency_ = 1e9;
-    double min_class_[2] = {1e9, 1e9};  // the fastest read / write seen
+    double min_class_[2] = {1e9, 1e9};  // the fastest read / write seen (this window and the last)
+    double min_window_[2] = {1e9, 1e9};  // ... this window
+    double min_window_at_ = 0;
     double tokens_[2] = {0, 0}, tokens_at_[2] = {0, 0};  // per API group: core, named groups
     std::deque<std::coroutine_handle<>> gate_;
     bool closed_ = false;
@@ -1004,13 +1011,24 @@ private:
                 }
             } else if (status > 0 && status < 500) {
                 min_latency_ = std::min(min_latency_, latency);
+                double now = now_s();
+                if (now - min_window_at_ > 30.0) {  // a new window: the last one's fastest carries over
+                    for (int k = 0; k < 2; ++k) {
+                        min_class_[k] = min_window_[k];
+                        min_window_[k] = 1e9;
+                    }
+                    min_window_at_ = now;
+                }
+                min_window_[cls] = std::min(min_window_[cls], latency);
                 double& floor = min_class_[cls];
                 floor = std::min(floor, latency);
                 if (slow_start_ && latency > 2 * floor + 0.002) {
                     slow_start_ = false;  // queueing began: additive increase from here
                     ++flow.hystart;
                 }
-                if (used >= limit_ / 2)
+                bool queued = !slow_start_ && latency > 1.5 * floor + 0.001;
+                if (queued) ++flow.held;
+                if (used >= limit_ / 2 && !queued)
                     limit_ = std::min(static_cast<double>(fl_.cap), limit_ + (slow_start_ ? 1.0 : 1.0 / limit_));
                 if (limit_ >= fl_.cap) slow_start_ = false;
             }
