@@ -10,6 +10,8 @@
 #   bash scripts/box/run.sh <out> abtree <n> <dir>       this tree against another built tree (<dir>, e.g. an
 #                                                        `abtree_*` copy shipped with the call), n pairs
 #   bash scripts/box/run.sh <out> suite [suite.py args]  the five BASELINE.json configurations
+#   bash scripts/box/run.sh <out> sweep [N...]           shards N (default 1 2 4; CPU ranks over gloo, torchrun) ×
+#                                                        injected shard latency 0/5/20 ms, then 8 shards on one rank
 #   bash scripts/box/run.sh <out> prof                   rocprofv3 --kernel-trace --stats over a short bench,
 #                                                        and the C++ executor's own sampling profile
 #
@@ -74,6 +76,25 @@ case "$what" in
       bench_once "$out/head_$i" || exit $?
       (cd "$other" && bench_once "$OLDPWD/$out/other_$i") || exit $?
     done
+    ;;
+  sweep)
+    ns=${*:-1 2 4}
+    port=29710
+    for n in $ns; do
+      for lat in 0 5 20; do
+        port=$((port + 1))
+        f="$out/n${n}_lat${lat}"
+        if [ "$n" = 1 ]; then
+          bench_once "$f" --shard-latency-ms "$lat" || exit $?
+        else
+          timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+            --master-port "$port" bench.py --gpus "$n" --steps 20 --warmup 5 --shard-latency-ms "$lat" \
+            > "$f.json" 2> "$f.err" || exit $?
+          summary "$f.json"
+        fi
+      done
+    done
+    bench_once "$out/s8" --shards-per-rank 8 || exit $?
     ;;
   suite)
     timeout -k 10 900 python3 bench/suite.py --modes native --out "$out/suite.json" "$@" > "$out/suite.log" 2>&1 \
