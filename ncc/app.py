@@ -733,6 +733,8 @@ def main(argv=None) -> int:
     if args.check_shards:
         from .preflight import run as preflight
         return preflight(cfg)
+    from . import sampler
+    sampler.start("coordinator" + os.environ.get("NCC_COORDINATOR_PART", "").replace("/", "of"))
     prof_path = os.environ.get("NCC_PROFILE")
     if prof_path:  # host-side profiling of the control loop: NCC_PROFILE=/path/out.prof
         import cProfile

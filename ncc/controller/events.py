@@ -161,7 +161,7 @@ class BroadcastRecorder(EventRecorder):
     def event(self, obj, event_type, reason, message, kind=None):
         self.stats["recorded"] += 1
         ref = involved_object(obj, kind)
-        if self.log_events:
+        if self.log_events and log.isEnabledFor(logging.INFO):
             log.info("Event occurred", extra={"object": f"{ref['namespace']}/{ref['name']}", "kind": ref["kind"],
                                               "type": event_type, "reason": reason, "message": message})
         now = time.monotonic()

@@ -557,6 +557,8 @@ def main(argv=None) -> int:
     cfg = load_config()
     configure_logging(cfg.log_level, cfg.log_format)
     logging.getLogger().handlers[0].addFilter(lambda r: setattr(r, "executor", a.index) or True)
+    from .. import sampler
+    sampler.start(f"executor{a.index}")
     prof_path = os.environ.get("NCC_PROFILE")
     if prof_path:
         import cProfile

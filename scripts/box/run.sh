@@ -12,6 +12,7 @@
 #   bash scripts/box/run.sh <out> suite [suite.py args]  the five BASELINE.json configurations
 #   bash scripts/box/run.sh <out> sweep [N...]           shards N (default 1 2 4; CPU ranks over gloo, torchrun) ×
 #                                                        injected shard latency 0/5/20 ms, then 8 shards on one rank
+#   bash scripts/box/run.sh <out> sample [steps]         sampling profiles of the C++ executor and the coordinator
 #   bash scripts/box/run.sh <out> prof                   rocprofv3 --kernel-trace --stats over a short bench,
 #                                                        and the C++ executor's own sampling profile
 #
@@ -100,6 +101,13 @@ case "$what" in
     timeout -k 10 900 python3 bench/suite.py --modes native --out "$out/suite.json" "$@" > "$out/suite.log" 2>&1 \
       || { tail -30 "$out/suite.log"; exit 1; }
     cut -c 1-300 "$out/suite.log" | tail -14
+    ;;
+  sample)  # the C++ executor's and the coordinator's sampling profiles over a long driver-shape run
+    NCC_SAMPLE_PROFILE="$PWD/$out/samples" NCC_SAMPLE_US=200 NCC_PY_SAMPLE="$PWD/$out/py" NCC_PY_SAMPLE_US=200 \
+      timeout -k 10 600 python3 bench.py --steps "${1:-100}" --warmup 5 > "$out/sampled_bench.json" \
+      2> "$out/sampled_bench.err" || exit $?
+    python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
+    summary "$out/sampled_bench.json"
     ;;
   prof)
     export TMPDIR=/tmp
