@@ -22,6 +22,8 @@
 //    bitmask of its owners' partitions, so the partition test itself builds no Python strings.
 //  * parse_response_head(bytes) / parse_request_head(bytes) — HTTP/1.1 heads for the client transport
 //    and the fake apiserver.
+//  * relay_index(lines, raw, ns) — the one-partition watch relay's index-and-forward loop.
+//  * chunk_lines(bytearray, state, bytearray) — a chunked watch body cut into its event lines in one call.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
 //  * dumps(obj) — compact JSON encoder for request bodies and the fake apiserver's responses.
@@ -54,7 +56,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 17
+#define NCC_NATIVE_ABI 19
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -713,6 +715,39 @@ py::object relay_scan(py::bytes line, int parts, const std::string& default_ns) 
                           static_cast<long long>(owners.size()));
 }
 
+// relay_index(lines, raw, default_ns) -> the lines to forward.  The one-partition relay's whole loop in one
+// call: each ADDED/MODIFIED line is stored in `raw` under (namespace, name), a DELETED one removes its key,
+// and every object event is forwarded; BOOKMARK/ERROR and unreadable lines are dropped (the coordinator's
+// informer handles those).  Same result as relay_scan per line (ncc/controller/relay.py `on_lines`).
+py::list relay_index(py::list lines, py::dict raw, const std::string& default_ns) {
+    py::list keep;
+    PyObject* rd = raw.ptr();
+    const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
+        char* buf = nullptr;
+        Py_ssize_t len = 0;
+        if (PyBytes_AsStringAndSize(line, &buf, &len) != 0) throw py::error_already_set();
+        std::string_view type, ns, name, rv;
+        Scanner sc(buf, static_cast<size_t>(len));
+        if (!sc.scan(type, ns, name, rv)) continue;
+        int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
+        if (code == 3) continue;
+        std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
+        py::tuple key = py::make_tuple(py::str(kns.data(), kns.size()), py::str(name.data(), name.size()));
+        if (code == 2) {
+            if (PyDict_DelItem(rd, key.ptr()) != 0) {
+                if (!PyErr_ExceptionMatches(PyExc_KeyError)) throw py::error_already_set();
+                PyErr_Clear();
+            }
+        } else if (PyDict_SetItem(rd, key.ptr(), line) != 0) {
+            throw py::error_already_set();
+        }
+        if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
+    }
+    return keep;
+}
+
 py::int_ key_partition(const std::string& ns, const std::string& name, int parts) {
     if (parts < 1) throw py::value_error("key_partition: parts must be >= 1");
     return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));
@@ -787,6 +822,104 @@ py::object parse_response_head(py::bytes head) {
         }
     }
     return py::make_tuple(status, clen, chunked, close, retry);
+}
+
+// chunk_lines(buf, state, linebuf) -> (lines, state, consumed, done, linebuf)
+// Walks the chunked-transfer body bytes in `buf` (a bytearray; the caller deletes the `consumed` prefix) and
+// returns the complete non-empty newline-terminated lines they carry, a chunk's data taken as it arrives,
+// not once the whole chunk is in.  `state`: -1 a chunk-size line is next, -2 trailer lines after the last
+// chunk, -3 the CRLF after a chunk's data, n > 0 data bytes left in the current chunk.  `linebuf` holds the
+// start of an unfinished line between calls; `done` once the blank line ending the trailers was read.
+// Same lines as ncc/kube/transport.py's Python path (`_parse_chunks` + `_feed_stream`).
+py::object chunk_lines(py::object buf_o, long long state, py::object linebuf_o) {
+    PyObject* b = buf_o.ptr();
+    PyObject* lb = linebuf_o.ptr();
+    if (!PyByteArray_Check(b) || !PyByteArray_Check(lb)) throw py::type_error("chunk_lines: bytearray expected");
+    const char* p = PyByteArray_AS_STRING(b);
+    const size_t n = static_cast<size_t>(PyByteArray_GET_SIZE(b));
+    std::string cur(PyByteArray_AS_STRING(lb), static_cast<size_t>(PyByteArray_GET_SIZE(lb)));
+    PyObject* lines = PyList_New(0);
+    if (lines == nullptr) throw py::error_already_set();
+    py::object lines_o = py::reinterpret_steal<py::object>(lines);
+    auto push = [&](const char* d, size_t len) {
+        PyObject* line = PyBytes_FromStringAndSize(d, static_cast<Py_ssize_t>(len));
+        if (line == nullptr || PyList_Append(lines, line) != 0) {
+            Py_XDECREF(line);
+            throw py::error_already_set();
+        }
+        Py_DECREF(line);
+    };
+    auto data = [&](const char* d, size_t len) {
+        size_t s0 = 0;
+        while (s0 < len) {
+            const char* nl = static_cast<const char*>(std::memchr(d + s0, '\n', len - s0));
+            if (nl == nullptr) {
+                cur.append(d + s0, len - s0);
+                return;
+            }
+            size_t e = static_cast<size_t>(nl - d);
+            if (cur.empty()) {
+                if (e > s0) push(d + s0, e - s0);
+            } else {
+                cur.append(d + s0, e - s0);
+                push(cur.data(), cur.size());
+                cur.clear();
+            }
+            s0 = e + 1;
+        }
+    };
+    auto crlf = [&](size_t from) -> size_t {
+        for (size_t i = from; i + 1 < n; ++i) {
+            const char* q = static_cast<const char*>(std::memchr(p + i, '\r', n - 1 - i));
+            if (q == nullptr) return std::string::npos;
+            i = static_cast<size_t>(q - p);
+            if (p[i + 1] == '\n') return i;
+        }
+        return std::string::npos;
+    };
+    size_t pos = 0;
+    bool done = false;
+    while (pos < n && !done) {
+        if (state == -1) {
+            size_t e = crlf(pos);
+            if (e == std::string::npos) break;
+            std::string_view line(p + pos, e - pos);
+            size_t semi = line.find(';');
+            std::string_view hex = trim(line.substr(0, semi));
+            if (hex.empty()) throw py::value_error("bad chunk size line");
+            long long size = 0;
+            for (char ch : hex) {
+                int v = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10
+                      : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+                if (v < 0) throw py::value_error("bad chunk size line");
+                size = size * 16 + v;
+                if (size > (1LL << 40)) throw py::value_error("chunk too large");
+            }
+            pos = e + 2;
+            state = size > 0 ? size : -2;
+        } else if (state == -2) {
+            size_t e = crlf(pos);
+            if (e == std::string::npos) break;
+            done = e == pos;
+            pos = e + 2;
+        } else if (state == -3) {
+            if (n - pos < 2) break;
+            if (p[pos] != '\r' || p[pos + 1] != '\n') throw py::value_error("chunk data not followed by CRLF");
+            pos += 2;
+            state = -1;
+        } else if (state > 0) {
+            size_t take = std::min(static_cast<size_t>(state), n - pos);
+            data(p + pos, take);
+            pos += take;
+            state -= static_cast<long long>(take);
+            if (state == 0) state = -3;
+        } else {
+            throw py::value_error("bad chunk state");
+        }
+    }
+    PyObject* rest = PyByteArray_FromStringAndSize(cur.data(), static_cast<Py_ssize_t>(cur.size()));
+    if (rest == nullptr) throw py::error_already_set();
+    return py::make_tuple(lines_o, state, pos, done, py::reinterpret_steal<py::object>(rest));
 }
 
 // parse_request_head(head) -> (method, target, {lower-cased header name: value}) of an HTTP/1.1 request
@@ -1439,6 +1572,7 @@ class PyJson {
         }
         ++p_;
         PyObject* env = nullptr;
+        uint64_t env_fp = 0;
         bool ok = true;
         if (!peek('}')) {
             for (;;) {
@@ -1452,8 +1586,13 @@ class PyJson {
                             if (!raw_key(k2)) { ok = false; break; }
                             if (k2 == "mappedEnvironmentVariables") {
                                 Py_XDECREF(env);
+                                ws();
+                                const char* e0 = p_;
                                 env = mapped_env();
                                 if (env == nullptr) { ok = false; break; }
+                                Hasher he;
+                                he.bytes(e0, static_cast<size_t>(p_ - e0));
+                                env_fp = he.digest();
                             } else if (!skip_value()) {
                                 ok = false;
                                 break;
@@ -1488,6 +1627,11 @@ class PyJson {
             Py_XDECREF(rt);
         }
         if (built) built = PyDict_SetItemString(spec, "_fp", fp) == 0;
+        if (built) {  // a digest of the references' text: the coordinator compares it instead of the list
+            PyObject* rfp = PyLong_FromUnsignedLongLong(env_fp);
+            built = rfp != nullptr && PyDict_SetItemString(spec, "_rfp", rfp) == 0;
+            Py_XDECREF(rfp);
+        }
         Py_XDECREF(env);
         Py_XDECREF(fp);
         if (!built) {
@@ -1512,6 +1656,22 @@ class PyJson {
                 v = slim_spec();
             } else if (key == "metadata" && peek('{')) {
                 v = object(1, "managedFields");
+            } else if (key == "status") {
+                // and a digest of the status text under "__ncc_sfp__": an unchanged status compares as one int
+                ws();
+                const char* s0 = p_;
+                v = value(1);
+                if (v != nullptr) {
+                    Hasher hs;
+                    hs.bytes(s0, static_cast<size_t>(p_ - s0));
+                    PyObject* sfp = PyLong_FromUnsignedLongLong(hs.digest());
+                    if (sfp == nullptr || PyDict_SetItemString(d, "__ncc_sfp__", sfp) != 0) {
+                        Py_XDECREF(sfp);
+                        Py_DECREF(v);
+                        break;
+                    }
+                    Py_DECREF(sfp);
+                }
             } else {
                 v = value(1);
             }
@@ -2032,10 +2192,14 @@ PYBIND11_MODULE(_native, m) {
           "scan_event_owners plus the key partition and the owner-partition bitmask (crc32 % parts)");
     m.def("parse_response_head", &parse_response_head, py::arg("head"),
           "(status, content_length|-1, chunked, connection_close, retry_after|None) of an HTTP/1.1 response head");
+    m.def("chunk_lines", &chunk_lines, py::arg("buf"), py::arg("state"), py::arg("linebuf"),
+          "complete event lines of a chunked watch body (see the comment at the definition)");
     m.def("parse_request_head", &parse_request_head, py::arg("head"),
           "(method, target, {lower-cased name: value}) of an HTTP/1.1 request head");
     m.def("relay_scan", &relay_scan, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
           "(type_code, namespace, name, key_partition, owner_partition_mask, n_owners) of a watch line");
+    m.def("relay_index", &relay_index, py::arg("lines"), py::arg("raw"), py::arg("default_ns"),
+          "the one-partition relay loop: index the lines in `raw`, return the object events to forward");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
           "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");

@@ -18,6 +18,7 @@ import json
 from .. import native as _native
 
 SLIM_FP = "__ncc_fp__"  # key under which slim-cache transforms store content digests
+SLIM_STATUS_FP = "__ncc_sfp__"  # a slim template's digest of its status text (_native.template_event_slim)
 # On a slim object published from our own write whose stored payload differs from what we sent (the
 # server defaulted, pruned or a webhook mutated it): the digests of what we sent.  That version counts as
 # in sync for exactly that intent; any later version (a new watch event, a relist) replaces the object

@@ -102,6 +102,7 @@ class Informer:
         # the write's own echo — the common case — or applied if it is someone else's newer version.
         self._inflight: dict = {}
         self._stash: dict = {}
+        self._owner_sigs: dict = {}  # key -> (cached object, owner names, owner uids): the metadata-only filter
         # set by the owner when the apiserver answers its other requests again (ncc/shards/shard.py): a
         # list/watch waiting out an outage backoff retries at once, once per outage
         self.answering: asyncio.Event | None = None
@@ -303,6 +304,7 @@ class Informer:
         store = self.store
         default_ns = self.namespace or ""
         inflight, stash = self._inflight, self._stash
+        sigs = self._owner_sigs
         for line in lines:
             sc = None
             if nparts:
@@ -327,13 +329,22 @@ class Informer:
                 if sc is None:
                     sc = scan(line)
                 if sc is not None and sc[0] == "MODIFIED":
-                    cur = store.get(sc[1] or default_ns, sc[2])
-                    refs = None if cur is None else ((cur.get("metadata") or {}).get("ownerReferences") or ())
-                    if refs is not None and tuple(r.get("name", "") for r in refs) == sc[4] and \
-                            tuple(r.get("uid", "") for r in refs) == sc[5]:
-                        rv = self.last_rv = sc[3]
-                        self.filtered += 1
-                        continue
+                    k2 = (sc[1] or default_ns, sc[2])
+                    cur = store.get(*k2)
+                    if cur is not None:
+                        # the owners of the cached version, as the scan reports them, kept per key while that
+                        # version stays cached (a metadata-only store changes only on an owner change)
+                        sig = sigs.get(k2)
+                        if sig is None or sig[0] is not cur:
+                            if len(sigs) > len(store._items) + 4096:
+                                sigs.clear()
+                            refs = (cur.get("metadata") or {}).get("ownerReferences") or ()
+                            sig = sigs[k2] = (cur, tuple(r.get("name", "") for r in refs),
+                                              tuple(r.get("uid", "") for r in refs))
+                        if sig[1] == sc[4] and sig[2] == sc[5]:
+                            rv = self.last_rv = sc[3]
+                            self.filtered += 1
+                            continue
             if store._assumed or inflight:
                 if sc is None:
                     sc = scan(line)

@@ -20,7 +20,7 @@ import time
 from ..api import constants as C
 from ..api import resources as R
 from ..api.constants import go_quote as q
-from ..api.fingerprint import SLIM_FP, SLIM_WROTE, fingerprint
+from ..api.fingerprint import SLIM_FP, SLIM_STATUS_FP, SLIM_WROTE, fingerprint
 from ..api.objects import meta, normalize_data, now_rfc3339, with_fields
 from ..api.refs import (configmap_names, dependent_names, is_owned_by_uid, ready_condition, same_references,
                         secret_names, template_owner_ref)
@@ -494,9 +494,14 @@ class ReconcileMixin:
         # status, the references and the shard list: a new template version (the next wave) with an equal
         # status and equal references reuses the last verdict (two C-level compares instead of the rebuild).
         shards = self.all_shard_names
-        refs = ((template.get("spec") or {}).get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
+        spec = template.get("spec") or {}
+        sfp, rfp = template.get(SLIM_STATUS_FP), spec.get("_rfp")
+        if sfp is not None and rfp is not None:  # a slim template: digests of the status and reference texts
+            status_id, refs = sfp, rfp
+        else:
+            status_id, refs = status, (spec.get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
         memo = self._inline_status_ok.get(key)
-        if memo is None or memo[2] is not shards or memo[0] != status or memo[1] != refs:
+        if memo is None or memo[2] is not shards or memo[0] != status_id or memo[1] != refs:
             secrets, configmaps = dependent_names(template)
             c0 = conds[0]
             if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE,
@@ -504,7 +509,7 @@ class ReconcileMixin:
                     or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
                     or status.get("syncedToClusters") != shards:
                 return False
-            self._inline_status_ok[key] = (status, refs, shards)
+            self._inline_status_ok[key] = (status_id, refs, shards)
         self.stats["reconciles"] += 1
         self.stats["inline_finishes"] += 1
         self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())  # a reconcile, done in place

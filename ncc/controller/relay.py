@@ -244,16 +244,8 @@ class WatchRelay:
                 if sc is not None and sc[0] < 2:
                     self.trace.append((kind, sc[1], sc[2], now))
         if parts <= 1:
-            keep = []
-            for line in lines:
-                sc = scan(line, 1, ns)
-                if sc is None or sc[0] == 3:
-                    continue  # BOOKMARK / ERROR: the coordinator's informer handles those
-                if sc[0] == 2:
-                    raw.pop((sc[1], sc[2]), None)
-                else:
-                    raw[(sc[1], sc[2])] = line
-                keep.append(line)
+            # index + forward in one native call; BOOKMARK / ERROR: the coordinator's informer handles those
+            keep = mod.relay_index(lines if type(lines) is list else list(lines), raw, ns)
             if keep:
                 self._send_all(handles, {"t": "w", "k": kind, "l": keep})
                 self.stats["lines_out"] += len(keep) * len(handles)

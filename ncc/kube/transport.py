@@ -32,6 +32,7 @@ _CRLF2 = b"\r\n\r\n"
 
 _native_mod = _native.load()
 _parse_native = getattr(_native_mod, "parse_response_head", None) if _native_mod is not None else None
+_chunk_lines = getattr(_native_mod, "chunk_lines", None) if _native_mod is not None else None
 _NO_HEADERS: dict = {}
 
 
@@ -214,6 +215,16 @@ class _Conn(asyncio.Protocol):
     def _parse_chunks(self) -> bool:
         """Consume complete chunks; True once the terminating chunk (and trailers) were read."""
         buf = self.buf
+        if self.stream is not None and _chunk_lines is not None:
+            # a watch body: every complete line of what arrived, cut in one native pass (data taken before
+            # its chunk is complete; chunk_left may then also be -3, the CRLF after a chunk's data)
+            lines, self.chunk_left, used, done, self.linebuf = _chunk_lines(buf, self.chunk_left, self.linebuf)
+            del buf[:used]
+            if lines:
+                self._emit(lines)
+            if done:
+                self._finish()
+            return done
         while True:
             if self.chunk_left == -1:  # expecting a chunk-size line
                 i = buf.find(b"\r\n")
@@ -250,7 +261,11 @@ class _Conn(asyncio.Protocol):
         tail = parts.pop()
         self.linebuf = bytearray(tail)
         lines = [bytes(p) for p in parts if p]
-        if self.line_tap is not None and lines:
+        if lines:
+            self._emit(lines)
+
+    def _emit(self, lines: list) -> None:
+        if self.line_tap is not None:
             self._tap(lines)
         self.stream.extend(lines)
         self.stream_event.set()

@@ -337,3 +337,84 @@ async def test_write_meta_fast_path_errors_and_retries():
     finally:
         await c.close()
         await srv.stop()
+
+
+def _python_stream_lines(body: bytes, cuts: list[int]) -> tuple[list, bool]:
+    """The Python chunked-stream path (`_parse_chunks` + `_feed_stream`) fed `body` in the given pieces."""
+    from ncc.kube import transport as T
+    saved, T._chunk_lines = T._chunk_lines, None
+    try:
+        return _stream_lines(body, cuts)
+    finally:
+        T._chunk_lines = saved
+
+
+def _stream_lines(body: bytes, cuts: list[int]) -> tuple[list, bool]:
+    from collections import deque
+    from ncc.kube.transport import _Conn
+
+    class _Pool:
+        pipeline_depth = 1
+
+    c = _Conn(_Pool())
+    c.stream, c.stream_event, c.head_done, c.chunked = deque(), asyncio.Event(), True, True
+    done = False
+    prev = 0
+    for cut in sorted(set(cuts)) + [len(body)]:
+        c.buf += body[prev:cut]
+        prev = cut
+        done = c._parse_chunks() or done
+        if done:
+            break
+    return list(c.stream), done
+
+
+def test_native_chunk_lines_match_the_python_path():
+    """The native splitter yields the same lines, in any split of the bytes, as the Python path, and the
+    same end-of-body verdict; malformed chunk framing raises ValueError."""
+    from hypothesis import given, settings, strategies as st
+    from ncc import native
+    from ncc.kube import transport as T
+    native.load(required=True)
+    assert T._chunk_lines is not None
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(st.binary(min_size=1, max_size=40), max_size=8), st.lists(st.integers(0, 400), max_size=6),
+           st.booleans())
+    def check(pieces, cuts, ext):
+        body = b"".join(b"%x%s\r\n%s\r\n" % (len(p), b";x=1" if ext else b"", p) for p in pieces) + b"0\r\nT: v\r\n\r\n"
+        cuts = [c for c in cuts if c < len(body)]
+        assert _stream_lines(body, cuts) == _python_stream_lines(body, cuts)
+    check()
+    lines, done = _stream_lines(b"5\r\n{\"a\":\r\n4\r\n1}\n\n\r\n0\r\n\r\n", [3, 9])
+    assert lines == [b'{"a":1}'] and done
+    m = native.load(required=True)
+    for bad in (b"zz\r\n", b"3\r\nabcXY"):
+        with pytest.raises(ValueError):
+            m.chunk_lines(bytearray(bad), -1, bytearray())
+
+
+def test_native_relay_index_matches_relay_scan():
+    """relay_index (the one-partition relay loop) stores, deletes and forwards exactly what a relay_scan loop
+    does."""
+    from ncc import native
+    m = native.load(required=True)
+
+    def ev(t, name, ns="n"):
+        return json.dumps({"type": t, "object": {"metadata": {"name": name, "namespace": ns,
+                                                              "resourceVersion": "1"}}}).encode()
+    lines = [ev("ADDED", "a"), ev("MODIFIED", "b", ""), ev("BOOKMARK", "c"), b"garbage", ev("DELETED", "a"),
+             ev("DELETED", "zz"), ev("ADDED", "d"), ev("ERROR", "e")]
+    raw_py, keep_py = {("n", "old"): b"x"}, []
+    for line in lines:
+        sc = m.relay_scan(line, 1, "dflt")
+        if sc is None or sc[0] == 3:
+            continue
+        if sc[0] == 2:
+            raw_py.pop((sc[1], sc[2]), None)
+        else:
+            raw_py[(sc[1], sc[2])] = line
+        keep_py.append(line)
+    raw = {("n", "old"): b"x"}
+    assert m.relay_index(lines, raw, "dflt") == keep_py
+    assert raw == raw_py and ("dflt", "b") in raw
