@@ -59,6 +59,11 @@ def dependent_names(template: Obj) -> tuple[list[str], list[str]]:
 def same_references(old: Obj, new: Obj) -> bool:
     """True when two template versions reference the same Secrets and ConfigMaps (in order).  Identical
     mapped-environment lists, the common case of a version bump, are recognised by one C-level compare."""
+    sa, sb = old.get("spec"), new.get("spec")
+    if sa and sb:
+        ra = sa.get("_rfp")  # slim templates (_native.template_event_slim): a digest of the references' text
+        if ra is not None and ra == sb.get("_rfp"):
+            return True
     a, b = _mapped_env(old), _mapped_env(new)
     return a == b or dependent_names(old) == dependent_names(new)
 

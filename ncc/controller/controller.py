@@ -48,6 +48,16 @@ def split_key(key: str) -> tuple[str, str, str]:
     return kind, ns, name
 
 
+def _reference_guard(t: dict):
+    """What the template indices read: the namespace and the mapped environment — of a slim template, the
+    digest of the environment's text (an int compare instead of a list-of-dicts compare)."""
+    spec = t.get("spec") or {}
+    r = spec.get("_rfp")
+    if r is None:
+        r = (spec.get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
+    return (t.get("metadata") or {}).get("namespace"), r
+
+
 class Controller(ReconcileMixin):
     def __init__(self, *, alias: str, namespace: str, client, shards: list,
                  template_informer: Informer, workgroup_informer: Informer,
@@ -116,9 +126,7 @@ class Controller(ReconcileMixin):
             self.template_informer.store.add_indexer(
                 "configmap", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in configmap_names(t)])
             # both indices read only the namespace and the mapped environment
-            self.template_informer.store.index_guard = \
-                lambda t: (meta(t).get("namespace"), ((t.get("spec") or {}).get("runtimeEnvironment") or {})
-                           .get("mappedEnvironmentVariables"))
+            self.template_informer.store.index_guard = _reference_guard
         self._register_handlers()
 
     @property
@@ -451,14 +459,8 @@ class Controller(ReconcileMixin):
             self._inline_timer = asyncio.get_running_loop().call_soon(self._flush_inline)
         else:
             keys, self._inline_keys = pending, set()
-        for key in keys:
-            try:
-                done = self.finish_inline(key)
-            except Exception:  # noqa: BLE001 — the queued pass will hit (and report) the same problem
-                log.exception("inline finish of %s failed; queueing a pass", key)
-                done = False
-            if not done:
-                self.queue.add(key)
+        for key in self.finish_inline_many(keys):
+            self.queue.add(key)
 
     def shard_ready_ok(self, key: str, obj: dict):
         """None while some shard has not reported on this object version, else whether all succeeded."""

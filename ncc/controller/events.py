@@ -124,6 +124,7 @@ class BroadcastRecorder(EventRecorder):
         self._deferred: dict[tuple, list] = {}  # repeat_window: correlation key -> held entry [.., n]
         self._flush_timer = None
         self._buckets: dict[tuple, TokenBucket] = {}
+        self._blocked: dict[tuple, float] = {}  # (kind, apiVersion, ns, name, uid) -> when its next token is due
         self._similar: dict[tuple, tuple[set, float]] = {}  # aggregate key -> (messages, first_seen)
         self._seen: dict[tuple, list] = {}  # full key -> [name, count] of the Event last written
         self._tasks: list[asyncio.Task] = []
@@ -160,6 +161,16 @@ class BroadcastRecorder(EventRecorder):
 
     def event(self, obj, event_type, reason, message, kind=None):
         self.stats["recorded"] += 1
+        blocked = self._blocked
+        if blocked and not (self.log_events and log.isEnabledFor(logging.INFO)):
+            # an object whose spam bucket is empty: dropped before its reference is built (the bucket's
+            # refill is linear, so skipping its update until the next token is due changes nothing)
+            m = obj.get("metadata") or {}
+            until = blocked.get((kind or obj.get("kind", ""), obj.get("apiVersion", ""), m.get("namespace", ""),
+                                 m.get("name", ""), m.get("uid", "")))
+            if until is not None and time.monotonic() < until:
+                self.stats["dropped_spam"] += 1
+                return
         ref = involved_object(obj, kind)
         if self.log_events and log.isEnabledFor(logging.INFO):
             log.info("Event occurred", extra={"object": f"{ref['namespace']}/{ref['name']}", "kind": ref["kind"],
@@ -167,6 +178,13 @@ class BroadcastRecorder(EventRecorder):
         now = time.monotonic()
         if not self._allow(ref, now):
             self.stats["dropped_spam"] += 1
+            b = self._buckets.get((self.component, ref["kind"], ref["namespace"], ref["name"], ref["uid"],
+                                   ref["apiVersion"]))
+            if b is not None and b.qps > 0:
+                m = obj.get("metadata") or {}
+                blocked[(kind or obj.get("kind", ""), obj.get("apiVersion", ""), m.get("namespace", ""),
+                         m.get("name", ""), m.get("uid", ""))] = now + (1.0 - b._tokens) / b.qps
+                _bound(blocked, self.cache_limit)
             return
         message, key = self._aggregate(ref, event_type, reason, message, now)
         if self.coalesce:

@@ -466,58 +466,89 @@ class ReconcileMixin:
         shard succeeded and the status already says so.  Saves the queue round trip, the worker hand-off and
         the pass preamble for the common case.  False (nothing done) when a real pass is needed: a status or
         adoption write, a failure to report, a deletion, or a pass already queued or running for the key."""
-        if not self.ready.is_set() or self.queue.shutting_down() or self.queue.busy(key) or \
-                not self.options.adoption_cache:
-            return False  # workers not running (standby, shutdown, lost Lease): nothing may be written
-        kind, ns, name = key.split("/", 2)
-        if kind != C.KIND_TEMPLATE:
-            return False
-        template = self.template_informer.store.get(ns, name)
-        if template is None:
-            return False
-        status = template.get("status") or {}
-        conds = status.get("conditions")
-        m = template.get("metadata") or {}
-        if not conds or self._adopted.get(key) != m.get("resourceVersion"):
-            return False
-        ok = self.reports.ready_ok(key, m.get("uid") or "", m.get("generation") or 0)
-        if ok is None:
-            # A newer version (the next wave) reached the cache between the last report and this flush.  It is
-            # initialised and adopted, so the pass would stop at the readiness check, exactly as the early pass
-            # `_on_crd_update` skips: the new version's last report brings the key back.
-            self.stats["inline_superseded"] += 1
-            return True
-        if not ok:
-            return False
-        # report_template_synced_condition would leave the status as it is (no write) exactly when the Ready
-        # condition and the three synced lists already hold what it would set.  That depends only on the
-        # status, the references and the shard list: a new template version (the next wave) with an equal
-        # status and equal references reuses the last verdict (two C-level compares instead of the rebuild).
+        return not self.finish_inline_many((key,))
+
+    def finish_inline_many(self, keys) -> list:
+        """`finish_inline` over a batch of keys (the loop invariants read once); returns the keys that need a
+        real pass."""
+        if not self.ready.is_set() or self.queue.shutting_down() or not self.options.adoption_cache:
+            return list(keys)  # workers not running (standby, shutdown, lost Lease): nothing may be written
+        busy = self.queue.busy
+        get = self.template_informer.store.get
+        adopted = self._adopted
+        ready_ok = self.reports.ready_ok
+        memos = self._inline_status_ok
+        pending_event = self._pending_event
+        event_on_noop = self.options.event_on_noop
         shards = self.all_shard_names
-        spec = template.get("spec") or {}
-        sfp, rfp = template.get(SLIM_STATUS_FP), spec.get("_rfp")
-        if sfp is not None and rfp is not None:  # a slim template: digests of the status and reference texts
-            status_id, refs = sfp, rfp
-        else:
-            status_id, refs = status, (spec.get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
-        memo = self._inline_status_ok.get(key)
-        if memo is None or memo[2] is not shards or memo[0] != status_id or memo[1] != refs:
-            secrets, configmaps = dependent_names(template)
-            c0 = conds[0]
-            if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE,
-                                     f"Algorithm {q(name)} ready") \
-                    or status.get("syncedSecrets") != secrets or status.get("syncedConfigurations") != configmaps \
-                    or status.get("syncedToClusters") != shards:
-                return False
-            self._inline_status_ok[key] = (status_id, refs, shards)
-        self.stats["reconciles"] += 1
-        self.stats["inline_finishes"] += 1
-        self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())  # a reconcile, done in place
-        if key in self._pending_event or self.options.event_on_noop:
-            self._pending_event.discard(key)
-            self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
-                                C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND), kind=C.TEMPLATE_KIND)
-        return True
+        kind_template = C.KIND_TEMPLATE
+        st = self.stats
+        rest = []
+        done = 0
+        for key in keys:
+            try:
+                kind, ns, name = key.split("/", 2)
+                if kind != kind_template or busy(key):
+                    rest.append(key)
+                    continue
+                template = get(ns, name)
+                if template is None:
+                    rest.append(key)
+                    continue
+                status = template.get("status") or {}
+                conds = status.get("conditions")
+                m = template.get("metadata") or {}
+                if not conds or adopted.get(key) != m.get("resourceVersion"):
+                    rest.append(key)
+                    continue
+                ok = ready_ok(key, m.get("uid") or "", m.get("generation") or 0)
+                if ok is None:
+                    # A newer version (the next wave) reached the cache between the last report and this
+                    # flush.  It is initialised and adopted, so the pass would stop at the readiness check,
+                    # exactly as the early pass `_on_crd_update` skips: the new version's last report brings
+                    # the key back.
+                    st["inline_superseded"] += 1
+                    continue
+                if not ok:
+                    rest.append(key)
+                    continue
+                # report_template_synced_condition would leave the status as it is (no write) exactly when the
+                # Ready condition and the three synced lists already hold what it would set.  That depends only
+                # on the status, the references and the shard list: a new template version (the next wave)
+                # with an equal status and equal references reuses the last verdict — of a slim template, two
+                # int compares of the digests of their texts.
+                spec = template.get("spec") or {}
+                sfp, rfp = template.get(SLIM_STATUS_FP), spec.get("_rfp")
+                if sfp is not None and rfp is not None:
+                    status_id, refs = sfp, rfp
+                else:
+                    status_id, refs = status, (spec.get("runtimeEnvironment") or {}).get("mappedEnvironmentVariables")
+                memo = memos.get(key)
+                if memo is None or memo[2] is not shards or memo[0] != status_id or memo[1] != refs:
+                    secrets, configmaps = dependent_names(template)
+                    c0 = conds[0]
+                    if c0 != ready_condition(c0.get("lastTransitionTime", ""), C.CONDITION_TRUE,
+                                             f"Algorithm {q(name)} ready") \
+                            or status.get("syncedSecrets") != secrets \
+                            or status.get("syncedConfigurations") != configmaps \
+                            or status.get("syncedToClusters") != shards:
+                        rest.append(key)
+                        continue
+                    memos[key] = (status_id, refs, shards)
+                done += 1
+                if key in pending_event or event_on_noop:
+                    pending_event.discard(key)
+                    self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                        C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND), kind=C.TEMPLATE_KIND)
+            except Exception:  # noqa: BLE001 — the queued pass will hit (and report) the same problem
+                log.exception("inline finish of %s failed; queueing a pass", key)
+                rest.append(key)
+        if done:
+            st["reconciles"] += done
+            st["inline_finishes"] += done
+            # a reconcile done in place takes no time: one gauge per batch (an aggregated gauge keeps the last)
+            self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())
+        return rest
 
     async def _sync_template_to_shard(self, template: dict, shard, spec_fp) -> None:
         if self.options.wait_for_shards_timeout is not None and not shard.has_synced():

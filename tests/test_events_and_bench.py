@@ -77,6 +77,30 @@ async def test_event_spam_filter_and_aggregation():
     await rec.stop()
 
 
+async def test_event_spam_fast_drop_lets_the_next_token_through(monkeypatch):
+    """An object whose spam bucket is empty is dropped on a fast path until its next token is due (1/300 s
+    refill): the event after that is written, and one more is dropped again — the bucket's own verdicts."""
+    from ncc.controller import events as ev
+    clock = [1000.0]
+    monkeypatch.setattr(ev.time, "monotonic", lambda: clock[0])
+    client = FakeClient(ClusterState(), simple=False)
+    rec = BroadcastRecorder(client, log_events=False)
+    t = client.state.create(R.TEMPLATES, "nexus", make_template(0, "nexus"))
+    other = client.state.create(R.TEMPLATES, "nexus", make_template(1, "nexus"))
+    for _ in range(SPAM_BURST + 5):
+        rec.event(t, "Normal", "Synced", "synced")
+    assert rec.stats["dropped_spam"] == 5 and len(rec._blocked) == 1
+    rec.event(other, "Normal", "Synced", "synced")  # another object is not held back
+    assert rec.stats["dropped_spam"] == 5
+    clock[0] += 299.0
+    rec.event(t, "Normal", "Synced", "synced")
+    assert rec.stats["dropped_spam"] == 6
+    clock[0] += 1.5
+    rec.event(t, "Normal", "Synced", "synced")
+    rec.event(t, "Normal", "Synced", "synced")
+    assert rec.stats["dropped_spam"] == 7 and rec.stats["recorded"] == SPAM_BURST + 9
+
+
 async def test_event_writers_keep_per_object_order():
     """Several writer tasks: each object's events stay on one writer, so dedup PATCHes count correctly."""
     client = FakeClient(ClusterState(), simple=False)
