@@ -763,6 +763,7 @@ private:
     };
     using PipePtr = std::shared_ptr<Pipe>;
     std::vector<PipePtr> pipes_;
+    PipePtr building_;  // the pipe the requests of this loop iteration go on (see pick)
 
     void reload_token(bool force) {
         if (creds_.token_file.empty()) return;
@@ -821,7 +822,16 @@ private:
 
     // The connection a request goes on: an idle one; else a new one while fewer than `max_` are open; else the
     // least loaded one below `depth_` (the admission gate keeps the requests in flight ≤ max_ × depth_).
+    // Requests issued in one loop iteration fill the pipe whose write is still to go out (up to `depth_`)
+    // before another is taken: they leave in one send, and their answers tend to arrive in one read.
     PipePtr pick() {
+        if (building_ && !building_->broken && static_cast<int>(building_->pending.size()) < depth_ &&
+            (building_->flush_posted || !building_->connected))
+            return building_;
+        building_ = pick_least_loaded();
+        return building_;
+    }
+    PipePtr pick_least_loaded() {
         PipePtr best;
         for (auto& p : pipes_) {
             if (p->broken || static_cast<int>(p->pending.size()) >= depth_) continue;
