@@ -330,6 +330,109 @@ def ctx_switches(named: dict) -> dict:
     return out
 
 
+def _cpu_list(text: str) -> list[int]:
+    out = []
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    return out
+
+
+class Placement:
+    """Where the busy processes ran during the timed waves: every 20 ms, the CPU each was last on
+    (/proc/<pid>/stat), mapped to its physical core (SMT siblings) and L3 domain.  Two of them on one
+    physical core at once halve each other's speed — a run-to-run variance the calibration loop, timed alone,
+    does not see.  Reported: the share of samples in which a process shared its core with another one, the
+    distinct cores and L3 domains used, and the CPUs the job may run on."""
+
+    def __init__(self, named: dict):
+        import threading
+        self.named = named
+        self.samples = 0
+        self.shared: dict[str, int] = {}
+        self.cores: dict[str, set] = {}
+        self.l3: set = set()
+        self._stop = threading.Event()
+        self._core: dict[int, int] = {}
+        self._l3: dict[int, int] = {}
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _topo(self, cpu: int) -> tuple[int, int]:
+        c = self._core.get(cpu)
+        if c is None:
+            base = f"/sys/devices/system/cpu/cpu{cpu}"
+            try:
+                with open(f"{base}/topology/thread_siblings_list") as f:
+                    c = min(_cpu_list(f.read()))
+            except (OSError, ValueError):
+                c = cpu
+            try:
+                with open(f"{base}/cache/index3/shared_cpu_list") as f:
+                    self._l3[cpu] = min(_cpu_list(f.read()))
+            except (OSError, ValueError):
+                self._l3[cpu] = -1
+            self._core[cpu] = c
+        return c, self._l3[cpu]
+
+    def _pids(self) -> dict:
+        import psutil
+        out = {}
+        for name, proc in self.named.items():
+            if proc is None:
+                continue
+            out[name] = proc.pid
+            if name == "coordinator":
+                try:
+                    for i, c in enumerate(psutil.Process(proc.pid).children(recursive=True)):
+                        out[f"coordinator-child{i}"] = c.pid
+                except (psutil.Error, OSError):
+                    pass
+        return out
+
+    def _run(self) -> None:
+        pids = self._pids()
+        while not self._stop.wait(0.02):
+            where = {}
+            for name, pid in pids.items():
+                try:
+                    with open(f"/proc/{pid}/stat") as f:
+                        fields = f.read().rsplit(")", 1)[1].split()
+                    if fields[0] not in ("R",):
+                        continue  # only processes running (or runnable) right now compete for a core
+                    cpu = int(fields[36])
+                except (OSError, IndexError, ValueError):
+                    continue
+                where[name] = self._topo(cpu)
+            self.samples += 1
+            by_core: dict[int, int] = {}
+            for core, l3 in where.values():
+                by_core[core] = by_core.get(core, 0) + 1
+                self.l3.add(l3)
+            for name, (core, _) in where.items():
+                self.cores.setdefault(name, set()).add(core)
+                if by_core[core] > 1:
+                    self.shared[name] = self.shared.get(name, 0) + 1
+
+    def start(self) -> "Placement":
+        self._t.start()
+        return self
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._t.join(timeout=2)
+        try:
+            allowed = len(os.sched_getaffinity(0))
+        except OSError:
+            allowed = None
+        n = max(1, self.samples)
+        return {"samples": self.samples, "allowed_cpus": allowed, "l3_domains_used": len(self.l3),
+                "core_shared_share": {k: round(v / n, 3) for k, v in sorted(self.shared.items())},
+                "cores_used": {k: len(v) for k, v in sorted(self.cores.items())}}
+
+
 def child_pids(proc) -> set:
     """PIDs of every process under the controller (coordinator partitions, executors)."""
     import psutil
@@ -560,6 +663,7 @@ async def run(args, d: Dist) -> dict | None:
                     sys0: dict = {}
                     cpu0 = cpu_seconds(named, sys_out=sys0)
                     kids0 = child_pids(controller) if controller is not None else set()
+                    placement = Placement(named).start() if d.rank == 0 else None
                 t0 = None
                 if d.rank == 0:
                     a = await post(session, f"{ctrl_url}/_fake/apply", {"staged": step})
@@ -577,6 +681,7 @@ async def run(args, d: Dist) -> dict | None:
                 d.barrier()  # the wave is done only when every shard has converged
             d.sync()
             elapsed = time.perf_counter() - t_start
+            placed = placement.stop() if placement is not None else None
             rss: dict = {}
             sys1: dict = {}
             cpu1 = cpu_seconds(named, rss, sys1)
@@ -588,7 +693,7 @@ async def run(args, d: Dist) -> dict | None:
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
                 with open(os.path.join(work, "topology.json")) as f:
                     ctrl_state["sizing"] = json.load(f)
-            debug = None
+            ctl_debug = None
             if d.rank == 0:
                 try:
                     await asyncio.sleep(1.2)  # one more status message from every executor, after the waves
@@ -598,9 +703,9 @@ async def run(args, d: Dist) -> dict | None:
                     flow = {}
                     for h in (st.get("executors") or {}).values():
                         flow.update((h.get("status") or {}).get("flow") or {})
-                    debug = {"executor_flow": flow, "coordinator_gc": st.get("gc")}
+                    ctl_debug = {"executor_flow": flow, "coordinator_gc": st.get("gc")}
                 except Exception as e:  # noqa: BLE001 — diagnostics only
-                    debug = {"error": repr(e)[:200]}
+                    ctl_debug = {"error": repr(e)[:200]}
             if d.rank == 0:  # LIST/WATCH load the controller put on its own cluster (watch relay: 1 each per kind)
                 import aiohttp as _aiohttp
                 async with session.get(f"{ctrl_url}/_fake/stats", timeout=_aiohttp.ClientTimeout(total=30)) as r:
@@ -638,6 +743,7 @@ async def run(args, d: Dist) -> dict | None:
                         "loadavg": [round(x, 2) for x in load0] + [round(x, 2) for x in load1],
                         "ctx_switches": {k: [v[0] - cs0.get(k, [0, 0])[0], v[1] - cs0.get(k, [0, 0])[1]]
                                          for k, v in cs1.items()},
+                        "placement": placed,
                         "calibration": calibrate()}
             rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)
@@ -700,7 +806,7 @@ async def run(args, d: Dist) -> dict | None:
                 "host": host,
                 # per shard: the C++ executor's adaptive concurrency limit at the end, the most requests in flight,
                 # 429s and overload signals seen (native/executor/http.hpp); the coordinator's GC passes
-                "controller_state": debug,
+                "controller_state": ctl_debug,
                 # kernel-mode share of that CPU (syscalls, the loopback TCP stack) per process
                 "controller_cpu_sys_share": {k: round((sys1.get(k, 0.0) - sys0.get(k, 0.0)) / v, 3)
                                              for k, v in ctl_cpu.items() if v > 0},

@@ -34,7 +34,8 @@ def test_smoke_on_box():
 
 
 def test_bench_contract_single_shard():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--templates", "100", "--steps", "2",
+    # 300 templates × 3 steps: enough CPU in every process for its 10 ms clock ticks to register
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--templates", "300", "--steps", "3",
                         "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -45,4 +46,5 @@ def test_bench_contract_single_shard():
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["controller_alive"]
     # the data plane that ran is the C++ shard executor, not the Python fallback
     assert res["controller_sizing"]["executor_impl"] == "native", res["controller_sizing"]
-    assert res["controller_to_substrate"] and res["host"]["calibration"].get("cpp_ctl_scan_ns"), res["host"]
+    assert res["controller_to_substrate"] is not None and res["host"]["calibration"].get("cpp_ctl_scan_ns"), \
+        (res["controller_cpu_us_per_object"], res["substrate_us_per_object"], res["host"])
