@@ -24,6 +24,8 @@ class ControllerOptions:
     concurrent_fanout: bool = False        # controller.go:790 loops shards sequentially
     shard_failure_isolation: bool = False  # controller.go:790-831 fails fast on the first shard error
     concurrent_dependents: bool = False    # controller.go:505,567 loop dependents sequentially
+    dependents_despite_template_failure: bool = False  # controller.go:790-831 stops the pass when the
+                                           # template update fails, before any dependent is written
     generation_filter: bool = False        # controller.go:286-305 enqueues on every update incl. resync
     dependent_data_filter: bool = False    # controller.go:319-355 re-reconciles on any RV change
     event_on_noop: bool = True             # controller.go:754,843 emit Synced on every pass
@@ -67,6 +69,7 @@ class ControllerOptions:
             concurrent_fanout=True,
             shard_failure_isolation=True,
             concurrent_dependents=False,  # measured: per-dependent tasks cost more CPU than the RTT they save
+            dependents_despite_template_failure=True,  # as the C++ executor (README "Modes")
             generation_filter=True,
             dependent_data_filter=True,
             event_on_noop=False,

@@ -557,17 +557,30 @@ class ReconcileMixin:
         name = meta(template).get("name", "")
         spec = template.get("spec")
         shard_template = shard.template_lister.try_get(ns, name)
-        update = None
+        update = update_error = None
         if self.options.server_side_apply:
             if shard_template is None or not spec_matches(spec, shard_template, spec_fp):
                 self._pass_wrote()
-                shard_template = await shard.apply_template(name, ns, spec, C.FIELD_MANAGER)
+                try:
+                    shard_template = await shard.apply_template(name, ns, spec, C.FIELD_MANAGER)
+                except Exception as e:  # noqa: BLE001 — as for the update below: the UID is known
+                    if shard_template is None or not self.options.dependents_despite_template_failure:
+                        raise
+                    update_error = e
         elif shard_template is not None and not spec_matches(spec, shard_template, spec_fp):
             log.debug("Content changed for NexusAlgorithmTemplate %s, updating", name)
             update = self._write(shard, "update_template", shard.template_informer, R.TEMPLATES,
                                  shard_template, spec, C.FIELD_MANAGER)
             if not self.options.concurrent_dependents:
-                shard_template = await update
+                try:
+                    shard_template = await update
+                except Exception as e:  # noqa: BLE001
+                    if not self.options.dependents_despite_template_failure:
+                        raise
+                    # native: the shard template keeps its UID, which is all its dependents' ownerRefs need,
+                    # so a refused update (a 422, say) does not hold back the new Secret/ConfigMap data; the
+                    # pass still fails with the template's error (README "Modes")
+                    update_error = e
                 update = None
             # native: an update keeps the shard template's UID, so its dependents go out alongside it
             # instead of one round trip later (controller.go:790-831 is strictly sequential)
@@ -588,8 +601,12 @@ class ReconcileMixin:
                 if isinstance(r, BaseException):
                     raise r
         else:
-            await self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard)
-            await self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard)
+            # after a refused update the shard template still has the old spec: the references are the source's
+            holder = template if update_error is not None else None
+            await self._sync_dependents_to_shard(R.SECRETS, template, shard_template, shard, holder)
+            await self._sync_dependents_to_shard(R.CONFIGMAPS, template, shard_template, shard, holder)
+            if update_error is not None:
+                raise update_error
 
     async def _write(self, shard, op: str, informer, rt, *args):
         """Issue a shard write; in native mode resolve create/update races by refetching."""
@@ -608,12 +625,15 @@ class ReconcileMixin:
                 return await getattr(shard, op)(*retry_args)
             return informer.store.get(ns, nm) or live
 
-    async def _sync_dependents_to_shard(self, rt, template: dict, shard_template: dict, shard) -> None:
+    async def _sync_dependents_to_shard(self, rt, template: dict, shard_template: dict, shard,
+                                        holder: dict | None = None) -> None:
         """syncSecretsToShard / syncConfigMapsToShard (controller.go:504-626)."""
         is_secret = rt is R.SECRETS
         # GetSecretNames() is read from the shard template (controller.go:505); its spec equals the
         # controller's after create/update.  A slim-cache shard template carries no spec: use the source.
-        holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) else shard_template
+        if holder is None:
+            holder = template if (SLIM_FP in shard_template or shard_template.get("spec") is None) \
+                else shard_template
         names = secret_names(holder) if is_secret else configmap_names(holder)
         if self.options.concurrent_dependents and len(names) > 1:
             res = await asyncio.gather(*(self._sync_dependent(rt, template, shard_template, shard, n) for n in names),

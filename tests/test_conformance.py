@@ -652,6 +652,25 @@ async def test_rejected_template_update_does_not_hold_back_dependents(tmp_path, 
         await cl.ready()
 
 
+async def test_rejected_template_apply_does_not_hold_back_dependents(tmp_path, impl):
+    """The same deviation under `server-side-apply: true`: a refused apply of the shard template leaves the
+    new dependent data on the shard and Ready=False naming the template's failure."""
+    async with Cluster(tmp_path, impl, n_shards=1, server_side_apply=True) as cl:
+        cl.seed()
+        await cl.start()
+        await cl.ready()
+        cl.rules(0, [{"method": "PATCH", "resource": "nexusalgorithmtemplates", "code": 422, "reason": "Invalid",
+                      "count": -1}])
+        await mutate(cl.cc, R.SECRETS, "s0", lambda o: o["data"].__setitem__("version", "djc="))
+        await mutate(cl.cc, R.TEMPLATES, T0, lambda o: o["spec"]["container"].__setitem__("versionTag", "v7"))
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.SECRETS, NS, "s0")["data"]["version"] == "djc="))
+        await cl.not_ready(T0, "shard-0", "Invalid")
+        cl.rules(0, [])
+        await wait_for(lambda: asyncio.sleep(0, cl.sstates[0].get(R.TEMPLATES, NS, T0)["spec"]["container"]
+                                             ["versionTag"] == "v7"))
+        await cl.ready()
+
+
 async def test_status_advances_under_a_steady_stream_of_dependent_events(tmp_path, impl):
     """A pass superseded by an event that arrived while it ran may skip its report (the next pass reports,
     carrying its writes) — but not for ever: with a Secret changing every few milliseconds every
