@@ -330,6 +330,19 @@ def ctx_switches(named: dict) -> dict:
     return out
 
 
+def host_busy() -> tuple[float, float] | None:
+    """(busy, total) CPU-seconds of the whole host so far (/proc/stat, not namespaced): the delta over the
+    timed waves, minus this job's own CPU, is what other tenants ran on the machine meanwhile."""
+    try:
+        with open("/proc/stat") as f:
+            v = [int(x) for x in f.readline().split()[1:]]
+    except (OSError, ValueError):
+        return None
+    hz = os.sysconf("SC_CLK_TCK")
+    idle = v[3] + (v[4] if len(v) > 4 else 0)
+    return (sum(v) - idle) / hz, sum(v) / hz
+
+
 def _cpu_list(text: str) -> list[int]:
     out = []
     for part in text.strip().split(","):
@@ -658,6 +671,7 @@ async def run(args, d: Dist) -> dict | None:
                     cg0 = cgroup_cpu()
                     cs0 = ctx_switches(named)
                     load0 = os.getloadavg()
+                    hb0 = host_busy()
                     d.sync()
                     t_start = time.perf_counter()
                     sys0: dict = {}
@@ -688,6 +702,7 @@ async def run(args, d: Dist) -> dict | None:
             cg1 = cgroup_cpu()
             cs1 = ctx_switches(named)
             load1 = os.getloadavg()
+            hb1 = host_busy()
             ctrl_api = None
             ctrl_state = {}
             if d.rank == 0 and os.path.exists(os.path.join(work, "topology.json")):
@@ -744,6 +759,8 @@ async def run(args, d: Dist) -> dict | None:
                         "ctx_switches": {k: [v[0] - cs0.get(k, [0, 0])[0], v[1] - cs0.get(k, [0, 0])[1]]
                                          for k, v in cs1.items()},
                         "placement": placed,
+                        # CPUs the whole host kept busy over the timed waves (every tenant, this job included)
+                        "host_busy_cpus": round((hb1[0] - hb0[0]) / elapsed, 1) if hb0 and hb1 else None,
                         "calibration": calibrate()}
             rsses = d.all_gather(rss)
             elapsed = d.max(elapsed)

@@ -33,7 +33,8 @@ print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99",
       "ctl_us", d["controller_cpu_us_per_object"], d["controller_cpu_us_per_object_split"],
       "substrate_us", d.get("substrate_us_per_object"), "ratio", d.get("controller_to_substrate"),
       "coord_cores", d["cpu_cores_busy"].get("coordinator"), "py_loop_ms", c.get("python_loop_ms"),
-      "cpp_scan_ns", c.get("cpp_ctl_scan_ns"), "throttled_us", h.get("throttled_usec"), flush=True)
+      "cpp_scan_ns", c.get("cpp_ctl_scan_ns"), "throttled_us", h.get("throttled_usec"),
+      "host_busy", h.get("host_busy_cpus"), flush=True)
 EOF
 }
 
