@@ -22,6 +22,7 @@
 //    bitmask of its owners' partitions, so the partition test itself builds no Python strings.
 //  * parse_response_head(bytes) / parse_request_head(bytes) — HTTP/1.1 heads for the client transport
 //    and the fake apiserver.
+//  * owner_filter(lines, items, assumed, ns) — the metadata-only informer's owner filter over a batch.
 //  * relay_index(lines, raw, ns) — the one-partition watch relay's index-and-forward loop.
 //  * chunk_lines(bytearray, state, bytearray) — a chunked watch body cut into its event lines in one call.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
@@ -56,7 +57,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 19
+#define NCC_NATIVE_ABI 20
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -713,6 +714,90 @@ py::object relay_scan(py::bytes line, int parts, const std::string& default_ns) 
     for (const auto& o : owners) mask |= 1ull << (key_crc(kns, o) % up);
     return py::make_tuple(code, py::str(kns.data(), kns.size()), py::str(name.data(), name.size()), kp, mask,
                           static_cast<long long>(owners.size()));
+}
+
+// Does a Python str equal these UTF-8 bytes?
+static bool str_eq(PyObject* o, std::string_view v) {
+    if (o == nullptr || !PyUnicode_Check(o)) return v.empty() && o == nullptr;
+    Py_ssize_t n = 0;
+    const char* u = PyUnicode_AsUTF8AndSize(o, &n);
+    if (u == nullptr) {
+        PyErr_Clear();
+        return false;
+    }
+    return static_cast<size_t>(n) == v.size() && std::memcmp(u, v.data(), v.size()) == 0;
+}
+
+// owner_filter(lines, items, assumed, default_ns) -> (kept lines, dropped, rv of the last line if dropped)
+// The metadata-only informer's filter over a whole batch (ncc/cache/informer.py `_consume`): a MODIFIED
+// line of an object cached in `items` (the store's dict, keyed (namespace, name)) whose ownerReferences
+// names and uids equal the cached ones carries nothing such a store keeps, and is dropped.  Every other line
+// — other event types, unknown or overlaid (`assumed`) keys, unreadable lines — is kept for the Python path.
+py::tuple owner_filter(py::list lines, py::dict items, py::dict assumed, const std::string& default_ns) {
+    py::list keep;
+    long long dropped = 0;
+    std::string_view last_rv;
+    bool last_dropped = false;
+    const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
+    std::vector<std::string_view> owners, uids;
+    static PyObject* k_meta = PyUnicode_InternFromString("metadata");
+    static PyObject* k_refs = PyUnicode_InternFromString("ownerReferences");
+    static PyObject* k_name = PyUnicode_InternFromString("name");
+    static PyObject* k_uid = PyUnicode_InternFromString("uid");
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
+        last_dropped = false;
+        char* buf = nullptr;
+        Py_ssize_t len = 0;
+        bool drop = false;
+        std::string_view type, ns, name, rv;
+        if (PyBytes_Check(line) && PyBytes_AsStringAndSize(line, &buf, &len) == 0) {
+            owners.clear();
+            uids.clear();
+            Scanner sc(buf, static_cast<size_t>(len));
+            sc.owners = &owners;
+            sc.owner_uids = &uids;
+            if (sc.scan(type, ns, name, rv) && type == "MODIFIED") {
+                std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
+                py::tuple key = py::make_tuple(py::str(kns.data(), kns.size()), py::str(name.data(), name.size()));
+                PyObject* cur = PyDict_GetItemWithError(items.ptr(), key.ptr());
+                if (cur == nullptr && PyErr_Occurred()) throw py::error_already_set();
+                int overlaid = PyDict_Contains(assumed.ptr(), key.ptr());
+                if (overlaid < 0) throw py::error_already_set();
+                if (cur != nullptr && !overlaid && PyDict_Check(cur)) {
+                    PyObject* m = PyDict_GetItem(cur, k_meta);
+                    PyObject* refs = m != nullptr && PyDict_Check(m) ? PyDict_GetItem(m, k_refs) : nullptr;
+                    if (refs == nullptr || refs == Py_None) {
+                        drop = owners.empty();
+                    } else if (PyList_Check(refs) && static_cast<size_t>(PyList_GET_SIZE(refs)) == owners.size()) {
+                        drop = true;
+                        for (size_t j = 0; j < owners.size() && drop; ++j) {
+                            PyObject* r = PyList_GET_ITEM(refs, static_cast<Py_ssize_t>(j));
+                            if (!PyDict_Check(r)) {
+                                drop = false;
+                                break;
+                            }
+                            PyObject* rn = PyDict_GetItem(r, k_name);
+                            PyObject* ru = PyDict_GetItem(r, k_uid);
+                            drop = (rn == nullptr ? owners[j].empty() : str_eq(rn, owners[j])) &&
+                                   (ru == nullptr ? uids[j].empty() : str_eq(ru, uids[j]));
+                        }
+                    }
+                }
+            }
+        } else {
+            PyErr_Clear();
+        }
+        if (drop) {
+            ++dropped;
+            last_rv = rv;
+            last_dropped = true;
+        } else if (PyList_Append(keep.ptr(), line) != 0) {
+            throw py::error_already_set();
+        }
+    }
+    py::object rv_o = last_dropped ? py::object(py::str(last_rv.data(), last_rv.size())) : py::object(py::none());
+    return py::make_tuple(keep, dropped, rv_o);
 }
 
 // relay_index(lines, raw, default_ns) -> the lines to forward.  The one-partition relay's whole loop in one
@@ -2198,6 +2283,8 @@ PYBIND11_MODULE(_native, m) {
           "(method, target, {lower-cased name: value}) of an HTTP/1.1 request head");
     m.def("relay_scan", &relay_scan, py::arg("line"), py::arg("parts"), py::arg("default_ns"),
           "(type_code, namespace, name, key_partition, owner_partition_mask, n_owners) of a watch line");
+    m.def("owner_filter", &owner_filter, py::arg("lines"), py::arg("items"), py::arg("assumed"),
+          py::arg("default_ns"), "the metadata-only informer's owner filter over a batch of watch lines");
     m.def("relay_index", &relay_index, py::arg("lines"), py::arg("raw"), py::arg("default_ns"),
           "the one-partition relay loop: index the lines in `raw`, return the object events to forward");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));

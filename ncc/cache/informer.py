@@ -267,7 +267,7 @@ class Informer:
             opart = of.part if of is not None else None
             oref = getattr(of, "referenced", None) if of is not None else None
             kf = of = None
-        return (scan, nparts, kpart, opart, oref, kf, of, mo)
+        return (scan, nparts, kpart, opart, oref, kf, of, mo, getattr(mod, "owner_filter", None) if mo else None)
 
     async def _watch(self, rv: str) -> str:
         """Consume one watch stream; returns the last RV seen.  Raises Gone to force a relist."""
@@ -298,13 +298,19 @@ class Informer:
 
     async def _consume(self, lines, ctx, rv: str) -> str:
         """Apply one batch of raw watch lines (see `_line_ctx`); returns the last RV seen."""
-        scan, nparts, kpart, opart, oref, kf, of, mo = ctx
+        scan, nparts, kpart, opart, oref, kf, of, mo, _owner_filter = ctx
         loads = loads_fast
         slim = self.slim_decode
         store = self.store
         default_ns = self.namespace or ""
         inflight, stash = self._inflight, self._stash
         sigs = self._owner_sigs
+        last = None
+        if mo and not nparts and kf is None and of is None and _owner_filter is not None:
+            # the whole batch through the native owner filter; what it keeps takes the path below
+            lines, dropped, last = _owner_filter(lines if type(lines) is list else list(lines), store._items,
+                                                 store._assumed, default_ns)
+            self.filtered += dropped
         for line in lines:
             sc = None
             if nparts:
@@ -372,6 +378,8 @@ class Informer:
                 continue
             ev = loads(line)
             rv = await self._handle(ev.get("type", ""), ev.get("object") or {}, rv)
+        if last is not None:  # the batch ended with a dropped line
+            rv = self.last_rv = last
         return rv
 
     async def _handle(self, t: str, obj: dict, rv: str) -> str:

@@ -418,3 +418,40 @@ def test_native_relay_index_matches_relay_scan():
     raw = {("n", "old"): b"x"}
     assert m.relay_index(lines, raw, "dflt") == keep_py
     assert raw == raw_py and ("dflt", "b") in raw
+
+
+def test_native_owner_filter_matches_the_python_filter():
+    """owner_filter drops exactly the MODIFIED lines of cached, non-overlaid objects whose owner names and uids
+    equal the cached ones (the metadata-only informer's Python filter), and reports the last dropped RV."""
+    from ncc import native
+    m = native.load(required=True)
+
+    def line(t, name, owners, ns="n", rv="5"):
+        md = {"name": name, "namespace": ns, "resourceVersion": rv}
+        if owners is not None:
+            md["ownerReferences"] = [{"apiVersion": "v1", "kind": "T", "name": o, "uid": u} for o, u in owners]
+        return json.dumps({"type": t, "object": {"metadata": md, "data": {"k": "v"}}}, ensure_ascii=False).encode()
+
+    def cached(owners):
+        md = {"name": "x"}
+        if owners is not None:
+            md["ownerReferences"] = [{"name": o, "uid": u} for o, u in owners]
+        return {"metadata": md}
+    items = {("n", "a"): cached([("t1", "u1")]), ("n", "b"): cached(None), ("n", "c"): cached([("t1", "u1")]),
+             ("n", "d"): cached([("t1", "u1"), ("t2", "u2")]), ("n", "e"): cached([]), ("n", "é"): cached([("t", "ü")])}
+    assumed = {("n", "c"): None}
+    lines = [line("MODIFIED", "a", [("t1", "u1")], rv="10"),       # same owners: dropped
+             line("MODIFIED", "a", [("t1", "u9")], rv="11"),       # uid changed: kept
+             line("MODIFIED", "b", None, rv="12"),                 # no owners either side: dropped
+             line("MODIFIED", "c", [("t1", "u1")], rv="13"),       # overlaid: kept
+             line("MODIFIED", "d", [("t2", "u2"), ("t1", "u1")]),  # order differs: kept
+             line("ADDED", "a", [("t1", "u1")]),                   # not MODIFIED: kept
+             line("MODIFIED", "zz", None),                         # not cached: kept
+             b"garbage",
+             line("MODIFIED", "e", None, rv="14"),                 # [] vs none: dropped
+             line("MODIFIED", "é", [("t", "ü")], rv="15")]         # UTF-8 names: dropped
+    kept, dropped, last = m.owner_filter(lines, items, assumed, "n")
+    assert dropped == 4 and last == "15"
+    assert kept == [lines[i] for i in (1, 3, 4, 5, 6, 7)]
+    kept, dropped, last = m.owner_filter(lines[:2], items, assumed, "n")
+    assert dropped == 1 and last is None and kept == [lines[1]]
