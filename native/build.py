@@ -20,6 +20,7 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "ncc_native.cpp")]
+COMMON_HEADERS = [os.path.join(HERE, "common", f) for f in ("byte_scan.hpp",)]  # shared with the executor
 
 
 def _werror() -> list:
@@ -52,7 +53,7 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
     if os.path.exists(out) and os.path.exists(stamp):
         with open(stamp) as f:
             same = f.read().strip() == flavor
-        if same and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in sources + [__file__]):
+        if same and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in sources + COMMON_HEADERS + [__file__]):
             return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
@@ -104,10 +105,11 @@ def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool =
         so_m = os.path.getmtime(out)
         with open(stamp) as f:
             same = f.read().strip() == flavor
-        if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + [__file__]):
+        if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + COMMON_HEADERS + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
-    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra",
+    # -mpopcnt: the shared JSON block scanner counts bracket bits (native/common/byte_scan.hpp)
+    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-mpopcnt", "-Wall", "-Wextra",
              "-Wno-unused-parameter"] + _werror()
     if debug or sanitize:
         flags += ["-O1", "-g", "-fno-omit-frame-pointer"]

@@ -20,146 +20,9 @@
 #include <vector>
 #include <charconv>
 #include <system_error>
-#include <emmintrin.h>
+#include "../common/byte_scan.hpp"
 
 namespace ncc {
-
-// ------------------------------------------------------------------------------------ byte search
-// 16 bytes per step (SSE2, part of every x86-64): JSON text is mostly string content and structure-free runs.
-// The first '"' or '\\' in [p, e), or e.
-inline const char* find_quote(const char* p, const char* e) {
-    const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\');
-    while (e - p >= 16) {
-        __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
-        int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, b)));
-        if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
-        p += 16;
-    }
-    while (p < e && *p != '"' && *p != '\\') ++p;
-    return p;
-}
-// The first '"', '{', '}', '[' or ']' in [p, e), or e ('[' | 0x20 == '{', ']' | 0x20 == '}').
-inline const char* find_structural(const char* p, const char* e) {
-    const __m128i q = _mm_set1_epi8('"'), lo = _mm_set1_epi8(0x20), open = _mm_set1_epi8('{'),
-                  close = _mm_set1_epi8('}');
-    while (e - p >= 16) {
-        __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
-        __m128i f = _mm_or_si128(x, lo);
-        int m = _mm_movemask_epi8(
-            _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_or_si128(_mm_cmpeq_epi8(f, open), _mm_cmpeq_epi8(f, close))));
-        if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
-        p += 16;
-    }
-    while (p < e && *p != '"' && (*p | 0x20) != '{' && (*p | 0x20) != '}') ++p;
-    return p;
-}
-// Past the string whose opening quote is at p (escapes skipped, not checked); nullptr when unterminated.
-inline const char* skip_string_text(const char* p, const char* e) {
-    ++p;
-    while (true) {
-        p = find_quote(p, e);
-        if (p >= e) return nullptr;
-        if (*p == '"') return p + 1;
-        p += 2;  // the escaped character
-    }
-}
-// 64 bytes as bit masks: bit i of each mask describes p[i]
-struct Block64 {
-    uint64_t quote, backslash, open, close;
-    explicit Block64(const char* p) {
-        const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lo = _mm_set1_epi8(0x20),
-                      op = _mm_set1_epi8('{'), cl = _mm_set1_epi8('}');
-        quote = backslash = open = close = 0;
-        for (int i = 0; i < 4; ++i) {
-            __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * i));
-            __m128i f = _mm_or_si128(x, lo);  // '[' | 0x20 == '{', ']' | 0x20 == '}'
-            int sh = 16 * i;
-            quote |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(x, q)))) << sh;
-            backslash |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(x, bs)))) << sh;
-            open |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(f, op)))) << sh;
-            close |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(f, cl)))) << sh;
-        }
-    }
-};
-inline uint64_t prefix_xor(uint64_t x) {
-    x ^= x << 1;
-    x ^= x << 2;
-    x ^= x << 4;
-    x ^= x << 8;
-    x ^= x << 16;
-    x ^= x << 32;
-    return x;
-}
-// Past the object or array whose bracket is at p; nullptr when unbalanced.  64 bytes per step while a block
-// has no backslash: the in-string mask is the prefix XOR of the quote bits, brackets outside strings move the
-// depth, and only a block where the depth could reach zero has its brackets walked one by one.  A block with
-// a backslash (or a string escape carried into it) is read byte by byte.
-inline const char* skip_container_text(const char* p, const char* e) {
-    int depth = 0;
-    bool in_str = false, esc = false;
-    while (e - p >= 64) {
-        Block64 b(p);
-        if (b.backslash == 0 && !esc) {
-            uint64_t str = prefix_xor(b.quote) ^ (in_str ? ~0ULL : 0ULL);  // 1 = inside a string (open quote incl.)
-            uint64_t op = b.open & ~str, cl = b.close & ~str;
-            int ncl = __builtin_popcountll(cl);
-            if (depth > ncl) {
-                depth += __builtin_popcountll(op) - ncl;
-            } else {
-                uint64_t br = op | cl;
-                while (br) {
-                    int i = __builtin_ctzll(br);
-                    br &= br - 1;
-                    if ((op >> i) & 1) {
-                        ++depth;
-                    } else if (--depth == 0) {
-                        return p + i + 1;
-                    }
-                }
-            }
-            in_str = (str >> 63) & 1;
-            p += 64;
-            continue;
-        }
-        for (const char* end = p + 64; p < end; ++p) {
-            char c = *p;
-            if (in_str) {
-                if (esc) {
-                    esc = false;
-                } else if (c == '\\') {
-                    esc = true;
-                } else if (c == '"') {
-                    in_str = false;
-                }
-            } else if (c == '"') {
-                in_str = true;
-            } else if ((c | 0x20) == '{') {
-                ++depth;
-            } else if ((c | 0x20) == '}') {
-                if (--depth == 0) return p + 1;
-            }
-        }
-    }
-    for (; p < e; ++p) {
-        char c = *p;
-        if (in_str) {
-            if (esc) {
-                esc = false;
-            } else if (c == '\\') {
-                esc = true;
-            } else if (c == '"') {
-                in_str = false;
-            }
-        } else if (c == '"') {
-            in_str = true;
-        } else if ((c | 0x20) == '{') {
-            ++depth;
-        } else if ((c | 0x20) == '}') {
-            if (--depth == 0) return p + 1;
-        }
-    }
-    return nullptr;
-}
 
 struct JsonError : std::runtime_error {
     using std::runtime_error::runtime_error;

@@ -35,6 +35,8 @@
 //    (metadata without managedFields, status, and a spec reduced to its references + raw digest).
 //  * ReportTable — the coordinator's fold of shard-executor reports, fed raw IPC frames.
 
+#include "common/byte_scan.hpp"
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -57,7 +59,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 20
+#define NCC_NATIVE_ABI 21
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -475,54 +477,29 @@ class Scanner {
         ws();
         if (p_ >= e_ || *p_ != '"') return false;
         const char* s = ++p_;
-        while (p_ < e_ && *p_ != '"') {
-            if (*p_ == '\\') return false;
-            ++p_;
-        }
-        if (p_ >= e_) return false;
+        p_ = ncc::find_quote(p_, e_);
+        if (p_ >= e_ || *p_ == '\\') return false;
         out = std::string_view(s, static_cast<size_t>(p_ - s));
         ++p_;
         return true;
     }
     bool skip_string() {
         if (p_ >= e_ || *p_ != '"') return false;
-        ++p_;
-        while (p_ < e_) {
-            if (*p_ == '\\') {
-                p_ += 2;
-                continue;
-            }
-            if (*p_ == '"') {
-                ++p_;
-                return true;
-            }
-            ++p_;
-        }
-        return false;
+        const char* q = ncc::skip_string_text(p_, e_);
+        if (q == nullptr) return false;
+        p_ = q;
+        return true;
     }
     bool skip_value() {
         ws();
         if (p_ >= e_) return false;
         char c = *p_;
         if (c == '"') return skip_string();
-        if (c == '{' || c == '[') {
-            int depth = 0;
-            while (p_ < e_) {
-                char d = *p_;
-                if (d == '"') {
-                    if (!skip_string()) return false;
-                    continue;
-                }
-                if (d == '{' || d == '[') ++depth;
-                else if (d == '}' || d == ']') {
-                    if (--depth == 0) {
-                        ++p_;
-                        return true;
-                    }
-                }
-                ++p_;
-            }
-            return false;
+        if (c == '{' || c == '[') {  // 64 bytes per step (native/common/byte_scan.hpp)
+            const char* q = ncc::skip_container_text(p_, e_);
+            if (q == nullptr) return false;
+            p_ = q;
+            return true;
         }
         while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n' &&
                *p_ != '\t' && *p_ != '\r')
@@ -1221,6 +1198,11 @@ class PyJson {
   public:
     PyJson(const char* p, size_t n) : p_(p), e_(p + n) {}
 
+    // template_event_slim with a cache: `items` (borrowed; the informer store's dict keyed (namespace, name))
+    // lets an unchanged status, or unchanged references, be taken from the cached version instead of decoded
+    PyObject* items_ = nullptr;
+    std::string default_ns_;
+
     // New reference, or nullptr: parse error (no Python exception set) or allocation failure (set).
     PyObject* value(int depth = 0) {
         ws();
@@ -1282,6 +1264,60 @@ class PyJson {
     const char* p_;
     const char* e_;
     std::string tmp_;
+    PyObject* prev_ = nullptr;  // borrowed: the cached version of the object being decoded, if any
+
+    // After the metadata: find the cached version of this object (items_[(namespace, name)]).
+    void find_prev(PyObject* md) {
+        prev_ = nullptr;
+        if (items_ == nullptr || md == nullptr || !PyDict_Check(md)) return;
+        PyObject* name = PyDict_GetItemString(md, "name");
+        PyObject* ns = PyDict_GetItemString(md, "namespace");
+        if (name == nullptr) return;
+        PyObject* nso = nullptr;
+        if (ns == nullptr || (PyUnicode_Check(ns) && PyUnicode_GET_LENGTH(ns) == 0)) {
+            nso = PyUnicode_FromStringAndSize(default_ns_.data(), static_cast<Py_ssize_t>(default_ns_.size()));
+            if (nso == nullptr) {
+                PyErr_Clear();
+                return;
+            }
+            ns = nso;
+        }
+        PyObject* key = PyTuple_Pack(2, ns, name);
+        Py_XDECREF(nso);
+        if (key == nullptr) {
+            PyErr_Clear();
+            return;
+        }
+        PyObject* cur = PyDict_GetItemWithError(items_, key);
+        Py_DECREF(key);
+        if (cur == nullptr) {
+            PyErr_Clear();
+            return;
+        }
+        if (PyDict_Check(cur)) prev_ = cur;
+    }
+    // The value at p_ when its text hashes to `want` (the cached version's digest of it): `reuse` (new
+    // reference) and *fp set, p_ past the value.  Otherwise p_ stays and nullptr is returned (*fp set when the
+    // value could be skipped).
+    PyObject* reuse_if_same(PyObject* want, PyObject* reuse, uint64_t* fp) {
+        ws();
+        const char* s0 = p_;
+        if (!skip_value()) {
+            p_ = s0;
+            return nullptr;
+        }
+        Hasher h;
+        h.bytes(s0, static_cast<size_t>(p_ - s0));
+        *fp = h.digest();
+        if (want != nullptr && reuse != nullptr && PyLong_Check(want) &&
+            PyLong_AsUnsignedLongLong(want) == *fp && !PyErr_Occurred()) {
+            Py_INCREF(reuse);
+            return reuse;
+        }
+        PyErr_Clear();
+        p_ = s0;
+        return nullptr;
+    }
 
     void ws() {
         while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
@@ -1338,11 +1374,8 @@ class PyJson {
         ws();
         if (p_ >= e_ || *p_ != '"') return false;
         const char* s = ++p_;
-        while (p_ < e_ && *p_ != '"' && *p_ != '\\') {
-            if (static_cast<unsigned char>(*p_) < 0x20) return false;
-            ++p_;
-        }
-        if (p_ >= e_) return false;
+        p_ = ncc::find_quote_or_ctl(p_, e_);
+        if (p_ >= e_ || static_cast<unsigned char>(*p_) < 0x20) return false;
         if (*p_ == '"') {
             out = std::string_view(s, static_cast<size_t>(p_ - s));
             ++p_;
@@ -1529,25 +1562,11 @@ class PyJson {
             std::string_view v;
             return raw_string(v);
         }
-        if (c == '{' || c == '[') {
-            int depth = 0;
-            while (p_ < e_) {
-                char d = *p_;
-                if (d == '"') {
-                    std::string_view v;
-                    if (!raw_string(v)) return false;
-                    continue;
-                }
-                if (d == '{' || d == '[') ++depth;
-                else if (d == '}' || d == ']') {
-                    if (--depth == 0) {
-                        ++p_;
-                        return true;
-                    }
-                }
-                ++p_;
-            }
-            return false;
+        if (c == '{' || c == '[') {  // a skipped member (managedFields) is not validated
+            const char* q = ncc::skip_container_text(p_, e_);
+            if (q == nullptr) return false;
+            p_ = q;
+            return true;
         }
         const char* s = p_;
         while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n' && *p_ != '\t' &&
@@ -1671,13 +1690,26 @@ class PyJson {
                             if (!raw_key(k2)) { ok = false; break; }
                             if (k2 == "mappedEnvironmentVariables") {
                                 Py_XDECREF(env);
-                                ws();
-                                const char* e0 = p_;
-                                env = mapped_env();
-                                if (env == nullptr) { ok = false; break; }
-                                Hasher he;
-                                he.bytes(e0, static_cast<size_t>(p_ - e0));
-                                env_fp = he.digest();
+                                env = nullptr;
+                                if (prev_ != nullptr) {  // unchanged references: the cached version's list
+                                    PyObject* ps = PyDict_GetItemString(prev_, "spec");
+                                    PyObject* prt = ps != nullptr && PyDict_Check(ps)
+                                                        ? PyDict_GetItemString(ps, "runtimeEnvironment") : nullptr;
+                                    PyObject* penv = prt != nullptr && PyDict_Check(prt)
+                                                         ? PyDict_GetItemString(prt, "mappedEnvironmentVariables")
+                                                         : nullptr;
+                                    if (penv != nullptr)
+                                        env = reuse_if_same(PyDict_GetItemString(ps, "_rfp"), penv, &env_fp);
+                                }
+                                if (env == nullptr) {
+                                    ws();
+                                    const char* e0 = p_;
+                                    env = mapped_env();
+                                    if (env == nullptr) { ok = false; break; }
+                                    Hasher he;
+                                    he.bytes(e0, static_cast<size_t>(p_ - e0));
+                                    env_fp = he.digest();
+                                }
                             } else if (!skip_value()) {
                                 ok = false;
                                 break;
@@ -1741,15 +1773,28 @@ class PyJson {
                 v = slim_spec();
             } else if (key == "metadata" && peek('{')) {
                 v = object(1, "managedFields");
+                find_prev(v);
             } else if (key == "status") {
-                // and a digest of the status text under "__ncc_sfp__": an unchanged status compares as one int
-                ws();
-                const char* s0 = p_;
-                v = value(1);
+                // and a digest of the status text under "__ncc_sfp__": an unchanged status compares as one int,
+                // and is taken from the cached version instead of decoded again
+                uint64_t fp = 0;
+                v = nullptr;
+                if (prev_ != nullptr) {
+                    PyObject* pst = PyDict_GetItemString(prev_, "status");
+                    if (pst != nullptr) v = reuse_if_same(PyDict_GetItemString(prev_, "__ncc_sfp__"), pst, &fp);
+                }
+                if (v == nullptr) {
+                    ws();
+                    const char* s0 = p_;
+                    v = value(1);
+                    if (v != nullptr) {
+                        Hasher hs;
+                        hs.bytes(s0, static_cast<size_t>(p_ - s0));
+                        fp = hs.digest();
+                    }
+                }
                 if (v != nullptr) {
-                    Hasher hs;
-                    hs.bytes(s0, static_cast<size_t>(p_ - s0));
-                    PyObject* sfp = PyLong_FromUnsignedLongLong(hs.digest());
+                    PyObject* sfp = PyLong_FromUnsignedLongLong(fp);
                     if (sfp == nullptr || PyDict_SetItemString(d, "__ncc_sfp__", sfp) != 0) {
                         Py_XDECREF(sfp);
                         Py_DECREF(v);
@@ -1804,9 +1849,14 @@ py::object loads(py::bytes data) {
 }
 
 // template_event_slim(line) -> (type, slim object) | None
-py::object template_event_slim(py::bytes line) {
+py::object template_event_slim(py::bytes line, py::object items, const std::string& default_ns) {
     std::string_view v = bytes_view(line);
     PyJson pj(v.data(), v.size());
+    if (!items.is_none()) {
+        if (!PyDict_Check(items.ptr())) throw py::type_error("template_event_slim: items must be a dict");
+        pj.items_ = items.ptr();
+        pj.default_ns_ = default_ns;
+    }
     PyObject* o = pj.template_event();
     if (o == nullptr) {
         if (PyErr_Occurred()) throw py::error_already_set();
@@ -2291,8 +2341,10 @@ PYBIND11_MODULE(_native, m) {
     m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
           "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");
     m.def("loads", &loads, py::arg("data"), "JSON bytes -> Python value, or None when malformed");
-    m.def("template_event_slim", &template_event_slim, py::arg("line"),
-          "template watch line -> (type, object with metadata/status decoded and the spec slimmed) | None");
+    m.def("template_event_slim", &template_event_slim, py::arg("line"), py::arg("items") = py::none(),
+          py::arg("default_ns") = std::string(),
+          "template watch line -> (type, object with metadata/status decoded and the spec slimmed) | None; "
+          "with `items` (the store's dict) an unchanged status or reference list is taken from the cached version");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")

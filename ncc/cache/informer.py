@@ -139,7 +139,8 @@ class Informer:
         self.tap = None
         self.feed = None
         # Optional native decoder for watch lines returning (type, object) or None (then the full decode):
-        # the coordinator's template informer keeps slim templates (`_native.template_event_slim`).
+        # the coordinator's template informer keeps slim templates (`_native.template_event_slim`; called as
+        # slim_decode(line, store items, default namespace) so unchanged parts come from the cached version).
         self.slim_decode = None
 
     # ------------------------------------------------------------- public API
@@ -372,7 +373,7 @@ class Informer:
                 prev = stash.pop(ObjectKey(sc[1] or default_ns, sc[2]), None)
                 if prev is not None:  # keep per-key order
                     await self._apply_line(prev[1])
-            sl = slim(line) if slim is not None else None
+            sl = slim(line, store._items, default_ns) if slim is not None else None
             if sl is not None:
                 rv = await self._handle(sl[0], sl[1], rv)
                 continue
@@ -417,7 +418,7 @@ class Informer:
             self.store.delete(ObjectKey(ns, name))  # left our partition: forget it (no handler dispatch)
 
     async def _apply_line(self, line: bytes) -> None:
-        sl = self.slim_decode(line) if self.slim_decode is not None else None
+        sl = self.slim_decode(line, self.store._items, self.namespace or "") if self.slim_decode is not None else None
         if sl is not None:
             await self._apply(sl[0], sl[1])
             return

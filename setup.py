@@ -29,5 +29,6 @@ class BuildWithExecutor(build_ext):
 
 setup(ext_modules=[Pybind11Extension(
     "ncc._native", ["native/ncc_native.cpp"], cxx_std=17,
-    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter"])],
+    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", "-mpopcnt", "-Wall", "-Wextra",
+                        "-Wno-unused-parameter"])],
     cmdclass={"build_ext": BuildWithExecutor})

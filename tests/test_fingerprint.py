@@ -160,3 +160,34 @@ def test_template_event_slim_keeps_what_the_coordinator_reads():
         == ([], [])
     for bad in [b"", b"{}", b'{"type": "ADDED"}', b'{"type": "ADDED", "object": {"spec": [}}', line[:-1]]:
         assert NATIVE.template_event_slim(bad) is None
+
+
+@pytest.mark.skipif(NATIVE is None, reason="native extension not built")
+def test_template_event_slim_reuses_unchanged_parts_of_the_cached_version():
+    """With the store's items, an unchanged status and an unchanged reference list are the cached version's
+    objects (not decoded again); a changed one is decoded; the result equals the uncached decode either way."""
+    from ncc.testing.workload import make_template
+    t = make_template(5, "nexus", secrets=["s1"], configmaps=["c1"], version="v1")
+    t["metadata"].update(uid="u-5", resourceVersion="10", generation=1)
+    t["status"] = {"conditions": [{"type": "Ready", "status": "True"}], "syncedSecrets": ["s1"]}
+    line = lambda: json.dumps({"type": "MODIFIED", "object": t}).encode()  # noqa: E731
+    first = NATIVE.template_event_slim(line())[1]
+    items = {("nexus", t["metadata"]["name"]): first}
+    t["metadata"]["resourceVersion"] = "11"
+    t["spec"]["container"]["versionTag"] = "v2"
+    second = NATIVE.template_event_slim(line(), items, "")[1]
+    assert second == NATIVE.template_event_slim(line())[1]
+    assert second["status"] is first["status"]
+    env = "runtimeEnvironment", "mappedEnvironmentVariables"
+    assert second["spec"][env[0]][env[1]] is first["spec"][env[0]][env[1]]
+    assert second["spec"]["_fp"] != first["spec"]["_fp"]
+    t["status"]["syncedSecrets"] = []
+    t["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"].append({"prefix": "Y_"})
+    third = NATIVE.template_event_slim(line(), {("nexus", t["metadata"]["name"]): second}, "")[1]
+    assert third == NATIVE.template_event_slim(line())[1]
+    assert third["status"] is not second["status"] and third["status"]["syncedSecrets"] == []
+    assert third["spec"]["_rfp"] != second["spec"]["_rfp"]
+    # the namespace defaults when the object carries none
+    del t["metadata"]["namespace"]
+    fourth = NATIVE.template_event_slim(line(), {("nexus", t["metadata"]["name"]): third}, "nexus")[1]
+    assert fourth["status"] is third["status"]
