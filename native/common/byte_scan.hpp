@@ -1,10 +1,13 @@
 // JSON byte scanning shared by the C++ shard executor (native/executor/json.hpp) and the Python extension
 // (native/ncc_native.cpp): SSE2 (part of every x86-64) searches for quotes and brackets, and a container skip
-// that goes 64 bytes per step.  Only valid JSON text is expected; a skipped container is not validated.
+// that goes 64 bytes per step; other targets get the same functions a byte at a time.  Only valid JSON text
+// is expected; a skipped container is not validated.
 #pragma once
 
 #include <cstdint>
+#if defined(__SSE2__)
 #include <emmintrin.h>
+#endif
 
 namespace ncc {
 
@@ -12,6 +15,7 @@ namespace ncc {
 // 16 bytes per step (SSE2, part of every x86-64): JSON text is mostly string content and structure-free runs.
 // The first '"' or '\\' in [p, e), or e.
 inline const char* find_quote(const char* p, const char* e) {
+#if defined(__SSE2__)
     const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\');
     while (e - p >= 16) {
         __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
@@ -19,11 +23,13 @@ inline const char* find_quote(const char* p, const char* e) {
         if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
         p += 16;
     }
+#endif
     while (p < e && *p != '"' && *p != '\\') ++p;
     return p;
 }
 // The first '"', '{', '}', '[' or ']' in [p, e), or e ('[' | 0x20 == '{', ']' | 0x20 == '}').
 inline const char* find_structural(const char* p, const char* e) {
+#if defined(__SSE2__)
     const __m128i q = _mm_set1_epi8('"'), lo = _mm_set1_epi8(0x20), open = _mm_set1_epi8('{'),
                   close = _mm_set1_epi8('}');
     while (e - p >= 16) {
@@ -34,6 +40,7 @@ inline const char* find_structural(const char* p, const char* e) {
         if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
         p += 16;
     }
+#endif
     while (p < e && *p != '"' && (*p | 0x20) != '{' && (*p | 0x20) != '}') ++p;
     return p;
 }
@@ -51,9 +58,10 @@ inline const char* skip_string_text(const char* p, const char* e) {
 struct Block64 {
     uint64_t quote, backslash, open, close;
     explicit Block64(const char* p) {
+        quote = backslash = open = close = 0;
+#if defined(__SSE2__)
         const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lo = _mm_set1_epi8(0x20),
                       op = _mm_set1_epi8('{'), cl = _mm_set1_epi8('}');
-        quote = backslash = open = close = 0;
         for (int i = 0; i < 4; ++i) {
             __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * i));
             __m128i f = _mm_or_si128(x, lo);  // '[' | 0x20 == '{', ']' | 0x20 == '}'
@@ -63,6 +71,16 @@ struct Block64 {
             open |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(f, op)))) << sh;
             close |= static_cast<uint64_t>(static_cast<uint16_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(f, cl)))) << sh;
         }
+#else  // portable: the same masks a byte at a time
+        for (int i = 0; i < 64; ++i) {
+            char c = p[i], f = static_cast<char>(c | 0x20);
+            uint64_t bit = 1ULL << i;
+            if (c == '"') quote |= bit;
+            if (c == '\\') backslash |= bit;
+            if (f == '{') open |= bit;
+            if (f == '}') close |= bit;
+        }
+#endif
     }
 };
 inline uint64_t prefix_xor(uint64_t x) {
@@ -147,6 +165,7 @@ inline const char* skip_container_text(const char* p, const char* e) {
 
 // The first '"', '\\' or control byte (< 0x20, invalid inside a JSON string) in [p, e), or e.
 inline const char* find_quote_or_ctl(const char* p, const char* e) {
+#if defined(__SSE2__)
     const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\'), c = _mm_set1_epi8(0x1F);
     while (e - p >= 16) {
         __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
@@ -155,6 +174,7 @@ inline const char* find_quote_or_ctl(const char* p, const char* e) {
         if (m) return p + __builtin_ctz(static_cast<unsigned>(m));
         p += 16;
     }
+#endif
     while (p < e && *p != '"' && *p != '\\' && static_cast<unsigned char>(*p) >= 0x20) ++p;
     return p;
 }
