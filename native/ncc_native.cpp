@@ -59,7 +59,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 21
+#define NCC_NATIVE_ABI 22
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -2183,8 +2183,151 @@ class ReportTable {
         return py::bool_(ok);
     }
 
+    // finish_batch(keys, items, assumed, adopted, memos, shards, queue, pending_event, event_on_noop)
+    //     -> (rest, verify, events, done, superseded)
+    // The coordinator's inline finish (ncc/controller/reconcile.py `finish_inline_many`, the specification) over
+    // a batch of template keys whose report sets completed, read straight off the Python state it uses:
+    // `items`/`assumed` the template store's dict and mutation overlay, `adopted` key -> adopted resourceVersion,
+    // `memos` key -> (status digest, references digest, shard list) of the last verified status, `queue` the
+    // work queue core (busy keys need a pass), `pending_event` the keys owing a Synced Event.  Per key: `rest`
+    // (a queued pass is needed), `verify` (the Python path decides: an overlaid object, a non-slim template, no
+    // memo for this status), `events` (finished, the template whose Synced Event is due), `done` finished
+    // without an Event, or `superseded` (a newer version reached the cache: its own last report brings it back).
+    py::tuple finish_batch(py::iterable keys, py::dict items, py::dict assumed, py::dict adopted, py::dict memos,
+                           py::object shards, py::object queue, py::set pending_event, bool event_on_noop) const {
+        static PyObject* k_status = PyUnicode_InternFromString("status");
+        static PyObject* k_conditions = PyUnicode_InternFromString("conditions");
+        static PyObject* k_metadata = PyUnicode_InternFromString("metadata");
+        static PyObject* k_rv = PyUnicode_InternFromString("resourceVersion");
+        static PyObject* k_uid = PyUnicode_InternFromString("uid");
+        static PyObject* k_gen = PyUnicode_InternFromString("generation");
+        static PyObject* k_sfp = PyUnicode_InternFromString("__ncc_sfp__");
+        static PyObject* k_spec = PyUnicode_InternFromString("spec");
+        static PyObject* k_rfp = PyUnicode_InternFromString("_rfp");
+        RateLimitingQueue* nq = nullptr;
+        if (py::isinstance<RateLimitingQueue>(queue)) nq = &queue.cast<RateLimitingQueue&>();
+        py::list rest, verify, events;
+        long long done = 0, superseded = 0;
+        std::string k;
+        const bool overlay = PyDict_GET_SIZE(assumed.ptr()) > 0;
+        for (py::handle kh : keys) {
+            PyObject* key = kh.ptr();
+            Py_ssize_t klen = 0;
+            const char* kc = PyUnicode_Check(key) ? PyUnicode_AsUTF8AndSize(key, &klen) : nullptr;
+            if (kc == nullptr) {
+                PyErr_Clear();
+                verify.append(kh);
+                continue;
+            }
+            k.assign(kc, static_cast<size_t>(klen));
+            size_t a = k.find('/'), b = a == std::string::npos ? a : k.find('/', a + 1);
+            bool is_busy = nq != nullptr ? nq->busy(k) : queue.attr("busy")(kh).cast<bool>();
+            if (b == std::string::npos || k.compare(0, a, "template") != 0 || is_busy) {
+                rest.append(kh);
+                continue;
+            }
+            py::tuple ik = py::make_tuple(py::str(kc + a + 1, b - a - 1), py::str(kc + b + 1, k.size() - b - 1));
+            if (overlay && PyDict_Contains(assumed.ptr(), ik.ptr()) == 1) {
+                verify.append(kh);
+                continue;
+            }
+            PyObject* t = PyDict_GetItem(items.ptr(), ik.ptr());
+            if (t == nullptr || !PyDict_Check(t)) {
+                rest.append(kh);
+                continue;
+            }
+            PyObject* st = PyDict_GetItem(t, k_status);
+            PyObject* conds = st != nullptr && PyDict_Check(st) ? PyDict_GetItem(st, k_conditions) : nullptr;
+            PyObject* m = PyDict_GetItem(t, k_metadata);
+            if (m == nullptr || !PyDict_Check(m)) m = nullptr;
+            int conds_true = conds == nullptr ? 0 : PyObject_IsTrue(conds);
+            if (conds_true < 0) throw py::error_already_set();
+            PyObject* rv = m != nullptr ? PyDict_GetItem(m, k_rv) : nullptr;
+            PyObject* ad = PyDict_GetItem(adopted.ptr(), key);
+            int ne = PyObject_RichCompareBool(ad != nullptr ? ad : Py_None, rv != nullptr ? rv : Py_None, Py_NE);
+            if (ne < 0) throw py::error_already_set();
+            if (!conds_true || ne) {
+                rest.append(kh);
+                continue;
+            }
+            PyObject* uid = m != nullptr ? PyDict_GetItem(m, k_uid) : nullptr;
+            PyObject* gen = m != nullptr ? PyDict_GetItem(m, k_gen) : nullptr;
+            std::string uid_s;
+            if (uid != nullptr && uid != Py_None) {
+                Py_ssize_t ul = 0;
+                const char* uc = PyUnicode_Check(uid) ? PyUnicode_AsUTF8AndSize(uid, &ul) : nullptr;
+                if (uc == nullptr) {
+                    PyErr_Clear();
+                    verify.append(kh);
+                    continue;
+                }
+                uid_s.assign(uc, static_cast<size_t>(ul));
+            }
+            int64_t g = 0;
+            if (gen != nullptr && gen != Py_None) {
+                if (!PyLong_Check(gen)) {
+                    verify.append(kh);
+                    continue;
+                }
+                g = PyLong_AsLongLong(gen);
+                if (g == -1 && PyErr_Occurred()) {
+                    PyErr_Clear();
+                    verify.append(kh);
+                    continue;
+                }
+            }
+            int ok = ready(k, uid_s, g);
+            if (ok < 0) {
+                ++superseded;
+                continue;
+            }
+            if (ok == 0) {
+                rest.append(kh);
+                continue;
+            }
+            PyObject* sfp = PyDict_GetItem(t, k_sfp);
+            PyObject* spec = PyDict_GetItem(t, k_spec);
+            PyObject* rfp = spec != nullptr && PyDict_Check(spec) ? PyDict_GetItem(spec, k_rfp) : nullptr;
+            PyObject* memo = PyDict_GetItem(memos.ptr(), key);
+            bool hit = sfp != nullptr && rfp != nullptr && memo != nullptr && PyTuple_Check(memo) &&
+                       PyTuple_GET_SIZE(memo) == 3 && PyTuple_GET_ITEM(memo, 2) == shards.ptr();
+            if (hit) {
+                int e0 = PyObject_RichCompareBool(PyTuple_GET_ITEM(memo, 0), sfp, Py_EQ);
+                int e1 = e0 == 1 ? PyObject_RichCompareBool(PyTuple_GET_ITEM(memo, 1), rfp, Py_EQ) : 0;
+                if (e0 < 0 || e1 < 0) throw py::error_already_set();
+                hit = e0 == 1 && e1 == 1;
+            }
+            if (!hit) {
+                verify.append(kh);
+                continue;
+            }
+            int pend = PySet_Contains(pending_event.ptr(), key);
+            if (pend < 0) throw py::error_already_set();
+            if (pend || event_on_noop) {
+                if (pend && PySet_Discard(pending_event.ptr(), key) < 0) throw py::error_already_set();
+                events.append(py::handle(t));
+            } else {
+                ++done;
+            }
+        }
+        return py::make_tuple(rest, verify, events, done, superseded);
+    }
+
   private:
     static constexpr uint32_t kMaxFrame = 64u * 1024 * 1024;  // ipc.MAX_FRAME
+
+    // ready_ok without Python objects: -1 some shard has not reported on this version, 0 a failure, 1 all ok
+    int ready(const std::string& key, const std::string& uid, int64_t gen) const {
+        auto it = state_.find(key);
+        if (it == state_.end()) return -1;
+        bool ok = true;
+        for (const auto& s : shards_) {
+            const Slot* e = find(it->second, s);
+            if (e == nullptr || e->uid != uid || e->gen < gen) return -1;
+            ok = ok && e->err.empty();
+        }
+        return ok ? 1 : 0;
+    }
 
     void fold_frame(const char* p, size_t len, bool batch, Folded& f) {
         MpReader r(p, len);
@@ -2377,6 +2520,9 @@ PYBIND11_MODULE(_native, m) {
              "fold every complete frame of a byte stream from `start`: feed()'s tuple + the end offset")
         .def("readiness", &ReportTable::readiness, py::arg("key"), py::arg("uid"), py::arg("generation"))
         .def("ready_ok", &ReportTable::ready_ok, py::arg("key"), py::arg("uid"), py::arg("generation"))
+        .def("finish_batch", &ReportTable::finish_batch, py::arg("keys"), py::arg("items"), py::arg("assumed"),
+             py::arg("adopted"), py::arg("memos"), py::arg("shards"), py::arg("queue"), py::arg("pending_event"),
+             py::arg("event_on_noop"))
         .def("pop", &ReportTable::pop, py::arg("key"))
         .def("set_partition", &ReportTable::set_partition, py::arg("part"), py::arg("parts"))
         .def("take_forwards", &ReportTable::take_forwards)

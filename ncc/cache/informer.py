@@ -306,6 +306,7 @@ class Informer:
         default_ns = self.namespace or ""
         inflight, stash = self._inflight, self._stash
         sigs = self._owner_sigs
+        unfiltered = self.key_filter is None and self.owner_filter is None
         last = None
         if mo and not nparts and kf is None and of is None and _owner_filter is not None:
             # the whole batch through the native owner filter; what it keeps takes the path below
@@ -375,6 +376,25 @@ class Informer:
                     await self._apply_line(prev[1])
             sl = slim(line, store._items, default_ns) if slim is not None else None
             if sl is not None:
+                if sl[0] == "MODIFIED" and not unfiltered:
+                    rv = await self._handle(sl[0], sl[1], rv)
+                    continue
+                if sl[0] == "MODIFIED":
+                    # _handle → _apply → _dispatch_update inlined for the common case (no coroutine per layer)
+                    obj = sl[1]
+                    self.events += 1
+                    stored, old = store.upsert(obj)
+                    if old is None:
+                        await self._dispatch_add(stored)
+                    else:
+                        for h in self._handlers:
+                            fn = h.on_update
+                            if fn is not None:
+                                r = fn(old, stored)
+                                if r is not None and inspect.isawaitable(r):
+                                    await r
+                    rv = self.last_rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
+                    continue
                 rv = await self._handle(sl[0], sl[1], rv)
                 continue
             ev = loads(line)

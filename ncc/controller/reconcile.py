@@ -469,10 +469,35 @@ class ReconcileMixin:
         return not self.finish_inline_many((key,))
 
     def finish_inline_many(self, keys) -> list:
-        """`finish_inline` over a batch of keys (the loop invariants read once); returns the keys that need a
-        real pass."""
+        """`finish_inline` over a batch of keys; returns the keys that need a real pass.  The native report
+        table decides the common case (a slim template whose status was verified before) without running
+        Python per key; what it cannot decide goes through `_finish_inline_py`, the specification."""
         if not self.ready.is_set() or self.queue.shutting_down() or not self.options.adoption_cache:
             return list(keys)  # workers not running (standby, shutdown, lost Lease): nothing may be written
+        fb = getattr(self.reports, "finish_batch", None)
+        core = getattr(self.queue, "core", None)
+        if fb is None or core is None:
+            return self._finish_inline_py(keys)
+        store = self.template_informer.store
+        rest, verify, events, done, superseded = fb(
+            keys, store._items, store._assumed, self._adopted, self._inline_status_ok, self.all_shard_names, core,
+            self._pending_event, self.options.event_on_noop)
+        st = self.stats
+        st["inline_superseded"] += superseded
+        done += len(events)
+        for template in events:
+            self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
+                                C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND), kind=C.TEMPLATE_KIND)
+        if done:
+            st["reconciles"] += done
+            st["inline_finishes"] += done
+            self.metrics.gauge_duration(C.RECONCILE_LATENCY_METRIC, time.monotonic())
+        if verify:
+            rest.extend(self._finish_inline_py(verify))
+        return rest
+
+    def _finish_inline_py(self, keys) -> list:
+        """finish_inline_many, one key at a time in Python (the loop invariants read once)."""
         busy = self.queue.busy
         get = self.template_informer.store.get
         adopted = self._adopted

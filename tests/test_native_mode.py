@@ -635,3 +635,77 @@ def test_coalescing_starts_only_inside_a_burst(monkeypatch):
     assert delays[:ctl.BURST_MIN] == [0.0] * ctl.BURST_MIN and delays[ctl.BURST_MIN:] == [0.002] * 3
     now[0] += 0.01
     assert ctl._coalesce_delay() == 0.0
+
+
+class _NoBatch:
+    """The native report table without finish_batch: the controller takes the Python path."""
+
+    def __init__(self, table):
+        self._t = table
+
+    def __getattr__(self, name):
+        if name == "finish_batch":
+            raise AttributeError(name)
+        return getattr(self._t, name)
+
+
+@pytest.mark.parametrize("native_queue", [False, True])
+async def test_native_inline_finish_batch_matches_the_python_path(native_queue):
+    """ReportTable.finish_batch decides exactly what `_finish_inline_py` decides, key by key: finished (with
+    or without the Synced Event), a queued pass, superseded, or handed to the Python path (an overlaid object,
+    a status not verified before) — same return value, memos, pending Events, stats and recorded Events."""
+    import json as _json
+    from ncc import native
+    mod = native.load(required=True)
+    good_status = lambda name: {  # noqa: E731
+        "conditions": [{"type": "Ready", "status": "True", "lastTransitionTime": "2026-01-01T00:00:00Z",
+                        "reason": C.CONDITION_READY_REASON, "message": f'Algorithm "{name}" ready'}],
+        "syncedSecrets": ["s"], "syncedConfigurations": ["c"], "syncedToClusters": ["s0", "s1"]}
+
+    def slim_template(i, status):
+        t = make_template(i, NS, secrets=["s"], configmaps=["c"])
+        t["metadata"].update(uid=f"u{i}", resourceVersion=str(100 + i), generation=2)
+        t["status"] = status
+        return mod.template_event_slim(_json.dumps({"type": "MODIFIED", "object": t}).encode())[1]
+
+    def run(use_native):
+        env = Env(2)
+        env.opts.native_queue = native_queue
+        ctl = env.build(role="coordinator")
+        ctl.ready.set()
+        if not use_native:
+            ctl.reports = _NoBatch(ctl.reports)
+        store = ctl.template_informer.store
+        keys = []
+        for i in range(11):
+            name = make_template(i, NS)["metadata"]["name"]
+            key = make_key(C.KIND_TEMPLATE, NS, name)
+            keys.append(key)
+            bad = i == 7
+            obj = slim_template(i, dict(good_status(name), syncedToClusters=["s0"]) if bad else good_status(name))
+            if i != 9:  # 9: not in the cache
+                store.upsert(obj)
+            if i != 4:  # 4: not adopted at this version
+                ctl._adopted[key] = obj["metadata"]["resourceVersion"]
+            if i not in (6, 7):  # 6, 7: this status not verified before
+                ctl._inline_status_ok[key] = (obj["__ncc_sfp__"], obj["spec"]["_rfp"], ctl.all_shard_names)
+            shards = {"s0": None} if i == 2 else {"s0": None, "s1": "boom" if i == 3 else None}
+            ctl.reports.feed(msgpack.packb({"t": "report", "k": key, "u": f"u{i}", "g": 2, "r": shards,
+                                            "w": False}), False)
+            if i == 8:  # an overlaid (assumed) newer version
+                store.assume(dict(obj, metadata=dict(obj["metadata"], resourceVersion=str(500 + i))))
+        ctl._pending_event.update([keys[1], keys[6]])
+        ctl.queue.add(keys[5])  # 5: a pass is queued
+        keys.append(make_key(C.KIND_WORKGROUP, NS, "wg"))
+        rest = ctl.finish_inline_many(keys)
+        memo_keys = sorted(k for k in ctl._inline_status_ok)
+        st = {k: ctl.stats[k] for k in ("reconciles", "inline_finishes", "inline_superseded")}
+        return sorted(rest), memo_keys, sorted(ctl._pending_event), st, list(env.recorder.events)
+
+    native_result, python_result = run(True), run(False)
+    assert native_result == python_result
+    rest, memos, pending, st, events = native_result
+    # finished: 0, 1 (Event), 6 (verified now, Event), 10; superseded: 2; a pass: 3 (failure), 4 (not adopted),
+    # 5 (busy), 7 (status needs a write), 8 (the overlaid version is not the adopted one), 9 (missing), workgroup
+    assert st["inline_superseded"] == 1 and st["inline_finishes"] == 4 and len(events) == 2
+    assert len(rest) == 7 and not pending
