@@ -1379,15 +1379,17 @@ static std::vector<std::string> synced_keys(const Value* ann, std::string_view w
     std::string_view s = v->s;
     while (!s.empty()) {
         size_t semi = s.find(';');
-        std::string_view part = s.substr(0, semi);
-        size_t eq = part.find('=');
+        std::string_view part(s.data(), semi == std::string_view::npos ? s.size() : semi);
+        const void* eqp = part.empty() ? nullptr : std::memchr(part.data(), '=', part.size());
+        size_t eq = eqp == nullptr ? std::string_view::npos : static_cast<size_t>(static_cast<const char*>(eqp) - part.data());
         if (eq != std::string_view::npos && part.substr(0, eq) == what) {
             std::string_view keys = part.substr(eq + 1);
-            while (!keys.empty()) {
-                size_t comma = keys.find(',');
-                if (comma) out.emplace_back(keys.substr(0, comma));
-                if (comma == std::string_view::npos) break;
-                keys.remove_prefix(comma + 1);
+            size_t start = 0;
+            while (start < keys.size()) {
+                size_t comma = keys.find(',', start);
+                size_t end = comma == std::string_view::npos ? keys.size() : comma;
+                if (end > start) out.emplace_back(keys.data() + start, end - start);
+                start = end + 1;
             }
         }
         if (semi == std::string_view::npos) break;
