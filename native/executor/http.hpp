@@ -217,6 +217,25 @@ inline SSL_CTX* make_ssl_ctx(const Credentials& c) {
 }
 
 // ------------------------------------------------------------------------------------ connection
+class Conn;
+// The connections in use, for the deadline sweep: O(1) insert and erase through the slot each connection
+// keeps (a request adds and removes its connection once each; a tree or hash set costs more than the rest of
+// the bookkeeping of a request).
+class ConnSet {
+public:
+    ConnSet() = default;
+    ConnSet(const ConnSet&) = delete;
+    ConnSet& operator=(const ConnSet&) = delete;
+    inline ~ConnSet();
+    inline void insert(Conn* c);
+    inline void erase(Conn* c);
+    bool empty() const { return v_.empty(); }
+    std::vector<Conn*> snapshot() const { return v_; }
+
+private:
+    std::vector<Conn*> v_;
+};
+
 class Conn {
 public:
     int fd = -1;
@@ -225,8 +244,13 @@ public:
     size_t pos = 0;
     double deadline = 0;  // request deadline (pool sweep shuts the socket down when passed)
     bool drained = false;  // the last recv returned less than it asked for: the socket had nothing more
+    int busy_slot = -1;    // its index in the client's set of connections in use (ConnSet), or -1
+    ConnSet* busy_set = nullptr;  // that set: a connection destroyed while in use leaves it (no dangling entry)
 
-    ~Conn() { close(); }
+    ~Conn() {
+        if (busy_set != nullptr) busy_set->erase(this);
+        close();
+    }
     void close() {
         if (ssl != nullptr) {
             SSL_free(ssl);
@@ -410,6 +434,29 @@ public:
         co_return out;
     }
 };
+
+inline ConnSet::~ConnSet() {
+    for (Conn* c : v_) {
+        c->busy_slot = -1;
+        c->busy_set = nullptr;
+    }
+}
+inline void ConnSet::insert(Conn* c) {
+    if (c->busy_slot >= 0) return;
+    c->busy_slot = static_cast<int>(v_.size());
+    c->busy_set = this;
+    v_.push_back(c);
+}
+inline void ConnSet::erase(Conn* c) {
+    int i = c->busy_slot;
+    if (i < 0 || c->busy_set != this) return;
+    Conn* last = v_.back();
+    v_[static_cast<size_t>(i)] = last;
+    last->busy_slot = i;
+    v_.pop_back();
+    c->busy_slot = -1;
+    c->busy_set = nullptr;
+}
 
 struct Head {
     int status = 0;
@@ -743,7 +790,7 @@ private:
     std::string token_;
     double token_read_at_ = -1e9;
     std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
-    std::set<Conn*> busy_;
+    ConnSet busy_;
 
     // One keep-alive connection carrying up to `depth_` pipelined requests (HTTP/1.1: the server answers in
     // request order; Go's net/http, i.e. kube-apiserver, serves them one after the other).  Requests issued in
@@ -1219,7 +1266,7 @@ private:
         while (!closed_ && !busy_.empty()) {
             co_await loop().sleep(0.5);
             double now = now_s();
-            for (Conn* c : busy_)
+            for (Conn* c : busy_.snapshot())
                 if (c->deadline > 0 && now >= c->deadline) c->abort();
         }
         sweeping_ = false;
