@@ -29,6 +29,7 @@ from ..kube.client import PATCH_MERGE, PATCH_STRATEGIC
 from . import failures as F
 
 log = logging.getLogger("ncc.reconcile")
+_SYNCED_MESSAGE = C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND)
 
 
 def _write_target(op: str, args: tuple) -> tuple:
@@ -485,9 +486,10 @@ class ReconcileMixin:
         st = self.stats
         st["inline_superseded"] += superseded
         done += len(events)
-        for template in events:
-            self.recorder.event(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED,
-                                C.MESSAGE_RESOURCE_SYNCED.format(C.TEMPLATE_KIND), kind=C.TEMPLATE_KIND)
+        if events:
+            record, msg = self.recorder.event, _SYNCED_MESSAGE
+            for template in events:
+                record(template, C.EVENT_TYPE_NORMAL, C.SUCCESS_SYNCED, msg, kind=C.TEMPLATE_KIND)
         if done:
             st["reconciles"] += done
             st["inline_finishes"] += done
