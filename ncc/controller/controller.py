@@ -431,8 +431,18 @@ class Controller(ReconcileMixin):
             self._pending_event.update(wrote)
         # Only a complete set of reports for this object version can change its status: re-evaluate
         # then, instead of once per executor report (N× fewer coordinator passes at N shards).
-        for key in complete:
-            self._reports_complete(key)
+        if not complete:
+            return
+        if not self.options.inline_finish:
+            for key in complete:
+                self._enqueue_key(key)
+            return
+        self._inline_keys.update(complete)  # _reports_complete for the whole batch
+        if self._inline_timer is None:
+            delay = self._coalesce_delay()
+            loop = asyncio.get_running_loop()
+            self._inline_timer = loop.call_later(delay, self._flush_inline) if delay > 0 else \
+                loop.call_soon(self._flush_inline)
 
     def _reports_complete(self, key: str) -> None:
         if not self.options.inline_finish:
