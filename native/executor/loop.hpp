@@ -155,22 +155,51 @@ public:
         std::coroutine_handle<> reader, writer;
         bool readable = false, writable = false;
     };
+    // Per-descriptor state indexed by the descriptor itself (small ints): no hashing on the per-event path.
+    // A pointer from find() is valid until the next add().
+    class FdTable {
+    public:
+        FdState* find(int fd) {
+            return fd >= 0 && static_cast<size_t>(fd) < live_.size() && live_[static_cast<size_t>(fd)]
+                       ? &st_[static_cast<size_t>(fd)]
+                       : nullptr;
+        }
+        const FdState* find(int fd) const { return const_cast<FdTable*>(this)->find(fd); }
+        FdState& add(int fd) {
+            size_t i = static_cast<size_t>(fd);
+            if (i >= st_.size()) {
+                st_.resize(i * 2 + 16);
+                live_.resize(i * 2 + 16, 0);
+            }
+            st_[i] = FdState{};
+            live_[i] = 1;
+            return st_[i];
+        }
+        void erase(int fd) {
+            if (find(fd) == nullptr) return;
+            st_[static_cast<size_t>(fd)] = FdState{};
+            live_[static_cast<size_t>(fd)] = 0;
+        }
+
+    private:
+        std::vector<FdState> st_;
+        std::vector<uint8_t> live_;
+    };
 
     void add_fd(int fd) {
         epoll_event ev{};
         ev.events = EPOLLIN | EPOLLOUT | EPOLLET | EPOLLRDHUP;
         ev.data.fd = fd;
-        fds_[fd] = FdState{};
+        fds_.add(fd);
         if (epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev) != 0) throw std::runtime_error("epoll_ctl ADD failed");
     }
     void del_fd(int fd) {
         epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
-        auto it = fds_.find(fd);
-        if (it != fds_.end()) {
+        if (FdState* st = fds_.find(fd)) {
             // wake anyone still parked on the fd: their next syscall fails and raises
-            if (it->second.reader) post(it->second.reader);
-            if (it->second.writer) post(it->second.writer);
-            fds_.erase(it);
+            if (st->reader) post(st->reader);
+            if (st->writer) post(st->writer);
+            fds_.erase(fd);
         }
     }
 
@@ -179,9 +208,9 @@ public:
         int fd;
         bool write;
         bool await_ready() {
-            auto it = loop->fds_.find(fd);
-            if (it == loop->fds_.end()) return true;
-            bool& flag = write ? it->second.writable : it->second.readable;
+            FdState* st = loop->fds_.find(fd);
+            if (st == nullptr) return true;
+            bool& flag = write ? st->writable : st->readable;
             if (flag) {
                 flag = false;  // consumed: the caller retries its syscall
                 return true;
@@ -189,8 +218,12 @@ public:
             return false;
         }
         void await_suspend(std::coroutine_handle<> h) {
-            auto& st = loop->fds_[fd];
-            (write ? st.writer : st.reader) = h;
+            FdState* st = loop->fds_.find(fd);
+            if (st == nullptr) {  // gone since await_ready: resume at once, the next syscall fails
+                loop->post(h);
+                return;
+            }
+            (write ? st->writer : st->reader) = h;
         }
         void await_resume() {}
     };
@@ -200,8 +233,8 @@ public:
     // socket can wait for the next edge without first trying a recv that would return EAGAIN: every new
     // arrival of data raises an edge.)  Unknown descriptors count as readable: the next syscall fails.
     bool readable_now(int fd) const {
-        auto it = fds_.find(fd);
-        return it == fds_.end() || it->second.readable;
+        const FdState* st = fds_.find(fd);
+        return st == nullptr || st->readable;
     }
     IoAwait writable(int fd) { return IoAwait{this, fd, true}; }
 
@@ -252,10 +285,10 @@ public:
             ++wakeups_;
             if (n < 0 && errno != EINTR) throw std::runtime_error("epoll_wait failed");
             for (int i = 0; i < n; ++i) {
-                auto it = fds_.find(evs[i].data.fd);
-                if (it == fds_.end()) continue;
+                FdState* sp = fds_.find(evs[i].data.fd);
+                if (sp == nullptr) continue;
                 uint32_t e = evs[i].events;
-                FdState& st = it->second;
+                FdState& st = *sp;
                 if (e & (EPOLLIN | EPOLLHUP | EPOLLERR | EPOLLRDHUP)) {
                     st.readable = true;
                     if (st.reader) {
@@ -297,7 +330,7 @@ private:
     bool stopped_ = false;
     uint64_t seq_ = 0;
     uint64_t wakeups_ = 0;
-    std::unordered_map<int, FdState> fds_;
+    FdTable fds_;
     std::deque<std::coroutine_handle<>> ready_;
     std::deque<std::function<void()>> calls_;
     std::priority_queue<Timer, std::vector<Timer>, std::greater<Timer>> timers_;
