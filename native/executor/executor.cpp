@@ -2267,6 +2267,8 @@ static void configure(const Value& c) {
     o.flow.initial = num(c, "initial_concurrency", o.flow.initial);
     o.flow.latency_s = num(c, "overload_latency", o.flow.latency_s);
     if (const char* v = std::getenv("NCC_AIMD")) o.flow.adaptive = std::atoi(v) != 0;  // experiments
+    if (const char* v = std::getenv("NCC_LOOP_COALESCE_US"))  // experiments: software interrupt coalescing
+        loop().set_coalesce(std::max(0L, std::atol(v)) * 1000L, 32);
     o.request_timeout = num(c, "request_timeout", o.request_timeout);
     o.coalesce = num(c, "coalesce_window", o.coalesce);
     o.base_delay = num(c, "failure_base_delay", o.base_delay);
@@ -2489,8 +2491,10 @@ static Task<void> shutdown_watch() {
             foreign += sp->inf[k].foreign;
         }
     if (std::getenv("NCC_CPU_REPORT"))
-        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu",
-                 shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()));
+        LOG_WARN("executor stats shard_events=%lld echoes_skipped=%lld other_partition_skipped=%lld loop_wakeups=%llu "
+                 "coalesced=%llu",
+                 shard_events, echoes, foreign, static_cast<unsigned long long>(loop().wakeups()),
+                 static_cast<unsigned long long>(loop().coalesced()));
     if (g_phases_on) {
         // ticks -> seconds: calibrate the TSC against the steady clock
         unsigned long long c0 = ticks();

@@ -197,7 +197,10 @@ public:
         epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
         if (FdState* st = fds_.find(fd)) {
             // wake anyone still parked on the fd: their next syscall fails and raises
-            if (st->reader) post(st->reader);
+            if (st->reader) {
+                post(st->reader);
+                --parked_readers_;
+            }
             if (st->writer) post(st->writer);
             fds_.erase(fd);
         }
@@ -224,6 +227,7 @@ public:
                 return;
             }
             (write ? st->writer : st->reader) = h;
+            if (!write) ++loop->parked_readers_;
         }
         void await_resume() {}
     };
@@ -250,6 +254,13 @@ public:
     void call_at(double at, std::function<void()> fn) { timers_.push(Timer{at, seq_++, {}, std::move(fn)}); }
     // epoll_wait returns so far (idle-loop diagnostics: an executor with nothing to do must not wake up)
     uint64_t wakeups() const { return wakeups_; }
+    uint64_t coalesced() const { return coalesced_; }
+    // Software interrupt coalescing (see run()): after a wake-up with few events while at least `min_parked`
+    // readers wait, sleep `ns` before collecting the rest; 0 = off.
+    void set_coalesce(long ns, int min_parked) {
+        coalesce_ns_ = ns;
+        coalesce_min_parked_ = min_parked;
+    }
 
     void post(std::coroutine_handle<> h) { ready_.push_back(h); }
     void call_soon(std::function<void()> fn) { calls_.push_back(std::move(fn)); }
@@ -284,6 +295,16 @@ public:
             int n = epoll_wait(ep_, evs, 256, timeout_ms);
             ++wakeups_;
             if (n < 0 && errno != EINTR) throw std::runtime_error("epoll_wait failed");
+            if (n > 0 && n < kCoalesceBelow && coalesce_ns_ > 0 && parked_readers_ >= coalesce_min_parked_) {
+                // Under load (many requests awaiting their answers) a wake-up for one or two events is mostly
+                // syscall and scheduler cost: let the answers that are on their way arrive, then take every
+                // ready event in one more non-blocking call (software interrupt coalescing)
+                timespec ts{0, coalesce_ns_};
+                nanosleep(&ts, nullptr);
+                int m = epoll_wait(ep_, evs + n, 256 - n, 0);
+                if (m > 0) n += m;
+                ++coalesced_;
+            }
             for (int i = 0; i < n; ++i) {
                 FdState* sp = fds_.find(evs[i].data.fd);
                 if (sp == nullptr) continue;
@@ -295,6 +316,7 @@ public:
                         auto h = std::exchange(st.reader, {});
                         st.readable = false;
                         ready_.push_back(h);
+                        --parked_readers_;
                     }
                 }
                 if (e & (EPOLLOUT | EPOLLHUP | EPOLLERR)) {
@@ -330,6 +352,11 @@ private:
     bool stopped_ = false;
     uint64_t seq_ = 0;
     uint64_t wakeups_ = 0;
+    uint64_t coalesced_ = 0;
+    long coalesce_ns_ = 0;
+    int coalesce_min_parked_ = 32;
+    int parked_readers_ = 0;  // coroutines waiting for a descriptor to become readable
+    static constexpr int kCoalesceBelow = 4;
     FdTable fds_;
     std::deque<std::coroutine_handle<>> ready_;
     std::deque<std::function<void()>> calls_;
