@@ -2439,10 +2439,11 @@ static void send_status() {
             e.str(inf.last_error);
         }
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
-        // connections, write batches, requests, slow starts left on rising latency, increases held back]
+        // connections, write batches, requests, slow starts left on rising latency, increases held back, and the
+        // executor loop's wake-ups and coalesced wake-ups (process-wide)]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(13);
+        e.array(15);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2456,6 +2457,8 @@ static void send_status() {
         e.integer(cl.requests);
         e.integer(cl.flow.hystart);
         e.integer(cl.flow.held);
+        e.integer(static_cast<long long>(loop().wakeups()));
+        e.integer(static_cast<long long>(loop().coalesced()));
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

@@ -408,7 +408,8 @@ class CoordinatorPartitions:
 # per shard in a C++ executor's status: its client's adaptive concurrency limit and what drove it
 # (native/executor/http.hpp `Client::finish`)
 FLOW_FIELDS = ("limit", "inflight", "max_inflight", "rejected_429", "overload_signals", "cuts", "gated",
-               "qps_wait_ms", "connections", "write_batches", "requests", "slow_start_exits", "increases_held")
+               "qps_wait_ms", "connections", "write_batches", "requests", "slow_start_exits", "increases_held",
+               "loop_wakeups", "loop_coalesced")
 
 
 def status_view(msg: dict) -> dict:
