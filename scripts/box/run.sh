@@ -34,7 +34,9 @@ print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99",
       "substrate_us", d.get("substrate_us_per_object"), "ratio", d.get("controller_to_substrate"),
       "coord_cores", d["cpu_cores_busy"].get("coordinator"), "py_loop_ms", c.get("python_loop_ms"),
       "cpp_scan_ns", c.get("cpp_ctl_scan_ns"), "throttled_us", h.get("throttled_usec"),
-      "host_busy", h.get("host_busy_cpus"), flush=True)
+      "host_busy", h.get("host_busy_cpus"),
+      "wakeups", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("loop_wakeups"),
+      flush=True)
 EOF
 }
 
