@@ -42,9 +42,9 @@ EOF
 
 bench_once() {  # <file> [ARGS...]
   local f=$1; shift
-  local envs=() flags=()
-  for a in "$@"; do  # KEY=VAL: environment (bench.py passes it on to the controller); anything else: a flag
-    if [[ "$a" == *=* && "$a" != -* ]]; then envs+=("$a"); else flags+=("$a"); fi
+  local envs=() flags=() arg  # `arg` local: the ab preset's own $a / $b must survive this loop
+  for arg in "$@"; do  # KEY=VAL: environment (bench.py passes it on to the controller); anything else: a flag
+    if [[ "$arg" == *=* && "$arg" != -* ]]; then envs+=("$arg"); else flags+=("$arg"); fi
   done
   env "${envs[@]}" timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 "${flags[@]}" \
     > "$f.json" 2> "$f.err" || return $?
