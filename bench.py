@@ -787,7 +787,9 @@ async def run(args, d: Dist) -> dict | None:
             # waves: the cost of the system under test, independent of how fast the fake apiservers are
             ctl_cpu = {k: cpu1.get(k, 0.0) - cpu0.get(k, 0.0) for k in ("coordinator", "executors")}
             us_per_obj = {k: round(v * 1e6 / objs, 1) for k, v in ctl_cpu.items()}
-            substrate = sum(subs) / len(subs) / S if subs else None
+            # every hosted shard has its own apiserver process; `sub` is the first one's CPU per object it
+            # committed, so the mean over ranks is already per object (no division by the shards per rank)
+            substrate = sum(subs) / len(subs) if subs else None
             ctl_us = sum(ctl_cpu.values()) * 1e6 / objs
             from ncc.app import cpu_share
             sizing = ctrl_state.get("sizing") or {}
