@@ -870,10 +870,14 @@ private:
     // The connection a request goes on: an idle one; else a new one while fewer than `max_` are open; else the
     // least loaded one below `depth_` (the admission gate keeps the requests in flight ≤ max_ × depth_).
     // Requests issued in one loop iteration fill the pipe whose write is still to go out (up to `depth_`)
-    // before another is taken: they leave in one send, and their answers tend to arrive in one read.
+    // before another is taken: they leave in one send, and their answers tend to arrive in one read.  Only
+    // against a server that answers fast (the fastest write of the window under kBatchFloor): where a write
+    // holds a seat for milliseconds (etcd, APF), requests sharing a connection would wait on each other — the
+    // server serves one connection's requests one after the other — so they spread over connections instead.
+    static constexpr double kBatchFloor = 0.002;
     PipePtr pick() {
         if (building_ && !building_->broken && static_cast<int>(building_->pending.size()) < depth_ &&
-            (building_->flush_posted || !building_->connected))
+            (building_->flush_posted || !building_->connected) && min_class_[1] < kBatchFloor)
             return building_;
         building_ = pick_least_loaded();
         return building_;
