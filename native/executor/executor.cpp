@@ -1993,6 +1993,25 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
     }
 }
 
+// The condition under which sync_dependent_steps ends without a write (either path), checked without
+// starting it: a pass triggered by one changed dependent leaves the others alone at the cost of two lookups.
+static bool dependent_in_sync(Shard& sh, int kind, const CtlObj& tpl, const ShardObj& st, const std::string& dep) {
+    Executor& ex = *g_ex;
+    CtlPtr src = ex.cget(kind, key_of(tpl.ns, dep));
+    if (!src) return false;
+    ShardPtr so = sh.get(kind, key_of(st.ns, dep));
+    if (!so || !so->has_owner_refs) return false;
+    bool owned = false;
+    for (const auto& o : so->template_owners)
+        if (o.second == st.uid) owned = true;
+    if (!owned) return false;
+    if (kind == SECRETS && g_opt.sync_secret_type &&
+        (src->type.empty() ? std::string_view("Opaque") : std::string_view(src->type)) !=
+            (so->type.empty() ? std::string_view("Opaque") : std::string_view(so->type)))
+        return false;
+    return data_in_sync(sh, kind, *so, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(*so, *src));
+}
+
 static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass) {
     Shard& sh = *shp;
     if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
@@ -2006,8 +2025,12 @@ static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass
         // later (the reference's loop is strictly sequential, controller.go:790-831)
         jobs.push_back(update_crd(shp, TEMPLATES, st, tpl, pass));
     }
-    for (const auto& n : tpl->secrets) jobs.push_back(sync_dependent(shp, SECRETS, tpl, st, n, pass));
-    for (const auto& n : tpl->configmaps) jobs.push_back(sync_dependent(shp, CONFIGMAPS, tpl, st, n, pass));
+    for (const auto& n : tpl->secrets)
+        if (!dependent_in_sync(sh, SECRETS, *tpl, *st, n)) jobs.push_back(sync_dependent(shp, SECRETS, tpl, st, n, pass));
+    for (const auto& n : tpl->configmaps)
+        if (!dependent_in_sync(sh, CONFIGMAPS, *tpl, *st, n))
+            jobs.push_back(sync_dependent(shp, CONFIGMAPS, tpl, st, n, pass));
+    if (jobs.empty()) co_return;
     auto errs = co_await when_all(std::move(jobs));
     for (auto& e : errs)
         if (e) std::rethrow_exception(e);
