@@ -285,6 +285,14 @@ def test_native_parsers_survive_arbitrary_bytes():
             assert r is None or len(r) == 8
             m.scan_event_owners(data)
             m.scan_object(data)
+            kept, dropped, _ = m.owner_filter([data], {("n", "s"): {"metadata": {"ownerReferences": []}}}, {}, "n")
+            assert len(kept) + dropped == 1
+            assert m.relay_index([data], {}, "n") in ([], [data])
+            m.template_event_slim(data, {("n", "s"): {"status": {}, "__ncc_sfp__": 1}}, "n")
+            try:
+                m.chunk_lines(bytearray(data), -1, bytearray())
+            except ValueError:
+                pass
     check()
 
 
