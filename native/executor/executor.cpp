@@ -704,8 +704,17 @@ static ShardPtr shard_obj_from_body(int kind, std::string_view body) {
 static bool is_ours(const ShardObj& s) { return s.label_owner == g_opt.alias && s.label_app == kAgent; }
 
 static std::string key_of(const std::string& ns, const std::string& name) { return ns + "/" + name; }
+// The same key in a scratch buffer, for a lookup or an erase that completes before the next call (never stored,
+// never held across a co_await): the hot path's finds cost no allocation.
+static const std::string& key_tmp(const std::string& ns, std::string_view name) {
+    static std::string buf;
+    buf.assign(ns);
+    buf += '/';
+    buf.append(name.data(), name.size());
+    return buf;
+}
 static bool in_partition(const std::string& ns, const std::string& name) {
-    return g_opt.parts <= 1 || static_cast<int>(crc32(key_of(ns, name)) % g_opt.parts) == g_opt.part;
+    return g_opt.parts <= 1 || static_cast<int>(crc32(key_tmp(ns, name)) % g_opt.parts) == g_opt.part;
 }
 
 // ------------------------------------------------------------------------------------ channel
@@ -1173,7 +1182,7 @@ static void index_template(const CtlPtr& old, const CtlPtr& cur) {
         if (ov && nv && *ov == *nv) continue;
         if (ov)
             for (const auto& n : *ov) {
-                auto it = ex.refs[i].find(key_of(any->ns, n));
+                auto it = ex.refs[i].find(key_tmp(any->ns, n));
                 if (it != ex.refs[i].end()) {
                     it->second.erase(tkey);
                     if (it->second.empty()) ex.refs[i].erase(it);
@@ -1246,7 +1255,7 @@ static double dependent_hold(const std::string& tkey) {
 static void on_dependent(int kind, const CtlObj& obj) {
     Executor& ex = *g_ex;
     std::set<std::string> seen;
-    auto it = ex.refs[kind == SECRETS ? 0 : 1].find(key_of(obj.ns, obj.name));
+    auto it = ex.refs[kind == SECRETS ? 0 : 1].find(key_tmp(obj.ns, obj.name));
     if (it != ex.refs[kind == SECRETS ? 0 : 1].end()) {
         for (const auto& tkey : it->second) {
             std::string tname = tkey.substr(tkey.find('/') + 1);
@@ -1301,7 +1310,7 @@ static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool de
 // ------------------------------------------------------------------------------------ shard side
 static bool spec_in_sync(const Shard& sh, int kind, const ShardObj& so, uint64_t desired) {
     if (so.fp_spec == desired) return true;
-    auto it = sh.memo[kind].find(key_of(so.ns, so.name));
+    auto it = sh.memo[kind].find(key_tmp(so.ns, so.name));
     // the server rewrote what we sent (defaulting / pruning / a mutating webhook): the version our own
     // write produced counts as in sync, or every pass would write again
     return it != sh.memo[kind].end() && it->second.rv == so.rv && it->second.fp_a == desired;
@@ -1309,7 +1318,7 @@ static bool spec_in_sync(const Shard& sh, int kind, const ShardObj& so, uint64_t
 static bool data_in_sync(const Shard& sh, int kind, const ShardObj& so, const CtlObj& src) {
     bool with_bin = kind == CONFIGMAPS && g_opt.sync_binary_data;
     if (so.fp_data == src.fp_data && (!with_bin || so.fp_bin == src.fp_bin)) return true;
-    auto it = sh.memo[kind].find(key_of(so.ns, so.name));
+    auto it = sh.memo[kind].find(key_tmp(so.ns, so.name));
     return it != sh.memo[kind].end() && it->second.rv == so.rv && it->second.fp_a == src.fp_data &&
            (!with_bin || it->second.fp_b == src.fp_bin);
 }
@@ -1421,7 +1430,7 @@ static void set_metadata(Value& m, const CtlObj& src) {
 static void repair_lost_owners(Shard& sh, int kind, const ShardObj& o) {
     Executor& ex = *g_ex;
     auto& idx = ex.refs[kind == SECRETS ? 0 : 1];
-    auto it = idx.find(key_of(o.ns, o.name));
+    auto it = idx.find(key_tmp(o.ns, o.name));
     if (it == idx.end()) return;
     for (const auto& tkey : it->second) {
         ShardPtr st = sh.get(TEMPLATES, tkey);
@@ -1441,7 +1450,7 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     if (!deleted && !old) return;  // adds are not drift (the reference only repairs on update/delete)
     const ShardObj& o = deleted ? *old : *cur;
     if (kind == TEMPLATES || kind == WORKGROUPS) {
-        CtlPtr c = ex.cget(kind, key_of(o.ns, o.name));
+        CtlPtr c = ex.cget(kind, key_tmp(o.ns, o.name));
         if (!c) return;
         if (deleted || !spec_in_sync(sh, kind, o, c->fp_spec)) {
             ++g_enq[ENQ_SHARD_OBJECT];
@@ -1449,7 +1458,7 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
         }
         return;
     }
-    CtlPtr src = ex.cget(kind, key_of(o.ns, o.name));
+    CtlPtr src = ex.cget(kind, key_tmp(o.ns, o.name));
     if (!src) return;
     if (!deleted && data_in_sync(sh, kind, o, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(o, *src))) {
         repair_lost_owners(sh, kind, o);
@@ -1459,7 +1468,7 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     for (const auto& p : o.template_owners) owners.push_back(p.first);
     if (owners.empty()) owners = src->owners;
     for (const auto& n : owners)
-        if (ex.cget(TEMPLATES, key_of(o.ns, n))) {
+        if (ex.cget(TEMPLATES, key_tmp(o.ns, n))) {
             ++g_enq[ENQ_SHARD_DEPENDENT];
             ex.enqueue(TEMPLATES, o.ns, n);
         }
@@ -1489,7 +1498,10 @@ static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch)
         if (old) inf.store.erase(it);
         return;
     }
-    inf.store[key] = so;
+    if (it != inf.store.end())
+        it->second = so;
+    else
+        inf.store.emplace(std::move(key), so);
     if (dispatch) on_shard_event(sh, kind, old, so, false);
 }
 
@@ -1735,7 +1747,7 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
     if (rewritten)
         sh.memo[kind][key_of(so->ns, so->name)] = Memo{so->rv, want_a, want_b};
     else
-        sh.memo[kind].erase(key_of(so->ns, so->name));
+        sh.memo[kind].erase(key_tmp(so->ns, so->name));
     shard_upsert(sh, kind, so, false);
     co_return so;
 }
@@ -1837,12 +1849,12 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
                                        PassState* pass) {
     Shard& sh = *shp;
     Executor& ex = *g_ex;
-    CtlPtr src = ex.cget(kind, key_of(tpl->ns, dep));
+    CtlPtr src = ex.cget(kind, key_tmp(tpl->ns, dep));
     if (!src) throw NamedError("ReferenceMissing", std::string(kPlural[kind]) + " \"" + dep + "\" not found");
     const std::string& shard_ns = st->ns;
     bool is_secret = kind == SECRETS;
     bool with_bin = !is_secret && g_opt.sync_binary_data;
-    ShardPtr so = sh.get(kind, key_of(shard_ns, dep));
+    ShardPtr so = sh.get(kind, key_tmp(shard_ns, dep));
     // `live`: with server-side apply, the shard copy whose template ownerRefs the applied configuration keeps
     // (every template's pass applies with the same field manager, and an apply drops the ownerRef entries its
     // manager applied before and omits now — applying only ours would take the other owners' refs off a
@@ -1906,7 +1918,7 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
                 if (type_changed) {  // Secret.type is immutable: an apply cannot change it, so replace the copy
                     pass->wrote = true;
                     co_await shard_delete(sh, kind, shard_ns, dep);
-                    sh.inf[kind].store.erase(key_of(shard_ns, dep));
+                    sh.inf[kind].store.erase(key_tmp(shard_ns, dep));
                     so = nullptr;
                 } else if (ours && data_in_sync(sh, kind, *so, *src) &&
                            (!g_opt.sync_dependent_metadata || meta_in_sync(*so, *src))) {
@@ -1941,7 +1953,7 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         // Secret.type is immutable: replace the shard copy (other owners re-add their refs on their passes)
         pass->wrote = true;
         co_await shard_delete(sh, kind, shard_ns, dep);
-        sh.inf[kind].store.erase(key_of(shard_ns, dep));
+        sh.inf[kind].store.erase(key_tmp(shard_ns, dep));
         co_await create();
         co_return;
     }
@@ -1997,9 +2009,9 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
 // starting it: a pass triggered by one changed dependent leaves the others alone at the cost of two lookups.
 static bool dependent_in_sync(Shard& sh, int kind, const CtlObj& tpl, const ShardObj& st, const std::string& dep) {
     Executor& ex = *g_ex;
-    CtlPtr src = ex.cget(kind, key_of(tpl.ns, dep));
+    CtlPtr src = ex.cget(kind, key_tmp(tpl.ns, dep));
     if (!src) return false;
-    ShardPtr so = sh.get(kind, key_of(st.ns, dep));
+    ShardPtr so = sh.get(kind, key_tmp(st.ns, dep));
     if (!so || !so->has_owner_refs) return false;
     bool owned = false;
     for (const auto& o : so->template_owners)
@@ -2039,7 +2051,7 @@ static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass
 static Task<void> sync_workgroup_to_shard(Shard* shp, CtlPtr wg, PassState* pass) {
     Shard& sh = *shp;
     if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
-    ShardPtr sw = sh.get(WORKGROUPS, key_of(wg->ns, wg->name));
+    ShardPtr sw = sh.get(WORKGROUPS, key_tmp(wg->ns, wg->name));
     if (!sw || !spec_in_sync(sh, WORKGROUPS, *sw, wg->fp_spec)) co_await write_crd(sh, WORKGROUPS, sw, *wg, pass);
 }
 
