@@ -59,6 +59,9 @@ def parse_args(argv=None):
     p.add_argument("--workers", type=int, default=0, help="controller workers (0 = mode default)")
     p.add_argument("--timeout", type=float, default=600.0, help="per-wave convergence timeout (s)")
     p.add_argument("--keep", action="store_true", help="keep the work directory")
+    p.add_argument("--pin", choices=("none", "l3"), default="none",
+                   help="l3: the controller (coordinator + executors) on the least busy L3 domain of the CPUs this job "
+                        "may use, the fake apiservers on the next one (one rank only; experiments)")
     p.add_argument("--extra-env", action="append", default=[], help="KEY=VAL passed to the controller process")
     p.add_argument("--shard-latency-ms", type=float, default=0.0,
                    help="added to every request a shard apiserver serves (emulates controller->shard RTT)")
@@ -343,6 +346,44 @@ def host_busy() -> tuple[float, float] | None:
     return (sum(v) - idle) / hz, sum(v) / hz
 
 
+def l3_pin_sets(k: int = 2) -> list[list[int]] | None:
+    """The CPUs of the `k` least busy L3 domains this process may run on (busy: /proc/stat over 0.3 s)."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except OSError:
+        return None
+    doms: dict[int, list[int]] = {}
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                dom = min(_cpu_list(f.read()))
+        except (OSError, ValueError):
+            return None
+        doms.setdefault(dom, []).append(c)
+    if len(doms) < k:
+        return None
+
+    def per_cpu():
+        out = {}
+        with open("/proc/stat") as f:
+            for ln in f:
+                if ln.startswith("cpu") and ln[3:4].isdigit():
+                    parts = ln.split()
+                    v = [int(x) for x in parts[1:]]
+                    out[int(parts[0][3:])] = (sum(v) - v[3] - (v[4] if len(v) > 4 else 0), sum(v))
+        return out
+    a = per_cpu()
+    time.sleep(0.3)
+    b = per_cpu()
+
+    def busy(cpus):
+        db = sum(b[c][0] - a[c][0] for c in cpus if c in a and c in b)
+        dt = sum(b[c][1] - a[c][1] for c in cpus if c in a and c in b)
+        return db / dt if dt else 1.0
+    ranked = sorted(doms.values(), key=busy)
+    return ranked[:k]
+
+
 def _cpu_list(text: str) -> list[int]:
     out = []
     for part in text.strip().split(","):
@@ -564,10 +605,19 @@ async def run(args, d: Dist) -> dict | None:
             ssl_ctx = client_ssl(pki)
         extra = sum((["--marker", m] for m in MARKERS), [])
         S = max(1, args.shards_per_rank)
+        pin_sets = l3_pin_sets(2) if args.pin == "l3" and d.world == 1 else None
+
+        def pin(proc, which: int) -> None:
+            if pin_sets:
+                try:
+                    os.sched_setaffinity(proc.pid, pin_sets[which])
+                except OSError:
+                    pass
         my_urls = []
         for j in range(S):
             pf = os.path.join(work, f"shard{j}.url")
             procs.append(spawn_fakeapi(f"shard-{d.rank * S + j}", pf, extra=extra, pki=pki))
+            pin(procs[-1], 1)
             my_urls.append(wait_port_file(pf, procs[-1]))
         my_url = my_urls[0]
         if args.shard_latency_ms or args.shard_jitter_ms:
@@ -579,6 +629,7 @@ async def run(args, d: Dist) -> dict | None:
         if d.rank == 0:
             cpf = os.path.join(work, "controller.url")
             procs.append(spawn_fakeapi("controller", cpf, extra=extra, pki=pki))
+            pin(procs[-1], 1)
             ctrl_url = wait_port_file(cpf, procs[-1])
             ctrl_proc = procs[-1]
             shard_dir = os.path.join(work, "shards")
@@ -623,6 +674,7 @@ async def run(args, d: Dist) -> dict | None:
                 t_boot = time.time_ns()
                 controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=log,
                                               stderr=subprocess.STDOUT, cwd=work)
+                pin(controller, 0)  # before it starts its executors: they inherit the mask
                 procs.append(controller)
             t_boot = d.broadcast(t_boot if d.rank == 0 else None)
             named = {"shard-apiserver": procs[0]}
@@ -759,6 +811,7 @@ async def run(args, d: Dist) -> dict | None:
                         "ctx_switches": {k: [v[0] - cs0.get(k, [0, 0])[0], v[1] - cs0.get(k, [0, 0])[1]]
                                          for k, v in cs1.items()},
                         "placement": placed,
+                        "pinned": {"controller": pin_sets[0], "apiservers": pin_sets[1]} if pin_sets else None,
                         # CPUs the whole host kept busy over the timed waves (every tenant, this job included)
                         "host_busy_cpus": round((hb1[0] - hb0[0]) / elapsed, 1) if hb0 and hb1 else None,
                         "calibration": calibrate()}
