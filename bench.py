@@ -59,9 +59,10 @@ def parse_args(argv=None):
     p.add_argument("--workers", type=int, default=0, help="controller workers (0 = mode default)")
     p.add_argument("--timeout", type=float, default=600.0, help="per-wave convergence timeout (s)")
     p.add_argument("--keep", action="store_true", help="keep the work directory")
-    p.add_argument("--pin", choices=("none", "l3"), default="none",
+    p.add_argument("--pin", choices=("none", "l3", "controller"), default="none",
                    help="l3: the controller (coordinator + executors) on the least busy L3 domain of the CPUs this job "
-                        "may use, the fake apiservers on the next one (one rank only; experiments)")
+                        "may use, the fake apiservers on the next one; controller: only the controller pinned (one "
+                        "rank only; experiments)")
     p.add_argument("--extra-env", action="append", default=[], help="KEY=VAL passed to the controller process")
     p.add_argument("--shard-latency-ms", type=float, default=0.0,
                    help="added to every request a shard apiserver serves (emulates controller->shard RTT)")
@@ -605,10 +606,10 @@ async def run(args, d: Dist) -> dict | None:
             ssl_ctx = client_ssl(pki)
         extra = sum((["--marker", m] for m in MARKERS), [])
         S = max(1, args.shards_per_rank)
-        pin_sets = l3_pin_sets(2) if args.pin == "l3" and d.world == 1 else None
+        pin_sets = l3_pin_sets(2) if args.pin != "none" and d.world == 1 else None
 
         def pin(proc, which: int) -> None:
-            if pin_sets:
+            if pin_sets and (which == 0 or args.pin == "l3"):
                 try:
                     os.sched_setaffinity(proc.pid, pin_sets[which])
                 except OSError:
@@ -811,7 +812,8 @@ async def run(args, d: Dist) -> dict | None:
                         "ctx_switches": {k: [v[0] - cs0.get(k, [0, 0])[0], v[1] - cs0.get(k, [0, 0])[1]]
                                          for k, v in cs1.items()},
                         "placement": placed,
-                        "pinned": {"controller": pin_sets[0], "apiservers": pin_sets[1]} if pin_sets else None,
+                        "pinned": {"controller": pin_sets[0], "apiservers": pin_sets[1] if args.pin == "l3" else None}
+                        if pin_sets else None,
                         # CPUs the whole host kept busy over the timed waves (every tenant, this job included)
                         "host_busy_cpus": round((hb1[0] - hb0[0]) / elapsed, 1) if hb0 and hb1 else None,
                         "calibration": calibrate()}
