@@ -1206,7 +1206,10 @@ static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
         on_ctl_event(kind, old ? old : cur, nullptr, true);
         return;
     }
-    store[key] = cur;
+    if (it != store.end())
+        it->second = cur;
+    else
+        it = store.emplace(key, cur).first;
     trace('r', kind, key);
     if (kind == TEMPLATES) index_template(old, cur);
     if (kind >= 2) ex.needed.erase(key);
