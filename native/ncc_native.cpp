@@ -734,9 +734,19 @@ py::tuple owner_filter(py::list lines, py::dict items, py::dict assumed, const s
             Scanner sc(buf, static_cast<size_t>(len));
             sc.owners = &owners;
             sc.owner_uids = &uids;
+            PyObject* kn = nullptr;
+            PyObject* nm = nullptr;
             if (sc.scan(type, ns, name, rv) && type == "MODIFIED") {
                 std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-                py::tuple key = py::make_tuple(py::str(kns.data(), kns.size()), py::str(name.data(), name.size()));
+                kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
+                nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
+                if (nm == nullptr) {  // not UTF-8: kept, the Python path decides
+                    Py_XDECREF(kn);
+                    PyErr_Clear();
+                }
+            }
+            if (nm != nullptr) {
+                py::tuple key = py::make_tuple(py::reinterpret_steal<py::object>(kn), py::reinterpret_steal<py::object>(nm));
                 PyObject* cur = PyDict_GetItemWithError(items.ptr(), key.ptr());
                 if (cur == nullptr && PyErr_Occurred()) throw py::error_already_set();
                 int overlaid = PyDict_Contains(assumed.ptr(), key.ptr());
@@ -796,7 +806,15 @@ py::list relay_index(py::list lines, py::dict raw, const std::string& default_ns
         int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
         if (code == 3) continue;
         std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-        py::tuple key = py::make_tuple(py::str(kns.data(), kns.size()), py::str(name.data(), name.size()));
+        PyObject* kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
+        PyObject* nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
+        if (nm == nullptr) {  // not UTF-8: forwarded for the executor to judge, not indexed
+            Py_XDECREF(kn);
+            PyErr_Clear();
+            if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
+            continue;
+        }
+        py::tuple key = py::make_tuple(py::reinterpret_steal<py::object>(kn), py::reinterpret_steal<py::object>(nm));
         if (code == 2) {
             if (PyDict_DelItem(rd, key.ptr()) != 0) {
                 if (!PyErr_ExceptionMatches(PyExc_KeyError)) throw py::error_already_set();
