@@ -245,8 +245,14 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
             nonlocal last
             last = _converged(cl, active, meta_sync)
             return last == ""
+        streak = [0]
+
+        async def settled():  # converged, and still so a second later: no pass of the chaos phase in flight
+            streak[0] = streak[0] + 1 if await done() else 0
+            return streak[0] >= 6
+
         try:
-            await wait_for(done, timeout=45, interval=0.2)
+            await wait_for(settled, timeout=45, interval=0.2)
         except AssertionError:
             raise AssertionError(f"seed {seed} ({topology}) did not converge: {last}") from None
         rogue = [e for e in cl.cstate.list(R.EVENTS, NS)["items"] if e["reason"] == C.ERR_RESOURCE_EXISTS]
