@@ -713,7 +713,7 @@ static const std::string& key_tmp(const std::string& ns, std::string_view name) 
     buf.append(name.data(), name.size());
     return buf;
 }
-static bool in_partition(const std::string& ns, const std::string& name) {
+static bool in_partition(const std::string& ns, std::string_view name) {
     return g_opt.parts <= 1 || static_cast<int>(crc32(key_tmp(ns, name)) % g_opt.parts) == g_opt.part;
 }
 
@@ -769,8 +769,8 @@ public:
                     co_return out;
                 }
             }
-            char buf[1 << 16];
-            ssize_t r = ::recv(fd_, buf, sizeof buf, 0);
+            char* buf = read_scratch();
+            ssize_t r = ::recv(fd_, buf, kReadScratch, 0);
             if (r > 0) {
                 in_.append(buf, static_cast<size_t>(r));
                 continue;
@@ -885,15 +885,24 @@ static void send_simple(const char* t) {
 // client-go's rate-limiting queue semantics (as ncc/workqueue + native/ncc_native.cpp RateLimitingQueue):
 // dedup of queued keys, a key is never processed twice at once (re-added keys wait for `done`),
 // delayed adds, per-key exponential failure backoff max'ed with a token bucket for AddRateLimited.
+// client-go's workqueue (dirty / processing sets, delayed and rate-limited adds) over one table of per-key
+// state: a key costs one node while it has work pending, the FIFO holds pointers to the nodes, and a pass's
+// add / get / done are a lookup each — no set of key copies per state.  A node is dropped once its key is
+// idle (not dirty, not processing, no delayed add or failure count pending, no timer holding it).
 class WorkQueue {
+    struct Item {
+        bool dirty = false, processing = false;
+        double wait_at = 0;  // a delayed add is due then (0: none)
+        int timers = 0;      // delayed() coroutines still holding the node
+        int failures = 0;
+    };
+    using Node = std::pair<const std::string, Item>;
+    using Items = std::unordered_map<std::string, Item>;
+
 public:
     void add(const std::string& key) {
         if (shutdown_) return;
-        if (dirty_.count(key)) return;
-        dirty_.insert(key);
-        if (processing_.count(key)) return;
-        queue_.push_back(key);
-        wake();
+        mark(node(key));
     }
     void add_after(const std::string& key, double delay) {
         if (shutdown_) return;
@@ -902,13 +911,16 @@ public:
             return;
         }
         double at = now_s() + delay;
-        auto it = waiting_.find(key);
-        if (it != waiting_.end() && it->second <= at) return;
-        waiting_[key] = at;
-        spawn(delayed(key, at), "delayed add");
+        Node& n = node(key);
+        Item& i = n.second;
+        if (i.wait_at > 0 && i.wait_at <= at) return;
+        if (i.wait_at == 0) ++waiting_;
+        i.wait_at = at;
+        ++i.timers;
+        spawn(delayed(&n, at), "delayed add");
     }
     void add_rate_limited(const std::string& key) {
-        int f = failures_[key]++;
+        int f = node(key).second.failures++;
         double exp_delay = std::min(g_opt.base_delay * std::pow(2.0, f), g_opt.max_delay);
         double now = now_s();
         tokens_ = std::min(g_opt.burst, tokens_ + (now - last_) * g_opt.qps);
@@ -917,18 +929,35 @@ public:
         double bucket = tokens_ < 0 ? -tokens_ / g_opt.qps : 0.0;
         add_after(key, std::max(exp_delay, bucket));
     }
-    void forget(const std::string& key) { failures_.erase(key); }
+    void forget(const std::string& key) {
+        auto it = items_.find(key);
+        if (it == items_.end()) return;
+        it->second.failures = 0;
+        drop_if_idle(it);
+    }
+    // (`key` may be the node's own key, as get() hands out: it is not used after the node is dropped)
     void done(const std::string& key) {
-        processing_.erase(key);
-        if (dirty_.count(key)) {
-            queue_.push_back(key);
-            wake();
+        auto it = items_.find(key);
+        if (it == items_.end()) return;
+        Item& i = it->second;
+        if (i.processing) {
+            i.processing = false;
+            --processing_;
         }
+        if (i.dirty) {
+            queue_.push_back(&*it);
+            wake();
+            return;
+        }
+        drop_if_idle(it);
     }
     size_t length() const { return queue_.size(); }
-    size_t load() const { return queue_.size() + processing_.size() + waiting_.size(); }  // keys with work pending
+    size_t load() const { return queue_.size() + processing_ + waiting_; }  // keys with work pending
     // a pass over `key` is pending (added while queued or processing): the next one will see the latest state
-    bool dirty(const std::string& key) const { return dirty_.count(key) > 0 && !shutdown_; }
+    bool dirty(const std::string& key) const {
+        auto it = items_.find(key);
+        return it != items_.end() && it->second.dirty && !shutdown_;
+    }
     void shutdown() {
         shutdown_ = true;
         for (auto h : getters_) loop().post(h);
@@ -941,38 +970,56 @@ public:
         void await_suspend(std::coroutine_handle<> h) { q->getters_.push_back(h); }
         void await_resume() {}
     };
-    // Next key to process ("" after shutdown).
-    Task<std::string> get() {
+    // Next key to process (nullptr after shutdown).  The key lives in the queue until done() on it.
+    Task<const std::string*> get() {
         while (queue_.empty() && !shutdown_) co_await GetAwait{this};
-        if (shutdown_) co_return std::string();
-        std::string k = std::move(queue_.front());
+        if (shutdown_) co_return nullptr;
+        Node* n = queue_.front();
         queue_.pop_front();
-        processing_.insert(k);
-        dirty_.erase(k);
-        co_return k;
+        n->second.processing = true;
+        ++processing_;
+        n->second.dirty = false;
+        co_return &n->first;
     }
 
 private:
-    std::deque<std::string> queue_;
-    std::unordered_set<std::string> dirty_, processing_;
-    std::unordered_map<std::string, double> waiting_;
-    std::unordered_map<std::string, int> failures_;
+    Items items_;
+    std::deque<Node*> queue_;  // dirty keys not being processed, in order (node pointers stay valid)
+    size_t processing_ = 0, waiting_ = 0;
     std::deque<std::coroutine_handle<>> getters_;
     double tokens_ = 300, last_ = now_s();
     bool shutdown_ = false;
 
+    Node& node(const std::string& key) { return *items_.try_emplace(key).first; }
+    void mark(Node& n) {
+        if (n.second.dirty) return;
+        n.second.dirty = true;
+        if (n.second.processing) return;
+        queue_.push_back(&n);
+        wake();
+    }
+    void drop_if_idle(Items::iterator it) {
+        const Item& i = it->second;
+        if (!i.dirty && !i.processing && i.wait_at == 0 && i.timers == 0 && i.failures == 0) items_.erase(it);
+    }
     void wake() {
         if (!getters_.empty()) {
             loop().post(getters_.front());
             getters_.pop_front();
         }
     }
-    Task<void> delayed(std::string key, double at) {
+    Task<void> delayed(Node* n, double at) {
         co_await loop().sleep(std::max(0.0, at - now_s()));
-        auto it = waiting_.find(key);
-        if (it == waiting_.end() || it->second > at + 1e-9) co_return;  // superseded by an earlier/later add
-        waiting_.erase(it);
-        add(key);
+        Item& i = n->second;
+        --i.timers;
+        if (i.wait_at == 0 || i.wait_at > at + 1e-9) {  // superseded by an earlier/later add
+            drop_if_idle(items_.find(n->first));
+            co_return;
+        }
+        i.wait_at = 0;
+        --waiting_;
+        if (shutdown_) co_return;
+        mark(*n);
     }
 };
 
@@ -1157,7 +1204,11 @@ struct Executor {
     int run_len = 0;
     void enqueue(int kind, const std::string& ns, const std::string& name, double hold = 1.0) {
         if (!in_partition(ns, name)) return;
-        std::string key = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + ns + "/" + name;
+        static std::string key;  // the queue copies it only when the key has no pending work yet
+        key.assign(kind == TEMPLATES ? "template/" : "workgroup/");
+        key += ns;
+        key += '/';
+        key += name;
         double now = now_s();
         run_len = now - last_event < g_opt.coalesce ? run_len + 1 : 1;
         bool burst = run_len > kBurstMin && queue.load() >= static_cast<size_t>(kBurstMin);
@@ -1196,9 +1247,8 @@ static void index_template(const CtlPtr& old, const CtlPtr& cur) {
 // Apply one relayed controller-side event.
 static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
     Executor& ex = *g_ex;
-    std::string key = key_of(cur->ns, cur->name);
     auto& store = ex.ctl[kind];
-    auto it = store.find(key);
+    auto it = store.find(key_tmp(cur->ns, cur->name));
     CtlPtr old = it == store.end() ? nullptr : it->second;
     if (type == "DELETED") {
         if (it != store.end()) store.erase(it);
@@ -1209,7 +1259,8 @@ static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
     if (it != store.end())
         it->second = cur;
     else
-        it = store.emplace(key, cur).first;
+        it = store.emplace(key_of(cur->ns, cur->name), cur).first;
+    const std::string& key = it->first;  // (a node's key stays put: index_template below touches only ex.refs)
     trace('r', kind, key);
     if (kind == TEMPLATES) index_template(old, cur);
     if (kind >= 2) ex.needed.erase(key);
@@ -1493,8 +1544,7 @@ static bool wanted(int kind, const ShardObj& s) {
 // echo arrive in either order).
 static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch) {
     Informer& inf = sh.inf[kind];
-    std::string key = key_of(so->ns, so->name);
-    auto it = inf.store.find(key);
+    auto it = inf.store.find(key_tmp(so->ns, so->name));
     ShardPtr old = it == inf.store.end() ? nullptr : it->second;
     if (old && so->rv >= 0 && old->rv >= so->rv) return;
     if (!wanted(kind, *so)) {
@@ -1504,7 +1554,7 @@ static void shard_upsert(Shard& sh, int kind, const ShardPtr& so, bool dispatch)
     if (it != inf.store.end())
         it->second = so;
     else
-        inf.store.emplace(std::move(key), so);
+        inf.store.emplace(key_of(so->ns, so->name), so);
     if (dispatch) on_shard_event(sh, kind, old, so, false);
 }
 
@@ -1518,34 +1568,33 @@ static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
         if (kind >= 2 && g_opt.parts > 1) sc.owners = &owners;
         if (sc.scan(type, ns, name, rv) && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) {
             Informer& inf = sh.inf[kind];
-            std::string sns = ns.empty() ? g_opt.ns : std::string(ns);
-            std::string key = key_of(sns, std::string(name));
-            auto it = inf.store.find(key);
+            std::string sns = ns.empty() ? g_opt.ns : std::string(ns);  // (short: no allocation)
+            auto it = inf.store.find(key_tmp(sns, name));
             long long r = rv_num(rv);
             bool mine = true;
             if (g_opt.parts > 1) {
                 if (kind < 2) {
-                    mine = in_partition(sns, std::string(name));
+                    mine = in_partition(sns, name);
                 } else if (!owners.empty()) {
                     mine = false;
                     for (auto o : owners)
-                        if (in_partition(sns, std::string(o))) mine = true;
+                        if (in_partition(sns, o)) mine = true;
                 }
             }
             if (!mine) {
                 ++inf.events;
                 ++inf.foreign;
-                inf.last_rv = std::string(rv);
+                inf.last_rv.assign(rv);
                 if (it != inf.store.end()) {  // it left our partition (as shard_upsert does for !wanted)
                     inf.store.erase(it);
-                    sh.memo[kind].erase(key);
+                    sh.memo[kind].erase(key_tmp(sns, name));
                 }
                 return;
             }
             if (type != "DELETED" && it != inf.store.end() && r >= 0 && it->second->rv >= r) {
                 ++inf.events;
                 ++inf.echoes;
-                inf.last_rv = std::string(rv);
+                inf.last_rv.assign(rv);
                 return;
             }
         }
@@ -2030,9 +2079,9 @@ static bool dependent_in_sync(Shard& sh, int kind, const CtlObj& tpl, const Shar
 static Task<void> sync_template_to_shard(Shard* shp, CtlPtr tpl, PassState* pass) {
     Shard& sh = *shp;
     if (!sh.synced()) throw NamedError("ShardNotReadyError", "shard " + sh.name + " caches not synced");
-    std::string key = key_of(tpl->ns, tpl->name);
-    ShardPtr st = sh.get(TEMPLATES, key);
+    ShardPtr st = sh.get(TEMPLATES, key_tmp(tpl->ns, tpl->name));
     std::vector<Task<void>> jobs;
+    jobs.reserve(1 + tpl->secrets.size() + tpl->configmaps.size());
     if (!st) {
         st = co_await write_crd(sh, TEMPLATES, st, *tpl, pass);  // the dependents' ownerRefs need its UID
     } else if (!spec_in_sync(sh, TEMPLATES, *st, tpl->fp_spec)) {
@@ -2154,6 +2203,7 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
     }
     PassState pass;
     std::vector<Task<void>> jobs;
+    jobs.reserve(ex.shards.size());
     for (auto& sp : ex.shards)
         jobs.push_back(kind == TEMPLATES ? sync_template_to_shard(sp.get(), obj, &pass)
                                          : sync_workgroup_to_shard(sp.get(), obj, &pass));
@@ -2197,12 +2247,14 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
 static Task<void> worker() {
     Executor& ex = *g_ex;
     while (true) {
-        std::string key = co_await ex.queue.get();
-        if (key.empty()) co_return;
+        const std::string* kp = co_await ex.queue.get();
+        if (kp == nullptr) co_return;
+        const std::string& key = *kp;  // (the queue's own copy: valid until done() below)
         trace('q', 0, key);
         size_t a = key.find('/');
         size_t b = key.find('/', a + 1);
-        std::string kind = key.substr(0, a), ns = key.substr(a + 1, b - a - 1), name = key.substr(b + 1);
+        std::string_view kind(key.data(), a);
+        std::string ns = key.substr(a + 1, b - a - 1), name = key.substr(b + 1);
         ++ex.stats_reconciles;
         bool ok = true;
         std::string err;

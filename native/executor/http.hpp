@@ -326,13 +326,13 @@ public:
             buf.erase(0, pos);
             pos = 0;
         }
-        char tmp[65536];
         // the socket was drained and no edge came since: wait for one instead of a recv that returns EAGAIN
         if (ssl == nullptr && drained && fd >= 0 && !loop().readable_now(fd)) co_await loop().readable(fd);
         while (true) {
             if (fd < 0) throw TransportError("connection closed");
             if (ssl != nullptr) {
-                int r = SSL_read(ssl, tmp, sizeof tmp);
+                char* tmp = read_scratch();
+                int r = SSL_read(ssl, tmp, static_cast<int>(kReadScratch));
                 if (r > 0) {
                     buf.append(tmp, static_cast<size_t>(r));
                     co_return;
@@ -348,10 +348,11 @@ public:
                     throw TransportError("TLS read: " + ssl_errors());
                 }
             } else {
-                ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+                char* tmp = read_scratch();
+                ssize_t r = ::recv(fd, tmp, kReadScratch, 0);
                 if (r > 0) {
                     buf.append(tmp, static_cast<size_t>(r));
-                    drained = static_cast<size_t>(r) < sizeof tmp;
+                    drained = static_cast<size_t>(r) < kReadScratch;
                     co_return;
                 }
                 if (r == 0) throw TransportError("connection closed by peer");

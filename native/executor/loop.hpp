@@ -32,6 +32,15 @@ inline double now_s() {
     return duration_cast<duration<double>>(steady_clock::now().time_since_epoch()).count();
 }
 
+// Scratch for one read: a coroutine that reads into a local array carries the array in its frame (a 64 KiB
+// frame is past the pooled allocator's largest class, so every read would malloc and free it — and glibc
+// trims the heap top with brk on that free).  Reads copy out of here before their next suspension point.
+constexpr size_t kReadScratch = 1 << 16;
+inline char* read_scratch() {
+    static thread_local char b[kReadScratch];
+    return b;
+}
+
 // ------------------------------------------------------------------------------------ Task
 template <class T>
 class Task;
