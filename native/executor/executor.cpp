@@ -86,13 +86,24 @@ constexpr const char* kAgent = "nexus-configuration-controller";
 enum Kind { TEMPLATES = 0, WORKGROUPS = 1, SECRETS = 2, CONFIGMAPS = 3 };
 constexpr const char* kPlural[] = {"nexusalgorithmtemplates", "nexusalgorithmworkgroups", "secrets", "configmaps"};
 
-inline std::string base_path(int k, const std::string& ns) {
-    if (k < 2) return std::string("/apis/science.sneaksanddata.com/v1/namespaces/") + ns + "/" + kPlural[k];
-    return "/api/v1/namespaces/" + ns + "/" + kPlural[k];
+// a collection's path, then optionally "/<name>" and a query: built in one reserved string
+inline std::string api_path(int k, const std::string& ns, const std::string* name = nullptr,
+                            std::string_view query = {}) {
+    std::string p;
+    p.reserve(64 + ns.size() + (name ? name->size() : 0) + query.size());
+    p += k < 2 ? "/apis/science.sneaksanddata.com/v1/namespaces/" : "/api/v1/namespaces/";
+    p += ns;
+    p += '/';
+    p += kPlural[k];
+    if (name != nullptr) {
+        p += '/';
+        p += *name;
+    }
+    p += query;
+    return p;
 }
-inline std::string item_path(int k, const std::string& ns, const std::string& name) {
-    return base_path(k, ns) + "/" + name;
-}
+inline std::string base_path(int k, const std::string& ns) { return api_path(k, ns); }
+inline std::string item_path(int k, const std::string& ns, const std::string& name) { return api_path(k, ns, &name); }
 
 // crc32 (zlib) of "ns/name": the key -> partition map shared with ncc.controller.executor.key_part
 static uint32_t g_crc[256];
@@ -811,22 +822,22 @@ private:
         flush_scheduled_ = false;
         last_flush_ = now_s();
         if (pending_.empty()) return;
-        std::string body;
+        // frame = 4-byte length (top bit: a batch) + one message, or a msgpack array header + the messages,
+        // written straight into the output buffer
         bool batch = pending_.size() > 1;
-        if (batch) {
-            mp::Encoder e;
-            e.array(pending_.size());
-            body = std::move(e.out);
-            for (auto& m : pending_) body += m;
-        } else {
-            body = std::move(pending_[0]);
-        }
-        pending_.clear();
-        uint32_t n = static_cast<uint32_t>(body.size()) | (batch ? 0x80000000u : 0u);
+        mp::Encoder e;
+        if (batch) e.array(pending_.size());
+        size_t size = e.out.size();
+        for (const auto& m : pending_) size += m.size();
+        uint32_t n = static_cast<uint32_t>(size) | (batch ? 0x80000000u : 0u);
         char hdr[4] = {static_cast<char>(n >> 24), static_cast<char>(n >> 16), static_cast<char>(n >> 8),
                        static_cast<char>(n)};
+        // (grow only: GCC 11's reserve() below the capacity reallocates to shrink)
+        if (out_.capacity() < out_.size() + 4 + size) out_.reserve(out_.size() + 4 + size);
         out_.append(hdr, 4);
-        out_ += body;
+        out_ += e.out;
+        for (const auto& m : pending_) out_ += m;
+        pending_.clear();
         drained_.clear();
         has_out_.set();
     }
@@ -1786,8 +1797,7 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
     ++g_ex->stats_writes;
     std::string_view m(method);
     bool apply = m == "PATCH";  // the only PATCH this executor sends is a server-side apply
-    std::string target = (m == "POST" ? base_path(kind, ns) : item_path(kind, ns, name)) +
-                         (apply ? kApplyQuery : kFieldManagerQuery);
+    std::string target = api_path(kind, ns, m == "POST" ? nullptr : &name, apply ? kApplyQuery : kFieldManagerQuery);
     Response r = co_await sh.client->request(method, target, &data, apply ? kApplyType : "application/json");
     note_answer(sh, r.status);
     if (r.status >= 300) throw api_error(r.status, r.body);
@@ -2110,6 +2120,7 @@ static Task<void> sync_workgroup_to_shard(Shard* shp, CtlPtr wg, PassState* pass
 static void report(const std::string& key, const CtlObj& obj,
                    const std::vector<std::pair<std::string, std::optional<Failure>>>& results, bool wrote) {
     mp::Encoder e;
+    e.out.reserve(64 + key.size() + obj.uid.size() + 48 * results.size());
     e.map(6);
     e.str("t");
     e.str("report");

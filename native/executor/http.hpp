@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <charconv>
 #include <cstring>
 #include <map>
 #include <fstream>
@@ -830,7 +831,8 @@ private:
 
     const std::string& headers(const char* content_type) {
         reload_token(false);
-        std::string key = content_type ? content_type : "";
+        static thread_local std::string key;  // ("application/json" is past the short-string buffer)
+        key.assign(content_type ? content_type : "");
         auto it = hdr_.find(key);
         if (it != hdr_.end()) return it->second;
         std::string h = "Host: " + host_ + "\r\nUser-Agent: nexus-configuration-controller/ncc-executor (linux/amd64)"
@@ -860,7 +862,11 @@ private:
         req += " HTTP/1.1\r\n";
         req += headers(body ? content_type : nullptr);
         if (body != nullptr) {
-            req += "Content-Length: " + std::to_string(body->size()) + "\r\n\r\n";
+            char num[24];
+            auto [end, ec] = std::to_chars(num, num + sizeof num, body->size());
+            req += "Content-Length: ";
+            req.append(num, static_cast<size_t>(end - num));
+            req += "\r\n\r\n";
             req += *body;
         } else {
             req += "\r\n";
