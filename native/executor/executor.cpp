@@ -183,6 +183,7 @@ static inline unsigned long long ticks() {
 #endif
 }
 static long long g_scan_hits = 0, g_scan_misses = 0;  // write responses read without / with a DOM
+static long long g_sent_hits = 0;  // response payloads recognised as the text we sent (not fingerprinted)
 struct PhaseTimer {
     int ph;
     unsigned long long t0;
@@ -641,9 +642,18 @@ static bool scan_meta(ShardObj& s, std::string_view meta) {
     });
 }
 
+// Payload texts a write sent (spec, or data and binaryData), each with its fingerprint as the controller side
+// computed it (raw_is_empty-normalised).  A response payload with the same text has the same fingerprint, so
+// the answer to a write is checked with a memcmp instead of fingerprinted again — the apiserver returns the
+// payload as sent unless something rewrote it (both sides are compact JSON with the keys in the same order).
+struct SentPayload {
+    std::string_view raw[2];
+    uint64_t fp[2] = {0, 0};
+};
+
 // A write response straight into the slim form without a DOM: the non-payload members are copied as text
 // (the next PUT's body), the metadata fields read in place, the payloads fingerprinted from their text.
-static ShardPtr shard_obj_scan(int kind, std::string_view body) {
+static ShardPtr shard_obj_scan(int kind, std::string_view body, const SentPayload* sent = nullptr) {
     auto s = std::make_shared<ShardObj>();
     const std::string_view* keys = payload_keys(kind);
     size_t nk = payload_count(kind);
@@ -659,6 +669,18 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body) {
             if (k == keys[i]) {  // fingerprinted as it is skipped
                 x.ws();
                 const char* b = x.p;
+                if (sent != nullptr && i < 2) {
+                    // a complete object's text as a prefix here is this member's whole value
+                    std::string_view h = sent->raw[i];
+                    if (h.size() > 1 && h.front() == '{' && static_cast<size_t>(x.e - b) >= h.size() &&
+                        std::memcmp(b, h.data(), h.size()) == 0) {
+                        fps[i] = sent->fp[i];
+                        raw[i] = std::string_view(b, h.size());
+                        x.p = b + h.size();
+                        ++g_sent_hits;
+                        return true;
+                    }
+                }
                 const char* end = nullptr;
                 fps[i] = Parser(b, static_cast<size_t>(x.e - b)).fingerprint_prefix(&end);
                 raw[i] = std::string_view(b, static_cast<size_t>(end - b));
@@ -700,9 +722,9 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body) {
 }
 
 // A write/GET response body straight into the slim form, payloads fingerprinted from their text.
-static ShardPtr shard_obj_from_body(int kind, std::string_view body) {
+static ShardPtr shard_obj_from_body(int kind, std::string_view body, const SentPayload* sent = nullptr) {
     PhaseTimer pt(PH_RESPONSE);
-    if (ShardPtr fast = shard_obj_scan(kind, body)) {
+    if (ShardPtr fast = shard_obj_scan(kind, body, sent)) {
         ++g_scan_hits;
         return fast;
     }
@@ -1792,7 +1814,7 @@ static Value owner_ref(const std::string& name, const std::string& uid) {
 // `data`: the request body (rendered with dumps_with: cached metadata + the raw controller-side payload)
 static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const std::string& ns,
                                   const std::string& name, std::string data, PassState* pass, uint64_t want_a,
-                                  uint64_t want_b) {
+                                  uint64_t want_b, std::string_view sent_a = {}, std::string_view sent_b = {}) {
     pass->wrote = true;
     ++g_ex->stats_writes;
     std::string_view m(method);
@@ -1801,7 +1823,12 @@ static Task<ShardPtr> shard_write(Shard& sh, int kind, const char* method, const
     Response r = co_await sh.client->request(method, target, &data, apply ? kApplyType : "application/json");
     note_answer(sh, r.status);
     if (r.status >= 300) throw api_error(r.status, r.body);
-    ShardPtr so = shard_obj_from_body(kind, r.body);
+    SentPayload sent;  // (sent_a/sent_b: texts whose fingerprints are want_a/want_b, as computed controller-side)
+    sent.raw[0] = sent_a;
+    sent.raw[1] = sent_b;
+    sent.fp[0] = want_a;
+    sent.fp[1] = want_b;
+    ShardPtr so = shard_obj_from_body(kind, r.body, &sent);
     // remember the intent only when the server stored something else (keeps the memo as small as the set
     // of rewritten objects)
     bool with_bin = kind == CONFIGMAPS && g_opt.sync_binary_data;
@@ -1853,7 +1880,8 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
             PhaseTimer pt(PH_BODY);
             body = dumps_with(crd_head(kind, want), {{"spec", spec}});
         }
-        co_return co_await shard_write(sh, kind, "PATCH", want.ns, want.name, std::move(body), pass, want.fp_spec, 0);
+        co_return co_await shard_write(sh, kind, "PATCH", want.ns, want.name, std::move(body), pass, want.fp_spec, 0,
+                                       want.spec_raw);
     }
     bool update = cur != nullptr;
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -1868,7 +1896,7 @@ static Task<ShardPtr> write_crd(Shard& sh, int kind, ShardPtr cur, const CtlObj&
         bool race = false, exists = false;
         try {
             co_return co_await shard_write(sh, kind, update ? "PUT" : "POST", want.ns, want.name, std::move(body),
-                                           pass, want.fp_spec, 0);
+                                           pass, want.fp_spec, 0, want.spec_raw);
         } catch (const ApiError& e) {
             if (e.conflict() || e.already_exists()) {
                 race = true;
@@ -1950,7 +1978,7 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         bool exists = false;
         try {
             co_return co_await shard_write(sh, kind, "POST", shard_ns, dep, create_body(), pass, src->fp_data,
-                                           src->fp_bin);
+                                           src->fp_bin, src->data_raw, src->bin_raw);
         } catch (const ApiError& e) {
             if (!e.already_exists()) throw;
             exists = true;
@@ -1990,7 +2018,7 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
             bool conflict = false;
             try {
                 ShardPtr w = co_await shard_write(sh, kind, "PATCH", shard_ns, dep, create_body(so.get()), pass,
-                                                  src->fp_data, src->fp_bin);
+                                                  src->fp_data, src->fp_bin, src->data_raw, src->bin_raw);
                 if (!so) repair_lost_owners(sh, kind, *w);  // applied without a view of the copy: refs may be gone
                 co_return;
             } catch (const ApiError& e) {
@@ -2049,7 +2077,8 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
         }
         bool conflict = false;
         try {
-            co_await shard_write(sh, kind, "PUT", shard_ns, dep, std::move(body), pass, src->fp_data, src->fp_bin);
+            co_await shard_write(sh, kind, "PUT", shard_ns, dep, std::move(body), pass, src->fp_data, src->fp_bin,
+                                 src->data_raw, src->bin_raw);
             co_return;
         } catch (const ApiError& e) {
             if (!e.conflict() || attempt == 1) throw;
@@ -2617,6 +2646,7 @@ static Task<void> shutdown_watch() {
         }
         LOG_WARN("executor cpu user=%.3fs sys=%.3fs phases:%s response_scan=%lld/%lld", user, sys, parts.c_str(),
                  g_scan_hits, g_scan_hits + g_scan_misses);
+        LOG_WARN("executor response payloads matched as sent: %lld", g_sent_hits);
     }
     if (std::getenv("NCC_CPU_REPORT"))
         LOG_WARN("executor stats reconciles=%lld writes=%lld errors=%lld reports_skipped=%lld enqueues: object=%lld "
