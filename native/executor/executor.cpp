@@ -2221,12 +2221,13 @@ static Task<void> propagate_delete(int kind, std::string ns, std::string name) {
     ex.pending_deletes[kind].erase(key);
 }
 
-static Task<void> sync_object(int kind, std::string ns, std::string name) {
+// `qkey`: the work queue's key, "template/<ns>/<name>" or "workgroup/<ns>/<name>" (the queue keeps it until the
+// pass is done)
+static Task<void> sync_object(int kind, std::string ns, std::string name, const std::string& qkey) {
     Executor& ex = *g_ex;
-    std::string key = key_of(ns, name);
-    CtlPtr obj = ex.cget(kind, key);
+    CtlPtr obj = ex.cget(kind, key_tmp(ns, name));
     if (!obj) {
-        ex.skipping_since.erase(std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key);
+        ex.skipping_since.erase(qkey);
         if (kind == TEMPLATES || g_opt.propagate_workgroup_deletes) co_await propagate_delete(kind, ns, name);
         co_return;
     }
@@ -2248,7 +2249,6 @@ static Task<void> sync_object(int kind, std::string ns, std::string name) {
         jobs.push_back(kind == TEMPLATES ? sync_template_to_shard(sp.get(), obj, &pass)
                                          : sync_workgroup_to_shard(sp.get(), obj, &pass));
     auto errs = co_await when_all(std::move(jobs));
-    std::string qkey = std::string(kind == TEMPLATES ? "template/" : "workgroup/") + key;
     if (ex.queue.dirty(qkey)) {
         // a newer version (or a dependent) re-queued the key while this pass ran: the next pass reports on
         // the version it sees, carrying this pass's writes — a report on a version the coordinator may already
@@ -2299,7 +2299,7 @@ static Task<void> worker() {
         bool ok = true;
         std::string err;
         try {
-            co_await sync_object(kind == "template" ? TEMPLATES : WORKGROUPS, ns, name);
+            co_await sync_object(kind == "template" ? TEMPLATES : WORKGROUPS, ns, name, key);
         } catch (const std::exception&) {
             ok = false;
             err = describe(std::current_exception());
