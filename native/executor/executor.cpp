@@ -1235,7 +1235,7 @@ struct Executor {
     static constexpr int kBurstMin = 32;
     double last_event = -1e18;
     int run_len = 0;
-    void enqueue(int kind, const std::string& ns, const std::string& name, double hold = 1.0) {
+    void enqueue(int kind, const std::string& ns, std::string_view name, double hold = 1.0) {
         if (!in_partition(ns, name)) return;
         static std::string key;  // the queue copies it only when the key has no pending work yet
         key.assign(kind == TEMPLATES ? "template/" : "workgroup/");
@@ -1341,18 +1341,17 @@ static double dependent_hold(const std::string& tkey) {
 
 static void on_dependent(int kind, const CtlObj& obj) {
     Executor& ex = *g_ex;
-    std::set<std::string> seen;
-    auto it = ex.refs[kind == SECRETS ? 0 : 1].find(key_tmp(obj.ns, obj.name));
-    if (it != ex.refs[kind == SECRETS ? 0 : 1].end()) {
+    auto& idx = ex.refs[kind == SECRETS ? 0 : 1];
+    auto it = idx.find(key_tmp(obj.ns, obj.name));
+    if (it != idx.end()) {
         for (const auto& tkey : it->second) {
-            std::string tname = tkey.substr(tkey.find('/') + 1);
-            seen.insert(tname);
+            std::string_view tname = std::string_view(tkey).substr(tkey.find('/') + 1);
             ++g_enq[ENQ_DEPENDENT];
             ex.enqueue(TEMPLATES, obj.ns, tname, dependent_hold(tkey));
         }
     }
     for (const auto& owner : obj.owners) {
-        if (seen.count(owner)) continue;
+        if (it != idx.end() && it->second.count(key_tmp(obj.ns, owner)) > 0) continue;  // enqueued above
         std::string tkey = key_of(obj.ns, owner);
         if (!ex.cget(TEMPLATES, tkey)) return;  // stops at the first orphaned owner
         ++g_enq[ENQ_DEPENDENT];
