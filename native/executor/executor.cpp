@@ -1093,6 +1093,10 @@ struct Shard {
         auto it = inf[k].store.find(key);
         return it == inf[k].store.end() ? nullptr : it->second;
     }
+    const ShardObj* find(int k, const std::string& key) const {
+        auto it = inf[k].store.find(key);
+        return it == inf[k].store.end() ? nullptr : it->second.get();
+    }
 };
 
 static double kDependentHold = 5.0;  // NCC_DEPENDENT_HOLD overrides
@@ -1223,6 +1227,11 @@ struct Executor {
         auto it = ctl[k].find(key);
         return it == ctl[k].end() ? nullptr : it->second;
     }
+    // the same without taking a reference (a check that completes before the cache changes)
+    const CtlObj* cfind(int k, const std::string& key) const {
+        auto it = ctl[k].find(key);
+        return it == ctl[k].end() ? nullptr : it->second.get();
+    }
 
     // Event-driven enqueue.  Inside a burst — a run of more than kBurstMin events, each less than one
     // coalesce window after the previous, while at least kBurstMin keys have work pending (back-to-back
@@ -1335,8 +1344,8 @@ static void ctl_snapshot(int kind, std::vector<CtlPtr> objs) {
 // (users roll dependents out first), unless that event already came (the template changed within the
 // hold): then the dependent is the follower and waits one window like any event in a burst.
 static double dependent_hold(const std::string& tkey) {
-    CtlPtr t = g_ex->cget(TEMPLATES, tkey);
-    return t && now_s() - t->recv_at < g_opt.coalesce * kDependentHold ? 1.0 : kDependentHold;
+    const CtlObj* t = g_ex->cfind(TEMPLATES, tkey);
+    return t != nullptr && now_s() - t->recv_at < g_opt.coalesce * kDependentHold ? 1.0 : kDependentHold;
 }
 
 static void on_dependent(int kind, const CtlObj& obj) {
@@ -1519,8 +1528,8 @@ static void repair_lost_owners(Shard& sh, int kind, const ShardObj& o) {
     auto it = idx.find(key_tmp(o.ns, o.name));
     if (it == idx.end()) return;
     for (const auto& tkey : it->second) {
-        ShardPtr st = sh.get(TEMPLATES, tkey);
-        if (!st) continue;
+        const ShardObj* st = sh.find(TEMPLATES, tkey);
+        if (st == nullptr) continue;
         bool owned = false;
         for (const auto& p : o.template_owners)
             if (p.second == st->uid) owned = true;
@@ -1536,16 +1545,16 @@ static void on_shard_event(Shard& sh, int kind, const ShardPtr& old, const Shard
     if (!deleted && !old) return;  // adds are not drift (the reference only repairs on update/delete)
     const ShardObj& o = deleted ? *old : *cur;
     if (kind == TEMPLATES || kind == WORKGROUPS) {
-        CtlPtr c = ex.cget(kind, key_tmp(o.ns, o.name));
-        if (!c) return;
+        const CtlObj* c = ex.cfind(kind, key_tmp(o.ns, o.name));
+        if (c == nullptr) return;
         if (deleted || !spec_in_sync(sh, kind, o, c->fp_spec)) {
             ++g_enq[ENQ_SHARD_OBJECT];
             ex.enqueue(kind, o.ns, o.name);
         }
         return;
     }
-    CtlPtr src = ex.cget(kind, key_tmp(o.ns, o.name));
-    if (!src) return;
+    const CtlObj* src = ex.cfind(kind, key_tmp(o.ns, o.name));
+    if (src == nullptr) return;
     if (!deleted && data_in_sync(sh, kind, o, *src) && (!g_opt.sync_dependent_metadata || meta_in_sync(o, *src))) {
         repair_lost_owners(sh, kind, o);
         return;
@@ -2099,10 +2108,10 @@ static Task<void> sync_dependent_steps(Shard* shp, int kind, CtlPtr tpl, ShardPt
 // starting it: a pass triggered by one changed dependent leaves the others alone at the cost of two lookups.
 static bool dependent_in_sync(Shard& sh, int kind, const CtlObj& tpl, const ShardObj& st, const std::string& dep) {
     Executor& ex = *g_ex;
-    CtlPtr src = ex.cget(kind, key_tmp(tpl.ns, dep));
-    if (!src) return false;
-    ShardPtr so = sh.get(kind, key_tmp(st.ns, dep));
-    if (!so || !so->has_owner_refs) return false;
+    const CtlObj* src = ex.cfind(kind, key_tmp(tpl.ns, dep));
+    if (src == nullptr) return false;
+    const ShardObj* so = sh.find(kind, key_tmp(st.ns, dep));
+    if (so == nullptr || !so->has_owner_refs) return false;
     bool owned = false;
     for (const auto& o : so->template_owners)
         if (o.second == st.uid) owned = true;
