@@ -239,6 +239,7 @@ class App:
         self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
         self.relay = None  # coordinator: WatchRelay feeding the executors
         self.executor_impl = ""  # coordinator: "native" (ncc/bin/ncc-executor) or "python" shard executors
+        self.cpu_affinity = ""  # coordinator: "l3:<cpus>" when it restricted itself to one L3 domain, else "none"
         self._cred_task = None
         self.native_cfg = None  # coordinator with C++ executors: NativeExecutorConfig (renders their config)
         self._relay_ok = False  # coordinator: the watch relay can run (decided once, in build)
@@ -509,6 +510,12 @@ class App:
             if not use_native:
                 log.debug("Python shard executors: %s", why)
             native_cfg = self.native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
+            if part == 0:
+                # the coordinator and its executors (and child partitions) on one L3 domain: they inherit the
+                # mask (ncc/affinity.py; NCC_CPU_AFFINITY=none leaves it to the kernel)
+                from . import affinity
+                cpus = affinity.apply(1 + self.n_executors * max(1, self.per_shard) + parts - 1)
+                self.cpu_affinity = f"l3:{len(cpus)}" if cpus else "none"
             # One executor group per shard group serves every template key, whatever the number of coordinator
             # partitions: a shard apiserver then serves one executor's watches, not C of them
             # (profiles/r2/c_on_one_shard/: C executors on one shard cost it 12-25 %).
@@ -572,7 +579,7 @@ class App:
         return {"shard_groups": self.n_executors, "executors_per_shard": self.per_shard,
                 "coordinator_partitions": parts, "executor_impl": self.executor_impl or "in-process",
                 "executor_processes": len(self.pool.handles) if self.pool is not None else 0,
-                "watch_relay": self.relay is not None}
+                "watch_relay": self.relay is not None, "cpu_affinity": self.cpu_affinity or "none"}
 
     def open_gate(self) -> None:
         """Leading now (or released by the parent): start reconciling here and in every child process."""
