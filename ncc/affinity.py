@@ -49,7 +49,7 @@ def l3_domains(allowed, sys_cpu: str = SYS_CPU) -> dict[int, list[int]] | None:
     return doms
 
 
-def cpu_busy(cpus, interval: float = 0.2, stat: str = "/proc/stat") -> dict[int, float]:
+def cpu_busy(cpus, interval: float = 0.05, stat: str = "/proc/stat") -> dict[int, float]:
     """Busy share of each CPU over `interval` seconds (host-wide /proc/stat: other tenants included)."""
     def sample():
         out = {}
