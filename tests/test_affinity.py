@@ -46,13 +46,12 @@ def test_policy_none_and_unknown_leave_the_mask(monkeypatch):
 
 @pytest.mark.skipif(not hasattr(os, "sched_getaffinity"), reason="Linux only")
 def test_apply_restricts_to_the_chosen_domain(monkeypatch, tmp_path):
-    sys_cpu = _fake_sys(tmp_path, [[0, 1, 2, 3], [4, 5, 6, 7]])
-    monkeypatch.setattr(affinity, "SYS_CPU", sys_cpu)
-    monkeypatch.setattr(affinity, "l3_domains", lambda allowed, s=sys_cpu: {0: [0, 1, 2, 3], 4: [4, 5, 6, 7]})
-    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
-    monkeypatch.setattr(affinity, "cpu_busy", lambda cpus: {c: (0.8 if c < 4 else 0.0) for c in cpus})
+    doms = {0: list(range(12)), 12: list(range(12, 24))}
+    monkeypatch.setattr(affinity, "l3_domains", lambda allowed: doms)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(24)))
+    monkeypatch.setattr(affinity, "cpu_busy", lambda cpus: {c: (0.8 if c < 12 else 0.0) for c in cpus})
     got = []
     monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.append(list(cpus)))
-    assert affinity.apply(2, "l3") == [4, 5, 6, 7]
-    assert got == [[4, 5, 6, 7]]
-    assert affinity.apply(3, "l3") is None  # 3 processes need 6 CPUs: no domain has room
+    assert affinity.apply(3, "l3") == list(range(12, 24))  # 3 processes: 12 threads
+    assert got == [list(range(12, 24))]
+    assert affinity.apply(4, "l3") is None  # 4 processes need 16 threads: no domain has room
