@@ -660,6 +660,10 @@ async def run(args, d: Dist) -> dict | None:
                     k, _, v = kv.partition("=")
                     env[k] = v
                 env["NCC_TOPOLOGY_FILE"] = os.path.join(work, "topology.json")
+                # the deployment knob (Helm controller.cpuAffinity, off by default) set to l3: the bench hosts are
+                # shared multi-CCD machines, where the coordinator and its executors on one L3 domain run in the
+                # fast regime (ncc/affinity.py); reported as controller_sizing.cpu_affinity
+                env.setdefault("NCC_CPU_AFFINITY", "l3")
                 # the ops port: /debug/state after the timed waves (each executor's client flow control, the
                 # coordinator's GC passes); executors report their state every second
                 import socket as _socket

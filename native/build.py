@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import platform
 import shlex
 import subprocess
 import sys
@@ -26,6 +27,14 @@ COMMON_HEADERS = [os.path.join(HERE, "common", f) for f in ("byte_scan.hpp",)]  
 def _werror() -> list:
     """NCC_WERROR=1 (the CI lint job): warnings fail the build."""
     return ["-Werror"] if os.environ.get("NCC_WERROR") == "1" else []
+
+
+def arch_flags(machine: str | None = None) -> list:
+    """-mpopcnt on x86-64 only: the JSON block scanner counts bracket bits (native/common/byte_scan.hpp) and
+    every x86-64 CPU since 2008 has the instruction; other targets (aarch64: the arm64 image) lower
+    `__builtin_popcountll` natively and reject the option."""
+    m = (machine or os.environ.get("NCC_TARGET_MACHINE") or platform.machine()).lower()
+    return ["-mpopcnt"] if m in ("x86_64", "amd64", "x64") else []
 
 
 def target_path() -> str:
@@ -57,8 +66,7 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
             return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
-    # -mpopcnt: the JSON block scanner counts bracket bits (every x86-64 CPU since 2008 has the instruction)
-    flags = ["-std=c++20", "-fcoroutines", "-mpopcnt", "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"] + _werror()
+    flags = ["-std=c++20", "-fcoroutines", *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", "-g"] + _werror()
     if coverage:
         flags += ["-O0", "--coverage", "-DNCC_COVERAGE", "-DNCC_SYSTEM_MALLOC"]
     elif debug or sanitize:
@@ -108,8 +116,7 @@ def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool =
         if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + COMMON_HEADERS + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
-    # -mpopcnt: the shared JSON block scanner counts bracket bits (native/common/byte_scan.hpp)
-    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-mpopcnt", "-Wall", "-Wextra",
+    flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra",
              "-Wno-unused-parameter"] + _werror()
     if debug or sanitize:
         flags += ["-O1", "-g", "-fno-omit-frame-pointer"]

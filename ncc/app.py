@@ -240,6 +240,8 @@ class App:
         self.relay = None  # coordinator: WatchRelay feeding the executors
         self.executor_impl = ""  # coordinator: "native" (ncc/bin/ncc-executor) or "python" shard executors
         self.cpu_affinity = ""  # coordinator: "l3:<cpus>" when it restricted itself to one L3 domain, else "none"
+        self.placement = None  # coordinator with NCC_CPU_AFFINITY=l3: ncc.affinity.Placement
+        self._placement_task = None
         self._cred_task = None
         self.native_cfg = None  # coordinator with C++ executors: NativeExecutorConfig (renders their config)
         self._relay_ok = False  # coordinator: the watch relay can run (decided once, in build)
@@ -288,6 +290,13 @@ class App:
                     if os.environ.get("NCC_COORDINATOR_PART"):
                         # a child: the parent's executors serve every key; it relays this partition's reports
                         self.n_executors = 0
+        if o.role == "coordinator" and self.n_executors > 0 and (self.coord_part or (0, 1))[0] == 0:
+            # NCC_CPU_AFFINITY=l3: the coordinator and its executors (and child partitions) on one L3 domain,
+            # chosen here — before anything is spawned (children inherit the mask) and off the propagation path
+            from . import affinity
+            parts = (self.coord_part or (0, 1))[1]
+            self.placement = await affinity.apply_async(1 + self.n_executors * max(1, self.per_shard) + parts - 1)
+            self.cpu_affinity = f"l3:{len(self.placement.cpus)}" if self.placement else "none"
         kf = partition_filter(*o.partition) if o.partition is not None else None
         infs = {rt: self.factory.informer(rt, key_filter=kf if rt in (R.TEMPLATES, R.WORKGROUPS) else None)
                 for rt in (R.SECRETS, R.CONFIGMAPS, R.TEMPLATES, R.WORKGROUPS)}
@@ -348,6 +357,10 @@ class App:
             from .telemetry.http import OpsServer
             self.ops = OpsServer(ready=self._ready,
                                  prometheus=prom, extra=self.debug_state)
+        if cfg.mode == "native":
+            # start-up garbage (imports, config parsing) collected and the survivors frozen now, before any
+            # informer or executor runs: a full pass over a large heap here is off the propagation path
+            gctune.collect_startup()
         return self.controller
 
     async def reload_shards(self) -> dict:
@@ -426,6 +439,9 @@ class App:
             out["executor_impl"] = self.executor_impl
         if self._gc_task is not None:
             out["gc"] = dict(gctune.STATS)
+        if self.placement is not None:
+            out["cpu_placement"] = {"cpus": self.placement.cpus, "checks": self.placement.checks,
+                                    "moves": self.placement.moves}
         if self.elector is not None:
             out["leader"] = {"identity": self.elector.identity, "leading": self.elector.leading,
                              "transitions": self.elector.transitions}
@@ -510,12 +526,6 @@ class App:
             if not use_native:
                 log.debug("Python shard executors: %s", why)
             native_cfg = self.native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
-            if part == 0:
-                # the coordinator and its executors (and child partitions) on one L3 domain: they inherit the
-                # mask (ncc/affinity.py; NCC_CPU_AFFINITY=none leaves it to the kernel)
-                from . import affinity
-                cpus = affinity.apply(1 + self.n_executors * max(1, self.per_shard) + parts - 1)
-                self.cpu_affinity = f"l3:{len(cpus)}" if cpus else "none"
             # One executor group per shard group serves every template key, whatever the number of coordinator
             # partitions: a shard apiserver then serves one executor's watches, not C of them
             # (profiles/r2/c_on_one_shard/: C executors on one shard cost it 12-25 %).
@@ -534,8 +544,12 @@ class App:
                 controller.reports.set_partition(0, parts)
                 controller.forward_reports = self.partitions.forward
                 self.partitions.start()
+            recheck = float(os.environ.get("NCC_CPU_AFFINITY_RECHECK_S", "30"))
+            if self.placement is not None and recheck > 0:
+                self._placement_task = asyncio.ensure_future(self.placement.loop(
+                    recheck, self._child_pids, controller.queue.idle))
         if self.cfg.mode == "native":
-            gctune.tune()
+            gctune.tune()  # thresholds and a freeze only: the start-up garbage was collected in build()
             # NCC_GC_FREEZE="<period>,<generation collected first, or none>" (experiments; default "1,none":
             # freeze every second, after a generation-0 pass when no automatic one ran since the last freeze);
             # NCC_GC_FULL_S: unfreeze + full collection this often, at an idle moment when there is one
@@ -557,6 +571,10 @@ class App:
                  "executors=%d×%d (%s) workers=%d%s", __version__, self.cfg.mode, self.options.role, self.cfg.alias,
                  self.cfg.controller_namespace, controller.all_shard_names, self.n_executors, self.per_shard,
                  self.executor_impl or "in-process", self.options.workers, " (standing by)" if gated else "")
+
+    def _child_pids(self) -> list[int]:
+        return [h.proc.pid for group in (self.pool, self.partitions) if group is not None
+                for h in group.handles if h.proc is not None and h.proc.returncode is None]
 
     def _shard_owner_filter(self, infs: dict):
         """A partitioned executor's filter for shard Secrets/ConfigMaps: owned by one of its partition's
@@ -593,7 +611,8 @@ class App:
 
     async def close(self) -> None:
         log.info("closing (role=%s)", self.options.role)
-        for t in (self._lease_task, self._reload_task, self._gc_task, self._cred_task, self._lag_task):
+        for t in (self._lease_task, self._reload_task, self._gc_task, self._cred_task, self._lag_task,
+                  self._placement_task):
             if t is not None:
                 t.cancel()
                 await asyncio.gather(t, return_exceptions=True)

@@ -617,8 +617,9 @@ class ReconcileMixin:
                                                name, ns, spec, C.FIELD_MANAGER)
         if self.options.concurrent_dependents:
             # dependents need the shard template's UID for their ownerRefs, so they go after it — all at once
-            holder = template if (update is not None or SLIM_FP in shard_template or shard_template.get("spec") is None) \
-                else shard_template  # a shard template still being updated carries the old references
+            # a shard template still being updated, or whose apply was refused, carries the old references
+            holder = template if (update is not None or update_error is not None or SLIM_FP in shard_template
+                                  or shard_template.get("spec") is None) else shard_template
             secrets, configmaps = dependent_names(holder)
             jobs = [self._sync_dependent(R.SECRETS, template, shard_template, shard, n) for n in secrets]
             jobs += [self._sync_dependent(R.CONFIGMAPS, template, shard_template, shard, n) for n in configmaps]
@@ -627,6 +628,8 @@ class ReconcileMixin:
             for r in await gather_all(jobs):
                 if isinstance(r, BaseException):
                     raise r
+            if update_error is not None:  # the dependents went out; the pass still fails with the apply's error
+                raise update_error
         else:
             # after a refused update the shard template still has the old spec: the references are the source's
             holder = template if update_error is not None else None

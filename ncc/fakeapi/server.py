@@ -614,6 +614,7 @@ async def serve(args) -> None:
             ctx.verify_mode = ssl.CERT_REQUIRED
     url = await server.start(args.host, args.port, ctx)
     from .. import gctune
+    gctune.collect_startup()  # before it serves anyone
     gctune.tune(account=False)
     # A test server that keeps what it allocates: freeze every second, never scan the survivors (gctune);
     # NCC_FAKEAPI_GC=collect restores the round-2 controller policy (generation-1 pass + freeze every 5 s)

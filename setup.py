@@ -27,8 +27,11 @@ class BuildWithExecutor(build_ext):
             print(f"warning: native shard executor not built ({e}); native mode will use the Python executor")
 
 
+sys.path.insert(0, os.path.join(HERE, "native"))
+from build import arch_flags  # noqa: E402 — native/build.py: -mpopcnt on x86-64 only
+
 setup(ext_modules=[Pybind11Extension(
     "ncc._native", ["native/ncc_native.cpp"], cxx_std=17,
-    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", "-mpopcnt", "-Wall", "-Wextra",
+    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra",
                         "-Wno-unused-parameter"])],
     cmdclass={"build_ext": BuildWithExecutor})

@@ -45,13 +45,24 @@ def _converged(cl, active=None, meta_sync: bool = False) -> str:
     active = sorted(active if active is not None else range(len(cl.sstates)))
     shards = [cl.env.shard_names[i] for i in active]
     templates = {t["metadata"]["name"]: t for t in cl.cstate.list(R.TEMPLATES, NS)["items"]}
+    missing_events = None
     for name, t in list(templates.items()):
         secrets, cms = _deps(t)
-        if any(cl.cstate.try_get(R.SECRETS, NS, n) is None for n in secrets) or \
-                any(cl.cstate.try_get(R.CONFIGMAPS, NS, n) is None for n in cms):
+        missing = [n for n in secrets if cl.cstate.try_get(R.SECRETS, NS, n) is None] + \
+            [n for n in cms if cl.cstate.try_get(R.CONFIGMAPS, NS, n) is None]
+        if missing:
             # a reference that does not exist: the controller-side GC deleted a Secret the user re-pointed this
             # template at while its previous owners went (adoption made it theirs) — the
-            # reference fails such a template with ErrResourceMissing until the Secret is back, and so do we
+            # reference fails such a template with ErrResourceMissing until the Secret is back, and so do we:
+            # its shard copies are not checked, its Warning Event is
+            if missing_events is None:
+                missing_events = [e for e in cl.cstate.list(R.EVENTS, NS)["items"]
+                                  if e["reason"] == C.ERR_RESOURCE_MISSING]
+            for n in missing:
+                want = C.MESSAGE_RESOURCE_MISSING.format(f'"{n}"', f'"{name}"')
+                if not any(e["involvedObject"]["name"] == name and want in e.get("message", "")
+                           for e in missing_events):
+                    return f"{name}: no {C.ERR_RESOURCE_MISSING} event for its missing reference {n}"
             templates.pop(name)
     for name, t in templates.items():
         st = t.get("status") or {}

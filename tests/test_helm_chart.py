@@ -80,6 +80,16 @@ def test_env_contract_with_the_config_loader():
     assert cfg.failure_rate_base_delay == 0.03 and cfg.failure_rate_max_delay == 5.0
 
 
+def test_cpu_affinity_knob():
+    """`controller.cpuAffinity` reaches the process as NCC_CPU_AFFINITY (ncc/affinity.py); off by default."""
+    env = _env(_one(_docs(), "Deployment"))
+    assert env["NCC_CPU_AFFINITY"] == "none" and env["NCC_CPU_AFFINITY_RECHECK_S"] == "30"
+    env = _env(_one(_docs({"controller": {"cpuAffinity": "l3", "cpuAffinityRecheckSeconds": 0}}), "Deployment"))
+    assert env["NCC_CPU_AFFINITY"] == "l3" and env["NCC_CPU_AFFINITY_RECHECK_S"] == "0"
+    from ncc import affinity
+    assert affinity.policy_from_env(env["NCC_CPU_AFFINITY"]) == "l3"
+
+
 def test_leader_election_branch():
     docs = _docs({"controller": {"leaderElection": {"enabled": True, "replicas": 3, "leaseName": "ncc-lease"}}},
                  release={"Namespace": "ops"})

@@ -276,6 +276,31 @@ async def test_server_side_apply_writes():
     assert env.sstates[0].get(R.CONFIGMAPS, NS, "rogue")["data"] != env.cstate.get(R.CONFIGMAPS, NS, "rogue")["data"]
 
 
+@pytest.mark.parametrize("concurrent", [False, True])
+async def test_server_side_apply_refused_template_still_fails_the_pass(concurrent):
+    """A refused shard-template apply (422) lets the new dependents go out — the shard template keeps its UID —
+    but the pass fails with the apply's error, whichever way the dependents are written; the dependents come
+    from the source template's references, since the shard template still has the old spec."""
+    env = Env(1, server_side_apply=True, concurrent_dependents=concurrent)
+    t = env.seed()
+    name = t["metadata"]["name"]
+    ctl = env.build()
+    await ctl.sync_template(NS, name)
+    env.cstate.create(R.SECRETS, NS, make_secret("s2", NS))
+    src = env.cstate.get(R.TEMPLATES, NS, name)
+    src["spec"]["runtimeEnvironment"]["mappedEnvironmentVariables"].append({"secretRef": {"name": "s2"}})
+    env.cstate.update(R.TEMPLATES, NS, src)
+    env.refresh()
+    env.sclients[0].prepend_reactor("patch", "nexusalgorithmtemplates",
+                                    lambda a: (True, None, E.Invalid("spec: refused")))
+    with pytest.raises(ShardSyncError) as ei:
+        await ctl.sync_template(NS, name)
+    assert isinstance(ei.value.failures["s0"], E.Invalid)
+    assert env.sstates[0].get(R.SECRETS, NS, "s2") is not None
+    st = env.cstate.get(R.TEMPLATES, NS, name)["status"]
+    assert st["conditions"][0]["status"] == "False" and st["syncedToClusters"] == []
+
+
 async def test_response_light_writes_match_server_state():
     """Slim-cache shards publish their own request body (plus the RV/UID scanned from the response): the
     cached slim object must equal what slim-transforming the server's stored object would give."""
