@@ -15,6 +15,12 @@
 #   bash scripts/box/run.sh <out> sample [steps]         sampling profiles of the C++ executor and the coordinator
 #   bash scripts/box/run.sh <out> prof                   rocprofv3 --kernel-trace --stats over a short bench,
 #                                                        and the C++ executor's own sampling profile
+#   bash scripts/box/run.sh <out> modes                  native vs compat-unthrottled vs compat in one session,
+#                                                        N=1 and 8 shards on one rank (reference-compat baseline)
+#   bash scripts/box/run.sh <out> aimd [n]               AIMD vs NCC_AIMD=0 (fixed 256) in alternation, n pairs,
+#                                                        shard RTT 5/20 ms × jitter 0/10/20 ms, N=1 and 8 shards
+#   bash scripts/box/run.sh <out> multishard [n]         n rounds of: suite configs 2, 5, 8 with --stages, then
+#                                                        bench.py N=1 and --shards-per-rank 8 --stages
 #
 # e.g.  gpurun -- 'bash scripts/box/run.sh r4a tier && bash scripts/box/run.sh r4a bench 3'
 set -o pipefail
@@ -36,6 +42,9 @@ print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99",
       "cpp_scan_ns", c.get("cpp_ctl_scan_ns"), "throttled_us", h.get("throttled_usec"),
       "host_busy", h.get("host_busy_cpus"),
       "wakeups", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("loop_wakeups"),
+      "cold_s", d.get("cold_start_s"),
+      "limit", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("limit"),
+      "held", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("increases_held"),
       flush=True)
 EOF
 }
@@ -46,7 +55,7 @@ bench_once() {  # <file> [ARGS...]
   for arg in "$@"; do  # KEY=VAL: environment (bench.py passes it on to the controller); anything else: a flag
     if [[ "$arg" == *=* && "$arg" != -* ]]; then envs+=("$arg"); else flags+=("$arg"); fi
   done
-  env "${envs[@]}" timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 "${flags[@]}" \
+  env "${envs[@]}" timeout -k 10 "${BENCH_TIMEOUT:-300}" python3 bench.py --gpus 1 --steps 20 --warmup 5 "${flags[@]}" \
     > "$f.json" 2> "$f.err" || return $?
   summary "$f.json"
 }
@@ -120,6 +129,47 @@ case "$what" in
       --warmup 5 > "$out/sampled_bench.json" 2> "$out/sampled_bench.err" || exit $?
     python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
     summary "$out/sampled_bench.json"
+    ;;
+  modes)
+    # the reference's scheduling (sequential fail-fast shard loop, Event per reconcile, 2 workers) with and
+    # without client-go's 5 QPS / burst 10, next to native, on one box in one session
+    bench_once "$out/n1_native" || exit $?
+    bench_once "$out/n1_unthrottled_t1000" --mode compat-unthrottled --steps 3 --warmup 1 || exit $?
+    bench_once "$out/n1_native_t100" --templates 100 || exit $?
+    # compat waves take ~40 s each: NCC_BENCH_DEBUG prints a line per wave (gpurun's idle watchdog sees it)
+    BENCH_TIMEOUT=420 bench_once "$out/n1_compat_t100" NCC_BENCH_DEBUG=1 --mode compat --templates 100 --steps 2 \
+      --warmup 1 || exit $?
+    bench_once "$out/s8_native" --shards-per-rank 8 --steps 10 --warmup 3 || exit $?
+    bench_once "$out/s8_unthrottled_t1000" --shards-per-rank 8 --mode compat-unthrottled --steps 2 --warmup 1 || exit $?
+    bench_once "$out/s8_native_t100" --shards-per-rank 8 --templates 100 || exit $?
+    BENCH_TIMEOUT=420 bench_once "$out/s8_compat_t50" NCC_BENCH_DEBUG=1 --shards-per-rank 8 --mode compat \
+      --templates 50 --steps 1 --warmup 1 --timeout 400 || exit $?
+    ;;
+  aimd)
+    n=${1:-1}
+    for i in $(seq 1 "$n"); do
+      for lat in 5 20; do
+        for jit in 0 10 20; do
+          for s in 1 8; do
+            f="l${lat}_j${jit}_s${s}"
+            bench_once "$out/${f}_aimd_$i" --shards-per-rank "$s" --shard-latency-ms "$lat" --shard-jitter-ms "$jit" \
+              --steps 10 --warmup 3 || exit $?
+            bench_once "$out/${f}_fixed_$i" NCC_AIMD=0 --shards-per-rank "$s" --shard-latency-ms "$lat" \
+              --shard-jitter-ms "$jit" --steps 10 --warmup 3 || exit $?
+          done
+        done
+      done
+    done
+    ;;
+  multishard)
+    n=${1:-1}
+    for i in $(seq 1 "$n"); do
+      timeout -k 10 600 python3 bench/suite.py --modes native --configs 2,5,8 --stages --out "$out/suite_$i.json" \
+        > "$out/suite_$i.log" 2>&1 || { tail -30 "$out/suite_$i.log"; exit 1; }
+      cut -c 1-400 "$out/suite_$i.log" | grep '^{'
+      bench_once "$out/n1_$i" --stages || exit $?
+      bench_once "$out/s8_$i" --shards-per-rank 8 --stages || exit $?
+    done
     ;;
   *)
     echo "unknown preset $what" >&2; exit 2;;

@@ -42,3 +42,25 @@ def test_every_environment_variable_is_documented():
     documented = set(re.findall(r"NCC_[A-Z][A-Z_]*[A-Z]", doc))
     missing = {n for n in names if n not in documented and not any(n.startswith(p) for p in ("NCC_OPT_",))}
     assert not missing, sorted(missing)
+
+
+def test_profile_archive_round_trip(tmp_path, monkeypatch):
+    """scripts/archive_profiles.py: a packed run directory reads back file for file (JSON and text)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import archive_profiles as ap
+    monkeypatch.setattr(ap, "ROOT", str(tmp_path))
+    rd = tmp_path / "profiles" / "r9"
+    (rd / "keepme").mkdir(parents=True)
+    (rd / "run1").mkdir()
+    (rd / "run1" / "a.json").write_text('{"value": 1}\n')
+    (rd / "run1" / "a.err").write_text("tail of stderr\n")
+    (rd / "README.md").write_text("# index\n")
+    (rd / "keepme" / "b.json").write_text("{}")
+    packed, left = ap.pack(str(rd), {"keepme"})
+    assert packed == 2 and left == 2
+    assert not (rd / "run1").exists() and (rd / "README.md").exists() and (rd / "keepme" / "b.json").exists()
+    assert json.loads(ap.show(str(rd / "run1" / "a.json"))) == {"value": 1}
+    assert ap.show(str(rd / "run1" / "a.err")) == "tail of stderr\n"
+    assert ap.show(str(rd / "keepme" / "b.json")) == "{}"

@@ -523,9 +523,20 @@ async def test_partitioned_coordinators(tmp_path, impl, monkeypatch):
                 uids = {o["metadata"]["uid"] for o in (await sc.list(R.TEMPLATES, NS))["items"]}
                 sec = await sc.get(R.SECRETS, NS, "shared")
                 assert {r["uid"] for r in sec["metadata"]["ownerReferences"]} == uids and len(uids) == T
-            events = (await cc.list(R.EVENTS, NS))["items"]
-            assert {e["involvedObject"]["name"] for e in events if e["reason"] == C.SUCCESS_SYNCED} == \
-                {f"algo-{i:05d}" for i in range(T)}
+            # Events go out asynchronously after the status write (the broadcaster's writers, as client-go's
+            # sink goroutine): a template can be Ready before its Synced Event is posted — wait for them
+            want = {f"algo-{i:05d}" for i in range(T)}
+            synced = set()
+
+            async def all_synced_events():
+                nonlocal synced
+                events = (await cc.list(R.EVENTS, NS))["items"]
+                synced = {e["involvedObject"]["name"] for e in events if e["reason"] == C.SUCCESS_SYNCED}
+                return synced == want
+            try:
+                await wait_for(all_synced_events, timeout=10, interval=0.05)
+            except AssertionError:
+                raise AssertionError(f"Synced Events missing for {sorted(want - synced)}") from None
             assert app.partitions.forwarded > 0  # the child's statuses came from forwarded reports
 
             # kill the child coordinator: it is restarted and keeps serving its partition
