@@ -21,7 +21,7 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "ncc_native.cpp")]
-COMMON_HEADERS = [os.path.join(HERE, "common", f) for f in ("byte_scan.hpp",)]  # shared with the executor
+COMMON_HEADERS = [os.path.join(HERE, "common", f) for f in ("byte_scan.hpp", "hpack.hpp")]  # shared with the executor
 
 
 def _werror() -> list:

@@ -128,6 +128,7 @@ struct Options {
     int workers = 256;
     int pool_size = 256;
     int pipeline_depth = 1;  // requests per connection (HTTP/1.1 pipelining); in flight ≤ pool_size × depth
+    int http2 = 1;  // client-http2: 0 off, 1 auto (ALPN h2 on TLS, as client-go), 2 on (prior knowledge on cleartext)
     FlowLimits flow;  // client-side flow control per shard (http.hpp): AIMD limit, client-qps bucket
     double request_timeout = 30;
     double coalesce = 0.002;
@@ -2399,6 +2400,8 @@ static void configure(const Value& c) {
     if (const char* ps = std::getenv("NCC_POOL_SIZE")) o.pool_size = std::max(1, std::atoi(ps));  // experiments
     o.pipeline_depth = std::max(1, static_cast<int>(num(c, "pipeline_depth", o.pipeline_depth)));
     if (const char* v = std::getenv("NCC_PIPELINE_DEPTH")) o.pipeline_depth = std::max(1, std::atoi(v));  // experiments
+    o.http2 = static_cast<int>(num(c, "http2", o.http2));
+    if (const char* v = std::getenv("NCC_HTTP2")) o.http2 = std::atoi(v);  // experiments
     o.flow.qps = num(c, "client_qps", 0);
     o.flow.burst = num(c, "client_burst", 10);
     o.flow.adaptive = num(c, "adaptive_concurrency", 1) != 0;
@@ -2430,7 +2433,7 @@ static void configure(const Value& c) {
             auto sh = std::make_unique<Shard>();
             sh->name = std::string(s.sget("name"));
             sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout, o.flow,
-                                                  o.pipeline_depth);
+                                                  o.pipeline_depth, o.http2);
             for (int k = 0; k < 4; ++k) {
                 sh->inf[k].shard = sh.get();
                 sh->inf[k].kind = k;
@@ -2577,11 +2580,12 @@ static void send_status() {
             e.str(inf.last_error);
         }
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
-        // connections, write batches, requests, slow starts left on rising latency, increases held back, and the
-        // executor loop's wake-ups and coalesced wake-ups (process-wide)]
+        // connections, write batches, requests, slow starts left on rising latency, increases held back, the
+        // executor loop's wake-ups and coalesced wake-ups (process-wide), and HTTP/2: in use (0/1), streams
+        // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(15);
+        e.array(19);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2597,6 +2601,10 @@ static void send_status() {
         e.integer(cl.flow.held);
         e.integer(static_cast<long long>(loop().wakeups()));
         e.integer(static_cast<long long>(loop().coalesced()));
+        e.integer(cl.http2() ? 1 : 0);
+        e.integer(cl.h2_streams);
+        e.integer(cl.h2_refused);
+        e.integer(cl.h2_goaways);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

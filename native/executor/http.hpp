@@ -247,6 +247,7 @@ public:
     bool drained = false;  // the last recv returned less than it asked for: the socket had nothing more
     int busy_slot = -1;    // its index in the client's set of connections in use (ConnSet), or -1
     ConnSet* busy_set = nullptr;  // that set: a connection destroyed while in use leaves it (no dangling entry)
+    std::string alpn_selected;    // the protocol TLS negotiated ("h2", "http/1.1", or "" without ALPN)
 
     ~Conn() {
         if (busy_set != nullptr) busy_set->erase(this);
@@ -267,7 +268,9 @@ public:
         if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
     }
 
-    Task<void> connect(const Url& u, SSL_CTX* ctx, const std::string& server_name) {
+    // `offer_h2`: offer ALPN "h2" on a TLS connection (the outcome lands in `alpn_selected`).  A flag, not a
+    // string: GCC 11 mishandles class-type coroutine parameters passed as temporaries.
+    Task<void> connect(const Url& u, SSL_CTX* ctx, const std::string& server_name, bool offer_h2 = false) {
         addrinfo hints{};
         hints.ai_family = AF_UNSPEC;
         hints.ai_socktype = SOCK_STREAM;
@@ -303,9 +306,19 @@ public:
                 X509_VERIFY_PARAM_set1_ip_asc(vp, name.c_str());
             else
                 X509_VERIFY_PARAM_set1_host(vp, name.c_str(), 0);
+            if (offer_h2) {
+                static const unsigned char kAlpnH2[] = {2, 'h', '2'};
+                SSL_set_alpn_protos(ssl, kAlpnH2, sizeof kAlpnH2);
+            }
             while (true) {
                 int r = SSL_connect(ssl);
-                if (r == 1) break;
+                if (r == 1) {
+                    const unsigned char* sel = nullptr;
+                    unsigned sel_len = 0;
+                    SSL_get0_alpn_selected(ssl, &sel, &sel_len);
+                    if (sel != nullptr) alpn_selected.assign(reinterpret_cast<const char*>(sel), sel_len);
+                    break;
+                }
                 int e = SSL_get_error(ssl, r);
                 if (e == SSL_ERROR_WANT_READ) {
                     co_await loop().readable(fd);
@@ -487,6 +500,12 @@ struct Response {
     std::string retry_after;
 };
 
+}  // namespace ncc
+
+#include "h2.hpp"  // HTTP/2 framing and connection state (uses Conn and Response)
+
+namespace ncc {
+
 // A response already complete in the connection's buffer, parsed in place (no coroutine, no per-line
 // strings): the usual case, as an apiserver's answer arrives in one read.  NEED_MORE: read more first;
 // SLOW: chunked or without a length — the coroutine readers below take it from the start.
@@ -648,8 +667,12 @@ struct FlowStats {
 // ------------------------------------------------------------------------------------ client
 class Client {
 public:
-    // `pool_size` keep-alive connections, each carrying up to `depth` pipelined requests
-    Client(Credentials creds, int pool_size, double request_timeout, FlowLimits fl = FlowLimits(), int depth = 1)
+    // `pool_size` keep-alive connections, each carrying up to `depth` pipelined requests.  `http2`: 0 off,
+    // 1 auto (HTTP/2 where TLS negotiates it by ALPN, as client-go), 2 on (also HTTP/2 with prior knowledge on
+    // cleartext) — then the pool is of HTTP/2 connections, each carrying up to the server's
+    // MAX_CONCURRENT_STREAMS streams, and requests in flight stay ≤ pool_size × depth (the admission gate).
+    Client(Credentials creds, int pool_size, double request_timeout, FlowLimits fl = FlowLimits(), int depth = 1,
+           int http2 = 0)
         : creds_(std::move(creds)), max_(std::max(1, pool_size)), depth_(std::max(1, depth)),
           timeout_(request_timeout), fl_(fl) {
         fl_.cap = max_ * depth_;
@@ -665,11 +688,14 @@ public:
                     : creds_.tls_server_name;
         token_ = creds_.token;
         reload_token(true);
+        h2_mode_ = http2;
+        h2_ok_ = http2 == 2 || (http2 == 1 && url_.tls);
     }
     ~Client() {
         closed_ = true;
         pipes_.clear();
         idle_.clear();
+        h2s_.clear();
         if (ctx_ != nullptr) SSL_CTX_free(ctx_);
     }
     void set_token(std::string t) {
@@ -681,7 +707,12 @@ public:
     FlowStats flow;
     double limit() const { return limit_; }
     int inflight() const { return inflight_; }
-    int connections() const { return depth_ > 1 ? static_cast<int>(pipes_.size()) : open_; }
+    int connections() const {
+        if (use_h2()) return static_cast<int>(h2s_.size());
+        return depth_ > 1 ? static_cast<int>(pipes_.size()) : open_;
+    }
+    bool http2() const { return use_h2(); }  // requests go over HTTP/2 (negotiated, or prior knowledge)
+    long long h2_streams = 0, h2_refused = 0, h2_goaways = 0;  // streams opened; re-sent after REFUSED/GOAWAY
     long long sends = 0;  // write batches (requests issued in one loop iteration go out together)
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
@@ -693,12 +724,16 @@ public:
         bool refreshed = false;
         int group = target.rfind("/apis/", 0) == 0 ? 1 : 0;
         while (true) {
-            std::string req = render(method.c_str(), target, body, content_type);
             Response r;  // (no co_await inside a conditional expression: GCC 11 mishandles its temporaries)
-            if (depth_ == 1)
-                r = co_await exchange_direct(method, target, req, group);
-            else
-                r = co_await exchange(method, target, req, group);
+            if (use_h2()) {
+                r = co_await exchange_h2(method, target, body, content_type, group);
+            } else {
+                std::string req = render(method.c_str(), target, body, content_type);
+                if (depth_ == 1)
+                    r = co_await exchange_direct(method, target, req, group);
+                else
+                    r = co_await exchange(method, target, req, group);
+            }
             if (r.status == 401 && !creds_.token_file.empty() && !refreshed) {
                 refreshed = true;
                 reload_token(true);
@@ -804,6 +839,13 @@ private:
     double token_read_at_ = -1e9;
     std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
     ConnSet busy_;
+    int h2_mode_ = 0;     // client-http2: 0 off, 1 auto (ALPN on TLS), 2 on (prior knowledge on cleartext too)
+    bool h2_ok_ = false;  // requests go over HTTP/2 (false again when the server does not negotiate it)
+    std::vector<h2::SessionPtr> h2s_;                 // HTTP/2 connections, oldest first
+    std::deque<std::coroutine_handle<>> h2_waiters_;  // requests waiting for stream room on one of them
+    std::string h2_block_;                            // scratch: the header block being encoded
+    std::string auth_;                                // memoised Authorization value
+    std::string auth_token_;                          // ... for this token
 
     // One keep-alive connection carrying up to `depth_` pipelined requests (HTTP/1.1: the server answers in
     // request order; Go's net/http, i.e. kube-apiserver, serves them one after the other).  Requests issued in
@@ -846,20 +888,31 @@ private:
         key.assign(content_type ? content_type : "");
         auto it = hdr_.find(key);
         if (it != hdr_.end()) return it->second;
-        std::string h = "Host: " + host_ + "\r\nUser-Agent: nexus-configuration-controller/ncc-executor (linux/amd64)"
-                        "\r\nAccept: application/json\r\n";
+        std::string h = "Host: " + host_ + "\r\nUser-Agent: " + kUserAgent + "\r\nAccept: application/json\r\n";
         if (content_type != nullptr) h += std::string("Content-Type: ") + content_type + "\r\n";
+        const std::string& auth = authorization();
+        if (!auth.empty()) h += "Authorization: " + auth + "\r\n";
+        return hdr_[key] = h;
+    }
+    static constexpr const char* kUserAgent = "nexus-configuration-controller/ncc-executor (linux/amd64)";
+    // The Authorization header's value: the bearer token (a file token is re-read once a minute), else basic
+    // auth, else "".
+    const std::string& authorization() {
+        if (!auth_.empty() && auth_token_ == token_) return auth_;
+        auth_token_ = token_;
         if (!token_.empty()) {
-            h += "Authorization: Bearer " + token_ + "\r\n";
+            auth_ = "Bearer " + token_;
         } else if (!creds_.username.empty()) {
             std::string up = creds_.username + ":" + creds_.password;
             std::string b64(4 * ((up.size() + 2) / 3) + 1, '\0');
             int n = EVP_EncodeBlock(reinterpret_cast<unsigned char*>(&b64[0]),
                                     reinterpret_cast<const unsigned char*>(up.data()), static_cast<int>(up.size()));
             b64.resize(static_cast<size_t>(n));
-            h += "Authorization: Basic " + b64 + "\r\n";
+            auth_ = "Basic " + b64;
+        } else {
+            auth_.clear();
         }
-        return hdr_[key] = h;
+        return auth_;
     }
 
     std::string render(const char* method, const std::string& target, const std::string* body,
@@ -1286,6 +1339,424 @@ private:
         }
     }
 
+    // ---- HTTP/2 (h2.hpp): requests as streams multiplexed over few connections
+    bool use_h2() const { return h2_ok_; }
+
+    struct NoH2 : TransportError {
+        using TransportError::TransportError;
+    };
+
+    // The connection a new stream goes on: the oldest with stream room (filling one before the next, as Go's
+    // transport does); a new one while all are at the server's MAX_CONCURRENT_STREAMS and fewer than
+    // `max_` are open; else null — wait for a stream to end.
+    h2::SessionPtr h2_pick() {
+        for (auto& s : h2s_)
+            if (s->has_room()) return s;
+        if (static_cast<int>(h2s_.size()) >= max_) return nullptr;
+        auto s = std::make_shared<h2::Session>();
+        h2s_.push_back(s);
+        spawn(h2_open(s), "h2 connect");
+        return s;
+    }
+    Task<void> h2_open(h2::SessionPtr s) {
+        s->c.deadline = now_s() + timeout_;  // the deadline sweep aborts a connect that hangs
+        track(&s->c);
+        try {
+            co_await s->c.connect(url_, ctx_, creds_.tls_server_name, url_.tls);
+            if (url_.tls && s->c.alpn_selected != "h2")
+                throw NoH2("the server did not negotiate HTTP/2 (ALPN); using HTTP/1.1");
+        } catch (const NoH2& e) {
+            h2_ok_ = false;  // every request from now on, and the ones queued here, go over HTTP/1.1
+            h2_break(s, e.what(), true);
+            co_return;
+        } catch (const std::exception& e) {
+            h2_break(s, e.what(), false);
+            co_return;
+        }
+        if (s->broken) co_return;
+        s->connected = true;
+        s->c.deadline = 0;  // streams carry their own deadlines
+        h2_kick(s);
+        s->reading = true;
+        spawn(h2_read(s), "h2 reader");
+    }
+    // Flush what the session has queued at the end of this loop iteration: every stream opened, window update
+    // and ack of the iteration goes out in one write.
+    void h2_kick(const h2::SessionPtr& s) {
+        if (!s->connected || s->broken || s->out.empty() || s->flush_posted || s->writing) return;
+        s->flush_posted = true;
+        loop().call_soon([this, s] {
+            s->flush_posted = false;
+            if (!s->writing && !s->broken && !s->out.empty()) {
+                s->writing = true;
+                spawn(h2_write(s), "h2 writer");
+            }
+        });
+    }
+    Task<void> h2_write(h2::SessionPtr s) {
+        while (!s->out.empty() && !s->broken) {
+            std::string data;
+            data.swap(s->out);
+            ++sends;
+            try {
+                co_await s->c.write_all(data);
+            } catch (const std::exception& e) {
+                h2_break(s, e.what(), false);
+            }
+        }
+        s->writing = false;
+    }
+    Task<void> h2_read(h2::SessionPtr s) {
+        Conn& c = s->c;
+        try {
+            while (!s->broken) {
+                while (c.buf.size() - c.pos >= 9) {
+                    const char* p = c.buf.data() + c.pos;
+                    uint32_t len = (uint32_t{static_cast<uint8_t>(p[0])} << 16) |
+                                   (uint32_t{static_cast<uint8_t>(p[1])} << 8) | static_cast<uint8_t>(p[2]);
+                    if (len > h2::kOurMaxFrame) throw TransportError("HTTP/2: frame larger than SETTINGS_MAX_FRAME_SIZE");
+                    if (c.buf.size() - c.pos < 9 + len) break;
+                    uint8_t type = static_cast<uint8_t>(p[3]), flags = static_cast<uint8_t>(p[4]);
+                    uint32_t sid = h2::get32(p + 5) & 0x7fffffffu;
+                    std::string_view payload(p + 9, len);
+                    h2_frame(*s, type, flags, sid, payload);  // (consumes the frame before anything can refill)
+                    c.pos += 9 + len;
+                    if (s->broken) break;
+                }
+                if (s->broken) break;
+                if (s->goaway && s->streams.empty()) {
+                    h2_break(s, "connection closed after GOAWAY", true);
+                    break;
+                }
+                h2_kick(s);  // acks, window updates and request bodies the frames released
+                co_await c.fill();
+            }
+        } catch (const hpack::Error& e) {
+            h2_break(s, std::string("HTTP/2: HPACK: ") + e.what(), false);
+        } catch (const std::exception& e) {
+            h2_break(s, e.what(), false);
+        }
+        s->reading = false;
+    }
+    static std::string_view h2_strip(uint8_t flags, std::string_view p, bool headers) {
+        size_t pad = 0;
+        if (flags & h2::PADDED) {
+            if (p.empty()) throw TransportError("HTTP/2: padded frame without a pad length");
+            pad = static_cast<uint8_t>(p[0]);
+            p.remove_prefix(1);
+        }
+        if (headers && (flags & h2::PRIORITY_FLAG)) {
+            if (p.size() < 5) throw TransportError("HTTP/2: short PRIORITY fields");
+            p.remove_prefix(5);
+        }
+        if (pad > p.size()) throw TransportError("HTTP/2: padding longer than the frame");
+        p.remove_suffix(pad);
+        return p;
+    }
+    void h2_frame(h2::Session& s, uint8_t type, uint8_t flags, uint32_t sid, std::string_view p) {
+        using namespace h2;
+        if (s.cont_id != 0 && (type != CONTINUATION || sid != s.cont_id))
+            throw TransportError("HTTP/2: a header block interrupted before its CONTINUATION");
+        switch (type) {
+            case DATA: {
+                s.conn_recv_unacked += static_cast<int64_t>(p.size());
+                std::string_view d = h2_strip(flags, p, false);
+                auto it = s.streams.find(sid);
+                if (it != s.streams.end()) {
+                    Stream* st = it->second;
+                    st->r.body.append(d.data(), d.size());
+                    st->recv_unacked += static_cast<int64_t>(p.size());
+                    if (flags & END_STREAM) {
+                        h2_complete(s, st, st->got_headers);
+                    } else if (st->recv_unacked >= kStreamWindow / 2) {
+                        s.window_update(sid, st->recv_unacked);
+                        st->recv_unacked = 0;
+                    }
+                }
+                if (s.conn_recv_unacked >= kConnWindow / 2) {
+                    s.window_update(0, s.conn_recv_unacked);
+                    s.conn_recv_unacked = 0;
+                }
+                break;
+            }
+            case HEADERS: {
+                std::string_view b = h2_strip(flags, p, true);
+                s.cont_block.assign(b.data(), b.size());
+                s.cont_end_stream = (flags & END_STREAM) != 0;
+                if (flags & END_HEADERS)
+                    h2_headers_in(s, sid);
+                else
+                    s.cont_id = sid;
+                break;
+            }
+            case CONTINUATION: {
+                if (s.cont_id == 0) throw TransportError("HTTP/2: CONTINUATION without HEADERS");
+                s.cont_block.append(p.data(), p.size());
+                if (flags & END_HEADERS) {
+                    uint32_t id = s.cont_id;
+                    s.cont_id = 0;
+                    h2_headers_in(s, id);
+                }
+                break;
+            }
+            case RST_STREAM: {
+                uint32_t code = p.size() >= 4 ? get32(p.data()) : 0;
+                auto it = s.streams.find(sid);
+                if (it != s.streams.end()) {
+                    Stream* st = it->second;
+                    st->err = "stream reset by the server (HTTP/2 error " + std::to_string(code) + ")";
+                    st->retryable = code == REFUSED_STREAM;
+                    if (st->retryable) ++h2_refused;
+                    h2_complete(s, st, false);
+                }
+                break;
+            }
+            case SETTINGS: {
+                if (flags & ACK) break;
+                if (p.size() % 6 != 0) throw TransportError("HTTP/2: SETTINGS of a bad length");
+                for (size_t k = 0; k + 6 <= p.size(); k += 6) {
+                    uint16_t id = static_cast<uint16_t>((static_cast<uint8_t>(p[k]) << 8) | static_cast<uint8_t>(p[k + 1]));
+                    uint32_t v = get32(p.data() + k + 2);
+                    if (id == INITIAL_WINDOW_SIZE) {
+                        if (v > 0x7fffffffu) throw TransportError("HTTP/2: INITIAL_WINDOW_SIZE above 2^31-1");
+                        int64_t delta = static_cast<int64_t>(v) - s.peer_initial_window;
+                        s.peer_initial_window = v;
+                        for (auto& kv : s.streams) kv.second->send_window += delta;
+                    } else if (id == MAX_FRAME_SIZE) {
+                        if (v < 16384 || v > 16777215) throw TransportError("HTTP/2: MAX_FRAME_SIZE out of range");
+                        s.peer_max_frame = v;
+                    } else if (id == MAX_CONCURRENT_STREAMS) {
+                        s.peer_max_streams = v;
+                    }
+                }
+                put_frame(s.out, SETTINGS, ACK, 0, nullptr, 0);
+                h2_resume(s);
+                h2_wake();  // the stream limit may have grown
+                break;
+            }
+            case PING:
+                if (!(flags & ACK)) put_frame(s.out, PING, ACK, 0, p.data(), p.size());
+                break;
+            case GOAWAY: {
+                uint32_t last = p.size() >= 4 ? get32(p.data()) & 0x7fffffffu : 0;
+                s.goaway = true;
+                s.goaway_last = last;
+                ++h2_goaways;
+                std::vector<Stream*> gone;
+                for (auto& kv : s.streams)
+                    if (kv.first > last) gone.push_back(kv.second);
+                for (Stream* st : gone) {  // never processed: safe to send again, on another connection
+                    st->err = "GOAWAY: the server will not process the stream";
+                    st->retryable = true;
+                    h2_complete(s, st, false);
+                }
+                h2_wake();
+                break;
+            }
+            case WINDOW_UPDATE: {
+                uint32_t inc = p.size() >= 4 ? get32(p.data()) & 0x7fffffffu : 0;
+                if (sid == 0) {
+                    s.conn_send_window += inc;
+                } else {
+                    auto it = s.streams.find(sid);
+                    if (it != s.streams.end()) it->second->send_window += inc;
+                }
+                h2_resume(s);
+                break;
+            }
+            case PUSH_PROMISE:
+                throw TransportError("HTTP/2: PUSH_PROMISE although push is disabled");
+            default:  // PRIORITY, and unknown types are ignored (RFC 9113 §4.1)
+                break;
+        }
+    }
+    // A complete header block: decoded whatever it belongs to (the HPACK table is the connection's), then the
+    // status and Retry-After of the stream's response; a second block is trailers, an 1xx is skipped.
+    void h2_headers_in(h2::Session& s, uint32_t sid) {
+        std::vector<hpack::Decoder::Header> hs;
+        s.dec.decode(reinterpret_cast<const uint8_t*>(s.cont_block.data()), s.cont_block.size(), hs);
+        auto it = s.streams.find(sid);
+        if (it == s.streams.end()) return;
+        h2::Stream* st = it->second;
+        if (!st->got_headers) {
+            int status = 0;
+            std::string retry_after;
+            for (auto& h : hs) {
+                if (h.first == ":status")
+                    status = std::atoi(h.second.c_str());
+                else if (h.first == "retry-after")
+                    retry_after = std::move(h.second);
+            }
+            if (status >= 100 && status < 200 && !s.cont_end_stream) return;  // interim response
+            st->r.status = status;
+            st->r.retry_after = std::move(retry_after);
+            st->got_headers = true;
+        }
+        if (s.cont_end_stream) h2_complete(s, st, true);
+    }
+    // Send the request bodies that were waiting for flow-control window.
+    void h2_resume(h2::Session& s) {
+        for (size_t i = 0; i < s.blocked.size();) {
+            h2::Stream* st = s.blocked[i];
+            if (s.send_body(st)) {
+                st->body_pending = false;
+                s.blocked.erase(s.blocked.begin() + static_cast<long>(i));
+            } else {
+                ++i;
+            }
+        }
+    }
+    void h2_complete(h2::Session& s, h2::Stream* st, bool ok) {
+        st->ok = ok && st->got_headers;
+        st->done = true;
+        s.streams.erase(st->id);
+        if (st->body_pending)
+            for (size_t i = 0; i < s.blocked.size(); ++i)
+                if (s.blocked[i] == st) {
+                    s.blocked.erase(s.blocked.begin() + static_cast<long>(i));
+                    break;
+                }
+        if (st->h) loop().post(st->h);
+        h2_wake();
+    }
+    void h2_wake() {
+        while (!h2_waiters_.empty()) {
+            loop().post(h2_waiters_.front());
+            h2_waiters_.pop_front();
+        }
+    }
+    // A connection failed (or was refused for HTTP/2, or drained after GOAWAY): its streams fail — `retryable`
+    // ones are sent again elsewhere, the others once more like a stale keep-alive connection's request.
+    void h2_break(const h2::SessionPtr& s, const std::string& err, bool retryable) {
+        if (s->broken) return;
+        s->broken = true;
+        std::vector<h2::Stream*> open;
+        for (auto& kv : s->streams) open.push_back(kv.second);
+        double now = now_s();
+        for (h2::Stream* st : open) {
+            st->err = err;
+            st->retryable = retryable;
+            st->timed_out = now >= st->deadline;
+            h2_complete(*s, st, false);
+        }
+        s->streams.clear();
+        s->blocked.clear();
+        s->out.clear();
+        busy_.erase(&s->c);
+        s->c.close();
+        for (size_t i = 0; i < h2s_.size(); ++i)
+            if (h2s_[i] == s) {
+                h2s_.erase(h2s_.begin() + static_cast<long>(i));
+                break;
+            }
+        h2_wake();
+    }
+    void h2_headers_out(h2::Session& s, uint32_t id, const std::string& method, const std::string& target,
+                        const std::string* body, const char* content_type) {
+        std::string& b = h2_block_;
+        b.clear();
+        if (method == "GET")
+            hpack::encode_indexed(b, 2);
+        else if (method == "POST")
+            hpack::encode_indexed(b, 3);
+        else
+            hpack::encode_literal(b, ":method", method);
+        hpack::encode_indexed(b, url_.tls ? 7 : 6);  // :scheme
+        hpack::encode_literal(b, ":authority", host_);
+        if (url_.prefix.empty()) {
+            hpack::encode_literal(b, ":path", target);
+        } else {
+            hpack::encode_literal(b, ":path", url_.prefix + target);
+        }
+        hpack::encode_literal(b, "user-agent", kUserAgent);
+        hpack::encode_literal(b, "accept", "application/json");
+        if (body != nullptr) {
+            hpack::encode_literal(b, "content-type", content_type != nullptr ? content_type : "application/json");
+            char num[24];
+            auto [end, ec] = std::to_chars(num, num + sizeof num, body->size());
+            hpack::encode_literal(b, "content-length", std::string_view(num, static_cast<size_t>(end - num)));
+        }
+        reload_token(false);
+        const std::string& auth = authorization();
+        if (!auth.empty()) hpack::encode_literal(b, "authorization", auth);
+        bool end_stream = body == nullptr || body->empty();
+        size_t off = 0, n = std::min<size_t>(b.size(), s.peer_max_frame);
+        bool more = n < b.size();
+        h2::put_frame(s.out, h2::HEADERS, static_cast<uint8_t>((end_stream ? h2::END_STREAM : 0) | (more ? 0 : h2::END_HEADERS)),
+                      id, b.data(), n);
+        off = n;
+        while (off < b.size()) {
+            n = std::min<size_t>(b.size() - off, s.peer_max_frame);
+            more = off + n < b.size();
+            h2::put_frame(s.out, h2::CONTINUATION, more ? 0 : h2::END_HEADERS, id, b.data() + off, n);
+            off += n;
+        }
+    }
+    Task<Response> exchange_h2(const std::string& method, const std::string& target, const std::string* body,
+                               const char* content_type, int group) {
+        int resent = 0;
+        for (int tries = 0;; ++tries) {
+            if (!use_h2()) {  // the server turned out not to speak HTTP/2: this request and the rest over HTTP/1.1
+                std::string req = render(method.c_str(), target, body, content_type);
+                if (depth_ == 1) co_return co_await exchange_direct(method, target, req, group);
+                co_return co_await exchange(method, target, req, group);
+            }
+            uint64_t seq;
+            if (!try_admit(group, seq)) seq = co_await admit(group);
+            if (closed_) {
+                finish(seq, 0, 0, false);
+                throw TransportError("client closed");
+            }
+            h2::SessionPtr s;
+            while ((s = h2_pick()) == nullptr) {  // every connection at its stream limit: wait for one to end
+                struct Park {
+                    Client* cl;
+                    bool await_ready() { return false; }
+                    void await_suspend(std::coroutine_handle<> h) { cl->h2_waiters_.push_back(h); }
+                    void await_resume() {}
+                };
+                co_await Park{this};
+            }
+            h2::Stream st;
+            double t0 = now_s();
+            st.deadline = t0 + timeout_;
+            st.send_window = s->peer_initial_window;
+            st.body = body;
+            st.id = s->next_id;
+            s->next_id += 2;
+            s->streams[st.id] = &st;
+            ++h2_streams;
+            h2_headers_out(*s, st.id, method, target, body, content_type);
+            if (body != nullptr && !body->empty() && !s->send_body(&st)) {
+                st.body_pending = true;
+                s->blocked.push_back(&st);
+            }
+            h2_kick(s);
+            struct Suspend {
+                h2::Stream* st;
+                bool await_ready() { return st->done; }
+                void await_suspend(std::coroutine_handle<> h) { st->h = h; }
+                void await_resume() {}
+            };
+            co_await Suspend{&st};
+            finish(seq, st.ok ? st.r.status : 0, now_s() - t0, st.timed_out, method == "GET" ? 0 : 1);
+            if (st.ok) {
+                ++requests;
+                co_return std::move(st.r);
+            }
+            ++request_errors;
+            if (st.timed_out) throw TransportError(method + " " + target + ": request timed out");
+            if (st.retryable && resent++ < 8) {  // never processed (REFUSED_STREAM, GOAWAY, no HTTP/2): again
+                --tries;
+                continue;
+            }
+            // the connection failed under it: once more on another (every write here is safe to repeat, see
+            // exchange)
+            if (tries == 0) continue;
+            throw TransportError(method + " " + target + ": " + st.err);
+        }
+    }
+
     // A connection in use (request or watch stream) is under the deadline sweep, which runs only while
     // there is one: an executor whose shard is unreachable or idle is not woken twice a second for nothing.
     void track(Conn* c) {
@@ -1302,6 +1773,20 @@ private:
             double now = now_s();
             for (Conn* c : busy_.snapshot())
                 if (c->deadline > 0 && now >= c->deadline) c->abort();
+            // HTTP/2: an overdue stream is cancelled alone; its connection carries on
+            std::vector<h2::SessionPtr> sessions = h2s_;
+            for (auto& s : sessions) {
+                std::vector<h2::Stream*> late;
+                for (auto& kv : s->streams)
+                    if (now >= kv.second->deadline) late.push_back(kv.second);
+                for (h2::Stream* st : late) {
+                    st->timed_out = true;
+                    st->err = "request timed out";
+                    s->rst(st->id, h2::CANCEL);
+                    h2_complete(*s, st, false);
+                }
+                if (!late.empty()) h2_kick(s);
+            }
         }
         sweeping_ = false;
     }

@@ -36,6 +36,7 @@
 //  * ReportTable — the coordinator's fold of shard-executor reports, fed raw IPC frames.
 
 #include "common/byte_scan.hpp"
+#include "common/hpack.hpp"
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -59,7 +60,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 22
+#define NCC_NATIVE_ABI 23
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -2472,6 +2473,47 @@ class ReportTable {
     int part_ = 0, parts_ = 1;
     std::map<int, std::vector<std::string>> forwards_;
 };
+// HPACK for the fake apiserver's HTTP/2 server (ncc/fakeapi/h2.py): the decoder keeps the connection's dynamic
+// table; the encoder is stateless (native/common/hpack.hpp)
+class HpackDecoder {
+public:
+    explicit HpackDecoder(size_t max_table) : d_(max_table) {}
+    py::list decode(const py::bytes& block) {
+        std::string_view b = block;
+        std::vector<ncc::hpack::Decoder::Header> hs;
+        try {
+            d_.decode(reinterpret_cast<const uint8_t*>(b.data()), b.size(), hs);
+        } catch (const ncc::hpack::Error& e) {
+            throw py::value_error(std::string("HPACK: ") + e.what());
+        }
+        py::list out;
+        for (auto& h : hs) out.append(py::make_tuple(py::str(h.first), py::str(h.second)));
+        return out;
+    }
+    void set_limit(size_t n) { d_.set_limit(n); }
+    size_t table_size() const { return d_.table_size(); }
+    size_t table_entries() const { return d_.table_entries(); }
+
+private:
+    ncc::hpack::Decoder d_;
+};
+
+py::bytes hpack_encode(const std::vector<std::pair<std::string, std::string>>& fields, bool huffman) {
+    std::string out;
+    for (const auto& f : fields) ncc::hpack::encode_field(out, f.first, f.second, huffman);
+    return py::bytes(out);
+}
+
+py::bytes hpack_huffman_decode(const py::bytes& data) {
+    std::string_view b = data;
+    std::string out;
+    try {
+        ncc::hpack::huffman_decode(reinterpret_cast<const uint8_t*>(b.data()), b.size(), out);
+    } catch (const ncc::hpack::Error& e) {
+        throw py::value_error(std::string("HPACK: ") + e.what());
+    }
+    return py::bytes(out);
+}
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -2508,6 +2550,18 @@ PYBIND11_MODULE(_native, m) {
           "with `items` (the store's dict) an unchanged status or reference list is taken from the cached version");
     m.def("scan_event_owners", &scan_event_owners, py::arg("line"),
           "scan_event plus the tuples of metadata.ownerReferences[*].name and [*].uid, or None");
+    py::class_<HpackDecoder>(m, "HpackDecoder")
+        .def(py::init<size_t>(), py::arg("max_table") = 4096)
+        .def("decode", &HpackDecoder::decode, py::arg("block"),
+             "one complete header block -> [(name, value)]; ValueError on a malformed block")
+        .def("set_limit", &HpackDecoder::set_limit)
+        .def("table_size", &HpackDecoder::table_size)
+        .def("table_entries", &HpackDecoder::table_entries);
+    m.def("hpack_encode", &hpack_encode, py::arg("fields"), py::arg("huffman") = false,
+          "a header block of static-table fields and literals without indexing");
+    m.def("hpack_huffman_encode", [](const py::bytes& s) { return py::bytes(ncc::hpack::huffman_encode(std::string_view(s))); },
+          py::arg("data"));
+    m.def("hpack_huffman_decode", &hpack_huffman_decode, py::arg("data"));
     py::class_<RateLimitingQueue>(m, "RateLimitingQueue")
         .def(py::init<double, double, double, int>(), py::arg("base_delay"), py::arg("max_delay"), py::arg("qps"),
              py::arg("burst"))

@@ -4,7 +4,7 @@ The coordinator relays every watch line to its executors and folds every report 
 sides exchange cache lines all the time.  On a host whose CPUs span several L3 domains (an EPYC has one per
 CCD), the kernel places them wherever it finds room, and moves them; the box measurements show two regimes for
 the same tree and load — coordinator ≈ 9 and executors ≈ 11 µs per object when they share a domain, ≈ 12 and
-≈ 14 when they do not — while pinning them to one domain held every run in the fast one (BENCHMARKS.md,
+≈ 14 when they do not — while pinning them to one domain held every run in the fast one (docs/BENCHMARKS_ARCHIVE.md,
 `profiles/r4/r4v`, `r4w`, `r4z`, `r4ab`).
 
 `NCC_CPU_AFFINITY` (Helm `controller.cpuAffinity`):

@@ -281,7 +281,7 @@ class Informer:
             tap = self.tap
             if batches is not None and tap is not None and getattr(self.client, "supports_line_tap", False):
                 # the relay gets every line straight off the socket: an executor is not kept waiting while
-                # this coordinator works through the batches before it (BENCHMARKS.md, latency stages)
+                # this coordinator works through the batches before it (docs/BENCHMARKS_ARCHIVE.md, latency stages)
                 source = batches(self.rt, self.namespace, on_lines=tap.on_lines, **kw)
                 tap = None
             elif batches is not None:

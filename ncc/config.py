@@ -11,7 +11,7 @@ The YAML files list every key with `""` (.container/appconfig.yaml:1-10): an emp
 Go zero values, so a bare `python -m ncc` is usable.
 
 Extra keys of this framework (all optional, same env convention): `mode`, `client-qps`,
-`client-burst`, `client-pool-size`, `client-pipeline-depth`, `transport`, `server-side-apply`, `sync-dependent-metadata`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `event-repeat-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
+`client-burst`, `client-pool-size`, `client-pipeline-depth`, `client-http2`, `transport`, `server-side-apply`, `sync-dependent-metadata`, `controller-adoption`, `executors`, `max-executors`, `executors-per-shard`, `resync-period`, `full-resync-period`, `shard-sync-timeout`, `shard-reload-period`, `coalesce-window`, `event-repeat-window`, `native-workers`, `coordinator-partitions`, `watch-relay`, `executor-impl`,
 `metrics-bind-address`, `health-bind-address`, `log-format`, `leader-elect`,
 `leader-election-namespace`, `leader-election-lease-name`, `lease-duration`, `renew-deadline`, `retry-period`.
 """
@@ -84,6 +84,8 @@ class AppConfig:
                                      # 256 for the C++ executor's shard clients
     client_pipeline_depth: int = 0   # HTTP/1.1-pipelined requests per connection (in flight ≤ pool × depth);
                                      # 0 = auto: 1 (no pipelining)
+    client_http2: str = "auto"       # the C++ executor's shard clients: auto (HTTP/2 where TLS negotiates it by
+                                     # ALPN, as client-go) | on (also prior-knowledge HTTP/2 on cleartext) | off
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     sync_dependent_metadata: bool = False  # native mode: shard Secrets/ConfigMaps carry the source's labels
@@ -152,6 +154,9 @@ def _read_yaml(path: str) -> dict:
         return yaml.safe_load(fh) or {}
 
 
+HTTP2_MODES = {"off": 0, "auto": 1, "on": 2}  # client-http2 -> the C++ executor's `http2` (native/executor/http.hpp)
+
+
 def load_config(config_dir: str | None = None, env: dict | None = None) -> AppConfig:
     env = os.environ if env is None else env
     config_dir = config_dir or env.get("NCC_CONFIG_DIR") or os.getcwd()
@@ -169,7 +174,12 @@ def load_config(config_dir: str | None = None, env: dict | None = None) -> AppCo
         if raw is None or raw == "":
             continue
         try:
-            setattr(cfg, f.name, _coerce(f, raw))
+            v = _coerce(f, raw)
+            if f.name == "client_http2":
+                v = str(v).strip().lower()
+                if v not in HTTP2_MODES:
+                    raise ValueError(f"one of {', '.join(HTTP2_MODES)}")
+            setattr(cfg, f.name, v)
         except ValueError as e:
             raise ValueError(f"invalid value for {AppConfig.key_of(f.name)}: {raw!r} ({e})") from e
     return cfg

@@ -32,7 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 # `client-pipeline-depth` are 0 (auto): 256 requests in flight at most.  No pipelining by default: an
 # HTTP/1.1 server (kube-apiserver's Go net/http) serves one connection's requests one after the other, so
 # only connections give a shard apiserver requests to run concurrently (APF seats, etcd round trips); and on
-# the bench, 32 connections × 8 coalesced only 1.3 requests per write (BENCHMARKS.md).  Pipelining pays for a
+# the bench, 32 connections × 8 coalesced only 1.3 requests per write (docs/BENCHMARKS_ARCHIVE.md).  Pipelining pays for a
 # far-away shard, where the round trip rather than the apiserver bounds a connection.
 DEFAULT_POOL_SIZE = 256
 DEFAULT_PIPELINE_DEPTH = 1
@@ -123,6 +123,7 @@ class NativeExecutorConfig:
 
     async def render(self, handle) -> str:
         from ..app import client_limits
+        from ..config import HTTP2_MODES
         o, cfg = self.options, self.cfg
         shards = [await self.shard_entry(n) for n in handle.shards]
         qps, burst = client_limits(cfg)
@@ -136,6 +137,7 @@ class NativeExecutorConfig:
             # 429/503/timeouts) and the client-qps bucket
             "workers": 4 * max(DEFAULT_POOL_SIZE * DEFAULT_PIPELINE_DEPTH, pool * depth), "pool_size": pool,
             "pipeline_depth": depth, "client_qps": qps, "client_burst": burst,
+            "http2": HTTP2_MODES.get(str(cfg.client_http2).lower(), 1),
             "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
             "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,
             "rate_limit_qps": o.rate_limit_qps, "rate_limit_burst": o.rate_limit_burst,

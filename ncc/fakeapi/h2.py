@@ -1,0 +1,400 @@
+"""HTTP/2 (RFC 9113) for the fake kube-apiserver: the server side of the shard executor's HTTP/2 client.
+
+client-go talks to kube-apiservers over HTTP/2 — ALPN "h2" on TLS — multiplexing every request of a clientset
+on one connection (`/root/reference/main.go:52-68` builds the clients; Go's transport negotiates h2).  The
+C++ shard executor does the same with `client-http2` (native/executor/h2.hpp); this module lets the fake
+apiserver answer it, so the HTTP/2 path runs against the same substrate as everything else:
+
+* negotiation: ALPN "h2" on a TLS connection (`--http2` puts it in the server's ALPN list), or the client
+  connection preface on a cleartext one ("prior knowledge", how the benches and tests run it unencrypted);
+* one `H2Connection` per connection on top of `httpserver._ServerConn`: frames parsed as they arrive, HPACK
+  decoded by the extension's decoder (native/common/hpack.hpp, one dynamic table per connection), each
+  complete stream handed to the same handlers as an HTTP/1.1 request — concurrently, as streams are;
+* responses as HEADERS + DATA within the client's flow-control windows (connection and stream), queued
+  until a WINDOW_UPDATE when they do not fit; watch streams as DATA frames without END_STREAM;
+* SETTINGS (MAX_CONCURRENT_STREAMS enforced with REFUSED_STREAM), PING, RST_STREAM, WINDOW_UPDATE, GOAWAY.
+
+Fault knobs (`POST /_fake/faults`), for connections opened afterwards: `h2_goaway_after` — after that many
+streams a connection sends GOAWAY naming the last stream it will serve, and refuses later ones (a
+kube-apiserver does this on shutdown and, with `--goaway-chance`, to rebalance clients); `h2_max_streams` — the
+MAX_CONCURRENT_STREAMS advertised; `h2_initial_window` — the stream window advertised (request bodies larger
+than it wait for the WINDOW_UPDATEs the server sends as it reads).
+"""
+from __future__ import annotations
+
+import asyncio
+import struct
+
+from .. import native as _native
+
+PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+
+DATA, HEADERS, PRIORITY, RST_STREAM, SETTINGS, PUSH_PROMISE, PING, GOAWAY, WINDOW_UPDATE, CONTINUATION = range(10)
+END_STREAM = ACK = 0x1
+END_HEADERS = 0x4
+PADDED = 0x8
+PRIORITY_FLAG = 0x20
+
+S_HEADER_TABLE_SIZE, S_ENABLE_PUSH, S_MAX_CONCURRENT_STREAMS, S_INITIAL_WINDOW_SIZE, S_MAX_FRAME_SIZE, \
+    S_MAX_HEADER_LIST_SIZE = range(1, 7)
+NO_ERROR, PROTOCOL_ERROR, INTERNAL_ERROR, FLOW_CONTROL_ERROR, _SETTINGS_TIMEOUT, STREAM_CLOSED, FRAME_SIZE_ERROR, \
+    REFUSED_STREAM, CANCEL, COMPRESSION_ERROR = range(10)
+
+OUR_WINDOW = 1 << 24  # per stream; the connection window is raised to 1 GiB at start
+OUR_MAX_FRAME = 1 << 14
+
+_HOP_BY_HOP = {"connection", "keep-alive", "transfer-encoding", "upgrade", "proxy-connection"}
+
+
+class ProtocolError(Exception):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def frame(ftype: int, flags: int, stream: int, payload: bytes = b"") -> bytes:
+    n = len(payload)
+    return struct.pack(">BHBBI", n >> 16, n & 0xFFFF, ftype, flags, stream & 0x7FFFFFFF) + payload
+
+
+class _Stream:
+    __slots__ = ("id", "headers", "block", "body", "send_window", "pending", "ended", "closed", "response_started",
+                 "eof_pending")
+
+    def __init__(self, sid: int, window: int):
+        self.id = sid
+        self.headers: list = []
+        self.block = bytearray()  # header block fragments (HEADERS + CONTINUATION)
+        self.body = bytearray()
+        self.send_window = window
+        self.pending = bytearray()  # response DATA not yet within the windows
+        self.eof_pending = False    # END_STREAM to send once `pending` is out
+        self.ended = False          # the client's half is closed
+        self.closed = False         # reset, or our END_STREAM sent
+        self.response_started = False
+
+
+class H2Connection:
+    """The HTTP/2 side of one `_ServerConn` (see the module doc)."""
+
+    def __init__(self, conn, server):
+        self.conn = conn
+        self.server = server
+        self.transport = conn.transport
+        self.buf = bytearray()
+        self.preface_seen = False
+        self.decoder = _native.load(required=True).HpackDecoder(4096)
+        self.streams: dict[int, _Stream] = {}
+        self.last_stream = 0
+        self.served = 0
+        self.goaway_sent = False
+        self.conn_send_window = 65535
+        self.peer_initial_window = 65535
+        self.peer_max_frame = 16384
+        self.recv_unacked = 0
+        self.continuation: _Stream | None = None
+        self.max_streams = int(server.h2_options.get("h2_max_streams", 0) or 0) or 250
+        self.goaway_after = int(server.h2_options.get("h2_goaway_after", 0) or 0)
+        # a small stream window makes a client's request bodies wait for our WINDOW_UPDATEs (tests)
+        self.our_window = int(server.h2_options.get("h2_initial_window", 0) or 0) or OUR_WINDOW
+        st = server.h2_stats
+        st["connections"] += 1
+        self.open_streams = 0
+        # our SETTINGS, and the connection window raised to 1 GiB
+        self.transport.write(frame(SETTINGS, 0, 0, struct.pack(
+            ">HIHIHIHI", S_MAX_CONCURRENT_STREAMS, self.max_streams, S_INITIAL_WINDOW_SIZE, self.our_window,
+            S_MAX_FRAME_SIZE, OUR_MAX_FRAME, S_ENABLE_PUSH, 0)) +
+            frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", (1 << 30) - 65535)))
+
+    # ------------------------------------------------------------------ input
+    def data_received(self, data: bytes) -> None:
+        self.buf += data
+        try:
+            self._parse()
+        except ProtocolError as e:
+            self._goaway(e.code, str(e))
+            self.transport.close()
+        except ValueError as e:  # HPACK: a COMPRESSION_ERROR ends the connection
+            self._goaway(COMPRESSION_ERROR, str(e))
+            self.transport.close()
+
+    def _parse(self) -> None:
+        buf = self.buf
+        if not self.preface_seen:
+            if len(buf) < len(PREFACE):
+                return
+            if bytes(buf[:len(PREFACE)]) != PREFACE:
+                raise ProtocolError(PROTOCOL_ERROR, "bad connection preface")
+            del buf[:len(PREFACE)]
+            self.preface_seen = True
+        while len(buf) >= 9:
+            n = (buf[0] << 16) | (buf[1] << 8) | buf[2]
+            if n > OUR_MAX_FRAME:
+                raise ProtocolError(FRAME_SIZE_ERROR, f"frame of {n} bytes")
+            if len(buf) < 9 + n:
+                return
+            ftype, flags = buf[3], buf[4]
+            sid = struct.unpack_from(">I", buf, 5)[0] & 0x7FFFFFFF
+            payload = bytes(buf[9:9 + n])
+            del buf[:9 + n]
+            if self.continuation is not None and (ftype != CONTINUATION or sid != self.continuation.id):
+                raise ProtocolError(PROTOCOL_ERROR, "expected CONTINUATION")
+            self._frame(ftype, flags, sid, payload)
+
+    def _frame(self, ftype: int, flags: int, sid: int, payload: bytes) -> None:
+        if ftype == SETTINGS:
+            if flags & ACK:
+                return
+            for k in range(0, len(payload) - len(payload) % 6, 6):
+                ident, value = struct.unpack_from(">HI", payload, k)
+                if ident == S_INITIAL_WINDOW_SIZE:
+                    delta = value - self.peer_initial_window
+                    self.peer_initial_window = value
+                    for s in self.streams.values():
+                        s.send_window += delta
+                elif ident == S_MAX_FRAME_SIZE:
+                    self.peer_max_frame = value
+            self.transport.write(frame(SETTINGS, ACK, 0))
+            self._flush_all()
+        elif ftype == HEADERS:
+            payload = self._strip(flags, payload, priority=True)
+            if sid % 2 == 0 or sid == 0:
+                raise ProtocolError(PROTOCOL_ERROR, f"HEADERS on stream {sid}")
+            s = self.streams.get(sid)
+            if s is None:  # a new stream (a second HEADERS block on an open stream is trailers)
+                if sid <= self.last_stream:
+                    raise ProtocolError(PROTOCOL_ERROR, f"stream {sid} reused")
+                self.last_stream = sid
+                s = _Stream(sid, self.peer_initial_window)
+                refused = self.goaway_sent or self.open_streams >= self.max_streams
+                self.streams[sid] = s
+                self.open_streams += 1
+                if refused:
+                    s.closed = True  # decode the block all the same: the HPACK state is the connection's
+                    self.server.h2_stats["refused"] += 1
+            s.block += payload
+            if flags & END_STREAM:
+                s.ended = True
+            if flags & END_HEADERS:
+                self._headers_done(s)
+            else:
+                self.continuation = s
+        elif ftype == CONTINUATION:
+            s = self.continuation
+            if s is None or s.id != sid:
+                raise ProtocolError(PROTOCOL_ERROR, "CONTINUATION without HEADERS")
+            s.block += payload
+            if flags & END_HEADERS:
+                self.continuation = None
+                self._headers_done(s)
+        elif ftype == DATA:
+            # flow control counts the whole payload, padding included; the connection window is topped up
+            # every 512 MiB, a stream's never (request bodies are far below OUR_WINDOW; an apiserver caps them
+            # at 3 MiB)
+            self.recv_unacked += len(payload)
+            if self.recv_unacked >= (1 << 29):
+                self.transport.write(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", self.recv_unacked)))
+                self.recv_unacked = 0
+            payload = self._strip(flags, payload)
+            s = self.streams.get(sid)
+            if s is None or s.ended:
+                self.transport.write(frame(RST_STREAM, 0, sid, struct.pack(">I", STREAM_CLOSED)))
+                return
+            s.body += payload
+            if flags & END_STREAM:
+                s.ended = True
+                self._dispatch(s)
+            elif self.our_window < OUR_WINDOW and payload:  # small-window mode: credit what was consumed
+                self.transport.write(frame(WINDOW_UPDATE, 0, sid, struct.pack(">I", len(payload))))
+        elif ftype == WINDOW_UPDATE:
+            inc = struct.unpack(">I", payload[:4])[0] & 0x7FFFFFFF
+            if sid == 0:
+                self.conn_send_window += inc
+                self._flush_all()
+            else:
+                s = self.streams.get(sid)
+                if s is not None:
+                    s.send_window += inc
+                    self._flush(s)
+        elif ftype == PING:
+            if not flags & ACK:
+                self.transport.write(frame(PING, ACK, 0, payload))
+        elif ftype == RST_STREAM:
+            s = self.streams.get(sid)
+            if s is not None:
+                self._close(s)
+        elif ftype == GOAWAY:
+            self.goaway_sent = True  # the client is leaving: nothing new
+        elif ftype == PUSH_PROMISE:
+            raise ProtocolError(PROTOCOL_ERROR, "PUSH_PROMISE from a client")
+        # PRIORITY and unknown frame types: ignored
+
+    @staticmethod
+    def _strip(flags: int, payload: bytes, priority: bool = False) -> bytes:
+        pad = 0
+        if flags & PADDED:
+            pad = payload[0]
+            payload = payload[1:]
+        if priority and flags & PRIORITY_FLAG:
+            payload = payload[5:]
+        if pad:
+            if pad > len(payload):
+                raise ProtocolError(PROTOCOL_ERROR, "padding longer than the frame")
+            payload = payload[:-pad]
+        return payload
+
+    def _headers_done(self, s: _Stream) -> None:
+        hs = self.decoder.decode(bytes(s.block))
+        s.block = bytearray()
+        if s.closed:  # refused (over the stream limit, or after GOAWAY)
+            self.transport.write(frame(RST_STREAM, 0, s.id, struct.pack(">I", REFUSED_STREAM)))
+            self.streams.pop(s.id, None)
+            self.open_streams -= 1
+            return
+        if not s.headers:
+            s.headers = hs
+        if s.ended:
+            self._dispatch(s)
+
+    # ------------------------------------------------------------------ requests
+    def _dispatch(self, s: _Stream) -> None:
+        from .httpserver import Deferred, Request, Response
+        pseudo, headers = {}, {}
+        for k, v in s.headers:
+            if k.startswith(":"):
+                pseudo[k] = v
+            elif k not in _HOP_BY_HOP:
+                headers[k] = v
+        if "host" not in headers and ":authority" in pseudo:
+            headers["host"] = pseudo[":authority"]
+        req = Request(pseudo.get(":method", "GET"), pseudo.get(":path", "/"), headers, bytes(s.body))
+        req._conn = self.conn  # type: ignore[attr-defined]
+        req._h2 = (self, s)    # type: ignore[attr-defined]
+        s.body = bytearray()
+        self.served += 1
+        self.server.h2_stats["streams"] += 1
+        st = self.server.h2_stats
+        st["max_open"] = max(st["max_open"], self.open_streams)
+        if self.goaway_after and self.served >= self.goaway_after and not self.goaway_sent:
+            self._goaway(NO_ERROR, "h2_goaway_after")
+        fast = self.server.fast
+        if fast is not None:
+            try:
+                resp = fast(req)
+            except Exception as e:  # noqa: BLE001
+                resp = Response(500, text=f"internal error: {e}")
+            if isinstance(resp, Deferred):
+                if resp.response is None:
+                    resp.then(lambda r, s=s: self.respond(s, r))
+                    return
+                resp = resp.response
+            if resp is not None:
+                self.respond(s, resp)
+                return
+        task = asyncio.ensure_future(self.server.handler(req))
+        task.add_done_callback(lambda t, s=s: self._done(s, t))
+
+    def _done(self, s: _Stream, task: asyncio.Task) -> None:
+        from .httpserver import Response
+        try:
+            resp = task.result()
+        except Exception as e:  # noqa: BLE001
+            resp = Response(500, text=f"internal error: {e}")
+        if isinstance(resp, Response):
+            self.respond(s, resp)
+        elif not s.closed and not s.eof_pending:  # a stream handler returned without ending its body
+            self.send_data(s, b"", end=True)
+
+    def respond(self, s: _Stream, resp) -> None:
+        if s.closed or self.conn.closed:
+            return
+        fields = [(":status", str(resp.status)), ("content-type", resp.content_type),
+                  ("content-length", str(len(resp.body)))]
+        fields += [(k.lower(), str(v)) for k, v in resp.headers.items()]
+        self.send_headers(s, fields, end=not resp.body)
+        if resp.body:
+            self.send_data(s, resp.body, end=True)
+
+    def send_headers(self, s: _Stream, fields: list, end: bool = False) -> None:
+        block = _native.load(required=True).hpack_encode(fields)
+        s.response_started = True
+        first, rest = block[:self.peer_max_frame], block[self.peer_max_frame:]
+        flags = (END_STREAM if end else 0) | (0 if rest else END_HEADERS)
+        out = [frame(HEADERS, flags, s.id, first)]
+        while rest:
+            chunk, rest = rest[:self.peer_max_frame], rest[self.peer_max_frame:]
+            out.append(frame(CONTINUATION, 0 if rest else END_HEADERS, s.id, chunk))
+        self.transport.write(b"".join(out))
+        if end:
+            self._close(s)
+
+    def send_data(self, s: _Stream, data: bytes, end: bool = False) -> None:
+        if s.closed:
+            return
+        s.pending += data
+        s.eof_pending = s.eof_pending or end
+        self._flush(s)
+
+    def _flush(self, s: _Stream) -> None:
+        out = []
+        while s.pending and not s.closed:
+            n = min(len(s.pending), s.send_window, self.conn_send_window, self.peer_max_frame)
+            if n <= 0:
+                break
+            chunk = bytes(s.pending[:n])
+            del s.pending[:n]
+            s.send_window -= n
+            self.conn_send_window -= n
+            last = not s.pending and s.eof_pending
+            out.append(frame(DATA, END_STREAM if last else 0, s.id, chunk))
+            if last:
+                s.eof_pending = False
+                self._close(s)
+        if not s.pending and s.eof_pending and not s.closed:  # an empty final frame
+            out.append(frame(DATA, END_STREAM, s.id))
+            s.eof_pending = False
+            self._close(s)
+        if out:
+            self.transport.write(b"".join(out))
+
+    def _flush_all(self) -> None:
+        for s in list(self.streams.values()):
+            if s.pending or s.eof_pending:
+                self._flush(s)
+
+    def _close(self, s: _Stream) -> None:
+        if not s.closed:
+            s.closed = True
+        if self.streams.pop(s.id, None) is not None:
+            self.open_streams -= 1
+
+    def _goaway(self, code: int, msg: str) -> None:
+        if self.goaway_sent and code == NO_ERROR:
+            return
+        self.goaway_sent = True
+        self.server.h2_stats["goaways"] += 1
+        self.transport.write(frame(GOAWAY, 0, 0, struct.pack(">II", self.last_stream, code) + msg.encode()[:64]))
+
+    def connection_lost(self) -> None:
+        for s in list(self.streams.values()):
+            self._close(s)
+
+
+class H2StreamWriter:
+    """`StreamResponse` over HTTP/2 (a watch): the head as HEADERS, each write a DATA frame, EOF as END_STREAM."""
+
+    def __init__(self, h2: H2Connection, s: _Stream):
+        self.h2, self.s = h2, s
+
+    def prepare(self, status: int, headers: dict) -> None:
+        fields = [(":status", str(status))] + [(k.lower(), str(v)) for k, v in headers.items()
+                                               if k.lower() not in _HOP_BY_HOP]
+        self.h2.send_headers(self.s, fields)
+
+    def write(self, data: bytes) -> None:
+        if self.s.closed:
+            raise ConnectionResetError("stream reset")
+        self.h2.send_data(self.s, data)
+
+    def write_eof(self) -> None:
+        self.h2.send_data(self.s, b"", end=True)

@@ -30,7 +30,7 @@ _QUERY_MEMO: dict = {}  # raw query → parsed (write requests repeat e.g. "fiel
 
 
 class Request:
-    __slots__ = ("method", "path", "raw_query", "headers", "body", "_query", "_conn")
+    __slots__ = ("method", "path", "raw_query", "headers", "body", "_query", "_conn", "_h2")
 
     def __init__(self, method: str, target: str, headers: dict, body: bytes):
         self.method = method
@@ -40,6 +40,7 @@ class Request:
         self.headers = headers
         self.body = body
         self._query = None
+        self._h2 = None  # (H2Connection, stream) when it came over HTTP/2 (ncc/fakeapi/h2.py)
 
     @property
     def query(self) -> dict:
@@ -121,11 +122,18 @@ class StreamResponse:
         self.status = status
         self.headers = {k: v for k, v in (headers or {}).items() if k.lower() != "transfer-encoding"}
         self._conn: "_ServerConn | None" = None
+        self._h2w = None
         self.prepared = False
 
     async def prepare(self, request: Request) -> None:
         conn = request._conn  # type: ignore[attr-defined]
         self._conn = conn
+        if request._h2 is not None:  # HTTP/2: HEADERS now, DATA frames per write, END_STREAM at EOF
+            from .h2 import H2StreamWriter
+            self._h2w = H2StreamWriter(*request._h2)
+            self._h2w.prepare(self.status, self.headers)
+            self.prepared = True
+            return
         h = [f"HTTP/1.1 {self.status} {_REASONS.get(self.status, 'Status')}", "Transfer-Encoding: chunked"]
         for k, v in self.headers.items():
             h.append(f"{k}: {v}")
@@ -136,14 +144,20 @@ class StreamResponse:
         c = self._conn
         if c is None or c.closed:
             raise ConnectionResetError("client went away")
-        if data:
+        if self._h2w is not None:
+            if data:
+                self._h2w.write(data)
+        elif data:
             c.transport.write(b"%x\r\n%s\r\n" % (len(data), data))
         await c.drain()
 
     async def write_eof(self) -> None:
         c = self._conn
         if c is not None and not c.closed:
-            c.transport.write(b"0\r\n\r\n")
+            if self._h2w is not None:
+                self._h2w.write_eof()
+            else:
+                c.transport.write(b"0\r\n\r\n")
 
 
 class _ServerConn(asyncio.Protocol):
@@ -155,12 +169,25 @@ class _ServerConn(asyncio.Protocol):
         self.busy = False
         self.api = False  # served a request other than a watch (connection statistics)
         self._drain: asyncio.Future | None = None
+        self.h2 = None  # ncc/fakeapi/h2.py H2Connection once the connection speaks HTTP/2
+        self.fresh = True  # nothing received yet (an HTTP/2 preface can only come first)
 
     def connection_made(self, transport):
         self.transport = transport
         srv = self.server
         srv._conns.add(self)
         srv.accepted += 1
+        ssl_obj = transport.get_extra_info("ssl_object")
+        if srv.http2 and ssl_obj is not None and ssl_obj.selected_alpn_protocol() == "h2":
+            self._start_h2()
+
+    def _start_h2(self):
+        from .h2 import H2Connection
+        self.h2 = H2Connection(self, self.server)
+        self.api = True
+        srv = self.server
+        srv.api_conns += 1
+        srv.max_api_conns = max(srv.max_api_conns, srv.api_conns)
 
     def connection_lost(self, exc):
         self.closed = True
@@ -168,6 +195,8 @@ class _ServerConn(asyncio.Protocol):
         srv._conns.discard(self)
         if self.api:
             srv.api_conns -= 1
+        if self.h2 is not None:
+            self.h2.connection_lost()
         if self._drain is not None and not self._drain.done():
             self._drain.set_result(None)
 
@@ -184,6 +213,15 @@ class _ServerConn(asyncio.Protocol):
             await self._drain
 
     def data_received(self, data: bytes):
+        if self.h2 is not None:
+            self.h2.data_received(data)
+            return
+        if self.fresh:
+            self.fresh = False
+            if self.server.http2 and data[:4] == b"PRI ":  # HTTP/2 with prior knowledge (cleartext)
+                self._start_h2()
+                self.h2.data_received(data)
+                return
         self.buf += data
         if not self.busy:
             self._next()
@@ -291,10 +329,13 @@ class HttpServer:
         self.port: int | None = None
         self.accepted = 0  # connections accepted so far
         self.api_conns = self.max_api_conns = 0  # open connections that served a non-watch request; the most at once
+        self.http2 = False  # accept HTTP/2: ALPN "h2" on TLS (the context must offer it), prior knowledge on TCP
+        self.h2_options: dict = {}  # h2_max_streams, h2_goaway_after (ncc/fakeapi/h2.py)
+        self.h2_stats = {"connections": 0, "streams": 0, "max_open": 0, "refused": 0, "goaways": 0}
 
     def conn_stats(self) -> dict:
         return {"open": len(self._conns), "accepted": self.accepted, "api_open": self.api_conns,
-                "api_max": self.max_api_conns}
+                "api_max": self.max_api_conns, "h2": dict(self.h2_stats)}
 
     async def start(self, host: str, port: int, ssl_context=None) -> int:
         loop = asyncio.get_running_loop()

@@ -82,6 +82,7 @@ class Faults:
         self.apf_queue_wait_s = 15.0
         self.service_ms = 0.0
         self.read_service_ms = 0.0
+        self.h2: dict = {}  # HTTP/2 connections opened from now on: h2_max_streams, h2_goaway_after (h2.py)
 
     def match(self, method: str, plural: str, name: str | None) -> tuple | None:
         """(error, after) of the targeted rule this request matches, or None.  `after`: the request is
@@ -118,6 +119,9 @@ class Faults:
             self.down = bool(d["down"])
         if "write_only" in d:
             self.write_only = bool(d["write_only"])
+        for k in ("h2_max_streams", "h2_goaway_after", "h2_initial_window"):
+            if k in d:
+                self.h2[k] = int(d[k])
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)
@@ -125,7 +129,7 @@ class Faults:
 
 class FakeApiServer:
     def __init__(self, state: ClusterState | None = None, *, name: str = "fake", token: str | None = None,
-                 bookmark_interval: float = 5.0, crd_dir: str | None = None):
+                 bookmark_interval: float = 5.0, crd_dir: str | None = None, http2: bool = True):
         self.state = state or ClusterState(name)
         if crd_dir:  # validate custom-resource writes against these CRDs' schemas (422 Invalid)
             from ..api.schema import load_crds
@@ -145,11 +149,16 @@ class FakeApiServer:
         self.record_writes = False  # in-process test servers turn it on (FakeEnvironment)
         self._streams: set = set()
         self._http = web.HttpServer(self._dispatch, fast=self.fast)
+        # HTTP/2 as a kube-apiserver serves it: ALPN "h2" on TLS, and prior knowledge on cleartext (ncc/fakeapi/h2.py)
+        self._http.http2 = http2
+        self._http.h2_options = self.faults.h2
         self.port: int | None = None
         self.url: str | None = None
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context: ssl.SSLContext | None = None) -> str:
+        if ssl_context is not None and self._http.http2:
+            ssl_context.set_alpn_protocols(["h2", "http/1.1"])
         self.port = await self._http.start(host, port, ssl_context)
         self.url = f"{'https' if ssl_context else 'http'}://{host}:{self.port}"
         return self.url
@@ -595,7 +604,7 @@ class FakeApiServer:
 async def serve(args) -> None:
     logging.basicConfig(level=logging.WARNING)
     server = FakeApiServer(name=args.name, token=args.token, bookmark_interval=args.bookmark_interval,
-                           crd_dir=args.crd_dir)
+                           crd_dir=args.crd_dir, http2=not getattr(args, "no_http2", False))
     for m in args.marker:
         plural, _, path = m.partition("=")
         server.markers.add_spec(plural, path)
@@ -669,6 +678,8 @@ def main(argv=None) -> None:
     p.add_argument("--admission-set", action="append", default=[], metavar="PLURAL=PATH=JSON",
                    help="mutating-webhook stand-in: write this field into every create/update (repeatable)")
     p.add_argument("--bookmark-interval", type=float, default=5.0)
+    p.add_argument("--no-http2", action="store_true",
+                   help="HTTP/1.1 only: no ALPN h2 on TLS, no prior-knowledge HTTP/2 on cleartext")
     p.add_argument("--parent-pid", type=int, default=0, help="exit when this process disappears")
     p.add_argument("--marker", action="append", default=[], help="plural=field.path propagation probe (repeatable)")
     args = p.parse_args(argv)

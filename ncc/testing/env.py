@@ -54,12 +54,15 @@ def wait_port_file(path: str, proc: subprocess.Popen | None = None, timeout: flo
 class FakeEnvironment:
     def __init__(self, n_shards: int, workdir: str, *, namespace: str = "nexus", token: str | None = None,
                  subprocesses: bool = False, shard_prefix: str = "shard", bookmark_interval: float = 5.0,
-                 tls: bool = False, tls_server_name: str | None = None, crd_dir: str | None = "default"):
+                 tls: bool = False, tls_server_name: str | None = None, crd_dir: str | None = "default",
+                 http2: bool = True):
         """`tls=True` serves every apiserver over HTTPS with mutual TLS (a throwaway CA, x509 client auth,
         like a kind cluster); `tls_server_name` additionally puts `tls-server-name` in the kubeconfigs.
         `crd_dir` ("default": the repository's deploy/crds) makes the apiservers validate custom-resource
-        writes against the shipped CRD schemas, as a real apiserver does; None disables it."""
+        writes against the shipped CRD schemas, as a real apiserver does; None disables it.  `http2=False`:
+        apiservers that speak HTTP/1.1 only (no ALPN h2, no prior-knowledge HTTP/2)."""
         self.n_shards = n_shards
+        self.http2 = http2
         self.workdir = workdir
         self.namespace = namespace
         self.token = token
@@ -92,9 +95,9 @@ class FakeEnvironment:
             files = []
             for n in names:
                 pf = os.path.join(self.workdir, f"{n}.url")
+                extra = (["--crd-dir", self.crd_dir] if self.crd_dir else []) + ([] if self.http2 else ["--no-http2"])
                 self.procs.append(spawn_fakeapi(n, pf, token=self.token, bookmark_interval=self.bookmark_interval,
-                                                pki=self.pki,
-                                                extra=["--crd-dir", self.crd_dir] if self.crd_dir else None))
+                                                pki=self.pki, extra=extra or None))
                 files.append(pf)
             urls = [await asyncio.get_running_loop().run_in_executor(None, wait_port_file, f, p)
                     for f, p in zip(files, self.procs)]
@@ -102,7 +105,7 @@ class FakeEnvironment:
             urls = []
             for n in names:
                 s = FakeApiServer(name=n, token=self.token, bookmark_interval=self.bookmark_interval,
-                                  crd_dir=self.crd_dir)
+                                  crd_dir=self.crd_dir, http2=self.http2)
                 s.record_writes = True
                 urls.append(await s.start(ssl_context=self.pki.server_context() if self.pki else None))
                 if n == "controller":

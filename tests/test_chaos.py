@@ -114,17 +114,20 @@ def _converged(cl, active=None, meta_sync: bool = False) -> str:
 
 
 @pytest.mark.parametrize("topology", ["inprocess", "python", "native", "native-c2", "native-reload", "native-ssa",
-                                      "native-meta"])
+                                      "native-meta", "native-h2"])
 @pytest.mark.parametrize("seed", list(range(1, SEEDS + 1)))
 async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatch):
     """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
     the kills then also hit the child coordinator.  `native-ssa`: shard writes by server-side apply.
-    `native-meta`: sync-dependent-metadata, with source labels/annotations changed along the way."""
+    `native-meta`: sync-dependent-metadata, with source labels/annotations changed along the way.
+    `native-h2`: the C++ executors write to the shards over HTTP/2 (`client-http2: on`, prior knowledge)."""
     from ncc.controller.native_executor import binary_path
     reload = topology.endswith("-reload")
     ssa = topology.endswith("-ssa")
     meta_sync = topology.endswith("-meta")
-    impl, _, parts = topology.replace("-reload", "").replace("-ssa", "").replace("-meta", "").partition("-c")
+    h2 = topology.endswith("-h2")
+    impl, _, parts = topology.replace("-reload", "").replace("-ssa", "").replace("-meta", "").replace(
+        "-h2", "").partition("-c")
     if impl == "native" and binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
@@ -136,6 +139,8 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         extra["server_side_apply"] = True
     if meta_sync:
         extra["sync_dependent_metadata"] = True
+    if h2:
+        extra["client_http2"] = "on"
     if os.environ.get("NCC_CHAOS_LOG"):
         extra["log_level"] = os.environ["NCC_CHAOS_LOG"]
     async with Cluster(tmp_path, impl, n_shards=3 if reload else 2, **extra) as cl:

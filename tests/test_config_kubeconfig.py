@@ -197,7 +197,7 @@ def test_helm_env_names_map_to_config_keys():
     from pathlib import Path
     tpl = (Path(__file__).parent.parent / "deploy/helm/nexus-configuration-controller/templates/deployment.yaml"
            ).read_text()
-    names = set(re.findall(r"name: (NEXUS__[A-Z_]+)", tpl))
+    names = set(re.findall(r"name: (NEXUS__[A-Z0-9_]+)", tpl))
     known = {AppConfig.env_of(f.name) for f in fields(AppConfig)}
     assert names and names <= known, names - known
     assert {"NEXUS__LEADER_ELECT", "NEXUS__SERVER_SIDE_APPLY", "NEXUS__WORKERS"} <= names

@@ -78,6 +78,7 @@ def test_env_contract_with_the_config_loader():
     assert cfg.leader_elect is True and cfg.mode == "native" and cfg.health_bind_address == ":8081"
     assert cfg.lease_duration == 15.0 and cfg.renew_deadline == 10.0 and cfg.retry_period == 2.0
     assert cfg.failure_rate_base_delay == 0.03 and cfg.failure_rate_max_delay == 5.0
+    assert cfg.client_http2 == "auto"
 
 
 def test_cpu_affinity_knob():

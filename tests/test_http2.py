@@ -1,0 +1,304 @@
+"""HTTP/2 between the C++ shard executor (native/executor/h2.hpp) and the fake apiserver (ncc/fakeapi/h2.py).
+
+client-go speaks HTTP/2 to kube-apiservers — negotiated by ALPN on TLS — and multiplexes a clientset's requests
+on one connection (`/root/reference/main.go:52-68`).  `client-http2` gives the C++ executor the same: `auto`
+(the default) where TLS negotiates it, `on` also with prior knowledge on cleartext.
+
+* HPACK (native/common/hpack.hpp) against RFC 7541 Appendix C — the request examples without and with Huffman
+  coding (C.3, C.4) and the response examples with eviction from a 256-byte table (C.5) — and round trips.
+* The executor over HTTP/2 against the same scenarios as HTTP/1.1: cold sync, updates, few connections carrying
+  many streams; TLS with ALPN; GOAWAY mid-run (streams past the last one re-sent on a new connection); a
+  MAX_CONCURRENT_STREAMS of 4 (more connections, never more streams than allowed); a 64-byte stream window
+  (request bodies wait for WINDOW_UPDATE); a header block larger than a frame (CONTINUATION).
+"""
+import asyncio
+import os
+import random
+
+import pytest
+
+from ncc import native
+from ncc.api import resources as R
+from ncc.testing.workload import make_configmap, make_secret, make_template
+
+from test_conformance import NS, Cluster, mutate, wait_for
+
+_m = native.load(required=True)
+
+
+# ---------------------------------------------------------------------------------------------- HPACK
+C3 = ["828684410f7777772e6578616d706c652e636f6d",
+      "828684be58086e6f2d6361636865",
+      "828785bf400a637573746f6d2d6b65790c637573746f6d2d76616c7565"]
+C4 = ["828684418cf1e3c2e5f23a6ba0ab90f4ff",
+      "828684be5886a8eb10649cbf",
+      "828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf"]
+C3_FIELDS = [
+    [(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com")],
+    [(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com"),
+     ("cache-control", "no-cache")],
+    [(":method", "GET"), (":scheme", "https"), (":path", "/index.html"), (":authority", "www.example.com"),
+     ("custom-key", "custom-value")]]
+C5 = ["4803333032580770726976617465611d4d6f6e2c203231204f637420323031332032303a31333a323120474d546e1768747470733a2f2f"
+      "7777772e6578616d706c652e636f6d",
+      "4803333037c1c0bf",
+      "88c1611d4d6f6e2c203231204f637420323031332032303a31333a323220474d54c05a04677a69707738666f6f3d4153444a4b48514b"
+      "425a584f5157454f50495541585157454f49553b206d61782d6167653d333630303b2076657273696f6e3d31"]
+
+
+@pytest.mark.parametrize("blocks", [C3, C4], ids=["C.3-plain", "C.4-huffman"])
+def test_hpack_rfc7541_request_examples(blocks):
+    d = _m.HpackDecoder(4096)
+    sizes = []
+    for blk, want in zip(blocks, C3_FIELDS):
+        assert d.decode(bytes.fromhex(blk)) == want
+        sizes.append(d.table_size())
+    assert sizes == [57, 110, 164]  # the dynamic table sizes the RFC lists after each request
+
+
+def test_hpack_rfc7541_response_examples_with_eviction():
+    d = _m.HpackDecoder(256)
+    got = [d.decode(bytes.fromhex(b)) for b in C5[:1]]
+    assert got[0] == [(":status", "302"), ("cache-control", "private"), ("date", "Mon, 21 Oct 2013 20:13:21 GMT"),
+                      ("location", "https://www.example.com")]
+    assert d.table_size() == 222
+    assert d.decode(bytes.fromhex(C5[1]))[0] == (":status", "307")
+    assert d.table_size() == 222 and d.table_entries() == 4  # ":status: 302" evicted for ":status: 307"
+    third = d.decode(bytes.fromhex(C5[2]))
+    assert third[-1] == ("set-cookie", "foo=ASDJKHQKBZXOQWEOPIUAXQWEOIU; max-age=3600; version=1")
+    assert d.table_size() == 215 and d.table_entries() == 3
+
+
+def test_hpack_huffman_rfc_strings_and_round_trip():
+    for s, h in ((b"www.example.com", "f1e3c2e5f23a6ba0ab90f4ff"), (b"no-cache", "a8eb10649cbf"),
+                 (b"custom-key", "25a849e95ba97d7f"), (b"custom-value", "25a849e95bb8e8b4bf")):
+        assert _m.hpack_huffman_encode(s).hex() == h
+        assert _m.hpack_huffman_decode(bytes.fromhex(h)) == s
+    rnd = random.Random(7)
+    for _ in range(300):
+        s = bytes(rnd.randrange(256) for _ in range(rnd.randrange(0, 64)))
+        assert _m.hpack_huffman_decode(_m.hpack_huffman_encode(s)) == s
+    with pytest.raises(ValueError):
+        _m.hpack_huffman_decode(b"\xff\xff\xff\xff")  # EOS inside a string
+
+
+def test_hpack_encoder_round_trip_and_malformed_blocks():
+    rnd = random.Random(3)
+    d = _m.HpackDecoder()
+    for _ in range(100):
+        fields = [(":status", str(rnd.choice([200, 201, 404, 409, 429, 503]))), ("content-type", "application/json")]
+        fields += [(f"x-{rnd.randrange(1000)}", "v" * rnd.randrange(0, 300)) for _ in range(rnd.randrange(4))]
+        for huff in (False, True):
+            assert d.decode(_m.hpack_encode(fields, huff)) == fields
+    assert d.table_size() == 0  # literals without indexing never touch the table
+    for bad in (b"\x80", b"\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\x7f", b"\x40\x05ab", b"\xbe"):
+        with pytest.raises(ValueError):
+            d.decode(bad)
+    fresh = _m.HpackDecoder()
+    with pytest.raises(ValueError):  # a table size update after a field
+        fresh.decode(bytes.fromhex("82") + b"\x20")
+    with pytest.raises(ValueError):  # above the limit we advertised
+        fresh.decode(b"\x3f\xe2\x1f")  # 4097
+
+
+# ---------------------------------------------------------------------------------------------- the executor
+@pytest.fixture
+def native_only():
+    from ncc.controller.native_executor import binary_path
+    if binary_path() is None:
+        pytest.skip("ncc/bin/ncc-executor is not built")
+
+
+def _flow(cl) -> dict:
+    ex = cl.app.debug_state().get("executors") or {}
+    out = {}
+    for h in ex.values():
+        out.update((h.get("status") or {}).get("flow") or {})
+    return out
+
+
+async def _converge(cl, n: int, tag: str = ""):
+    async def ok():
+        for s in cl.sstates:
+            for i in range(n):
+                t = s.try_get(R.TEMPLATES, NS, f"algo-{i:05d}")
+                if t is None or (tag and t["spec"]["container"]["versionTag"] != tag):
+                    return False
+                if s.try_get(R.CONFIGMAPS, NS, f"c{i}") is None or s.try_get(R.SECRETS, NS, f"s{i}") is None:
+                    return False
+        return True
+    await wait_for(ok, timeout=30, interval=0.05)
+    for i in range(n):
+        await cl.ready(f"algo-{i:05d}")
+
+
+async def _h2_status(cl):
+    async def ok():
+        fl = _flow(cl)
+        return bool(fl) and all(f.get("http2") == 1 and f.get("h2_streams", 0) > 0 for f in fl.values()) and fl
+    return await wait_for(ok, timeout=10, interval=0.1)
+
+
+async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, monkeypatch):
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, "native", n_shards=2, client_http2="on", executors_per_shard=1) as cl:
+        n = 30
+        for i in range(n):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        await _converge(cl, n)
+        for i in range(n):
+            await mutate(cl.cc, R.TEMPLATES, f"algo-{i:05d}",
+                         lambda o: o["spec"]["container"].__setitem__("versionTag", "h2v"))
+        await _converge(cl, n, "h2v")
+        fl = await _h2_status(cl)
+        for i, srv in enumerate(cl.env.shard_servers):
+            st = srv._http.conn_stats()
+            # every write and list of the executor went over a few HTTP/2 connections
+            assert st["h2"]["connections"] >= 1 and st["h2"]["streams"] >= 2 * n, st
+            assert st["h2"]["connections"] <= 2, st
+            assert fl[f"shard-{i}"]["connections"] <= 2, fl
+        assert all(f["rejected_429"] == 0 for f in fl.values())
+
+
+async def test_executor_negotiates_http2_by_alpn_on_tls(tmp_path, native_only, monkeypatch):
+    """`client-http2: auto` (the default): on TLS the executor offers "h2" and the server selects it."""
+    from ncc.app import App
+    from ncc.testing.env import FakeEnvironment
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    env = await FakeEnvironment(1, str(tmp_path), tls=True).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    app, stop, task = None, asyncio.Event(), None
+    try:
+        for i in range(5):
+            await cc.create(R.SECRETS, NS, make_secret(f"s{i}", NS))
+            await cc.create(R.CONFIGMAPS, NS, make_configmap(f"c{i}", NS))
+            await cc.create(R.TEMPLATES, NS, make_template(i, NS, secrets=[f"s{i}"], configmaps=[f"c{i}"]))
+        app = App(env.app_config(mode="native", executor_impl="native", failure_rate_max_delay=0.2))
+        await app.build()
+        task = asyncio.ensure_future(app.run(stop))
+
+        async def ready():
+            for i in range(5):
+                t = await cc.get(R.TEMPLATES, NS, f"algo-{i:05d}")
+                c = (t.get("status") or {}).get("conditions") or [{}]
+                if c[0].get("status") != "True":
+                    return False
+            return True
+        await wait_for(ready, timeout=30, interval=0.05)
+        st = env.shard_servers[0]._http.conn_stats()
+        assert st["h2"]["connections"] >= 1 and st["h2"]["streams"] >= 15, st
+        assert (await sc.get(R.SECRETS, NS, "s4"))["metadata"]["ownerReferences"]
+    finally:
+        stop.set()
+        if task is not None:
+            await task
+        await cc.close()
+        await sc.close()
+        await env.stop()
+
+
+async def test_goaway_mid_run_moves_streams_to_a_new_connection(tmp_path, native_only, monkeypatch):
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, "native", n_shards=1, client_http2="on", executors_per_shard=1) as cl:
+        cl.env.shard_servers[0].faults.update({"h2_goaway_after": 7})
+        n = 20
+        for i in range(n):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        await _converge(cl, n)
+        st = cl.env.shard_servers[0]._http.conn_stats()["h2"]
+        assert st["goaways"] >= 3 and st["connections"] >= 4, st  # ≥ 3·n writes, 7 streams per connection
+        await _h2_status(cl)
+
+        async def saw_goaway():  # (the status messages come every 0.2 s)
+            fl = _flow(cl)
+            return fl.get("shard-0", {}).get("h2_goaways", 0) >= 1
+        await wait_for(saw_goaway, timeout=5, interval=0.1)
+
+
+async def test_stream_limit_is_obeyed_and_small_windows_hold_bodies(tmp_path, native_only, monkeypatch):
+    """MAX_CONCURRENT_STREAMS 4: the executor never has more streams open on a connection (the server refuses
+    any extra with REFUSED_STREAM — none come) and opens more connections; a 64-byte stream window makes every
+    request body wait for the server's WINDOW_UPDATEs."""
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, "native", n_shards=1, client_http2="on", executors_per_shard=1,
+                       client_pool_size=8) as cl:
+        cl.env.shard_servers[0].faults.update({"h2_max_streams": 4, "h2_initial_window": 64})
+        n = 25
+        for i in range(n):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        await _converge(cl, n)
+        st = cl.env.shard_servers[0]._http.conn_stats()["h2"]
+        assert st["max_open"] <= 4 and st["refused"] == 0, st
+        assert 1 <= st["connections"] <= 8, st
+        fl = await _h2_status(cl)
+        assert fl["shard-0"]["h2_refused"] == 0, fl
+
+
+async def test_large_header_block_goes_out_in_continuation_frames(tmp_path, native_only, monkeypatch):
+    """A 40 kB bearer token (an OIDC token with many groups can be that large) makes the header block longer
+    than a 16 kB frame: HEADERS + CONTINUATION."""
+    from ncc.app import App
+    from ncc.testing.env import FakeEnvironment
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    token = "t" * 40000
+    env = await FakeEnvironment(1, str(tmp_path), token=token).start()
+    cc = env.controller_client()
+    stop, task = asyncio.Event(), None
+    try:
+        await cc.create(R.SECRETS, NS, make_secret("s0", NS))
+        await cc.create(R.CONFIGMAPS, NS, make_configmap("c0", NS))
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=["c0"]))
+        app = App(env.app_config(mode="native", executor_impl="native", client_http2="on",
+                                 failure_rate_max_delay=0.2))
+        await app.build()
+        task = asyncio.ensure_future(app.run(stop))
+
+        async def synced():
+            return env.shard_servers[0].state.try_get(R.CONFIGMAPS, NS, "c0") is not None
+        await wait_for(synced, timeout=30, interval=0.05)
+        st = env.shard_servers[0]._http.conn_stats()["h2"]
+        assert st["streams"] >= 3, st
+    finally:
+        stop.set()
+        if task is not None:
+            await task
+        await cc.close()
+        await env.stop()
+
+
+async def test_http2_off_and_a_server_without_h2_fall_back_to_http11(tmp_path, native_only, monkeypatch):
+    """`client-http2: off` never speaks it; `auto` on TLS against a server that does not offer h2 in ALPN
+    carries on over HTTP/1.1."""
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, "native", n_shards=1, client_http2="off", executors_per_shard=1) as cl:
+        cl.seed(0)
+        await cl.start()
+        await cl.ready()
+        assert cl.env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
+    from ncc.app import App
+    from ncc.testing.env import FakeEnvironment
+    os.makedirs(tmp_path / "tls", exist_ok=True)
+    env = await FakeEnvironment(1, str(tmp_path / "tls"), tls=True, http2=False).start()
+    cc = env.controller_client()
+    stop, task = asyncio.Event(), None
+    try:
+        await cc.create(R.SECRETS, NS, make_secret("s0", NS))
+        await cc.create(R.CONFIGMAPS, NS, make_configmap("c0", NS))
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=["c0"]))
+        app = App(env.app_config(mode="native", executor_impl="native", failure_rate_max_delay=0.2))
+        await app.build()
+        task = asyncio.ensure_future(app.run(stop))
+
+        async def synced():
+            return env.shard_servers[0].state.try_get(R.CONFIGMAPS, NS, "c0") is not None
+        await wait_for(synced, timeout=30, interval=0.05)
+        assert env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
+    finally:
+        stop.set()
+        if task is not None:
+            await task
+        await cc.close()
+        await env.stop()
