@@ -19,6 +19,8 @@
 #                                                        N=1 and 8 shards on one rank (reference-compat baseline)
 #   bash scripts/box/run.sh <out> aimd [n]               AIMD vs NCC_AIMD=0 (fixed 256) in alternation, n pairs,
 #                                                        shard RTT 5/20 ms × jitter 0/10/20 ms, N=1 and 8 shards
+#   bash scripts/box/run.sh <out> http2 [n]              n rounds of: the driver shape over HTTP/1.1 and over HTTP/2
+#                                                        (prior knowledge), then --tls over HTTP/1.1 and HTTP/2 (ALPN)
 #   bash scripts/box/run.sh <out> multishard [n]         n rounds of: suite configs 2, 5, 8 with --stages, then
 #                                                        bench.py N=1 and --shards-per-rank 8 --stages
 #
@@ -45,6 +47,8 @@ print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99",
       "cold_s", d.get("cold_start_s"),
       "limit", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("limit"),
       "held", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("increases_held"),
+      "h2", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("http2"),
+      "conns", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("connections"),
       flush=True)
 EOF
 }
@@ -159,6 +163,15 @@ case "$what" in
           done
         done
       done
+    done
+    ;;
+  http2)
+    n=${1:-1}
+    for i in $(seq 1 "$n"); do
+      bench_once "$out/h1_$i" NEXUS__CLIENT_HTTP2=off || exit $?
+      bench_once "$out/h2_$i" NEXUS__CLIENT_HTTP2=on || exit $?
+      bench_once "$out/tls_h1_$i" NEXUS__CLIENT_HTTP2=off --tls || exit $?
+      bench_once "$out/tls_h2_$i" --tls || exit $?
     done
     ;;
   multishard)
