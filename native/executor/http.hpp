@@ -626,7 +626,9 @@ inline Task<std::string> read_body(Conn& c, const Head& h) {
 // (max-in-flight, API Priority and Fairness seats with bounded queues) and answers the rest 429 +
 // Retry-After; it also serves kubelets, the scheduler and the GPU operator.  Instead of a fixed number of
 // requests in flight, the client keeps an adaptive limit (AIMD, as TCP's congestion window):
-//   * slow start from `initial`: +1 per success (doubling per round trip) until the first overload signal,
+//   * slow start from `initial` (default: half the cap — one round trip to the cap; from 32 the three doublings
+//     cost a remote shard's cold start 5-8 % against a fixed limit, profiles/r5/r5c): +1 per success
+//     (doubling per round trip) until the first overload signal,
 //     or until responses come back slower than 2× the fastest of their kind plus 2 ms (HyStart: the server
 //     has started to queue them — leave before the queue overflows into 429s, each of which costs a
 //     Retry-After);
@@ -649,7 +651,7 @@ inline Task<std::string> read_body(Conn& c, const Head& h) {
 // burst 10; native mode has none unless configured).
 struct FlowLimits {
     int cap = 256;     // the most requests in flight: connections × pipeline depth
-    double initial = 32;
+    double initial = 0;  // 0: half the cap
     double beta = 0.7;
     double latency_s = 1.0;
     bool adaptive = true;
@@ -676,6 +678,7 @@ public:
         : creds_(std::move(creds)), max_(std::max(1, pool_size)), depth_(std::max(1, depth)),
           timeout_(request_timeout), fl_(fl) {
         fl_.cap = max_ * depth_;
+        if (fl_.initial <= 0) fl_.initial = std::max(1.0, fl_.cap / 2.0);
         limit_ = fl_.adaptive ? std::clamp(fl_.initial, 1.0, static_cast<double>(fl_.cap)) : fl_.cap;
         slow_start_ = fl_.adaptive && limit_ < fl_.cap;
         tokens_[0] = tokens_[1] = std::max(fl_.burst, 1.0);

@@ -100,11 +100,29 @@ class H2Connection:
         st = server.h2_stats
         st["connections"] += 1
         self.open_streams = 0
+        # frames produced in one loop iteration (every response a batch of requests gets) leave in one write
+        self._wbuf: list = []
+        self._flush_scheduled = False
         # our SETTINGS, and the connection window raised to 1 GiB
-        self.transport.write(frame(SETTINGS, 0, 0, struct.pack(
+        self._out(frame(SETTINGS, 0, 0, struct.pack(
             ">HIHIHIHI", S_MAX_CONCURRENT_STREAMS, self.max_streams, S_INITIAL_WINDOW_SIZE, self.our_window,
             S_MAX_FRAME_SIZE, OUR_MAX_FRAME, S_ENABLE_PUSH, 0)) +
             frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", (1 << 30) - 65535)))
+
+    def _out(self, data: bytes) -> None:
+        self._wbuf.append(data)
+        if not self._flush_scheduled:
+            self._flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._flush_out)
+
+    def _flush_out(self) -> None:
+        self._flush_scheduled = False
+        if self._wbuf and not self.conn.closed:
+            data = b"".join(self._wbuf) if len(self._wbuf) > 1 else self._wbuf[0]
+            self._wbuf.clear()
+            self.transport.write(data)
+        else:
+            self._wbuf.clear()
 
     # ------------------------------------------------------------------ input
     def data_received(self, data: bytes) -> None:
@@ -113,9 +131,11 @@ class H2Connection:
             self._parse()
         except ProtocolError as e:
             self._goaway(e.code, str(e))
+            self._flush_out()
             self.transport.close()
         except ValueError as e:  # HPACK: a COMPRESSION_ERROR ends the connection
             self._goaway(COMPRESSION_ERROR, str(e))
+            self._flush_out()
             self.transport.close()
 
     def _parse(self) -> None:
@@ -154,7 +174,7 @@ class H2Connection:
                         s.send_window += delta
                 elif ident == S_MAX_FRAME_SIZE:
                     self.peer_max_frame = value
-            self.transport.write(frame(SETTINGS, ACK, 0))
+            self._out(frame(SETTINGS, ACK, 0))
             self._flush_all()
         elif ftype == HEADERS:
             payload = self._strip(flags, payload, priority=True)
@@ -193,19 +213,19 @@ class H2Connection:
             # at 3 MiB)
             self.recv_unacked += len(payload)
             if self.recv_unacked >= (1 << 29):
-                self.transport.write(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", self.recv_unacked)))
+                self._out(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", self.recv_unacked)))
                 self.recv_unacked = 0
             payload = self._strip(flags, payload)
             s = self.streams.get(sid)
             if s is None or s.ended:
-                self.transport.write(frame(RST_STREAM, 0, sid, struct.pack(">I", STREAM_CLOSED)))
+                self._out(frame(RST_STREAM, 0, sid, struct.pack(">I", STREAM_CLOSED)))
                 return
             s.body += payload
             if flags & END_STREAM:
                 s.ended = True
                 self._dispatch(s)
             elif self.our_window < OUR_WINDOW and payload:  # small-window mode: credit what was consumed
-                self.transport.write(frame(WINDOW_UPDATE, 0, sid, struct.pack(">I", len(payload))))
+                self._out(frame(WINDOW_UPDATE, 0, sid, struct.pack(">I", len(payload))))
         elif ftype == WINDOW_UPDATE:
             inc = struct.unpack(">I", payload[:4])[0] & 0x7FFFFFFF
             if sid == 0:
@@ -218,7 +238,7 @@ class H2Connection:
                     self._flush(s)
         elif ftype == PING:
             if not flags & ACK:
-                self.transport.write(frame(PING, ACK, 0, payload))
+                self._out(frame(PING, ACK, 0, payload))
         elif ftype == RST_STREAM:
             s = self.streams.get(sid)
             if s is not None:
@@ -247,7 +267,7 @@ class H2Connection:
         hs = self.decoder.decode(bytes(s.block))
         s.block = bytearray()
         if s.closed:  # refused (over the stream limit, or after GOAWAY)
-            self.transport.write(frame(RST_STREAM, 0, s.id, struct.pack(">I", REFUSED_STREAM)))
+            self._out(frame(RST_STREAM, 0, s.id, struct.pack(">I", REFUSED_STREAM)))
             self.streams.pop(s.id, None)
             self.open_streams -= 1
             return
@@ -324,7 +344,7 @@ class H2Connection:
         while rest:
             chunk, rest = rest[:self.peer_max_frame], rest[self.peer_max_frame:]
             out.append(frame(CONTINUATION, 0 if rest else END_HEADERS, s.id, chunk))
-        self.transport.write(b"".join(out))
+        self._out(b"".join(out))
         if end:
             self._close(s)
 
@@ -355,7 +375,7 @@ class H2Connection:
             s.eof_pending = False
             self._close(s)
         if out:
-            self.transport.write(b"".join(out))
+            self._out(b"".join(out))
 
     def _flush_all(self) -> None:
         for s in list(self.streams.values()):
@@ -373,7 +393,7 @@ class H2Connection:
             return
         self.goaway_sent = True
         self.server.h2_stats["goaways"] += 1
-        self.transport.write(frame(GOAWAY, 0, 0, struct.pack(">II", self.last_stream, code) + msg.encode()[:64]))
+        self._out(frame(GOAWAY, 0, 0, struct.pack(">II", self.last_stream, code) + msg.encode()[:64]))
 
     def connection_lost(self) -> None:
         for s in list(self.streams.values()):
