@@ -91,6 +91,7 @@ struct Stream {
 struct Session {
     Conn c;
     bool connected = false, broken = false, goaway = false;
+    bool got_settings = false;  // the server's first frame (must be SETTINGS: else it does not speak HTTP/2)
     bool flush_posted = false, writing = false, reading = false;
     uint32_t next_id = 1;
     uint32_t goaway_last = 0;

@@ -1415,6 +1415,11 @@ private:
             while (!s->broken) {
                 while (c.buf.size() - c.pos >= 9) {
                     const char* p = c.buf.data() + c.pos;
+                    if (!s->got_settings) {  // a server without HTTP/2 answers the preface in HTTP/1.1, or not at all
+                        if (static_cast<uint8_t>(p[3]) != h2::SETTINGS)
+                            throw NoH2("the server does not speak HTTP/2 (prior knowledge); using HTTP/1.1");
+                        s->got_settings = true;
+                    }
                     uint32_t len = (uint32_t{static_cast<uint8_t>(p[0])} << 16) |
                                    (uint32_t{static_cast<uint8_t>(p[1])} << 8) | static_cast<uint8_t>(p[2]);
                     if (len > h2::kOurMaxFrame) throw TransportError("HTTP/2: frame larger than SETTINGS_MAX_FRAME_SIZE");
@@ -1434,10 +1439,20 @@ private:
                 h2_kick(s);  // acks, window updates and request bodies the frames released
                 co_await c.fill();
             }
+        } catch (const NoH2& e) {
+            h2_ok_ = false;  // this request and every later one over HTTP/1.1
+            h2_break(s, e.what(), true);
         } catch (const hpack::Error& e) {
             h2_break(s, std::string("HTTP/2: HPACK: ") + e.what(), false);
         } catch (const std::exception& e) {
-            h2_break(s, e.what(), false);
+            // the connection ended before the server said anything: on cleartext that is what a server
+            // without HTTP/2 may do with a preface — fall back as for an HTTP/1.1 answer
+            if (!s->got_settings && !url_.tls) {
+                h2_ok_ = false;
+                h2_break(s, std::string("no HTTP/2 answer to the preface (") + e.what() + "); using HTTP/1.1", true);
+            } else {
+                h2_break(s, e.what(), false);
+            }
         }
         s->reading = false;
     }

@@ -278,6 +278,13 @@ async def test_http2_off_and_a_server_without_h2_fall_back_to_http11(tmp_path, n
         await cl.start()
         await cl.ready()
         assert cl.env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
+    # `on` against a cleartext server that answers the preface in HTTP/1.1: the executor falls back
+    async with Cluster(tmp_path / "h1only", "native", n_shards=1, client_http2="on", executors_per_shard=1) as cl:
+        cl.env.shard_servers[0]._http.http2 = False
+        cl.seed(0)
+        await cl.start()
+        await cl.ready()
+        assert cl.env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
     from ncc.app import App
     from ncc.testing.env import FakeEnvironment
     os.makedirs(tmp_path / "tls", exist_ok=True)
