@@ -11,12 +11,14 @@
 // connection and stream windows (a request body waits for WINDOW_UPDATE), WINDOW_UPDATE for what we consume,
 // PING acks, RST_STREAM (REFUSED_STREAM: re-sent), GOAWAY (streams past the last one the server will serve are
 // re-sent on another connection; the connection takes no new ones and closes when its streams are done),
-// per-stream deadlines (RST_STREAM CANCEL).  Watches stay on HTTP/1.1 connections of their own (one stream
-// per long-lived connection: multiplexing buys them nothing).
+// per-stream deadlines (RST_STREAM CANCEL).  Watches are streams too (`Client::stream`), as client-go's: a
+// shard's four watches and its writes share its HTTP/2 connection.
 #pragma once
 
 #include <cstdint>
 #include <deque>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -84,6 +86,12 @@ struct Stream {
     bool retryable = false;  // refused before the server processed it (REFUSED_STREAM, past a GOAWAY, no h2)
     std::string err;
     std::coroutine_handle<> h;
+    // a watch: DATA goes to `on_data` as it arrives (once the status is a 2xx) and each DATA frame moves the
+    // deadline `idle` seconds on — a silent watch is cancelled as an HTTP/1.1 one's connection is aborted
+    std::function<void(std::string_view)> on_data;
+    double idle = 0;
+    std::exception_ptr failure;  // what `on_data` threw (an in-stream 410, say): the stream is cancelled, and the
+                                 // watcher rethrows it — never out of the connection's reader
 };
 
 // One HTTP/2 connection.  Everything the client writes goes through `out`, flushed once per loop iteration

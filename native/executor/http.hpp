@@ -756,6 +756,15 @@ public:
     // A watch stream: `on_lines` gets every complete line of one read; returns at the end of the stream.
     template <class F>
     Task<void> stream(const std::string& target, F on_lines, double idle_timeout) {
+        if (use_h2()) {  // a stream on the shard's HTTP/2 connection (falls back by itself when there is none)
+            std::function<void(std::vector<std::string>&)> cb = on_lines;
+            co_await stream_h2(target, std::move(cb), idle_timeout);
+            co_return;
+        }
+        co_await stream_h1(target, on_lines, idle_timeout);
+    }
+    template <class F>
+    Task<void> stream_h1(const std::string& target, F on_lines, double idle_timeout) {
         auto conn = std::make_unique<Conn>();
         co_await conn->connect(url_, ctx_, creds_.tls_server_name);
         // a silent dead peer must not hold the watch forever: the deadline sweep aborts the stream
@@ -1482,7 +1491,17 @@ private:
                 auto it = s.streams.find(sid);
                 if (it != s.streams.end()) {
                     Stream* st = it->second;
-                    st->r.body.append(d.data(), d.size());
+                    if (st->on_data && st->got_headers && st->r.status < 300) {
+                        st->deadline = now_s() + st->idle;
+                        if (!d.empty()) st->on_data(d);
+                        if (st->failure) {  // the watcher refused what came (e.g. 410 Gone): end this stream only
+                            s.rst(sid, CANCEL);
+                            h2_complete(s, st, false);
+                            break;
+                        }
+                    } else {
+                        st->r.body.append(d.data(), d.size());
+                    }
                     st->recv_unacked += static_cast<int64_t>(p.size());
                     if (flags & END_STREAM) {
                         h2_complete(s, st, st->got_headers);
@@ -1710,6 +1729,76 @@ private:
             off += n;
         }
     }
+    // A watch over HTTP/2: a GET stream whose DATA is cut into lines as it arrives.  Not under the admission gate
+    // (a watch is not a request in flight, as on HTTP/1.1), but it takes a stream slot.
+    Task<void> stream_h2(const std::string& target, std::function<void(std::vector<std::string>&)> on_lines,
+                         double idle_timeout) {
+        for (int resent = 0;; ++resent) {
+            if (!use_h2()) {  // the server turned out not to speak HTTP/2
+                co_await stream_h1(target, on_lines, idle_timeout);
+                co_return;
+            }
+            if (closed_) throw TransportError("client closed");
+            h2::SessionPtr s;
+            while ((s = h2_pick()) == nullptr) {
+                struct Park {
+                    Client* cl;
+                    bool await_ready() { return false; }
+                    void await_suspend(std::coroutine_handle<> h) { cl->h2_waiters_.push_back(h); }
+                    void await_resume() {}
+                };
+                co_await Park{this};
+            }
+            h2::Stream st;
+            std::string pending;
+            std::vector<std::string> lines;
+            st.idle = idle_timeout;
+            st.deadline = now_s() + idle_timeout;
+            st.send_window = s->peer_initial_window;
+            st.on_data = [&pending, &lines, &on_lines, &st](std::string_view d) {
+                pending.append(d.data(), d.size());
+                size_t start = 0, nl;
+                while ((nl = pending.find('\n', start)) != std::string::npos) {
+                    if (nl > start) lines.emplace_back(pending, start, nl - start);
+                    start = nl + 1;
+                }
+                pending.erase(0, start);
+                if (!lines.empty()) {
+                    try {
+                        on_lines(lines);
+                    } catch (...) {
+                        st.failure = std::current_exception();
+                    }
+                    lines.clear();
+                }
+            };
+            st.id = s->next_id;
+            s->next_id += 2;
+            s->streams[st.id] = &st;
+            ++h2_streams;
+            h2_headers_out(*s, st.id, "GET", target, nullptr, nullptr);
+            h2_kick(s);
+            struct Suspend {
+                h2::Stream* st;
+                bool await_ready() { return st->done; }
+                void await_suspend(std::coroutine_handle<> h) { st->h = h; }
+                void await_resume() {}
+            };
+            co_await Suspend{&st};
+            if (st.failure) std::rethrow_exception(st.failure);
+            if (st.got_headers && st.r.status >= 300) throw api_error(st.r.status, st.r.body);
+            if (st.ok) {
+                if (!pending.empty()) {  // a last line without its newline
+                    lines.push_back(pending);
+                    on_lines(lines);
+                }
+                co_return;
+            }
+            if (st.retryable && resent < 8) continue;  // never processed: again, on another connection
+            throw TransportError("watch " + target + ": " + st.err);
+        }
+    }
+
     Task<Response> exchange_h2(const std::string& method, const std::string& target, const std::string* body,
                                const char* content_type, int group) {
         int resent = 0;

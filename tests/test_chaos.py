@@ -282,4 +282,7 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         try:
             await wait_for(done, timeout=15, interval=0.1)
         except AssertionError:
-            raise AssertionError(f"seed {seed} ({topology}): drift on shard-0 not repaired: {last}") from None
+            import json as _json
+            st = cl.app.debug_state().get("executors") if cl.app is not None else None
+            raise AssertionError(f"seed {seed} ({topology}): drift on shard-0 not repaired: {last}; executors: "
+                                 f"{_json.dumps(st, default=str)[:3000]}") from None

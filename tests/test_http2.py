@@ -158,6 +158,9 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
             assert st["h2"]["connections"] >= 1 and st["h2"]["streams"] >= 2 * n, st
             assert st["h2"]["connections"] <= 2, st
             assert fl[f"shard-{i}"]["connections"] <= 2, fl
+            # the executor's four watches are streams on the same connection: nothing else is open to the shard
+            assert st["open"] <= 2, st
+            assert srv.requests["watch_streams"] >= 4
         assert all(f["rejected_429"] == 0 for f in fl.values())
 
 
