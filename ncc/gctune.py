@@ -116,6 +116,12 @@ def full_collect() -> int:
     return n
 
 
+def full_due(waited: float, full_period: float, idle=None) -> bool:
+    """Is the unfreeze + full collection due, `waited` seconds after the last one?  After `full_period` at an
+    idle moment (`idle()`: the controller's queue is drained), and after twice that whatever the load."""
+    return waited >= full_period and (idle is None or waited >= 2 * full_period or idle())
+
+
 async def freeze_loop(period: float = 1.0, collect: int | None = None, full_period: float = 300.0,
                       idle=None, young: bool = True) -> None:
     """Every `period` seconds: collect young garbage (see the module doc; or, with `collect`, always a pass
@@ -144,7 +150,7 @@ async def freeze_loop(period: float = 1.0, collect: int | None = None, full_peri
             gc.freeze()
         if full_period > 0:
             waited = time.monotonic() - last_full
-            if waited >= full_period and (idle is None or waited >= 2 * full_period or idle()):
+            if full_due(waited, full_period, idle):
                 full_collect()
                 seen = _auto["gen1_runs"]
                 last_full = time.monotonic()

@@ -14,6 +14,7 @@ from __future__ import annotations
 import asyncio
 import gc
 import tempfile
+import time
 
 
 async def first_sync(timeout: float = 30.0, poll: float = 0.002, **cfg) -> dict:
@@ -40,6 +41,7 @@ async def first_sync(timeout: float = 30.0, poll: float = 0.002, **cfg) -> dict:
             gc.callbacks.append(on_gc)
             loop = asyncio.get_running_loop()
             t0 = loop.time()
+            run_started = time.monotonic()
             task = asyncio.ensure_future(app.run(stop))
             try:
                 while True:
@@ -56,7 +58,8 @@ async def first_sync(timeout: float = 30.0, poll: float = 0.002, **cfg) -> dict:
                 dt = loop.time() - t0
             finally:
                 gc.callbacks.remove(on_gc)
-            out = {"seconds": dt, "full_collections": full[0], "executor_impl": app.executor_impl,
+            out = {"seconds": dt, "run_started": run_started, "full_collections": full[0],
+                   "executor_impl": app.executor_impl,
                    "queue_native": app.controller.queue.is_native, "reports": app.controller.stats["reports"],
                    "pids": [h.proc.pid for h in app.pool.handles if h.proc is not None] if app.pool else [],
                    "cpu_affinity": app.cpu_affinity or "none"}

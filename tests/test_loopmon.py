@@ -53,16 +53,29 @@ def test_freeze_loop_policies(monkeypatch):
     monkeypatch.setattr(gctune.gc, "get_freeze_count", lambda: 0)
     monkeypatch.setitem(gctune._auto, "freeze_due", False)
 
-    async def main(**kw):
+    async def main(until, **kw):
+        # run the loop until `until()` holds (at most 5 s): a loaded host may give it fewer ticks than the
+        # wall clock would — waiting a fixed 35 ms made this test flaky under a parallel suite
         t = asyncio.ensure_future(gctune.freeze_loop(0.01, **kw))
+        loop = asyncio.get_running_loop()
+        end = loop.time() + 5.0
         await asyncio.sleep(0.035)
+        while not until() and loop.time() < end:
+            await asyncio.sleep(0.01)
         t.cancel()
         await asyncio.gather(t, return_exceptions=True)
-    asyncio.run(main(young=False, full_period=0))
+    asyncio.run(main(lambda: bool(calls), young=False, full_period=0))
     assert calls and all(c == ("freeze",) for c in calls)
     calls.clear()
     young = gctune.STATS["young_n"]
-    asyncio.run(main(full_period=0))  # quiet process: no collection ran, so a generation-1 pass of ours
+    # quiet process: no collection ran, so a generation-1 pass of ours (an automatic generation-1 collection
+    # in between makes the tick leave the freeze to it instead: the test's own gc hooks are mocked out, so
+    # keep the interpreter's collector from running meanwhile)
+    gctune.gc.disable()
+    try:
+        asyncio.run(main(lambda: len(calls) >= 2, full_period=0))
+    finally:
+        gctune.gc.enable()
     assert calls[:2] == [("collect", 1), ("freeze",)] and ("unfreeze",) not in calls
     assert gctune.STATS["young_n"] > young
     calls.clear()
@@ -79,13 +92,13 @@ def test_freeze_loop_policies(monkeypatch):
     assert calls == [("freeze",)] and not gctune._auto["freeze_due"]
     calls.clear()
     full = gctune.STATS["full_n"]
-    asyncio.run(main(full_period=0.015, idle=lambda: True))
+    asyncio.run(main(lambda: ("unfreeze",) in calls, full_period=0.015, idle=lambda: True))
     assert ("unfreeze",) in calls and ("collect", 2) in calls and gctune.STATS["full_n"] > full
     calls.clear()
-    full = gctune.STATS["full_n"]
-    asyncio.run(main(full_period=0.03, idle=lambda: False))  # busy: waits for idle, at most another period
-    assert gctune.STATS["full_n"] == full
-    calls.clear()
+    # busy: the full collection waits for an idle moment, at most another period
+    assert not gctune.full_due(0.9, 1.0, lambda: True)
+    assert gctune.full_due(1.0, 1.0, lambda: True) and gctune.full_due(1.0, 1.0, None)
+    assert not gctune.full_due(1.5, 1.0, lambda: False) and gctune.full_due(2.0, 1.0, lambda: False)
     passes = gctune.STATS["passes"]
-    asyncio.run(main(collect=1, full_period=0))
+    asyncio.run(main(lambda: ("collect", 1) in calls and ("freeze",) in calls, collect=1, full_period=0))
     assert ("collect", 1) in calls and ("freeze",) in calls and gctune.STATS["passes"] > passes
