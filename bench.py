@@ -136,6 +136,14 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def _shard_transport(ctl_debug) -> str:
+    flows = ((ctl_debug or {}).get("executor_flow") or {}).values()
+    h2 = [f.get("http2") for f in flows if isinstance(f, dict)]
+    if not h2:
+        return "n/a"
+    return "http2" if all(h2) else ("http/1.1" if not any(h2) else "mixed")
+
+
 # ------------------------------------------------------------------ workload
 def wave_objects(T: int, version: int, payload: int) -> list:
     """One wave: per template its Secret, its ConfigMap, then the template itself (dependencies first,
@@ -870,7 +878,10 @@ async def run(args, d: Dist) -> dict | None:
                            "global_batch": T, "seq_len": 3, "parallelism": f"shards{d.world}",
                            "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload,
                            "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms,
-                           "tls": bool(args.tls)},
+                           "tls": bool(args.tls),
+                           # what the C++ executors spoke to the shard apiservers (client-http2: HTTP/2 where TLS
+                           # negotiates it, as client-go; the driver's cleartext shape stays on HTTP/1.1)
+                           "shard_transport": _shard_transport(ctl_debug)},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
                 "controller_cpu_us_per_object": round(ctl_us, 1),
