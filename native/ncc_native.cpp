@@ -60,7 +60,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 23
+#define NCC_NATIVE_ABI 24
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -2498,6 +2498,236 @@ private:
     ncc::hpack::Decoder d_;
 };
 
+// The fake apiserver's HTTP/2 framing (ncc/fakeapi/h2.py `H2Connection`): the frame parser, stream assembly and
+// HPACK decoding of a connection, and the response encoder — the per-request work of its HTTP/2 path in C++, as
+// the HTTP/1.1 path has its head parser here (parse_request_head).  Python keeps the policy: flow control of
+// responses, the stream limit, GOAWAY, dispatch.
+class H2ServerParser {
+public:
+    explicit H2ServerParser(bool credit_data) : credit_(credit_data) {}
+
+    // Feed received bytes; returns the events they complete, in order:
+    //   ("req", sid, method, path, {lower-cased name: value}, body)  a request whose END_STREAM arrived
+    //   ("settings", [(id, value), ...])                              a SETTINGS frame to apply and ack
+    //   ("window", sid, increment)   ("rst", sid, code)   ("ping", payload)   ("goaway", last, code)
+    //   ("credit", sid, n)            DATA consumed (only with credit_data: a small advertised window)
+    //   ("error", code, message)      a connection error: send GOAWAY and close
+    py::list feed(const py::bytes& data) {
+        std::string_view d = data;
+        buf_.append(d.data(), d.size());
+        py::list out;
+        try {
+            parse(out);
+        } catch (const ncc::hpack::Error& e) {
+            out.append(py::make_tuple("error", 9, std::string("HPACK: ") + e.what()));
+            buf_.clear();
+            pos_ = 0;
+        } catch (const std::runtime_error& e) {
+            out.append(py::make_tuple("error", 1, std::string(e.what())));
+            buf_.clear();
+            pos_ = 0;
+        }
+        if (pos_ > 0 && (pos_ == buf_.size() || pos_ > 65536)) {
+            buf_.erase(0, pos_);
+            pos_ = 0;
+        }
+        return out;
+    }
+    size_t open_streams() const { return streams_.size(); }
+
+private:
+    struct Stream {
+        std::string method, path, authority;
+        std::vector<std::pair<std::string, std::string>> headers;
+        std::string body;
+        bool have_headers = false, ended = false;
+    };
+    std::string buf_;
+    size_t pos_ = 0;
+    bool preface_ = false, credit_;
+    uint32_t last_stream_ = 0, cont_id_ = 0;
+    bool cont_end_ = false;
+    std::string cont_block_;
+    ncc::hpack::Decoder dec_{4096};
+    std::unordered_map<uint32_t, Stream> streams_;
+
+    static uint32_t u32(const char* p) {
+        const auto* u = reinterpret_cast<const unsigned char*>(p);
+        return (uint32_t{u[0]} << 24) | (uint32_t{u[1]} << 16) | (uint32_t{u[2]} << 8) | u[3];
+    }
+    static std::string_view strip(uint8_t flags, std::string_view p, bool headers) {
+        size_t pad = 0;
+        if (flags & 0x8) {
+            if (p.empty()) throw std::runtime_error("padded frame without a pad length");
+            pad = static_cast<uint8_t>(p[0]);
+            p.remove_prefix(1);
+        }
+        if (headers && (flags & 0x20)) {
+            if (p.size() < 5) throw std::runtime_error("short PRIORITY fields");
+            p.remove_prefix(5);
+        }
+        if (pad > p.size()) throw std::runtime_error("padding longer than the frame");
+        p.remove_suffix(pad);
+        return p;
+    }
+    void emit_request(py::list& out, uint32_t sid, Stream& st) {
+        py::dict h;
+        for (auto& kv : st.headers) h[py::str(kv.first)] = py::str(kv.second);
+        if (!h.contains("host") && !st.authority.empty()) h["host"] = py::str(st.authority);
+        out.append(py::make_tuple("req", sid, py::str(st.method.empty() ? "GET" : st.method),
+                                  py::str(st.path.empty() ? "/" : st.path), h, py::bytes(st.body)));
+        streams_.erase(sid);
+    }
+    void headers_done(py::list& out, uint32_t sid) {
+        std::vector<ncc::hpack::Decoder::Header> hs;
+        dec_.decode(reinterpret_cast<const uint8_t*>(cont_block_.data()), cont_block_.size(), hs);
+        auto it = streams_.find(sid);
+        if (it == streams_.end()) {  // a new stream (a HEADERS block on an open one is trailers)
+            if (sid <= last_stream_ && sid != 0) throw std::runtime_error("stream id reused");
+            last_stream_ = sid;
+            it = streams_.emplace(sid, Stream{}).first;
+        }
+        Stream& st = it->second;
+        if (!st.have_headers) {
+            st.have_headers = true;
+            for (auto& h : hs) {
+                if (h.first == ":method")
+                    st.method = std::move(h.second);
+                else if (h.first == ":path")
+                    st.path = std::move(h.second);
+                else if (h.first == ":authority")
+                    st.authority = std::move(h.second);
+                else if (!h.first.empty() && h.first[0] != ':' && h.first != "connection" && h.first != "keep-alive" &&
+                         h.first != "transfer-encoding" && h.first != "upgrade" && h.first != "proxy-connection")
+                    st.headers.emplace_back(std::move(h.first), std::move(h.second));
+            }
+        }
+        if (cont_end_) emit_request(out, sid, st);
+    }
+    void parse(py::list& out) {
+        static const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
+        if (!preface_) {
+            if (buf_.size() - pos_ < 24) return;
+            if (buf_.compare(pos_, 24, kPreface, 24) != 0) throw std::runtime_error("bad connection preface");
+            pos_ += 24;
+            preface_ = true;
+        }
+        while (buf_.size() - pos_ >= 9) {
+            const char* p = buf_.data() + pos_;
+            uint32_t len = (uint32_t{static_cast<uint8_t>(p[0])} << 16) | (uint32_t{static_cast<uint8_t>(p[1])} << 8) |
+                           static_cast<uint8_t>(p[2]);
+            if (len > (1u << 14)) throw std::runtime_error("frame larger than SETTINGS_MAX_FRAME_SIZE");
+            if (buf_.size() - pos_ < 9 + len) return;
+            uint8_t type = static_cast<uint8_t>(p[3]), flags = static_cast<uint8_t>(p[4]);
+            uint32_t sid = u32(p + 5) & 0x7fffffffu;
+            std::string_view pl(p + 9, len);
+            pos_ += 9 + len;
+            if (cont_id_ != 0 && (type != 9 || sid != cont_id_)) throw std::runtime_error("expected CONTINUATION");
+            switch (type) {
+                case 0: {  // DATA
+                    if (credit_ && len > 0) out.append(py::make_tuple("credit", sid, len));
+                    std::string_view d = strip(flags, pl, false);
+                    auto it = streams_.find(sid);
+                    if (it == streams_.end() || it->second.ended) {
+                        out.append(py::make_tuple("rst_closed", sid));
+                        break;
+                    }
+                    it->second.body.append(d.data(), d.size());
+                    if (flags & 0x1) emit_request(out, sid, it->second);
+                    break;
+                }
+                case 1: {  // HEADERS
+                    if (sid == 0 || sid % 2 == 0) throw std::runtime_error("HEADERS on an even stream");
+                    std::string_view b = strip(flags, pl, true);
+                    cont_block_.assign(b.data(), b.size());
+                    cont_end_ = (flags & 0x1) != 0;
+                    if (flags & 0x4)
+                        headers_done(out, sid);
+                    else
+                        cont_id_ = sid;
+                    break;
+                }
+                case 9: {  // CONTINUATION
+                    if (cont_id_ == 0) throw std::runtime_error("CONTINUATION without HEADERS");
+                    cont_block_.append(pl.data(), pl.size());
+                    if (flags & 0x4) {
+                        uint32_t id = cont_id_;
+                        cont_id_ = 0;
+                        headers_done(out, id);
+                    }
+                    break;
+                }
+                case 4: {  // SETTINGS
+                    if (flags & 0x1) break;
+                    py::list kv;
+                    for (size_t k = 0; k + 6 <= pl.size(); k += 6)
+                        kv.append(py::make_tuple((static_cast<uint8_t>(pl[k]) << 8) | static_cast<uint8_t>(pl[k + 1]),
+                                                 u32(pl.data() + k + 2)));
+                    out.append(py::make_tuple("settings", kv));
+                    break;
+                }
+                case 8:  // WINDOW_UPDATE
+                    out.append(py::make_tuple("window", sid, pl.size() >= 4 ? (u32(pl.data()) & 0x7fffffffu) : 0u));
+                    break;
+                case 3:  // RST_STREAM
+                    streams_.erase(sid);
+                    out.append(py::make_tuple("rst", sid, pl.size() >= 4 ? u32(pl.data()) : 0u));
+                    break;
+                case 6:  // PING
+                    if (!(flags & 0x1)) out.append(py::make_tuple("ping", py::bytes(pl.data(), pl.size())));
+                    break;
+                case 7:  // GOAWAY
+                    out.append(py::make_tuple("goaway", pl.size() >= 4 ? (u32(pl.data()) & 0x7fffffffu) : 0u,
+                                              pl.size() >= 8 ? u32(pl.data() + 4) : 0u));
+                    break;
+                case 5:
+                    throw std::runtime_error("PUSH_PROMISE from a client");
+                default:  // PRIORITY, unknown types
+                    break;
+            }
+        }
+    }
+};
+
+// HEADERS (+ CONTINUATION) and DATA frames of a whole response on stream `sid`, the last frame ending the stream;
+// `extra`: further header fields.  The caller has checked the flow-control windows.
+py::bytes h2_response(uint32_t sid, int status, const std::string& content_type, const py::bytes& body,
+                      const std::vector<std::pair<std::string, std::string>>& extra, size_t max_frame) {
+    std::string_view b = body;
+    std::string block;
+    ncc::hpack::encode_field(block, ":status", std::to_string(status));
+    ncc::hpack::encode_literal(block, "content-type", content_type);
+    ncc::hpack::encode_literal(block, "content-length", std::to_string(b.size()));
+    for (const auto& kv : extra) ncc::hpack::encode_field(block, kv.first, kv.second);
+    std::string out;
+    out.reserve(block.size() + b.size() + 32);
+    auto frame = [&out](uint8_t type, uint8_t flags, uint32_t id, const char* p, size_t n) {
+        out.push_back(static_cast<char>(n >> 16));
+        out.push_back(static_cast<char>(n >> 8));
+        out.push_back(static_cast<char>(n));
+        out.push_back(static_cast<char>(type));
+        out.push_back(static_cast<char>(flags));
+        out.push_back(static_cast<char>((id >> 24) & 0x7f));
+        out.push_back(static_cast<char>(id >> 16));
+        out.push_back(static_cast<char>(id >> 8));
+        out.push_back(static_cast<char>(id));
+        out.append(p, n);
+    };
+    max_frame = std::max<size_t>(max_frame, 1);
+    size_t n = std::min(block.size(), max_frame);
+    bool more = n < block.size();
+    frame(1, static_cast<uint8_t>((b.empty() ? 0x1 : 0) | (more ? 0 : 0x4)), sid, block.data(), n);
+    for (size_t off = n; off < block.size(); off += n) {
+        n = std::min(block.size() - off, max_frame);
+        frame(9, off + n < block.size() ? 0 : 0x4, sid, block.data() + off, n);
+    }
+    for (size_t off = 0; off < b.size(); off += n) {
+        n = std::min(b.size() - off, max_frame);
+        frame(0, off + n == b.size() ? 0x1 : 0, sid, b.data() + off, n);
+    }
+    return py::bytes(out);
+}
+
 py::bytes hpack_encode(const std::vector<std::pair<std::string, std::string>>& fields, bool huffman) {
     std::string out;
     for (const auto& f : fields) ncc::hpack::encode_field(out, f.first, f.second, huffman);
@@ -2557,6 +2787,12 @@ PYBIND11_MODULE(_native, m) {
         .def("set_limit", &HpackDecoder::set_limit)
         .def("table_size", &HpackDecoder::table_size)
         .def("table_entries", &HpackDecoder::table_entries);
+    py::class_<H2ServerParser>(m, "H2ServerParser")
+        .def(py::init<bool>(), py::arg("credit_data") = false)
+        .def("feed", &H2ServerParser::feed, py::arg("data"))
+        .def("open_streams", &H2ServerParser::open_streams);
+    m.def("h2_response", &h2_response, py::arg("sid"), py::arg("status"), py::arg("content_type"), py::arg("body"),
+          py::arg("extra"), py::arg("max_frame"), "the HEADERS and DATA frames of a whole HTTP/2 response");
     m.def("hpack_encode", &hpack_encode, py::arg("fields"), py::arg("huffman") = false,
           "a header block of static-table fields and literals without indexing");
     m.def("hpack_huffman_encode", [](const py::bytes& s) { return py::bytes(ncc::hpack::huffman_encode(std::string_view(s))); },

@@ -7,9 +7,10 @@ apiserver answer it, so the HTTP/2 path runs against the same substrate as every
 
 * negotiation: ALPN "h2" on a TLS connection (`--http2` puts it in the server's ALPN list), or the client
   connection preface on a cleartext one ("prior knowledge", how the benches and tests run it unencrypted);
-* one `H2Connection` per connection on top of `httpserver._ServerConn`: frames parsed as they arrive, HPACK
-  decoded by the extension's decoder (native/common/hpack.hpp, one dynamic table per connection), each
-  complete stream handed to the same handlers as an HTTP/1.1 request — concurrently, as streams are;
+* one `H2Connection` per connection on top of `httpserver._ServerConn`: frames parsed, streams assembled and
+  HPACK decoded as they arrive by the extension's `H2ServerParser` (native/common/hpack.hpp, one dynamic table
+  per connection), each complete stream handed to the same handlers as an HTTP/1.1 request — concurrently,
+  as streams are; a response that fits the windows is framed natively in one call (`h2_response`);
 * responses as HEADERS + DATA within the client's flow-control windows (connection and stream), queued
   until a WINDOW_UPDATE when they do not fit; watch streams as DATA frames without END_STREAM;
 * SETTINGS (MAX_CONCURRENT_STREAMS enforced with REFUSED_STREAM), PING, RST_STREAM, WINDOW_UPDATE, GOAWAY.
@@ -46,45 +47,39 @@ OUR_MAX_FRAME = 1 << 14
 _HOP_BY_HOP = {"connection", "keep-alive", "transfer-encoding", "upgrade", "proxy-connection"}
 
 
-class ProtocolError(Exception):
-    def __init__(self, code: int, msg: str):
-        super().__init__(msg)
-        self.code = code
-
-
 def frame(ftype: int, flags: int, stream: int, payload: bytes = b"") -> bytes:
     n = len(payload)
     return struct.pack(">BHBBI", n >> 16, n & 0xFFFF, ftype, flags, stream & 0x7FFFFFFF) + payload
 
 
 class _Stream:
-    __slots__ = ("id", "headers", "block", "body", "send_window", "pending", "ended", "closed", "response_started",
-                 "eof_pending")
+    __slots__ = ("id", "send_window", "pending", "closed", "response_started", "eof_pending")
 
     def __init__(self, sid: int, window: int):
         self.id = sid
-        self.headers: list = []
-        self.block = bytearray()  # header block fragments (HEADERS + CONTINUATION)
-        self.body = bytearray()
         self.send_window = window
         self.pending = bytearray()  # response DATA not yet within the windows
         self.eof_pending = False    # END_STREAM to send once `pending` is out
-        self.ended = False          # the client's half is closed
         self.closed = False         # reset, or our END_STREAM sent
         self.response_started = False
 
 
 class H2Connection:
-    """The HTTP/2 side of one `_ServerConn` (see the module doc)."""
+    """The HTTP/2 side of one `_ServerConn` (see the module doc).  Frames, stream assembly and HPACK are the
+    extension's `H2ServerParser`; this class keeps the policy and the responses' flow control."""
 
     def __init__(self, conn, server):
         self.conn = conn
         self.server = server
         self.transport = conn.transport
-        self.buf = bytearray()
-        self.preface_seen = False
-        self.decoder = _native.load(required=True).HpackDecoder(4096)
-        self.streams: dict[int, _Stream] = {}
+        mod = _native.load(required=True)
+        self.max_streams = int(server.h2_options.get("h2_max_streams", 0) or 0) or 250
+        self.goaway_after = int(server.h2_options.get("h2_goaway_after", 0) or 0)
+        # a small stream window makes a client's request bodies wait for our WINDOW_UPDATEs (tests)
+        self.our_window = int(server.h2_options.get("h2_initial_window", 0) or 0) or OUR_WINDOW
+        self.parser = mod.H2ServerParser(self.our_window < OUR_WINDOW)
+        self._encode = mod.h2_response
+        self.streams: dict[int, _Stream] = {}  # dispatched, not yet answered to the end
         self.last_stream = 0
         self.served = 0
         self.goaway_sent = False
@@ -92,14 +87,7 @@ class H2Connection:
         self.peer_initial_window = 65535
         self.peer_max_frame = 16384
         self.recv_unacked = 0
-        self.continuation: _Stream | None = None
-        self.max_streams = int(server.h2_options.get("h2_max_streams", 0) or 0) or 250
-        self.goaway_after = int(server.h2_options.get("h2_goaway_after", 0) or 0)
-        # a small stream window makes a client's request bodies wait for our WINDOW_UPDATEs (tests)
-        self.our_window = int(server.h2_options.get("h2_initial_window", 0) or 0) or OUR_WINDOW
-        st = server.h2_stats
-        st["connections"] += 1
-        self.open_streams = 0
+        server.h2_stats["connections"] += 1
         # frames produced in one loop iteration (every response a batch of requests gets) leave in one write
         self._wbuf: list = []
         self._flush_scheduled = False
@@ -108,6 +96,10 @@ class H2Connection:
             ">HIHIHIHI", S_MAX_CONCURRENT_STREAMS, self.max_streams, S_INITIAL_WINDOW_SIZE, self.our_window,
             S_MAX_FRAME_SIZE, OUR_MAX_FRAME, S_ENABLE_PUSH, 0)) +
             frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", (1 << 30) - 65535)))
+
+    @property
+    def open_streams(self) -> int:
+        return len(self.streams)
 
     def _out(self, data: bytes) -> None:
         self._wbuf.append(data)
@@ -126,175 +118,69 @@ class H2Connection:
 
     # ------------------------------------------------------------------ input
     def data_received(self, data: bytes) -> None:
-        self.buf += data
-        try:
-            self._parse()
-        except ProtocolError as e:
-            self._goaway(e.code, str(e))
-            self._flush_out()
-            self.transport.close()
-        except ValueError as e:  # HPACK: a COMPRESSION_ERROR ends the connection
-            self._goaway(COMPRESSION_ERROR, str(e))
-            self._flush_out()
-            self.transport.close()
-
-    def _parse(self) -> None:
-        buf = self.buf
-        if not self.preface_seen:
-            if len(buf) < len(PREFACE):
-                return
-            if bytes(buf[:len(PREFACE)]) != PREFACE:
-                raise ProtocolError(PROTOCOL_ERROR, "bad connection preface")
-            del buf[:len(PREFACE)]
-            self.preface_seen = True
-        while len(buf) >= 9:
-            n = (buf[0] << 16) | (buf[1] << 8) | buf[2]
-            if n > OUR_MAX_FRAME:
-                raise ProtocolError(FRAME_SIZE_ERROR, f"frame of {n} bytes")
-            if len(buf) < 9 + n:
-                return
-            ftype, flags = buf[3], buf[4]
-            sid = struct.unpack_from(">I", buf, 5)[0] & 0x7FFFFFFF
-            payload = bytes(buf[9:9 + n])
-            del buf[:9 + n]
-            if self.continuation is not None and (ftype != CONTINUATION or sid != self.continuation.id):
-                raise ProtocolError(PROTOCOL_ERROR, "expected CONTINUATION")
-            self._frame(ftype, flags, sid, payload)
-
-    def _frame(self, ftype: int, flags: int, sid: int, payload: bytes) -> None:
-        if ftype == SETTINGS:
-            if flags & ACK:
-                return
-            for k in range(0, len(payload) - len(payload) % 6, 6):
-                ident, value = struct.unpack_from(">HI", payload, k)
-                if ident == S_INITIAL_WINDOW_SIZE:
-                    delta = value - self.peer_initial_window
-                    self.peer_initial_window = value
-                    for s in self.streams.values():
-                        s.send_window += delta
-                elif ident == S_MAX_FRAME_SIZE:
-                    self.peer_max_frame = value
-            self._out(frame(SETTINGS, ACK, 0))
-            self._flush_all()
-        elif ftype == HEADERS:
-            payload = self._strip(flags, payload, priority=True)
-            if sid % 2 == 0 or sid == 0:
-                raise ProtocolError(PROTOCOL_ERROR, f"HEADERS on stream {sid}")
-            s = self.streams.get(sid)
-            if s is None:  # a new stream (a second HEADERS block on an open stream is trailers)
-                if sid <= self.last_stream:
-                    raise ProtocolError(PROTOCOL_ERROR, f"stream {sid} reused")
-                self.last_stream = sid
-                s = _Stream(sid, self.peer_initial_window)
-                refused = self.goaway_sent or self.open_streams >= self.max_streams
-                self.streams[sid] = s
-                self.open_streams += 1
-                if refused:
-                    s.closed = True  # decode the block all the same: the HPACK state is the connection's
-                    self.server.h2_stats["refused"] += 1
-            s.block += payload
-            if flags & END_STREAM:
-                s.ended = True
-            if flags & END_HEADERS:
-                self._headers_done(s)
-            else:
-                self.continuation = s
-        elif ftype == CONTINUATION:
-            s = self.continuation
-            if s is None or s.id != sid:
-                raise ProtocolError(PROTOCOL_ERROR, "CONTINUATION without HEADERS")
-            s.block += payload
-            if flags & END_HEADERS:
-                self.continuation = None
-                self._headers_done(s)
-        elif ftype == DATA:
-            # flow control counts the whole payload, padding included; the connection window is topped up
-            # every 512 MiB, a stream's never (request bodies are far below OUR_WINDOW; an apiserver caps them
-            # at 3 MiB)
-            self.recv_unacked += len(payload)
-            if self.recv_unacked >= (1 << 29):
-                self._out(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", self.recv_unacked)))
-                self.recv_unacked = 0
-            payload = self._strip(flags, payload)
-            s = self.streams.get(sid)
-            if s is None or s.ended:
-                self._out(frame(RST_STREAM, 0, sid, struct.pack(">I", STREAM_CLOSED)))
-                return
-            s.body += payload
-            if flags & END_STREAM:
-                s.ended = True
-                self._dispatch(s)
-            elif self.our_window < OUR_WINDOW and payload:  # small-window mode: credit what was consumed
-                self._out(frame(WINDOW_UPDATE, 0, sid, struct.pack(">I", len(payload))))
-        elif ftype == WINDOW_UPDATE:
-            inc = struct.unpack(">I", payload[:4])[0] & 0x7FFFFFFF
-            if sid == 0:
-                self.conn_send_window += inc
+        for ev in self.parser.feed(data):
+            kind = ev[0]
+            if kind == "req":
+                self._request(*ev[1:])
+            elif kind == "window":
+                _, sid, inc = ev
+                if sid == 0:
+                    self.conn_send_window += inc
+                    self._flush_all()
+                else:
+                    s = self.streams.get(sid)
+                    if s is not None:
+                        s.send_window += inc
+                        self._flush(s)
+            elif kind == "credit":  # small-window mode: credit what the client's DATA consumed
+                self._out(frame(WINDOW_UPDATE, 0, ev[1], struct.pack(">I", ev[2])))
+            elif kind == "settings":
+                for ident, value in ev[1]:
+                    if ident == S_INITIAL_WINDOW_SIZE:
+                        delta = value - self.peer_initial_window
+                        self.peer_initial_window = value
+                        for st in self.streams.values():
+                            st.send_window += delta
+                    elif ident == S_MAX_FRAME_SIZE:
+                        self.peer_max_frame = value
+                self._out(frame(SETTINGS, ACK, 0))
                 self._flush_all()
-            else:
-                s = self.streams.get(sid)
-                if s is not None:
-                    s.send_window += inc
-                    self._flush(s)
-        elif ftype == PING:
-            if not flags & ACK:
-                self._out(frame(PING, ACK, 0, payload))
-        elif ftype == RST_STREAM:
-            s = self.streams.get(sid)
-            if s is not None:
-                self._close(s)
-        elif ftype == GOAWAY:
-            self.goaway_sent = True  # the client is leaving: nothing new
-        elif ftype == PUSH_PROMISE:
-            raise ProtocolError(PROTOCOL_ERROR, "PUSH_PROMISE from a client")
-        # PRIORITY and unknown frame types: ignored
+            elif kind == "ping":
+                self._out(frame(PING, ACK, 0, ev[1]))
+            elif kind == "rst":
+                st = self.streams.get(ev[1])
+                if st is not None:
+                    self._close(st)
+            elif kind == "rst_closed":  # DATA on a stream that is not open
+                self._out(frame(RST_STREAM, 0, ev[1], struct.pack(">I", STREAM_CLOSED)))
+            elif kind == "goaway":
+                self.goaway_sent = True  # the client is leaving: nothing new
+            elif kind == "error":
+                self._goaway(ev[1], ev[2])
+                self._flush_out()
+                self.transport.close()
+                return
 
-    @staticmethod
-    def _strip(flags: int, payload: bytes, priority: bool = False) -> bytes:
-        pad = 0
-        if flags & PADDED:
-            pad = payload[0]
-            payload = payload[1:]
-        if priority and flags & PRIORITY_FLAG:
-            payload = payload[5:]
-        if pad:
-            if pad > len(payload):
-                raise ProtocolError(PROTOCOL_ERROR, "padding longer than the frame")
-            payload = payload[:-pad]
-        return payload
-
-    def _headers_done(self, s: _Stream) -> None:
-        hs = self.decoder.decode(bytes(s.block))
-        s.block = bytearray()
-        if s.closed:  # refused (over the stream limit, or after GOAWAY)
-            self._out(frame(RST_STREAM, 0, s.id, struct.pack(">I", REFUSED_STREAM)))
-            self.streams.pop(s.id, None)
-            self.open_streams -= 1
+    def _request(self, sid: int, method: str, path: str, headers: dict, body: bytes) -> None:
+        self.last_stream = max(self.last_stream, sid)
+        if self.goaway_sent or len(self.streams) >= self.max_streams:
+            self.server.h2_stats["refused"] += 1
+            self._out(frame(RST_STREAM, 0, sid, struct.pack(">I", REFUSED_STREAM)))
             return
-        if not s.headers:
-            s.headers = hs
-        if s.ended:
-            self._dispatch(s)
+        s = self.streams[sid] = _Stream(sid, self.peer_initial_window)
+        self._dispatch(s, method, path, headers, body)
 
     # ------------------------------------------------------------------ requests
-    def _dispatch(self, s: _Stream) -> None:
+    def _dispatch(self, s: _Stream, method: str, path: str, headers: dict, body: bytes) -> None:
         from .httpserver import Deferred, Request, Response
-        pseudo, headers = {}, {}
-        for k, v in s.headers:
-            if k.startswith(":"):
-                pseudo[k] = v
-            elif k not in _HOP_BY_HOP:
-                headers[k] = v
-        if "host" not in headers and ":authority" in pseudo:
-            headers["host"] = pseudo[":authority"]
-        req = Request(pseudo.get(":method", "GET"), pseudo.get(":path", "/"), headers, bytes(s.body))
+        req = Request(method, path, headers, body)
         req._conn = self.conn  # type: ignore[attr-defined]
         req._h2 = (self, s)    # type: ignore[attr-defined]
-        s.body = bytearray()
         self.served += 1
-        self.server.h2_stats["streams"] += 1
         st = self.server.h2_stats
-        st["max_open"] = max(st["max_open"], self.open_streams)
+        st["streams"] += 1
+        if len(self.streams) > st["max_open"]:
+            st["max_open"] = len(self.streams)
         if self.goaway_after and self.served >= self.goaway_after and not self.goaway_sent:
             self._goaway(NO_ERROR, "h2_goaway_after")
         fast = self.server.fast
@@ -328,12 +214,21 @@ class H2Connection:
     def respond(self, s: _Stream, resp) -> None:
         if s.closed or self.conn.closed:
             return
-        fields = [(":status", str(resp.status)), ("content-type", resp.content_type),
-                  ("content-length", str(len(resp.body)))]
-        fields += [(k.lower(), str(v)) for k, v in resp.headers.items()]
-        self.send_headers(s, fields, end=not resp.body)
-        if resp.body:
-            self.send_data(s, resp.body, end=True)
+        body = resp.body
+        n = len(body)
+        extra = [(k.lower(), str(v)) for k, v in resp.headers.items()] if resp.headers else []
+        if n <= s.send_window and n <= self.conn_send_window and not s.pending:
+            # the common case, whole within the windows: every frame of it encoded natively in one go
+            self._out(self._encode(s.id, resp.status, resp.content_type, body, extra, self.peer_max_frame))
+            s.send_window -= n
+            self.conn_send_window -= n
+            s.response_started = True
+            self._close(s)
+            return
+        fields = [(":status", str(resp.status)), ("content-type", resp.content_type), ("content-length", str(n))]
+        self.send_headers(s, fields + extra, end=not body)
+        if body:
+            self.send_data(s, body, end=True)
 
     def send_headers(self, s: _Stream, fields: list, end: bool = False) -> None:
         block = _native.load(required=True).hpack_encode(fields)
@@ -383,10 +278,8 @@ class H2Connection:
                 self._flush(s)
 
     def _close(self, s: _Stream) -> None:
-        if not s.closed:
-            s.closed = True
-        if self.streams.pop(s.id, None) is not None:
-            self.open_streams -= 1
+        s.closed = True
+        self.streams.pop(s.id, None)
 
     def _goaway(self, code: int, msg: str) -> None:
         if self.goaway_sent and code == NO_ERROR:

@@ -69,7 +69,10 @@ def collect_startup() -> None:
 
 def tune(thresholds: tuple = THRESHOLDS, account: bool = True) -> None:
     gc.set_threshold(*thresholds)
-    gc.freeze()  # O(1): what survived until now is not scanned again
+    # the young generations only — what was allocated since `collect_startup` froze the heap (a few ms at most,
+    # not a pass over the heap) — so start-up garbage cycles are not frozen unscanned; then freeze the rest
+    gc.collect(1)
+    gc.freeze()
     if account and _on_gc not in gc.callbacks:  # the young-pass rule of freeze_loop needs the counter
         gc.callbacks.append(_on_gc)
 

@@ -312,3 +312,47 @@ async def test_http2_off_and_a_server_without_h2_fall_back_to_http11(tmp_path, n
             await task
         await cc.close()
         await env.stop()
+
+
+def test_server_parser_assembles_streams_from_any_framing():
+    """The fake apiserver's native frame parser (ncc/fakeapi/h2.py): a request split over HEADERS with padding
+    and priority, CONTINUATION and padded DATA frames, fed one byte at a time, comes out as one request;
+    control frames come out as events; a broken preface is a connection error."""
+    from ncc.fakeapi import h2
+    block = _m.hpack_encode([(":method", "PUT"), (":scheme", "http"), (":authority", "a:1"),
+                             (":path", "/api/v1/namespaces/n/configmaps/c"), ("content-type", "application/json")])
+    first, rest = block[:10], block[10:]
+    pad = 3
+    frames = [h2.PREFACE, h2.frame(h2.SETTINGS, 0, 0, bytes.fromhex("000400010000")),
+              h2.frame(h2.HEADERS, h2.PADDED | h2.PRIORITY_FLAG, 1, bytes([pad]) + b"\0\0\0\0\x10" + first + b"\0" * pad),
+              h2.frame(h2.CONTINUATION, h2.END_HEADERS, 1, rest),
+              h2.frame(h2.DATA, h2.PADDED, 1, bytes([2]) + b'{"a":' + b"\0\0"),
+              h2.frame(h2.DATA, h2.END_STREAM, 1, b"1}"),
+              h2.frame(h2.WINDOW_UPDATE, 0, 0, (1000).to_bytes(4, "big")),
+              h2.frame(h2.PING, 0, 0, b"12345678"), h2.frame(h2.RST_STREAM, 0, 3, (8).to_bytes(4, "big"))]
+    data = b"".join(frames)
+    p = _m.H2ServerParser(False)
+    events = []
+    for i in range(len(data)):
+        events += p.feed(data[i:i + 1])
+    assert events[0] == ("settings", [(4, 65536)])
+    kind, sid, method, path, headers, body = events[1]
+    assert (kind, sid, method, path, body) == ("req", 1, "PUT", "/api/v1/namespaces/n/configmaps/c", b'{"a":1}')
+    assert headers == {"content-type": "application/json", "host": "a:1"}
+    assert events[2:] == [("window", 0, 1000), ("ping", b"12345678"), ("rst", 3, 8)]
+    assert p.open_streams() == 0
+    bad = _m.H2ServerParser(False)
+    assert bad.feed(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")[0][0] == "error"
+    resp = _m.h2_response(5, 200, "application/json", b"x" * 40000, [("retry-after", "1")], 16384)
+    d = _m.HpackDecoder()
+    n = int.from_bytes(resp[:3], "big")
+    assert resp[3] == h2.HEADERS and resp[4] == h2.END_HEADERS
+    assert d.decode(resp[9:9 + n]) == [(":status", "200"), ("content-type", "application/json"),
+                                       ("content-length", "40000"), ("retry-after", "1")]
+    off, got, flags = 9 + n, b"", []
+    while off < len(resp):
+        n = int.from_bytes(resp[off:off + 3], "big")
+        flags.append(resp[off + 4])
+        got += resp[off + 9:off + 9 + n]
+        off += 9 + n
+    assert got == b"x" * 40000 and flags == [0, 0, h2.END_STREAM]
