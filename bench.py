@@ -672,6 +672,10 @@ async def run(args, d: Dist) -> dict | None:
                 # shared multi-CCD machines, where the coordinator and its executors on one L3 domain run in the
                 # fast regime (ncc/affinity.py); reported as controller_sizing.cpu_affinity
                 env.setdefault("NCC_CPU_AFFINITY", "l3")
+                # the executors speak HTTP/2 to the shard apiservers, as client-go does to a kube-apiserver (by
+                # ALPN on TLS; here, on the bench's cleartext connections, with prior knowledge): `--extra-env
+                # NEXUS__CLIENT_HTTP2=off` measures the HTTP/1.1 pool instead (BENCHMARKS.md "HTTP/2")
+                env.setdefault("NEXUS__CLIENT_HTTP2", "on")
                 # the ops port: /debug/state after the timed waves (each executor's client flow control, the
                 # coordinator's GC passes); executors report their state every second
                 import socket as _socket

@@ -145,6 +145,7 @@ class Topology:
             self.ops = f"127.0.0.1:{sk.getsockname()[1]}"
         env["NEXUS__HEALTH_BIND_ADDRESS"] = self.ops
         env.setdefault("NCC_STATUS_S", "1")
+        env.setdefault("NEXUS__CLIENT_HTTP2", "on")  # as bench.py: HTTP/2 to the shards, as client-go
         env.update(self.extra_env)
         if self.stages:
             env["NCC_TRACE_STAGES"] = os.path.join(self.work, "trace")
