@@ -61,6 +61,8 @@ bench_once() {  # <file> [ARGS...]
   done
   env "${envs[@]}" timeout -k 10 "${BENCH_TIMEOUT:-300}" python3 bench.py --gpus 1 --steps 20 --warmup 5 "${flags[@]}" \
     > "$f.json" 2> "$f.err" || return $?
+  # a stderr holding nothing but the ROCm runtime's amdgpu.ids notice is not kept
+  grep -qv 'amdgpu.ids: No such file' "$f.err" || rm -f "$f.err"
   summary "$f.json"
 }
 
