@@ -226,6 +226,12 @@ inline void encode_literal(std::string& out, std::string_view name, std::string_
     encode_string(out, value, huffman);
 }
 
+// A literal without indexing whose name is static-table entry `name_index` (no lookup: the caller knows it).
+inline void encode_literal_indexed_name(std::string& out, int name_index, std::string_view value) {
+    encode_int(out, static_cast<uint64_t>(name_index), 4, 0x00);
+    encode_string(out, value, false);
+}
+
 // A field from the static table when it holds (name, value) exactly, else a literal.
 inline void encode_field(std::string& out, std::string_view name, std::string_view value, bool huffman = false) {
     for (int i = 1; i <= kStaticCount; ++i)

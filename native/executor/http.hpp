@@ -856,6 +856,8 @@ private:
     std::vector<h2::SessionPtr> h2s_;                 // HTTP/2 connections, oldest first
     std::deque<std::coroutine_handle<>> h2_waiters_;  // requests waiting for stream room on one of them
     std::string h2_block_;                            // scratch: the header block being encoded
+    std::string h2_fixed_;                            // :scheme, :authority, user-agent, accept, encoded once
+    std::string h2_auth_block_, h2_auth_for_;         // the authorization field, encoded for this value
     std::string auth_;                                // memoised Authorization value
     std::string auth_token_;                          // ... for this token
 
@@ -1688,6 +1690,11 @@ private:
             }
         h2_wake();
     }
+    // The request's header block: the fields that never change for this client (:scheme, :authority,
+    // user-agent, accept) come from a block encoded once, the authorization field from one encoded per token;
+    // only :method, :path and the body's type and length are encoded per request (static-table name indexes,
+    // RFC 7541 Appendix A: 2/3 GET/POST, 4 :path, 6/7 :scheme, 19 accept, 23 authorization, 28 content-length,
+    // 31 content-type, 58 user-agent, 1 :authority).
     void h2_headers_out(h2::Session& s, uint32_t id, const std::string& method, const std::string& target,
                         const std::string* body, const char* content_type) {
         std::string& b = h2_block_;
@@ -1697,25 +1704,33 @@ private:
         else if (method == "POST")
             hpack::encode_indexed(b, 3);
         else
-            hpack::encode_literal(b, ":method", method);
-        hpack::encode_indexed(b, url_.tls ? 7 : 6);  // :scheme
-        hpack::encode_literal(b, ":authority", host_);
-        if (url_.prefix.empty()) {
-            hpack::encode_literal(b, ":path", target);
-        } else {
-            hpack::encode_literal(b, ":path", url_.prefix + target);
+            hpack::encode_literal_indexed_name(b, 2, method);
+        if (h2_fixed_.empty()) {
+            hpack::encode_indexed(h2_fixed_, url_.tls ? 7 : 6);
+            hpack::encode_literal_indexed_name(h2_fixed_, 1, host_);
+            hpack::encode_literal_indexed_name(h2_fixed_, 58, kUserAgent);
+            hpack::encode_literal_indexed_name(h2_fixed_, 19, "application/json");
         }
-        hpack::encode_literal(b, "user-agent", kUserAgent);
-        hpack::encode_literal(b, "accept", "application/json");
+        b += h2_fixed_;
+        if (url_.prefix.empty()) {
+            hpack::encode_literal_indexed_name(b, 4, target);
+        } else {
+            hpack::encode_literal_indexed_name(b, 4, url_.prefix + target);
+        }
         if (body != nullptr) {
-            hpack::encode_literal(b, "content-type", content_type != nullptr ? content_type : "application/json");
+            hpack::encode_literal_indexed_name(b, 31, content_type != nullptr ? content_type : "application/json");
             char num[24];
             auto [end, ec] = std::to_chars(num, num + sizeof num, body->size());
-            hpack::encode_literal(b, "content-length", std::string_view(num, static_cast<size_t>(end - num)));
+            hpack::encode_literal_indexed_name(b, 28, std::string_view(num, static_cast<size_t>(end - num)));
         }
         reload_token(false);
         const std::string& auth = authorization();
-        if (!auth.empty()) hpack::encode_literal(b, "authorization", auth);
+        if (auth != h2_auth_for_) {  // (a token file re-read to a new token)
+            h2_auth_for_ = auth;
+            h2_auth_block_.clear();
+            if (!auth.empty()) hpack::encode_literal_indexed_name(h2_auth_block_, 23, auth);
+        }
+        b += h2_auth_block_;
         bool end_stream = body == nullptr || body->empty();
         size_t off = 0, n = std::min<size_t>(b.size(), s.peer_max_frame);
         bool more = n < b.size();

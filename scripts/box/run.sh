@@ -21,6 +21,7 @@
 #                                                        shard RTT 5/20 ms × jitter 0/10/20 ms, N=1 and 8 shards
 #   bash scripts/box/run.sh <out> http2 [n]              n rounds of: the driver shape over HTTP/1.1 and over HTTP/2
 #                                                        (prior knowledge), then --tls over HTTP/1.1 and HTTP/2 (ALPN)
+#   bash scripts/box/run.sh <out> ranks [N] [pairs]      torchrun with N CPU ranks (N shards), HTTP/1.1 vs HTTP/2
 #   bash scripts/box/run.sh <out> multishard [n]         n rounds of: suite configs 2, 5, 8 with --stages, then
 #                                                        bench.py N=1 and --shards-per-rank 8 --stages
 #
@@ -174,6 +175,21 @@ case "$what" in
       bench_once "$out/h2_$i" NEXUS__CLIENT_HTTP2=on || exit $?
       bench_once "$out/tls_h1_$i" NEXUS__CLIENT_HTTP2=off --tls || exit $?
       bench_once "$out/tls_h2_$i" --tls || exit $?
+    done
+    ;;
+  ranks)  # torchrun over CPU ranks on this box (N shards, one per rank), HTTP/1.1 (a_) and HTTP/2 (b_) alternating
+    n=${1:-2}; pairs=${2:-2}
+    port=29740
+    for i in $(seq 1 "$pairs"); do
+      for arm in a b; do
+        port=$((port + 1))
+        h2=on; [ "$arm" = a ] && h2=off
+        NEXUS__CLIENT_HTTP2=$h2 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+          --master-addr 127.0.0.1 --master-port "$port" bench.py --gpus "$n" --steps 20 --warmup 5 \
+          > "$out/n${n}_${arm}_$i.json" 2> "$out/n${n}_${arm}_$i.err" || exit $?
+        grep -qv 'amdgpu.ids: No such file' "$out/n${n}_${arm}_$i.err" || rm -f "$out/n${n}_${arm}_$i.err"
+        summary "$out/n${n}_${arm}_$i.json"
+      done
     done
     ;;
   multishard)
