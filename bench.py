@@ -787,7 +787,8 @@ async def run(args, d: Dist) -> dict | None:
                     flow = {}
                     for h in (st.get("executors") or {}).values():
                         flow.update((h.get("status") or {}).get("flow") or {})
-                    ctl_debug = {"executor_flow": flow, "coordinator_gc": st.get("gc")}
+                    ctl_debug = {"executor_flow": flow, "coordinator_gc": st.get("gc"),
+                                 "controller_transport": st.get("controller_transport", "n/a")}
                 except Exception as e:  # noqa: BLE001 — diagnostics only
                     ctl_debug = {"error": repr(e)[:200]}
             if d.rank == 0:  # LIST/WATCH load the controller put on its own cluster (watch relay: 1 each per kind)
@@ -883,9 +884,10 @@ async def run(args, d: Dist) -> dict | None:
                            "templates": T, "shards": d.world * S, "mode": args.mode, "payload_bytes": args.payload,
                            "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms,
                            "tls": bool(args.tls),
-                           # what the C++ executors spoke to the shard apiservers (client-http2: HTTP/2 where TLS
-                           # negotiates it, as client-go; the driver's cleartext shape stays on HTTP/1.1)
-                           "shard_transport": _shard_transport(ctl_debug)},
+                           # what the C++ executors spoke to the shard apiservers and the coordinator to the
+                           # controller apiserver (client-http2; bench.py: HTTP/2, prior knowledge on cleartext)
+                           "shard_transport": _shard_transport(ctl_debug),
+                           "controller_transport": (ctl_debug or {}).get("controller_transport", "n/a")},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,
                 "p99_latency_ms": round(pct(lat, 99), 2) if lat else None,
                 "controller_cpu_us_per_object": round(ctl_us, 1),

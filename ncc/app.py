@@ -224,7 +224,8 @@ class App:
         self.per_shard = 1
         qps, burst = client_limits(cfg)
         self.client_factory = client_factory or default_client_factory(qps, burst, cfg.pool_size(),
-                                                                       cfg.transport, cfg.pipeline_depth())
+                                                                       cfg.transport, cfg.pipeline_depth(),
+                                                                       cfg.client_http2)
         self._controller_client = controller_client
         self.metrics = metrics
         self.ops = None
@@ -264,7 +265,7 @@ class App:
         if client is None:
             qps, burst = client_limits(cfg)
             client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.pool_size(),
-                                pipeline_depth=cfg.pipeline_depth(),
+                                pipeline_depth=cfg.pipeline_depth(), http2=cfg.client_http2,
                                 cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)
@@ -437,6 +438,12 @@ class App:
             out["watch_relay"] = dict(self.relay.stats)
         if self.executor_impl:
             out["executor_impl"] = self.executor_impl
+        client = self.client
+        while client is not None and not hasattr(client, "protocol") and hasattr(client, "inner"):
+            client = client.inner  # under a RateLimitedClient
+        proto = getattr(client, "protocol", None)
+        if proto is not None:  # what the coordinator speaks to the controller apiserver (client-http2)
+            out["controller_transport"] = proto
         if self._gc_task is not None:
             out["gc"] = dict(gctune.STATS)
         if self.placement is not None:

@@ -84,8 +84,9 @@ class AppConfig:
                                      # 256 for the C++ executor's shard clients
     client_pipeline_depth: int = 0   # HTTP/1.1-pipelined requests per connection (in flight ≤ pool × depth);
                                      # 0 = auto: 1 (no pipelining)
-    client_http2: str = "auto"       # the C++ executor's shard clients: auto (HTTP/2 where TLS negotiates it by
-                                     # ALPN, as client-go) | on (also prior-knowledge HTTP/2 on cleartext) | off
+    client_http2: str = "auto"       # every client (controller cluster and shards): auto (HTTP/2 where TLS
+                                     # negotiates it by ALPN, as client-go) | on (also prior-knowledge HTTP/2 on
+                                     # cleartext) | off
     transport: str = "fast"          # fast (raw asyncio HTTP/1.1) | aiohttp
     server_side_apply: bool = False  # native mode: write shard objects with server-side apply
     sync_dependent_metadata: bool = False  # native mode: shard Secrets/ConfigMaps carry the source's labels

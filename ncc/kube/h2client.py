@@ -1,0 +1,609 @@
+"""HTTP/2 for the Python clients: the coordinator's connection to the controller cluster (and the Python executor's
+to its shards), as client-go's transport speaks it (`/root/reference/main.go:52-68` builds the clientsets; Go's
+transport negotiates h2 by ALPN and multiplexes a clientset's requests on one connection).
+
+`H2Pool` has `ConnectionPool`'s interface (`request`, `stream`, `close`), so `RestClient` uses either:
+
+* every request is a stream; all streams opened in one loop iteration leave in one write (one TLS record), and
+  a read brings many responses back at once — where HTTP/1.1 needs a connection per request in flight and a
+  system call per request and per response;
+* frames, HPACK and watch-body line splitting are native (`H2ClientParser`, `h2_request` in
+  native/ncc_native.cpp over native/common/hpack.hpp); the policy is here: the server's stream limit (another
+  connection opens only when every one is full), request-body flow control, GOAWAY (streams above its last id
+  are retried on a fresh connection, as REFUSED_STREAM ones are), per-request deadlines, and the watch streams'
+  windows, credited as their consumer takes the lines (the back-pressure `pause_reading` gives HTTP/1.1);
+* negotiation: ALPN "h2" on TLS (`client-http2: auto`, the default), or prior knowledge on cleartext (`on`).
+  A server that does not speak HTTP/2 — ALPN picks http/1.1, or it answers the preface with anything but
+  SETTINGS — makes the pool fall back to HTTP/1.1 (`transport.ConnectionPool`) for good.
+"""
+from __future__ import annotations
+
+import asyncio
+import ssl as _ssl
+import struct
+from collections import deque
+from urllib.parse import urlsplit
+
+from .. import native as _native
+from ..aio import wait_timeout
+from . import errors as E
+from .transport import ConnectionPool, _Response
+
+_mod = _native.load()
+_Parser = getattr(_mod, "H2ClientParser", None) if _mod is not None else None
+_h2_request = getattr(_mod, "h2_request", None) if _mod is not None else None
+_hpack_encode = getattr(_mod, "hpack_encode", None) if _mod is not None else None
+
+AVAILABLE = _Parser is not None
+_BODY_METHODS = frozenset(("POST", "PUT", "PATCH"))
+_NO_BODY = b""
+# RFC 9113 error codes used here
+NO_ERROR, PROTOCOL_ERROR, CANCEL, REFUSED_STREAM = 0x0, 0x1, 0x8, 0x7
+WATCH_CREDIT = 1 << 16  # a watch stream's consumed bytes are credited back in updates of at least this much
+
+
+def _frame(type_: int, flags: int, sid: int, payload: bytes) -> bytes:
+    return struct.pack(">I", len(payload))[1:] + struct.pack(">BBI", type_, flags, sid & 0x7fffffff) + payload
+
+
+def _window_update(sid: int, n: int) -> bytes:
+    return _frame(8, 0, sid, struct.pack(">I", n & 0x7fffffff))
+
+
+def _tap(tap, lines: list) -> None:
+    try:
+        tap(lines)
+    except Exception:  # noqa: BLE001 — a tap must not break the stream its consumer reads
+        import logging
+        logging.getLogger("ncc.transport").exception("watch line tap failed")
+
+
+class _NoH2(Exception):
+    """The server does not speak HTTP/2 on this connection."""
+
+
+class _Retry(Exception):
+    """The server did not process the stream (REFUSED_STREAM, or above a GOAWAY's last id): safe to send again.
+    `refused`: REFUSED_STREAM — the same server is busy, so the retry backs off (a GOAWAY's goes straight to a
+    new connection)."""
+
+    def __init__(self, refused: bool = False):
+        super().__init__()
+        self.refused = refused
+
+
+MAX_UNPROCESSED_RETRIES = 16  # re-sends of a request no server processed (a GOAWAY each time is progress elsewhere)
+
+
+class _Stream:
+    __slots__ = ("sid", "fut", "deadline", "what", "body", "send_window", "watch", "lines", "event", "done",
+                 "tap", "uncredited", "head")
+
+    def __init__(self, sid: int, fut, what: str, send_window: int, watch: bool = False):
+        self.sid, self.fut, self.what, self.send_window, self.watch = sid, fut, what, send_window, watch
+        self.deadline = None
+        self.body = _NO_BODY  # request body still to send (blocked on a flow-control window)
+        self.lines: deque | None = deque() if watch else None
+        self.event: asyncio.Event | None = asyncio.Event() if watch else None
+        self.done = False
+        self.tap = None
+        self.uncredited = 0
+        self.head = None
+
+
+class _H2Conn(asyncio.Protocol):
+    """One HTTP/2 connection: its streams, send windows and the native parser of what the server sends."""
+
+    def __init__(self, pool: "H2Pool"):
+        self.pool = pool
+        self.parser = _Parser()
+        self.transport: asyncio.Transport | None = None
+        self.streams: dict[int, _Stream] = {}
+        self.next_sid = 1
+        self.peer_max_streams = 100  # until the server's SETTINGS say otherwise
+        self.peer_window = 65535     # its SETTINGS_INITIAL_WINDOW_SIZE: each new stream's send window
+        self.peer_max_frame = 16384
+        self.send_window = 65535     # the connection's
+        self.blocked: deque = deque()
+        self.ready = asyncio.get_running_loop().create_future()
+        self.draining = False        # GOAWAY received (or sent): no new streams
+        self.closed = False
+        self._out: list = []
+        self._flush_handle = None
+
+    # ------------------------------------------------------------------ protocol
+    def connection_made(self, transport):
+        self.transport = transport
+        if self.pool.tls:
+            sslobj = transport.get_extra_info("ssl_object")
+            if sslobj is None or sslobj.selected_alpn_protocol() != "h2":
+                self._fail_ready(_NoH2("the server did not negotiate HTTP/2 (ALPN)"))
+                self.closed = True
+                transport.close()
+                return
+        transport.write(_Parser.preface())
+
+    def _fail_ready(self, exc: BaseException) -> None:
+        if not self.ready.done():
+            self.ready.set_exception(exc)
+            self.ready.exception()  # retrieved: a pool that gave up on the connect must not log it
+
+    def connection_lost(self, exc):
+        self.closed = True
+        if self._flush_handle is not None:
+            self._flush_handle.cancel()
+            self._flush_handle = None
+        if not self.ready.done():
+            # closed before its SETTINGS: on cleartext with prior knowledge, an HTTP/1.1 server hanging up on the
+            # preface; on TLS (ALPN said h2) a plain failure
+            self._fail_ready(_NoH2("closed before SETTINGS") if not self.pool.tls else
+                             E.TransportError(f"connection lost: {exc or 'closed by peer'}"))
+        err = E.TransportError(f"connection lost: {exc or 'closed by peer'}")
+        for st in list(self.streams.values()):
+            self._end(st, err)
+        self.streams.clear()
+        self.blocked.clear()
+        self.pool._discard(self)
+
+    def pause_writing(self):  # pragma: no cover - large request bodies only
+        pass
+
+    def resume_writing(self):  # pragma: no cover
+        pass
+
+    def data_received(self, data: bytes):
+        events, out = self.parser.feed(data)
+        if out:
+            self._send(out)
+        streams = self.streams
+        for ev in events:
+            kind = ev[0]
+            if kind == "resp":
+                st = streams.pop(ev[1], None)
+                if st is not None:
+                    if not st.fut.done():
+                        st.fut.set_result(_Response(ev[2], _NO_HEADERS if ev[3] is None else {"retry-after": ev[3]},
+                                                    ev[4]))
+                    self.pool._stream_closed(self)
+            elif kind == "lines":
+                st = streams.get(ev[1])
+                if st is None:
+                    continue
+                lines = ev[2]
+                if lines:
+                    if st.tap is not None:
+                        _tap(st.tap, lines)
+                    st.lines.extend(lines)
+                if st.tap is not None:
+                    if ev[3]:
+                        self._send(_window_update(st.sid, ev[3]))  # a tapped stream is read as it arrives
+                else:
+                    st.uncredited += ev[3]
+                if ev[4]:
+                    st.done = True
+                    del streams[st.sid]
+                    self.pool._stream_closed(self)
+                st.event.set()
+            elif kind == "head":
+                st = streams.get(ev[1])
+                if st is not None and not st.fut.done():
+                    st.head = _Response(ev[2], _NO_HEADERS if ev[3] is None else {"retry-after": ev[3]}, b"")
+                    st.fut.set_result(st.head)
+            elif kind == "settings":
+                self._settings(ev[1])
+            elif kind == "window":
+                self._window(ev[1], ev[2])
+            elif kind == "rst":
+                st = streams.pop(ev[1], None)
+                if st is not None:
+                    self._end(st, _Retry(True) if ev[2] == REFUSED_STREAM else
+                              E.TransportError(f"{st.what}: stream reset by the server (code {ev[2]})"))
+                    if ev[2] == REFUSED_STREAM:
+                        self.pool.stats["h2_refused"] += 1
+                    self.pool._stream_closed(self)
+            elif kind == "goaway":
+                self._goaway(ev[1], ev[2])
+            elif kind == "noh2":
+                self._fail_ready(_NoH2("the server answered the HTTP/2 preface with something else"))
+                self.close()
+                return
+            elif kind == "error":
+                self._send(_frame(7, 0, 0, struct.pack(">II", 0, ev[1]) + ev[2].encode()[:200]))
+                self._flush()
+                err = E.TransportError(f"HTTP/2 connection error: {ev[2]}")
+                self._fail_ready(err)
+                for st in list(streams.values()):
+                    self._end(st, err)
+                streams.clear()
+                self.close()
+                return
+
+    # ------------------------------------------------------------------ frames in
+    def _settings(self, kv) -> None:
+        for k, v in kv:
+            if k == 0x3:
+                self.peer_max_streams = v
+            elif k == 0x4:
+                delta = v - self.peer_window
+                self.peer_window = v
+                for st in self.streams.values():
+                    st.send_window += delta
+            elif k == 0x5:
+                self.peer_max_frame = v
+        if not self.ready.done():
+            self.ready.set_result(None)
+        self._drain_blocked()
+        self.pool._stream_closed(self)  # a raised stream limit is room for waiters
+
+    def _window(self, sid: int, n: int) -> None:
+        if sid == 0:
+            self.send_window += n
+        else:
+            st = self.streams.get(sid)
+            if st is None:
+                return
+            st.send_window += n
+        self._drain_blocked()
+
+    def _goaway(self, last: int, code: int) -> None:
+        self.draining = True
+        self.pool.stats["h2_goaways"] += 1
+        for sid in [s for s in self.streams if s > last]:
+            st = self.streams.pop(sid)
+            self._end(st, _Retry())
+        if not self.streams:
+            self.close()
+        self.pool._stream_closed(self)
+
+    def _end(self, st: _Stream, exc: BaseException) -> None:
+        if st.watch:
+            st.done = True
+            if not st.fut.done():
+                st.fut.set_exception(exc if not isinstance(exc, _Retry) else
+                                     E.TransportError(f"{st.what}: refused by the server"))
+            st.event.set()
+        elif not st.fut.done():
+            st.fut.set_exception(exc)
+
+    # ------------------------------------------------------------------ frames out
+    def _send(self, data: bytes) -> None:
+        self._out.append(data)
+        if self._flush_handle is None:
+            self._flush_handle = asyncio.get_running_loop().call_soon(self._flush)
+
+    def _flush(self) -> None:
+        self._flush_handle = None
+        out, self._out = self._out, []
+        if out and not self.closed and self.transport is not None:
+            self.transport.write(out[0] if len(out) == 1 else b"".join(out))
+
+    def has_room(self) -> bool:
+        return not self.closed and not self.draining and len(self.streams) < self.peer_max_streams
+
+    def open(self, method: str, target: str, fixed: bytes, clen: int, body: bytes, what: str,
+             watch: bool = False) -> _Stream:
+        sid = self.next_sid
+        self.next_sid += 2
+        fut = asyncio.get_running_loop().create_future()
+        st = _Stream(sid, fut, what, self.peer_window, watch)
+        self.streams[sid] = st
+        if watch:
+            self.parser.watch(sid)
+        n = len(body)
+        if n <= st.send_window and n <= self.send_window:
+            data = _h2_request(sid, method, target, fixed, clen, body, True, self.peer_max_frame)
+            if len(self.streams) == 1 and not self._out and self.transport is not None:
+                # the only stream in flight: out now (batching would cost it a loop iteration and gain nothing)
+                self.transport.write(data)
+            else:
+                self._send(data)
+            st.send_window -= n
+            self.send_window -= n
+        else:  # the body waits for WINDOW_UPDATEs
+            self._send(_h2_request(sid, method, target, fixed, clen, _NO_BODY, False, self.peer_max_frame))
+            st.body = body
+            self.blocked.append(st)
+            self._drain_blocked()
+        self.pool.stats["h2_streams"] += 1
+        return st
+
+    def _drain_blocked(self) -> None:
+        while self.blocked and self.send_window > 0:
+            st = self.blocked[0]
+            if st.done or self.streams.get(st.sid) is not st:
+                self.blocked.popleft()
+                continue
+            room = min(st.send_window, self.send_window)
+            if room <= 0:
+                # this stream waits for its own window; others behind it may not
+                self.blocked.rotate(-1)
+                if all(s.send_window <= 0 for s in self.blocked):
+                    return
+                continue
+            n = min(room, len(st.body), self.peer_max_frame)
+            chunk, st.body = st.body[:n], st.body[n:]
+            st.send_window -= n
+            self.send_window -= n
+            last = not st.body
+            self._send(_frame(0, 0x1 if last else 0, st.sid, chunk))
+            if last:
+                self.blocked.popleft()
+
+    def cancel(self, st: _Stream) -> None:
+        """Reset a stream the client gives up on (a deadline, a closed watch)."""
+        if self.streams.pop(st.sid, None) is not None:
+            self.parser.forget(st.sid)
+            self._send(_frame(3, 0, st.sid, struct.pack(">I", CANCEL)))
+            self.pool._stream_closed(self)
+
+    def credit(self, st: _Stream) -> None:
+        if st.uncredited >= WATCH_CREDIT and not st.done:
+            self._send(_window_update(st.sid, st.uncredited))
+            st.uncredited = 0
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            if self.transport is not None:
+                if self._out:
+                    self._flush()
+                self.transport.close()
+
+
+_NO_HEADERS: dict = {}
+
+
+class H2Pool:
+    """HTTP/2 connections to one apiserver, `ConnectionPool`'s interface.  `prior_knowledge`: speak HTTP/2 on
+    cleartext without negotiation (TLS always negotiates by ALPN)."""
+
+    SWEEP_PERIOD = 0.5
+
+    def __init__(self, server: str, *, ssl_context: _ssl.SSLContext | None = None, server_hostname: str | None = None,
+                 max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1,
+                 prior_knowledge: bool = False):
+        if not AVAILABLE:
+            raise RuntimeError("HTTP/2 needs the native extension (ncc/_native)")
+        u = urlsplit(server)
+        self.server = server
+        self.host = u.hostname or "127.0.0.1"
+        self.port = u.port or (443 if u.scheme == "https" else 80)
+        self.authority = u.netloc
+        self.tls = u.scheme == "https"
+        self.ssl = ssl_context if self.tls else None
+        if self.ssl is not None:
+            self.ssl.set_alpn_protocols(["h2", "http/1.1"])
+        self.server_hostname = server_hostname
+        self.max_size = max(1, max_size)
+        self.connect_timeout = connect_timeout
+        self.pipeline_depth = pipeline_depth
+        self.prior_knowledge = prior_knowledge
+        self.conns: list[_H2Conn] = []
+        self._connecting: asyncio.Future | None = None
+        self._waiters: deque = deque()
+        self._fixed: dict = {}
+        self._sweep_handle = None
+        self.fallback: ConnectionPool | None = None
+        self.opened = 0
+        self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0}
+
+    @property
+    def protocol(self) -> str:
+        return "http/1.1" if self.fallback is not None else "h2"
+
+    # ------------------------------------------------------------------ connections
+    async def _connect(self) -> _H2Conn:
+        loop = asyncio.get_running_loop()
+        kw = {}
+        if self.ssl is not None:
+            kw["ssl"] = self.ssl
+            kw["server_hostname"] = self.server_hostname or self.host
+        try:
+            _, conn = await wait_timeout(
+                loop.create_connection(lambda: _H2Conn(self), self.host, self.port, **kw), self.connect_timeout)
+        except (OSError, asyncio.TimeoutError, _ssl.SSLError) as e:
+            raise E.TransportError(f"connect {self.host}:{self.port}: {type(e).__name__}: {e}") from e
+        try:
+            await wait_timeout(asyncio.shield(conn.ready), self.connect_timeout)
+        except asyncio.TimeoutError as e:
+            conn.close()
+            raise (_NoH2("no SETTINGS from the server") if not self.tls else
+                   E.TransportError(f"connect {self.host}:{self.port}: no HTTP/2 SETTINGS")) from e
+        self.opened += 1
+        self.conns.append(conn)
+        return conn
+
+    def _h1(self) -> ConnectionPool:
+        if self.fallback is None:
+            self.fallback = ConnectionPool(self.server, ssl_context=self.ssl, server_hostname=self.server_hostname,
+                                           max_size=self.max_size, connect_timeout=self.connect_timeout,
+                                           pipeline_depth=self.pipeline_depth)
+        return self.fallback
+
+    def _pick(self) -> _H2Conn | None:
+        for c in self.conns:
+            if c.has_room():
+                return c
+        return None
+
+    async def _conn(self) -> _H2Conn | None:
+        """A connection with room for a stream; None once the server turned out not to speak HTTP/2."""
+        while True:
+            c = self._pick()
+            if c is not None:
+                return c
+            if self.fallback is not None:
+                return None
+            if self._connecting is not None:
+                await asyncio.shield(self._connecting)  # one connect at a time; then look again
+                continue
+            if len([c for c in self.conns if not c.closed]) < self.max_size:
+                fut = self._connecting = asyncio.get_running_loop().create_future()
+                try:
+                    return await self._connect()
+                except _NoH2:
+                    if self.opened == 0:
+                        self._h1()  # this server speaks HTTP/1.1 only: from now on, every request goes there
+                        return None
+                    raise E.TransportError(f"connect {self.host}:{self.port}: HTTP/2 no longer offered")
+                finally:
+                    self._connecting = None
+                    fut.set_result(None)
+            w = asyncio.get_running_loop().create_future()
+            self._waiters.append(w)
+            await w
+
+    def _stream_closed(self, c: _H2Conn) -> None:
+        """Room on `c` (or `c` gone): wake as many waiters as it has free streams; they pick again."""
+        if not self._waiters:
+            return
+        free = c.peer_max_streams - len(c.streams) if c.has_room() else (1 if c.closed or c.draining else 0)
+        while self._waiters and free > 0:
+            w = self._waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+                free -= 1
+
+    def _discard(self, c: _H2Conn) -> None:
+        try:
+            self.conns.remove(c)
+        except ValueError:
+            pass
+        while self._waiters:  # let them connect afresh
+            w = self._waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+
+    def _fixed_block(self, headers: dict, block: bytes | None) -> bytes:
+        key = block if block is not None else tuple(headers.items())
+        got = self._fixed.get(key)
+        if got is None:
+            if len(self._fixed) > 16:
+                self._fixed.clear()
+            fields = [(":scheme", "https" if self.tls else "http"), (":authority", headers.get("Host", self.authority))]
+            fields += [(k.lower(), str(v)) for k, v in headers.items() if k.lower() not in ("host", "connection")]
+            got = self._fixed[key] = _hpack_encode(fields)
+        return got
+
+    # ------------------------------------------------------------------ deadlines
+    def _arm_sweep(self) -> None:
+        if self._sweep_handle is None:
+            self._sweep_handle = asyncio.get_running_loop().call_later(self.SWEEP_PERIOD, self._sweep)
+
+    def _sweep(self) -> None:
+        self._sweep_handle = None
+        now = asyncio.get_running_loop().time()
+        pending = False
+        for c in list(self.conns):
+            for st in [s for s in c.streams.values() if s.deadline is not None]:
+                if st.deadline <= now:
+                    c.cancel(st)
+                    c._end(st, E.TransportError(f"{st.what}: timed out"))
+                else:
+                    pending = True
+        if pending:
+            self._arm_sweep()
+
+    # ------------------------------------------------------------------ API
+    async def request(self, method: str, target: str, headers: dict, body: bytes | None,
+                      timeout: float | None = 30.0, block: bytes | None = None) -> _Response:
+        if self.fallback is not None:
+            return await self.fallback.request(method, target, headers, body, timeout=timeout, block=block)
+        fixed = self._fixed_block(headers, block)
+        clen = len(body) if body is not None else (0 if method in _BODY_METHODS else -1)
+        what = f"{method} {target}"
+        for attempt in range(MAX_UNPROCESSED_RETRIES + 1):
+            c = self._pick() or await self._conn()
+            if c is None:
+                return await self.fallback.request(method, target, headers, body, timeout=timeout, block=block)
+            st = c.open(method, target, fixed, clen, body or _NO_BODY, what)
+            if timeout:
+                st.deadline = asyncio.get_running_loop().time() + timeout
+                self._arm_sweep()
+            try:
+                return await st.fut
+            except _Retry as r:
+                if attempt < MAX_UNPROCESSED_RETRIES:
+                    if r.refused:
+                        await asyncio.sleep(min(0.001 * (2 ** attempt), 0.1))
+                    continue
+                raise E.TransportError(f"{what}: refused by the server") from None
+            except asyncio.CancelledError:
+                c.cancel(st)
+                raise
+        raise E.TransportError("unreachable")  # pragma: no cover
+
+    async def stream(self, target: str, headers: dict, timeout: float | None = None, batch: bool = False,
+                     on_lines=None):
+        """`ConnectionPool.stream` over a stream of a shared connection: yields (response, None) — or (response,
+        error body) for a non-2xx — then (None, line) or, with `batch`, (None, [lines])."""
+        if self.fallback is None:
+            c = self._pick() or await self._conn()
+        else:
+            c = None
+        if c is None:
+            async for x in self.fallback.stream(target, headers, timeout=timeout, batch=batch, on_lines=on_lines):
+                yield x
+            return
+        loop = asyncio.get_running_loop()
+        st = c.open("GET", target, self._fixed_block(headers, None), -1, _NO_BODY, f"GET {target}", watch=True)
+        st.deadline = loop.time() + self.connect_timeout + 20  # for the response head
+        self._arm_sweep()
+        stream_timer = None
+        try:
+            resp = await st.fut
+            st.deadline = None
+            if timeout:
+                stream_timer = loop.call_later(timeout, self._end_watch, c, st)
+            if resp.status >= 300:
+                while not st.done:
+                    st.event.clear()
+                    await st.event.wait()
+                yield resp, b"\n".join(st.lines)
+                return
+            if on_lines is not None:
+                if st.lines:
+                    on_lines(list(st.lines))
+                st.tap = on_lines
+                if st.uncredited:
+                    c._send(_window_update(st.sid, st.uncredited))
+                    st.uncredited = 0
+            yield resp, None
+            while True:
+                if batch:
+                    while st.lines:
+                        lines = list(st.lines)
+                        st.lines.clear()
+                        c.credit(st)
+                        yield None, lines
+                else:
+                    while st.lines:
+                        yield None, st.lines.popleft()
+                        c.credit(st)
+                if st.done:
+                    return
+                st.event.clear()
+                await st.event.wait()
+        finally:
+            if stream_timer is not None:
+                stream_timer.cancel()
+            if not st.done:
+                c.cancel(st)
+                st.done = True
+
+    @staticmethod
+    def _end_watch(c: _H2Conn, st: _Stream) -> None:
+        if not st.done:
+            c.cancel(st)
+            st.done = True
+            st.event.set()
+
+    def close(self) -> None:
+        if self._sweep_handle is not None:
+            self._sweep_handle.cancel()
+            self._sweep_handle = None
+        for c in list(self.conns):
+            c.close()
+        self.conns.clear()
+        if self.fallback is not None:
+            self.fallback.close()

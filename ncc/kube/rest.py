@@ -41,6 +41,7 @@ from .. import native as _native
 from ..api.jsonenc import dumps_bytes, loads_fast
 from ..api.resources import ResourceType
 from . import errors as E
+from . import h2client
 from .client import PATCH_MERGE, KubeClient, WatchEvent
 from .kubeconfig import ClusterConfig, CredentialSource
 from .transport import ConnectionPool
@@ -98,10 +99,13 @@ _members_equal = getattr(_native.load(), "members_equal", None)
 class RestClient(KubeClient):
     def __init__(self, cfg: ClusterConfig, *, pool_size: int = 64, request_timeout: float = 30.0,
                  max_retries: int = 5, cluster_name: str | None = None, transport: str = "fast",
-                 pipeline_depth: int = 1):
+                 pipeline_depth: int = 1, http2: str = "auto"):
         if transport not in ("fast", "aiohttp"):
             raise ValueError(f"unknown transport {transport!r}")
+        if http2 not in ("off", "auto", "on"):
+            raise ValueError(f"unknown http2 mode {http2!r}")
         self.transport = transport
+        self.http2 = http2
         self._pool: ConnectionPool | None = None
         self.cfg = cfg
         self.cluster_name = cluster_name or cfg.name or cfg.server
@@ -135,11 +139,24 @@ class RestClient(KubeClient):
                 if self._pool is None:
                     exec_cert = await self.creds.exec_client_cert()
                     ctx = _ssl_context(self.cfg, exec_cert)
-                    self._pool = ConnectionPool(self.cfg.server, ssl_context=ctx or None,
-                                                server_hostname=self.cfg.tls_server_name, max_size=self.pool_size,
-                                                connect_timeout=self.request_timeout,
-                                                pipeline_depth=self.pipeline_depth)
+                    kw = dict(ssl_context=ctx or None, server_hostname=self.cfg.tls_server_name,
+                              max_size=self.pool_size, connect_timeout=self.request_timeout,
+                              pipeline_depth=self.pipeline_depth)
+                    tls = self.cfg.server.startswith("https:")
+                    if h2client.AVAILABLE and (self.http2 == "on" or (self.http2 == "auto" and tls)):
+                        # client-go's transport: HTTP/2 negotiated by ALPN (prior knowledge on cleartext with "on")
+                        self._pool = h2client.H2Pool(self.cfg.server, prior_knowledge=self.http2 == "on", **kw)
+                    else:
+                        self._pool = ConnectionPool(self.cfg.server, **kw)
         return self._pool
+
+    @property
+    def protocol(self) -> str | None:
+        """"h2" or "http/1.1" once the first connection is made (None before, or with the aiohttp transport)."""
+        pool = self._pool
+        if pool is None:
+            return None
+        return pool.protocol if isinstance(pool, h2client.H2Pool) else "http/1.1"
 
     async def _send(self, method: str, target: str, headers: dict, data, block: bytes | None = None):
         """One HTTP exchange → (status, raw body, Retry-After header or None).  `block` is the pre-rendered

@@ -39,10 +39,11 @@ def discover(shard_config_path: str) -> list[tuple[str, str]]:
 
 
 def default_client_factory(qps: float = 0.0, burst: int = 10, pool_size: int = 64,
-                           transport: str = "fast", pipeline_depth: int = 1) -> Callable[[str, str], KubeClient]:
+                           transport: str = "fast", pipeline_depth: int = 1,
+                           http2: str = "auto") -> Callable[[str, str], KubeClient]:
     def make(name: str, path: str) -> KubeClient:
         client: KubeClient = RestClient(load_kubeconfig(path, name=name), pool_size=pool_size, cluster_name=name,
-                                        transport=transport, pipeline_depth=pipeline_depth)
+                                        transport=transport, pipeline_depth=pipeline_depth, http2=http2)
         if qps > 0:
             client = RateLimitedClient(client, qps, burst)
         return client

@@ -50,7 +50,7 @@ print(sys.argv[1].split("/")[-1], d["value"], "p50", d["p50_latency_ms"], "p99",
       "held", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("increases_held"),
       "h2", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("http2"),
       "conns", ((d.get("controller_state") or {}).get("executor_flow") or {}).get("shard-0", {}).get("connections"),
-      flush=True)
+      "ctl", (d.get("config") or {}).get("controller_transport"), flush=True)
 EOF
 }
 
@@ -121,9 +121,9 @@ case "$what" in
       || { tail -30 "$out/suite.log"; exit 1; }
     cut -c 1-300 "$out/suite.log" | tail -14
     ;;
-  sample)  # the C++ executor's and the coordinator's sampling profiles over a long driver-shape run
+  sample)  # the C++ executor's and the coordinator's sampling profiles over a long driver-shape run (args: steps, bench flags)
     NCC_SAMPLE_PROFILE="$PWD/$out/samples" NCC_SAMPLE_US=200 NCC_PY_SAMPLE="$PWD/$out/py" NCC_PY_SAMPLE_US=200 \
-      timeout -k 10 600 python3 bench.py --steps "${1:-100}" --warmup 5 > "$out/sampled_bench.json" \
+      timeout -k 10 600 python3 bench.py --steps "${1:-100}" --warmup 5 "${@:2}" > "$out/sampled_bench.json" \
       2> "$out/sampled_bench.err" || exit $?
     python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
     summary "$out/sampled_bench.json"
@@ -166,6 +166,16 @@ case "$what" in
           done
         done
       done
+    done
+    ;;
+  coord)  # the coordinator's transport to the controller apiserver: HTTP/1.1 (a_) vs HTTP/2 (b_), executors on
+           # HTTP/2 in both arms; cleartext and TLS (tls_a_, tls_b_)
+    n=${1:-2}
+    for i in $(seq 1 "$n"); do
+      bench_once "$out/a_$i" NCC_HTTP2=2 NEXUS__CLIENT_HTTP2=off || exit $?
+      bench_once "$out/b_$i" NCC_HTTP2=2 NEXUS__CLIENT_HTTP2=on || exit $?
+      bench_once "$out/tls_a_$i" NCC_HTTP2=1 NEXUS__CLIENT_HTTP2=off --tls || exit $?
+      bench_once "$out/tls_b_$i" NCC_HTTP2=1 NEXUS__CLIENT_HTTP2=auto --tls || exit $?
     done
     ;;
   http2)
