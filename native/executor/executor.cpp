@@ -2582,10 +2582,10 @@ static void send_status() {
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
         // connections, write batches, requests, slow starts left on rising latency, increases held back, the
         // executor loop's wake-ups and coalesced wake-ups (process-wide), and HTTP/2: in use (0/1), streams
-        // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received]
+        // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received, connections dropped for an unanswered PING]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(19);
+        e.array(20);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2605,6 +2605,7 @@ static void send_status() {
         e.integer(cl.h2_streams);
         e.integer(cl.h2_refused);
         e.integer(cl.h2_goaways);
+        e.integer(cl.h2_dead);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

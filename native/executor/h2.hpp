@@ -112,6 +112,8 @@ struct Session {
     uint32_t peer_max_streams = 100;  // until the server's SETTINGS say otherwise
     int64_t conn_recv_unacked = 0;
     hpack::Decoder dec{4096};
+    double last_read = 0;  // when bytes last arrived (liveness: Client::sweep PINGs a connection silent too long)
+    double ping_sent = 0;  // an unanswered PING's send time, 0 = none
     uint32_t cont_id = 0;  // the stream whose header block continues in CONTINUATION frames
     bool cont_end_stream = false;
     std::string cont_block;
@@ -139,6 +141,10 @@ struct Session {
         std::string p;
         put32(p, code);
         put_frame(out, RST_STREAM, 0, id, p.data(), p.size());
+    }
+    void ping(double now) {
+        ping_sent = now;
+        put_frame(out, PING, 0, 0, "ncc-live", 8);
     }
     void window_update(uint32_t id, int64_t n) {
         std::string p;

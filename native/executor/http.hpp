@@ -693,6 +693,13 @@ public:
         reload_token(true);
         h2_mode_ = http2;
         h2_ok_ = http2 == 2 || (http2 == 1 && url_.tls);
+        // client-go's HTTP/2 health check, same variables and defaults: a connection with streams open that read
+        // nothing for READ_IDLE s (or whose stream just timed out) gets a PING; no answer in PING_TIMEOUT s and it
+        // is closed, its requests re-sent and its watches restarted on a new one
+        if (const char* v = std::getenv("HTTP2_READ_IDLE_TIMEOUT_SECONDS"); v != nullptr && std::atof(v) > 0)
+            h2_read_idle_ = std::atof(v);
+        if (const char* v = std::getenv("HTTP2_PING_TIMEOUT_SECONDS"); v != nullptr && std::atof(v) > 0)
+            h2_ping_timeout_ = std::atof(v);
     }
     ~Client() {
         closed_ = true;
@@ -716,6 +723,7 @@ public:
     }
     bool http2() const { return use_h2(); }  // requests go over HTTP/2 (negotiated, or prior knowledge)
     long long h2_streams = 0, h2_refused = 0, h2_goaways = 0;  // streams opened; re-sent after REFUSED/GOAWAY
+    long long h2_dead = 0;  // connections closed for an unanswered PING
     long long sends = 0;  // write batches (requests issued in one loop iteration go out together)
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
@@ -853,6 +861,7 @@ private:
     ConnSet busy_;
     int h2_mode_ = 0;     // client-http2: 0 off, 1 auto (ALPN on TLS), 2 on (prior knowledge on cleartext too)
     bool h2_ok_ = false;  // requests go over HTTP/2 (false again when the server does not negotiate it)
+    double h2_read_idle_ = 30, h2_ping_timeout_ = 15;  // the liveness check (see the constructor)
     std::vector<h2::SessionPtr> h2s_;                 // HTTP/2 connections, oldest first
     std::deque<std::coroutine_handle<>> h2_waiters_;  // requests waiting for stream room on one of them
     std::string h2_block_;                            // scratch: the header block being encoded
@@ -1389,6 +1398,7 @@ private:
         }
         if (s->broken) co_return;
         s->connected = true;
+        s->last_read = now_s();
         s->c.deadline = 0;  // streams carry their own deadlines
         h2_kick(s);
         s->reading = true;
@@ -1449,6 +1459,7 @@ private:
                 }
                 h2_kick(s);  // acks, window updates and request bodies the frames released
                 co_await c.fill();
+                s->last_read = now_s();
             }
         } catch (const NoH2& e) {
             h2_ok_ = false;  // this request and every later one over HTTP/1.1
@@ -1895,9 +1906,10 @@ private:
             double now = now_s();
             for (Conn* c : busy_.snapshot())
                 if (c->deadline > 0 && now >= c->deadline) c->abort();
-            // HTTP/2: an overdue stream is cancelled alone; its connection carries on
+            // HTTP/2: an overdue stream is cancelled alone; its connection carries on unless it stopped answering
             std::vector<h2::SessionPtr> sessions = h2s_;
             for (auto& s : sessions) {
+                if (!s->connected || s->broken) continue;
                 std::vector<h2::Stream*> late;
                 for (auto& kv : s->streams)
                     if (now >= kv.second->deadline) late.push_back(kv.second);
@@ -1907,7 +1919,16 @@ private:
                     s->rst(st->id, h2::CANCEL);
                     h2_complete(*s, st, false);
                 }
-                if (!late.empty()) h2_kick(s);
+                if (s->ping_sent > 0 && s->last_read >= s->ping_sent) s->ping_sent = 0;  // anything read answers it
+                if (s->ping_sent > 0 && now - s->ping_sent >= h2_ping_timeout_) {
+                    ++h2_dead;
+                    h2_break(s, "HTTP/2: no answer to PING within " + std::to_string(static_cast<int>(h2_ping_timeout_)) +
+                                    " s", false);
+                    continue;
+                }
+                if (s->ping_sent == 0 && !s->streams.empty() && (!late.empty() || now - s->last_read >= h2_read_idle_))
+                    s->ping(now);
+                if (!late.empty() || s->ping_sent == now) h2_kick(s);
             }
         }
         sweeping_ = false;

@@ -19,6 +19,7 @@ transport negotiates h2 by ALPN and multiplexes a clientset's requests on one co
 from __future__ import annotations
 
 import asyncio
+import os
 import ssl as _ssl
 import struct
 from collections import deque
@@ -106,7 +107,10 @@ class _H2Conn(asyncio.Protocol):
         self.send_window = 65535     # the connection's
         self.blocked: deque = deque()
         self.ready = asyncio.get_running_loop().create_future()
+        self.last_recv = asyncio.get_running_loop().time()
+        self.ping_sent = 0.0         # loop time of an unanswered PING (liveness check), 0 = none
         self.draining = False        # GOAWAY received (or sent): no new streams
+        self.lost_why = "closed by peer"
         self.closed = False
         self._out: list = []
         self._flush_handle = None
@@ -138,7 +142,7 @@ class _H2Conn(asyncio.Protocol):
             # preface; on TLS (ALPN said h2) a plain failure
             self._fail_ready(_NoH2("closed before SETTINGS") if not self.pool.tls else
                              E.TransportError(f"connection lost: {exc or 'closed by peer'}"))
-        err = E.TransportError(f"connection lost: {exc or 'closed by peer'}")
+        err = E.TransportError(f"connection lost: {exc or self.lost_why}")
         for st in list(self.streams.values()):
             self._end(st, err)
         self.streams.clear()
@@ -152,6 +156,7 @@ class _H2Conn(asyncio.Protocol):
         pass
 
     def data_received(self, data: bytes):
+        self.last_recv = self.pool._now()
         events, out = self.parser.feed(data)
         if out:
             self._send(out)
@@ -305,6 +310,7 @@ class _H2Conn(asyncio.Protocol):
             self.blocked.append(st)
             self._drain_blocked()
         self.pool.stats["h2_streams"] += 1
+        self.pool._arm_sweep()
         return st
 
     def _drain_blocked(self) -> None:
@@ -336,6 +342,10 @@ class _H2Conn(asyncio.Protocol):
             self._send(_frame(3, 0, st.sid, struct.pack(">I", CANCEL)))
             self.pool._stream_closed(self)
 
+    def ping(self, now: float) -> None:
+        self.ping_sent = now
+        self._send(_frame(6, 0, 0, b"ncc-live"))
+
     def credit(self, st: _Stream) -> None:
         if st.uncredited >= WATCH_CREDIT and not st.done:
             self._send(_window_update(st.sid, st.uncredited))
@@ -348,6 +358,13 @@ class _H2Conn(asyncio.Protocol):
                 if self._out:
                     self._flush()
                 self.transport.close()
+
+    def abort(self, why: str) -> None:
+        """Drop a dead connection at once (close() would wait for its send buffer to drain)."""
+        self.lost_why = why
+        self.closed = True
+        if self.transport is not None:
+            self.transport.abort()
 
 
 _NO_HEADERS: dict = {}
@@ -385,7 +402,12 @@ class H2Pool:
         self._sweep_handle = None
         self.fallback: ConnectionPool | None = None
         self.opened = 0
-        self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0}
+        # liveness, as client-go's transport: a connection with streams open that read nothing for READ_IDLE
+        # seconds (or whose stream just timed out) is PINGed, and closed when PING_TIMEOUT passes without an
+        # answer — a silently dead TCP connection would otherwise hold every stream until the kernel gives up
+        self.read_idle = float(os.environ.get("HTTP2_READ_IDLE_TIMEOUT_SECONDS", "30") or 30)
+        self.ping_timeout = float(os.environ.get("HTTP2_PING_TIMEOUT_SECONDS", "15") or 15)
+        self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0, "h2_dead": 0}
 
     @property
     def protocol(self) -> str:
@@ -490,17 +512,35 @@ class H2Pool:
         if self._sweep_handle is None:
             self._sweep_handle = asyncio.get_running_loop().call_later(self.SWEEP_PERIOD, self._sweep)
 
+    @staticmethod
+    def _now() -> float:
+        return asyncio.get_running_loop().time()
+
     def _sweep(self) -> None:
+        """Every SWEEP_PERIOD while streams are open: request deadlines and connection liveness."""
         self._sweep_handle = None
-        now = asyncio.get_running_loop().time()
+        now = self._now()
         pending = False
         for c in list(self.conns):
-            for st in [s for s in c.streams.values() if s.deadline is not None]:
-                if st.deadline <= now:
-                    c.cancel(st)
-                    c._end(st, E.TransportError(f"{st.what}: timed out"))
-                else:
-                    pending = True
+            late = False
+            for st in [s for s in c.streams.values() if s.deadline is not None and s.deadline <= now]:
+                c.cancel(st)
+                c._end(st, E.TransportError(f"{st.what}: timed out"))
+                late = True
+            if c.ping_sent and c.last_recv >= c.ping_sent:
+                c.ping_sent = 0.0  # anything read since the PING answers it
+            if c.ping_sent and now - c.ping_sent >= self.ping_timeout:
+                self.stats["h2_dead"] += 1
+                import logging
+                logging.getLogger("ncc.transport").warning(
+                    "HTTP/2 connection to %s:%s: no answer to PING within %.0f s; closing it", self.host, self.port,
+                    self.ping_timeout)
+                c.abort("no answer to PING")  # its streams fail; requests and watches start over on a new one
+                continue
+            if c.streams:
+                pending = True
+                if not c.ping_sent and (late or now - c.last_recv >= self.read_idle):
+                    c.ping(now)
         if pending:
             self._arm_sweep()
 

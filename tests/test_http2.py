@@ -356,3 +356,38 @@ def test_server_parser_assembles_streams_from_any_framing():
         got += resp[off + 9:off + 9 + n]
         off += 9 + n
     assert got == b"x" * 40000 and flags == [0, 0, h2.END_STREAM]
+
+
+async def test_a_silent_shard_connection_is_pinged_and_replaced(tmp_path, native_only, monkeypatch):
+    """The C++ executor's HTTP/2 health check (client-go's HTTP2_READ_IDLE_TIMEOUT_SECONDS and
+    HTTP2_PING_TIMEOUT_SECONDS): the path to shard-0 goes silent mid-run — bytes swallowed both ways, sockets
+    open. Without the check the next writes would wait out their 30 s deadline and be re-sent on the same dead
+    connection; with it the connection is PINGed, dropped, and the writes and watches move to a new one."""
+    from test_http2_client import Blackhole
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    monkeypatch.setenv("HTTP2_READ_IDLE_TIMEOUT_SECONDS", "1")
+    monkeypatch.setenv("HTTP2_PING_TIMEOUT_SECONDS", "1")
+    async with Cluster(tmp_path, "native", n_shards=1, client_http2="on", executors_per_shard=1) as cl:
+        bh = Blackhole(int(cl.env.shard_servers[0].url.rsplit(":", 1)[1]))
+        purl = await bh.start()
+        with open(os.path.join(cl.env.shard_dir, "shard-0.kubeconfig"), "w") as f:
+            f.write(cl.env.kubeconfig(purl, "shard-0"))
+        try:
+            n = 5
+            for i in range(n):
+                cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+            await cl.start()
+            await _converge(cl, n)
+            bh.freeze()
+            t0 = asyncio.get_running_loop().time()
+            for i in range(n):
+                await mutate(cl.cc, R.TEMPLATES, f"algo-{i:05d}",
+                             lambda o: o["spec"]["container"].__setitem__("versionTag", "after"))
+            await _converge(cl, n, "after")
+            assert asyncio.get_running_loop().time() - t0 < 15
+
+            async def dropped():
+                return _flow(cl).get("shard-0", {}).get("h2_dead", 0) >= 1
+            await wait_for(dropped, timeout=5, interval=0.1)
+        finally:
+            await bh.stop()

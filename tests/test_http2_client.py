@@ -253,3 +253,84 @@ def test_client_parser_from_any_framing():
                                (":authority", "a:1"), ("authorization", "x" * 100), ("content-length", "5")]
     assert h2client.AVAILABLE
     assert os.path.basename(h2client.__file__) == "h2client.py"
+
+
+class Blackhole:
+    """A TCP proxy whose connections can be frozen: from `freeze()` on, bytes already flowing through it are
+    swallowed both ways while both sockets stay open — a path that died silently (a dropped NAT entry, a peer
+    that lost power). Connections opened after the freeze pass normally."""
+
+    def __init__(self, port: int):
+        self.port, self.pairs, self.server = port, [], None
+
+    async def start(self) -> str:
+        self.server = await asyncio.start_server(self._handle, "127.0.0.1", 0)
+        return f"http://127.0.0.1:{self.server.sockets[0].getsockname()[1]}"
+
+    def freeze(self) -> None:
+        for p in self.pairs:
+            p["frozen"] = True
+
+    async def _handle(self, r, w):
+        ur, uw = await asyncio.open_connection("127.0.0.1", self.port)
+        pair = {"frozen": False, "writers": (w, uw)}
+        self.pairs.append(pair)
+
+        async def pump(src, dst):
+            try:
+                while True:
+                    data = await src.read(65536)
+                    if not data:
+                        break
+                    if not pair["frozen"]:
+                        dst.write(data)
+            except (ConnectionError, asyncio.CancelledError):
+                pass
+            finally:
+                if not pair["frozen"]:
+                    dst.close()
+        await asyncio.gather(pump(r, uw), pump(ur, w))
+
+    async def stop(self) -> None:
+        self.server.close()
+        for p in self.pairs:
+            for w in p["writers"]:
+                w.close()
+
+
+async def test_a_silent_connection_is_pinged_and_replaced(monkeypatch):
+    """client-go's HTTP/2 health check: a connection that reads nothing for HTTP2_READ_IDLE_TIMEOUT_SECONDS while
+    streams are open is PINGed, and dropped when HTTP2_PING_TIMEOUT_SECONDS pass without an answer. Its request
+    fails at once rather than at its deadline, its watch ends (the informer re-watches), and the next request
+    goes out on a new connection."""
+    monkeypatch.setenv("HTTP2_READ_IDLE_TIMEOUT_SECONDS", "0.5")
+    monkeypatch.setenv("HTTP2_PING_TIMEOUT_SECONDS", "0.5")
+    async with _Server() as (srv, url):
+        bh = Blackhole(int(url.rsplit(":", 1)[1]))
+        purl = await bh.start()
+        c = RestClient(ClusterConfig(server=purl), http2="on", request_timeout=20, max_retries=0)
+        try:
+            ended = asyncio.Event()
+
+            async def watch():  # ends, or fails before its response head: either way the informer re-watches
+                try:
+                    async for _ in c.watch_raw_batches(R.CONFIGMAPS, NS, resource_version="0"):
+                        pass
+                except E.TransportError:
+                    pass
+                ended.set()
+            w = asyncio.ensure_future(watch())
+            assert (await c.list(R.SECRETS, NS))["items"] == []
+            bh.freeze()
+            loop = asyncio.get_running_loop()
+            t0 = loop.time()
+            with pytest.raises(E.TransportError, match="PING"):
+                await c.list(R.SECRETS, NS)
+            assert loop.time() - t0 < 5  # read-idle + PING timeout + sweep granularity, far below the 20 s deadline
+            await asyncio.wait_for(ended.wait(), 5)
+            await w
+            assert (await c.list(R.SECRETS, NS))["items"] == []
+            assert c._pool.stats["h2_dead"] == 1 and c._pool.opened == 2, c._pool.stats
+        finally:
+            await c.close()
+            await bh.stop()
