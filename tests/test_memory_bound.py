@@ -63,7 +63,10 @@ async def test_inprocess_failing_passes_leave_no_frozen_garbage(tmp_path, monkey
             leaked = gc.collect()  # what the freezes had kept
             gc.freeze()
             freezes = gctune.STATS.get("freezes", 0)
-        assert leaked <= 1500, f"{leaked} unreachable objects frozen after {passes} failing passes ({freezes} freezes)"
+        # bounded per freeze (what was in flight at that instant), never per pass: round 3's policy left ~1.5 per
+        # failing pass, 7 500+ here; a slow run (coverage tracing) has more freezes over its 5 000 passes
+        msg = f"{leaked} unreachable objects frozen after {passes} failing passes ({freezes} freezes)"
+        assert leaked <= max(1500, 25 * freezes) and leaked < 0.5 * passes, msg
     finally:
         gc.unfreeze()
         gc.collect()
