@@ -222,6 +222,8 @@ class _H2Conn(asyncio.Protocol):
                 streams.clear()
                 self.close()
                 return
+        if self.draining and not streams and not self.closed:
+            self.close()  # after a GOAWAY, once the streams it let finish have finished
 
     # ------------------------------------------------------------------ frames in
     def _settings(self, kv) -> None:
