@@ -246,6 +246,17 @@ class H2Connection:
     def send_data(self, s: _Stream, data: bytes, end: bool = False) -> None:
         if s.closed:
             return
+        n = len(data)
+        if not s.pending and n <= s.send_window and n <= self.conn_send_window and n <= self.peer_max_frame:
+            # the common case (a watch event within the windows): one frame, no copy through `pending`
+            s.send_window -= n
+            self.conn_send_window -= n
+            end = end or s.eof_pending
+            self._out(frame(DATA, END_STREAM if end else 0, s.id, data))
+            if end:
+                s.eof_pending = False
+                self._close(s)
+            return
         s.pending += data
         s.eof_pending = s.eof_pending or end
         self._flush(s)
