@@ -4,8 +4,8 @@ Loads the controller cluster's kubeconfig and every `<cluster>.kubeconfig` in `s
 the controller does (credentials, `exec` plugins, CA), then LISTs each kind the controller reads and writes
 in `controller-namespace` on each cluster.  One JSON line per cluster, then a summary line; exit status 0 when
 every cluster answered every list.  A missing CRD shows up as NotFound, missing RBAC as Forbidden, a wrong
-server or CA as TransportError — before the controller starts and waits for caches that never sync.  Write
-permissions are not probed (that would need writes, or SelfSubjectAccessReviews the reference never needed).
+server or CA as TransportError — before the controller starts and waits for caches that never sync.  Each
+line also names the protocol negotiated (`h2` or `http/1.1`, per `client-http2`).  Write permissions are not probed (that would need writes, or SelfSubjectAccessReviews the reference never needed).
 """
 from __future__ import annotations
 
@@ -41,7 +41,11 @@ async def check_cluster(name: str, client, namespace: str, timeout: float = 10.0
             kinds[rt.plural] = f"{type(e).__name__} ({e.code}): {e.message}"[:300]
         except Exception as e:  # noqa: BLE001 - TLS and other client-side failures
             kinds[rt.plural] = f"{type(e).__name__}: {e}"[:300]
-    return {"cluster": name, "ok": all(v == "ok" for v in kinds.values()), "kinds": kinds}
+    out = {"cluster": name, "ok": all(v == "ok" for v in kinds.values()), "kinds": kinds}
+    proto = getattr(client, "protocol", None)
+    if proto is not None:  # what the controller will speak to it (client-http2: HTTP/2 where TLS negotiates it)
+        out["protocol"] = proto
+    return out
 
 
 async def check(cfg, timeout: float = 10.0) -> list[dict]:
@@ -51,7 +55,7 @@ async def check(cfg, timeout: float = 10.0) -> list[dict]:
                 for name, path in discover(cfg.shard_config_path)]
     for name, make_cfg in targets:
         try:
-            client = RestClient(make_cfg(), pool_size=2, cluster_name=name)
+            client = RestClient(make_cfg(), pool_size=2, cluster_name=name, http2=cfg.client_http2)
         except Exception as e:  # noqa: BLE001 - an unreadable kubeconfig
             out.append({"cluster": name, "ok": False, "error": f"{type(e).__name__}: {e}"[:300]})
             continue
