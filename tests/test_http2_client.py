@@ -61,15 +61,23 @@ async def test_rest_client_over_prior_knowledge_http2():
                 await c.get(R.SECRETS, NS, "missing")
             with pytest.raises(E.AlreadyExists):
                 await c.create(R.SECRETS, NS, make_secret("s0", NS))
+            # a 429 with Retry-After (the retry-after field of the response head): retried, then served
+            srv.faults.update({"rules": [{"method": "PUT", "resource": "secrets", "code": 429, "count": 2,
+                                          "retry_after": 0, "message": "slow down"}]})
+            retries = c.stats["retries"]
+            got = await c.get(R.SECRETS, NS, "s8")
+            got["data"] = {"k": "dmFsdWU="}
+            await c.update(R.SECRETS, NS, got)
+            assert c.stats["retries"] == retries + 2
             await c.delete(R.SECRETS, NS, "s1")
 
             async def settled():
-                return len(seen) >= 202
+                return len(seen) >= 203
             for _ in range(200):
                 if await settled():
                     break
                 await asyncio.sleep(0.01)
-            assert len(seen) == 202 and tapped == seen  # 200 ADDED, a MODIFIED, a DELETED; the tap saw each first
+            assert len(seen) == 203 and tapped == seen  # 200 ADDED, 2 MODIFIED, a DELETED; the tap saw each first
             w.cancel()
             st = srv._http.conn_stats()["h2"]
             # everything, the watch included, went over one connection (250 streams allowed on it)
