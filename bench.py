@@ -885,7 +885,8 @@ async def run(args, d: Dist) -> dict | None:
                            "shard_latency_ms": args.shard_latency_ms, "shard_jitter_ms": args.shard_jitter_ms,
                            "tls": bool(args.tls),
                            # what the C++ executors spoke to the shard apiservers and the coordinator to the
-                           # controller apiserver (client-http2; bench.py: HTTP/2, prior knowledge on cleartext)
+                           # controller apiserver (client-http2 on: HTTP/2 with prior knowledge to the shards; the
+                           # controller cluster as client-go on cleartext, HTTP/1.1 — ncc/config.py controller_http2)
                            "shard_transport": _shard_transport(ctl_debug),
                            "controller_transport": (ctl_debug or {}).get("controller_transport", "n/a")},
                 "p50_latency_ms": round(statistics.median(lat), 2) if lat else None,

@@ -27,7 +27,7 @@ from . import native as native_ext
 from .api import constants as C
 from .api import resources as R
 from .cache.informer import InformerFactory
-from .config import AppConfig, config_to_env, load_config
+from .config import AppConfig, config_to_env, controller_http2, load_config
 from .controller.controller import Controller
 from .controller.events import BroadcastRecorder, FakeRecorder
 from .controller.executor import CoordinatorPartitions, ExecutorPool, partition_filter, partition_owner_filter
@@ -265,7 +265,7 @@ class App:
         if client is None:
             qps, burst = client_limits(cfg)
             client = RestClient(build_config(cfg.controller_config_path), pool_size=cfg.pool_size(),
-                                pipeline_depth=cfg.pipeline_depth(), http2=cfg.client_http2,
+                                pipeline_depth=cfg.pipeline_depth(), http2=controller_http2(cfg.client_http2),
                                 cluster_name=cfg.alias, transport=cfg.transport)
             if qps > 0:
                 client = RateLimitedClient(client, qps, burst)

@@ -12,7 +12,8 @@ transport negotiates h2 by ALPN and multiplexes a clientset's requests on one co
   connection opens only when every one is full), request-body flow control, GOAWAY (streams above its last id
   are retried on a fresh connection, as REFUSED_STREAM ones are), per-request deadlines, and the watch streams'
   windows, credited as their consumer takes the lines (the back-pressure `pause_reading` gives HTTP/1.1);
-* negotiation: ALPN "h2" on TLS (`client-http2: auto`, the default), or prior knowledge on cleartext (`on`).
+* negotiation: ALPN "h2" on TLS (`client-http2: auto`, the default), or prior knowledge on cleartext (`on`, for
+  the shard clients: the controller cluster's negotiates, `ncc/config.py` `controller_http2`).
   A server that does not speak HTTP/2 — ALPN picks http/1.1, or it answers the preface with anything but
   SETTINGS — makes the pool fall back to HTTP/1.1 (`transport.ConnectionPool`) for good.
 """

@@ -13,6 +13,7 @@ import asyncio
 import json
 
 from .api import resources as R
+from .config import controller_http2
 from .kube import errors as E
 from .kube.kubeconfig import build_config, load_kubeconfig
 from .kube.rest import RestClient
@@ -55,7 +56,8 @@ async def check(cfg, timeout: float = 10.0) -> list[dict]:
                 for name, path in discover(cfg.shard_config_path)]
     for name, make_cfg in targets:
         try:
-            client = RestClient(make_cfg(), pool_size=2, cluster_name=name, http2=cfg.client_http2)
+            mode = controller_http2(cfg.client_http2) if name == "controller" else cfg.client_http2
+            client = RestClient(make_cfg(), pool_size=2, cluster_name=name, http2=mode)
         except Exception as e:  # noqa: BLE001 - an unreadable kubeconfig
             out.append({"cluster": name, "ok": False, "error": f"{type(e).__name__}: {e}"[:300]})
             continue

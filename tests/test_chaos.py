@@ -120,9 +120,8 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
     """`native-c2`: two coordinator partitions (a child coordinator process owns half the template keys);
     the kills then also hit the child coordinator.  `native-ssa`: shard writes by server-side apply.
     `native-meta`: sync-dependent-metadata, with source labels/annotations changed along the way.
-    `native-h2`: the C++ executors write to the shards over HTTP/2 (`client-http2: on`, prior knowledge), and
-    the coordinator talks HTTP/2 to the controller apiserver; `python-h2`: the same with the Python executors
-    (ncc/kube/h2client.py on every connection)."""
+    `native-h2`: the C++ executors write to the shards over HTTP/2 (`client-http2: on`, prior knowledge);
+    `python-h2`: the same with the Python executors (ncc/kube/h2client.py on every shard connection)."""
     from ncc.controller.native_executor import binary_path
     reload = topology.endswith("-reload")
     ssa = topology.endswith("-ssa")

@@ -14,8 +14,10 @@ async def test_preflight_reports_each_cluster_and_names_the_failure(tmp_path):
         assert [r["cluster"] for r in ok] == ["controller", "shard-0", "shard-1", "shard-2"]
         assert all(r["ok"] for r in ok), ok
         assert all(r["protocol"] == "http/1.1" for r in ok)  # cleartext with client-http2 auto
-        h2 = await check(env.app_config(mode="native", client_http2="on"))
-        assert all(r["ok"] and r["protocol"] == "h2" for r in h2), h2
+        h2 = {r["cluster"]: r for r in await check(env.app_config(mode="native", client_http2="on"))}
+        # `on` adds prior knowledge for the shards; the controller cluster negotiates (ALPN on TLS only)
+        assert all(r["ok"] for r in h2.values()) and h2["controller"]["protocol"] == "http/1.1", h2
+        assert all(h2[f"shard-{i}"]["protocol"] == "h2" for i in range(3)), h2
         # shard-1's credentials may not list Secrets; shard-2 lacks the workgroup CRD; a broken kubeconfig
         env.shard_servers[1].faults.update({"rules": [{"method": "GET", "resource": "secrets", "code": 403,
                                                        "message": "secrets is forbidden"}]})
