@@ -87,7 +87,8 @@ def test_kubeconfig_variants(tmp_path):
         parse_kubeconfig(doc, context="missing")
 
 
-async def test_exec_plugin_token_is_cached_and_refreshed(tmp_path):
+@pytest.mark.parametrize("http2", ["off", "on"])
+async def test_exec_plugin_token_is_cached_and_refreshed(tmp_path, http2):
     counter = tmp_path / "count"
     script = tmp_path / "get-token"
     script.write_text(f"""#!{sys.executable}
@@ -115,11 +116,12 @@ print(json.dumps({{"apiVersion": "client.authentication.k8s.io/v1", "kind": "Exe
     srv = FakeApiServer(token="tok-3")
     url = await srv.start()
     cfg.server = url
-    client = RestClient(cfg)
+    client = RestClient(cfg, http2=http2)  # over HTTP/2 the authorization field is re-encoded with the new token
     try:
         client.creds._token = "tok-2"
         assert (await client.list(R.SECRETS, "nexus"))["items"] == []
         assert client.creds.exec_runs == 1 and counter.read_text() == "3"
+        assert client.protocol == ("h2" if http2 == "on" else "http/1.1")
     finally:
         await client.close()
         await srv.stop()
