@@ -19,7 +19,8 @@ Fault knobs (`POST /_fake/faults`), for connections opened afterwards: `h2_goawa
 streams a connection sends GOAWAY naming the last stream it will serve, and refuses later ones (a
 kube-apiserver does this on shutdown and, with `--goaway-chance`, to rebalance clients); `h2_max_streams` — the
 MAX_CONCURRENT_STREAMS advertised; `h2_initial_window` — the stream window advertised (request bodies larger
-than it wait for the WINDOW_UPDATEs the server sends as it reads).
+than it wait for the WINDOW_UPDATEs the server sends as it reads); `h2_small_conn_window` — the connection window
+left at 65 535 and credited as DATA is read, so concurrent bodies also wait on the connection's window.
 """
 from __future__ import annotations
 
@@ -77,7 +78,10 @@ class H2Connection:
         self.goaway_after = int(server.h2_options.get("h2_goaway_after", 0) or 0)
         # a small stream window makes a client's request bodies wait for our WINDOW_UPDATEs (tests)
         self.our_window = int(server.h2_options.get("h2_initial_window", 0) or 0) or OUR_WINDOW
-        self.parser = mod.H2ServerParser(self.our_window < OUR_WINDOW)
+        # the connection window left at the protocol's 65 535 (credited back as DATA is consumed): every client
+        # request body then also waits for connection-level WINDOW_UPDATEs (tests)
+        self.small_conn_window = bool(server.h2_options.get("h2_small_conn_window"))
+        self.parser = mod.H2ServerParser(self.our_window < OUR_WINDOW or self.small_conn_window)
         self._encode = mod.h2_response
         self.streams: dict[int, _Stream] = {}  # dispatched, not yet answered to the end
         self.last_stream = 0
@@ -95,7 +99,7 @@ class H2Connection:
         self._out(frame(SETTINGS, 0, 0, struct.pack(
             ">HIHIHIHI", S_MAX_CONCURRENT_STREAMS, self.max_streams, S_INITIAL_WINDOW_SIZE, self.our_window,
             S_MAX_FRAME_SIZE, OUR_MAX_FRAME, S_ENABLE_PUSH, 0)) +
-            frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", (1 << 30) - 65535)))
+            (b"" if self.small_conn_window else frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", (1 << 30) - 65535))))
 
     @property
     def open_streams(self) -> int:
@@ -134,6 +138,8 @@ class H2Connection:
                         self._flush(s)
             elif kind == "credit":  # small-window mode: credit what the client's DATA consumed
                 self._out(frame(WINDOW_UPDATE, 0, ev[1], struct.pack(">I", ev[2])))
+                if self.small_conn_window:
+                    self._out(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", ev[2])))
             elif kind == "settings":
                 for ident, value in ev[1]:
                     if ident == S_INITIAL_WINDOW_SIZE:

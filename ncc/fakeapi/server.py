@@ -119,7 +119,7 @@ class Faults:
             self.down = bool(d["down"])
         if "write_only" in d:
             self.write_only = bool(d["write_only"])
-        for k in ("h2_max_streams", "h2_goaway_after", "h2_initial_window"):
+        for k in ("h2_max_streams", "h2_goaway_after", "h2_initial_window", "h2_small_conn_window"):
             if k in d:
                 self.h2[k] = int(d[k])
 

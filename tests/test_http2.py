@@ -222,12 +222,13 @@ async def test_goaway_mid_run_moves_streams_to_a_new_connection(tmp_path, native
 
 async def test_stream_limit_is_obeyed_and_small_windows_hold_bodies(tmp_path, native_only, monkeypatch):
     """MAX_CONCURRENT_STREAMS 4: the executor never has more streams open on a connection (the server refuses
-    any extra with REFUSED_STREAM — none come) and opens more connections; a 64-byte stream window makes every
-    request body wait for the server's WINDOW_UPDATEs."""
+    any extra with REFUSED_STREAM — none come) and opens more connections; a 64-byte stream window and a
+    connection window left at 65 535 make every request body wait for the server's WINDOW_UPDATEs."""
     monkeypatch.setenv("NCC_STATUS_S", "0.2")
     async with Cluster(tmp_path, "native", n_shards=1, client_http2="on", executors_per_shard=1,
                        client_pool_size=8) as cl:
-        cl.env.shard_servers[0].faults.update({"h2_max_streams": 4, "h2_initial_window": 64})
+        cl.env.shard_servers[0].faults.update({"h2_max_streams": 4, "h2_initial_window": 64,
+                                               "h2_small_conn_window": 1})
         n = 25
         for i in range(n):
             cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))

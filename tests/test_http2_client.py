@@ -122,11 +122,22 @@ async def test_server_limits_windows_goaway_and_large_headers():
             assert st["max_open"] <= 4 and st["refused"] == 0 and 1 <= st["connections"] <= 2, st
         finally:
             await c.close()
-        srv.faults.update({"h2_max_streams": 0, "h2_initial_window": 0, "h2_goaway_after": 7})
+        # a connection window of 64 KiB shared by 100 concurrent 600-byte bodies (credited as the server reads)
+        srv.faults.update({"h2_max_streams": 0, "h2_initial_window": 0, "h2_small_conn_window": 1})
+        c = RestClient(ClusterConfig(server=url), http2="on")
+        try:
+            big = [make_secret(f"w{i}", NS) for i in range(100)]
+            for o in big:
+                o["data"] = {"k": "A" * 4000}
+            await asyncio.gather(*[c.create(R.SECRETS, NS, o) for o in big])
+            assert srv.state.count(R.SECRETS, NS) == 140
+        finally:
+            await c.close()
+        srv.faults.update({"h2_small_conn_window": 0, "h2_goaway_after": 7})
         c = RestClient(ClusterConfig(server=url, token="t" * 40000), http2="on")  # HEADERS + CONTINUATION
         try:
             await asyncio.gather(*[c.create(R.SECRETS, NS, make_secret(f"b{i}", NS)) for i in range(50)])
-            assert srv.state.count(R.SECRETS, NS) == 90
+            assert srv.state.count(R.SECRETS, NS) == 190
             assert c._pool.stats["h2_goaways"] >= 5 and c._pool.opened >= 6, c._pool.stats
         finally:
             await c.close()
