@@ -77,7 +77,8 @@ case "$what" in
     ;;
   bench)
     n=$1; shift
-    for i in $(seq 1 "$n"); do bench_once "$out/bench_$i" "$@" || exit $?; done
+    k=$(find "$out" -maxdepth 1 -name 'bench_*.json' | wc -l)  # a second `bench` into the same dir appends
+    for i in $(seq $((k + 1)) $((k + n))); do bench_once "$out/bench_$i" "$@" || exit $?; done
     ;;
   ab)
     n=$1; a=$2; b=$3
