@@ -38,6 +38,13 @@ SHARD_SYNC_ERRORS_METRIC = "shard_sync_errors"        # count, tag shard (coordi
 SHARDS_METRIC = "shards"                              # gauge: shards served
 LEADER_METRIC = "leader"                              # gauge 1/0 when leader election is on
 SHARD_FAILING_METRIC = "shard_failing_objects"        # gauge, tag shard: templates whose last sync there failed
+# the C++ executors' shard clients (their status messages, native/executor/http.hpp), gauges tagged shard:
+SHARD_CLIENT_METRICS = {"limit": "shard_client_inflight_limit",      # adaptive concurrency limit (AIMD)
+                        "inflight": "shard_client_inflight",         # requests in flight
+                        "rejected_429": "shard_client_throttled",    # 429s received (cumulative)
+                        "connections": "shard_client_connections",   # open connections
+                        "http2": "shard_client_http2",               # 1 when the shard is spoken to over HTTP/2
+                        "h2_dead": "shard_client_dead_connections"}  # connections dropped for an unanswered PING
 
 # Event reasons, controller.go:60-70
 SUCCESS_SYNCED = "Synced"

@@ -418,6 +418,12 @@ class App:
             self.metrics.gauge(C.SHARD_FAILING_METRIC, n, {"shard": shard})
         if self.elector is not None:
             self.metrics.gauge(C.LEADER_METRIC, 1 if self.elector.leading else 0)
+        if self.pool is not None:
+            for h in self.pool.stats().values():
+                for shard, flow in ((h.get("status") or {}).get("flow") or {}).items():
+                    for field, name in C.SHARD_CLIENT_METRICS.items():
+                        if field in flow:
+                            self.metrics.gauge(name, flow[field], {"shard": shard})
 
     def _ready(self) -> bool:
         """Ready once caches synced and workers run — or while standing by for the leader Lease."""

@@ -162,6 +162,15 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
             assert st["open"] <= 2, st
             assert srv.requests["watch_streams"] >= 4
         assert all(f["rejected_429"] == 0 for f in fl.values())
+        # the same flow status as per-shard gauges (statsd / Prometheus)
+        from ncc.api import constants as C
+        from ncc.telemetry.statsd import MemoryMetrics
+        cl.app.metrics = MemoryMetrics()
+        cl.app._gauges()
+        v = cl.app.metrics.values
+        assert v[C.SHARD_CLIENT_METRICS["http2"]] == [1.0, 1.0], v
+        assert all(x >= 1 for x in v[C.SHARD_CLIENT_METRICS["limit"]]) and len(v[C.SHARD_CLIENT_METRICS["limit"]]) == 2
+        assert v[C.SHARD_CLIENT_METRICS["rejected_429"]] == [0.0, 0.0]
 
 
 async def test_executor_negotiates_http2_by_alpn_on_tls(tmp_path, native_only, monkeypatch):
