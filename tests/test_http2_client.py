@@ -353,3 +353,72 @@ async def test_a_silent_connection_is_pinged_and_replaced(monkeypatch):
         finally:
             await c.close()
             await bh.stop()
+
+
+async def test_stream_resets_refusals_and_early_watch_exit():
+    """A scripted HTTP/2 server (the native server parser and response encoder over a bare asyncio server):
+    REFUSED_STREAM is retried (after a backoff) and then served; another reset code fails the request; a
+    consumer that leaves a watch early resets its stream and the connection carries on; a malformed frame is a
+    connection error (GOAWAY, the connection dropped) and the next request gets a new connection."""
+    script = {"/refuse-once": ["refuse", "ok"], "/reset": ["reset"]}
+    seen = []
+
+    async def handle(reader, writer):
+        parser = _m.H2ServerParser(False)
+        writer.write(_frame(4, 0, 0, (3).to_bytes(2, "big") + (100).to_bytes(4, "big")) +
+                     _frame(8, 0, 0, ((1 << 30) - 65535).to_bytes(4, "big")))
+        while True:
+            data = await reader.read(65536)
+            if not data:
+                break
+            for ev in parser.feed(data):
+                if ev[0] == "settings":
+                    writer.write(_frame(4, 1, 0, b""))
+                elif ev[0] == "req":
+                    _, sid, method, path, headers, body = ev
+                    seen.append((sid, path))
+                    plan = script.get(path.split("?")[0])
+                    step = plan.pop(0) if plan else "ok"
+                    if step == "refuse":
+                        writer.write(_frame(3, 0, sid, (7).to_bytes(4, "big")))
+                    elif step == "reset":
+                        writer.write(_frame(3, 0, sid, (2).to_bytes(4, "big")))
+                    elif path == "/garbage":  # HEADERS on stream 0: a connection error
+                        writer.write(_frame(1, 0x4, 0, b""))
+                    elif "watch=1" in path:  # a watch: the head and two events, the stream left open
+                        block = _m.hpack_encode([(":status", "200"), ("content-type", "application/json")])
+                        writer.write(_frame(1, 0x4, sid, block) +
+                                     _frame(0, 0, sid, b'{"type":"ADDED","object":{}}\n{"type":"ADDED","object":{}}\n'))
+                    else:
+                        writer.write(_m.h2_response(sid, 200, "application/json", b'{"kind":"SecretList","items":[]}',
+                                                    [], 16384))
+            await writer.drain()
+
+    server = await asyncio.start_server(handle, "127.0.0.1", 0)
+    url = f"http://127.0.0.1:{server.sockets[0].getsockname()[1]}"
+    pool = h2client.H2Pool(url, prior_knowledge=True, connect_timeout=5)
+    try:
+        r = await pool.request("GET", "/refuse-once", {"Accept": "application/json"}, None, timeout=5)
+        assert r.status == 200 and pool.stats["h2_refused"] == 1
+        with pytest.raises(E.TransportError, match="reset by the server"):
+            await pool.request("GET", "/reset", {"Accept": "application/json"}, None, timeout=5)
+        got = []
+        gen = pool.stream("/api/v1/namespaces/nexus/secrets?watch=1", {"Accept": "application/json"}, batch=True)
+        async for resp, lines in gen:
+            if resp is not None:
+                assert resp.status == 200
+                continue
+            got.extend(lines)
+            break  # leave early: the stream is reset, the connection stays
+        await gen.aclose()
+        assert len(got) == 2 and pool.conns and not pool.conns[0].streams
+        assert (await pool.request("GET", "/after", {"Accept": "application/json"}, None, timeout=5)).status == 200
+        assert pool.opened == 1
+        with pytest.raises(E.TransportError, match="connection error"):
+            await pool.request("GET", "/garbage", {"Accept": "application/json"}, None, timeout=5)
+        assert (await pool.request("GET", "/after", {"Accept": "application/json"}, None, timeout=5)).status == 200
+        assert pool.opened == 2  # the broken connection was closed (GOAWAY sent); a new one took over
+    finally:
+        pool.close()
+        server.close()
+        await server.wait_closed()
