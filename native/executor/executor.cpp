@@ -2381,6 +2381,8 @@ static Credentials creds_of(const Value& s) {
     c.token_file = std::string(s.sget("token_file"));
     c.username = std::string(s.sget("username"));
     c.password = std::string(s.sget("password"));
+    c.proxy = std::string(s.sget("proxy"));
+    c.proxy_connect = std::string(s.sget("proxy_connect"));
     return c;
 }
 

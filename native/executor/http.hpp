@@ -113,6 +113,9 @@ struct Credentials {
     std::string cert_pem, key_pem;
     std::string token, token_file;
     std::string username, password;
+    // an HTTP CONNECT proxy (kubeconfig proxy-url, or client-go's HTTPS_PROXY rules: ncc/kube/proxy.py) and the
+    // CONNECT request the coordinator rendered for it (proxy credentials included)
+    std::string proxy, proxy_connect;
 };
 
 struct Url {
@@ -135,6 +138,7 @@ inline Url parse_url(const std::string& s) {
     }
     size_t slash = rest.find('/');
     std::string hostport = rest.substr(0, slash);
+    if (size_t at = hostport.rfind('@'); at != std::string::npos) hostport.erase(0, at + 1);  // userinfo
     if (slash != std::string::npos) u.prefix = rest.substr(slash);
     while (!u.prefix.empty() && u.prefix.back() == '/') u.prefix.pop_back();
     if (!hostport.empty() && hostport[0] == '[') {  // [v6]:port
@@ -153,6 +157,12 @@ inline Url parse_url(const std::string& s) {
     if (u.port == 0) u.port = u.tls ? 443 : 80;
     return u;
 }
+
+// The tunnel a connection opens first: the proxy's address and the CONNECT request to send it.
+struct Proxy {
+    Url url;
+    std::string connect;
+};
 
 inline bool is_ip(const std::string& h) {
     in6_addr a6;
@@ -270,14 +280,16 @@ public:
 
     // `offer_h2`: offer ALPN "h2" on a TLS connection (the outcome lands in `alpn_selected`).  A flag, not a
     // string: GCC 11 mishandles class-type coroutine parameters passed as temporaries.
-    Task<void> connect(const Url& u, SSL_CTX* ctx, const std::string& server_name, bool offer_h2 = false) {
+    Task<void> connect(const Url& u, SSL_CTX* ctx, const std::string& server_name, bool offer_h2 = false,
+                       const Proxy* proxy = nullptr) {
+        const Url& dial = proxy != nullptr ? proxy->url : u;  // through a proxy: its address, then CONNECT
         addrinfo hints{};
         hints.ai_family = AF_UNSPEC;
         hints.ai_socktype = SOCK_STREAM;
         addrinfo* res = nullptr;
-        std::string port = std::to_string(u.port);
-        int rc = getaddrinfo(u.host.c_str(), port.c_str(), &hints, &res);
-        if (rc != 0 || res == nullptr) throw TransportError("resolve " + u.host + ": " + gai_strerror(rc));
+        std::string port = std::to_string(dial.port);
+        int rc = getaddrinfo(dial.host.c_str(), port.c_str(), &hints, &res);
+        if (rc != 0 || res == nullptr) throw TransportError("resolve " + dial.host + ": " + gai_strerror(rc));
         fd = ::socket(res->ai_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
         if (fd < 0) {
             freeaddrinfo(res);
@@ -288,13 +300,29 @@ public:
         loop().add_fd(fd);
         rc = ::connect(fd, res->ai_addr, res->ai_addrlen);
         freeaddrinfo(res);
-        if (rc != 0 && errno != EINPROGRESS) throw TransportError("connect " + u.host + ": " + std::strerror(errno));
+        if (rc != 0 && errno != EINPROGRESS) throw TransportError("connect " + dial.host + ": " + std::strerror(errno));
         if (rc != 0) {
             co_await loop().writable(fd);
             int err = 0;
             socklen_t len = sizeof err;
             getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
-            if (err != 0) throw TransportError("connect " + u.host + ":" + port + ": " + std::strerror(err));
+            if (err != 0) throw TransportError("connect " + dial.host + ":" + port + ": " + std::strerror(err));
+        }
+        if (proxy != nullptr) {  // the tunnel: CONNECT answered 200, nothing after the answer's head
+            co_await write_all(proxy->connect);
+            size_t end;
+            while ((end = buf.find("\r\n\r\n", pos)) == std::string::npos) {
+                if (buf.size() - pos > 65536) throw TransportError("proxy " + dial.host + ": CONNECT answer too large");
+                co_await fill();
+            }
+            std::string_view line(buf.data() + pos, buf.find("\r\n", pos) - pos);
+            size_t sp = line.find(' ');
+            if (sp == std::string_view::npos || line.substr(sp + 1, 3) != "200")
+                throw TransportError("proxy " + dial.host + ":" + port + " refused CONNECT to " + u.host + ": " +
+                                     std::string(line.substr(0, 120)));
+            if (end + 4 != buf.size()) throw TransportError("proxy " + dial.host + " sent data before the tunnel was used");
+            buf.clear();
+            pos = 0;
         }
         if (ctx != nullptr) {
             ssl = SSL_new(ctx);
@@ -693,6 +721,11 @@ public:
         reload_token(true);
         h2_mode_ = http2;
         h2_ok_ = http2 == 2 || (http2 == 1 && url_.tls);
+        if (!creds_.proxy.empty()) {
+            proxy_.url = parse_url(creds_.proxy);
+            proxy_.connect = creds_.proxy_connect;
+            has_proxy_ = true;
+        }
         // client-go's HTTP/2 health check, same variables and defaults: a connection with streams open that read
         // nothing for READ_IDLE s (or whose stream just timed out) gets a PING; no answer in PING_TIMEOUT s and it
         // is closed, its requests re-sent and its watches restarted on a new one
@@ -774,7 +807,7 @@ public:
     template <class F>
     Task<void> stream_h1(const std::string& target, F on_lines, double idle_timeout) {
         auto conn = std::make_unique<Conn>();
-        co_await conn->connect(url_, ctx_, creds_.tls_server_name);
+        co_await conn->connect(url_, ctx_, creds_.tls_server_name, false, proxy());
         // a silent dead peer must not hold the watch forever: the deadline sweep aborts the stream
         // when nothing (events or bookmarks) arrived for `idle_timeout` seconds
         conn->deadline = now_s() + idle_timeout;
@@ -862,6 +895,9 @@ private:
     int h2_mode_ = 0;     // client-http2: 0 off, 1 auto (ALPN on TLS), 2 on (prior knowledge on cleartext too)
     bool h2_ok_ = false;  // requests go over HTTP/2 (false again when the server does not negotiate it)
     double h2_read_idle_ = 30, h2_ping_timeout_ = 15;  // the liveness check (see the constructor)
+    Proxy proxy_;
+    bool has_proxy_ = false;
+    const Proxy* proxy() const { return has_proxy_ ? &proxy_ : nullptr; }
     std::vector<h2::SessionPtr> h2s_;                 // HTTP/2 connections, oldest first
     std::deque<std::coroutine_handle<>> h2_waiters_;  // requests waiting for stream room on one of them
     std::string h2_block_;                            // scratch: the header block being encoded
@@ -995,7 +1031,7 @@ private:
     }
     Task<void> open_pipe(PipePtr p) {
         try {
-            co_await p->c.connect(url_, ctx_, creds_.tls_server_name);
+            co_await p->c.connect(url_, ctx_, creds_.tls_server_name, false, proxy());
         } catch (const std::exception& e) {
             break_pipe(p, e.what());
             co_return;
@@ -1220,7 +1256,7 @@ private:
                 ++open_;
                 auto c = std::make_unique<Conn>();
                 try {
-                    co_await c->connect(url_, ctx_, creds_.tls_server_name);
+                    co_await c->connect(url_, ctx_, creds_.tls_server_name, false, proxy());
                 } catch (...) {
                     --open_;
                     wake_one();
@@ -1385,7 +1421,7 @@ private:
         s->c.deadline = now_s() + timeout_;  // the deadline sweep aborts a connect that hangs
         track(&s->c);
         try {
-            co_await s->c.connect(url_, ctx_, creds_.tls_server_name, url_.tls);
+            co_await s->c.connect(url_, ctx_, creds_.tls_server_name, url_.tls, proxy());
             if (url_.tls && s->c.alpn_selected != "h2")
                 throw NoH2("the server did not negotiate HTTP/2 (ALPN); using HTTP/1.1");
         } catch (const NoH2& e) {

@@ -73,6 +73,23 @@ def _file_digest(path: str) -> str:
         return ""
 
 
+def proxy_entry(cc) -> dict:
+    """The shard's proxy for the C++ executor: its URL and the CONNECT request (credentials included), rendered
+    here so the executor needs no URL or base64 handling of its own (ncc/kube/proxy.py)."""
+    from urllib.parse import urlsplit
+
+    from ..kube.proxy import connect_request, proxy_for
+    proxy = proxy_for(cc.server, cc.proxy_url)
+    if not proxy:
+        return {}
+    u, p = urlsplit(cc.server), urlsplit(proxy)
+    phost = f"[{p.hostname}]" if p.hostname and ":" in p.hostname else (p.hostname or "")
+    # the credentials travel in the rendered request only
+    return {"proxy": f"http://{phost}:{p.port or 80}",
+            "proxy_connect": connect_request(proxy, u.hostname or "",
+                                             u.port or (443 if u.scheme == "https" else 80)).decode()}
+
+
 class NativeExecutorConfig:
     """Renders the `cfg` message of one executor and keeps exec-plugin tokens fresh."""
 
@@ -119,7 +136,7 @@ class NativeExecutorConfig:
                 "tls_server_name": cc.tls_server_name or "", "cert_pem": (cert or b"").decode(),
                 "key_pem": (key or b"").decode(), "token": token or "",
                 "token_file": cc.token_file if (cc.token_file and not cc.token and cc.exec is None) else "",
-                "username": cc.username or "", "password": cc.password or ""}
+                "username": cc.username or "", "password": cc.password or "", **proxy_entry(cc)}
 
     async def render(self, handle) -> str:
         from ..app import client_limits

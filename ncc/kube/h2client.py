@@ -381,7 +381,7 @@ class H2Pool:
 
     def __init__(self, server: str, *, ssl_context: _ssl.SSLContext | None = None, server_hostname: str | None = None,
                  max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1,
-                 prior_knowledge: bool = False):
+                 prior_knowledge: bool = False, proxy: str | None = None):
         if not AVAILABLE:
             raise RuntimeError("HTTP/2 needs the native extension (ncc/_native)")
         u = urlsplit(server)
@@ -398,6 +398,7 @@ class H2Pool:
         self.connect_timeout = connect_timeout
         self.pipeline_depth = pipeline_depth
         self.prior_knowledge = prior_knowledge
+        self.proxy = proxy  # an HTTP CONNECT proxy (ncc/kube/proxy.py); HTTP/2 runs inside the tunnel
         self.conns: list[_H2Conn] = []
         self._connecting: asyncio.Future | None = None
         self._waiters: deque = deque()
@@ -424,8 +425,13 @@ class H2Pool:
             kw["ssl"] = self.ssl
             kw["server_hostname"] = self.server_hostname or self.host
         try:
-            _, conn = await wait_timeout(
-                loop.create_connection(lambda: _H2Conn(self), self.host, self.port, **kw), self.connect_timeout)
+            if self.proxy:
+                from .proxy import open_tunnel
+                sock = await open_tunnel(self.proxy, self.host, self.port, self.connect_timeout)
+                coro = loop.create_connection(lambda: _H2Conn(self), sock=sock, **kw)
+            else:
+                coro = loop.create_connection(lambda: _H2Conn(self), self.host, self.port, **kw)
+            _, conn = await wait_timeout(coro, self.connect_timeout)
         except (OSError, asyncio.TimeoutError, _ssl.SSLError) as e:
             raise E.TransportError(f"connect {self.host}:{self.port}: {type(e).__name__}: {e}") from e
         try:
@@ -442,7 +448,7 @@ class H2Pool:
         if self.fallback is None:
             self.fallback = ConnectionPool(self.server, ssl_context=self.ssl, server_hostname=self.server_hostname,
                                            max_size=self.max_size, connect_timeout=self.connect_timeout,
-                                           pipeline_depth=self.pipeline_depth)
+                                           pipeline_depth=self.pipeline_depth, proxy=self.proxy)
         return self.fallback
 
     def _pick(self) -> _H2Conn | None:

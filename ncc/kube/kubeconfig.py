@@ -7,7 +7,8 @@ Shards on EKS authenticate through the kubeconfig `exec` plugin (`aws eks get-to
 why the reference image bundles the AWS CLI (.container/Dockerfile:16-41).
 
 Supported: current-context / explicit context, `server`, `certificate-authority(-data)`,
-`insecure-skip-tls-verify`, `tls-server-name`, `client-certificate(-data)`/`client-key(-data)`,
+`insecure-skip-tls-verify`, `tls-server-name`, `proxy-url` (an HTTP CONNECT proxy; without it, client-go's
+`HTTPS_PROXY`/`HTTP_PROXY`/`NO_PROXY`, `ncc/kube/proxy.py`), `client-certificate(-data)`/`client-key(-data)`,
 `token`/`tokenFile`, basic auth, and `exec` credential plugins
 (client.authentication.k8s.io/v1 and v1beta1) with expiry-aware caching.
 """
@@ -56,6 +57,7 @@ class ClusterConfig:
     exec: ExecConfig | None = None
     namespace: str | None = None
     base_dir: str = ""
+    proxy_url: str | None = None  # kubeconfig `proxy-url`
 
     @property
     def is_tls(self) -> bool:
@@ -96,6 +98,7 @@ def parse_kubeconfig(doc: dict, *, context: str | None = None, base_dir: str = "
         cfg.ca_data = _read(cluster["certificate-authority"], base_dir)
     cfg.insecure = bool(cluster.get("insecure-skip-tls-verify", False))
     cfg.tls_server_name = cluster.get("tls-server-name")
+    cfg.proxy_url = cluster.get("proxy-url") or None
     if user.get("client-certificate-data"):
         cfg.client_cert_data = base64.b64decode(user["client-certificate-data"])
     elif user.get("client-certificate"):
@@ -160,7 +163,7 @@ def build_config(path: str | None) -> ClusterConfig:
 def render_kubeconfig(server: str, name: str, *, token: str | None = None, ca_data: bytes | None = None,
                       insecure: bool = False, namespace: str | None = None, exec_cfg: dict | None = None,
                       client_cert_data: bytes | None = None, client_key_data: bytes | None = None,
-                      tls_server_name: str | None = None) -> str:
+                      tls_server_name: str | None = None, proxy_url: str | None = None) -> str:
     """Write a minimal single-context kubeconfig (used by tests, benches and the Helm README example)."""
     cluster = {"server": server}
     if ca_data:
@@ -169,6 +172,8 @@ def render_kubeconfig(server: str, name: str, *, token: str | None = None, ca_da
         cluster["insecure-skip-tls-verify"] = True
     if tls_server_name:
         cluster["tls-server-name"] = tls_server_name
+    if proxy_url:
+        cluster["proxy-url"] = proxy_url
     user: dict = {}
     if client_cert_data and client_key_data:  # x509 client auth, as in a kind cluster's admin kubeconfig
         user["client-certificate-data"] = base64.b64encode(client_cert_data).decode()

@@ -44,6 +44,7 @@ from . import errors as E
 from . import h2client
 from .client import PATCH_MERGE, KubeClient, WatchEvent
 from .kubeconfig import ClusterConfig, CredentialSource
+from .proxy import proxy_for
 from .transport import ConnectionPool
 
 USER_AGENT = "nexus-configuration-controller/ncc (linux/amd64)"
@@ -118,6 +119,8 @@ class RestClient(KubeClient):
         self._session: aiohttp.ClientSession | None = None
         self._session_lock = asyncio.Lock()
         self.stats = {"requests": 0, "retries": 0, "errors": 0, "watch_streams": 0}
+        # kubeconfig proxy-url, else client-go's HTTPS_PROXY / HTTP_PROXY / NO_PROXY (ncc/kube/proxy.py)
+        self.proxy = proxy_for(cfg.server, cfg.proxy_url)
 
     async def _get_session(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
@@ -141,7 +144,7 @@ class RestClient(KubeClient):
                     ctx = _ssl_context(self.cfg, exec_cert)
                     kw = dict(ssl_context=ctx or None, server_hostname=self.cfg.tls_server_name,
                               max_size=self.pool_size, connect_timeout=self.request_timeout,
-                              pipeline_depth=self.pipeline_depth)
+                              pipeline_depth=self.pipeline_depth, proxy=self.proxy)
                     tls = self.cfg.server.startswith("https:")
                     if h2client.AVAILABLE and (self.http2 == "on" or (self.http2 == "auto" and tls)):
                         # client-go's transport: HTTP/2 negotiated by ALPN (prior knowledge on cleartext with "on")
@@ -168,7 +171,7 @@ class RestClient(KubeClient):
             return resp.status, resp.body, resp.headers.get("retry-after")
         session = await self._get_session()
         try:
-            async with session.request(method, self.cfg.server + target, data=data, headers=headers,
+            async with session.request(method, self.cfg.server + target, data=data, headers=headers, proxy=self.proxy,
                                        timeout=aiohttp.ClientTimeout(total=self.request_timeout)) as resp:
                 raw = await resp.read()
                 return resp.status, raw, resp.headers.get("Retry-After")
@@ -401,7 +404,7 @@ class RestClient(KubeClient):
         client_timeout = aiohttp.ClientTimeout(total=(timeout_seconds + 30) if timeout_seconds else None,
                                                sock_connect=self.request_timeout)
         try:
-            async with session.get(url, headers=headers, timeout=client_timeout) as resp:
+            async with session.get(url, headers=headers, timeout=client_timeout, proxy=self.proxy) as resp:
                 if resp.status >= 300:
                     raw = await resp.read()
                     try:

@@ -344,8 +344,10 @@ class _Conn(asyncio.Protocol):
 
 class ConnectionPool:
     def __init__(self, server: str, *, ssl_context: _ssl.SSLContext | None = None, server_hostname: str | None = None,
-                 max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1):
+                 max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1,
+                 proxy: str | None = None):
         u = urlsplit(server)
+        self.proxy = proxy  # an HTTP CONNECT proxy (ncc/kube/proxy.py) every connection tunnels through
         self.scheme = u.scheme
         self.host = u.hostname or "127.0.0.1"
         self.port = u.port or (443 if u.scheme == "https" else 80)
@@ -372,8 +374,13 @@ class ConnectionPool:
             kw["ssl"] = self.ssl
             kw["server_hostname"] = self.server_hostname or self.host
         try:
-            _, proto = await wait_timeout(
-                loop.create_connection(lambda: _Conn(self), self.host, self.port, **kw), self.connect_timeout)
+            if self.proxy:
+                from .proxy import open_tunnel
+                sock = await open_tunnel(self.proxy, self.host, self.port, self.connect_timeout)
+                coro = loop.create_connection(lambda: _Conn(self), sock=sock, **kw)
+            else:
+                coro = loop.create_connection(lambda: _Conn(self), self.host, self.port, **kw)
+            _, proto = await wait_timeout(coro, self.connect_timeout)
         except (OSError, asyncio.TimeoutError, _ssl.SSLError) as e:
             raise E.TransportError(f"connect {self.host}:{self.port}: {type(e).__name__}: {e}") from e
         self.opened += 1
