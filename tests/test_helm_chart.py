@@ -123,6 +123,28 @@ def test_health_port_datadog_and_extras():
     assert dep["metadata"]["labels"]["team"] == "ml"
 
 
+def test_metrics_port_service_and_service_monitor():
+    """ncc extension: `controller.metricsBindAddress` opens a `metrics` container port; `metrics.service` puts
+    it behind a Service and `metrics.serviceMonitor` adds a Prometheus-operator ServiceMonitor for it."""
+    assert not [d for d in _docs({}) if d["kind"] in ("Service", "ServiceMonitor")]  # off by default
+    docs = _docs({"controller": {"metricsBindAddress": ":9090", "healthBindAddress": ":8081"},
+                  "metrics": {"service": {"enabled": True},
+                              "serviceMonitor": {"enabled": True, "interval": "15s",
+                                                 "additionalLabels": {"release": "prom"}}}})
+    c = _one(docs, "Deployment")["spec"]["template"]["spec"]["containers"][0]
+    assert c["ports"] == [{"name": "health", "containerPort": 8081}, {"name": "metrics", "containerPort": 9090}]
+    svc, sm = _one(docs, "Service"), _one(docs, "ServiceMonitor")
+    assert svc["spec"]["ports"] == [{"name": "metrics", "port": 9090, "targetPort": "metrics"}]
+    dep_labels = _one(docs, "Deployment")["spec"]["selector"]["matchLabels"]
+    assert svc["spec"]["selector"] == dep_labels
+    assert sm["spec"]["endpoints"] == [{"port": "metrics", "path": "/metrics", "interval": "15s"}]
+    assert sm["metadata"]["labels"]["release"] == "prom" and sm["spec"]["selector"]["matchLabels"] == dep_labels
+    # the metrics port alone (no health address): ports without probes
+    c = _one(_docs({"controller": {"metricsBindAddress": "0.0.0.0:9100", "healthBindAddress": ""}}),
+             "Deployment")["spec"]["template"]["spec"]["containers"][0]
+    assert c["ports"] == [{"name": "metrics", "containerPort": 9100}] and "livenessProbe" not in c
+
+
 def test_names_and_switches():
     docs = _docs({"fullnameOverride": "ncc", "serviceAccount": {"create": False, "name": "existing"},
                   "rbac": {"clusterRoleBindings": {"create": False},
