@@ -704,6 +704,8 @@ async def run(args, d: Dist) -> dict | None:
                 # timed step commits a staged wave (the load generator's request is not the system under test)
                 for v in range(1, total + 1):
                     await post(session, f"{ctrl_url}/_fake/stage", wave_body(T, v, args.payload, stage_id=v))
+                    if total > 200 and v % 100 == 0:  # a long soak: a sign of life while it stages
+                        print(f"# staged {v}/{total} waves", file=sys.stderr, flush=True)
 
             async def converge(version: int, times: bool, url=None):
                 if url is None and S > 1:  # every shard this rank hosts; times keyed per shard
@@ -762,6 +764,8 @@ async def run(args, d: Dist) -> dict | None:
                               f"p50 {(ts[len(ts) // 2] - t0) / 1e6:.1f} last {(ts[-1] - t0) / 1e6:.1f} ms",
                               file=sys.stderr)
                 d.barrier()  # the wave is done only when every shard has converged
+                if total > 200 and step % 100 == 0 and d.rank == 0:
+                    print(f"# wave {step}/{total}", file=sys.stderr, flush=True)
             d.sync()
             elapsed = time.perf_counter() - t_start
             placed = placement.stop() if placement is not None else None
