@@ -61,7 +61,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 25
+#define NCC_NATIVE_ABI 26
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -2505,13 +2505,15 @@ private:
 // responses, the stream limit, GOAWAY, dispatch.
 class H2ServerParser {
 public:
-    explicit H2ServerParser(bool credit_data) : credit_(credit_data) {}
+    explicit H2ServerParser(bool credit_data, int64_t conn_credit_at = int64_t{1} << 29)
+        : credit_(credit_data), conn_credit_at_(conn_credit_at) {}
 
     // Feed received bytes; returns the events they complete, in order:
     //   ("req", sid, method, path, {lower-cased name: value}, body)  a request whose END_STREAM arrived
     //   ("settings", [(id, value), ...])                              a SETTINGS frame to apply and ack
     //   ("window", sid, increment)   ("rst", sid, code)   ("ping", payload)   ("goaway", last, code)
-    //   ("credit", sid, n)            DATA consumed (only with credit_data: a small advertised window)
+    //   ("credit", sid, n)            DATA consumed (with credit_data, a small advertised window: per frame and
+    //                                 stream; always, for the connection (sid 0), once half its 1 GiB is used)
     //   ("error", code, message)      a connection error: send GOAWAY and close
     py::list feed(const py::bytes& data) {
         std::string_view d = data;
@@ -2546,6 +2548,8 @@ private:
     std::string buf_;
     size_t pos_ = 0;
     bool preface_ = false, credit_;
+    int64_t conn_unacked_ = 0;  // DATA bytes read since the last connection-level credit
+    int64_t conn_credit_at_;
     uint32_t last_stream_ = 0, cont_id_ = 0;
     bool cont_end_ = false;
     std::string cont_block_;
@@ -2627,6 +2631,13 @@ private:
             switch (type) {
                 case 0: {  // DATA
                     if (credit_ && len > 0) out.append(py::make_tuple("credit", sid, len));
+                    // the connection window the server opened to 1 GiB is given back as it is used: without this
+                    // a client stops sending request bodies after 1 GiB of them (a soak of ~300 bench waves)
+                    conn_unacked_ += len;
+                    if (conn_unacked_ >= conn_credit_at_) {
+                        out.append(py::make_tuple("credit", 0, conn_unacked_));
+                        conn_unacked_ = 0;
+                    }
                     std::string_view d = strip(flags, pl, false);
                     auto it = streams_.find(sid);
                     if (it == streams_.end() || it->second.ended) {
@@ -3120,7 +3131,7 @@ PYBIND11_MODULE(_native, m) {
         .def("table_size", &HpackDecoder::table_size)
         .def("table_entries", &HpackDecoder::table_entries);
     py::class_<H2ServerParser>(m, "H2ServerParser")
-        .def(py::init<bool>(), py::arg("credit_data") = false)
+        .def(py::init<bool, int64_t>(), py::arg("credit_data") = false, py::arg("conn_credit_at") = int64_t{1} << 29)
         .def("feed", &H2ServerParser::feed, py::arg("data"))
         .def("open_streams", &H2ServerParser::open_streams);
     m.def("h2_response", &h2_response, py::arg("sid"), py::arg("status"), py::arg("content_type"), py::arg("body"),

@@ -136,9 +136,9 @@ class H2Connection:
                     if s is not None:
                         s.send_window += inc
                         self._flush(s)
-            elif kind == "credit":  # small-window mode: credit what the client's DATA consumed
+            elif kind == "credit":  # DATA consumed: a stream's (small-window mode), or the connection's (sid 0)
                 self._out(frame(WINDOW_UPDATE, 0, ev[1], struct.pack(">I", ev[2])))
-                if self.small_conn_window:
+                if self.small_conn_window and ev[1] != 0:
                     self._out(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", ev[2])))
             elif kind == "settings":
                 for ident, value in ev[1]:

@@ -353,6 +353,11 @@ def test_server_parser_assembles_streams_from_any_framing():
     assert p.open_streams() == 0
     bad = _m.H2ServerParser(False)
     assert bad.feed(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")[0][0] == "error"
+    # the connection window is given back as request bodies use it (a soak once stalled after 1 GiB of them)
+    cp = _m.H2ServerParser(False, 1000)
+    hdr = h2.frame(h2.HEADERS, h2.END_HEADERS, 1, block)
+    ev = cp.feed(h2.PREFACE + hdr + b"".join(h2.frame(h2.DATA, 0, 1, b"x" * 600) for _ in range(3)))
+    assert ("credit", 0, 1200) in ev and [e for e in ev if e[0] == "credit"] == [("credit", 0, 1200)]
     resp = _m.h2_response(5, 200, "application/json", b"x" * 40000, [("retry-after", "1")], 16384)
     d = _m.HpackDecoder()
     n = int.from_bytes(resp[:3], "big")
