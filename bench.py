@@ -27,6 +27,7 @@ import base64
 import json
 import os
 import shutil
+import signal
 import statistics
 import subprocess
 import sys
@@ -945,6 +946,9 @@ def main():
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {d.world}; using WORLD_SIZE", file=sys.stderr)
     if d.world == 1 and args.gpus > 1:
         raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
+    # a SIGTERM (a `timeout` around the run) unwinds like an exception, so `run`'s cleanup stops the fake
+    # apiservers and the controller instead of leaving the controller and its executors behind
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
     try:
         res = asyncio.run(run(args, d))
     finally:
