@@ -1836,6 +1836,7 @@ private:
             };
             st.id = s->next_id;
             s->next_id += 2;
+            if (s->next_id >= 0x7ffffff0u) s->goaway = true;  // stream ids spent: drain, then close (h2_read)
             s->streams[st.id] = &st;
             ++h2_streams;
             h2_headers_out(*s, st.id, "GET", target, nullptr, nullptr);
@@ -1893,6 +1894,7 @@ private:
             st.body = body;
             st.id = s->next_id;
             s->next_id += 2;
+            if (s->next_id >= 0x7ffffff0u) s->goaway = true;  // stream ids spent: drain, then close (h2_read)
             s->streams[st.id] = &st;
             ++h2_streams;
             h2_headers_out(*s, st.id, method, target, body, content_type);

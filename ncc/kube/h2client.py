@@ -74,6 +74,7 @@ class _Retry(Exception):
         self.refused = refused
 
 
+MAX_STREAM_ID = 0x7FFFFFF0  # a connection's client stream ids run out below 2^31 (RFC 9113 §5.1.1)
 MAX_UNPROCESSED_RETRIES = 16  # re-sends of a request no server processed (a GOAWAY each time is progress elsewhere)
 
 
@@ -292,6 +293,8 @@ class _H2Conn(asyncio.Protocol):
              watch: bool = False) -> _Stream:
         sid = self.next_sid
         self.next_sid += 2
+        if self.next_sid >= MAX_STREAM_ID:
+            self.draining = True  # stream ids spent (2^31): no new streams here; closed once these finish
         fut = asyncio.get_running_loop().create_future()
         st = _Stream(sid, fut, what, self.peer_window, watch)
         self.streams[sid] = st

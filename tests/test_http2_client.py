@@ -422,3 +422,21 @@ async def test_stream_resets_refusals_and_early_watch_exit():
         pool.close()
         server.close()
         await server.wait_closed()
+
+
+async def test_a_connection_whose_stream_ids_run_out_is_replaced():
+    """Client stream ids are odd and below 2^31: a long-lived connection (≈ 7 h at 40 000 requests/s) runs out.
+    The pool stops opening streams on it, moves to a new connection and closes the old one once drained."""
+    async with _Server() as (srv, url):
+        pool = h2client.H2Pool(url, prior_knowledge=True, connect_timeout=5)
+        try:
+            hdr = {"Accept": "application/json"}
+            assert (await pool.request("GET", "/api/v1/namespaces/nexus/secrets", hdr, None)).status == 200
+            first = pool.conns[0]
+            first.next_sid = h2client.MAX_STREAM_ID - 2  # as after ~1e9 streams
+            assert (await pool.request("GET", "/api/v1/namespaces/nexus/secrets", hdr, None)).status == 200
+            assert first.draining and first.closed  # its last stream served, then closed
+            assert (await pool.request("GET", "/api/v1/namespaces/nexus/configmaps", hdr, None)).status == 200
+            assert pool.opened == 2 and pool.conns and pool.conns[0] is not first
+        finally:
+            pool.close()
