@@ -2383,6 +2383,8 @@ static Credentials creds_of(const Value& s) {
     c.password = std::string(s.sget("password"));
     c.proxy = std::string(s.sget("proxy"));
     c.proxy_connect = std::string(s.sget("proxy_connect"));
+    c.proxy_user = std::string(s.sget("proxy_user"));
+    c.proxy_pass = std::string(s.sget("proxy_pass"));
     return c;
 }
 

@@ -114,8 +114,9 @@ struct Credentials {
     std::string token, token_file;
     std::string username, password;
     // an HTTP CONNECT proxy (kubeconfig proxy-url, or client-go's HTTPS_PROXY rules: ncc/kube/proxy.py) and the
-    // CONNECT request the coordinator rendered for it (proxy credentials included)
-    std::string proxy, proxy_connect;
+    // CONNECT request the coordinator rendered for it (proxy credentials included); a socks5:// proxy's
+    // username/password (RFC 1929) travel on their own
+    std::string proxy, proxy_connect, proxy_user, proxy_pass;
 };
 
 struct Url {
@@ -158,11 +159,37 @@ inline Url parse_url(const std::string& s) {
     return u;
 }
 
-// The tunnel a connection opens first: the proxy's address and the CONNECT request to send it.
+// The tunnel a connection opens first: the proxy's address and the CONNECT request to send it, or a SOCKS5
+// proxy (RFC 1928) and its credentials.
 struct Proxy {
     Url url;
     std::string connect;
+    bool socks = false;
+    std::string user, pass;
 };
+
+// RFC 1928 CONNECT for `host:port`: an IPv4/IPv6 address as such, a name as a domain the proxy resolves (as Go's
+// SOCKS5 dialer sends them).
+inline std::string socks5_connect(const std::string& host, int port) {
+    std::string m("\x05\x01\x00", 3);
+    in_addr a4;
+    in6_addr a6;
+    if (inet_pton(AF_INET, host.c_str(), &a4) == 1) {
+        m += '\x01';
+        m.append(reinterpret_cast<const char*>(&a4), 4);
+    } else if (inet_pton(AF_INET6, host.c_str(), &a6) == 1) {
+        m += '\x04';
+        m.append(reinterpret_cast<const char*>(&a6), 16);
+    } else {
+        if (host.size() > 255) throw TransportError("socks5: host name too long");
+        m += '\x03';
+        m += static_cast<char>(host.size());
+        m += host;
+    }
+    m += static_cast<char>((port >> 8) & 0xff);
+    m += static_cast<char>(port & 0xff);
+    return m;
+}
 
 inline bool is_ip(const std::string& h) {
     in6_addr a6;
@@ -308,7 +335,44 @@ public:
             getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
             if (err != 0) throw TransportError("connect " + dial.host + ":" + port + ": " + std::strerror(err));
         }
-        if (proxy != nullptr) {  // the tunnel: CONNECT answered 200, nothing after the answer's head
+        if (proxy != nullptr && proxy->socks) {  // RFC 1928 / 1929, one step at a time
+            const std::string where = "socks5 proxy " + dial.host + ":" + port;
+            const bool auth = !proxy->user.empty();
+            std::string hello = auth ? std::string("\x05\x02\x00\x02", 4) : std::string("\x05\x01\x00", 3);
+            co_await write_all(hello);
+            co_await need(2);
+            const auto method = static_cast<unsigned char>(buf[pos + 1]);
+            if (buf[pos] != 5 || !(method == 0 || (method == 2 && auth)))
+                throw TransportError(where + " refused every authentication method offered");
+            pos += 2;
+            if (method == 2) {
+                if (proxy->user.size() > 255 || proxy->pass.size() > 255)
+                    throw TransportError(where + ": credentials longer than 255 bytes");
+                std::string up("\x01", 1);
+                up += static_cast<char>(proxy->user.size());
+                up += proxy->user;
+                up += static_cast<char>(proxy->pass.size());
+                up += proxy->pass;
+                co_await write_all(up);
+                co_await need(2);
+                if (buf[pos + 1] != 0) throw TransportError(where + " rejected the username/password");
+                pos += 2;
+            }
+            std::string req = socks5_connect(u.host, u.port);
+            co_await write_all(req);
+            co_await need(5);  // VER REP RSV ATYP and the address's first byte
+            const auto rep = static_cast<unsigned char>(buf[pos + 1]);
+            if (buf[pos] != 5 || rep != 0)
+                throw TransportError(where + " refused CONNECT to " + u.host + ": reply " + std::to_string(rep));
+            const auto atyp = static_cast<unsigned char>(buf[pos + 3]);
+            size_t total = atyp == 1 ? 4 + 4 + 2 : atyp == 4 ? 4 + 16 + 2
+                         : 4 + 1 + static_cast<unsigned char>(buf[pos + 4]) + 2;
+            co_await need(total);  // the bound address and port: unused
+            pos += total;
+            if (pos != buf.size()) throw TransportError(where + " sent data before the tunnel was used");
+            buf.clear();
+            pos = 0;
+        } else if (proxy != nullptr) {  // the tunnel: CONNECT answered 200, nothing after the answer's head
             co_await write_all(proxy->connect);
             size_t end;
             while ((end = buf.find("\r\n\r\n", pos)) == std::string::npos) {
@@ -360,6 +424,9 @@ public:
     }
 
     // Read more bytes into `buf`; throws on EOF/error.
+    Task<void> need(size_t n) {  // at least `n` unread bytes in `buf`
+        while (buf.size() - pos < n) co_await fill();
+    }
     Task<void> fill() {
         if (pos > 0 && pos == buf.size()) {
             buf.clear();
@@ -722,8 +789,14 @@ public:
         h2_mode_ = http2;
         h2_ok_ = http2 == 2 || (http2 == 1 && url_.tls);
         if (!creds_.proxy.empty()) {
-            proxy_.url = parse_url(creds_.proxy);
+            const std::string& p = creds_.proxy;
+            size_t sep = p.find("://");
+            proxy_.socks = p.rfind("socks5", 0) == 0;  // socks5:// and socks5h://: the proxy resolves names
+            proxy_.url = proxy_.socks ? parse_url("http://" + p.substr(sep + 3)) : parse_url(p);
+            if (proxy_.socks && p.find(':', sep + 3) == std::string::npos) proxy_.url.port = 1080;
             proxy_.connect = creds_.proxy_connect;
+            proxy_.user = creds_.proxy_user;
+            proxy_.pass = creds_.proxy_pass;
             has_proxy_ = true;
         }
         // client-go's HTTP/2 health check, same variables and defaults: a connection with streams open that read

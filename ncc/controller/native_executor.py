@@ -76,7 +76,7 @@ def _file_digest(path: str) -> str:
 def proxy_entry(cc) -> dict:
     """The shard's proxy for the C++ executor: its URL and the CONNECT request (credentials included), rendered
     here so the executor needs no URL or base64 handling of its own (ncc/kube/proxy.py)."""
-    from urllib.parse import urlsplit
+    from urllib.parse import unquote, urlsplit
 
     from ..kube.proxy import connect_request, proxy_for
     proxy = proxy_for(cc.server, cc.proxy_url)
@@ -84,6 +84,10 @@ def proxy_entry(cc) -> dict:
         return {}
     u, p = urlsplit(cc.server), urlsplit(proxy)
     phost = f"[{p.hostname}]" if p.hostname and ":" in p.hostname else (p.hostname or "")
+    if p.scheme in ("socks5", "socks5h"):  # the executor runs the SOCKS5 handshake itself (http.hpp Conn::connect)
+        return {"proxy": f"socks5://{phost}:{p.port or 1080}",
+                "proxy_user": unquote(p.username) if p.username is not None else "",
+                "proxy_pass": unquote(p.password or "")}
     # the credentials travel in the rendered request only
     return {"proxy": f"http://{phost}:{p.port or 80}",
             "proxy_connect": connect_request(proxy, u.hostname or "",

@@ -8,7 +8,9 @@ kube-apiserver is reached through the proxy with an HTTP CONNECT tunnel, and TLS
 `proxy_for` picks the proxy for a server URL by those rules; `open_tunnel` opens the CONNECT tunnel and hands
 back the connected socket, which the connection pools then wrap (`ncc/kube/transport.py`, `h2client.py`).
 The C++ shard executor is given the same proxy URL by the coordinator and opens the same tunnel
-(`native/executor/http.hpp` `Conn::connect`).  Only `http://` proxies are supported (no socks5).
+(`native/executor/http.hpp` `Conn::connect`).  `socks5://` (and `socks5h://`) proxies are supported as Go's
+transport supports them (RFC 1928, username/password authentication RFC 1929): the target's IP address when it
+is one, its name for the proxy to resolve otherwise.
 """
 from __future__ import annotations
 
@@ -96,12 +98,63 @@ def connect_request(proxy: str, host: str, port: int) -> bytes:
     return (head + "\r\n").encode("latin-1")
 
 
+def socks5_connect_request(host: str, port: int) -> bytes:
+    """RFC 1928 CONNECT: an IPv4/IPv6 address as such, a name as a domain (the proxy resolves it)."""
+    h = host.strip("[]")
+    try:
+        ip = ipaddress.ip_address(h)
+        addr = (b"\x01" if ip.version == 4 else b"\x04") + ip.packed
+    except ValueError:
+        name = h.encode("idna")
+        if len(name) > 255:
+            raise E.TransportError(f"socks5: host name too long: {h[:64]}...")
+        addr = b"\x03" + bytes([len(name)]) + name
+    return b"\x05\x01\x00" + addr + port.to_bytes(2, "big")
+
+
+async def _socks5_handshake(loop, sock, p, host: str, port: int, timeout: float) -> None:
+    where = f"socks5 proxy {p.hostname}:{p.port or 1080}"
+
+    async def exactly(n: int) -> bytes:
+        out = b""
+        while len(out) < n:
+            chunk = await wait_timeout(loop.sock_recv(sock, n - len(out)), timeout)
+            if not chunk:
+                raise E.TransportError(f"{where} closed the connection during the handshake")
+            out += chunk
+        return out
+
+    user = unquote(p.username) if p.username is not None else None
+    await wait_timeout(loop.sock_sendall(sock, b"\x05\x02\x00\x02" if user is not None else b"\x05\x01\x00"),
+                       timeout)
+    ver, method = await exactly(2)
+    if ver != 5 or method == 0xFF or (method == 2 and user is None) or method not in (0, 2):
+        raise E.TransportError(f"{where} refused every authentication method offered (chose {method:#x})")
+    if method == 2:
+        u, pw = user.encode(), unquote(p.password or "").encode()
+        if len(u) > 255 or len(pw) > 255:
+            raise E.TransportError(f"{where}: credentials longer than 255 bytes")
+        await wait_timeout(loop.sock_sendall(sock, b"\x01" + bytes([len(u)]) + u + bytes([len(pw)]) + pw), timeout)
+        if (await exactly(2))[1] != 0:
+            raise E.TransportError(f"{where} rejected the username/password")
+    await wait_timeout(loop.sock_sendall(sock, socks5_connect_request(host, port)), timeout)
+    ver, rep, _, atyp = await exactly(4)
+    if ver != 5 or rep != 0:
+        raise E.TransportError(f"{where} refused CONNECT {host}:{port}: reply {rep:#x}")
+    alen = {1: 4, 4: 16}.get(atyp)
+    if alen is None:
+        alen = (await exactly(1))[0]
+    await exactly(alen + 2)  # the bound address and port: unused
+
+
 async def open_tunnel(proxy: str, host: str, port: int, timeout: float) -> socket.socket:
-    """A socket connected through `proxy` to `host:port` (CONNECT answered 200), ready for TLS or HTTP."""
+    """A socket connected through `proxy` to `host:port` (CONNECT answered 200, or the SOCKS5 handshake done),
+    ready for TLS or HTTP."""
     p = urlsplit(proxy)
-    if p.scheme not in ("http", ""):
-        raise E.TransportError(f"proxy {proxy}: only http:// (CONNECT) proxies are supported")
-    phost, pport = p.hostname or "", p.port or 80
+    socks = p.scheme in ("socks5", "socks5h")
+    if p.scheme not in ("http", "") and not socks:
+        raise E.TransportError(f"proxy {proxy}: only http:// (CONNECT) and socks5:// proxies are supported")
+    phost, pport = p.hostname or "", p.port or (1080 if socks else 80)
     loop = asyncio.get_running_loop()
     try:
         infos = await wait_timeout(loop.getaddrinfo(phost, pport, type=socket.SOCK_STREAM), timeout)
@@ -112,6 +165,9 @@ async def open_tunnel(proxy: str, host: str, port: int, timeout: float) -> socke
     sock.setblocking(False)
     try:
         await wait_timeout(loop.sock_connect(sock, addr), timeout)
+        if socks:
+            await _socks5_handshake(loop, sock, p, host, port, timeout)
+            return sock
         await wait_timeout(loop.sock_sendall(sock, connect_request(proxy, host, port)), timeout)
         buf = b""
         while b"\r\n\r\n" not in buf:

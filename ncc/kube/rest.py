@@ -121,6 +121,8 @@ class RestClient(KubeClient):
         self.stats = {"requests": 0, "retries": 0, "errors": 0, "watch_streams": 0}
         # kubeconfig proxy-url, else client-go's HTTPS_PROXY / HTTP_PROXY / NO_PROXY (ncc/kube/proxy.py)
         self.proxy = proxy_for(cfg.server, cfg.proxy_url)
+        if self.proxy and self.proxy.startswith("socks") and transport != "fast":
+            raise ValueError("a socks5 proxy needs the fast transport (aiohttp speaks only http:// proxies)")
 
     async def _get_session(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:

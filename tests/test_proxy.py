@@ -4,7 +4,9 @@
 * `proxy_for`'s rules, including Go's NO_PROXY forms (domains, leading dots, IPs, CIDRs, ports, `*`);
 * the Python clients through a proxy to a TLS apiserver, over HTTP/2 (ALPN inside the tunnel) and HTTP/1.1,
   with proxy credentials, and a proxy that refuses;
-* the C++ shard executor through a proxy (the coordinator renders the CONNECT request for it).
+* the C++ shard executor through a proxy (the coordinator renders the CONNECT request for it);
+* the same over a SOCKS5 proxy (RFC 1928, username/password per RFC 1929), as Go's transport dials
+  `socks5://` proxy URLs.
 """
 import asyncio
 import base64
@@ -15,7 +17,7 @@ import pytest
 from ncc.api import resources as R
 from ncc.kube import errors as E
 from ncc.kube.kubeconfig import load_kubeconfig
-from ncc.kube.proxy import connect_request, proxy_for
+from ncc.kube.proxy import connect_request, proxy_for, socks5_connect_request
 from ncc.kube.rest import RestClient
 from ncc.testing.env import FakeEnvironment
 from ncc.testing.workload import make_configmap, make_secret, make_template
@@ -57,23 +59,76 @@ class ConnectProxy:
         self.tunnels += 1
         self.targets.append(target)
         w.write(b"HTTP/1.1 200 Connection established\r\n\r\n")
+        await asyncio.gather(self._pump(r, uw), self._pump(ur, w))
 
-        async def pump(src, dst):
-            try:
-                while True:
-                    data = await src.read(65536)
-                    if not data:
-                        break
-                    dst.write(data)
-                    await dst.drain()
-            except (ConnectionError, asyncio.CancelledError):
-                pass
-            finally:
-                dst.close()
-        await asyncio.gather(pump(r, uw), pump(ur, w))
+    @staticmethod
+    async def _pump(src, dst):
+        try:
+            while True:
+                data = await src.read(65536)
+                if not data:
+                    break
+                dst.write(data)
+                await dst.drain()
+        except (ConnectionError, asyncio.CancelledError):
+            pass
+        finally:
+            dst.close()
 
     async def stop(self):
         self.server.close()
+
+
+class Socks5Proxy:
+    """A minimal SOCKS5 proxy (CONNECT only): username/password when `auth` ("user:pass") is set, else none."""
+
+    def __init__(self, auth: str | None = None):
+        self.auth, self.tunnels, self.targets, self.server = auth, 0, [], None
+
+    async def start(self) -> str:
+        self.server = await asyncio.start_server(self._handle, "127.0.0.1", 0)
+        return f"socks5://127.0.0.1:{self.server.sockets[0].getsockname()[1]}"
+
+    async def _handle(self, r, w):
+        try:
+            ver, n = await r.readexactly(2)
+            methods = await r.readexactly(n)
+            want = 2 if self.auth is not None else 0
+            if ver != 5 or want not in methods:
+                w.write(b"\x05\xff")
+                w.close()
+                return
+            w.write(bytes([5, want]))
+            if want == 2:
+                _, ulen = await r.readexactly(2)
+                user = await r.readexactly(ulen)
+                pw = await r.readexactly((await r.readexactly(1))[0])
+                ok = f"{user.decode()}:{pw.decode()}" == self.auth
+                w.write(b"\x01" + (b"\x00" if ok else b"\x01"))
+                if not ok:
+                    w.close()
+                    return
+            _, cmd, _, atyp = await r.readexactly(4)
+            if atyp == 3:
+                host = (await r.readexactly((await r.readexactly(1))[0])).decode()
+            else:
+                import ipaddress
+                host = str(ipaddress.ip_address(await r.readexactly(4 if atyp == 1 else 16)))
+            port = int.from_bytes(await r.readexactly(2), "big")
+        except (asyncio.IncompleteReadError, ConnectionError):
+            w.close()
+            return
+        ur, uw = await asyncio.open_connection(host, port)
+        self.tunnels += 1
+        self.targets.append(f"{host}:{port}")
+        w.write(b"\x05\x00\x00\x01\x7f\x00\x00\x01\x00\x00")
+        await asyncio.gather(ConnectProxy._pump(r, uw), ConnectProxy._pump(ur, w))
+
+    async def stop(self):
+        self.server.close()
+
+
+PROXIES = {"connect": ConnectProxy, "socks5": Socks5Proxy}
 
 
 def test_proxy_for_follows_client_go():
@@ -97,16 +152,21 @@ def test_proxy_for_follows_client_go():
     req = connect_request("http://u%40x:p%3Aw@p:1", "k8s.example", 443).decode()
     assert req.startswith("CONNECT k8s.example:443 HTTP/1.1\r\nHost: k8s.example:443\r\n")
     assert "Proxy-Authorization: Basic " + base64.b64encode(b"u@x:p:w").decode() in req
+    assert proxy_for("https://k8s.example", environ={"HTTPS_PROXY": "socks5://s:1080"}) == "socks5://s:1080"
+    assert socks5_connect_request("10.0.0.1", 443) == b"\x05\x01\x00\x01\x0a\x00\x00\x01\x01\xbb"
+    assert socks5_connect_request("[::1]", 6443)[3:4] == b"\x04"
+    assert socks5_connect_request("k8s.example", 443) == b"\x05\x01\x00\x03\x0bk8s.example\x01\xbb"
 
 
+@pytest.mark.parametrize("kind", sorted(PROXIES))
 @pytest.mark.parametrize("http2", ["auto", "off"])
-async def test_rest_client_through_a_connect_proxy(tmp_path, http2):
+async def test_rest_client_through_a_proxy(tmp_path, http2, kind):
     env = await FakeEnvironment(0, str(tmp_path), tls=True).start()
-    proxy = ConnectProxy(auth="alice:s3cret")
+    proxy = PROXIES[kind](auth="alice:s3cret")
     purl = await proxy.start()
     try:
         cfg = load_kubeconfig(env.controller_kubeconfig)
-        cfg.proxy_url = purl.replace("http://", "http://alice:s3cret@")
+        cfg.proxy_url = purl.replace("://", "://alice:s3cret@")
         c = RestClient(cfg, http2=http2)
         try:
             await c.create(R.SECRETS, NS, make_secret("via-proxy", NS))
@@ -115,10 +175,20 @@ async def test_rest_client_through_a_connect_proxy(tmp_path, http2):
             assert proxy.tunnels >= 1 and all(t.endswith(env.controller_url.rsplit(":", 1)[1]) for t in proxy.targets)
         finally:
             await c.close()
-        cfg.proxy_url = purl.replace("http://", "http://alice:wrong@")
+        if kind == "socks5":  # aiohttp dials only http:// proxies: refused up front, not at the first request
+            with pytest.raises(ValueError, match="socks5"):
+                RestClient(cfg, transport="aiohttp")
+            cfg.proxy_url = purl  # a proxy that wants credentials, offered none
+            c = RestClient(cfg, http2=http2, max_retries=0)
+            try:
+                with pytest.raises(E.TransportError, match="authentication method"):
+                    await c.list(R.SECRETS, NS)
+            finally:
+                await c.close()
+        cfg.proxy_url = purl.replace("://", "://alice:wrong@")
         c = RestClient(cfg, http2=http2, max_retries=0)
         try:
-            with pytest.raises(E.TransportError, match="refused CONNECT"):
+            with pytest.raises(E.TransportError, match="refused CONNECT" if kind == "connect" else "rejected"):
                 await c.list(R.SECRETS, NS)
         finally:
             await c.close()
@@ -127,15 +197,16 @@ async def test_rest_client_through_a_connect_proxy(tmp_path, http2):
         await env.stop()
 
 
+@pytest.mark.parametrize("kind", sorted(PROXIES))
 @pytest.mark.parametrize("http2", ["auto", "off"])
-async def test_shard_executor_through_a_connect_proxy(tmp_path, monkeypatch, http2):
+async def test_shard_executor_through_a_proxy(tmp_path, monkeypatch, http2, kind):
     from ncc.app import App
     from ncc.controller.native_executor import binary_path
     if binary_path() is None:
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.setenv("NCC_STATUS_S", "0.2")
     env = await FakeEnvironment(1, str(tmp_path), tls=True).start()
-    proxy = ConnectProxy(auth="exec:pw")
+    proxy = PROXIES[kind](auth="exec:pw")
     purl = await proxy.start()
     cc = env.controller_client()
     stop, task = asyncio.Event(), None
@@ -144,7 +215,7 @@ async def test_shard_executor_through_a_connect_proxy(tmp_path, monkeypatch, htt
         with open(kc) as f:
             text = f.read()
         with open(kc, "w") as f:  # the shard's kubeconfig names the proxy, with credentials
-            f.write(text.replace("    server:", f"    proxy-url: {purl.replace('http://', 'http://exec:pw@')}\n"
+            f.write(text.replace("    server:", f"    proxy-url: {purl.replace('://', '://exec:pw@')}\n"
                                               "    server:", 1))
         assert load_kubeconfig(kc).proxy_url
         await cc.create(R.SECRETS, NS, make_secret("s0", NS))
