@@ -197,7 +197,7 @@ async def test_rest_client_through_a_proxy(tmp_path, http2, kind):
         await env.stop()
 
 
-@pytest.mark.parametrize("kind", sorted(PROXIES))
+@pytest.mark.parametrize("kind", sorted(PROXIES) + ["socks5-open"])
 @pytest.mark.parametrize("http2", ["auto", "off"])
 async def test_shard_executor_through_a_proxy(tmp_path, monkeypatch, http2, kind):
     from ncc.app import App
@@ -206,7 +206,7 @@ async def test_shard_executor_through_a_proxy(tmp_path, monkeypatch, http2, kind
         pytest.skip("ncc/bin/ncc-executor is not built")
     monkeypatch.setenv("NCC_STATUS_S", "0.2")
     env = await FakeEnvironment(1, str(tmp_path), tls=True).start()
-    proxy = PROXIES[kind](auth="exec:pw")
+    proxy = Socks5Proxy() if kind == "socks5-open" else PROXIES[kind](auth="exec:pw")
     purl = await proxy.start()
     cc = env.controller_client()
     stop, task = asyncio.Event(), None
@@ -215,7 +215,7 @@ async def test_shard_executor_through_a_proxy(tmp_path, monkeypatch, http2, kind
         with open(kc) as f:
             text = f.read()
         with open(kc, "w") as f:  # the shard's kubeconfig names the proxy, with credentials
-            f.write(text.replace("    server:", f"    proxy-url: {purl.replace('://', '://exec:pw@')}\n"
+            f.write(text.replace("    server:", f"    proxy-url: {purl if proxy.auth is None else purl.replace('://', '://exec:pw@')}\n"
                                               "    server:", 1))
         assert load_kubeconfig(kc).proxy_url
         await cc.create(R.SECRETS, NS, make_secret("s0", NS))
