@@ -974,7 +974,7 @@ private:
     std::vector<h2::SessionPtr> h2s_;                 // HTTP/2 connections, oldest first
     std::deque<std::coroutine_handle<>> h2_waiters_;  // requests waiting for stream room on one of them
     std::string h2_block_;                            // scratch: the header block being encoded
-    std::string h2_fixed_;                            // :scheme, :authority, user-agent, accept, encoded once
+    std::string h2_pseudo_, h2_fixed_;                // :scheme + :authority, and user-agent + accept, encoded once
     std::string h2_auth_block_, h2_auth_for_;         // the authorization field, encoded for this value
     std::string auth_;                                // memoised Authorization value
     std::string auth_token_;                          // ... for this token
@@ -1825,18 +1825,21 @@ private:
             hpack::encode_indexed(b, 3);
         else
             hpack::encode_literal_indexed_name(b, 2, method);
+        // every pseudo-header before the first regular field (RFC 9113 §8.3; Go's server resets the stream
+        // otherwise): :method :scheme :authority :path, then user-agent, accept
         if (h2_fixed_.empty()) {
-            hpack::encode_indexed(h2_fixed_, url_.tls ? 7 : 6);
-            hpack::encode_literal_indexed_name(h2_fixed_, 1, host_);
+            hpack::encode_indexed(h2_pseudo_, url_.tls ? 7 : 6);
+            hpack::encode_literal_indexed_name(h2_pseudo_, 1, host_);
             hpack::encode_literal_indexed_name(h2_fixed_, 58, kUserAgent);
             hpack::encode_literal_indexed_name(h2_fixed_, 19, "application/json");
         }
-        b += h2_fixed_;
+        b += h2_pseudo_;
         if (url_.prefix.empty()) {
             hpack::encode_literal_indexed_name(b, 4, target);
         } else {
             hpack::encode_literal_indexed_name(b, 4, url_.prefix + target);
         }
+        b += h2_fixed_;
         if (body != nullptr) {
             hpack::encode_literal_indexed_name(b, 31, content_type != nullptr ? content_type : "application/json");
             char num[24];

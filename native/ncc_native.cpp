@@ -61,7 +61,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 26
+#define NCC_NATIVE_ABI 27
 
 // ----------------------------------------------------------------------------- hashing
 namespace {
@@ -2544,6 +2544,7 @@ private:
         std::vector<std::pair<std::string, std::string>> headers;
         std::string body;
         bool have_headers = false, ended = false;
+        bool malformed = false;  // a pseudo-header after a regular field (RFC 9113 §8.3)
     };
     std::string buf_;
     size_t pos_ = 0;
@@ -2576,6 +2577,11 @@ private:
         return p;
     }
     void emit_request(py::list& out, uint32_t sid, Stream& st) {
+        if (st.malformed) {  // as Go's server: the stream is reset with PROTOCOL_ERROR, the connection lives on
+            out.append(py::make_tuple("malformed", sid));
+            streams_.erase(sid);
+            return;
+        }
         py::dict h;
         for (auto& kv : st.headers) h[py::str(kv.first)] = py::str(kv.second);
         if (!h.contains("host") && !st.authority.empty()) h["host"] = py::str(st.authority);
@@ -2595,7 +2601,13 @@ private:
         Stream& st = it->second;
         if (!st.have_headers) {
             st.have_headers = true;
+            bool regular = false;
             for (auto& h : hs) {
+                if (!h.first.empty() && h.first[0] == ':') {
+                    if (regular) st.malformed = true;
+                } else {
+                    regular = true;
+                }
                 if (h.first == ":method")
                     st.method = std::move(h.second);
                 else if (h.first == ":path")

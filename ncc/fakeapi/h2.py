@@ -157,6 +157,9 @@ class H2Connection:
                 st = self.streams.get(ev[1])
                 if st is not None:
                     self._close(st)
+            elif kind == "malformed":  # a pseudo-header after a regular field: Go's server resets the stream
+                self.server.h2_stats["malformed"] += 1
+                self._out(frame(RST_STREAM, 0, ev[1], struct.pack(">I", PROTOCOL_ERROR)))
             elif kind == "rst_closed":  # DATA on a stream that is not open
                 self._out(frame(RST_STREAM, 0, ev[1], struct.pack(">I", STREAM_CLOSED)))
             elif kind == "goaway":

@@ -331,7 +331,7 @@ class HttpServer:
         self.api_conns = self.max_api_conns = 0  # open connections that served a non-watch request; the most at once
         self.http2 = False  # accept HTTP/2: ALPN "h2" on TLS (the context must offer it), prior knowledge on TCP
         self.h2_options: dict = {}  # h2_max_streams, h2_goaway_after (ncc/fakeapi/h2.py)
-        self.h2_stats = {"connections": 0, "streams": 0, "max_open": 0, "refused": 0, "goaways": 0}
+        self.h2_stats = {"connections": 0, "streams": 0, "max_open": 0, "refused": 0, "goaways": 0, "malformed": 0}
 
     def conn_stats(self) -> dict:
         return {"open": len(self._conns), "accepted": self.accepted, "api_open": self.api_conns,

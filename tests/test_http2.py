@@ -161,6 +161,7 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
             # the executor's four watches are streams on the same connection: nothing else is open to the shard
             assert st["open"] <= 2, st
             assert srv.requests["watch_streams"] >= 4
+            assert st["h2"]["malformed"] == 0, st  # every header block well-formed (pseudo-headers first)
         assert all(f["rejected_429"] == 0 for f in fl.values())
         # the same flow status as per-shard gauges (statsd / Prometheus)
         from ncc.api import constants as C
@@ -371,6 +372,13 @@ def test_server_parser_assembles_streams_from_any_framing():
         got += resp[off + 9:off + 9 + n]
         off += 9 + n
     assert got == b"x" * 40000 and flags == [0, 0, h2.END_STREAM]
+    # a pseudo-header after a regular field is a malformed request (RFC 9113 §8.3): Go's server, and this one,
+    # reset that stream and keep the connection
+    late = _m.hpack_encode([(":method", "GET"), (":scheme", "http"), ("user-agent", "x"), (":path", "/api")])
+    mp = _m.H2ServerParser(False)
+    ev = mp.feed(h2.PREFACE + h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 1, late)
+                 + h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 3, block))
+    assert ev[0] == ("malformed", 1) and ev[1][:2] == ("req", 3) and mp.open_streams() == 0
 
 
 async def test_a_silent_shard_connection_is_pinged_and_replaced(tmp_path, native_only, monkeypatch):
