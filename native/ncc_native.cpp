@@ -2544,7 +2544,7 @@ private:
         std::vector<std::pair<std::string, std::string>> headers;
         std::string body;
         bool have_headers = false, ended = false;
-        bool malformed = false;  // a pseudo-header after a regular field (RFC 9113 §8.3)
+        bool malformed = false;  // a pseudo-header after a regular field, or :method/:scheme/:path missing (RFC 9113 §8.3)
     };
     std::string buf_;
     size_t pos_ = 0;
@@ -2601,10 +2601,11 @@ private:
         Stream& st = it->second;
         if (!st.have_headers) {
             st.have_headers = true;
-            bool regular = false;
+            bool regular = false, scheme = false;
             for (auto& h : hs) {
                 if (!h.first.empty() && h.first[0] == ':') {
                     if (regular) st.malformed = true;
+                    scheme = scheme || h.first == ":scheme";
                 } else {
                     regular = true;
                 }
@@ -2618,6 +2619,8 @@ private:
                          h.first != "transfer-encoding" && h.first != "upgrade" && h.first != "proxy-connection")
                     st.headers.emplace_back(std::move(h.first), std::move(h.second));
             }
+            // :method, :scheme and :path are required (RFC 9113 §8.3.1), as Go's server checks
+            if (st.method.empty() || st.path.empty() || !scheme) st.malformed = true;
         }
         if (cont_end_) emit_request(out, sid, st);
     }
