@@ -2544,7 +2544,7 @@ private:
         std::vector<std::pair<std::string, std::string>> headers;
         std::string body;
         bool have_headers = false, ended = false;
-        bool malformed = false;  // a pseudo-header after a regular field, or :method/:scheme/:path missing (RFC 9113 §8.3)
+        bool malformed = false;  // RFC 9113 §8.2-8.3: misordered or missing pseudo-headers, uppercase names
     };
     std::string buf_;
     size_t pos_ = 0;
@@ -2608,6 +2608,9 @@ private:
                     scheme = scheme || h.first == ":scheme";
                 } else {
                     regular = true;
+                    // field names are lowercase in HTTP/2 (RFC 9113 §8.2.1)
+                    for (char c : h.first)
+                        if (c >= 'A' && c <= 'Z') st.malformed = true;
                 }
                 if (h.first == ":method")
                     st.method = std::move(h.second);

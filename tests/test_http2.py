@@ -381,6 +381,8 @@ def test_server_parser_assembles_streams_from_any_framing():
     assert ev[0] == ("malformed", 1) and ev[1][:2] == ("req", 3) and mp.open_streams() == 0
     no_path = _m.hpack_encode([(":method", "GET"), (":scheme", "http"), (":authority", "a:1")])
     assert mp.feed(h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 5, no_path)) == [("malformed", 5)]
+    upper = _m.hpack_encode([(":method", "GET"), (":scheme", "http"), (":path", "/"), ("User-Agent", "x")])
+    assert mp.feed(h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 7, upper)) == [("malformed", 7)]
 
 
 async def test_a_silent_shard_connection_is_pinged_and_replaced(tmp_path, native_only, monkeypatch):
