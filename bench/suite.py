@@ -67,6 +67,15 @@ MODE_ENV = {"native": {"NEXUS__MODE": "native"},
             "compat-unthrottled": {"NEXUS__MODE": "compat", "NEXUS__CLIENT_QPS": "-1"}}
 
 
+def parse_bytes(s: str) -> int:
+    """Kubernetes-style quantities: 1Gi, 768Mi, 512M, 1073741824."""
+    units = {"Ki": 1 << 10, "Mi": 1 << 20, "Gi": 1 << 30, "K": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9}
+    for u in ("Ki", "Mi", "Gi", "K", "M", "G"):
+        if s.endswith(u):
+            return int(float(s[:-len(u)]) * units[u])
+    return int(s)
+
+
 def b64(s: str) -> str:
     return base64.b64encode(s.encode()).decode()
 
@@ -85,14 +94,21 @@ def summarize(lat_ms: list) -> dict:
             "max_ms": round(max(lat_ms), 2)}
 
 
+class ControllerExited(Exception):
+    def __init__(self, rc):
+        super().__init__(f"the controller exited (status {rc})")
+        self.rc = rc
+
+
 class Topology:
     def __init__(self, n_shards: int, mode: str, workers: int | None = None, extra_env: dict | None = None,
-                 stages: bool = False):
+                 stages: bool = False, cgroup=None):
         self.stages = stages  # trace where latency goes (bench.py --stages): controller markers + NCC_TRACE_STAGES
         self.n = n_shards
         self.mode = mode
         self.workers = workers
         self.extra_env = extra_env or {}
+        self.cgroup = cgroup  # ncc.testing.procstats.Cgroup: the controller (and its children) run inside it
         self.work = tempfile.mkdtemp(prefix="ncc-suite-")
         self.procs: list = []
         self.controller = None
@@ -150,12 +166,42 @@ class Topology:
         if self.stages:
             env["NCC_TRACE_STAGES"] = os.path.join(self.work, "trace")
             os.makedirs(env["NCC_TRACE_STAGES"], exist_ok=True)
+        self.topology_file = env["NCC_TOPOLOGY_FILE"] = os.path.join(self.work, "topology.json")
         self.log = open(os.path.join(self.work, "controller.log"), "wb")
         t = time.time_ns()
         self.controller = subprocess.Popen([sys.executable, "-m", "ncc"], env=env, stdout=self.log,
-                                           stderr=subprocess.STDOUT, cwd=self.work)
+                                           stderr=subprocess.STDOUT, cwd=self.work,
+                                           preexec_fn=self.cgroup.enter if self.cgroup is not None else None)
         self.procs.append(self.controller)
         return t
+
+    async def guard(self, coro):
+        """Await `coro` unless the controller exits first (OOM-killed in a cgroup, a crash): then raise at once
+        instead of waiting out the marker timeout."""
+        task = asyncio.ensure_future(coro)
+        while not task.done():
+            await asyncio.wait({task}, timeout=0.5)
+            if not task.done() and self.controller is not None and self.controller.poll() is not None:
+                task.cancel()
+                await asyncio.gather(task, return_exceptions=True)
+                raise ControllerExited(self.controller.returncode)
+        return task.result()
+
+    def sizing(self) -> dict:
+        """What the controller's automatic sizing chose (NCC_TOPOLOGY_FILE)."""
+        try:
+            with open(self.topology_file) as f:
+                return json.load(f)
+        except (OSError, ValueError, AttributeError):
+            return {}
+
+    async def server_stats(self) -> list:
+        """/_fake/stats of every apiserver: shards first, the controller apiserver last."""
+        out = []
+        for u in self.shard_urls + [self.ctrl_url]:
+            async with self.session.get(f"{u}/_fake/stats") as r:
+                out.append(await r.json())
+        return out
 
     async def executor_flow(self) -> dict:
         """{shard: the C++ executor's client flow-control state} from the coordinator's /debug/state."""
@@ -395,46 +441,190 @@ async def config3_churn(mode, T, rate, duration, timeout):
         await topo.stop()
 
 
-async def config4_adoption(mode, T, timeout):
+WRITE_VERBS = ("create", "update", "status", "patch", "delete", "noop_update")
+
+
+def writes_of(st: dict) -> int:
+    return sum(st["state"].get(k, 0) for k in WRITE_VERBS)
+
+
+async def relist_storm(topo: Topology, timeout: float, quiet: float = 2.0, tree=None) -> dict:
+    """Every apiserver at once (the controller's and all shards'): compact the watch history past every
+    client's revision and drop every watch, so each informer of the controller must relist
+    (`/_fake/faults {"relist": true}`).  Reports when every apiserver again serves as many watches as before
+    with at least one new LIST per dropped watch ("back to ready"), and the writes the controller issued from
+    the storm until `quiet` seconds after that: everything is in sync, so the expectation is none.  The
+    reference gets the same relist from client-go's reflector (/root/reference/main.go:70-71)."""
+    urls = topo.shard_urls + [topo.ctrl_url]
+    # quiet first: the last wave's `Synced` Events are folded for `event-repeat-window` (1 s) and written
+    # after it; they are not the storm's
+    last, since = None, time.perf_counter()
+    give_up = since + timeout
+    while time.perf_counter() - since < 2.5 and time.perf_counter() < give_up:
+        cur = [writes_of(s) for s in await topo.server_stats()]
+        if cur != last:
+            last, since = cur, time.perf_counter()
+        await asyncio.sleep(0.1)
+    await asyncio.gather(*(topo._post(f"{u}/_fake/faults", {"record_writes": True}) for u in urls))
+    before = await topo.server_stats()
+    if tree is not None:  # the storm's own CPU seconds and peak resident set
+        tree.reset_peaks()
+        tree.mark("storm")
+    t0 = time.perf_counter()
+    await asyncio.gather(*(topo._post(f"{u}/_fake/faults", {"relist": True}) for u in urls))
+    back = [None] * len(before)
+    deadline = t0 + timeout
+    while time.perf_counter() < deadline and None in back:
+        await asyncio.sleep(0.05)
+        now = await topo.server_stats()
+        for i, (b, n) in enumerate(zip(before, now)):
+            if back[i] is None and n["watchers"] >= b["watchers"] and \
+                    n["state"]["list"] - b["state"]["list"] >= b["watchers"]:
+                back[i] = time.perf_counter() - t0
+    await asyncio.sleep(quiet)
+    after = await topo.server_stats()
+    written = {}  # "apiserver method plural[/subresource]" -> count: what the writes were, if any
+    for i, u in enumerate(urls):
+        async with topo.session.get(f"{u}/_fake/writes") as r:
+            for method, plural, _name, sub, _status, _t in (await r.json())["writes"]:
+                k = f"{'controller' if i == len(urls) - 1 else f'shard-{i}'} {method} {plural}{'/' + sub if sub else ''}"
+                written[k] = written.get(k, 0) + 1
+        await topo._post(f"{u}/_fake/faults", {"record_writes": False})
+    shard_w = sum(writes_of(a) - writes_of(b) for a, b in zip(after[:-1], before[:-1]))
+    ctrl_w = writes_of(after[-1]) - writes_of(before[-1])
+    out = {"ok": None not in back, "apiservers": len(before),
+           "watches_dropped": sum(b["watchers"] for b in before),
+           "relists": sum(a["state"]["list"] - b["state"]["list"] for a, b in zip(after, before)),
+           "shard_writes": shard_w, "controller_writes": ctrl_w,
+           "writes_by_request": written}
+    if out["ok"]:
+        out["back_to_ready_s"] = round(max(back), 3)
+        out["back_to_ready_s_controller_apiserver"] = round(back[-1], 3)
+    else:
+        out["not_back"] = [i for i, b in enumerate(back) if b is None]
+    return out
+
+
+async def config4_adoption(mode, T, timeout, n_shards=8, waves=5, storm=True, cgroup=None, payload=256):
     """8 shards with pre-existing objects: every template exists unlabelled (half drifted); half the
-    dependents exist owned by the shard template with stale data."""
-    topo = Topology(8, mode)
+    dependents exist owned by the shard template with stale data.
+
+    Then, as VERDICT r5 "next 1" asks at this shape: `waves` steady-state update waves of all T templates and
+    their dependents, and a relist storm on all n+1 apiservers at once (`relist_storm`).  Every phase reports
+    the controller's per-component CPU seconds and peak resident set (`ncc.testing.procstats`); `cgroup`
+    (a procstats.Cgroup) runs the controller under a CPU quota and memory limit and adds what the kernel
+    saw."""
+    from ncc.testing.procstats import ProcTree
+    topo = Topology(n_shards, mode, cgroup=cgroup)
+    tree = None
     try:
         await topo.start_servers()
-        await topo.apply(objects(T, 0))
-        for i in range(8):
+        await topo.apply(objects(T, 0, payload=payload))
+        for i in range(n_shards):
             tmpls, deps = [], []
             for k in range(T):
                 t = make_template(k, NS, secrets=[secret_name(k)], configmaps=[configmap_name(k)],
                                   version="stale" if k % 2 else "v0")
                 tmpls.append(t)
                 if k % 2 == 0:
-                    s = make_secret(secret_name(k), NS, version=99)
+                    s = make_secret(secret_name(k), NS, payload=payload, version=99)
                     s["__owner_template__"] = template_name(k)
-                    c = make_configmap(configmap_name(k), NS, version=99)
+                    c = make_configmap(configmap_name(k), NS, payload=payload, version=99)
                     c["__owner_template__"] = template_name(k)
                     deps += [s, c]
             await topo.seed(topo.shard_urls[i], tmpls)
             await topo.seed(topo.shard_urls[i], deps)
         w0 = await topo.shard_writes()
+        label = f"4: {n_shards} shards, cold-start adoption"
+        out = {"config": label, "mode": mode, "shards": n_shards, "templates": T, "payload_bytes": payload}
         t_boot = topo.start_controller()
-        res = await wave_all(topo, T, 0, timeout)
-        ok = all(r["ok"] for r in res)
-        out = {"config": "4: 8 shards, cold-start adoption", "mode": mode, "shards": 8, "templates": T, "ok": ok}
-        if ok:
-            done = max(max(max(ts) for ts in r["times"].values()) for r in res)
-            secs = (done - t_boot) / 1e9
-            written = await topo.shard_writes() - w0
-            # converged: every object checked on every shard (a quarter of them — the v0 templates — were
-            # already right and need no write); written: the shard writes that convergence actually took
-            out.update(converge_s=round(secs, 3), objects_converged_per_s=round(3 * T * 8 / secs, 1),
-                       objects_written=written, objects_written_per_s=round(written / secs, 1))
-        else:
-            out["counts"] = [r["counts"] for r in res]
-            out["log_tail"] = topo.log_tail()
-        return out
+        tree = ProcTree(topo.controller.pid).start()
+        try:
+            return await _config4_phases(topo, tree, out, T, n_shards, waves, storm, cgroup, payload, timeout,
+                                         w0, t_boot)
+        except ControllerExited as e:  # e.g. OOM-killed in the cgroup: what it had reached, and the kernel's view
+            await tree.stop()
+            out.update(ok=False, controller_exited=e.rc, resources=tree.report(), log_tail=topo.log_tail())
+            if cgroup is not None:
+                out["cgroup"] = cgroup.stats()
+            return out
     finally:
+        if tree is not None:
+            await tree.stop()
         await topo.stop()
+
+
+async def _config4_phases(topo, tree, out, T, n_shards, waves, storm, cgroup, payload, timeout, w0, t_boot):
+    tree.mark("cold")
+    res = await topo.guard(wave_all(topo, T, 0, timeout))
+    ok = out["ok"] = all(r["ok"] for r in res)
+    if not ok:
+        out["counts"] = [r["counts"] for r in res]
+        out["log_tail"] = topo.log_tail()
+        return out
+    done = max(max(max(ts) for ts in r["times"].values()) for r in res)
+    secs = (done - t_boot) / 1e9
+    written = await topo.shard_writes() - w0
+    # converged: every object checked on every shard (a quarter of them — the v0 templates — were
+    # already right and need no write); written: the shard writes that convergence actually took
+    out.update(converge_s=round(secs, 3), objects_converged_per_s=round(3 * T * n_shards / secs, 1),
+               objects_written=written, objects_written_per_s=round(written / secs, 1))
+    out["all_ready"] = await topo.guard(topo.settle(T, timeout))
+    res_phase = {"cold_start": {**tree.since("cold"), "peak_rss_mib": tree.report()["peak_rss_mib"]}}
+    out["sizing"] = topo.sizing()
+    # steady state: `waves` update waves of every template and dependent
+    if waves:
+        kw = {"secrets": True, "configmaps": True}
+        for v in range(1, waves + 1):
+            await topo.stage(objects(T, v, payload=payload), v)
+        tree.reset_peaks()
+        tree.mark("steady")
+        t_total = 0.0
+        for v in range(1, waves + 1):
+            s = time.perf_counter()
+            await topo.commit(v)
+            r = await topo.guard(wave_all(topo, T, v, timeout, **kw))
+            t_total += time.perf_counter() - s
+            if not all(x["ok"] for x in r):
+                out["waves"] = {"ok": False, "at_wave": v, "counts": [x["counts"] for x in r]}
+                out["log_tail"] = topo.log_tail()
+                return out
+        res_phase["steady_waves"] = {**tree.since("steady"), "peak_rss_mib": tree.report()["peak_rss_mib"]}
+        lat, wave_max = [], []
+        for v in range(1, waves + 1):
+            wl = await topo.object_latencies(range(n_shards), T, v, timeout, **kw)
+            wave_max.append(round(max(wl), 1))
+            lat.extend(wl)
+        out["waves"] = {"ok": True, "waves": waves,
+                        "objects_per_s": round(waves * 3 * T * n_shards / t_total, 1), **summarize(lat),
+                        "max_ms_per_wave": wave_max}
+        await topo.guard(topo.settle(T, timeout))
+    idle = tree.sample()
+    mib = 1 << 20
+    res_phase["settled"] = {"rss_mib": {r: round(v / mib, 1) for r, v in idle.items() if v}}
+    # per template: what the controller keeps resident for one template (its two dependents included)
+    # on the controller cluster and on all n shards
+    out["rss_bytes_per_template"] = round(idle["total"] / T)
+    if storm:
+        st = await topo.guard(relist_storm(topo, timeout, tree=tree))
+        st.update(tree.since("storm"), peak_rss_mib=tree.report()["peak_rss_mib"])
+        out["relist_storm"] = st
+        # and the controller still propagates: one more wave after the storm
+        v = waves + 1
+        await topo.stage(objects(T, v, payload=payload), v)
+        s = time.perf_counter()
+        await topo.commit(v)
+        r = await topo.guard(wave_all(topo, T, v, timeout))
+        st["wave_after"] = {"ok": all(x["ok"] for x in r), "seconds": round(time.perf_counter() - s, 3)}
+    await tree.stop()
+    out["resources"] = {**tree.report(), "phases": res_phase}
+    if cgroup is not None:
+        out["cgroup"] = cgroup.stats()
+    alive = topo.controller.poll() is None
+    out["controller_alive"] = alive
+    if not alive:
+        out["log_tail"] = topo.log_tail()
+    return out
 
 
 async def config5_flaky(mode, T, timeout, flap=1.5, stages=False, flapping=True):
@@ -599,7 +789,19 @@ async def _run(args) -> list:
                 r = await config3_churn(mode, size(1000, mode), rate=10.0, duration=args.churn_seconds,
                                         timeout=args.timeout)
             elif c == 4:
-                r = await config4_adoption(mode, size(10000, mode), timeout=args.timeout)
+                cg = None
+                if args.cgroup:
+                    from ncc.testing.procstats import Cgroup
+                    lim = dict(kv.split("=", 1) for kv in args.cgroup.split(","))
+                    cg = Cgroup(f"ncc-suite-{os.getpid()}", float(lim.get("cpus", 1)),
+                                parse_bytes(lim.get("memory", "1Gi"))).create()
+                try:
+                    r = await config4_adoption(mode, size(10000, mode), timeout=args.timeout,
+                                               n_shards=args.c4_shards, waves=args.c4_waves,
+                                               storm=not args.no_storm, cgroup=cg)
+                finally:
+                    if cg is not None:
+                        cg.remove()
             elif c == 5:
                 r = await config5_flaky(mode, size(1000, mode), timeout=args.timeout, stages=args.stages)
             elif c == 8:
@@ -635,6 +837,11 @@ def main():
     p.add_argument("--out", default="")
     p.add_argument("--admission", default="", help='configs 6/7: JSON overrides of the admission model, e.g. '
                    '\'{"service_ms": 5}\' (ncc/fakeapi/flowcontrol.py)')
+    p.add_argument("--cgroup", default="", help='config 4: run the controller in a cgroup, e.g. "cpus=1,memory=1Gi" '
+                   "(needs write access to the cgroup mounts)")
+    p.add_argument("--c4-shards", type=int, default=8, help="config 4: shard count (BASELINE: 8)")
+    p.add_argument("--c4-waves", type=int, default=5, help="config 4: steady-state waves after the cold start")
+    p.add_argument("--no-storm", action="store_true", help="config 4: skip the relist storm")
     p.add_argument("--stages", action="store_true",
                    help="configs 1, 2, 5, 8, native: per-stage latency split of the (last) timed wave (bench.py "
                         "--stages)")

@@ -1,8 +1,10 @@
 #!/usr/bin/env python
 """Build the in-tree native code: the extension `ncc/_native*.so` (C++17 + pybind11) and the native
-shard executor `ncc/bin/ncc-executor` (C++20 coroutines + epoll + OpenSSL, sources in native/executor/).
+shard executor `ncc/bin/ncc-executor` (C++20 coroutines + epoll + OpenSSL, sources in native/executor/) — the
+product — and, for tests and benchmarks, the fake apiserver's extension `ncc/fakeapi/_native*.so`
+(native/fakeapi/) and the test tool `build/tools/ncc-h2probe` (native/tools/).
 
-Usage: python native/build.py [--debug] [--sanitize]
+Usage: python native/build.py [--debug] [--sanitize] [--product-only]
 `--sanitize` builds with AddressSanitizer/UBSan for host-side testing; run the tests with
   NCC_SKIP_NATIVE_BUILD=1 ASAN_OPTIONS=detect_leaks=0 \
   LD_PRELOAD="$(g++ -print-file-name=libasan.so) $(g++ -print-file-name=libstdc++.so)" python -m pytest ...
@@ -87,12 +89,43 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
     return out
 
 
-def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
+TOOLS_DIR = os.path.join(HERE, "tools")
+
+
+def tool_path(name: str = "ncc-h2probe") -> str:
+    """Test tools live outside the package (build/tools/, git-ignored): nothing under ncc/ ships them."""
+    return os.path.join(ROOT, "build", "tools", name)
+
+
+def build_tools(verbose: bool = False) -> str:
+    """ncc-h2probe (native/tools/h2probe.cpp): the executor's HTTP client (native/executor/http.hpp) driven from
+    stdin, for tests against scripted and independent HTTP/2 servers.  Test-only; not part of the product."""
+    out = tool_path()
+    src = os.path.join(TOOLS_DIR, "h2probe.cpp")
+    deps = [src] + [os.path.join(EXECUTOR_DIR, f) for f in os.listdir(EXECUTOR_DIR) if f.endswith(".hpp")]
+    if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps + COMMON_HEADERS):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    tmp = out + ".tmp"
+    cmd = [cxx, "-std=c++20", "-fcoroutines", *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", "-O1",
+           "-DNCC_SYSTEM_MALLOC", *_werror(), src, "-o", tmp, "-lssl", "-lcrypto"]
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
+def build(debug: bool = False, sanitize: bool = False, verbose: bool = False, substrate: bool = True) -> str:
     """The extension first (the relay and the report table need it), then the C++ executor.  A host that
     cannot build the executor (no libssl-dev, no C++20 coroutines) still gets a working package: native mode
     falls back to the Python executor, with a warning here.  NCC_WERROR=1 or NCC_REQUIRE_EXECUTOR=1 (CI, the
-    container image) make that failure fatal."""
+    container image) make that failure fatal.  `substrate`: also the fake apiserver's extension (tests,
+    benchmarks; the container image builds without it)."""
     out = build_extension(debug, sanitize, verbose)
+    if substrate:
+        build_extension(debug, sanitize, verbose, sources=FAKEAPI_SOURCES, out=fakeapi_path())
     try:
         build_executor(debug, sanitize, verbose)
     except (subprocess.CalledProcessError, OSError) as e:
@@ -103,17 +136,27 @@ def build(debug: bool = False, sanitize: bool = False, verbose: bool = False) ->
     return out
 
 
-def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool = False) -> str:
+FAKEAPI_SOURCES = [os.path.join(HERE, "fakeapi", "fakeapi_native.cpp")]
+
+
+def fakeapi_path() -> str:
+    return os.path.join(ROOT, "ncc", "fakeapi", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool = False, sources: list | None = None,
+                    out: str | None = None) -> str:
+    """A pybind11 extension: the product's `ncc._native` by default, or `sources` into `out`."""
     import pybind11
 
-    out = target_path()
+    out = out or target_path()
+    sources = sources or SOURCES
     flavor = "sanitize" if sanitize else ("debug" if debug else "release")
     stamp = out + ".flavor"
     if flavor == "release" and os.path.exists(out) and os.path.exists(stamp):
         so_m = os.path.getmtime(out)
         with open(stamp) as f:
             same = f.read().strip() == flavor
-        if same and all(os.path.getmtime(s) <= so_m for s in SOURCES + COMMON_HEADERS + [__file__]):
+        if same and all(os.path.getmtime(s) <= so_m for s in sources + COMMON_HEADERS + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
     flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra",
@@ -126,7 +169,7 @@ def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool =
         flags += ["-fsanitize=address,undefined"]
     incs = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
     tmp = out + ".tmp"
-    cmd = [cxx, *flags, *incs, *SOURCES, "-o", tmp]
+    cmd = [cxx, *flags, *incs, *sources, "-o", tmp]
     if verbose:
         print(" ".join(shlex.quote(c) for c in cmd))
     subprocess.run(cmd, check=True)
@@ -140,11 +183,19 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--sanitize", action="store_true")
+    ap.add_argument("--product-only", action="store_true",
+                    help="the controller's extension and executor only (the container image): no fake-apiserver "
+                         "extension, no test tools")
     ap.add_argument("--executor-coverage", action="store_true",
                     help="rebuild only ncc/bin/ncc-executor with gcov instrumentation (scripts/cpp_coverage.py)")
     a = ap.parse_args()
     if a.executor_coverage:
         print(build_executor(coverage=True, verbose=True))
         sys.exit(0)
-    print(build(a.debug, a.sanitize, verbose=True))
+    print(build(a.debug, a.sanitize, verbose=True, substrate=not a.product_only))
+    if not a.product_only:
+        try:
+            print(build_tools(verbose=True))
+        except (subprocess.CalledProcessError, OSError) as e:  # a test tool: its tests skip without it
+            print(f"warning: build/tools/ncc-h2probe was not built ({e})", file=sys.stderr)
     sys.exit(0)

@@ -2438,6 +2438,9 @@ static void configure(const Value& c) {
             sh->name = std::string(s.sget("name"));
             sh->client = std::make_unique<Client>(creds_of(s), o.pool_size, o.request_timeout, o.flow,
                                                   o.pipeline_depth, o.http2);
+            sh->client->on_notice = [name = sh->name](const std::string& m) {
+                LOG_WARN("shard %s: %s", name.c_str(), m.c_str());
+            };
             for (int k = 0; k < 4; ++k) {
                 sh->inf[k].shard = sh.get();
                 sh->inf[k].kind = k;
@@ -2586,10 +2589,11 @@ static void send_status() {
         // client-side flow control: [limit, in flight, most in flight, 429s, overload signals, cuts, gated, qps wait ms,
         // connections, write batches, requests, slow starts left on rising latency, increases held back, the
         // executor loop's wake-ups and coalesced wake-ups (process-wide), and HTTP/2: in use (0/1), streams
-        // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received, connections dropped for an unanswered PING]
+        // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received, connections dropped for an unanswered PING,
+        // GOAWAYs with an error code, downgraded to HTTP/1.1 by HTTP_1_1_REQUIRED (0/1)]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(20);
+        e.array(22);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2610,6 +2614,8 @@ static void send_status() {
         e.integer(cl.h2_refused);
         e.integer(cl.h2_goaways);
         e.integer(cl.h2_dead);
+        e.integer(cl.h2_goaway_errors);
+        e.integer(cl.h2_downgraded ? 1 : 0);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

@@ -13,6 +13,13 @@
 // re-sent on another connection; the connection takes no new ones and closes when its streams are done),
 // per-stream deadlines (RST_STREAM CANCEL).  Watches are streams too (`Client::stream`), as client-go's: a
 // shard's four watches and its writes share its HTTP/2 connection.
+//
+// Error codes: a GOAWAY with an error code (ENHANCE_YOUR_CALM, PROTOCOL_ERROR, ...) makes
+// the re-sends of the streams it refused back off (`Client::h2_backoff_until_`) instead of going out at once;
+// HTTP_1_1_REQUIRED in RST_STREAM or GOAWAY downgrades the shard to HTTP/1.1, as an ALPN refusal does, with a
+// Warning; a WINDOW_UPDATE of 0 or one that overflows a window past 2^31-1 is an error (RFC 9113 §6.9, a
+// stream error on a stream, a connection error on the connection); and a connection error is announced with
+// GOAWAY before the connection closes (§5.4.1).
 #pragma once
 
 #include <cstdint>
@@ -20,7 +27,9 @@
 #include <exception>
 #include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 
 #include "../common/hpack.hpp"
@@ -41,8 +50,18 @@ enum Setting : uint16_t {
 };
 enum ErrorCode : uint32_t {
     NO_ERROR = 0, PROTOCOL_ERROR = 1, FLOW_CONTROL_ERROR = 3, FRAME_SIZE_ERROR = 6, REFUSED_STREAM = 7, CANCEL = 8,
-    COMPRESSION_ERROR = 9
+    COMPRESSION_ERROR = 9, ENHANCE_YOUR_CALM = 0xb, HTTP_1_1_REQUIRED = 0xd
 };
+inline constexpr int64_t kMaxWindow = 0x7fffffff;  // a flow-control window never exceeds 2^31-1 (RFC 9113 §6.9.1)
+
+// A connection error (RFC 9113 §5.4.1): the client sends GOAWAY with `code` and closes the connection.
+struct ConnectionError : std::runtime_error {
+    uint32_t code;
+    ConnectionError(uint32_t c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+// GOAWAY (last stream id 0: the server opens no streams here) with `code` and a short debug text.
+inline std::string goaway_frame(uint32_t code, std::string_view debug);
 
 inline constexpr int64_t kStreamWindow = 1 << 24;  // what we let the server send per stream before an update
 inline constexpr int64_t kConnWindow = 1 << 30;
@@ -69,6 +88,14 @@ inline void put_frame_header(std::string& out, size_t len, uint8_t type, uint8_t
 inline void put_frame(std::string& out, uint8_t type, uint8_t flags, uint32_t stream, const char* p, size_t n) {
     put_frame_header(out, n, type, flags, stream);
     out.append(p, n);
+}
+inline std::string goaway_frame(uint32_t code, std::string_view debug) {
+    std::string p, out;
+    put32(p, 0);
+    put32(p, code);
+    p.append(debug.substr(0, 200));
+    put_frame(out, GOAWAY, 0, 0, p.data(), p.size());
+    return out;
 }
 
 // One request/response exchange: owned by the requesting coroutine (exchange_h2), referenced by the session

@@ -830,6 +830,11 @@ public:
     bool http2() const { return use_h2(); }  // requests go over HTTP/2 (negotiated, or prior knowledge)
     long long h2_streams = 0, h2_refused = 0, h2_goaways = 0;  // streams opened; re-sent after REFUSED/GOAWAY
     long long h2_dead = 0;  // connections closed for an unanswered PING
+    long long h2_goaway_errors = 0;  // GOAWAYs carrying an error code (their refused streams were re-sent after a backoff)
+    bool h2_downgraded = false;      // HTTP_1_1_REQUIRED: this shard is spoken to over HTTP/1.1 from then on
+    // what the operator should hear about (a downgrade, a GOAWAY with an error code): the executor logs it as a
+    // Warning (executor.cpp)
+    std::function<void(const std::string&)> on_notice;
     long long sends = 0;  // write batches (requests issued in one loop iteration go out together)
 
     // One API call: send, retry on 429/5xx with Retry-After (≤ 5 times, ≤ 10 s each), refresh a file
@@ -966,6 +971,8 @@ private:
     std::map<std::string, std::string> hdr_;  // memoised header blocks per content type
     ConnSet busy_;
     int h2_mode_ = 0;     // client-http2: 0 off, 1 auto (ALPN on TLS), 2 on (prior knowledge on cleartext too)
+    double h2_backoff_until_ = 0;  // after a GOAWAY with an error code: refused streams wait until then to re-send
+    int h2_backoff_n_ = 0;         // consecutive error GOAWAYs (the backoff doubles with each; a success resets it)
     bool h2_ok_ = false;  // requests go over HTTP/2 (false again when the server does not negotiate it)
     double h2_read_idle_ = 30, h2_ping_timeout_ = 15;  // the liveness check (see the constructor)
     Proxy proxy_;
@@ -1552,7 +1559,8 @@ private:
                     }
                     uint32_t len = (uint32_t{static_cast<uint8_t>(p[0])} << 16) |
                                    (uint32_t{static_cast<uint8_t>(p[1])} << 8) | static_cast<uint8_t>(p[2]);
-                    if (len > h2::kOurMaxFrame) throw TransportError("HTTP/2: frame larger than SETTINGS_MAX_FRAME_SIZE");
+                    if (len > h2::kOurMaxFrame)
+                        throw h2::ConnectionError(h2::FRAME_SIZE_ERROR, "HTTP/2: frame larger than SETTINGS_MAX_FRAME_SIZE");
                     if (c.buf.size() - c.pos < 9 + len) break;
                     uint8_t type = static_cast<uint8_t>(p[3]), flags = static_cast<uint8_t>(p[4]);
                     uint32_t sid = h2::get32(p + 5) & 0x7fffffffu;
@@ -1573,8 +1581,10 @@ private:
         } catch (const NoH2& e) {
             h2_ok_ = false;  // this request and every later one over HTTP/1.1
             h2_break(s, e.what(), true);
+        } catch (const h2::ConnectionError& e) {  // the server broke the protocol: say so (GOAWAY), then close
+            h2_break(s, e.what(), false, e.code);
         } catch (const hpack::Error& e) {
-            h2_break(s, std::string("HTTP/2: HPACK: ") + e.what(), false);
+            h2_break(s, std::string("HTTP/2: HPACK: ") + e.what(), false, h2::COMPRESSION_ERROR);
         } catch (const std::exception& e) {
             // the connection ended before the server said anything: on cleartext that is what a server
             // without HTTP/2 may do with a preface — fall back as for an HTTP/1.1 answer
@@ -1590,22 +1600,22 @@ private:
     static std::string_view h2_strip(uint8_t flags, std::string_view p, bool headers) {
         size_t pad = 0;
         if (flags & h2::PADDED) {
-            if (p.empty()) throw TransportError("HTTP/2: padded frame without a pad length");
+            if (p.empty()) throw h2::ConnectionError(h2::FRAME_SIZE_ERROR, "HTTP/2: padded frame without a pad length");
             pad = static_cast<uint8_t>(p[0]);
             p.remove_prefix(1);
         }
         if (headers && (flags & h2::PRIORITY_FLAG)) {
-            if (p.size() < 5) throw TransportError("HTTP/2: short PRIORITY fields");
+            if (p.size() < 5) throw h2::ConnectionError(h2::FRAME_SIZE_ERROR, "HTTP/2: short PRIORITY fields");
             p.remove_prefix(5);
         }
-        if (pad > p.size()) throw TransportError("HTTP/2: padding longer than the frame");
+        if (pad > p.size()) throw h2::ConnectionError(h2::PROTOCOL_ERROR, "HTTP/2: padding longer than the frame");
         p.remove_suffix(pad);
         return p;
     }
     void h2_frame(h2::Session& s, uint8_t type, uint8_t flags, uint32_t sid, std::string_view p) {
         using namespace h2;
         if (s.cont_id != 0 && (type != CONTINUATION || sid != s.cont_id))
-            throw TransportError("HTTP/2: a header block interrupted before its CONTINUATION");
+            throw ConnectionError(PROTOCOL_ERROR, "HTTP/2: a header block interrupted before its CONTINUATION");
         switch (type) {
             case DATA: {
                 s.conn_recv_unacked += static_cast<int64_t>(p.size());
@@ -1649,7 +1659,7 @@ private:
                 break;
             }
             case CONTINUATION: {
-                if (s.cont_id == 0) throw TransportError("HTTP/2: CONTINUATION without HEADERS");
+                if (s.cont_id == 0) throw ConnectionError(PROTOCOL_ERROR, "HTTP/2: CONTINUATION without HEADERS");
                 s.cont_block.append(p.data(), p.size());
                 if (flags & END_HEADERS) {
                     uint32_t id = s.cont_id;
@@ -1664,25 +1674,34 @@ private:
                 if (it != s.streams.end()) {
                     Stream* st = it->second;
                     st->err = "stream reset by the server (HTTP/2 error " + std::to_string(code) + ")";
-                    st->retryable = code == REFUSED_STREAM;
-                    if (st->retryable) ++h2_refused;
+                    // REFUSED_STREAM: not processed; HTTP_1_1_REQUIRED: refused for the protocol — both safe to send
+                    // again (the second over HTTP/1.1, from now on)
+                    st->retryable = code == REFUSED_STREAM || code == HTTP_1_1_REQUIRED;
+                    if (code == REFUSED_STREAM) ++h2_refused;
                     h2_complete(s, st, false);
                 }
+                if (code == HTTP_1_1_REQUIRED) h2_downgrade(s, "RST_STREAM HTTP_1_1_REQUIRED");
                 break;
             }
             case SETTINGS: {
                 if (flags & ACK) break;
-                if (p.size() % 6 != 0) throw TransportError("HTTP/2: SETTINGS of a bad length");
+                if (p.size() % 6 != 0) throw ConnectionError(FRAME_SIZE_ERROR, "HTTP/2: SETTINGS of a bad length");
                 for (size_t k = 0; k + 6 <= p.size(); k += 6) {
                     uint16_t id = static_cast<uint16_t>((static_cast<uint8_t>(p[k]) << 8) | static_cast<uint8_t>(p[k + 1]));
                     uint32_t v = get32(p.data() + k + 2);
                     if (id == INITIAL_WINDOW_SIZE) {
-                        if (v > 0x7fffffffu) throw TransportError("HTTP/2: INITIAL_WINDOW_SIZE above 2^31-1");
+                        if (v > 0x7fffffffu)
+                            throw ConnectionError(FLOW_CONTROL_ERROR, "HTTP/2: INITIAL_WINDOW_SIZE above 2^31-1");
                         int64_t delta = static_cast<int64_t>(v) - s.peer_initial_window;
                         s.peer_initial_window = v;
-                        for (auto& kv : s.streams) kv.second->send_window += delta;
+                        for (auto& kv : s.streams) {
+                            kv.second->send_window += delta;
+                            if (kv.second->send_window > kMaxWindow)  // §6.9.2: a connection error
+                                throw ConnectionError(FLOW_CONTROL_ERROR, "HTTP/2: INITIAL_WINDOW_SIZE overflows a stream window");
+                        }
                     } else if (id == MAX_FRAME_SIZE) {
-                        if (v < 16384 || v > 16777215) throw TransportError("HTTP/2: MAX_FRAME_SIZE out of range");
+                        if (v < 16384 || v > 16777215)
+                            throw ConnectionError(PROTOCOL_ERROR, "HTTP/2: MAX_FRAME_SIZE out of range");
                         s.peer_max_frame = v;
                     } else if (id == MAX_CONCURRENT_STREAMS) {
                         s.peer_max_streams = v;
@@ -1697,10 +1716,25 @@ private:
                 if (!(flags & ACK)) put_frame(s.out, PING, ACK, 0, p.data(), p.size());
                 break;
             case GOAWAY: {
-                uint32_t last = p.size() >= 4 ? get32(p.data()) & 0x7fffffffu : 0;
+                if (p.size() < 8) throw ConnectionError(FRAME_SIZE_ERROR, "HTTP/2: GOAWAY shorter than 8 bytes");
+                uint32_t last = get32(p.data()) & 0x7fffffffu;
+                uint32_t code = get32(p.data() + 4);
                 s.goaway = true;
                 s.goaway_last = last;
                 ++h2_goaways;
+                if (code == HTTP_1_1_REQUIRED) {
+                    h2_downgrade(s, "GOAWAY HTTP_1_1_REQUIRED");
+                } else if (code != NO_ERROR) {
+                    // the server is shedding us (ENHANCE_YOUR_CALM) or saw an error: the streams it refused are
+                    // re-sent after a backoff that doubles with every such GOAWAY in a row (50 ms .. 5 s), not at once
+                    ++h2_goaway_errors;
+                    double wait = std::min(5.0, 0.05 * static_cast<double>(1 << std::min(h2_backoff_n_, 7)));
+                    ++h2_backoff_n_;
+                    h2_backoff_until_ = std::max(h2_backoff_until_, now_s() + wait);
+                    std::string debug(p.substr(8, 200));
+                    notice("GOAWAY with HTTP/2 error " + std::to_string(code) + (debug.empty() ? "" : " (" + debug + ")") +
+                           "; re-sending its refused streams after " + std::to_string(static_cast<int>(wait * 1000)) + " ms");
+                }
                 std::vector<Stream*> gone;
                 for (auto& kv : s.streams)
                     if (kv.first > last) gone.push_back(kv.second);
@@ -1713,18 +1747,35 @@ private:
                 break;
             }
             case WINDOW_UPDATE: {
-                uint32_t inc = p.size() >= 4 ? get32(p.data()) & 0x7fffffffu : 0;
-                if (sid == 0) {
+                if (p.size() != 4) throw ConnectionError(FRAME_SIZE_ERROR, "HTTP/2: WINDOW_UPDATE not 4 bytes long");
+                uint32_t inc = get32(p.data()) & 0x7fffffffu;
+                if (sid == 0) {  // the connection's window: any error is a connection error
+                    if (inc == 0) throw ConnectionError(PROTOCOL_ERROR, "HTTP/2: WINDOW_UPDATE of 0 on the connection");
+                    if (s.conn_send_window + inc > kMaxWindow)
+                        throw ConnectionError(FLOW_CONTROL_ERROR, "HTTP/2: connection window past 2^31-1");
                     s.conn_send_window += inc;
                 } else {
                     auto it = s.streams.find(sid);
-                    if (it != s.streams.end()) it->second->send_window += inc;
+                    if (it != s.streams.end()) {
+                        Stream* st = it->second;
+                        // a stream error: that stream is reset and fails, the connection carries on
+                        uint32_t bad = inc == 0                                ? uint32_t{PROTOCOL_ERROR}
+                                       : st->send_window + inc > kMaxWindow ? uint32_t{FLOW_CONTROL_ERROR}
+                                                                            : 0u;
+                        if (bad != 0) {
+                            s.rst(sid, bad);
+                            st->err = inc == 0 ? "HTTP/2: WINDOW_UPDATE of 0" : "HTTP/2: stream window past 2^31-1";
+                            h2_complete(s, st, false);
+                        } else {
+                            st->send_window += inc;
+                        }
+                    }
                 }
                 h2_resume(s);
                 break;
             }
             case PUSH_PROMISE:
-                throw TransportError("HTTP/2: PUSH_PROMISE although push is disabled");
+                throw ConnectionError(PROTOCOL_ERROR, "HTTP/2: PUSH_PROMISE although push is disabled");
             default:  // PRIORITY, and unknown types are ignored (RFC 9113 §4.1)
                 break;
         }
@@ -1786,7 +1837,10 @@ private:
     }
     // A connection failed (or was refused for HTTP/2, or drained after GOAWAY): its streams fail — `retryable`
     // ones are sent again elsewhere, the others once more like a stale keep-alive connection's request.
-    void h2_break(const h2::SessionPtr& s, const std::string& err, bool retryable) {
+    static constexpr uint32_t kNoGoaway = 0xffffffffu;
+    // `goaway`: a connection error of ours to announce — GOAWAY with that code goes out before the close
+    // (RFC 9113 §5.4.1), best effort: only when no write is in progress on the connection.
+    void h2_break(const h2::SessionPtr& s, const std::string& err, bool retryable, uint32_t goaway = kNoGoaway) {
         if (s->broken) return;
         s->broken = true;
         std::vector<h2::Stream*> open;
@@ -1802,13 +1856,38 @@ private:
         s->blocked.clear();
         s->out.clear();
         busy_.erase(&s->c);
-        s->c.close();
+        if (goaway != kNoGoaway && s->connected && !s->writing && s->c.fd >= 0)
+            spawn(h2_goodbye(s, h2::goaway_frame(goaway, err)), "h2 goaway");
+        else
+            s->c.close();
         for (size_t i = 0; i < h2s_.size(); ++i)
             if (h2s_[i] == s) {
                 h2s_.erase(h2s_.begin() + static_cast<long>(i));
                 break;
             }
         h2_wake();
+    }
+    Task<void> h2_goodbye(h2::SessionPtr s, std::string frame) {
+        s->c.deadline = now_s() + 1;  // a peer that reads nothing does not hold the socket: the sweep aborts it
+        track(&s->c);
+        try {
+            co_await s->c.write_all(frame);
+        } catch (const std::exception&) {
+        }
+        busy_.erase(&s->c);
+        s->c.close();
+    }
+    // HTTP_1_1_REQUIRED: this shard over HTTP/1.1 from now on, as when ALPN refuses h2.  The connection's other
+    // streams finish where they are (it takes no new ones).
+    void h2_downgrade(h2::Session& s, const char* why) {
+        s.goaway = true;
+        if (!h2_ok_) return;
+        h2_ok_ = false;
+        h2_downgraded = true;
+        notice(std::string(why) + ": the server requires HTTP/1.1; using HTTP/1.1 for this cluster from now on");
+    }
+    void notice(const std::string& m) {
+        if (on_notice) on_notice(m);
     }
     // The request's header block: the fields that never change for this client (:scheme, :authority,
     // user-agent, accept) come from a block encoded once, the authorization field from one encoded per token;
@@ -1933,7 +2012,11 @@ private:
                 }
                 co_return;
             }
-            if (st.retryable && resent < 8) continue;  // never processed: again, on another connection
+            if (st.retryable && resent < 8) {  // never processed: again, on another connection
+                double wait = h2_backoff_until_ - now_s();
+                if (wait > 0) co_await loop().sleep(wait);
+                continue;
+            }
             throw TransportError("watch " + target + ": " + st.err);
         }
     }
@@ -1989,11 +2072,14 @@ private:
             finish(seq, st.ok ? st.r.status : 0, now_s() - t0, st.timed_out, method == "GET" ? 0 : 1);
             if (st.ok) {
                 ++requests;
+                h2_backoff_n_ = 0;
                 co_return std::move(st.r);
             }
             ++request_errors;
             if (st.timed_out) throw TransportError(method + " " + target + ": request timed out");
             if (st.retryable && resent++ < 8) {  // never processed (REFUSED_STREAM, GOAWAY, no HTTP/2): again
+                double wait = h2_backoff_until_ - now_s();
+                if (wait > 0) co_await loop().sleep(wait);
                 --tries;
                 continue;
             }

@@ -44,7 +44,9 @@ SHARD_CLIENT_METRICS = {"limit": "shard_client_inflight_limit",      # adaptive 
                         "rejected_429": "shard_client_throttled",    # 429s received (cumulative)
                         "connections": "shard_client_connections",   # open connections
                         "http2": "shard_client_http2",               # 1 when the shard is spoken to over HTTP/2
-                        "h2_dead": "shard_client_dead_connections"}  # connections dropped for an unanswered PING
+                        "h2_dead": "shard_client_dead_connections",  # connections dropped for an unanswered PING
+                        "h2_goaway_errors": "shard_client_goaway_errors",  # GOAWAYs with an error code
+                        "h2_downgraded": "shard_client_http2_downgraded"}  # 1: HTTP_1_1_REQUIRED moved it to HTTP/1.1
 
 # Event reasons, controller.go:60-70
 SUCCESS_SYNCED = "Synced"

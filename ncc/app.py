@@ -105,25 +105,58 @@ def strip_payload(obj: dict) -> dict:
     return {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
 
 
-def cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> float | None:
-    """CPU limit from the cgroup CFS quota (v2 `cpu.max`, v1 `cpu.cfs_quota_us`), None if unlimited.
-    A Kubernetes pod's `resources.limits.cpu` lands here, not in the affinity mask."""
+def own_cgroups(proc_file: str = "/proc/self/cgroup") -> dict:
+    """{controller: path} of this process's cgroups ("" = the v2 unified hierarchy).  Inside a pod (a cgroup
+    namespace) every path is "/"; a process placed in a sub-cgroup (a sidecar-less limit, or bench/suite.py's
+    `--cgroup`) sees its own path here, and its limit lives there, not at the mount root."""
+    out = {}
     try:
-        with open(os.path.join(root, "cpu.max")) as f:
-            quota, _, period = f.read().strip().partition(" ")
-        if quota != "max":
-            return int(quota) / int(period or 100000)
-        return None
+        with open(proc_file) as f:
+            for line in f:
+                _, ctrls, path = line.rstrip("\n").split(":", 2)
+                for c in (ctrls.split(",") if ctrls else [""]):
+                    out[c] = path
     except (OSError, ValueError):
         pass
-    try:
-        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
-            quota = int(f.read().strip())
-        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
-            period = int(f.read().strip())
-        return quota / period if quota > 0 and period > 0 else None
-    except (OSError, ValueError):
-        return None
+    return out
+
+
+def _cgroup_dirs(root: str, v1_controller: str, proc_file: str) -> list:
+    """Candidate directories of this process's cgroup for one v1 controller (and the v2 hierarchy), most
+    specific first, ending at the mount roots."""
+    mine = own_cgroups(proc_file)
+    dirs = []
+    for base, key in ((os.path.join(root, v1_controller), v1_controller), (root, ""),
+                      (os.path.join(root, "unified"), "")):
+        p = mine.get(key)
+        if p and p != "/":
+            dirs.append(os.path.join(base, p.lstrip("/")))
+        dirs.append(base)
+    return dirs
+
+
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup", proc_file: str = "/proc/self/cgroup") -> float | None:
+    """CPU limit from the cgroup CFS quota (v2 `cpu.max`, v1 `cpu.cfs_quota_us`), None if unlimited.
+    A Kubernetes pod's `resources.limits.cpu` lands here, not in the affinity mask.  The process's own cgroup
+    (/proc/self/cgroup) is read first, then the mount root (a pod's cgroup namespace puts its cgroup there)."""
+    for d in _cgroup_dirs(root, "cpu", proc_file):
+        try:
+            with open(os.path.join(d, "cpu.max")) as f:
+                quota, _, period = f.read().strip().partition(" ")
+            if quota != "max":
+                return int(quota) / int(period or 100000)
+            return None
+        except (OSError, ValueError):
+            pass
+        try:
+            with open(os.path.join(d, "cpu.cfs_quota_us")) as f:
+                quota = int(f.read().strip())
+            with open(os.path.join(d, "cpu.cfs_period_us")) as f:
+                period = int(f.read().strip())
+            return quota / period if quota > 0 and period > 0 else None
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def cpu_share() -> int:

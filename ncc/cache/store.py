@@ -176,6 +176,23 @@ class Store:
             self._index(key, old, obj)
         return obj
 
+    def promote(self, key, resource_version: str) -> dict | None:
+        """A watch event at `resource_version` carries nothing the stored form keeps that differs from our
+        assumed write result (a metadata-only store: same owners): make the overlay the stored version when the
+        event is at least as new.  Without this, an echo skipped as "owners unchanged" would leave the
+        pre-write version in the store once the overlay expires (`assume_ttl`), and the next relist would see
+        every adopted dependent as changed."""
+        a = self._assumed.get(key)
+        if a is None or rv_int(resource_version) < a[1]:
+            return None
+        del self._assumed[key]
+        obj = a[0]
+        old = self._items.get(key)
+        self._items[key] = obj
+        if self._indexers:
+            self._index(key, old, obj)
+        return obj
+
     # ------------------------------------------------------------ reads
     def get(self, namespace: str, name: str) -> dict | None:
         key = (namespace, name)  # hashes and compares equal to ObjectKey(namespace, name), built faster

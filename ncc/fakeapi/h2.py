@@ -27,7 +27,7 @@ from __future__ import annotations
 import asyncio
 import struct
 
-from .. import native as _native
+from . import native as _native
 
 PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
 

@@ -16,7 +16,7 @@ import asyncio
 import json
 from urllib.parse import parse_qsl, unquote
 
-from .. import native as _native
+from . import native as _native
 
 _CRLF2 = b"\r\n\r\n"
 _HEADS: dict = {}

@@ -9,7 +9,9 @@ paths, namespaced and cluster-wide, `GET` (get / list / `?watch=1`), `POST`, `PU
 Test/bench control endpoints (not part of the Kubernetes API):
   GET  /_fake/stats    request counters and object counts
   POST /_fake/faults   {"latency_ms", "jitter_ms", "error_rate", "error_code", "throttle_rate",
-                        "down", "drop_watches", "compact", "rules", and the request-admission model
+                        "down", "drop_watches", "compact", "relist" (compact past every client's
+                        revision, then drop every watch: each informer must relist), "rules", and the
+                        request-admission model
                         "max_mutating_inflight", "apf_seats", "apf_queue", "apf_queue_wait_s",
                         "service_ms", "read_service_ms" (ncc/fakeapi/flowcontrol.py)} — fault injection for the
                        retry/backoff benchmark (BASELINE.json config 5) and for targeted tests:
@@ -517,10 +519,14 @@ class FakeApiServer:
         if what == "faults" and request.method == "POST":
             body = self._body(request)
             self.faults.update(body)
-            if body.get("drop_watches") or body.get("down"):
+            if "record_writes" in body:  # a subprocess server's write log (GET /_fake/writes), on demand
+                self.record_writes = bool(body["record_writes"])
+                self.writes.clear()
+            if body.get("compact") or body.get("relist"):
+                # compaction first: a client whose watch is dropped next must find its revision gone
+                self.state.compact(advance=bool(body.get("relist")))
+            if body.get("drop_watches") or body.get("down") or body.get("relist"):
                 self.drop_watches()
-            if body.get("compact"):
-                self.state.compact()
             return self._json(self.faults.as_dict())
         if what == "admission" and request.method == "POST":
             self.state.admission.update(self._body(request))

@@ -539,8 +539,14 @@ class ClusterState:
         self._by_rt.setdefault(w.rt_key, set()).add(w)
         return w
 
-    def compact(self) -> None:
-        """Drop all watch history (forces 410 Gone on every resume), like an etcd compaction."""
+    def compact(self, advance: bool = False) -> None:
+        """Drop all watch history (forces 410 Gone on every resume), like an etcd compaction.
+
+        `advance`: also move the revision past every client's last-seen one (a real apiserver's revision
+        keeps moving with Lease and Event writes), so that even a watcher that was fully caught up must relist
+        — the relist storm of bench/suite.py config 4."""
+        if advance:
+            self.rv += 1
         self._history.clear()
 
     def close_watchers(self) -> None:

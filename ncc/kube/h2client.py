@@ -15,7 +15,12 @@ transport negotiates h2 by ALPN and multiplexes a clientset's requests on one co
 * negotiation: ALPN "h2" on TLS (`client-http2: auto`, the default), or prior knowledge on cleartext (`on`, for
   the shard clients: the controller cluster's negotiates, `ncc/config.py` `controller_http2`).
   A server that does not speak HTTP/2 — ALPN picks http/1.1, or it answers the preface with anything but
-  SETTINGS — makes the pool fall back to HTTP/1.1 (`transport.ConnectionPool`) for good.
+  SETTINGS — makes the pool fall back to HTTP/1.1 (`transport.ConnectionPool`) for good;
+* error codes (the C++ executor's client does the same, native/executor/h2.hpp): a GOAWAY
+  with an error code makes the re-sends of the streams it refused back off (50 ms doubling to 5 s) instead of
+  going out at once; HTTP_1_1_REQUIRED in RST_STREAM or GOAWAY moves the pool to HTTP/1.1, with a warning; a
+  WINDOW_UPDATE of 0 or one overflowing a window past 2^31-1 is a stream error on a stream (RST_STREAM) and a
+  connection error on the connection; a connection error sends GOAWAY with its code before the close.
 """
 from __future__ import annotations
 
@@ -40,7 +45,9 @@ AVAILABLE = _Parser is not None
 _BODY_METHODS = frozenset(("POST", "PUT", "PATCH"))
 _NO_BODY = b""
 # RFC 9113 error codes used here
-NO_ERROR, PROTOCOL_ERROR, CANCEL, REFUSED_STREAM = 0x0, 0x1, 0x8, 0x7
+NO_ERROR, PROTOCOL_ERROR, FLOW_CONTROL_ERROR, CANCEL, REFUSED_STREAM = 0x0, 0x1, 0x3, 0x8, 0x7
+HTTP_1_1_REQUIRED = 0xd
+MAX_WINDOW = 0x7FFFFFFF  # a flow-control window never exceeds 2^31-1 (RFC 9113 §6.9.1)
 WATCH_CREDIT = 1 << 16  # a watch stream's consumed bytes are credited back in updates of at least this much
 
 
@@ -197,17 +204,25 @@ class _H2Conn(asyncio.Protocol):
                     st.head = _Response(ev[2], _NO_HEADERS if ev[3] is None else {"retry-after": ev[3]}, b"")
                     st.fut.set_result(st.head)
             elif kind == "settings":
-                self._settings(ev[1])
+                if not self._settings(ev[1]):
+                    return
             elif kind == "window":
-                self._window(ev[1], ev[2])
+                if not self._window(ev[1], ev[2]):
+                    return
             elif kind == "rst":
                 st = streams.pop(ev[1], None)
+                code = ev[2]
                 if st is not None:
-                    self._end(st, _Retry(True) if ev[2] == REFUSED_STREAM else
-                              E.TransportError(f"{st.what}: stream reset by the server (code {ev[2]})"))
-                    if ev[2] == REFUSED_STREAM:
+                    # REFUSED_STREAM: not processed; HTTP_1_1_REQUIRED: refused for the protocol — both safe to send
+                    # again (the second over HTTP/1.1, from now on)
+                    self._end(st, _Retry(code == REFUSED_STREAM) if code in (REFUSED_STREAM, HTTP_1_1_REQUIRED) else
+                              E.TransportError(f"{st.what}: stream reset by the server (code {code})"))
+                    if code == REFUSED_STREAM:
                         self.pool.stats["h2_refused"] += 1
                     self.pool._stream_closed(self)
+                if code == HTTP_1_1_REQUIRED:
+                    self.draining = True
+                    self.pool._downgrade("RST_STREAM HTTP_1_1_REQUIRED")
             elif kind == "goaway":
                 self._goaway(ev[1], ev[2])
             elif kind == "noh2":
@@ -215,48 +230,82 @@ class _H2Conn(asyncio.Protocol):
                 self.close()
                 return
             elif kind == "error":
-                self._send(_frame(7, 0, 0, struct.pack(">II", 0, ev[1]) + ev[2].encode()[:200]))
-                self._flush()
-                err = E.TransportError(f"HTTP/2 connection error: {ev[2]}")
-                self._fail_ready(err)
-                for st in list(streams.values()):
-                    self._end(st, err)
-                streams.clear()
-                self.close()
+                self._connection_error(ev[1], ev[2])
                 return
         if self.draining and not streams and not self.closed:
             self.close()  # after a GOAWAY, once the streams it let finish have finished
 
+    def _connection_error(self, code: int, why: str) -> None:
+        """RFC 9113 §5.4.1: GOAWAY with the error code, then close; every stream fails."""
+        self._send(_frame(7, 0, 0, struct.pack(">II", 0, code) + why.encode()[:200]))
+        self._flush()
+        err = E.TransportError(f"HTTP/2 connection error: {why}")
+        self._fail_ready(err)
+        for st in list(self.streams.values()):
+            self._end(st, err)
+        self.streams.clear()
+        self.close()
+
     # ------------------------------------------------------------------ frames in
-    def _settings(self, kv) -> None:
+    def _settings(self, kv) -> bool:
         for k, v in kv:
             if k == 0x3:
                 self.peer_max_streams = v
             elif k == 0x4:
+                if v > MAX_WINDOW:
+                    self._connection_error(FLOW_CONTROL_ERROR, "INITIAL_WINDOW_SIZE above 2^31-1")
+                    return False
                 delta = v - self.peer_window
                 self.peer_window = v
                 for st in self.streams.values():
                     st.send_window += delta
+                    if st.send_window > MAX_WINDOW:  # §6.9.2: a connection error
+                        self._connection_error(FLOW_CONTROL_ERROR, "INITIAL_WINDOW_SIZE overflows a stream window")
+                        return False
             elif k == 0x5:
                 self.peer_max_frame = v
         if not self.ready.done():
             self.ready.set_result(None)
         self._drain_blocked()
         self.pool._stream_closed(self)  # a raised stream limit is room for waiters
+        return True
 
-    def _window(self, sid: int, n: int) -> None:
+    def _window(self, sid: int, n: int) -> bool:
+        """WINDOW_UPDATE (§6.9): an increment of 0, or a window pushed past 2^31-1, is a connection error on
+        the connection and a stream error (RST_STREAM, the stream fails) on a stream.  False: the connection
+        is gone."""
         if sid == 0:
+            if n == 0:
+                self._connection_error(PROTOCOL_ERROR, "WINDOW_UPDATE of 0 on the connection")
+                return False
+            if self.send_window + n > MAX_WINDOW:
+                self._connection_error(FLOW_CONTROL_ERROR, "connection window past 2^31-1")
+                return False
             self.send_window += n
         else:
             st = self.streams.get(sid)
             if st is None:
-                return
+                return True
+            bad = PROTOCOL_ERROR if n == 0 else FLOW_CONTROL_ERROR if st.send_window + n > MAX_WINDOW else 0
+            if bad:
+                self.streams.pop(sid, None)
+                self.parser.forget(sid)
+                self._send(_frame(3, 0, sid, struct.pack(">I", bad)))
+                self._end(st, E.TransportError(f"{st.what}: HTTP/2 stream error: " +
+                                               ("WINDOW_UPDATE of 0" if n == 0 else "stream window past 2^31-1")))
+                self.pool._stream_closed(self)
+                return True
             st.send_window += n
         self._drain_blocked()
+        return True
 
     def _goaway(self, last: int, code: int) -> None:
         self.draining = True
         self.pool.stats["h2_goaways"] += 1
+        if code == HTTP_1_1_REQUIRED:
+            self.pool._downgrade("GOAWAY HTTP_1_1_REQUIRED")
+        elif code != NO_ERROR:
+            self.pool._goaway_error(code)
         for sid in [s for s in self.streams if s > last]:
             st = self.streams.pop(sid)
             self._end(st, _Retry())
@@ -384,7 +433,11 @@ class H2Pool:
 
     def __init__(self, server: str, *, ssl_context: _ssl.SSLContext | None = None, server_hostname: str | None = None,
                  max_size: int = 64, connect_timeout: float = 10.0, pipeline_depth: int = 1,
-                 prior_knowledge: bool = False, proxy: str | None = None):
+                 prior_knowledge: bool = False, proxy: str | None = None,
+                 fallback_ssl_context: _ssl.SSLContext | None = None):
+        """`fallback_ssl_context`: the TLS context of the HTTP/1.1 fallback pool — one that offers only
+        "http/1.1" by ALPN (`ssl_context` offers "h2" too, and a server behind a mixed load balancer that picks
+        h2 would then be spoken to in HTTP/1.1 over an h2 connection)."""
         if not AVAILABLE:
             raise RuntimeError("HTTP/2 needs the native extension (ncc/_native)")
         u = urlsplit(server)
@@ -396,6 +449,9 @@ class H2Pool:
         self.ssl = ssl_context if self.tls else None
         if self.ssl is not None:
             self.ssl.set_alpn_protocols(["h2", "http/1.1"])
+        self.fallback_ssl = fallback_ssl_context if self.tls else None
+        if self.fallback_ssl is not None:
+            self.fallback_ssl.set_alpn_protocols(["http/1.1"])
         self.server_hostname = server_hostname
         self.max_size = max(1, max_size)
         self.connect_timeout = connect_timeout
@@ -414,7 +470,10 @@ class H2Pool:
         # answer — a silently dead TCP connection would otherwise hold every stream until the kernel gives up
         self.read_idle = float(os.environ.get("HTTP2_READ_IDLE_TIMEOUT_SECONDS", "30") or 30)
         self.ping_timeout = float(os.environ.get("HTTP2_PING_TIMEOUT_SECONDS", "15") or 15)
-        self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0, "h2_dead": 0}
+        self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0, "h2_dead": 0, "h2_goaway_errors": 0,
+                      "h2_downgraded": 0}
+        self.backoff_until = 0.0  # after a GOAWAY with an error code: refused streams re-send from then on
+        self._backoff_n = 0       # error GOAWAYs in a row (the backoff doubles with each; a response resets it)
 
     @property
     def protocol(self) -> str:
@@ -447,9 +506,35 @@ class H2Pool:
         self.conns.append(conn)
         return conn
 
+    def _downgrade(self, why: str) -> None:
+        """HTTP_1_1_REQUIRED: every request from now on over HTTP/1.1, as when ALPN refuses h2; the HTTP/2
+        connections finish the streams they have and take no new ones."""
+        if self.fallback is not None:
+            return
+        import logging
+        logging.getLogger("ncc.transport").warning(
+            "%s from %s:%s: the server requires HTTP/1.1; using HTTP/1.1 for it from now on", why, self.host, self.port)
+        self.stats["h2_downgraded"] = 1
+        for c in self.conns:
+            c.draining = True
+        self._h1()
+
+    def _goaway_error(self, code: int) -> None:
+        """A GOAWAY with an error code (ENHANCE_YOUR_CALM: we are being shed; or a server-side error): the streams
+        it refused wait 50 ms, doubling with every such GOAWAY in a row up to 5 s, before they are sent again."""
+        self.stats["h2_goaway_errors"] += 1
+        wait = min(5.0, 0.05 * (2 ** min(self._backoff_n, 7)))
+        self._backoff_n += 1
+        self.backoff_until = max(self.backoff_until, self._now() + wait)
+        import logging
+        logging.getLogger("ncc.transport").warning(
+            "GOAWAY with HTTP/2 error %#x from %s:%s; re-sending its refused streams after %d ms", code, self.host,
+            self.port, int(wait * 1000))
+
     def _h1(self) -> ConnectionPool:
         if self.fallback is None:
-            self.fallback = ConnectionPool(self.server, ssl_context=self.ssl, server_hostname=self.server_hostname,
+            ctx = self.fallback_ssl if self.fallback_ssl is not None else self.ssl
+            self.fallback = ConnectionPool(self.server, ssl_context=ctx, server_hostname=self.server_hostname,
                                            max_size=self.max_size, connect_timeout=self.connect_timeout,
                                            pipeline_depth=self.pipeline_depth, proxy=self.proxy)
         return self.fallback
@@ -475,11 +560,15 @@ class H2Pool:
                 fut = self._connecting = asyncio.get_running_loop().create_future()
                 try:
                     return await self._connect()
-                except _NoH2:
-                    if self.opened == 0:
-                        self._h1()  # this server speaks HTTP/1.1 only: from now on, every request goes there
-                        return None
-                    raise E.TransportError(f"connect {self.host}:{self.port}: HTTP/2 no longer offered")
+                except _NoH2 as e:
+                    if self.opened:
+                        # it spoke HTTP/2 before (a load balancer whose backends differ, a server downgraded):
+                        # fall back as on the first connection, as Go's transport decides per connection
+                        import logging
+                        logging.getLogger("ncc.transport").warning(
+                            "%s:%s no longer offers HTTP/2 (%s); using HTTP/1.1 for it", self.host, self.port, e)
+                    self._h1()  # from now on, every request goes there
+                    return None
                 finally:
                     self._connecting = None
                     fut.set_result(None)
@@ -565,7 +654,9 @@ class H2Pool:
         clen = len(body) if body is not None else (0 if method in _BODY_METHODS else -1)
         what = f"{method} {target}"
         for attempt in range(MAX_UNPROCESSED_RETRIES + 1):
-            c = self._pick() or await self._conn()
+            c = self._pick() if self.fallback is None else None
+            if c is None:
+                c = await self._conn()
             if c is None:
                 return await self.fallback.request(method, target, headers, body, timeout=timeout, block=block)
             st = c.open(method, target, fixed, clen, body or _NO_BODY, what)
@@ -573,11 +664,16 @@ class H2Pool:
                 st.deadline = asyncio.get_running_loop().time() + timeout
                 self._arm_sweep()
             try:
-                return await st.fut
+                resp = await st.fut
+                self._backoff_n = 0
+                return resp
             except _Retry as r:
                 if attempt < MAX_UNPROCESSED_RETRIES:
+                    wait = self.backoff_until - self._now()
                     if r.refused:
-                        await asyncio.sleep(min(0.001 * (2 ** attempt), 0.1))
+                        wait = max(wait, min(0.001 * (2 ** attempt), 0.1))
+                    if wait > 0:
+                        await asyncio.sleep(wait)
                     continue
                 raise E.TransportError(f"{what}: refused by the server") from None
             except asyncio.CancelledError:

@@ -150,7 +150,9 @@ class RestClient(KubeClient):
                     tls = self.cfg.server.startswith("https:")
                     if h2client.AVAILABLE and (self.http2 == "on" or (self.http2 == "auto" and tls)):
                         # client-go's transport: HTTP/2 negotiated by ALPN (prior knowledge on cleartext with "on")
-                        self._pool = h2client.H2Pool(self.cfg.server, prior_knowledge=self.http2 == "on", **kw)
+                        self._pool = h2client.H2Pool(self.cfg.server, prior_knowledge=self.http2 == "on",
+                                                     fallback_ssl_context=_ssl_context(self.cfg, exec_cert) or None,
+                                                     **kw)
                     else:
                         self._pool = ConnectionPool(self.cfg.server, **kw)
         return self._pool

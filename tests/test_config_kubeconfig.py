@@ -215,6 +215,31 @@ def test_cpu_share_reads_cgroup_quota(tmp_path):
     assert auto_executors_per_shard(8, cpus=128) == 4 and auto_executors_per_shard(1, cpus=2) == 2
 
 
+def test_cgroup_quota_of_own_cgroup(tmp_path):
+    """A process placed in a sub-cgroup (v1 `cpu:/pods/x`, v2 `0::/pods/x`) reads its limit there, not at
+    the unlimited mount root; in a pod's cgroup namespace (path "/") the mount root is its own cgroup."""
+    from ncc.app import cgroup_cpu_quota
+    root = tmp_path / "cg"
+    (root / "cpu").mkdir(parents=True)
+    (root / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    (root / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    sub = root / "cpu" / "pods" / "x"
+    sub.mkdir(parents=True)
+    (sub / "cpu.cfs_quota_us").write_text("100000\n")
+    (sub / "cpu.cfs_period_us").write_text("100000\n")
+    proc = tmp_path / "cgroup"
+    proc.write_text("4:memory:/pods/x\n1:cpu,cpuacct:/pods/x\n0::/\n")
+    assert cgroup_cpu_quota(str(root), str(proc)) == 1.0
+    proc.write_text("1:cpu,cpuacct:/\n0::/\n")
+    assert cgroup_cpu_quota(str(root), str(proc)) is None
+    v2 = tmp_path / "v2"
+    (v2 / "pods" / "y").mkdir(parents=True)
+    (v2 / "cpu.max").write_text("max 100000\n")
+    (v2 / "pods" / "y" / "cpu.max").write_text("250000 100000\n")
+    proc.write_text("0::/pods/y\n")
+    assert cgroup_cpu_quota(str(v2), str(proc)) == 2.5
+
+
 def test_klog_style_flags(monkeypatch, capsys):
     """main.go:36-37 — klog.InitFlags + flag.Parse: `-v=4` and klog's output flags are accepted, Go style."""
     import ncc.app as app

@@ -18,12 +18,14 @@ import random
 import pytest
 
 from ncc import native
+from ncc.fakeapi import native as fnative
 from ncc.api import resources as R
 from ncc.testing.workload import make_configmap, make_secret, make_template
 
 from test_conformance import NS, Cluster, mutate, wait_for
 
 _m = native.load(required=True)
+_f = fnative.load(required=True)  # the fake apiserver's extension (server side)
 
 
 # ---------------------------------------------------------------------------------------------- HPACK
@@ -48,7 +50,7 @@ C5 = ["4803333032580770726976617465611d4d6f6e2c203231204f637420323031332032303a3
 
 @pytest.mark.parametrize("blocks", [C3, C4], ids=["C.3-plain", "C.4-huffman"])
 def test_hpack_rfc7541_request_examples(blocks):
-    d = _m.HpackDecoder(4096)
+    d = _f.HpackDecoder(4096)
     sizes = []
     for blk, want in zip(blocks, C3_FIELDS):
         assert d.decode(bytes.fromhex(blk)) == want
@@ -57,7 +59,7 @@ def test_hpack_rfc7541_request_examples(blocks):
 
 
 def test_hpack_rfc7541_response_examples_with_eviction():
-    d = _m.HpackDecoder(256)
+    d = _f.HpackDecoder(256)
     got = [d.decode(bytes.fromhex(b)) for b in C5[:1]]
     assert got[0] == [(":status", "302"), ("cache-control", "private"), ("date", "Mon, 21 Oct 2013 20:13:21 GMT"),
                       ("location", "https://www.example.com")]
@@ -84,7 +86,7 @@ def test_hpack_huffman_rfc_strings_and_round_trip():
 
 def test_hpack_encoder_round_trip_and_malformed_blocks():
     rnd = random.Random(3)
-    d = _m.HpackDecoder()
+    d = _f.HpackDecoder()
     for _ in range(100):
         fields = [(":status", str(rnd.choice([200, 201, 404, 409, 429, 503]))), ("content-type", "application/json")]
         fields += [(f"x-{rnd.randrange(1000)}", "v" * rnd.randrange(0, 300)) for _ in range(rnd.randrange(4))]
@@ -94,7 +96,7 @@ def test_hpack_encoder_round_trip_and_malformed_blocks():
     for bad in (b"\x80", b"\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\x7f", b"\x40\x05ab", b"\xbe"):
         with pytest.raises(ValueError):
             d.decode(bad)
-    fresh = _m.HpackDecoder()
+    fresh = _f.HpackDecoder()
     with pytest.raises(ValueError):  # a table size update after a field
         fresh.decode(bytes.fromhex("82") + b"\x20")
     with pytest.raises(ValueError):  # above the limit we advertised
@@ -342,7 +344,7 @@ def test_server_parser_assembles_streams_from_any_framing():
               h2.frame(h2.WINDOW_UPDATE, 0, 0, (1000).to_bytes(4, "big")),
               h2.frame(h2.PING, 0, 0, b"12345678"), h2.frame(h2.RST_STREAM, 0, 3, (8).to_bytes(4, "big"))]
     data = b"".join(frames)
-    p = _m.H2ServerParser(False)
+    p = _f.H2ServerParser(False)
     events = []
     for i in range(len(data)):
         events += p.feed(data[i:i + 1])
@@ -352,15 +354,15 @@ def test_server_parser_assembles_streams_from_any_framing():
     assert headers == {"content-type": "application/json", "host": "a:1"}
     assert events[2:] == [("window", 0, 1000), ("ping", b"12345678"), ("rst", 3, 8)]
     assert p.open_streams() == 0
-    bad = _m.H2ServerParser(False)
+    bad = _f.H2ServerParser(False)
     assert bad.feed(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")[0][0] == "error"
     # the connection window is given back as request bodies use it (a soak once stalled after 1 GiB of them)
-    cp = _m.H2ServerParser(False, 1000)
+    cp = _f.H2ServerParser(False, 1000)
     hdr = h2.frame(h2.HEADERS, h2.END_HEADERS, 1, block)
     ev = cp.feed(h2.PREFACE + hdr + b"".join(h2.frame(h2.DATA, 0, 1, b"x" * 600) for _ in range(3)))
     assert ("credit", 0, 1200) in ev and [e for e in ev if e[0] == "credit"] == [("credit", 0, 1200)]
-    resp = _m.h2_response(5, 200, "application/json", b"x" * 40000, [("retry-after", "1")], 16384)
-    d = _m.HpackDecoder()
+    resp = _f.h2_response(5, 200, "application/json", b"x" * 40000, [("retry-after", "1")], 16384)
+    d = _f.HpackDecoder()
     n = int.from_bytes(resp[:3], "big")
     assert resp[3] == h2.HEADERS and resp[4] == h2.END_HEADERS
     assert d.decode(resp[9:9 + n]) == [(":status", "200"), ("content-type", "application/json"),
@@ -375,7 +377,7 @@ def test_server_parser_assembles_streams_from_any_framing():
     # a pseudo-header after a regular field is a malformed request (RFC 9113 §8.3): Go's server, and this one,
     # reset that stream and keep the connection
     late = _m.hpack_encode([(":method", "GET"), (":scheme", "http"), ("user-agent", "x"), (":path", "/api")])
-    mp = _m.H2ServerParser(False)
+    mp = _f.H2ServerParser(False)
     ev = mp.feed(h2.PREFACE + h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 1, late)
                  + h2.frame(h2.HEADERS, h2.END_HEADERS | h2.END_STREAM, 3, block))
     assert ev[0] == ("malformed", 1) and ev[1][:2] == ("req", 3) and mp.open_streams() == 0

@@ -17,6 +17,7 @@ import os
 import pytest
 
 from ncc import native
+from ncc.fakeapi import native as fnative
 from ncc.api import resources as R
 from ncc.fakeapi.server import FakeApiServer
 from ncc.kube import errors as E
@@ -28,6 +29,7 @@ from ncc.testing.workload import make_configmap, make_secret, make_template
 
 NS = "nexus"
 _m = native.load(required=True)
+_f = fnative.load(required=True)  # the fake apiserver's extension (server side)
 
 
 class _Server:
@@ -258,7 +260,7 @@ def test_client_parser_from_any_framing():
     # the request encoder: HEADERS split at the peer's frame size, DATA ending the stream
     fixed = _m.hpack_encode([(":scheme", "http"), (":authority", "a:1"), ("authorization", "x" * 100)])
     req = _m.h2_request(9, "PUT", "/api/v1/x", fixed, 5, b"hello", True, 64)
-    d, off, kinds, block = _m.HpackDecoder(), 0, [], b""
+    d, off, kinds, block = _f.HpackDecoder(), 0, [], b""
     while off < len(req):
         n = int.from_bytes(req[off:off + 3], "big")
         kinds.append((req[off + 3], req[off + 4]))
@@ -364,7 +366,7 @@ async def test_stream_resets_refusals_and_early_watch_exit():
     seen = []
 
     async def handle(reader, writer):
-        parser = _m.H2ServerParser(False)
+        parser = _f.H2ServerParser(False)
         writer.write(_frame(4, 0, 0, (3).to_bytes(2, "big") + (100).to_bytes(4, "big")) +
                      _frame(8, 0, 0, ((1 << 30) - 65535).to_bytes(4, "big")))
         while True:
@@ -390,7 +392,7 @@ async def test_stream_resets_refusals_and_early_watch_exit():
                         writer.write(_frame(1, 0x4, sid, block) +
                                      _frame(0, 0, sid, b'{"type":"ADDED","object":{}}\n{"type":"ADDED","object":{}}\n'))
                     else:
-                        writer.write(_m.h2_response(sid, 200, "application/json", b'{"kind":"SecretList","items":[]}',
+                        writer.write(_f.h2_response(sid, 200, "application/json", b'{"kind":"SecretList","items":[]}',
                                                     [], 16384))
             await writer.drain()
 

@@ -196,9 +196,9 @@ def test_native_response_head_parser_rejects_malformed(head):
 
 
 def test_native_request_head_parser_matches_python():
-    from ncc import native
+    from ncc.fakeapi import native as fnative
     from ncc.fakeapi.httpserver import _parse_head_py
-    m = native.load(required=True)
+    m = fnative.load(required=True)
     for head in (b"PUT /api/v1/namespaces/n/secrets/a?fieldManager=x HTTP/1.1\r\nHost: h:1\r\nContent-Length: 12",
                  b"GET /apis/x/y?watch=1 HTTP/1.1\r\nAuthorization:  Bearer t \r\nX-Odd: a: b\r\nNoColonLine",
                  b"DELETE /a HTTP/1.1"):
@@ -265,7 +265,9 @@ def test_native_parsers_survive_arbitrary_bytes():
     """Random and truncated inputs: the C++ parsers return or raise ValueError, never crash."""
     from hypothesis import given, settings, strategies as st
     from ncc import native
+    from ncc.fakeapi import native as fnative
     m = native.load(required=True)
+    f = fnative.load(required=True)  # the fake apiserver's request-head parser
     good_resp = b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\nRetry-After: 1"
     good_req = b"PUT /api/v1/namespaces/n/secrets/a HTTP/1.1\r\nContent-Length: 3"
     good_line = (b'{"type":"MODIFIED","object":{"metadata":{"name":"s","namespace":"n","resourceVersion":"7",'
@@ -274,7 +276,7 @@ def test_native_parsers_survive_arbitrary_bytes():
     @settings(max_examples=300, deadline=None)
     @given(st.binary(max_size=200), st.integers(0, 200))
     def check(blob, cut):
-        for fn in (m.parse_response_head, m.parse_request_head):
+        for fn in (m.parse_response_head, f.parse_request_head):
             for data in (blob, good_resp[:cut] + blob, good_req[:cut] + blob):
                 try:
                     fn(data)
