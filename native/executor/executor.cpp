@@ -2590,10 +2590,11 @@ static void send_status() {
         // connections, write batches, requests, slow starts left on rising latency, increases held back, the
         // executor loop's wake-ups and coalesced wake-ups (process-wide), and HTTP/2: in use (0/1), streams
         // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received, connections dropped for an unanswered PING,
-        // GOAWAYs with an error code, downgraded to HTTP/1.1 by HTTP_1_1_REQUIRED (0/1)]
+        // GOAWAYs with an error code, downgraded to HTTP/1.1 by HTTP_1_1_REQUIRED (0/1), streams reset with
+        // ENHANCE_YOUR_CALM]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(22);
+        e.array(23);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2616,6 +2617,7 @@ static void send_status() {
         e.integer(cl.h2_dead);
         e.integer(cl.h2_goaway_errors);
         e.integer(cl.h2_downgraded ? 1 : 0);
+        e.integer(cl.h2_calm);
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

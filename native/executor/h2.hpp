@@ -22,6 +22,7 @@
 // GOAWAY before the connection closes (§5.4.1).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <deque>
 #include <exception>
@@ -53,6 +54,9 @@ enum ErrorCode : uint32_t {
     COMPRESSION_ERROR = 9, ENHANCE_YOUR_CALM = 0xb, HTTP_1_1_REQUIRED = 0xd
 };
 inline constexpr int64_t kMaxWindow = 0x7fffffff;  // a flow-control window never exceeds 2^31-1 (RFC 9113 §6.9.1)
+// re-sends of a request the server did not take (REFUSED_STREAM, ENHANCE_YOUR_CALM, past a GOAWAY, no HTTP/2), as
+// ncc/kube/h2client.py MAX_UNPROCESSED_RETRIES: with the refusal backoff (50 ms doubling to 5 s) about a minute
+inline constexpr int kMaxResends = 16;
 
 // A connection error (RFC 9113 §5.4.1): the client sends GOAWAY with `code` and closes the connection.
 struct ConnectionError : std::runtime_error {
@@ -137,6 +141,10 @@ struct Session {
     int64_t peer_initial_window = 65535;
     uint32_t peer_max_frame = 16384;
     uint32_t peer_max_streams = 100;  // until the server's SETTINGS say otherwise
+    // lowered for good, to 7/8 of the streams in flight, each time the server refuses one (REFUSED_STREAM,
+    // ENHANCE_YOUR_CALM): a server whose own count of open streams lags ours (nghttp2 under Node frees a stream
+    // some time after its END_STREAM went out) refuses streams opened at or near its limit
+    uint32_t stream_cap = 0xffffffffu;
     int64_t conn_recv_unacked = 0;
     hpack::Decoder dec{4096};
     double last_read = 0;  // when bytes last arrived (liveness: Client::sweep PINGs a connection silent too long)
@@ -162,7 +170,13 @@ struct Session {
         put_frame(out, WINDOW_UPDATE, 0, 0, wu.data(), wu.size());
     }
     bool usable() const { return !broken && !goaway && next_id < 0x7ffffff0u; }
-    bool has_room() const { return usable() && streams.size() < peer_max_streams; }
+    // Until the server's SETTINGS arrive its MAX_CONCURRENT_STREAMS is unknown: one stream goes out with the
+    // preface, the rest wait for the SETTINGS (one round trip, once per connection).  Opening up to a guessed
+    // 100 instead had nghttp2 (50 streams) reset the excess with ENHANCE_YOUR_CALM on a TLS connection, where
+    // the handshake leaves time to queue many (tests/test_http2_interop.py).
+    bool has_room() const {
+        return usable() && streams.size() < (got_settings ? std::min(peer_max_streams, stream_cap) : 1u);
+    }
 
     void rst(uint32_t id, uint32_t code) {
         std::string p;

@@ -831,6 +831,7 @@ public:
     long long h2_streams = 0, h2_refused = 0, h2_goaways = 0;  // streams opened; re-sent after REFUSED/GOAWAY
     long long h2_dead = 0;  // connections closed for an unanswered PING
     long long h2_goaway_errors = 0;  // GOAWAYs carrying an error code (their refused streams were re-sent after a backoff)
+    long long h2_calm = 0;           // streams reset with ENHANCE_YOUR_CALM (re-sent after the same backoff)
     bool h2_downgraded = false;      // HTTP_1_1_REQUIRED: this shard is spoken to over HTTP/1.1 from then on
     // what the operator should hear about (a downgrade, a GOAWAY with an error code): the executor logs it as a
     // Warning (executor.cpp)
@@ -973,6 +974,7 @@ private:
     int h2_mode_ = 0;     // client-http2: 0 off, 1 auto (ALPN on TLS), 2 on (prior knowledge on cleartext too)
     double h2_backoff_until_ = 0;  // after a GOAWAY with an error code: refused streams wait until then to re-send
     int h2_backoff_n_ = 0;         // consecutive error GOAWAYs (the backoff doubles with each; a success resets it)
+    uint32_t h2_stream_cap_ = 0xffffffffu;  // the lowest stream cap a refusal taught (h2::Session::stream_cap)
     bool h2_ok_ = false;  // requests go over HTTP/2 (false again when the server does not negotiate it)
     double h2_read_idle_ = 30, h2_ping_timeout_ = 15;  // the liveness check (see the constructor)
     Proxy proxy_;
@@ -1489,10 +1491,14 @@ private:
     // transport does); a new one while all are at the server's MAX_CONCURRENT_STREAMS and fewer than
     // `max_` are open; else null — wait for a stream to end.
     h2::SessionPtr h2_pick() {
-        for (auto& s : h2s_)
+        bool settling = false;  // a connection still waiting for the server's SETTINGS: wait for it, not another
+        for (auto& s : h2s_) {
             if (s->has_room()) return s;
-        if (static_cast<int>(h2s_.size()) >= max_) return nullptr;
+            settling = settling || (s->usable() && !s->got_settings);
+        }
+        if (settling || static_cast<int>(h2s_.size()) >= max_) return nullptr;
         auto s = std::make_shared<h2::Session>();
+        s->stream_cap = h2_stream_cap_;
         h2s_.push_back(s);
         spawn(h2_open(s), "h2 connect");
         return s;
@@ -1675,10 +1681,21 @@ private:
                     Stream* st = it->second;
                     st->err = "stream reset by the server (HTTP/2 error " + std::to_string(code) + ")";
                     // REFUSED_STREAM: not processed; HTTP_1_1_REQUIRED: refused for the protocol — both safe to send
-                    // again (the second over HTTP/1.1, from now on)
-                    st->retryable = code == REFUSED_STREAM || code == HTTP_1_1_REQUIRED;
+                    // again (the second over HTTP/1.1, from now on).  ENHANCE_YOUR_CALM: the server sheds load
+                    // (nghttp2 under Node resets streams it will not take with it): again, after the backoff of an
+                    // error GOAWAY — every write the executor sends is safe to repeat (see `exchange`)
+                    st->retryable = code == REFUSED_STREAM || code == HTTP_1_1_REQUIRED || code == ENHANCE_YOUR_CALM;
                     if (code == REFUSED_STREAM) ++h2_refused;
+                    if (code == ENHANCE_YOUR_CALM) {
+                        ++h2_calm;
+                        h2_back_off(false, "RST_STREAM ENHANCE_YOUR_CALM");
+                    }
                     h2_complete(s, st, false);
+                    if (code == REFUSED_STREAM || code == ENHANCE_YOUR_CALM) {  // 7/8 of what was in flight, for good
+                        size_t n = std::min<size_t>(s.stream_cap, s.streams.size() + 1);
+                        s.stream_cap = static_cast<uint32_t>(std::max<size_t>(1, n - std::max<size_t>(1, n / 8)));
+                        h2_stream_cap_ = std::min(h2_stream_cap_, s.stream_cap);  // and for the next connections
+                    }
                 }
                 if (code == HTTP_1_1_REQUIRED) h2_downgrade(s, "RST_STREAM HTTP_1_1_REQUIRED");
                 break;
@@ -1728,12 +1745,9 @@ private:
                     // the server is shedding us (ENHANCE_YOUR_CALM) or saw an error: the streams it refused are
                     // re-sent after a backoff that doubles with every such GOAWAY in a row (50 ms .. 5 s), not at once
                     ++h2_goaway_errors;
-                    double wait = std::min(5.0, 0.05 * static_cast<double>(1 << std::min(h2_backoff_n_, 7)));
-                    ++h2_backoff_n_;
-                    h2_backoff_until_ = std::max(h2_backoff_until_, now_s() + wait);
                     std::string debug(p.substr(8, 200));
-                    notice("GOAWAY with HTTP/2 error " + std::to_string(code) + (debug.empty() ? "" : " (" + debug + ")") +
-                           "; re-sending its refused streams after " + std::to_string(static_cast<int>(wait * 1000)) + " ms");
+                    h2_back_off(true, "GOAWAY with HTTP/2 error " + std::to_string(code) +
+                                          (debug.empty() ? "" : " (" + debug + ")"));
                 }
                 std::vector<Stream*> gone;
                 for (auto& kv : s.streams)
@@ -1886,6 +1900,15 @@ private:
         h2_downgraded = true;
         notice(std::string(why) + ": the server requires HTTP/1.1; using HTTP/1.1 for this cluster from now on");
     }
+    // Refused streams wait until h2_backoff_until_: 50 ms, doubling with every refusal in a row up to 5 s (a
+    // response resets it).  `loud`: announce it (a GOAWAY); a stream reset only at the start of a run.
+    void h2_back_off(bool loud, const std::string& why) {
+        double wait = std::min(5.0, 0.05 * static_cast<double>(1 << std::min(h2_backoff_n_, 7)));
+        if (loud || h2_backoff_n_ == 0)
+            notice(why + "; re-sending the refused streams after " + std::to_string(static_cast<int>(wait * 1000)) + " ms");
+        ++h2_backoff_n_;
+        h2_backoff_until_ = std::max(h2_backoff_until_, now_s() + wait);
+    }
     void notice(const std::string& m) {
         if (on_notice) on_notice(m);
     }
@@ -2012,7 +2035,7 @@ private:
                 }
                 co_return;
             }
-            if (st.retryable && resent < 8) {  // never processed: again, on another connection
+            if (st.retryable && resent < h2::kMaxResends) {  // never processed: again, on another connection
                 double wait = h2_backoff_until_ - now_s();
                 if (wait > 0) co_await loop().sleep(wait);
                 continue;
@@ -2077,7 +2100,7 @@ private:
             }
             ++request_errors;
             if (st.timed_out) throw TransportError(method + " " + target + ": request timed out");
-            if (st.retryable && resent++ < 8) {  // never processed (REFUSED_STREAM, GOAWAY, no HTTP/2): again
+            if (st.retryable && resent++ < h2::kMaxResends) {  // never processed (REFUSED_STREAM, GOAWAY, no HTTP/2): again
                 double wait = h2_backoff_until_ - now_s();
                 if (wait > 0) co_await loop().sleep(wait);
                 --tries;

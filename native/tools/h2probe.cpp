@@ -68,10 +68,10 @@ struct Probe {
         }
         while (pending > 0) co_await loop().sleep(0.002);
         std::printf("{\"stats\":{\"http2\":%d,\"h2_streams\":%lld,\"h2_refused\":%lld,\"h2_goaways\":%lld,"
-                    "\"h2_goaway_errors\":%lld,\"h2_downgraded\":%d,\"h2_dead\":%lld,\"connections\":%d,\"requests\":%lld,"
+                    "\"h2_goaway_errors\":%lld,\"h2_calm\":%lld,\"h2_downgraded\":%d,\"h2_dead\":%lld,\"connections\":%d,\"requests\":%lld,"
                     "\"request_errors\":%lld},\"notices\":[",
                     cl->http2() ? 1 : 0, cl->h2_streams, cl->h2_refused, cl->h2_goaways, cl->h2_goaway_errors,
-                    cl->h2_downgraded ? 1 : 0, cl->h2_dead, cl->connections(), cl->requests, cl->request_errors);
+                    cl->h2_calm, cl->h2_downgraded ? 1 : 0, cl->h2_dead, cl->connections(), cl->requests, cl->request_errors);
         std::printf("%s]}\n", notices.c_str());
         std::fflush(stdout);
         loop().stop();

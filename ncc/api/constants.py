@@ -37,6 +37,7 @@ RECONCILE_ERRORS_METRIC = "reconcile_errors"          # count, tag kind
 SHARD_SYNC_ERRORS_METRIC = "shard_sync_errors"        # count, tag shard (coordinator, from executor reports)
 SHARDS_METRIC = "shards"                              # gauge: shards served
 LEADER_METRIC = "leader"                              # gauge 1/0 when leader election is on
+EXECUTOR_NATIVE_METRIC = "executor_native"            # gauge 1: the C++ shard executors run, 0: the Python ones
 SHARD_FAILING_METRIC = "shard_failing_objects"        # gauge, tag shard: templates whose last sync there failed
 # the C++ executors' shard clients (their status messages, native/executor/http.hpp), gauges tagged shard:
 SHARD_CLIENT_METRICS = {"limit": "shard_client_inflight_limit",      # adaptive concurrency limit (AIMD)

@@ -173,6 +173,18 @@ def cpu_share() -> int:
     return max(1, min(n, int(q))) if q else n
 
 
+def auto_shard_groups(shards: int, cpus: int | None = None) -> int:
+    """Shard-executor processes (`executors: -1`): one per shard, but no more than the CPUs the pod may use.
+
+    Each executor process holds its own copy of the controller-side objects its shards need (fed by the watch
+    relay), so a process per shard costs memory in proportion; under a CPU quota smaller than the shard count
+    the extra processes cannot run in parallel anyway.  At BASELINE config 4 (8 shards × 10 000 templates,
+    bench/suite.py) one process for all 8 shards settled at 822 MiB for the whole controller against 1 517 MiB
+    with eight (BENCHMARKS.md "Config 4 at scale")."""
+    cpus = cpu_share() if cpus is None else cpus
+    return max(1, min(shards, cpus))
+
+
 def auto_executors_per_shard(groups: int, cpus: int | None = None) -> int:
     """Key-partitioned executors per shard group: one per CPU share of the group, 1..4.
 
@@ -273,6 +285,7 @@ class App:
         self.gate: asyncio.Event | None = None  # workers wait for it (warm standby / pre-spawned child)
         self.relay = None  # coordinator: WatchRelay feeding the executors
         self.executor_impl = ""  # coordinator: "native" (ncc/bin/ncc-executor) or "python" shard executors
+        self.executor_fallback = ""  # coordinator: why the Python executors run instead of the C++ ones ("" = they don't)
         self.cpu_affinity = ""  # coordinator: "l3:<cpus>" when it restricted itself to one L3 domain, else "none"
         self.placement = None  # coordinator with NCC_CPU_AFFINITY=l3: ncc.affinity.Placement
         self._placement_task = None
@@ -310,7 +323,7 @@ class App:
         all_names = [n for n, _ in discover(cfg.shard_config_path)]
         self._shard_files = shard_files(cfg.shard_config_path)
         if o.role == "all" and o.mode == "native" and all_names:
-            n = cfg.executors if cfg.executors >= 0 else len(all_names)
+            n = cfg.executors if cfg.executors >= 0 else auto_shard_groups(len(all_names))
             self.n_executors = max(0, min(n, cfg.max_executors, len(all_names)))
             if self.n_executors > 0:
                 o.role = "coordinator"
@@ -390,7 +403,7 @@ class App:
         if cfg.metrics_bind_address or cfg.health_bind_address:
             from .telemetry.http import OpsServer
             self.ops = OpsServer(ready=self._ready,
-                                 prometheus=prom, extra=self.debug_state)
+                                 prometheus=prom, extra=self.debug_state, checks=self._ready_checks)
         if cfg.mode == "native":
             # start-up garbage (imports, config parsing) collected and the survivors frozen now, before any
             # informer or executor runs: a full pass over a large heap here is off the propagation path
@@ -451,12 +464,26 @@ class App:
             self.metrics.gauge(C.SHARD_FAILING_METRIC, n, {"shard": shard})
         if self.elector is not None:
             self.metrics.gauge(C.LEADER_METRIC, 1 if self.elector.leading else 0)
+        if self.executor_impl:
+            self.metrics.gauge(C.EXECUTOR_NATIVE_METRIC, 1 if self.executor_impl == "native" else 0)
         if self.pool is not None:
             for h in self.pool.stats().values():
                 for shard, flow in ((h.get("status") or {}).get("flow") or {}).items():
                     for field, name in C.SHARD_CLIENT_METRICS.items():
                         if field in flow:
                             self.metrics.gauge(name, flow[field], {"shard": shard})
+
+    def _ready_checks(self) -> list:
+        """`/readyz?verbose`: the caches, and which shard executor implementation runs (and why not the C++ one)."""
+        c = self.controller
+        out = [("informer-sync", c is not None and c.caches_synced.is_set(), ""),
+               ("workers", c is not None and c.ready.is_set(), "")]
+        if self.executor_impl:
+            out.append(("shard-executors", True, self.executor_impl +
+                        (f" (fallback from the C++ executor: {self.executor_fallback})" if self.executor_fallback else "")))
+        if self.elector is not None:
+            out.append(("leader", True, "leading" if self.elector.leading else "standing by"))
+        return out
 
     def _ready(self) -> bool:
         """Ready once caches synced and workers run — or while standing by for the leader Lease."""
@@ -477,6 +504,8 @@ class App:
             out["watch_relay"] = dict(self.relay.stats)
         if self.executor_impl:
             out["executor_impl"] = self.executor_impl
+            if self.executor_fallback:
+                out["executor_fallback"] = self.executor_fallback
         client = self.client
         while client is not None and not hasattr(client, "protocol") and hasattr(client, "inner"):
             client = client.inner  # under a RateLimitedClient
@@ -570,7 +599,13 @@ class App:
             use_native, why = choose(self.cfg, self.options, self.relay is not None)
             self.executor_impl = "native" if use_native else "python"
             if not use_native:
-                log.debug("Python shard executors: %s", why)
+                # loud: the image requires the C++ executor, so a pod on the Python one is misconfigured or
+                # mis-built — a Warning, the executor_native gauge at 0, /readyz?verbose
+                self.executor_fallback = why
+                if why != "executor-impl: python":
+                    log.warning("shard executors: the Python implementation runs instead of the C++ one (%s)", why)
+            if self.metrics is not None:
+                self.metrics.gauge(C.EXECUTOR_NATIVE_METRIC, 1 if use_native else 0)
             native_cfg = self.native_cfg = NativeExecutorConfig(self.cfg, self.options) if use_native else None
             # One executor group per shard group serves every template key, whatever the number of coordinator
             # partitions: a shard apiserver then serves one executor's watches, not C of them

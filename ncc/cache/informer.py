@@ -209,21 +209,43 @@ class Informer:
         items: list[dict] = []
         token = None
         rv = ""
+        tap = self.tap
+        paged_tap = getattr(tap, "on_list_page", None)
+        transform = self.store.transform
         while True:
             resp = await self.client.list(self.rt, self.namespace, label_selector=self.label_selector,
                                           limit=self.page_size, continue_token=token,
                                           resource_version=resource_version if token is None else None)
-            items.extend(resp.get("items") or ())
+            page = resp.get("items") or []
+            # Each page goes to the relay (full objects: executors need the specs) and into its stored form at
+            # once, so a listing holds one page of full objects at a time, not all of them: at 10 000 templates
+            # with their Secrets and ConfigMaps that is the coordinator's start-up and relist peak
+            # (bench/suite.py config 4).
+            if paged_tap is not None:
+                paged_tap(page)
+            elif tap is not None:
+                items.extend(page)
+                page = None
+            if page is not None:
+                if self.slim_decode is not None:
+                    page = self._slim_listing(page)
+                elif transform is not None:
+                    page = [transform(o) for o in page]
+                items.extend(page)
             lm = resp.get("metadata") or {}
             rv = lm.get("resourceVersion", rv)
             token = lm.get("continue")
             if not token:
                 break
-        if self.tap is not None:
-            self.tap.on_list(items)  # (the relay forwards the full objects: executors need the specs)
-        if self.slim_decode is not None:
-            items = self._slim_listing(items)
-        await self._replace_items(items)
+        if paged_tap is not None:
+            tap.on_list(None)  # the listing is complete: the relay swaps it in and sends the snapshots
+        elif tap is not None:
+            tap.on_list(items)
+            if self.slim_decode is not None:
+                items = self._slim_listing(items)
+            elif transform is not None:
+                items = [transform(o) for o in items]
+        await self._replace_items(items, transformed=True)
         return rv
 
     def _slim_listing(self, items: list) -> list:
@@ -241,12 +263,13 @@ class Informer:
             out.append(sl[1] if sl is not None else o)
         return out
 
-    async def _replace_items(self, items: list) -> None:
-        """Swap in a complete listing (LIST, or a relayed snapshot) and deliver the differences."""
+    async def _replace_items(self, items: list, transformed: bool = False) -> None:
+        """Swap in a complete listing (LIST, or a relayed snapshot) and deliver the differences.  `transformed`:
+        the items are already in stored form (`Store.transform` applied)."""
         if self.key_filter is not None or self.owner_filter is not None:
             items = [o for o in items if self._wanted(o.get("metadata") or {})]
         self._stash.clear()  # the relist is newer than anything parked
-        added, updated, deleted = self.store.replace(items)
+        added, updated, deleted = self.store.replace(items, transformed=transformed)
         self.relists += 1
         synced_before = self.has_synced()
         self._synced.set()

@@ -107,12 +107,14 @@ class Store:
             self._index(key, old, None)
         return old
 
-    def replace(self, objs: Iterable[dict]) -> tuple[list, list, list]:
-        """Swap the whole content (relist).  Returns (added, updated[(old,new)], deleted)."""
+    def replace(self, objs: Iterable[dict], transformed: bool = False) -> tuple[list, list, list]:
+        """Swap the whole content (relist).  Returns (added, updated[(old,new)], deleted).  `transformed`: the
+        objects are already in stored form."""
         new_items: dict[ObjectKey, dict] = {}
+        transform = None if transformed else self.transform
         for o in objs:
-            if self.transform is not None:
-                o = self.transform(o)
+            if transform is not None:
+                o = transform(o)
             new_items[key_of(o)] = o
         old_items = self._items
         added, updated, deleted = [], [], []

@@ -13,7 +13,16 @@ and a bearer token; exec tokens are refreshed here and pushed as `{"t": "cred"}`
 
 `executor-impl: auto` (default) picks the native executor whenever the binary is built and the
 configuration is one it implements (native mode with the watch relay; POST/PUT writes, or server-side
-apply with `server-side-apply: true`); otherwise the Python executor runs.
+apply with `server-side-apply: true`); otherwise the Python executor runs — loudly: a Warning at start-up,
+the `executor_native` gauge at 0, and `/readyz?verbose` and `/debug/state` name the reason (ncc/app.py).
+
+Why three implementations of the reconcile semantics — the in-process one
+(ncc/controller/reconcile.py: compat mode and the reference's own test harness), the Python executor and the
+C++ executor — and not two: the Python executor is what `pip install` gives a host without a C++20 compiler or
+libssl headers (setup.py builds the executor best-effort), and what runs with `watch-relay: false`; and it is
+the readable specification the C++ executor is conformance-tested against, scenario by scenario
+(tests/test_conformance.py runs every scenario on "inprocess", "python" and "native").  The container image
+requires the C++ executor (NCC_REQUIRE_EXECUTOR=1 at build, NCC_REQUIRE_NATIVE=1 at run).
 """
 from __future__ import annotations
 

@@ -115,8 +115,11 @@ class _Tap:
     def __init__(self, relay: "WatchRelay", kind: int):
         self.relay, self.kind = relay, kind
 
-    def on_list(self, items: list) -> None:
+    def on_list(self, items: list | None) -> None:
         self.relay.on_list(self.kind, items)
+
+    def on_list_page(self, items: list) -> None:
+        self.relay.on_list_page(self.kind, items)
 
     def on_lines(self, lines: list) -> None:
         self.relay.on_lines(self.kind, lines)
@@ -134,6 +137,7 @@ class WatchRelay:
         self.namespace = namespace or ""
         self.template_store = template_store
         self.raw: list[dict] = [{} for _ in KINDS]  # (ns, name) -> latest line of the object
+        self._listing: dict[int, dict] = {}  # kind -> lines of a listing still arriving page by page
         self.synced = [False] * len(KINDS)
         self.handles: list = []
         self.parts = 1
@@ -200,9 +204,21 @@ class WatchRelay:
         return self._mod.relay_scan(line, self.parts, self.namespace)
 
     # ------------------------------------------------------------------ informer side
-    def on_list(self, kind: int, items: list) -> None:
+    def on_list_page(self, kind: int, items: list) -> None:
+        """One page of a listing in progress: kept as lines (the objects themselves are not held on to)."""
         ns = self.namespace
-        self.raw[kind] = {((meta(o).get("namespace") or ns), meta(o).get("name", "")): _line_of(o) for o in items}
+        page = self._listing.setdefault(kind, {})
+        for o in items:
+            page[((meta(o).get("namespace") or ns), meta(o).get("name", ""))] = _line_of(o)
+
+    def on_list(self, kind: int, items: list | None) -> None:
+        """A complete listing — `items`, or the pages `on_list_page` collected (None) — replaces the kind's lines
+        and goes to every executor as a snapshot."""
+        ns = self.namespace
+        if items is None:
+            self.raw[kind] = self._listing.pop(kind, {})
+        else:
+            self.raw[kind] = {((meta(o).get("namespace") or ns), meta(o).get("name", "")): _line_of(o) for o in items}
         self.synced[kind] = True
         self._send_snapshot(kind, self.handles)
 

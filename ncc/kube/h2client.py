@@ -46,7 +46,7 @@ _BODY_METHODS = frozenset(("POST", "PUT", "PATCH"))
 _NO_BODY = b""
 # RFC 9113 error codes used here
 NO_ERROR, PROTOCOL_ERROR, FLOW_CONTROL_ERROR, CANCEL, REFUSED_STREAM = 0x0, 0x1, 0x3, 0x8, 0x7
-HTTP_1_1_REQUIRED = 0xd
+ENHANCE_YOUR_CALM, HTTP_1_1_REQUIRED = 0xb, 0xd
 MAX_WINDOW = 0x7FFFFFFF  # a flow-control window never exceeds 2^31-1 (RFC 9113 §6.9.1)
 WATCH_CREDIT = 1 << 16  # a watch stream's consumed bytes are credited back in updates of at least this much
 
@@ -111,6 +111,11 @@ class _H2Conn(asyncio.Protocol):
         self.streams: dict[int, _Stream] = {}
         self.next_sid = 1
         self.peer_max_streams = 100  # until the server's SETTINGS say otherwise
+        # streams this connection may carry: the server's limit, lowered for good to 7/8 of what was in flight each
+        # time the server refuses a stream (REFUSED_STREAM / ENHANCE_YOUR_CALM) — a server whose own count of open
+        # streams lags ours (nghttp2 under Node frees a stream some time after its END_STREAM went out) refuses
+        # streams opened at or near its limit
+        self.stream_cap = pool.stream_cap
         self.peer_window = 65535     # its SETTINGS_INITIAL_WINDOW_SIZE: each new stream's send window
         self.peer_max_frame = 16384
         self.send_window = 65535     # the connection's
@@ -214,8 +219,17 @@ class _H2Conn(asyncio.Protocol):
                 code = ev[2]
                 if st is not None:
                     # REFUSED_STREAM: not processed; HTTP_1_1_REQUIRED: refused for the protocol — both safe to send
-                    # again (the second over HTTP/1.1, from now on)
-                    self._end(st, _Retry(code == REFUSED_STREAM) if code in (REFUSED_STREAM, HTTP_1_1_REQUIRED) else
+                    # again (the second over HTTP/1.1, from now on); ENHANCE_YOUR_CALM: the server sheds load
+                    # (nghttp2 under Node resets the streams it will not take with it) — again after a backoff
+                    if code == ENHANCE_YOUR_CALM:
+                        self.pool.stats["h2_calm"] += 1
+                        self.pool._back_off(False, "RST_STREAM ENHANCE_YOUR_CALM")
+                    if code in (REFUSED_STREAM, ENHANCE_YOUR_CALM):  # 7/8 of what was in flight, for good
+                        n = min(self.stream_cap, len(streams) + 1)
+                        self.stream_cap = max(1, n - max(1, n // 8))
+                        self.pool.stream_cap = min(self.pool.stream_cap, self.stream_cap)  # and the next connections
+                    self._end(st, _Retry(code == REFUSED_STREAM)
+                              if code in (REFUSED_STREAM, HTTP_1_1_REQUIRED, ENHANCE_YOUR_CALM) else
                               E.TransportError(f"{st.what}: stream reset by the server (code {code})"))
                     if code == REFUSED_STREAM:
                         self.pool.stats["h2_refused"] += 1
@@ -336,7 +350,7 @@ class _H2Conn(asyncio.Protocol):
             self.transport.write(out[0] if len(out) == 1 else b"".join(out))
 
     def has_room(self) -> bool:
-        return not self.closed and not self.draining and len(self.streams) < self.peer_max_streams
+        return not self.closed and not self.draining and len(self.streams) < min(self.peer_max_streams, self.stream_cap)
 
     def open(self, method: str, target: str, fixed: bytes, clen: int, body: bytes, what: str,
              watch: bool = False) -> _Stream:
@@ -471,9 +485,10 @@ class H2Pool:
         self.read_idle = float(os.environ.get("HTTP2_READ_IDLE_TIMEOUT_SECONDS", "30") or 30)
         self.ping_timeout = float(os.environ.get("HTTP2_PING_TIMEOUT_SECONDS", "15") or 15)
         self.stats = {"h2_streams": 0, "h2_refused": 0, "h2_goaways": 0, "h2_dead": 0, "h2_goaway_errors": 0,
-                      "h2_downgraded": 0}
+                      "h2_downgraded": 0, "h2_calm": 0}
         self.backoff_until = 0.0  # after a GOAWAY with an error code: refused streams re-send from then on
         self._backoff_n = 0       # error GOAWAYs in a row (the backoff doubles with each; a response resets it)
+        self.stream_cap = 1 << 31  # the lowest per-connection stream cap a refusal taught (_H2Conn.stream_cap)
 
     @property
     def protocol(self) -> str:
@@ -521,15 +536,20 @@ class H2Pool:
 
     def _goaway_error(self, code: int) -> None:
         """A GOAWAY with an error code (ENHANCE_YOUR_CALM: we are being shed; or a server-side error): the streams
-        it refused wait 50 ms, doubling with every such GOAWAY in a row up to 5 s, before they are sent again."""
+        it refused wait before they are sent again (`_back_off`)."""
         self.stats["h2_goaway_errors"] += 1
+        self._back_off(True, f"GOAWAY with HTTP/2 error {code:#x}")
+
+    def _back_off(self, loud: bool, why: str) -> None:
+        """Refused streams re-send from `backoff_until` on: 50 ms, doubling with every refusal in a row up to 5 s (a
+        response resets it).  `loud`: a warning each time (a GOAWAY); a stream reset only at the start of a run."""
         wait = min(5.0, 0.05 * (2 ** min(self._backoff_n, 7)))
+        if loud or self._backoff_n == 0:
+            import logging
+            logging.getLogger("ncc.transport").warning("%s from %s:%s; re-sending the refused streams after %d ms",
+                                                       why, self.host, self.port, int(wait * 1000))
         self._backoff_n += 1
         self.backoff_until = max(self.backoff_until, self._now() + wait)
-        import logging
-        logging.getLogger("ncc.transport").warning(
-            "GOAWAY with HTTP/2 error %#x from %s:%s; re-sending its refused streams after %d ms", code, self.host,
-            self.port, int(wait * 1000))
 
     def _h1(self) -> ConnectionPool:
         if self.fallback is None:
@@ -580,7 +600,8 @@ class H2Pool:
         """Room on `c` (or `c` gone): wake as many waiters as it has free streams; they pick again."""
         if not self._waiters:
             return
-        free = c.peer_max_streams - len(c.streams) if c.has_room() else (1 if c.closed or c.draining else 0)
+        free = min(c.peer_max_streams, c.stream_cap) - len(c.streams) if c.has_room() else \
+            (1 if c.closed or c.draining else 0)
         while self._waiters and free > 0:
             w = self._waiters.popleft()
             if not w.done():

@@ -67,10 +67,12 @@ def _split(addr: str) -> tuple[str, int]:
 
 class OpsServer:
     def __init__(self, ready: Callable[[], bool], prometheus: PrometheusMetrics | None = None,
-                 extra: Callable[[], dict] | None = None):
+                 extra: Callable[[], dict] | None = None, checks: Callable[[], list] | None = None):
+        """`checks()` → [(name, ok, detail)]: what `/readyz?verbose` lists, as the kube-apiserver's does."""
         self.ready = ready
         self.prometheus = prometheus
         self.extra = extra
+        self.checks = checks
         self.app = web.Application()
         self.app.router.add_get("/healthz", self._healthz)
         self.app.router.add_get("/readyz", self._readyz)
@@ -82,8 +84,14 @@ class OpsServer:
     async def _healthz(self, _r):
         return web.Response(text="ok")
 
-    async def _readyz(self, _r):
-        return web.Response(text="ok") if self.ready() else web.Response(status=503, text="not ready")
+    async def _readyz(self, r):
+        ready = self.ready()
+        if "verbose" not in r.query:
+            return web.Response(text="ok") if ready else web.Response(status=503, text="not ready")
+        lines = [f"[{'+' if ok else '-'}]{name} {detail}".rstrip() for name, ok, detail in
+                 (self.checks() if self.checks else [])]
+        lines.append("readyz check passed" if ready else "readyz check failed")
+        return web.Response(status=200 if ready else 503, text="\n".join(lines) + "\n")
 
     async def _metrics(self, _r):
         if self.prometheus is None:

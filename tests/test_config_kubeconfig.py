@@ -215,6 +215,14 @@ def test_cpu_share_reads_cgroup_quota(tmp_path):
     assert auto_executors_per_shard(8, cpus=128) == 4 and auto_executors_per_shard(1, cpus=2) == 2
 
 
+def test_shard_groups_capped_by_cpus():
+    """One executor process per shard, no more than the CPUs (each holds its own controller-side cache)."""
+    from ncc.app import auto_shard_groups
+    assert [auto_shard_groups(n, cpus=16) for n in (1, 2, 8, 20)] == [1, 2, 8, 16]
+    assert [auto_shard_groups(n, cpus=1) for n in (1, 8)] == [1, 1]
+    assert auto_shard_groups(8, cpus=3) == 3
+
+
 def test_cgroup_quota_of_own_cgroup(tmp_path):
     """A process placed in a sub-cgroup (v1 `cpu:/pods/x`, v2 `0::/pods/x`) reads its limit there, not at
     the unlimited mount root; in a pod's cgroup namespace (path "/") the mount root is its own cgroup."""

@@ -1,5 +1,6 @@
 """End-to-end: `App` against fake apiservers over real HTTP (Test_ControllerMain analogue, controller_test.go:1287-1336)."""
 import asyncio
+import logging
 
 import pytest
 
@@ -663,4 +664,57 @@ async def test_reload_with_changed_kubeconfig_reaches_native_executor(tmp_path, 
             assert app.native_cfg.creds["shard-0"].cfg.server == env.shard_urls[1]
     finally:
         await cc.close()
+        await env.stop()
+
+
+async def test_python_executor_fallback_is_loud(tmp_path, monkeypatch, caplog):
+    """under `executor-impl: auto`, a coordinator that cannot run the C++ executors (here:
+    the watch relay switched off) runs the Python ones with a Warning, the executor_native gauge at 0, and the
+    reason in /readyz?verbose and /debug/state — not silently.  With the relay on, the gauge is 1."""
+    import aiohttp
+
+    from ncc.controller.native_executor import binary_path
+    if binary_path() is None:
+        pytest.skip("the C++ executor is not built")
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+
+    class Gauges:
+        def __init__(self):
+            self.g = {}
+
+        def gauge(self, name, value, tags=None):
+            self.g[name] = value
+
+        def __getattr__(self, _name):
+            return lambda *a, **k: None
+
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    try:
+        for relay, impl in ((False, "python"), (True, "native")):
+            caplog.clear()
+            metrics = Gauges()
+            app = App(env.app_config(mode="native", watch_relay=relay, health_bind_address="127.0.0.1:0"),
+                      metrics=metrics)
+            stop = asyncio.Event()
+            with caplog.at_level(logging.WARNING, logger="ncc"):
+                await app.build()
+                task = asyncio.ensure_future(app.run(stop))
+                try:
+                    await asyncio.wait_for(app.controller.ready.wait(), 15)
+                    assert app.executor_impl == impl
+                    assert metrics.g[C.EXECUTOR_NATIVE_METRIC] == (1 if impl == "native" else 0)
+                    async with aiohttp.ClientSession() as s:
+                        async with s.get(f"http://127.0.0.1:{app.ops.port}/readyz?verbose") as r:
+                            text = await r.text()
+                    assert r.status == 200 and "[+]shard-executors " + impl in text and "readyz check passed" in text
+                    fallback = [m for m in caplog.messages if "Python implementation runs instead" in m]
+                    if impl == "python":
+                        assert "the watch relay is off" in text and fallback
+                        assert app.debug_state()["executor_fallback"] == "the watch relay is off"
+                    else:
+                        assert "fallback" not in text and not fallback
+                finally:
+                    stop.set()
+                    await asyncio.wait_for(task, 20)
+    finally:
         await env.stop()
