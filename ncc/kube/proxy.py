@@ -59,6 +59,8 @@ def _bypassed(host: str, port: int, no_proxy: str) -> bool:
             continue
         except ValueError:
             pass
+        if e.startswith("*."):  # Go's parseNoProxy: "*.example.com" is ".example.com" (subdomains only)
+            e = e[1:]
         if e.startswith("."):
             if host.endswith(e):
                 return True

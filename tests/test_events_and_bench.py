@@ -213,7 +213,7 @@ def test_bench_two_ranks_over_gloo():
     pytest.importorskip("torch.distributed")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1"]
+           "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1", "--no-tls-run"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -238,7 +238,8 @@ def test_bench_eight_ranks_auto_sized_topology():
     env = dict(os.environ, NCC_CPU_SHARE="128")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "8", "--templates", "40", "--steps", "2", "--warmup", "1", "--timeout", "120"]
+           "--gpus", "8", "--templates", "40", "--steps", "2", "--warmup", "1", "--timeout", "120",
+           "--no-tls-run"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

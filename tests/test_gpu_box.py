@@ -48,3 +48,7 @@ def test_bench_contract_single_shard():
     assert res["controller_sizing"]["executor_impl"] == "native", res["controller_sizing"]
     assert res["controller_to_substrate"] is not None and res["host"]["calibration"].get("cpp_ctl_scan_ns"), \
         (res["controller_cpu_us_per_object"], res["substrate_us_per_object"], res["host"])
+    # the production transport beside the headline: TLS on every apiserver, HTTP/2 by ALPN, product defaults
+    assert res["tls_value"] > 0 and res["tls_config"]["shard_transport"] == "http2" and \
+        res["tls_config"]["controller_transport"] == "h2" and res["tls_config"]["cpu_affinity"] == "none", res
+    assert res["bench_settings"]["NEXUS__CLIENT_HTTP2"] == "on"

@@ -66,6 +66,7 @@ class Scripted:
         self.settings = settings or [(3, 100)]
         self.seen = []  # (time, kind, ...) — "req" (proto, path, sid), "rst" (sid, code), "goaway" (last, code)
         self.server = None
+        self.h2 = True  # False: answer the HTTP/2 preface as an HTTP/1.1-only server does
 
     def log(self, *ev):
         self.seen.append((time.monotonic(), *ev))
@@ -88,7 +89,7 @@ class Scripted:
             writer.close()
             return
         try:
-            if head == PREFACE:
+            if head == PREFACE and self.h2:
                 await self._h2(reader, writer)
             else:
                 await self._h1(head, reader, writer)
@@ -296,4 +297,25 @@ async def test_server_header_table_size_zero_keeps_our_decoder_table(client):
         assert [r.get("status") for r in res] == [200, 200], res
         assert not srv.of("goaway"), srv.seen  # no COMPRESSION_ERROR
     finally:
+        await srv.stop()
+
+
+async def test_pool_falls_back_per_connection_after_speaking_http2():
+    """a connection that no longer negotiates HTTP/2 after earlier ones did (a load balancer with mixed
+    backends, a server downgraded) moves the pool to HTTP/1.1 instead of failing for good, as Go's transport
+    decides per connection."""
+    srv = Scripted({})
+    url = await srv.start()
+    pool = h2client.H2Pool(url, prior_knowledge=True, connect_timeout=5)
+    try:
+        assert (await pool.request("GET", "/a", HDR, None, timeout=5)).status == 200 and pool.protocol == "h2"
+        srv.h2 = False
+        for c in list(pool.conns):
+            c.abort("test: the backend changed")
+        await asyncio.sleep(0.05)
+        assert (await pool.request("GET", "/b", HDR, None, timeout=5)).status == 200
+        assert pool.protocol == "http/1.1" and pool.opened == 1
+        assert [(r[1], r[2]) for r in srv.of("req")][-1] == ("http/1.1", "/b")
+    finally:
+        pool.close()
         await srv.stop()

@@ -146,6 +146,10 @@ def test_proxy_for_follows_client_go():
     assert proxy_for("https://127.0.0.1:6443", environ=env) is None         # loopback is never proxied
     assert proxy_for("https://localhost:6443", environ=env) is None
     assert proxy_for("https://k8s.example", environ={"HTTPS_PROXY": "http://p", "NO_PROXY": "*"}) is None
+    # "*.example.com" is Go's ".example.com": subdomains bypass, the domain itself does not
+    star = {"HTTPS_PROXY": "http://p", "NO_PROXY": "*.shards.example"}
+    assert proxy_for("https://eu-1.shards.example", environ=star) is None
+    assert proxy_for("https://shards.example", environ=star) == "http://p"
     assert proxy_for("https://k8s.example", environ={}) is None
     # the kubeconfig's proxy-url wins, loopback included (client-go's rest.Config.Proxy)
     assert proxy_for("https://127.0.0.1:6443", "http://p:1", environ=env) == "http://p:1"
