@@ -195,6 +195,14 @@ class Topology:
         except (OSError, ValueError, AttributeError):
             return {}
 
+    async def coordinator_stats(self) -> dict:
+        """The coordinator's counters (/debug/state "stats")."""
+        try:
+            async with self.session.get(f"http://{self.ops}/debug/state") as r:
+                return (await r.json()).get("stats") or {}
+        except Exception:  # noqa: BLE001 — diagnostics only
+            return {}
+
     async def server_stats(self) -> list:
         """/_fake/stats of every apiserver: shards first, the controller apiserver last."""
         out = []
@@ -467,6 +475,7 @@ async def relist_storm(topo: Topology, timeout: float, quiet: float = 2.0, tree=
         await asyncio.sleep(0.1)
     await asyncio.gather(*(topo._post(f"{u}/_fake/faults", {"record_writes": True}) for u in urls))
     before = await topo.server_stats()
+    passes0 = await topo.coordinator_stats()
     if tree is not None:  # the storm's own CPU seconds and peak resident set
         tree.reset_peaks()
         tree.mark("storm")
@@ -483,6 +492,7 @@ async def relist_storm(topo: Topology, timeout: float, quiet: float = 2.0, tree=
                 back[i] = time.perf_counter() - t0
     await asyncio.sleep(quiet)
     after = await topo.server_stats()
+    passes1 = await topo.coordinator_stats()
     written = {}  # "apiserver method plural[/subresource]" -> count: what the writes were, if any
     for i, u in enumerate(urls):
         async with topo.session.get(f"{u}/_fake/writes") as r:
@@ -496,7 +506,9 @@ async def relist_storm(topo: Topology, timeout: float, quiet: float = 2.0, tree=
            "watches_dropped": sum(b["watchers"] for b in before),
            "relists": sum(a["state"]["list"] - b["state"]["list"] for a, b in zip(after, before)),
            "shard_writes": shard_w, "controller_writes": ctrl_w,
-           "writes_by_request": written}
+           "writes_by_request": written,
+           # template/workgroup passes the coordinator ran because of the storm (queued and inline finishes)
+           "coordinator_passes": {k: passes1.get(k, 0) - passes0.get(k, 0) for k in ("reconciles", "inline_finishes")}}
     if out["ok"]:
         out["back_to_ready_s"] = round(max(back), 3)
         out["back_to_ready_s_controller_apiserver"] = round(back[-1], 3)
