@@ -547,6 +547,9 @@ using ShardPtr = std::shared_ptr<const ShardObj>;
 // `raw` (optional): the payload members' text when `obj` was parsed without them (parse_split)
 static ShardPtr make_shard_obj(int kind, Value obj, const std::string_view* raw = nullptr) {
     auto s = std::make_shared<ShardObj>();
+    // managedFields (server-side apply's field ownership, hundreds of bytes per object on a real apiserver)
+    // is not kept: an update without it leaves the server's as they are (metadata.managedFields unset = keep)
+    if (Value* mm = obj.get("metadata"); mm != nullptr && mm->is_obj()) mm->erase("managedFields");
     const Value* m = meta_of(obj);
     if (m) {
         s->ns = std::string(m->sget("namespace"));
@@ -695,6 +698,24 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body, const SentPayloa
         rest.push_back('"');
         rest.append(k);
         rest.append("\":");
+        if (k == "metadata" && v.find("\"managedFields\"") != std::string_view::npos) {
+            // kept without managedFields (see make_shard_obj): the other members copied as text
+            rest.push_back('{');
+            bool mfirst = true;
+            bool mok = RawCursor(v).members([&](std::string_view mk, std::string_view mv) {
+                if (mk == "managedFields") return true;
+                if (!mfirst) rest.push_back(',');
+                mfirst = false;
+                rest.push_back('"');
+                rest.append(mk);
+                rest.append("\":");
+                rest.append(mv);
+                return true;
+            });
+            if (!mok) return false;
+            rest.push_back('}');
+            return scan_meta(*s, v);
+        }
         rest.append(v);
         if (k == "metadata") return scan_meta(*s, v);
         if (k == "type" && kind >= 2) {  // Secret.type

@@ -102,7 +102,13 @@ def shard_files(path: str) -> dict:
 
 
 def strip_payload(obj: dict) -> dict:
-    return {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
+    """The coordinator's stored form of a Secret/ConfigMap: no payload, and no metadata.managedFields (server-side
+    apply's field ownership: hundreds of bytes per object on a real apiserver, never read here)."""
+    out = {k: v for k, v in obj.items() if k not in ("data", "binaryData", "stringData")}
+    m = out.get("metadata")
+    if isinstance(m, dict) and "managedFields" in m:
+        out["metadata"] = {k: v for k, v in m.items() if k != "managedFields"}
+    return out
 
 
 def own_cgroups(proc_file: str = "/proc/self/cgroup") -> dict:

@@ -378,6 +378,8 @@ class ClusterState:
                     nm[k] = cm[k]
                 else:
                     nm.pop(k, None)
+            if "managedFields" not in nm and "managedFields" in cm:
+                nm["managedFields"] = cm["managedFields"]  # unset in the request: the apiserver keeps its own
             new["apiVersion"] = rt.api_version
             new["kind"] = rt.kind
             if self.status_subresource and rt.has_status:

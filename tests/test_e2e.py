@@ -718,3 +718,47 @@ async def test_python_executor_fallback_is_loud(tmp_path, monkeypatch, caplog):
                     await asyncio.wait_for(task, 20)
     finally:
         await env.stop()
+
+
+async def test_managed_fields_are_not_cached_and_survive_updates(tmp_path, monkeypatch):
+    """metadata.managedFields (server-side apply's field ownership; hundreds of bytes per object on a real
+    apiserver) is dropped from the C++ executor's cached shard objects and the coordinator's metadata-only store:
+    an update that omits it leaves the server's as it is (kube-apiserver semantics, mirrored by the fake), so a
+    shard copy with managedFields and stale data is brought up to date and keeps them."""
+    from ncc.controller.native_executor import binary_path
+    if binary_path() is None:
+        pytest.skip("the C++ executor is not built")
+    monkeypatch.delenv("NCC_EXECUTOR_IMPL", raising=False)
+    mf = [{"manager": "kubectl", "operation": "Update", "apiVersion": "v1", "time": "2025-01-01T00:00:00Z",
+           "fieldsType": "FieldsV1", "fieldsV1": {"f:data": {".": {}, "f:version": {}}}}]
+    env = await FakeEnvironment(1, str(tmp_path)).start()
+    cc, sc = env.controller_client(), env.shard_client(0)
+    try:
+        s = make_secret("s0", NS, version=2)
+        s["metadata"]["managedFields"] = mf
+        await cc.create(R.SECRETS, NS, s)
+        await cc.create(R.TEMPLATES, NS, make_template(0, NS, secrets=["s0"], configmaps=[]))
+        async with Running(env, "native", executor_impl="native") as app:
+            assert app.executor_impl == "native"
+
+            async def synced():
+                try:
+                    o = await sc.get(R.SECRETS, NS, "s0")
+                except E.NotFound:
+                    return False
+                return o["data"] == s["data"]
+            await wait_for(synced, timeout=5.0)
+            # the stale-data update path: the shard copy gains managedFields of its own, then the source changes
+            o = await sc.get(R.SECRETS, NS, "s0")
+            o["metadata"]["managedFields"] = mf
+            await sc.update(R.SECRETS, NS, o)
+            await mutate(cc, R.SECRETS, "s0", lambda x: x.__setitem__("data", {"version": "Mw=="}))
+
+            async def updated():
+                return (await sc.get(R.SECRETS, NS, "s0"))["data"] == {"version": "Mw=="}
+            await wait_for(updated, timeout=5.0)
+            assert (await sc.get(R.SECRETS, NS, "s0"))["metadata"].get("managedFields") == mf
+            cached = app.controller.secret_informer.store.get(NS, "s0")
+            assert cached is not None and "managedFields" not in cached["metadata"]
+    finally:
+        await env.stop()
