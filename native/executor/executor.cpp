@@ -1709,7 +1709,12 @@ static Task<void> shard_list(Shard& sh, int kind, std::string list_rv) {
         if (items && items->is_arr())
             for (auto& it : items->a) {
                 ShardPtr so = make_shard_obj(kind, std::move(it));
-                if (wanted(kind, *so)) fresh[key_of(so->ns, so->name)] = so;
+                if (!wanted(kind, *so)) continue;
+                std::string key = key_of(so->ns, so->name);
+                // the cached version when the listing has the same one: a relist of an unchanged shard holds one
+                // copy of its objects, not two (the relist-storm peak, bench/suite.py config 4)
+                auto old = inf.store.find(key);
+                fresh[std::move(key)] = old != inf.store.end() && old->second->rv == so->rv ? old->second : so;
             }
         const Value* lm = lst.get("metadata");
         rv = lm ? std::string(lm->sget("resourceVersion")) : rv;
@@ -2484,9 +2489,14 @@ static void handle_message(const mp::Obj& m) {
             // a large listing arrives in chunks: every one but the last carries "more" (relay.py)
             std::vector<CtlPtr>& objs = ex.partial_snapshot[kind];
             objs.reserve(objs.size() + lines->a.size());
+            auto& cached = ex.ctl[kind];
             for (const auto& l : lines->a) {
                 if (CtlPtr fast = ctl_scan(kind, l.s, type)) {
-                    if (type == "ADDED" || type == "MODIFIED") objs.push_back(std::move(fast));
+                    if (type == "ADDED" || type == "MODIFIED") {
+                        // the cached version when the snapshot has the same one (a coordinator relist): one copy
+                        auto old = cached.find(key_tmp(fast->ns, fast->name));
+                        objs.push_back(old != cached.end() && old->second->rv == fast->rv ? old->second : std::move(fast));
+                    }
                     continue;
                 }
                 try {

@@ -112,11 +112,18 @@ class Store:
         objects are already in stored form."""
         new_items: dict[ObjectKey, dict] = {}
         transform = None if transformed else self.transform
+        old_items = self._items
         for o in objs:
             if transform is not None:
                 o = transform(o)
-            new_items[key_of(o)] = o
-        old_items = self._items
+            k = key_of(o)
+            prev = old_items.get(k)
+            # the cached version when the listing has the same one: a relist of an unchanged cluster then holds
+            # one copy of its objects, not two, and handlers see the very same object (old is new)
+            if prev is not None and (prev.get("metadata") or {}).get("resourceVersion") == \
+                    (o.get("metadata") or {}).get("resourceVersion"):
+                o = prev
+            new_items[k] = o
         added, updated, deleted = [], [], []
         for k, o in new_items.items():
             prev = old_items.get(k)
