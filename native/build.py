@@ -24,6 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "ncc_native.cpp")]
 COMMON_HEADERS = [os.path.join(HERE, "common", f) for f in ("byte_scan.hpp", "hpack.hpp")]  # shared with the executor
+# the extension's parts by concern (ncc_native.cpp includes them in order)
+EXT_HEADERS = sorted(os.path.join(HERE, "ext", f) for f in os.listdir(os.path.join(HERE, "ext")) if f.endswith(".hpp"))
 
 
 def _werror() -> list:
@@ -156,7 +158,7 @@ def build_extension(debug: bool = False, sanitize: bool = False, verbose: bool =
         so_m = os.path.getmtime(out)
         with open(stamp) as f:
             same = f.read().strip() == flavor
-        if same and all(os.path.getmtime(s) <= so_m for s in sources + COMMON_HEADERS + [__file__]):
+        if same and all(os.path.getmtime(s) <= so_m for s in sources + COMMON_HEADERS + EXT_HEADERS + [__file__]):
             return out
     cxx = os.environ.get("CXX", "g++")
     flags = ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra",

@@ -23,6 +23,9 @@
 //  * parse_response_head(bytes) — HTTP/1.1 response heads for the client transport.
 //  * H2ClientParser / h2_request / hpack_encode — HTTP/2 framing and HPACK for the Python clients.
 //
+// The code is split by concern into native/ext/*.hpp (hashing, workqueue, scan, http1, pyjson, reports,
+// h2client), included in that order below; this file holds the bindings.
+//
 // The fake apiserver's native pieces (its HTTP/1.1 request-head parser, HTTP/2 server parser and response
 // encoder) are not here: they are test substrate, built into ncc/fakeapi/_native from native/fakeapi/
 //  — the product extension carries no server code.
@@ -67,2716 +70,14 @@ namespace py = pybind11;
 
 #define NCC_NATIVE_ABI 28
 
-// ----------------------------------------------------------------------------- hashing
 namespace {
-
-constexpr uint64_t kC1 = 0x87c37b91114253d5ULL;
-constexpr uint64_t kC2 = 0x4cf5ad432745937fULL;
-
-inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-
-inline uint64_t fmix(uint64_t k) {
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdULL;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ULL;
-    k ^= k >> 33;
-    return k;
-}
-
-// Streaming murmur3-style 64-bit hasher (word-at-a-time; not adversarially secure — it only has
-// to tell controller-desired content from shard-observed content).
-struct Hasher {
-    uint64_t h = 0x9e3779b97f4a7c15ULL;
-    uint64_t n = 0;
-
-    inline void word(uint64_t k) {
-        k *= kC1;
-        k = rotl(k, 31);
-        k *= kC2;
-        h ^= k;
-        h = rotl(h, 27) * 5 + 0x52dce729;
-        n += 8;
-    }
-    inline void tag(char t, uint64_t len) { word((static_cast<uint64_t>(static_cast<unsigned char>(t)) << 56) ^ len); }
-    void bytes(const char* p, size_t len) {
-        size_t i = 0;
-        for (; i + 8 <= len; i += 8) {
-            uint64_t k;
-            std::memcpy(&k, p + i, 8);
-            word(k);
-        }
-        uint64_t tail = 0;
-        size_t rem = len - i;
-        if (rem) {
-            std::memcpy(&tail, p + i, rem);
-            word(tail ^ (static_cast<uint64_t>(rem) << 59));
-        }
-    }
-    uint64_t digest() const { return fmix(h ^ n); }
-};
-
-struct KV {
-    const char* k;
-    Py_ssize_t klen;
-    PyObject* v;
-};
-
-void hash_obj(Hasher& hs, PyObject* o, int depth);
-
-void hash_str(Hasher& hs, PyObject* o) {
-    Py_ssize_t len = 0;
-    const char* s = PyUnicode_AsUTF8AndSize(o, &len);
-    if (!s) throw py::error_already_set();
-    hs.tag('s', static_cast<uint64_t>(len));
-    hs.bytes(s, static_cast<size_t>(len));
-}
-
-void hash_obj(Hasher& hs, PyObject* o, int depth) {
-    if (depth > 512) throw py::value_error("fingerprint: nesting too deep");
-    if (o == Py_None) {
-        hs.tag('n', 0);
-    } else if (o == Py_True) {
-        hs.tag('t', 1);
-    } else if (o == Py_False) {
-        hs.tag('f', 0);
-    } else if (PyUnicode_Check(o)) {
-        hash_str(hs, o);
-    } else if (PyLong_Check(o)) {
-        int overflow = 0;
-        long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
-        if (overflow) {
-            PyObject* r = PyObject_Str(o);
-            if (!r) throw py::error_already_set();
-            hs.tag('I', 0);
-            hash_str(hs, r);
-            Py_DECREF(r);
-        } else {
-            hs.tag('i', 8);
-            hs.word(static_cast<uint64_t>(v));
-        }
-    } else if (PyFloat_Check(o)) {
-        double d = PyFloat_AS_DOUBLE(o);
-        if (d == 0.0) d = 0.0;  // fold -0.0
-        uint64_t bits;
-        std::memcpy(&bits, &d, 8);
-        hs.tag('r', 8);
-        hs.word(bits);
-    } else if (PyDict_Check(o)) {
-        Py_ssize_t n = PyDict_Size(o);
-        hs.tag('d', static_cast<uint64_t>(n));
-        std::vector<KV> items;
-        items.reserve(static_cast<size_t>(n));
-        PyObject *k, *v;
-        Py_ssize_t pos = 0;
-        while (PyDict_Next(o, &pos, &k, &v)) {
-            if (!PyUnicode_Check(k)) throw py::type_error("fingerprint: dict keys must be str");
-            Py_ssize_t klen = 0;
-            const char* ks = PyUnicode_AsUTF8AndSize(k, &klen);
-            if (!ks) throw py::error_already_set();
-            items.push_back({ks, klen, v});
-        }
-        std::sort(items.begin(), items.end(), [](const KV& a, const KV& b) {
-            int c = std::memcmp(a.k, b.k, static_cast<size_t>(std::min(a.klen, b.klen)));
-            return c != 0 ? c < 0 : a.klen < b.klen;
-        });
-        for (const auto& it : items) {
-            hs.tag('k', static_cast<uint64_t>(it.klen));
-            hs.bytes(it.k, static_cast<size_t>(it.klen));
-            hash_obj(hs, it.v, depth + 1);
-        }
-    } else if (PyList_Check(o) || PyTuple_Check(o)) {
-        PyObject* seq = o;
-        Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-        PyObject** items = PySequence_Fast_ITEMS(seq);
-        hs.tag('l', static_cast<uint64_t>(n));
-        for (Py_ssize_t i = 0; i < n; ++i) hash_obj(hs, items[i], depth + 1);
-    } else if (PyBytes_Check(o)) {
-        hs.tag('b', static_cast<uint64_t>(PyBytes_GET_SIZE(o)));
-        hs.bytes(PyBytes_AS_STRING(o), static_cast<size_t>(PyBytes_GET_SIZE(o)));
-    } else {
-        PyObject* r = PyObject_Repr(o);
-        if (!r) throw py::error_already_set();
-        hs.tag('o', 0);
-        hash_str(hs, r);
-        Py_DECREF(r);
-    }
-}
-
-uint64_t fingerprint(py::handle obj) {
-    Hasher hs;
-    hash_obj(hs, obj.ptr(), 0);
-    return hs.digest();
-}
-
-py::list fingerprint_many(py::sequence objs) {
-    py::list out;
-    for (auto o : objs) out.append(py::int_(fingerprint(o)));
-    return out;
-}
-
-// ----------------------------------------------------------------------------- work queue
-class RateLimitingQueue {
-  public:
-    RateLimitingQueue(double base_delay, double max_delay, double qps, int burst)
-        : base_(base_delay), max_(max_delay), qps_(qps), burst_(burst), tokens_(static_cast<double>(burst)) {}
-
-    // Type
-    bool add(const std::string& key) {
-        std::lock_guard<std::mutex> g(mu_);
-        return add_locked(key);
-    }
-
-    py::object try_get() {
-        std::string key;
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            if (queue_.empty()) return py::none();
-            key = std::move(queue_.front());
-            queue_.pop_front();
-            processing_.insert(key);
-            dirty_.erase(key);
-        }
-        return py::str(key);
-    }
-
-    bool done(const std::string& key) {
-        std::lock_guard<std::mutex> g(mu_);
-        processing_.erase(key);
-        if (dirty_.count(key)) {
-            queue_.push_back(key);
-            return true;
-        }
-        return false;
-    }
-
-    size_t length() {
-        std::lock_guard<std::mutex> g(mu_);
-        return queue_.size();
-    }
-    size_t processing() {
-        std::lock_guard<std::mutex> g(mu_);
-        return processing_.size();
-    }
-    void shutdown() {
-        std::lock_guard<std::mutex> g(mu_);
-        shutting_down_ = true;
-    }
-    bool shutting_down() {
-        std::lock_guard<std::mutex> g(mu_);
-        return shutting_down_;
-    }
-
-    // Delaying
-    bool add_after(const std::string& key, double delay, double now) {
-        std::lock_guard<std::mutex> g(mu_);
-        return add_after_locked(key, delay, now);
-    }
-
-    size_t promote(double now) {
-        std::lock_guard<std::mutex> g(mu_);
-        size_t n = 0;
-        while (!heap_.empty() && heap_.top().ready <= now) {
-            Waiting w = heap_.top();
-            heap_.pop();
-            auto it = waiting_ready_.find(w.key);
-            if (it == waiting_ready_.end() || it->second != w.ready) continue;  // superseded
-            waiting_ready_.erase(it);
-            if (add_locked(w.key)) ++n;
-        }
-        return n;
-    }
-
-    double next_ready_in(double now) {
-        std::lock_guard<std::mutex> g(mu_);
-        while (!heap_.empty()) {
-            const Waiting& w = heap_.top();
-            auto it = waiting_ready_.find(w.key);
-            if (it != waiting_ready_.end() && it->second == w.ready) break;
-            heap_.pop();
-        }
-        if (heap_.empty()) return -1.0;
-        return std::max(0.0, heap_.top().ready - now);
-    }
-
-    size_t waiting() {
-        std::lock_guard<std::mutex> g(mu_);
-        return waiting_ready_.size();
-    }
-
-    // Queued, being processed or waiting for a delayed add: a worker pass for the key is pending or running.
-    bool busy(const std::string& key) {
-        std::lock_guard<std::mutex> g(mu_);
-        return dirty_.count(key) || processing_.count(key) || waiting_ready_.count(key);
-    }
-
-    // RateLimiting: MaxOf(ItemExponentialFailure(base, max), Bucket(qps, burst))
-    double add_rate_limited(const std::string& key, double now) {
-        std::lock_guard<std::mutex> g(mu_);
-        double d = std::max(exp_when(key), bucket_when(now));
-        add_after_locked(key, d, now);
-        return d;
-    }
-
-    void forget(const std::string& key) {
-        std::lock_guard<std::mutex> g(mu_);
-        failures_.erase(key);
-    }
-
-    int num_requeues(const std::string& key) {
-        std::lock_guard<std::mutex> g(mu_);
-        auto it = failures_.find(key);
-        return it == failures_.end() ? 0 : it->second;
-    }
-
-  private:
-    struct Waiting {
-        double ready;
-        uint64_t seq;
-        std::string key;
-    };
-    struct Later {
-        bool operator()(const Waiting& a, const Waiting& b) const {
-            return a.ready != b.ready ? a.ready > b.ready : a.seq > b.seq;
-        }
-    };
-
-    bool add_locked(const std::string& key) {
-        if (shutting_down_ || dirty_.count(key)) return false;
-        dirty_.insert(key);
-        if (processing_.count(key)) return false;
-        queue_.push_back(key);
-        return true;
-    }
-
-    bool add_after_locked(const std::string& key, double delay, double now) {
-        if (shutting_down_) return false;
-        if (delay <= 0) return add_locked(key);
-        double ready = now + delay;
-        auto it = waiting_ready_.find(key);
-        if (it != waiting_ready_.end() && it->second <= ready) return false;
-        waiting_ready_[key] = ready;
-        heap_.push(Waiting{ready, ++seq_, key});
-        return false;
-    }
-
-    double exp_when(const std::string& key) {
-        int& f = failures_[key];
-        int e = f++;
-        if (e >= 64) return max_;
-        double d = base_ * std::ldexp(1.0, e);
-        return d > max_ ? max_ : d;
-    }
-
-    double bucket_when(double now) {
-        if (qps_ <= 0) return 0.0;
-        if (!has_last_) {
-            last_ = now;
-            has_last_ = true;
-        }
-        double elapsed = now - last_;
-        if (elapsed > 0) {
-            tokens_ = std::min(static_cast<double>(burst_), tokens_ + elapsed * qps_);
-            last_ = now;
-        }
-        tokens_ -= 1.0;
-        return tokens_ >= 0 ? 0.0 : -tokens_ / qps_;
-    }
-
-    std::mutex mu_;
-    double base_, max_, qps_;
-    int burst_;
-    double tokens_;
-    double last_ = 0.0;
-    bool has_last_ = false;
-    std::unordered_map<std::string, int> failures_;
-    std::deque<std::string> queue_;
-    std::unordered_set<std::string> dirty_, processing_;
-    std::priority_queue<Waiting, std::vector<Waiting>, Later> heap_;
-    std::unordered_map<std::string, double> waiting_ready_;
-    uint64_t seq_ = 0;
-    bool shutting_down_ = false;
-};
-
-
-// ----------------------------------------------------------------------------- watch-event scanner
-// scan_event(line) -> (type, namespace, name, resourceVersion) | None
-//
-// Structural scan of one watch-stream line {"type":..., "object":{..., "metadata":{...}}} that reads
-// only the four strings the informer needs to recognise the echo of its own write, skipping every
-// other value by bracket matching.  No Python objects are built for the (large) spec/data payloads;
-// a full json.loads happens only for events that are not our own echoes.  Any input it does not
-// fully understand (escaped keys or values, malformed JSON) returns None and the caller falls back.
-class Scanner {
-  public:
-    Scanner(const char* p, size_t n) : p_(p), e_(p + n) {}
-
-    // owners != nullptr → also collect metadata.ownerReferences[*].name and .uid (escapes → failure)
-    std::vector<std::string_view>* owners = nullptr;
-    std::vector<std::string_view>* owner_uids = nullptr;
-    std::string_view* uid = nullptr;  // non-null → also read metadata.uid
-
-    // top-level object {"apiVersion":..., "metadata":{...}, ...} (a write response)
-    bool scan_object(std::string_view& ns, std::string_view& name, std::string_view& rv) {
-        return object_meta(ns, name, rv);
-    }
-
-    // raw JSON of the top-level members named in `keys` (out[i].data() == nullptr: absent)
-    bool members(const std::vector<std::string>& keys, std::vector<std::string_view>& out) {
-        out.assign(keys.size(), std::string_view());
-        if (!expect('{')) return false;
-        if (peek('}')) { ++p_; return true; }
-        for (;;) {
-            std::string_view key;
-            if (!str(key) || !expect(':')) return false;
-            ws();
-            const char* s = p_;
-            if (!skip_value()) return false;
-            for (size_t i = 0; i < keys.size(); ++i)
-                if (key == keys[i]) out[i] = std::string_view(s, static_cast<size_t>(p_ - s));
-            if (peek(',')) { ++p_; continue; }
-            return expect('}');
-        }
-    }
-
-    bool scan(std::string_view& type, std::string_view& ns, std::string_view& name, std::string_view& rv) {
-        if (!expect('{')) return false;
-        bool have_type = false, have_obj = false;
-        if (peek('}')) return false;
-        for (;;) {
-            std::string_view key;
-            if (!str(key) || !expect(':')) return false;
-            if (key == "type") {
-                if (!str(type)) return false;
-                have_type = true;
-            } else if (key == "object") {
-                if (!object_meta(ns, name, rv)) return false;
-                have_obj = true;
-            } else if (!skip_value()) {
-                return false;
-            }
-            if (have_type && have_obj) return true;
-            if (peek(',')) { ++p_; continue; }
-            return false;
-        }
-    }
-
-  private:
-    const char* p_;
-    const char* e_;
-
-    void ws() {
-        while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
-    }
-    bool peek(char c) {
-        ws();
-        return p_ < e_ && *p_ == c;
-    }
-    bool expect(char c) {
-        ws();
-        if (p_ >= e_ || *p_ != c) return false;
-        ++p_;
-        return true;
-    }
-    // a string without escapes (anything escaped makes the caller fall back to json.loads)
-    bool str(std::string_view& out) {
-        ws();
-        if (p_ >= e_ || *p_ != '"') return false;
-        const char* s = ++p_;
-        p_ = ncc::find_quote(p_, e_);
-        if (p_ >= e_ || *p_ == '\\') return false;
-        out = std::string_view(s, static_cast<size_t>(p_ - s));
-        ++p_;
-        return true;
-    }
-    bool skip_string() {
-        if (p_ >= e_ || *p_ != '"') return false;
-        const char* q = ncc::skip_string_text(p_, e_);
-        if (q == nullptr) return false;
-        p_ = q;
-        return true;
-    }
-    bool skip_value() {
-        ws();
-        if (p_ >= e_) return false;
-        char c = *p_;
-        if (c == '"') return skip_string();
-        if (c == '{' || c == '[') {  // 64 bytes per step (native/common/byte_scan.hpp)
-            const char* q = ncc::skip_container_text(p_, e_);
-            if (q == nullptr) return false;
-            p_ = q;
-            return true;
-        }
-        while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n' &&
-               *p_ != '\t' && *p_ != '\r')
-            ++p_;
-        return true;
-    }
-    bool object_meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
-        if (!expect('{')) return false;
-        bool found = false;
-        if (peek('}')) { ++p_; return false; }
-        for (;;) {
-            std::string_view key;
-            if (!str(key) || !expect(':')) return false;
-            if (key == "metadata") {
-                if (!meta(ns, name, rv)) return false;
-                found = true;
-            } else if (!skip_value()) {
-                return false;
-            }
-            if (peek(',')) { ++p_; continue; }
-            if (!expect('}')) return false;
-            return found;
-        }
-    }
-    // [{"apiVersion":..., "kind":..., "name": "...", "uid": ...}, ...] → owners->push_back(name)
-    bool owner_refs() {
-        ws();
-        if (p_ < e_ && *p_ == 'n') return skip_value();  // null
-        if (!expect('[')) return false;
-        if (peek(']')) { ++p_; return true; }
-        for (;;) {
-            if (!expect('{')) return false;
-            std::string_view oname, ouid;
-            if (!peek('}')) {
-                for (;;) {
-                    std::string_view key;
-                    if (!str(key) || !expect(':')) return false;
-                    if (key == "name") {
-                        if (!str(oname)) return false;
-                    } else if (key == "uid") {
-                        if (!str(ouid)) return false;
-                    } else if (!skip_value()) {
-                        return false;
-                    }
-                    if (peek(',')) { ++p_; continue; }
-                    break;
-                }
-            }
-            if (!expect('}')) return false;
-            owners->push_back(oname);
-            owner_uids->push_back(ouid);
-            if (peek(',')) { ++p_; continue; }
-            return expect(']');
-        }
-    }
-    bool meta(std::string_view& ns, std::string_view& name, std::string_view& rv) {
-        if (!expect('{')) return false;
-        bool have_name = false, have_rv = false;
-        if (peek('}')) { ++p_; return false; }
-        for (;;) {
-            std::string_view key;
-            if (!str(key) || !expect(':')) return false;
-            if (key == "name") {
-                if (!str(name)) return false;
-                have_name = true;
-            } else if (key == "namespace") {
-                if (!str(ns)) return false;
-            } else if (key == "resourceVersion") {
-                if (!str(rv)) return false;
-                have_rv = true;
-            } else if (uid != nullptr && key == "uid") {
-                if (!str(*uid)) return false;
-            } else if (owners != nullptr && key == "ownerReferences") {
-                if (!owner_refs()) return false;
-            } else if (!skip_value()) {
-                return false;
-            }
-            if (peek(',')) { ++p_; continue; }
-            if (!expect('}')) return false;
-            return have_name && have_rv;
-        }
-    }
-};
-
-py::object scan_event(py::bytes line) {
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view type, ns, name, rv;
-    Scanner sc(buf, static_cast<size_t>(len));
-    if (!sc.scan(type, ns, name, rv)) return py::none();
-    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
-                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()));
-}
-
-// scan_event_owners(line) -> (type, namespace, name, resourceVersion, (owner names...), (owner uids...)) | None
-py::object scan_event_owners(py::bytes line) {
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view type, ns, name, rv;
-    std::vector<std::string_view> owners, uids;
-    Scanner sc(buf, static_cast<size_t>(len));
-    sc.owners = &owners;
-    sc.owner_uids = &uids;
-    if (!sc.scan(type, ns, name, rv)) return py::none();
-    py::tuple o(owners.size()), u(uids.size());
-    for (size_t i = 0; i < owners.size(); ++i) o[i] = py::str(owners[i].data(), owners[i].size());
-    for (size_t i = 0; i < uids.size(); ++i) u[i] = py::str(uids[i].data(), uids[i].size());
-    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
-                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u);
-}
-
-// ----------------------------------------------------------------------------- partitions
-// crc32 (IEEE, reflected; identical to zlib.crc32) of "<ns>/<name>": the executors' key → partition map
-// (ncc.controller.executor.key_part), computed here so foreign-partition watch lines are dropped without
-// building Python strings.
-static uint32_t kCrcTable[256];
-static bool crc_table_init() {
-    for (uint32_t i = 0; i < 256; ++i) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        kCrcTable[i] = c;
-    }
-    return true;
-}
-static const bool kCrcReady = crc_table_init();
-
-static uint32_t crc_update(uint32_t c, std::string_view s) {
-    for (unsigned char ch : s) c = kCrcTable[(c ^ ch) & 0xFFu] ^ (c >> 8);
-    return c;
-}
-
-static uint32_t key_crc(std::string_view ns, std::string_view name) {
-    uint32_t c = crc_update(0xFFFFFFFFu, ns);
-    c = crc_update(c, std::string_view("/", 1));
-    return crc_update(c, name) ^ 0xFFFFFFFFu;
-}
-
-// scan_event_part(line, parts, default_ns) -> (type, namespace, name, resourceVersion, (owner names...),
-//     (owner uids...), key_partition, owner_partition_mask) | None
-// key_partition = crc32("ns/name") % parts; bit p of owner_partition_mask is set when some owner
-// template "ns/<owner>" falls in partition p (parts <= 63).  An empty namespace uses `default_ns`.
-py::object scan_event_part(py::bytes line, int parts, const std::string& default_ns) {
-    if (parts < 1 || parts > 63) throw py::value_error("scan_event_part: parts must be in 1..63");
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view type, ns, name, rv;
-    std::vector<std::string_view> owners, uids;
-    Scanner sc(buf, static_cast<size_t>(len));
-    sc.owners = &owners;
-    sc.owner_uids = &uids;
-    if (!sc.scan(type, ns, name, rv)) return py::none();
-    std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-    const uint32_t up = static_cast<uint32_t>(parts);
-    long long kp = static_cast<long long>(key_crc(kns, name) % up);
-    unsigned long long mask = 0;
-    py::tuple o(owners.size()), u(uids.size());
-    for (size_t i = 0; i < owners.size(); ++i) {
-        mask |= 1ull << (key_crc(kns, owners[i]) % up);
-        o[i] = py::str(owners[i].data(), owners[i].size());
-    }
-    for (size_t i = 0; i < uids.size(); ++i) u[i] = py::str(uids[i].data(), uids[i].size());
-    return py::make_tuple(py::str(type.data(), type.size()), py::str(ns.data(), ns.size()),
-                          py::str(name.data(), name.size()), py::str(rv.data(), rv.size()), o, u, kp, mask);
-}
-
-// relay_scan(line, parts, default_ns) -> (type_code, namespace, name, key_partition, owner_partition_mask,
-//     n_owners) | None.  The coordinator's watch relay (ncc/controller/relay.py) routes every controller-side
-// watch line to the executors whose key partitions need it with this one call: type_code 0 ADDED,
-// 1 MODIFIED, 2 DELETED, 3 anything else (BOOKMARK, ERROR); `namespace` is already defaulted.
-py::object relay_scan(py::bytes line, int parts, const std::string& default_ns) {
-    if (parts < 1 || parts > 63) throw py::value_error("relay_scan: parts must be in 1..63");
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(line.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view type, ns, name, rv;
-    std::vector<std::string_view> owners, uids;
-    Scanner sc(buf, static_cast<size_t>(len));
-    sc.owners = &owners;
-    sc.owner_uids = &uids;
-    if (!sc.scan(type, ns, name, rv)) return py::none();
-    int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
-    std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-    const uint32_t up = static_cast<uint32_t>(parts);
-    long long kp = static_cast<long long>(key_crc(kns, name) % up);
-    unsigned long long mask = 0;
-    for (const auto& o : owners) mask |= 1ull << (key_crc(kns, o) % up);
-    return py::make_tuple(code, py::str(kns.data(), kns.size()), py::str(name.data(), name.size()), kp, mask,
-                          static_cast<long long>(owners.size()));
-}
-
-// Does a Python str equal these UTF-8 bytes?
-static bool str_eq(PyObject* o, std::string_view v) {
-    if (o == nullptr || !PyUnicode_Check(o)) return v.empty() && o == nullptr;
-    Py_ssize_t n = 0;
-    const char* u = PyUnicode_AsUTF8AndSize(o, &n);
-    if (u == nullptr) {
-        PyErr_Clear();
-        return false;
-    }
-    return static_cast<size_t>(n) == v.size() && std::memcmp(u, v.data(), v.size()) == 0;
-}
-
-// owner_filter(lines, items, assumed, default_ns) -> (kept lines, dropped, rv of the last line if dropped)
-// The metadata-only informer's filter over a whole batch (ncc/cache/informer.py `_consume`): a MODIFIED
-// line of an object cached in `items` (the store's dict, keyed (namespace, name)) whose ownerReferences
-// names and uids equal the cached ones carries nothing such a store keeps, and is dropped.  Every other line
-// — other event types, unknown or overlaid (`assumed`) keys, unreadable lines — is kept for the Python path.
-py::tuple owner_filter(py::list lines, py::dict items, py::dict assumed, const std::string& default_ns) {
-    py::list keep;
-    long long dropped = 0;
-    std::string_view last_rv;
-    bool last_dropped = false;
-    const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
-    std::vector<std::string_view> owners, uids;
-    static PyObject* k_meta = PyUnicode_InternFromString("metadata");
-    static PyObject* k_refs = PyUnicode_InternFromString("ownerReferences");
-    static PyObject* k_name = PyUnicode_InternFromString("name");
-    static PyObject* k_uid = PyUnicode_InternFromString("uid");
-    for (Py_ssize_t i = 0; i < n; ++i) {
-        PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
-        last_dropped = false;
-        char* buf = nullptr;
-        Py_ssize_t len = 0;
-        bool drop = false;
-        std::string_view type, ns, name, rv;
-        if (PyBytes_Check(line) && PyBytes_AsStringAndSize(line, &buf, &len) == 0) {
-            owners.clear();
-            uids.clear();
-            Scanner sc(buf, static_cast<size_t>(len));
-            sc.owners = &owners;
-            sc.owner_uids = &uids;
-            PyObject* kn = nullptr;
-            PyObject* nm = nullptr;
-            if (sc.scan(type, ns, name, rv) && type == "MODIFIED") {
-                std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-                kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
-                nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
-                if (nm == nullptr) {  // not UTF-8: kept, the Python path decides
-                    Py_XDECREF(kn);
-                    PyErr_Clear();
-                }
-            }
-            if (nm != nullptr) {
-                py::tuple key = py::make_tuple(py::reinterpret_steal<py::object>(kn), py::reinterpret_steal<py::object>(nm));
-                PyObject* cur = PyDict_GetItemWithError(items.ptr(), key.ptr());
-                if (cur == nullptr && PyErr_Occurred()) throw py::error_already_set();
-                int overlaid = PyDict_Contains(assumed.ptr(), key.ptr());
-                if (overlaid < 0) throw py::error_already_set();
-                if (cur != nullptr && !overlaid && PyDict_Check(cur)) {
-                    PyObject* m = PyDict_GetItem(cur, k_meta);
-                    PyObject* refs = m != nullptr && PyDict_Check(m) ? PyDict_GetItem(m, k_refs) : nullptr;
-                    if (refs == nullptr || refs == Py_None) {
-                        drop = owners.empty();
-                    } else if (PyList_Check(refs) && static_cast<size_t>(PyList_GET_SIZE(refs)) == owners.size()) {
-                        drop = true;
-                        for (size_t j = 0; j < owners.size() && drop; ++j) {
-                            PyObject* r = PyList_GET_ITEM(refs, static_cast<Py_ssize_t>(j));
-                            if (!PyDict_Check(r)) {
-                                drop = false;
-                                break;
-                            }
-                            PyObject* rn = PyDict_GetItem(r, k_name);
-                            PyObject* ru = PyDict_GetItem(r, k_uid);
-                            drop = (rn == nullptr ? owners[j].empty() : str_eq(rn, owners[j])) &&
-                                   (ru == nullptr ? uids[j].empty() : str_eq(ru, uids[j]));
-                        }
-                    }
-                }
-            }
-        } else {
-            PyErr_Clear();
-        }
-        if (drop) {
-            ++dropped;
-            last_rv = rv;
-            last_dropped = true;
-        } else if (PyList_Append(keep.ptr(), line) != 0) {
-            throw py::error_already_set();
-        }
-    }
-    py::object rv_o = last_dropped ? py::object(py::str(last_rv.data(), last_rv.size())) : py::object(py::none());
-    return py::make_tuple(keep, dropped, rv_o);
-}
-
-// relay_index(lines, raw, default_ns) -> the lines to forward.  The one-partition relay's whole loop in one
-// call: each ADDED/MODIFIED line is stored in `raw` under (namespace, name), a DELETED one removes its key,
-// and every object event is forwarded; BOOKMARK/ERROR and unreadable lines are dropped (the coordinator's
-// informer handles those).  Same result as relay_scan per line (ncc/controller/relay.py `on_lines`).
-py::list relay_index(py::list lines, py::dict raw, const std::string& default_ns) {
-    py::list keep;
-    PyObject* rd = raw.ptr();
-    const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
-    for (Py_ssize_t i = 0; i < n; ++i) {
-        PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
-        char* buf = nullptr;
-        Py_ssize_t len = 0;
-        if (PyBytes_AsStringAndSize(line, &buf, &len) != 0) throw py::error_already_set();
-        std::string_view type, ns, name, rv;
-        Scanner sc(buf, static_cast<size_t>(len));
-        if (!sc.scan(type, ns, name, rv)) continue;
-        int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
-        if (code == 3) continue;
-        std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
-        PyObject* kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
-        PyObject* nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
-        if (nm == nullptr) {  // not UTF-8: forwarded for the executor to judge, not indexed
-            Py_XDECREF(kn);
-            PyErr_Clear();
-            if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
-            continue;
-        }
-        py::tuple key = py::make_tuple(py::reinterpret_steal<py::object>(kn), py::reinterpret_steal<py::object>(nm));
-        if (code == 2) {
-            if (PyDict_DelItem(rd, key.ptr()) != 0) {
-                if (!PyErr_ExceptionMatches(PyExc_KeyError)) throw py::error_already_set();
-                PyErr_Clear();
-            }
-        } else if (PyDict_SetItem(rd, key.ptr(), line) != 0) {
-            throw py::error_already_set();
-        }
-        if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
-    }
-    return keep;
-}
-
-py::int_ key_partition(const std::string& ns, const std::string& name, int parts) {
-    if (parts < 1) throw py::value_error("key_partition: parts must be >= 1");
-    return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));
-}
-
-// ----------------------------------------------------------------------------- HTTP/1.1 response heads
-static std::string_view trim(std::string_view v) {
-    while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
-    while (!v.empty() && (v.back() == ' ' || v.back() == '\t' || v.back() == '\r')) v.remove_suffix(1);
-    return v;
-}
-
-static bool ieq(std::string_view a, std::string_view b) {
-    if (a.size() != b.size()) return false;
-    for (size_t i = 0; i < a.size(); ++i) {
-        char x = a[i], y = b[i];
-        if (x >= 'A' && x <= 'Z') x = static_cast<char>(x - 'A' + 'a');
-        if (x != y) return false;
-    }
-    return true;
-}
-
-static bool icontains(std::string_view hay, std::string_view needle) {
-    if (needle.size() > hay.size()) return false;
-    for (size_t i = 0; i + needle.size() <= hay.size(); ++i)
-        if (ieq(hay.substr(i, needle.size()), needle)) return true;
-    return false;
-}
-
-// parse_response_head(head) -> (status, content_length | -1, chunked, connection_close, retry_after | None)
-// `head` is everything before the blank line.  Only the headers the client acts on are extracted.
-py::object parse_response_head(py::bytes head) {
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(head.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view h(buf, static_cast<size_t>(len));
-    size_t eol = h.find("\r\n");
-    std::string_view first = h.substr(0, eol);
-    size_t sp = first.find(' ');
-    if (sp == std::string_view::npos || first.substr(0, 5) != "HTTP/") throw py::value_error("bad status line");
-    long status = 0;
-    size_t i = sp + 1;
-    int digits = 0;
-    for (; i < first.size() && first[i] >= '0' && first[i] <= '9'; ++i, ++digits) status = status * 10 + (first[i] - '0');
-    if (digits != 3) throw py::value_error("bad status code");
-    long long clen = -1;
-    bool chunked = false, close = false;
-    py::object retry = py::none();
-    size_t pos = eol == std::string_view::npos ? h.size() : eol + 2;
-    while (pos < h.size()) {
-        size_t e = h.find("\r\n", pos);
-        std::string_view line = h.substr(pos, e == std::string_view::npos ? std::string_view::npos : e - pos);
-        pos = e == std::string_view::npos ? h.size() : e + 2;
-        size_t c = line.find(':');
-        if (c == std::string_view::npos) continue;
-        std::string_view k = trim(line.substr(0, c)), v = trim(line.substr(c + 1));
-        if (ieq(k, "content-length")) {
-            long long n = 0;
-            if (v.empty()) throw py::value_error("bad content-length");
-            for (char ch : v) {
-                if (ch < '0' || ch > '9') throw py::value_error("bad content-length");
-                n = n * 10 + (ch - '0');
-                if (n > (1LL << 40)) throw py::value_error("content-length too large");
-            }
-            clen = n;
-        } else if (ieq(k, "transfer-encoding")) {
-            chunked = chunked || icontains(v, "chunked");
-        } else if (ieq(k, "connection")) {
-            close = ieq(v, "close");
-        } else if (ieq(k, "retry-after")) {
-            retry = py::str(v.data(), v.size());
-        }
-    }
-    return py::make_tuple(status, clen, chunked, close, retry);
-}
-
-// chunk_lines(buf, state, linebuf) -> (lines, state, consumed, done, linebuf)
-// Walks the chunked-transfer body bytes in `buf` (a bytearray; the caller deletes the `consumed` prefix) and
-// returns the complete non-empty newline-terminated lines they carry, a chunk's data taken as it arrives,
-// not once the whole chunk is in.  `state`: -1 a chunk-size line is next, -2 trailer lines after the last
-// chunk, -3 the CRLF after a chunk's data, n > 0 data bytes left in the current chunk.  `linebuf` holds the
-// start of an unfinished line between calls; `done` once the blank line ending the trailers was read.
-// Same lines as ncc/kube/transport.py's Python path (`_parse_chunks` + `_feed_stream`).
-py::object chunk_lines(py::object buf_o, long long state, py::object linebuf_o) {
-    PyObject* b = buf_o.ptr();
-    PyObject* lb = linebuf_o.ptr();
-    if (!PyByteArray_Check(b) || !PyByteArray_Check(lb)) throw py::type_error("chunk_lines: bytearray expected");
-    const char* p = PyByteArray_AS_STRING(b);
-    const size_t n = static_cast<size_t>(PyByteArray_GET_SIZE(b));
-    std::string cur(PyByteArray_AS_STRING(lb), static_cast<size_t>(PyByteArray_GET_SIZE(lb)));
-    PyObject* lines = PyList_New(0);
-    if (lines == nullptr) throw py::error_already_set();
-    py::object lines_o = py::reinterpret_steal<py::object>(lines);
-    auto push = [&](const char* d, size_t len) {
-        PyObject* line = PyBytes_FromStringAndSize(d, static_cast<Py_ssize_t>(len));
-        if (line == nullptr || PyList_Append(lines, line) != 0) {
-            Py_XDECREF(line);
-            throw py::error_already_set();
-        }
-        Py_DECREF(line);
-    };
-    auto data = [&](const char* d, size_t len) {
-        size_t s0 = 0;
-        while (s0 < len) {
-            const char* nl = static_cast<const char*>(std::memchr(d + s0, '\n', len - s0));
-            if (nl == nullptr) {
-                cur.append(d + s0, len - s0);
-                return;
-            }
-            size_t e = static_cast<size_t>(nl - d);
-            if (cur.empty()) {
-                if (e > s0) push(d + s0, e - s0);
-            } else {
-                cur.append(d + s0, e - s0);
-                push(cur.data(), cur.size());
-                cur.clear();
-            }
-            s0 = e + 1;
-        }
-    };
-    auto crlf = [&](size_t from) -> size_t {
-        for (size_t i = from; i + 1 < n; ++i) {
-            const char* q = static_cast<const char*>(std::memchr(p + i, '\r', n - 1 - i));
-            if (q == nullptr) return std::string::npos;
-            i = static_cast<size_t>(q - p);
-            if (p[i + 1] == '\n') return i;
-        }
-        return std::string::npos;
-    };
-    size_t pos = 0;
-    bool done = false;
-    while (pos < n && !done) {
-        if (state == -1) {
-            size_t e = crlf(pos);
-            if (e == std::string::npos) break;
-            std::string_view line(p + pos, e - pos);
-            size_t semi = line.find(';');
-            std::string_view hex = trim(line.substr(0, semi));
-            if (hex.empty()) throw py::value_error("bad chunk size line");
-            long long size = 0;
-            for (char ch : hex) {
-                int v = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10
-                      : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
-                if (v < 0) throw py::value_error("bad chunk size line");
-                size = size * 16 + v;
-                if (size > (1LL << 40)) throw py::value_error("chunk too large");
-            }
-            pos = e + 2;
-            state = size > 0 ? size : -2;
-        } else if (state == -2) {
-            size_t e = crlf(pos);
-            if (e == std::string::npos) break;
-            done = e == pos;
-            pos = e + 2;
-        } else if (state == -3) {
-            if (n - pos < 2) break;
-            if (p[pos] != '\r' || p[pos + 1] != '\n') throw py::value_error("chunk data not followed by CRLF");
-            pos += 2;
-            state = -1;
-        } else if (state > 0) {
-            size_t take = std::min(static_cast<size_t>(state), n - pos);
-            data(p + pos, take);
-            pos += take;
-            state -= static_cast<long long>(take);
-            if (state == 0) state = -3;
-        } else {
-            throw py::value_error("bad chunk state");
-        }
-    }
-    PyObject* rest = PyByteArray_FromStringAndSize(cur.data(), static_cast<Py_ssize_t>(cur.size()));
-    if (rest == nullptr) throw py::error_already_set();
-    return py::make_tuple(lines_o, state, pos, done, py::reinterpret_steal<py::object>(rest));
-}
-
-
-// ----------------------------------------------------------------------------- JSON encoder
-// dumps(obj) -> bytes: compact JSON (separators "," and ":") of a JSON-shaped Python value, key order
-// preserved.  Non-ASCII text is emitted as UTF-8 (valid JSON; json.loads reads it back identically),
-// so strings need only the quote/backslash/control-character escapes.  Used for request bodies and the
-// fake apiserver's responses and watch lines, where json.dumps was the largest single per-object cost.
-class JsonWriter {
-  public:
-    std::string out;
-
-    void value(PyObject* o, int depth) {
-        if (depth > 512) throw py::value_error("dumps: nesting too deep");
-        if (o == Py_None) {
-            out.append("null", 4);
-        } else if (o == Py_True) {
-            out.append("true", 4);
-        } else if (o == Py_False) {
-            out.append("false", 5);
-        } else if (PyUnicode_Check(o)) {
-            str(o);
-        } else if (PyLong_Check(o)) {
-            int overflow = 0;
-            long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
-            if (overflow) {
-                PyObject* r = PyObject_Str(o);
-                if (!r) throw py::error_already_set();
-                Py_ssize_t n = 0;
-                const char* s = PyUnicode_AsUTF8AndSize(r, &n);
-                out.append(s, static_cast<size_t>(n));
-                Py_DECREF(r);
-            } else {
-                char buf[32];
-                int n = std::snprintf(buf, sizeof buf, "%lld", v);
-                out.append(buf, static_cast<size_t>(n));
-            }
-        } else if (PyFloat_Check(o)) {
-            double d = PyFloat_AS_DOUBLE(o);
-            if (!std::isfinite(d)) throw py::value_error("dumps: out of range float values are not JSON compliant");
-            char* s = PyOS_double_to_string(d, 'r', 0, Py_DTSF_ADD_DOT_0, nullptr);
-            if (!s) throw py::error_already_set();
-            out.append(s);
-            PyMem_Free(s);
-        } else if (PyDict_Check(o)) {
-            out.push_back('{');
-            PyObject *k, *v;
-            Py_ssize_t pos = 0;
-            bool first = true;
-            while (PyDict_Next(o, &pos, &k, &v)) {
-                if (!first) out.push_back(',');
-                first = false;
-                if (PyUnicode_Check(k)) {
-                    str(k);
-                } else {
-                    PyObject* ks = PyObject_Str(k);  // json.dumps coerces int/float/bool keys to strings
-                    if (!ks) throw py::error_already_set();
-                    str(ks);
-                    Py_DECREF(ks);
-                }
-                out.push_back(':');
-                value(v, depth + 1);
-            }
-            out.push_back('}');
-        } else if (PyList_Check(o) || PyTuple_Check(o)) {
-            out.push_back('[');
-            PyObject* seq = o;
-            Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-            PyObject** items = PySequence_Fast_ITEMS(seq);
-            for (Py_ssize_t i = 0; i < n; ++i) {
-                if (i) out.push_back(',');
-                value(items[i], depth + 1);
-            }
-            out.push_back(']');
-        } else {
-            throw py::type_error(std::string("dumps: object of type ") + Py_TYPE(o)->tp_name +
-                                 " is not JSON serializable");
-        }
-    }
-
-  private:
-    void str(PyObject* o) {
-        Py_ssize_t n = 0;
-        const char* s = PyUnicode_AsUTF8AndSize(o, &n);
-        if (!s) throw py::error_already_set();
-        out.push_back('"');
-        const char* run = s;
-        const char* end = s + n;
-        for (const char* p = s; p < end; ++p) {
-            unsigned char c = static_cast<unsigned char>(*p);
-            if (c >= 0x20 && c != '"' && c != '\\') continue;
-            out.append(run, static_cast<size_t>(p - run));
-            run = p + 1;
-            switch (c) {
-                case '"': out.append("\\\"", 2); break;
-                case '\\': out.append("\\\\", 2); break;
-                case '\n': out.append("\\n", 2); break;
-                case '\r': out.append("\\r", 2); break;
-                case '\t': out.append("\\t", 2); break;
-                case '\b': out.append("\\b", 2); break;
-                case '\f': out.append("\\f", 2); break;
-                default: {
-                    char buf[8];
-                    std::snprintf(buf, sizeof buf, "\\u%04x", c);
-                    out.append(buf, 6);
-                }
-            }
-        }
-        out.append(run, static_cast<size_t>(end - run));
-        out.push_back('"');
-    }
-};
-
-py::bytes dumps(py::handle obj) {
-    JsonWriter w;
-    w.out.reserve(1024);
-    w.value(obj.ptr(), 0);
-    return py::bytes(w.out.data(), w.out.size());
-}
-
-// scan_object(body) -> (namespace, name, resourceVersion, uid) of a JSON object's metadata | None
-py::object scan_object(py::bytes body) {
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(body.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    std::string_view ns, name, rv, uid;
-    Scanner sc(buf, static_cast<size_t>(len));
-    sc.uid = &uid;
-    if (!sc.scan_object(ns, name, rv)) return py::none();
-    return py::make_tuple(py::str(ns.data(), ns.size()), py::str(name.data(), name.size()),
-                          py::str(rv.data(), rv.size()), py::str(uid.data(), uid.size()));
-}
-
-// members_equal(a, b, keys) -> True iff every top-level member named in `keys` has byte-identical raw
-// JSON in both objects (or is absent from both).  False when either is not a JSON object this scanner
-// reads (e.g. escaped keys): the caller then decodes.  A slim writer compares its request body with the
-// write response this way to see whether the server rewrote the payload (defaulting, pruning, webhooks).
-bool members_equal(py::bytes a, py::bytes b, py::sequence key_seq) {
-    std::vector<std::string> keys;
-    for (auto k : key_seq) keys.push_back(k.cast<std::string>());
-    char* pa = nullptr;
-    char* pb = nullptr;
-    Py_ssize_t na = 0, nb = 0;
-    if (PyBytes_AsStringAndSize(a.ptr(), &pa, &na) != 0 || PyBytes_AsStringAndSize(b.ptr(), &pb, &nb) != 0)
-        throw py::error_already_set();
-    std::vector<std::string_view> ma, mb;
-    Scanner sa(pa, static_cast<size_t>(na)), sb(pb, static_cast<size_t>(nb));
-    if (!sa.members(keys, ma) || !sb.members(keys, mb)) return false;
-    for (size_t i = 0; i < keys.size(); ++i) {
-        if ((ma[i].data() == nullptr) != (mb[i].data() == nullptr)) return false;
-        if (ma[i].data() != nullptr && ma[i] != mb[i]) return false;
-    }
-    return true;
-}
-
-
-// ----------------------------------------------------------------------------- JSON -> Python
-// A direct JSON decoder into CPython objects (dict/list/str/int/float/bool/None, key order kept), and
-// `template_event_slim`, which decodes a template watch line into the coordinator's slim form: metadata
-// (without managedFields) and status as Python values, the spec reduced to the references the
-// coordinator reads plus a digest of its raw bytes.  A malformed line returns None (callers fall back
-// to json.loads, which raises the proper error).
-class PyJson {
-  public:
-    PyJson(const char* p, size_t n) : p_(p), e_(p + n) {}
-
-    // template_event_slim with a cache: `items` (borrowed; the informer store's dict keyed (namespace, name))
-    // lets an unchanged status, or unchanged references, be taken from the cached version instead of decoded
-    PyObject* items_ = nullptr;
-    std::string default_ns_;
-
-    // New reference, or nullptr: parse error (no Python exception set) or allocation failure (set).
-    PyObject* value(int depth = 0) {
-        ws();
-        if (p_ >= e_ || depth > 512) return nullptr;
-        switch (*p_) {
-            case '{': return object(depth);
-            case '[': return array(depth);
-            case '"': return string();
-            case 't': return literal("true", 4, Py_True);
-            case 'f': return literal("false", 5, Py_False);
-            case 'n': return literal("null", 4, Py_None);
-            default: return number();
-        }
-    }
-    bool at_end() {
-        ws();
-        return p_ == e_;
-    }
-
-    // {"type": "...", "object": {...}} with the object's spec slimmed → (type, object) | nullptr
-    PyObject* template_event() {
-        if (!expect('{')) return nullptr;
-        PyObject* type = nullptr;
-        PyObject* obj = nullptr;
-        bool ok = true;
-        if (!peek('}')) {
-            for (;;) {
-                std::string_view key;
-                if (!raw_key(key)) { ok = false; break; }
-                if (key == "type") {
-                    Py_XDECREF(type);
-                    type = value(1);
-                    if (type == nullptr) { ok = false; break; }
-                } else if (key == "object") {
-                    Py_XDECREF(obj);
-                    obj = slim_template();
-                    if (obj == nullptr) { ok = false; break; }
-                } else if (!skip_value()) {
-                    ok = false;
-                    break;
-                }
-                if (peek(',')) { ++p_; continue; }
-                break;
-            }
-        }
-        if (ok) ok = expect('}') && at_end() && type != nullptr && obj != nullptr;
-        if (!ok) {
-            Py_XDECREF(type);
-            Py_XDECREF(obj);
-            return nullptr;
-        }
-        PyObject* t = PyTuple_Pack(2, type, obj);
-        Py_DECREF(type);
-        Py_DECREF(obj);
-        return t;
-    }
-
-  private:
-    const char* p_;
-    const char* e_;
-    std::string tmp_;
-    PyObject* prev_ = nullptr;  // borrowed: the cached version of the object being decoded, if any
-
-    // After the metadata: find the cached version of this object (items_[(namespace, name)]).
-    void find_prev(PyObject* md) {
-        prev_ = nullptr;
-        if (items_ == nullptr || md == nullptr || !PyDict_Check(md)) return;
-        PyObject* name = PyDict_GetItemString(md, "name");
-        PyObject* ns = PyDict_GetItemString(md, "namespace");
-        if (name == nullptr) return;
-        PyObject* nso = nullptr;
-        if (ns == nullptr || (PyUnicode_Check(ns) && PyUnicode_GET_LENGTH(ns) == 0)) {
-            nso = PyUnicode_FromStringAndSize(default_ns_.data(), static_cast<Py_ssize_t>(default_ns_.size()));
-            if (nso == nullptr) {
-                PyErr_Clear();
-                return;
-            }
-            ns = nso;
-        }
-        PyObject* key = PyTuple_Pack(2, ns, name);
-        Py_XDECREF(nso);
-        if (key == nullptr) {
-            PyErr_Clear();
-            return;
-        }
-        PyObject* cur = PyDict_GetItemWithError(items_, key);
-        Py_DECREF(key);
-        if (cur == nullptr) {
-            PyErr_Clear();
-            return;
-        }
-        if (PyDict_Check(cur)) prev_ = cur;
-    }
-    // The value at p_ when its text hashes to `want` (the cached version's digest of it): `reuse` (new
-    // reference) and *fp set, p_ past the value.  Otherwise p_ stays and nullptr is returned (*fp set when the
-    // value could be skipped).
-    PyObject* reuse_if_same(PyObject* want, PyObject* reuse, uint64_t* fp) {
-        ws();
-        const char* s0 = p_;
-        if (!skip_value()) {
-            p_ = s0;
-            return nullptr;
-        }
-        Hasher h;
-        h.bytes(s0, static_cast<size_t>(p_ - s0));
-        *fp = h.digest();
-        if (want != nullptr && reuse != nullptr && PyLong_Check(want) &&
-            PyLong_AsUnsignedLongLong(want) == *fp && !PyErr_Occurred()) {
-            Py_INCREF(reuse);
-            return reuse;
-        }
-        PyErr_Clear();
-        p_ = s0;
-        return nullptr;
-    }
-
-    void ws() {
-        while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
-    }
-    bool peek(char c) {
-        ws();
-        return p_ < e_ && *p_ == c;
-    }
-    bool expect(char c) {
-        ws();
-        if (p_ >= e_ || *p_ != c) return false;
-        ++p_;
-        return true;
-    }
-    PyObject* literal(const char* lit, size_t n, PyObject* v) {
-        if (static_cast<size_t>(e_ - p_) < n || std::memcmp(p_, lit, n) != 0) return nullptr;
-        p_ += n;
-        Py_INCREF(v);
-        return v;
-    }
-    static void put_utf8(std::string& out, uint32_t cp) {
-        if (cp < 0x80) {
-            out.push_back(static_cast<char>(cp));
-        } else if (cp < 0x800) {
-            out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
-            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
-        } else if (cp < 0x10000) {  // lone surrogates too: "surrogatepass" decodes them back, as json.loads keeps them
-            out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
-            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
-            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
-        } else {
-            out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
-            out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
-            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
-            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
-        }
-    }
-    bool hex4(uint32_t& v) {
-        if (e_ - p_ < 4) return false;
-        v = 0;
-        for (int i = 0; i < 4; ++i) {
-            char c = p_[i];
-            v <<= 4;
-            if (c >= '0' && c <= '9') v |= static_cast<uint32_t>(c - '0');
-            else if (c >= 'a' && c <= 'f') v |= static_cast<uint32_t>(c - 'a' + 10);
-            else if (c >= 'A' && c <= 'F') v |= static_cast<uint32_t>(c - 'A' + 10);
-            else return false;
-        }
-        p_ += 4;
-        return true;
-    }
-    // The string at p_ (after ws) as UTF-8 bytes: a view into the input when it has no escapes, else tmp_.
-    bool raw_string(std::string_view& out) {
-        ws();
-        if (p_ >= e_ || *p_ != '"') return false;
-        const char* s = ++p_;
-        p_ = ncc::find_quote_or_ctl(p_, e_);
-        if (p_ >= e_ || static_cast<unsigned char>(*p_) < 0x20) return false;
-        if (*p_ == '"') {
-            out = std::string_view(s, static_cast<size_t>(p_ - s));
-            ++p_;
-            return true;
-        }
-        tmp_.assign(s, static_cast<size_t>(p_ - s));
-        while (p_ < e_) {
-            char c = *p_;
-            if (c == '"') {
-                ++p_;
-                out = tmp_;
-                return true;
-            }
-            if (static_cast<unsigned char>(c) < 0x20) return false;
-            if (c != '\\') {
-                tmp_.push_back(c);
-                ++p_;
-                continue;
-            }
-            if (++p_ >= e_) return false;
-            char esc = *p_++;
-            switch (esc) {
-                case '"': tmp_.push_back('"'); break;
-                case '\\': tmp_.push_back('\\'); break;
-                case '/': tmp_.push_back('/'); break;
-                case 'b': tmp_.push_back('\b'); break;
-                case 'f': tmp_.push_back('\f'); break;
-                case 'n': tmp_.push_back('\n'); break;
-                case 'r': tmp_.push_back('\r'); break;
-                case 't': tmp_.push_back('\t'); break;
-                case 'u': {
-                    uint32_t cp;
-                    if (!hex4(cp)) return false;
-                    if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
-                        const char* save = p_;
-                        p_ += 2;
-                        uint32_t lo;
-                        if (hex4(lo) && lo >= 0xDC00 && lo < 0xE000) {
-                            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-                        } else {
-                            p_ = save;
-                        }
-                    }
-                    put_utf8(tmp_, cp);
-                    break;
-                }
-                default: return false;
-            }
-        }
-        return false;
-    }
-    // ASCII (almost every Kubernetes string) is copied straight into a compact str; the rest is decoded.
-    static PyObject* make_str(std::string_view v) {
-        const unsigned char* b = reinterpret_cast<const unsigned char*>(v.data());
-        size_t i = 0;
-        while (i < v.size() && b[i] < 0x80) ++i;
-        if (i < v.size()) return PyUnicode_DecodeUTF8(v.data(), static_cast<Py_ssize_t>(v.size()), "surrogatepass");
-        PyObject* o = PyUnicode_New(static_cast<Py_ssize_t>(v.size()), 127);
-        if (o != nullptr && !v.empty()) std::memcpy(PyUnicode_1BYTE_DATA(o), v.data(), v.size());
-        return o;
-    }
-    PyObject* string() {
-        std::string_view v;
-        if (!raw_string(v)) return nullptr;
-        return make_str(v);
-    }
-    bool raw_key(std::string_view& key) { return raw_string(key) && expect(':'); }
-    // Object keys repeat across every object of a kind: a small direct-mapped cache of interned key strings
-    // (GIL-protected; entries live for the process) saves building and hashing them again.
-    struct KeySlot {
-        std::string text;
-        PyObject* obj = nullptr;
-    };
-    static KeySlot* key_cache() {
-        static KeySlot slots[1024];
-        return slots;
-    }
-    PyObject* key_object(std::string_view key) {
-        if (key.size() > 48) return make_str(key);
-        uint64_t h = 1469598103934665603ULL;
-        for (unsigned char c : key) h = (h ^ c) * 1099511628211ULL;
-        KeySlot& slot = key_cache()[h & 1023];
-        if (slot.obj != nullptr && slot.text == key) {
-            Py_INCREF(slot.obj);
-            return slot.obj;
-        }
-        PyObject* k = make_str(key);
-        if (k == nullptr) return nullptr;
-        PyUnicode_InternInPlace(&k);
-        Py_XDECREF(slot.obj);
-        slot.text.assign(key.data(), key.size());
-        slot.obj = k;
-        Py_INCREF(k);
-        return k;
-    }
-    PyObject* number() {
-        const char* s = p_;
-        if (p_ < e_ && *p_ == '-') ++p_;
-        if (p_ >= e_ || *p_ < '0' || *p_ > '9') return nullptr;
-        if (*p_ == '0') {
-            ++p_;
-        } else {
-            while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
-        }
-        bool is_float = false;
-        if (p_ < e_ && *p_ == '.') {
-            is_float = true;
-            ++p_;
-            if (p_ >= e_ || *p_ < '0' || *p_ > '9') return nullptr;
-            while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
-        }
-        if (p_ < e_ && (*p_ == 'e' || *p_ == 'E')) {
-            is_float = true;
-            ++p_;
-            if (p_ < e_ && (*p_ == '+' || *p_ == '-')) ++p_;
-            if (p_ >= e_ || *p_ < '0' || *p_ > '9') return nullptr;
-            while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
-        }
-        std::string num(s, static_cast<size_t>(p_ - s));
-        if (is_float) return PyFloat_FromDouble(std::strtod(num.c_str(), nullptr));
-        if (num.size() <= 18) return PyLong_FromLongLong(std::strtoll(num.c_str(), nullptr, 10));
-        return PyLong_FromString(num.c_str(), nullptr, 10);
-    }
-    PyObject* array(int depth) {
-        ++p_;  // '['
-        PyObject* list = PyList_New(0);
-        if (list == nullptr) return nullptr;
-        if (peek(']')) {
-            ++p_;
-            return list;
-        }
-        for (;;) {
-            PyObject* v = value(depth + 1);
-            if (v == nullptr || PyList_Append(list, v) != 0) {
-                Py_XDECREF(v);
-                Py_DECREF(list);
-                return nullptr;
-            }
-            Py_DECREF(v);
-            if (peek(',')) { ++p_; continue; }
-            if (expect(']')) return list;
-            Py_DECREF(list);
-            return nullptr;
-        }
-    }
-    // `skip` (may be empty): a member name left out (metadata.managedFields)
-    PyObject* object(int depth, std::string_view skip = std::string_view()) {
-        ++p_;  // '{'
-        PyObject* d = PyDict_New();
-        if (d == nullptr) return nullptr;
-        if (peek('}')) {
-            ++p_;
-            return d;
-        }
-        for (;;) {
-            std::string_view key;
-            if (!raw_key(key)) break;
-            if (!skip.empty() && key == skip) {
-                if (!skip_value()) break;
-            } else {
-                PyObject* k = key_object(key);
-                if (k == nullptr) break;
-                PyObject* v = value(depth + 1);
-                if (v == nullptr || PyDict_SetItem(d, k, v) != 0) {
-                    Py_DECREF(k);
-                    Py_XDECREF(v);
-                    break;
-                }
-                Py_DECREF(k);
-                Py_DECREF(v);
-            }
-            if (peek(',')) { ++p_; continue; }
-            if (expect('}')) return d;
-            break;
-        }
-        Py_DECREF(d);
-        return nullptr;
-    }
-    bool skip_value() {
-        ws();
-        if (p_ >= e_) return false;
-        char c = *p_;
-        if (c == '"') {
-            std::string_view v;
-            return raw_string(v);
-        }
-        if (c == '{' || c == '[') {  // a skipped member (managedFields) is not validated
-            const char* q = ncc::skip_container_text(p_, e_);
-            if (q == nullptr) return false;
-            p_ = q;
-            return true;
-        }
-        const char* s = p_;
-        while (p_ < e_ && *p_ != ',' && *p_ != '}' && *p_ != ']' && *p_ != ' ' && *p_ != '\n' && *p_ != '\t' &&
-               *p_ != '\r')
-            ++p_;
-        return p_ > s;
-    }
-    // {"name": "..."} → a new {"name": str} dict (other members dropped), or None for null
-    PyObject* name_ref() {
-        ws();
-        if (p_ < e_ && *p_ == 'n') return literal("null", 4, Py_None);
-        if (!expect('{')) return nullptr;
-        PyObject* d = PyDict_New();
-        if (d == nullptr) return nullptr;
-        if (peek('}')) {
-            ++p_;
-            return d;
-        }
-        for (;;) {
-            std::string_view key;
-            if (!raw_key(key)) break;
-            if (key == "name") {
-                PyObject* v = value(8);
-                if (v == nullptr || PyDict_SetItemString(d, "name", v) != 0) {
-                    Py_XDECREF(v);
-                    break;
-                }
-                Py_DECREF(v);
-            } else if (!skip_value()) {
-                break;
-            }
-            if (peek(',')) { ++p_; continue; }
-            if (expect('}')) return d;
-            break;
-        }
-        Py_DECREF(d);
-        return nullptr;
-    }
-    // mappedEnvironmentVariables: [{"secretRef": {"name"}, "configMapRef": {"name"}, ...}, ...] keeping the refs
-    PyObject* mapped_env() {
-        ws();
-        if (p_ < e_ && *p_ == 'n') return literal("null", 4, Py_None);
-        if (!expect('[')) return nullptr;
-        PyObject* list = PyList_New(0);
-        if (list == nullptr) return nullptr;
-        if (peek(']')) {
-            ++p_;
-            return list;
-        }
-        for (;;) {
-            ws();
-            PyObject* item = nullptr;
-            if (p_ < e_ && *p_ == '{') {
-                ++p_;
-                item = PyDict_New();
-                if (item == nullptr) break;
-                bool ok = true;
-                if (peek('}')) {
-                    ++p_;
-                } else {
-                    for (;;) {
-                        std::string_view key;
-                        if (!raw_key(key)) { ok = false; break; }
-                        if (key == "secretRef" || key == "configMapRef") {
-                            PyObject* r = name_ref();
-                            if (r == nullptr) { ok = false; break; }
-                            int rc = r == Py_None ? 0 : PyDict_SetItemString(item, key == "secretRef" ? "secretRef"
-                                                                                                        : "configMapRef", r);
-                            Py_DECREF(r);
-                            if (rc != 0) { ok = false; break; }
-                        } else if (!skip_value()) {
-                            ok = false;
-                            break;
-                        }
-                        if (peek(',')) { ++p_; continue; }
-                        ok = expect('}');
-                        break;
-                    }
-                }
-                if (!ok) {
-                    Py_DECREF(item);
-                    break;
-                }
-            } else {
-                if (!skip_value()) break;
-                item = PyDict_New();  // null / non-object entries carry no reference
-                if (item == nullptr) break;
-            }
-            int rc = PyList_Append(list, item);
-            Py_DECREF(item);
-            if (rc != 0) break;
-            if (peek(',')) { ++p_; continue; }
-            if (expect(']')) return list;
-            break;
-        }
-        Py_DECREF(list);
-        return nullptr;
-    }
-    // spec → {"runtimeEnvironment": {"mappedEnvironmentVariables": [...]}, "_fp": digest of the raw spec}
-    PyObject* slim_spec() {
-        ws();
-        const char* s = p_;
-        if (p_ >= e_ || *p_ != '{') {
-            if (!skip_value()) return nullptr;
-            Py_INCREF(Py_None);
-            return Py_None;
-        }
-        ++p_;
-        PyObject* env = nullptr;
-        uint64_t env_fp = 0;
-        bool ok = true;
-        if (!peek('}')) {
-            for (;;) {
-                std::string_view key;
-                if (!raw_key(key)) { ok = false; break; }
-                if (key == "runtimeEnvironment" && peek('{')) {
-                    ++p_;
-                    if (!peek('}')) {
-                        for (;;) {
-                            std::string_view k2;
-                            if (!raw_key(k2)) { ok = false; break; }
-                            if (k2 == "mappedEnvironmentVariables") {
-                                Py_XDECREF(env);
-                                env = nullptr;
-                                if (prev_ != nullptr) {  // unchanged references: the cached version's list
-                                    PyObject* ps = PyDict_GetItemString(prev_, "spec");
-                                    PyObject* prt = ps != nullptr && PyDict_Check(ps)
-                                                        ? PyDict_GetItemString(ps, "runtimeEnvironment") : nullptr;
-                                    PyObject* penv = prt != nullptr && PyDict_Check(prt)
-                                                         ? PyDict_GetItemString(prt, "mappedEnvironmentVariables")
-                                                         : nullptr;
-                                    if (penv != nullptr)
-                                        env = reuse_if_same(PyDict_GetItemString(ps, "_rfp"), penv, &env_fp);
-                                }
-                                if (env == nullptr) {
-                                    ws();
-                                    const char* e0 = p_;
-                                    env = mapped_env();
-                                    if (env == nullptr) { ok = false; break; }
-                                    Hasher he;
-                                    he.bytes(e0, static_cast<size_t>(p_ - e0));
-                                    env_fp = he.digest();
-                                }
-                            } else if (!skip_value()) {
-                                ok = false;
-                                break;
-                            }
-                            if (peek(',')) { ++p_; continue; }
-                            break;
-                        }
-                    }
-                    if (!ok || !expect('}')) { ok = false; break; }
-                } else if (!skip_value()) {
-                    ok = false;
-                    break;
-                }
-                if (peek(',')) { ++p_; continue; }
-                break;
-            }
-        }
-        if (ok) ok = expect('}');
-        if (!ok) {
-            Py_XDECREF(env);
-            return nullptr;
-        }
-        Hasher hs;
-        hs.bytes(s, static_cast<size_t>(p_ - s));
-        PyObject* spec = PyDict_New();
-        PyObject* fp = PyLong_FromUnsignedLongLong(hs.digest());
-        bool built = spec != nullptr && fp != nullptr;
-        if (built && env != nullptr && env != Py_None) {
-            PyObject* rt = PyDict_New();
-            built = rt != nullptr && PyDict_SetItemString(rt, "mappedEnvironmentVariables", env) == 0 &&
-                    PyDict_SetItemString(spec, "runtimeEnvironment", rt) == 0;
-            Py_XDECREF(rt);
-        }
-        if (built) built = PyDict_SetItemString(spec, "_fp", fp) == 0;
-        if (built) {  // a digest of the references' text: the coordinator compares it instead of the list
-            PyObject* rfp = PyLong_FromUnsignedLongLong(env_fp);
-            built = rfp != nullptr && PyDict_SetItemString(spec, "_rfp", rfp) == 0;
-            Py_XDECREF(rfp);
-        }
-        Py_XDECREF(env);
-        Py_XDECREF(fp);
-        if (!built) {
-            Py_XDECREF(spec);
-            return nullptr;
-        }
-        return spec;
-    }
-    PyObject* slim_template() {
-        if (!expect('{')) return nullptr;
-        PyObject* d = PyDict_New();
-        if (d == nullptr) return nullptr;
-        if (peek('}')) {
-            ++p_;
-            return d;
-        }
-        for (;;) {
-            std::string_view key;
-            if (!raw_key(key)) break;
-            PyObject* v;
-            if (key == "spec") {
-                v = slim_spec();
-            } else if (key == "metadata" && peek('{')) {
-                v = object(1, "managedFields");
-                find_prev(v);
-            } else if (key == "status") {
-                // and a digest of the status text under "__ncc_sfp__": an unchanged status compares as one int,
-                // and is taken from the cached version instead of decoded again
-                uint64_t fp = 0;
-                v = nullptr;
-                if (prev_ != nullptr) {
-                    PyObject* pst = PyDict_GetItemString(prev_, "status");
-                    if (pst != nullptr) v = reuse_if_same(PyDict_GetItemString(prev_, "__ncc_sfp__"), pst, &fp);
-                }
-                if (v == nullptr) {
-                    ws();
-                    const char* s0 = p_;
-                    v = value(1);
-                    if (v != nullptr) {
-                        Hasher hs;
-                        hs.bytes(s0, static_cast<size_t>(p_ - s0));
-                        fp = hs.digest();
-                    }
-                }
-                if (v != nullptr) {
-                    PyObject* sfp = PyLong_FromUnsignedLongLong(fp);
-                    if (sfp == nullptr || PyDict_SetItemString(d, "__ncc_sfp__", sfp) != 0) {
-                        Py_XDECREF(sfp);
-                        Py_DECREF(v);
-                        break;
-                    }
-                    Py_DECREF(sfp);
-                }
-            } else {
-                v = value(1);
-            }
-            PyObject* k = v == nullptr ? nullptr : key_object(key);
-            if (k == nullptr || PyDict_SetItem(d, k, v) != 0) {
-                Py_XDECREF(k);
-                Py_XDECREF(v);
-                break;
-            }
-            Py_DECREF(k);
-            Py_DECREF(v);
-            if (peek(',')) { ++p_; continue; }
-            if (expect('}')) return d;
-            break;
-        }
-        Py_DECREF(d);
-        return nullptr;
-    }
-};
-
-static std::string_view bytes_view(const py::bytes& b) {
-    char* buf = nullptr;
-    Py_ssize_t len = 0;
-    if (PyBytes_AsStringAndSize(b.ptr(), &buf, &len) != 0) throw py::error_already_set();
-    return std::string_view(buf, static_cast<size_t>(len));
-}
-
-// loads(bytes) -> value | None (malformed: the caller falls back to json.loads for the error)
-py::object loads(py::bytes data) {
-    std::string_view v = bytes_view(data);
-    PyJson pj(v.data(), v.size());
-    PyObject* o = pj.value();
-    if (o != nullptr && !pj.at_end()) {
-        Py_DECREF(o);
-        o = nullptr;
-    }
-    if (o == nullptr) {
-        // invalid UTF-8 inside a string is malformed input too: None, and the caller's stdlib fallback
-        // reports it
-        if (PyErr_Occurred() && !PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) throw py::error_already_set();
-        PyErr_Clear();
-        return py::none();
-    }
-    return py::reinterpret_steal<py::object>(o);
-}
-
-// template_event_slim(line) -> (type, slim object) | None
-py::object template_event_slim(py::bytes line, py::object items, const std::string& default_ns) {
-    std::string_view v = bytes_view(line);
-    PyJson pj(v.data(), v.size());
-    if (!items.is_none()) {
-        if (!PyDict_Check(items.ptr())) throw py::type_error("template_event_slim: items must be a dict");
-        pj.items_ = items.ptr();
-        pj.default_ns_ = default_ns;
-    }
-    PyObject* o = pj.template_event();
-    if (o == nullptr) {
-        if (PyErr_Occurred()) throw py::error_already_set();
-        return py::none();
-    }
-    return py::reinterpret_steal<py::object>(o);
-}
-
-
-// ----------------------------------------------------------------------------- executor reports
-// The coordinator folds every shard executor's per-pass reports into "which shards have reported on which
-// version of each object" (ncc/controller/reports.py is the Python twin and the specification).  At 8
-// shards that is 8 reports per template and wave; decoding them into dicts and folding them in Python was
-// a third of the coordinator's CPU.  ReportTable.feed takes a raw IPC frame (ncc/controller/ipc.py: one
-// msgpack message, or an array of them), folds the reports natively and hands back only what Python acts
-// on: the keys whose report set became complete, the keys whose pass wrote, the failing shards, and every
-// other message decoded.
-
-class MpReader {
-  public:
-    MpReader(const char* p, size_t n) : p_(reinterpret_cast<const uint8_t*>(p)), e_(p_ + n) {}
-    bool at_end() const { return p_ == e_; }
-
-    [[noreturn]] static void fail() { throw py::value_error("msgpack: malformed frame"); }
-    void need(size_t n) const {
-        if (static_cast<size_t>(e_ - p_) < n) fail();
-    }
-    uint8_t peek() const {
-        need(1);
-        return *p_;
-    }
-    uint64_t be(int n) {
-        need(static_cast<size_t>(n));
-        uint64_t v = 0;
-        for (int k = 0; k < n; ++k) v = (v << 8) | p_[k];
-        p_ += n;
-        return v;
-    }
-    // container headers: false (nothing consumed) when the next value is not of that kind
-    // (a container cannot hold more elements than there are bytes left: one byte each at least, so a
-    // corrupt length fails here instead of sizing a huge list)
-    bool map_len(size_t& n) {
-        uint8_t c = peek();
-        if ((c & 0xf0) == 0x80) { ++p_; n = c & 0x0f; }
-        else if (c == 0xde) { ++p_; n = be(2); }
-        else if (c == 0xdf) { ++p_; n = be(4); }
-        else return false;
-        if (n > static_cast<size_t>(e_ - p_) / 2) fail();
-        return true;
-    }
-    bool arr_len(size_t& n) {
-        uint8_t c = peek();
-        if ((c & 0xf0) == 0x90) { ++p_; n = c & 0x0f; }
-        else if (c == 0xdc) { ++p_; n = be(2); }
-        else if (c == 0xdd) { ++p_; n = be(4); }
-        else return false;
-        if (n > static_cast<size_t>(e_ - p_)) fail();
-        return true;
-    }
-    bool str(std::string_view& out) {  // str or bin
-        uint8_t c = peek();
-        size_t n;
-        if ((c & 0xe0) == 0xa0) { ++p_; n = c & 0x1f; }
-        else if (c == 0xd9 || c == 0xc4) { ++p_; n = be(1); }
-        else if (c == 0xda || c == 0xc5) { ++p_; n = be(2); }
-        else if (c == 0xdb || c == 0xc6) { ++p_; n = be(4); }
-        else return false;
-        need(n);
-        out = std::string_view(reinterpret_cast<const char*>(p_), n);
-        p_ += n;
-        return true;
-    }
-    bool integer(int64_t& v) {
-        uint8_t c = peek();
-        if (c <= 0x7f) { ++p_; v = c; return true; }
-        if (c >= 0xe0) { ++p_; v = static_cast<int8_t>(c); return true; }
-        switch (c) {
-            case 0xcc: ++p_; v = static_cast<int64_t>(be(1)); return true;
-            case 0xcd: ++p_; v = static_cast<int64_t>(be(2)); return true;
-            case 0xce: ++p_; v = static_cast<int64_t>(be(4)); return true;
-            case 0xcf: ++p_; v = static_cast<int64_t>(be(8)); return true;
-            case 0xd0: ++p_; v = static_cast<int8_t>(be(1)); return true;
-            case 0xd1: ++p_; v = static_cast<int16_t>(be(2)); return true;
-            case 0xd2: ++p_; v = static_cast<int32_t>(be(4)); return true;
-            case 0xd3: ++p_; v = static_cast<int64_t>(be(8)); return true;
-            default: return false;
-        }
-    }
-    bool nil() {
-        if (peek() != 0xc0) return false;
-        ++p_;
-        return true;
-    }
-    // Python truthiness of the next value, consuming it (nil/false/0/""/empty containers are false)
-    bool truthy() {
-        uint8_t c = peek();
-        if (c == 0xc0 || c == 0xc2) { ++p_; return false; }
-        if (c == 0xc3) { ++p_; return true; }
-        int64_t i;
-        if (integer(i)) return i != 0;
-        std::string_view s;
-        if (str(s)) return !s.empty();
-        size_t n;
-        const uint8_t* at = p_;
-        if (map_len(n) || arr_len(n)) {
-            p_ = at;
-            skip();
-            return n != 0;
-        }
-        skip();  // floats
-        return true;
-    }
-    void skip(int depth = 0) {
-        if (depth > 64) fail();
-        size_t n;
-        std::string_view s;
-        int64_t i;
-        if (map_len(n)) {
-            for (size_t k = 0; k < 2 * n; ++k) skip(depth + 1);
-        } else if (arr_len(n)) {
-            for (size_t k = 0; k < n; ++k) skip(depth + 1);
-        } else if (str(s) || integer(i) || nil()) {
-        } else {
-            uint8_t c = peek();
-            if (c == 0xc2 || c == 0xc3) { ++p_; }
-            else if (c == 0xca) { ++p_; be(4); }
-            else if (c == 0xcb) { ++p_; be(8); }
-            else fail();
-        }
-    }
-    // generic decode into a new reference (msgpack -> Python, as msgpack.unpackb(raw=False) does)
-    PyObject* value(int depth = 0) {
-        if (depth > 64) fail();
-        size_t n;
-        std::string_view s;
-        int64_t i;
-        uint8_t c = peek();
-        if (map_len(n)) {
-            PyObject* d = PyDict_New();
-            if (d == nullptr) throw py::error_already_set();
-            for (size_t k = 0; k < n; ++k) {
-                PyObject* kk = nullptr;
-                PyObject* vv = nullptr;
-                try {
-                    kk = value(depth + 1);
-                    vv = value(depth + 1);
-                } catch (...) {
-                    Py_XDECREF(kk);
-                    Py_DECREF(d);
-                    throw;
-                }
-                int rc = PyDict_SetItem(d, kk, vv);
-                Py_DECREF(kk);
-                Py_DECREF(vv);
-                if (rc != 0) { Py_DECREF(d); throw py::error_already_set(); }
-            }
-            return d;
-        }
-        if (arr_len(n)) {
-            PyObject* l = PyList_New(static_cast<Py_ssize_t>(n));
-            if (l == nullptr) throw py::error_already_set();
-            for (size_t k = 0; k < n; ++k) {
-                try {
-                    PyList_SET_ITEM(l, static_cast<Py_ssize_t>(k), value(depth + 1));
-                } catch (...) {
-                    for (size_t j = k; j < n; ++j) { Py_INCREF(Py_None); PyList_SET_ITEM(l, static_cast<Py_ssize_t>(j), Py_None); }
-                    Py_DECREF(l);
-                    throw;
-                }
-            }
-            return l;
-        }
-        if ((c & 0xe0) == 0xa0 || c == 0xd9 || c == 0xda || c == 0xdb) {
-            str(s);
-            PyObject* o = PyUnicode_DecodeUTF8(s.data(), static_cast<Py_ssize_t>(s.size()), "strict");
-            if (o == nullptr) throw py::error_already_set();
-            return o;
-        }
-        if (c == 0xc4 || c == 0xc5 || c == 0xc6) {
-            str(s);
-            return PyBytes_FromStringAndSize(s.data(), static_cast<Py_ssize_t>(s.size()));
-        }
-        if (c == 0xcf) {  // uint64: may not fit int64
-            ++p_;
-            return PyLong_FromUnsignedLongLong(be(8));
-        }
-        if (integer(i)) return PyLong_FromLongLong(i);
-        if (nil()) Py_RETURN_NONE;
-        if (c == 0xc2) { ++p_; Py_RETURN_FALSE; }
-        if (c == 0xc3) { ++p_; Py_RETURN_TRUE; }
-        if (c == 0xca) {
-            ++p_;
-            uint32_t u = static_cast<uint32_t>(be(4));
-            float f;
-            std::memcpy(&f, &u, 4);
-            return PyFloat_FromDouble(f);
-        }
-        if (c == 0xcb) {
-            ++p_;
-            uint64_t u = be(8);
-            double d;
-            std::memcpy(&d, &u, 8);
-            return PyFloat_FromDouble(d);
-        }
-        fail();
-    }
-    const uint8_t* pos() const { return p_; }
-    void seek(const uint8_t* q) { p_ = q; }
-
-  private:
-    const uint8_t* p_;
-    const uint8_t* e_;
-};
-
-class ReportTable {
-  public:
-    struct Slot {
-        std::string shard;
-        std::string uid;
-        int64_t gen = 0;
-        // the reported failure as its raw msgpack value (a typed failure map, ncc/controller/failures.py, or
-        // a free-form string); empty: success (nil, or an empty string, which is falsy in the Python twin too)
-        std::string err;
-    };
-
-    void set_shards(const std::vector<std::string>& shards) { shards_ = shards; }
-    // This coordinator owns the keys of partition `part` of `parts`; reports on other keys are not folded but
-    // kept, raw, for take_forwards() (the parent coordinator relays them to the partition's process).
-    void set_partition(int part, int parts) {
-        if (parts < 1 || part < 0 || part >= parts) throw py::value_error("set_partition: 0 <= part < parts");
-        part_ = part;
-        parts_ = parts;
-    }
-    // {partition: [raw msgpack report message, ...]} collected since the last call
-    py::dict take_forwards() {
-        py::dict out;
-        for (auto& kv : forwards_) {
-            py::list l;
-            for (auto& m : kv.second) l.append(py::bytes(m));
-            out[py::int_(kv.first)] = l;
-        }
-        forwards_.clear();
-        return out;
-    }
-    std::vector<std::string> shards() const { return shards_; }
-    size_t size() const { return state_.size(); }
-    void pop(const std::string& key) { state_.erase(key); }
-    void drop_shards(const std::vector<std::string>& names) {
-        for (auto& kv : state_) {
-            auto& v = kv.second;
-            v.erase(std::remove_if(v.begin(), v.end(), [&](const Slot& s) {
-                        return std::find(names.begin(), names.end(), s.shard) != names.end();
-                    }), v.end());
-        }
-    }
-
-    // feed(frame body, batch) -> (complete keys, wrote keys, failing shards, other messages, reports, pending)
-    struct Folded {
-        py::list complete, wrote, errors, others;
-        int64_t reports = 0, pending = 0;
-    };
-
-    py::tuple feed(py::bytes body, bool batch) {
-        std::string_view v = bytes_view(body);
-        Folded f;
-        fold_frame(v.data(), v.size(), batch, f);
-        return py::make_tuple(f.complete, f.wrote, f.errors, f.others, f.reports, f.pending);
-    }
-
-    // feed_stream(buffer, start) -> (complete, wrote, errors, others, reports, pending, end): every complete
-    // frame (4-byte big-endian length, high bit = batch, then the msgpack body) in buffer[start:], folded;
-    // `end` is the offset of the first byte not consumed (a partial frame's header or body).
-    py::tuple feed_stream(py::buffer buf, size_t start) {
-        py::buffer_info info = buf.request();
-        if (info.ndim != 1 || info.itemsize != 1) throw py::value_error("feed_stream: a byte buffer is required");
-        const char* p = static_cast<const char*>(info.ptr);
-        size_t len = static_cast<size_t>(info.size);
-        if (start > len) throw py::value_error("feed_stream: start past the end");
-        Folded f;
-        size_t pos = start;
-        while (len - pos >= 4) {
-            const auto* h = reinterpret_cast<const uint8_t*>(p + pos);
-            uint32_t n = (uint32_t(h[0]) << 24) | (uint32_t(h[1]) << 16) | (uint32_t(h[2]) << 8) | uint32_t(h[3]);
-            bool batch = (n & 0x80000000u) != 0;
-            n &= 0x7fffffffu;
-            if (n > kMaxFrame) throw py::value_error("frame too large: " + std::to_string(n));
-            if (len - pos - 4 < n) break;
-            fold_frame(p + pos + 4, n, batch, f);
-            pos += 4 + n;
-        }
-        return py::make_tuple(f.complete, f.wrote, f.errors, f.others, f.reports, f.pending, pos);
-    }
-
-    // readiness(key, uid, generation) -> None while some shard has not reported on this version, else
-    // {shard: error | None} in shard order
-    py::object readiness(const std::string& key, const std::string& uid, int64_t gen) const {
-        auto it = state_.find(key);
-        if (it == state_.end()) return py::none();
-        py::dict out;
-        for (const auto& s : shards_) {
-            const Slot* e = find(it->second, s);
-            if (e == nullptr || e->uid != uid || e->gen < gen) return py::none();
-            if (e->err.empty()) {
-                out[py::str(s)] = py::none();
-            } else {
-                MpReader er(e->err.data(), e->err.size());
-                out[py::str(s)] = py::reinterpret_steal<py::object>(er.value());
-            }
-        }
-        return std::move(out);
-    }
-
-    // ready_ok(key, uid, generation) -> None while some shard has not reported on this version, else
-    // whether every shard succeeded (readiness() without building the dict)
-    py::object ready_ok(const std::string& key, const std::string& uid, int64_t gen) const {
-        auto it = state_.find(key);
-        if (it == state_.end()) return py::none();
-        bool ok = true;
-        for (const auto& s : shards_) {
-            const Slot* e = find(it->second, s);
-            if (e == nullptr || e->uid != uid || e->gen < gen) return py::none();
-            ok = ok && e->err.empty();
-        }
-        return py::bool_(ok);
-    }
-
-    // finish_batch(keys, items, assumed, adopted, memos, shards, queue, pending_event, event_on_noop)
-    //     -> (rest, verify, events, done, superseded)
-    // The coordinator's inline finish (ncc/controller/reconcile.py `finish_inline_many`, the specification) over
-    // a batch of template keys whose report sets completed, read straight off the Python state it uses:
-    // `items`/`assumed` the template store's dict and mutation overlay, `adopted` key -> adopted resourceVersion,
-    // `memos` key -> (status digest, references digest, shard list) of the last verified status, `queue` the
-    // work queue core (busy keys need a pass), `pending_event` the keys owing a Synced Event.  Per key: `rest`
-    // (a queued pass is needed), `verify` (the Python path decides: an overlaid object, a non-slim template, no
-    // memo for this status), `events` (finished, the template whose Synced Event is due), `done` finished
-    // without an Event, or `superseded` (a newer version reached the cache: its own last report brings it back).
-    py::tuple finish_batch(py::iterable keys, py::dict items, py::dict assumed, py::dict adopted, py::dict memos,
-                           py::object shards, py::object queue, py::set pending_event, bool event_on_noop) const {
-        static PyObject* k_status = PyUnicode_InternFromString("status");
-        static PyObject* k_conditions = PyUnicode_InternFromString("conditions");
-        static PyObject* k_metadata = PyUnicode_InternFromString("metadata");
-        static PyObject* k_rv = PyUnicode_InternFromString("resourceVersion");
-        static PyObject* k_uid = PyUnicode_InternFromString("uid");
-        static PyObject* k_gen = PyUnicode_InternFromString("generation");
-        static PyObject* k_sfp = PyUnicode_InternFromString("__ncc_sfp__");
-        static PyObject* k_spec = PyUnicode_InternFromString("spec");
-        static PyObject* k_rfp = PyUnicode_InternFromString("_rfp");
-        RateLimitingQueue* nq = nullptr;
-        if (py::isinstance<RateLimitingQueue>(queue)) nq = &queue.cast<RateLimitingQueue&>();
-        py::list rest, verify, events;
-        long long done = 0, superseded = 0;
-        std::string k;
-        const bool overlay = PyDict_GET_SIZE(assumed.ptr()) > 0;
-        for (py::handle kh : keys) {
-            PyObject* key = kh.ptr();
-            Py_ssize_t klen = 0;
-            const char* kc = PyUnicode_Check(key) ? PyUnicode_AsUTF8AndSize(key, &klen) : nullptr;
-            if (kc == nullptr) {
-                PyErr_Clear();
-                verify.append(kh);
-                continue;
-            }
-            k.assign(kc, static_cast<size_t>(klen));
-            size_t a = k.find('/'), b = a == std::string::npos ? a : k.find('/', a + 1);
-            bool is_busy = nq != nullptr ? nq->busy(k) : queue.attr("busy")(kh).cast<bool>();
-            if (b == std::string::npos || k.compare(0, a, "template") != 0 || is_busy) {
-                rest.append(kh);
-                continue;
-            }
-            py::tuple ik = py::make_tuple(py::str(kc + a + 1, b - a - 1), py::str(kc + b + 1, k.size() - b - 1));
-            if (overlay && PyDict_Contains(assumed.ptr(), ik.ptr()) == 1) {
-                verify.append(kh);
-                continue;
-            }
-            PyObject* t = PyDict_GetItem(items.ptr(), ik.ptr());
-            if (t == nullptr || !PyDict_Check(t)) {
-                rest.append(kh);
-                continue;
-            }
-            PyObject* st = PyDict_GetItem(t, k_status);
-            PyObject* conds = st != nullptr && PyDict_Check(st) ? PyDict_GetItem(st, k_conditions) : nullptr;
-            PyObject* m = PyDict_GetItem(t, k_metadata);
-            if (m == nullptr || !PyDict_Check(m)) m = nullptr;
-            int conds_true = conds == nullptr ? 0 : PyObject_IsTrue(conds);
-            if (conds_true < 0) throw py::error_already_set();
-            PyObject* rv = m != nullptr ? PyDict_GetItem(m, k_rv) : nullptr;
-            PyObject* ad = PyDict_GetItem(adopted.ptr(), key);
-            int ne = PyObject_RichCompareBool(ad != nullptr ? ad : Py_None, rv != nullptr ? rv : Py_None, Py_NE);
-            if (ne < 0) throw py::error_already_set();
-            if (!conds_true || ne) {
-                rest.append(kh);
-                continue;
-            }
-            PyObject* uid = m != nullptr ? PyDict_GetItem(m, k_uid) : nullptr;
-            PyObject* gen = m != nullptr ? PyDict_GetItem(m, k_gen) : nullptr;
-            std::string uid_s;
-            if (uid != nullptr && uid != Py_None) {
-                Py_ssize_t ul = 0;
-                const char* uc = PyUnicode_Check(uid) ? PyUnicode_AsUTF8AndSize(uid, &ul) : nullptr;
-                if (uc == nullptr) {
-                    PyErr_Clear();
-                    verify.append(kh);
-                    continue;
-                }
-                uid_s.assign(uc, static_cast<size_t>(ul));
-            }
-            int64_t g = 0;
-            if (gen != nullptr && gen != Py_None) {
-                if (!PyLong_Check(gen)) {
-                    verify.append(kh);
-                    continue;
-                }
-                g = PyLong_AsLongLong(gen);
-                if (g == -1 && PyErr_Occurred()) {
-                    PyErr_Clear();
-                    verify.append(kh);
-                    continue;
-                }
-            }
-            int ok = ready(k, uid_s, g);
-            if (ok < 0) {
-                ++superseded;
-                continue;
-            }
-            if (ok == 0) {
-                rest.append(kh);
-                continue;
-            }
-            PyObject* sfp = PyDict_GetItem(t, k_sfp);
-            PyObject* spec = PyDict_GetItem(t, k_spec);
-            PyObject* rfp = spec != nullptr && PyDict_Check(spec) ? PyDict_GetItem(spec, k_rfp) : nullptr;
-            PyObject* memo = PyDict_GetItem(memos.ptr(), key);
-            bool hit = sfp != nullptr && rfp != nullptr && memo != nullptr && PyTuple_Check(memo) &&
-                       PyTuple_GET_SIZE(memo) == 3 && PyTuple_GET_ITEM(memo, 2) == shards.ptr();
-            if (hit) {
-                int e0 = PyObject_RichCompareBool(PyTuple_GET_ITEM(memo, 0), sfp, Py_EQ);
-                int e1 = e0 == 1 ? PyObject_RichCompareBool(PyTuple_GET_ITEM(memo, 1), rfp, Py_EQ) : 0;
-                if (e0 < 0 || e1 < 0) throw py::error_already_set();
-                hit = e0 == 1 && e1 == 1;
-            }
-            if (!hit) {
-                verify.append(kh);
-                continue;
-            }
-            int pend = PySet_Contains(pending_event.ptr(), key);
-            if (pend < 0) throw py::error_already_set();
-            if (pend || event_on_noop) {
-                if (pend && PySet_Discard(pending_event.ptr(), key) < 0) throw py::error_already_set();
-                events.append(py::handle(t));
-            } else {
-                ++done;
-            }
-        }
-        return py::make_tuple(rest, verify, events, done, superseded);
-    }
-
-  private:
-    static constexpr uint32_t kMaxFrame = 64u * 1024 * 1024;  // ipc.MAX_FRAME
-
-    // ready_ok without Python objects: -1 some shard has not reported on this version, 0 a failure, 1 all ok
-    int ready(const std::string& key, const std::string& uid, int64_t gen) const {
-        auto it = state_.find(key);
-        if (it == state_.end()) return -1;
-        bool ok = true;
-        for (const auto& s : shards_) {
-            const Slot* e = find(it->second, s);
-            if (e == nullptr || e->uid != uid || e->gen < gen) return -1;
-            ok = ok && e->err.empty();
-        }
-        return ok ? 1 : 0;
-    }
-
-    void fold_frame(const char* p, size_t len, bool batch, Folded& f) {
-        MpReader r(p, len);
-        size_t n = 1;
-        if (batch && !r.arr_len(n)) MpReader::fail();
-        for (size_t k = 0; k < n; ++k) {
-            const uint8_t* at = r.pos();
-            int rc = report(r, f.complete, f.wrote, f.errors);
-            if (rc < 0) {  // not a report: decode it for Python
-                r.seek(at);
-                f.others.append(py::reinterpret_steal<py::object>(r.value()));
-                continue;
-            }
-            if (rc == 2) continue;  // forwarded
-            ++f.reports;
-            if (rc == 0) ++f.pending;
-        }
-        if (!r.at_end()) MpReader::fail();
-    }
-
-    static const Slot* find(const std::vector<Slot>& v, std::string_view shard) {
-        for (const auto& s : v)
-            if (s.shard == shard) return &s;
-        return nullptr;
-    }
-
-    // One message at the reader.  -1: not a report (nothing folded; the caller rewinds), 0: folded, some
-    // shard still to report on this version, 1: folded and complete.
-    int report(MpReader& r, py::list& complete, py::list& wrote, py::list& errors) {
-        const uint8_t* msg = r.pos();
-        size_t n;
-        if (!r.map_len(n)) return -1;
-        const uint8_t* body = r.pos();
-        // first pass: is it {"t": "report", ...}?  (key order is the sender's)
-        bool is_report = false;
-        for (size_t k = 0; k < n; ++k) {
-            std::string_view key, val;
-            if (!r.str(key)) return -1;
-            if (key == "t") {
-                if (!r.str(val)) return -1;
-                is_report = val == "report";
-                break;
-            }
-            r.skip();
-        }
-        if (!is_report) return -1;
-        r.seek(body);
-        std::string_view rkey, uid;
-        int64_t gen = 0;
-        bool w = false, have_k = false;
-        const uint8_t* results = nullptr;
-        for (size_t k = 0; k < n; ++k) {
-            std::string_view key;
-            if (!r.str(key)) MpReader::fail();
-            if (key == "k") {
-                if (!r.str(rkey)) MpReader::fail();
-                have_k = true;
-            } else if (key == "u") {
-                if (!r.str(uid)) MpReader::fail();
-            } else if (key == "g") {
-                if (!r.integer(gen) && !r.nil()) MpReader::fail();
-            } else if (key == "w") {
-                w = r.truthy();
-            } else if (key == "r") {
-                results = r.pos();
-                r.skip();
-            } else {
-                r.skip();
-            }
-        }
-        if (!have_k || results == nullptr) MpReader::fail();
-        const uint8_t* end = r.pos();
-        if (parts_ > 1) {  // ipc key "kind/ns/name": its partition is crc32("ns/name") % C (executor.key_part)
-            size_t slash = rkey.find('/');
-            std::string_view nsname = slash == std::string_view::npos ? std::string_view() : rkey.substr(slash + 1);
-            int p = static_cast<int>((crc_update(0xFFFFFFFFu, nsname) ^ 0xFFFFFFFFu) % static_cast<uint32_t>(parts_));
-            if (p != part_) {  // another coordinator partition's key: hand its raw bytes on, unfolded
-                forwards_[p].emplace_back(reinterpret_cast<const char*>(msg), static_cast<size_t>(end - msg));
-                return 2;
-            }
-        }
-        std::string skey(rkey);
-        auto& slots = state_[skey];
-        r.seek(results);
-        size_t m;
-        if (!r.map_len(m)) MpReader::fail();
-        bool changed = false;
-        for (size_t k = 0; k < m; ++k) {
-            std::string_view shard, err, text;
-            if (!r.str(shard)) MpReader::fail();
-            const uint8_t* v = r.pos();
-            if (!r.nil()) {
-                bool is_str = r.str(text);
-                if (!is_str) r.skip();  // a typed failure map (or any other value): kept raw
-                if (!is_str || !text.empty())  // an empty string is a success
-                    err = std::string_view(reinterpret_cast<const char*>(v), static_cast<size_t>(r.pos() - v));
-            }
-            Slot* s = const_cast<Slot*>(find(slots, shard));
-            if (s == nullptr) {
-                slots.push_back(Slot{std::string(shard), {}, 0, {}});
-                s = &slots.back();
-                changed = true;
-            } else if (!changed && (s->uid != uid || s->gen != gen || s->err != err)) {
-                changed = true;
-            }
-            s->uid.assign(uid.data(), uid.size());
-            s->gen = gen;
-            s->err.assign(err.data(), err.size());
-            if (!err.empty()) errors.append(py::str(shard.data(), shard.size()));
-        }
-        r.seek(end);
-        py::str pkey(skey);
-        if (w) wrote.append(pkey);
-        for (const auto& sh : shards_) {
-            const Slot* e = find(slots, sh);
-            if (e == nullptr || e->uid != uid || e->gen < gen) return 0;
-        }
-        if (changed || w) complete.append(pkey);  // a repeat of a complete set changes nothing
-        return 1;
-    }
-
-    std::vector<std::string> shards_;
-    std::unordered_map<std::string, std::vector<Slot>> state_;
-    int part_ = 0, parts_ = 1;
-    std::map<int, std::vector<std::string>> forwards_;
-};
-// The Python clients' HTTP/2 framing (ncc/kube/h2client.py `H2Conn`, the coordinator's connection to the
-// controller cluster and the Python executor's to its shards): the frame parser, HPACK decoding of response heads,
-// body assembly, the line splitting of watch bodies, and the replies the connection owes by itself (SETTINGS and
-// PING acks, WINDOW_UPDATE for consumed DATA).  Python keeps the policy: streams, send windows, limits, GOAWAY.
-class H2ClientParser {
-public:
-    static constexpr uint32_t kMaxFrame = 1u << 20;       // what the client advertises (SETTINGS_MAX_FRAME_SIZE)
-    static constexpr int64_t kStreamWindow = 1 << 24;      // SETTINGS_INITIAL_WINDOW_SIZE from the client
-    static constexpr int64_t kConnWindow = int64_t{1} << 30;  // the connection window after the opening update
-
-    // The client's connection preface, SETTINGS and the connection-window update.
-    static py::bytes preface() {
-        std::string out("PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n", 24);
-        std::string s;
-        auto setting = [&s](uint16_t id, uint32_t v) {
-            s.push_back(static_cast<char>(id >> 8));
-            s.push_back(static_cast<char>(id));
-            put32(s, v);
-        };
-        setting(0x2, 0);  // ENABLE_PUSH
-        setting(0x4, static_cast<uint32_t>(kStreamWindow));
-        setting(0x5, kMaxFrame);
-        frame(out, 4, 0, 0, s);
-        std::string w;
-        put32(w, static_cast<uint32_t>(kConnWindow - 65535));
-        frame(out, 8, 0, 0, w);
-        return py::bytes(out);
-    }
-
-    // DATA of stream `sid` comes back as complete lines ("lines" events) instead of one body.
-    void watch(uint32_t sid) { streams_[sid].watch = true; }
-    // A stream the client reset: its remaining frames are dropped.  (Other streams are known from their response
-    // HEADERS on; the set of reset ones is pruned of its oldest half past 1024: the server stopped those long ago.)
-    void forget(uint32_t sid) {
-        streams_.erase(sid);
-        dead_.insert(sid);
-        if (dead_.size() > 1024) dead_.erase(dead_.begin(), std::next(dead_.begin(), 512));
-    }
-    size_t open_streams() const { return streams_.size(); }
-
-    // Feed received bytes -> (events, bytes to send).  Events, in order:
-    //   ("resp", sid, status, retry_after | None, body)  a whole response (END_STREAM seen)
-    //   ("head", sid, status, retry_after | None)        a watch stream's response head
-    //   ("lines", sid, [line, ...], data_bytes, ended)   a watch stream's complete lines (and its end)
-    //   ("settings", [(id, value), ...])  ("window", sid, n)  ("rst", sid, code)  ("goaway", last, code, debug)
-    //   ("error", code, message)   a connection error (send GOAWAY, close)
-    //   ("noh2",)                   the first frame was not SETTINGS: the server does not speak HTTP/2
-    // Sent bytes: SETTINGS / PING acks and WINDOW_UPDATEs for the connection and for unwatched streams (a watch's
-    // stream window is credited by Python as its consumer takes the lines).
-    py::tuple feed(const py::bytes& data) {
-        std::string_view d = data;
-        buf_.append(d.data(), d.size());
-        py::list ev;
-        out_.clear();
-        try {
-            parse(ev);
-        } catch (const ncc::hpack::Error& e) {
-            ev.append(py::make_tuple("error", 9, std::string("HPACK: ") + e.what()));
-            buf_.clear();
-            pos_ = 0;
-        } catch (const std::runtime_error& e) {
-            ev.append(py::make_tuple("error", 1, std::string(e.what())));
-            buf_.clear();
-            pos_ = 0;
-        }
-        if (pos_ > 0 && (pos_ == buf_.size() || pos_ > 65536)) {
-            buf_.erase(0, pos_);
-            pos_ = 0;
-        }
-        if (conn_unacked_ >= (1 << 24)) {
-            std::string w;
-            put32(w, static_cast<uint32_t>(conn_unacked_));
-            frame(out_, 8, 0, 0, w);
-            conn_unacked_ = 0;
-        }
-        return py::make_tuple(ev, py::bytes(out_));
-    }
-
-private:
-    struct Stream {
-        std::string body, pending;  // unary: the body; watch: the partial line
-        int status = 0;
-        py::object retry = py::none();
-        int64_t unacked = 0;
-        bool watch = false, have_head = false;
-    };
-    std::string buf_, out_;
-    size_t pos_ = 0;
-    bool first_ = true;
-    uint32_t cont_id_ = 0;
-    bool cont_end_ = false;
-    std::string cont_block_;
-    int64_t conn_unacked_ = 0;
-    ncc::hpack::Decoder dec_{4096};
-    std::unordered_map<uint32_t, Stream> streams_;
-    std::set<uint32_t> dead_;
-
-    static uint32_t u32(const char* p) {
-        const auto* u = reinterpret_cast<const unsigned char*>(p);
-        return (uint32_t{u[0]} << 24) | (uint32_t{u[1]} << 16) | (uint32_t{u[2]} << 8) | u[3];
-    }
-    static void put32(std::string& s, uint32_t v) {
-        s.push_back(static_cast<char>(v >> 24));
-        s.push_back(static_cast<char>(v >> 16));
-        s.push_back(static_cast<char>(v >> 8));
-        s.push_back(static_cast<char>(v));
-    }
-    static void frame(std::string& out, uint8_t type, uint8_t flags, uint32_t id, std::string_view p) {
-        size_t n = p.size();
-        out.push_back(static_cast<char>(n >> 16));
-        out.push_back(static_cast<char>(n >> 8));
-        out.push_back(static_cast<char>(n));
-        out.push_back(static_cast<char>(type));
-        out.push_back(static_cast<char>(flags));
-        put32(out, id & 0x7fffffffu);
-        out.append(p.data(), n);
-    }
-    static std::string_view strip(uint8_t flags, std::string_view p, bool headers) {
-        size_t pad = 0;
-        if (flags & 0x8) {
-            if (p.empty()) throw std::runtime_error("padded frame without a pad length");
-            pad = static_cast<uint8_t>(p[0]);
-            p.remove_prefix(1);
-        }
-        if (headers && (flags & 0x20)) {
-            if (p.size() < 5) throw std::runtime_error("short PRIORITY fields");
-            p.remove_prefix(5);
-        }
-        if (pad > p.size()) throw std::runtime_error("padding longer than the frame");
-        p.remove_suffix(pad);
-        return p;
-    }
-    void finish(py::list& ev, uint32_t sid, Stream& st) {
-        if (st.watch) {
-            py::list lines;
-            size_t a = st.pending.find_first_not_of(" \t\r\n");
-            if (a != std::string::npos) lines.append(py::bytes(st.pending));
-            ev.append(py::make_tuple("lines", sid, lines, 0, true));
-        } else {
-            ev.append(py::make_tuple("resp", sid, st.status, st.retry, py::bytes(st.body)));
-        }
-        streams_.erase(sid);
-    }
-    void headers_done(py::list& ev, uint32_t sid) {
-        std::vector<ncc::hpack::Decoder::Header> hs;
-        dec_.decode(reinterpret_cast<const uint8_t*>(cont_block_.data()), cont_block_.size(), hs);
-        auto it = streams_.find(sid);
-        if (it == streams_.end()) {
-            if (sid % 2 == 0 || dead_.count(sid)) return;  // a stream the client gave up on (the block fed the table)
-            it = streams_.emplace(sid, Stream{}).first;
-        }
-        Stream& st = it->second;
-        if (!st.have_head) {
-            int status = 0;
-            for (auto& h : hs) {
-                if (h.first == ":status") {
-                    status = std::atoi(h.second.c_str());
-                } else if (h.first == "retry-after") {
-                    st.retry = py::str(h.second);
-                }
-            }
-            if (status == 0) throw std::runtime_error("response without :status");
-            if (status >= 200) {  // 1xx heads are informational: the real one follows
-                st.status = status;
-                st.have_head = true;
-                if (st.watch) ev.append(py::make_tuple("head", sid, status, st.retry));
-            }
-        }  // else trailers: nothing in them is used
-        if (cont_end_) finish(ev, sid, st);
-    }
-    void on_data(py::list& ev, uint32_t sid, uint8_t flags, std::string_view pl, uint32_t len) {
-        conn_unacked_ += len;
-        std::string_view d = strip(flags, pl, false);
-        auto it = streams_.find(sid);
-        if (it == streams_.end()) return;  // reset by us: already counted against the connection, dropped
-        Stream& st = it->second;
-        if (!st.have_head) throw std::runtime_error("DATA before the response head");
-        if (st.watch) {
-            py::list lines;
-            std::string& p = st.pending;
-            size_t start = 0, nl;
-            while ((nl = d.find('\n', start)) != std::string_view::npos) {
-                if (p.empty()) {
-                    if (nl > start) lines.append(py::bytes(d.data() + start, nl - start));
-                } else {
-                    p.append(d.data() + start, nl - start);
-                    lines.append(py::bytes(p));
-                    p.clear();
-                }
-                start = nl + 1;
-            }
-            p.append(d.data() + start, d.size() - start);
-            if (py::len(lines) > 0 || len > 0)
-                ev.append(py::make_tuple("lines", sid, lines, len, false));
-        } else {
-            st.body.append(d.data(), d.size());
-            st.unacked += len;
-            if (st.unacked >= kStreamWindow / 2 && !(flags & 0x1)) {
-                std::string w;
-                put32(w, static_cast<uint32_t>(st.unacked));
-                frame(out_, 8, 0, sid, w);
-                st.unacked = 0;
-            }
-        }
-        if (flags & 0x1) finish(ev, sid, st);
-    }
-    void parse(py::list& ev) {
-        while (buf_.size() - pos_ >= 9) {
-            const char* p = buf_.data() + pos_;
-            uint32_t len = (uint32_t{static_cast<uint8_t>(p[0])} << 16) | (uint32_t{static_cast<uint8_t>(p[1])} << 8) |
-                           static_cast<uint8_t>(p[2]);
-            uint8_t type = static_cast<uint8_t>(p[3]), flags = static_cast<uint8_t>(p[4]);
-            if (first_) {  // a server speaking HTTP/2 opens with SETTINGS (not an ack)
-                if (type != 4 || (flags & 0x1) || len % 6 != 0 || len > 6 * 64) {
-                    ev.append(py::make_tuple("noh2"));
-                    buf_.clear();
-                    pos_ = 0;
-                    return;
-                }
-                first_ = false;
-            }
-            if (len > kMaxFrame) throw std::runtime_error("frame larger than SETTINGS_MAX_FRAME_SIZE");
-            if (buf_.size() - pos_ < 9 + len) return;
-            uint32_t sid = u32(p + 5) & 0x7fffffffu;
-            std::string_view pl(p + 9, len);
-            pos_ += 9 + len;
-            if (cont_id_ != 0 && (type != 9 || sid != cont_id_)) throw std::runtime_error("expected CONTINUATION");
-            switch (type) {
-                case 0:
-                    on_data(ev, sid, flags, pl, len);
-                    break;
-                case 1: {  // HEADERS
-                    if (sid == 0) throw std::runtime_error("HEADERS on stream 0");
-                    std::string_view b = strip(flags, pl, true);
-                    cont_block_.assign(b.data(), b.size());
-                    cont_end_ = (flags & 0x1) != 0;
-                    if (flags & 0x4)
-                        headers_done(ev, sid);
-                    else
-                        cont_id_ = sid;
-                    break;
-                }
-                case 9:  // CONTINUATION
-                    if (cont_id_ == 0) throw std::runtime_error("CONTINUATION without HEADERS");
-                    cont_block_.append(pl.data(), pl.size());
-                    if (flags & 0x4) {
-                        uint32_t id = cont_id_;
-                        cont_id_ = 0;
-                        headers_done(ev, id);
-                    }
-                    break;
-                case 4: {  // SETTINGS
-                    if (flags & 0x1) break;
-                    if (len % 6 != 0) throw std::runtime_error("SETTINGS length not a multiple of 6");
-                    py::list kv;
-                    for (size_t k = 0; k + 6 <= pl.size(); k += 6) {
-                        uint32_t id = (static_cast<uint8_t>(pl[k]) << 8) | static_cast<uint8_t>(pl[k + 1]);
-                        uint32_t v = u32(pl.data() + k + 2);
-                        // SETTINGS_HEADER_TABLE_SIZE (0x1) bounds the table of *our* encoder, which keeps none;
-                        // the server's encoder stays bound by the size we advertise (the 4096 default), so our
-                        // decoder keeps it (RFC 9113 §6.5.2, RFC 7541 §4.2) whatever the server sends here
-                        kv.append(py::make_tuple(id, v));
-                    }
-                    frame(out_, 4, 0x1, 0, {});
-                    ev.append(py::make_tuple("settings", kv));
-                    break;
-                }
-                case 8:  // WINDOW_UPDATE
-                    ev.append(py::make_tuple("window", sid, pl.size() >= 4 ? (u32(pl.data()) & 0x7fffffffu) : 0u));
-                    break;
-                case 3:  // RST_STREAM (also of a stream whose response had not begun: Python knows it)
-                    streams_.erase(sid);
-                    ev.append(py::make_tuple("rst", sid, pl.size() >= 4 ? u32(pl.data()) : 0u));
-                    break;
-                case 6:  // PING
-                    if (!(flags & 0x1)) frame(out_, 6, 0x1, 0, pl);
-                    break;
-                case 7:  // GOAWAY
-                    ev.append(py::make_tuple("goaway", pl.size() >= 4 ? (u32(pl.data()) & 0x7fffffffu) : 0u,
-                                             pl.size() >= 8 ? u32(pl.data() + 4) : 0u,
-                                             py::bytes(pl.size() > 8 ? pl.substr(8) : std::string_view())));
-                    break;
-                case 5:
-                    throw std::runtime_error("PUSH_PROMISE with push disabled");
-                default:  // PRIORITY, unknown types
-                    break;
-            }
-        }
-    }
-};
-
-// A request's HEADERS (+ CONTINUATION) and, when `body` is not empty, its DATA frames on stream `sid`.  `fixed` is
-// the caller's pre-encoded block of the fields every request repeats (:scheme, :authority, user-agent, accept,
-// content-type, authorization); `content_length` < 0 sends none; `end` ends the stream on the last frame (false:
-// the body follows as DATA frames the caller sends when the flow-control windows allow).
-py::bytes h2_request(uint32_t sid, const std::string& method, const std::string& path, const py::bytes& fixed,
-                     int64_t content_length, const py::bytes& body, bool end, size_t max_frame) {
-    std::string_view f = fixed, b = body;
-    std::string block;
-    block.reserve(f.size() + path.size() + 16);
-    ncc::hpack::encode_field(block, ":method", method);
-    ncc::hpack::encode_literal_indexed_name(block, 4, path);  // :path
-    block.append(f.data(), f.size());
-    if (content_length >= 0) ncc::hpack::encode_literal_indexed_name(block, 28, std::to_string(content_length));
-    std::string out;
-    out.reserve(block.size() + b.size() + 32);
-    auto frame = [&out](uint8_t type, uint8_t flags, uint32_t id, const char* p, size_t n) {
-        out.push_back(static_cast<char>(n >> 16));
-        out.push_back(static_cast<char>(n >> 8));
-        out.push_back(static_cast<char>(n));
-        out.push_back(static_cast<char>(type));
-        out.push_back(static_cast<char>(flags));
-        out.push_back(static_cast<char>((id >> 24) & 0x7f));
-        out.push_back(static_cast<char>(id >> 16));
-        out.push_back(static_cast<char>(id >> 8));
-        out.push_back(static_cast<char>(id));
-        out.append(p, n);
-    };
-    max_frame = std::max<size_t>(max_frame, 1);
-    size_t n = std::min(block.size(), max_frame);
-    bool more = n < block.size();
-    frame(1, static_cast<uint8_t>((b.empty() && end ? 0x1 : 0) | (more ? 0 : 0x4)), sid, block.data(), n);
-    for (size_t off = n; off < block.size(); off += n) {
-        n = std::min(block.size() - off, max_frame);
-        frame(9, off + n < block.size() ? 0 : 0x4, sid, block.data() + off, n);
-    }
-    for (size_t off = 0; off < b.size(); off += n) {
-        n = std::min(b.size() - off, max_frame);
-        frame(0, off + n == b.size() && end ? 0x1 : 0, sid, b.data() + off, n);
-    }
-    return py::bytes(out);
-}
-
-py::bytes hpack_encode(const std::vector<std::pair<std::string, std::string>>& fields, bool huffman) {
-    std::string out;
-    for (const auto& f : fields) ncc::hpack::encode_field(out, f.first, f.second, huffman);
-    return py::bytes(out);
-}
-
-py::bytes hpack_huffman_decode(const py::bytes& data) {
-    std::string_view b = data;
-    std::string out;
-    try {
-        ncc::hpack::huffman_decode(reinterpret_cast<const uint8_t*>(b.data()), b.size(), out);
-    } catch (const ncc::hpack::Error& e) {
-        throw py::value_error(std::string("HPACK: ") + e.what());
-    }
-    return py::bytes(out);
-}
+#include "ext/hashing.hpp"
+#include "ext/workqueue.hpp"
+#include "ext/scan.hpp"
+#include "ext/http1.hpp"
+#include "ext/pyjson.hpp"
+#include "ext/reports.hpp"
+#include "ext/h2client.hpp"
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {

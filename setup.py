@@ -1,5 +1,6 @@
-"""Packaging hook for the native code: the C++ runtime extension `ncc._native` (sources in native/) and
-the native shard executor `ncc/bin/ncc-executor` (native/executor/, C++20 + OpenSSL).
+"""Packaging hook for the native code: the C++ runtime extension `ncc._native` (sources in native/), the fake
+apiserver's `ncc.fakeapi._native` (native/fakeapi/) and the native shard executor `ncc/bin/ncc-executor`
+(native/executor/, C++20 + OpenSSL).
 
 `pip install .` / `python -m build` compile both with the same flags as `python native/build.py`, which
 remains the in-tree development build (it is what CI, `__graft_entry__.build()` and the tests use).  The
@@ -30,8 +31,10 @@ class BuildWithExecutor(build_ext):
 sys.path.insert(0, os.path.join(HERE, "native"))
 from build import arch_flags  # noqa: E402 — native/build.py: -mpopcnt on x86-64 only
 
-setup(ext_modules=[Pybind11Extension(
-    "ncc._native", ["native/ncc_native.cpp"], cxx_std=17,
-    extra_compile_args=["-O3", "-DNDEBUG", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra",
-                        "-Wno-unused-parameter"])],
-    cmdclass={"build_ext": BuildWithExecutor})
+_FLAGS = ["-O3", "-DNDEBUG", "-fvisibility=hidden", *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter"]
+# the controller's extension, and the fake apiserver's (ncc.fakeapi: test/bench substrate, kept out of the
+# controller's .so — native/fakeapi/)
+setup(ext_modules=[Pybind11Extension("ncc._native", ["native/ncc_native.cpp"], cxx_std=17, extra_compile_args=_FLAGS),
+                   Pybind11Extension("ncc.fakeapi._native", ["native/fakeapi/fakeapi_native.cpp"], cxx_std=17,
+                                     extra_compile_args=_FLAGS)],
+      cmdclass={"build_ext": BuildWithExecutor})

@@ -40,6 +40,7 @@ def line(obj: dict) -> bytes:
 class Executor:
     def __init__(self, config: dict, env: dict | None = None):
         self.config, self.env = config, env
+        self.pending: list = []  # messages received but not yet returned by next_message
 
     async def __aenter__(self):
         parent, child = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -57,13 +58,19 @@ class Executor:
         self.ch.send({"t": "s", "k": kind, "l": [line(o) for o in objs]})
 
     async def next_message(self, t: str, timeout: float = 10.0) -> dict:
+        """The next message of type `t`.  A batch holds several messages (reports travel in batches): the ones
+        after the match stay buffered for the next call, instead of being dropped (driving
+        the executor with the first-match-only version under-counted 50 reports as 13–46)."""
         async def go():
             while True:
+                for i, m in enumerate(self.pending):
+                    if m.get("t") == t:
+                        del self.pending[:i + 1]  # earlier messages of other types are consumed, as before
+                        return m
+                self.pending.clear()
                 batch = await self.ch.recv()
                 assert batch is not None, "executor closed the channel"
-                for m in batch:
-                    if m.get("t") == t:
-                        return m
+                self.pending.extend(batch)
         return await asyncio.wait_for(go(), timeout)
 
     async def close(self) -> str:
@@ -156,6 +163,28 @@ async def test_sampling_profile_is_written_and_symbolized(tmp_path):
     counts = prof.load_samples([str(tmp_path)])
     out = prof.report(counts, binary_path(), 10)
     assert out.split()[0].isdigit() and "== self" in out if counts else out == "no samples"
+
+
+async def test_every_report_of_a_batch_is_seen():
+    """50 templates in one snapshot: the executor reports on each, several reports to a frame; the helper keeps
+    the rest of a batch for its next call, so all 50 are counted (the first-match version saw 13–46)."""
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        ts = []
+        for i in range(50):
+            t = make_template(i, NS)
+            t["metadata"].update(uid=f"u-{i}", resourceVersion=str(10 + i), generation=1)
+            ts.append(t)
+        async with Executor(cfg([{"name": "shard-0", "server": url}])) as ex:
+            for k, objs in ((0, ts), (1, []), (2, []), (3, [])):
+                ex.snapshot(k, objs)
+            seen = set()
+            while len(seen) < 50:
+                seen.add((await ex.next_message("report", timeout=20))["k"])
+            assert seen == {f"template/{NS}/algo-{i:05d}" for i in range(50)}
+    finally:
+        await srv.stop()
 
 
 async def test_unreadable_relayed_line_costs_only_itself():
