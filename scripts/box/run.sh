@@ -127,6 +127,7 @@ case "$what" in
       timeout -k 10 600 python3 bench.py --steps "${1:-100}" --warmup 5 "${@:2}" > "$out/sampled_bench.json" \
       2> "$out/sampled_bench.err" || exit $?
     python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
+    python3 scripts/py_profile.py "$out"/py.*.json > "$out/coordinator_profile.txt" 2>&1 || true
     summary "$out/sampled_bench.json"
     ;;
   prof)
@@ -136,6 +137,7 @@ case "$what" in
     NCC_SAMPLE_PROFILE="$PWD/$out/samples" NCC_SAMPLE_US=200 timeout -k 10 300 python3 bench.py --steps 20 \
       --warmup 5 > "$out/sampled_bench.json" 2> "$out/sampled_bench.err" || exit $?
     python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
+    python3 scripts/py_profile.py "$out"/py.*.json > "$out/coordinator_profile.txt" 2>&1 || true
     summary "$out/sampled_bench.json"
     ;;
   modes)
