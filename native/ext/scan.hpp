@@ -397,6 +397,170 @@ py::tuple owner_filter(py::list lines, py::dict items, py::dict assumed, const s
     return py::make_tuple(keep, dropped, rv_o);
 }
 
+// OwnerFilter()(lines, items, assumed, default_ns): owner_filter's result, with a memo per informer so a dropped
+// line builds no Python object.  The memo maps "namespace\0name" to the store's key tuple, the cached object it
+// last compared against (a strong reference: identity is the test, so the address cannot be reused) and that
+// object's owners in a canonical byte form (length-prefixed name, uid per reference).  A line is then one scan,
+// one C++ lookup, one dict lookup of the memoised key to see that the store still holds the same object, and a
+// byte compare of the owners.  An entry whose object was replaced is refreshed from the new one; the memo is
+// dropped whole when it outgrows the store by 4096 keys (deleted keys), as the Python filter's signatures are.
+class OwnerFilter {
+  public:
+    OwnerFilter() = default;
+    OwnerFilter(const OwnerFilter&) = delete;
+    OwnerFilter& operator=(const OwnerFilter&) = delete;
+    ~OwnerFilter() { clear(); }  // the Python object's deallocation: the GIL is held
+
+    void clear() {
+        for (auto& kv : memo_) {
+            Py_XDECREF(kv.second.key);
+            Py_XDECREF(kv.second.obj);
+        }
+        memo_.clear();
+    }
+    size_t size() const { return memo_.size(); }
+
+    py::tuple call(py::list lines, py::dict items, py::dict assumed, const std::string& default_ns) {
+        py::list keep;
+        long long dropped = 0;
+        std::string_view last_rv;
+        bool last_dropped = false;
+        const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
+        PyObject* itd = items.ptr();
+        const bool any_assumed = PyDict_GET_SIZE(assumed.ptr()) > 0;
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
+            last_dropped = false;
+            char* buf = nullptr;
+            Py_ssize_t len = 0;
+            bool drop = false;
+            std::string_view type, ns, name, rv;
+            if (PyBytes_Check(line) && PyBytes_AsStringAndSize(line, &buf, &len) == 0) {
+                owners_.clear();
+                uids_.clear();
+                Scanner sc(buf, static_cast<size_t>(len));
+                sc.owners = &owners_;
+                sc.owner_uids = &uids_;
+                if (sc.scan(type, ns, name, rv) && type == "MODIFIED")
+                    drop = judge(ns.empty() ? std::string_view(default_ns) : ns, name, itd, assumed.ptr(), any_assumed);
+            } else {
+                PyErr_Clear();
+            }
+            if (drop) {
+                ++dropped;
+                last_rv = rv;
+                last_dropped = true;
+            } else if (PyList_Append(keep.ptr(), line) != 0) {
+                throw py::error_already_set();
+            }
+        }
+        py::object rv_o = last_dropped ? py::object(py::str(last_rv.data(), last_rv.size())) : py::object(py::none());
+        return py::make_tuple(keep, dropped, rv_o);
+    }
+
+  private:
+    struct Entry {
+        PyObject* key = nullptr;  // the store's (namespace, name) tuple
+        PyObject* obj = nullptr;  // the cached object `owners` was read from
+        std::string owners;       // canonical owners of `obj`
+        bool comparable = false;  // false: some reference is not {name: str, uid: str}; never dropped
+    };
+    std::unordered_map<std::string, Entry> memo_;
+    std::string kbuf_, line_owners_;
+    std::vector<std::string_view> owners_, uids_;
+
+    static void put(std::string& out, std::string_view v) {
+        uint32_t l = static_cast<uint32_t>(v.size());
+        out.append(reinterpret_cast<const char*>(&l), sizeof l);
+        out.append(v.data(), v.size());
+    }
+    // the cached object's owners in canonical form; false when they cannot compare equal to a scanned line
+    static bool cached_owners(PyObject* cur, std::string& out) {
+        static PyObject* k_meta = PyUnicode_InternFromString("metadata");
+        static PyObject* k_refs = PyUnicode_InternFromString("ownerReferences");
+        static PyObject* k_name = PyUnicode_InternFromString("name");
+        static PyObject* k_uid = PyUnicode_InternFromString("uid");
+        out.clear();
+        if (!PyDict_Check(cur)) return false;
+        PyObject* m = PyDict_GetItem(cur, k_meta);
+        PyObject* refs = m != nullptr && PyDict_Check(m) ? PyDict_GetItem(m, k_refs) : nullptr;
+        if (refs == nullptr || refs == Py_None) return true;
+        if (!PyList_Check(refs)) return false;
+        for (Py_ssize_t j = 0; j < PyList_GET_SIZE(refs); ++j) {
+            PyObject* r = PyList_GET_ITEM(refs, j);
+            if (!PyDict_Check(r)) return false;
+            for (PyObject* k : {k_name, k_uid}) {
+                PyObject* v = PyDict_GetItem(r, k);
+                if (v == nullptr) {
+                    put(out, std::string_view());
+                    continue;
+                }
+                if (!PyUnicode_Check(v)) return false;
+                Py_ssize_t vn = 0;
+                const char* u = PyUnicode_AsUTF8AndSize(v, &vn);
+                if (u == nullptr) {
+                    PyErr_Clear();
+                    return false;
+                }
+                put(out, std::string_view(u, static_cast<size_t>(vn)));
+            }
+        }
+        return true;
+    }
+    bool judge(std::string_view kns, std::string_view name, PyObject* items, PyObject* assumed, bool any_assumed) {
+        kbuf_.assign(kns.data(), kns.size());
+        kbuf_ += '\0';
+        kbuf_.append(name.data(), name.size());
+        auto it = memo_.find(kbuf_);
+        if (it == memo_.end()) {
+            PyObject* kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
+            PyObject* nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
+            if (nm == nullptr) {  // not UTF-8: kept, the Python path decides
+                Py_XDECREF(kn);
+                PyErr_Clear();
+                return false;
+            }
+            PyObject* key = PyTuple_Pack(2, kn, nm);
+            Py_DECREF(kn);
+            Py_DECREF(nm);
+            if (key == nullptr) throw py::error_already_set();
+            PyObject* cur = PyDict_GetItemWithError(items, key);
+            if (cur == nullptr) {
+                Py_DECREF(key);
+                if (PyErr_Occurred()) throw py::error_already_set();
+                return false;  // not cached: kept, and not memoised (the store may never hold it)
+            }
+            if (memo_.size() > static_cast<size_t>(PyDict_GET_SIZE(items)) + 4096) clear();
+            it = memo_.emplace(kbuf_, Entry{}).first;
+            it->second.key = key;  // the reference PyTuple_Pack gave
+        }
+        Entry& e = it->second;
+        if (any_assumed) {
+            int overlaid = PyDict_Contains(assumed, e.key);
+            if (overlaid < 0) throw py::error_already_set();
+            if (overlaid) return false;
+        }
+        PyObject* cur = PyDict_GetItemWithError(items, e.key);
+        if (cur == nullptr) {
+            if (PyErr_Occurred()) throw py::error_already_set();
+            return false;
+        }
+        if (cur != e.obj) {
+            Py_INCREF(cur);
+            Py_XDECREF(e.obj);
+            e.obj = cur;
+            e.comparable = cached_owners(cur, e.owners);
+        }
+        if (!e.comparable) return false;
+        line_owners_.clear();
+        for (size_t j = 0; j < owners_.size(); ++j) {
+            put(line_owners_, owners_[j]);
+            put(line_owners_, uids_[j]);
+        }
+        return line_owners_ == e.owners;
+    }
+};
+
 // relay_index(lines, raw, default_ns) -> the lines to forward.  The one-partition relay's whole loop in one
 // call: each ADDED/MODIFIED line is stored in `raw` under (namespace, name), a DELETED one removes its key,
 // and every object event is forwarded; BOOKMARK/ERROR and unreadable lines are dropped (the coordinator's

@@ -29,7 +29,8 @@
 // The fake apiserver's native pieces (its HTTP/1.1 request-head parser, HTTP/2 server parser and response
 // encoder) are not here: they are test substrate, built into ncc/fakeapi/_native from native/fakeapi/
 //  — the product extension carries no server code.
-//  * owner_filter(lines, items, assumed, ns) — the metadata-only informer's owner filter over a batch.
+//  * owner_filter(lines, items, assumed, ns) — the metadata-only informer's owner filter over a batch;
+//    OwnerFilter — the same with a memo per informer (no Python object built for a dropped line).
 //  * relay_index(lines, raw, ns) — the one-partition watch relay's index-and-forward loop.
 //  * chunk_lines(bytearray, state, bytearray) — a chunked watch body cut into its event lines in one call.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
@@ -68,7 +69,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 28
+#define NCC_NATIVE_ABI 29
 
 namespace {
 #include "ext/hashing.hpp"
@@ -100,6 +101,12 @@ PYBIND11_MODULE(_native, m) {
           "(type_code, namespace, name, key_partition, owner_partition_mask, n_owners) of a watch line");
     m.def("owner_filter", &owner_filter, py::arg("lines"), py::arg("items"), py::arg("assumed"),
           py::arg("default_ns"), "the metadata-only informer's owner filter over a batch of watch lines");
+    py::class_<OwnerFilter>(m, "OwnerFilter")
+        .def(py::init<>())
+        .def("__call__", &OwnerFilter::call, py::arg("lines"), py::arg("items"), py::arg("assumed"),
+             py::arg("default_ns"), "owner_filter over a batch, memoising keys, cached objects and their owners")
+        .def("clear", &OwnerFilter::clear)
+        .def("__len__", &OwnerFilter::size);
     m.def("relay_index", &relay_index, py::arg("lines"), py::arg("raw"), py::arg("default_ns"),
           "the one-partition relay loop: index the lines in `raw`, return the object events to forward");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));

@@ -103,6 +103,7 @@ class Informer:
         self._inflight: dict = {}
         self._stash: dict = {}
         self._owner_sigs: dict = {}  # key -> (cached object, owner names, owner uids): the metadata-only filter
+        self._owner_memo = None  # the native metadata-only filter with its memo (native/ext/scan.hpp OwnerFilter)
         # set by the owner when the apiserver answers its other requests again (ncc/shards/shard.py): a
         # list/watch waiting out an outage backoff retries at once, once per outage
         self.answering: asyncio.Event | None = None
@@ -308,7 +309,12 @@ class Informer:
             opart = of.part if of is not None else None
             oref = getattr(of, "referenced", None) if of is not None else None
             kf = of = None
-        return (scan, nparts, kpart, opart, oref, kf, of, mo, getattr(mod, "owner_filter", None) if mo else None)
+        batch_filter = None
+        if mo:
+            if self._owner_memo is None and hasattr(mod, "OwnerFilter"):
+                self._owner_memo = mod.OwnerFilter()
+            batch_filter = self._owner_memo if self._owner_memo is not None else getattr(mod, "owner_filter", None)
+        return (scan, nparts, kpart, opart, oref, kf, of, mo, batch_filter)
 
     async def _watch(self, rv: str) -> str:
         """Consume one watch stream; returns the last RV seen.  Raises Gone to force a relist."""

@@ -90,6 +90,70 @@ def symbolize(binary: str, addrs: list[int]) -> dict[int, list[tuple[str, str]]]
     return out
 
 
+_IFUNCS = ("memmove", "memcpy", "memset", "memcmp", "bcmp", "memchr", "strlen", "strcmp", "strchr", "rawmemchr")
+
+
+def exported_spans(lib: str) -> list[tuple[int, int]]:
+    """(start, end) of every exported function of a shared library (`nm -D -S`)."""
+    try:
+        r = subprocess.run(["nm", "-D", "-S", "--defined-only", lib], capture_output=True, text=True, check=True)
+    except (OSError, subprocess.CalledProcessError):
+        return []
+    spans = []
+    for line in r.stdout.splitlines():
+        w = line.split()
+        if len(w) >= 4 and w[2] in ("T", "t", "W", "i"):
+            spans.append((int(w[0], 16), int(w[0], 16) + int(w[1], 16)))
+    return spans
+
+
+def ifunc_bodies(lib: str) -> list[tuple[int, str]]:
+    """(offset in the library's file, name) of the string/memory routines this machine's dynamic linker picked
+    (glibc's IFUNC bodies, e.g. __memmove_avx512_unaligned_erms, are not exported: `nm -D` and addr2line name
+    them after the nearest exported symbol, e.g. `__nss_database_lookup`).  Resolved here with dlsym, so the
+    report must run on the machine the samples came from (scripts/box/run.sh does)."""
+    import ctypes
+    try:
+        h = ctypes.CDLL(lib)
+    except OSError:
+        return []
+    maps = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) > 5 and os.path.realpath(parts[5]) == os.path.realpath(lib):
+                lo, hi = (int(x, 16) for x in parts[0].split("-"))
+                maps.append((lo, hi, int(parts[2], 16)))
+    out = []
+    for name in _IFUNCS:
+        try:
+            addr = ctypes.cast(getattr(h, name), ctypes.c_void_p).value
+        except AttributeError:
+            continue
+        for lo, hi, off in maps:
+            if lo <= addr < hi:
+                out.append((addr - lo + off, name))
+    return sorted(set(out))
+
+
+def relabel_library(path: str, chains: dict) -> None:
+    """Names a library sample outside every exported function after the IFUNC body it falls in (the nearest
+    picked routine below it, within 8 KiB), else `<lib> internal`."""
+    if not os.path.isfile(path):
+        return
+    spans = exported_spans(path)
+    bodies = ifunc_bodies(path) if os.path.basename(path).startswith("libc.") else []
+    for (p, a), chain in chains.items():
+        if p != path or any(lo <= a < hi for lo, hi in spans):
+            continue
+        below = [(o, n) for o, n in bodies if o <= a < o + 0x2000]
+        if below:
+            names = "/".join(n for o, n in bodies if o == max(below)[0])
+            chain[:] = [(f"{names} (IFUNC body)", chain[0][1] if chain else "??:0")]
+        else:
+            chain[:] = [(f"{os.path.basename(path)} internal", chain[0][1] if chain else "??:0")]
+
+
 def report(counts: collections.Counter, binary: str, top: int) -> str:
     total = sum(counts.values())
     if not total:
@@ -106,6 +170,8 @@ def report(counts: collections.Counter, binary: str, top: int) -> str:
         if os.path.isfile(path):
             for a, chain in symbolize(path, sorted(addrs)).items():
                 chains[(path, a)] = chain
+            if os.path.realpath(path) != os.path.realpath(binary):
+                relabel_library(path, chains)
     self_c: collections.Counter = collections.Counter()
     frame_c: collections.Counter = collections.Counter()
     line_c: collections.Counter = collections.Counter()

@@ -468,3 +468,63 @@ def test_native_owner_filter_matches_the_python_filter():
     assert kept == [lines[i] for i in (1, 3, 4, 5, 6, 7)]
     kept, dropped, last = m.owner_filter(lines[:2], items, assumed, "n")
     assert dropped == 1 and last is None and kept == [lines[1]]
+
+
+def test_memoising_owner_filter_matches_owner_filter():
+    """OwnerFilter (the informer's per-store memo) gives owner_filter's result batch after batch while the store's
+    objects are replaced, overlaid and deleted under it; a replaced object is compared by its new owners."""
+    import random
+    from ncc import native
+    m = native.load(required=True)
+    rnd = random.Random(7)
+
+    def line(t, name, owners, rv):
+        md = {"name": name, "namespace": "n", "resourceVersion": str(rv)}
+        if owners is not None:
+            md["ownerReferences"] = [{"apiVersion": "v1", "kind": "T", "name": o, "uid": u} for o, u in owners]
+        return json.dumps({"type": t, "object": {"metadata": md, "data": {"k": "v"}}}).encode()
+
+    owner_sets = [None, [], [("t1", "u1")], [("t1", "u2")], [("t1", "u1"), ("t2", "u2")]]
+    names = [f"o{i}" for i in range(12)]
+    items: dict = {}
+    assumed: dict = {}
+    flt = m.OwnerFilter()
+    rv = 0
+    for _ in range(300):
+        for _ in range(rnd.randint(0, 4)):  # the store changes between batches
+            name = rnd.choice(names)
+            op = rnd.random()
+            if op < 0.5:
+                o = owner_sets[rnd.randrange(len(owner_sets))]
+                md = {"name": name} if o is None else {"name": name, "ownerReferences": [{"name": a, "uid": b}
+                                                                                         for a, b in o]}
+                items[("n", name)] = {"metadata": md}
+            elif op < 0.7:
+                items.pop(("n", name), None)
+            elif op < 0.85:
+                assumed[("n", name)] = None
+            else:
+                assumed.pop(("n", name), None)
+        batch = []
+        for _ in range(rnd.randint(1, 6)):
+            rv += 1
+            batch.append(line(rnd.choice(["MODIFIED", "MODIFIED", "ADDED"]), rnd.choice(names),
+                              owner_sets[rnd.randrange(len(owner_sets))], rv))
+        assert flt(list(batch), items, assumed, "n") == m.owner_filter(list(batch), items, assumed, "n")
+    assert 0 < len(flt) <= len(names)
+    flt.clear()
+    assert len(flt) == 0
+
+
+def test_memoising_owner_filter_keeps_a_bounded_memo():
+    """Deleted keys do not accumulate: the memo is dropped whole once it outgrows the store by 4096 keys."""
+    from ncc import native
+    m = native.load(required=True)
+    flt = m.OwnerFilter()
+    for i in range(5000):
+        key = ("n", f"x{i}")
+        items = {key: {"metadata": {"name": key[1]}}}
+        line = json.dumps({"type": "MODIFIED", "object": {"metadata": {"name": key[1], "resourceVersion": str(i)}}})
+        kept, dropped, last = flt([line.encode()], items, {}, "n")
+        assert dropped == 1 and last == str(i) and kept == []
+    assert len(flt) <= 4098
