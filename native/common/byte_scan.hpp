@@ -95,12 +95,15 @@ inline uint64_t prefix_xor(uint64_t x) {
 // Past the object or array whose bracket is at p; nullptr when unbalanced.  64 bytes per step while a block
 // has no backslash: the in-string mask is the prefix XOR of the quote bits, brackets outside strings move the
 // depth, and only a block where the depth could reach zero has its brackets walked one by one.  A block with
-// a backslash (or a string escape carried into it) is read byte by byte.
-inline const char* skip_container_text(const char* p, const char* e) {
+// a backslash (or a string escape carried into it) is read byte by byte.  The last, short block is copied
+// into a zero-padded one (NUL is no JSON structure), so a container ending near the end of its buffer — a
+// watch line's object, a response body — does not fall back to bytes.
+struct ContainerSkip {
     int depth = 0;
     bool in_str = false, esc = false;
-    while (e - p >= 64) {
-        Block64 b(p);
+    // the `n` bytes of `blk` (64 readable): the offset just past the closing bracket, or -1
+    int block(const char* blk, int n) {
+        Block64 b(blk);
         if (b.backslash == 0 && !esc) {
             uint64_t str = prefix_xor(b.quote) ^ (in_str ? ~0ULL : 0ULL);  // 1 = inside a string (open quote incl.)
             uint64_t op = b.open & ~str, cl = b.close & ~str;
@@ -115,16 +118,15 @@ inline const char* skip_container_text(const char* p, const char* e) {
                     if ((op >> i) & 1) {
                         ++depth;
                     } else if (--depth == 0) {
-                        return p + i + 1;
+                        return i + 1;
                     }
                 }
             }
             in_str = (str >> 63) & 1;
-            p += 64;
-            continue;
+            return -1;
         }
-        for (const char* end = p + 64; p < end; ++p) {
-            char c = *p;
+        for (int i = 0; i < n; ++i) {
+            char c = blk[i];
             if (in_str) {
                 if (esc) {
                     esc = false;
@@ -138,27 +140,25 @@ inline const char* skip_container_text(const char* p, const char* e) {
             } else if ((c | 0x20) == '{') {
                 ++depth;
             } else if ((c | 0x20) == '}') {
-                if (--depth == 0) return p + 1;
+                if (--depth == 0) return i + 1;
             }
         }
+        return -1;
     }
-    for (; p < e; ++p) {
-        char c = *p;
-        if (in_str) {
-            if (esc) {
-                esc = false;
-            } else if (c == '\\') {
-                esc = true;
-            } else if (c == '"') {
-                in_str = false;
-            }
-        } else if (c == '"') {
-            in_str = true;
-        } else if ((c | 0x20) == '{') {
-            ++depth;
-        } else if ((c | 0x20) == '}') {
-            if (--depth == 0) return p + 1;
-        }
+};
+inline const char* skip_container_text(const char* p, const char* e) {
+    ContainerSkip st;
+    while (e - p >= 64) {
+        int r = st.block(p, 64);
+        if (r >= 0) return p + r;
+        p += 64;
+    }
+    if (p < e) {
+        char tail[64] = {};
+        const int n = static_cast<int>(e - p);
+        __builtin_memcpy(tail, p, static_cast<unsigned long>(n));
+        int r = st.block(tail, n);
+        if (r >= 0) return p + r;
     }
     return nullptr;
 }

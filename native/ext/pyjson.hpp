@@ -162,6 +162,10 @@ bool members_equal(py::bytes a, py::bytes b, py::sequence key_seq) {
 // (without managedFields) and status as Python values, the spec reduced to the references the
 // coordinator reads plus a digest of its raw bytes.  A malformed line returns None (callers fall back
 // to json.loads, which raises the proper error).
+// An interned str for a constant key, made once per call site: PyDict_GetItemString / SetItemString would build
+// and hash a new str on every call (a dozen per template line).
+#define PY_CONST_KEY(lit) ([]() -> PyObject* { static PyObject* k_ = PyUnicode_InternFromString(lit); return k_; }())
+
 class PyJson {
   public:
     PyJson(const char* p, size_t n) : p_(p), e_(p + n) {}
@@ -238,8 +242,8 @@ class PyJson {
     void find_prev(PyObject* md) {
         prev_ = nullptr;
         if (items_ == nullptr || md == nullptr || !PyDict_Check(md)) return;
-        PyObject* name = PyDict_GetItemString(md, "name");
-        PyObject* ns = PyDict_GetItemString(md, "namespace");
+        PyObject* name = PyDict_GetItem(md, PY_CONST_KEY("name"));
+        PyObject* ns = PyDict_GetItem(md, PY_CONST_KEY("namespace"));
         if (name == nullptr) return;
         PyObject* nso = nullptr;
         if (ns == nullptr || (PyUnicode_Check(ns) && PyUnicode_GET_LENGTH(ns) == 0)) {
@@ -558,7 +562,7 @@ class PyJson {
             if (!raw_key(key)) break;
             if (key == "name") {
                 PyObject* v = value(8);
-                if (v == nullptr || PyDict_SetItemString(d, "name", v) != 0) {
+                if (v == nullptr || PyDict_SetItem(d, PY_CONST_KEY("name"), v) != 0) {
                     Py_XDECREF(v);
                     break;
                 }
@@ -601,8 +605,7 @@ class PyJson {
                         if (key == "secretRef" || key == "configMapRef") {
                             PyObject* r = name_ref();
                             if (r == nullptr) { ok = false; break; }
-                            int rc = r == Py_None ? 0 : PyDict_SetItemString(item, key == "secretRef" ? "secretRef"
-                                                                                                        : "configMapRef", r);
+                            int rc = r == Py_None ? 0 : PyDict_SetItem(item, key == "secretRef" ? PY_CONST_KEY("secretRef") : PY_CONST_KEY("configMapRef"), r);
                             Py_DECREF(r);
                             if (rc != 0) { ok = false; break; }
                         } else if (!skip_value()) {
@@ -660,14 +663,14 @@ class PyJson {
                                 Py_XDECREF(env);
                                 env = nullptr;
                                 if (prev_ != nullptr) {  // unchanged references: the cached version's list
-                                    PyObject* ps = PyDict_GetItemString(prev_, "spec");
+                                    PyObject* ps = PyDict_GetItem(prev_, PY_CONST_KEY("spec"));
                                     PyObject* prt = ps != nullptr && PyDict_Check(ps)
-                                                        ? PyDict_GetItemString(ps, "runtimeEnvironment") : nullptr;
+                                                        ? PyDict_GetItem(ps, PY_CONST_KEY("runtimeEnvironment")) : nullptr;
                                     PyObject* penv = prt != nullptr && PyDict_Check(prt)
-                                                         ? PyDict_GetItemString(prt, "mappedEnvironmentVariables")
+                                                         ? PyDict_GetItem(prt, PY_CONST_KEY("mappedEnvironmentVariables"))
                                                          : nullptr;
                                     if (penv != nullptr)
-                                        env = reuse_if_same(PyDict_GetItemString(ps, "_rfp"), penv, &env_fp);
+                                        env = reuse_if_same(PyDict_GetItem(ps, PY_CONST_KEY("_rfp")), penv, &env_fp);
                                 }
                                 if (env == nullptr) {
                                     ws();
@@ -707,14 +710,14 @@ class PyJson {
         bool built = spec != nullptr && fp != nullptr;
         if (built && env != nullptr && env != Py_None) {
             PyObject* rt = PyDict_New();
-            built = rt != nullptr && PyDict_SetItemString(rt, "mappedEnvironmentVariables", env) == 0 &&
-                    PyDict_SetItemString(spec, "runtimeEnvironment", rt) == 0;
+            built = rt != nullptr && PyDict_SetItem(rt, PY_CONST_KEY("mappedEnvironmentVariables"), env) == 0 &&
+                    PyDict_SetItem(spec, PY_CONST_KEY("runtimeEnvironment"), rt) == 0;
             Py_XDECREF(rt);
         }
-        if (built) built = PyDict_SetItemString(spec, "_fp", fp) == 0;
+        if (built) built = PyDict_SetItem(spec, PY_CONST_KEY("_fp"), fp) == 0;
         if (built) {  // a digest of the references' text: the coordinator compares it instead of the list
             PyObject* rfp = PyLong_FromUnsignedLongLong(env_fp);
-            built = rfp != nullptr && PyDict_SetItemString(spec, "_rfp", rfp) == 0;
+            built = rfp != nullptr && PyDict_SetItem(spec, PY_CONST_KEY("_rfp"), rfp) == 0;
             Py_XDECREF(rfp);
         }
         Py_XDECREF(env);
@@ -748,8 +751,8 @@ class PyJson {
                 uint64_t fp = 0;
                 v = nullptr;
                 if (prev_ != nullptr) {
-                    PyObject* pst = PyDict_GetItemString(prev_, "status");
-                    if (pst != nullptr) v = reuse_if_same(PyDict_GetItemString(prev_, "__ncc_sfp__"), pst, &fp);
+                    PyObject* pst = PyDict_GetItem(prev_, PY_CONST_KEY("status"));
+                    if (pst != nullptr) v = reuse_if_same(PyDict_GetItem(prev_, PY_CONST_KEY("__ncc_sfp__")), pst, &fp);
                 }
                 if (v == nullptr) {
                     ws();
@@ -763,7 +766,7 @@ class PyJson {
                 }
                 if (v != nullptr) {
                     PyObject* sfp = PyLong_FromUnsignedLongLong(fp);
-                    if (sfp == nullptr || PyDict_SetItemString(d, "__ncc_sfp__", sfp) != 0) {
+                    if (sfp == nullptr || PyDict_SetItem(d, PY_CONST_KEY("__ncc_sfp__"), sfp) != 0) {
                         Py_XDECREF(sfp);
                         Py_DECREF(v);
                         break;

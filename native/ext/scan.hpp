@@ -602,6 +602,85 @@ py::list relay_index(py::list lines, py::dict raw, const std::string& default_ns
     return keep;
 }
 
+// RelayIndex()(lines, raw, default_ns): relay_index with a memo of the (namespace, name) key tuples, so a line
+// of a key seen before builds no Python object: one scan, one C++ lookup, one dict store.  The memo forgets a
+// key on its DELETED line, and is dropped whole when it outgrows `raw` by 4096 keys.
+class RelayIndex {
+  public:
+    RelayIndex() = default;
+    RelayIndex(const RelayIndex&) = delete;
+    RelayIndex& operator=(const RelayIndex&) = delete;
+    ~RelayIndex() { clear(); }
+
+    void clear() {
+        for (auto& kv : memo_) Py_XDECREF(kv.second);
+        memo_.clear();
+    }
+    size_t size() const { return memo_.size(); }
+
+    py::list call(py::list lines, py::dict raw, const std::string& default_ns) {
+        py::list keep;
+        PyObject* rd = raw.ptr();
+        const Py_ssize_t n = PyList_GET_SIZE(lines.ptr());
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject* line = PyList_GET_ITEM(lines.ptr(), i);
+            char* buf = nullptr;
+            Py_ssize_t len = 0;
+            if (PyBytes_AsStringAndSize(line, &buf, &len) != 0) throw py::error_already_set();
+            std::string_view type, ns, name, rv;
+            Scanner sc(buf, static_cast<size_t>(len));
+            if (!sc.scan(type, ns, name, rv)) continue;
+            int code = type == "ADDED" ? 0 : type == "MODIFIED" ? 1 : type == "DELETED" ? 2 : 3;
+            if (code == 3) continue;
+            std::string_view kns = ns.empty() ? std::string_view(default_ns) : ns;
+            kbuf_.assign(kns.data(), kns.size());
+            kbuf_ += '\0';
+            kbuf_.append(name.data(), name.size());
+            PyObject* key = nullptr;
+            auto it = memo_.find(kbuf_);
+            if (it != memo_.end()) {
+                key = it->second;
+            } else {
+                PyObject* kn = PyUnicode_DecodeUTF8(kns.data(), static_cast<Py_ssize_t>(kns.size()), nullptr);
+                PyObject* nm = kn == nullptr ? nullptr : PyUnicode_DecodeUTF8(name.data(), static_cast<Py_ssize_t>(name.size()), nullptr);
+                if (nm == nullptr) {  // not UTF-8: forwarded for the executor to judge, not indexed
+                    Py_XDECREF(kn);
+                    PyErr_Clear();
+                    if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
+                    continue;
+                }
+                key = PyTuple_Pack(2, kn, nm);
+                Py_DECREF(kn);
+                Py_DECREF(nm);
+                if (key == nullptr) throw py::error_already_set();
+                if (code != 2) {
+                    if (memo_.size() > static_cast<size_t>(PyDict_GET_SIZE(rd)) + 4096) clear();
+                    it = memo_.emplace(kbuf_, key).first;  // the memo owns the reference PyTuple_Pack gave
+                }
+            }
+            if (code == 2) {
+                int rc = PyDict_DelItem(rd, key);
+                if (it != memo_.end()) {
+                    memo_.erase(it);
+                }
+                Py_DECREF(key);  // the memo's reference, or the one PyTuple_Pack gave
+                if (rc != 0) {
+                    if (!PyErr_ExceptionMatches(PyExc_KeyError)) throw py::error_already_set();
+                    PyErr_Clear();
+                }
+            } else if (PyDict_SetItem(rd, key, line) != 0) {
+                throw py::error_already_set();
+            }
+            if (PyList_Append(keep.ptr(), line) != 0) throw py::error_already_set();
+        }
+        return keep;
+    }
+
+  private:
+    std::unordered_map<std::string, PyObject*> memo_;  // "namespace\0name" -> (namespace, name), a strong reference
+    std::string kbuf_;
+};
+
 py::int_ key_partition(const std::string& ns, const std::string& name, int parts) {
     if (parts < 1) throw py::value_error("key_partition: parts must be >= 1");
     return py::int_(key_crc(ns, name) % static_cast<uint32_t>(parts));

@@ -31,7 +31,8 @@
 //  — the product extension carries no server code.
 //  * owner_filter(lines, items, assumed, ns) — the metadata-only informer's owner filter over a batch;
 //    OwnerFilter — the same with a memo per informer (no Python object built for a dropped line).
-//  * relay_index(lines, raw, ns) — the one-partition watch relay's index-and-forward loop.
+//  * relay_index(lines, raw, ns) — the one-partition watch relay's index-and-forward loop; RelayIndex — the
+//    same with a memo of the key tuples.
 //  * chunk_lines(bytearray, state, bytearray) — a chunked watch body cut into its event lines in one call.
 //  * scan_object(bytes) — namespace/name/resourceVersion/uid of a write response, so a slim-cache
 //    writer can publish its write without decoding the echoed object.
@@ -69,7 +70,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 29
+#define NCC_NATIVE_ABI 30
 
 namespace {
 #include "ext/hashing.hpp"
@@ -109,6 +110,12 @@ PYBIND11_MODULE(_native, m) {
         .def("__len__", &OwnerFilter::size);
     m.def("relay_index", &relay_index, py::arg("lines"), py::arg("raw"), py::arg("default_ns"),
           "the one-partition relay loop: index the lines in `raw`, return the object events to forward");
+    py::class_<RelayIndex>(m, "RelayIndex")
+        .def(py::init<>())
+        .def("__call__", &RelayIndex::call, py::arg("lines"), py::arg("raw"), py::arg("default_ns"),
+             "relay_index over a batch, memoising the key tuples")
+        .def("clear", &RelayIndex::clear)
+        .def("__len__", &RelayIndex::size);
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
           "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");

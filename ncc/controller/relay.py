@@ -138,6 +138,7 @@ class WatchRelay:
         self.template_store = template_store
         self.raw: list[dict] = [{} for _ in KINDS]  # (ns, name) -> latest line of the object
         self._listing: dict[int, dict] = {}  # kind -> lines of a listing still arriving page by page
+        self._index: list = [None] * len(KINDS)  # per kind, the native one-partition index loop (RelayIndex)
         self.synced = [False] * len(KINDS)
         self.handles: list = []
         self.parts = 1
@@ -261,7 +262,10 @@ class WatchRelay:
                     self.trace.append((kind, sc[1], sc[2], now))
         if parts <= 1:
             # index + forward in one native call; BOOKMARK / ERROR: the coordinator's informer handles those
-            keep = mod.relay_index(lines if type(lines) is list else list(lines), raw, ns)
+            index = self._index[kind]
+            if index is None:
+                index = self._index[kind] = mod.RelayIndex() if hasattr(mod, "RelayIndex") else mod.relay_index
+            keep = index(lines if type(lines) is list else list(lines), raw, ns)
             if keep:
                 self._send_all(handles, {"t": "w", "k": kind, "l": keep})
                 self.stats["lines_out"] += len(keep) * len(handles)

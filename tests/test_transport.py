@@ -273,6 +273,8 @@ def test_native_parsers_survive_arbitrary_bytes():
     good_line = (b'{"type":"MODIFIED","object":{"metadata":{"name":"s","namespace":"n","resourceVersion":"7",'
                  b'"ownerReferences":[{"name":"t","uid":"u"}]}}}')
 
+    flt, idx = m.OwnerFilter(), m.RelayIndex()  # their memos persist across the examples
+
     @settings(max_examples=300, deadline=None)
     @given(st.binary(max_size=200), st.integers(0, 200))
     def check(blob, cut):
@@ -290,6 +292,9 @@ def test_native_parsers_survive_arbitrary_bytes():
             kept, dropped, _ = m.owner_filter([data], {("n", "s"): {"metadata": {"ownerReferences": []}}}, {}, "n")
             assert len(kept) + dropped == 1
             assert m.relay_index([data], {}, "n") in ([], [data])
+            kept, dropped, _ = flt([data], {("n", "s"): {"metadata": {"ownerReferences": []}}}, {}, "n")
+            assert len(kept) + dropped == 1
+            assert idx([data], {}, "n") in ([], [data])
             try:  # undecodable text (not UTF-8) raises ValueError, as json.loads does
                 m.template_event_slim(data, {("n", "s"): {"status": {}, "__ncc_sfp__": 1}}, "n")
             except ValueError:
@@ -528,3 +533,30 @@ def test_memoising_owner_filter_keeps_a_bounded_memo():
         kept, dropped, last = flt([line.encode()], items, {}, "n")
         assert dropped == 1 and last == str(i) and kept == []
     assert len(flt) <= 4098
+
+
+def test_memoising_relay_index_matches_relay_index():
+    """RelayIndex (the relay's per-kind memo of key tuples) indexes and forwards exactly as relay_index, batch
+    after batch, through deletes, re-creates and a `raw` dict swapped for a relist."""
+    import random
+    from ncc import native
+    m = native.load(required=True)
+    rnd = random.Random(11)
+    names = [f"o{i}" for i in range(10)] + ["é"]
+    idx = m.RelayIndex()
+    raw_a: dict = {}
+    raw_b: dict = {}
+    for step in range(400):
+        batch = []
+        for _ in range(rnd.randint(1, 6)):
+            t = rnd.choice(["ADDED", "MODIFIED", "MODIFIED", "DELETED", "BOOKMARK"])
+            ns = rnd.choice(["", "n"])
+            batch.append(json.dumps({"type": t, "object": {"metadata": {"name": rnd.choice(names), "namespace": ns,
+                                                                        "resourceVersion": str(step)}}}).encode())
+        if rnd.random() < 0.05:
+            batch.append(b"not json")
+        assert idx(list(batch), raw_a, "dflt") == m.relay_index(list(batch), raw_b, "dflt")
+        assert raw_a == raw_b
+        if step == 200:  # a relist swaps the dict
+            raw_a, raw_b = dict(raw_a), dict(raw_b)
+    assert len(idx) <= len(names) * 2
