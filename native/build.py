@@ -99,24 +99,41 @@ def tool_path(name: str = "ncc-h2probe") -> str:
     return os.path.join(ROOT, "build", "tools", name)
 
 
-def build_tools(verbose: bool = False) -> str:
-    """ncc-h2probe (native/tools/h2probe.cpp): the executor's HTTP client (native/executor/http.hpp) driven from
-    stdin, for tests against scripted and independent HTTP/2 servers.  Test-only; not part of the product."""
-    out = tool_path()
-    src = os.path.join(TOOLS_DIR, "h2probe.cpp")
+TOOLS = {  # test-only programs (build/tools/): name -> (source, extra flags, libraries)
+    "ncc-h2probe": ("h2probe.cpp", ["-fcoroutines", "-DNCC_SYSTEM_MALLOC"], ["-lssl", "-lcrypto"]),
+    "ncc-strmap-check": ("strmap_check.cpp", [], []),
+}
+
+
+def build_tool(name: str, verbose: bool = False) -> str:
+    """One test tool of TOOLS, rebuilt when it or an executor header changed."""
+    source, flags, libs = TOOLS[name]
+    out = tool_path(name)
+    src = os.path.join(TOOLS_DIR, source)
     deps = [src] + [os.path.join(EXECUTOR_DIR, f) for f in os.listdir(EXECUTOR_DIR) if f.endswith(".hpp")]
     if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps + COMMON_HEADERS):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
     tmp = out + ".tmp"
-    cmd = [cxx, "-std=c++20", "-fcoroutines", *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", "-O1",
-           "-DNCC_SYSTEM_MALLOC", *_werror(), src, "-o", tmp, "-lssl", "-lcrypto"]
+    cmd = [cxx, "-std=c++20", *flags, *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", "-O1",
+           *_werror(), src, "-o", tmp, *libs]
     if verbose:
         print(" ".join(shlex.quote(c) for c in cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
     return out
+
+
+def build_tools(verbose: bool = False) -> str:
+    """The test tools: ncc-h2probe (native/tools/h2probe.cpp: the executor's HTTP client, native/executor/http.hpp,
+    driven from stdin, for tests against scripted and independent HTTP/2 servers) and ncc-strmap-check (the
+    executor's open-addressing map against std::unordered_map).  Test-only; not part of the product.  Returns
+    ncc-h2probe's path."""
+    for name in TOOLS:
+        if name != "ncc-h2probe":
+            build_tool(name, verbose)
+    return build_tool("ncc-h2probe", verbose)
 
 
 def build(debug: bool = False, sanitize: bool = False, verbose: bool = False, substrate: bool = True) -> str:

@@ -68,6 +68,7 @@ extern "C" void __gcov_dump(void);
 #include "json.hpp"
 #include "loop.hpp"
 #include "msgpack.hpp"
+#include "strmap.hpp"
 
 namespace ncc {
 
@@ -1086,7 +1087,7 @@ static Executor* g_ex = nullptr;
 struct Informer {
     Shard* shard = nullptr;
     int kind = 0;
-    std::unordered_map<std::string, ShardPtr> store;
+    StrMap<ShardPtr> store;
     bool synced = false;
     bool watching = false;   // a watch request is open (status reports)
     std::string last_error;  // the last list/watch failure, "" once a watch succeeds again
@@ -1104,7 +1105,7 @@ struct Shard {
     std::string name;
     std::unique_ptr<Client> client;
     Informer inf[4];
-    std::unordered_map<std::string, Memo> memo[4];
+    StrMap<Memo> memo[4];
     Event answering;  // set when a write or read was answered (< 500): reflectors in an outage backoff retry
     bool synced() const {
         for (const auto& i : inf)
@@ -1231,10 +1232,10 @@ static void on_ctl_event(int kind, const CtlPtr& old, const CtlPtr& cur, bool de
 
 struct Executor {
     std::vector<std::unique_ptr<Shard>> shards;
-    std::unordered_map<std::string, CtlPtr> ctl[4];
+    StrMap<CtlPtr> ctl[4];
     bool ctl_synced[4] = {false, false, false, false};
     Event ctl_synced_ev;
-    std::unordered_map<std::string, std::set<std::string>> refs[2];  // dep key -> template keys (secret, configmap)
+    StrMap<std::set<std::string>> refs[2];  // dep key -> template keys (secret, configmap)
     std::unordered_set<std::string> pending_deletes[2];              // templates, workgroups
     WorkQueue queue;
     Event gate;
@@ -1334,7 +1335,7 @@ static void ctl_apply(int kind, const std::string& type, CtlPtr cur) {
 static void ctl_snapshot(int kind, std::vector<CtlPtr> objs) {
     Executor& ex = *g_ex;
     auto& store = ex.ctl[kind];
-    std::unordered_map<std::string, CtlPtr> fresh;
+    StrMap<CtlPtr> fresh;
     for (auto& c : objs) fresh[key_of(c->ns, c->name)] = c;
     bool was_synced = ex.ctl_synced[kind];
     std::vector<std::pair<CtlPtr, CtlPtr>> changes;  // (old, new); new null = deleted
@@ -1694,7 +1695,7 @@ static void shard_apply_line(Shard& sh, int kind, const std::string& line) {
 
 static Task<void> shard_list(Shard& sh, int kind, std::string list_rv) {
     Informer& inf = sh.inf[kind];
-    std::unordered_map<std::string, ShardPtr> fresh;
+    StrMap<ShardPtr> fresh;
     std::string token, rv;
     bool first = true;
     while (true) {
