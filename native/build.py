@@ -105,18 +105,21 @@ TOOLS = {  # test-only programs (build/tools/): name -> (source, extra flags, li
 }
 
 
-def build_tool(name: str, verbose: bool = False) -> str:
-    """One test tool of TOOLS, rebuilt when it or an executor header changed."""
+def build_tool(name: str, verbose: bool = False, coverage: bool = False, force: bool = False) -> str:
+    """One test tool of TOOLS, rebuilt when it or an executor header changed (`coverage`: gcov-instrumented,
+    for scripts/cpp_coverage.py; `force`: rebuilt regardless, e.g. to put the plain build back)."""
     source, flags, libs = TOOLS[name]
     out = tool_path(name)
     src = os.path.join(TOOLS_DIR, source)
     deps = [src] + [os.path.join(EXECUTOR_DIR, f) for f in os.listdir(EXECUTOR_DIR) if f.endswith(".hpp")]
-    if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps + COMMON_HEADERS):
+    if not (coverage or force) and os.path.exists(out) and \
+            all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps + COMMON_HEADERS):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
     tmp = out + ".tmp"
-    cmd = [cxx, "-std=c++20", *flags, *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", "-O1",
+    opt = ["-g", "-O0", "--coverage", "-DNCC_COVERAGE"] if coverage else ["-O1"]
+    cmd = [cxx, "-std=c++20", *flags, *arch_flags(), "-Wall", "-Wextra", "-Wno-unused-parameter", *opt,
            *_werror(), src, "-o", tmp, *libs]
     if verbose:
         print(" ".join(shlex.quote(c) for c in cmd))

@@ -11,6 +11,9 @@
 //   SLEEP MS
 // Output: one JSON line per request as it completes ({"i", "status", "bytes", "ms"} or {"i", "error", "ms"}),
 // then {"stats": {...}, "notices": [...]} — the client's HTTP/2 counters and what it would log as Warnings.
+#ifdef NCC_COVERAGE
+extern "C" void __gcov_dump(void);
+#endif
 #include <csignal>
 #include <cstdio>
 #include <iostream>
@@ -137,5 +140,8 @@ int main(int argc, char** argv) {
     spawn(p.main(std::move(steps)), "probe");
     lp.run();
     std::fflush(stdout);
+#ifdef NCC_COVERAGE
+    __gcov_dump();  // coverage builds (scripts/cpp_coverage.py): the counters, before skipping the exit handlers
+#endif
     std::_Exit(0);  // skip destructors of still-suspended coroutines
 }

@@ -28,9 +28,10 @@ SRC = os.path.join(ROOT, "native", "executor")
 _LINE = re.compile(r"^\s*([^:]+):\s*(\d+):(.*)$")
 
 
-def parse_gcov(path: str) -> tuple[str, int, int, list[int]]:
-    """(source, executable lines, executed lines, unexecuted line numbers) of one .gcov file."""
-    source, total, hit, missing = "", 0, 0, []
+def line_sets(path: str) -> tuple[str, set, set]:
+    """(source, executable line numbers, executed line numbers) of one .gcov file; a line of a template counts as
+    executed when any of its instantiations ran."""
+    source, exe, hit = "", set(), set()
     with open(path, errors="replace") as f:
         for raw in f:
             m = _LINE.match(raw)
@@ -43,12 +44,10 @@ def parse_gcov(path: str) -> tuple[str, int, int, list[int]]:
                 continue
             if count == "-":
                 continue
-            total += 1
-            if count.startswith("#####") or count.startswith("====="):
-                missing.append(lineno)
-            else:
-                hit += 1
-    return source, total, hit, missing
+            exe.add(lineno)
+            if not (count.startswith("#####") or count.startswith("=====")):
+                hit.add(lineno)
+    return source, exe, hit
 
 
 def ranges(nums: list[int]) -> str:
@@ -78,9 +77,14 @@ def main(argv=None) -> int:
     sys.path.insert(0, os.path.join(ROOT, "native"))
     import build as native_build  # native/build.py
 
-    for f in glob.glob(os.path.join(BIN, "*.gcda")) + glob.glob(os.path.join(BIN, "*.gcno")):
+    tools = os.path.dirname(native_build.tool_path())
+    for f in glob.glob(os.path.join(BIN, "*.gcda")) + glob.glob(os.path.join(BIN, "*.gcno")) + \
+            glob.glob(os.path.join(tools, "*.gcda")) + glob.glob(os.path.join(tools, "*.gcno")):
         os.remove(f)
     native_build.build_executor(coverage=True, verbose=True)
+    # the executor's HTTP/2 client also runs inside the test tool ncc-h2probe (the RFC 9113 error-code and
+    # interop tests drive it): instrumented too, and its counts merged per source line
+    native_build.build_tool("ncc-h2probe", verbose=True, coverage=True)
     env = dict(os.environ, NCC_SKIP_NATIVE_BUILD="1")
     env.pop("NCC_EXECUTOR_IMPL", None)
     rc = subprocess.call([sys.executable, "-m", "pytest", *a.pytest_args], cwd=ROOT, env=env)
@@ -94,15 +98,25 @@ def main(argv=None) -> int:
         if not gcda:
             print("no .gcda counters were written: did any test run the C++ executor?", file=sys.stderr)
             return 1
-        work = os.path.join(BIN, "gcov")
-        os.makedirs(work, exist_ok=True)
-        subprocess.run(["gcov", "-p", "-o", BIN, *gcda], cwd=work, check=True, stdout=subprocess.DEVNULL)
-        rows = []
-        for g in sorted(glob.glob(os.path.join(work, "*.gcov"))):
-            source, total, hit, missing = parse_gcov(g)
-            if not source.startswith(SRC) and not os.path.join(ROOT, source).startswith(SRC):
+        merged: dict = {}  # source -> (executable lines, executed lines), over the executor and the tool
+        for obj_dir, counters in ((BIN, gcda), (tools, glob.glob(os.path.join(tools, "*.gcda")))):
+            if not counters:
                 continue
-            rows.append((os.path.relpath(os.path.join(ROOT, source), ROOT), total, hit, missing))
+            work = os.path.join(obj_dir, "gcov")
+            os.makedirs(work, exist_ok=True)
+            subprocess.run(["gcov", "-p", "-o", obj_dir, *counters], cwd=work, check=True, stdout=subprocess.DEVNULL)
+            for g in sorted(glob.glob(os.path.join(work, "*.gcov"))):
+                source, exe, hit = line_sets(g)
+                full = os.path.normpath(source if os.path.isabs(source) else os.path.join(ROOT, source))
+                if not full.startswith(SRC):
+                    continue
+                e0, h0 = merged.setdefault(os.path.relpath(full, ROOT), (set(), set()))
+                e0 |= exe
+                h0 |= hit
+        rows = []
+        for name in sorted(merged):
+            exe, hit = merged[name]
+            rows.append((name, len(exe), len(exe & hit), sorted(exe - hit)))
         report.append(f"{'file':<36} {'lines':>7} {'hit':>7} {'cover':>7}")
         gate = None
         for name, total, hit, missing in rows:
@@ -135,10 +149,13 @@ def main(argv=None) -> int:
     finally:
         if not a.keep_build:
             import shutil
-            for f in glob.glob(os.path.join(BIN, "*.gcda")) + glob.glob(os.path.join(BIN, "*.gcno")):
+            for f in glob.glob(os.path.join(BIN, "*.gcda")) + glob.glob(os.path.join(BIN, "*.gcno")) + \
+                    glob.glob(os.path.join(tools, "*.gcda")) + glob.glob(os.path.join(tools, "*.gcno")):
                 os.remove(f)
             shutil.rmtree(os.path.join(BIN, "gcov"), ignore_errors=True)
+            shutil.rmtree(os.path.join(tools, "gcov"), ignore_errors=True)
             native_build.build_executor()  # the release build back in place
+            native_build.build_tool("ncc-h2probe", force=True)
     return 0 if ok else 1
 
 

@@ -11,7 +11,10 @@ the same header):
 * WINDOW_UPDATE of 0, and one pushing a window past 2^31-1: a stream error (RST_STREAM PROTOCOL_ERROR /
   FLOW_CONTROL_ERROR) on a stream, a connection error (GOAWAY with that code, then close) on the connection;
 * a server whose SETTINGS_HEADER_TABLE_SIZE is 0 (it limits *our* encoder) and which indexes its response fields
-  in its own 4096-byte table: both decoders keep that table.
+  in its own 4096-byte table: both decoders keep that table (ADVICE r5, medium);
+* framing: padded HEADERS/DATA and PRIORITY fields, a header block split over CONTINUATION frames are read; a pad
+  length past its frame, a header block interrupted by another frame, and a CONTINUATION without HEADERS are
+  connection errors (GOAWAY PROTOCOL_ERROR, then a new connection).
 
 Reference behaviour being matched: client-go's HTTP/2 transport (Go's x/net/http2), /root/reference/main.go:52-68.
 """
@@ -171,6 +174,20 @@ class Scripted:
                         writer.write(_frame(8, 0, sid, (0x7FFFFFFF).to_bytes(4, "big")))
                     elif action == "winmax_conn":
                         writer.write(_frame(8, 0, 0, (0x7FFFFFFF).to_bytes(4, "big")))
+                    elif action == "padded":  # HEADERS with PADDED + PRIORITY, DATA with PADDED: legal framing
+                        hdr = b"\x03" + b"\x00\x00\x00\x00\x10" + b"\x88" + b"\x00" * 3
+                        data = b"\x05" + OK_BODY + b"\x00" * 5
+                        writer.write(_frame(1, 0x4 | 0x8 | 0x20, sid, hdr) + _frame(0, 0x1 | 0x8, sid, data))
+                    elif action == "continuation":  # a header block split over HEADERS + CONTINUATION
+                        block = b"\x88" + b"\x40\x06x-test\x03abc"
+                        writer.write(_frame(1, 0, sid, block[:4]) + _frame(9, 0, sid, block[4:9]) +
+                                     _frame(9, 0x4, sid, block[9:]) + _frame(0, 0x1, sid, OK_BODY))
+                    elif action == "bad_padding":  # a pad length past the frame: PROTOCOL_ERROR (RFC 9113 6.1)
+                        writer.write(_frame(1, 0x4, sid, b"\x88") + _frame(0, 0x1 | 0x8, sid, b"\x40" + OK_BODY))
+                    elif action == "interrupted":  # a header block interrupted by another frame (RFC 9113 6.10)
+                        writer.write(_frame(1, 0, sid, b"\x88") + _frame(0, 0x1, sid, OK_BODY))
+                    elif action == "lone_continuation":  # CONTINUATION without HEADERS
+                        writer.write(_frame(9, 0x4, sid, b"\x88"))
                     elif action == "indexed":
                         # our fields indexed in the server's own (4096-byte) dynamic table, whatever
                         # SETTINGS_HEADER_TABLE_SIZE the client sent or we sent
@@ -318,4 +335,32 @@ async def test_pool_falls_back_per_connection_after_speaking_http2():
         assert [(r[1], r[2]) for r in srv.of("req")][-1] == ("http/1.1", "/b")
     finally:
         pool.close()
+        await srv.stop()
+
+
+@pytest.mark.parametrize("client", sorted(CLIENTS))
+@pytest.mark.parametrize("action", ["padded", "continuation"])
+async def test_legal_framing_variants_are_read(client, action):
+    srv = Scripted({"/f": [action]})
+    url = await srv.start()
+    try:
+        res, stats = await CLIENTS[client](url, ["/f", "/after"])
+        assert [r.get("status") for r in res] == [200, 200], res
+        assert not srv.of("goaway") and not srv.of("rst"), srv.seen
+        assert len(srv.of("req")) == 2  # nothing re-sent
+    finally:
+        await srv.stop()
+
+
+@pytest.mark.parametrize("client", sorted(CLIENTS))
+@pytest.mark.parametrize("action", ["bad_padding", "interrupted", "lone_continuation"])
+async def test_framing_violations_are_connection_errors(client, action):
+    srv = Scripted({"/f": [action]})
+    url = await srv.start()
+    try:
+        res, stats = await CLIENTS[client](url, ["/f", "/after"])
+        goaways = srv.of("goaway")
+        assert goaways and goaways[0][2] == 1, srv.seen  # GOAWAY(PROTOCOL_ERROR) before the close
+        assert res[-1].get("status") == 200  # a new connection serves what follows
+    finally:
         await srv.stop()
