@@ -270,6 +270,8 @@ class Informer:
         if self.key_filter is not None or self.owner_filter is not None:
             items = [o for o in items if self._wanted(o.get("metadata") or {})]
         self._stash.clear()  # the relist is newer than anything parked
+        if self._owner_memo is not None:
+            self._owner_memo.clear()  # it holds the versions it compared against: not past a relist
         added, updated, deleted = self.store.replace(items, transformed=transformed)
         self.relists += 1
         synced_before = self.has_synced()

@@ -220,6 +220,9 @@ class WatchRelay:
             self.raw[kind] = self._listing.pop(kind, {})
         else:
             self.raw[kind] = {((meta(o).get("namespace") or ns), meta(o).get("name", "")): _line_of(o) for o in items}
+        index = self._index[kind]
+        if index is not None and hasattr(index, "clear"):
+            index.clear()  # its key tuples are the old dict's: let them go with it (relist-storm peak)
         self.synced[kind] = True
         self._send_snapshot(kind, self.handles)
 
