@@ -54,12 +54,15 @@ def executor_path() -> str:
 
 
 def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = False, out: str | None = None,
-                   coverage: bool = False) -> str:
+                   coverage: bool = False, profile: bool = False) -> str:
     """The native shard executor (one translation unit; headers alongside); `out` overrides the in-tree
     path (setup.py builds it into the wheel's ncc/bin/).  `coverage`: gcov instrumentation (the executor
-    flushes its counters on exit; scripts/cpp_coverage.py gates the line coverage)."""
-    out = out or executor_path()
-    flavor = "coverage" if coverage else ("sanitize" if sanitize else ("debug" if debug else "release"))
+    flushes its counters on exit; scripts/cpp_coverage.py gates the line coverage).  `profile`: the release
+    build with frame pointers, so the sampling profiler (NCC_SAMPLE_PROFILE) records call stacks
+    (profile_executor_path(); scripts/box/run.sh `sample` runs it)."""
+    out = out or (profile_executor_path() if profile else executor_path())
+    flavor = "coverage" if coverage else ("sanitize" if sanitize else ("debug" if debug else
+                                                                      ("profile" if profile else "release")))
     stamp = out + ".flavor"
     sources = [os.path.join(EXECUTOR_DIR, f) for f in sorted(os.listdir(EXECUTOR_DIR))
                if f.endswith((".cpp", ".hpp"))]
@@ -77,6 +80,8 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
         flags += ["-O1", "-fno-omit-frame-pointer"]
     else:
         flags += ["-O2", "-DNDEBUG"]
+    if profile:
+        flags += ["-fno-omit-frame-pointer", "-mno-omit-leaf-frame-pointer", "-DNCC_FRAME_POINTERS"]
     if sanitize:
         # ASan must see every heap allocation: keep malloc instead of the executor's pool allocator
         flags += ["-fsanitize=address,undefined", "-DNCC_SYSTEM_MALLOC"]
@@ -92,6 +97,11 @@ def build_executor(debug: bool = False, sanitize: bool = False, verbose: bool = 
 
 
 TOOLS_DIR = os.path.join(HERE, "tools")
+
+
+def profile_executor_path() -> str:
+    """The frame-pointer build of the executor for sampling profiles (build/, git-ignored; never shipped)."""
+    return os.path.join(ROOT, "build", "profile", "ncc-executor")
 
 
 def tool_path(name: str = "ncc-h2probe") -> str:
@@ -220,4 +230,8 @@ if __name__ == "__main__":
             print(build_tools(verbose=True))
         except (subprocess.CalledProcessError, OSError) as e:  # a test tool: its tests skip without it
             print(f"warning: build/tools/ncc-h2probe was not built ({e})", file=sys.stderr)
+        try:  # the frame-pointer executor for sampling profiles (scripts/box/run.sh sample)
+            print(build_executor(profile=True))
+        except (subprocess.CalledProcessError, OSError) as e:
+            print(f"warning: the profiling executor was not built ({e})", file=sys.stderr)
     sys.exit(0)

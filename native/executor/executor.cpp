@@ -35,6 +35,7 @@
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <ucontext.h>
+#include <pthread.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -1161,16 +1162,35 @@ static void dump_trace() {
 // inlined code correctly; time in the kernel lands on the libc system-call wrapper that entered it.
 // Each sample also keeps the word at the top of the stack: in a frameless leaf (memcpy, a system-call
 // wrapper) that is the return address, i.e. the caller.
-static constexpr size_t kMaxSamples = 1 << 20;
-static uintptr_t* g_samples = nullptr;  // pairs: pc, top-of-stack word
+// Each sample: the interrupted pc, the word on top of the stack (a leaf's return address: who called a libc
+// routine), and — in the frame-pointer build (native/build.py profile flavor, NCC_FRAME_POINTERS) — the return
+// addresses of up to kWalk frames up the rbp chain, 0 past its end.  Without frame pointers rbp is an ordinary
+// register, so the release build records no chain.
+static constexpr size_t kMaxSamples = 1 << 18;
+static constexpr size_t kWalk = 6;
+static constexpr size_t kWords = 2 + kWalk;
+static uintptr_t* g_samples = nullptr;
 static volatile size_t g_nsamples = 0;
+static uintptr_t g_stack_lo = 0, g_stack_hi = 0;  // the main thread's stack: the only memory the walk reads
 #if defined(__x86_64__)
 static void on_sigprof(int, siginfo_t*, void* ucv) {
     auto* uc = static_cast<ucontext_t*>(ucv);
     size_t n = g_nsamples;
     if (n < kMaxSamples) {
-        g_samples[2 * n] = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
-        g_samples[2 * n + 1] = *reinterpret_cast<const uintptr_t*>(uc->uc_mcontext.gregs[REG_RSP]);
+        uintptr_t* out = g_samples + kWords * n;
+        out[0] = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
+        out[1] = *reinterpret_cast<const uintptr_t*>(uc->uc_mcontext.gregs[REG_RSP]);
+        for (size_t k = 0; k < kWalk; ++k) out[2 + k] = 0;
+#ifdef NCC_FRAME_POINTERS
+        uintptr_t fp = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RBP]);
+        for (size_t k = 0; k < kWalk; ++k) {
+            if (fp < g_stack_lo || fp + 16 > g_stack_hi || (fp & 7) != 0) break;
+            const uintptr_t* f = reinterpret_cast<const uintptr_t*>(fp);
+            out[2 + k] = f[1];
+            if (f[0] <= fp) break;  // the chain only goes up the stack
+            fp = f[0];
+        }
+#endif
         g_nsamples = n + 1;
     }
 }
@@ -1181,7 +1201,17 @@ static void start_sampling() {
     LOG_WARN("NCC_SAMPLE_PROFILE: the sampling profiler reads x86_64 registers; not available on this build");
     return;
 #else
-    g_samples = new uintptr_t[2 * kMaxSamples];
+    g_samples = new uintptr_t[kWords * kMaxSamples];
+    pthread_attr_t attr;
+    if (pthread_getattr_np(pthread_self(), &attr) == 0) {
+        void* lo = nullptr;
+        size_t size = 0;
+        if (pthread_attr_getstack(&attr, &lo, &size) == 0) {
+            g_stack_lo = reinterpret_cast<uintptr_t>(lo);
+            g_stack_hi = g_stack_lo + size;
+        }
+        pthread_attr_destroy(&attr);
+    }
     struct sigaction sa {};
     sa.sa_sigaction = on_sigprof;
     sa.sa_flags = SA_SIGINFO | SA_RESTART;
@@ -1212,8 +1242,12 @@ static void dump_samples() {
             if (std::strstr(line, " r-xp ") != nullptr) std::fprintf(f, "# map %s", line);
         std::fclose(maps);
     }
-    for (size_t i = 0; i < g_nsamples; ++i)
-        std::fprintf(f, "%zx %zx\n", static_cast<size_t>(g_samples[2 * i]), static_cast<size_t>(g_samples[2 * i + 1]));
+    for (size_t i = 0; i < g_nsamples; ++i) {
+        const uintptr_t* w = g_samples + kWords * i;
+        std::fprintf(f, "%zx %zx", static_cast<size_t>(w[0]), static_cast<size_t>(w[1]));
+        for (size_t k = 0; k < kWalk && w[2 + k] != 0; ++k) std::fprintf(f, " %zx", static_cast<size_t>(w[2 + k]));
+        std::fputc('\n', f);
+    }
     std::fclose(f);
 }
 

@@ -123,10 +123,14 @@ case "$what" in
     cut -c 1-300 "$out/suite.log" | tail -14
     ;;
   sample)  # the C++ executor's and the coordinator's sampling profiles over a long driver-shape run (args: steps, bench flags)
+    # the frame-pointer build of the executor when it was built (native/build.py): call stacks in the profile
+    exe=ncc/bin/ncc-executor
+    [ -x build/profile/ncc-executor ] && exe=build/profile/ncc-executor
+    NCC_EXECUTOR_BINARY="$PWD/$exe" \
     NCC_SAMPLE_PROFILE="$PWD/$out/samples" NCC_SAMPLE_US=200 NCC_PY_SAMPLE="$PWD/$out/py" NCC_PY_SAMPLE_US=200 \
       timeout -k 10 600 python3 bench.py --steps "${1:-100}" --warmup 5 "${@:2}" > "$out/sampled_bench.json" \
       2> "$out/sampled_bench.err" || exit $?
-    python3 scripts/executor_profile.py "$out/samples" > "$out/executor_profile.txt" 2>&1 || true
+    python3 scripts/executor_profile.py "$out/samples" --binary "$exe" > "$out/executor_profile.txt" 2>&1 || true
     python3 scripts/py_profile.py "$out"/py.*.json > "$out/coordinator_profile.txt" 2>&1 || true
     summary "$out/sampled_bench.json"
     ;;

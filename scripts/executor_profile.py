@@ -10,8 +10,10 @@ offset, in the executable, of the instruction each SIGPROF interrupted (native/e
 * frame — the function whose machine code it is (what an inlined helper was inlined into; coroutine bodies
   show up as their own frames);
 * line — the hottest source lines;
-* library code by caller — time in libc/libstdc++ leaves (memcpy, system-call wrappers) by the executor's
-  call site (the return address on top of the stack at the sample).
+* library code by caller — time in libc/libstdc++ leaves (memcpy, system-call wrappers) and library templates by
+  the executor's call site: the first of its own functions up the frame-pointer chain (the `profile` build,
+  build/profile/ncc-executor), else the return address on top of the stack;
+* inclusive (frame-pointer build only) — each of the executor's functions once per sample it is on the stack.
 
     NCC_SAMPLE_PROFILE=/tmp/prof python bench.py --steps 20 --warmup 5
     python scripts/executor_profile.py /tmp/prof [--binary ncc/bin/ncc-executor] [--top 30]
@@ -30,8 +32,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load_samples(paths: list[str]) -> collections.Counter:
-    """((module, address in the module's file), (module, address) of the top-of-stack word, or None when it
-    is not code) -> samples, over every process's file."""
+    """((module, address in the module's file), (module, address) of the top-of-stack word or None when it is not
+    code, (call sites up the frame-pointer chain, each (module, return address - 1)...)) -> samples, over every
+    process's file.  The chain is empty unless the executor was the frame-pointer build (`build/profile/`)."""
     counts: collections.Counter = collections.Counter()
     for p in paths:
         files = sorted(glob.glob(os.path.join(p, "*.samples"))) if os.path.isdir(p) else [p]
@@ -45,8 +48,8 @@ def load_samples(paths: list[str]) -> collections.Counter:
                         lo, hi = (int(x, 16) for x in parts[0].split("-"))
                         maps.append((lo, hi, int(parts[2], 16), parts[5] if len(parts) > 5 else "[anon]"))
                     elif line.strip():
-                        words = line.split()
-                        raw[(int(words[0], 16), int(words[1], 16) if len(words) > 1 else 0)] += 1
+                        words = [int(w, 16) for w in line.split()]
+                        raw[(words[0], words[1] if len(words) > 1 else 0, tuple(words[2:]))] += 1
 
             def where(addr):
                 for lo, hi, off, path in maps:
@@ -54,8 +57,9 @@ def load_samples(paths: list[str]) -> collections.Counter:
                         return path, addr - lo + off
                 return None
 
-            for (pc, top), n in raw.items():
-                counts[(where(pc) or ("[unknown]", pc), where(top))] += n
+            for (pc, top, chain), n in raw.items():
+                sites = tuple(w for w in (where(r - 1) for r in chain) if w is not None)
+                counts[(where(pc) or ("[unknown]", pc), where(top), sites)] += n
     return counts
 
 
@@ -154,6 +158,15 @@ def relabel_library(path: str, chains: dict) -> None:
             chain[:] = [(f"{os.path.basename(path)} internal", chain[0][1] if chain else "??:0")]
 
 
+_LIB_NAMES = ("std::", "__gnu_cxx::", "void std::", "bool std::", "__gnu_cxx::__enable_if", "operator new",
+              "operator delete", "ncc::alloc::")
+
+
+def _ours(name: str) -> bool:
+    """A function of the executor's own code, not a library template instantiated in it."""
+    return not name.startswith(_LIB_NAMES)
+
+
 def report(counts: collections.Counter, binary: str, top: int) -> str:
     total = sum(counts.values())
     if not total:
@@ -161,41 +174,63 @@ def report(counts: collections.Counter, binary: str, top: int) -> str:
     chains = {}
     modules: collections.Counter = collections.Counter()
     wanted = collections.defaultdict(set)
-    for (pc, tos), n in counts.items():
+    rbin = os.path.realpath(binary)
+    have_stacks = False
+    for (pc, tos, sites), n in counts.items():
         modules[os.path.basename(pc[0])] += n
         wanted[pc[0]].add(pc[1])
-        if tos is not None and pc[0] != os.path.realpath(binary) and tos[0] == os.path.realpath(binary):
+        if tos is not None and pc[0] != rbin and tos[0] == rbin:
             wanted[tos[0]].add(tos[1])
+        for site in sites:
+            have_stacks = True
+            if site[0] == rbin:
+                wanted[site[0]].add(site[1])
     for path, addrs in wanted.items():
         if os.path.isfile(path):
             for a, chain in symbolize(path, sorted(addrs)).items():
                 chains[(path, a)] = chain
-            if os.path.realpath(path) != os.path.realpath(binary):
+            if os.path.realpath(path) != rbin:
                 relabel_library(path, chains)
     self_c: collections.Counter = collections.Counter()
     frame_c: collections.Counter = collections.Counter()
     line_c: collections.Counter = collections.Counter()
     lib_c: collections.Counter = collections.Counter()
-    for (pc, tos), n in counts.items():
+    incl_c: collections.Counter = collections.Counter()
+    for (pc, tos, sites), n in counts.items():
         path = pc[0]
         chain = chains.get(pc) or [("??", "??:0")]
-        ours = os.path.realpath(path) == os.path.realpath(binary)
+        ours = os.path.realpath(path) == rbin
         tag = "" if ours else f"  [{os.path.basename(path)}]"
         self_c[chain[0][0] + tag] += n
         frame_c[chain[-1][0] + tag] += n
         line_c[f"{chain[0][1].split(' ')[0]}  ({short(chain[0][0], 50)}){tag}"] += n
-        if not ours:  # a leaf in a library: its caller is the return address on top of the stack
-            caller = chains.get(tos) if tos is not None else None
-            who = f"{caller[0][1].split(' ')[0]} ({short(caller[-1][0], 60)})" if caller else "?"
-            lib_c[f"{chain[0][0]}{tag}  <-  {who}"] += n
-    out = [f"{total} samples"]
+        # the executor's own call sites up the stack (frame-pointer build), innermost first, inlined callers kept
+        up = [c for s in sites for c in (chains.get(s) or [])]
+        if not ours or not _ours(chain[-1][0]):  # a leaf in a library or a library template: who called it
+            site = next((c for c in up if _ours(c[0])), None)
+            if site is not None:
+                who = f"{site[1].split(' ')[0]} ({short(site[0], 60)})"
+            else:
+                caller = chains.get(tos) if tos is not None else None
+                who = f"{caller[0][1].split(' ')[0]} ({short(caller[-1][0], 60)})" if caller else "?"
+            lib_c[f"{short(chain[0][0], 40)}{tag}  <-  {who}"] += n
+        if have_stacks:
+            seen = set()
+            for fn in [c[0] for c in chain] + [c[0] for c in up]:
+                if _ours(fn) and fn not in seen:
+                    seen.add(fn)
+                    incl_c[fn] += n
+    out = [f"{total} samples" + ("" if have_stacks else " (no call stacks: not the frame-pointer build)")]
     out.append("\n== module")
     for name, n in modules.most_common():
         out.append(f"{100.0 * n / total:6.2f}%  {n:7d}  {name}")
-    for title, c in (("self (innermost function, inlined code counted as itself)", self_c),
-                     ("frame (the function whose code ran: inlined helpers folded into their caller)", frame_c),
-                     ("line", line_c),
-                     ("library code by caller (the executor's call site that entered it)", lib_c)):
+    views = [("self (innermost function, inlined code counted as itself)", self_c),
+             ("frame (the function whose code ran: inlined helpers folded into their caller)", frame_c),
+             ("line", line_c),
+             ("library code by caller (the executor's call site that entered it)", lib_c)]
+    if have_stacks:
+        views.append(("inclusive (the executor's functions on the sampled stack, each once per sample)", incl_c))
+    for title, c in views:
         out.append(f"\n== {title}")
         for name, n in c.most_common(top):
             out.append(f"{100.0 * n / total:6.2f}%  {n:7d}  {short(name)}")

@@ -11,6 +11,7 @@ import json
 import os
 import re
 import socket
+import sys
 
 import pytest
 
@@ -163,6 +164,51 @@ async def test_sampling_profile_is_written_and_symbolized(tmp_path):
     counts = prof.load_samples([str(tmp_path)])
     out = prof.report(counts, binary_path(), 10)
     assert out.split()[0].isdigit() and "== self" in out if counts else out == "no samples"
+
+
+async def test_frame_pointer_build_records_call_stacks(tmp_path, monkeypatch):
+    """The profile flavor (native/build.py: frame pointers, NCC_FRAME_POINTERS) adds the return addresses up the
+    rbp chain to each sample, and the report gains call sites and an inclusive view."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "native"))
+    import build
+    try:
+        fp_bin = build.build_executor(profile=True)
+    except Exception as e:  # noqa: BLE001 — no compiler here
+        pytest.skip(f"the profiling executor is not buildable here: {e}")
+    monkeypatch.setenv("NCC_EXECUTOR_BINARY", fp_bin)
+    spec = importlib.util.spec_from_file_location("executor_profile", os.path.join(root, "scripts", "executor_profile.py"))
+    prof = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(prof)
+    srv = FakeApiServer(name="shard-0")
+    url = await srv.start()
+    try:
+        tpls, secs = [], []
+        for i in range(200):
+            t = make_template(i, NS, secrets=[f"s{i}"])
+            t["metadata"].update(uid=f"u-{i}", resourceVersion=str(10 + i), generation=1)
+            sec = make_secret(f"s{i}", NS, payload=4096)
+            sec["metadata"].update(uid=f"u-s{i}", resourceVersion=str(1000 + i))
+            tpls.append(t)
+            secs.append(sec)
+        async with Executor(cfg([{"name": "shard-0", "server": url}]),
+                            env={"NCC_SAMPLE_PROFILE": str(tmp_path), "NCC_SAMPLE_US": "50"}) as ex:
+            for k, objs in ((0, tpls), (1, []), (2, secs), (3, [])):
+                ex.snapshot(k, objs)
+            for _ in range(200):
+                await ex.next_message("report")
+            await ex.close()
+    finally:
+        await srv.stop()
+    files = list(tmp_path.glob("executor-0-*.samples"))
+    assert len(files) == 1
+    rows = [ln.split() for ln in files[0].read_text().splitlines() if ln and not ln.startswith("#")]
+    if not rows:
+        pytest.skip("no CPU sample taken on this host")
+    assert any(len(r) > 2 for r in rows), rows[:5]  # return addresses up the frame-pointer chain
+    out = prof.report(prof.load_samples([str(tmp_path)]), fp_bin, 10)
+    assert "== inclusive" in out and "no call stacks" not in out
 
 
 async def test_every_report_of_a_batch_is_seen():
