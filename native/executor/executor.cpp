@@ -600,11 +600,16 @@ static ShardPtr make_shard_obj(int kind, Value obj, const std::string_view* raw 
 
 // metadata fields of a shard object from its raw text (no DOM); false: anything unexpected (an escaped
 // string, a non-string where a string belongs) — the caller parses the object instead
-static bool scan_meta(ShardObj& s, std::string_view meta) {
+// `managed` (optional): set when the metadata has a managedFields member
+static bool scan_meta(ShardObj& s, std::string_view meta, bool* managed = nullptr) {
     RawCursor c(meta);
     return c.members([&](std::string_view k, std::string_view v) {
         RawCursor vc(v);
         std::string_view t;
+        if (k == "managedFields") {
+            if (managed != nullptr) *managed = true;
+            return true;
+        }
         if (k == "name" || k == "namespace" || k == "uid" || k == "resourceVersion") {
             if (!vc.str(t)) return v == "null";
             if (k == "name") s.name.assign(t);
@@ -700,7 +705,9 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body, const SentPayloa
         rest.push_back('"');
         rest.append(k);
         rest.append("\":");
-        if (k == "metadata" && v.find("\"managedFields\"") != std::string_view::npos) {
+        bool managed = false;
+        if (k == "metadata" && !scan_meta(*s, v, &managed)) return false;
+        if (managed) {
             // kept without managedFields (see make_shard_obj): the other members copied as text
             rest.push_back('{');
             bool mfirst = true;
@@ -716,10 +723,10 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body, const SentPayloa
             });
             if (!mok) return false;
             rest.push_back('}');
-            return scan_meta(*s, v);
+            return true;
         }
         rest.append(v);
-        if (k == "metadata") return scan_meta(*s, v);
+        if (k == "metadata") return true;
         if (k == "type" && kind >= 2) {  // Secret.type
             std::string_view t;
             if (!RawCursor(v).str(t)) return v == "null";
