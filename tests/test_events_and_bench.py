@@ -209,11 +209,12 @@ def _free_port() -> int:
 
 @pytest.mark.slow
 def test_bench_two_ranks_over_gloo():
-    """The driver's N>1 launch shape: torch.distributed.run, one shard apiserver per rank, rank 0 reports."""
+    """The driver's N>1 launch shape: torch.distributed.run, one shard apiserver per rank, rank 0 reports — with
+    the TLS + product-defaults second run the driver's command includes (both runs share the process group)."""
     pytest.importorskip("torch.distributed")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1", "--no-tls-run"]
+           "--gpus", "2", "--templates", "40", "--steps", "2", "--warmup", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -221,6 +222,7 @@ def test_bench_two_ranks_over_gloo():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["shards"] == 2 and res["scaling"] == "weak"
     assert res["value"] > 0 and res["p50_latency_ms"] is not None and res["controller_alive"]
+    assert res["tls_value"] > 0 and res["tls_config"]["controller_transport"] == "h2"
 
 
 @pytest.mark.slow
