@@ -597,6 +597,7 @@ static ShardPtr make_shard_obj(int kind, Value obj, const std::string_view* raw 
         obj.erase("stringData");
     }
     s->rest = dumps(obj);
+    s->rest.shrink_to_fit();  // cached for the object's lifetime: no growth slack (240 000 of them at config 4)
     return s;
 }
 
@@ -744,6 +745,7 @@ static ShardPtr shard_obj_scan(int kind, std::string_view body, const SentPayloa
     }
     if (!ok) return nullptr;
     rest.push_back('}');
+    rest.shrink_to_fit();  // reserved for the whole body, payloads included: cached, it keeps only its own text
     if (s->ns.empty()) s->ns = g_opt.ns;
     static const uint64_t kNullFp = fingerprint(Value());
     if (kind < 2) {
