@@ -40,6 +40,15 @@ def _deps(t: dict) -> tuple[list, list]:
             [e["configMapRef"]["name"] for e in mev if e.get("configMapRef")])
 
 
+def _missing_refs(cl, t) -> list:
+    """The Secrets / ConfigMaps template `t` references that do not exist on the controller cluster."""
+    if t is None:
+        return []
+    secrets, cms = _deps(t)
+    return [n for n in secrets if cl.cstate.try_get(R.SECRETS, NS, n) is None] + \
+        [n for n in cms if cl.cstate.try_get(R.CONFIGMAPS, NS, n) is None]
+
+
 def _converged(cl, active=None, meta_sync: bool = False) -> str:
     """'' when every (active) shard matches the model, else the first difference found."""
     active = sorted(active if active is not None else range(len(cl.sstates)))
@@ -47,9 +56,7 @@ def _converged(cl, active=None, meta_sync: bool = False) -> str:
     templates = {t["metadata"]["name"]: t for t in cl.cstate.list(R.TEMPLATES, NS)["items"]}
     missing_events = None
     for name, t in list(templates.items()):
-        secrets, cms = _deps(t)
-        missing = [n for n in secrets if cl.cstate.try_get(R.SECRETS, NS, n) is None] + \
-            [n for n in cms if cl.cstate.try_get(R.CONFIGMAPS, NS, n) is None]
+        missing = _missing_refs(cl, t)
         if missing:
             # a reference that does not exist: the controller-side GC deleted a Secret the user re-pointed this
             # template at while its previous owners went (adoption made it theirs) — the
@@ -277,9 +284,20 @@ async def test_chaos_converges_to_the_model(tmp_path, topology, seed, monkeypatc
         # the model check sees a difference (and the controller repairs it): drift on one shard copy.  After
         # a "down" episode too: a shard watch in its reconnect backoff (client-go's 0.8 s doubling to 30 s)
         # retries as soon as the shard answers the executor's writes again.
-        name = live[0]
-        await mutate(cl.sc[0], R.TEMPLATES, name, lambda o: o["spec"]["container"].__setitem__("versionTag", "drift"))
-        assert "spec differs" in _converged(cl, active)
+        # (a template the model checks: not one whose reference the controller-side GC removed — its shard copy
+        # is legitimately left alone, see _converged)
+        checked = [n for n in live if not _missing_refs(cl, cl.cstate.try_get(R.TEMPLATES, NS, n))]
+        name = checked[0] if checked else None
+        if name is None:
+            return
+        drifted = await mutate(cl.sc[0], R.TEMPLATES, name,
+                               lambda o: o["spec"]["container"].__setitem__("versionTag", "drift"))
+        seen = _converged(cl, active)
+        if "spec differs" not in seen:
+            # already repaired: the C++ executor can answer the drift's watch event before this client has read
+            # the response to its own write — then the copy was written again after the drift
+            cur = await cl.sc[0].get(R.TEMPLATES, NS, name)
+            assert int(cur["metadata"]["resourceVersion"]) > int(drifted["metadata"]["resourceVersion"]), (seen, cur)
         try:
             await wait_for(done, timeout=15, interval=0.1)
         except AssertionError:
