@@ -24,7 +24,7 @@
 //  * H2ClientParser / h2_request / hpack_encode — HTTP/2 framing and HPACK for the Python clients.
 //
 // The code is split by concern into native/ext/*.hpp (hashing, workqueue, scan, http1, pyjson, reports,
-// h2client), included in that order below; this file holds the bindings.
+// h2client, sampler), included in that order below; this file holds the bindings.
 //
 // The fake apiserver's native pieces (its HTTP/1.1 request-head parser, HTTP/2 server parser and response
 // encoder) are not here: they are test substrate, built into ncc/fakeapi/_native from native/fakeapi/
@@ -51,6 +51,9 @@
 #include <pybind11/stl.h>
 
 #include <Python.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -70,7 +73,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 30
+#define NCC_NATIVE_ABI 31
 
 namespace {
 #include "ext/hashing.hpp"
@@ -80,6 +83,7 @@ namespace {
 #include "ext/pyjson.hpp"
 #include "ext/reports.hpp"
 #include "ext/h2client.hpp"
+#include "ext/sampler.hpp"
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -116,6 +120,9 @@ PYBIND11_MODULE(_native, m) {
              "relay_index over a batch, memoising the key tuples")
         .def("clear", &RelayIndex::clear)
         .def("__len__", &RelayIndex::size);
+    m.def("native_sample_start", &native_sample_start, py::arg("us"),
+          "sample the interrupted instruction on every SIGPROF (NCC_NATIVE_SAMPLE; ncc/sampler.py)");
+    m.def("native_sample_dump", &native_sample_dump, py::arg("path"), "write the samples; returns their count");
     m.def("key_partition", &key_partition, py::arg("namespace"), py::arg("name"), py::arg("parts"));
     m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
           "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");

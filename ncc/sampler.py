@@ -7,7 +7,10 @@ of the process's CPU); each SIGPROF records the interrupted Python stack, and at
 
 Python runs signal handlers between bytecodes, so time inside a C call (a native decode, a socket send) is
 charged to the Python line that made it — which is where it would be cut anyway.  The C++ executor has
-its own sampler (`NCC_SAMPLE_PROFILE`, native/executor/executor.cpp).
+its own sampler (`NCC_SAMPLE_PROFILE`, native/executor/executor.cpp).  With `NCC_NATIVE_SAMPLE=1` too, the
+extension records the C++ instruction each tick interrupted (native/ext/sampler.hpp) into
+`<path>.<role>.<pid>.native.samples`, which scripts/executor_profile.py symbolizes against the extension
+(`--binary ncc/_native*.so`).
 """
 from __future__ import annotations
 
@@ -68,4 +71,11 @@ def start(role: str) -> bool:
         except OSError:
             pass
     atexit.register(dump)
+    if os.environ.get("NCC_NATIVE_SAMPLE"):
+        # the extension's own time, by C++ function (native/ext/sampler.hpp): what each native line above spends
+        from . import native as _native
+        mod = _native.load()
+        if mod is not None and hasattr(mod, "native_sample_start") and mod.native_sample_start(us):
+            nat_path = f"{path}.{role}.{os.getpid()}.native.samples"
+            atexit.register(lambda: mod.native_sample_dump(nat_path))
     return True
