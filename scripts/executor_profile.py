@@ -31,6 +31,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def local_path(path: str) -> str:
+    """`path` itself when it exists here, else the file of this checkout with the longest common tail."""
+    if os.path.isfile(path) or not path.startswith("/"):
+        return path
+    parts = path.strip("/").split("/")
+    for i in range(1, len(parts)):
+        cand = os.path.join(ROOT, *parts[i:])
+        if os.path.isfile(cand):
+            return cand
+    return path
+
+
 def load_samples(paths: list[str]) -> collections.Counter:
     """((module, address in the module's file), (module, address) of the top-of-stack word or None when it is not
     code, (call sites up the frame-pointer chain, each (module, return address - 1)...)) -> samples, over every
@@ -56,6 +68,10 @@ def load_samples(paths: list[str]) -> collections.Counter:
                     if lo <= addr < hi:
                         return path, addr - lo + off
                 return None
+
+            # a profile taken on another machine (the GPU box runs a copy of this tree elsewhere): its files
+            # under the repository map to this checkout by their path relative to it
+            maps = [(lo, hi, off, local_path(path)) for lo, hi, off, path in maps]
 
             for (pc, top, chain), n in raw.items():
                 sites = tuple(w for w in (where(r - 1) for r in chain) if w is not None)
