@@ -40,13 +40,14 @@ bool native_sample_start(long us) {
 #if !defined(__x86_64__)
     return false;
 #else
-    if (g_nsamples_buf != nullptr) return true;
-    g_nsamples_buf = new uintptr_t[2 * kNativeMaxSamples];
+    if (g_nsamples_buf == nullptr) g_nsamples_buf = new uintptr_t[2 * kNativeMaxSamples];
     struct sigaction sa {};
     sa.sa_sigaction = native_on_sigprof;
     sa.sa_flags = SA_SIGINFO | SA_RESTART;
     sigemptyset(&sa.sa_mask);
-    sigaction(SIGPROF, &sa, &g_nsamples_prev);
+    struct sigaction prev {};
+    sigaction(SIGPROF, &sa, &prev);
+    if (prev.sa_sigaction != native_on_sigprof) g_nsamples_prev = prev;  // never chain to ourselves
     struct itimerval cur {};
     getitimer(ITIMER_PROF, &cur);
     if (cur.it_interval.tv_sec == 0 && cur.it_interval.tv_usec == 0) {

@@ -560,3 +560,31 @@ def test_memoising_relay_index_matches_relay_index():
         if step == 200:  # a relist swaps the dict
             raw_a, raw_b = dict(raw_a), dict(raw_b)
     assert len(idx) <= len(names) * 2
+
+
+def test_native_sampler_records_and_hands_the_signal_on(tmp_path):
+    """NCC_NATIVE_SAMPLE's sampler (native/ext/sampler.hpp): installed in front of a Python SIGPROF handler, it
+    records the interrupted instruction and still lets the Python handler run; the dump holds the executable
+    mappings and one "pc tos" line per sample."""
+    import signal
+    from ncc import native
+    m = native.load(required=True)
+    hits = [0]
+    old = signal.signal(signal.SIGPROF, lambda *_: hits.__setitem__(0, hits[0] + 1))
+    signal.setitimer(signal.ITIMER_PROF, 0.0005, 0.0005)
+    try:
+        assert m.native_sample_start(500)
+        objs = [{"k": list(range(200)), "s": "x" * 500}] * 200
+        deadline = time.process_time() + 1.0
+        while time.process_time() < deadline and hits[0] < 20:
+            m.fingerprint_many(objs)
+        path = tmp_path / "native.samples"
+        n = m.native_sample_dump(str(path))
+    finally:
+        signal.setitimer(signal.ITIMER_PROF, 0, 0)
+        signal.signal(signal.SIGPROF, old)
+    assert hits[0] > 0  # the Python handler still ran
+    text = path.read_text()
+    assert "# map " in text
+    rows = [ln for ln in text.splitlines() if ln and not ln.startswith("#")]
+    assert len(rows) == n and n > 0 and all(len(r.split()) == 2 for r in rows)
