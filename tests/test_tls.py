@@ -129,3 +129,32 @@ def test_pki_unavailable_is_reported(tmp_path, monkeypatch):
     monkeypatch.setattr("shutil.which", lambda _name: None)
     with pytest.raises(PKIUnavailable):
         make_pki(str(tmp_path))
+
+
+async def test_http11_fallback_offers_only_http11_over_tls(tmp_path):
+    """after the pool moves to HTTP/1.1 (HTTP_1_1_REQUIRED), its TLS connections must not offer h2
+    by ALPN — a server that picks h2 whenever it is offered (the fake apiserver does, as Go's) would get
+    HTTP/1.1 bytes on an h2 connection.  The control: the same pool falling back on its own HTTP/2 context
+    (ALPN h2 + http/1.1, the round-5 behaviour) fails."""
+    env = await FakeEnvironment(0, str(tmp_path), tls=True).start()
+    try:
+        for control in (False, True):
+            c = RestClient(load_kubeconfig(env.controller_kubeconfig), http2="auto", max_retries=0)
+            try:
+                assert (await c.list(R.SECRETS, NS))["items"] == []
+                pool = c._pool
+                assert pool.protocol == "h2"
+                if control:
+                    pool.fallback_ssl = None  # fall back on the HTTP/2 context
+                pool._downgrade("test")
+                if control:
+                    with pytest.raises(E.TransportError):
+                        await c.list(R.SECRETS, NS)
+                else:
+                    for _ in range(3):
+                        assert (await c.list(R.SECRETS, NS))["items"] == []
+                    assert pool.protocol == "http/1.1" and pool.stats["h2_downgraded"] == 1
+            finally:
+                await c.close()
+    finally:
+        await env.stop()
