@@ -418,3 +418,18 @@ async def test_answered_write_ends_the_reflectors_outage_backoff():
             await ex.close()
     finally:
         await srv.stop()
+
+
+def test_profile_report_maps_another_machines_paths():
+    """A profile taken on the GPU box names the box's copy of this tree; the report maps it to this checkout by
+    the longest path tail that exists here (scripts/executor_profile.py `local_path`)."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("executor_profile", os.path.join(root, "scripts", "executor_profile.py"))
+    prof = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(prof)
+    here = os.path.join(root, "scripts", "executor_profile.py")
+    assert prof.local_path("/tmp/code/Some__repo/repo/scripts/executor_profile.py") == here
+    assert prof.local_path(here) == here
+    assert prof.local_path("/no/such/dir/file.so") == "/no/such/dir/file.so"
+    assert prof.local_path("[vdso]") == "[vdso]"
