@@ -42,7 +42,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 # HTTP/1.1 server (kube-apiserver's Go net/http) serves one connection's requests one after the other, so
 # only connections give a shard apiserver requests to run concurrently (APF seats, etcd round trips); and on
 # the bench, 32 connections × 8 coalesced only 1.3 requests per write (docs/BENCHMARKS_ARCHIVE.md).  Pipelining pays for a
-# far-away shard, where the round trip rather than the apiserver bounds a connection.
+# far-away shard, where the round trip rather than the apiserver bounds a connection; so does a larger pool over
+# HTTP/2, where it only caps the streams in flight (BENCHMARKS.md "Shards × round-trip latency": 1024 gave +35 % at
+# 5 ms and +121 % at 20 ms).  256 stays the default: it is also the HTTP/1.1 connection count, and a kube-apiserver
+# admits 200 mutating requests at a time by default.
 DEFAULT_POOL_SIZE = 256
 DEFAULT_PIPELINE_DEPTH = 1
 _LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "WARN": 30, "ERROR": 40, "CRITICAL": 50}
