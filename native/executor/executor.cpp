@@ -2476,7 +2476,12 @@ static void configure(const Value& c) {
     o.alias = std::string(c.sget("alias"));
     o.workers = static_cast<int>(num(c, "workers", o.workers));
     o.pool_size = static_cast<int>(num(c, "pool_size", o.pool_size));
-    if (const char* ps = std::getenv("NCC_POOL_SIZE")) o.pool_size = std::max(1, std::atoi(ps));  // experiments
+    o.flow.h2_cap = static_cast<int>(num(c, "h2_inflight", 0));
+    if (const char* ps = std::getenv("NCC_POOL_SIZE")) {  // experiments: the cap over either protocol
+        o.pool_size = std::max(1, std::atoi(ps));
+        o.flow.h2_cap = 0;
+    }
+    if (const char* v = std::getenv("NCC_H2_INFLIGHT")) o.flow.h2_cap = std::atoi(v);  // experiments
     o.pipeline_depth = std::max(1, static_cast<int>(num(c, "pipeline_depth", o.pipeline_depth)));
     if (const char* v = std::getenv("NCC_PIPELINE_DEPTH")) o.pipeline_depth = std::max(1, std::atoi(v));  // experiments
     o.http2 = static_cast<int>(num(c, "http2", o.http2));
@@ -2671,10 +2676,10 @@ static void send_status() {
         // executor loop's wake-ups and coalesced wake-ups (process-wide), and HTTP/2: in use (0/1), streams
         // opened, streams re-sent after REFUSED_STREAM, GOAWAYs received, connections dropped for an unanswered PING,
         // GOAWAYs with an error code, downgraded to HTTP/1.1 by HTTP_1_1_REQUIRED (0/1), streams reset with
-        // ENHANCE_YOUR_CALM]
+        // ENHANCE_YOUR_CALM, the in-flight cap]
         const Client& cl = *sp->client;
         e.str("flow");
-        e.array(23);
+        e.array(24);
         e.integer(static_cast<long long>(cl.limit()));
         e.integer(cl.inflight());
         e.integer(cl.flow.max_inflight);
@@ -2698,6 +2703,7 @@ static void send_status() {
         e.integer(cl.h2_goaway_errors);
         e.integer(cl.h2_downgraded ? 1 : 0);
         e.integer(cl.h2_calm);
+        e.integer(cl.cap());
     }
     e.str("q");
     e.integer(static_cast<long long>(ex.queue.load()));

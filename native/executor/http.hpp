@@ -746,6 +746,10 @@ inline Task<std::string> read_body(Conn& c, const Head& h) {
 // burst 10; native mode has none unless configured).
 struct FlowLimits {
     int cap = 256;     // the most requests in flight: connections × pipeline depth
+    // over HTTP/2, when larger: the most requests in flight there.  A stream costs no connection, and a shard a
+    // round trip of milliseconds away is bound by in-flight ÷ RTT (Little's law), not by its apiserver; back to
+    // `cap` when the shard turns out to speak HTTP/1.1 only
+    int h2_cap = 0;
     double initial = 0;  // 0: half the cap
     double beta = 0.7;
     double latency_s = 1.0;
@@ -772,7 +776,7 @@ public:
            int http2 = 0)
         : creds_(std::move(creds)), max_(std::max(1, pool_size)), depth_(std::max(1, depth)),
           timeout_(request_timeout), fl_(fl) {
-        fl_.cap = max_ * depth_;
+        fl_.cap = base_cap_ = max_ * depth_;
         if (fl_.initial <= 0) fl_.initial = std::max(1.0, fl_.cap / 2.0);
         limit_ = fl_.adaptive ? std::clamp(fl_.initial, 1.0, static_cast<double>(fl_.cap)) : fl_.cap;
         slow_start_ = fl_.adaptive && limit_ < fl_.cap;
@@ -788,6 +792,11 @@ public:
         reload_token(true);
         h2_mode_ = http2;
         h2_ok_ = http2 == 2 || (http2 == 1 && url_.tls);
+        if (h2_ok_ && fl_.h2_cap > fl_.cap) {  // slow start from the same initial limit, up to the HTTP/2 cap
+            fl_.cap = fl_.h2_cap;
+            if (!fl_.adaptive) limit_ = fl_.cap;
+            slow_start_ = fl_.adaptive && limit_ < fl_.cap;
+        }
         if (!creds_.proxy.empty()) {
             const std::string& p = creds_.proxy;
             size_t sep = p.find("://");
@@ -822,6 +831,7 @@ public:
     long long requests = 0, request_errors = 0;  // completed exchanges / transport failures
     FlowStats flow;
     double limit() const { return limit_; }
+    int cap() const { return fl_.cap; }
     int inflight() const { return inflight_; }
     int connections() const {
         if (use_h2()) return static_cast<int>(h2s_.size());
@@ -943,6 +953,7 @@ private:
     SSL_CTX* ctx_ = nullptr;
     std::string host_;
     int max_;
+    int base_cap_ = 0;  // pool × depth: the in-flight cap over HTTP/1.1
     int depth_;
     double timeout_;
     FlowLimits fl_;
@@ -1511,7 +1522,7 @@ private:
             if (url_.tls && s->c.alpn_selected != "h2")
                 throw NoH2("the server did not negotiate HTTP/2 (ALPN); using HTTP/1.1");
         } catch (const NoH2& e) {
-            h2_ok_ = false;  // every request from now on, and the ones queued here, go over HTTP/1.1
+            h2_off();  // every request from now on, and the ones queued here, go over HTTP/1.1
             h2_break(s, e.what(), true);
             co_return;
         } catch (const std::exception& e) {
@@ -1585,7 +1596,7 @@ private:
                 s->last_read = now_s();
             }
         } catch (const NoH2& e) {
-            h2_ok_ = false;  // this request and every later one over HTTP/1.1
+            h2_off();  // this request and every later one over HTTP/1.1
             h2_break(s, e.what(), true);
         } catch (const h2::ConnectionError& e) {  // the server broke the protocol: say so (GOAWAY), then close
             h2_break(s, e.what(), false, e.code);
@@ -1595,7 +1606,7 @@ private:
             // the connection ended before the server said anything: on cleartext that is what a server
             // without HTTP/2 may do with a preface — fall back as for an HTTP/1.1 answer
             if (!s->got_settings && !url_.tls) {
-                h2_ok_ = false;
+                h2_off();
                 h2_break(s, std::string("no HTTP/2 answer to the preface (") + e.what() + "); using HTTP/1.1", true);
             } else {
                 h2_break(s, e.what(), false);
@@ -1891,12 +1902,20 @@ private:
         busy_.erase(&s->c);
         s->c.close();
     }
+    // The shard is spoken to over HTTP/1.1 from now on: the in-flight cap is pool × depth again (requests already
+    // in flight beyond it finish; no new one starts until they are under it).
+    void h2_off() {
+        h2_ok_ = false;
+        fl_.cap = base_cap_;
+        limit_ = std::min(limit_, static_cast<double>(fl_.cap));
+        if (limit_ >= fl_.cap) slow_start_ = false;
+    }
     // HTTP_1_1_REQUIRED: this shard over HTTP/1.1 from now on, as when ALPN refuses h2.  The connection's other
     // streams finish where they are (it takes no new ones).
     void h2_downgrade(h2::Session& s, const char* why) {
         s.goaway = true;
         if (!h2_ok_) return;
-        h2_ok_ = false;
+        h2_off();
         h2_downgraded = true;
         notice(std::string(why) + ": the server requires HTTP/1.1; using HTTP/1.1 for this cluster from now on");
     }

@@ -2,7 +2,7 @@
 // header the executor compiles) driven from stdin, so tests can run it against scripted HTTP/2 servers and
 // independent implementations (tests/test_http2_errors.py, tests/test_http2_interop.py).
 //
-//   ncc-h2probe URL HTTP2 [--ca FILE] [--insecure] [--timeout S] [--pool N]
+//   ncc-h2probe URL HTTP2 [--ca FILE] [--insecure] [--timeout S] [--pool N] [--h2-cap N]
 //
 // HTTP2 is client-http2's mode (0 off, 1 ALPN on TLS, 2 prior knowledge).  Each stdin line is one step:
 //   METHOD PATH [BODY]   a request (issued at once: the steps of a group run concurrently)
@@ -72,9 +72,10 @@ struct Probe {
         while (pending > 0) co_await loop().sleep(0.002);
         std::printf("{\"stats\":{\"http2\":%d,\"h2_streams\":%lld,\"h2_refused\":%lld,\"h2_goaways\":%lld,"
                     "\"h2_goaway_errors\":%lld,\"h2_calm\":%lld,\"h2_downgraded\":%d,\"h2_dead\":%lld,\"connections\":%d,\"requests\":%lld,"
-                    "\"request_errors\":%lld},\"notices\":[",
+                    "\"request_errors\":%lld,\"max_inflight\":%d,\"cap\":%d},\"notices\":[",
                     cl->http2() ? 1 : 0, cl->h2_streams, cl->h2_refused, cl->h2_goaways, cl->h2_goaway_errors,
-                    cl->h2_calm, cl->h2_downgraded ? 1 : 0, cl->h2_dead, cl->connections(), cl->requests, cl->request_errors);
+                    cl->h2_calm, cl->h2_downgraded ? 1 : 0, cl->h2_dead, cl->connections(), cl->requests, cl->request_errors,
+                    cl->flow.max_inflight, cl->cap());
         std::printf("%s]}\n", notices.c_str());
         std::fflush(stdout);
         loop().stop();
@@ -87,7 +88,7 @@ struct Probe {
 int main(int argc, char** argv) {
     using namespace ncc;
     if (argc < 3) {
-        std::fprintf(stderr, "usage: ncc-h2probe URL HTTP2 [--ca FILE] [--insecure] [--timeout S] [--pool N]\n");
+        std::fprintf(stderr, "usage: ncc-h2probe URL HTTP2 [--ca FILE] [--insecure] [--timeout S] [--pool N] [--h2-cap N]\n");
         return 2;
     }
     Credentials creds;
@@ -95,6 +96,7 @@ int main(int argc, char** argv) {
     int http2 = std::atoi(argv[2]);
     double timeout = 10;
     int pool = 4;
+    int h2_cap = 0;
     for (int k = 3; k < argc; ++k) {
         std::string a = argv[k];
         if (a == "--ca" && k + 1 < argc) {
@@ -108,6 +110,8 @@ int main(int argc, char** argv) {
             timeout = std::atof(argv[++k]);
         } else if (a == "--pool" && k + 1 < argc) {
             pool = std::atoi(argv[++k]);
+        } else if (a == "--h2-cap" && k + 1 < argc) {
+            h2_cap = std::atoi(argv[++k]);
         }
     }
     std::vector<Step> steps;
@@ -129,6 +133,7 @@ int main(int argc, char** argv) {
     g_loop = &lp;
     FlowLimits fl;
     fl.adaptive = false;
+    fl.h2_cap = h2_cap;
     Client cl(creds, pool, timeout, fl, 1, http2);
     Probe p;
     p.cl = &cl;

@@ -410,7 +410,7 @@ class CoordinatorPartitions:
 FLOW_FIELDS = ("limit", "inflight", "max_inflight", "rejected_429", "overload_signals", "cuts", "gated",
                "qps_wait_ms", "connections", "write_batches", "requests", "slow_start_exits", "increases_held",
                "loop_wakeups", "loop_coalesced", "http2", "h2_streams", "h2_refused", "h2_goaways", "h2_dead",
-               "h2_goaway_errors", "h2_downgraded", "h2_calm")
+               "h2_goaway_errors", "h2_downgraded", "h2_calm", "cap")
 
 
 def status_view(msg: dict) -> dict:

@@ -42,12 +42,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 # HTTP/1.1 server (kube-apiserver's Go net/http) serves one connection's requests one after the other, so
 # only connections give a shard apiserver requests to run concurrently (APF seats, etcd round trips); and on
 # the bench, 32 connections × 8 coalesced only 1.3 requests per write (docs/BENCHMARKS_ARCHIVE.md).  Pipelining pays for a
-# far-away shard, where the round trip rather than the apiserver bounds a connection; so does a larger pool over
-# HTTP/2, where it only caps the streams in flight (BENCHMARKS.md "Shards × round-trip latency": 1024 gave +35 % at
-# 5 ms and +121 % at 20 ms).  256 stays the default: it is also the HTTP/1.1 connection count, and a kube-apiserver
-# admits 200 mutating requests at a time by default.
+# far-away shard, where the round trip rather than the apiserver bounds a connection.  256 is also the HTTP/1.1
+# connection count, and a kube-apiserver admits 200 mutating requests at a time by default.
 DEFAULT_POOL_SIZE = 256
 DEFAULT_PIPELINE_DEPTH = 1
+# Over HTTP/2 a request in flight is a stream, not a connection: with client-pool-size auto, a shard that speaks
+# HTTP/2 may have this many in flight (the adaptive limit still starts at 128 and backs off on 429s), so a shard
+# milliseconds away is not bound by 256 ÷ RTT (BENCHMARKS.md "Shards × round-trip latency": 1024 in flight gave
+# +35 % at 5 ms and +121 % at 20 ms).  An explicit client-pool-size caps both protocols; a shard that falls back to
+# HTTP/1.1 gets pool × depth again (http.hpp `Client::h2_off`).
+DEFAULT_H2_INFLIGHT = 1024
 _LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "WARN": 30, "ERROR": 40, "CRITICAL": 50}
 
 
@@ -170,6 +174,7 @@ class NativeExecutorConfig:
             # 429/503/timeouts) and the client-qps bucket
             "workers": 4 * max(DEFAULT_POOL_SIZE * DEFAULT_PIPELINE_DEPTH, pool * depth), "pool_size": pool,
             "pipeline_depth": depth, "client_qps": qps, "client_burst": burst,
+            "h2_inflight": DEFAULT_H2_INFLIGHT if cfg.client_pool_size <= 0 else 0,
             "http2": HTTP2_MODES.get(str(cfg.client_http2).lower(), 1),
             "request_timeout": 30.0, "coalesce_window": o.coalesce_window,
             "failure_base_delay": o.failure_base_delay, "failure_max_delay": o.failure_max_delay,

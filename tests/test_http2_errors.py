@@ -12,6 +12,8 @@ the same header):
   FLOW_CONTROL_ERROR) on a stream, a connection error (GOAWAY with that code, then close) on the connection;
 * a server whose SETTINGS_HEADER_TABLE_SIZE is 0 (it limits *our* encoder) and which indexes its response fields
   in its own 4096-byte table: both decoders keep that table (ADVICE r5, medium);
+* the in-flight cap: over HTTP/2 the C++ client keeps up to `h2_cap` requests in flight on `pool` connections, and
+  falls back to pool × depth when the shard moves to HTTP/1.1;
 * framing: padded HEADERS/DATA and PRIORITY fields, a header block split over CONTINUATION frames are read; a pad
   length past its frame, a header block interrupted by another frame, and a CONTINUATION without HEADERS are
   connection errors (GOAWAY PROTOCOL_ERROR, then a new connection).
@@ -121,6 +123,8 @@ class Scripted:
                 buf += await reader.read(65536)
             buf = buf[clen:]
             self.log("req", "http/1.1", path, 0)
+            if path == "/slow":
+                await asyncio.sleep(0.05)
             writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
                          % (len(OK_BODY), OK_BODY))
             await writer.drain()
@@ -149,7 +153,10 @@ class Scripted:
                     plan = self.script.get(path)
                     action = plan.pop(0) if plan else "ok"
                     last = sid - 2 if sid > 1 else 0
-                    if action == "ok":
+                    if action == "ok" and path == "/slow":  # answered 200 ms later, the connection serving others
+                        asyncio.get_running_loop().call_later(
+                            0.2, writer.write, _f.h2_response(sid, 200, "application/json", OK_BODY, [], 16384))
+                    elif action == "ok":
                         writer.write(_f.h2_response(sid, 200, "application/json", OK_BODY, [], 16384))
                     elif action == "goaway_calm":  # ENHANCE_YOUR_CALM: this stream refused
                         writer.write(_goaway(last, 0xB, b"too many requests"))
@@ -213,10 +220,10 @@ async def py_requests(url, paths, **kw):
         pool.close()
 
 
-async def cpp_requests(url, paths):
+async def cpp_requests(url, paths, steps=None, args=()):
     probe = probe_path()
-    steps = "".join(f"GET {p}\nWAIT\n" for p in paths)
-    proc = await asyncio.create_subprocess_exec(probe, url, "2", "--timeout", "5", stdin=asyncio.subprocess.PIPE,
+    steps = steps if steps is not None else "".join(f"GET {p}\nWAIT\n" for p in paths)
+    proc = await asyncio.create_subprocess_exec(probe, url, "2", "--timeout", "5", *args, stdin=asyncio.subprocess.PIPE,
                                                 stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.PIPE)
     t0 = time.monotonic()
     out, err = await asyncio.wait_for(proc.communicate(steps.encode()), 60)
@@ -362,5 +369,35 @@ async def test_framing_violations_are_connection_errors(client, action):
         goaways = srv.of("goaway")
         assert goaways and goaways[0][2] == 1, srv.seen  # GOAWAY(PROTOCOL_ERROR) before the close
         assert res[-1].get("status") == 200  # a new connection serves what follows
+    finally:
+        await srv.stop()
+
+
+async def test_cpp_http2_inflight_cap_and_its_fallback():
+    """`h2_cap` (coordinator `DEFAULT_H2_INFLIGHT` when client-pool-size is auto): over HTTP/2, 12 slow requests
+    run 8 at a time on a pool of 2 connections; once the shard requires HTTP/1.1, the cap is pool × depth (2) again."""
+    srv = Scripted({})
+    url = await srv.start()
+    try:
+        steps = "GET /slow\n" * 12 + "WAIT\n"
+        res, stats = await cpp_requests(url, None, steps, ("--pool", "2", "--h2-cap", "8"))
+        assert [r.get("status") for r in res] == [200] * 12, res
+        assert stats["protocol"] == "h2" and stats["cap"] == 8 and stats["max_inflight"] == 8, stats
+        assert stats["connections"] <= 2
+        assert 0.35 <= max(r["ms"] for r in res) / 1000.0 < 1.5  # two rounds of 200 ms, not six
+        # control: no h2 cap -> pool x depth over HTTP/2 too
+        res, stats = await cpp_requests(url, None, steps, ("--pool", "2"))
+        assert stats["cap"] == 2 and stats["max_inflight"] == 2, stats
+    finally:
+        await srv.stop()
+    srv = Scripted({"/x": ["rst_h11"]})
+    url = await srv.start()
+    try:
+        steps = "GET /x\nWAIT\n" + "GET /slow\n" * 12 + "WAIT\n"
+        res, stats = await cpp_requests(url, None, steps, ("--pool", "2", "--h2-cap", "8"))
+        assert [r.get("status") for r in res] == [200] * 13, res
+        assert stats["protocol"] == "http/1.1" and stats["h2_downgraded"] == 1
+        assert stats["cap"] == 2 and stats["max_inflight"] <= 2, stats
+        assert {r[1] for r in srv.of("req") if r[2] == "/slow"} == {"http/1.1"}
     finally:
         await srv.stop()
