@@ -706,7 +706,8 @@ async def config6_admission(mode, T, timeout, aimd=True, admission=None):
     Ready), the share of shard requests answered 429 after the first second, and the shard write rate
     against the seats ÷ service-time bound."""
     adm = dict(APF, **(admission or {}))
-    topo = Topology(8, mode, extra_env=None if aimd else {"NCC_AIMD": "0"})
+    # config 7: round 3's data plane, a fixed 256 in flight per shard (not the HTTP/2 cap of 1024)
+    topo = Topology(8, mode, extra_env=None if aimd else {"NCC_AIMD": "0", "NCC_H2_INFLIGHT": "0"})
     try:
         await topo.start_servers()
         for i in range(8):
