@@ -165,6 +165,9 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
             assert srv.requests["watch_streams"] >= 4
             assert st["h2"]["malformed"] == 0, st  # every header block well-formed (pseudo-headers first)
         assert all(f["rejected_429"] == 0 for f in fl.values())
+        # client-pool-size auto: an HTTP/2 shard may have 1024 requests in flight (streams, not connections)
+        from ncc.controller.native_executor import DEFAULT_H2_INFLIGHT
+        assert all(f["cap"] == DEFAULT_H2_INFLIGHT for f in fl.values()), fl
         # the same flow status as per-shard gauges (statsd / Prometheus)
         from ncc.api import constants as C
         from ncc.telemetry.statsd import MemoryMetrics
@@ -174,6 +177,19 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
         assert v[C.SHARD_CLIENT_METRICS["http2"]] == [1.0, 1.0], v
         assert all(x >= 1 for x in v[C.SHARD_CLIENT_METRICS["limit"]]) and len(v[C.SHARD_CLIENT_METRICS["limit"]]) == 2
         assert v[C.SHARD_CLIENT_METRICS["rejected_429"]] == [0.0, 0.0]
+
+
+async def test_explicit_pool_size_caps_http2_too(tmp_path, native_only, monkeypatch):
+    """An explicit client-pool-size is the in-flight cap over HTTP/2 as over HTTP/1.1 (no 1024-stream default)."""
+    monkeypatch.setenv("NCC_STATUS_S", "0.2")
+    async with Cluster(tmp_path, "native", n_shards=1, client_http2="on", client_pool_size=8,
+                       executors_per_shard=1) as cl:
+        for i in range(10):
+            cl.seed(i, secrets=(f"s{i}",), configmaps=(f"c{i}",))
+        await cl.start()
+        await _converge(cl, 10)
+        fl = await _h2_status(cl)
+        assert fl["shard-0"]["cap"] == 8 and fl["shard-0"]["max_inflight"] <= 8, fl
 
 
 async def test_executor_negotiates_http2_by_alpn_on_tls(tmp_path, native_only, monkeypatch):
