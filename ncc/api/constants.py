@@ -41,6 +41,7 @@ EXECUTOR_NATIVE_METRIC = "executor_native"            # gauge 1: the C++ shard e
 SHARD_FAILING_METRIC = "shard_failing_objects"        # gauge, tag shard: templates whose last sync there failed
 # the C++ executors' shard clients (their status messages, native/executor/http.hpp), gauges tagged shard:
 SHARD_CLIENT_METRICS = {"limit": "shard_client_inflight_limit",      # adaptive concurrency limit (AIMD)
+                        "cap": "shard_client_inflight_cap",          # the most the limit may reach (pool; HTTP/2 cap)
                         "inflight": "shard_client_inflight",         # requests in flight
                         "rejected_429": "shard_client_throttled",    # 429s received (cumulative)
                         "connections": "shard_client_connections",   # open connections

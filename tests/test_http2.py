@@ -177,6 +177,7 @@ async def test_executor_syncs_over_http2_prior_knowledge(tmp_path, native_only, 
         assert v[C.SHARD_CLIENT_METRICS["http2"]] == [1.0, 1.0], v
         assert all(x >= 1 for x in v[C.SHARD_CLIENT_METRICS["limit"]]) and len(v[C.SHARD_CLIENT_METRICS["limit"]]) == 2
         assert v[C.SHARD_CLIENT_METRICS["rejected_429"]] == [0.0, 0.0]
+        assert v[C.SHARD_CLIENT_METRICS["cap"]] == [float(DEFAULT_H2_INFLIGHT)] * 2, v
 
 
 async def test_explicit_pool_size_caps_http2_too(tmp_path, native_only, monkeypatch):
