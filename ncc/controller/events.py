@@ -98,6 +98,16 @@ def involved_object(obj: dict, kind: str | None) -> dict:
     return ref
 
 
+def _blocked_key(obj: dict, kind: str | None):
+    """The spam filter's shortcut key for an object: its UID (one object incarnation, whatever its kind), or
+    kind, apiVersion, namespace and name for an object without one."""
+    m = obj.get("metadata") or {}
+    uid = m.get("uid")
+    if uid:
+        return uid
+    return kind or obj.get("kind", ""), obj.get("apiVersion", ""), m.get("namespace", ""), m.get("name", "")
+
+
 class BroadcastRecorder(EventRecorder):
     """Asynchronous recorder with the client-go correlator, writing Events through `client`."""
 
@@ -165,9 +175,7 @@ class BroadcastRecorder(EventRecorder):
         if blocked and not (self.log_events and log.isEnabledFor(logging.INFO)):
             # an object whose spam bucket is empty: dropped before its reference is built (the bucket's
             # refill is linear, so skipping its update until the next token is due changes nothing)
-            m = obj.get("metadata") or {}
-            until = blocked.get((kind or obj.get("kind", ""), obj.get("apiVersion", ""), m.get("namespace", ""),
-                                 m.get("name", ""), m.get("uid", "")))
+            until = blocked.get(_blocked_key(obj, kind))
             if until is not None and time.monotonic() < until:
                 self.stats["dropped_spam"] += 1
                 return
@@ -181,9 +189,7 @@ class BroadcastRecorder(EventRecorder):
             b = self._buckets.get((self.component, ref["kind"], ref["namespace"], ref["name"], ref["uid"],
                                    ref["apiVersion"]))
             if b is not None and b.qps > 0:
-                m = obj.get("metadata") or {}
-                blocked[(kind or obj.get("kind", ""), obj.get("apiVersion", ""), m.get("namespace", ""),
-                         m.get("name", ""), m.get("uid", ""))] = now + (1.0 - b._tokens) / b.qps
+                blocked[_blocked_key(obj, kind)] = now + (1.0 - b._tokens) / b.qps
                 _bound(blocked, self.cache_limit)
             return
         message, key = self._aggregate(ref, event_type, reason, message, now)
