@@ -318,6 +318,13 @@ async def test_http2_off_and_a_server_without_h2_fall_back_to_http11(tmp_path, n
         await cl.start()
         await cl.ready()
         assert cl.env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
+
+        async def h1_flow():  # back to HTTP/1.1: the in-flight cap is the pool again, not the HTTP/2 cap
+            fl = _flow(cl).get("shard-0") or {}
+            return fl.get("http2") == 0 and fl.get("requests", 0) > 0 and fl
+        from ncc.controller.native_executor import DEFAULT_POOL_SIZE
+        fl = await wait_for(h1_flow, timeout=5, interval=0.1)
+        assert fl["cap"] == DEFAULT_POOL_SIZE and fl["limit"] <= DEFAULT_POOL_SIZE, fl
     from ncc.app import App
     from ncc.testing.env import FakeEnvironment
     os.makedirs(tmp_path / "tls", exist_ok=True)
@@ -336,6 +343,15 @@ async def test_http2_off_and_a_server_without_h2_fall_back_to_http11(tmp_path, n
             return env.shard_servers[0].state.try_get(R.CONFIGMAPS, NS, "c0") is not None
         await wait_for(synced, timeout=30, interval=0.05)
         assert env.shard_servers[0]._http.conn_stats()["h2"]["connections"] == 0
+
+        async def h1_cap():  # ALPN chose http/1.1: the cap is the pool (256), not the HTTP/2 cap
+            ex = app.debug_state().get("executors") or {}
+            fl = [(h.get("status") or {}).get("flow", {}).get("shard-0") for h in ex.values()]
+            fl = [f for f in fl if f and f.get("http2") == 0 and f.get("requests", 0) > 0]
+            return fl and fl[0]
+        from ncc.controller.native_executor import DEFAULT_POOL_SIZE
+        fl = await wait_for(h1_cap, timeout=5, interval=0.1)
+        assert fl["cap"] == DEFAULT_POOL_SIZE, fl
     finally:
         stop.set()
         if task is not None:
