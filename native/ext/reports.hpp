@@ -320,6 +320,115 @@ class ReportTable {
         return py::bool_(ok);
     }
 
+    // template_update(old, new, adopted, generation_filter, same_references) -> None | False | key
+    // The coordinator's on_update handler for a template (ncc/controller/controller.py `_on_crd_update`, the
+    // specification, with the adoption cache on) without running Python per event: None — nothing to do (an
+    // informer resync or a status-only change); False — an early pass skipped (some shard has not reported on
+    // the adopted version yet; its last report enqueues it); else the work-queue key to enqueue.  A new version
+    // with the same references stays adopted.  `same_references` (ncc/api/refs.py) is called only when the
+    // slim form's references digest cannot decide.  Anything of an unexpected type raises TypeError, and the
+    // caller runs the Python handler instead.
+    py::object template_update(py::dict old, py::dict nw, py::dict adopted, bool generation_filter,
+                               py::object same_references) const {
+        static PyObject* k_metadata = PyUnicode_InternFromString("metadata");
+        static PyObject* k_rv = PyUnicode_InternFromString("resourceVersion");
+        static PyObject* k_uid = PyUnicode_InternFromString("uid");
+        static PyObject* k_gen = PyUnicode_InternFromString("generation");
+        static PyObject* k_ns = PyUnicode_InternFromString("namespace");
+        static PyObject* k_name = PyUnicode_InternFromString("name");
+        static PyObject* k_labels = PyUnicode_InternFromString("labels");
+        static PyObject* k_ann = PyUnicode_InternFromString("annotations");
+        static PyObject* k_spec = PyUnicode_InternFromString("spec");
+        static PyObject* k_rfp = PyUnicode_InternFromString("_rfp");
+        static PyObject* k_status = PyUnicode_InternFromString("status");
+        static PyObject* k_conditions = PyUnicode_InternFromString("conditions");
+        auto get = [](PyObject* d, PyObject* k) -> PyObject* {  // borrowed; Py_None when absent
+            PyObject* v = PyDict_GetItemWithError(d, k);
+            if (v == nullptr && PyErr_Occurred()) throw py::error_already_set();
+            return v != nullptr ? v : Py_None;
+        };
+        auto truthy = [](PyObject* v) {
+            int t = PyObject_IsTrue(v);
+            if (t < 0) throw py::error_already_set();
+            return t == 1;
+        };
+        auto eq = [](PyObject* a, PyObject* b) {
+            int r = PyObject_RichCompareBool(a, b, Py_EQ);
+            if (r < 0) throw py::error_already_set();
+            return r == 1;
+        };
+        // `x.get("metadata") or {}`: a dict, or None for an empty/absent one
+        auto sub = [&](PyObject* d, PyObject* k) -> PyObject* {
+            PyObject* v = get(d, k);
+            if (!truthy(v)) return nullptr;
+            if (!PyDict_Check(v)) throw py::type_error("template_update: not a mapping");
+            return v;
+        };
+        auto str_of = [](PyObject* v, std::string& out) {  // `v or ""` of a string field
+            if (v == Py_None) return;
+            if (!PyUnicode_Check(v)) throw py::type_error("template_update: not a string");
+            Py_ssize_t n = 0;
+            const char* c = PyUnicode_AsUTF8AndSize(v, &n);
+            if (c == nullptr) throw py::error_already_set();
+            out.assign(c, static_cast<size_t>(n));
+        };
+        PyObject* om = sub(old.ptr(), k_metadata);
+        PyObject* nm = sub(nw.ptr(), k_metadata);
+        PyObject* nrv = nm != nullptr ? get(nm, k_rv) : Py_None;
+        PyObject* orv = om != nullptr ? get(om, k_rv) : Py_None;
+        std::string ns, name, key = "template/";
+        if (nm != nullptr) {
+            str_of(get(nm, k_ns), ns);
+            PyObject* nv = get(nm, k_name);
+            if (nv == Py_None && PyDict_Contains(nm, k_name) == 1)
+                throw py::type_error("template_update: name is None");  // f"{None}" in the Python handler
+            str_of(nv, name);
+        }
+        key.append(ns).append(1, '/').append(name);
+        py::str pkey(key);
+        // a new version with the same references stays adopted
+        if (eq(get(adopted.ptr(), pkey.ptr()), orv) &&
+            eq(om != nullptr ? get(om, k_uid) : Py_None, nm != nullptr ? get(nm, k_uid) : Py_None)) {
+            bool same = false;
+            PyObject* sa = get(old.ptr(), k_spec);
+            PyObject* sb = get(nw.ptr(), k_spec);
+            if (PyDict_Check(sa) && PyDict_Check(sb) && truthy(sa) && truthy(sb)) {
+                PyObject* ra = get(sa, k_rfp);
+                same = ra != Py_None && eq(ra, get(sb, k_rfp));
+            }
+            if (!same) same = same_references(old, nw).cast<bool>();
+            if (same && PyDict_SetItem(adopted.ptr(), pkey.ptr(), nrv) < 0) throw py::error_already_set();
+        }
+        if (generation_filter) {
+            if (eq(orv, nrv)) return py::none();  // informer resync: nothing changed
+            PyObject* gen = om != nullptr ? get(om, k_gen) : Py_None;
+            PyObject* none_ = Py_None;
+            if (gen != Py_None && eq(gen, nm != nullptr ? get(nm, k_gen) : none_) &&
+                eq(om != nullptr ? get(om, k_labels) : none_, nm != nullptr ? get(nm, k_labels) : none_) &&
+                eq(om != nullptr ? get(om, k_ann) : none_, nm != nullptr ? get(nm, k_ann) : none_) &&
+                eq(get(old.ptr(), k_spec), get(nw.ptr(), k_spec)))
+                return py::none();  // status-only change (typically our own status write)
+        }
+        // an initialised, adopted version that not every shard has reported on: its last report enqueues it
+        PyObject* st = sub(nw.ptr(), k_status);
+        if (st != nullptr && truthy(get(st, k_conditions)) && eq(get(adopted.ptr(), pkey.ptr()), nrv)) {
+            std::string uid;
+            int64_t g = 0;
+            if (nm != nullptr) {
+                PyObject* u = get(nm, k_uid);
+                if (truthy(u)) str_of(u, uid);
+                PyObject* gv = get(nm, k_gen);
+                if (truthy(gv)) {
+                    if (!PyLong_Check(gv)) throw py::type_error("template_update: generation is not an int");
+                    g = PyLong_AsLongLong(gv);
+                    if (g == -1 && PyErr_Occurred()) throw py::error_already_set();
+                }
+            }
+            if (ready(key, uid, g) < 0) return py::bool_(false);
+        }
+        return std::move(pkey);
+    }
+
     // finish_batch(keys, items, assumed, adopted, memos, shards, queue, pending_event, event_on_noop)
     //     -> (rest, verify, events, done, superseded)
     // The coordinator's inline finish (ncc/controller/reconcile.py `finish_inline_many`, the specification) over

@@ -73,7 +73,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 31
+#define NCC_NATIVE_ABI 32
 
 namespace {
 #include "ext/hashing.hpp"
@@ -178,6 +178,8 @@ PYBIND11_MODULE(_native, m) {
              "fold every complete frame of a byte stream from `start`: feed()'s tuple + the end offset")
         .def("readiness", &ReportTable::readiness, py::arg("key"), py::arg("uid"), py::arg("generation"))
         .def("ready_ok", &ReportTable::ready_ok, py::arg("key"), py::arg("uid"), py::arg("generation"))
+        .def("template_update", &ReportTable::template_update, py::arg("old"), py::arg("new"), py::arg("adopted"),
+             py::arg("generation_filter"), py::arg("same_references"))
         .def("finish_batch", &ReportTable::finish_batch, py::arg("keys"), py::arg("items"), py::arg("assumed"),
              py::arg("adopted"), py::arg("memos"), py::arg("shards"), py::arg("queue"), py::arg("pending_event"),
              py::arg("event_on_noop"))

@@ -144,7 +144,7 @@ class Controller(ReconcileMixin):
         o = self.options
         self.template_informer.add_event_handler(
             on_add=lambda obj: self.enqueue_resource(obj, C.KIND_TEMPLATE),
-            on_update=lambda old, new: self._on_crd_update(old, new, C.KIND_TEMPLATE),
+            on_update=self._template_update_handler(),
             on_delete=self._on_template_delete)
         self.workgroup_informer.add_event_handler(
             on_add=lambda obj: self.enqueue_resource(obj, C.KIND_WORKGROUP),
@@ -157,6 +157,28 @@ class Controller(ReconcileMixin):
         if o.watch_shards:
             for shard in self.shards:
                 self._register_shard_handlers(shard)
+
+    def _template_update_handler(self):
+        """The template informer's on_update: `_on_crd_update` (the specification), or — coordinator role with the
+        adoption cache, the native report table loaded — the same decision in one native call
+        (`ReportTable.template_update`), falling back to `_on_crd_update` on anything of an unexpected type."""
+        fn = getattr(self.reports, "template_update", None)
+        if fn is None or self.role != "coordinator" or not self.options.adoption_cache:
+            return lambda old, new: self._on_crd_update(old, new, C.KIND_TEMPLATE)
+        gf = bool(self.options.generation_filter)
+
+        def on_update(old, new):
+            try:
+                r = fn(old, new, self._adopted, gf, same_references)
+            except TypeError:
+                return self._on_crd_update(old, new, C.KIND_TEMPLATE)
+            if r is None:
+                return None
+            if r is False:
+                self.stats["early_passes_skipped"] += 1
+                return None
+            self._enqueue_key(r)
+        return on_update
 
     def _on_crd_update(self, old: dict, new: dict, kind: str) -> None:
         o = self.options

@@ -442,6 +442,39 @@ async def test_adoption_cache_rechecks_after_dependent_events():
     assert ctl._adopted[key] == "999999"  # references changed: the new version is not marked
 
 
+async def test_coordinator_template_handler_is_native_and_skips_the_early_pass():
+    """The template informer's on_update in the coordinator is the native decision (`ReportTable.template_update`)
+    when the extension is loaded: a resync is filtered, a spec update of an adopted template whose reports are
+    not in is skipped, and one whose reports are in is enqueued."""
+    env = Env(2)
+    t = env.seed()
+    ctl = env.build(role="coordinator")
+    if not hasattr(ctl.reports, "template_update"):
+        pytest.skip("native extension not built")
+    name = t["metadata"]["name"]
+    key = make_key(C.KIND_TEMPLATE, NS, name)
+    await ctl.sync_template(NS, name)
+    env.refresh()
+    handler = ctl.template_informer._handlers[0].on_update
+    assert handler.__qualname__.endswith("_template_update_handler.<locals>.on_update")
+    old = ctl.template_lister.get(NS, name)
+    handler(old, old)
+    assert len(ctl.queue) == 0 and ctl.queue.core.waiting() == 0
+    new = dict(old, metadata=dict(old["metadata"], resourceVersion="900", generation=old["metadata"]["generation"] + 1),
+               spec=dict(old["spec"], container=dict(old["spec"]["container"], versionTag="v-next")))
+    handler(old, new)
+    assert ctl.stats["early_passes_skipped"] == 1 and ctl.queue.core.waiting() == 0 and len(ctl.queue) == 0
+    assert ctl._adopted[key] == "900"  # same references: the new version stays adopted
+    m = new["metadata"]
+    for i in range(2):
+        ctl.reports.feed(msgpack.packb({"t": "report", "k": key, "u": m["uid"], "g": m["generation"],
+                                        "r": {f"s{i}": None}, "w": False}), False)
+    newer = dict(new, metadata=dict(new["metadata"], resourceVersion="901"),
+                 spec=dict(new["spec"], container=dict(new["spec"]["container"], versionTag="v-next2")))
+    handler(new, newer)  # every shard has reported on this generation: a pass is due
+    assert ctl.stats["early_passes_skipped"] == 1 and ctl.queue.core.waiting() + len(ctl.queue) == 1
+
+
 async def test_coordinator_skips_early_pass_until_reports_complete():
     """A spec update of an initialised, adopted template is not reconciled by the coordinator on its
     informer event (nothing to do before the executors report); the last report enqueues it — and if

@@ -224,3 +224,63 @@ async def test_channel_raw_frames_fold_through_the_controller_path():
     tx.close()
     assert await rx.recv_folded(fold) is None
     rx.close()
+
+
+# ------------------------------------------------------------------ the coordinator's template on_update
+_val = st.one_of(st.none(), st.sampled_from(["1", "2", "3"]))
+_meta = st.fixed_dictionaries({}, optional={
+    "namespace": st.sampled_from(["ns", "", None]), "name": st.sampled_from(["a", "b"]),
+    "resourceVersion": _val, "uid": st.sampled_from(["u1", "u2", "", None]),
+    "generation": st.one_of(st.none(), st.integers(0, 3)),
+    "labels": st.one_of(st.none(), st.just({}), st.just({"x": "1"})),
+    "annotations": st.one_of(st.none(), st.just({"y": "1"}))})
+_env = st.sampled_from([[], [{"name": "E", "valueFrom": {"secretKeyRef": {"name": "s0", "key": "k"}}}],
+                        [{"name": "E", "valueFrom": {"configMapKeyRef": {"name": "c0", "key": "k"}}}]])
+_spec = st.one_of(st.none(), st.just({}),
+                  st.fixed_dictionaries({"runtimeEnvironment": st.fixed_dictionaries({"mappedEnvironmentVariables": _env}),
+                                         "container": st.sampled_from([{"image": "a"}, {"image": "b"}])},
+                                        optional={"_rfp": st.sampled_from([1, 2])}))
+_status = st.one_of(st.none(), st.just({}), st.just({"conditions": []}),
+                    st.just({"conditions": [{"type": "Ready", "status": "True"}]}))
+_template = st.fixed_dictionaries({}, optional={"metadata": _meta, "spec": _spec, "status": _status})
+
+
+@pytest.mark.skipif(NATIVE is None or not hasattr(NATIVE.ReportTable(), "template_update"),
+                    reason="native extension not built")
+@settings(max_examples=600, deadline=None)
+@given(old=_template, new=_template, adopted=st.dictionaries(st.sampled_from(["template/ns/a", "template//a",
+                                                                              "template/ns/b"]), _val, max_size=3),
+       reports=st.lists(st.tuples(st.sampled_from(["template/ns/a", "template//a"]), st.sampled_from(["u1", "u2"]),
+                                  st.integers(0, 3)), max_size=3),
+       gf=st.booleans())
+def test_native_template_update_matches_the_python_handler(old, new, adopted, reports, gf):
+    """`ReportTable.template_update` (the coordinator's template on_update in one native call) decides as
+    `Controller._on_crd_update` does — enqueue, skip the early pass, or nothing — and leaves the adoption cache
+    the same; inputs it does not handle raise TypeError (the handler then runs in Python)."""
+    from types import SimpleNamespace
+
+    from ncc.api.refs import same_references
+    from ncc.controller.controller import Controller
+    table = NATIVE.ReportTable()
+    table.set_shards(["s0", "s1"])
+    for key, uid, gen in reports:
+        for sh in ("s0", "s1"):
+            table.feed(*frame([{"t": "report", "k": key, "u": uid, "g": gen, "r": {sh: None}, "w": False}]))
+    enq = []
+    stub = SimpleNamespace(options=SimpleNamespace(adoption_cache=True, generation_filter=gf), role="coordinator",
+                           _adopted=dict(adopted), stats={"early_passes_skipped": 0}, reports=table,
+                           _enqueue_key=enq.append)
+    stub.shard_ready_ok = lambda key, obj: Controller.shard_ready_ok(stub, key, obj)
+    try:
+        Controller._on_crd_update(stub, old, new, "template")
+        want = ("ok", enq[0] if enq else None, stub.stats["early_passes_skipped"], stub._adopted)
+    except (TypeError, AttributeError) as e:
+        want = ("error", type(e).__name__)
+    nat_adopted = dict(adopted)
+    try:
+        r = table.template_update(old, new, nat_adopted, gf, same_references)
+        got = ("ok", r if isinstance(r, str) else None, 1 if r is False else 0, nat_adopted)
+    except TypeError:
+        got = None  # the Python handler decides
+    if got is not None:
+        assert got == want, (old, new, adopted)
