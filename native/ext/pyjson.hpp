@@ -819,6 +819,45 @@ py::object loads(py::bytes data) {
     return py::reinterpret_steal<py::object>(o);
 }
 
+// template_index_same(old, new) -> bool: the coordinator's template indices read the same in both versions —
+// ncc/controller/controller.py `_reference_guard(old) == _reference_guard(new)` (namespace, and the references
+// digest `spec._rfp` of a slim template or else the mapped environment) in one call instead of two tuples.
+// Anything but dicts where the guard reads dicts raises TypeError (the caller then compares the guards).
+bool template_index_same(py::handle old, py::handle nw) {
+    auto get = [](PyObject* d, PyObject* k) -> PyObject* {  // borrowed, Py_None when absent
+        PyObject* v = PyDict_GetItemWithError(d, k);
+        if (v == nullptr && PyErr_Occurred()) throw py::error_already_set();
+        return v != nullptr ? v : Py_None;
+    };
+    auto sub = [&](PyObject* d, PyObject* k) -> PyObject* {  // `d.get(k) or {}`: nullptr for an empty one
+        PyObject* v = get(d, k);
+        int t = PyObject_IsTrue(v);
+        if (t < 0) throw py::error_already_set();
+        if (t == 0) return nullptr;
+        if (!PyDict_Check(v)) throw py::type_error("template_index_same: not a mapping");
+        return v;
+    };
+    auto refs = [&](PyObject* t) -> PyObject* {
+        PyObject* spec = sub(t, PY_CONST_KEY("spec"));
+        if (spec == nullptr) return Py_None;
+        PyObject* r = get(spec, PY_CONST_KEY("_rfp"));
+        if (r != Py_None) return r;
+        PyObject* env = sub(spec, PY_CONST_KEY("runtimeEnvironment"));
+        return env != nullptr ? get(env, PY_CONST_KEY("mappedEnvironmentVariables")) : Py_None;
+    };
+    auto eq = [](PyObject* a, PyObject* b) {
+        int r = PyObject_RichCompareBool(a, b, Py_EQ);
+        if (r < 0) throw py::error_already_set();
+        return r == 1;
+    };
+    if (!PyDict_Check(old.ptr()) || !PyDict_Check(nw.ptr())) throw py::type_error("template_index_same: not a dict");
+    PyObject* om = sub(old.ptr(), PY_CONST_KEY("metadata"));
+    PyObject* nm = sub(nw.ptr(), PY_CONST_KEY("metadata"));
+    PyObject* ons = om != nullptr ? get(om, PY_CONST_KEY("namespace")) : Py_None;
+    PyObject* nns = nm != nullptr ? get(nm, PY_CONST_KEY("namespace")) : Py_None;
+    return eq(ons, nns) && eq(refs(old.ptr()), refs(nw.ptr()));
+}
+
 // template_event_slim(line) -> (type, slim object) | None
 py::object template_event_slim(py::bytes line, py::object items, const std::string& default_ns) {
     std::string_view v = bytes_view(line);

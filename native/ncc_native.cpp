@@ -73,7 +73,7 @@
 
 namespace py = pybind11;
 
-#define NCC_NATIVE_ABI 32
+#define NCC_NATIVE_ABI 33
 
 namespace {
 #include "ext/hashing.hpp"
@@ -127,6 +127,8 @@ PYBIND11_MODULE(_native, m) {
     m.def("members_equal", &members_equal, py::arg("a"), py::arg("b"), py::arg("keys"),
           "True iff the named top-level members of two JSON objects are byte-identical (or both absent)");
     m.def("loads", &loads, py::arg("data"), "JSON bytes -> Python value, or None when malformed");
+    m.def("template_index_same", &template_index_same, py::arg("old"), py::arg("new"),
+          "the template indices read the same in both versions (namespace and references)");
     m.def("template_event_slim", &template_event_slim, py::arg("line"), py::arg("items") = py::none(),
           py::arg("default_ns") = std::string(),
           "template watch line -> (type, object with metadata/status decoded and the spec slimmed) | None; "

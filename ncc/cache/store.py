@@ -34,6 +34,9 @@ class Store:
         # index_guard(obj): a cheap projection of everything the indexers read; an update that leaves it
         # equal skips the indexers altogether (templates: the mapped environment, i.e. the references)
         self.index_guard: Callable[[dict], object] | None = None
+        # index_same(old, new): index_guard(old) == index_guard(new) in one call (a native twin); TypeError from it
+        # falls back to comparing the guards
+        self.index_same: Callable[[dict, dict], bool] | None = None
 
     # ------------------------------------------------------------ indices
     def add_indexer(self, name: str, fn: IndexFunc) -> None:
@@ -53,8 +56,17 @@ class Store:
         """Move `key` between index buckets.  Each key's current index values are remembered, so an update
         that leaves them unchanged (the common case: a spec edit keeps the references) touches no set."""
         g = self.index_guard
-        if g is not None and old is not None and new is not None and g(old) == g(new):
-            return
+        if g is not None and old is not None and new is not None:
+            same = self.index_same
+            if same is not None:
+                try:
+                    if same(old, new):
+                        return
+                except TypeError:
+                    if g(old) == g(new):
+                        return
+            elif g(old) == g(new):
+                return
         for name, fn in self._indexers.items():
             vals = self._index_vals[name]
             ov = vals.get(key, ())

@@ -22,6 +22,7 @@ import time
 
 import msgpack
 
+from .. import native as _native
 from ..api import constants as C
 from ..api.objects import ObjectKey, meta
 from ..api.refs import configmap_names, same_references, secret_names, template_owner_names
@@ -127,6 +128,9 @@ class Controller(ReconcileMixin):
                 "configmap", lambda t: [f"{meta(t).get('namespace', '')}/{n}" for n in configmap_names(t)])
             # both indices read only the namespace and the mapped environment
             self.template_informer.store.index_guard = _reference_guard
+            mod = _native.load()
+            if mod is not None and hasattr(mod, "template_index_same"):
+                self.template_informer.store.index_same = mod.template_index_same
         self._register_handlers()
 
     @property

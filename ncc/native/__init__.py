@@ -17,7 +17,7 @@ import os
 
 _mod = None
 _err: BaseException | None = None
-ABI_VERSION = 32  # bump together with NCC_NATIVE_ABI in native/ncc_native.cpp
+ABI_VERSION = 33  # bump together with NCC_NATIVE_ABI in native/ncc_native.cpp
 
 
 def load(required: bool = False):

@@ -284,3 +284,13 @@ def test_native_template_update_matches_the_python_handler(old, new, adopted, re
         got = None  # the Python handler decides
     if got is not None:
         assert got == want, (old, new, adopted)
+
+
+@pytest.mark.skipif(NATIVE is None or not hasattr(NATIVE, "template_index_same"), reason="native extension not built")
+@settings(max_examples=400, deadline=None)
+@given(old=_template, new=_template)
+def test_native_template_index_same_matches_the_guard(old, new):
+    """`template_index_same` (the template store's index short-cut) equals comparing `_reference_guard`s."""
+    from ncc.controller.controller import _reference_guard
+    assert NATIVE.template_index_same(old, new) == (_reference_guard(old) == _reference_guard(new))
+    assert NATIVE.template_index_same(old, old)
